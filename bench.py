@@ -1,0 +1,170 @@
+#!/usr/bin/env python
+"""Headline benchmark: Llama-3-8B DPO preference-pairs/s (whole job), BASELINE.json config 2.
+
+One process per GPU (torchrun / torch.distributed.run launches N ranks over RCCL). Each rank:
+policy (trainable, bf16 weights, fp32 master + Adam moments, ZeRO-1 sharded across ranks) and a
+frozen reference model co-resident on its MI355X; every optimizer step consumes
+`--micro-pairs x --accum` synthetic preference pairs of `--seq-len` tokens per side on each rank
+(weak scaling). The timed region is K full optimizer steps: policy fwd+bwd on chosen+rejected,
+reference fwd, fused DPO loss, bucketed RCCL reduce-scatter overlapped with backward, clip,
+fused AdamW, all-gather. Data: synthetic token ids, random-init weights (no network).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--seq-len", type=int, default=1024)
+    ap.add_argument("--micro-pairs", type=int, default=4)
+    ap.add_argument("--accum", type=int, default=4)
+    ap.add_argument("--beta", type=float, default=0.1)
+    ap.add_argument("--zero", type=int, default=None)
+    ap.add_argument("--bucket-mb", type=float, default=256.0)
+    ap.add_argument("--profile-dir", default=None, help="write a torch.profiler trace of 1 step")
+    ap.add_argument("--layers", type=int, default=None, help="debug only: override layer count "
+                    "(a reduced model is NOT the benchmark config)")
+    return ap.parse_args()
+
+
+def main() -> int:
+    args = parse()
+    import distributed_llm_alignment_amd as dla  # noqa: F401  (loads the HIP extension)
+    from distributed_llm_alignment_amd.data.synthetic import synthetic_preference_batch
+    from distributed_llm_alignment_amd.models import build_model, get_config
+    from distributed_llm_alignment_amd.objectives import dpo_step_loss
+    from distributed_llm_alignment_amd.ops import _ext
+    from distributed_llm_alignment_amd.parallel.data_parallel import DataParallelEngine
+    from distributed_llm_alignment_amd.parallel.dist import barrier, init_distributed
+
+    st = init_distributed()
+    dev = st.device
+    if dev.type == "cuda":
+        _ext.require()
+    world = st.world_size
+    overrides = {} if args.layers is None else {"num_layers": args.layers}
+    cfg = get_config(args.model, **overrides)
+    dtype = torch.bfloat16 if dev.type == "cuda" else torch.float32
+
+    policy = build_model(cfg, device=dev, dtype=dtype, seed=1234)
+    ref = build_model(cfg, device=dev, dtype=dtype, seed=1234)
+    ref.eval()
+    for p in ref.parameters():
+        p.requires_grad_(False)
+    engine = DataParallelEngine(policy, lr=1e-6, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01,
+                                max_grad_norm=1.0, zero_stage=args.zero, bucket_mb=args.bucket_mb)
+    policy.train()
+
+    gen = torch.Generator().manual_seed(17 + st.rank)
+    n_batches = 4
+    batches = [synthetic_preference_batch(args.micro_pairs, args.seq_len, cfg.vocab_size, device=dev,
+                                          generator=gen) for _ in range(n_batches)]
+    state = {"i": 0, "loss": None}
+
+    def train_step():
+        for a in range(args.accum):
+            b = batches[state["i"] % n_batches]
+            state["i"] += 1
+            ctx = engine.no_sync() if a < args.accum - 1 else _null()
+            with ctx:
+                loss, _ = dpo_step_loss(policy, ref, b, beta=args.beta)
+                (loss / args.accum).backward()
+            state["loss"] = loss
+        engine.step()
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        train_step()
+    sync()
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    if args.profile_dir:
+        from torch.profiler import ProfilerActivity, profile
+
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+            for _ in range(args.steps):
+                train_step()
+            sync()
+    else:
+        for _ in range(args.steps):
+            train_step()
+    sync()
+    barrier()
+    sync()
+    elapsed = time.perf_counter() - t0
+    t_max = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if st.initialized:
+        import torch.distributed as dist
+
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+    elapsed = float(t_max.item())
+    if args.profile_dir and st.rank == 0:
+        os.makedirs(args.profile_dir, exist_ok=True)
+        prof.export_chrome_trace(os.path.join(args.profile_dir, "trace.json"))
+        with open(os.path.join(args.profile_dir, "kernels.txt"), "w") as fh:
+            fh.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=60))
+
+    pairs_per_step = args.micro_pairs * args.accum * world
+    ms = elapsed / args.steps * 1000.0
+    value = pairs_per_step * args.steps / elapsed
+    # model FLOPs: policy fwd+bwd (3x) + ref fwd (1x) over 2*seq tokens per pair
+    tokens_per_pair = 2 * args.seq_len
+    flops_pair = 4 * cfg.flops_per_token(args.seq_len) * tokens_per_pair
+    tflops_gpu = value * flops_pair / world / 1e12
+    if st.rank == 0:
+        rec = {
+            "metric": "preference-samples/sec (whole node), Llama-3-8B DPO",
+            "value": round(value, 4),
+            "unit": "preference_pairs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16" if dtype == torch.bfloat16 else "fp32",
+            "data": "synthetic preference pairs (random token ids), random-init weights",
+            "config": {
+                "model": cfg.name if args.layers is None else f"{cfg.name}-L{args.layers}(debug)",
+                "global_batch": pairs_per_step,
+                "seq_len": args.seq_len,
+                "parallelism": f"dp{world}" + (f"-zero{engine.zero}" if world > 1 else ""),
+                "micro_batch_pairs": args.micro_pairs,
+                "grad_accum": args.accum,
+                "ref_model": "frozen, co-resident",
+                "model_tflops_per_gpu": round(tflops_gpu, 1),
+                "final_loss": round(float(state["loss"].item()), 5),
+            },
+        }
+        print(json.dumps(rec), flush=True)
+    return 0
+
+
+class _null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,52 @@
+// Kernel-argument structs shared by attention.hip (device side) and bindings.cpp (host side).
+#pragma once
+#include <stdint.h>
+
+namespace dla {
+
+using bf16_t = uint16_t;
+
+struct AttnParams {
+  const bf16_t* q;
+  const bf16_t* k;
+  const bf16_t* v;
+  bf16_t* o;
+  float* lse2;  // [B, Hq, Tq], log2 domain: m2 + log2(l) of scores scaled by scale*log2(e)
+  int64_t q_sb, q_st, q_sh;
+  int64_t k_sb, k_st, k_sh;
+  int64_t v_sb, v_st, v_sh;
+  int64_t o_sb, o_st, o_sh;
+  int B, Hq, Hkv, Tq, Tk;
+  float scale2;     // softmax scale * log2(e)
+  int causal_off;   // key j visible to query i iff j <= i + causal_off (causal only)
+  int window;       // >0: also require j > i + causal_off - window
+  const int* kv_start;  // [B] or null
+  const int* kv_end;    // [B] or null
+};
+
+struct AttnBwdParams {
+  const bf16_t* q;
+  const bf16_t* k;
+  const bf16_t* v;
+  const bf16_t* dout;
+  const float* lse2;   // [B, Hq, Tq]
+  const float* delta;  // [B, Hq, Tq] = rowsum(dO * O)
+  float* dq;           // [B, Tq, Hq, D] fp32, pre-zeroed, accumulated atomically
+  bf16_t* dk;          // strided like k
+  bf16_t* dv;          // strided like v
+  int64_t q_sb, q_st, q_sh;
+  int64_t k_sb, k_st, k_sh;
+  int64_t v_sb, v_st, v_sh;
+  int64_t do_sb, do_st, do_sh;
+  int64_t dk_sb, dk_st, dk_sh;
+  int64_t dv_sb, dv_st, dv_sh;
+  int B, Hq, Hkv, Tq, Tk;
+  float scale;   // softmax scale (natural)
+  float scale2;  // scale * log2(e)
+  int causal_off;
+  int window;
+  const int* kv_start;
+  const int* kv_end;
+};
+
+}  // namespace dla

@@ -1,0 +1,107 @@
+// Shared device helpers for the gfx950 (CDNA4, MI355X) kernels of this package.
+//
+// Conventions used by every kernel file:
+//   * bf16 tensors travel as raw 16-bit words (`bf16_t` = uint16_t); math is fp32.
+//   * wave = 64 lanes (never 32); block sizes are multiples of 64.
+//   * global loads/stores of bf16 are vectorized to 16 B per lane (8 x bf16).
+//   * every launcher takes an explicit hipStream_t (the caller's current torch stream),
+//     performs no allocation and no host synchronisation (graph-capture safe).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dla {
+
+using bf16_t = uint16_t;
+
+// 8 x bf16 = 16 bytes: the native global-load width per lane.
+typedef uint16_t bf16x8 __attribute__((ext_vector_type(8)));
+typedef uint16_t bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+// MFMA operand fragments (bf16 payload in short lanes).
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ float bf2f(bf16_t v) {
+  return __uint_as_float(static_cast<uint32_t>(v) << 16);
+}
+
+// Round-to-nearest-even fp32 -> bf16, NaN preserving (quietened).
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return static_cast<bf16_t>((u >> 16) | 0x40u);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return static_cast<bf16_t>(u >> 16);
+}
+
+// Pack two fp32 into one dword of two bf16 (lo in bits 0..15).
+__device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
+  return static_cast<uint32_t>(f2bf(lo)) | (static_cast<uint32_t>(f2bf(hi)) << 16);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum for blockDim.x == NT (multiple of 64). `scratch` holds NT/64 floats.
+template <int NT>
+__device__ __forceinline__ float block_sum(float v, float* scratch) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) scratch[w] = v;
+  __syncthreads();
+  float r = 0.f;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) r += scratch[i];
+  return r;
+}
+
+template <int NT>
+__device__ __forceinline__ float block_max(float v, float* scratch) {
+  v = wave_max(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) scratch[w] = v;
+  __syncthreads();
+  float r = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) r = fmaxf(r, scratch[i]);
+  return r;
+}
+
+__device__ __forceinline__ bf16x8 load_bf16x8(const bf16_t* p) {
+  return *reinterpret_cast<const bf16x8*>(p);
+}
+__device__ __forceinline__ void store_bf16x8(bf16_t* p, bf16x8 v) {
+  *reinterpret_cast<bf16x8*>(p) = v;
+}
+
+__device__ __forceinline__ float fast_exp(float x) { return __expf(x); }
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+// log(sigmoid(x)) computed stably.
+__device__ __forceinline__ float log_sigmoid(float x) {
+  return fminf(x, 0.f) - log1pf(__expf(-fabsf(x)));
+}
+
+// XCD-aware bijective block remap (8 XCDs, blocks dealt round-robin): consecutive logical tiles
+// land on the same XCD so they share its L2. Speed only, never correctness.
+__device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
+  const int q = nblocks / 8, r = nblocks % 8;
+  const int xcd = bid % 8, idx = bid / 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+}  // namespace dla

@@ -1,0 +1,109 @@
+// Elementwise activation kernels: fused SwiGLU and tanh-GELU, forward + backward.
+//
+// Reference: HF LlamaMLP `down(silu(gate(x)) * up(x))` and GPT-2/phi-2 `gelu_new`, reached via
+// every model forward in src/training/train_*.py. Eager PyTorch runs silu, mul (and their
+// backward) as 3-5 separate HBM passes; here each direction is ONE pass, 16 B per lane.
+//
+// SwiGLU input is the fused gate_up GEMM output gu[N, 2F] (gate = columns [0,F), up = [F,2F)).
+#include "common.h"
+
+namespace dla {
+
+__device__ __forceinline__ float silu_f(float g) { return g * sigmoidf_(g); }
+
+__global__ __launch_bounds__(256) void swiglu_fwd_kernel(const bf16_t* __restrict__ gu,
+                                                          bf16_t* __restrict__ out, int64_t rows,
+                                                          int F) {
+  const int fv = F >> 3;
+  const int64_t total = rows * fv;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += static_cast<int64_t>(gridDim.x) * 256) {
+    const int64_t r = i / fv;
+    const int c = static_cast<int>(i - r * fv) * 8;
+    const bf16_t* row = gu + r * 2 * F;
+    bf16x8 g = load_bf16x8(row + c), u = load_bf16x8(row + F + c), o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = f2bf(silu_f(bf2f(g[j])) * bf2f(u[j]));
+    store_bf16x8(out + r * F + c, o);
+  }
+}
+
+__global__ __launch_bounds__(256) void swiglu_bwd_kernel(const bf16_t* __restrict__ gu,
+                                                          const bf16_t* __restrict__ dout,
+                                                          bf16_t* __restrict__ dgu, int64_t rows,
+                                                          int F) {
+  const int fv = F >> 3;
+  const int64_t total = rows * fv;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += static_cast<int64_t>(gridDim.x) * 256) {
+    const int64_t r = i / fv;
+    const int c = static_cast<int>(i - r * fv) * 8;
+    const bf16_t* row = gu + r * 2 * F;
+    bf16x8 g = load_bf16x8(row + c), u = load_bf16x8(row + F + c);
+    bf16x8 d = load_bf16x8(dout + r * F + c), dg, du;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float gf = bf2f(g[j]), uf = bf2f(u[j]), df = bf2f(d[j]);
+      const float sg = sigmoidf_(gf);
+      const float sl = gf * sg;
+      du[j] = f2bf(df * sl);
+      dg[j] = f2bf(df * uf * sg * (1.f + gf * (1.f - sg)));
+    }
+    store_bf16x8(dgu + r * 2 * F + c, dg);
+    store_bf16x8(dgu + r * 2 * F + F + c, du);
+  }
+}
+
+// gelu_new (tanh approximation), as used by GPT-2 and phi-2.
+__device__ __forceinline__ float gelu_tanh(float x, float* dgdx) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float inner = k0 * (x + k1 * x * x * x);
+  const float t = tanhf(inner);
+  if (dgdx) *dgdx = 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x * x);
+  return 0.5f * x * (1.f + t);
+}
+
+__global__ __launch_bounds__(256) void gelu_fwd_kernel(const bf16_t* __restrict__ x,
+                                                        bf16_t* __restrict__ y, int64_t nvec) {
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < nvec; i += static_cast<int64_t>(gridDim.x) * 256) {
+    bf16x8 a = load_bf16x8(x + i * 8), o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = f2bf(gelu_tanh(bf2f(a[j]), nullptr));
+    store_bf16x8(y + i * 8, o);
+  }
+}
+
+__global__ __launch_bounds__(256) void gelu_bwd_kernel(const bf16_t* __restrict__ x,
+                                                        const bf16_t* __restrict__ dy,
+                                                        bf16_t* __restrict__ dx, int64_t nvec) {
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < nvec; i += static_cast<int64_t>(gridDim.x) * 256) {
+    bf16x8 a = load_bf16x8(x + i * 8), d = load_bf16x8(dy + i * 8), o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float der;
+      gelu_tanh(bf2f(a[j]), &der);
+      o[j] = f2bf(bf2f(d[j]) * der);
+    }
+    store_bf16x8(dx + i * 8, o);
+  }
+}
+
+static inline unsigned grid_for(int64_t work) {
+  int64_t g = (work + 255) / 256;
+  if (g > 256 * 8) g = 256 * 8;  // 8 blocks per CU, grid-stride the rest
+  return static_cast<unsigned>(g < 1 ? 1 : g);
+}
+
+void launch_swiglu_fwd(const bf16_t* gu, bf16_t* out, int64_t rows, int F, hipStream_t st) {
+  swiglu_fwd_kernel<<<grid_for(rows * (F / 8)), 256, 0, st>>>(gu, out, rows, F);
+}
+void launch_swiglu_bwd(const bf16_t* gu, const bf16_t* dout, bf16_t* dgu, int64_t rows, int F,
+                       hipStream_t st) {
+  swiglu_bwd_kernel<<<grid_for(rows * (F / 8)), 256, 0, st>>>(gu, dout, dgu, rows, F);
+}
+void launch_gelu_fwd(const bf16_t* x, bf16_t* y, int64_t n, hipStream_t st) {
+  gelu_fwd_kernel<<<grid_for(n / 8), 256, 0, st>>>(x, y, n / 8);
+}
+void launch_gelu_bwd(const bf16_t* x, const bf16_t* dy, bf16_t* dx, int64_t n, hipStream_t st) {
+  gelu_bwd_kernel<<<grid_for(n / 8), 256, 0, st>>>(x, dy, dx, n / 8);
+}
+
+}  // namespace dla

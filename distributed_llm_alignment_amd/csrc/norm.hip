@@ -1,0 +1,294 @@
+// Fused (residual-add +) RMSNorm / LayerNorm forward and backward for gfx950.
+//
+// Replaces HF LlamaRMSNorm / nn.LayerNorm: reference call sites are every decoder
+// layer of the HF model reached from src/training/train_dpo.py:31-39 / train_sft.py:145.
+//
+// Layout: rows x H, bf16 I/O, fp32 math. One wave (64 lanes) owns a row; each lane holds NC
+// 16-byte chunks (8 bf16) of the row in registers, so the row is read exactly once per pass.
+// Residual fusion: s = bf16(x + r) is written out (the new residual stream) and normalised,
+// saving a separate elementwise pass in both directions.
+#include "common.h"
+
+namespace dla {
+
+template <int NC, bool RMS, bool HAS_RES, bool HAS_BIAS>
+__global__ __launch_bounds__(256) void norm_fwd_kernel(const bf16_t* __restrict__ x,
+                                                        const bf16_t* __restrict__ res,
+                                                        bf16_t* __restrict__ sum_out,
+                                                        const bf16_t* __restrict__ w,
+                                                        const bf16_t* __restrict__ b,
+                                                        bf16_t* __restrict__ y,
+                                                        float* __restrict__ rstd_out,
+                                                        float* __restrict__ mean_out, int rows,
+                                                        int H, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int nvec = H >> 3;
+  const size_t base = static_cast<size_t>(row) * H;
+  float v[NC][8];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int vi = c * 64 + lane;
+    if (vi < nvec) {
+      bf16x8 a = load_bf16x8(x + base + vi * 8);
+      if constexpr (HAS_RES) {
+        bf16x8 r = load_bf16x8(res + base + vi * 8);
+        bf16x8 s;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          s[j] = f2bf(bf2f(a[j]) + bf2f(r[j]));
+          v[c][j] = bf2f(s[j]);
+        }
+        store_bf16x8(sum_out + base + vi * 8, s);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[c][j] = bf2f(a[j]);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[c][j] = 0.f;
+    }
+  }
+  float mean = 0.f;
+  if constexpr (!RMS) {
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[c][j];
+    mean = wave_sum(s) / H;
+  }
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int vi = c * 64 + lane;
+    if (vi < nvec) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = v[c][j] - mean;
+        ss += d * d;
+      }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(ss) / H + eps);
+  if (lane == 0) {
+    rstd_out[row] = rstd;
+    if constexpr (!RMS) mean_out[row] = mean;
+  }
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int vi = c * 64 + lane;
+    if (vi < nvec) {
+      bf16x8 wv = load_bf16x8(w + vi * 8);
+      bf16x8 bv;
+      if constexpr (HAS_BIAS) bv = load_bf16x8(b + vi * 8);
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float t = (v[c][j] - mean) * rstd * bf2f(wv[j]);
+        if constexpr (HAS_BIAS) t += bf2f(bv[j]);
+        o[j] = f2bf(t);
+      }
+      store_bf16x8(y + base + vi * 8, o);
+    }
+  }
+}
+
+// Backward. One 256-thread block owns a row at a time (grid-stride over rows with a fixed
+// grid); each thread owns NC fixed 8-column chunks, so its dw/db partials stay in NC*8
+// registers across all rows of the block. One fp32 partial row per block ([grid, H]) is then
+// folded by norm_wgrad_reduce_kernel. Row reductions: wave shuffle + 4-entry LDS.
+template <int NC, bool RMS, bool HAS_DRES, bool HAS_BIAS>
+__global__ __launch_bounds__(256) void norm_bwd_kernel(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ s, const bf16_t* __restrict__ w,
+    const float* __restrict__ rstd_in, const float* __restrict__ mean_in,
+    const bf16_t* __restrict__ dres, bf16_t* __restrict__ ds, float* __restrict__ dw_part,
+    float* __restrict__ db_part, int rows, int H) {
+  __shared__ float red[2][4], redg[2][4];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int nvec = H >> 3;
+  float dwa[NC][8], dba[NC][8], wf[NC][8];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int vi = c * 256 + tid;
+    bf16x8 wv = vi < nvec ? load_bf16x8(w + vi * 8) : bf16x8{};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      dwa[c][j] = dba[c][j] = 0.f;
+      wf[c][j] = bf2f(wv[j]);
+    }
+  }
+  int parity = 0;
+  for (int row = blockIdx.x; row < rows; row += gridDim.x, parity ^= 1) {
+    const size_t base = static_cast<size_t>(row) * H;
+    const float rstd = rstd_in[row];
+    const float mean = RMS ? 0.f : mean_in[row];
+    float xh[NC][8], g[NC][8];
+    float sum_g = 0.f, sum_gx = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int vi = c * 256 + tid;
+      if (vi < nvec) {
+        bf16x8 dv = load_bf16x8(dy + base + vi * 8);
+        bf16x8 sv = load_bf16x8(s + base + vi * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = bf2f(dv[j]);
+          xh[c][j] = (bf2f(sv[j]) - mean) * rstd;
+          g[c][j] = d * wf[c][j];
+          dwa[c][j] += d * xh[c][j];
+          if constexpr (HAS_BIAS) dba[c][j] += d;
+          sum_g += g[c][j];
+          sum_gx += g[c][j] * xh[c][j];
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xh[c][j] = g[c][j] = 0.f;
+      }
+    }
+    // block reduction; double-buffered slots (parity) make one barrier per row sufficient.
+    sum_gx = wave_sum(sum_gx);
+    if constexpr (!RMS) sum_g = wave_sum(sum_g);
+    if (lane == 0) {
+      red[parity][wid] = sum_gx;
+      if constexpr (!RMS) redg[parity][wid] = sum_g;
+    }
+    __syncthreads();
+    sum_gx = (red[parity][0] + red[parity][1] + red[parity][2] + red[parity][3]) / H;
+    if constexpr (!RMS) sum_g = (redg[parity][0] + redg[parity][1] + redg[parity][2] + redg[parity][3]) / H;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int vi = c * 256 + tid;
+      if (vi < nvec) {
+        bf16x8 rv;
+        if constexpr (HAS_DRES) rv = load_bf16x8(dres + base + vi * 8);
+        bf16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float t = g[c][j] - xh[c][j] * sum_gx;
+          if constexpr (!RMS) t -= sum_g;
+          t *= rstd;
+          if constexpr (HAS_DRES) t += bf2f(rv[j]);
+          o[j] = f2bf(t);
+        }
+        store_bf16x8(ds + base + vi * 8, o);
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int vi = c * 256 + tid;
+    if (vi < nvec) {
+      float* o = dw_part + static_cast<size_t>(blockIdx.x) * H + vi * 8;
+      *reinterpret_cast<f32x4*>(o) = f32x4{dwa[c][0], dwa[c][1], dwa[c][2], dwa[c][3]};
+      *reinterpret_cast<f32x4*>(o + 4) = f32x4{dwa[c][4], dwa[c][5], dwa[c][6], dwa[c][7]};
+      if constexpr (HAS_BIAS) {
+        float* ob = db_part + static_cast<size_t>(blockIdx.x) * H + vi * 8;
+        *reinterpret_cast<f32x4*>(ob) = f32x4{dba[c][0], dba[c][1], dba[c][2], dba[c][3]};
+        *reinterpret_cast<f32x4*>(ob + 4) = f32x4{dba[c][4], dba[c][5], dba[c][6], dba[c][7]};
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void norm_wgrad_reduce_kernel(const float* __restrict__ part,
+                                                                 int nparts, int H,
+                                                                 bf16_t* __restrict__ out) {
+  const int h = blockIdx.x * 256 + threadIdx.x;
+  if (h >= H) return;
+  float acc = 0.f;
+  for (int p = 0; p < nparts; ++p) acc += part[static_cast<size_t>(p) * H + h];
+  out[h] = f2bf(acc);
+}
+
+// ----------------------------------------------------------------------------------------------
+// launchers
+// ----------------------------------------------------------------------------------------------
+template <bool RMS, bool HAS_RES, bool HAS_BIAS>
+static void launch_fwd_nc(int nc, dim3 grid, hipStream_t st, const bf16_t* x, const bf16_t* r,
+                          bf16_t* so, const bf16_t* w, const bf16_t* b, bf16_t* y, float* rstd,
+                          float* mean, int rows, int H, float eps) {
+#define DLA_NORM_FWD(NC)                                                                 \
+  norm_fwd_kernel<NC, RMS, HAS_RES, HAS_BIAS>                                            \
+      <<<grid, 256, 0, st>>>(x, r, so, w, b, y, rstd, mean, rows, H, eps)
+  switch (nc) {
+    case 1: DLA_NORM_FWD(1); break;
+    case 2: DLA_NORM_FWD(2); break;
+    case 4: DLA_NORM_FWD(4); break;
+    case 8: DLA_NORM_FWD(8); break;
+    default: DLA_NORM_FWD(16); break;
+  }
+#undef DLA_NORM_FWD
+}
+
+static int chunks_for(int H, int threads) {
+  const int need = (H / 8 + threads - 1) / threads;
+  return need <= 1 ? 1 : need <= 2 ? 2 : need <= 4 ? 4 : need <= 8 ? 8 : 16;
+}
+
+void launch_norm_fwd(const bf16_t* x, const bf16_t* res, bf16_t* sum_out, const bf16_t* w,
+                     const bf16_t* b, bf16_t* y, float* rstd, float* mean, int rows, int H,
+                     float eps, bool rms, hipStream_t st) {
+  const int nc = chunks_for(H, 64);
+  dim3 grid((rows + 3) / 4);
+  const bool hr = res != nullptr, hb = b != nullptr;
+  if (rms) {
+    if (hr) launch_fwd_nc<true, true, false>(nc, grid, st, x, res, sum_out, w, b, y, rstd, mean, rows, H, eps);
+    else launch_fwd_nc<true, false, false>(nc, grid, st, x, res, sum_out, w, b, y, rstd, mean, rows, H, eps);
+  } else {
+    if (hr) {
+      if (hb) launch_fwd_nc<false, true, true>(nc, grid, st, x, res, sum_out, w, b, y, rstd, mean, rows, H, eps);
+      else launch_fwd_nc<false, true, false>(nc, grid, st, x, res, sum_out, w, b, y, rstd, mean, rows, H, eps);
+    } else {
+      if (hb) launch_fwd_nc<false, false, true>(nc, grid, st, x, res, sum_out, w, b, y, rstd, mean, rows, H, eps);
+      else launch_fwd_nc<false, false, false>(nc, grid, st, x, res, sum_out, w, b, y, rstd, mean, rows, H, eps);
+    }
+  }
+}
+
+int norm_bwd_grid(int rows) { return rows < 768 ? rows : 768; }
+
+template <bool RMS, bool HAS_DRES, bool HAS_BIAS>
+static void launch_bwd_t(int nc, int grid, hipStream_t st, const bf16_t* dy, const bf16_t* s,
+                         const bf16_t* w, const float* rstd, const float* mean,
+                         const bf16_t* dres, bf16_t* ds, float* dwp, float* dbp, int rows,
+                         int H) {
+#define DLA_NORM_BWD(NC)                                                                     \
+  norm_bwd_kernel<NC, RMS, HAS_DRES, HAS_BIAS>                                               \
+      <<<grid, 256, 0, st>>>(dy, s, w, rstd, mean, dres, ds, dwp, dbp, rows, H)
+  switch (nc) {
+    case 1: DLA_NORM_BWD(1); break;
+    case 2: DLA_NORM_BWD(2); break;
+    case 4: DLA_NORM_BWD(4); break;
+    case 8: DLA_NORM_BWD(8); break;
+    default: DLA_NORM_BWD(16); break;
+  }
+#undef DLA_NORM_BWD
+}
+
+void launch_norm_bwd(const bf16_t* dy, const bf16_t* s, const bf16_t* w, const float* rstd,
+                     const float* mean, const bf16_t* dres, bf16_t* ds, float* dw_part,
+                     float* db_part, bf16_t* dw, bf16_t* db, int rows, int H, bool rms,
+                     hipStream_t st) {
+  const int nc = chunks_for(H, 256);
+  const int grid = norm_bwd_grid(rows);
+  const bool hd = dres != nullptr, hb = db != nullptr;
+  if (rms) {
+    if (hd) launch_bwd_t<true, true, false>(nc, grid, st, dy, s, w, rstd, mean, dres, ds, dw_part, db_part, rows, H);
+    else launch_bwd_t<true, false, false>(nc, grid, st, dy, s, w, rstd, mean, dres, ds, dw_part, db_part, rows, H);
+  } else {
+    if (hd) {
+      if (hb) launch_bwd_t<false, true, true>(nc, grid, st, dy, s, w, rstd, mean, dres, ds, dw_part, db_part, rows, H);
+      else launch_bwd_t<false, true, false>(nc, grid, st, dy, s, w, rstd, mean, dres, ds, dw_part, db_part, rows, H);
+    } else {
+      if (hb) launch_bwd_t<false, false, true>(nc, grid, st, dy, s, w, rstd, mean, dres, ds, dw_part, db_part, rows, H);
+      else launch_bwd_t<false, false, false>(nc, grid, st, dy, s, w, rstd, mean, dres, ds, dw_part, db_part, rows, H);
+    }
+  }
+  const dim3 rg((H + 255) / 256);
+  norm_wgrad_reduce_kernel<<<rg, 256, 0, st>>>(dw_part, grid, H, dw);
+  if (hb) norm_wgrad_reduce_kernel<<<rg, 256, 0, st>>>(db_part, grid, H, db);
+}
+
+}  // namespace dla

@@ -1,0 +1,70 @@
+"""Scalar reward model: native backbone + Dropout + Linear(H, 1) head.
+
+Mirrors src/models/reward_model.py:38-64: `backbone` is the headless decoder (HF AutoModel
+layout), `scorer = Sequential(Dropout(p), Linear(H, 1))`, pooling `last_token` (index
+`mask.sum - 1` for right padding; generalised here to the last valid position for left padding
+too) or `mean` (masked mean). Checkpoint keys: `backbone.*` + `scorer.1.weight` / `scorer.1.bias`.
+"""
+from __future__ import annotations
+
+from typing import Dict
+
+import torch
+import torch.nn as nn
+
+from .transformer import CausalLM, attention_layout
+
+
+class RewardModel(nn.Module):
+    def __init__(self, backbone: CausalLM, pooling: str = "last_token", dropout: float = 0.1):
+        super().__init__()
+        if pooling not in ("last_token", "mean"):
+            raise ValueError(f"pooling must be last_token|mean, got {pooling!r}")
+        self.backbone = backbone
+        self.pooling = pooling
+        H = backbone.cfg.hidden_size
+        dev, dt = backbone.embed.device, backbone.embed.dtype
+        self.scorer = nn.Sequential(nn.Dropout(dropout), nn.Linear(H, 1, device=dev, dtype=dt))
+        with torch.no_grad():
+            nn.init.normal_(self.scorer[1].weight, std=1.0 / (H + 1) ** 0.5)
+            self.scorer[1].bias.zero_()
+
+    def pool(self, hidden: torch.Tensor, attention_mask: torch.Tensor) -> torch.Tensor:
+        if attention_mask is None:
+            return hidden[:, -1] if self.pooling == "last_token" else hidden.mean(1)
+        if self.pooling == "last_token":
+            _, end, _ = attention_layout(attention_mask)
+            idx = (end.long() - 1).clamp(min=0)
+            return hidden[torch.arange(hidden.shape[0], device=hidden.device), idx]
+        m = attention_mask.to(hidden.dtype).unsqueeze(-1)
+        return (hidden * m).sum(1) / attention_mask.sum(1, keepdim=True).clamp(min=1).to(hidden.dtype)
+
+    def forward(self, input_ids: torch.Tensor, attention_mask: torch.Tensor = None) -> torch.Tensor:
+        h = self.backbone(input_ids, attention_mask)
+        return self.scorer(self.pool(h, attention_mask)).squeeze(-1).float()
+
+    def hf_state_dict(self) -> Dict[str, torch.Tensor]:
+        from .hf_io import to_hf_state_dict
+
+        sd = {f"backbone.{k}": v for k, v in to_hf_state_dict(self.backbone, base=True).items()}
+        sd["scorer.1.weight"] = self.scorer[1].weight.detach()
+        sd["scorer.1.bias"] = self.scorer[1].bias.detach()
+        return sd
+
+    @torch.no_grad()
+    def load_hf_state_dict(self, sd: Dict[str, torch.Tensor], strict: bool = True):
+        from .hf_io import load_hf_state_dict
+
+        sd = {(k[len("module."):] if k.startswith("module.") else k): v for k, v in sd.items()}
+        bb = {k[len("backbone."):]: v for k, v in sd.items() if k.startswith("backbone.")}
+        missing, unexpected = load_hf_state_dict(self.backbone, bb, strict=False, base=True)
+        missing = [m for m in missing if not m.startswith("lm_head")]
+        for name in ("weight", "bias"):
+            key = f"scorer.1.{name}"
+            if key in sd:
+                getattr(self.scorer[1], name).copy_(sd[key].to(self.scorer[1].weight.dtype))
+            else:
+                missing.append(key)
+        if strict and missing:
+            raise KeyError(f"reward checkpoint missing keys: {missing[:8]}")
+        return missing, unexpected

@@ -1,0 +1,325 @@
+"""Native decoder-only transformer for every model family the reference touches.
+
+One implementation, configured by `ModelConfig`, covers Llama-3 / Mistral (RMSNorm, GQA, RoPE,
+SwiGLU, optional sliding window), Mixtral (top-k routed SwiGLU experts), GPT-2 (LayerNorm,
+learned positions, GELU, tied head) and phi-2 (parallel attn+MLP block, partial rotary, biases).
+It replaces the HF modeling code the reference runs through `AutoModelForCausalLM`
+(src/models/base_model.py:17-42) with the gfx950 op set of `..ops`:
+
+  layer:  (h, s) = add_norm(x, s)          HIP fused residual-add + norm
+          qkv    = h @ Wqkv^T              ONE fused QKV GEMM (hipBLASLt)
+          a      = qkv_attention(qkv)      HIP RoPE + HIP flash attention (fwd/bwd)
+          x      = a @ Wo^T
+          (h, s) = add_norm(x, s)
+          x      = down(swiglu(h @ Wgu^T)) ONE fused gate|up GEMM + HIP SwiGLU
+Parameters are stored fused (`qkv_proj`, `gate_up_proj`); `hf_state_dict()` /
+`load_hf_state_dict()` convert to/from the HF key layout the reference checkpoints use.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+from torch.utils.checkpoint import checkpoint
+
+from .. import ops
+from .config import ModelConfig
+
+
+def _param(*shape, device=None, dtype=None) -> nn.Parameter:
+    return nn.Parameter(torch.empty(*shape, device=device, dtype=dtype))
+
+
+def attention_layout(attention_mask: Optional[torch.Tensor]):
+    """From a [B, T] 0/1 mask with one contiguous valid span per row (left or right padding)
+    return (kv_start, kv_end, positions) on device, no host sync."""
+    if attention_mask is None:
+        return None, None, None
+    m = attention_mask.to(torch.int32)
+    first = (m.cumsum(1) == 0).sum(1).to(torch.int32)
+    end = first + m.sum(1).to(torch.int32)
+    T = m.shape[1]
+    pos = (torch.arange(T, device=m.device, dtype=torch.int32).unsqueeze(0) - first.unsqueeze(1)).clamp(min=0)
+    return first, end, pos
+
+
+class Attention(nn.Module):
+    def __init__(self, cfg: ModelConfig, device=None, dtype=None):
+        super().__init__()
+        self.cfg = cfg
+        H = cfg.hidden_size
+        self.qkv_proj = _param(cfg.q_size + 2 * cfg.kv_size, H, device=device, dtype=dtype)
+        self.qkv_bias = _param(cfg.q_size + 2 * cfg.kv_size, device=device, dtype=dtype) if cfg.attn_bias else None
+        self.o_proj = _param(H, cfg.q_size, device=device, dtype=dtype)
+        o_bias = cfg.attn_bias and cfg.arch in ("gpt2", "phi")
+        self.o_bias = _param(H, device=device, dtype=dtype) if o_bias else None
+
+    def forward(self, h, rope, kv_start, kv_end, positions, cache=None, layer_idx=0):
+        cfg = self.cfg
+        qkv = F.linear(h, self.qkv_proj, self.qkv_bias)
+        window = cfg.sliding_window if cfg.sliding_window else 0
+        if cache is None:
+            a = ops.qkv_attention(qkv, cfg.num_heads, cfg.num_kv_heads, cfg.head_dim, rope,
+                                  causal=True, window=window, kv_start=kv_start, kv_end=kv_end,
+                                  positions=positions)
+        else:
+            a = cache.attend(layer_idx, qkv, rope, window)
+        return F.linear(a, self.o_proj, self.o_bias)
+
+
+class MLP(nn.Module):
+    def __init__(self, cfg: ModelConfig, device=None, dtype=None):
+        super().__init__()
+        self.cfg = cfg
+        H, Fd = cfg.hidden_size, cfg.intermediate_size
+        if cfg.activation == "swiglu":
+            self.up_proj = _param(2 * Fd, H, device=device, dtype=dtype)  # [gate; up]
+        else:
+            self.up_proj = _param(Fd, H, device=device, dtype=dtype)
+        self.up_bias = _param(self.up_proj.shape[0], device=device, dtype=dtype) if cfg.mlp_bias else None
+        self.down_proj = _param(H, Fd, device=device, dtype=dtype)
+        self.down_bias = _param(H, device=device, dtype=dtype) if cfg.mlp_bias else None
+
+    def forward(self, h):
+        u = F.linear(h, self.up_proj, self.up_bias)
+        m = ops.swiglu(u) if self.cfg.activation == "swiglu" else ops.gelu_new(u)
+        return F.linear(m, self.down_proj, self.down_bias)
+
+
+class MoE(nn.Module):
+    """Top-k routed SwiGLU experts (Mixtral). Softmax router in fp32, top-k renormalised,
+    dropless token dispatch (sort by expert, one GEMM pair per expert, weighted scatter-add).
+    Under expert parallelism `ep_group` routes tokens with all-to-all (see parallel.expert)."""
+
+    def __init__(self, cfg: ModelConfig, device=None, dtype=None):
+        super().__init__()
+        self.cfg = cfg
+        H, Fd, E = cfg.hidden_size, cfg.intermediate_size, cfg.num_experts
+        self.router = _param(E, H, device=device, dtype=dtype)
+        self.expert_up = _param(E, 2 * Fd, H, device=device, dtype=dtype)
+        self.expert_down = _param(E, H, Fd, device=device, dtype=dtype)
+        self.ep = None  # set by parallel.expert.shard_experts
+        self.last_aux_loss = None
+
+    def route(self, h2: torch.Tensor):
+        logits = F.linear(h2, self.router).float()
+        probs = torch.softmax(logits, dim=-1)
+        topv, topi = torch.topk(probs, self.cfg.num_experts_per_tok, dim=-1)
+        topv = topv / topv.sum(-1, keepdim=True)
+        if self.training and self.cfg.router_aux_loss_coef > 0:
+            E = self.cfg.num_experts
+            frac = F.one_hot(topi, E).float().sum(1).mean(0)
+            self.last_aux_loss = E * (frac * probs.mean(0)).sum() * self.cfg.router_aux_loss_coef
+        return topv, topi
+
+    def expert_ffn(self, e: int, x: torch.Tensor) -> torch.Tensor:
+        return F.linear(ops.swiglu(F.linear(x, self.expert_up[e])), self.expert_down[e])
+
+    def forward(self, h):
+        shp = h.shape
+        h2 = h.reshape(-1, shp[-1])
+        topv, topi = self.route(h2)
+        if self.ep is not None:
+            out = self.ep.dispatch_combine(self, h2, topv, topi)
+            return out.view(shp)
+        k = self.cfg.num_experts_per_tok
+        flat_e = topi.reshape(-1)
+        order = torch.argsort(flat_e, stable=True)
+        tok = order // k
+        counts = torch.bincount(flat_e, minlength=self.cfg.num_experts).tolist()
+        xs = h2.index_select(0, tok)
+        w = topv.reshape(-1).index_select(0, order).to(h.dtype).unsqueeze(-1)
+        outs = []
+        start = 0
+        for e, c in enumerate(counts):
+            if c:
+                outs.append(self.expert_ffn(e, xs[start:start + c]))
+            start += c
+        ys = torch.cat(outs, 0) * w
+        out = torch.zeros_like(h2).index_add_(0, tok, ys)
+        return out.view(shp)
+
+
+class DecoderLayer(nn.Module):
+    def __init__(self, cfg: ModelConfig, device=None, dtype=None):
+        super().__init__()
+        self.cfg = cfg
+        H = cfg.hidden_size
+        bias = cfg.norm_type == "layer"
+        self.ln1_w = _param(H, device=device, dtype=dtype)
+        self.ln1_b = _param(H, device=device, dtype=dtype) if bias else None
+        if not cfg.parallel_block:
+            self.ln2_w = _param(H, device=device, dtype=dtype)
+            self.ln2_b = _param(H, device=device, dtype=dtype) if bias else None
+        self.attn = Attention(cfg, device, dtype)
+        self.mlp = MoE(cfg, device, dtype) if cfg.is_moe else MLP(cfg, device, dtype)
+
+    def forward(self, x, resid, rope, kv_start, kv_end, positions, cache=None, layer_idx=0):
+        cfg = self.cfg
+        rms = cfg.norm_type == "rms"
+        h, resid = ops.add_norm(x, resid, self.ln1_w, self.ln1_b, cfg.norm_eps, rms)
+        a = self.attn(h, rope, kv_start, kv_end, positions, cache, layer_idx)
+        if cfg.parallel_block:
+            return a + self.mlp(h), resid
+        h, resid = ops.add_norm(a, resid, self.ln2_w, self.ln2_b, cfg.norm_eps, rms)
+        return self.mlp(h), resid
+
+
+class CausalLM(nn.Module):
+    """Decoder-only LM. forward() returns the final normed hidden states [B, T, H]; the LM head
+    is applied by the fused log-prob / CE ops (or `logits()` for generation)."""
+
+    def __init__(self, cfg: ModelConfig, device=None, dtype=None, headless: bool = False):
+        super().__init__()
+        self.cfg = cfg
+        self.headless = headless
+        H, V = cfg.hidden_size, cfg.vocab_size
+        self.embed = _param(V, H, device=device, dtype=dtype)
+        self.wpe = _param(cfg.max_position_embeddings, H, device=device, dtype=dtype) if cfg.learned_pos_emb else None
+        self.layers = nn.ModuleList([DecoderLayer(cfg, device, dtype) for _ in range(cfg.num_layers)])
+        self.norm_w = _param(H, device=device, dtype=dtype)
+        self.norm_b = _param(H, device=device, dtype=dtype) if cfg.norm_type == "layer" else None
+        self.lm_head = None if (cfg.tie_word_embeddings or headless) else _param(V, H, device=device, dtype=dtype)
+        self.lm_head_bias = _param(V, device=device, dtype=dtype) if (cfg.lm_head_bias and not headless) else None
+        self.rope = (ops.RotaryCache(cfg.rot_dim, cfg.rope_theta, cfg.max_position_embeddings,
+                                     cfg.rope_scaling) if cfg.rot_dim > 0 else None)
+        self.gradient_checkpointing = False
+
+    # --------------------------------------------------------------------------------- init
+    @torch.no_grad()
+    def init_weights(self, seed: int = 0):
+        """Deterministic random init (identical on every rank -> no broadcast needed)."""
+        dev = self.embed.device
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(seed)
+        std = self.cfg.init_std
+        out_std = std / math.sqrt(2 * self.cfg.num_layers)
+        for name, p in self.named_parameters():
+            if p.dim() == 1:
+                if name.endswith(("ln1_w", "ln2_w", "norm_w")):
+                    p.fill_(1.0)
+                else:
+                    p.zero_()
+            else:
+                s = out_std if name.endswith(("o_proj", "down_proj", "expert_down")) else std
+                p.copy_(torch.randn(p.shape, generator=gen, device=dev, dtype=torch.float32).mul_(s).to(p.dtype)
+                        if p.numel() < (1 << 26) else _chunked_randn(p, gen, s))
+        return self
+
+    def gradient_checkpointing_enable(self):
+        self.gradient_checkpointing = True
+
+    def gradient_checkpointing_disable(self):
+        self.gradient_checkpointing = False
+
+    # ------------------------------------------------------------------------------ forward
+    @property
+    def head_weight(self) -> torch.Tensor:
+        return self.embed if self.lm_head is None else self.lm_head
+
+    def embed_tokens(self, input_ids, positions=None):
+        x = F.embedding(input_ids, self.embed)
+        if self.wpe is not None:
+            T = input_ids.shape[1]
+            pos = positions.long() if positions is not None else torch.arange(T, device=input_ids.device)
+            x = x + F.embedding(pos, self.wpe)
+        return x
+
+    def forward(self, input_ids: torch.Tensor, attention_mask: Optional[torch.Tensor] = None,
+                cache=None) -> torch.Tensor:
+        if cache is not None:
+            return self._forward_cached(input_ids, attention_mask, cache)
+        kv_start, kv_end, positions = attention_layout(attention_mask)
+        x = self.embed_tokens(input_ids, positions)
+        resid = None
+        for layer in self.layers:
+            if self.gradient_checkpointing and self.training and torch.is_grad_enabled():
+                x, resid = checkpoint(layer, x, resid, self.rope, kv_start, kv_end, positions,
+                                      use_reentrant=False)
+            else:
+                x, resid = layer(x, resid, self.rope, kv_start, kv_end, positions)
+        h, _ = ops.add_norm(x, resid, self.norm_w, self.norm_b, self.cfg.norm_eps,
+                            self.cfg.norm_type == "rms")
+        return h
+
+    def _forward_cached(self, input_ids, attention_mask, cache):
+        positions = cache.positions_for(input_ids.shape[1])
+        x = self.embed_tokens(input_ids, positions)
+        resid = None
+        for i, layer in enumerate(self.layers):
+            x, resid = layer(x, resid, self.rope, None, None, None, cache, i)
+        h, _ = ops.add_norm(x, resid, self.norm_w, self.norm_b, self.cfg.norm_eps,
+                            self.cfg.norm_type == "rms")
+        cache.advance(input_ids.shape[1])
+        return h
+
+    def logits(self, hidden: torch.Tensor) -> torch.Tensor:
+        return F.linear(hidden, self.head_weight, self.lm_head_bias)
+
+    def aux_loss(self):
+        if not self.cfg.is_moe:
+            return None
+        terms = [l.mlp.last_aux_loss for l in self.layers if l.mlp.last_aux_loss is not None]
+        return sum(terms) if terms else None
+
+    # ----------------------------------------------------------------- objective helpers
+    def sequence_logprob(self, input_ids, attention_mask=None, reduction: str = "mean"):
+        """Reference `compute_logprobs` (train_dpo.py:31-39): masked mean log p per sequence."""
+        h = self.forward(input_ids, attention_mask)
+        if self.lm_head_bias is not None:
+            return _biased_seq_logprob(self, h, input_ids, attention_mask, reduction)
+        return ops.sequence_logprob(h, self.head_weight, input_ids, attention_mask, reduction)
+
+    def causal_lm_loss(self, input_ids, labels, attention_mask=None):
+        """HF ForCausalLMLoss (train_sft.py:145-146): mean token NLL over labels != -100."""
+        h = self.forward(input_ids, attention_mask)
+        if self.lm_head_bias is not None:
+            lg = self.logits(h).float()
+            return F.cross_entropy(lg[:, :-1].reshape(-1, lg.shape[-1]), labels[:, 1:].reshape(-1),
+                                   ignore_index=-100)
+        return ops.token_nll(h, self.head_weight, labels)
+
+    # ----------------------------------------------------------------- HF key mapping
+    def hf_state_dict(self) -> Dict[str, torch.Tensor]:
+        from .hf_io import to_hf_state_dict
+
+        return to_hf_state_dict(self)
+
+    def load_hf_state_dict(self, sd: Dict[str, torch.Tensor], strict: bool = True):
+        from .hf_io import load_hf_state_dict
+
+        return load_hf_state_dict(self, sd, strict=strict)
+
+
+def _chunked_randn(p: torch.Tensor, gen: torch.Generator, std: float) -> torch.Tensor:
+    flat = p.view(-1)
+    step = 1 << 24
+    for s in range(0, flat.numel(), step):
+        e = min(flat.numel(), s + step)
+        flat[s:e] = torch.randn(e - s, generator=gen, device=p.device, dtype=torch.float32).mul_(std).to(p.dtype)
+    return p
+
+
+def _biased_seq_logprob(model, h, input_ids, attention_mask, reduction):
+    lg = model.logits(h).float()
+    tgt, mask = ops.shifted_targets(input_ids, attention_mask)
+    lp = torch.log_softmax(lg, -1).gather(-1, tgt.clamp(min=0).unsqueeze(-1)).squeeze(-1)
+    lp = torch.where(tgt >= 0, lp, torch.zeros_like(lp))
+    return ops.seq_reduce(lp, mask, mean=(reduction == "mean"))
+
+
+def default_dtype(device) -> torch.dtype:
+    """bf16 on the GPU, fp32 on CPU (the reference: bf16 if CUDA else fp32, base_model.py:27-29)."""
+    return torch.bfloat16 if (device is not None and torch.device(device).type == "cuda") else torch.float32
+
+
+def build_model(cfg: ModelConfig, device=None, dtype=None, seed: int = 0, init: bool = True,
+                headless: bool = False) -> CausalLM:
+    dtype = dtype or default_dtype(device)
+    model = CausalLM(cfg, device=device, dtype=dtype, headless=headless)
+    if init:
+        model.init_weights(seed)
+    return model

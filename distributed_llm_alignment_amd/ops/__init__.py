@@ -1,0 +1,15 @@
+"""gfx950 compute ops. GPU tensors run the in-tree HIP kernels (`torch.ops.dla.*`); CPU tensors
+run the pure-PyTorch references (test tier / numerics oracles)."""
+from . import _ext
+from .activations import gelu_new, swiglu
+from .attention import RotaryCache, attention_core, qkv_attention, ref_attention
+from .logprob import linear_logprob, seq_reduce, sequence_logprob, shifted_targets, token_nll
+from .losses import dpo_loss, ensemble_kl, kl_penalty_pg, pairwise_loss
+from .norm import add_norm, layer_norm, rms_norm
+
+__all__ = [
+    "_ext", "gelu_new", "swiglu", "RotaryCache", "attention_core", "qkv_attention",
+    "ref_attention", "linear_logprob", "seq_reduce", "sequence_logprob", "shifted_targets",
+    "token_nll", "dpo_loss", "ensemble_kl", "kl_penalty_pg", "pairwise_loss", "add_norm",
+    "layer_norm", "rms_norm",
+]

@@ -1,0 +1,288 @@
+"""Rotary embedding + flash attention.
+
+Entry points
+  * `qkv_attention(qkv, ...)`: the training/prefill path. Takes the fused QKV projection output
+    `[B, T, (Hq + 2*Hkv) * D]` and returns `[B, T, Hq * D]` (ready for o_proj). On the GPU this
+    is ONE autograd node: HIP RoPE -> HIP flash-attention forward; the backward runs the HIP
+    flash-attention backward and the HIP RoPE backward and returns a single fused dQKV buffer
+    (dV is written in place by the attention kernel, dQ/dK un-rotated straight into it).
+  * `attention_core(q, k, v, ...)`: [B, T, H, D] tensors (KV-cache decode, odd head dims).
+  * `RotaryCache`: host-precomputed fp32 cos/sin tables (HF `rotate_half` convention, optional
+    partial rotary and Llama-3.1 frequency scaling).
+
+Masking semantics (all paths, matching HF SDPA with a causal + padding mask): key j is visible
+to query i of batch b iff kv_start[b] <= j < kv_end[b], and for causal attention
+j <= i + causal_off (causal_off = Tk - Tq), and with a sliding window j > i + causal_off - window.
+Fully-masked query rows produce zeros.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, Optional
+
+import torch
+import torch.nn.functional as F
+
+from . import _ext
+
+
+class RotaryCache:
+    """cos/sin tables [max_pos, rot_dim/2] in fp32, one copy per device."""
+
+    def __init__(self, rot_dim: int, theta: float = 10000.0, max_pos: int = 4096,
+                 scaling: Optional[dict] = None):
+        self.rot_dim = rot_dim
+        self.theta = theta
+        self.max_pos = max_pos
+        inv = 1.0 / (theta ** (torch.arange(0, rot_dim, 2, dtype=torch.float64) / rot_dim))
+        if scaling and scaling.get("rope_type", scaling.get("type")) == "llama3":
+            factor = scaling.get("factor", 8.0)
+            lo = scaling.get("low_freq_factor", 1.0)
+            hi = scaling.get("high_freq_factor", 4.0)
+            old = scaling.get("original_max_position_embeddings", 8192)
+            lo_wl, hi_wl = old / lo, old / hi
+            wl = 2 * math.pi / inv
+            scaled = torch.where(wl > lo_wl, inv / factor, inv)
+            smooth = (old / wl - lo) / (hi - lo)
+            mid = (1 - smooth) * scaled / factor + smooth * scaled
+            is_mid = (wl >= hi_wl) & (wl <= lo_wl)
+            inv = torch.where(is_mid, mid, scaled)
+        elif scaling and scaling.get("rope_type", scaling.get("type")) == "linear":
+            inv = inv / scaling.get("factor", 1.0)
+        t = torch.arange(max_pos, dtype=torch.float64)
+        freqs = torch.outer(t, inv)
+        self._cos = freqs.cos().float()
+        self._sin = freqs.sin().float()
+        self._dev: Dict[torch.device, tuple] = {}
+
+    def tables(self, device: torch.device):
+        device = torch.device(device)
+        if device.type == "cpu":
+            return self._cos, self._sin
+        if device not in self._dev:
+            self._dev[device] = (self._cos.to(device), self._sin.to(device))
+        return self._dev[device]
+
+
+# ---------------------------------------------------------------------------------------------
+# pure-PyTorch reference (CPU path + numerics oracle)
+# ---------------------------------------------------------------------------------------------
+def _ref_rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, pos: torch.Tensor,
+              rot: int) -> torch.Tensor:
+    """x [B, T, H, D]; pos [B, T] long. rotate-half over the first `rot` dims."""
+    xf = x.float()
+    c = cos[pos].unsqueeze(2)  # [B, T, 1, rot/2]
+    s = sin[pos].unsqueeze(2)
+    half = rot // 2
+    x1, x2, rest = xf[..., :half], xf[..., half:rot], xf[..., rot:]
+    o1 = x1 * c - x2 * s
+    o2 = x2 * c + x1 * s
+    return torch.cat([o1, o2, rest], dim=-1).to(x.dtype)
+
+
+def _visibility(B, Tq, Tk, causal, causal_off, window, kv_start, kv_end, device):
+    qi = torch.arange(Tq, device=device).view(1, Tq, 1)
+    kj = torch.arange(Tk, device=device).view(1, 1, Tk)
+    ok = torch.ones(B, Tq, Tk, dtype=torch.bool, device=device)
+    if kv_start is not None:
+        ok = ok & (kj >= kv_start.view(B, 1, 1).to(device))
+    if kv_end is not None:
+        ok = ok & (kj < kv_end.view(B, 1, 1).to(device))
+    if causal:
+        ok = ok & (kj <= qi + causal_off)
+        if window and window > 0:
+            ok = ok & (kj > qi + causal_off - window)
+    return ok
+
+
+def ref_attention(q, k, v, scale, causal=True, causal_off=0, window=0, kv_start=None,
+                  kv_end=None) -> torch.Tensor:
+    """q [B, Tq, Hq, D], k/v [B, Tk, Hkv, D] -> [B, Tq, Hq, D] (fp32 math)."""
+    B, Tq, Hq, D = q.shape
+    Tk, Hkv = k.shape[1], k.shape[2]
+    rep = Hq // Hkv
+    qf = q.float().transpose(1, 2)
+    kf = k.float().transpose(1, 2).repeat_interleave(rep, dim=1)
+    vf = v.float().transpose(1, 2).repeat_interleave(rep, dim=1)
+    s = torch.matmul(qf, kf.transpose(-1, -2)) * scale
+    ok = _visibility(B, Tq, Tk, causal, causal_off, window, kv_start, kv_end, q.device)
+    s = s.masked_fill(~ok.unsqueeze(1), float("-inf"))
+    p = torch.softmax(s, dim=-1)
+    p = torch.nan_to_num(p, nan=0.0)
+    o = torch.matmul(p, vf).transpose(1, 2)
+    return o.to(q.dtype)
+
+
+# ---------------------------------------------------------------------------------------------
+# GPU autograd nodes
+# ---------------------------------------------------------------------------------------------
+def _i32(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+    return None if t is None else t.to(dtype=torch.int32).contiguous()
+
+
+class _FusedQKVAttnFn(torch.autograd.Function):
+    """qkv [B, T, C] -> o [B, T, Hq*D]; RoPE (optional) fused in; returns one dqkv."""
+
+    @staticmethod
+    def forward(ctx, qkv, cos, sin, pos, Hq, Hkv, D, rot, scale, causal, window, kv_start, kv_end):
+        ops = _ext.require()
+        B, T, C = qkv.shape
+        q2 = qkv.reshape(B * T, C)
+        if rot > 0:
+            q_r, k_r = ops.rope_fwd(q2, cos, sin, pos, Hq, Hkv, D, rot, T, 0)
+            q4 = q_r.view(B, T, Hq, D)
+            k4 = k_r.view(B, T, Hkv, D)
+        else:
+            q4 = qkv.as_strided((B, T, Hq, D), (T * C, C, D, 1), qkv.storage_offset())
+            k4 = qkv.as_strided((B, T, Hkv, D), (T * C, C, D, 1), qkv.storage_offset() + Hq * D)
+        v4 = qkv.as_strided((B, T, Hkv, D), (T * C, C, D, 1), qkv.storage_offset() + (Hq + Hkv) * D)
+        o, lse2 = ops.attn_fwd(q4, k4, v4, float(scale), bool(causal), 0, int(window), kv_start, kv_end)
+        ctx.save_for_backward(qkv, q4 if rot > 0 else None, k4 if rot > 0 else None, o, lse2,
+                              cos, sin, pos, kv_start, kv_end)
+        ctx.cfg = (B, T, C, Hq, Hkv, D, rot, scale, causal, window)
+        return o.view(B, T, Hq * D)
+
+    @staticmethod
+    def backward(ctx, do):
+        ops = _ext.require()
+        qkv, q4, k4, o, lse2, cos, sin, pos, kv_start, kv_end = ctx.saved_tensors
+        B, T, C, Hq, Hkv, D, rot, scale, causal, window = ctx.cfg
+        off = qkv.storage_offset()
+        if rot == 0:
+            q4 = qkv.as_strided((B, T, Hq, D), (T * C, C, D, 1), off)
+            k4 = qkv.as_strided((B, T, Hkv, D), (T * C, C, D, 1), off + Hq * D)
+        v4 = qkv.as_strided((B, T, Hkv, D), (T * C, C, D, 1), off + (Hq + Hkv) * D)
+        do4 = do.contiguous().view(B, T, Hq, D)
+        dqkv = torch.empty((B, T, C), dtype=qkv.dtype, device=qkv.device)
+        dv = dqkv.as_strided((B, T, Hkv, D), (T * C, C, D, 1), (Hq + Hkv) * D)
+        if rot > 0:
+            dk = torch.empty((B, T, Hkv, D), dtype=qkv.dtype, device=qkv.device)
+        else:
+            dk = dqkv.as_strided((B, T, Hkv, D), (T * C, C, D, 1), Hq * D)
+        dq32 = ops.attn_bwd(do4, q4, k4, v4, o, lse2, dk, dv, float(scale), bool(causal), 0,
+                            int(window), kv_start, kv_end)
+        d2 = dqkv.view(B * T, C)
+        if rot > 0:
+            dq = dq32.to(torch.bfloat16).view(B * T, Hq * D)
+            ops.rope_bwd(dq, dk.view(B * T, Hkv * D), d2, cos, sin, pos, Hq, Hkv, D, rot, T, 0)
+        else:
+            ops.f32_to_bf16_rows(dq32.view(B * T, Hq * D), d2[:, : Hq * D])
+        return dqkv, None, None, None, None, None, None, None, None, None, None, None, None
+
+
+class _AttnCoreFn(torch.autograd.Function):
+    """[B, T, H, D] q/k/v -> o. Used for KV-cache decode and padded head dims."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, scale, causal, causal_off, window, kv_start, kv_end):
+        ops = _ext.require()
+        o, lse2 = ops.attn_fwd(q, k, v, float(scale), bool(causal), int(causal_off), int(window),
+                               kv_start, kv_end)
+        ctx.save_for_backward(q, k, v, o, lse2, kv_start, kv_end)
+        ctx.cfg = (scale, causal, causal_off, window)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        ops = _ext.require()
+        q, k, v, o, lse2, kv_start, kv_end = ctx.saved_tensors
+        scale, causal, causal_off, window = ctx.cfg
+        dk = torch.empty_like(k, memory_format=torch.contiguous_format)
+        dv = torch.empty_like(v, memory_format=torch.contiguous_format)
+        dq32 = ops.attn_bwd(do.contiguous(), q, k, v, o, lse2, dk, dv, float(scale), bool(causal),
+                            int(causal_off), int(window), kv_start, kv_end)
+        return dq32.to(q.dtype), dk, dv, None, None, None, None, None, None
+
+
+def _pad_d(x: torch.Tensor, Dp: int) -> torch.Tensor:
+    return F.pad(x, (0, Dp - x.shape[-1]))
+
+
+def attention_core(q, k, v, scale=None, causal=True, causal_off=None, window=0, kv_start=None,
+                   kv_end=None) -> torch.Tensor:
+    """q [B, Tq, Hq, D], k/v [B, Tk, Hkv, D] (unit stride on D) -> [B, Tq, Hq, D]."""
+    D = q.shape[-1]
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    if causal_off is None:
+        causal_off = k.shape[1] - q.shape[1]
+    if not _ext.use_native(q):
+        return ref_attention(q, k, v, scale, causal, causal_off, window, kv_start, kv_end)
+    ks, ke = _i32(kv_start), _i32(kv_end)
+    if D in (64, 128):
+        return _AttnCoreFn.apply(q, k, v, scale, causal, causal_off, window, ks, ke)
+    Dp = 64 if D < 64 else 128
+    o = _AttnCoreFn.apply(_pad_d(q, Dp), _pad_d(k, Dp), _pad_d(v, Dp), scale, causal, causal_off,
+                          window, ks, ke)
+    return o[..., :D]
+
+
+def apply_rope(x: torch.Tensor, rope: RotaryCache, positions: torch.Tensor) -> torch.Tensor:
+    """x [B, T, H, D] -> rotated (reference math; used on small decode tensors and CPU)."""
+    cos, sin = rope.tables(x.device)
+    return _ref_rope(x, cos, sin, positions.long(), rope.rot_dim)
+
+
+def qkv_attention(qkv: torch.Tensor, Hq: int, Hkv: int, D: int, rope: Optional[RotaryCache],
+                  causal: bool = True, window: int = 0, kv_start=None, kv_end=None,
+                  positions: Optional[torch.Tensor] = None, scale: Optional[float] = None
+                  ) -> torch.Tensor:
+    """Fused QKV -> (RoPE) -> attention. qkv [B, T, (Hq+2Hkv)*D] -> [B, T, Hq*D]."""
+    B, T, C = qkv.shape
+    assert C == (Hq + 2 * Hkv) * D, "qkv width mismatch"
+    if rope is not None and T > rope.max_pos:
+        raise ValueError(f"sequence length {T} exceeds the rotary table ({rope.max_pos})")
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    rot = rope.rot_dim if rope is not None else 0
+    if not _ext.use_native(qkv):
+        q = qkv[..., : Hq * D].reshape(B, T, Hq, D)
+        k = qkv[..., Hq * D:(Hq + Hkv) * D].reshape(B, T, Hkv, D)
+        v = qkv[..., (Hq + Hkv) * D:].reshape(B, T, Hkv, D)
+        if rope is not None:
+            pos = positions if positions is not None else torch.arange(T, device=qkv.device).expand(B, T)
+            q = apply_rope(q, rope, pos)
+            k = apply_rope(k, rope, pos)
+        o = ref_attention(q, k, v, scale, causal, 0, window, kv_start, kv_end)
+        return o.reshape(B, T, Hq * D)
+    ks, ke = _i32(kv_start), _i32(kv_end)
+    pos32 = _i32(positions.reshape(-1)) if positions is not None else None
+    if D in (64, 128):
+        if rope is not None:
+            cos, sin = rope.tables(qkv.device)
+        else:
+            cos = sin = torch.empty(0, device=qkv.device)
+        return _FusedQKVAttnFn.apply(qkv.contiguous(), cos, sin, pos32, Hq, Hkv, D, rot, scale,
+                                     causal, window, ks, ke)
+    # odd head dims (e.g. phi-2 D=80): reference RoPE glue + padded native attention core
+    q = qkv[..., : Hq * D].reshape(B, T, Hq, D)
+    k = qkv[..., Hq * D:(Hq + Hkv) * D].reshape(B, T, Hkv, D)
+    v = qkv[..., (Hq + Hkv) * D:].reshape(B, T, Hkv, D)
+    if rope is not None:
+        pos = positions if positions is not None else torch.arange(T, device=qkv.device).expand(B, T)
+        q = apply_rope(q, rope, pos)
+        k = apply_rope(k, rope, pos)
+    o = attention_core(q, k, v, scale, causal, 0, window, kv_start, kv_end)
+    return o.reshape(B, T, Hq * D)
+
+
+def rope_qk(qkv: torch.Tensor, rope: Optional[RotaryCache], Hq: int, Hkv: int, D: int,
+            positions: Optional[torch.Tensor] = None, pos_offset: int = 0):
+    """Inference helper (no autograd): qkv [B, T, C] -> rotated q [B,T,Hq,D], k [B,T,Hkv,D] and
+    the v view [B,T,Hkv,D]. positions [B, T] (or t + pos_offset when None)."""
+    B, T, C = qkv.shape
+    v = qkv[..., (Hq + Hkv) * D:].reshape(B, T, Hkv, D)
+    if rope is not None and T + pos_offset > rope.max_pos:
+        raise ValueError("positions exceed the rotary table")
+    if rope is None:
+        return (qkv[..., : Hq * D].reshape(B, T, Hq, D),
+                qkv[..., Hq * D:(Hq + Hkv) * D].reshape(B, T, Hkv, D), v)
+    if _ext.use_native(qkv) and D % 8 == 0 and rope.rot_dim % 16 == 0:
+        cos, sin = rope.tables(qkv.device)
+        pos32 = _i32(positions.reshape(-1)) if positions is not None else None
+        q, k = _ext.require().rope_fwd(qkv.reshape(B * T, C).contiguous(), cos, sin, pos32, Hq, Hkv,
+                                       D, rope.rot_dim, T, int(pos_offset))
+        return q.view(B, T, Hq, D), k.view(B, T, Hkv, D), v
+    if positions is None:
+        positions = (torch.arange(T, device=qkv.device) + pos_offset).expand(B, T)
+    q = apply_rope(qkv[..., : Hq * D].reshape(B, T, Hq, D), rope, positions)
+    k = apply_rope(qkv[..., Hq * D:(Hq + Hkv) * D].reshape(B, T, Hkv, D), rope, positions)
+    return q, k, v

@@ -1,0 +1,149 @@
+"""Sequence-level alignment objectives as fused HIP epilogue kernels.
+
+Each GPU path is one launch computing loss, gradient coefficients and metrics together (no
+host sync); CPU paths are the literal reference formulas:
+  * dpo_loss        src/training/train_dpo.py:42-44
+  * pairwise_loss   src/models/reward_model.py:67-68
+  * kl_penalty_pg   src/training/train_rlhf.py:149-153
+  * ensemble_kl     src/training/train_distill.py:127-144
+"""
+from __future__ import annotations
+
+from typing import Dict, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from . import _ext
+
+
+# ------------------------------------------------------------------------------------- DPO
+class _DPOFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, pol, ref, beta, label_smoothing):
+        loss, dpol, rewards, metrics = _ext.require().dpo_loss(pol, ref, beta, label_smoothing)
+        ctx.save_for_backward(dpol)
+        ctx.mark_non_differentiable(rewards, metrics)
+        return loss, rewards, metrics
+
+    @staticmethod
+    def backward(ctx, gloss, _gr, _gm):
+        (dpol,) = ctx.saved_tensors
+        return dpol * gloss, None, None, None
+
+
+def dpo_loss(policy_chosen: torch.Tensor, policy_rejected: torch.Tensor, ref_chosen: torch.Tensor,
+             ref_rejected: torch.Tensor, beta: float = 0.1, label_smoothing: float = 0.0
+             ) -> Tuple[torch.Tensor, Dict[str, torch.Tensor]]:
+    """-logsigmoid(beta*((pc-pr)-(rc-rr))).mean() (+ optional conservative label smoothing).
+
+    Returns (loss, metrics) where metrics holds device tensors: chosen/rejected implicit
+    rewards, reward accuracy and margin (no host sync)."""
+    pol = torch.cat([policy_chosen, policy_rejected]).float().contiguous()
+    ref = torch.cat([ref_chosen, ref_rejected]).float().detach().contiguous()
+    B = policy_chosen.shape[0]
+    if _ext.use_native(pol):
+        loss, rewards, m = _DPOFn.apply(pol, ref, float(beta), float(label_smoothing))
+        metrics = {"rewards/chosen": m[0], "rewards/rejected": m[1], "rewards/accuracy": m[2],
+                   "rewards/margin": m[3], "rewards_per_seq": rewards}
+        return loss, metrics
+    z = beta * ((pol[:B] - pol[B:]) - (ref[:B] - ref[B:]))
+    loss = (-(1 - label_smoothing) * F.logsigmoid(z) - label_smoothing * F.logsigmoid(-z)).mean()
+    rc = (beta * (pol[:B] - ref[:B])).detach()
+    rr = (beta * (pol[B:] - ref[B:])).detach()
+    metrics = {"rewards/chosen": rc.mean(), "rewards/rejected": rr.mean(),
+               "rewards/accuracy": (rc > rr).float().mean(), "rewards/margin": z.detach().mean(),
+               "rewards_per_seq": torch.cat([rc, rr])}
+    return loss, metrics
+
+
+# ------------------------------------------------------------------------------ pairwise RM
+class _PairwiseFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, sc, sr):
+        loss, dsc, dsr, acc = _ext.require().pairwise_loss(sc, sr)
+        ctx.save_for_backward(dsc, dsr)
+        ctx.mark_non_differentiable(acc)
+        return loss, acc
+
+    @staticmethod
+    def backward(ctx, gloss, _gacc):
+        dsc, dsr = ctx.saved_tensors
+        return dsc * gloss, dsr * gloss
+
+
+def pairwise_loss(chosen_scores: torch.Tensor, rejected_scores: torch.Tensor,
+                  return_accuracy: bool = False):
+    """Bradley-Terry: -logsigmoid(s_c - s_r).mean()."""
+    sc = chosen_scores.float().contiguous()
+    sr = rejected_scores.float().contiguous()
+    if _ext.use_native(sc):
+        loss, acc = _PairwiseFn.apply(sc, sr)
+    else:
+        loss = -F.logsigmoid(sc - sr).mean()
+        acc = (sc > sr).float().mean().detach()
+    return (loss, acc) if return_accuracy else loss
+
+
+# ------------------------------------------------------------------- REINFORCE + KL penalty
+class _KLPGFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, lp, lr, reward, kl_coef):
+        loss, klm, dlp, adv = _ext.require().kl_penalty_pg(lp, lr, reward, kl_coef)
+        ctx.save_for_backward(dlp)
+        ctx.mark_non_differentiable(klm, adv)
+        return loss, klm, adv
+
+    @staticmethod
+    def backward(ctx, gloss, _gk, _ga):
+        (dlp,) = ctx.saved_tensors
+        return dlp * gloss, None, None, None
+
+
+def kl_penalty_pg(policy_logp: torch.Tensor, ref_logp: torch.Tensor, reward: torch.Tensor,
+                  kl_coef: float = 0.1):
+    """kl = lp - lr; r' = r - c*kl; A = r' - mean(r'); loss = -mean(stopgrad(A) * lp).
+
+    Returns (loss, kl_mean, advantages)."""
+    lp = policy_logp.float().contiguous()
+    lr = ref_logp.float().detach().contiguous()
+    r = reward.float().detach().contiguous()
+    if _ext.use_native(lp):
+        return _KLPGFn.apply(lp, lr, r, float(kl_coef))
+    kl = lp.detach() - lr
+    shaped = r - kl_coef * kl
+    adv = shaped - shaped.mean()
+    loss = -(adv * lp).mean()
+    return loss, kl.mean(), adv
+
+
+# ----------------------------------------------------------------- ensemble-KL distillation
+class _EnsembleKLFn(torch.autograd.Function):
+    """KL(p_bar || q) per row from student logits [N, V] and K teacher logits [K, N, V]."""
+
+    @staticmethod
+    def forward(ctx, s_logits, t_logits):
+        ops = _ext.require()
+        s_lse = ops.row_lse(s_logits)
+        K, N, V = t_logits.shape
+        t_lse = ops.row_lse(t_logits.view(K * N, V)).view(K, N)
+        kl = ops.ensemble_kl(s_logits, t_logits, s_lse, t_lse, None, False)  # read-only here
+        ctx.save_for_backward(s_logits, t_logits, s_lse, t_lse)
+        return kl
+
+    @staticmethod
+    def backward(ctx, g):
+        ops = _ext.require()
+        s_logits, t_logits, s_lse, t_lse = ctx.saved_tensors
+        ds = s_logits.clone()
+        ops.ensemble_kl(ds, t_logits, s_lse, t_lse, g.float().contiguous(), True)
+        return ds, None
+
+
+def ensemble_kl(student_logits: torch.Tensor, teacher_logits: torch.Tensor) -> torch.Tensor:
+    """student [N, V], teachers [K, N, V] (same vocab) -> per-row KL(mean_k p_k || q) [N]."""
+    if _ext.use_native(student_logits):
+        return _EnsembleKLFn.apply(student_logits.contiguous(), teacher_logits.contiguous().detach())
+    logq = F.log_softmax(student_logits.float(), dim=-1)
+    pbar = torch.softmax(teacher_logits.float(), dim=-1).mean(0)
+    return F.kl_div(logq, pbar, reduction="none").sum(-1)

@@ -1,0 +1,132 @@
+"""Process-group runtime: one process per GPU, RCCL (torch backend "nccl") over xGMI on MI355X,
+gloo on CPU (test tier).
+
+Replaces accelerate's `Accelerator()` process-group creation (src/training/utils.py:55-75,
+config/accelerate_config.yaml: MULTI_GPU, 8 processes, static rendezvous). Reads the standard
+torchrun env (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR, MASTER_PORT); a single process with no
+env runs world_size=1 without creating a group.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+from typing import Any, List, Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistState:
+    rank: int = 0
+    world_size: int = 1
+    local_rank: int = 0
+    device: torch.device = torch.device("cpu")
+    backend: Optional[str] = None
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+    @property
+    def initialized(self) -> bool:
+        return self.world_size > 1 and dist.is_available() and dist.is_initialized()
+
+
+_STATE = DistState()
+
+
+def init_distributed(backend: Optional[str] = None, timeout_s: int = 1800,
+                     device: Optional[str] = None) -> DistState:
+    """Initialise (idempotent). backend defaults to nccl(=RCCL) on GPU, gloo on CPU."""
+    global _STATE
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    use_gpu = torch.cuda.is_available() and device != "cpu"
+    if use_gpu:
+        n = torch.cuda.device_count()
+        dev = torch.device("cuda", local % max(n, 1))
+        torch.cuda.set_device(dev)
+    else:
+        dev = torch.device("cpu")
+    be = backend or ("nccl" if use_gpu else "gloo")
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29500")
+        kwargs = dict(backend=be, rank=rank, world_size=world,
+                      timeout=datetime.timedelta(seconds=timeout_s))
+        if be == "nccl":
+            kwargs["device_id"] = dev
+        dist.init_process_group(**kwargs)
+    _STATE = DistState(rank=rank, world_size=world, local_rank=local, device=dev,
+                       backend=be if world > 1 else None)
+    return _STATE
+
+
+def state() -> DistState:
+    return _STATE
+
+
+def is_main() -> bool:
+    return _STATE.rank == 0
+
+
+def barrier():
+    if _STATE.initialized:
+        if _STATE.backend == "nccl":
+            dist.barrier(device_ids=[_STATE.device.index])
+        else:
+            dist.barrier()
+
+
+def all_reduce_(t: torch.Tensor, op: str = "sum", group=None) -> torch.Tensor:
+    if _STATE.initialized:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM if op in ("sum", "mean") else dist.ReduceOp.MAX,
+                        group=group)
+        if op == "mean":
+            t.div_(dist.get_world_size(group))
+    return t
+
+
+def all_gather_tensor(t: torch.Tensor, group=None) -> torch.Tensor:
+    """Concatenate equal-shape tensors from all ranks along dim 0 (C5 eval gather)."""
+    if not _STATE.initialized:
+        return t
+    ws = dist.get_world_size(group)
+    out = torch.empty((ws * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    dist.all_gather_into_tensor(out, t.contiguous(), group=group)
+    return out
+
+
+def broadcast_object(obj: Any, src: int = 0) -> Any:
+    if not _STATE.initialized:
+        return obj
+    lst = [obj]
+    dist.broadcast_object_list(lst, src=src)
+    return lst[0]
+
+
+def gather_objects(obj: Any) -> List[Any]:
+    if not _STATE.initialized:
+        return [obj]
+    out: List[Any] = [None] * _STATE.world_size
+    dist.all_gather_object(out, obj)
+    return out
+
+
+def destroy():
+    if dist.is_available() and dist.is_initialized():
+        dist.destroy_process_group()
+
+
+def split_for_rank(items: list, rank: Optional[int] = None, world: Optional[int] = None) -> list:
+    """Contiguous slice of `items` for this rank (fixes the reference's misuse of
+    `split_between_processes` at train_rlhf.py:114)."""
+    rank = _STATE.rank if rank is None else rank
+    world = _STATE.world_size if world is None else world
+    n = len(items)
+    per, extra = divmod(n, world)
+    start = rank * per + min(rank, extra)
+    return items[start:start + per + (1 if rank < extra else 0)]

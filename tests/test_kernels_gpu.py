@@ -1,0 +1,309 @@
+"""Numerics of every HIP kernel against a plain PyTorch fp32 reference of the same op (gpu tier).
+
+Inputs are generated in fp32, rounded to bf16 for the kernel, and the reference runs in fp32 on
+the SAME rounded values; tolerances are bf16-output scale.
+"""
+import math
+
+import pytest
+import torch
+
+import distributed_llm_alignment_amd as dla  # noqa: F401
+from distributed_llm_alignment_amd import ops
+from distributed_llm_alignment_amd.ops import _ext
+from distributed_llm_alignment_amd.ops.attention import RotaryCache, _ref_rope, ref_attention
+from distributed_llm_alignment_amd.ops.norm import _ref_norm
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def setup_module(module):
+    assert _ext.available(), "HIP extension must be built and loaded on the GPU box"
+    torch.manual_seed(0)
+
+
+def rel_err(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def bf(x):
+    return x.to(DEV, torch.bfloat16)
+
+
+# --------------------------------------------------------------------------------- norms
+@pytest.mark.parametrize("H", [128, 4096, 2560])
+@pytest.mark.parametrize("rms,res,bias", [(True, False, False), (True, True, False), (False, True, True), (False, False, True)])
+def test_norm_fwd_bwd(H, rms, res, bias):
+    N = 300
+    x = bf(torch.randn(N, H)).requires_grad_()
+    r = bf(torch.randn(N, H)).requires_grad_() if res else None
+    w = bf(1 + 0.1 * torch.randn(H)).requires_grad_()
+    b = bf(0.1 * torch.randn(H)).requires_grad_() if bias else None
+    y, s = ops.add_norm(x, r, w, b, 1e-5, rms)
+    gy = bf(torch.randn(N, H))
+    gs = bf(torch.randn(N, H)) if res else None
+    loss = (y.float() * gy.float()).sum() + ((s.float() * gs.float()).sum() if res else 0)
+    loss.backward()
+    # reference
+    xr = x.detach().float().requires_grad_()
+    rr = r.detach().float().requires_grad_() if res else None
+    wr = w.detach().float().requires_grad_()
+    br = b.detach().float().requires_grad_() if bias else None
+    sr = xr + rr if res else xr
+    yr = _ref_norm(sr, wr, br, 1e-5, rms)
+    lr = (yr * gy.float()).sum() + ((sr * gs.float()).sum() if res else 0)
+    lr.backward()
+    assert rel_err(y, yr) < 1e-2
+    if res:
+        assert rel_err(s, sr) < 1e-2
+    assert rel_err(x.grad, xr.grad) < 2e-2
+    assert rel_err(w.grad, wr.grad) < 2e-2
+    if bias:
+        assert rel_err(b.grad, br.grad) < 2e-2
+
+
+# ----------------------------------------------------------------------------- activations
+def test_swiglu_and_gelu():
+    gu = bf(torch.randn(257, 2 * 384)).requires_grad_()
+    y = ops.swiglu(gu)
+    g = bf(torch.randn(257, 384))
+    (y.float() * g.float()).sum().backward()
+    gr = gu.detach().float().requires_grad_()
+    a, u = gr.chunk(2, -1)
+    yr = torch.nn.functional.silu(a) * u
+    (yr * g.float()).sum().backward()
+    assert rel_err(y, yr) < 1e-2 and rel_err(gu.grad, gr.grad) < 2e-2
+    x = bf(torch.randn(64, 1024)).requires_grad_()
+    z = ops.gelu_new(x)
+    (z.float() * 2).sum().backward()
+    xr = x.detach().float().requires_grad_()
+    zr = torch.nn.functional.gelu(xr, approximate="tanh")
+    (zr * 2).sum().backward()
+    assert rel_err(z, zr) < 1e-2 and rel_err(x.grad, xr.grad) < 2e-2
+
+
+# ------------------------------------------------------------------------------- attention
+def _qkv_ref(qkv, Hq, Hkv, D, rope, kv_start, kv_end, window, positions):
+    B, T, _ = qkv.shape
+    q = qkv[..., : Hq * D].reshape(B, T, Hq, D)
+    k = qkv[..., Hq * D:(Hq + Hkv) * D].reshape(B, T, Hkv, D)
+    v = qkv[..., (Hq + Hkv) * D:].reshape(B, T, Hkv, D)
+    if rope is not None:
+        cos, sin = rope.tables(qkv.device)
+        pos = positions.long() if positions is not None else torch.arange(T, device=qkv.device).expand(B, T)
+        q = _ref_rope(q, cos, sin, pos, rope.rot_dim)
+        k = _ref_rope(k, cos, sin, pos, rope.rot_dim)
+    o = ref_attention(q, k, v, 1.0 / math.sqrt(D), True, 0, window, kv_start, kv_end)
+    return o.reshape(B, T, Hq * D)
+
+
+@pytest.mark.parametrize("D", [128, 64])
+@pytest.mark.parametrize("case", ["plain", "rightpad", "leftpad", "window", "norope"])
+def test_qkv_attention_fwd_bwd(D, case):
+    B, T, Hq, Hkv = 2, 200, 8, 2
+    C = (Hq + 2 * Hkv) * D
+    qkv = bf(torch.randn(B, T, C)).requires_grad_()
+    rope = None if case == "norope" else RotaryCache(D, 500000.0, 4096)
+    kv_start = kv_end = positions = None
+    window = 0
+    if case == "rightpad":
+        kv_start = torch.tensor([0, 0], device=DEV, dtype=torch.int32)
+        kv_end = torch.tensor([T, 131], device=DEV, dtype=torch.int32)
+    if case == "leftpad":
+        kv_start = torch.tensor([0, 57], device=DEV, dtype=torch.int32)
+        kv_end = torch.tensor([T, T], device=DEV, dtype=torch.int32)
+        positions = (torch.arange(T, device=DEV).unsqueeze(0) - kv_start.unsqueeze(1)).clamp(min=0).int()
+    if case == "window":
+        window = 48
+    o = ops.qkv_attention(qkv, Hq, Hkv, D, rope, True, window, kv_start, kv_end, positions)
+    go = bf(torch.randn_like(o.float()))
+    (o.float() * go.float()).sum().backward()
+    qr = qkv.detach().float().requires_grad_()
+    orf = _qkv_ref(qr, Hq, Hkv, D, rope, kv_start, kv_end, window, positions)
+    (orf * go.float()).sum().backward()
+    # compare valid query rows only (fully masked rows are don't-care)
+    valid = torch.ones(B, T, dtype=torch.bool, device=DEV)
+    if case == "rightpad":
+        valid[1, 131:] = False
+    if case == "leftpad":
+        valid[1, :57] = False
+    assert rel_err(o[valid], orf[valid]) < 2e-2, "forward"
+    gmask = valid.unsqueeze(-1)
+    assert rel_err(qkv.grad * gmask, qr.grad * gmask) < 3e-2, "backward"
+
+
+def test_attention_core_decode_offset():
+    B, Tq, Tk, Hq, Hkv, D = 3, 5, 300, 8, 2, 128
+    q = bf(torch.randn(B, Tq, Hq, D))
+    k = bf(torch.randn(B, Tk, Hkv, D))
+    v = bf(torch.randn(B, Tk, Hkv, D))
+    ks = torch.tensor([0, 10, 33], device=DEV, dtype=torch.int32)
+    o = ops.attention_core(q, k, v, causal=True, causal_off=Tk - Tq, kv_start=ks)
+    r = ref_attention(q.float(), k.float(), v.float(), 1 / math.sqrt(D), True, Tk - Tq, 0, ks, None)
+    assert rel_err(o, r) < 2e-2
+
+
+def test_attention_long_seq_grad_llama_shape():
+    B, T, Hq, Hkv, D = 1, 1024, 32, 8, 128
+    C = (Hq + 2 * Hkv) * D
+    qkv = bf(torch.randn(B, T, C)).requires_grad_()
+    rope = RotaryCache(D, 500000.0, 8192)
+    o = ops.qkv_attention(qkv, Hq, Hkv, D, rope)
+    go = bf(torch.randn_like(o.float()))
+    (o.float() * go.float()).sum().backward()
+    qr = qkv.detach().float().requires_grad_()
+    orf = _qkv_ref(qr, Hq, Hkv, D, rope, None, None, 0, None)
+    (orf * go.float()).sum().backward()
+    assert rel_err(o, orf) < 2e-2
+    assert rel_err(qkv.grad, qr.grad) < 3e-2
+
+
+# ------------------------------------------------------------------------------- logprob
+@pytest.mark.parametrize("V", [32000, 50257])
+def test_linear_logprob(V):
+    N, H = 96, 256
+    h = bf(torch.randn(N, H)).requires_grad_()
+    W = bf(torch.randn(V, H) * 0.05).requires_grad_()
+    tgt = torch.randint(0, V, (N,), device=DEV)
+    tgt[5] = -100
+    lp = ops.linear_logprob(h, W, tgt)
+    g = torch.randn(N, device=DEV)
+    (lp * g).sum().backward()
+    hr = h.detach().float().requires_grad_()
+    Wr = W.detach().float().requires_grad_()
+    logits = (hr @ Wr.t()).to(torch.bfloat16).float()  # the model's logits are bf16 (HF)
+    lr = torch.log_softmax(logits, -1).gather(-1, tgt.clamp(min=0).unsqueeze(-1)).squeeze(-1)
+    lr = torch.where(tgt >= 0, lr, torch.zeros_like(lr))
+    (lr * g).sum().backward()
+    assert (lp - lr).abs().max().item() < 2e-2
+    assert rel_err(h.grad, hr.grad) < 3e-2
+    assert rel_err(W.grad, Wr.grad) < 3e-2
+
+
+def test_sequence_logprob_and_dpo_loss_kernels():
+    S, T = 6, 50
+    lp = torch.randn(S, T, device=DEV).requires_grad_()
+    mask = (torch.rand(S, T, device=DEV) > 0.3).float()
+    s = ops.seq_reduce(lp, mask, mean=True)
+    s.sum().backward()
+    lr_ = lp.detach().clone().requires_grad_()
+    sr = (lr_ * mask).sum(1) / mask.sum(1).clamp(min=1)
+    sr.sum().backward()
+    assert torch.allclose(s, sr, atol=1e-5) and torch.allclose(lp.grad, lr_.grad, atol=1e-6)
+    pc, pr, rc, rr = [torch.randn(4, device=DEV) for _ in range(4)]
+    pc.requires_grad_()
+    pr.requires_grad_()
+    loss, m = ops.dpo_loss(pc, pr, rc, rr, beta=0.1)
+    loss.backward()
+    pc2, pr2 = pc.detach().cpu().requires_grad_(), pr.detach().cpu().requires_grad_()
+    l2, m2 = ops.dpo_loss(pc2, pr2, rc.cpu(), rr.cpu(), beta=0.1)
+    l2.backward()
+    assert abs(loss.item() - l2.item()) < 1e-5
+    assert torch.allclose(pc.grad.cpu(), pc2.grad, atol=1e-6) and torch.allclose(pr.grad.cpu(), pr2.grad, atol=1e-6)
+    assert abs(m["rewards/accuracy"].item() - m2["rewards/accuracy"].item()) < 1e-6
+
+
+def test_pairwise_and_kl_penalty_kernels():
+    sc, sr = torch.randn(8, device=DEV).requires_grad_(), torch.randn(8, device=DEV).requires_grad_()
+    l = ops.pairwise_loss(sc, sr)
+    l.backward()
+    a, b = sc.detach().cpu().requires_grad_(), sr.detach().cpu().requires_grad_()
+    l2 = ops.pairwise_loss(a, b)
+    l2.backward()
+    assert abs(l.item() - l2.item()) < 1e-5 and torch.allclose(sc.grad.cpu(), a.grad, atol=1e-6)
+    lp = torch.randn(16, device=DEV).requires_grad_()
+    lref, rew = torch.randn(16, device=DEV), torch.randn(16, device=DEV)
+    loss, kl, adv = ops.kl_penalty_pg(lp, lref, rew, 0.1)
+    loss.backward()
+    lp2 = lp.detach().cpu().requires_grad_()
+    loss2, kl2, adv2 = ops.kl_penalty_pg(lp2, lref.cpu(), rew.cpu(), 0.1)
+    loss2.backward()
+    assert abs(loss.item() - loss2.item()) < 1e-5 and abs(kl.item() - kl2.item()) < 1e-5
+    assert torch.allclose(lp.grad.cpu(), lp2.grad, atol=1e-6)
+
+
+def test_ensemble_kl_kernel():
+    N, V, K = 33, 1000, 3
+    s = bf(torch.randn(N, V)).requires_grad_()
+    t = bf(torch.randn(K, N, V))
+    kl = ops.ensemble_kl(s, t)
+    g = torch.rand(N, device=DEV)
+    (kl * g).sum().backward()
+    sr = s.detach().float().requires_grad_()
+    logq = torch.log_softmax(sr, -1)
+    pbar = torch.softmax(t.float(), -1).mean(0)
+    klr = torch.nn.functional.kl_div(logq, pbar, reduction="none").sum(-1)
+    (klr * g).sum().backward()
+    assert rel_err(kl, klr) < 1e-2 and rel_err(s.grad, sr.grad) < 3e-2
+
+
+# ------------------------------------------------------------------------------- optimizer
+@pytest.mark.parametrize("grad_dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("master", [True, False])
+def test_adamw_kernel(grad_dtype, master):
+    from distributed_llm_alignment_amd.optim.adamw import adamw_update, clip_coefficient, grad_sumsq
+
+    n = 8 * 1000
+    p0 = torch.randn(n)
+    g = torch.randn(n).to(DEV, grad_dtype)
+    p = p0.to(DEV, torch.bfloat16)
+    mst = p.float().clone() if master else None
+    m, v = torch.zeros(n, device=DEV), torch.zeros(n, device=DEV)
+    ss = torch.zeros(1, device=DEV)
+    grad_sumsq(g, ss)
+    norm, coef = clip_coefficient(ss, 1.0)
+    assert abs(norm.item() - g.float().norm().item()) / g.float().norm().item() < 1e-4
+    for step in (1, 2):
+        adamw_update(p, mst, g, m, v, 1e-3, 0.9, 0.95, 1e-8, 0.01, step, coef, 0.5)
+    # reference: torch AdamW on fp32 param with the same scaled gradient
+    ref = p0.to(DEV).to(torch.bfloat16).float().clone().requires_grad_()
+    opt = torch.optim.AdamW([ref], lr=1e-3, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.01)
+    for _ in (1, 2):
+        ref.grad = g.float() * 0.5 * coef
+        opt.step()
+    out = mst if master else p.float()
+    assert (out - ref.detach()).abs().max().item() < (2e-5 if master else 1e-2)
+
+
+# --------------------------------------------------------------------------- whole model
+def test_tiny_model_gpu_matches_cpu_reference():
+    from distributed_llm_alignment_amd.models import build_model, get_config
+
+    cfg = get_config("tiny-llama-d128")
+    cpu = build_model(cfg, device="cpu", dtype=torch.float32, seed=3)
+    gpu = build_model(cfg, device=DEV, dtype=torch.bfloat16, seed=3, init=False)
+    with torch.no_grad():
+        for (n1, p1), (n2, p2) in zip(cpu.named_parameters(), gpu.named_parameters()):
+            p2.copy_(p1.to(torch.bfloat16))
+            p1.copy_(p2.float())
+    ids = torch.randint(3, cfg.vocab_size, (2, 160))
+    mask = torch.ones_like(ids)
+    mask[1, 100:] = 0
+    a = cpu.sequence_logprob(ids, mask)
+    b = gpu.sequence_logprob(ids.to(DEV), mask.to(DEV))
+    assert (a - b.cpu()).abs().max().item() < 0.05
+
+
+def test_dpo_training_reduces_loss_gpu():
+    from distributed_llm_alignment_amd.data.synthetic import synthetic_preference_batch
+    from distributed_llm_alignment_amd.models import build_model, get_config
+    from distributed_llm_alignment_amd.objectives import dpo_step_loss
+    from distributed_llm_alignment_amd.parallel.data_parallel import DataParallelEngine
+
+    cfg = get_config("tiny-llama-d128")
+    pol = build_model(cfg, device=DEV, seed=1)
+    ref = build_model(cfg, device=DEV, seed=1)
+    ref.requires_grad_(False)
+    eng = DataParallelEngine(pol, lr=1e-3, weight_decay=0.0, max_grad_norm=1.0)
+    g = torch.Generator().manual_seed(0)
+    batch = synthetic_preference_batch(4, 128, cfg.vocab_size, device=DEV, generator=g, min_len=64)
+    losses = []
+    for _ in range(8):
+        loss, _ = dpo_step_loss(pol, ref, batch, beta=0.1)
+        loss.backward()
+        eng.step()
+        losses.append(loss.item())
+    assert losses[0] == pytest.approx(math.log(2), abs=1e-3)
+    assert losses[-1] < losses[0] - 0.05
