@@ -5,8 +5,8 @@
 // can fault the GPU), allocates outputs through the torch caching allocator and launches on
 // the caller's current HIP stream. No op synchronises the host.
 #include <ATen/ATen.h>
-#include <c10/hip/HIPGuard.h>
-#include <c10/hip/HIPStream.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <torch/library.h>
 
 #include <cstdint>
@@ -61,7 +61,7 @@ void launch_f32_to_bf16_rows(const float*, int64_t, int, bf16_t*, int64_t, hipSt
 
 // ---- helpers ----
 static inline hipStream_t cur_stream(const at::Tensor& t) {
-  return c10::hip::getCurrentHIPStream(t.device().index()).stream();
+  return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(t.device().index()).stream();
 }
 static inline bf16_t* bp(const at::Tensor& t) { return reinterpret_cast<bf16_t*>(t.data_ptr()); }
 static inline const bf16_t* cbp(const at::Tensor& t) {
@@ -98,7 +98,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> norm_fwd(
   TORCH_CHECK(w.numel() == H && w.is_contiguous(), "w shape");
   const int64_t rows = x.numel() / H;
   TORCH_CHECK(rows < (1ll << 31), "too many rows");
-  c10::hip::HIPGuard g(x.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   auto y = at::empty_like(x);
   at::Tensor so;
   const bf16_t* rptr = nullptr;
@@ -151,7 +151,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> norm_bwd(const at::Tensor& dy, co
     TORCH_CHECK(dres->sizes() == s.sizes() && dres->is_contiguous(), "dres shape");
     dr = cbp(*dres);
   }
-  c10::hip::HIPGuard g(s.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(s.device());
   auto ds = at::empty_like(s);
   const int grid = norm_bwd_grid(static_cast<int>(rows));
   auto fopt = s.options().dtype(at::kFloat);
@@ -175,7 +175,7 @@ at::Tensor swiglu_fwd(const at::Tensor& gu) {
   const int64_t F = two_f / 2, rows = gu.numel() / two_f;
   auto sizes = gu.sizes().vec();
   sizes.back() = F;
-  c10::hip::HIPGuard g(gu.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(gu.device());
   auto out = at::empty(sizes, gu.options());
   launch_swiglu_fwd(cbp(gu), bp(out), rows, static_cast<int>(F), cur_stream(gu));
   return out;
@@ -187,7 +187,7 @@ at::Tensor swiglu_bwd(const at::Tensor& gu, const at::Tensor& dout) {
   TORCH_CHECK(gu.is_contiguous() && dout.is_contiguous(), "contiguous");
   const int64_t two_f = gu.size(-1), F = two_f / 2, rows = gu.numel() / two_f;
   TORCH_CHECK(two_f % 16 == 0 && dout.numel() == rows * F, "shapes");
-  c10::hip::HIPGuard g(gu.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(gu.device());
   auto dgu = at::empty_like(gu);
   launch_swiglu_bwd(cbp(gu), cbp(dout), bp(dgu), rows, static_cast<int>(F), cur_stream(gu));
   return dgu;
@@ -196,7 +196,7 @@ at::Tensor swiglu_bwd(const at::Tensor& gu, const at::Tensor& dout) {
 at::Tensor gelu_fwd(const at::Tensor& x) {
   check_bf16(x, "x");
   TORCH_CHECK(x.is_contiguous() && x.numel() % 8 == 0, "x contiguous, numel % 8");
-  c10::hip::HIPGuard g(x.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   auto y = at::empty_like(x);
   launch_gelu_fwd(cbp(x), bp(y), x.numel(), cur_stream(x));
   return y;
@@ -208,7 +208,7 @@ at::Tensor gelu_bwd(const at::Tensor& x, const at::Tensor& dy) {
   TORCH_CHECK(x.is_contiguous() && dy.is_contiguous() && x.numel() == dy.numel() &&
                   x.numel() % 8 == 0,
               "shapes");
-  c10::hip::HIPGuard g(x.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   auto dx = at::empty_like(x);
   launch_gelu_bwd(cbp(x), cbp(dy), bp(dx), x.numel(), cur_stream(x));
   return dx;
@@ -242,7 +242,7 @@ std::tuple<at::Tensor, at::Tensor> rope_fwd(const at::Tensor& qkv, const at::Ten
   const int64_t tokens = qkv.size(0);
   TORCH_CHECK(T > 0 && tokens % T == 0, "tokens must be a multiple of T");
   check_rope_common(cos_t, sin_t, pos, tokens, D, rot);
-  c10::hip::HIPGuard g(qkv.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(qkv.device());
   auto q = at::empty({tokens, Hq * D}, qkv.options());
   auto k = at::empty({tokens, Hkv * D}, qkv.options());
   launch_rope_fwd(cbp(qkv), qkv.stride(0), bp(q), bp(k), cos_t.data_ptr<float>(),
@@ -270,7 +270,7 @@ void rope_bwd(const at::Tensor& dq, const at::Tensor& dk, at::Tensor& dqkv,
               "dqkv layout");
   TORCH_CHECK(T > 0 && tokens % T == 0, "tokens must be a multiple of T");
   check_rope_common(cos_t, sin_t, pos, tokens, D, rot);
-  c10::hip::HIPGuard g(dqkv.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(dqkv.device());
   launch_rope_bwd(cbp(dq), cbp(dk), bp(dqkv), dqkv.stride(0), cos_t.data_ptr<float>(),
                   sin_t.data_ptr<float>(),
                   (pos && pos->defined()) ? pos->data_ptr<int>() : nullptr, tokens,
@@ -314,7 +314,7 @@ std::tuple<at::Tensor, at::Tensor> attn_fwd(const at::Tensor& q, const at::Tenso
   TORCH_CHECK(Hkv > 0 && Hq % Hkv == 0, "Hq must be a multiple of Hkv");
   check_kv_range(kv_start, B, "kv_start");
   check_kv_range(kv_end, B, "kv_end");
-  c10::hip::HIPGuard g(q.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
   auto o = at::empty({B, Tq, Hq, D}, q.options());
   auto lse2 = at::empty({B, Hq, Tq}, q.options().dtype(at::kFloat));
   AttnParams p{};
@@ -360,7 +360,7 @@ at::Tensor attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tenso
   TORCH_CHECK(Hkv > 0 && Hq % Hkv == 0, "GQA ratio");
   check_kv_range(kv_start, B, "kv_start");
   check_kv_range(kv_end, B, "kv_end");
-  c10::hip::HIPGuard g(q.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
   auto st = cur_stream(q);
   auto delta = at::empty({B, Hq, Tq}, q.options().dtype(at::kFloat));
   launch_attn_bwd_delta(cbp(o), cbp(dout), o.stride(0), o.stride(1), o.stride(2),
@@ -394,7 +394,7 @@ void f32_to_bf16_rows(const at::Tensor& src, at::Tensor& dst) {
   TORCH_CHECK(src.is_contiguous() && src.dim() == 2 && dst.dim() == 2 && dst.stride(1) == 1 &&
                   src.sizes() == dst.sizes() && src.size(1) % 8 == 0 && dst.stride(0) % 8 == 0,
               "f32_to_bf16_rows layout");
-  c10::hip::HIPGuard g(src.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(src.device());
   launch_f32_to_bf16_rows(src.data_ptr<float>(), src.size(0), static_cast<int>(src.size(1)),
                           bp(dst), dst.stride(0), cur_stream(src));
 }
@@ -410,7 +410,7 @@ std::tuple<at::Tensor, at::Tensor> logprob_fwd(const at::Tensor& logits, const a
   TORCH_CHECK(tgt.scalar_type() == at::kLong && tgt.is_contiguous() && tgt.numel() == logits.size(0),
               "targets int64 [N]");
   same_device(logits, tgt);
-  c10::hip::HIPGuard g(logits.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(logits.device());
   auto opt = logits.options().dtype(at::kFloat);
   auto logp = at::empty({logits.size(0)}, opt);
   auto lse = at::empty({logits.size(0)}, opt);
@@ -428,7 +428,7 @@ void logprob_bwd(at::Tensor& logits, const at::Tensor& tgt, const at::Tensor& ls
   const int64_t N = logits.size(0);
   TORCH_CHECK(tgt.scalar_type() == at::kLong && tgt.numel() == N && tgt.is_contiguous(), "targets");
   TORCH_CHECK(lse.numel() == N && grad.numel() == N && grad.is_contiguous(), "lse/grad shape");
-  c10::hip::HIPGuard g(logits.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(logits.device());
   launch_logprob_bwd(bp(logits), logits.stride(0), static_cast<int>(logits.size(1)), N,
                      tgt.data_ptr<int64_t>(), lse.data_ptr<float>(), grad.data_ptr<float>(),
                      cur_stream(logits));
@@ -436,7 +436,7 @@ void logprob_bwd(at::Tensor& logits, const at::Tensor& tgt, const at::Tensor& ls
 
 at::Tensor row_lse(const at::Tensor& logits) {
   check_logits(logits);
-  c10::hip::HIPGuard g(logits.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(logits.device());
   auto lse = at::empty({logits.size(0)}, logits.options().dtype(at::kFloat));
   launch_row_lse(cbp(logits), logits.stride(0), static_cast<int>(logits.size(1)), logits.size(0),
                  lse.data_ptr<float>(), cur_stream(logits));
@@ -463,7 +463,7 @@ at::Tensor ensemble_kl(at::Tensor& s_logits, const at::Tensor& t_logits, const a
     check_f32(*grad, "grad");
     gp = grad->data_ptr<float>();
   }
-  c10::hip::HIPGuard g(s_logits.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(s_logits.device());
   auto kl = at::empty({N}, s_logits.options().dtype(at::kFloat));
   launch_ensemble_kl(bp(s_logits), cbp(t_logits), s_logits.size(1), N * s_logits.size(1),
                      static_cast<int>(K), static_cast<int>(s_logits.size(1)),
@@ -478,7 +478,7 @@ std::tuple<at::Tensor, at::Tensor> seq_reduce(const at::Tensor& lp, const at::Te
   check_f32(mask, "mask");
   TORCH_CHECK(lp.dim() == 2 && lp.is_contiguous() && mask.sizes() == lp.sizes() && mask.is_contiguous(),
               "lp/mask [S, T]");
-  c10::hip::HIPGuard g(lp.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(lp.device());
   auto sum = at::empty({lp.size(0)}, lp.options());
   auto cnt = at::empty({lp.size(0)}, lp.options());
   launch_seq_reduce(lp.data_ptr<float>(), mask.data_ptr<float>(), static_cast<int>(lp.size(0)),
@@ -495,7 +495,7 @@ at::Tensor seq_expand_grad(const at::Tensor& coef, const at::Tensor& mask, const
   TORCH_CHECK(mask.dim() == 2 && mask.is_contiguous() && coef.numel() == mask.size(0) &&
                   cnt.numel() == mask.size(0) && coef.is_contiguous() && cnt.is_contiguous(),
               "shapes");
-  c10::hip::HIPGuard g(mask.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(mask.device());
   auto out = at::empty_like(mask);
   launch_seq_expand_grad(coef.data_ptr<float>(), mask.data_ptr<float>(), cnt.data_ptr<float>(),
                          static_cast<int>(mask.size(0)), static_cast<int>(mask.size(1)), mean,
@@ -513,7 +513,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> dpo_loss(const at::Te
                   pol.numel() % 2 == 0,
               "pol/ref must be [2B] (chosen then rejected)");
   const int B = static_cast<int>(pol.numel() / 2);
-  c10::hip::HIPGuard g(pol.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(pol.device());
   auto opt = pol.options();
   auto loss = at::empty({}, opt);
   auto dpol = at::empty({2 * B}, opt);
@@ -532,7 +532,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> pairwise_loss(const a
   check_f32(sr, "sr");
   TORCH_CHECK(sc.is_contiguous() && sr.is_contiguous() && sc.numel() == sr.numel(), "shapes");
   const int B = static_cast<int>(sc.numel());
-  c10::hip::HIPGuard g(sc.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(sc.device());
   auto opt = sc.options();
   auto loss = at::empty({}, opt);
   auto dsc = at::empty({B}, opt);
@@ -555,7 +555,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> kl_penalty_pg(const a
                   lp.numel() == lr.numel() && lp.numel() == reward.numel() && lp.numel() > 0,
               "shapes");
   const int n = static_cast<int>(lp.numel());
-  c10::hip::HIPGuard g(lp.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(lp.device());
   auto opt = lp.options();
   auto loss = at::empty({}, opt);
   auto klm = at::empty({}, opt);
@@ -600,7 +600,7 @@ void adamw_step(const c10::optional<at::Tensor>& param, const c10::optional<at::
     cp = clip->data_ptr<float>();
   }
   TORCH_CHECK(step >= 1, "step must be >= 1");
-  c10::hip::HIPGuard g(grad.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(grad.device());
   launch_adamw(pp, mp, grad.data_ptr(), grad.scalar_type() == at::kBFloat16, m.data_ptr<float>(),
                v.data_ptr<float>(), n, static_cast<float>(lr), static_cast<float>(b1),
                static_cast<float>(b2), static_cast<float>(eps), static_cast<float>(wd),
@@ -613,7 +613,7 @@ void grad_sumsq(const at::Tensor& grad, at::Tensor& out, bool accumulate) {
   TORCH_CHECK(grad.is_contiguous() && grad.numel() % 8 == 0, "grad contiguous, numel % 8");
   TORCH_CHECK(grad.scalar_type() == at::kBFloat16 || grad.scalar_type() == at::kFloat, "dtype");
   TORCH_CHECK(out.numel() >= 1, "out");
-  c10::hip::HIPGuard g(grad.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(grad.device());
   auto partial = at::empty({sumsq_grid(grad.numel())}, out.options());
   launch_grad_sumsq(grad.data_ptr(), grad.scalar_type() == at::kBFloat16, grad.numel(),
                     partial.data_ptr<float>(), out.data_ptr<float>(), accumulate,
@@ -622,7 +622,7 @@ void grad_sumsq(const at::Tensor& grad, at::Tensor& out, bool accumulate) {
 
 std::tuple<at::Tensor, at::Tensor> clip_coef(const at::Tensor& sumsq, double max_norm) {
   check_f32(sumsq, "sumsq");
-  c10::hip::HIPGuard g(sumsq.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(sumsq.device());
   auto norm = at::empty({}, sumsq.options());
   auto coef = at::empty({}, sumsq.options());
   launch_clip_coef(sumsq.data_ptr<float>(), static_cast<float>(max_norm), norm.data_ptr<float>(),
