@@ -23,6 +23,7 @@ void launch_norm_bwd(const bf16_t*, const bf16_t*, const bf16_t*, const float*, 
                      const bf16_t*, bf16_t*, float*, float*, bf16_t*, bf16_t*, int, int, bool,
                      hipStream_t);
 int norm_bwd_grid(int rows);
+int norm_wgrad_scratch_rows();
 void launch_swiglu_fwd(const bf16_t*, bf16_t*, int64_t, int, hipStream_t);
 void launch_swiglu_bwd(const bf16_t*, const bf16_t*, bf16_t*, int64_t, int, hipStream_t);
 void launch_gelu_fwd(const bf16_t*, bf16_t*, int64_t, hipStream_t);
@@ -155,8 +156,9 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> norm_bwd(const at::Tensor& dy, co
   auto ds = at::empty_like(s);
   const int grid = norm_bwd_grid(static_cast<int>(rows));
   auto fopt = s.options().dtype(at::kFloat);
-  auto dwp = at::empty({grid, H}, fopt);
-  auto dbp = has_bias ? at::empty({grid, H}, fopt) : at::empty({0}, fopt);
+  const int srows = grid + norm_wgrad_scratch_rows();  // partials + stage-1 scratch
+  auto dwp = at::empty({srows, H}, fopt);
+  auto dbp = has_bias ? at::empty({srows, H}, fopt) : at::empty({0}, fopt);
   auto dw = at::empty({H}, w.options());
   auto db = has_bias ? at::empty({H}, w.options()) : at::empty({0}, w.options());
   launch_norm_bwd(cbp(dy), cbp(s), cbp(w), rstd.data_ptr<float>(), mptr, dr, bp(ds),

@@ -160,9 +160,10 @@ def load_hf_state_dict(model, sd: Dict[str, torch.Tensor], strict: bool = True, 
                 missing.append(hf)
                 continue
         src = sd[key]
-        dst = _slice(params[native].data, spec)
-        if spec == "T":
-            src = src.t()
+        if spec == "T":  # HF Conv1D [in, out] -> native [out, in]
+            dst, src = params[native].data, src.t()
+        else:
+            dst = _slice(params[native].data, spec)
         if tuple(dst.shape) != tuple(src.shape):
             raise ValueError(f"shape mismatch for {hf}: ckpt {tuple(src.shape)} vs model {tuple(dst.shape)}")
         dst.copy_(src.to(dst.dtype))

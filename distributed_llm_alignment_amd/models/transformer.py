@@ -59,7 +59,7 @@ class Attention(nn.Module):
 
     def forward(self, h, rope, kv_start, kv_end, positions, cache=None, layer_idx=0):
         cfg = self.cfg
-        qkv = F.linear(h, self.qkv_proj, self.qkv_bias)
+        qkv = ops.linear(h, self.qkv_proj, self.qkv_bias)
         window = cfg.sliding_window if cfg.sliding_window else 0
         if cache is None:
             a = ops.qkv_attention(qkv, cfg.num_heads, cfg.num_kv_heads, cfg.head_dim, rope,
@@ -67,7 +67,7 @@ class Attention(nn.Module):
                                   positions=positions)
         else:
             a = cache.attend(layer_idx, qkv, rope, window)
-        return F.linear(a, self.o_proj, self.o_bias)
+        return ops.linear(a, self.o_proj, self.o_bias)
 
 
 class MLP(nn.Module):
@@ -84,9 +84,9 @@ class MLP(nn.Module):
         self.down_bias = _param(H, device=device, dtype=dtype) if cfg.mlp_bias else None
 
     def forward(self, h):
-        u = F.linear(h, self.up_proj, self.up_bias)
+        u = ops.linear(h, self.up_proj, self.up_bias)
         m = ops.swiglu(u) if self.cfg.activation == "swiglu" else ops.gelu_new(u)
-        return F.linear(m, self.down_proj, self.down_bias)
+        return ops.linear(m, self.down_proj, self.down_bias)
 
 
 class MoE(nn.Module):
@@ -187,6 +187,10 @@ class CausalLM(nn.Module):
         self.rope = (ops.RotaryCache(cfg.rot_dim, cfg.rope_theta, cfg.max_position_embeddings,
                                      cfg.rope_scaling) if cfg.rot_dim > 0 else None)
         self.gradient_checkpointing = False
+        if self.lm_head is None and not headless:
+            # tied input/output embedding: its gradient arrives from two ops, so it must go through
+            # autograd's AccumulateGrad (one hook call) rather than the GEMM main-grad path
+            self.embed._dla_shared = True
 
     # --------------------------------------------------------------------------------- init
     @torch.no_grad()

@@ -3,6 +3,7 @@ run the pure-PyTorch references (test tier / numerics oracles)."""
 from . import _ext
 from .activations import gelu_new, swiglu
 from .attention import RotaryCache, attention_core, qkv_attention, ref_attention
+from .linear import accumulate_weight_grad, linear
 from .logprob import linear_logprob, seq_reduce, sequence_logprob, shifted_targets, token_nll
 from .losses import dpo_loss, ensemble_kl, kl_penalty_pg, pairwise_loss
 from .norm import add_norm, layer_norm, rms_norm
@@ -11,5 +12,5 @@ __all__ = [
     "_ext", "gelu_new", "swiglu", "RotaryCache", "attention_core", "qkv_attention",
     "ref_attention", "linear_logprob", "seq_reduce", "sequence_logprob", "shifted_targets",
     "token_nll", "dpo_loss", "ensemble_kl", "kl_penalty_pg", "pairwise_loss", "add_norm",
-    "layer_norm", "rms_norm",
+    "layer_norm", "rms_norm", "linear", "accumulate_weight_grad",
 ]

@@ -60,7 +60,12 @@ class _LinearLogprobFn(torch.autograd.Function):
         ops.logprob_bwd(logits, targets, lse, g.float().contiguous())
         dlogits = logits  # rewritten in place
         dh = dlogits @ weight if ctx.needs_input_grad[0] else None
-        dw = dlogits.t() @ hidden if ctx.needs_input_grad[1] else None
+        dw = None
+        if ctx.needs_input_grad[1]:
+            from .linear import accumulate_weight_grad
+
+            if not accumulate_weight_grad(weight, dlogits, hidden):
+                dw = dlogits.t() @ hidden
         return dh, dw, None
 
 
@@ -97,7 +102,11 @@ def seq_reduce(token_lp: torch.Tensor, mask: torch.Tensor, mean: bool = True) ->
 
 def shifted_targets(input_ids: torch.Tensor, attention_mask: Optional[torch.Tensor],
                     ignore_index: int = -100):
-    """targets[t] = input_ids[t+1]; last position ignored. mask[t] = attention_mask[t+1]."""
+    """targets[t] = input_ids[t+1]; last position ignored. mask[t] = am[t] * am[t+1].
+
+    For right padding this equals the reference's `attention_mask[:, 1:]`; for left padding it
+    also drops the pad -> first-token "prediction" the reference would score (its query row
+    sees no valid keys)."""
     S, T = input_ids.shape
     tgt = torch.full_like(input_ids, ignore_index)
     tgt[:, :-1] = input_ids[:, 1:]
@@ -105,7 +114,8 @@ def shifted_targets(input_ids: torch.Tensor, attention_mask: Optional[torch.Tens
     if attention_mask is None:
         mask[:, :-1] = 1.0
     else:
-        mask[:, :-1] = attention_mask[:, 1:].float()
+        am = attention_mask.float()
+        mask[:, :-1] = am[:, 1:] * am[:, :-1]
     tgt = torch.where(mask > 0, tgt, torch.full_like(tgt, ignore_index))
     return tgt, mask
 

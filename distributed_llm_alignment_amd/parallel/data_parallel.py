@@ -111,6 +111,9 @@ class DataParallelEngine:
                 view.copy_(p.data)
                 p.data = view
                 p.grad = self.grad_buf[o:o + p.numel()].view_as(p)
+                # ops.linear / linear_logprob accumulate weight grads here inside the GEMM
+                p.main_grad = p.grad
+                p._dla_grad_hook = self._on_grad
         self._offsets = offsets
         # ---- shard layout
         shard = 0

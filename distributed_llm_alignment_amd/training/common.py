@@ -1,0 +1,163 @@
+"""Shared trainer core ("all share one Trainer core").
+
+Reference loop semantics kept (src/training/train_{sft,reward,dpo,distill}.py):
+  * `global_step` counts MICRO-batches; log / eval / save / max_train_steps are in micro-steps
+    (Appendix A #12);
+  * gradients accumulate over `hardware.gradient_accumulation_steps` micro-batches, the loss is
+    divided by that count (accelerator.backward), the optimizer + clipping run on sync steps and
+    at the end of the dataloader (accelerate's `accumulate` semantics);
+  * checkpoints at `step_{N}` every `save_every_steps` and at `final`.
+What differs: no accelerate; one process per GPU with RCCL; the DataParallelEngine (flat buffers,
+overlapped bucketed reduce-scatter, ZeRO-1, fused AdamW) replaces DDP/DeepSpeed/FSDP; metrics are
+really logged (JSONL); `--resume` restores weights, optimizer, scheduler, RNG and step.
+"""
+from __future__ import annotations
+
+import contextlib
+import os
+import random
+from dataclasses import dataclass, field
+from pathlib import Path
+from typing import Any, Callable, Dict, Iterable, List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from ..optim.scheduler import LRSchedule
+from ..parallel.data_parallel import DataParallelEngine
+from ..parallel.dist import DistState, init_distributed
+from ..utils.checkpoint import load_state, resolve_checkpoint, save_state
+from ..utils.config import hardware_parallel
+from ..utils.logging import MetricsLogger, RunningLoss, log_rank_zero
+
+
+def seed_everything(seed: int) -> None:
+    random.seed(seed)
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    if torch.cuda.is_available():
+        torch.cuda.manual_seed_all(seed)
+
+
+@dataclass
+class TrainContext:
+    cfg: Dict[str, Any]
+    dist: DistState
+    device: torch.device
+    logger: MetricsLogger
+    hw: Dict[str, Any]
+    output_dir: str
+    log_dir: str
+    seed: int
+    stage: str
+    extras: Dict[str, Any] = field(default_factory=dict)
+
+    @property
+    def is_main(self) -> bool:
+        return self.dist.is_main
+
+    def log(self, msg: str):
+        log_rank_zero(msg, self.is_main)
+
+
+def setup(cfg: Dict[str, Any], stage: str, default_seed: int = 0) -> TrainContext:
+    st = init_distributed()
+    seed = int(cfg.get("seed", default_seed))
+    seed_everything(seed)
+    lg = cfg.get("logging", {}) or {}
+    out = lg.get("output_dir", f"checkpoints/{stage}")
+    log_dir = lg.get("log_dir", f"logs/{stage}")
+    if st.is_main:
+        Path(out).mkdir(parents=True, exist_ok=True)
+        Path(log_dir).mkdir(parents=True, exist_ok=True)
+    logger = MetricsLogger(log_dir, st.is_main, use_wandb=bool(lg.get("use_wandb", False)),
+                           config=cfg, run_name=cfg.get("experiment_name"))
+    return TrainContext(cfg=cfg, dist=st, device=st.device, logger=logger, hw=hardware_parallel(cfg),
+                        output_dir=out, log_dir=log_dir, seed=seed, stage=stage)
+
+
+def make_engine(ctx: TrainContext, model, lr: float, betas=(0.9, 0.999), weight_decay: float = 0.0,
+                max_grad_norm: float = 1.0) -> DataParallelEngine:
+    return DataParallelEngine(model, lr=lr, betas=betas, weight_decay=weight_decay,
+                              max_grad_norm=max_grad_norm, zero_stage=ctx.hw.get("zero_stage"),
+                              bucket_mb=ctx.hw.get("bucket_mb", 256.0),
+                              master_weights=ctx.hw.get("master_weights", True))
+
+
+def effective_batch_msg(ctx: TrainContext, micro: int) -> str:
+    eff = micro * ctx.dist.world_size * ctx.hw["grad_accum"]
+    target = (ctx.cfg.get("optimization", {}) or {}).get("total_batch_size", eff)
+    return f"Effective global batch size: {eff} (target {target})"
+
+
+def move_to(batch, device):
+    if isinstance(batch, torch.Tensor):
+        return batch.to(device, non_blocking=True)
+    if isinstance(batch, dict):
+        return {k: move_to(v, device) for k, v in batch.items()}
+    if isinstance(batch, (list, tuple)):
+        return type(batch)(move_to(v, device) for v in batch)
+    return batch
+
+
+StepFn = Callable[[Any], Tuple[torch.Tensor, Dict[str, Any]]]
+
+
+def train_loop(ctx: TrainContext, loader, sampler, engine: DataParallelEngine, step_fn: StepFn,
+               total_steps: int, models_to_save: List[Any], tokenizer=None,
+               scheduler: Optional[LRSchedule] = None, log_every: int = 10, eval_every: int = 0,
+               save_every: int = 0, eval_fn: Optional[Callable[[int], Dict[str, Any]]] = None,
+               extra_log_fn: Optional[Callable[[int, Dict[str, Any]], Dict[str, Any]]] = None,
+               resume: Optional[str] = None, keep_last: Optional[int] = None) -> int:
+    accum = ctx.hw["grad_accum"]
+    global_step = 0
+    if resume:
+        path = resolve_checkpoint(resume)
+        if path is not None:
+            global_step = load_state(path, models_to_save[:1], engine, scheduler)
+            ctx.log(f"Resumed from {path} at step {global_step}")
+    running = RunningLoss()
+    last_metrics: Dict[str, Any] = {}
+    done = global_step >= total_steps
+    epoch = 0
+    while not done:
+        if sampler is not None:
+            sampler.set_epoch(epoch)
+        n_batches = len(loader)
+        for bi, batch in enumerate(loader):
+            batch = move_to(batch, ctx.device)
+            micro_idx = global_step % accum
+            sync = (micro_idx == accum - 1) or (bi == n_batches - 1)
+            ctx_mgr = contextlib.nullcontext() if sync else engine.no_sync()
+            with ctx_mgr:
+                loss, metrics = step_fn(batch)
+                (loss / accum).backward()
+            if sync:
+                lr = scheduler.lr(global_step) if scheduler is not None else None
+                engine.step(lr)
+            if scheduler is not None:
+                scheduler.step()
+            running.update(loss.detach())
+            last_metrics = metrics
+            global_step += 1
+            if log_every and global_step % log_every == 0:
+                rec = {"train/loss": running.average, "train/grad_norm": engine.last_grad_norm}
+                if scheduler is not None:
+                    rec["train/lr"] = scheduler.lr(global_step)
+                if extra_log_fn is not None:
+                    rec.update(extra_log_fn(global_step, metrics))
+                ctx.logger.log(rec, global_step)
+                running = RunningLoss()
+            if eval_fn is not None and eval_every and global_step % eval_every == 0:
+                ctx.logger.log(eval_fn(global_step), global_step)
+            if save_every and global_step % save_every == 0:
+                save_state(Path(ctx.output_dir) / f"step_{global_step}", models_to_save, engine,
+                           scheduler, global_step, tokenizer, keep_last=keep_last)
+            if global_step >= total_steps:
+                done = True
+                break
+        epoch += 1
+        if n_batches == 0:
+            raise RuntimeError("empty training dataset")
+    save_state(Path(ctx.output_dir) / "final", models_to_save, engine, scheduler, global_step, tokenizer)
+    return global_step

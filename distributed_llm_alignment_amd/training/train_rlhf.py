@@ -1,0 +1,150 @@
+"""KL-penalised policy-gradient RLHF ("PPO-style"; reference: src/training/train_rlhf.py:61-166).
+
+Per step: sample `ppo.batch_size` prompts (same seed on every rank), take this rank's contiguous
+slice (fixes Appendix A #1), left-pad and generate with the native KV-cache decoder (HIP flash
+attention over the cache), score `prompt\\n\\nresponse` with the reward model (eval mode, no grad:
+fixes #8), then REINFORCE with a KL-shaped reward and a mean baseline:
+    kl = logp_pi - logp_ref ;  r' = r - kl_coef*kl ;  A = r' - mean(r') ;  loss = -mean(A * logp_pi)
+(fused HIP kernel). The log-prob mask covers prompt + generated tokens up to and including EOS
+(fixes #10). `generation_params.do_sample` defaults to True (#9).
+
+Overlap (BASELINE north star, `ppo.async_rollouts: true`, off by default since it changes the
+semantics to one-step-stale rollouts): step k+1's rollouts are generated while step k's gradient
+reduce-scatter is still in flight on RCCL's stream.
+"""
+from __future__ import annotations
+
+import argparse
+import random
+from pathlib import Path
+from typing import Dict, List
+
+import torch
+
+from ..data import read_jsonl
+from ..models import build_reward_model, generate, load_causal_lm, load_reward_checkpoint
+from ..objectives import rlhf_loss
+from ..parallel.dist import barrier, split_for_rank
+from ..utils.checkpoint import save_state
+from ..utils.config import add_config_args, config_from_args
+from ..utils.logging import RunningLoss
+from .common import make_engine, setup
+
+
+def parse_args(argv=None) -> argparse.Namespace:
+    return add_config_args(argparse.ArgumentParser(description="RLHF PPO loop")).parse_args(argv)
+
+
+def load_prompts(cfg: Dict[str, str]) -> List[str]:
+    source = cfg.get("source", "local")
+    if source == "hf":
+        try:
+            from datasets import load_dataset
+
+            ds = load_dataset(cfg["hf_path"], cfg.get("hf_name"), split=cfg.get("split", "train"))
+            key = cfg.get("prompt_key", "prompt")
+            return [row[key] for row in ds if row.get(key)]
+        except Exception:
+            if not (cfg.get("prompt_path") or cfg.get("path")):
+                raise
+    if source == "synthetic":
+        from ..data.synthetic import synthetic_prompt_records
+
+        return [r["prompt"] for r in synthetic_prompt_records(int(cfg.get("num_samples", 256)))]
+    path = cfg.get("prompt_path") or cfg.get("path")
+    return [r["prompt"] for r in read_jsonl(path) if r.get("prompt")]
+
+
+def _tokenize_left(tok, texts, max_len, device):
+    side = getattr(tok, "padding_side", "right")
+    tok.padding_side = "left"
+    enc = tok(texts, return_tensors="pt", padding=True, truncation=True, max_length=max_len)
+    tok.padding_side = side
+    return enc["input_ids"].to(device), enc["attention_mask"].to(device)
+
+
+def main(argv=None) -> int:
+    args = parse_args(argv)
+    config = config_from_args(args)
+    ctx = setup(config, "rlhf", default_seed=0)
+    model_cfg: Dict = config["model"]
+    ppo = config["ppo"]
+    policy = load_causal_lm(model_cfg["policy_model_name_or_path"],
+                            gradient_checkpointing=model_cfg.get("gradient_checkpointing", True),
+                            device=ctx.device, seed=ctx.seed)
+    ref = load_causal_lm(model_cfg["reference_model_name_or_path"], gradient_checkpointing=False,
+                         device=ctx.device, seed=ctx.seed)
+    ref.model.eval().requires_grad_(False)
+    rcfg = config.get("reward_model", {}) or {}
+    rbase = rcfg.get("base_model_name_or_path", model_cfg["policy_model_name_or_path"])
+    rpath = rcfg.get("path")
+    if rpath and Path(rpath).is_dir() and (Path(rpath) / "config.json").exists() and "base_model_name_or_path" not in rcfg:
+        rbase = rpath
+    rm, rtok = build_reward_model(rbase, pooling="last_token", dropout=0.1, device=ctx.device, seed=ctx.seed)
+    if rpath and Path(rpath).exists():
+        ctx.log(f"Loaded reward weights from {load_reward_checkpoint(rm, rpath)}")
+    rm.eval().requires_grad_(False)
+
+    prompts = load_prompts(config["sampling"])
+    gen = dict(ppo.get("generation_params", {"max_new_tokens": 256}))
+    gen.setdefault("do_sample", True)
+    engine = make_engine(ctx, policy.model, lr=ppo.get("learning_rate", 1e-6), betas=(0.9, 0.95),
+                         weight_decay=ppo.get("weight_decay", 0.01),
+                         max_grad_norm=ppo.get("max_grad_norm", 1.0))
+    steps = ppo.get("steps", 1024)
+    batch_size = ppo.get("batch_size", 64)
+    kl_coef = ppo.get("kl_coef", 0.1)
+    max_len = model_cfg.get("max_seq_length", 1024)
+    tok = policy.tokenizer
+    rng = random.Random(ctx.seed)
+    gen_g = torch.Generator(device=ctx.device)
+    gen_g.manual_seed(ctx.seed * 1000 + ctx.dist.rank)
+    running = RunningLoss()
+    log_every = (config.get("logging", {}) or {}).get("log_every_steps", 10)
+
+    def rollout():
+        batch_prompts = rng.sample(prompts, k=min(batch_size, len(prompts)))
+        mine = split_for_rank(batch_prompts)
+        ids, am = _tokenize_left(tok, mine, max_len, ctx.device)
+        seqs, mask = generate(policy.model, ids, am, max_new_tokens=gen.get("max_new_tokens", 256),
+                              do_sample=gen["do_sample"], temperature=gen.get("temperature", 1.0),
+                              top_p=gen.get("top_p", 1.0), top_k=gen.get("top_k", 0),
+                              pad_token_id=tok.pad_token_id, eos_token_id=getattr(tok, "eos_token_id", None),
+                              generator=gen_g, return_mask=True)
+        responses = tok.batch_decode(seqs[:, ids.shape[1]:], skip_special_tokens=True)
+        fused = [f"{p}\n\n{r}" for p, r in zip(mine, responses)]
+        renc = rtok(fused, return_tensors="pt", padding=True, truncation=True, max_length=max_len)
+        with torch.no_grad():
+            scores = rm(renc["input_ids"].to(ctx.device), renc["attention_mask"].to(ctx.device))
+        return seqs, mask, scores
+
+    policy.model.train()
+    pending = rollout()
+    for step in range(steps):
+        seqs, mask, scores = pending
+        loss, m = rlhf_loss(policy.model, ref.model, seqs, mask, scores, kl_coef)
+        loss.backward()
+        if ppo.get("async_rollouts", False) and step + 1 < steps:
+            # the bucketed reduce-scatter launched by the backward hooks is in flight on RCCL's
+            # stream; generating the next rollouts (pre-update weights) overlaps it
+            pending = rollout()
+            engine.step()
+        else:
+            engine.step()
+            if step + 1 < steps:
+                pending = rollout()
+        running.update(loss.detach())
+        if (step + 1) % log_every == 0:
+            ctx.logger.log({"train/loss": running.average, "train/kl": m["kl"],
+                            "train/reward_mean": scores.mean(), "train/grad_norm": engine.last_grad_norm},
+                           step + 1)
+            running = RunningLoss()
+    barrier()
+    save_state(config["logging"]["output_dir"], [policy.model, ref.model, rm], engine, None, steps, tok)
+    ctx.log("RLHF PPO loop complete")
+    ctx.logger.close()
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())
