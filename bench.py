@@ -50,10 +50,14 @@ def main() -> int:
     from distributed_llm_alignment_amd.parallel.data_parallel import DataParallelEngine
     from distributed_llm_alignment_amd.parallel.dist import barrier, init_distributed
 
+    from distributed_llm_alignment_amd.utils.tuning import enable_gemm_tuning
+
     st = init_distributed()
     dev = st.device
+    gemm_mode = "off"
     if dev.type == "cuda":
         _ext.require()
+        gemm_mode = enable_gemm_tuning(dev.index)
     world = st.world_size
     overrides = {} if args.layers is None else {"num_layers": args.layers}
     cfg = get_config(args.model, **overrides)
@@ -152,6 +156,7 @@ def main() -> int:
                 "ref_model": "frozen, co-resident",
                 "model_tflops_per_gpu": round(tflops_gpu, 1),
                 "final_loss": round(float(state["loss"].item()), 5),
+                "gemm_selection": "tunableop:" + gemm_mode,
             },
         }
         print(json.dumps(rec), flush=True)

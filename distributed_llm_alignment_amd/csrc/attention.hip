@@ -50,11 +50,17 @@ __device__ __forceinline__ s16x8 cat4(s16x4 a, s16x4 b) {
 }
 
 __device__ __forceinline__ s16x8 pack8(const f32x16& x, int base) {
-  s16x8 r;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = static_cast<short>(f2bf(x[base + j]));
-  return r;
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 r = {pack2bf(x[base], x[base + 1]), pack2bf(x[base + 2], x[base + 3]),
+             pack2bf(x[base + 4], x[base + 5]), pack2bf(x[base + 6], x[base + 7])};
+  return __builtin_bit_cast(s16x8, r);
 }
+
+__device__ __forceinline__ float ex2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// Deferred-max threshold (cdna guide T13, log2 units): the running max is only raised when a
+// tile's max exceeds it by more than this, so most tiles skip the O rescale. P <= 2^8.
+constexpr float kRescaleThr = 8.0f;
 
 __device__ __forceinline__ f32x16 mfma32(s16x8 a, s16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
@@ -110,11 +116,20 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams p) {
   const bf16_t* kp = p.k + b * p.k_sb + static_cast<int64_t>(hk) * p.k_sh;
   const bf16_t* vp = p.v + b * p.v_sb + static_cast<int64_t>(hk) * p.v_sh;
 
+  // Q fragments stay in registers, pre-scaled by softmax_scale*log2(e) so the scores come
+  // out of the MFMA already in the exp2 domain (no per-score multiply).
   s16x8 qf[KS];
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
-    if (qi < p.Tq) qf[s] = *reinterpret_cast<const s16x8*>(qp + qi * p.q_st + 16 * s + 8 * h);
-    else qf[s] = s16x8{};
+    if (qi < p.Tq) {
+      const bf16x8 raw = load_bf16x8(qp + qi * p.q_st + 16 * s + 8 * h);
+      float t[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) t[j] = bf2f(raw[j]) * p.scale2;
+      qf[s] = __builtin_bit_cast(s16x8, pack_bf16x8(t));
+    } else {
+      qf[s] = s16x8{};
+    }
   }
 
   f32x16 o[DT];
@@ -181,37 +196,48 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams p) {
         sacc[st] = mfma32(a, qf[s], sacc[st]);
       }
     }
-    // scale + mask, per-lane column (query qi) maxima
-    float mloc = -INFINITY;
+    // mask only tiles that touch a boundary (kv range, causal diagonal, window edge)
+    bool need_mask = kt < kbeg || kt + BK > kend;
+    if (CAUSAL) {
+      need_mask = need_mask || (kt + BK - 1 > q0 + p.causal_off);
+      if (p.window > 0) need_mask = need_mask || (kt <= q0 + 31 + p.causal_off - p.window);
+    }
+    if (need_mask) {
 #pragma unroll
-    for (int st = 0; st < 2; ++st) {
+      for (int st = 0; st < 2; ++st) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int key = kt + 32 * st + (i & 3) + 8 * (i >> 2) + 4 * h;
-        float x = sacc[st][i] * p.scale2;
-        bool ok = key >= kbeg && key < kend;
-        if (CAUSAL) {
-          ok = ok && key <= qi + p.causal_off;
-          if (p.window > 0) ok = ok && key > qi + p.causal_off - p.window;
+        for (int i = 0; i < 16; ++i) {
+          const int key = kt + 32 * st + (i & 3) + 8 * (i >> 2) + 4 * h;
+          bool ok = key >= kbeg && key < kend;
+          if (CAUSAL) {
+            ok = ok && key <= qi + p.causal_off;
+            if (p.window > 0) ok = ok && key > qi + p.causal_off - p.window;
+          }
+          sacc[st][i] = ok ? sacc[st][i] : -INFINITY;
         }
-        x = ok ? x : -INFINITY;
-        sacc[st][i] = x;
-        mloc = fmaxf(mloc, x);
       }
     }
-    mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
-    const float mnew = fmaxf(m, mloc);
-    const float muse = mnew == -INFINITY ? 0.f : mnew;
-    const float alpha = exp2f(m - muse);
-    m = mnew;
-    lsum *= alpha;
+    float mloc = -INFINITY;
 #pragma unroll
-    for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
+    for (int st = 0; st < 2; ++st)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) mloc = fmaxf(mloc, sacc[st][i]);
+    mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+    // deferred max: rescale O only when some row's max grew by more than kRescaleThr
+    if (!__all(mloc <= m + kRescaleThr)) {
+      const float mnew = fmaxf(m, mloc);
+      const float alpha = ex2(m - (mnew == -INFINITY ? 0.f : mnew));
+      m = mnew;
+      lsum *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
+    }
+    const float muse = m == -INFINITY ? 0.f : m;
 #pragma unroll
     for (int st = 0; st < 2; ++st) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const float pv = exp2f(sacc[st][i] - muse);
+        const float pv = ex2(sacc[st][i] - muse);
         sacc[st][i] = pv;
         lsum += pv;
       }
@@ -347,38 +373,65 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnBwdParams p) {
   const int qt0 = (qlo / BQ) * BQ;
 
   constexpr int QCPT = BQ * NCH / 256;  // chunks per thread for a [32][D] tile (D=128 -> 2)
-  for (int hh = 0; hh < group && block_has_keys; ++hh) {
-    const int hq = hk * group + hh;
+  __shared__ float rowc[2][BQ];           // per-query lse2 / delta of the current tile
+  const int nqt = qhi > qt0 ? (qhi - qt0 + BQ - 1) / BQ : 0;
+  const int n_iter = block_has_keys ? group * nqt : 0;
+  const int64_t dq_st = static_cast<int64_t>(p.Hq) * D;
+
+  // register prefetch of the NEXT (head, q-tile) while the current one is computed (T14)
+  bf16x8 qreg[QCPT], dreg[QCPT];
+  float rreg = 0.f;
+  auto prefetch = [&](int it) {
+    const int hq = hk * group + it / nqt;
+    const int qt = qt0 + (it % nqt) * BQ;
     const bf16_t* qp = p.q + b * p.q_sb + static_cast<int64_t>(hq) * p.q_sh;
     const bf16_t* dop = p.dout + b * p.do_sb + static_cast<int64_t>(hq) * p.do_sh;
-    const float* lsep = p.lse2 + (static_cast<int64_t>(b) * p.Hq + hq) * p.Tq;
-    const float* dlp = p.delta + (static_cast<int64_t>(b) * p.Hq + hq) * p.Tq;
+#pragma unroll
+    for (int c = 0; c < QCPT; ++c) {
+      const int ci = tid + 256 * c;
+      const int row = ci / NCH, ch = ci % NCH;
+      const int qq = qt + row;
+      qreg[c] = qq < p.Tq ? load_bf16x8(qp + qq * p.q_st + ch * 8) : bf16x8{};
+      dreg[c] = qq < p.Tq ? load_bf16x8(dop + qq * p.do_st + ch * 8) : bf16x8{};
+    }
+    if (tid < 2 * BQ) {
+      const int qq = qt + (tid & (BQ - 1));
+      const float* src = (tid < BQ ? p.lse2 : p.delta) + (static_cast<int64_t>(b) * p.Hq + hq) * p.Tq;
+      rreg = qq < p.Tq ? src[qq] : 0.f;
+    }
+  };
+  if (n_iter > 0) prefetch(0);
+
+  for (int it = 0; it < n_iter; ++it) {
+    const int hq = hk * group + it / nqt;
+    const int qt = qt0 + (it % nqt) * BQ;
     float* dqp = p.dq + (static_cast<int64_t>(b) * p.Tq) * p.Hq * D + static_cast<int64_t>(hq) * D;
-    const int64_t dq_st = static_cast<int64_t>(p.Hq) * D;
-
-    for (int qt = qt0; qt < qhi; qt += BQ) {
-      // stage Q and dO tiles
-      bf16x8 qreg[QCPT], dreg[QCPT];
+    __syncthreads();  // previous iteration finished with Qs/dOs/dSs/rowc
 #pragma unroll
-      for (int c = 0; c < QCPT; ++c) {
-        const int ci = tid + 256 * c;
-        const int row = ci / NCH, ch = ci % NCH;
-        const int qq = qt + row;
-        qreg[c] = qq < p.Tq ? load_bf16x8(qp + qq * p.q_st + ch * 8) : bf16x8{};
-        dreg[c] = qq < p.Tq ? load_bf16x8(dop + qq * p.do_st + ch * 8) : bf16x8{};
-      }
-      __syncthreads();  // previous iteration finished with Qs/dOs/dSs
-#pragma unroll
-      for (int c = 0; c < QCPT; ++c) {
-        const int ci = tid + 256 * c;
-        const int row = ci / NCH, ch = ci % NCH;
-        store_bf16x8(Qs + swz<D>(row, ch), qreg[c]);
-        store_bf16x8(dOs + swz<D>(row, ch), dreg[c]);
-      }
-      __syncthreads();
+    for (int c = 0; c < QCPT; ++c) {
+      const int ci = tid + 256 * c;
+      const int row = ci / NCH, ch = ci % NCH;
+      store_bf16x8(Qs + swz<D>(row, ch), qreg[c]);
+      store_bf16x8(dOs + swz<D>(row, ch), dreg[c]);
+    }
+    if (tid < 2 * BQ) rowc[tid / BQ][tid & (BQ - 1)] = rreg;
+    __syncthreads();
+    if (it + 1 < n_iter) prefetch(it + 1);
 
+    // does this wave's key slice see any query of the tile? (wave-uniform)
+    bool wave_active = kw < kend && kw + 32 > kbeg;
+    bool need_mask = kw < kbeg || kw + 32 > kend || qt + BQ > p.Tq;
+    if (CAUSAL) {
+      wave_active = wave_active && kw <= qt + BQ - 1 + p.causal_off;
+      need_mask = need_mask || (kw + 31 > qt + p.causal_off);
+      if (p.window > 0) {
+        wave_active = wave_active && (kw + 31 > qt + p.causal_off - p.window);
+        need_mask = need_mask || (kw <= qt + BQ - 1 + p.causal_off - p.window);
+      }
+    }
+    f32x16 sacc = f32x16{}, dpacc = f32x16{};
+    if (wave_active) {
       // S (rows = queries, cols = this wave's keys) and dP = dO V^T
-      f32x16 sacc = f32x16{}, dpacc = f32x16{};
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
         const s16x8 aq = *reinterpret_cast<const s16x8*>(Qs + swz<D>(l32, 2 * s + h));
@@ -391,17 +444,19 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnBwdParams p) {
       // P and dS (rows i -> query qt + (i&3) + 8(i>>2) + 4h, column -> key kj)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const int qq = qt + (i & 3) + 8 * (i >> 2) + 4 * h;
-        bool ok = qq < p.Tq && kj >= kbeg && kj < kend;
-        if (CAUSAL) {
-          ok = ok && kj <= qq + p.causal_off;
-          if (p.window > 0) ok = ok && kj > qq + p.causal_off - p.window;
+        const int r = (i & 3) + 8 * (i >> 2) + 4 * h;
+        float pv = ex2(fmaf(sacc[i], p.scale2, -rowc[0][r]));
+        if (need_mask) {
+          const int qq = qt + r;
+          bool ok = qq < p.Tq && kj >= kbeg && kj < kend;
+          if (CAUSAL) {
+            ok = ok && kj <= qq + p.causal_off;
+            if (p.window > 0) ok = ok && kj > qq + p.causal_off - p.window;
+          }
+          pv = ok ? pv : 0.f;
         }
-        const float l2 = ok ? lsep[qq] : 0.f;
-        const float dl = ok ? dlp[qq] : 0.f;
-        const float pv = ok ? exp2f(sacc[i] * p.scale2 - l2) : 0.f;
         sacc[i] = pv;
-        dpacc[i] = pv * (dpacc[i] - dl);
+        dpacc[i] = pv * (dpacc[i] - rowc[1][r]);
       }
       const s16x8 pb0 = pack8(sacc, 0), pb1 = pack8(sacc, 8);
       const s16x8 sb0 = pack8(dpacc, 0), sb1 = pack8(dpacc, 8);
@@ -414,39 +469,38 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnBwdParams p) {
         dk[dt] = mfma32(tr_frag_perm<D>(Qs, 4 * h, c0, lane), sb0, dk[dt]);
         dk[dt] = mfma32(tr_frag_perm<D>(Qs, 16 + 4 * h, c0, lane), sb1, dk[dt]);
       }
-      __syncthreads();  // everyone done reading Qs/dOs
-      // dS^T image [key 0..127][query 0..31], 64-B rows: lane writes its key row,
-      // 4 groups of 4 consecutive queries (8 B each).
+    }
+    __syncthreads();  // everyone done reading Qs/dOs
+    // dS^T image [key 0..127][query 0..31], 64-B rows: lane writes its key row,
+    // 4 groups of 4 consecutive queries (8 B each).
 #pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int qq = 8 * g4 + 4 * h;
-        uint2 pk;
-        pk.x = pack2bf(dpacc[4 * g4 + 0], dpacc[4 * g4 + 1]);
-        pk.y = pack2bf(dpacc[4 * g4 + 2], dpacc[4 * g4 + 3]);
-        *reinterpret_cast<uint2*>(dSs + (32 * w + l32) * 32 + qq) = pk;
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int qq = 8 * g4 + 4 * h;
+      uint2 pk;
+      pk.x = pack2bf(dpacc[4 * g4 + 0], dpacc[4 * g4 + 1]);
+      pk.y = pack2bf(dpacc[4 * g4 + 2], dpacc[4 * g4 + 3]);
+      *reinterpret_cast<uint2*>(dSs + (32 * w + l32) * 32 + qq) = pk;
+    }
+    __syncthreads();
+    // dQ[q][d] for d in this wave's slices: sum over 128 keys. A = dS (q rows, keys k) via
+    // transposed reads of dS^T; B = K (keys, d cols) via transposed reads of K.
+    for (int dt = w; dt < DT; dt += 4) {
+      f32x16 dqacc = f32x16{};
+#pragma unroll
+      for (int s = 0; s < BKV / 16; ++s) {
+        const int i16 = lane & 15, qq2 = i16 >> 2, pp = i16 & 3;
+        const int r0 = 16 * s + 8 * h;
+        const int col = 16 * ((lane >> 4) & 1) + 4 * pp;  // query column block
+        const s16x4 a0 = tr_read(dSs + (r0 + qq2) * 32 + col);
+        const s16x4 a1 = tr_read(dSs + (r0 + 4 + qq2) * 32 + col);
+        const s16x8 bkf = tr_frag_nat<D>(Ks, r0, 32 * dt + 16 * ((lane >> 4) & 1), lane);
+        dqacc = mfma32(cat4(a0, a1), bkf, dqacc);
       }
-      __syncthreads();
-      // dQ[q][d] for d in this wave's slices: sum over 128 keys. A = dS (q rows, keys k) via
-      // transposed reads of dS^T; B = K (keys, d cols) via transposed reads of K.
-      for (int dt = w; dt < DT; dt += 4) {
-        f32x16 dqacc = f32x16{};
+      // accumulate: lane holds d = 32dt + l32 (col), rows q = (i&3) + 8(i>>2) + 4h
 #pragma unroll
-        for (int s = 0; s < BKV / 16; ++s) {
-          // A: lane (q = l32) needs dS[q][16s + 8h + j]  -> rows of dS^T image, column q
-          const int i16 = lane & 15, qq2 = i16 >> 2, pp = i16 & 3;
-          const int r0 = 16 * s + 8 * h;
-          const int col = 16 * ((lane >> 4) & 1) + 4 * pp;  // query column block
-          const s16x4 a0 = tr_read(dSs + (r0 + qq2) * 32 + col);
-          const s16x4 a1 = tr_read(dSs + (r0 + 4 + qq2) * 32 + col);
-          const s16x8 bkf = tr_frag_nat<D>(Ks, r0, 32 * dt + 16 * ((lane >> 4) & 1), lane);
-          dqacc = mfma32(cat4(a0, a1), bkf, dqacc);
-        }
-        // accumulate: lane holds d = 32dt + l32 (col), rows q = (i&3) + 8(i>>2) + 4h
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int qq = qt + (i & 3) + 8 * (i >> 2) + 4 * h;
-          if (qq < p.Tq) atomicAdd(dqp + qq * dq_st + 32 * dt + l32, dqacc[i] * p.scale);
-        }
+      for (int i = 0; i < 16; ++i) {
+        const int qq = qt + (i & 3) + 8 * (i >> 2) + 4 * h;
+        if (qq < p.Tq) atomicAdd(dqp + qq * dq_st + 32 * dt + l32, dqacc[i] * p.scale);
       }
     }
   }

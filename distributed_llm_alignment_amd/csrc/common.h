@@ -30,17 +30,25 @@ __device__ __forceinline__ float bf2f(bf16_t v) {
   return __uint_as_float(static_cast<uint32_t>(v) << 16);
 }
 
-// Round-to-nearest-even fp32 -> bf16, NaN preserving (quietened).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 hbf16x2 __attribute__((ext_vector_type(2)));
+
+// fp32 -> bf16 round-to-nearest-even, NaN preserving: a plain cast lowers to the gfx950
+// hardware v_cvt_pk_bf16_f32 (the integer-rounding form costs ~5 VALU ops per element).
 __device__ __forceinline__ bf16_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return static_cast<bf16_t>((u >> 16) | 0x40u);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return static_cast<bf16_t>(u >> 16);
+  return __builtin_bit_cast(bf16_t, static_cast<__bf16>(f));
 }
 
-// Pack two fp32 into one dword of two bf16 (lo in bits 0..15).
+// Pack two fp32 into one dword of two bf16 (lo in bits 0..15): ONE v_cvt_pk_bf16_f32.
 __device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
-  return static_cast<uint32_t>(f2bf(lo)) | (static_cast<uint32_t>(f2bf(hi)) << 16);
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{lo, hi}, hbf16x2));
+}
+
+// 8 fp32 -> 8 bf16 (16 bytes) with 4 packed conversions.
+__device__ __forceinline__ bf16x8 pack_bf16x8(const float* v) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 r = {pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7])};
+  return __builtin_bit_cast(bf16x8, r);
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

@@ -62,6 +62,10 @@ class TrainContext:
 
 def setup(cfg: Dict[str, Any], stage: str, default_seed: int = 0) -> TrainContext:
     st = init_distributed()
+    if st.device.type == "cuda":
+        from ..utils.tuning import enable_gemm_tuning
+
+        enable_gemm_tuning(st.device.index)
     seed = int(cfg.get("seed", default_seed))
     seed_everything(seed)
     lg = cfg.get("logging", {}) or {}
