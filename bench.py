@@ -33,6 +33,7 @@ def parse():
     ap.add_argument("--accum", type=int, default=4)
     ap.add_argument("--beta", type=float, default=0.1)
     ap.add_argument("--zero", type=int, default=None)
+    ap.add_argument("--tp", type=int, default=1, help="tensor-parallel degree (dp = gpus / tp)")
     ap.add_argument("--bucket-mb", type=float, default=256.0)
     ap.add_argument("--profile-dir", default=None, help="write a torch.profiler trace of 1 step")
     ap.add_argument("--layers", type=int, default=None, help="debug only: override layer count "
@@ -49,6 +50,8 @@ def main() -> int:
     from distributed_llm_alignment_amd.ops import _ext
     from distributed_llm_alignment_amd.parallel.data_parallel import DataParallelEngine
     from distributed_llm_alignment_amd.parallel.dist import barrier, init_distributed
+    from distributed_llm_alignment_amd.parallel.mesh import build_mesh
+    from distributed_llm_alignment_amd.parallel.tensor_parallel import apply_tensor_parallel
 
     from distributed_llm_alignment_amd.utils.tuning import enable_gemm_tuning
 
@@ -59,6 +62,7 @@ def main() -> int:
         _ext.require()
         gemm_mode = enable_gemm_tuning(dev.index)
     world = st.world_size
+    mesh = build_mesh(tp=args.tp)
     overrides = {} if args.layers is None else {"num_layers": args.layers}
     cfg = get_config(args.model, **overrides)
     dtype = torch.bfloat16 if dev.type == "cuda" else torch.float32
@@ -68,11 +72,15 @@ def main() -> int:
     ref.eval()
     for p in ref.parameters():
         p.requires_grad_(False)
+    if mesh.tp > 1:
+        apply_tensor_parallel(policy, mesh.tp_group)
+        apply_tensor_parallel(ref, mesh.tp_group)
     engine = DataParallelEngine(policy, lr=1e-6, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01,
-                                max_grad_norm=1.0, zero_stage=args.zero, bucket_mb=args.bucket_mb)
+                                max_grad_norm=1.0, zero_stage=args.zero, bucket_mb=args.bucket_mb,
+                                group=mesh.dp_group, tp_group=mesh.tp_group)
     policy.train()
 
-    gen = torch.Generator().manual_seed(17 + st.rank)
+    gen = torch.Generator().manual_seed(17 + mesh.dp_rank)  # TP ranks share a batch
     n_batches = 4
     batches = [synthetic_preference_batch(args.micro_pairs, args.seq_len, cfg.vocab_size, device=dev,
                                           generator=gen) for _ in range(n_batches)]
@@ -125,7 +133,7 @@ def main() -> int:
         with open(os.path.join(args.profile_dir, "kernels.txt"), "w") as fh:
             fh.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=60))
 
-    pairs_per_step = args.micro_pairs * args.accum * world
+    pairs_per_step = args.micro_pairs * args.accum * mesh.dp
     ms = elapsed / args.steps * 1000.0
     value = pairs_per_step * args.steps / elapsed
     # model FLOPs: policy fwd+bwd (3x) + ref fwd (1x) over 2*seq tokens per pair
@@ -150,7 +158,8 @@ def main() -> int:
                 "model": cfg.name if args.layers is None else f"{cfg.name}-L{args.layers}(debug)",
                 "global_batch": pairs_per_step,
                 "seq_len": args.seq_len,
-                "parallelism": f"dp{world}" + (f"-zero{engine.zero}" if world > 1 else ""),
+                "parallelism": f"dp{mesh.dp}" + (f"-tp{mesh.tp}" if mesh.tp > 1 else "")
+                               + (f"-zero{engine.zero}" if mesh.dp > 1 else ""),
                 "micro_batch_pairs": args.micro_pairs,
                 "grad_accum": args.accum,
                 "ref_model": "frozen, co-resident",

@@ -32,9 +32,9 @@ void launch_rope_fwd(const bf16_t*, int64_t, bf16_t*, bf16_t*, const float*, con
                      const int*, int64_t, int, int, int, int, int, int, hipStream_t);
 void launch_rope_bwd(const bf16_t*, const bf16_t*, bf16_t*, int64_t, const float*, const float*,
                      const int*, int64_t, int, int, int, int, int, int, hipStream_t);
-void launch_logprob_fwd(const bf16_t*, int64_t, int, int64_t, const int64_t*, float*, float*,
-                        hipStream_t);
-void launch_logprob_bwd(bf16_t*, int64_t, int, int64_t, const int64_t*, const float*,
+void launch_logprob_fwd(const bf16_t*, int64_t, int, int64_t, int64_t, const int64_t*, float*,
+                        float*, hipStream_t);
+void launch_logprob_bwd(bf16_t*, int64_t, int, int64_t, int64_t, const int64_t*, const float*,
                         const float*, hipStream_t);
 void launch_row_lse(const bf16_t*, int64_t, int, int64_t, float*, hipStream_t);
 void launch_ensemble_kl(bf16_t*, const bf16_t*, int64_t, int64_t, int, int, const float*,
@@ -407,7 +407,8 @@ static void check_logits(const at::Tensor& logits) {
   TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "logits must be [N, V] row-major");
 }
 
-std::tuple<at::Tensor, at::Tensor> logprob_fwd(const at::Tensor& logits, const at::Tensor& tgt) {
+std::tuple<at::Tensor, at::Tensor> logprob_fwd(const at::Tensor& logits, const at::Tensor& tgt,
+                                               int64_t vocab_offset) {
   check_logits(logits);
   TORCH_CHECK(tgt.scalar_type() == at::kLong && tgt.is_contiguous() && tgt.numel() == logits.size(0),
               "targets int64 [N]");
@@ -417,13 +418,13 @@ std::tuple<at::Tensor, at::Tensor> logprob_fwd(const at::Tensor& logits, const a
   auto logp = at::empty({logits.size(0)}, opt);
   auto lse = at::empty({logits.size(0)}, opt);
   launch_logprob_fwd(cbp(logits), logits.stride(0), static_cast<int>(logits.size(1)),
-                     logits.size(0), tgt.data_ptr<int64_t>(), logp.data_ptr<float>(),
+                     vocab_offset, logits.size(0), tgt.data_ptr<int64_t>(), logp.data_ptr<float>(),
                      lse.data_ptr<float>(), cur_stream(logits));
   return {logp, lse};
 }
 
 void logprob_bwd(at::Tensor& logits, const at::Tensor& tgt, const at::Tensor& lse,
-                 const at::Tensor& grad) {
+                 const at::Tensor& grad, int64_t vocab_offset) {
   check_logits(logits);
   check_f32(lse, "lse");
   check_f32(grad, "grad");
@@ -431,8 +432,8 @@ void logprob_bwd(at::Tensor& logits, const at::Tensor& tgt, const at::Tensor& ls
   TORCH_CHECK(tgt.scalar_type() == at::kLong && tgt.numel() == N && tgt.is_contiguous(), "targets");
   TORCH_CHECK(lse.numel() == N && grad.numel() == N && grad.is_contiguous(), "lse/grad shape");
   c10::hip::HIPGuardMasqueradingAsCUDA g(logits.device());
-  launch_logprob_bwd(bp(logits), logits.stride(0), static_cast<int>(logits.size(1)), N,
-                     tgt.data_ptr<int64_t>(), lse.data_ptr<float>(), grad.data_ptr<float>(),
+  launch_logprob_bwd(bp(logits), logits.stride(0), static_cast<int>(logits.size(1)), vocab_offset,
+                     N, tgt.data_ptr<int64_t>(), lse.data_ptr<float>(), grad.data_ptr<float>(),
                      cur_stream(logits));
 }
 
@@ -646,8 +647,8 @@ TORCH_LIBRARY(dla, m) {
   m.def("attn_fwd(Tensor q, Tensor k, Tensor v, float scale, bool causal, int causal_off, int window, Tensor? kv_start, Tensor? kv_end) -> (Tensor, Tensor)");
   m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse2, Tensor(a!) dk, Tensor(b!) dv, float scale, bool causal, int causal_off, int window, Tensor? kv_start, Tensor? kv_end) -> Tensor");
   m.def("f32_to_bf16_rows(Tensor src, Tensor(a!) dst) -> ()");
-  m.def("logprob_fwd(Tensor logits, Tensor targets) -> (Tensor, Tensor)");
-  m.def("logprob_bwd(Tensor(a!) logits, Tensor targets, Tensor lse, Tensor grad) -> ()");
+  m.def("logprob_fwd(Tensor logits, Tensor targets, int vocab_offset=0) -> (Tensor, Tensor)");
+  m.def("logprob_bwd(Tensor(a!) logits, Tensor targets, Tensor lse, Tensor grad, int vocab_offset=0) -> ()");
   m.def("row_lse(Tensor logits) -> Tensor");
   m.def("ensemble_kl(Tensor(a!) s_logits, Tensor t_logits, Tensor s_lse, Tensor t_lse, Tensor? grad, bool write_grad) -> Tensor");
   m.def("seq_reduce(Tensor lp, Tensor mask) -> (Tensor, Tensor)");

@@ -74,10 +74,12 @@ __device__ __forceinline__ void row_lse(const bf16_t* __restrict__ row, int V, f
   s_out = s;
 }
 
-// logp[r] = logits[r, tgt[r]] - lse[r]; ignored rows (tgt < 0) -> logp 0, lse still written.
+// logp[r] = logits[r, tgt[r] - off] - lse[r] when this vocab shard [off, off+V) owns the
+// target; rows with tgt < 0 (ignored) or a target owned by another shard -> logp 0. lse (of the
+// local shard) is always written. off = 0, V = full vocab for the unsharded LM head.
 template <bool VEC>
 __global__ __launch_bounds__(256) void logprob_fwd_kernel(const bf16_t* __restrict__ logits,
-                                                           int64_t ld, int V,
+                                                           int64_t ld, int V, int64_t off,
                                                            const int64_t* __restrict__ tgt,
                                                            float* __restrict__ logp,
                                                            float* __restrict__ lse_out) {
@@ -88,21 +90,23 @@ __global__ __launch_bounds__(256) void logprob_fwd_kernel(const bf16_t* __restri
   if (threadIdx.x == 0) {
     const float lse = m + __logf(s);
     lse_out[r] = lse;
-    const int64_t t = tgt[r];
-    logp[r] = (t >= 0 && t < V) ? bf2f(row[t]) - lse : 0.f;
+    const int64_t t = tgt[r] - off;
+    logp[r] = (tgt[r] >= 0 && t >= 0 && t < V) ? bf2f(row[t]) - lse : 0.f;
   }
 }
 
-// In place: logits[r, v] <- g[r] * (1[v == tgt] - exp(logits - lse)). g = dL/dlogp[r].
+// In place: logits[r, v] <- g[r] * (1[v == tgt - off] - exp(logits - lse)), g = dL/dlogp[r];
+// lse is the GLOBAL (all-shard) log-sum-exp. Ignored rows (tgt < 0) -> 0.
 template <bool VEC>
 __global__ __launch_bounds__(256) void logprob_bwd_kernel(bf16_t* __restrict__ logits, int64_t ld,
-                                                           int V, const int64_t* __restrict__ tgt,
+                                                           int V, int64_t off,
+                                                           const int64_t* __restrict__ tgt,
                                                            const float* __restrict__ lse_in,
                                                            const float* __restrict__ g) {
   const int64_t r = blockIdx.x;
   bf16_t* row = logits + r * ld;
-  const int64_t t = tgt[r];
-  const float gr = (t >= 0 && t < V) ? g[r] : 0.f;
+  const int64_t t = tgt[r] - off;
+  const float gr = tgt[r] >= 0 ? g[r] : 0.f;
   const float lse = lse_in[r];
   if constexpr (VEC) {
     const int nv = V >> 3;
@@ -167,20 +171,20 @@ __global__ __launch_bounds__(256) void row_lse_kernel(const bf16_t* __restrict__
 }
 
 // ----------------------------------------------------------------------------------------------
-void launch_logprob_fwd(const bf16_t* logits, int64_t ld, int V, int64_t rows,
+void launch_logprob_fwd(const bf16_t* logits, int64_t ld, int V, int64_t off, int64_t rows,
                         const int64_t* tgt, float* logp, float* lse, hipStream_t st) {
   if (rows == 0) return;
   const bool vec = (V % 8 == 0) && (ld % 8 == 0);
-  if (vec) logprob_fwd_kernel<true><<<rows, 256, 0, st>>>(logits, ld, V, tgt, logp, lse);
-  else logprob_fwd_kernel<false><<<rows, 256, 0, st>>>(logits, ld, V, tgt, logp, lse);
+  if (vec) logprob_fwd_kernel<true><<<rows, 256, 0, st>>>(logits, ld, V, off, tgt, logp, lse);
+  else logprob_fwd_kernel<false><<<rows, 256, 0, st>>>(logits, ld, V, off, tgt, logp, lse);
 }
 
-void launch_logprob_bwd(bf16_t* logits, int64_t ld, int V, int64_t rows, const int64_t* tgt,
-                        const float* lse, const float* g, hipStream_t st) {
+void launch_logprob_bwd(bf16_t* logits, int64_t ld, int V, int64_t off, int64_t rows,
+                        const int64_t* tgt, const float* lse, const float* g, hipStream_t st) {
   if (rows == 0) return;
   const bool vec = (V % 8 == 0) && (ld % 8 == 0);
-  if (vec) logprob_bwd_kernel<true><<<rows, 256, 0, st>>>(logits, ld, V, tgt, lse, g);
-  else logprob_bwd_kernel<false><<<rows, 256, 0, st>>>(logits, ld, V, tgt, lse, g);
+  if (vec) logprob_bwd_kernel<true><<<rows, 256, 0, st>>>(logits, ld, V, off, tgt, lse, g);
+  else logprob_bwd_kernel<false><<<rows, 256, 0, st>>>(logits, ld, V, off, tgt, lse, g);
 }
 
 void launch_row_lse(const bf16_t* logits, int64_t ld, int V, int64_t rows, float* lse,

@@ -14,9 +14,15 @@ from ..parallel.dist import state as dist_state
 
 
 def get_distributed_sampler(dataset, shuffle: bool = True, seed: int = 0, drop_last: bool = False):
+    """Shard over DATA-parallel replicas: under tensor parallelism every rank of a TP group must
+    see the same samples, so the replica index is the mesh's dp_rank, not the global rank."""
+    from ..parallel.mesh import current_mesh
+
     st = dist_state()
-    if st.world_size > 1:
-        return DistributedSampler(dataset, num_replicas=st.world_size, rank=st.rank, shuffle=shuffle,
+    mesh = current_mesh()
+    n, r = (mesh.dp, mesh.dp_rank) if mesh is not None else (st.world_size, st.rank)
+    if n > 1:
+        return DistributedSampler(dataset, num_replicas=n, rank=r, shuffle=shuffle,
                                   seed=seed, drop_last=drop_last)
     return None
 

@@ -23,7 +23,8 @@ class KVCache:
     def __init__(self, model: CausalLM, batch: int, max_len: int, kv_start: Optional[torch.Tensor]):
         cfg = model.cfg
         dev, dt = model.embed.device, model.embed.dtype
-        L, Hkv, D = cfg.num_layers, cfg.num_kv_heads, cfg.head_dim
+        L, Hkv, D = cfg.num_layers, model.layers[0].attn.kv_local, cfg.head_dim
+        self.h_local, self.kv_local = model.layers[0].attn.h_local, Hkv
         self.cfg = cfg
         self.k = torch.empty((L, batch, max_len, Hkv, D), device=dev, dtype=dt)
         self.v = torch.empty((L, batch, max_len, Hkv, D), device=dev, dtype=dt)
@@ -45,7 +46,7 @@ class KVCache:
         B, T, _ = qkv.shape
         if self.len + T > self.max_len:
             raise RuntimeError("KV cache overflow")
-        q, k, v = ops.attention.rope_qk(qkv, rope, cfg.num_heads, cfg.num_kv_heads, cfg.head_dim,
+        q, k, v = ops.attention.rope_qk(qkv, rope, self.h_local, self.kv_local, cfg.head_dim,
                                         positions=self._pos)
         self.k[layer, :, self.len:self.len + T] = k
         self.v[layer, :, self.len:self.len + T] = v
@@ -53,7 +54,7 @@ class KVCache:
         o = ops.attention_core(q.contiguous(), self.k[layer, :, :end], self.v[layer, :, :end],
                                causal=True, causal_off=self.len, window=window,
                                kv_start=self.kv_start, kv_end=None)
-        return o.reshape(B, T, cfg.num_heads * cfg.head_dim)
+        return o.reshape(B, T, self.h_local * cfg.head_dim)
 
     def advance(self, T: int):
         self.len += T
@@ -118,6 +119,10 @@ def generate(model: CausalLM, input_ids: torch.Tensor, attention_mask: Optional[
     for step in range(max_new_tokens):
         logits = model.logits(last).float()
         nxt = sample_next(logits, do_sample, temperature, top_p, top_k, generator)
+        if model.tp_size > 1:  # every TP rank must continue with the same token
+            import torch.distributed as dist
+
+            dist.broadcast(nxt, src=dist.get_global_rank(model.tp, 0), group=model.tp)
         nxt = torch.where(finished, torch.full_like(nxt, pad), nxt)
         gen_mask.append((~finished).long())
         out.append(nxt.unsqueeze(1))

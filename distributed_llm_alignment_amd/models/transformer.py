@@ -56,18 +56,29 @@ class Attention(nn.Module):
         self.o_proj = _param(H, cfg.q_size, device=device, dtype=dtype)
         o_bias = cfg.attn_bias and cfg.arch in ("gpt2", "phi")
         self.o_bias = _param(H, device=device, dtype=dtype) if o_bias else None
+        self.tp = None  # tensor-parallel group (parallel.tensor_parallel.apply_tensor_parallel)
+        self.h_local, self.kv_local = cfg.num_heads, cfg.num_kv_heads
 
     def forward(self, h, rope, kv_start, kv_end, positions, cache=None, layer_idx=0):
         cfg = self.cfg
+        if self.tp is not None:
+            from ..parallel.tensor_parallel import tp_copy
+
+            h = tp_copy(h, self.tp)
         qkv = ops.linear(h, self.qkv_proj, self.qkv_bias)
         window = cfg.sliding_window if cfg.sliding_window else 0
         if cache is None:
-            a = ops.qkv_attention(qkv, cfg.num_heads, cfg.num_kv_heads, cfg.head_dim, rope,
+            a = ops.qkv_attention(qkv, self.h_local, self.kv_local, cfg.head_dim, rope,
                                   causal=True, window=window, kv_start=kv_start, kv_end=kv_end,
                                   positions=positions)
         else:
             a = cache.attend(layer_idx, qkv, rope, window)
-        return ops.linear(a, self.o_proj, self.o_bias)
+        if self.tp is None:
+            return ops.linear(a, self.o_proj, self.o_bias)
+        from ..parallel.tensor_parallel import tp_reduce
+
+        out = tp_reduce(ops.linear(a, self.o_proj, None), self.tp)
+        return out + self.o_bias if self.o_bias is not None else out
 
 
 class MLP(nn.Module):
@@ -82,11 +93,21 @@ class MLP(nn.Module):
         self.up_bias = _param(self.up_proj.shape[0], device=device, dtype=dtype) if cfg.mlp_bias else None
         self.down_proj = _param(H, Fd, device=device, dtype=dtype)
         self.down_bias = _param(H, device=device, dtype=dtype) if cfg.mlp_bias else None
+        self.tp = None
 
     def forward(self, h):
+        if self.tp is not None:
+            from ..parallel.tensor_parallel import tp_copy
+
+            h = tp_copy(h, self.tp)
         u = ops.linear(h, self.up_proj, self.up_bias)
         m = ops.swiglu(u) if self.cfg.activation == "swiglu" else ops.gelu_new(u)
-        return ops.linear(m, self.down_proj, self.down_bias)
+        if self.tp is None:
+            return ops.linear(m, self.down_proj, self.down_bias)
+        from ..parallel.tensor_parallel import tp_reduce
+
+        out = tp_reduce(ops.linear(m, self.down_proj, None), self.tp)
+        return out + self.down_bias if self.down_bias is not None else out
 
 
 class MoE(nn.Module):
@@ -187,6 +208,10 @@ class CausalLM(nn.Module):
         self.rope = (ops.RotaryCache(cfg.rot_dim, cfg.rope_theta, cfg.max_position_embeddings,
                                      cfg.rope_scaling) if cfg.rot_dim > 0 else None)
         self.gradient_checkpointing = False
+        self.tp = None             # set by parallel.tensor_parallel.apply_tensor_parallel
+        self.tp_size = 1
+        self.tp_rank = 0
+        self.vocab_parallel = None  # (vocab offset, local vocab) when embed/head are vocab-sharded
         if self.lm_head is None and not headless:
             # tied input/output embedding: its gradient arrives from two ops, so it must go through
             # autograd's AccumulateGrad (one hook call) rather than the GEMM main-grad path
@@ -225,7 +250,12 @@ class CausalLM(nn.Module):
         return self.embed if self.lm_head is None else self.lm_head
 
     def embed_tokens(self, input_ids, positions=None):
-        x = F.embedding(input_ids, self.embed)
+        if self.vocab_parallel is not None:
+            from ..parallel.tensor_parallel import vocab_parallel_embedding
+
+            x = vocab_parallel_embedding(input_ids, self.embed, self.vocab_parallel[0], self.tp)
+        else:
+            x = F.embedding(input_ids, self.embed)
         if self.wpe is not None:
             T = input_ids.shape[1]
             pos = positions.long() if positions is not None else torch.arange(T, device=input_ids.device)
@@ -261,7 +291,20 @@ class CausalLM(nn.Module):
         return h
 
     def logits(self, hidden: torch.Tensor) -> torch.Tensor:
-        return F.linear(hidden, self.head_weight, self.lm_head_bias)
+        lg = F.linear(hidden, self.head_weight, self.lm_head_bias)
+        if self.vocab_parallel is not None:
+            from ..parallel.tensor_parallel import tp_all_gather_last
+
+            lg = tp_all_gather_last(lg, self.tp)
+        return lg
+
+    def _token_logprob(self, h2: torch.Tensor, targets: torch.Tensor) -> torch.Tensor:
+        """Per-token log p(target) from final hidden rows [N, H] (fused HIP LM-head path)."""
+        if self.vocab_parallel is not None:
+            from ..parallel.tensor_parallel import vocab_parallel_logprob
+
+            return vocab_parallel_logprob(h2, self.head_weight, targets, self.vocab_parallel[0], self.tp)
+        return ops.linear_logprob(h2, self.head_weight, targets)
 
     def aux_loss(self):
         if not self.cfg.is_moe:
@@ -275,7 +318,10 @@ class CausalLM(nn.Module):
         h = self.forward(input_ids, attention_mask)
         if self.lm_head_bias is not None:
             return _biased_seq_logprob(self, h, input_ids, attention_mask, reduction)
-        return ops.sequence_logprob(h, self.head_weight, input_ids, attention_mask, reduction)
+        S, T, H = h.shape
+        tgt, mask = ops.shifted_targets(input_ids, attention_mask)
+        lp = self._token_logprob(h.reshape(S * T, H), tgt.reshape(-1)).view(S, T)
+        return ops.seq_reduce(lp, mask, mean=(reduction == "mean"))
 
     def causal_lm_loss(self, input_ids, labels, attention_mask=None):
         """HF ForCausalLMLoss (train_sft.py:145-146): mean token NLL over labels != -100."""
@@ -284,7 +330,12 @@ class CausalLM(nn.Module):
             lg = self.logits(h).float()
             return F.cross_entropy(lg[:, :-1].reshape(-1, lg.shape[-1]), labels[:, 1:].reshape(-1),
                                    ignore_index=-100)
-        return ops.token_nll(h, self.head_weight, labels)
+        S, T, H = h.shape
+        tgt = torch.full_like(labels, -100)
+        tgt[:, :-1] = labels[:, 1:]
+        tgt = tgt.reshape(-1)
+        lp = self._token_logprob(h.reshape(S * T, H), tgt)
+        return -(lp.sum() / (tgt >= 0).sum().clamp(min=1))
 
     # ----------------------------------------------------------------- HF key mapping
     def hf_state_dict(self) -> Dict[str, torch.Tensor]:

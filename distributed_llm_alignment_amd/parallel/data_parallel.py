@@ -57,11 +57,25 @@ class DataParallelEngine:
     def __init__(self, module: nn.Module, lr: float = 1e-5, betas=(0.9, 0.999), eps: float = 1e-8,
                  weight_decay: float = 0.0, max_grad_norm: float = 1.0, zero_stage: Optional[int] = None,
                  bucket_mb: float = 256.0, master_weights: bool = True,
-                 dist_st: Optional[DistState] = None, group=None):
+                 dist_st: Optional[DistState] = None, group=None, tp_group=None):
         self.module = module
         self.dist = dist_st or dist_state()
-        self.world = self.dist.world_size if self.dist.initialized else 1
-        self.rank = self.dist.rank if self.world > 1 else 0
+        # tensor parallel: grads of TP-sharded params differ per TP rank; params marked
+        # `_dla_tp_replicated` are identical across TP ranks (counted once in the clip norm)
+        self.tp_group = tp_group
+        self.tp_size = dist.get_world_size(tp_group) if (tp_group is not None and self.dist.initialized) else 1
+        if self.dist.initialized:
+            if group is not None:
+                self.world, self.rank = dist.get_world_size(group), dist.get_rank(group)
+            elif self.tp_size > 1:
+                # TP without a DP group: only legal when TP spans the whole world (dp = 1)
+                if self.tp_size != self.dist.world_size:
+                    raise ValueError("pass the data-parallel group (mesh.dp_group) when tp < world")
+                self.world, self.rank = 1, 0
+            else:
+                self.world, self.rank = self.dist.world_size, self.dist.rank
+        else:
+            self.world, self.rank = 1, 0
         self.group = group
         self.zero = (1 if self.world > 1 else 0) if zero_stage is None else (zero_stage if self.world > 1 else 0)
         self.lr, self.betas, self.eps, self.wd = lr, tuple(betas), eps, weight_decay
@@ -129,6 +143,19 @@ class DataParallelEngine:
         else:
             self.grad_shard = self.grad_buf
             self.param_shard = self.param_buf
+        # shard-coordinate ranges of TP-replicated params (for the clip norm)
+        self._repl_ranges = []
+        if self.tp_size > 1:
+            for b in self.buckets:
+                c = b.size // self.world
+                lo, hi = (b.start + self.rank * c, b.start + (self.rank + 1) * c) if self.zero else (b.start, b.end)
+                base = (b.shard_off - lo) if self.zero else 0
+                for p in b.params:
+                    if getattr(p, "_dla_tp_replicated", False):
+                        o = offsets[id(p)]
+                        a, e = max(lo, o), min(hi, o + p.numel())
+                        if a < e:
+                            self._repl_ranges.append((a + base, e + base))
         n_state = self.param_shard.numel()
         self.master = self.param_shard.float().clone() if master_weights else None
         self.exp_avg = torch.zeros(n_state, dtype=torch.float32, device=self.device)
@@ -194,8 +221,13 @@ class DataParallelEngine:
     def clip_and_norm(self):
         gs = 1.0 / self.world
         grad_sumsq(self.grad_shard, self._sumsq, accumulate=False)
+        if self._repl_ranges:
+            rep = sum(self.grad_shard[a:e].float().pow(2).sum() for a, e in self._repl_ranges)
+            self._sumsq -= (1.0 - 1.0 / self.tp_size) * rep
         if self.zero and self.world > 1:
             dist.all_reduce(self._sumsq, op=dist.ReduceOp.SUM, group=self.group)
+        if self.tp_size > 1:
+            dist.all_reduce(self._sumsq, op=dist.ReduceOp.SUM, group=self.tp_group)
         sumsq = self._sumsq * (gs * gs)
         norm, coef = clip_coefficient(sumsq, self.max_grad_norm if self.max_grad_norm else 0.0)
         self.last_grad_norm = norm
@@ -228,7 +260,8 @@ class DataParallelEngine:
     @torch.no_grad()
     def broadcast_params(self, src: int = 0):
         if self.world > 1:
-            dist.broadcast(self.param_buf, src=src, group=self.group)
+            gsrc = dist.get_global_rank(self.group, src) if self.group is not None else src
+            dist.broadcast(self.param_buf, src=gsrc, group=self.group)
             if self.zero:
                 self.param_shard.copy_(torch.cat([self._chunk(self.param_buf, b) for b in self.buckets]))
             if self.master is not None:

@@ -124,8 +124,13 @@ def destroy():
 def split_for_rank(items: list, rank: Optional[int] = None, world: Optional[int] = None) -> list:
     """Contiguous slice of `items` for this rank (fixes the reference's misuse of
     `split_between_processes` at train_rlhf.py:114, SURVEY Appendix A #1)."""
-    rank = _STATE.rank if rank is None else rank
-    world = _STATE.world_size if world is None else world
+    if rank is None or world is None:
+        from .mesh import current_mesh
+
+        m = current_mesh()  # data-parallel replicas: TP ranks of one replica share a slice
+        r0, w0 = (m.dp_rank, m.dp) if m is not None else (_STATE.rank, _STATE.world_size)
+        rank = r0 if rank is None else rank
+        world = w0 if world is None else world
     n = len(items)
     per, extra = divmod(n, world)
     start = rank * per + min(rank, extra)

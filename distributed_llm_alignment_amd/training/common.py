@@ -51,6 +51,11 @@ class TrainContext:
     seed: int
     stage: str
     extras: Dict[str, Any] = field(default_factory=dict)
+    mesh: Any = None
+
+    @property
+    def dp_size(self) -> int:
+        return self.mesh.dp if self.mesh is not None else self.dist.world_size
 
     @property
     def is_main(self) -> bool:
@@ -76,8 +81,30 @@ def setup(cfg: Dict[str, Any], stage: str, default_seed: int = 0) -> TrainContex
         Path(log_dir).mkdir(parents=True, exist_ok=True)
     logger = MetricsLogger(log_dir, st.is_main, use_wandb=bool(lg.get("use_wandb", False)),
                            config=cfg, run_name=cfg.get("experiment_name"))
-    return TrainContext(cfg=cfg, dist=st, device=st.device, logger=logger, hw=hardware_parallel(cfg),
-                        output_dir=out, log_dir=log_dir, seed=seed, stage=stage)
+    hw = hardware_parallel(cfg)
+    from ..parallel.mesh import build_mesh
+
+    mesh = build_mesh(tp=hw["tp_size"], ep=hw["ep_size"])  # collective; DP x TP x EP groups
+    return TrainContext(cfg=cfg, dist=st, device=st.device, logger=logger, hw=hw,
+                        output_dir=out, log_dir=log_dir, seed=seed, stage=stage, mesh=mesh)
+
+
+def parallelize(ctx: TrainContext, model):
+    """Apply the configured model parallelism (hardware.tp_size / ep_size) in place. Every rank
+    built the same seeded (or loaded) weights, so sharding is a local slice — no broadcast."""
+    m = ctx.mesh
+    if m is None:
+        return model
+    base = getattr(model, "backbone", model)
+    if m.tp > 1:
+        from ..parallel.tensor_parallel import apply_tensor_parallel
+
+        apply_tensor_parallel(model, m.tp_group)
+    if m.ep > 1 and base.cfg.is_moe:
+        from ..parallel.expert import apply_expert_parallel
+
+        apply_expert_parallel(model, m)
+    return model
 
 
 def make_engine(ctx: TrainContext, model, lr: float, betas=(0.9, 0.999), weight_decay: float = 0.0,
@@ -85,11 +112,13 @@ def make_engine(ctx: TrainContext, model, lr: float, betas=(0.9, 0.999), weight_
     return DataParallelEngine(model, lr=lr, betas=betas, weight_decay=weight_decay,
                               max_grad_norm=max_grad_norm, zero_stage=ctx.hw.get("zero_stage"),
                               bucket_mb=ctx.hw.get("bucket_mb", 256.0),
-                              master_weights=ctx.hw.get("master_weights", True))
+                              master_weights=ctx.hw.get("master_weights", True),
+                              group=ctx.mesh.dp_group if ctx.mesh is not None else None,
+                              tp_group=ctx.mesh.tp_group if ctx.mesh is not None else None)
 
 
 def effective_batch_msg(ctx: TrainContext, micro: int) -> str:
-    eff = micro * ctx.dist.world_size * ctx.hw["grad_accum"]
+    eff = micro * ctx.dp_size * ctx.hw["grad_accum"]
     target = (ctx.cfg.get("optimization", {}) or {}).get("total_batch_size", eff)
     return f"Effective global batch size: {eff} (target {target})"
 

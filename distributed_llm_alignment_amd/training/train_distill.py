@@ -16,7 +16,7 @@ from ..data import TeacherRolloutDataset, build_dataloader
 from ..models import load_causal_lm
 from ..objectives import distill_loss
 from ..utils.config import add_config_args, config_from_args
-from .common import effective_batch_msg, make_engine, setup, train_loop
+from .common import effective_batch_msg, make_engine, parallelize, setup, train_loop
 
 
 def parse_args(argv=None) -> argparse.Namespace:
@@ -45,6 +45,9 @@ def main(argv=None) -> int:
             tb = load_causal_lm(tp, gradient_checkpointing=False, device=ctx.device, seed=ctx.seed + 1 + i)
             tb.model.eval().requires_grad_(False)
             teachers.append(tb.model)
+    parallelize(ctx, student.model)
+    for t in teachers:
+        parallelize(ctx, t)
     tok = student.tokenizer
     ds = TeacherRolloutDataset(config["data"]["teacher_samples_path"], tok,
                                max_length=model_cfg.get("max_seq_length", 2048))

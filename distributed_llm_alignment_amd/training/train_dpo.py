@@ -25,7 +25,7 @@ from ..models import load_causal_lm
 from ..objectives import dpo_step_loss
 from ..optim.scheduler import LRSchedule
 from ..utils.config import add_config_args, config_from_args
-from .common import effective_batch_msg, make_engine, setup, train_loop
+from .common import effective_batch_msg, make_engine, parallelize, setup, train_loop
 
 
 def parse_args(argv=None) -> argparse.Namespace:
@@ -44,6 +44,8 @@ def main(argv=None) -> int:
                          device=ctx.device, seed=ctx.seed)
     ref.model.eval()
     ref.model.requires_grad_(False)
+    parallelize(ctx, policy.model)
+    parallelize(ctx, ref.model)
     tok = policy.tokenizer
     data_cfg = dict(config["data"])
     data_cfg["preference_path"] = data_cfg.get("preference_path")

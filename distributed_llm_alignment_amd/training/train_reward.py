@@ -14,7 +14,7 @@ from ..models import build_reward_model
 from ..objectives import reward_loss
 from ..parallel.dist import all_gather_tensor
 from ..utils.config import add_config_args, config_from_args
-from .common import effective_batch_msg, make_engine, move_to, setup, train_loop
+from .common import effective_batch_msg, make_engine, move_to, parallelize, setup, train_loop
 
 
 def parse_args(argv=None) -> argparse.Namespace:
@@ -48,6 +48,7 @@ def main(argv=None) -> int:
                                  dropout=model_cfg.get("dropout", 0.1), device=ctx.device, seed=ctx.seed)
     if model_cfg.get("gradient_checkpointing", False):
         rm.backbone.gradient_checkpointing_enable()
+    parallelize(ctx, rm)
     data_cfg = dict(config["data"])
     max_len = model_cfg.get("max_seq_length", 1024)
     opt = config["optimization"]

@@ -28,7 +28,7 @@ from ..parallel.dist import barrier, split_for_rank
 from ..utils.checkpoint import save_state
 from ..utils.config import add_config_args, config_from_args
 from ..utils.logging import RunningLoss
-from .common import make_engine, setup
+from .common import make_engine, parallelize, setup
 
 
 def parse_args(argv=None) -> argparse.Namespace:
@@ -84,6 +84,8 @@ def main(argv=None) -> int:
     if rpath and Path(rpath).exists():
         ctx.log(f"Loaded reward weights from {load_reward_checkpoint(rm, rpath)}")
     rm.eval().requires_grad_(False)
+    for m in (policy.model, ref.model, rm):
+        parallelize(ctx, m)
 
     prompts = load_prompts(config["sampling"])
     gen = dict(ppo.get("generation_params", {"max_new_tokens": 256}))
@@ -98,7 +100,7 @@ def main(argv=None) -> int:
     tok = policy.tokenizer
     rng = random.Random(ctx.seed)
     gen_g = torch.Generator(device=ctx.device)
-    gen_g.manual_seed(ctx.seed * 1000 + ctx.dist.rank)
+    gen_g.manual_seed(ctx.seed * 1000 + (ctx.mesh.dp_rank if ctx.mesh is not None else ctx.dist.rank))
     running = RunningLoss()
     log_every = (config.get("logging", {}) or {}).get("log_every_steps", 10)
 

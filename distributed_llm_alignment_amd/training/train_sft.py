@@ -19,7 +19,7 @@ from ..objectives import sft_loss
 from ..optim.scheduler import LRSchedule
 from ..parallel.dist import all_gather_tensor
 from ..utils.config import add_config_args, config_from_args
-from .common import effective_batch_msg, make_engine, move_to, setup, train_loop
+from .common import effective_batch_msg, make_engine, move_to, parallelize, setup, train_loop
 
 
 def parse_args(argv=None) -> argparse.Namespace:
@@ -53,6 +53,7 @@ def main(argv=None) -> int:
                             use_flash_attention=model_cfg.get("use_flash_attention", False),
                             device=ctx.device, seed=ctx.seed)
     model, tok = bundle.model, bundle.tokenizer
+    parallelize(ctx, model)
     data_cfg = dict(config["data"])
     max_len = model_cfg.get("max_seq_length", 2048)
     opt = config["optimization"]

@@ -73,15 +73,27 @@ def save_state(output_dir, models: Sequence, engine=None, scheduler=None, step: 
     if st.is_main:
         out.mkdir(parents=True, exist_ok=True)
     pdist.barrier()
-    if st.is_main:
-        for i, m in enumerate(models):
-            save_file(_state_dict_of(m), str(out / _model_file(i)), metadata={"format": "pt"})
-        if scheduler is not None:
-            torch.save(scheduler.state_dict(), out / "scheduler.bin")
+    from contextlib import ExitStack
+
+    from ..parallel.tensor_parallel import is_tensor_parallel, tp_unsharded
+
+    tp = any(is_tensor_parallel(m) for m in models)
+    with ExitStack() as stack:
+        for m in models:  # TP-sharded weights are gathered on every rank (collective)
+            stack.enter_context(tp_unsharded(m))
+        if st.is_main:
+            for i, m in enumerate(models):
+                save_file(_state_dict_of(m), str(out / _model_file(i)), metadata={"format": "pt"})
+            if hf_export and models:
+                from ..models.loader import save_hf_pretrained
+
+                save_hf_pretrained(models[0], tokenizer, str(out / "hf"))
+    if st.is_main and scheduler is not None:
+        torch.save(scheduler.state_dict(), out / "scheduler.bin")
     if engine is not None:
         torch.save({k: (v.cpu() if isinstance(v, torch.Tensor) else v)
                     for k, v in engine.optimizer_state().items()}, out / f"optimizer_shard_{st.rank}.pt")
-        if engine.numel <= CONSOLIDATE_MAX_NUMEL:
+        if engine.numel <= CONSOLIDATE_MAX_NUMEL and not tp:
             osd = engine.torch_optimizer_state_dict()  # collective under ZeRO
             if st.is_main:
                 torch.save(osd, out / "optimizer.bin")
@@ -98,10 +110,6 @@ def save_state(output_dir, models: Sequence, engine=None, scheduler=None, step: 
                 (out / "dla_config.json").write_text(json.dumps(base.cfg.to_dict(), indent=2))
             if tokenizer is not None and hasattr(tokenizer, "save_pretrained"):
                 tokenizer.save_pretrained(str(out))
-        if hf_export and models:
-            from ..models.loader import save_hf_pretrained
-
-            save_hf_pretrained(models[0], tokenizer, str(out / "hf"))
         _update_latest(out)
         if keep_last:
             _rotate(out.parent, keep_last)
@@ -153,10 +161,13 @@ def load_model_weights(model, ckpt_dir, index: int = 0, strict: bool = True):
         sd = torch.load(str(d / "pytorch_model.bin"), map_location="cpu", weights_only=True)
     else:
         raise FileNotFoundError(f"no weights for model {index} in {d}")
-    if hasattr(model, "load_hf_state_dict"):
-        return model.load_hf_state_dict(sd, strict=strict)
-    sd = {(k[7:] if k.startswith("module.") else k): v for k, v in sd.items()}
-    return model.load_state_dict(sd, strict=strict)
+    from ..parallel.tensor_parallel import tp_unsharded
+
+    with tp_unsharded(model, writeback=True):  # full tensors in, re-sliced to this TP rank
+        if hasattr(model, "load_hf_state_dict"):
+            return model.load_hf_state_dict(sd, strict=strict)
+        sd = {(k[7:] if k.startswith("module.") else k): v for k, v in sd.items()}
+        return model.load_state_dict(sd, strict=strict)
 
 
 def load_state(ckpt_dir, models: Sequence, engine=None, scheduler=None, load_models: bool = True) -> int:
