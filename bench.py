@@ -75,9 +75,16 @@ def main() -> int:
     if mesh.tp > 1:
         apply_tensor_parallel(policy, mesh.tp_group)
         apply_tensor_parallel(ref, mesh.tp_group)
-    engine = DataParallelEngine(policy, lr=1e-6, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01,
-                                max_grad_norm=1.0, zero_stage=args.zero, bucket_mb=args.bucket_mb,
-                                group=mesh.dp_group, tp_group=mesh.tp_group)
+    if args.zero == 3:  # ZeRO-3 / FSDP: per-layer gather, sharded frozen reference
+        from distributed_llm_alignment_amd.parallel.fsdp import FullyShardedEngine, ShardedInference
+
+        engine = FullyShardedEngine(policy, lr=1e-6, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01,
+                                    max_grad_norm=1.0, group=mesh.dp_group, tp_group=mesh.tp_group)
+        ShardedInference(ref, group=mesh.dp_group)
+    else:
+        engine = DataParallelEngine(policy, lr=1e-6, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01,
+                                    max_grad_norm=1.0, zero_stage=args.zero, bucket_mb=args.bucket_mb,
+                                    group=mesh.dp_group, tp_group=mesh.tp_group)
     policy.train()
 
     gen = torch.Generator().manual_seed(17 + mesh.dp_rank)  # TP ranks share a batch
@@ -159,7 +166,7 @@ def main() -> int:
                 "global_batch": pairs_per_step,
                 "seq_len": args.seq_len,
                 "parallelism": f"dp{mesh.dp}" + (f"-tp{mesh.tp}" if mesh.tp > 1 else "")
-                               + (f"-zero{engine.zero}" if mesh.dp > 1 else ""),
+                               + (f"-zero{engine.zero}" if mesh.dp > 1 or engine.zero == 3 else ""),
                 "micro_batch_pairs": args.micro_pairs,
                 "grad_accum": args.accum,
                 "ref_model": "frozen, co-resident",

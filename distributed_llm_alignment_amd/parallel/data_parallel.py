@@ -84,6 +84,7 @@ class DataParallelEngine:
         self._sync = True
         self._handles = []
         self._launched = 0
+        self._seen = set()
 
         params = [p for p in module.parameters() if p.requires_grad]
         if not params:
@@ -187,6 +188,11 @@ class DataParallelEngine:
     def _on_grad(self, p: nn.Parameter):
         if not self._sync or self.world == 1:
             return
+        # a main_grad (GEMM-accumulated) weight reports twice: from the GEMM epilogue and from
+        # its AccumulateGrad node (which still runs with an undefined grad) -> count once
+        if id(p) in self._seen:
+            return
+        self._seen.add(id(p))
         bi = self._bucket_of[id(p)]
         self._ready[bi] += 1
         # launch strictly in bucket order so every rank issues identical collective sequences
@@ -216,6 +222,7 @@ class DataParallelEngine:
         self._handles = []
         self._launched = 0
         self._ready = [0] * len(self.buckets)
+        self._seen = set()
 
     # ------------------------------------------------------------------------ step
     def clip_and_norm(self):

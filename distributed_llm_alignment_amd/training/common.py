@@ -104,17 +104,36 @@ def parallelize(ctx: TrainContext, model):
         from ..parallel.expert import apply_expert_parallel
 
         apply_expert_parallel(model, m)
+    if use_fsdp(ctx) and not any(p.requires_grad for p in model.parameters()):
+        # frozen reference / teachers are sharded too (C10): 1/dp of their weights resident
+        from ..parallel.fsdp import ShardedInference
+
+        ShardedInference(model, group=m.dp_group)
     return model
 
 
+def use_fsdp(ctx: TrainContext) -> bool:
+    """ZeRO-3 / FSDP FULL_SHARD requested (hardware.zero_stage: 3, a DeepSpeed stage-3 JSON or an
+    `fsdp` block) and there is more than one data-parallel rank to shard over."""
+    z = ctx.hw.get("zero_stage")
+    return (ctx.hw.get("fsdp") or (z is not None and int(z) >= 3)) and ctx.dp_size > 1
+
+
 def make_engine(ctx: TrainContext, model, lr: float, betas=(0.9, 0.999), weight_decay: float = 0.0,
-                max_grad_norm: float = 1.0) -> DataParallelEngine:
+                max_grad_norm: float = 1.0):
+    groups = dict(group=ctx.mesh.dp_group if ctx.mesh is not None else None,
+                  tp_group=ctx.mesh.tp_group if ctx.mesh is not None else None)
+    if use_fsdp(ctx):
+        from ..parallel.fsdp import FullyShardedEngine
+
+        return FullyShardedEngine(model, lr=lr, betas=betas, weight_decay=weight_decay,
+                                  max_grad_norm=max_grad_norm,
+                                  master_weights=ctx.hw.get("master_weights", True), **groups)
+    z = ctx.hw.get("zero_stage")
     return DataParallelEngine(model, lr=lr, betas=betas, weight_decay=weight_decay,
-                              max_grad_norm=max_grad_norm, zero_stage=ctx.hw.get("zero_stage"),
+                              max_grad_norm=max_grad_norm, zero_stage=None if z is None else min(int(z), 1),
                               bucket_mb=ctx.hw.get("bucket_mb", 256.0),
-                              master_weights=ctx.hw.get("master_weights", True),
-                              group=ctx.mesh.dp_group if ctx.mesh is not None else None,
-                              tp_group=ctx.mesh.tp_group if ctx.mesh is not None else None)
+                              master_weights=ctx.hw.get("master_weights", True), **groups)
 
 
 def effective_batch_msg(ctx: TrainContext, micro: int) -> str:

@@ -75,11 +75,13 @@ def save_state(output_dir, models: Sequence, engine=None, scheduler=None, step: 
     pdist.barrier()
     from contextlib import ExitStack
 
+    from ..parallel.fsdp import fsdp_full_params
     from ..parallel.tensor_parallel import is_tensor_parallel, tp_unsharded
 
     tp = any(is_tensor_parallel(m) for m in models)
     with ExitStack() as stack:
-        for m in models:  # TP-sharded weights are gathered on every rank (collective)
+        for m in models:  # sharded weights are gathered on every rank (collectives)
+            stack.enter_context(fsdp_full_params(m))
             stack.enter_context(tp_unsharded(m))
         if st.is_main:
             for i, m in enumerate(models):
@@ -161,9 +163,11 @@ def load_model_weights(model, ckpt_dir, index: int = 0, strict: bool = True):
         sd = torch.load(str(d / "pytorch_model.bin"), map_location="cpu", weights_only=True)
     else:
         raise FileNotFoundError(f"no weights for model {index} in {d}")
+    from ..parallel.fsdp import fsdp_full_params
     from ..parallel.tensor_parallel import tp_unsharded
 
-    with tp_unsharded(model, writeback=True):  # full tensors in, re-sliced to this TP rank
+    # full tensors in, re-sliced to this TP rank / FSDP shard
+    with fsdp_full_params(model, writeback=True), tp_unsharded(model, writeback=True):
         if hasattr(model, "load_hf_state_dict"):
             return model.load_hf_state_dict(sd, strict=strict)
         sd = {(k[7:] if k.startswith("module.") else k): v for k, v in sd.items()}

@@ -242,7 +242,7 @@ def test_tensor_parallel_matches_dense(name):
         assert dq < 1e-5 and dd < 1e-5 and de < 1e-5 and dn < 1e-5, (dq, dd, de, dn)
 
 
-def _tp_dpo_step(rank, world, tp):
+def _tp_dpo_step(rank, world, tp, fsdp=False):
     import torch
 
     from distributed_llm_alignment_amd.data.synthetic import synthetic_preference_batch
@@ -259,8 +259,15 @@ def _tp_dpo_step(rank, world, tp):
     if tp > 1:
         apply_tensor_parallel(pol, mesh.tp_group)
         apply_tensor_parallel(ref, mesh.tp_group)
-    eng = DataParallelEngine(pol, lr=1e-2, weight_decay=0.01, max_grad_norm=0.05, group=mesh.dp_group,
-                             tp_group=mesh.tp_group, bucket_mb=0.05)
+    if fsdp:
+        from distributed_llm_alignment_amd.parallel.fsdp import FullyShardedEngine, ShardedInference
+
+        eng = FullyShardedEngine(pol, lr=1e-2, weight_decay=0.01, max_grad_norm=0.05, group=mesh.dp_group,
+                                 tp_group=mesh.tp_group)
+        ShardedInference(ref, group=mesh.dp_group)
+    else:
+        eng = DataParallelEngine(pol, lr=1e-2, weight_decay=0.01, max_grad_norm=0.05, group=mesh.dp_group,
+                                 tp_group=mesh.tp_group, bucket_mb=0.05)
     g = torch.Generator().manual_seed(11)
     b = synthetic_preference_batch(4, 16, cfg.vocab_size, generator=g)
     per = 4 // mesh.dp
@@ -282,16 +289,17 @@ def test_tp2_vs_dp2_dpo_step_and_clip_norm():
     assert float(mean_dp) == pytest.approx(float(tp[0][1]), abs=1e-5)
 
 
-def test_dp2_tp2_mesh_matches_dp2():
-    """World 4 as DP=2 x TP=2 (ZeRO-1 over the DP group) == plain DP=2 on the same batch."""
+@pytest.mark.parametrize("fsdp", [False, True])
+def test_dp2_tp2_mesh_matches_dp2(fsdp):
+    """World 4 as DP=2 x TP=2 (ZeRO-1 or ZeRO-3 over the DP group) == plain DP=2 on the same batch."""
     dp = run_ranks(_tp_dpo_step, 2, (1,))
-    mesh = run_ranks(_tp_dpo_step, 4, (2,))
+    mesh = run_ranks(_tp_dpo_step, 4, (2, fsdp))
     assert dp[0][0] == pytest.approx(mesh[0][0], rel=1e-4)
     for r in range(4):  # rank r holds dp_rank r // 2
         assert float(mesh[r][1]) == pytest.approx(float(dp[r // 2][1]), abs=1e-5)
 
 
-def _tp_trainers(rank, world, root):
+def _tp_trainers(rank, world, root, hw=None):
     import json
     from pathlib import Path
 
@@ -302,7 +310,7 @@ def _tp_trainers(rank, world, root):
     d = Path(root)
     common = lambda st: {"logging": {"output_dir": str(d / "ck" / st), "log_dir": str(d / "logs" / st),
                                      "log_every_steps": 1, "save_every_steps": 3},
-                         "hardware": {"tp_size": 2, "gradient_accumulation_steps": 1}}
+                         "hardware": hw or {"tp_size": 2, "gradient_accumulation_steps": 1}}
     sft = {"seed": 3, "model": {"model_name_or_path": "tiny-llama", "max_seq_length": 64,
                                 "gradient_checkpointing": True},
            "data": {"source": "local", "train_path": str(d / "sft.jsonl"), "num_workers": 0},
@@ -330,9 +338,10 @@ def _tp_trainers(rank, world, root):
     return losses
 
 
-def test_trainers_with_tensor_parallel(tmp_path):
-    """SFT then DPO with hardware.tp_size=2 on 2 gloo ranks: checkpoints hold FULL (gathered)
-    weights that load into an unsharded model, and the DPO loss starts at ln 2."""
+@pytest.mark.parametrize("hw", [None, {"zero_stage": 3, "gradient_accumulation_steps": 2}])
+def test_trainers_with_tensor_parallel(tmp_path, hw):
+    """SFT then DPO with hardware.tp_size=2 (or ZeRO-3) on 2 gloo ranks: checkpoints hold FULL
+    (gathered) weights that load into an unsharded model, and the DPO loss starts at ln 2."""
     from distributed_llm_alignment_amd.data import write_jsonl
     from distributed_llm_alignment_amd.data.synthetic import (synthetic_instruction_records,
                                                               synthetic_preference_records)
@@ -340,10 +349,101 @@ def test_trainers_with_tensor_parallel(tmp_path):
 
     write_jsonl(tmp_path / "sft.jsonl", synthetic_instruction_records(16, seed=1))
     write_jsonl(tmp_path / "pref.jsonl", synthetic_preference_records(16, seed=3))
-    res = run_ranks(_tp_trainers, 2, (str(tmp_path),))
+    res = run_ranks(_tp_trainers, 2, (str(tmp_path), hw))
     losses = res[0]
     assert losses and abs(losses[0] - 0.6931) < 0.02
     b = load_causal_lm(str(tmp_path / "ck" / "dpo" / "final" / "hf"), device="cpu")
     cfg = get_config("tiny-llama")
     assert b.model.embed.shape == (cfg.vocab_size, cfg.hidden_size)
     assert b.model.layers[0].attn.qkv_proj.shape[0] == cfg.q_size + 2 * cfg.kv_size
+
+
+# ------------------------------------------------------------------------------ ZeRO-3 / FSDP
+def _fsdp_run(rank, world, mode, ckpt, accum):
+    import torch
+
+    from distributed_llm_alignment_amd.data.synthetic import synthetic_preference_batch
+    from distributed_llm_alignment_amd.models import build_model, get_config
+    from distributed_llm_alignment_amd.objectives import dpo_step_loss
+    from distributed_llm_alignment_amd.parallel.data_parallel import DataParallelEngine
+    from distributed_llm_alignment_amd.parallel.fsdp import FullyShardedEngine, ShardedInference
+
+    cfg = get_config("tiny-llama")
+    pol = build_model(cfg, device="cpu", seed=0)
+    ref = build_model(cfg, device="cpu", seed=0).requires_grad_(False)
+    if ckpt:
+        pol.gradient_checkpointing_enable()
+    kw = dict(lr=1e-2, weight_decay=0.01, max_grad_norm=0.05)
+    if mode == "fsdp":
+        eng = FullyShardedEngine(pol, **kw)
+        ShardedInference(ref)
+    else:
+        eng = DataParallelEngine(pol, zero_stage=1, bucket_mb=0.05, **kw)
+    g = torch.Generator().manual_seed(11 + rank)
+    batches = [synthetic_preference_batch(2, 16, cfg.vocab_size, generator=g) for _ in range(accum)]
+    out = []
+    for step in range(3):
+        for a, b in enumerate(batches):
+            loss, _ = dpo_step_loss(pol, ref, b)
+            (loss / accum).backward()
+        out.append(float(eng.step()))
+    loss, _ = dpo_step_loss(pol, ref, batches[0])
+    out.append(float(loss))
+    return out
+
+
+@pytest.mark.parametrize("ckpt,accum", [(False, 1), (True, 2)])
+def test_fsdp_matches_zero1(ckpt, accum):
+    """ZeRO-3 (per-layer gather / reduce-scatter, sharded frozen ref) == ZeRO-1 numerically."""
+    a = run_ranks(_fsdp_run, 2, ("zero1", ckpt, accum))
+    b = run_ranks(_fsdp_run, 2, ("fsdp", ckpt, accum))
+    for r in (0, 1):
+        assert a[r] == pytest.approx(b[r], rel=1e-4, abs=1e-6), (a[r], b[r])
+
+
+def _fsdp_ckpt(rank, world, root):
+    import torch
+
+    from distributed_llm_alignment_amd.data.synthetic import synthetic_preference_batch
+    from distributed_llm_alignment_amd.models import build_model, get_config
+    from distributed_llm_alignment_amd.objectives import dpo_step_loss
+    from distributed_llm_alignment_amd.parallel.fsdp import FullyShardedEngine, ShardedInference
+    from distributed_llm_alignment_amd.utils.checkpoint import load_state, save_state
+
+    cfg = get_config("tiny-llama")
+
+    def make(seed):
+        pol = build_model(cfg, device="cpu", seed=seed)
+        ref = build_model(cfg, device="cpu", seed=0).requires_grad_(False)
+        eng = FullyShardedEngine(pol, lr=1e-2)
+        ShardedInference(ref)
+        return pol, ref, eng
+
+    pol, ref, eng = make(0)
+    g = torch.Generator().manual_seed(3 + rank)
+    b = synthetic_preference_batch(2, 16, cfg.vocab_size, generator=g)
+    dpo_step_loss(pol, ref, b)[0].backward()
+    eng.step()
+    save_state(f"{root}/ck", [pol, ref], eng, step=1)
+    dpo_step_loss(pol, ref, b)[0].backward()
+    eng.step()
+    want = float(dpo_step_loss(pol, ref, b)[0])
+    pol2, ref2, eng2 = make(99)  # different init: everything must come from the checkpoint
+    load_state(f"{root}/ck", [pol2, ref2], eng2)
+    dpo_step_loss(pol2, ref2, b)[0].backward()
+    eng2.step()
+    got = float(dpo_step_loss(pol2, ref2, b)[0])
+    return want, got
+
+
+def test_fsdp_checkpoint_resume(tmp_path):
+    res = run_ranks(_fsdp_ckpt, 2, (str(tmp_path),))
+    for r in (0, 1):
+        assert res[r][0] == pytest.approx(res[r][1], abs=1e-6)
+    from safetensors.torch import load_file
+
+    from distributed_llm_alignment_amd.models import get_config
+
+    sd = load_file(str(tmp_path / "ck" / "model.safetensors"))
+    cfg = get_config("tiny-llama")
+    assert sd["model.embed_tokens.weight"].shape == (cfg.vocab_size, cfg.hidden_size)
