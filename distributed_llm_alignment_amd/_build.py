@@ -44,7 +44,7 @@ def _hipcc() -> str:
 
 def _sources():
     hips = sorted(CSRC.glob("*.hip"))
-    return hips, CSRC / "bindings.cpp"
+    return hips, sorted(CSRC.glob("*.cpp"))
 
 
 def _headers():
@@ -69,7 +69,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
     """Compile every HIP kernel for gfx950 and link `_C.so`. Returns the .so path."""
     inc, lib, abi = _torch_paths()
     OBJ_DIR.mkdir(parents=True, exist_ok=True)
-    hips, binding = _sources()
+    hips, bindings = _sources()
     headers = _headers()
     jobs = jobs or min(8, os.cpu_count() or 4)
     hipcc = _hipcc()
@@ -82,15 +82,16 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
         if force or _newer(src, obj, headers):
             tasks.append([hipcc, f"--offload-arch={ARCH}", "-munsafe-fp-atomics", *common,
                           "-c", str(src), "-o", str(obj)])
-    bobj = OBJ_DIR / "bindings.o"
-    objs.append(bobj)
-    if force or _newer(binding, bobj, headers):
-        cxx = shutil.which("g++") or shutil.which("c++") or "c++"
-        py_inc = sysconfig.get_paths()["include"]
-        tasks.append([cxx, *common, f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-D__HIP_PLATFORM_AMD__=1",
-                      "-DUSE_ROCM=1", "-DHIPBLAS_V2", *[f"-I{p}" for p in inc],
-                      f"-I{ROCM / 'include'}", f"-I{py_inc}", "-Wno-deprecated-declarations",
-                      "-c", str(binding), "-o", str(bobj)])
+    cxx = shutil.which("g++") or shutil.which("c++") or "c++"
+    py_inc = sysconfig.get_paths()["include"]
+    for binding in bindings:  # host-only op registration (torch headers, g++)
+        bobj = OBJ_DIR / (binding.stem + ".o")
+        objs.append(bobj)
+        if force or _newer(binding, bobj, headers):
+            tasks.append([cxx, *common, f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-D__HIP_PLATFORM_AMD__=1",
+                          "-DUSE_ROCM=1", "-DHIPBLAS_V2", *[f"-I{p}" for p in inc],
+                          f"-I{ROCM / 'include'}", f"-I{py_inc}", "-Wno-deprecated-declarations",
+                          "-c", str(binding), "-o", str(bobj)])
     if tasks:
         with ThreadPoolExecutor(max_workers=jobs) as ex:
             for out in ex.map(_run, tasks):

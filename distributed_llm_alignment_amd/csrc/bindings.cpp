@@ -13,6 +13,7 @@
 #include <tuple>
 
 #include "attn_params.h"
+#include "bind_util.h"
 
 namespace dla {
 
@@ -59,33 +60,6 @@ void launch_attn_bwd_delta(const bf16_t*, const bf16_t*, int64_t, int64_t, int64
                            int64_t, int64_t, int, int, int, int, float*, hipStream_t);
 void launch_attn_bwd(const AttnBwdParams&, int, bool, hipStream_t);
 void launch_f32_to_bf16_rows(const float*, int64_t, int, bf16_t*, int64_t, hipStream_t);
-
-// ---- helpers ----
-static inline hipStream_t cur_stream(const at::Tensor& t) {
-  return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(t.device().index()).stream();
-}
-static inline bf16_t* bp(const at::Tensor& t) { return reinterpret_cast<bf16_t*>(t.data_ptr()); }
-static inline const bf16_t* cbp(const at::Tensor& t) {
-  return reinterpret_cast<const bf16_t*>(t.data_ptr());
-}
-static inline void check_cuda(const at::Tensor& t, const char* name) {
-  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
-}
-static inline void check_bf16(const at::Tensor& t, const char* name) {
-  check_cuda(t, name);
-  TORCH_CHECK(t.scalar_type() == at::kBFloat16, name, " must be bfloat16");
-}
-static inline void check_f32(const at::Tensor& t, const char* name) {
-  check_cuda(t, name);
-  TORCH_CHECK(t.scalar_type() == at::kFloat, name, " must be float32");
-}
-static inline void check_aligned16(const at::Tensor& t, const char* name) {
-  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name,
-              " must be 16-byte aligned");
-}
-static inline void same_device(const at::Tensor& a, const at::Tensor& b) {
-  TORCH_CHECK(a.device() == b.device(), "operands on different devices");
-}
 
 // ================================= norms ======================================================
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> norm_fwd(

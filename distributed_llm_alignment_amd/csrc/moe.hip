@@ -1,0 +1,179 @@
+// Mixture-of-experts routing / permutation kernels (HF Mixtral semantics,
+// transformers/models/mixtral/modeling_mixtral.py sparse MoE block: softmax -> top-k ->
+// renormalise -> dispatch -> expert SwiGLU -> weighted combine).
+//
+// Layout: token-slot (t, j) (j < k) is sent to row pos[t, j] of the expert-sorted activation
+// matrix xs [N*k, H] (rows of one expert contiguous, experts in order; under expert parallelism
+// experts of one destination rank are contiguous too, so the all-to-all payload needs no extra
+// copy). Every kernel is a GATHER over that map — no atomics, deterministic:
+//   dispatch  : xs[pos[t,j]]  = x[t]                        (forward permute)
+//   combine   : out[t]        = sum_j w[t,j] * ys[pos[t,j]]  (forward un-permute + weighting;
+//                                                             with w = 1: dispatch backward)
+//   combine_bwd: dys[pos[t,j]] = w[t,j] * dout[t],  dw[t,j] = <dout[t], ys[pos[t,j]]>
+// Router: the renormalised top-k softmax equals a softmax over the selected logits, so the
+// forward needs one pass over E logits per token and the backward touches only k of them.
+#include "common.h"
+
+namespace dla {
+
+constexpr int kMaxK = 8;
+
+// one thread per token; E <= 256 logits read twice from L1/L2 (E * 2 B per token)
+__global__ __launch_bounds__(256) void moe_topk_fwd_kernel(const bf16_t* __restrict__ logits,
+                                                            int64_t N, int E, int k,
+                                                            float* __restrict__ topv,
+                                                            int* __restrict__ topi) {
+  const int64_t t = blockIdx.x * 256ll + threadIdx.x;
+  if (t >= N) return;
+  const bf16_t* row = logits + t * E;
+  float v[kMaxK];
+  int id[kMaxK];
+#pragma unroll
+  for (int j = 0; j < kMaxK; ++j) {
+    v[j] = -INFINITY;
+    id[j] = -1;
+  }
+  for (int e = 0; e < E; ++e) {
+    const float x = bf2f(row[e]);
+    // insertion into the descending top-k list; ties keep the lower expert index first
+    if (x > v[k - 1] || id[k - 1] < 0) {
+      int p = k - 1;
+      while (p > 0 && (x > v[p - 1] || id[p - 1] < 0)) {
+        v[p] = v[p - 1];
+        id[p] = id[p - 1];
+        --p;
+      }
+      v[p] = x;
+      id[p] = e;
+    }
+  }
+  float s = 0.f;
+  float ex[kMaxK];
+#pragma unroll
+  for (int j = 0; j < kMaxK; ++j) {
+    ex[j] = j < k ? __expf(v[j] - v[0]) : 0.f;
+    s += ex[j];
+  }
+  const float inv = 1.f / s;
+  for (int j = 0; j < k; ++j) {
+    topv[t * k + j] = ex[j] * inv;
+    topi[t * k + j] = id[j];
+  }
+}
+
+// dlogits[t, e] = topv*(g - <g, topv>) on the k selected experts, 0 elsewhere
+__global__ __launch_bounds__(256) void moe_topk_bwd_kernel(const float* __restrict__ topv,
+                                                            const int* __restrict__ topi,
+                                                            const float* __restrict__ g,
+                                                            int64_t N, int E, int k,
+                                                            bf16_t* __restrict__ dlogits) {
+  const int64_t t = blockIdx.x * 256ll + threadIdx.x;
+  if (t >= N) return;
+  bf16_t* row = dlogits + t * E;
+  for (int e = 0; e < E; ++e) row[e] = 0;
+  float dot = 0.f;
+  for (int j = 0; j < k; ++j) dot += g[t * k + j] * topv[t * k + j];
+  for (int j = 0; j < k; ++j) {
+    const float p = topv[t * k + j];
+    row[topi[t * k + j]] = f2bf(p * (g[t * k + j] - dot));
+  }
+}
+
+// block per token; 16-byte vectors over H
+__global__ __launch_bounds__(256) void moe_dispatch_kernel(const bf16_t* __restrict__ x,
+                                                            const int* __restrict__ pos,
+                                                            int64_t N, int H, int k,
+                                                            bf16_t* __restrict__ xs) {
+  const int64_t t = blockIdx.x;
+  const bf16_t* src = x + t * H;
+  int p[kMaxK];
+  for (int j = 0; j < k; ++j) p[j] = pos[t * k + j];
+  for (int i = threadIdx.x; i < H / 8; i += 256) {
+    const bf16x8 a = load_bf16x8(src + i * 8);
+    for (int j = 0; j < k; ++j) store_bf16x8(xs + (int64_t)p[j] * H + i * 8, a);
+  }
+}
+
+template <bool HAS_W>
+__global__ __launch_bounds__(256) void moe_combine_kernel(const bf16_t* __restrict__ ys,
+                                                           const int* __restrict__ pos,
+                                                           const float* __restrict__ w,
+                                                           int64_t N, int H, int k,
+                                                           bf16_t* __restrict__ out) {
+  const int64_t t = blockIdx.x;
+  int p[kMaxK];
+  float wt[kMaxK];
+  for (int j = 0; j < k; ++j) {
+    p[j] = pos[t * k + j];
+    wt[j] = HAS_W ? w[t * k + j] : 1.f;
+  }
+  for (int i = threadIdx.x; i < H / 8; i += 256) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < k; ++j) {
+      const bf16x8 a = load_bf16x8(ys + (int64_t)p[j] * H + i * 8);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] += wt[j] * bf2f(a[q]);
+    }
+    store_bf16x8(out + t * H + i * 8, pack_bf16x8(acc));
+  }
+}
+
+__global__ __launch_bounds__(256) void moe_combine_bwd_kernel(const bf16_t* __restrict__ dout,
+                                                               const bf16_t* __restrict__ ys,
+                                                               const int* __restrict__ pos,
+                                                               const float* __restrict__ w,
+                                                               int64_t N, int H, int k,
+                                                               bf16_t* __restrict__ dys,
+                                                               float* __restrict__ dw) {
+  __shared__ float red[4];
+  const int64_t t = blockIdx.x;
+  for (int j = 0; j < k; ++j) {
+    const int64_t p = pos[t * k + j];
+    const float wt = w[t * k + j];
+    float dot = 0.f;
+    for (int i = threadIdx.x; i < H / 8; i += 256) {
+      const bf16x8 g = load_bf16x8(dout + t * H + i * 8);
+      const bf16x8 y = load_bf16x8(ys + p * H + i * 8);
+      float o[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float gq = bf2f(g[q]);
+        dot += gq * bf2f(y[q]);
+        o[q] = wt * gq;
+      }
+      store_bf16x8(dys + p * H + i * 8, pack_bf16x8(o));
+    }
+    const float s = block_sum<256>(dot, red);
+    if (threadIdx.x == 0) dw[t * k + j] = s;
+  }
+}
+
+// ----------------------------------------------------------------------------------------------
+void launch_moe_topk_fwd(const bf16_t* logits, int64_t N, int E, int k, float* topv, int* topi,
+                         hipStream_t st) {
+  if (N == 0) return;
+  moe_topk_fwd_kernel<<<(N + 255) / 256, 256, 0, st>>>(logits, N, E, k, topv, topi);
+}
+void launch_moe_topk_bwd(const float* topv, const int* topi, const float* g, int64_t N, int E,
+                         int k, bf16_t* dlogits, hipStream_t st) {
+  if (N == 0) return;
+  moe_topk_bwd_kernel<<<(N + 255) / 256, 256, 0, st>>>(topv, topi, g, N, E, k, dlogits);
+}
+void launch_moe_dispatch(const bf16_t* x, const int* pos, int64_t N, int H, int k, bf16_t* xs,
+                         hipStream_t st) {
+  if (N == 0) return;
+  moe_dispatch_kernel<<<N, 256, 0, st>>>(x, pos, N, H, k, xs);
+}
+void launch_moe_combine(const bf16_t* ys, const int* pos, const float* w, int64_t N, int H, int k,
+                        bf16_t* out, hipStream_t st) {
+  if (N == 0) return;
+  if (w) moe_combine_kernel<true><<<N, 256, 0, st>>>(ys, pos, w, N, H, k, out);
+  else moe_combine_kernel<false><<<N, 256, 0, st>>>(ys, pos, w, N, H, k, out);
+}
+void launch_moe_combine_bwd(const bf16_t* dout, const bf16_t* ys, const int* pos, const float* w,
+                            int64_t N, int H, int k, bf16_t* dys, float* dw, hipStream_t st) {
+  if (N == 0) return;
+  moe_combine_bwd_kernel<<<N, 256, 0, st>>>(dout, ys, pos, w, N, H, k, dys, dw);
+}
+
+}  // namespace dla

@@ -125,19 +125,18 @@ class MoE(nn.Module):
         self.ep = None  # set by parallel.expert.shard_experts
         self.last_aux_loss = None
 
+    fp8 = False  # e4m3 expert GEMMs in the forward (north star; bf16 backward)
+    collect_aux = False  # HF `output_router_logits`: off by default, as in MixtralConfig
+
     def route(self, h2: torch.Tensor):
-        logits = F.linear(h2, self.router).float()
-        probs = torch.softmax(logits, dim=-1)
-        topv, topi = torch.topk(probs, self.cfg.num_experts_per_tok, dim=-1)
-        topv = topv / topv.sum(-1, keepdim=True)
-        if self.training and self.cfg.router_aux_loss_coef > 0:
+        logits = ops.linear(h2, self.router)
+        topv, topi = ops.moe.route_topk(logits, self.cfg.num_experts_per_tok)
+        if self.collect_aux and self.training and self.cfg.router_aux_loss_coef > 0 and torch.is_grad_enabled():
             E = self.cfg.num_experts
-            frac = F.one_hot(topi, E).float().sum(1).mean(0)
+            probs = torch.softmax(logits.float(), dim=-1)
+            frac = F.one_hot(topi.long(), E).float().sum(1).mean(0)
             self.last_aux_loss = E * (frac * probs.mean(0)).sum() * self.cfg.router_aux_loss_coef
         return topv, topi
-
-    def expert_ffn(self, e: int, x: torch.Tensor) -> torch.Tensor:
-        return F.linear(ops.swiglu(F.linear(x, self.expert_up[e])), self.expert_down[e])
 
     def forward(self, h):
         shp = h.shape
@@ -146,22 +145,10 @@ class MoE(nn.Module):
         if self.ep is not None:
             out = self.ep.dispatch_combine(self, h2, topv, topi)
             return out.view(shp)
-        k = self.cfg.num_experts_per_tok
-        flat_e = topi.reshape(-1)
-        order = torch.argsort(flat_e, stable=True)
-        tok = order // k
-        counts = torch.bincount(flat_e, minlength=self.cfg.num_experts).tolist()
-        xs = h2.index_select(0, tok)
-        w = topv.reshape(-1).index_select(0, order).to(h.dtype).unsqueeze(-1)
-        outs = []
-        start = 0
-        for e, c in enumerate(counts):
-            if c:
-                outs.append(self.expert_ffn(e, xs[start:start + c]))
-            start += c
-        ys = torch.cat(outs, 0) * w
-        out = torch.zeros_like(h2).index_add_(0, tok, ys)
-        return out.view(shp)
+        pos, counts = ops.moe.expert_positions(topi, self.cfg.num_experts)
+        xs = ops.moe.dispatch(h2, pos)
+        ys = ops.moe.experts_swiglu(xs, self.expert_up, self.expert_down, counts.tolist(), fp8=self.fp8)
+        return ops.moe.combine(ys, pos, topv).view(shp)
 
 
 class DecoderLayer(nn.Module):

@@ -1,0 +1,236 @@
+"""Mixture-of-experts ops: top-k router, token dispatch/combine and the grouped expert SwiGLU
+(north-star "Mixtral 8x7B DPO with expert-parallel all-to-all").
+
+HF Mixtral's sparse block (transformers/models/mixtral/modeling_mixtral.py) loops over experts
+with boolean masks, `index_add_` and a fresh weight-gradient tensor per expert. Here:
+  * router: `moe_topk_fwd` (renormalised top-k softmax == softmax over the k selected logits)
+    and its analytic backward touching only k logits per token;
+  * dispatch / combine: gather kernels over a token-slot -> expert-sorted-row map `pos`
+    (deterministic, no atomics); combine's backward also returns the routing-weight grads;
+  * experts: one hipBLASLt GEMM pair per expert on contiguous row ranges of the expert-sorted
+    matrix (outputs written in place, no concatenation), SwiGLU via the fused HIP kernel, and
+    weight gradients accumulated straight into the engine's flat grad buffer (`main_grad`),
+    so an expert that received no tokens costs nothing;
+  * optional fp8 (e4m3, per-tensor scales) forward GEMMs (`fp8=True`), bf16 backward.
+CPU (and non-bf16) inputs use the PyTorch reference path with identical semantics.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence
+
+import torch
+import torch.nn.functional as F
+
+from . import _ext
+from .activations import swiglu
+
+
+# ------------------------------------------------------------------------------ router
+class _TopKFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, k):
+        topv, topi = _ext.require().moe_topk_fwd(logits, int(k))
+        ctx.save_for_backward(topv, topi)
+        ctx.E = logits.shape[-1]
+        ctx.mark_non_differentiable(topi)
+        return topv, topi
+
+    @staticmethod
+    def backward(ctx, gv, _gi):
+        topv, topi = ctx.saved_tensors
+        dl = _ext.require().moe_topk_bwd(topv, topi, gv.float().contiguous(), ctx.E)
+        return dl, None
+
+
+def route_topk(logits: torch.Tensor, k: int):
+    """logits [N, E] -> (weights fp32 [N, k], expert ids int32 [N, k]); weights are the softmax
+    renormalised over the selected experts (Mixtral), descending."""
+    if _ext.use_native(logits) and logits.dtype == torch.bfloat16:
+        return _TopKFn.apply(logits.contiguous(), k)
+    v, i = torch.topk(logits.float(), k, dim=-1)
+    return torch.softmax(v, dim=-1), i.to(torch.int32)
+
+
+def expert_positions(topi: torch.Tensor, num_experts: int):
+    """Stable expert-major order of the N*k token slots.
+    Returns pos [N, k] int32 (row of slot (t, j) in the expert-sorted matrix) and per-expert
+    counts [E] (device)."""
+    flat = topi.reshape(-1).long()
+    order = torch.argsort(flat, stable=True)
+    pos = torch.empty_like(order)
+    pos[order] = torch.arange(order.numel(), device=order.device)
+    counts = torch.bincount(flat, minlength=num_experts)
+    return pos.view(topi.shape).to(torch.int32), counts
+
+
+# ------------------------------------------------------------------------------ dispatch
+def _ref_dispatch(x, pos):
+    k = pos.shape[1]
+    xs = x.new_empty((x.shape[0] * k, x.shape[1]))
+    return xs.index_copy(0, pos.reshape(-1).long(), x.repeat_interleave(k, dim=0))
+
+
+def _ref_combine(ys, pos, w):
+    g = ys.index_select(0, pos.reshape(-1).long()).view(pos.shape[0], pos.shape[1], -1)
+    if w is not None:
+        g = g * w.to(g.dtype).unsqueeze(-1)
+    return g.sum(1)
+
+
+class _DispatchFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, pos):
+        ctx.save_for_backward(pos)
+        return _ext.require().moe_dispatch(x, pos)
+
+    @staticmethod
+    def backward(ctx, dxs):
+        (pos,) = ctx.saved_tensors
+        return _ext.require().moe_combine(dxs.contiguous(), pos, None), None
+
+
+class _CombineFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ys, pos, w):
+        ctx.save_for_backward(ys, pos, w)
+        return _ext.require().moe_combine(ys, pos, w)
+
+    @staticmethod
+    def backward(ctx, dout):
+        ys, pos, w = ctx.saved_tensors
+        dys, dw = _ext.require().moe_combine_bwd(dout.contiguous(), ys, pos, w)
+        return dys, None, dw
+
+
+def dispatch(x: torch.Tensor, pos: torch.Tensor) -> torch.Tensor:
+    """x [N, H] -> xs [N*k, H] with xs[pos[t, j]] = x[t]."""
+    if _ext.use_native(x) and x.dtype == torch.bfloat16:
+        return _DispatchFn.apply(x.contiguous(), pos.contiguous())
+    return _ref_dispatch(x, pos)
+
+
+def combine(ys: torch.Tensor, pos: torch.Tensor, w: Optional[torch.Tensor]) -> torch.Tensor:
+    """out[t] = sum_j w[t, j] * ys[pos[t, j]]."""
+    if _ext.use_native(ys) and ys.dtype == torch.bfloat16:
+        return _CombineFn.apply(ys.contiguous(), pos.contiguous(),
+                                w.float().contiguous() if w is not None else None)
+    return _ref_combine(ys, pos, w)
+
+
+# ------------------------------------------------------------------------------ fp8 GEMM
+_FP8 = getattr(torch, "float8_e4m3fn", None)
+_FP8_MAX = 448.0
+
+
+def _quant_fp8(t: torch.Tensor):
+    amax = t.abs().amax().float().clamp(min=1e-12)
+    scale = _FP8_MAX / amax
+    return (t.float() * scale).clamp(-_FP8_MAX, _FP8_MAX).to(_FP8), (1.0 / scale).reshape(())
+
+
+def fp8_linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """y = x @ w^T with e4m3 operands and per-tensor scales on the gfx950 fp8 MFMA path
+    (hipBLASLt via torch._scaled_mm), bf16 output. Forward only."""
+    xq, sx = _quant_fp8(x)
+    wq, sw = _quant_fp8(w)
+    return torch._scaled_mm(xq, wq.t(), scale_a=sx, scale_b=sw, out_dtype=torch.bfloat16)
+
+
+# ------------------------------------------------------------------------------ experts
+class _ExpertsFn(torch.autograd.Function):
+    """Grouped SwiGLU experts over the expert-sorted rows. counts is a host list."""
+
+    @staticmethod
+    def forward(ctx, xs, w_up, w_down, counts: List[int], fp8: bool):
+        M, H = xs.shape
+        F2 = w_up.shape[1]
+        gu = xs.new_empty((M, F2))
+        ys = xs.new_empty((M, H))
+        s = 0
+        for e, c in enumerate(counts):
+            if c:
+                seg = xs[s:s + c]
+                if fp8:
+                    gu[s:s + c] = fp8_linear(seg, w_up[e])
+                    ys[s:s + c] = fp8_linear(swiglu(gu[s:s + c]), w_down[e])
+                else:
+                    torch.mm(seg, w_up[e].t(), out=gu[s:s + c])
+                    torch.mm(swiglu(gu[s:s + c]), w_down[e].t(), out=ys[s:s + c])
+            s += c
+        ctx.save_for_backward(xs, gu, w_up, w_down)
+        ctx.counts = list(counts)
+        return ys
+
+    @staticmethod
+    def backward(ctx, dys):
+        xs, gu, w_up, w_down = ctx.saved_tensors
+        dys = dys.contiguous()
+        need_x = ctx.needs_input_grad[0]
+        dxs = torch.zeros_like(xs) if need_x else None
+        mg_up = getattr(w_up, "main_grad", None)
+        mg_down = getattr(w_down, "main_grad", None)
+        g_up = mg_up if mg_up is not None else (torch.zeros_like(w_up) if ctx.needs_input_grad[1] else None)
+        g_down = mg_down if mg_down is not None else (torch.zeros_like(w_down) if ctx.needs_input_grad[2] else None)
+        s = 0
+        for e, c in enumerate(ctx.counts):
+            if c:
+                dy = dys[s:s + c]
+                g = gu[s:s + c]
+                a = swiglu(g)
+                da = dy @ w_down[e]
+                if g_down is not None:
+                    g_down[e].addmm_(dy.t(), a)
+                dg = _swiglu_bwd(g, da)
+                if need_x:
+                    torch.mm(dg, w_up[e], out=dxs[s:s + c])
+                if g_up is not None:
+                    g_up[e].addmm_(dg.t(), xs[s:s + c])
+            s += c
+        outs = []
+        for w, g, mg in ((w_up, g_up, mg_up), (w_down, g_down, mg_down)):
+            if mg is not None:
+                hook = getattr(w, "_dla_grad_hook", None)
+                if hook is not None:
+                    hook(w)
+                outs.append(None)
+            else:
+                outs.append(g)
+        return dxs, outs[0], outs[1], None, None
+
+
+def _swiglu_bwd(gu, dout):
+    if _ext.use_native(gu) and gu.dtype == torch.bfloat16:
+        return _ext.require().swiglu_bwd(gu.contiguous(), dout.contiguous())
+    with torch.enable_grad():
+        g = gu.detach().requires_grad_(True)
+        y = swiglu(g)
+        (dg,) = torch.autograd.grad(y, g, dout)
+    return dg
+
+
+def experts_swiglu(xs: torch.Tensor, w_up: torch.Tensor, w_down: torch.Tensor,
+                   counts: Sequence[int], fp8: bool = False) -> torch.Tensor:
+    """xs [M, H] expert-sorted rows, w_up [E, 2F, H] ([gate; up]), w_down [E, H, F]."""
+    if fp8 and not (xs.is_cuda and _FP8 is not None):
+        fp8 = False
+    return _ExpertsFn.apply(xs, w_up, w_down, [int(c) for c in counts], bool(fp8))
+
+
+def ref_moe(h2, router, w_up, w_down, k):
+    """Plain PyTorch fp32 Mixtral block (HF semantics: the router GEMM runs in the model dtype,
+    softmax / top-k / expert math in fp32) for tests."""
+    logits = F.linear(h2, router).float()
+    probs = torch.softmax(logits, dim=-1)
+    topv, topi = torch.topk(probs, k, dim=-1)
+    topv = topv / topv.sum(-1, keepdim=True)
+    out = torch.zeros_like(h2, dtype=torch.float32)
+    for j in range(k):
+        for e in range(w_up.shape[0]):
+            m = topi[:, j] == e
+            if m.any():
+                x = h2[m].float()
+                gu = x @ w_up[e].float().t()
+                Fd = gu.shape[-1] // 2
+                a = F.silu(gu[:, :Fd]) * gu[:, Fd:]
+                out[m] += topv[m, j:j + 1] * (a @ w_down[e].float().t())
+    return out

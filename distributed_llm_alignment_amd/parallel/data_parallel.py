@@ -43,6 +43,10 @@ class Bucket:
     end: int
     params: List[nn.Parameter] = field(default_factory=list)
     shard_off: int = 0  # offset of this rank's chunk inside the local shard buffers
+    expert: bool = False  # holds expert-parallel weights (reduced over the expert-DP group)
+    group: object = None
+    world: int = 1
+    rank: int = 0
 
     @property
     def size(self) -> int:
@@ -57,7 +61,7 @@ class DataParallelEngine:
     def __init__(self, module: nn.Module, lr: float = 1e-5, betas=(0.9, 0.999), eps: float = 1e-8,
                  weight_decay: float = 0.0, max_grad_norm: float = 1.0, zero_stage: Optional[int] = None,
                  bucket_mb: float = 256.0, master_weights: bool = True,
-                 dist_st: Optional[DistState] = None, group=None, tp_group=None):
+                 dist_st: Optional[DistState] = None, group=None, tp_group=None, expert_group=None):
         self.module = module
         self.dist = dist_st or dist_state()
         # tensor parallel: grads of TP-sharded params differ per TP rank; params marked
@@ -96,25 +100,41 @@ class DataParallelEngine:
         self.device = params[0].device
         params = list(reversed(params))  # ~ the order gradients are produced in
         bucket_elems = max(ALIGN, int(bucket_mb * (1 << 20)) // params[0].element_size())
-        unit = ALIGN * self.world
+        # expert-parallel weights (parallel.expert) are reduced over the group of ranks holding
+        # the SAME experts; dense weights over the data-parallel group
+        self.expert_group = expert_group
+        if expert_group is not None and self.dist.initialized:
+            ew, er = dist.get_world_size(expert_group), dist.get_rank(expert_group)
+        else:
+            ew, er = 1, 0
+        kinds = {False: (group, self.world, self.rank), True: (expert_group, ew, er)}
         # ---- layout
         self.buckets: List[Bucket] = []
         offsets: Dict[int, int] = {}
-        cur = Bucket(0, 0)
+
+        def new_bucket(pos, expert):
+            g, w, r = kinds[expert]
+            return Bucket(pos, pos, expert=expert, group=g, world=w, rank=r)
+
+        cur = new_bucket(0, bool(getattr(params[0], "_dla_expert", False)))
         pos = 0
         for p in params:
             n = _round_up(p.numel(), ALIGN)
-            if cur.params and (pos - cur.start) + n > bucket_elems:
-                cur.end = cur.start + _round_up(pos - cur.start, unit)
+            is_exp = bool(getattr(p, "_dla_expert", False))
+            if cur.params and ((pos - cur.start) + n > bucket_elems or is_exp != cur.expert):
+                cur.end = cur.start + _round_up(pos - cur.start, ALIGN * cur.world)
                 self.buckets.append(cur)
                 pos = cur.end
-                cur = Bucket(pos, pos)
+                cur = new_bucket(pos, is_exp)
             offsets[id(p)] = pos
             cur.params.append(p)
             pos += n
-        cur.end = cur.start + _round_up(pos - cur.start, unit)
+        cur.end = cur.start + _round_up(pos - cur.start, ALIGN * cur.world)
         self.buckets.append(cur)
         self.numel = cur.end
+        self.has_experts = any(b.expert for b in self.buckets)
+        # communication needed at all? (ZeRO with a 1-rank expert group still copies shards)
+        self._comm = self.world > 1
         # ---- flat storage (params re-pointed into it)
         self.param_buf = torch.zeros(self.numel, dtype=self.dtype, device=self.device)
         self.grad_buf = torch.zeros(self.numel, dtype=self.dtype, device=self.device)
@@ -134,7 +154,7 @@ class DataParallelEngine:
         shard = 0
         for b in self.buckets:
             b.shard_off = shard
-            shard += b.size // self.world
+            shard += b.size // b.world
         self.shard_numel = shard
         if self.zero:
             self.grad_shard = torch.zeros(shard, dtype=self.dtype, device=self.device)
@@ -148,8 +168,8 @@ class DataParallelEngine:
         self._repl_ranges = []
         if self.tp_size > 1:
             for b in self.buckets:
-                c = b.size // self.world
-                lo, hi = (b.start + self.rank * c, b.start + (self.rank + 1) * c) if self.zero else (b.start, b.end)
+                c = b.size // b.world
+                lo, hi = (b.start + b.rank * c, b.start + (b.rank + 1) * c) if self.zero else (b.start, b.end)
                 base = (b.shard_off - lo) if self.zero else 0
                 for p in b.params:
                     if getattr(p, "_dla_tp_replicated", False):
@@ -173,8 +193,8 @@ class DataParallelEngine:
 
     # ------------------------------------------------------------------------ helpers
     def _chunk(self, buf: torch.Tensor, b: Bucket) -> torch.Tensor:
-        c = b.size // self.world
-        return buf[b.start + self.rank * c: b.start + (self.rank + 1) * c]
+        c = b.size // b.world
+        return buf[b.start + b.rank * c: b.start + (b.rank + 1) * c]
 
     @contextlib.contextmanager
     def no_sync(self):
@@ -186,7 +206,7 @@ class DataParallelEngine:
             self._sync = prev
 
     def _on_grad(self, p: nn.Parameter):
-        if not self._sync or self.world == 1:
+        if not self._sync or not self._comm:
             return
         # a main_grad (GEMM-accumulated) weight reports twice: from the GEMM epilogue and from
         # its AccumulateGrad node (which still runs with an undefined grad) -> count once
@@ -204,16 +224,20 @@ class DataParallelEngine:
     def _launch(self, bi: int):
         b = self.buckets[bi]
         g = self.grad_buf[b.start:b.end]
+        if b.world == 1:  # expert bucket whose experts live on this rank only
+            if self.zero:
+                self.grad_shard[b.shard_off:b.shard_off + b.size].copy_(g)
+            return
         if self.zero:
-            out = self.grad_shard[b.shard_off:b.shard_off + b.size // self.world]
-            h = dist.reduce_scatter_tensor(out, g, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            out = self.grad_shard[b.shard_off:b.shard_off + b.size // b.world]
+            h = dist.reduce_scatter_tensor(out, g, op=dist.ReduceOp.SUM, group=b.group, async_op=True)
         else:
-            h = dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            h = dist.all_reduce(g, op=dist.ReduceOp.SUM, group=b.group, async_op=True)
         self._handles.append(h)
 
     def finish_grad_sync(self):
         """Launch buckets whose params got no gradient (unused params), then wait for all."""
-        if self.world > 1:
+        if self._comm:
             while self._launched < len(self.buckets):
                 self._launch(self._launched)
                 self._launched += 1
@@ -231,7 +255,26 @@ class DataParallelEngine:
         if self._repl_ranges:
             rep = sum(self.grad_shard[a:e].float().pow(2).sum() for a, e in self._repl_ranges)
             self._sumsq -= (1.0 - 1.0 / self.tp_size) * rep
-        if self.zero and self.world > 1:
+        if self.has_experts and self.world > 1:
+            # weight every element by 1/(#ranks holding it) and sum over the DP group: dense
+            # grads are replicated dp times (ZeRO-0) or unique (ZeRO-1); expert grads are
+            # replicated over the expert-DP group (ZeRO-0) or unique, and differ across EP ranks
+            if not hasattr(self, "_esumsq"):
+                self._esumsq = torch.zeros(1, dtype=torch.float32, device=self.device)
+            self._esumsq.zero_()
+            for b in self.buckets:
+                if b.expert:
+                    n = b.size // b.world if self.zero else b.size
+                    o = b.shard_off if self.zero else b.start
+                    grad_sumsq(self.grad_shard[o:o + n], self._esumsq, accumulate=True)
+            dense = self._sumsq - self._esumsq
+            if self.zero:
+                self._sumsq = dense + self._esumsq
+            else:
+                ew = self.buckets[[b.expert for b in self.buckets].index(True)].world
+                self._sumsq = dense / self.world + self._esumsq / ew
+            dist.all_reduce(self._sumsq, op=dist.ReduceOp.SUM, group=self.group)
+        elif self.zero and self.world > 1:
             dist.all_reduce(self._sumsq, op=dist.ReduceOp.SUM, group=self.group)
         if self.tp_size > 1:
             dist.all_reduce(self._sumsq, op=dist.ReduceOp.SUM, group=self.tp_group)
@@ -252,10 +295,13 @@ class DataParallelEngine:
                      clip=coef if self.max_grad_norm else None, grad_scale=1.0 / self.world)
         if self.zero:
             for b in self.buckets:
-                c = b.size // self.world
-                dist.all_gather_into_tensor(self.param_buf[b.start:b.end],
-                                            self.param_shard[b.shard_off:b.shard_off + c],
-                                            group=self.group)
+                c = b.size // b.world
+                if b.world == 1:
+                    self.param_buf[b.start:b.end].copy_(self.param_shard[b.shard_off:b.shard_off + c])
+                else:
+                    dist.all_gather_into_tensor(self.param_buf[b.start:b.end],
+                                                self.param_shard[b.shard_off:b.shard_off + c],
+                                                group=b.group)
         self.zero_grad()
         return self.last_grad_norm
 
@@ -267,8 +313,10 @@ class DataParallelEngine:
     @torch.no_grad()
     def broadcast_params(self, src: int = 0):
         if self.world > 1:
-            gsrc = dist.get_global_rank(self.group, src) if self.group is not None else src
-            dist.broadcast(self.param_buf, src=gsrc, group=self.group)
+            for b in self.buckets:
+                if b.world > 1:
+                    gsrc = dist.get_global_rank(b.group, src) if b.group is not None else src
+                    dist.broadcast(self.param_buf[b.start:b.end], src=gsrc, group=b.group)
             if self.zero:
                 self.param_shard.copy_(torch.cat([self._chunk(self.param_buf, b) for b in self.buckets]))
             if self.master is not None:
@@ -320,7 +368,10 @@ class DataParallelEngine:
     def _gather_full(self, shard: torch.Tensor) -> torch.Tensor:
         full = torch.empty(self.numel, dtype=shard.dtype, device=shard.device)
         for b in self.buckets:
-            c = b.size // self.world
-            dist.all_gather_into_tensor(full[b.start:b.end], shard[b.shard_off:b.shard_off + c].contiguous(),
-                                        group=self.group)
+            c = b.size // b.world
+            if b.world == 1:
+                full[b.start:b.end].copy_(shard[b.shard_off:b.shard_off + c])
+            else:
+                dist.all_gather_into_tensor(full[b.start:b.end], shard[b.shard_off:b.shard_off + c].contiguous(),
+                                            group=b.group)
         return full

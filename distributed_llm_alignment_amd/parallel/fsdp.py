@@ -258,6 +258,8 @@ class FullyShardedEngine(_ShardedBase):
             raise ValueError("no trainable parameters")
         if len({p.dtype for p in params}) != 1:
             raise ValueError("mixed parameter dtypes")
+        if any(getattr(p, "_dla_expert", False) for p in params):
+            raise NotImplementedError("expert-parallel weights: use the ZeRO-1 engine (zero_stage <= 2)")
         if any(not p.requires_grad for p in module.parameters()):
             raise ValueError("FullyShardedEngine shards every parameter; freeze by wrapping the "
                              "frozen part in ShardedInference instead")

@@ -123,6 +123,8 @@ def make_engine(ctx: TrainContext, model, lr: float, betas=(0.9, 0.999), weight_
                 max_grad_norm: float = 1.0):
     groups = dict(group=ctx.mesh.dp_group if ctx.mesh is not None else None,
                   tp_group=ctx.mesh.tp_group if ctx.mesh is not None else None)
+    if ctx.mesh is not None and ctx.mesh.ep > 1:
+        groups["expert_group"] = ctx.mesh.edp_group
     if use_fsdp(ctx):
         from ..parallel.fsdp import FullyShardedEngine
 

@@ -447,3 +447,50 @@ def test_fsdp_checkpoint_resume(tmp_path):
     sd = load_file(str(tmp_path / "ck" / "model.safetensors"))
     cfg = get_config("tiny-llama")
     assert sd["model.embed_tokens.weight"].shape == (cfg.vocab_size, cfg.hidden_size)
+
+
+# ------------------------------------------------------------------------------ expert parallel
+def _ep_step(rank, world, ep, zero):
+    import torch
+
+    from distributed_llm_alignment_amd.data.synthetic import synthetic_preference_batch
+    from distributed_llm_alignment_amd.models import build_model, get_config
+    from distributed_llm_alignment_amd.objectives import dpo_step_loss
+    from distributed_llm_alignment_amd.parallel.data_parallel import DataParallelEngine
+    from distributed_llm_alignment_amd.parallel.expert import apply_expert_parallel
+    from distributed_llm_alignment_amd.parallel.mesh import build_mesh
+
+    mesh = build_mesh(ep=ep)
+    cfg = get_config("tiny-mixtral")
+    pol = build_model(cfg, device="cpu", seed=0)
+    ref = build_model(cfg, device="cpu", seed=0).requires_grad_(False)
+    apply_expert_parallel(pol, mesh)
+    apply_expert_parallel(ref, mesh)
+    eng = DataParallelEngine(pol, lr=1e-2, weight_decay=0.01, max_grad_norm=0.05, zero_stage=zero,
+                             group=mesh.dp_group, expert_group=mesh.edp_group, bucket_mb=0.05)
+    g = torch.Generator().manual_seed(21 + rank)
+    b = synthetic_preference_batch(2, 16, cfg.vocab_size, generator=g)
+    out = []
+    for _ in range(2):
+        loss, _ = dpo_step_loss(pol, ref, b)
+        loss.backward()
+        out.append(float(eng.step()))
+    out.append(float(dpo_step_loss(pol, ref, b)[0].detach()))
+    return out
+
+
+@pytest.mark.parametrize("zero", [0, 1])
+def test_expert_parallel_matches_replicated_experts(zero):
+    """EP=2 (all-to-all token routing, expert grads local) == DP=2 with replicated experts."""
+    a = run_ranks(_ep_step, 2, (1, zero))
+    b = run_ranks(_ep_step, 2, (2, zero))
+    for r in (0, 1):
+        assert a[r] == pytest.approx(b[r], rel=1e-4, abs=1e-6), (a[r], b[r])
+
+
+def test_expert_parallel_world4_edp2():
+    """World 4, EP=2: experts sharded 2-way and replicated 2-way (expert-DP group reduction)."""
+    a = run_ranks(_ep_step, 4, (1, 1))
+    b = run_ranks(_ep_step, 4, (2, 1))
+    for r in range(4):
+        assert a[r] == pytest.approx(b[r], rel=1e-4, abs=1e-6), (a[r], b[r])

@@ -1,0 +1,89 @@
+"""MI355X numerics of the MoE HIP kernels (router top-k fwd/bwd, dispatch, combine fwd/bwd)
+and the Mixtral layer built on them, against plain PyTorch fp32 references."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda", 0)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _native():
+    from distributed_llm_alignment_amd.ops import _ext
+
+    _ext.require()
+
+
+def test_topk_kernel_fwd_bwd():
+    from distributed_llm_alignment_amd import ops
+
+    g = torch.Generator(device=DEV).manual_seed(0)
+    # distinct logits per row (bf16 ties would make the top-k order implementation-defined)
+    perm = torch.argsort(torch.rand(4099, 8, device=DEV, generator=g), -1).float()
+    logits = (perm * 0.375 - 1.3).to(torch.bfloat16).requires_grad_(True)
+    v, i = ops.moe.route_topk(logits, 2)
+    lf = logits.detach().float().requires_grad_(True)
+    rv, ri = torch.topk(torch.softmax(lf, -1), 2, -1)
+    rv = rv / rv.sum(-1, keepdim=True)
+    assert torch.equal(i.long(), ri)
+    assert torch.allclose(v, rv, atol=1e-5)
+    gv = torch.randn_like(v)
+    (dl,) = torch.autograd.grad(v, logits, gv)
+    (rdl,) = torch.autograd.grad(rv, lf, gv)
+    assert torch.allclose(dl.float(), rdl, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("N,H,k,E", [(1000, 4096, 2, 8), (77, 136, 3, 5)])
+def test_dispatch_combine_kernels(N, H, k, E):
+    from distributed_llm_alignment_amd import ops
+
+    g = torch.Generator(device=DEV).manual_seed(1)
+    x = torch.randn(N, H, device=DEV, generator=g).to(torch.bfloat16)
+    topi = torch.stack([torch.randperm(E, device=DEV, generator=g)[:k] for _ in range(N)]).to(torch.int32)
+    pos, counts = ops.moe.expert_positions(topi, E)
+    xs = ops.moe.dispatch(x, pos)
+    assert torch.equal(xs, ops.moe._ref_dispatch(x, pos))
+    w = torch.rand(N, k, device=DEV, generator=g).requires_grad_(True)
+    ys = torch.randn(N * k, H, device=DEV, generator=g).to(torch.bfloat16).requires_grad_(True)
+    out = ops.moe.combine(ys, pos, w)
+    ysf = ys.detach().float().requires_grad_(True)
+    wf = w.detach().clone().requires_grad_(True)
+    ref = ops.moe._ref_combine(ysf, pos, wf)
+    assert torch.allclose(out.float(), ref, atol=2e-2, rtol=1e-2)
+    go = torch.randn(N, H, device=DEV, generator=g).to(torch.bfloat16)
+    dys, dw = torch.autograd.grad(out, [ys, w], go)
+    rdys, rdw = torch.autograd.grad(ref, [ysf, wf], go.float())
+    assert torch.allclose(dys.float(), rdys, atol=2e-2, rtol=1e-2)
+    assert torch.allclose(dw, rdw, atol=1e-1, rtol=1e-2)
+
+
+def test_mixtral_layer_bf16_vs_fp32_reference():
+    from distributed_llm_alignment_amd import ops
+    from distributed_llm_alignment_amd.models import build_model, get_config
+
+    cfg = get_config("tiny-mixtral", hidden_size=256, intermediate_size=512, num_experts=8)
+    m = build_model(cfg, device=DEV, dtype=torch.bfloat16, seed=2)
+    moe = m.layers[0].mlp
+    g = torch.Generator(device=DEV).manual_seed(3)
+    h = (torch.randn(4, 256, cfg.hidden_size, device=DEV, generator=g)).to(torch.bfloat16).requires_grad_(True)
+    out = moe(h)
+    ref = ops.moe.ref_moe(h.detach().reshape(-1, cfg.hidden_size), moe.router, moe.expert_up,
+                          moe.expert_down, cfg.num_experts_per_tok).view_as(h)
+    err = (out.float() - ref).abs().max() / ref.abs().max()
+    assert err < 3e-2, err
+    out.float().pow(2).sum().backward()
+    for p in (h, moe.router, moe.expert_up, moe.expert_down):
+        assert p.grad is not None and torch.isfinite(p.grad.float()).all()
+
+
+def test_fp8_expert_forward_close_to_bf16():
+    from distributed_llm_alignment_amd import ops
+
+    g = torch.Generator(device=DEV).manual_seed(4)
+    x = torch.randn(512, 1024, device=DEV, generator=g).to(torch.bfloat16)
+    w = (torch.randn(2048, 1024, device=DEV, generator=g) * 0.02).to(torch.bfloat16)
+    y8 = ops.moe.fp8_linear(x, w)
+    y = x.float() @ w.float().t()
+    rel = (y8.float() - y).norm() / y.norm()
+    assert rel < 6e-2, rel
