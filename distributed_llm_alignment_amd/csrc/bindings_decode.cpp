@@ -1,0 +1,96 @@
+// torch.ops.dla decode-path ops: split-KV decode attention (decode.hip) and the fused sampler
+// (sampling.hip). Host-side validation only; both are graph-capture safe (device-side lengths
+// and RNG counter, outputs from the caching allocator, no host sync).
+#include <ATen/ATen.h>
+#include <torch/library.h>
+
+#include <cmath>
+
+#include "bind_util.h"
+
+namespace dla {
+
+void launch_decode_attn(const bf16_t*, int64_t, int64_t, const bf16_t*, const bf16_t*, int64_t,
+                        int64_t, int64_t, const int*, const int*, int, float, int, int, int, int,
+                        int, float*, float*, bf16_t*, int64_t, int64_t, hipStream_t);
+int decode_num_splits(int Tmax);
+void launch_sample(const void*, bool, int64_t, int64_t, int, float, int, float, bool,
+                   const int64_t*, int64_t*, hipStream_t);
+
+at::Tensor decode_attn(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
+                       const at::Tensor& kv_len, const c10::optional<at::Tensor>& kv_start,
+                       int64_t window, double scale) {
+  check_bf16(q, "q");
+  check_bf16(k_cache, "k_cache");
+  check_bf16(v_cache, "v_cache");
+  check_i32(kv_len, "kv_len");
+  TORCH_CHECK(q.dim() == 3 && k_cache.dim() == 4 && v_cache.sizes() == k_cache.sizes(),
+              "q [B, Hq, D], caches [B, Tmax, Hkv, D]");
+  const int64_t B = q.size(0), Hq = q.size(1), D = q.size(2);
+  const int64_t Tmax = k_cache.size(1), Hkv = k_cache.size(2);
+  TORCH_CHECK(k_cache.size(0) == B && k_cache.size(3) == D, "cache batch / head dim");
+  TORCH_CHECK(D == 64 || D == 128, "decode attention supports head_dim 64 or 128");
+  TORCH_CHECK(Hq % Hkv == 0, "Hq % Hkv");
+  const int64_t G = Hq / Hkv;
+  TORCH_CHECK(G == 1 || G == 2 || G == 4 || G == 8, "GQA group size must be 1, 2, 4 or 8");
+  TORCH_CHECK(q.stride(2) == 1 && k_cache.stride(3) == 1 && v_cache.stride(3) == 1,
+              "head dim must be contiguous");
+  TORCH_CHECK(k_cache.strides() == v_cache.strides(), "k/v caches must share strides");
+  TORCH_CHECK(q.stride(1) % 8 == 0 && k_cache.stride(1) % 8 == 0 && k_cache.stride(2) % 8 == 0 &&
+                  k_cache.stride(0) % 8 == 0,
+              "16-byte aligned rows");
+  check_aligned16(k_cache, "k_cache");
+  check_aligned16(v_cache, "v_cache");
+  TORCH_CHECK(kv_len.numel() >= 1, "kv_len");
+  const int* ks = nullptr;
+  if (kv_start && kv_start->defined()) {
+    check_i32(*kv_start, "kv_start");
+    TORCH_CHECK(kv_start->numel() == B && kv_start->is_contiguous(), "kv_start [B]");
+    ks = kv_start->data_ptr<int>();
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
+  const int nsplit = decode_num_splits(static_cast<int>(Tmax));
+  auto fopt = q.options().dtype(at::kFloat);
+  auto part_o = at::empty({B, Hq, nsplit, D}, fopt);
+  auto part_ml = at::empty({B, Hq, nsplit, 2}, fopt);
+  auto out = at::empty({B, Hq, D}, q.options());
+  launch_decode_attn(cbp(q), q.stride(0), q.stride(1), cbp(k_cache), cbp(v_cache),
+                     k_cache.stride(0), k_cache.stride(1), k_cache.stride(2),
+                     kv_len.data_ptr<int>(), ks, static_cast<int>(window),
+                     static_cast<float>(scale * 1.4426950408889634), (int)B, (int)Hq, (int)Hkv,
+                     (int)D, (int)Tmax, part_o.data_ptr<float>(), part_ml.data_ptr<float>(),
+                     bp(out), out.stride(0), out.stride(1), cur_stream(q));
+  return out;
+}
+
+at::Tensor sample_tokens(const at::Tensor& logits, double temperature, int64_t top_k,
+                         double top_p, bool greedy, const at::Tensor& rng) {
+  check_cuda(logits, "logits");
+  TORCH_CHECK(logits.scalar_type() == at::kBFloat16 || logits.scalar_type() == at::kFloat,
+              "logits must be bf16 or fp32");
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "logits [B, V] with unit vocab stride");
+  check_cuda(rng, "rng");
+  TORCH_CHECK(rng.scalar_type() == at::kLong && rng.numel() >= 2, "rng int64 [seed, counter]");
+  TORCH_CHECK(top_p > 0.0 && top_p <= 1.0, "top_p in (0, 1]");
+  const int64_t B = logits.size(0), V = logits.size(1);
+  TORCH_CHECK(V < (1ll << 31), "vocab too large");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(logits.device());
+  auto out = at::empty({B}, logits.options().dtype(at::kLong));
+  const float inv_t = temperature > 0.0 ? static_cast<float>(1.0 / temperature) : 0.f;
+  launch_sample(logits.data_ptr(), logits.scalar_type() == at::kBFloat16, logits.stride(0), B,
+                (int)V, inv_t, (int)top_k, static_cast<float>(top_p), greedy,
+                rng.data_ptr<int64_t>(), out.data_ptr<int64_t>(), cur_stream(logits));
+  return out;
+}
+
+}  // namespace dla
+
+TORCH_LIBRARY_FRAGMENT(dla, m) {
+  m.def("decode_attn(Tensor q, Tensor k_cache, Tensor v_cache, Tensor kv_len, Tensor? kv_start, int window, float scale) -> Tensor");
+  m.def("sample_tokens(Tensor logits, float temperature, int top_k, float top_p, bool greedy, Tensor rng) -> Tensor");
+}
+
+TORCH_LIBRARY_IMPL(dla, CUDA, m) {
+  m.impl("decode_attn", &dla::decode_attn);
+  m.impl("sample_tokens", &dla::sample_tokens);
+}

@@ -20,6 +20,12 @@ from .transformer import CausalLM, attention_layout
 
 
 class KVCache:
+    """Contiguous per-layer K/V cache [L, B, T_max, Hkv, D] sized once for prompt + new tokens.
+
+    The write slot, attended length and next positions also live on the device (`slot`,
+    `kv_len`, `pos`), so a single-token decode step touches no host value: it can be captured
+    in a hipGraph and replayed (`advance_device`)."""
+
     def __init__(self, model: CausalLM, batch: int, max_len: int, kv_start: Optional[torch.Tensor]):
         cfg = model.cfg
         dev, dt = model.embed.device, model.embed.dtype
@@ -33,8 +39,16 @@ class KVCache:
         self.batch = batch
         self.kv_start = kv_start.to(torch.int32) if kv_start is not None else None
         self._pos = None
+        self.slot = torch.zeros(1, dtype=torch.long, device=dev)
+        self.kv_len = torch.ones(1, dtype=torch.int32, device=dev)
+        self.pos = torch.zeros((batch, 1), dtype=torch.int32, device=dev)
+        self.fast_decode = (dev.type == "cuda" and dt == torch.bfloat16
+                            and ops.decode.decode_supported(self.h_local, Hkv, D))
 
     def positions_for(self, T: int) -> torch.Tensor:
+        if T == 1 and self.len > 0:
+            self._pos = self.pos
+            return self.pos
         dev = self.k.device
         t = torch.arange(self.len, self.len + T, device=dev, dtype=torch.int32).unsqueeze(0)
         start = self.kv_start.unsqueeze(1) if self.kv_start is not None else 0
@@ -48,6 +62,13 @@ class KVCache:
             raise RuntimeError("KV cache overflow")
         q, k, v = ops.attention.rope_qk(qkv, rope, self.h_local, self.kv_local, cfg.head_dim,
                                         positions=self._pos)
+        if T == 1 and self.len > 0 and self.fast_decode:
+            # device-indexed write + split-KV decode kernel (graph-capturable)
+            self.k[layer].index_copy_(1, self.slot, k)
+            self.v[layer].index_copy_(1, self.slot, v)
+            o = ops.decode.decode_attention(q.reshape(B, self.h_local, cfg.head_dim), self.k[layer],
+                                            self.v[layer], self.kv_len, self.kv_start, window)
+            return o.reshape(B, 1, self.h_local * cfg.head_dim)
         self.k[layer, :, self.len:self.len + T] = k
         self.v[layer, :, self.len:self.len + T] = v
         end = self.len + T
@@ -57,7 +78,27 @@ class KVCache:
         return o.reshape(B, T, self.h_local * cfg.head_dim)
 
     def advance(self, T: int):
+        """Host-driven advance (prefill / eager decode) keeping the device state in step."""
         self.len += T
+        self.slot.fill_(self.len)
+        self.kv_len.fill_(self.len + 1)
+        start = self.kv_start.view(-1, 1) if self.kv_start is not None else 0
+        self.pos.copy_((self.len - start) if self.kv_start is not None
+                       else torch.full_like(self.pos, self.len))
+
+    capturing = False  # set while a decode step is being captured / replayed as a graph
+
+    def step_done(self, T: int):
+        if self.capturing:
+            self.advance_device()
+        else:
+            self.advance(T)
+
+    def advance_device(self):
+        """Device-only advance for a captured decode step (host `len` is tracked by the caller)."""
+        self.slot.add_(1)
+        self.kv_len.add_(1)
+        self.pos.add_(1)
 
 
 @dataclass
@@ -91,17 +132,74 @@ def sample_next(logits: torch.Tensor, do_sample: bool, temperature: float, top_p
     return torch.multinomial(probs, 1, generator=generator).squeeze(-1)
 
 
+def _graph_ok(model: CausalLM, cache: KVCache) -> bool:
+    return (cache.fast_decode and model.tp_size == 1 and getattr(model, "_dla_fsdp", None) is None
+            and ops._ext.use_native(cache.k))
+
+
+class _DecodeGraph:
+    """One captured decode step: embed -> layers (device-indexed cache writes, decode kernel)
+    -> norm -> LM head -> fused sampler -> finished/pad bookkeeping, all on device."""
+
+    def __init__(self, model, cache, B, max_new, eos, pad, greedy, temperature, top_k, top_p, seed):
+        dev = cache.k.device
+        self.model, self.cache = model, cache
+        self.tok = torch.zeros((B, 1), dtype=torch.long, device=dev)
+        self.finished = torch.zeros(B, dtype=torch.bool, device=dev)
+        self.out = torch.full((B, max_new), pad, dtype=torch.long, device=dev)
+        self.gen_mask = torch.zeros((B, max_new), dtype=torch.long, device=dev)
+        self.col = torch.zeros(1, dtype=torch.long, device=dev)
+        self.rng = torch.tensor([seed, 0], dtype=torch.long, device=dev)
+        self.eos, self.pad = eos, pad
+        self.args = (temperature, top_k, top_p, greedy)
+        self.graph = None
+
+    def _body(self):
+        h = self.model(self.tok, cache=self.cache)
+        logits = self.model.logits(h[:, -1])
+        self.sample(logits)
+
+    def sample(self, logits):
+        t, k, p, g = self.args
+        nxt = ops.decode.sample_tokens(logits, t, k, p, g, self.rng)
+        nxt = torch.where(self.finished, torch.full_like(nxt, self.pad), nxt)
+        self.gen_mask.index_copy_(1, self.col, (~self.finished).long().unsqueeze(1))
+        self.out.index_copy_(1, self.col, nxt.unsqueeze(1))
+        self.finished |= nxt == self.eos
+        self.tok.copy_(nxt.unsqueeze(1))
+        self.col.add_(1)
+        self.rng[1:].add_(1)
+
+    def capture(self):
+        self.cache.capturing = True
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(self.graph, stream=s):
+                self._body()
+        torch.cuda.current_stream().wait_stream(s)
+
+    def replay(self):
+        self.graph.replay()
+        self.cache.len += 1
+
+
 @torch.no_grad()
 def generate(model: CausalLM, input_ids: torch.Tensor, attention_mask: Optional[torch.Tensor] = None,
              max_new_tokens: int = 256, do_sample: bool = True, temperature: float = 1.0,
              top_p: float = 1.0, top_k: int = 0, eos_token_id: Optional[int] = None,
              pad_token_id: Optional[int] = None, generator: Optional[torch.Generator] = None,
-             return_mask: bool = False):
+             return_mask: bool = False, use_graph: Optional[bool] = None, seed: Optional[int] = None):
     """Left-padded prompts [B, Tp] -> sequences [B, Tp + n] (n <= max_new_tokens).
 
     With `return_mask`, also returns the attention mask of the full sequence (prompt mask, then
     1 for every generated token up to and including EOS, 0 afterwards) — the correct mask for
-    the RLHF log-prob pass (fixes Appendix A #10's `generated != pad` which drops real EOS)."""
+    the RLHF log-prob pass (fixes Appendix A #10's `generated != pad` which drops real EOS).
+
+    On MI355X the prompt is prefilled with the flash-attention kernel, then every new token is
+    ONE replay of a captured hipGraph (decode kernel + fused sampler, no host sync except an
+    all-finished check every 16 tokens). `use_graph=False` forces the eager per-op loop."""
     was_training = model.training
     model.eval()
     B, Tp = input_ids.shape
@@ -112,29 +210,56 @@ def generate(model: CausalLM, input_ids: torch.Tensor, attention_mask: Optional[
         kv_start, _, _ = attention_layout(attention_mask)
     cache = KVCache(model, B, Tp + max_new_tokens, kv_start)
     h = model(input_ids, cache=cache)
-    out = [input_ids]
-    gen_mask = []
-    finished = torch.zeros(B, dtype=torch.bool, device=input_ids.device)
-    last = h[:, -1]
-    for step in range(max_new_tokens):
-        logits = model.logits(last).float()
-        nxt = sample_next(logits, do_sample, temperature, top_p, top_k, generator)
-        if model.tp_size > 1:  # every TP rank must continue with the same token
-            import torch.distributed as dist
-
-            dist.broadcast(nxt, src=dist.get_global_rank(model.tp, 0), group=model.tp)
-        nxt = torch.where(finished, torch.full_like(nxt, pad), nxt)
-        gen_mask.append((~finished).long())
-        out.append(nxt.unsqueeze(1))
-        finished = finished | (nxt == eos)
-        if step + 1 < max_new_tokens:
-            if step % 16 == 15 and bool(finished.all()):
+    greedy = not do_sample or temperature <= 0
+    if seed is None:
+        seed = int(torch.randint(0, 2 ** 62, (1,), generator=generator).item()) if generator is not None \
+            and generator.device.type == "cpu" else int(torch.randint(0, 2 ** 62, (1,)).item())
+    graph_ok = _graph_ok(model, cache) if use_graph is None else (use_graph and _graph_ok(model, cache))
+    if graph_ok and max_new_tokens > 2:
+        dg = _DecodeGraph(model, cache, B, max_new_tokens, eos, pad, greedy, temperature, top_k, top_p, seed)
+        dg.sample(model.logits(h[:, -1]))  # token 1 from the prefill, eager
+        h = model(dg.tok, cache=cache)  # token 2 eagerly: warms every decode-shape kernel/GEMM
+        dg.sample(model.logits(h[:, -1]))
+        n = 2
+        if n < max_new_tokens:
+            dg.capture()  # records (does not run) one decode step
+        while n < max_new_tokens:
+            dg.replay()
+            n += 1
+            if n % 16 == 0 and bool(dg.finished.all()):
                 break
-            last = model(nxt.unsqueeze(1), cache=cache)[:, -1]
+        cache.capturing = False
+        seqs = torch.cat([input_ids, dg.out[:, :n]], dim=1)
+        gm = dg.gen_mask[:, :n]
+    else:
+        out, gen_mask = [input_ids], []
+        finished = torch.zeros(B, dtype=torch.bool, device=input_ids.device)
+        rng = torch.tensor([seed, 0], dtype=torch.long, device=input_ids.device)
+        last = h[:, -1]
+        for step in range(max_new_tokens):
+            logits = model.logits(last)
+            if ops._ext.use_native(logits):
+                nxt = ops.decode.sample_tokens(logits, temperature, top_k, top_p, greedy, rng)
+                rng[1:].add_(1)
+            else:
+                nxt = sample_next(logits.float(), do_sample, temperature, top_p, top_k, generator)
+            if model.tp_size > 1:  # every TP rank must continue with the same token
+                import torch.distributed as dist
+
+                dist.broadcast(nxt, src=dist.get_global_rank(model.tp, 0), group=model.tp)
+            nxt = torch.where(finished, torch.full_like(nxt, pad), nxt)
+            gen_mask.append((~finished).long())
+            out.append(nxt.unsqueeze(1))
+            finished = finished | (nxt == eos)
+            if step + 1 < max_new_tokens:
+                if step % 16 == 15 and bool(finished.all()):
+                    break
+                last = model(nxt.unsqueeze(1), cache=cache)[:, -1]
+        seqs = torch.cat(out, dim=1)
+        gm = torch.stack(gen_mask, 1)
     if was_training:
         model.train()
-    seqs = torch.cat(out, dim=1)
     if not return_mask:
         return seqs
     pm = attention_mask if attention_mask is not None else torch.ones_like(input_ids)
-    return seqs, torch.cat([pm.long(), torch.stack(gen_mask, 1)], dim=1)
+    return seqs, torch.cat([pm.long(), gm], dim=1)

@@ -274,7 +274,7 @@ class CausalLM(nn.Module):
             x, resid = layer(x, resid, self.rope, None, None, None, cache, i)
         h, _ = ops.add_norm(x, resid, self.norm_w, self.norm_b, self.cfg.norm_eps,
                             self.cfg.norm_type == "rms")
-        cache.advance(input_ids.shape[1])
+        cache.step_done(input_ids.shape[1])
         return h
 
     def logits(self, hidden: torch.Tensor) -> torch.Tensor:

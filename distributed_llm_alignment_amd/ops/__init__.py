@@ -1,6 +1,6 @@
 """gfx950 compute ops. GPU tensors run the in-tree HIP kernels (`torch.ops.dla.*`); CPU tensors
 run the pure-PyTorch references (test tier / numerics oracles)."""
-from . import _ext, moe
+from . import _ext, decode, moe
 from .activations import gelu_new, swiglu
 from .attention import RotaryCache, attention_core, qkv_attention, ref_attention
 from .linear import accumulate_weight_grad, linear
@@ -9,7 +9,7 @@ from .losses import dpo_loss, ensemble_kl, kl_penalty_pg, pairwise_loss
 from .norm import add_norm, layer_norm, rms_norm
 
 __all__ = [
-    "_ext", "moe", "gelu_new", "swiglu", "RotaryCache", "attention_core", "qkv_attention",
+    "_ext", "decode", "moe", "gelu_new", "swiglu", "RotaryCache", "attention_core", "qkv_attention",
     "ref_attention", "linear_logprob", "seq_reduce", "sequence_logprob", "shifted_targets",
     "token_nll", "dpo_loss", "ensemble_kl", "kl_penalty_pg", "pairwise_loss", "add_norm",
     "layer_norm", "rms_norm", "linear", "accumulate_weight_grad",
