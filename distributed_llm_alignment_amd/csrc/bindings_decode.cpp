@@ -14,6 +14,9 @@ void launch_decode_attn(const bf16_t*, int64_t, int64_t, const bf16_t*, const bf
                         int64_t, int64_t, const int*, const int*, int, float, int, int, int, int,
                         int, float*, float*, bf16_t*, int64_t, int64_t, hipStream_t);
 int decode_num_splits(int Tmax);
+void launch_rope_cache(const bf16_t*, int64_t, bf16_t*, bf16_t*, bf16_t*, int64_t, int64_t,
+                       int64_t, const int64_t*, const float*, const float*, const int*, int, int,
+                       int, int, int, hipStream_t);
 void launch_sample(const void*, bool, int64_t, int64_t, int, float, int, float, bool,
                    const int64_t*, int64_t*, hipStream_t);
 
@@ -63,6 +66,42 @@ at::Tensor decode_attn(const at::Tensor& q, const at::Tensor& k_cache, const at:
   return out;
 }
 
+// qkv [B, 1, (Hq + 2 Hkv) D] of the newest token -> rotated q [B, Hq, D]; k/v written into
+// k_cache/v_cache [B, Tmax, Hkv, D] at row `slot` (int64 [1] on device).
+at::Tensor rope_cache_write(const at::Tensor& qkv, const at::Tensor& cos, const at::Tensor& sin,
+                            const at::Tensor& pos, at::Tensor& k_cache, at::Tensor& v_cache,
+                            const at::Tensor& slot, int64_t Hq, int64_t Hkv, int64_t D, int64_t rot) {
+  check_bf16(qkv, "qkv");
+  check_bf16(k_cache, "k_cache");
+  check_bf16(v_cache, "v_cache");
+  check_f32(cos, "cos");
+  check_f32(sin, "sin");
+  check_i32(pos, "pos");
+  check_cuda(slot, "slot");
+  TORCH_CHECK(slot.scalar_type() == at::kLong && slot.numel() >= 1, "slot int64");
+  const int64_t B = qkv.size(0);
+  TORCH_CHECK(qkv.dim() == 3 && qkv.size(1) == 1 && qkv.size(2) == (Hq + 2 * Hkv) * D &&
+                  qkv.stride(2) == 1 && qkv.stride(0) % 8 == 0,
+              "qkv [B, 1, (Hq+2Hkv)D] with 16-byte aligned rows");
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(0) == B && k_cache.size(2) == Hkv &&
+                  k_cache.size(3) == D && k_cache.sizes() == v_cache.sizes() &&
+                  k_cache.strides() == v_cache.strides() && k_cache.stride(3) == 1,
+              "caches [B, Tmax, Hkv, D]");
+  TORCH_CHECK(D % 8 == 0 && rot % 16 == 0 && rot <= D, "D % 8, rot % 16");
+  TORCH_CHECK(cos.is_contiguous() && sin.is_contiguous() && cos.size(-1) == rot / 2, "rope tables");
+  TORCH_CHECK(pos.numel() == B && pos.is_contiguous(), "pos [B]");
+  check_aligned16(qkv, "qkv");
+  check_aligned16(k_cache, "k_cache");
+  check_aligned16(v_cache, "v_cache");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(qkv.device());
+  auto q = at::empty({B, Hq, D}, qkv.options());
+  launch_rope_cache(cbp(qkv), qkv.stride(0), bp(q), bp(k_cache), bp(v_cache), k_cache.stride(0),
+                    k_cache.stride(1), k_cache.stride(2), slot.data_ptr<int64_t>(),
+                    cos.data_ptr<float>(), sin.data_ptr<float>(), pos.data_ptr<int>(), (int)B,
+                    (int)Hq, (int)Hkv, (int)D, (int)rot, cur_stream(qkv));
+  return q;
+}
+
 at::Tensor sample_tokens(const at::Tensor& logits, double temperature, int64_t top_k,
                          double top_p, bool greedy, const at::Tensor& rng) {
   check_cuda(logits, "logits");
@@ -87,10 +126,12 @@ at::Tensor sample_tokens(const at::Tensor& logits, double temperature, int64_t t
 
 TORCH_LIBRARY_FRAGMENT(dla, m) {
   m.def("decode_attn(Tensor q, Tensor k_cache, Tensor v_cache, Tensor kv_len, Tensor? kv_start, int window, float scale) -> Tensor");
+  m.def("rope_cache_write(Tensor qkv, Tensor cos, Tensor sin, Tensor pos, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor slot, int Hq, int Hkv, int D, int rot) -> Tensor");
   m.def("sample_tokens(Tensor logits, float temperature, int top_k, float top_p, bool greedy, Tensor rng) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(dla, CUDA, m) {
   m.impl("decode_attn", &dla::decode_attn);
   m.impl("sample_tokens", &dla::sample_tokens);
+  m.impl("rope_cache_write", &dla::rope_cache_write);
 }

@@ -4,20 +4,24 @@
 //
 // Decode is bandwidth bound: each step streams the whole KV cache once. Design:
 //   * split-KV (flash-decoding): grid = (splits, Hkv, B); a block owns one KV head, ALL its
-//     G = Hq/Hkv query heads (GQA: the K/V rows are read once, not G times) and a 256-key chunk;
-//   * phase 1: one thread per key — the K row (D bf16) is streamed with 16-byte loads, q comes
-//     from LDS as a broadcast, G dot products per thread;
-//   * phase 2: lanes over the head dim (coalesced 256-byte V rows), 4 waves over 64-key quarters,
-//     probabilities from LDS;
+//     G = Hq/Hkv query heads (GQA: the K/V rows are read once, not G times) and a 128-key chunk;
+//   * rows are read cooperatively: D/8 lanes x 16 B per K/V row (one 256-byte row per 16 lanes
+//     for D = 128, 4 rows per wave instruction, fully coalesced); each lane keeps its 8-dim slice
+//     of the G query vectors in registers; dot products reduce across the row's lanes by
+//     shuffles; P.V accumulates per lane and reduces across row groups, then across waves;
 //   * partial (m, l, o) per split in fp32, merged by `decode_combine_kernel`.
 // Lengths are DEVICE values (kv_len scalar, per-row kv_start for left padding), so the same
 // launch replays inside a captured hipGraph while the cache grows; splits beyond kv_len exit.
+#include <algorithm>
+
 #include "common.h"
 
 namespace dla {
 
-constexpr int kDecChunk = 256;
+constexpr int kDecChunk = 128;  // keys per block (4 waves x 32)
 
+// Lanes cooperate on rows: LPK = D/8 lanes x 16 B cover one K/V row (coalesced 256-byte rows
+// for D = 128), KPI = 64/LPK rows per wave instruction.
 template <int D, int G>
 __global__ __launch_bounds__(256) void decode_attn_kernel(
     const bf16_t* __restrict__ q, int64_t q_sb, int64_t q_sh,     // q [B, Hq, D]
@@ -27,6 +31,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
     float* __restrict__ part_o,  // [B, Hq, nsplit, D]
     float* __restrict__ part_ml, // [B, Hq, nsplit, 2]
     int Hq) {
+  constexpr int LPK = D / 8, KPI = 64 / LPK, KPW = kDecChunk / 4;
   __shared__ float qs[G][D];
   __shared__ float ps[G][kDecChunk];
   __shared__ float red[G][4];
@@ -36,7 +41,8 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
   const int len = kv_len[0];
   int lo = kv_start ? kv_start[b] : 0;
   if (window > 0) lo = max(lo, len - window);
-  const int k0 = max(split * kDecChunk, lo), k1 = min((split + 1) * kDecChunk, len);
+  const int base = split * kDecChunk;
+  const int k0 = max(base, lo), k1 = min(base + kDecChunk, len);
   const int64_t pbase = ((int64_t)b * Hq + (int64_t)hk * G) * nsplit + split;
   if (k0 >= k1) {  // empty split (beyond the current length or fully masked)
     if (tid < G) {
@@ -50,76 +56,100 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
     qs[g][d] = bf2f(q[(int64_t)b * q_sb + (int64_t)(hk * G + g) * q_sh + d]) * scale_log2;
   }
   __syncthreads();
-  // ---- phase 1: scores (log2 domain), thread per key
-  const int key = split * kDecChunk + tid;
-  float s[G];
+  const int sub = lane / LPK, dl = (lane % LPK) * 8;
+  const bf16_t* kbase = kc + (int64_t)b * c_sb + (int64_t)hk * c_sh + dl;
+  const bf16_t* vbase = vc + (int64_t)b * c_sb + (int64_t)hk * c_sh + dl;
+  float qr[G][8];
 #pragma unroll
-  for (int g = 0; g < G; ++g) s[g] = -INFINITY;
-  if (key >= k0 && key < k1) {
-    const bf16_t* krow = kc + (int64_t)b * c_sb + (int64_t)key * c_st + (int64_t)hk * c_sh;
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) qr[g][j] = qs[g][dl + j];
+  // ---- phase 1: scores (log2 domain)
+#pragma unroll
+  for (int it = 0; it < KPW / KPI; ++it) {
+    const int kl = wv * KPW + it * KPI + sub;  // key within the chunk
+    const int key = base + kl;
+    const bool ok = key >= k0 && key < k1;
+    float s[G];
 #pragma unroll
     for (int g = 0; g < G; ++g) s[g] = 0.f;
-#pragma unroll 4
-    for (int d8 = 0; d8 < D / 8; ++d8) {
-      const bf16x8 kv = load_bf16x8(krow + d8 * 8);
+    if (ok) {
+      const bf16x8 kv = load_bf16x8(kbase + (int64_t)key * c_st);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float kf = bf2f(kv[j]);
 #pragma unroll
-        for (int g = 0; g < G; ++g) s[g] += qs[g][d8 * 8 + j] * kf;
+        for (int g = 0; g < G; ++g) s[g] += qr[g][j] * kf;
       }
     }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+#pragma unroll
+      for (int o = 1; o < LPK; o <<= 1) s[g] += __shfl_xor(s[g], o, 64);
+    }
+    if ((lane % LPK) == 0) {
+#pragma unroll
+      for (int g = 0; g < G; ++g) ps[g][kl] = ok ? s[g] : -INFINITY;
+    }
   }
-  // block max per head
+  __syncthreads();
+  // ---- softmax over the chunk: thread t < 128 owns key t for every head
+  float mg[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) {
-    const float m = wave_max(s[g]);
+    const float v = tid < kDecChunk ? ps[g][tid] : -INFINITY;
+    const float m = wave_max(v);
     if (lane == 0) red[g][wv] = m;
   }
   __syncthreads();
-  float mg[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) mg[g] = fmaxf(fmaxf(red[g][0], red[g][1]), fmaxf(red[g][2], red[g][3]));
   __syncthreads();
 #pragma unroll
   for (int g = 0; g < G; ++g) {
-    const float p = (key >= k0 && key < k1) ? __builtin_amdgcn_exp2f(s[g] - mg[g]) : 0.f;
-    ps[g][tid] = p;
+    float p = 0.f;
+    if (tid < kDecChunk) {
+      const float sv = ps[g][tid];
+      p = sv == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(sv - mg[g]);
+      ps[g][tid] = p;
+    }
     const float l = wave_sum(p);
     if (lane == 0) red[g][wv] = l;
   }
   __syncthreads();
-  // ---- phase 2: o[g][d] = sum_key p[g][key] * v[key][d]; wave wv covers keys [64 wv, 64 wv + 64)
-  constexpr int DPT = D / 64;  // dims per lane
-  float o[G][DPT];
+  // ---- phase 2: o[g][d] = sum_key p[g][key] v[key][d]; wave wv owns keys [wv*KPW, wv*KPW+KPW)
+  float o[G][8];
 #pragma unroll
   for (int g = 0; g < G; ++g)
 #pragma unroll
-    for (int j = 0; j < DPT; ++j) o[g][j] = 0.f;
-  const int kb = split * kDecChunk + wv * 64;
-  const int ka = max(kb, k0), ke = min(kb + 64, k1);
-  for (int kk = ka; kk < ke; ++kk) {
-    const bf16_t* vrow = vc + (int64_t)b * c_sb + (int64_t)kk * c_st + (int64_t)hk * c_sh + lane * DPT;
-    float vf[DPT];
-    if constexpr (DPT == 2) {
-      const uint32_t w = *reinterpret_cast<const uint32_t*>(vrow);
-      vf[0] = bf2f(w & 0xffff);
-      vf[1] = bf2f(w >> 16);
-    } else {
-      vf[0] = bf2f(vrow[0]);
-    }
-    const int pi = kk - split * kDecChunk;
+    for (int j = 0; j < 8; ++j) o[g][j] = 0.f;
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-      const float p = ps[g][pi];
+  for (int it = 0; it < KPW / KPI; ++it) {
+    const int kl = wv * KPW + it * KPI + sub;
+    const int key = base + kl;
+    if (key >= k0 && key < k1) {
+      const bf16x8 vv = load_bf16x8(vbase + (int64_t)key * c_st);
 #pragma unroll
-      for (int j = 0; j < DPT; ++j) o[g][j] += p * vf[j];
+      for (int g = 0; g < G; ++g) {
+        const float p = ps[g][kl];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[g][j] += p * bf2f(vv[j]);
+      }
     }
   }
+  // reduce the KPI key sub-groups of the wave (lanes sharing dl)
 #pragma unroll
   for (int g = 0; g < G; ++g)
 #pragma unroll
-    for (int j = 0; j < DPT; ++j) acc_s[wv][g][lane * DPT + j] = o[g][j];
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int off = LPK; off < 64; off <<= 1) o[g][j] += __shfl_xor(o[g][j], off, 64);
+  if (sub == 0) {
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc_s[wv][g][dl + j] = o[g][j];
+  }
   __syncthreads();
   for (int i = tid; i < G * D; i += 256) {
     const int g = i / D, d = i % D;
@@ -130,6 +160,56 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
     part_ml[(pbase + (int64_t)tid * nsplit) * 2 + 0] = mg[tid];
     part_ml[(pbase + (int64_t)tid * nsplit) * 2 + 1] = red[tid][0] + red[tid][1] + red[tid][2] + red[tid][3];
   }
+}
+
+// Decode-step prologue: rotate q (-> q_out [B, Hq, D]) and k of the newest token and write k and
+// v straight into the cache slot `*slot` (device value), replacing rope + two index_copy
+// launches. qkv [B, (Hq + 2 Hkv) * D] rows; same rotate-half math as rope.hip.
+__global__ __launch_bounds__(256) void rope_cache_kernel(
+    const bf16_t* __restrict__ qkv, int64_t ld, bf16_t* __restrict__ q_out,
+    bf16_t* __restrict__ kc, bf16_t* __restrict__ vc, int64_t c_sb, int64_t c_st, int64_t c_sh,
+    const int64_t* __restrict__ slot, const float* __restrict__ cos_t,
+    const float* __restrict__ sin_t, const int* __restrict__ pos, int B, int Hq, int Hkv, int D,
+    int rot) {
+  const int dv = D >> 3, heads = Hq + 2 * Hkv, half = rot >> 1, hv = half >> 3;
+  const int64_t total = (int64_t)B * heads * dv;
+  const int64_t t_slot = slot[0];
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int v = (int)(i % dv);
+    const int h = (int)((i / dv) % heads);
+    const int b = (int)(i / ((int64_t)dv * heads));
+    const bf16_t* s = qkv + (int64_t)b * ld + (int64_t)h * D;
+    bf16_t* d;
+    if (h < Hq) d = q_out + ((int64_t)b * Hq + h) * D;
+    else if (h < Hq + Hkv) d = kc + (int64_t)b * c_sb + t_slot * c_st + (int64_t)(h - Hq) * c_sh;
+    else d = vc + (int64_t)b * c_sb + t_slot * c_st + (int64_t)(h - Hq - Hkv) * c_sh;
+    if (h < Hq + Hkv && v < hv) {
+      const int p = pos[b];
+      const float* cp = cos_t + (int64_t)p * half + v * 8;
+      const float* sp = sin_t + (int64_t)p * half + v * 8;
+      bf16x8 lo = load_bf16x8(s + v * 8), hi = load_bf16x8(s + half + v * 8), olo, ohi;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float c = cp[j], sn = sp[j], a = bf2f(lo[j]), bb = bf2f(hi[j]);
+        olo[j] = f2bf(a * c - bb * sn);
+        ohi[j] = f2bf(bb * c + a * sn);
+      }
+      store_bf16x8(d + v * 8, olo);
+      store_bf16x8(d + half + v * 8, ohi);
+    } else if (h >= Hq + Hkv || v >= 2 * hv) {
+      store_bf16x8(d + v * 8, load_bf16x8(s + v * 8));
+    }
+  }
+}
+
+void launch_rope_cache(const bf16_t* qkv, int64_t ld, bf16_t* q_out, bf16_t* kc, bf16_t* vc,
+                       int64_t c_sb, int64_t c_st, int64_t c_sh, const int64_t* slot,
+                       const float* cos_t, const float* sin_t, const int* pos, int B, int Hq,
+                       int Hkv, int D, int rot, hipStream_t st) {
+  const int64_t work = (int64_t)B * (Hq + 2 * Hkv) * (D / 8);
+  const int grid = (int)std::min<int64_t>((work + 255) / 256, 1024);
+  rope_cache_kernel<<<grid, 256, 0, st>>>(qkv, ld, q_out, kc, vc, c_sb, c_st, c_sh, slot, cos_t,
+                                          sin_t, pos, B, Hq, Hkv, D, rot);
 }
 
 // one block per (b, h): merge the splits (log2-domain running max)

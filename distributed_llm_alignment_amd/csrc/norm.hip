@@ -95,6 +95,81 @@ __global__ __launch_bounds__(256) void norm_fwd_kernel(const bf16_t* __restrict_
   }
 }
 
+// Few-row variant (decode: rows = batch): one block per row, one 16-byte chunk per thread
+// (blockDim = H/8 rounded to a wave multiple, <= 1024), so a row costs one load round trip
+// instead of NC sequential chunks on a single wave.
+template <bool RMS, bool HAS_RES, bool HAS_BIAS>
+__global__ __launch_bounds__(1024) void norm_fwd_row_kernel(const bf16_t* __restrict__ x,
+                                                             const bf16_t* __restrict__ res,
+                                                             bf16_t* __restrict__ sum_out,
+                                                             const bf16_t* __restrict__ w,
+                                                             const bf16_t* __restrict__ b,
+                                                             bf16_t* __restrict__ y,
+                                                             float* __restrict__ rstd_out,
+                                                             float* __restrict__ mean_out, int H,
+                                                             float eps) {
+  __shared__ float red[16];
+  const int row = blockIdx.x, t = threadIdx.x, nw = blockDim.x >> 6;
+  const size_t base = static_cast<size_t>(row) * H;
+  const bool on = t < (H >> 3);
+  float v[8];
+  if (on) {
+    bf16x8 a = load_bf16x8(x + base + t * 8);
+    if constexpr (HAS_RES) {
+      bf16x8 r = load_bf16x8(res + base + t * 8), sm;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sm[j] = f2bf(bf2f(a[j]) + bf2f(r[j]));
+        v[j] = bf2f(sm[j]);
+      }
+      store_bf16x8(sum_out + base + t * 8, sm);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = bf2f(a[j]);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = 0.f;
+  }
+  auto bsum = [&](float q) {
+    q = wave_sum(q);
+    __syncthreads();
+    if ((t & 63) == 0) red[t >> 6] = q;
+    __syncthreads();
+    float r = 0.f;
+    for (int i = 0; i < nw; ++i) r += red[i];
+    return r;
+  };
+  float mean = 0.f;
+  if constexpr (!RMS) {
+    float q = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) q += v[j];
+    mean = bsum(q) / H;
+  }
+  float ss = 0.f;
+  if (on) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ss += (v[j] - mean) * (v[j] - mean);
+  }
+  const float rstd = rsqrtf(bsum(ss) / H + eps);
+  if (t == 0) {
+    rstd_out[row] = rstd;
+    if constexpr (!RMS) mean_out[row] = mean;
+  }
+  if (on) {
+    bf16x8 wv = load_bf16x8(w + t * 8), bv, o;
+    if constexpr (HAS_BIAS) bv = load_bf16x8(b + t * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float q = (v[j] - mean) * rstd * bf2f(wv[j]);
+      if constexpr (HAS_BIAS) q += bf2f(bv[j]);
+      o[j] = f2bf(q);
+    }
+    store_bf16x8(y + base + t * 8, o);
+  }
+}
+
 // Backward. One 256-thread block owns a row at a time (grid-stride over rows with a fixed
 // grid); each thread owns NC fixed 8-column chunks, so its dw/db partials stay in NC*8
 // registers across all rows of the block. One fp32 partial row per block ([grid, H]) is then
@@ -256,9 +331,26 @@ static int chunks_for(int H, int threads) {
 void launch_norm_fwd(const bf16_t* x, const bf16_t* res, bf16_t* sum_out, const bf16_t* w,
                      const bf16_t* b, bf16_t* y, float* rstd, float* mean, int rows, int H,
                      float eps, bool rms, hipStream_t st) {
+  const bool hr = res != nullptr, hb = b != nullptr;
+  if (rows < 512 && H <= 8192) {  // few rows (decode): block per row
+    const int nt = ((H / 8 + 63) / 64) * 64;
+#define DLA_NORM_ROW(R, HR, HB) \
+  norm_fwd_row_kernel<R, HR, HB><<<rows, nt, 0, st>>>(x, res, sum_out, w, b, y, rstd, mean, H, eps)
+    if (rms) {
+      if (hr) DLA_NORM_ROW(true, true, false);
+      else DLA_NORM_ROW(true, false, false);
+    } else if (hr) {
+      if (hb) DLA_NORM_ROW(false, true, true);
+      else DLA_NORM_ROW(false, true, false);
+    } else {
+      if (hb) DLA_NORM_ROW(false, false, true);
+      else DLA_NORM_ROW(false, false, false);
+    }
+#undef DLA_NORM_ROW
+    return;
+  }
   const int nc = chunks_for(H, 64);
   dim3 grid((rows + 3) / 4);
-  const bool hr = res != nullptr, hb = b != nullptr;
   if (rms) {
     if (hr) launch_fwd_nc<true, true, false>(nc, grid, st, x, res, sum_out, w, b, y, rstd, mean, rows, H, eps);
     else launch_fwd_nc<true, false, false>(nc, grid, st, x, res, sum_out, w, b, y, rstd, mean, rows, H, eps);

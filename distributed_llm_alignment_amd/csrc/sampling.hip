@@ -4,12 +4,14 @@
 // eval_alignment.py:68-79).
 //
 // One 1024-thread block per row streams the (bf16) logits row, which stays L2-resident across
-// the passes (V = 128256 -> 256 KB):
+// the passes (V = 128256 -> 256 KB). Work in z = (x - max) / T:
 //   1. max / argmax (greedy rows stop here);
-//   2. top-k threshold: bisection on the logit value, counting tokens >= mid;
-//   3. top-p threshold on the renormalised top-k mass: bisection on the value so that the kept
-//      set is the smallest prefix (descending) whose mass reaches top_p (HF TopPLogitsWarper);
-//   4. draw u ~ U(0, kept mass) with Philox4x32-10 keyed by (seed, row, step counter) and locate
+//   2. thresholds by two-level LDS histograms instead of a sort: 2048 coarse bins over
+//      z in [-64, 0] (counts + exp-masses, LDS atomics), a block suffix scan locates the bin
+//      holding the k-th largest value (top-k) / the nucleus edge (top-p on the renormalised
+//      top-k mass, HF TopKLogitsWarper -> TopPLogitsWarper order); a second 2048-bin histogram
+//      inside that bin pins the threshold to 64/2048^2 ~ 1.5e-5 in z (2-5 passes per row);
+//   3. draw u ~ U(0, kept mass) with Philox4x32-10 keyed by (seed, row, step counter) and locate
 //      the token with a block prefix scan over contiguous per-thread vocab segments.
 // No sort, no [B, V] temporaries, no host sync; the step counter lives in device memory so a
 // captured hipGraph draws fresh numbers on every replay.
@@ -50,8 +52,79 @@ __device__ __forceinline__ float ld<bf16_t>(const bf16_t* p, int64_t i) { return
 template <>
 __device__ __forceinline__ float ld<float>(const float* p, int64_t i) { return p[i]; }
 
-__device__ __forceinline__ float bsum(float v, float* sc) { return block_sum<kSampNT>(v, sc); }
-__device__ __forceinline__ float bmax(float v, float* sc) { return block_max<kSampNT>(v, sc); }
+constexpr int kBins = 2048;    // histogram bins per refinement level
+constexpr float kRange = 64.f;  // z = (x - max)/T in [-64, 0]; below: e^-64 relative mass, dropped
+
+// In-place SUFFIX sums (from the top bin down) of c[kBins] / m[kBins] in LDS; 2 bins per thread.
+__device__ void suffix_scan(int* c, float* m, int* tc, float* tm) {
+  const int t = threadIdx.x;
+  const int b0 = kBins - 2 - 2 * t;  // thread t owns bins b0, b0+1 (t = 0 owns the top pair)
+  int lc = c[b0] + c[b0 + 1];
+  float lm = m[b0] + m[b0 + 1];
+  tc[t] = lc;
+  tm[t] = lm;
+  __syncthreads();
+  for (int o = 1; o < kSampNT; o <<= 1) {  // inclusive prefix over t == suffix over bins
+    const int ac = t >= o ? tc[t - o] : 0;
+    const float am = t >= o ? tm[t - o] : 0.f;
+    __syncthreads();
+    tc[t] += ac;
+    tm[t] += am;
+    __syncthreads();
+  }
+  const int ec = tc[t] - lc;  // mass strictly above this thread's pair
+  const float em = tm[t] - lm;
+  const int c1 = c[b0 + 1];
+  const float m1 = m[b0 + 1];
+  __syncthreads();
+  c[b0 + 1] = ec + c1;
+  m[b0 + 1] = em + m1;
+  c[b0] = ec + lc;
+  m[b0] = em + lm;
+  __syncthreads();
+}
+
+// Histogram of the row's z over [lo, lo + w) into kBins bins (counts + exp masses), optionally
+// restricted to z >= floor_z.
+template <typename T>
+__device__ void histogram(const T* row, int V, float gmax, float inv_t, float lo, float w,
+                          float floor_z, int* c, float* m) {
+  for (int i = threadIdx.x; i < kBins; i += kSampNT) {
+    c[i] = 0;
+    m[i] = 0.f;
+  }
+  __syncthreads();
+  const float sc = kBins / w;
+  const float hi = lo + w;
+  const bool top = hi >= 0.f;  // the top bin also holds z == 0 (the max itself)
+  for (int v = threadIdx.x; v < V; v += kSampNT) {
+    const float z = (ld(row, v) - gmax) * inv_t;
+    if (z >= lo && (z < hi || (top && z <= 0.f)) && z >= floor_z) {
+      const int b = min(kBins - 1, (int)((z - lo) * sc));
+      atomicAdd(&c[b], 1);
+      atomicAdd(&m[b], __expf(z));
+    }
+  }
+  __syncthreads();
+}
+
+// Largest bin b whose suffix value reaches `need` (suffix arrays are non-increasing in b).
+__device__ int find_bin_count(const int* sc, int need, int* out) {
+  if (threadIdx.x == 0) *out = 0;
+  __syncthreads();
+  for (int b = threadIdx.x; b < kBins; b += kSampNT)
+    if (sc[b] >= need && (b == kBins - 1 || sc[b + 1] < need)) *out = b;
+  __syncthreads();
+  return *out;
+}
+__device__ int find_bin_mass(const float* sm, float need, int* out) {
+  if (threadIdx.x == 0) *out = 0;
+  __syncthreads();
+  for (int b = threadIdx.x; b < kBins; b += kSampNT)
+    if (sm[b] >= need && (b == kBins - 1 || sm[b + 1] < need)) *out = b;
+  __syncthreads();
+  return *out;
+}
 
 template <typename T>
 __global__ __launch_bounds__(kSampNT) void sample_kernel(const T* __restrict__ logits, int64_t ld_,
@@ -60,7 +133,12 @@ __global__ __launch_bounds__(kSampNT) void sample_kernel(const T* __restrict__ l
                                                           const int64_t* __restrict__ rng,
                                                           int64_t* __restrict__ out) {
   __shared__ float sc[kSampNT / 64];
-  __shared__ float seg[kSampNT];
+  __shared__ int amin[kSampNT / 64];
+  __shared__ int hc[kBins];
+  __shared__ float hm[kBins];
+  __shared__ int tc[kSampNT];
+  __shared__ float tm[kSampNT];
+  __shared__ int sel;
   __shared__ int ans;
   const int64_t r = blockIdx.x;
   const T* row = logits + r * ld_;
@@ -75,59 +153,76 @@ __global__ __launch_bounds__(kSampNT) void sample_kernel(const T* __restrict__ l
       am = v;
     }
   }
-  const float gmax = bmax(m, sc);
+  const float gmax = block_max<kSampNT>(m, sc);
   int cand = (m == gmax) ? am : 0x7fffffff;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) cand = min(cand, __shfl_xor(cand, o, 64));
-  __shared__ int amin[kSampNT / 64];
   if ((tid & 63) == 0) amin[tid >> 6] = cand;
   __syncthreads();
+  int argmax = amin[0];
+  for (int i = 1; i < kSampNT / 64; ++i) argmax = min(argmax, amin[i]);
   if (greedy || inv_temp <= 0.f) {
-    if (tid == 0) {
-      int a = amin[0];
-      for (int i = 1; i < kSampNT / 64; ++i) a = min(a, amin[i]);
-      out[r] = a;
-    }
+    if (tid == 0) out[r] = argmax;
     return;
   }
-  // work in scaled-logit space z = (x - max) * inv_temp (<= 0); weight e(z) = exp(z)
-  // 2. top-k threshold: largest tau with count(z >= tau) >= k
-  float tau_lo = -INFINITY;
-  if (top_k > 0 && top_k < V) {
-    float lo = -80.f, hi = 0.f;  // exp(-80) ~ 0: below is irrelevant mass
-    for (int it = 0; it < 24; ++it) {
-      const float mid = 0.5f * (lo + hi);
-      float c = 0.f;
-      for (int v = tid; v < V; v += kSampNT) c += ((ld(row, v) - gmax) * inv_temp >= mid) ? 1.f : 0.f;
-      c = bsum(c, sc);
-      if (c >= (float)top_k) lo = mid;
-      else hi = mid;
+  const float W = kRange / kBins;  // coarse bin width
+  float tau = -kRange;             // keep z >= tau
+  const bool need_k = top_k > 0 && top_k < V, need_p = top_p < 1.f;
+  if (need_k || need_p) {
+    // 2. coarse histogram over [-64, 0]
+    histogram(row, V, gmax, inv_temp, -kRange, kRange, -INFINITY, hc, hm);
+    suffix_scan(hc, hm, tc, tm);
+    float total = hm[0];
+    int kbin = 0;
+    int above_c = 0;
+    float above_m = 0.f;
+    if (need_k) {
+      kbin = find_bin_count(hc, top_k, &sel);
+      above_c = kbin + 1 < kBins ? hc[kbin + 1] : 0;
+      above_m = kbin + 1 < kBins ? hm[kbin + 1] : 0.f;
     }
-    tau_lo = lo;
-  }
-  // 3. top-p threshold on the renormalised top-k mass
-  float tau = tau_lo;
-  if (top_p < 1.f) {
-    float z_tot = 0.f;
-    for (int v = tid; v < V; v += kSampNT) {
-      const float z = (ld(row, v) - gmax) * inv_temp;
-      z_tot += z >= tau_lo ? __expf(z) : 0.f;
-    }
-    z_tot = bsum(z_tot, sc);
-    const float target = top_p * z_tot;
-    float lo = fmaxf(tau_lo, -80.f), hi = 0.f;  // mass(z >= hi=0) >= exp(0) > 0
-    for (int it = 0; it < 24; ++it) {
-      const float mid = 0.5f * (lo + hi);
-      float s = 0.f;
-      for (int v = tid; v < V; v += kSampNT) {
-        const float z = (ld(row, v) - gmax) * inv_temp;
-        s += z >= mid ? __expf(z) : 0.f;
+    // coarse suffix masses must survive the fine pass: stash the one needed later
+    float pbin_need = 0.f;
+    int pbin = 0;
+    if (need_k) {
+      // 3. refine the top-k threshold inside bin kbin
+      const float lo = -kRange + kbin * W;
+      __syncthreads();
+      // keep the coarse suffix mass of bins >= kbin+1 for the top-p search below
+      histogram(row, V, gmax, inv_temp, lo, W, -INFINITY, hc, hm);
+      suffix_scan(hc, hm, tc, tm);
+      const int sb = find_bin_count(hc, top_k - above_c, &sel);
+      tau = lo + sb * (W / kBins);
+      total = above_m + hm[sb];
+      if (need_p) {
+        const float target = top_p * total;
+        if (above_m < target) {  // the nucleus edge lies inside this same coarse bin
+          const int sp = find_bin_mass(hm, target - above_m, &sel);
+          tau = fmaxf(tau, lo + sp * (W / kBins));
+          pbin = -1;  // done
+        } else {
+          pbin = 1;  // edge is in a higher coarse bin: needs the coarse suffix again
+          pbin_need = target;
+        }
       }
-      s = bsum(s, sc);
-      if (s >= target) lo = mid;
-      else hi = mid;
+    } else {
+      pbin = 1;
+      pbin_need = top_p * total;
     }
-    tau = fmaxf(tau_lo, lo);
+    if (need_p && pbin == 1) {
+      // coarse pass restricted to z >= tau (the top-k floor), then refine
+      __syncthreads();
+      histogram(row, V, gmax, inv_temp, -kRange, kRange, tau, hc, hm);
+      suffix_scan(hc, hm, tc, tm);
+      const int cb = find_bin_mass(hm, pbin_need, &sel);
+      const float above = cb + 1 < kBins ? hm[cb + 1] : 0.f;
+      const float lo = -kRange + cb * W;
+      __syncthreads();
+      histogram(row, V, gmax, inv_temp, lo, W, tau, hc, hm);
+      suffix_scan(hc, hm, tc, tm);
+      const int sp = find_bin_mass(hm, pbin_need - above, &sel);
+      tau = fmaxf(tau, lo + sp * (W / kBins));
+    }
   }
   // 4. categorical draw over {z >= tau}: contiguous segment per thread, block scan
   const int per = (V + kSampNT - 1) / kSampNT;
@@ -137,20 +232,19 @@ __global__ __launch_bounds__(kSampNT) void sample_kernel(const T* __restrict__ l
     const float z = (ld(row, v) - gmax) * inv_temp;
     mine += z >= tau ? __expf(z) : 0.f;
   }
-  seg[tid] = mine;
+  tm[tid] = mine;
   if (tid == 0) ans = -1;
   __syncthreads();
-  // inclusive scan (Hillis-Steele) over 1024 partial masses
   for (int o = 1; o < kSampNT; o <<= 1) {
-    const float add = tid >= o ? seg[tid - o] : 0.f;
+    const float add = tid >= o ? tm[tid - o] : 0.f;
     __syncthreads();
-    seg[tid] += add;
+    tm[tid] += add;
     __syncthreads();
   }
-  const float total = seg[kSampNT - 1];
+  const float total = tm[kSampNT - 1];
   const float u = philox_uniform((uint64_t)rng[0], (uint64_t)r, (uint64_t)rng[1]) * total;
-  const float before = tid > 0 ? seg[tid - 1] : 0.f;
-  if (mine > 0.f && u >= before && u < seg[tid]) {
+  const float before = tid > 0 ? tm[tid - 1] : 0.f;
+  if (mine > 0.f && u >= before && u < tm[tid]) {
     float acc = before;
     int pick = -1;
     for (int v = s0; v < s1; ++v) {
@@ -164,14 +258,7 @@ __global__ __launch_bounds__(kSampNT) void sample_kernel(const T* __restrict__ l
     ans = pick;
   }
   __syncthreads();
-  if (tid == 0) {
-    int a = ans;
-    if (a < 0) {  // u landed on a rounding gap at the very top: take the argmax
-      a = amin[0];
-      for (int i = 1; i < kSampNT / 64; ++i) a = min(a, amin[i]);
-    }
-    out[r] = a;
-  }
+  if (tid == 0) out[r] = ans >= 0 ? ans : argmax;  // u on a rounding gap at the top: argmax
 }
 
 void launch_sample(const void* logits, bool is_bf16, int64_t ld_, int64_t rows, int V,

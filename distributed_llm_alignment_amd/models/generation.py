@@ -60,15 +60,24 @@ class KVCache:
         B, T, _ = qkv.shape
         if self.len + T > self.max_len:
             raise RuntimeError("KV cache overflow")
+        if T == 1 and self.len > 0 and self.fast_decode:
+            # device-indexed cache write + split-KV decode kernel (graph-capturable)
+            D = cfg.head_dim
+            if rope is not None and rope.rot_dim % 16 == 0:
+                cos, sin = rope.tables(qkv.device)
+                q = ops._ext.require().rope_cache_write(qkv, cos, sin, self.pos.view(-1), self.k[layer],
+                                                        self.v[layer], self.slot, self.h_local,
+                                                        self.kv_local, D, rope.rot_dim)
+            else:
+                q, k, v = ops.attention.rope_qk(qkv, rope, self.h_local, self.kv_local, D,
+                                                positions=self._pos)
+                self.k[layer].index_copy_(1, self.slot, k)
+                self.v[layer].index_copy_(1, self.slot, v)
+            o = ops.decode.decode_attention(q.reshape(B, self.h_local, D), self.k[layer],
+                                            self.v[layer], self.kv_len, self.kv_start, window)
+            return o.reshape(B, 1, self.h_local * D)
         q, k, v = ops.attention.rope_qk(qkv, rope, self.h_local, self.kv_local, cfg.head_dim,
                                         positions=self._pos)
-        if T == 1 and self.len > 0 and self.fast_decode:
-            # device-indexed write + split-KV decode kernel (graph-capturable)
-            self.k[layer].index_copy_(1, self.slot, k)
-            self.v[layer].index_copy_(1, self.slot, v)
-            o = ops.decode.decode_attention(q.reshape(B, self.h_local, cfg.head_dim), self.k[layer],
-                                            self.v[layer], self.kv_len, self.kv_start, window)
-            return o.reshape(B, 1, self.h_local * cfg.head_dim)
         self.k[layer, :, self.len:self.len + T] = k
         self.v[layer, :, self.len:self.len + T] = v
         end = self.len + T
