@@ -21,7 +21,9 @@ def get_distributed_sampler(dataset, shuffle: bool = True, seed: int = 0, drop_l
     st = dist_state()
     mesh = current_mesh()
     n, r = (mesh.dp, mesh.dp_rank) if mesh is not None else (st.world_size, st.rank)
-    if n > 1:
+    if n > 1 or shuffle:
+        # also for one replica: the epoch-seeded permutation makes a resumed run see exactly
+        # the batches the interrupted run would have (set_epoch + skip in train_loop)
         return DistributedSampler(dataset, num_replicas=n, rank=r, shuffle=shuffle,
                                   seed=seed, drop_last=drop_last)
     return None

@@ -52,6 +52,10 @@ def init_distributed(backend: Optional[str] = None, timeout_s: int = 1800,
     else:
         dev = torch.device("cpu")
     be = backend or ("nccl" if use_gpu else "gloo")
+    # a hung / failed collective raises (with the op and group in the message) instead of
+    # blocking the job forever; DLA_COLLECTIVE_TIMEOUT_S overrides the timeout
+    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+    timeout_s = int(os.environ.get("DLA_COLLECTIVE_TIMEOUT_S", timeout_s))
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29500")

@@ -16,6 +16,7 @@ from __future__ import annotations
 import contextlib
 import os
 import random
+import time
 from dataclasses import dataclass, field
 from pathlib import Path
 from typing import Any, Callable, Dict, Iterable, List, Optional, Tuple
@@ -28,7 +29,9 @@ from ..parallel.data_parallel import DataParallelEngine
 from ..parallel.dist import DistState, init_distributed
 from ..utils.checkpoint import load_state, resolve_checkpoint, save_state
 from ..utils.config import hardware_parallel
+from ..utils.debug import FaultInjector, check_replicas_in_sync
 from ..utils.logging import MetricsLogger, RunningLoss, log_rank_zero
+from ..utils.tracing import PHASES, ProfileWindow, trace_range
 
 
 def seed_everything(seed: int) -> None:
@@ -66,7 +69,8 @@ class TrainContext:
 
 
 def setup(cfg: Dict[str, Any], stage: str, default_seed: int = 0) -> TrainContext:
-    st = init_distributed()
+    hw_cfg = cfg.get("hardware", {}) or {}
+    st = init_distributed(timeout_s=int(hw_cfg.get("collective_timeout_s", 1800)))
     if st.device.type == "cuda":
         from ..utils.tuning import enable_gemm_tuning
 
@@ -154,6 +158,21 @@ def move_to(batch, device):
     return batch
 
 
+def _batch_rows(batch) -> int:
+    """Samples in a micro-batch: pairs for preference batches, rows otherwise."""
+    if isinstance(batch, torch.Tensor):
+        return int(batch.shape[0]) if batch.dim() else 1
+    if isinstance(batch, dict):
+        for k in ("chosen", "input_ids"):
+            if k in batch:
+                return _batch_rows(batch[k])
+        for v in batch.values():
+            return _batch_rows(v)
+    if isinstance(batch, (list, tuple)) and batch:
+        return _batch_rows(batch[0])
+    return 0
+
+
 StepFn = Callable[[Any], Tuple[torch.Tensor, Dict[str, Any]]]
 
 
@@ -170,25 +189,46 @@ def train_loop(ctx: TrainContext, loader, sampler, engine: DataParallelEngine, s
         if path is not None:
             global_step = load_state(path, models_to_save[:1], engine, scheduler)
             ctx.log(f"Resumed from {path} at step {global_step}")
+    lg = ctx.cfg.get("logging", {}) or {}
+    dbg = ctx.cfg.get("debug", {}) or {}
+    prof = ProfileWindow(lg.get("profile_steps"), lg.get("profile_dir", str(Path(ctx.log_dir) / "profile")),
+                         enabled=ctx.is_main or bool(lg.get("profile_all_ranks", False)))
+    faults = FaultInjector(dbg.get("fault_at_step"), dbg.get("fault_rank"))
+    sync_every = int(dbg.get("check_sync_every", 0) or 0)
+    dp_group = ctx.mesh.dp_group if ctx.mesh is not None else None
     running = RunningLoss()
     last_metrics: Dict[str, Any] = {}
     done = global_step >= total_steps
-    epoch = 0
+    n_batches = len(loader)
+    if n_batches == 0:
+        raise RuntimeError("empty training dataset")
+    # resume at the exact data position: epoch-seeded sampler order, skip consumed batches
+    epoch, skip = divmod(global_step, n_batches)
+    t_log, rows_log = time.perf_counter(), 0
     while not done:
         if sampler is not None:
             sampler.set_epoch(epoch)
-        n_batches = len(loader)
         for bi, batch in enumerate(loader):
-            batch = move_to(batch, ctx.device)
+            if skip:
+                skip -= 1
+                continue
+            prof.step(global_step + 1)
+            faults.maybe_fail(global_step + 1, ctx.dist.rank)
+            with trace_range("data"):
+                batch = move_to(batch, ctx.device)
+            rows_log += _batch_rows(batch)
             micro_idx = global_step % accum
             sync = (micro_idx == accum - 1) or (bi == n_batches - 1)
             ctx_mgr = contextlib.nullcontext() if sync else engine.no_sync()
-            with ctx_mgr:
+            with ctx_mgr, trace_range("fwd_bwd"):
                 loss, metrics = step_fn(batch)
                 (loss / accum).backward()
             if sync:
-                lr = scheduler.lr(global_step) if scheduler is not None else None
-                engine.step(lr)
+                with trace_range("optim"):
+                    lr = scheduler.lr(global_step) if scheduler is not None else None
+                    engine.step(lr)
+                if sync_every and (global_step + 1) // accum % sync_every == 0:
+                    check_replicas_in_sync(models_to_save[0], dp_group)
             if scheduler is not None:
                 scheduler.step()
             running.update(loss.detach())
@@ -200,18 +240,26 @@ def train_loop(ctx: TrainContext, loader, sampler, engine: DataParallelEngine, s
                     rec["train/lr"] = scheduler.lr(global_step)
                 if extra_log_fn is not None:
                     rec.update(extra_log_fn(global_step, metrics))
+                dt = time.perf_counter() - t_log
+                rec["perf/samples_per_s"] = rows_log * ctx.dp_size / max(dt, 1e-9)
+                rec["perf/step_s"] = dt / log_every
+                if torch.cuda.is_available():
+                    rec["perf/max_mem_gb"] = torch.cuda.max_memory_allocated() / 2 ** 30
+                rec.update(PHASES.pop())
                 ctx.logger.log(rec, global_step)
                 running = RunningLoss()
+                t_log, rows_log = time.perf_counter(), 0
             if eval_fn is not None and eval_every and global_step % eval_every == 0:
-                ctx.logger.log(eval_fn(global_step), global_step)
+                with trace_range("eval"):
+                    ctx.logger.log(eval_fn(global_step), global_step)
             if save_every and global_step % save_every == 0:
-                save_state(Path(ctx.output_dir) / f"step_{global_step}", models_to_save, engine,
-                           scheduler, global_step, tokenizer, keep_last=keep_last)
+                with trace_range("save"):
+                    save_state(Path(ctx.output_dir) / f"step_{global_step}", models_to_save, engine,
+                               scheduler, global_step, tokenizer, keep_last=keep_last)
             if global_step >= total_steps:
                 done = True
                 break
         epoch += 1
-        if n_batches == 0:
-            raise RuntimeError("empty training dataset")
+    prof.close()
     save_state(Path(ctx.output_dir) / "final", models_to_save, engine, scheduler, global_step, tokenizer)
     return global_step

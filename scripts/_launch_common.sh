@@ -5,6 +5,9 @@ set -euo pipefail
 export TOKENIZERS_PARALLELISM=false
 export HSA_ENABLE_IPC_MODE_LEGACY=0          # dmabuf IPC for RCCL peer buffers
 export NCCL_MIN_NCHANNELS=${NCCL_MIN_NCHANNELS:-16}   # keep all 7 xGMI links busy
+if [ "${DLA_DEBUG:-0}" = "1" ]; then   # serialised HIP + loud RCCL errors
+  export AMD_SERIALIZE_KERNEL=3 HIP_LAUNCH_BLOCKING=1 TORCH_NCCL_ASYNC_ERROR_HANDLING=1 NCCL_DEBUG=WARN
+fi
 REPO="$(cd "$(dirname "${BASH_SOURCE[0]}")/.." && pwd)"
 export PYTHONPATH="$REPO${PYTHONPATH:+:$PYTHONPATH}"
 if [ -z "${NPROC:-}" ]; then

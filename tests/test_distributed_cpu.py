@@ -494,3 +494,26 @@ def test_expert_parallel_world4_edp2():
     b = run_ranks(_ep_step, 4, (2, 1))
     for r in range(4):
         assert a[r] == pytest.approx(b[r], rel=1e-4, abs=1e-6), (a[r], b[r])
+
+
+def _replica_check(rank, world):
+    import torch
+
+    from distributed_llm_alignment_amd.models import build_model, get_config
+    from distributed_llm_alignment_amd.utils.debug import check_replicas_in_sync
+
+    m = build_model(get_config("tiny-llama"), device="cpu", seed=0)
+    check_replicas_in_sync(m)  # identical seeded init: in sync
+    if rank == 1:
+        with torch.no_grad():
+            m.layers[0].ln1_w[3] += 1e-3
+    try:
+        check_replicas_in_sync(m)
+        return "missed"
+    except RuntimeError as e:
+        return "caught" if "diverged" in str(e) else str(e)
+
+
+def test_replica_divergence_detector():
+    res = run_ranks(_replica_check, 2)
+    assert res[0] == "caught" and res[1] == "caught"

@@ -166,3 +166,52 @@ def test_gpt2_cpu_plumbing_config(tmp_path, monkeypatch):
     m = _metrics(tmp_path / "logs" / "sft_gpt2_cpu")
     assert len(m) == 2 and all(r["train/loss"] == r["train/loss"] for r in m)
     assert (tmp_path / "checkpoints" / "sft_gpt2_cpu" / "final" / "model.safetensors").exists()
+
+
+def test_fault_injection_and_resume_reproduces_trajectory(tmp_path, monkeypatch):
+    """kill the run at step 5 (after the step-4 checkpoint), restart with --resume
+    from `latest`, and the losses of steps 5..8 equal an uninterrupted run's."""
+    from distributed_llm_alignment_amd.training import train_sft
+    from distributed_llm_alignment_amd.utils.debug import FaultInjected
+
+    d = tmp_path
+    write_jsonl(d / "sft.jsonl", synthetic_instruction_records(32, seed=1))
+
+    def cfg(name, out):
+        body = {"seed": 5, "model": {"model_name_or_path": "tiny-llama", "max_seq_length": 160,
+                                     "gradient_checkpointing": False},
+                "data": {"source": "local", "train_path": str(d / "sft.jsonl"), "num_workers": 0},
+                "optimization": {"micro_batch_size": 2, "learning_rate": 3e-3, "max_train_steps": 8,
+                                 "warmup_steps": 2, "lr_scheduler": "cosine"},
+                "logging": {"output_dir": str(d / out), "log_dir": str(d / f"logs_{out}"),
+                            "log_every_steps": 1, "save_every_steps": 4},
+                "debug": {"check_sync_every": 1}}
+        return _cfg(d, name, body)
+
+    assert train_sft.main(["--config", cfg("a", "full")]) == 0
+    ref = {r["step"]: r["train/loss"] for r in _metrics(d / "logs_full") if "train/loss" in r}
+    monkeypatch.setenv("DLA_FAULT_STEP", "5")
+    with pytest.raises(FaultInjected):
+        train_sft.main(["--config", cfg("b", "crash")])
+    monkeypatch.delenv("DLA_FAULT_STEP")
+    assert train_sft.main(["--config", cfg("b", "crash"), "--resume", str(d / "crash" / "latest")]) == 0
+    got = {r["step"]: r["train/loss"] for r in _metrics(d / "logs_crash") if "train/loss" in r}
+    for s in range(5, 9):
+        assert got[s] == pytest.approx(ref[s], rel=1e-5, abs=1e-6), (s, got[s], ref[s])
+    rec = [r for r in _metrics(d / "logs_full") if "perf/samples_per_s" in r]
+    assert rec and "time/fwd_bwd_s" in rec[-1]
+
+
+def test_tracing_and_profile_window(tmp_path):
+    from distributed_llm_alignment_amd.utils.tracing import PHASES, ProfileWindow, trace_range
+
+    with trace_range("unit"):
+        sum(range(1000))
+    assert "time/unit_s" in PHASES.pop()
+    pw = ProfileWindow([1, 2], str(tmp_path / "prof"))
+    pw.step(1)
+    import torch
+
+    torch.ones(4).sum()
+    pw.step(2)
+    assert (tmp_path / "prof" / "trace.json").exists() and (tmp_path / "prof" / "kernels.txt").exists()
