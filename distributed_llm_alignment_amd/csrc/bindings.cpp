@@ -60,6 +60,7 @@ void launch_attn_bwd_delta(const bf16_t*, const bf16_t*, int64_t, int64_t, int64
                            int64_t, int64_t, int, int, int, int, float*, hipStream_t);
 void launch_attn_bwd(const AttnBwdParams&, int, bool, hipStream_t);
 void launch_f32_to_bf16_rows(const float*, int64_t, int, bf16_t*, int64_t, hipStream_t);
+void launch_transpose_bf16(const bf16_t*, int64_t, int64_t, int64_t, bf16_t*, int64_t, hipStream_t);
 
 // ================================= norms ======================================================
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> norm_fwd(
@@ -375,6 +376,22 @@ void f32_to_bf16_rows(const at::Tensor& src, at::Tensor& dst) {
                           bp(dst), dst.stride(0), cur_stream(src));
 }
 
+// out [C, R] <- in [R, C]^T (both row-major with unit column stride, 16-byte aligned rows)
+void transpose_bf16(const at::Tensor& in, at::Tensor& out) {
+  check_bf16(in, "in");
+  check_bf16(out, "out");
+  TORCH_CHECK(in.dim() == 2 && out.dim() == 2 && in.stride(1) == 1 && out.stride(1) == 1 &&
+                  out.size(0) == in.size(1) && out.size(1) == in.size(0),
+              "transpose_bf16: in [R, C], out [C, R], unit column stride");
+  TORCH_CHECK(in.stride(0) % 8 == 0 && out.stride(0) % 8 == 0, "16-byte aligned rows");
+  check_aligned16(in, "in");
+  check_aligned16(out, "out");
+  same_device(in, out);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(in.device());
+  launch_transpose_bf16(cbp(in), in.size(0), in.size(1), in.stride(0), bp(out), out.stride(0),
+                        cur_stream(in));
+}
+
 // ================================= vocab reductions ===========================================
 static void check_logits(const at::Tensor& logits) {
   check_bf16(logits, "logits");
@@ -621,6 +638,7 @@ TORCH_LIBRARY(dla, m) {
   m.def("attn_fwd(Tensor q, Tensor k, Tensor v, float scale, bool causal, int causal_off, int window, Tensor? kv_start, Tensor? kv_end) -> (Tensor, Tensor)");
   m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse2, Tensor(a!) dk, Tensor(b!) dv, float scale, bool causal, int causal_off, int window, Tensor? kv_start, Tensor? kv_end) -> Tensor");
   m.def("f32_to_bf16_rows(Tensor src, Tensor(a!) dst) -> ()");
+  m.def("transpose_bf16(Tensor input, Tensor(a!) out) -> ()");
   m.def("logprob_fwd(Tensor logits, Tensor targets, int vocab_offset=0) -> (Tensor, Tensor)");
   m.def("logprob_bwd(Tensor(a!) logits, Tensor targets, Tensor lse, Tensor grad, int vocab_offset=0) -> ()");
   m.def("row_lse(Tensor logits) -> Tensor");
@@ -647,6 +665,7 @@ TORCH_LIBRARY_IMPL(dla, CUDA, m) {
   m.impl("attn_fwd", &dla::attn_fwd);
   m.impl("attn_bwd", &dla::attn_bwd);
   m.impl("f32_to_bf16_rows", &dla::f32_to_bf16_rows);
+  m.impl("transpose_bf16", &dla::transpose_bf16);
   m.impl("logprob_fwd", &dla::logprob_fwd);
   m.impl("logprob_bwd", &dla::logprob_bwd);
   m.impl("row_lse", &dla::row_lse);

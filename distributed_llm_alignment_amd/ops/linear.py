@@ -10,8 +10,66 @@ temporary, one rounding — and notifies the engine's bucket scheduler itself.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
+
+from . import _ext
+
+# dX = dY @ W in the NN layout runs at 1.22-1.36 PF/s on gfx950 for Llama-3-8B shapes, the TN
+# layout of the forward at 1.43-1.52 (tools/gemm_layout_probe.py, MI355X). The engine marks its
+# 2-D weights `_dla_wt_ok`; the backward then keeps a transposed copy W^T (HIP tiled transpose,
+# refreshed lazily when the weight's version counter or the engine's weight epoch moved, i.e.
+# once per optimizer step) and
+# computes dX = linear(dY, W^T). 16 GB of HBM for an 8B policy buys ~8 % of the step.
+TRANSPOSED_DGRAD = os.environ.get("DLA_TRANSPOSED_DGRAD", "1") != "0"
+
+
+def transposed_weight(weight: torch.Tensor) -> torch.Tensor:
+    wt = getattr(weight, "_dla_wt", None)
+    ep = getattr(weight, "_dla_epoch", None)
+    key = (weight._version, ep[0] if ep is not None else 0)
+    if wt is None or getattr(weight, "_dla_wt_ver", None) != key:
+        with torch.no_grad():
+            if wt is None:
+                wt = torch.empty((weight.shape[1], weight.shape[0]), dtype=weight.dtype, device=weight.device)
+            _ext.require().transpose_bf16(weight.detach(), wt)
+        weight._dla_wt = wt
+        weight._dla_wt_ver = key
+    return wt
+
+
+def input_grad(dy2: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    """dX = dy2 @ weight ([M, N] x [N, K]); TN layout through the cached W^T when enabled."""
+    if (TRANSPOSED_DGRAD and getattr(weight, "_dla_wt_ok", False) and weight.dtype == torch.bfloat16
+            and _ext.use_native(weight) and weight.shape[0] % 8 == 0 and weight.shape[1] % 8 == 0):
+        return F.linear(dy2, transposed_weight(weight))
+    return dy2 @ weight
+
+
+# Weight gradient dW += dY^T X reduces over the token dim, which is the slow dim of both
+# operands (NT layout). For the large FFN weights it is faster to transpose both activations
+# with the HIP tiled transpose and run the TN GEMM: Llama-3-8B up 1.66 -> 1.22 + 0.24 ms,
+# down 0.95 -> 0.68 + 0.14 ms; no gain for qkv / o (tools/_probe_dw_tn.py, MI355X).
+TN_WGRAD = os.environ.get("DLA_TN_WGRAD", "1") != "0"
+TN_WGRAD_MIN_ELEMS = int(os.environ.get("DLA_TN_WGRAD_MIN", str(48 * 1024 * 1024)))
+
+
+def _wgrad_accumulate(mg: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor) -> None:
+    N, K = mg.shape
+    if (TN_WGRAD and N * K >= TN_WGRAD_MIN_ELEMS and mg.dtype == torch.bfloat16 and _ext.use_native(mg)
+            and dy2.is_contiguous() and x2.is_contiguous() and dy2.shape[0] % 8 == 0
+            and N % 8 == 0 and K % 8 == 0):
+        M = dy2.shape[0]
+        tr = _ext.require().transpose_bf16
+        dyt = torch.empty((N, M), dtype=dy2.dtype, device=dy2.device)
+        xt = torch.empty((K, M), dtype=x2.dtype, device=x2.device)
+        tr(dy2, dyt)
+        tr(x2, xt)
+        mg.addmm_(dyt, xt.t())
+        return
+    mg.addmm_(dy2.t(), x2)
 
 
 def accumulate_weight_grad(weight: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor) -> bool:
@@ -19,7 +77,7 @@ def accumulate_weight_grad(weight: torch.Tensor, dy2: torch.Tensor, x2: torch.Te
     mg = getattr(weight, "main_grad", None)
     if mg is None or getattr(weight, "_dla_shared", False):
         return False
-    mg.addmm_(dy2.t(), x2)
+    _wgrad_accumulate(mg, dy2, x2)
     hook = getattr(weight, "_dla_grad_hook", None)
     if hook is not None:
         hook(weight)
@@ -38,7 +96,7 @@ class _LinearMainGradFn(torch.autograd.Function):
         x, weight = ctx.saved_tensors
         K, N = x.shape[-1], dy.shape[-1]
         dy2 = dy.reshape(-1, N)
-        dx = (dy2 @ weight).view(x.shape) if ctx.needs_input_grad[0] else None
+        dx = input_grad(dy2, weight).view(x.shape) if ctx.needs_input_grad[0] else None
         dw = None
         if ctx.needs_input_grad[1]:
             x2 = x.reshape(-1, K)

@@ -22,6 +22,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _ext
+from .linear import input_grad
 
 _NO_GRAD_CHUNK = 4096
 
@@ -59,7 +60,7 @@ class _LinearLogprobFn(torch.autograd.Function):
         hidden, weight, targets, lse, logits = ctx.saved_tensors
         ops.logprob_bwd(logits, targets, lse, g.float().contiguous())
         dlogits = logits  # rewritten in place
-        dh = dlogits @ weight if ctx.needs_input_grad[0] else None
+        dh = input_grad(dlogits, weight) if ctx.needs_input_grad[0] else None
         dw = None
         if ctx.needs_input_grad[1]:
             from .linear import accumulate_weight_grad

@@ -139,6 +139,9 @@ class DataParallelEngine:
         self.param_buf = torch.zeros(self.numel, dtype=self.dtype, device=self.device)
         self.grad_buf = torch.zeros(self.numel, dtype=self.dtype, device=self.device)
         self.params = params
+        # weights change in place inside the flat buffer (fused AdamW, all-gathers): the
+        # per-parameter _version does not move, so caches key on this shared epoch too
+        self._wt_epoch = [0]
         with torch.no_grad():
             for p in params:
                 o = offsets[id(p)]
@@ -149,6 +152,9 @@ class DataParallelEngine:
                 # ops.linear / linear_logprob accumulate weight grads here inside the GEMM
                 p.main_grad = p.grad
                 p._dla_grad_hook = self._on_grad
+                # persistent W^T for the TN-layout input-gradient GEMM (ops.linear.input_grad)
+                p._dla_wt_ok = p.dim() == 2 and not getattr(p, "_dla_shared", False)
+                p._dla_epoch = self._wt_epoch
         self._offsets = offsets
         # ---- shard layout
         shard = 0
@@ -302,6 +308,7 @@ class DataParallelEngine:
                     dist.all_gather_into_tensor(self.param_buf[b.start:b.end],
                                                 self.param_shard[b.shard_off:b.shard_off + c],
                                                 group=b.group)
+        self._wt_epoch[0] += 1  # invalidates weight-derived caches (ops.linear W^T)
         self.zero_grad()
         return self.last_grad_norm
 
@@ -312,6 +319,7 @@ class DataParallelEngine:
 
     @torch.no_grad()
     def broadcast_params(self, src: int = 0):
+        self._wt_epoch[0] += 1
         if self.world > 1:
             for b in self.buckets:
                 if b.world > 1:
@@ -324,6 +332,7 @@ class DataParallelEngine:
 
     @torch.no_grad()
     def sync_master_from_params(self):
+        self._wt_epoch[0] += 1
         if self.zero:
             self.param_shard.copy_(torch.cat([self._chunk(self.param_buf, b) for b in self.buckets]))
         if self.master is not None:

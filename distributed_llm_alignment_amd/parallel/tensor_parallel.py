@@ -132,7 +132,9 @@ class _VPLogprobFn(torch.autograd.Function):
         dlog = _local_bwd(logits_l, targets, lse, g, ctx.off)
         dh = None
         if ctx.needs_input_grad[0]:
-            dh = (dlog @ weight_l).contiguous()
+            from ..ops.linear import input_grad
+
+            dh = input_grad(dlog, weight_l).contiguous()
             dist.all_reduce(dh, group=ctx.group)
         dw = None
         if ctx.needs_input_grad[1]:

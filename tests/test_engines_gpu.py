@@ -46,3 +46,29 @@ def test_fsdp_engine_matches_flat_engine_gpu(ckpt):
     a = _run("dp", ckpt)
     b = _run("fsdp", ckpt)
     assert a == pytest.approx(b, rel=2e-2, abs=1e-3), (a, b)
+
+
+@pytest.mark.parametrize("R,C", [(4096, 6144), (1000, 136), (64, 8)])
+def test_transpose_kernel(R, C):
+    from distributed_llm_alignment_amd.ops import _ext
+
+    x = torch.randn(R, C, device="cuda", dtype=torch.bfloat16)
+    out = torch.empty(C, R, device="cuda", dtype=torch.bfloat16)
+    _ext.require().transpose_bf16(x, out)
+    assert torch.equal(out, x.t())
+
+
+def test_transposed_dgrad_matches_nn_dgrad():
+    """The engine's persistent-W^T input-gradient path and the transposed-activation TN weight
+    gradient give the same steps as plain dY @ W / dY^T X, including the lazy W^T refresh after
+    the optimizer updated W."""
+    from distributed_llm_alignment_amd.ops import linear as lin
+
+    try:
+        lin.TRANSPOSED_DGRAD, lin.TN_WGRAD, lin.TN_WGRAD_MIN_ELEMS = True, True, 0
+        a = _run("dp", False)
+        lin.TRANSPOSED_DGRAD, lin.TN_WGRAD = False, False
+        b = _run("dp", False)
+    finally:
+        lin.TRANSPOSED_DGRAD, lin.TN_WGRAD, lin.TN_WGRAD_MIN_ELEMS = True, True, 48 * 1024 * 1024
+    assert a == pytest.approx(b, rel=1e-2, abs=1e-3), (a, b)
