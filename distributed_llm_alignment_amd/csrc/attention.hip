@@ -41,6 +41,12 @@ __device__ __forceinline__ int swz(int row, int ch) {
   return row * D + ((ch ^ f) << 3);
 }
 
+// dS^T image [128 keys][32 queries] bf16 (64-B rows): 8-byte unit c4 of row `row`, XOR-swizzled
+// with row bits 2..4 so the 32 key rows written by a half-wave land on 32 distinct bank pairs
+// (unswizzled: 16-bank row stride -> 8-way conflicts; the swizzle is a per-row permutation, so
+// the ds_read_b64_tr_b16 reads of the dQ MFMA stay conflict-free).
+__device__ __forceinline__ int ds_off(int row, int c4) { return row * 32 + ((c4 ^ ((row >> 2) & 7)) << 2); }
+
 __device__ __forceinline__ s16x4 tr_read(const bf16_t* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
 }
@@ -294,20 +300,25 @@ __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(const bf16_t* __res
                                                               int64_t do_st, int64_t do_sh,
                                                               int B, int H, int T, int D,
                                                               float* __restrict__ delta) {
-  const int64_t row = blockIdx.x * 4ll + (threadIdx.x >> 6);
+  // delta[row] = <O[row], dO[row]>: D/8 lanes x 16-B loads per row (16 lanes at D = 128),
+  // 64 / (D/8) rows per wave, shuffle reduction inside the lane group
+  const int lpr = D >> 3;  // lanes per row (power of two: 8 or 16)
   const int lane = threadIdx.x & 63;
-  if (row >= static_cast<int64_t>(B) * H * T) return;
-  const int t = static_cast<int>(row % T);
-  const int64_t bh = row / T;
-  const int hh = static_cast<int>(bh % H), b = static_cast<int>(bh / H);
-  const bf16_t* op = o + b * o_sb + t * o_st + hh * o_sh;
-  const bf16_t* dp = dout + b * do_sb + t * do_st + hh * do_sh;
+  const int64_t row = (blockIdx.x * 4ll + (threadIdx.x >> 6)) * (64 / lpr) + lane / lpr;
+  const int c = (lane % lpr) * 8;
   float acc = 0.f;
-  for (int d = lane * 2; d < D; d += 128) {
-    acc += bf2f(op[d]) * bf2f(dp[d]) + bf2f(op[d + 1]) * bf2f(dp[d + 1]);
+  const bool ok = row < static_cast<int64_t>(B) * H * T;
+  if (ok) {
+    const int t = static_cast<int>(row % T);
+    const int64_t bh = row / T;
+    const int hh = static_cast<int>(bh % H), b = static_cast<int>(bh / H);
+    const bf16x8 a = load_bf16x8(o + b * o_sb + t * o_st + hh * o_sh + c);
+    const bf16x8 g = load_bf16x8(dout + b * do_sb + t * do_st + hh * do_sh + c);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += bf2f(a[j]) * bf2f(g[j]);
   }
-  acc = wave_sum(acc);
-  if (lane == 0) delta[row] = acc;
+  for (int off = 1; off < lpr; off <<= 1) acc += __shfl_xor(acc, off, 64);
+  if (ok && (lane % lpr) == 0) delta[row] = acc;
 }
 
 // ==============================================================================================
@@ -431,43 +442,74 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnBwdParams p) {
     }
     f32x16 sacc = f32x16{}, dpacc = f32x16{};
     if (wave_active) {
-      // S (rows = queries, cols = this wave's keys) and dP = dO V^T
+      // row constants of this lane's 16 accumulator rows r = (i&3) + 8(i>>2) + 4h: 4 x 16-B LDS
+      // reads each for lse2 / delta, issued ahead of the MFMA chain so their latency hides
+      float lr[16], dl[16];
 #pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        const s16x8 aq = *reinterpret_cast<const s16x8*>(Qs + swz<D>(l32, 2 * s + h));
-        const s16x8 bk = *reinterpret_cast<const s16x8*>(Ks + swz<D>(32 * w + l32, 2 * s + h));
-        sacc = mfma32(aq, bk, sacc);
-        const s16x8 ad = *reinterpret_cast<const s16x8*>(dOs + swz<D>(l32, 2 * s + h));
-        const s16x8 bv = *reinterpret_cast<const s16x8*>(Vs + swz<D>(32 * w + l32, 2 * s + h));
-        dpacc = mfma32(ad, bv, dpacc);
+      for (int j = 0; j < 4; ++j) {
+        const f32x4 a = *reinterpret_cast<const f32x4*>(&rowc[0][8 * j + 4 * h]);
+        const f32x4 c = *reinterpret_cast<const f32x4*>(&rowc[1][8 * j + 4 * h]);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          lr[4 * j + t] = a[t];
+          dl[4 * j + t] = c[t];
+        }
       }
-      // P and dS (rows i -> query qt + (i&3) + 8(i>>2) + 4h, column -> key kj)
+      // S (rows = queries, cols = this wave's keys) and dP = dO V^T; operand fragments are
+      // double-buffered one k-step ahead so no MFMA waits on its own LDS read
+      s16x8 fa[2], fb[2], fc[2], fd[2];
+      auto ld_sdp = [&](int ks, int sl) {
+        fa[sl] = *reinterpret_cast<const s16x8*>(Qs + swz<D>(l32, 2 * ks + h));
+        fb[sl] = *reinterpret_cast<const s16x8*>(Ks + swz<D>(32 * w + l32, 2 * ks + h));
+        fc[sl] = *reinterpret_cast<const s16x8*>(dOs + swz<D>(l32, 2 * ks + h));
+        fd[sl] = *reinterpret_cast<const s16x8*>(Vs + swz<D>(32 * w + l32, 2 * ks + h));
+      };
+      ld_sdp(0, 0);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        if (ks + 1 < KS) ld_sdp(ks + 1, (ks + 1) & 1);
+        sacc = mfma32(fa[ks & 1], fb[ks & 1], sacc);
+        dpacc = mfma32(fc[ks & 1], fd[ks & 1], dpacc);
+      }
+      // P and dS; masking is branch-free: per lane, key kj vs query qt + rr + 4h
+      const int dlt = kj - qt - p.causal_off - 4 * h;  // causal: visible iff rr >= dlt
+      const int rlim = p.Tq - qt - 4 * h;              // rr < rlim
+      const bool lane_ok = kj >= kbeg && kj < kend;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const int r = (i & 3) + 8 * (i >> 2) + 4 * h;
-        float pv = ex2(fmaf(sacc[i], p.scale2, -rowc[0][r]));
+        const int rr = (i & 3) + 8 * (i >> 2);
+        float pv = ex2(fmaf(sacc[i], p.scale2, -lr[i]));
         if (need_mask) {
-          const int qq = qt + r;
-          bool ok = qq < p.Tq && kj >= kbeg && kj < kend;
+          bool ok = lane_ok && rr < rlim;
           if (CAUSAL) {
-            ok = ok && kj <= qq + p.causal_off;
-            if (p.window > 0) ok = ok && kj > qq + p.causal_off - p.window;
+            ok = ok && rr >= dlt;
+            if (p.window > 0) ok = ok && rr < dlt + p.window;
           }
           pv = ok ? pv : 0.f;
         }
         sacc[i] = pv;
-        dpacc[i] = pv * (dpacc[i] - rowc[1][r]);
+        dpacc[i] = pv * (dpacc[i] - dl[i]);
       }
       const s16x8 pb0 = pack8(sacc, 0), pb1 = pack8(sacc, 8);
       const s16x8 sb0 = pack8(dpacc, 0), sb1 = pack8(dpacc, 8);
-      // dV^T += dO^T P ; dK^T += Q^T dS   (k = query, permuted accumulator-row order)
+      // dV^T += dO^T P ; dK^T += Q^T dS   (k = query, permuted accumulator-row order); the four
+      // transposed fragments of tile dt+1 are read while tile dt's MFMAs run
+      s16x8 ta[2], tb[2], tc[2], td[2];
+      auto ld_kv = [&](int dt, int sl) {
+        const int c0 = 32 * dt + 16 * ((lane >> 4) & 1);
+        ta[sl] = tr_frag_perm<D>(dOs, 4 * h, c0, lane);
+        tb[sl] = tr_frag_perm<D>(dOs, 16 + 4 * h, c0, lane);
+        tc[sl] = tr_frag_perm<D>(Qs, 4 * h, c0, lane);
+        td[sl] = tr_frag_perm<D>(Qs, 16 + 4 * h, c0, lane);
+      };
+      ld_kv(0, 0);
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
-        const int c0 = 32 * dt + 16 * ((lane >> 4) & 1);
-        dv[dt] = mfma32(tr_frag_perm<D>(dOs, 4 * h, c0, lane), pb0, dv[dt]);
-        dv[dt] = mfma32(tr_frag_perm<D>(dOs, 16 + 4 * h, c0, lane), pb1, dv[dt]);
-        dk[dt] = mfma32(tr_frag_perm<D>(Qs, 4 * h, c0, lane), sb0, dk[dt]);
-        dk[dt] = mfma32(tr_frag_perm<D>(Qs, 16 + 4 * h, c0, lane), sb1, dk[dt]);
+        if (dt + 1 < DT) ld_kv(dt + 1, (dt + 1) & 1);
+        dv[dt] = mfma32(ta[dt & 1], pb0, dv[dt]);
+        dv[dt] = mfma32(tb[dt & 1], pb1, dv[dt]);
+        dk[dt] = mfma32(tc[dt & 1], sb0, dk[dt]);
+        dk[dt] = mfma32(td[dt & 1], sb1, dk[dt]);
       }
     }
     __syncthreads();  // everyone done reading Qs/dOs
@@ -475,32 +517,46 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnBwdParams p) {
     // 4 groups of 4 consecutive queries (8 B each).
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
-      const int qq = 8 * g4 + 4 * h;
+      const int row = 32 * w + l32;
       uint2 pk;
       pk.x = pack2bf(dpacc[4 * g4 + 0], dpacc[4 * g4 + 1]);
       pk.y = pack2bf(dpacc[4 * g4 + 2], dpacc[4 * g4 + 3]);
-      *reinterpret_cast<uint2*>(dSs + (32 * w + l32) * 32 + qq) = pk;
+      *reinterpret_cast<uint2*>(dSs + ds_off(row, 2 * g4 + h)) = pk;
     }
     __syncthreads();
     // dQ[q][d] for d in this wave's slices: sum over 128 keys. A = dS (q rows, keys k) via
     // transposed reads of dS^T; B = K (keys, d cols) via transposed reads of K.
     for (int dt = w; dt < DT; dt += 4) {
       f32x16 dqacc = f32x16{};
+      const int i16 = lane & 15, qq2 = i16 >> 2, pp = i16 & 3;
+      const int colc4 = (16 * ((lane >> 4) & 1) + 4 * pp) >> 2;  // query column block (8-B unit)
+      s16x8 qa[2], qb[2];
+      auto ld_dq = [&](int ks, int sl) {
+        const int r0 = 16 * ks + 8 * h;
+        qa[sl] = cat4(tr_read(dSs + ds_off(r0 + qq2, colc4)), tr_read(dSs + ds_off(r0 + 4 + qq2, colc4)));
+        qb[sl] = tr_frag_nat<D>(Ks, r0, 32 * dt + 16 * ((lane >> 4) & 1), lane);
+      };
+      ld_dq(0, 0);
 #pragma unroll
-      for (int s = 0; s < BKV / 16; ++s) {
-        const int i16 = lane & 15, qq2 = i16 >> 2, pp = i16 & 3;
-        const int r0 = 16 * s + 8 * h;
-        const int col = 16 * ((lane >> 4) & 1) + 4 * pp;  // query column block
-        const s16x4 a0 = tr_read(dSs + (r0 + qq2) * 32 + col);
-        const s16x4 a1 = tr_read(dSs + (r0 + 4 + qq2) * 32 + col);
-        const s16x8 bkf = tr_frag_nat<D>(Ks, r0, 32 * dt + 16 * ((lane >> 4) & 1), lane);
-        dqacc = mfma32(cat4(a0, a1), bkf, dqacc);
+      for (int ks = 0; ks < BKV / 16; ++ks) {
+        if (ks + 1 < BKV / 16) ld_dq(ks + 1, (ks + 1) & 1);
+        dqacc = mfma32(qa[ks & 1], qb[ks & 1], dqacc);
       }
-      // accumulate: lane holds d = 32dt + l32 (col), rows q = (i&3) + 8(i>>2) + 4h
+      // accumulate: lane holds d = 32dt + l32 (col), rows q = qt + (i&3) + 8(i>>2) + 4h.
+      // Buffer atomics: the per-row offset is a scalar (soffset), one VGPR holds the lane part,
+      // and the descriptor's num_records ends at the last valid query row of this tile, so the
+      // hardware drops rows >= Tq (no per-element compares, no 64-bit address per element).
+      {
+        const int nrow = p.Tq - qt;  // > 0
+        float* base = dqp + static_cast<int64_t>(qt) * dq_st;
+        const int nrec = ((nrow - 1) * static_cast<int>(dq_st) + D) * 4;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, nrec, 0x00020000);
+        const int voff = ((4 * h) * static_cast<int>(dq_st) + 32 * dt + l32) * 4;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int qq = qt + (i & 3) + 8 * (i >> 2) + 4 * h;
-        if (qq < p.Tq) atomicAdd(dqp + qq * dq_st + 32 * dt + l32, dqacc[i] * p.scale);
+        for (int i = 0; i < 16; ++i) {
+          const int soff = ((i & 3) + 8 * (i >> 2)) * static_cast<int>(dq_st) * 4;
+          __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(dqacc[i] * p.scale, rs, voff, soff, 0);
+        }
       }
     }
   }
@@ -572,7 +628,8 @@ void launch_attn_bwd_delta(const bf16_t* o, const bf16_t* dout, int64_t o_sb, in
                            int H, int T, int D, float* delta, hipStream_t st) {
   const int64_t rows = static_cast<int64_t>(B) * H * T;
   if (rows == 0) return;
-  attn_bwd_delta_kernel<<<static_cast<unsigned>((rows + 3) / 4), 256, 0, st>>>(
+  const int64_t rows_per_block = 4 * (64 / (D / 8));
+  attn_bwd_delta_kernel<<<static_cast<unsigned>((rows + rows_per_block - 1) / rows_per_block), 256, 0, st>>>(
       o, dout, o_sb, o_st, o_sh, do_sb, do_st, do_sh, B, H, T, D, delta);
 }
 

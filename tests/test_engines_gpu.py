@@ -70,5 +70,5 @@ def test_transposed_dgrad_matches_nn_dgrad():
         lin.TRANSPOSED_DGRAD, lin.TN_WGRAD = False, False
         b = _run("dp", False)
     finally:
-        lin.TRANSPOSED_DGRAD, lin.TN_WGRAD, lin.TN_WGRAD_MIN_ELEMS = True, True, 48 * 1024 * 1024
+        lin.TRANSPOSED_DGRAD, lin.TN_WGRAD, lin.TN_WGRAD_MIN_ELEMS = True, True, 0
     assert a == pytest.approx(b, rel=1e-2, abs=1e-3), (a, b)
