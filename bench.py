@@ -22,6 +22,9 @@ import time
 import torch
 
 
+HF_STACK_PAIRS_PER_S_1GPU = 5.2648  # BASELINE.md, measured on MI355X
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -34,6 +37,9 @@ def parse():
     ap.add_argument("--beta", type=float, default=0.1)
     ap.add_argument("--zero", type=int, default=None)
     ap.add_argument("--tp", type=int, default=1, help="tensor-parallel degree (dp = gpus / tp)")
+    ap.add_argument("--ep", type=int, default=1, help="expert-parallel degree for MoE models")
+    ap.add_argument("--fp8", action="store_true", help="MoE: e4m3 expert GEMMs in the forward")
+    ap.add_argument("--grad-ckpt", action="store_true", help="activation checkpointing (policy)")
     ap.add_argument("--bucket-mb", type=float, default=256.0)
     ap.add_argument("--profile-dir", default=None, help="write a torch.profiler trace of 1 step")
     ap.add_argument("--layers", type=int, default=None, help="debug only: override layer count "
@@ -62,7 +68,7 @@ def main() -> int:
         _ext.require()
         gemm_mode = enable_gemm_tuning(dev.index)
     world = st.world_size
-    mesh = build_mesh(tp=args.tp)
+    mesh = build_mesh(tp=args.tp, ep=args.ep)
     overrides = {} if args.layers is None else {"num_layers": args.layers}
     cfg = get_config(args.model, **overrides)
     dtype = torch.bfloat16 if dev.type == "cuda" else torch.float32
@@ -75,6 +81,17 @@ def main() -> int:
     if mesh.tp > 1:
         apply_tensor_parallel(policy, mesh.tp_group)
         apply_tensor_parallel(ref, mesh.tp_group)
+    if mesh.ep > 1:
+        from distributed_llm_alignment_amd.parallel.expert import apply_expert_parallel
+
+        apply_expert_parallel(policy, mesh)
+        apply_expert_parallel(ref, mesh)
+    if cfg.is_moe and args.fp8:
+        for m in (policy, ref):
+            for layer in m.layers:
+                layer.mlp.fp8 = True
+    if args.grad_ckpt:
+        policy.gradient_checkpointing_enable()
     if args.zero == 3:  # ZeRO-3 / FSDP: per-layer gather, sharded frozen reference
         from distributed_llm_alignment_amd.parallel.fsdp import FullyShardedEngine, ShardedInference
 
@@ -84,7 +101,8 @@ def main() -> int:
     else:
         engine = DataParallelEngine(policy, lr=1e-6, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01,
                                     max_grad_norm=1.0, zero_stage=args.zero, bucket_mb=args.bucket_mb,
-                                    group=mesh.dp_group, tp_group=mesh.tp_group)
+                                    group=mesh.dp_group, tp_group=mesh.tp_group,
+                                    expert_group=mesh.edp_group if mesh.ep > 1 else None)
     policy.train()
 
     gen = torch.Generator().manual_seed(17 + mesh.dp_rank)  # TP ranks share a batch
@@ -149,7 +167,8 @@ def main() -> int:
     tflops_gpu = value * flops_pair / world / 1e12
     if st.rank == 0:
         rec = {
-            "metric": "preference-samples/sec (whole node), Llama-3-8B DPO",
+            "metric": "preference-samples/sec (whole node), Llama-3-8B DPO" if cfg.name == "llama3-8b"
+                      else f"preference-samples/sec (whole node), {cfg.name} DPO",
             "value": round(value, 4),
             "unit": "preference_pairs/s",
             "n_gpus": world,
@@ -158,7 +177,10 @@ def main() -> int:
             "ms_per_step": round(ms, 2),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": None,
+            # BASELINE.md comparison point: the reference's DPO step on stock PyTorch-ROCm + HF
+            # (tools/hf_stack_dpo_bench.py, same shapes, 1x MI355X) = 5.2648 pairs/s per GPU,
+            # scaled ideally (x N) for N GPUs
+            "vs_baseline": round(value / (HF_STACK_PAIRS_PER_S_1GPU * world), 3) if cfg.name == "llama3-8b" else None,
             "dtype": "bf16" if dtype == torch.bfloat16 else "fp32",
             "data": "synthetic preference pairs (random token ids), random-init weights",
             "config": {
@@ -166,6 +188,7 @@ def main() -> int:
                 "global_batch": pairs_per_step,
                 "seq_len": args.seq_len,
                 "parallelism": f"dp{mesh.dp}" + (f"-tp{mesh.tp}" if mesh.tp > 1 else "")
+                               + (f"-ep{mesh.ep}" if mesh.ep > 1 else "")
                                + (f"-zero{engine.zero}" if mesh.dp > 1 or engine.zero == 3 else ""),
                 "micro_batch_pairs": args.micro_pairs,
                 "grad_accum": args.accum,
