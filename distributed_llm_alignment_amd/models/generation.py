@@ -185,7 +185,9 @@ class _DecodeGraph:
         s.wait_stream(torch.cuda.current_stream())
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.stream(s):
-            with torch.cuda.graph(self.graph, stream=s):
+            # thread_local: RCCL's watchdog thread (and in-flight gradient collectives of an
+            # overlapped RLHF step) keep making HIP calls while this stream captures
+            with torch.cuda.graph(self.graph, stream=s, capture_error_mode="thread_local"):
                 self._body()
         torch.cuda.current_stream().wait_stream(s)
 

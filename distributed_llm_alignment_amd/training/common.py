@@ -108,6 +108,9 @@ def parallelize(ctx: TrainContext, model):
         from ..parallel.expert import apply_expert_parallel
 
         apply_expert_parallel(model, m)
+    if base.cfg.is_moe and (ctx.cfg.get("model", {}) or {}).get("moe_fp8", False):
+        for layer in base.layers:  # e4m3 expert GEMMs in the forward (bf16 backward)
+            layer.mlp.fp8 = True
     if use_fsdp(ctx) and not any(p.requires_grad for p in model.parameters()):
         # frozen reference / teachers are sharded too (C10): 1/dp of their weights resident
         from ..parallel.fsdp import ShardedInference

@@ -215,3 +215,29 @@ def test_tracing_and_profile_window(tmp_path):
     torch.ones(4).sum()
     pw.step(2)
     assert (tmp_path / "prof" / "trace.json").exists() and (tmp_path / "prof" / "kernels.txt").exists()
+
+
+@pytest.mark.parametrize("cfg_name,ov", [
+    ("dpo_llama3_70b", ["model.policy_model_name_or_path=tiny-llama", "model.reference_model_name_or_path=tiny-llama",
+                        "hardware.tp_size=1", "hardware.gradient_accumulation_steps=1"]),
+    ("dpo_mixtral_8x7b", ["model.policy_model_name_or_path=tiny-mixtral",
+                          "model.reference_model_name_or_path=tiny-mixtral", "hardware.ep_size=1",
+                          "hardware.gradient_accumulation_steps=1"]),
+    ("dpo_llama3_8b", ["model.policy_model_name_or_path=tiny-llama", "model.reference_model_name_or_path=tiny-llama",
+                       "hardware.gradient_accumulation_steps=1"]),
+])
+def test_north_star_configs_run_scaled_down(tmp_path, cfg_name, ov):
+    """The shipped north-star configs parse and drive the DPO trainer (architecture overridden to
+    the tiny preset of the same family, world 1)."""
+    from distributed_llm_alignment_amd.training import train_dpo
+
+    root = Path(__file__).resolve().parents[1]
+    args = ["--config", str(root / "config" / f"{cfg_name}.yaml"),
+            "--override", "optimization.max_train_steps=2", "--override", "optimization.micro_batch_size=2",
+            "--override", "model.max_seq_length=64", "--override", "data.num_samples=8",
+            "--override", "data.num_workers=0", "--override", f"logging.output_dir={tmp_path / 'ck'}",
+            "--override", f"logging.log_dir={tmp_path / 'logs'}", "--override", "logging.save_every_steps=0"]
+    for o in ov:
+        args += ["--override", o]
+    assert train_dpo.main(args) == 0
+    assert (tmp_path / "ck" / "final" / "model.safetensors").exists()

@@ -1,0 +1,85 @@
+#!/usr/bin/env python
+"""One-GPU RLHF step throughput for the BASELINE "Llama-3-8B PPO-style RLHF" config: per step,
+generate B rollouts (prompt T_p, up to N new tokens, hipGraph decode + fused sampler), score
+them with a Llama-3-8B-backbone reward model, compute policy / reference sequence log-probs and
+the KL-penalised policy-gradient loss (fused HIP kernel), backward and fused AdamW. Random init,
+synthetic prompts. Prints one JSON line (rollouts/s and the phase split)."""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--prompt", type=int, default=512)
+    ap.add_argument("--new", type=int, default=256)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    a = ap.parse_args()
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from distributed_llm_alignment_amd.models import build_model, generate, get_config
+    from distributed_llm_alignment_amd.models.reward import RewardModel
+    from distributed_llm_alignment_amd.objectives import rlhf_loss
+    from distributed_llm_alignment_amd.ops import _ext
+    from distributed_llm_alignment_amd.parallel.data_parallel import DataParallelEngine
+    from distributed_llm_alignment_amd.utils.tuning import enable_gemm_tuning
+
+    dev = torch.device("cuda", 0)
+    _ext.require()
+    enable_gemm_tuning(0)
+    cfg = get_config(a.model)
+    pol = build_model(cfg, device=dev, dtype=torch.bfloat16, seed=1)
+    ref = build_model(cfg, device=dev, dtype=torch.bfloat16, seed=1).requires_grad_(False).eval()
+    rm = RewardModel(build_model(cfg, device=dev, dtype=torch.bfloat16, seed=2, headless=True)).to(dev, torch.bfloat16)
+    rm.eval().requires_grad_(False)
+    eng = DataParallelEngine(pol, lr=1e-6, betas=(0.9, 0.95), weight_decay=0.01, max_grad_norm=1.0)
+    g = torch.Generator(device=dev).manual_seed(0)
+    phases = {"generate": 0.0, "score": 0.0, "train": 0.0}
+
+    def sync():
+        torch.cuda.synchronize()
+        return time.perf_counter()
+
+    def step(record):
+        ids = torch.randint(3, cfg.vocab_size, (a.batch, a.prompt), device=dev, generator=g)
+        am = torch.ones_like(ids)
+        t0 = sync()
+        seqs, mask = generate(pol, ids, am, max_new_tokens=a.new, do_sample=True, temperature=0.7,
+                              top_p=0.9, eos_token_id=-1, return_mask=True, seed=3)
+        t1 = sync()
+        with torch.no_grad():
+            scores = rm(seqs, mask)
+        t2 = sync()
+        pol.train()
+        loss, _ = rlhf_loss(pol, ref, seqs, mask, scores.float(), 0.1)
+        loss.backward()
+        eng.step()
+        t3 = sync()
+        if record:
+            phases["generate"] += t1 - t0
+            phases["score"] += t2 - t1
+            phases["train"] += t3 - t2
+
+    for _ in range(a.warmup):
+        step(False)
+    t = sync()
+    for _ in range(a.steps):
+        step(True)
+    dt = sync() - t
+    print(json.dumps({"bench": "rlhf_step", "model": cfg.name, "rollouts_per_step": a.batch,
+                      "prompt": a.prompt, "new_tokens": a.new, "s_per_step": round(dt / a.steps, 3),
+                      "rollouts_per_s": round(a.batch * a.steps / dt, 3),
+                      **{f"{k}_s": round(v / a.steps, 3) for k, v in phases.items()}}), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
