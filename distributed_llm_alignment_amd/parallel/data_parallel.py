@@ -356,6 +356,20 @@ class DataParallelEngine:
         if self.master is not None and sd.get("master") is not None:
             self.master.copy_(sd["master"])
 
+    def layout(self) -> Dict[str, object]:
+        """Where every parameter's optimizer state lives in the per-rank shards (written next to
+        the shards as dla_optimizer_layout.json; tools/consolidate_checkpoint.py rebuilds a
+        torch-format optimizer.bin offline from it)."""
+        all_params = [p for p in self.module.parameters() if p.requires_grad]
+        index = {id(p): i for i, p in enumerate(all_params)}
+        names = {id(p): n for n, p in self.module.named_parameters()}
+        return {"kind": "flat", "zero": self.zero, "world": self.world, "numel": self.numel,
+                "tp_size": self.tp_size,
+                "buckets": [{"start": b.start, "end": b.end, "world": b.world, "shard_off": b.shard_off,
+                             "expert": b.expert} for b in self.buckets],
+                "params": [{"index": index[id(p)], "name": names.get(id(p), ""), "shape": list(p.shape),
+                            "offset": self._offsets[id(p)]} for p in self.params]}
+
     def torch_optimizer_state_dict(self) -> Dict[str, object]:
         """Consolidated torch.optim.AdamW-format state dict (param index -> step/exp_avg/
         exp_avg_sq), as accelerate writes to optimizer.bin. Gathers shards under ZeRO."""

@@ -467,6 +467,18 @@ class FullyShardedEngine(_ShardedBase):
             out.copy_(src)
         return out
 
+    def layout(self) -> Dict[str, object]:
+        """Per-unit shard layout of the optimizer state (see DataParallelEngine.layout)."""
+        all_params = [p for p in self.module.parameters() if p.requires_grad]
+        index = {id(p): i for i, p in enumerate(all_params)}
+        names = {id(p): n for n, p in self.module.named_parameters()}
+        return {"kind": "fsdp", "zero": 3, "world": self.world, "numel": self.numel,
+                "tp_size": self.tp_size,
+                "units": [{"numel": u.numel, "chunk": u.chunk, "shard_off": u.shard_off,
+                           "params": [{"index": index[id(p)], "name": names.get(id(p), ""),
+                                       "shape": list(p.shape), "offset": u.offsets[id(p)]} for p in u.params]}
+                          for u in self.units]}
+
     def torch_optimizer_state_dict(self) -> Dict[str, object]:
         """torch.optim.AdamW-format state (param index in module order), gathered per unit."""
         state = {}

@@ -95,6 +95,8 @@ def save_state(output_dir, models: Sequence, engine=None, scheduler=None, step: 
     if engine is not None:
         torch.save({k: (v.cpu() if isinstance(v, torch.Tensor) else v)
                     for k, v in engine.optimizer_state().items()}, out / f"optimizer_shard_{st.rank}.pt")
+        if st.is_main and hasattr(engine, "layout"):
+            (out / "dla_optimizer_layout.json").write_text(json.dumps(engine.layout()))
         if engine.numel <= CONSOLIDATE_MAX_NUMEL and not tp:
             osd = engine.torch_optimizer_state_dict()  # collective under ZeRO
             if st.is_main:

@@ -8,6 +8,7 @@
 import os
 import socket
 import tempfile
+from pathlib import Path
 
 import pytest
 import torch
@@ -517,3 +518,43 @@ def _replica_check(rank, world):
 def test_replica_divergence_detector():
     res = run_ranks(_replica_check, 2)
     assert res[0] == "caught" and res[1] == "caught"
+
+
+def _ckpt_for_consolidation(rank, world, root, fsdp):
+    import torch
+
+    from distributed_llm_alignment_amd.data.synthetic import synthetic_preference_batch
+    from distributed_llm_alignment_amd.models import build_model, get_config
+    from distributed_llm_alignment_amd.objectives import dpo_step_loss
+    from distributed_llm_alignment_amd.parallel.data_parallel import DataParallelEngine
+    from distributed_llm_alignment_amd.parallel.fsdp import FullyShardedEngine
+    from distributed_llm_alignment_amd.utils.checkpoint import save_state
+
+    cfg = get_config("tiny-llama")
+    pol = build_model(cfg, device="cpu", seed=0)
+    ref = build_model(cfg, device="cpu", seed=0).requires_grad_(False)
+    eng = FullyShardedEngine(pol, lr=1e-2) if fsdp else DataParallelEngine(pol, lr=1e-2, zero_stage=1, bucket_mb=0.05)
+    b = synthetic_preference_batch(2, 16, cfg.vocab_size, generator=torch.Generator().manual_seed(rank))
+    dpo_step_loss(pol, ref, b)[0].backward()
+    eng.step()
+    save_state(f"{root}/ck", [pol], eng, step=1, hf_export=False)
+    return 0
+
+
+@pytest.mark.parametrize("fsdp", [False, True])
+def test_consolidate_optimizer_shards_matches_gathered(tmp_path, fsdp):
+    """tools/consolidate_checkpoint.py rebuilds exactly the optimizer.bin the engine gathers."""
+    import importlib.util
+
+    run_ranks(_ckpt_for_consolidation, 2, (str(tmp_path), fsdp))
+    ck = tmp_path / "ck"
+    want = torch.load(str(ck / "optimizer.bin"), weights_only=True)
+    spec = importlib.util.spec_from_file_location("cons", Path(__file__).resolve().parents[1] / "tools" / "consolidate_checkpoint.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    out = mod.consolidate(ck, tmp_path / "opt2.bin")
+    got = torch.load(str(out), weights_only=True)
+    assert sorted(got["state"]) == sorted(want["state"])
+    for i in want["state"]:
+        for k in ("exp_avg", "exp_avg_sq"):
+            assert torch.equal(got["state"][i][k], want["state"][i][k]), (i, k)
