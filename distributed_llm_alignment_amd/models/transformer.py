@@ -302,7 +302,7 @@ class CausalLM(nn.Module):
     # ----------------------------------------------------------------- objective helpers
     def sequence_logprob(self, input_ids, attention_mask=None, reduction: str = "mean"):
         """Reference `compute_logprobs` (train_dpo.py:31-39): masked mean log p per sequence."""
-        h = self.forward(input_ids, attention_mask)
+        h = self(input_ids, attention_mask)  # __call__: module hooks (param all-gather waits) run
         if self.lm_head_bias is not None:
             return _biased_seq_logprob(self, h, input_ids, attention_mask, reduction)
         S, T, H = h.shape
@@ -312,7 +312,7 @@ class CausalLM(nn.Module):
 
     def causal_lm_loss(self, input_ids, labels, attention_mask=None):
         """HF ForCausalLMLoss (train_sft.py:145-146): mean token NLL over labels != -100."""
-        h = self.forward(input_ids, attention_mask)
+        h = self(input_ids, attention_mask)  # __call__: module hooks (param all-gather waits) run
         if self.lm_head_bias is not None:
             lg = self.logits(h).float()
             return F.cross_entropy(lg[:, :-1].reshape(-1, lg.shape[-1]), labels[:, 1:].reshape(-1),

@@ -38,7 +38,7 @@ def sequence_logps(model, ids, mask, reduction: str = "mean", loss_mask=None):
     """Per-sequence log-prob; `loss_mask` (optional) restricts scoring to response tokens."""
     if loss_mask is None:
         return model.sequence_logprob(ids, mask, reduction)
-    h = model.forward(ids, mask)
+    h = model(ids, mask)
     tgt, m = ops.shifted_targets(ids, loss_mask)
     S, T, H = h.shape
     lp = ops.linear_logprob(h.reshape(S * T, H), model.head_weight, tgt.reshape(-1)).view(S, T)
@@ -89,10 +89,10 @@ def distill_loss(student, teachers: Sequence, batch, use_kl: bool):
         if t.cfg.vocab_size != student.cfg.vocab_size:
             raise ValueError("KL distillation requires teacher and student to share a vocabulary "
                              "(SURVEY Appendix A #15)")
-    hs = student.forward(ids, mask)
+    hs = student(ids, mask)
     s_logits = student.logits(hs)
     with torch.no_grad():
-        t_logits = torch.stack([t.logits(t.forward(ids, mask)) for t in teachers])
+        t_logits = torch.stack([t.logits(t(ids, mask)) for t in teachers])
     S, T, V = s_logits.shape
     kl = ops.ensemble_kl(s_logits.reshape(S * T, V), t_logits.reshape(len(teachers), S * T, V)).view(S, T)
     m = mask.float()

@@ -24,6 +24,7 @@ clip-norm computation (no extra pass over the gradients).
 from __future__ import annotations
 
 import contextlib
+import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
@@ -61,7 +62,8 @@ class DataParallelEngine:
     def __init__(self, module: nn.Module, lr: float = 1e-5, betas=(0.9, 0.999), eps: float = 1e-8,
                  weight_decay: float = 0.0, max_grad_norm: float = 1.0, zero_stage: Optional[int] = None,
                  bucket_mb: float = 256.0, master_weights: bool = True,
-                 dist_st: Optional[DistState] = None, group=None, tp_group=None, expert_group=None):
+                 dist_st: Optional[DistState] = None, group=None, tp_group=None, expert_group=None,
+                 overlap_param_gather: bool = os.environ.get("DLA_OVERLAP_AG", "1") != "0"):
         self.module = module
         self.dist = dist_st or dist_state()
         # tensor parallel: grads of TP-sharded params differ per TP rank; params marked
@@ -196,8 +198,37 @@ class DataParallelEngine:
             for p in b.params:
                 self._bucket_of[id(p)] = bi
                 p.register_post_accumulate_grad_hook(self._on_grad)
+        # ZeRO-1 parameter all-gather overlapped with the next forward: step() issues the
+        # per-bucket all-gathers asynchronously in forward order (the last buckets hold the
+        # first-used parameters); a forward pre-hook on every module that owns parameters waits
+        # only for the buckets of its own weights, so layer i computes while later layers'
+        # weights are still in flight on RCCL's stream.
+        self._ag_pending: Dict[int, object] = {}
+        module._dla_dp_engine = self
+        self.overlap_param_gather = overlap_param_gather and self.zero and self._comm
+        if self.overlap_param_gather:
+            for mod in module.modules():
+                own = [self._bucket_of[id(p)] for p in mod.parameters(recurse=False) if id(p) in self._bucket_of]
+                if own:
+                    mod.register_forward_pre_hook(self._make_wait_hook(sorted(set(own))))
 
     # ------------------------------------------------------------------------ helpers
+    def _make_wait_hook(self, buckets):
+        def hook(_mod, _inp):
+            if self._ag_pending:
+                for bi in buckets:
+                    h = self._ag_pending.pop(bi, None)
+                    if h is not None:
+                        h.wait()
+        return hook
+
+    def wait_params(self):
+        """Block (on the current stream) until every in-flight parameter all-gather landed.
+        Needed before reading weights outside a module forward (checkpoints, exports)."""
+        for h in self._ag_pending.values():
+            h.wait()
+        self._ag_pending.clear()
+
     def _chunk(self, buf: torch.Tensor, b: Bucket) -> torch.Tensor:
         c = b.size // b.world
         return buf[b.start + b.rank * c: b.start + (b.rank + 1) * c]
@@ -300,14 +331,18 @@ class DataParallelEngine:
                      lr, self.betas[0], self.betas[1], self.eps, self.wd, self.step_count,
                      clip=coef if self.max_grad_norm else None, grad_scale=1.0 / self.world)
         if self.zero:
-            for b in self.buckets:
+            self.wait_params()
+            for bi in reversed(range(len(self.buckets))):  # forward order
+                b = self.buckets[bi]
                 c = b.size // b.world
                 if b.world == 1:
                     self.param_buf[b.start:b.end].copy_(self.param_shard[b.shard_off:b.shard_off + c])
                 else:
-                    dist.all_gather_into_tensor(self.param_buf[b.start:b.end],
-                                                self.param_shard[b.shard_off:b.shard_off + c],
-                                                group=b.group)
+                    h = dist.all_gather_into_tensor(self.param_buf[b.start:b.end],
+                                                    self.param_shard[b.shard_off:b.shard_off + c],
+                                                    group=b.group, async_op=self.overlap_param_gather)
+                    if self.overlap_param_gather:
+                        self._ag_pending[bi] = h
         self._wt_epoch[0] += 1  # invalidates weight-derived caches (ops.linear W^T)
         self.zero_grad()
         return self.last_grad_norm
@@ -319,6 +354,7 @@ class DataParallelEngine:
 
     @torch.no_grad()
     def broadcast_params(self, src: int = 0):
+        self.wait_params()
         self._wt_epoch[0] += 1
         if self.world > 1:
             for b in self.buckets:
@@ -332,6 +368,7 @@ class DataParallelEngine:
 
     @torch.no_grad()
     def sync_master_from_params(self):
+        self.wait_params()
         self._wt_epoch[0] += 1
         if self.zero:
             self.param_shard.copy_(torch.cat([self._chunk(self.param_buf, b) for b in self.buckets]))
@@ -341,6 +378,7 @@ class DataParallelEngine:
     # ------------------------------------------------------------------------ state
     def optimizer_state(self) -> Dict[str, object]:
         """Local (possibly sharded) optimizer state."""
+        self.wait_params()
         return {"step": self.step_count, "lr": self.lr, "betas": self.betas, "eps": self.eps,
                 "weight_decay": self.wd, "world": self.world, "zero": self.zero,
                 "rank": self.rank, "numel": self.numel,

@@ -73,6 +73,8 @@ def save_state(output_dir, models: Sequence, engine=None, scheduler=None, step: 
     if st.is_main:
         out.mkdir(parents=True, exist_ok=True)
     pdist.barrier()
+    if engine is not None and hasattr(engine, "wait_params"):
+        engine.wait_params()  # overlapped ZeRO-1 all-gathers must land before weights are read
     from contextlib import ExitStack
 
     from ..parallel.fsdp import fsdp_full_params

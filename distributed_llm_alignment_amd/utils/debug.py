@@ -49,6 +49,9 @@ def check_replicas_in_sync(module: torch.nn.Module, group=None, rtol: float = 0.
     eng = getattr(module, "_dla_fsdp", None)
     if eng is not None:
         return  # ZeRO-3: ranks hold disjoint shards by design
+    dp = getattr(module, "_dla_dp_engine", None)
+    if dp is not None:
+        dp.wait_params()  # overlapped ZeRO-1 all-gathers
     sums = replica_checksums(module, group)
     ref = sums[0]
     bad = [i for i, s in enumerate(sums) if abs(s - ref) > rtol * max(abs(ref), 1.0)]

@@ -104,6 +104,7 @@ def _train_dp(rank, world, zero, accum):
             loss, _ = dpo_step_loss(pol, ref, mine, beta=0.1)
             (loss / accum).backward()
     eng.step()
+    eng.wait_params()  # ZeRO-1 all-gathers overlap the next forward; reading weights directly
     return {n: p.detach().clone() for n, p in pol.named_parameters()}, len(eng.buckets)
 
 
