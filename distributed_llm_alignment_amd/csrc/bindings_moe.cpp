@@ -17,6 +17,23 @@ void launch_moe_combine(const bf16_t*, const int*, const float*, int64_t, int, i
 void launch_moe_combine_bwd(const bf16_t*, const bf16_t*, const int*, const float*, int64_t, int,
                             int, bf16_t*, float*, hipStream_t);
 
+void launch_quant_fp8_rows(const bf16_t*, int64_t, int64_t, int, uint8_t*, float*, hipStream_t);
+
+// x [M, K] bf16 (unit column stride, 16-B aligned rows) -> (q [M, K] float8_e4m3fn, inv_scale [M, 1])
+std::tuple<at::Tensor, at::Tensor> quant_fp8_rows(const at::Tensor& x) {
+  check_bf16(x, "x");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0 && x.size(1) % 8 == 0,
+              "x [M, K], K % 8 == 0, 16-byte aligned rows");
+  check_aligned16(x, "x");
+  const int64_t M = x.size(0), K = x.size(1);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  auto q = at::empty({M, K}, x.options().dtype(at::kFloat8_e4m3fn));
+  auto inv = at::empty({M, 1}, x.options().dtype(at::kFloat));
+  launch_quant_fp8_rows(cbp(x), x.stride(0), M, (int)K, reinterpret_cast<uint8_t*>(q.data_ptr()),
+                        inv.data_ptr<float>(), cur_stream(x));
+  return {q, inv};
+}
+
 static void check_pos(const at::Tensor& pos, int64_t N, int64_t k) {
   check_i32(pos, "pos");
   TORCH_CHECK(pos.is_contiguous() && pos.dim() == 2 && pos.size(0) == N && pos.size(1) == k,
@@ -114,6 +131,7 @@ std::tuple<at::Tensor, at::Tensor> moe_combine_bwd(const at::Tensor& dout, const
 
 TORCH_LIBRARY_FRAGMENT(dla, m) {
   m.def("moe_topk_fwd(Tensor logits, int k) -> (Tensor, Tensor)");
+  m.def("quant_fp8_rows(Tensor x) -> (Tensor, Tensor)");
   m.def("moe_topk_bwd(Tensor topv, Tensor topi, Tensor grad, int E) -> Tensor");
   m.def("moe_dispatch(Tensor x, Tensor pos) -> Tensor");
   m.def("moe_combine(Tensor ys, Tensor pos, Tensor? w) -> Tensor");
@@ -122,6 +140,7 @@ TORCH_LIBRARY_FRAGMENT(dla, m) {
 
 TORCH_LIBRARY_IMPL(dla, CUDA, m) {
   m.impl("moe_topk_fwd", &dla::moe_topk_fwd);
+  m.impl("quant_fp8_rows", &dla::quant_fp8_rows);
   m.impl("moe_topk_bwd", &dla::moe_topk_bwd);
   m.impl("moe_dispatch", &dla::moe_dispatch);
   m.impl("moe_combine", &dla::moe_combine);

@@ -148,6 +148,45 @@ __global__ __launch_bounds__(256) void moe_combine_bwd_kernel(const bf16_t* __re
   }
 }
 
+// Row-wise e4m3 quantisation for the fp8 MFMA GEMMs (hipBLASLt row-wise scaled fp8):
+// q[r, :] = sat(x[r, :] * 448 / amax_r) as OCP e4m3fn (gfx950 v_cvt_pk_fp8_f32), inv[r] =
+// amax_r / 448. One 256-thread block per row: the row is read twice (amax, then convert) and
+// stays in L1/L2 between the passes; no intermediate fp32 copy.
+__global__ __launch_bounds__(256) void quant_fp8_rows_kernel(const bf16_t* __restrict__ x,
+                                                              int64_t ld, int K,
+                                                              uint8_t* __restrict__ q,
+                                                              float* __restrict__ inv) {
+  __shared__ float red[4];
+  const int64_t r = blockIdx.x;
+  const bf16_t* row = x + r * ld;
+  float m = 0.f;
+  for (int i = threadIdx.x; i < K / 8; i += 256) {
+    const bf16x8 a = load_bf16x8(row + i * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(bf2f(a[j])));
+  }
+  m = block_max<256>(m, red);
+  const float amax = fmaxf(m, 1e-12f);
+  const float sc = 448.f / amax;
+  if (threadIdx.x == 0) inv[r] = amax / 448.f;
+  uint8_t* qrow = q + r * (int64_t)K;
+  for (int i = threadIdx.x; i < K / 8; i += 256) {
+    const bf16x8 a = load_bf16x8(row + i * 8);
+    uint32_t lo = 0, hi = 0;
+    lo = __builtin_amdgcn_cvt_pk_fp8_f32(bf2f(a[0]) * sc, bf2f(a[1]) * sc, lo, false);
+    lo = __builtin_amdgcn_cvt_pk_fp8_f32(bf2f(a[2]) * sc, bf2f(a[3]) * sc, lo, true);
+    hi = __builtin_amdgcn_cvt_pk_fp8_f32(bf2f(a[4]) * sc, bf2f(a[5]) * sc, hi, false);
+    hi = __builtin_amdgcn_cvt_pk_fp8_f32(bf2f(a[6]) * sc, bf2f(a[7]) * sc, hi, true);
+    *reinterpret_cast<uint2*>(qrow + i * 8) = make_uint2(lo, hi);
+  }
+}
+
+void launch_quant_fp8_rows(const bf16_t* x, int64_t ld, int64_t rows, int K, uint8_t* q, float* inv,
+                           hipStream_t st) {
+  if (rows == 0) return;
+  quant_fp8_rows_kernel<<<rows, 256, 0, st>>>(x, ld, K, q, inv);
+}
+
 // ----------------------------------------------------------------------------------------------
 void launch_moe_topk_fwd(const bf16_t* logits, int64_t N, int E, int k, float* topv, int* topi,
                          hipStream_t st) {

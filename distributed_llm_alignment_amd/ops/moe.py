@@ -122,18 +122,40 @@ _FP8 = getattr(torch, "float8_e4m3fn", None)
 _FP8_MAX = 448.0
 
 
-def _quant_fp8(t: torch.Tensor):
-    amax = t.abs().amax().float().clamp(min=1e-12)
-    scale = _FP8_MAX / amax
-    return (t.float() * scale).clamp(-_FP8_MAX, _FP8_MAX).to(_FP8), (1.0 / scale).reshape(())
+def quant_fp8_rows(t: torch.Tensor):
+    """Row-wise e4m3: (q [M, K] float8_e4m3fn, inv_scale [M, 1] fp32). Fused HIP kernel on GPU."""
+    t = t.contiguous()
+    if _ext.use_native(t) and t.dtype == torch.bfloat16 and t.shape[-1] % 8 == 0:
+        return _ext.require().quant_fp8_rows(t)
+    amax = t.abs().amax(dim=1, keepdim=True).float().clamp(min=1e-12)
+    sc = _FP8_MAX / amax
+    return (t.float() * sc).clamp(-_FP8_MAX, _FP8_MAX).to(_FP8), 1.0 / sc
+
+
+def fp8_weight(w: torch.Tensor):
+    """Cached row-wise e4m3 copy of a weight [..., N, K] (re-quantised when the weight's version
+    counter or its engine's weight epoch moved, i.e. once per optimizer step)."""
+    ep = getattr(w, "_dla_epoch", None)
+    key = (w._version, ep[0] if ep is not None else 0)
+    c = getattr(w, "_dla_fp8", None)
+    if c is None or c[0] != key:
+        with torch.no_grad():
+            q, inv = quant_fp8_rows(w.detach().reshape(-1, w.shape[-1]))
+        c = (key, q.view(w.shape), inv.view(*w.shape[:-1], 1))
+        w._dla_fp8 = c
+    return c[1], c[2]
+
+
+def fp8_mm(xq, sx, wq, sw) -> torch.Tensor:
+    """[M, K] x [N, K]^T with row-wise scales on the gfx950 fp8 MFMA path (hipBLASLt)."""
+    return torch._scaled_mm(xq, wq.t(), scale_a=sx, scale_b=sw.t(), out_dtype=torch.bfloat16)
 
 
 def fp8_linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-    """y = x @ w^T with e4m3 operands and per-tensor scales on the gfx950 fp8 MFMA path
-    (hipBLASLt via torch._scaled_mm), bf16 output. Forward only."""
-    xq, sx = _quant_fp8(x)
-    wq, sw = _quant_fp8(w)
-    return torch._scaled_mm(xq, wq.t(), scale_a=sx, scale_b=sw, out_dtype=torch.bfloat16)
+    """y = x @ w^T with e4m3 operands and row-wise scales, bf16 output. Forward only."""
+    xq, sx = quant_fp8_rows(x)
+    wq, sw = quant_fp8_rows(w)
+    return fp8_mm(xq, sx, wq, sw)
 
 
 # ------------------------------------------------------------------------------ experts
@@ -146,17 +168,30 @@ class _ExpertsFn(torch.autograd.Function):
         F2 = w_up.shape[1]
         gu = xs.new_empty((M, F2))
         ys = xs.new_empty((M, H))
-        s = 0
-        for e, c in enumerate(counts):
-            if c:
-                seg = xs[s:s + c]
-                if fp8:
-                    gu[s:s + c] = fp8_linear(seg, w_up[e])
-                    ys[s:s + c] = fp8_linear(swiglu(gu[s:s + c]), w_down[e])
-                else:
-                    torch.mm(seg, w_up[e].t(), out=gu[s:s + c])
+        if fp8:
+            # e4m3 forward: activations quantised once per GEMM by the fused row-wise kernel,
+            # expert weights cached quantised per optimizer step; fp32 accumulate, bf16 out
+            wu_q, wu_s = fp8_weight(w_up)
+            wd_q, wd_s = fp8_weight(w_down)
+            xq, xsc = quant_fp8_rows(xs)
+            s = 0
+            for e, c in enumerate(counts):
+                if c:
+                    gu[s:s + c] = fp8_mm(xq[s:s + c], xsc[s:s + c], wu_q[e], wu_s[e])
+                s += c
+            aq, asc = quant_fp8_rows(swiglu(gu))
+            s = 0
+            for e, c in enumerate(counts):
+                if c:
+                    ys[s:s + c] = fp8_mm(aq[s:s + c], asc[s:s + c], wd_q[e], wd_s[e])
+                s += c
+        else:
+            s = 0
+            for e, c in enumerate(counts):
+                if c:
+                    torch.mm(xs[s:s + c], w_up[e].t(), out=gu[s:s + c])
                     torch.mm(swiglu(gu[s:s + c]), w_down[e].t(), out=ys[s:s + c])
-            s += c
+                s += c
         ctx.save_for_backward(xs, gu, w_up, w_down)
         ctx.counts = list(counts)
         return ys

@@ -87,3 +87,24 @@ def test_fp8_expert_forward_close_to_bf16():
     y = x.float() @ w.float().t()
     rel = (y8.float() - y).norm() / y.norm()
     assert rel < 6e-2, rel
+
+
+def test_fp8_rowwise_quant_kernel_and_moe_layer():
+    from distributed_llm_alignment_amd import ops
+    from distributed_llm_alignment_amd.models import build_model, get_config
+
+    g = torch.Generator(device=DEV).manual_seed(5)
+    x = (torch.randn(333, 4096, device=DEV, generator=g) * 3).to(torch.bfloat16)
+    q, inv = ops.moe.quant_fp8_rows(x)
+    assert q.dtype == torch.float8_e4m3fn and inv.shape == (333, 1)
+    deq = q.float() * inv
+    assert ((deq - x.float()).abs() / x.float().abs().amax(1, keepdim=True)).max() < 0.07
+    assert torch.allclose(inv, x.float().abs().amax(1, keepdim=True) / 448.0, rtol=1e-6)
+    cfg = get_config("tiny-mixtral", hidden_size=256, intermediate_size=512, num_experts=8)
+    m = build_model(cfg, device=DEV, dtype=torch.bfloat16, seed=2)
+    moe = m.layers[0].mlp
+    h = torch.randn(3, 171, cfg.hidden_size, device=DEV, generator=g).to(torch.bfloat16)
+    ref = moe(h).float()
+    moe.fp8 = True
+    out = moe(h).float()
+    assert (out - ref).norm() / ref.norm() < 0.08
