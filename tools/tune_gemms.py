@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--out", required=True)
     ap.add_argument("--iters", type=int, default=4)
     ap.add_argument("--ms", type=int, default=12)
-    ap.add_argument("--only", default="", help="comma list of fwd,dx,dw,lm")
+    ap.add_argument("--only", default="", help="comma list of fwd,dx,dw,dxt,dwt,lm")
     a = ap.parse_args()
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from distributed_llm_alignment_amd.models import get_config
@@ -49,7 +49,7 @@ def main():
         pass
     dev = torch.device("cuda", 0)
     M = a.tokens
-    only = set(a.only.split(",")) if a.only else {"fwd", "dx", "dw", "lm"}
+    only = set(a.only.split(",")) if a.only else {"fwd", "dx", "dw", "dxt", "dwt", "lm"}
 
     def run(tag, fn):
         t0 = time.time()
@@ -64,13 +64,24 @@ def main():
         W = torch.randn(N, K, device=dev, dtype=torch.bfloat16) * 0.02
         X = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
         dY = torch.randn(M, N, device=dev, dtype=torch.bfloat16)
-        if "fwd" in only or name == "lm_head":
+        if "fwd" in only:
             run(f"fwd {name} M={M} N={N} K={K}", lambda: torch.nn.functional.linear(X, W))
-        if "dx" in only or name == "lm_head":
+        if "dx" in only:
             run(f"dx  {name} M={M} N={K} K={N}", lambda: dY @ W)
-        if "dw" in only or name == "lm_head":
+        if "dw" in only:
             G = torch.zeros(N, K, device=dev, dtype=torch.bfloat16)
             run(f"dw  {name} M={N} N={K} K={M}", lambda: G.addmm_(dY.t(), X))
+        # layouts the engine actually issues (ops/linear.py): TN input grad through the persistent
+        # W^T, TN weight grad on transposed activations accumulated with beta = 1
+        if "dxt" in only:
+            Wt = W.t().contiguous()
+            run(f"dxT {name} M={M} N={K} K={N}", lambda: torch.nn.functional.linear(dY, Wt))
+            del Wt
+        if "dwt" in only:
+            G = torch.zeros(N, K, device=dev, dtype=torch.bfloat16)
+            dYt, Xt = dY.t().contiguous(), X.t().contiguous()
+            run(f"dwT {name} M={N} N={K} K={M}", lambda: G.addmm_(dYt, Xt.t()))
+            del G, dYt, Xt
         if name == "lm_head" and a.chunk and a.chunk != M:
             Xc = X[: a.chunk]
             run(f"fwd {name} chunk M={a.chunk}", lambda: torch.nn.functional.linear(Xc, W))
