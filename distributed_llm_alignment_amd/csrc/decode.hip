@@ -64,17 +64,26 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
   for (int g = 0; g < G; ++g)
 #pragma unroll
     for (int j = 0; j < 8; ++j) qr[g][j] = qs[g][dl + j];
-  // ---- phase 1: scores (log2 domain)
+  // ---- phase 1: scores (log2 domain). All of the wave's K rows are loaded up front
+  // (unconditional loads at clamped keys, so the NIT 16-byte loads issue back to back and the
+  // wave has them all in flight), then consumed.
+  constexpr int NIT = KPW / KPI;
+  bf16x8 kvr[NIT];
 #pragma unroll
-  for (int it = 0; it < KPW / KPI; ++it) {
+  for (int it = 0; it < NIT; ++it) {
+    const int key = min(max(base + wv * KPW + it * KPI + sub, k0), k1 - 1);
+    kvr[it] = load_bf16x8(kbase + (int64_t)key * c_st);
+  }
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
     const int kl = wv * KPW + it * KPI + sub;  // key within the chunk
     const int key = base + kl;
     const bool ok = key >= k0 && key < k1;
     float s[G];
 #pragma unroll
     for (int g = 0; g < G; ++g) s[g] = 0.f;
-    if (ok) {
-      const bf16x8 kv = load_bf16x8(kbase + (int64_t)key * c_st);
+    {
+      const bf16x8 kv = kvr[it];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float kf = bf2f(kv[j]);
@@ -123,18 +132,20 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
   for (int g = 0; g < G; ++g)
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[g][j] = 0.f;
+  bf16x8 vvr[NIT];
 #pragma unroll
-  for (int it = 0; it < KPW / KPI; ++it) {
-    const int kl = wv * KPW + it * KPI + sub;
-    const int key = base + kl;
-    if (key >= k0 && key < k1) {
-      const bf16x8 vv = load_bf16x8(vbase + (int64_t)key * c_st);
+  for (int it = 0; it < NIT; ++it) {
+    const int key = min(max(base + wv * KPW + it * KPI + sub, k0), k1 - 1);
+    vvr[it] = load_bf16x8(vbase + (int64_t)key * c_st);
+  }
 #pragma unroll
-      for (int g = 0; g < G; ++g) {
-        const float p = ps[g][kl];
+  for (int it = 0; it < NIT; ++it) {
+    const int kl = wv * KPW + it * KPI + sub;  // p = 0 outside [k0, k1) (set above)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[g][j] += p * bf2f(vv[j]);
-      }
+    for (int g = 0; g < G; ++g) {
+      const float p = ps[g][kl];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[g][j] += p * bf2f(vvr[it][j]);
     }
   }
   // reduce the KPI key sub-groups of the wave (lanes sharing dl)

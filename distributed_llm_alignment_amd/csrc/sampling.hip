@@ -52,6 +52,42 @@ __device__ __forceinline__ float ld<bf16_t>(const bf16_t* p, int64_t i) { return
 template <>
 __device__ __forceinline__ float ld<float>(const float* p, int64_t i) { return p[i]; }
 
+// 8 consecutive logits as fp32 (one 16-byte load for bf16, two for fp32); rows are 16-B aligned
+// and V % 8 == 0 (checked on the host, scalar fallback otherwise)
+template <typename T>
+__device__ __forceinline__ void ld8(const T* p, int64_t i8, float* x);
+template <>
+__device__ __forceinline__ void ld8<bf16_t>(const bf16_t* p, int64_t i8, float* x) {
+  const bf16x8 a = load_bf16x8(p + i8 * 8);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) x[j] = bf2f(a[j]);
+}
+template <>
+__device__ __forceinline__ void ld8<float>(const float* p, int64_t i8, float* x) {
+  const f32x4 a = reinterpret_cast<const f32x4*>(p + i8 * 8)[0];
+  const f32x4 b = reinterpret_cast<const f32x4*>(p + i8 * 8)[1];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    x[j] = a[j];
+    x[4 + j] = b[j];
+  }
+}
+
+// visit every logit of the row: fn(index, value); vectorised when VEC
+template <bool VEC, typename T, typename F>
+__device__ __forceinline__ void for_each_logit(const T* row, int V, F&& fn) {
+  if constexpr (VEC) {
+    for (int i = threadIdx.x; i < V / 8; i += kSampNT) {
+      float x[8];
+      ld8(row, i, x);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) fn(i * 8 + j, x[j]);
+    }
+  } else {
+    for (int v = threadIdx.x; v < V; v += kSampNT) fn(v, ld(row, v));
+  }
+}
+
 constexpr int kBins = 2048;    // histogram bins per refinement level
 constexpr float kRange = 64.f;  // z = (x - max)/T in [-64, 0]; below: e^-64 relative mass, dropped
 
@@ -86,7 +122,7 @@ __device__ void suffix_scan(int* c, float* m, int* tc, float* tm) {
 
 // Histogram of the row's z over [lo, lo + w) into kBins bins (counts + exp masses), optionally
 // restricted to z >= floor_z.
-template <typename T>
+template <bool VEC, typename T>
 __device__ void histogram(const T* row, int V, float gmax, float inv_t, float lo, float w,
                           float floor_z, int* c, float* m) {
   for (int i = threadIdx.x; i < kBins; i += kSampNT) {
@@ -97,14 +133,14 @@ __device__ void histogram(const T* row, int V, float gmax, float inv_t, float lo
   const float sc = kBins / w;
   const float hi = lo + w;
   const bool top = hi >= 0.f;  // the top bin also holds z == 0 (the max itself)
-  for (int v = threadIdx.x; v < V; v += kSampNT) {
-    const float z = (ld(row, v) - gmax) * inv_t;
+  for_each_logit<VEC>(row, V, [&](int, float xv) {
+    const float z = (xv - gmax) * inv_t;
     if (z >= lo && (z < hi || (top && z <= 0.f)) && z >= floor_z) {
       const int b = min(kBins - 1, (int)((z - lo) * sc));
       atomicAdd(&c[b], 1);
       atomicAdd(&m[b], __expf(z));
     }
-  }
+  });
   __syncthreads();
 }
 
@@ -126,7 +162,7 @@ __device__ int find_bin_mass(const float* sm, float need, int* out) {
   return *out;
 }
 
-template <typename T>
+template <typename T, bool VEC>
 __global__ __launch_bounds__(kSampNT) void sample_kernel(const T* __restrict__ logits, int64_t ld_,
                                                           int V, float inv_temp, int top_k,
                                                           float top_p, bool greedy,
@@ -146,13 +182,12 @@ __global__ __launch_bounds__(kSampNT) void sample_kernel(const T* __restrict__ l
   // 1. max / argmax (first index on ties)
   float m = -INFINITY;
   int am = 0x7fffffff;
-  for (int v = tid; v < V; v += kSampNT) {
-    const float x = ld(row, v);
+  for_each_logit<VEC>(row, V, [&](int v, float x) {
     if (x > m) {
       m = x;
       am = v;
     }
-  }
+  });
   const float gmax = block_max<kSampNT>(m, sc);
   int cand = (m == gmax) ? am : 0x7fffffff;
 #pragma unroll
@@ -170,7 +205,7 @@ __global__ __launch_bounds__(kSampNT) void sample_kernel(const T* __restrict__ l
   const bool need_k = top_k > 0 && top_k < V, need_p = top_p < 1.f;
   if (need_k || need_p) {
     // 2. coarse histogram over [-64, 0]
-    histogram(row, V, gmax, inv_temp, -kRange, kRange, -INFINITY, hc, hm);
+    histogram<VEC>(row, V, gmax, inv_temp, -kRange, kRange, -INFINITY, hc, hm);
     suffix_scan(hc, hm, tc, tm);
     float total = hm[0];
     int kbin = 0;
@@ -189,7 +224,7 @@ __global__ __launch_bounds__(kSampNT) void sample_kernel(const T* __restrict__ l
       const float lo = -kRange + kbin * W;
       __syncthreads();
       // keep the coarse suffix mass of bins >= kbin+1 for the top-p search below
-      histogram(row, V, gmax, inv_temp, lo, W, -INFINITY, hc, hm);
+      histogram<VEC>(row, V, gmax, inv_temp, lo, W, -INFINITY, hc, hm);
       suffix_scan(hc, hm, tc, tm);
       const int sb = find_bin_count(hc, top_k - above_c, &sel);
       tau = lo + sb * (W / kBins);
@@ -206,31 +241,45 @@ __global__ __launch_bounds__(kSampNT) void sample_kernel(const T* __restrict__ l
         }
       }
     } else {
-      pbin = 1;
+      pbin = 2;  // no top-k floor: the coarse suffix sums above are already the right ones
       pbin_need = top_p * total;
     }
-    if (need_p && pbin == 1) {
-      // coarse pass restricted to z >= tau (the top-k floor), then refine
-      __syncthreads();
-      histogram(row, V, gmax, inv_temp, -kRange, kRange, tau, hc, hm);
-      suffix_scan(hc, hm, tc, tm);
+    if (need_p && pbin >= 1) {
+      if (pbin == 1) {  // coarse pass restricted to z >= tau (the top-k floor)
+        __syncthreads();
+        histogram<VEC>(row, V, gmax, inv_temp, -kRange, kRange, tau, hc, hm);
+        suffix_scan(hc, hm, tc, tm);
+      }
       const int cb = find_bin_mass(hm, pbin_need, &sel);
       const float above = cb + 1 < kBins ? hm[cb + 1] : 0.f;
       const float lo = -kRange + cb * W;
       __syncthreads();
-      histogram(row, V, gmax, inv_temp, lo, W, tau, hc, hm);
+      histogram<VEC>(row, V, gmax, inv_temp, lo, W, tau, hc, hm);
       suffix_scan(hc, hm, tc, tm);
       const int sp = find_bin_mass(hm, pbin_need - above, &sel);
       tau = fmaxf(tau, lo + sp * (W / kBins));
     }
   }
   // 4. categorical draw over {z >= tau}: contiguous segment per thread, block scan
-  const int per = (V + kSampNT - 1) / kSampNT;
-  const int s0 = tid * per, s1 = min(V, s0 + per);
+  // contiguous per-thread segments, in 8-element vectors when VEC
+  const int per = VEC ? ((V / 8 + kSampNT - 1) / kSampNT) * 8 : (V + kSampNT - 1) / kSampNT;
+  const int s0 = min(V, tid * per), s1 = min(V, s0 + per);
   float mine = 0.f;
-  for (int v = s0; v < s1; ++v) {
-    const float z = (ld(row, v) - gmax) * inv_temp;
-    mine += z >= tau ? __expf(z) : 0.f;
+  if constexpr (VEC) {
+    for (int v = s0; v < s1; v += 8) {
+      float x[8];
+      ld8(row, v / 8, x);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float z = (x[j] - gmax) * inv_temp;
+        mine += z >= tau ? __expf(z) : 0.f;
+      }
+    }
+  } else {
+    for (int v = s0; v < s1; ++v) {
+      const float z = (ld(row, v) - gmax) * inv_temp;
+      mine += z >= tau ? __expf(z) : 0.f;
+    }
   }
   tm[tid] = mine;
   if (tid == 0) ans = -1;
@@ -265,12 +314,19 @@ void launch_sample(const void* logits, bool is_bf16, int64_t ld_, int64_t rows, 
                    float inv_temp, int top_k, float top_p, bool greedy, const int64_t* rng,
                    int64_t* out, hipStream_t st) {
   if (rows == 0) return;
-  if (is_bf16)
-    sample_kernel<bf16_t><<<rows, kSampNT, 0, st>>>(static_cast<const bf16_t*>(logits), ld_, V,
-                                                     inv_temp, top_k, top_p, greedy, rng, out);
-  else
-    sample_kernel<float><<<rows, kSampNT, 0, st>>>(static_cast<const float*>(logits), ld_, V,
-                                                    inv_temp, top_k, top_p, greedy, rng, out);
+  const bool vec = V % 8 == 0 && ld_ % 8 == 0 &&
+                   reinterpret_cast<uintptr_t>(logits) % 16 == 0;
+#define DLA_SAMPLE(T, VV)                                                                         \
+  sample_kernel<T, VV><<<rows, kSampNT, 0, st>>>(static_cast<const T*>(logits), ld_, V, inv_temp, \
+                                                 top_k, top_p, greedy, rng, out)
+  if (is_bf16) {
+    if (vec) DLA_SAMPLE(bf16_t, true);
+    else DLA_SAMPLE(bf16_t, false);
+  } else {
+    if (vec) DLA_SAMPLE(float, true);
+    else DLA_SAMPLE(float, false);
+  }
+#undef DLA_SAMPLE
 }
 
 }  // namespace dla
