@@ -182,6 +182,9 @@ def _ckpt_resume(rank, world, d):
     loss, _ = dpo_step_loss(pol2, ref2, batches[2])
     loss.backward()
     eng2.step()
+    # ZeRO-1 all-gathers land asynchronously (awaited by the next forward's pre-hooks)
+    eng.wait_params()
+    eng2.wait_params()
     same = all(torch.equal(a, b) for a, b in zip(pol.parameters(), pol2.parameters()))
     return step, losses[2], loss.item(), same
 
