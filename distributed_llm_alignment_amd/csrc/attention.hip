@@ -6,23 +6,21 @@
 // 64 / 128. Scores never touch HBM; the forward stores only O and a per-row log2-domain
 // LSE, the backward recomputes P from it (FA2 scheme).
 //
-// Forward structure (block = 4 waves = 128 queries of one (batch, q-head); KV tile = 64 keys):
+// Forward (workgroup = 8 waves, two per SIMD = 256 queries of one (batch, q head); wave w owns
+// query rows 32w..32w+31; KV tile = 64 keys; cdna guide Appendix B "Fused attention prefill"):
 //   * "swapped" scores S^T = K Q^T: the query sits on the MFMA column (lane), keys on the
 //     16 accumulator registers, so each lane owns whole score columns -> the row max / sum is
 //     in-register + one xor-32 shuffle, and the alpha rescale of O^T is a per-lane scalar.
-//   * Q lives in registers for the whole kernel (B operand, 8 x 16 B per lane at D=128).
+//   * Q lives in registers for the whole kernel (B operand, 8 x 16 B per lane at D=128),
+//     pre-scaled by softmax_scale*log2(e) so the scores come out in the exp2 domain.
 //   * P^T feeds the PV MFMA straight from the accumulator (cdna guide §3 "accumulator tile as
 //     the next MFMA's operand"); V^T fragments come from ds_read_b64_tr_b16 transposed LDS reads.
-//   * K/V tiles are register-staged (global loads for tile t+1 issued before computing tile t,
-//     LDS write after the barrier: async-STAGE split), XOR-swizzled LDS image usable both for
-//     row (ds_read_b128) and transposed reads.
-// Backward structure (block = 4 waves = 128 keys of one (batch, kv-head); wave owns 32 keys):
-//   * loops over every q head of the GQA group x 32-query tiles; dK^T/dV^T for the wave's keys
-//     stay in accumulators for the whole sweep -> no cross-block reduction for dK/dV.
-//   * "key on the lane": S and dP are computed with keys on the lane, so P and dS are already
-//     the B operands of dV^T += dO^T P and dK^T += Q^T dS.
-//   * dS crosses LDS once (as a [key][query] image) for dQ += dS K, summed over the block's
-//     128 keys by MFMA, then added to an fp32 dQ accumulator with 128-B-segment atomics.
+//   * K/V tiles are double-buffered in LDS and register-staged one tile ahead (the global loads
+//     of tile t+2 are issued right after tile t+1's LDS write: async-STAGE split), so a tile
+//     costs one barrier; all 256 queries of the workgroup share each K/V tile.
+//   * XOR-swizzled LDS image usable both for row (ds_read_b128) and transposed reads.
+//   * query blocks are the slowest grid dimension, heaviest causal blocks first (LPT order).
+// Backward: see attn_bwd_kernel.
 #include "common.h"
 #include "attn_params.h"
 
@@ -41,7 +39,7 @@ __device__ __forceinline__ int swz(int row, int ch) {
   return row * D + ((ch ^ f) << 3);
 }
 
-// dS^T image [128 keys][32 queries] bf16 (64-B rows): 8-byte unit c4 of row `row`, XOR-swizzled
+// dS^T image [keys][32 queries] bf16 (64-B rows): 8-byte unit c4 of row `row`, XOR-swizzled
 // with row bits 2..4 so the 32 key rows written by a half-wave land on 32 distinct bank pairs
 // (unswizzled: 16-bank row stride -> 8-way conflicts; the swizzle is a per-row permutation, so
 // the ds_read_b64_tr_b16 reads of the dQ MFMA stay conflict-free).
@@ -55,8 +53,9 @@ __device__ __forceinline__ s16x8 cat4(s16x4 a, s16x4 b) {
   return s16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
 }
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
 __device__ __forceinline__ s16x8 pack8(const f32x16& x, int base) {
-  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   u32x4 r = {pack2bf(x[base], x[base + 1]), pack2bf(x[base + 2], x[base + 3]),
              pack2bf(x[base + 4], x[base + 5]), pack2bf(x[base + 6], x[base + 7])};
   return __builtin_bit_cast(s16x8, r);
@@ -96,23 +95,30 @@ __device__ __forceinline__ s16x8 tr_frag_nat(const bf16_t* img, int r0, int c0, 
 // ==============================================================================================
 // forward
 // ==============================================================================================
+constexpr int kFwdThreads = 512;  // 8 waves
+constexpr int kFwdRows = 256;     // queries per workgroup
+constexpr int kFwdKeys = 64;      // keys per K/V tile
+
 template <int D, bool CAUSAL>
-__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams p) {
-  constexpr int BQ = 128, BK = 64;
+__global__ __launch_bounds__(kFwdThreads) void attn_fwd_kernel(AttnParams p) {
+  constexpr int NT = kFwdThreads, BQ = kFwdRows, BK = kFwdKeys;
   constexpr int NCH = D / 8;
   constexpr int KS = D / 16;
   constexpr int DT = D / 32;
-  constexpr int CPT = BK * NCH / 256;  // 16-B chunks per thread per K (or V) tile
-  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * BK * D];
-  bf16_t* Ks = smem;
-  bf16_t* Vs = smem + BK * D;
+  constexpr int CPT = BK * NCH / NT;  // 16-B chunks per thread per K (or V) tile
+  static_assert(CPT >= 1, "K/V tile smaller than the workgroup");
+  __shared__ __attribute__((aligned(16))) bf16_t Kb[2][BK * D];
+  __shared__ __attribute__((aligned(16))) bf16_t Vb[2][BK * D];
 
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  // readfirstlane: the wave index is wave-uniform, so everything derived from it (key / query
+  // ranges, activity and mask flags) stays in SGPRs and its branches are scalar
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l32 = lane & 31, h = lane >> 5;
   const int nqb = (p.Tq + BQ - 1) / BQ;
+  const int nbh = p.Hq * p.B;
   const int bid = blockIdx.x;
-  const int qb = CAUSAL ? nqb - 1 - (bid % nqb) : bid % nqb;  // heaviest causal blocks first
-  const int rest = bid / nqb;
+  const int qb = CAUSAL ? nqb - 1 - bid / nbh : bid / nbh;
+  const int rest = bid % nbh;
   const int hq = rest % p.Hq, b = rest / p.Hq;
   const int hk = hq / (p.Hq / p.Hkv);
   const int q0 = qb * BQ + w * 32;
@@ -151,12 +157,13 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams p) {
   int kmin = kbeg;
   if (CAUSAL && p.window > 0) kmin = max(kmin, qb * BQ + p.causal_off - p.window + 1);
   const int tile0 = (max(kmin, 0) / BK) * BK;
+  const int ntiles = kmax > tile0 ? (kmax - tile0 + BK - 1) / BK : 0;
 
   bf16x8 kreg[CPT], vreg[CPT];
   auto gload = [&](int kt) {
 #pragma unroll
     for (int c = 0; c < CPT; ++c) {
-      const int ci = tid + 256 * c;
+      const int ci = tid + NT * c;
       const int row = ci / NCH, ch = ci % NCH;
       const int key = kt + row;
       if (key < p.Tk) {
@@ -168,104 +175,113 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnParams p) {
       }
     }
   };
-  auto lwrite = [&]() {
+  auto lwrite = [&](int buf) {
 #pragma unroll
     for (int c = 0; c < CPT; ++c) {
-      const int ci = tid + 256 * c;
+      const int ci = tid + NT * c;
       const int row = ci / NCH, ch = ci % NCH;
-      store_bf16x8(Ks + swz<D>(row, ch), kreg[c]);
-      store_bf16x8(Vs + swz<D>(row, ch), vreg[c]);
+      store_bf16x8(&Kb[buf][swz<D>(row, ch)], kreg[c]);
+      store_bf16x8(&Vb[buf][swz<D>(row, ch)], vreg[c]);
     }
   };
 
-  if (tile0 < kmax) gload(tile0);
-  for (int kt = tile0; kt < kmax; kt += BK) {
-    __syncthreads();
-    lwrite();
-    __syncthreads();
-    if (kt + BK < kmax) gload(kt + BK);
-
+  if (ntiles > 0) {
+    gload(tile0);
+    lwrite(0);
+    if (ntiles > 1) gload(tile0 + BK);
+  }
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    const int kt = tile0 + t * BK;
+    const bf16_t* Ks = Kb[t & 1];
+    const bf16_t* Vs = Vb[t & 1];
     bool active = q0 < p.Tq;
     if (CAUSAL) {
       active = active && (kt <= q0 + 31 + p.causal_off);
       if (p.window > 0) active = active && (kt + BK - 1 > q0 + p.causal_off - p.window);
     }
-    if (!active) continue;  // wave-uniform
-
-    f32x16 sacc[2];
+    if (active) {  // wave-uniform
+      f32x16 sacc[2];
 #pragma unroll
-    for (int st = 0; st < 2; ++st) {
-      sacc[st] = f32x16{};
+      for (int st = 0; st < 2; ++st) {
+        sacc[st] = f32x16{};
 #pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        const s16x8 a = *reinterpret_cast<const s16x8*>(Ks + swz<D>(32 * st + l32, 2 * s + h));
-        sacc[st] = mfma32(a, qf[s], sacc[st]);
+        for (int s = 0; s < KS; ++s) {
+          const s16x8 a = *reinterpret_cast<const s16x8*>(Ks + swz<D>(32 * st + l32, 2 * s + h));
+          sacc[st] = mfma32(a, qf[s], sacc[st]);
+        }
       }
-    }
-    // mask only tiles that touch a boundary (kv range, causal diagonal, window edge)
-    bool need_mask = kt < kbeg || kt + BK > kend;
-    if (CAUSAL) {
-      need_mask = need_mask || (kt + BK - 1 > q0 + p.causal_off);
-      if (p.window > 0) need_mask = need_mask || (kt <= q0 + 31 + p.causal_off - p.window);
-    }
-    if (need_mask) {
+      // mask only tiles that touch a boundary (kv range, causal diagonal, window edge)
+      bool need_mask = kt < kbeg || kt + BK > kend;
+      if (CAUSAL) {
+        need_mask = need_mask || (kt + BK - 1 > q0 + p.causal_off);
+        if (p.window > 0) need_mask = need_mask || (kt <= q0 + 31 + p.causal_off - p.window);
+      }
+      if (need_mask) {
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int key = kt + 32 * st + (i & 3) + 8 * (i >> 2) + 4 * h;
+            bool ok = key >= kbeg && key < kend;
+            if (CAUSAL) {
+              ok = ok && key <= qi + p.causal_off;
+              if (p.window > 0) ok = ok && key > qi + p.causal_off - p.window;
+            }
+            sacc[st][i] = ok ? sacc[st][i] : -INFINITY;
+          }
+        }
+      }
+      float mloc = -INFINITY;
+#pragma unroll
+      for (int st = 0; st < 2; ++st)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) mloc = fmaxf(mloc, sacc[st][i]);
+      mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+      // deferred max: rescale O only when some row's max grew by more than kRescaleThr (the
+      // previous tile's P.V is complete, and this tile's P is exponentiated after the decision)
+      if (!__all(mloc <= m + kRescaleThr)) {
+        const float mnew = fmaxf(m, mloc);
+        const float alpha = ex2(m - (mnew == -INFINITY ? 0.f : mnew));
+        m = mnew;
+        lsum *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
+      }
+      const float muse = m == -INFINITY ? 0.f : m;
 #pragma unroll
       for (int st = 0; st < 2; ++st) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          const int key = kt + 32 * st + (i & 3) + 8 * (i >> 2) + 4 * h;
-          bool ok = key >= kbeg && key < kend;
-          if (CAUSAL) {
-            ok = ok && key <= qi + p.causal_off;
-            if (p.window > 0) ok = ok && key > qi + p.causal_off - p.window;
-          }
-          sacc[st][i] = ok ? sacc[st][i] : -INFINITY;
+          const float pv = ex2(sacc[st][i] - muse);
+          sacc[st][i] = pv;
+          lsum += pv;
         }
       }
-    }
-    float mloc = -INFINITY;
-#pragma unroll
-    for (int st = 0; st < 2; ++st)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) mloc = fmaxf(mloc, sacc[st][i]);
-    mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
-    // deferred max: rescale O only when some row's max grew by more than kRescaleThr
-    if (!__all(mloc <= m + kRescaleThr)) {
-      const float mnew = fmaxf(m, mloc);
-      const float alpha = ex2(m - (mnew == -INFINITY ? 0.f : mnew));
-      m = mnew;
-      lsum *= alpha;
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
-    }
-    const float muse = m == -INFINITY ? 0.f : m;
-#pragma unroll
-    for (int st = 0; st < 2; ++st) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float pv = ex2(sacc[st][i] - muse);
-        sacc[st][i] = pv;
-        lsum += pv;
-      }
-    }
-    s16x8 pf[2][2];
-#pragma unroll
-    for (int st = 0; st < 2; ++st) {
-      pf[st][0] = pack8(sacc[st], 0);
-      pf[st][1] = pack8(sacc[st], 8);
-    }
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) {
-      const int c0 = 32 * dt + 16 * ((lane >> 4) & 1);
+      s16x8 pf[2][2];
 #pragma unroll
       for (int st = 0; st < 2; ++st) {
+        pf[st][0] = pack8(sacc[st], 0);
+        pf[st][1] = pack8(sacc[st], 8);
+      }
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          const s16x8 a = tr_frag_perm<D>(Vs, 32 * st + 16 * s + 4 * h, c0, lane);
-          o[dt] = mfma32(a, pf[st][s], o[dt]);
+      for (int dt = 0; dt < DT; ++dt) {
+        const int c0 = 32 * dt + 16 * ((lane >> 4) & 1);
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            const s16x8 a = tr_frag_perm<D>(Vs, 32 * st + 16 * s + 4 * h, c0, lane);
+            o[dt] = mfma32(a, pf[st][s], o[dt]);
+          }
         }
       }
     }
+    if (t + 1 < ntiles) {  // stage tile t+1 into the other buffer, prefetch tile t+2
+      lwrite((t + 1) & 1);
+      if (t + 2 < ntiles) gload(kt + 2 * BK);
+    }
+    __syncthreads();
   }
 
   lsum += __shfl_xor(lsum, 32, 64);
@@ -324,76 +340,98 @@ __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(const bf16_t* __res
 // ==============================================================================================
 // backward main kernel
 // ==============================================================================================
+// Query tiles [qt0, qend) swept by the workgroup that owns keys [k0, k0 + 256): every query
+// that can see one of its keys. Shared by the main kernel and the dQ reduce pass (which must
+// know exactly which slab rows a key block wrote).
+template <bool CAUSAL>
+__device__ __forceinline__ void bwd_q_range(int k0, int Tq, int causal_off, int window, int& qt0,
+                                            int& qend) {
+  int qlo = 0, qhi = Tq;
+  if (CAUSAL) {
+    qlo = max(0, k0 - causal_off);
+    if (window > 0) qhi = min(qhi, k0 + kAttnBwdKeys - 1 - causal_off + window);
+  }
+  qt0 = (qlo / kAttnBwdQRows) * kAttnBwdQRows;
+  qend = max(qhi, qt0);
+}
+
+// Workgroup = 4 waves, ONE per SIMD (the 512-register budget holds the accumulators) = 256 keys
+// of one (batch, kv head) and Hq/Hkv/hsplit of its query heads. Wave w owns keys
+// k0 + 64w .. +63 as two 32-key sub-tiles and keeps dK^T / dV^T of all 64 in accumulators (256
+// registers at D = 128) for the whole sweep over (head, 32-query tile), so dK/dV need no
+// cross-workgroup sum (cdna guide Appendix B "Attention backward"). Per query tile:
+//   phase A, per sub-tile: S = Q K^T and dP = dO V^T with the key on the lane (K, V rows of the
+//     wave's keys and the Q / dO tile from LDS); p = exp2(scale2*S - lse2), dS = p (dP - delta)
+//     with the row constants read straight from L2 while the MFMA chains run; dV^T += dO^T P
+//     and dK^T += Q^T dS from transposed LDS reads (P and dS are already the B operands);
+//     dS^T -> LDS.
+//   barrier
+//   phase B: the next Q / dO tile (register-prefetched one tile ahead) is staged into LDS, and
+//     wave w computes dQ[32 q][32w .. 32w+31] = scale * dS K over all 256 keys and stores it
+//     into this key block's fp32 slab row. Plain stores, no atomics: the reduce pass sums the
+//     <= ceil(Tk/256) slabs of each row in key-block order, so dQ is deterministic and the
+//     chip-wide float-atomic rate is no floor (it was for the earlier 128-key atomic version).
+//   barrier
+// LDS at D = 128: K 64 KB + V 64 KB + Q 8 KB + dO 8 KB + dS 16 KB = the full 160 KB.
+// Every LDS read address is one of ~26 lane offsets computed once plus a wave-uniform or
+// compile-time row offset (the swizzles are periodic): with one address register per unrolled
+// read the kernel spilled, the dK/dV accumulators holding the whole AGPR file.
 template <int D, bool CAUSAL>
 __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnBwdParams p) {
-  constexpr int BKV = 128, BQ = 32;
+  constexpr int BKV = kAttnBwdKeys, BQ = kAttnBwdQRows;
   constexpr int NCH = D / 8;
   constexpr int KS = D / 16;
   constexpr int DT = D / 32;
-  // LDS: K [128][D], V [128][D], Q [32][D], dO [32][D]; dS^T [128][32] aliases Q+dO
-  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * BKV * D + 2 * BQ * D];
-  bf16_t* Ks = smem;
-  bf16_t* Vs = smem + BKV * D;
-  bf16_t* Qs = smem + 2 * BKV * D;
-  bf16_t* dOs = Qs + BQ * D;
-  bf16_t* dSs = Qs;  // [128 keys][32 queries], 64-B rows (needs 8 KB = Q+dO region for D>=64)
+  constexpr int QCPT = BQ * NCH / 256;  // 16-B chunks per thread per [32][D] tile
+  static_assert(QCPT >= 1 && BKV == 256 && BQ == 32, "tile geometry");
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[BKV * D];
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[BKV * D];
+  __shared__ __attribute__((aligned(16))) bf16_t Qs[BQ * D];
+  __shared__ __attribute__((aligned(16))) bf16_t dOs[BQ * D];
+  __shared__ __attribute__((aligned(16))) bf16_t dSs[BKV * BQ];
 
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  // readfirstlane: the wave index is wave-uniform, so everything derived from it (key / query
+  // ranges, activity and mask flags) stays in SGPRs and its branches are scalar
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l32 = lane & 31, h = lane >> 5;
-  const int nkb = (p.Tk + BKV - 1) / BKV;
-  const int bid = blockIdx.x;
-  const int kb = bid % nkb;
-  const int rest = bid / nkb;
-  const int hk = rest % p.Hkv, b = rest / p.Hkv;
   const int group = p.Hq / p.Hkv;
+  const int hpb = group / p.hsplit;  // query heads per workgroup
+  const int nrest = p.Hkv * p.B * p.hsplit;
+  const int kb = static_cast<int>(blockIdx.x) / nrest;  // key blocks outermost: heaviest first
+  int rest = static_cast<int>(blockIdx.x) - kb * nrest;
+  const int sidx = rest % p.hsplit;
+  rest /= p.hsplit;
+  const int hk = rest % p.Hkv, b = rest / p.Hkv;
   const int k0 = kb * BKV;
-  const int kw = k0 + 32 * w;  // this wave's first key
-  const int kj = kw + l32;     // key on this lane
-
+  const int kw = k0 + 64 * w;  // this wave's first key
   const int kbeg = p.kv_start ? p.kv_start[b] : 0;
   const int kend = p.kv_end ? p.kv_end[b] : p.Tk;
 
-  // stage K, V tiles (zero rows past Tk)
-  {
+  {  // K and V blocks -> LDS (rows past Tk zeroed)
     const bf16_t* kp = p.k + b * p.k_sb + static_cast<int64_t>(hk) * p.k_sh;
     const bf16_t* vp = p.v + b * p.v_sb + static_cast<int64_t>(hk) * p.v_sh;
-    for (int ci = tid; ci < BKV * NCH; ci += 256) {
+#pragma unroll 4
+    for (int c = 0; c < BKV * NCH / 256; ++c) {
+      const int ci = tid + 256 * c;
       const int row = ci / NCH, ch = ci % NCH;
       const int key = k0 + row;
-      bf16x8 kv = key < p.Tk ? load_bf16x8(kp + key * p.k_st + ch * 8) : bf16x8{};
-      bf16x8 vv = key < p.Tk ? load_bf16x8(vp + key * p.v_st + ch * 8) : bf16x8{};
-      store_bf16x8(Ks + swz<D>(row, ch), kv);
-      store_bf16x8(Vs + swz<D>(row, ch), vv);
+      const bool in = key < p.Tk;
+      store_bf16x8(Ks + swz<D>(row, ch), in ? load_bf16x8(kp + key * p.k_st + ch * 8) : bf16x8{});
+      store_bf16x8(Vs + swz<D>(row, ch), in ? load_bf16x8(vp + key * p.v_st + ch * 8) : bf16x8{});
     }
   }
 
-  f32x16 dk[DT], dv[DT];
-#pragma unroll
-  for (int dt = 0; dt < DT; ++dt) {
-    dk[dt] = f32x16{};
-    dv[dt] = f32x16{};
-  }
-
-  // query range that can see any key of this block
-  int qlo = 0, qhi = p.Tq;  // [qlo, qhi)
-  if (CAUSAL) {
-    qlo = max(0, k0 - p.causal_off);
-    if (p.window > 0) qhi = min(qhi, k0 + BKV - 1 - p.causal_off + p.window);
-  }
+  int qt0, qend;
+  bwd_q_range<CAUSAL>(k0, p.Tq, p.causal_off, p.window, qt0, qend);
+  const int nqt = (qend - qt0 + BQ - 1) / BQ;
   const bool block_has_keys = k0 < kend && k0 + BKV > kbeg;
-  const int qt0 = (qlo / BQ) * BQ;
+  const int n_iter = block_has_keys ? hpb * nqt : 0;
+  const int hq0 = hk * group + sidx * hpb;
 
-  constexpr int QCPT = BQ * NCH / 256;  // chunks per thread for a [32][D] tile (D=128 -> 2)
-  __shared__ float rowc[2][BQ];           // per-query lse2 / delta of the current tile
-  const int nqt = qhi > qt0 ? (qhi - qt0 + BQ - 1) / BQ : 0;
-  const int n_iter = block_has_keys ? group * nqt : 0;
-  const int64_t dq_st = static_cast<int64_t>(p.Hq) * D;
-
-  // register prefetch of the NEXT (head, q-tile) while the current one is computed (T14)
+  // register prefetch of the next (head, q-tile)'s Q and dO rows
   bf16x8 qreg[QCPT], dreg[QCPT];
-  float rreg = 0.f;
   auto prefetch = [&](int it) {
-    const int hq = hk * group + it / nqt;
+    const int hq = hq0 + it / nqt;
     const int qt = qt0 + (it % nqt) * BQ;
     const bf16_t* qp = p.q + b * p.q_sb + static_cast<int64_t>(hq) * p.q_sh;
     const bf16_t* dop = p.dout + b * p.do_sb + static_cast<int64_t>(hq) * p.do_sh;
@@ -405,19 +443,8 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnBwdParams p) {
       qreg[c] = qq < p.Tq ? load_bf16x8(qp + qq * p.q_st + ch * 8) : bf16x8{};
       dreg[c] = qq < p.Tq ? load_bf16x8(dop + qq * p.do_st + ch * 8) : bf16x8{};
     }
-    if (tid < 2 * BQ) {
-      const int qq = qt + (tid & (BQ - 1));
-      const float* src = (tid < BQ ? p.lse2 : p.delta) + (static_cast<int64_t>(b) * p.Hq + hq) * p.Tq;
-      rreg = qq < p.Tq ? src[qq] : 0.f;
-    }
   };
-  if (n_iter > 0) prefetch(0);
-
-  for (int it = 0; it < n_iter; ++it) {
-    const int hq = hk * group + it / nqt;
-    const int qt = qt0 + (it % nqt) * BQ;
-    float* dqp = p.dq + (static_cast<int64_t>(b) * p.Tq) * p.Hq * D + static_cast<int64_t>(hq) * D;
-    __syncthreads();  // previous iteration finished with Qs/dOs/dSs/rowc
+  auto stage = [&]() {
 #pragma unroll
     for (int c = 0; c < QCPT; ++c) {
       const int ci = tid + 256 * c;
@@ -425,194 +452,330 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnBwdParams p) {
       store_bf16x8(Qs + swz<D>(row, ch), qreg[c]);
       store_bf16x8(dOs + swz<D>(row, ch), dreg[c]);
     }
-    if (tid < 2 * BQ) rowc[tid / BQ][tid & (BQ - 1)] = rreg;
-    __syncthreads();
-    if (it + 1 < n_iter) prefetch(it + 1);
+  };
 
-    // does this wave's key slice see any query of the tile? (wave-uniform)
-    bool wave_active = kw < kend && kw + 32 > kbeg;
-    bool need_mask = kw < kbeg || kw + 32 > kend || qt + BQ > p.Tq;
-    if (CAUSAL) {
-      wave_active = wave_active && kw <= qt + BQ - 1 + p.causal_off;
-      need_mask = need_mask || (kw + 31 > qt + p.causal_off);
-      if (p.window > 0) {
-        wave_active = wave_active && (kw + 31 > qt + p.causal_off - p.window);
-        need_mask = need_mask || (kw <= qt + BQ - 1 + p.causal_off - p.window);
-      }
+  // Lane-dependent LDS offsets (elements), computed once. swz is periodic in 16 rows and ds_off
+  // in 32 rows, so every read below is one of these + a wave-uniform / compile-time row offset.
+  const int i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3, half16 = (lane >> 4) & 1;
+  int roff[KS];  // row reads: row l32 (+16k), chunk 2s + h
+#pragma unroll
+  for (int s = 0; s < KS; ++s) roff[s] = swz<D>(l32, 2 * s + h);
+  int toff[DT][2];  // tr_frag_perm: rows 4h + qq and 4h + 8 + qq (+16k), columns 32dt + 16*half16
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) {
+    const int ch = 4 * dt + 2 * half16 + (pp >> 1), sub = (pp & 1) * 4;
+    toff[dt][0] = swz<D>(4 * h + qq, ch) + sub;
+    toff[dt][1] = swz<D>(4 * h + 8 + qq, ch) + sub;
+  }
+  int noff[2];  // phase B K reads (tr_frag_nat): rows 8h + qq and 8h + 4 + qq (+16s), dt = w
+  {
+    const int ch = 4 * (w % DT) + 2 * half16 + (pp >> 1), sub = (pp & 1) * 4;
+    noff[0] = swz<D>(8 * h + qq, ch) + sub;
+    noff[1] = swz<D>(8 * h + 4 + qq, ch) + sub;
+  }
+  int doff[2][2];  // phase B dS^T reads: rows 16*par + 8h + qq (+4) (+32k), query unit colc4
+  {
+    const int colc4 = (16 * half16 + 4 * pp) >> 2;
+#pragma unroll
+    for (int par = 0; par < 2; ++par) {
+      doff[par][0] = ds_off(16 * par + 8 * h + qq, colc4);
+      doff[par][1] = ds_off(16 * par + 8 * h + 4 + qq, colc4);
     }
-    f32x16 sacc = f32x16{}, dpacc = f32x16{};
-    if (wave_active) {
-      // row constants of this lane's 16 accumulator rows r = (i&3) + 8(i>>2) + 4h: 4 x 16-B LDS
-      // reads each for lse2 / delta, issued ahead of the MFMA chain so their latency hides
-      float lr[16], dl[16];
+  }
+  int woff[4];  // dS^T writes: row l32 (+32k), 8-byte units 2g + h
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const f32x4 a = *reinterpret_cast<const f32x4*>(&rowc[0][8 * j + 4 * h]);
-        const f32x4 c = *reinterpret_cast<const f32x4*>(&rowc[1][8 * j + 4 * h]);
+  for (int g = 0; g < 4; ++g) woff[g] = ds_off(l32, 2 * g + h);
+
+  f32x16 dk[2][DT], dv[2][DT];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          lr[4 * j + t] = a[t];
-          dl[4 * j + t] = c[t];
-        }
-      }
-      // S (rows = queries, cols = this wave's keys) and dP = dO V^T; operand fragments are
-      // double-buffered one k-step ahead so no MFMA waits on its own LDS read
-      s16x8 fa[2], fb[2], fc[2], fd[2];
-      auto ld_sdp = [&](int ks, int sl) {
-        fa[sl] = *reinterpret_cast<const s16x8*>(Qs + swz<D>(l32, 2 * ks + h));
-        fb[sl] = *reinterpret_cast<const s16x8*>(Ks + swz<D>(32 * w + l32, 2 * ks + h));
-        fc[sl] = *reinterpret_cast<const s16x8*>(dOs + swz<D>(l32, 2 * ks + h));
-        fd[sl] = *reinterpret_cast<const s16x8*>(Vs + swz<D>(32 * w + l32, 2 * ks + h));
-      };
-      ld_sdp(0, 0);
+  for (int j = 0; j < 2; ++j) {
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        if (ks + 1 < KS) ld_sdp(ks + 1, (ks + 1) & 1);
-        sacc = mfma32(fa[ks & 1], fb[ks & 1], sacc);
-        dpacc = mfma32(fc[ks & 1], fd[ks & 1], dpacc);
-      }
-      // P and dS; masking is branch-free: per lane, key kj vs query qt + rr + 4h
-      const int dlt = kj - qt - p.causal_off - 4 * h;  // causal: visible iff rr >= dlt
-      const int rlim = p.Tq - qt - 4 * h;              // rr < rlim
-      const bool lane_ok = kj >= kbeg && kj < kend;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int rr = (i & 3) + 8 * (i >> 2);
-        float pv = ex2(fmaf(sacc[i], p.scale2, -lr[i]));
-        if (need_mask) {
-          bool ok = lane_ok && rr < rlim;
-          if (CAUSAL) {
-            ok = ok && rr >= dlt;
-            if (p.window > 0) ok = ok && rr < dlt + p.window;
-          }
-          pv = ok ? pv : 0.f;
-        }
-        sacc[i] = pv;
-        dpacc[i] = pv * (dpacc[i] - dl[i]);
-      }
-      const s16x8 pb0 = pack8(sacc, 0), pb1 = pack8(sacc, 8);
-      const s16x8 sb0 = pack8(dpacc, 0), sb1 = pack8(dpacc, 8);
-      // dV^T += dO^T P ; dK^T += Q^T dS   (k = query, permuted accumulator-row order); the four
-      // transposed fragments of tile dt+1 are read while tile dt's MFMAs run
-      s16x8 ta[2], tb[2], tc[2], td[2];
-      auto ld_kv = [&](int dt, int sl) {
-        const int c0 = 32 * dt + 16 * ((lane >> 4) & 1);
-        ta[sl] = tr_frag_perm<D>(dOs, 4 * h, c0, lane);
-        tb[sl] = tr_frag_perm<D>(dOs, 16 + 4 * h, c0, lane);
-        tc[sl] = tr_frag_perm<D>(Qs, 4 * h, c0, lane);
-        td[sl] = tr_frag_perm<D>(Qs, 16 + 4 * h, c0, lane);
-      };
-      ld_kv(0, 0);
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt) {
-        if (dt + 1 < DT) ld_kv(dt + 1, (dt + 1) & 1);
-        dv[dt] = mfma32(ta[dt & 1], pb0, dv[dt]);
-        dv[dt] = mfma32(tb[dt & 1], pb1, dv[dt]);
-        dk[dt] = mfma32(tc[dt & 1], sb0, dk[dt]);
-        dk[dt] = mfma32(td[dt & 1], sb1, dk[dt]);
-      }
-    }
-    __syncthreads();  // everyone done reading Qs/dOs
-    // dS^T image [key 0..127][query 0..31], 64-B rows: lane writes its key row,
-    // 4 groups of 4 consecutive queries (8 B each).
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      const int row = 32 * w + l32;
-      uint2 pk;
-      pk.x = pack2bf(dpacc[4 * g4 + 0], dpacc[4 * g4 + 1]);
-      pk.y = pack2bf(dpacc[4 * g4 + 2], dpacc[4 * g4 + 3]);
-      *reinterpret_cast<uint2*>(dSs + ds_off(row, 2 * g4 + h)) = pk;
-    }
-    __syncthreads();
-    // dQ[q][d] for d in this wave's slices: sum over 128 keys. A = dS (q rows, keys k) via
-    // transposed reads of dS^T; B = K (keys, d cols) via transposed reads of K.
-    for (int dt = w; dt < DT; dt += 4) {
-      f32x16 dqacc = f32x16{};
-      const int i16 = lane & 15, qq2 = i16 >> 2, pp = i16 & 3;
-      const int colc4 = (16 * ((lane >> 4) & 1) + 4 * pp) >> 2;  // query column block (8-B unit)
-      s16x8 qa[2], qb[2];
-      auto ld_dq = [&](int ks, int sl) {
-        const int r0 = 16 * ks + 8 * h;
-        qa[sl] = cat4(tr_read(dSs + ds_off(r0 + qq2, colc4)), tr_read(dSs + ds_off(r0 + 4 + qq2, colc4)));
-        qb[sl] = tr_frag_nat<D>(Ks, r0, 32 * dt + 16 * ((lane >> 4) & 1), lane);
-      };
-      ld_dq(0, 0);
-#pragma unroll
-      for (int ks = 0; ks < BKV / 16; ++ks) {
-        if (ks + 1 < BKV / 16) ld_dq(ks + 1, (ks + 1) & 1);
-        dqacc = mfma32(qa[ks & 1], qb[ks & 1], dqacc);
-      }
-      // accumulate: lane holds d = 32dt + l32 (col), rows q = qt + (i&3) + 8(i>>2) + 4h.
-      // Buffer atomics: the per-row offset is a scalar (soffset), one VGPR holds the lane part,
-      // and the descriptor's num_records ends at the last valid query row of this tile, so the
-      // hardware drops rows >= Tq (no per-element compares, no 64-bit address per element).
-      {
-        const int nrow = p.Tq - qt;  // > 0
-        float* base = dqp + static_cast<int64_t>(qt) * dq_st;
-        const int nrec = ((nrow - 1) * static_cast<int>(dq_st) + D) * 4;
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, nrec, 0x00020000);
-        const int voff = ((4 * h) * static_cast<int>(dq_st) + 32 * dt + l32) * 4;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int soff = ((i & 3) + 8 * (i >> 2)) * static_cast<int>(dq_st) * 4;
-          __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(dqacc[i] * p.scale, rs, voff, soff, 0);
-        }
-      }
+    for (int dt = 0; dt < DT; ++dt) {
+      dk[j][dt] = f32x16{};
+      dv[j][dt] = f32x16{};
     }
   }
 
-  // write dK (scaled) and dV: lane = key kj, regs = d rows (i&3) + 8(i>>2) + 4h of tile dt
-  if (kj < p.Tk) {
-    bf16_t* dkp = p.dk + b * p.dk_sb + kj * p.dk_st + static_cast<int64_t>(hk) * p.dk_sh;
-    bf16_t* dvp = p.dv + b * p.dv_sb + kj * p.dv_st + static_cast<int64_t>(hk) * p.dv_sh;
+  if (n_iter > 0) {
+    prefetch(0);
+    stage();
+    if (n_iter > 1) prefetch(1);
+  }
+  __syncthreads();
+
+  for (int it = 0; it < n_iter; ++it) {
+    const int hq = hq0 + it / nqt;
+    const int qt = qt0 + (it % nqt) * BQ;
+
+    // row constants of this lane's 16 accumulator rows r = (i&3) + 8(i>>2) + 4h, from L2; they
+    // are first needed after the sub-tile-0 MFMA chains
+    float lr[16], dl[16];
+    {
+      const int64_t rb = (static_cast<int64_t>(b) * p.Hq + hq) * p.Tq + qt + 4 * h;
+      const int rlim = p.Tq - qt - 4 * h;
 #pragma unroll
-    for (int dt = 0; dt < DT; ++dt) {
+      for (int i = 0; i < 16; ++i) {
+        const int r = (i & 3) + 8 * (i >> 2);
+        lr[i] = r < rlim ? p.lse2[rb + r] : INFINITY;  // rows past Tq: p = 0
+        dl[i] = r < rlim ? p.delta[rb + r] : 0.f;
+      }
+    }
+
+    // ---------------------------------------------------------------- phase A (per sub-tile)
 #pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int d = 32 * dt + 8 * g4 + 4 * h;
-        uint2 a, c;
-        a.x = pack2bf(dk[dt][4 * g4] * p.scale, dk[dt][4 * g4 + 1] * p.scale);
-        a.y = pack2bf(dk[dt][4 * g4 + 2] * p.scale, dk[dt][4 * g4 + 3] * p.scale);
-        c.x = pack2bf(dv[dt][4 * g4], dv[dt][4 * g4 + 1]);
-        c.y = pack2bf(dv[dt][4 * g4 + 2], dv[dt][4 * g4 + 3]);
-        *reinterpret_cast<uint2*>(dkp + d) = a;
-        *reinterpret_cast<uint2*>(dvp + d) = c;
+    for (int j = 0; j < 2; ++j) {
+      const int kj0 = kw + 32 * j;
+      // does this sub-tile see any query of the tile? which masks apply? (wave-uniform)
+      bool act = kj0 < kend && kj0 + 32 > kbeg;
+      bool need_mask = kj0 < kbeg || kj0 + 32 > kend || qt + BQ > p.Tq;
+      if (CAUSAL) {
+        act = act && kj0 <= qt + BQ - 1 + p.causal_off;
+        need_mask = need_mask || (kj0 + 31 > qt + p.causal_off);
+        if (p.window > 0) {
+          act = act && (kj0 + 31 > qt + p.causal_off - p.window);
+          need_mask = need_mask || (kj0 <= qt + BQ - 1 + p.causal_off - p.window);
+        }
+      }
+      // P / dS fragments (zero for an inactive sub-tile). Only these cross the branch: the dK / dV
+      // MFMAs below run unconditionally, since accumulators updated under a branch get phi
+      // copies, which for 256 accumulator registers means spilling every iteration.
+      s16x8 pb0 = {}, pb1 = {}, sb0 = {}, sb1 = {};
+      if (act) {
+        // S (rows = queries, cols = this sub-tile's keys) and dP = dO V^T; operand fragments
+        // double-buffered one k-step ahead
+        f32x16 sacc = f32x16{}, dpacc = f32x16{};
+        const bf16_t* Kj = Ks + (64 * w + 32 * j) * D;
+        const bf16_t* Vj = Vs + (64 * w + 32 * j) * D;
+        s16x8 fa[2], fb[2], fc[2], fd[2];
+        auto ld_sdp = [&](int s, int sl) {
+          fa[sl] = *reinterpret_cast<const s16x8*>(Qs + roff[s]);
+          fb[sl] = *reinterpret_cast<const s16x8*>(Kj + roff[s]);
+          fc[sl] = *reinterpret_cast<const s16x8*>(dOs + roff[s]);
+          fd[sl] = *reinterpret_cast<const s16x8*>(Vj + roff[s]);
+        };
+        ld_sdp(0, 0);
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          if (s + 1 < KS) ld_sdp(s + 1, (s + 1) & 1);
+          sacc = mfma32(fa[s & 1], fb[s & 1], sacc);
+          dpacc = mfma32(fc[s & 1], fd[s & 1], dpacc);
+        }
+        // P and dS; masking is branch-free: per lane, key kj vs query qt + rr + 4h
+        const int kj = kj0 + l32;
+        const int dlt = kj - qt - p.causal_off - 4 * h;  // causal: visible iff rr >= dlt
+        const int rlim = p.Tq - qt - 4 * h;              // rr < rlim
+        const bool lane_ok = kj >= kbeg && kj < kend;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int rr = (i & 3) + 8 * (i >> 2);
+          float pv = ex2(fmaf(sacc[i], p.scale2, -lr[i]));
+          if (need_mask) {
+            bool ok = lane_ok && rr < rlim;
+            if (CAUSAL) {
+              ok = ok && rr >= dlt;
+              if (p.window > 0) ok = ok && rr < dlt + p.window;
+            }
+            pv = ok ? pv : 0.f;
+          }
+          sacc[i] = pv;
+          dpacc[i] = pv * (dpacc[i] - dl[i]);
+        }
+        pb0 = pack8(sacc, 0);
+        pb1 = pack8(sacc, 8);
+        sb0 = pack8(dpacc, 0);
+        sb1 = pack8(dpacc, 8);
+      }
+      {
+        // dV^T += dO^T P ; dK^T += Q^T dS   (k = query in the accumulator's permuted row order);
+        // the four transposed fragments of tile dt+1 are read while tile dt's MFMAs run
+        s16x8 ta[2], tb[2], tc[2], td[2];
+        auto ld_kv = [&](int dt, int sl) {  // tr_frag_perm of rows 4h.. / 16+4h.., column tile dt
+          ta[sl] = cat4(tr_read(dOs + toff[dt][0]), tr_read(dOs + toff[dt][1]));
+          tb[sl] = cat4(tr_read(dOs + 16 * D + toff[dt][0]), tr_read(dOs + 16 * D + toff[dt][1]));
+          tc[sl] = cat4(tr_read(Qs + toff[dt][0]), tr_read(Qs + toff[dt][1]));
+          td[sl] = cat4(tr_read(Qs + 16 * D + toff[dt][0]), tr_read(Qs + 16 * D + toff[dt][1]));
+        };
+        ld_kv(0, 0);
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          if (dt + 1 < DT) ld_kv(dt + 1, (dt + 1) & 1);
+          dv[j][dt] = mfma32(ta[dt & 1], pb0, dv[j][dt]);
+          dv[j][dt] = mfma32(tb[dt & 1], pb1, dv[j][dt]);
+          dk[j][dt] = mfma32(tc[dt & 1], sb0, dk[j][dt]);
+          dk[j][dt] = mfma32(td[dt & 1], sb1, dk[j][dt]);
+        }
+      }
+      // dS^T rows of this sub-tile -> [key][32 queries] image: accumulator rows 4g..4g+3 are
+      // queries 8g + 4h + 0..3, i.e. 8-byte unit 2g + h of the key's row
+      const u32x4 ds0 = __builtin_bit_cast(u32x4, sb0), ds1 = __builtin_bit_cast(u32x4, sb1);
+      bf16_t* dSw = dSs + (64 * w + 32 * j) * 32;
+      *reinterpret_cast<uint2*>(dSw + woff[0]) = make_uint2(ds0[0], ds0[1]);
+      *reinterpret_cast<uint2*>(dSw + woff[1]) = make_uint2(ds0[2], ds0[3]);
+      *reinterpret_cast<uint2*>(dSw + woff[2]) = make_uint2(ds1[0], ds1[1]);
+      *reinterpret_cast<uint2*>(dSw + woff[3]) = make_uint2(ds1[2], ds1[3]);
+    }
+    __syncthreads();  // dS visible; every wave is done reading this Q / dO tile
+
+    // ---------------------------------------------------------------- phase B
+    if (it + 1 < n_iter) {  // stage the next tile, prefetch the one after it
+      stage();
+      if (it + 2 < n_iter) prefetch(it + 2);
+    }
+    if (w < DT) {  // dQ partial; D = 64: waves 2, 3 have no column slice
+      const int dt = w;
+      f32x16 acc = f32x16{};
+      s16x8 qa[2], qb[2];
+      auto ld_dq = [&](int s, int sl) {  // A = dS (rows 16s + 8h..), B = K (rows 16s + 8h..)
+        const bf16_t* dsr = dSs + (s >> 1) * 32 * 32;
+        qa[sl] = cat4(tr_read(dsr + doff[s & 1][0]), tr_read(dsr + doff[s & 1][1]));
+        qb[sl] = cat4(tr_read(Ks + 16 * s * D + noff[0]), tr_read(Ks + 16 * s * D + noff[1]));
+      };
+      ld_dq(0, 0);
+#pragma unroll
+      for (int s = 0; s < BKV / 16; ++s) {
+        if (s + 1 < BKV / 16) ld_dq(s + 1, (s + 1) & 1);
+        acc = mfma32(qa[s & 1], qb[s & 1], acc);
+      }
+      // lane holds column d = 32dt + l32, rows q = qt + (i&3) + 8(i>>2) + 4h (128-B row segments)
+      const int64_t rs = static_cast<int64_t>(p.Hq) * D;
+      float* sp = p.dq_slab + ((static_cast<int64_t>(kb) * p.B + b) * p.Tq + qt) * rs +
+                  static_cast<int64_t>(hq) * D + 32 * dt + l32;
+      const int nrow = p.Tq - qt;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int r = (i & 3) + 8 * (i >> 2) + 4 * h;
+        if (r < nrow) sp[r * rs] = acc[i] * p.scale;
+      }
+    }
+    __syncthreads();  // next Q / dO tile visible; every wave is done reading dS
+  }
+
+  // dK (scaled) and dV: lane = key, registers = d rows (i&3) + 8(i>>2) + 4h of column tile dt
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int kj = kw + 32 * j + l32;
+    if (kj >= p.Tk) continue;
+    if (p.hsplit == 1) {
+      bf16_t* dkp = p.dk + b * p.dk_sb + kj * p.dk_st + static_cast<int64_t>(hk) * p.dk_sh;
+      bf16_t* dvp = p.dv + b * p.dv_sb + kj * p.dv_st + static_cast<int64_t>(hk) * p.dv_sh;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int d = 32 * dt + 8 * g4 + 4 * h;
+          uint2 a, c;
+          a.x = pack2bf(dk[j][dt][4 * g4] * p.scale, dk[j][dt][4 * g4 + 1] * p.scale);
+          a.y = pack2bf(dk[j][dt][4 * g4 + 2] * p.scale, dk[j][dt][4 * g4 + 3] * p.scale);
+          c.x = pack2bf(dv[j][dt][4 * g4], dv[j][dt][4 * g4 + 1]);
+          c.y = pack2bf(dv[j][dt][4 * g4 + 2], dv[j][dt][4 * g4 + 3]);
+          *reinterpret_cast<uint2*>(dkp + d) = a;
+          *reinterpret_cast<uint2*>(dvp + d) = c;
+        }
+      }
+    } else {  // fp32 partials of this head subset, summed by attn_dkv_reduce_kernel
+      const int64_t off = ((static_cast<int64_t>(sidx) * p.B + b) * p.Tk + kj) * p.Hkv * D +
+                          static_cast<int64_t>(hk) * D;
+      float* dkp = p.dk_part + off;
+      float* dvp = p.dv_part + off;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int d = 32 * dt + 8 * g4 + 4 * h;
+          *reinterpret_cast<f32x4*>(dkp + d) = f32x4{dk[j][dt][4 * g4], dk[j][dt][4 * g4 + 1],
+                                                     dk[j][dt][4 * g4 + 2], dk[j][dt][4 * g4 + 3]};
+          *reinterpret_cast<f32x4*>(dvp + d) = f32x4{dv[j][dt][4 * g4], dv[j][dt][4 * g4 + 1],
+                                                     dv[j][dt][4 * g4 + 2], dv[j][dt][4 * g4 + 3]};
+        }
       }
     }
   }
 }
 
-// fp32 dQ accumulator [rows, D] -> bf16 (strided destination)
-__global__ __launch_bounds__(256) void f32_to_bf16_rows_kernel(const float* __restrict__ src,
-                                                                int64_t rows, int cols,
-                                                                bf16_t* __restrict__ dst,
-                                                                int64_t dst_ld) {
-  const int cv = cols / 8;
-  const int64_t total = rows * cv;
+// dQ[b, t, h, :] = sum over the key blocks whose workgroups swept row t (fixed kb order)
+// -> bf16 into a strided destination. One thread per 8 columns.
+template <bool CAUSAL>
+__global__ __launch_bounds__(256) void attn_dq_reduce_kernel(
+    const float* __restrict__ slab, int nkb, int B, int Tq, int Hq, int D, int causal_off,
+    int window, const int* __restrict__ kv_start, const int* __restrict__ kv_end, int Tk,
+    bf16_t* __restrict__ dst, int64_t d_sb, int64_t d_st, int64_t d_sh) {
+  const int cv = D / 8;
+  const int64_t total = static_cast<int64_t>(B) * Tq * Hq * cv;
+  const int64_t rs = static_cast<int64_t>(Hq) * D;
+  const int64_t slab_stride = static_cast<int64_t>(B) * Tq * rs;
   for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += static_cast<int64_t>(gridDim.x) * 256) {
-    const int64_t r = i / cv;
-    const int c = static_cast<int>(i - r * cv) * 8;
-    const f32x4* s = reinterpret_cast<const f32x4*>(src + r * cols + c);
-    f32x4 a = s[0], bb = s[1];
-    bf16x8 o;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      o[j] = f2bf(a[j]);
-      o[4 + j] = f2bf(bb[j]);
+    const int c = static_cast<int>(i % cv);
+    int64_t r = i / cv;
+    const int hq = static_cast<int>(r % Hq);
+    r /= Hq;
+    const int t = static_cast<int>(r % Tq);
+    const int b = static_cast<int>(r / Tq);
+    const int kbeg = kv_start ? kv_start[b] : 0;
+    const int kend = kv_end ? kv_end[b] : Tk;
+    const float* src = slab + (static_cast<int64_t>(b) * Tq + t) * rs + static_cast<int64_t>(hq) * D + c * 8;
+    f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+    for (int kb = 0; kb < nkb; ++kb) {
+      const int k0 = kb * kAttnBwdKeys;
+      int qt0, qend;
+      bwd_q_range<CAUSAL>(k0, Tq, causal_off, window, qt0, qend);
+      if (k0 >= kend || k0 + kAttnBwdKeys <= kbeg || t < qt0 || t >= qend) continue;
+      const f32x4* sv = reinterpret_cast<const f32x4*>(src + kb * slab_stride);
+      a0 += sv[0];
+      a1 += sv[1];
     }
-    store_bf16x8(dst + r * dst_ld + c, o);
+    const float v[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+    store_bf16x8(dst + b * d_sb + t * d_st + hq * d_sh + c * 8, pack_bf16x8(v));
+  }
+}
+
+// dK = scale * sum_s dk_part[s], dV = sum_s dv_part[s] -> bf16 strided (head-split workgroups)
+__global__ __launch_bounds__(256) void attn_dkv_reduce_kernel(
+    const float* __restrict__ dkp, const float* __restrict__ dvp, int hs, int B, int Tk, int Hkv,
+    int D, float scale, bf16_t* __restrict__ dk, int64_t dk_sb, int64_t dk_st, int64_t dk_sh,
+    bf16_t* __restrict__ dv, int64_t dv_sb, int64_t dv_st, int64_t dv_sh) {
+  const int cv = D / 8;
+  const int64_t total = static_cast<int64_t>(B) * Tk * Hkv * cv;
+  const int64_t pstride = static_cast<int64_t>(B) * Tk * Hkv * D;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += static_cast<int64_t>(gridDim.x) * 256) {
+    const int c = static_cast<int>(i % cv);
+    int64_t r = i / cv;
+    const int hk = static_cast<int>(r % Hkv);
+    r /= Hkv;
+    const int t = static_cast<int>(r % Tk);
+    const int b = static_cast<int>(r / Tk);
+    const int64_t off = ((static_cast<int64_t>(b) * Tk + t) * Hkv + hk) * D + c * 8;
+    f32x4 k0 = {0.f, 0.f, 0.f, 0.f}, k1 = k0, v0 = k0, v1 = k0;
+    for (int s = 0; s < hs; ++s) {
+      const f32x4* ks = reinterpret_cast<const f32x4*>(dkp + s * pstride + off);
+      const f32x4* vs = reinterpret_cast<const f32x4*>(dvp + s * pstride + off);
+      k0 += ks[0];
+      k1 += ks[1];
+      v0 += vs[0];
+      v1 += vs[1];
+    }
+    const float kf[8] = {k0[0] * scale, k0[1] * scale, k0[2] * scale, k0[3] * scale,
+                         k1[0] * scale, k1[1] * scale, k1[2] * scale, k1[3] * scale};
+    const float vf[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+    store_bf16x8(dk + b * dk_sb + t * dk_st + hk * dk_sh + c * 8, pack_bf16x8(kf));
+    store_bf16x8(dv + b * dv_sb + t * dv_st + hk * dv_sh + c * 8, pack_bf16x8(vf));
   }
 }
 
 // ----------------------------------------------------------------------------------------------
 // launchers
 // ----------------------------------------------------------------------------------------------
+static inline unsigned stream_grid(int64_t work) {
+  int64_t g = (work + 255) / 256;
+  if (g > 2048) g = 2048;
+  return static_cast<unsigned>(g < 1 ? 1 : g);
+}
+
 template <int D>
 static void fwd_dispatch(const AttnParams& p, bool causal, hipStream_t st) {
-  const int nqb = (p.Tq + 127) / 128;
+  const int nqb = (p.Tq + kFwdRows - 1) / kFwdRows;
   const dim3 grid(nqb * p.Hq * p.B);
-  if (causal) attn_fwd_kernel<D, true><<<grid, 256, 0, st>>>(p);
-  else attn_fwd_kernel<D, false><<<grid, 256, 0, st>>>(p);
+  if (causal) attn_fwd_kernel<D, true><<<grid, kFwdThreads, 0, st>>>(p);
+  else attn_fwd_kernel<D, false><<<grid, kFwdThreads, 0, st>>>(p);
 }
 
 void launch_attn_fwd(const AttnParams& p, int D, bool causal, hipStream_t st) {
@@ -635,27 +798,43 @@ void launch_attn_bwd_delta(const bf16_t* o, const bf16_t* dout, int64_t o_sb, in
 
 template <int D>
 static void bwd_dispatch(const AttnBwdParams& p, bool causal, hipStream_t st) {
-  const int nkb = (p.Tk + 127) / 128;
-  const dim3 grid(nkb * p.Hkv * p.B);
+  const int nkb = (p.Tk + kAttnBwdKeys - 1) / kAttnBwdKeys;
+  const dim3 grid(nkb * p.Hkv * p.B * p.hsplit);
   if (causal) attn_bwd_kernel<D, true><<<grid, 256, 0, st>>>(p);
   else attn_bwd_kernel<D, false><<<grid, 256, 0, st>>>(p);
 }
 
 void launch_attn_bwd(const AttnBwdParams& p, int D, bool causal, hipStream_t st) {
-  if (p.B == 0 || p.Tq == 0) return;
+  if (p.B == 0 || p.Tq == 0 || p.Tk == 0) return;
   switch (D) {
     case 64: bwd_dispatch<64>(p, causal, st); break;
     default: bwd_dispatch<128>(p, causal, st); break;
   }
 }
 
-void launch_f32_to_bf16_rows(const float* src, int64_t rows, int cols, bf16_t* dst,
-                             int64_t dst_ld, hipStream_t st) {
-  const int64_t work = rows * (cols / 8);
+void launch_attn_dq_reduce(const float* slab, int nkb, int B, int Tq, int Hq, int D, bool causal,
+                           int causal_off, int window, const int* kv_start, const int* kv_end,
+                           int Tk, bf16_t* dst, int64_t d_sb, int64_t d_st, int64_t d_sh,
+                           hipStream_t st) {
+  const int64_t work = static_cast<int64_t>(B) * Tq * Hq * (D / 8);
   if (work == 0) return;
-  int64_t g = (work + 255) / 256;
-  if (g > 2048) g = 2048;
-  f32_to_bf16_rows_kernel<<<static_cast<unsigned>(g), 256, 0, st>>>(src, rows, cols, dst, dst_ld);
+  if (causal)
+    attn_dq_reduce_kernel<true><<<stream_grid(work), 256, 0, st>>>(
+        slab, nkb, B, Tq, Hq, D, causal_off, window, kv_start, kv_end, Tk, dst, d_sb, d_st, d_sh);
+  else
+    attn_dq_reduce_kernel<false><<<stream_grid(work), 256, 0, st>>>(
+        slab, nkb, B, Tq, Hq, D, causal_off, window, kv_start, kv_end, Tk, dst, d_sb, d_st, d_sh);
+}
+
+void launch_attn_dkv_reduce(const float* dkp, const float* dvp, int hs, int B, int Tk, int Hkv,
+                            int D, float scale, bf16_t* dk, int64_t dk_sb, int64_t dk_st,
+                            int64_t dk_sh, bf16_t* dv, int64_t dv_sb, int64_t dv_st,
+                            int64_t dv_sh, hipStream_t st) {
+  const int64_t work = static_cast<int64_t>(B) * Tk * Hkv * (D / 8);
+  if (work == 0) return;
+  attn_dkv_reduce_kernel<<<stream_grid(work), 256, 0, st>>>(dkp, dvp, hs, B, Tk, Hkv, D, scale, dk,
+                                                            dk_sb, dk_st, dk_sh, dv, dv_sb, dv_st,
+                                                            dv_sh);
 }
 
 }  // namespace dla

@@ -9,7 +9,11 @@
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <torch/library.h>
 
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 #include <tuple>
 
 #include "attn_params.h"
@@ -59,7 +63,11 @@ void launch_attn_fwd(const AttnParams&, int, bool, hipStream_t);
 void launch_attn_bwd_delta(const bf16_t*, const bf16_t*, int64_t, int64_t, int64_t, int64_t,
                            int64_t, int64_t, int, int, int, int, float*, hipStream_t);
 void launch_attn_bwd(const AttnBwdParams&, int, bool, hipStream_t);
-void launch_f32_to_bf16_rows(const float*, int64_t, int, bf16_t*, int64_t, hipStream_t);
+void launch_attn_dq_reduce(const float*, int, int, int, int, int, bool, int, int, const int*,
+                           const int*, int, bf16_t*, int64_t, int64_t, int64_t, hipStream_t);
+void launch_attn_dkv_reduce(const float*, const float*, int, int, int, int, int, float, bf16_t*,
+                            int64_t, int64_t, int64_t, bf16_t*, int64_t, int64_t, int64_t,
+                            hipStream_t);
 void launch_transpose_bf16(const bf16_t*, int64_t, int64_t, int64_t, bf16_t*, int64_t, hipStream_t);
 
 // ================================= norms ======================================================
@@ -314,24 +322,54 @@ std::tuple<at::Tensor, at::Tensor> attn_fwd(const at::Tensor& q, const at::Tenso
   return {o, lse2};
 }
 
-// returns dq as fp32 [B, Tq, Hq, D]; dk / dv written into the given (possibly strided) outputs
-at::Tensor attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k,
-                    const at::Tensor& v, const at::Tensor& o, const at::Tensor& lse2,
-                    at::Tensor& dk, at::Tensor& dv, double scale, bool causal, int64_t causal_off,
-                    int64_t window, const c10::optional<at::Tensor>& kv_start,
-                    const c10::optional<at::Tensor>& kv_end) {
+static int device_cus(int dev) {
+  static int cache[64] = {0};
+  if (dev < 0 || dev >= 64) return 256;
+  if (cache[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cache[dev] = n;
+  }
+  return cache[dev];
+}
+
+// GQA heads of one kv head split across `hs` backward workgroups when the (key block x kv head x
+// batch) grid alone would under-fill the chip: causal key blocks carry unequal work (block 0
+// sees every query), so target two workgroups per CU there and let the heaviest-first dispatch
+// balance them. Partial dK/dV of the splits are summed by a reduce pass.
+static int attn_bwd_hsplit(int64_t nkb, int64_t Hkv, int64_t B, int64_t group, bool causal, int cus) {
+  static const int forced = [] {
+    const char* e = std::getenv("DLA_ATTN_BWD_HSPLIT");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (forced > 0 && group % forced == 0) return forced;
+  const int64_t base = nkb * Hkv * B;
+  const int64_t target = causal ? 2 * static_cast<int64_t>(cus) : cus;
+  int hs = 1;
+  while (base * hs < target && group % (2 * hs) == 0) hs *= 2;
+  return hs;
+}
+
+// dq / dk / dv are written into the given (possibly strided, e.g. fused-dqkv) bf16 outputs
+void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k,
+              const at::Tensor& v, const at::Tensor& o, const at::Tensor& lse2, at::Tensor& dq,
+              at::Tensor& dk, at::Tensor& dv, double scale, bool causal, int64_t causal_off,
+              int64_t window, const c10::optional<at::Tensor>& kv_start,
+              const c10::optional<at::Tensor>& kv_end) {
   check_bthd(dout, "dout");
   check_bthd(q, "q");
   check_bthd(k, "k");
   check_bthd(v, "v");
   check_bthd(o, "o");
+  check_bthd(dq, "dq");
   check_bthd(dk, "dk");
   check_bthd(dv, "dv");
   check_f32(lse2, "lse2");
   const int64_t B = q.size(0), Tq = q.size(1), Hq = q.size(2), D = q.size(3);
   const int64_t Tk = k.size(1), Hkv = k.size(2);
   TORCH_CHECK(D == 64 || D == 128, "head_dim must be 64 or 128");
-  TORCH_CHECK(dout.sizes() == q.sizes() && o.sizes() == q.sizes(), "dout/o shape");
+  TORCH_CHECK(dout.sizes() == q.sizes() && o.sizes() == q.sizes() && dq.sizes() == q.sizes(),
+              "dout/o/dq shape");
   TORCH_CHECK(dk.sizes() == k.sizes() && dv.sizes() == v.sizes(), "dk/dv shape");
   TORCH_CHECK(lse2.is_contiguous() && lse2.numel() == B * Hq * Tq, "lse2 shape");
   TORCH_CHECK(Hkv > 0 && Hq % Hkv == 0, "GQA ratio");
@@ -339,15 +377,29 @@ at::Tensor attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tenso
   check_kv_range(kv_end, B, "kv_end");
   c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
   auto st = cur_stream(q);
-  auto delta = at::empty({B, Hq, Tq}, q.options().dtype(at::kFloat));
+  auto fopt = q.options().dtype(at::kFloat);
+  auto delta = at::empty({B, Hq, Tq}, fopt);
   launch_attn_bwd_delta(cbp(o), cbp(dout), o.stride(0), o.stride(1), o.stride(2),
                         dout.stride(0), dout.stride(1), dout.stride(2), B, Hq, Tq, D,
                         delta.data_ptr<float>(), st);
-  auto dq = at::zeros({B, Tq, Hq, D}, q.options().dtype(at::kFloat));
+  const int64_t nkb = (Tk + kAttnBwdKeys - 1) / kAttnBwdKeys;
+  // one fp32 dQ partial per key block (no zero fill: the reduce pass reads exactly the rows
+  // each key block's workgroups wrote)
+  auto slab = at::empty({std::max<int64_t>(nkb, 1), B, Tq, Hq, D}, fopt);
+  const int hs = attn_bwd_hsplit(nkb, Hkv, B, Hq / Hkv, causal, device_cus(q.get_device()));
+  at::Tensor dkp, dvp;
+  if (hs > 1) {
+    dkp = at::empty({hs, B, Tk, Hkv, D}, fopt);
+    dvp = at::empty({hs, B, Tk, Hkv, D}, fopt);
+  }
   AttnBwdParams p{};
   p.q = cbp(q); p.k = cbp(k); p.v = cbp(v); p.dout = cbp(dout);
   p.lse2 = lse2.data_ptr<float>(); p.delta = delta.data_ptr<float>();
-  p.dq = dq.data_ptr<float>(); p.dk = bp(dk); p.dv = bp(dv);
+  p.dq_slab = slab.data_ptr<float>();
+  p.dk_part = hs > 1 ? dkp.data_ptr<float>() : nullptr;
+  p.dv_part = hs > 1 ? dvp.data_ptr<float>() : nullptr;
+  p.dk = bp(dk); p.dv = bp(dv);
+  p.hsplit = hs;
   p.q_sb = q.stride(0); p.q_st = q.stride(1); p.q_sh = q.stride(2);
   p.k_sb = k.stride(0); p.k_st = k.stride(1); p.k_sh = k.stride(2);
   p.v_sb = v.stride(0); p.v_st = v.stride(1); p.v_sh = v.stride(2);
@@ -362,18 +414,16 @@ at::Tensor attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tenso
   p.kv_start = (kv_start && kv_start->defined()) ? kv_start->data_ptr<int>() : nullptr;
   p.kv_end = (kv_end && kv_end->defined()) ? kv_end->data_ptr<int>() : nullptr;
   launch_attn_bwd(p, static_cast<int>(D), causal, st);
-  return dq;
-}
-
-void f32_to_bf16_rows(const at::Tensor& src, at::Tensor& dst) {
-  check_f32(src, "src");
-  check_bf16(dst, "dst");
-  TORCH_CHECK(src.is_contiguous() && src.dim() == 2 && dst.dim() == 2 && dst.stride(1) == 1 &&
-                  src.sizes() == dst.sizes() && src.size(1) % 8 == 0 && dst.stride(0) % 8 == 0,
-              "f32_to_bf16_rows layout");
-  c10::hip::HIPGuardMasqueradingAsCUDA g(src.device());
-  launch_f32_to_bf16_rows(src.data_ptr<float>(), src.size(0), static_cast<int>(src.size(1)),
-                          bp(dst), dst.stride(0), cur_stream(src));
+  launch_attn_dq_reduce(p.dq_slab, static_cast<int>(nkb), static_cast<int>(B), static_cast<int>(Tq),
+                        static_cast<int>(Hq), static_cast<int>(D), causal, p.causal_off, p.window,
+                        p.kv_start, p.kv_end, static_cast<int>(Tk), bp(dq), dq.stride(0),
+                        dq.stride(1), dq.stride(2), st);
+  if (hs > 1) {
+    launch_attn_dkv_reduce(p.dk_part, p.dv_part, hs, static_cast<int>(B), static_cast<int>(Tk),
+                           static_cast<int>(Hkv), static_cast<int>(D), p.scale, bp(dk),
+                           dk.stride(0), dk.stride(1), dk.stride(2), bp(dv), dv.stride(0),
+                           dv.stride(1), dv.stride(2), st);
+  }
 }
 
 // out [C, R] <- in [R, C]^T (both row-major with unit column stride, 16-byte aligned rows)
@@ -636,8 +686,7 @@ TORCH_LIBRARY(dla, m) {
   m.def("rope_fwd(Tensor qkv, Tensor cos, Tensor sin, Tensor? pos, int Hq, int Hkv, int D, int rot, int T, int pos_offset) -> (Tensor, Tensor)");
   m.def("rope_bwd(Tensor dq, Tensor dk, Tensor(a!) dqkv, Tensor cos, Tensor sin, Tensor? pos, int Hq, int Hkv, int D, int rot, int T, int pos_offset) -> ()");
   m.def("attn_fwd(Tensor q, Tensor k, Tensor v, float scale, bool causal, int causal_off, int window, Tensor? kv_start, Tensor? kv_end) -> (Tensor, Tensor)");
-  m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse2, Tensor(a!) dk, Tensor(b!) dv, float scale, bool causal, int causal_off, int window, Tensor? kv_start, Tensor? kv_end) -> Tensor");
-  m.def("f32_to_bf16_rows(Tensor src, Tensor(a!) dst) -> ()");
+  m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse2, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, float scale, bool causal, int causal_off, int window, Tensor? kv_start, Tensor? kv_end) -> ()");
   m.def("transpose_bf16(Tensor input, Tensor(a!) out) -> ()");
   m.def("logprob_fwd(Tensor logits, Tensor targets, int vocab_offset=0) -> (Tensor, Tensor)");
   m.def("logprob_bwd(Tensor(a!) logits, Tensor targets, Tensor lse, Tensor grad, int vocab_offset=0) -> ()");
@@ -664,7 +713,6 @@ TORCH_LIBRARY_IMPL(dla, CUDA, m) {
   m.impl("rope_bwd", &dla::rope_bwd);
   m.impl("attn_fwd", &dla::attn_fwd);
   m.impl("attn_bwd", &dla::attn_bwd);
-  m.impl("f32_to_bf16_rows", &dla::f32_to_bf16_rows);
   m.impl("transpose_bf16", &dla::transpose_bf16);
   m.impl("logprob_fwd", &dla::logprob_fwd);
   m.impl("logprob_bwd", &dla::logprob_bwd);

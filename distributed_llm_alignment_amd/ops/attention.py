@@ -155,18 +155,17 @@ class _FusedQKVAttnFn(torch.autograd.Function):
         do4 = do.contiguous().view(B, T, Hq, D)
         dqkv = torch.empty((B, T, C), dtype=qkv.dtype, device=qkv.device)
         dv = dqkv.as_strided((B, T, Hkv, D), (T * C, C, D, 1), (Hq + Hkv) * D)
-        if rot > 0:
+        if rot > 0:  # rotated-space dq / dk, un-rotated into dqkv by the RoPE backward
+            dq = torch.empty((B, T, Hq, D), dtype=qkv.dtype, device=qkv.device)
             dk = torch.empty((B, T, Hkv, D), dtype=qkv.dtype, device=qkv.device)
-        else:
+        else:  # written straight into the fused dqkv buffer
+            dq = dqkv.as_strided((B, T, Hq, D), (T * C, C, D, 1), 0)
             dk = dqkv.as_strided((B, T, Hkv, D), (T * C, C, D, 1), Hq * D)
-        dq32 = ops.attn_bwd(do4, q4, k4, v4, o, lse2, dk, dv, float(scale), bool(causal), 0,
-                            int(window), kv_start, kv_end)
-        d2 = dqkv.view(B * T, C)
+        ops.attn_bwd(do4, q4, k4, v4, o, lse2, dq, dk, dv, float(scale), bool(causal), 0,
+                     int(window), kv_start, kv_end)
         if rot > 0:
-            dq = dq32.to(torch.bfloat16).view(B * T, Hq * D)
-            ops.rope_bwd(dq, dk.view(B * T, Hkv * D), d2, cos, sin, pos, Hq, Hkv, D, rot, T, 0)
-        else:
-            ops.f32_to_bf16_rows(dq32.view(B * T, Hq * D), d2[:, : Hq * D])
+            ops.rope_bwd(dq.view(B * T, Hq * D), dk.view(B * T, Hkv * D), dqkv.view(B * T, C),
+                         cos, sin, pos, Hq, Hkv, D, rot, T, 0)
         return dqkv, None, None, None, None, None, None, None, None, None, None, None, None
 
 
@@ -187,11 +186,12 @@ class _AttnCoreFn(torch.autograd.Function):
         ops = _ext.require()
         q, k, v, o, lse2, kv_start, kv_end = ctx.saved_tensors
         scale, causal, causal_off, window = ctx.cfg
+        dq = torch.empty_like(q, memory_format=torch.contiguous_format)
         dk = torch.empty_like(k, memory_format=torch.contiguous_format)
         dv = torch.empty_like(v, memory_format=torch.contiguous_format)
-        dq32 = ops.attn_bwd(do.contiguous(), q, k, v, o, lse2, dk, dv, float(scale), bool(causal),
-                            int(causal_off), int(window), kv_start, kv_end)
-        return dq32.to(q.dtype), dk, dv, None, None, None, None, None, None
+        ops.attn_bwd(do.contiguous(), q, k, v, o, lse2, dq, dk, dv, float(scale), bool(causal),
+                     int(causal_off), int(window), kv_start, kv_end)
+        return dq, dk, dv, None, None, None, None, None, None
 
 
 def _pad_d(x: torch.Tensor, Dp: int) -> torch.Tensor:

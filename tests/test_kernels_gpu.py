@@ -145,6 +145,68 @@ def test_attention_core_decode_offset():
     assert rel_err(o, r) < 2e-2
 
 
+@pytest.mark.parametrize("case", ["causal_gqa", "leftpad_window", "noncausal_rightpad", "mha"])
+def test_attention_multi_keyblock_bwd(case):
+    """T spans several 256-key backward workgroups: per-key-block dQ slabs + ordered reduce,
+    head-split dK/dV partials (GQA) and the single-split path (MHA)."""
+    B, T, Hq, Hkv, D = 2, 600, 8, 2, 128
+    causal, window, ks, ke = True, 0, None, None
+    if case == "leftpad_window":
+        ks = torch.tensor([0, 77], device=DEV, dtype=torch.int32)
+        window = 300
+    if case == "noncausal_rightpad":
+        causal = False
+        ke = torch.tensor([T, 411], device=DEV, dtype=torch.int32)
+    if case == "mha":
+        Hkv = Hq
+    q = bf(torch.randn(B, T, Hq, D)).requires_grad_()
+    k = bf(torch.randn(B, T, Hkv, D)).requires_grad_()
+    v = bf(torch.randn(B, T, Hkv, D)).requires_grad_()
+    o = ops.attention_core(q, k, v, causal=causal, window=window, kv_start=ks, kv_end=ke)
+    go = bf(torch.randn_like(o.float()))
+    gq, gk, gv = torch.autograd.grad(o, [q, k, v], go)
+    qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
+    orf = ref_attention(qr, kr, vr, 1 / math.sqrt(D), causal, 0, window, ks, ke)
+    rq, rk, rv = torch.autograd.grad(orf, [qr, kr, vr], go.float())
+    valid = torch.ones(B, T, 1, 1, dtype=torch.bool, device=DEV)
+    if case == "leftpad_window":
+        valid[1, :77] = False
+    assert rel_err(o * valid, orf * valid) < 2e-2, "forward"
+    assert rel_err(gq * valid, rq * valid) < 3e-2, "dq"
+    assert rel_err(gk, rk) < 3e-2, "dk"
+    assert rel_err(gv, rv) < 3e-2, "dv"
+
+
+def test_attention_bwd_deterministic():
+    """dQ is summed from per-key-block slabs in a fixed order (no float atomics): bitwise
+    reproducible gradients."""
+    B, T, Hq, Hkv, D = 2, 700, 8, 2, 128
+    q = bf(torch.randn(B, T, Hq, D)).requires_grad_()
+    k = bf(torch.randn(B, T, Hkv, D)).requires_grad_()
+    v = bf(torch.randn(B, T, Hkv, D)).requires_grad_()
+    go = bf(torch.randn(B, T, Hq, D))
+    g1 = torch.autograd.grad(ops.attention_core(q, k, v), [q, k, v], go)
+    g2 = torch.autograd.grad(ops.attention_core(q, k, v), [q, k, v], go)
+    for a, b in zip(g1, g2):
+        assert torch.equal(a, b)
+
+
+def test_attention_fwd_forced_rescale():
+    """Deferred-max rescale branch (cdna guide §5.4 rule 26): one key spikes against one query
+    row so that row's running max jumps far past the threshold at a late tile."""
+    B, T, Hq, Hkv, D = 1, 512, 4, 1, 128
+    q = torch.randn(B, T, Hq, D) * 0.3
+    k = torch.randn(B, T, Hkv, D) * 0.3
+    v = torch.randn(B, T, Hkv, D)
+    k[0, 300, 0] = q[0, 310, 0] * 40.0  # score(310, 300) ~ 40: +58 in log2 units at tile 4
+    k[0, 301, 0] = q[0, 450, 2] * 25.0
+    q, k, v = bf(q), bf(k), bf(v)
+    o = ops.attention_core(q, k, v, causal=True)
+    r = ref_attention(q.float(), k.float(), v.float(), 1 / math.sqrt(D), True, 0, 0, None, None)
+    assert rel_err(o, r) < 2e-2
+    assert (o[0, 310, 0].float() - r[0, 310, 0]).abs().max().item() < 5e-2
+
+
 def test_attention_long_seq_grad_llama_shape():
     B, T, Hq, Hkv, D = 1, 1024, 32, 8, 128
     C = (Hq + 2 * Hkv) * D
