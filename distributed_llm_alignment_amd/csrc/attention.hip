@@ -218,17 +218,22 @@ __global__ __launch_bounds__(kFwdThreads) void attn_fwd_kernel(AttnParams p) {
         if (p.window > 0) need_mask = need_mask || (kt <= q0 + 31 + p.causal_off - p.window);
       }
       if (need_mask) {
+        // key = base + r with r = 32st + (i&3) + 8(i>>2) a compile-time constant per register:
+        // the visible keys of this lane's query are r in [lo, hi), tested as one unsigned
+        // compare per score
+        const int base = kt + 4 * h;
+        int lo = kbeg - base, hi = kend - base;
+        if (CAUSAL) {
+          hi = min(hi, qi + p.causal_off + 1 - base);
+          if (p.window > 0) lo = max(lo, qi + p.causal_off - p.window + 1 - base);
+        }
+        const unsigned span = hi > lo ? static_cast<unsigned>(hi - lo) : 0u;
 #pragma unroll
         for (int st = 0; st < 2; ++st) {
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
-            const int key = kt + 32 * st + (i & 3) + 8 * (i >> 2) + 4 * h;
-            bool ok = key >= kbeg && key < kend;
-            if (CAUSAL) {
-              ok = ok && key <= qi + p.causal_off;
-              if (p.window > 0) ok = ok && key > qi + p.causal_off - p.window;
-            }
-            sacc[st][i] = ok ? sacc[st][i] : -INFINITY;
+            const int r = 32 * st + (i & 3) + 8 * (i >> 2);
+            sacc[st][i] = static_cast<unsigned>(r - lo) < span ? sacc[st][i] : -INFINITY;
           }
         }
       }
@@ -439,9 +444,17 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnBwdParams p) {
     for (int c = 0; c < QCPT; ++c) {
       const int ci = tid + 256 * c;
       const int row = ci / NCH, ch = ci % NCH;
-      const int qq = qt + row;
-      qreg[c] = qq < p.Tq ? load_bf16x8(qp + qq * p.q_st + ch * 8) : bf16x8{};
-      dreg[c] = qq < p.Tq ? load_bf16x8(dop + qq * p.do_st + ch * 8) : bf16x8{};
+      if (qt + BQ <= p.Tq) {  // full tile (wave-uniform)
+        qreg[c] = load_bf16x8(qp + (qt + row) * p.q_st + ch * 8);
+        dreg[c] = load_bf16x8(dop + (qt + row) * p.do_st + ch * 8);
+      } else {  // rows past Tq: loaded clamped (unpredicated), zeroed
+        const int qq = min(qt + row, p.Tq - 1);
+        const bf16x8 a = load_bf16x8(qp + qq * p.q_st + ch * 8);
+        const bf16x8 g = load_bf16x8(dop + qq * p.do_st + ch * 8);
+        const bool in = qt + row < p.Tq;
+        qreg[c] = in ? a : bf16x8{};
+        dreg[c] = in ? g : bf16x8{};
+      }
     }
   };
   auto stage = [&]() {
@@ -511,13 +524,26 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnBwdParams p) {
     // are first needed after the sub-tile-0 MFMA chains
     float lr[16], dl[16];
     {
-      const int64_t rb = (static_cast<int64_t>(b) * p.Hq + hq) * p.Tq + qt + 4 * h;
-      const int rlim = p.Tq - qt - 4 * h;
+      const int64_t rb = (static_cast<int64_t>(b) * p.Hq + hq) * p.Tq;
+      if (qt + BQ <= p.Tq) {  // full tile (wave-uniform): one base, immediate offsets
+        const float* lp = p.lse2 + rb + qt + 4 * h;
+        const float* dp = p.delta + rb + qt + 4 * h;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int r = (i & 3) + 8 * (i >> 2);
-        lr[i] = r < rlim ? p.lse2[rb + r] : INFINITY;  // rows past Tq: p = 0
-        dl[i] = r < rlim ? p.delta[rb + r] : 0.f;
+        for (int i = 0; i < 16; ++i) {
+          const int r = (i & 3) + 8 * (i >> 2);
+          lr[i] = lp[r];
+          dl[i] = dp[r];
+        }
+      } else {  // last partial tile: clamped unpredicated loads, rows past Tq masked (p = 0)
+        const int rlim = p.Tq - qt - 4 * h;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int r = (i & 3) + 8 * (i >> 2);
+          const int64_t ri = rb + min(qt + 4 * h + r, p.Tq - 1);
+          const float a = p.lse2[ri], c = p.delta[ri];
+          lr[i] = r < rlim ? a : INFINITY;
+          dl[i] = r < rlim ? c : 0.f;
+        }
       }
     }
 
@@ -561,22 +587,22 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnBwdParams p) {
           dpacc = mfma32(fc[s & 1], fd[s & 1], dpacc);
         }
         // P and dS; masking is branch-free: per lane, key kj vs query qt + rr + 4h
+        // visible queries of this lane's key kj: accumulator rows rr = (i&3) + 8(i>>2) (query
+        // qt + rr + 4h) in [lo, hi), one unsigned compare per element
         const int kj = kj0 + l32;
-        const int dlt = kj - qt - p.causal_off - 4 * h;  // causal: visible iff rr >= dlt
-        const int rlim = p.Tq - qt - 4 * h;              // rr < rlim
-        const bool lane_ok = kj >= kbeg && kj < kend;
+        int lo = 0, hi = p.Tq - qt - 4 * h;
+        if (kj < kbeg || kj >= kend) hi = 0;
+        if (CAUSAL) {
+          const int dlt = kj - qt - p.causal_off - 4 * h;  // visible iff rr >= dlt
+          lo = max(lo, dlt);
+          if (p.window > 0) hi = min(hi, dlt + p.window);
+        }
+        const unsigned span = hi > lo ? static_cast<unsigned>(hi - lo) : 0u;
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int rr = (i & 3) + 8 * (i >> 2);
           float pv = ex2(fmaf(sacc[i], p.scale2, -lr[i]));
-          if (need_mask) {
-            bool ok = lane_ok && rr < rlim;
-            if (CAUSAL) {
-              ok = ok && rr >= dlt;
-              if (p.window > 0) ok = ok && rr < dlt + p.window;
-            }
-            pv = ok ? pv : 0.f;
-          }
+          if (need_mask) pv = static_cast<unsigned>(rr - lo) < span ? pv : 0.f;
           sacc[i] = pv;
           dpacc[i] = pv * (dpacc[i] - dl[i]);
         }
@@ -637,14 +663,14 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnBwdParams p) {
         acc = mfma32(qa[s & 1], qb[s & 1], acc);
       }
       // lane holds column d = 32dt + l32, rows q = qt + (i&3) + 8(i>>2) + 4h (128-B row segments)
+      // (slab rows are padded to a multiple of 32: every store is in bounds, none predicated)
       const int64_t rs = static_cast<int64_t>(p.Hq) * D;
-      float* sp = p.dq_slab + ((static_cast<int64_t>(kb) * p.B + b) * p.Tq + qt) * rs +
+      float* sp = p.dq_slab + ((static_cast<int64_t>(kb) * p.B + b) * p.slab_rows + qt) * rs +
                   static_cast<int64_t>(hq) * D + 32 * dt + l32;
-      const int nrow = p.Tq - qt;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int r = (i & 3) + 8 * (i >> 2) + 4 * h;
-        if (r < nrow) sp[r * rs] = acc[i] * p.scale;
+        sp[r * rs] = acc[i] * p.scale;
       }
     }
     __syncthreads();  // next Q / dO tile visible; every wave is done reading dS
@@ -696,13 +722,13 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnBwdParams p) {
 // -> bf16 into a strided destination. One thread per 8 columns.
 template <bool CAUSAL>
 __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(
-    const float* __restrict__ slab, int nkb, int B, int Tq, int Hq, int D, int causal_off,
-    int window, const int* __restrict__ kv_start, const int* __restrict__ kv_end, int Tk,
-    bf16_t* __restrict__ dst, int64_t d_sb, int64_t d_st, int64_t d_sh) {
+    const float* __restrict__ slab, int nkb, int B, int Tq, int slab_rows, int Hq, int D,
+    int causal_off, int window, const int* __restrict__ kv_start, const int* __restrict__ kv_end,
+    int Tk, bf16_t* __restrict__ dst, int64_t d_sb, int64_t d_st, int64_t d_sh) {
   const int cv = D / 8;
   const int64_t total = static_cast<int64_t>(B) * Tq * Hq * cv;
   const int64_t rs = static_cast<int64_t>(Hq) * D;
-  const int64_t slab_stride = static_cast<int64_t>(B) * Tq * rs;
+  const int64_t slab_stride = static_cast<int64_t>(B) * slab_rows * rs;
   for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += static_cast<int64_t>(gridDim.x) * 256) {
     const int c = static_cast<int>(i % cv);
     int64_t r = i / cv;
@@ -712,7 +738,7 @@ __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(
     const int b = static_cast<int>(r / Tq);
     const int kbeg = kv_start ? kv_start[b] : 0;
     const int kend = kv_end ? kv_end[b] : Tk;
-    const float* src = slab + (static_cast<int64_t>(b) * Tq + t) * rs + static_cast<int64_t>(hq) * D + c * 8;
+    const float* src = slab + (static_cast<int64_t>(b) * slab_rows + t) * rs + static_cast<int64_t>(hq) * D + c * 8;
     f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
     for (int kb = 0; kb < nkb; ++kb) {
       const int k0 = kb * kAttnBwdKeys;
@@ -812,18 +838,18 @@ void launch_attn_bwd(const AttnBwdParams& p, int D, bool causal, hipStream_t st)
   }
 }
 
-void launch_attn_dq_reduce(const float* slab, int nkb, int B, int Tq, int Hq, int D, bool causal,
-                           int causal_off, int window, const int* kv_start, const int* kv_end,
-                           int Tk, bf16_t* dst, int64_t d_sb, int64_t d_st, int64_t d_sh,
-                           hipStream_t st) {
+void launch_attn_dq_reduce(const float* slab, int nkb, int B, int Tq, int slab_rows, int Hq, int D,
+                           bool causal, int causal_off, int window, const int* kv_start,
+                           const int* kv_end, int Tk, bf16_t* dst, int64_t d_sb, int64_t d_st,
+                           int64_t d_sh, hipStream_t st) {
   const int64_t work = static_cast<int64_t>(B) * Tq * Hq * (D / 8);
   if (work == 0) return;
   if (causal)
     attn_dq_reduce_kernel<true><<<stream_grid(work), 256, 0, st>>>(
-        slab, nkb, B, Tq, Hq, D, causal_off, window, kv_start, kv_end, Tk, dst, d_sb, d_st, d_sh);
+        slab, nkb, B, Tq, slab_rows, Hq, D, causal_off, window, kv_start, kv_end, Tk, dst, d_sb, d_st, d_sh);
   else
     attn_dq_reduce_kernel<false><<<stream_grid(work), 256, 0, st>>>(
-        slab, nkb, B, Tq, Hq, D, causal_off, window, kv_start, kv_end, Tk, dst, d_sb, d_st, d_sh);
+        slab, nkb, B, Tq, slab_rows, Hq, D, causal_off, window, kv_start, kv_end, Tk, dst, d_sb, d_st, d_sh);
 }
 
 void launch_attn_dkv_reduce(const float* dkp, const float* dvp, int hs, int B, int Tk, int Hkv,

@@ -36,13 +36,14 @@ struct AttnBwdParams {
   const bf16_t* dout;
   const float* lse2;   // [B, Hq, Tq]
   const float* delta;  // [B, Hq, Tq] = rowsum(dO * O)
-  float* dq_slab;      // [nkb, B, Tq, Hq, D] fp32: one dQ partial per 256-key block (plain
+  float* dq_slab;      // [nkb, B, slab_rows, Hq, D] fp32: one dQ partial per 256-key block (plain
                        // stores, no atomics), summed in key-block order by the reduce pass
   float* dk_part;      // [hsplit, B, Tk, Hkv, D] fp32 partials (hsplit > 1 only)
   float* dv_part;
   bf16_t* dk;          // strided like k (hsplit == 1)
   bf16_t* dv;          // strided like v (hsplit == 1)
   int hsplit;          // GQA group split across workgroups (balances causal key blocks)
+  int slab_rows;       // Tq rounded up to a multiple of kAttnBwdQRows (dq_slab row count)
   int64_t q_sb, q_st, q_sh;
   int64_t k_sb, k_st, k_sh;
   int64_t v_sb, v_st, v_sh;

@@ -63,8 +63,9 @@ void launch_attn_fwd(const AttnParams&, int, bool, hipStream_t);
 void launch_attn_bwd_delta(const bf16_t*, const bf16_t*, int64_t, int64_t, int64_t, int64_t,
                            int64_t, int64_t, int, int, int, int, float*, hipStream_t);
 void launch_attn_bwd(const AttnBwdParams&, int, bool, hipStream_t);
-void launch_attn_dq_reduce(const float*, int, int, int, int, int, bool, int, int, const int*,
-                           const int*, int, bf16_t*, int64_t, int64_t, int64_t, hipStream_t);
+void launch_attn_dq_reduce(const float*, int, int, int, int, int, int, bool, int, int,
+                           const int*, const int*, int, bf16_t*, int64_t, int64_t, int64_t,
+                           hipStream_t);
 void launch_attn_dkv_reduce(const float*, const float*, int, int, int, int, int, float, bf16_t*,
                             int64_t, int64_t, int64_t, bf16_t*, int64_t, int64_t, int64_t,
                             hipStream_t);
@@ -385,7 +386,8 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k,
   const int64_t nkb = (Tk + kAttnBwdKeys - 1) / kAttnBwdKeys;
   // one fp32 dQ partial per key block (no zero fill: the reduce pass reads exactly the rows
   // each key block's workgroups wrote)
-  auto slab = at::empty({std::max<int64_t>(nkb, 1), B, Tq, Hq, D}, fopt);
+  const int64_t slab_rows = (Tq + kAttnBwdQRows - 1) / kAttnBwdQRows * kAttnBwdQRows;
+  auto slab = at::empty({std::max<int64_t>(nkb, 1), B, slab_rows, Hq, D}, fopt);
   const int hs = attn_bwd_hsplit(nkb, Hkv, B, Hq / Hkv, causal, device_cus(q.get_device()));
   at::Tensor dkp, dvp;
   if (hs > 1) {
@@ -400,6 +402,7 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k,
   p.dv_part = hs > 1 ? dvp.data_ptr<float>() : nullptr;
   p.dk = bp(dk); p.dv = bp(dv);
   p.hsplit = hs;
+  p.slab_rows = static_cast<int>(slab_rows);
   p.q_sb = q.stride(0); p.q_st = q.stride(1); p.q_sh = q.stride(2);
   p.k_sb = k.stride(0); p.k_st = k.stride(1); p.k_sh = k.stride(2);
   p.v_sb = v.stride(0); p.v_st = v.stride(1); p.v_sh = v.stride(2);
@@ -415,7 +418,7 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k,
   p.kv_end = (kv_end && kv_end->defined()) ? kv_end->data_ptr<int>() : nullptr;
   launch_attn_bwd(p, static_cast<int>(D), causal, st);
   launch_attn_dq_reduce(p.dq_slab, static_cast<int>(nkb), static_cast<int>(B), static_cast<int>(Tq),
-                        static_cast<int>(Hq), static_cast<int>(D), causal, p.causal_off, p.window,
+                        p.slab_rows, static_cast<int>(Hq), static_cast<int>(D), causal, p.causal_off, p.window,
                         p.kv_start, p.kv_end, static_cast<int>(Tk), bp(dq), dq.stride(0),
                         dq.stride(1), dq.stride(2), st);
   if (hs > 1) {

@@ -16,7 +16,8 @@ import torch
 
 _LOCK = threading.Lock()
 _STATE = {"loaded": False, "error": None}
-SO_PATH = Path(__file__).resolve().parent.parent / "_C.so"
+# DLA_EXT_PATH: load an alternative build of the extension (A/B kernel experiments on one box)
+SO_PATH = Path(os.environ.get("DLA_EXT_PATH") or Path(__file__).resolve().parent.parent / "_C.so")
 
 
 def load(build_if_missing: bool | None = None) -> bool:
