@@ -53,6 +53,12 @@ void launch_pairwise_loss(const float*, const float*, int, float*, float*, float
                           hipStream_t);
 void launch_kl_penalty_pg(const float*, const float*, const float*, int, float, float*, float*,
                           float*, float*, hipStream_t);
+void launch_gae(const float*, const float*, const float*, int, int, float, float, float*, float*,
+                hipStream_t);
+void launch_ppo_policy_loss(const float*, const float*, const float*, const float*, int64_t, float,
+                            float*, float*, float*, hipStream_t);
+void launch_ppo_value_loss(const float*, const float*, const float*, const float*, int64_t, float,
+                           float*, float*, hipStream_t);
 void launch_adamw(bf16_t*, float*, const void*, bool, float*, float*, int64_t, float, float,
                   float, float, float, int, const float*, float, hipStream_t);
 void launch_grad_sumsq(const void*, bool, int64_t, float*, float*, bool, hipStream_t);
@@ -591,6 +597,67 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> pairwise_loss(const a
   return {loss, dsc, dsr, acc};
 }
 
+// ---- PPO (actor-critic) token objectives: [S, T] fp32 grids ----
+static void check_grid(const at::Tensor& t, const at::Tensor& like, const char* name) {
+  check_f32(t, name);
+  TORCH_CHECK(t.is_contiguous() && t.sizes() == like.sizes(), name, " must be a contiguous fp32 grid like the first operand");
+}
+
+std::tuple<at::Tensor, at::Tensor> gae(const at::Tensor& rewards, const at::Tensor& values,
+                                       const at::Tensor& mask, double gamma, double lam) {
+  check_f32(rewards, "rewards");
+  TORCH_CHECK(rewards.dim() == 2 && rewards.is_contiguous(), "rewards [S, T] contiguous");
+  check_grid(values, rewards, "values");
+  check_grid(mask, rewards, "mask");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(rewards.device());
+  auto adv = at::empty_like(rewards);
+  auto ret = at::empty_like(rewards);
+  launch_gae(rewards.data_ptr<float>(), values.data_ptr<float>(), mask.data_ptr<float>(),
+             static_cast<int>(rewards.size(0)), static_cast<int>(rewards.size(1)),
+             static_cast<float>(gamma), static_cast<float>(lam), adv.data_ptr<float>(),
+             ret.data_ptr<float>(), cur_stream(rewards));
+  return {adv, ret};
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> ppo_policy_loss(const at::Tensor& lp,
+                                                               const at::Tensor& old,
+                                                               const at::Tensor& adv,
+                                                               const at::Tensor& mask,
+                                                               double eps) {
+  check_f32(lp, "lp");
+  TORCH_CHECK(lp.is_contiguous(), "lp contiguous");
+  check_grid(old, lp, "old");
+  check_grid(adv, lp, "adv");
+  check_grid(mask, lp, "mask");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(lp.device());
+  auto opt = lp.options();
+  auto loss = at::empty({}, opt);
+  auto dlp = at::empty_like(lp);
+  auto metrics = at::empty({3}, opt);
+  launch_ppo_policy_loss(lp.data_ptr<float>(), old.data_ptr<float>(), adv.data_ptr<float>(),
+                         mask.data_ptr<float>(), lp.numel(), static_cast<float>(eps),
+                         loss.data_ptr<float>(), dlp.data_ptr<float>(), metrics.data_ptr<float>(),
+                         cur_stream(lp));
+  return {loss, dlp, metrics};
+}
+
+std::tuple<at::Tensor, at::Tensor> ppo_value_loss(const at::Tensor& values, const at::Tensor& old,
+                                                  const at::Tensor& returns,
+                                                  const at::Tensor& mask, double clip) {
+  check_f32(values, "values");
+  TORCH_CHECK(values.is_contiguous(), "values contiguous");
+  check_grid(old, values, "old");
+  check_grid(returns, values, "returns");
+  check_grid(mask, values, "mask");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(values.device());
+  auto loss = at::empty({}, values.options());
+  auto dval = at::empty_like(values);
+  launch_ppo_value_loss(values.data_ptr<float>(), old.data_ptr<float>(), returns.data_ptr<float>(),
+                        mask.data_ptr<float>(), values.numel(), static_cast<float>(clip),
+                        loss.data_ptr<float>(), dval.data_ptr<float>(), cur_stream(values));
+  return {loss, dval};
+}
+
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> kl_penalty_pg(const at::Tensor& lp,
                                                                          const at::Tensor& lr,
                                                                          const at::Tensor& reward,
@@ -699,6 +766,9 @@ TORCH_LIBRARY(dla, m) {
   m.def("seq_expand_grad(Tensor coef, Tensor mask, Tensor cnt, bool mean) -> Tensor");
   m.def("dpo_loss(Tensor pol, Tensor ref, float beta, float label_smoothing) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("pairwise_loss(Tensor sc, Tensor sr) -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def("gae(Tensor rewards, Tensor values, Tensor mask, float gamma, float lam) -> (Tensor, Tensor)");
+  m.def("ppo_policy_loss(Tensor lp, Tensor old, Tensor adv, Tensor mask, float eps) -> (Tensor, Tensor, Tensor)");
+  m.def("ppo_value_loss(Tensor values, Tensor old, Tensor returns, Tensor mask, float clip) -> (Tensor, Tensor)");
   m.def("kl_penalty_pg(Tensor lp, Tensor lr, Tensor reward, float kl_coef) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("adamw_step(Tensor(a!)? param, Tensor(b!)? master, Tensor grad, Tensor(c!) m, Tensor(d!) v, float lr, float b1, float b2, float eps, float wd, int step, Tensor? clip, float grad_scale) -> ()");
   m.def("grad_sumsq(Tensor grad, Tensor(a!) out, bool accumulate) -> ()");
@@ -726,6 +796,9 @@ TORCH_LIBRARY_IMPL(dla, CUDA, m) {
   m.impl("dpo_loss", &dla::dpo_loss);
   m.impl("pairwise_loss", &dla::pairwise_loss);
   m.impl("kl_penalty_pg", &dla::kl_penalty_pg);
+  m.impl("gae", &dla::gae);
+  m.impl("ppo_policy_loss", &dla::ppo_policy_loss);
+  m.impl("ppo_value_loss", &dla::ppo_value_loss);
   m.impl("adamw_step", &dla::adamw_step);
   m.impl("grad_sumsq", &dla::grad_sumsq);
   m.impl("clip_coef", &dla::clip_coef);

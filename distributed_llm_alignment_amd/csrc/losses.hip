@@ -8,6 +8,7 @@
 //   pairwise_loss   : -logsigmoid(sc - sr).mean()                   src/models/reward_model.py:67-68
 //   kl_penalty_pg   : kl = lp - lr; r' = r - c*kl; A = r' - mean(r'); loss = -mean(A*lp)
 //                                                                   train_rlhf.py:149-153
+//   gae / ppo_policy_loss / ppo_value_loss : token-level actor-critic PPO (below)
 // Batch dimensions here are small (pairs per micro-batch), so each loss is a single
 // 256-thread block; the point is fusing fwd+bwd+metrics into one launch with no host sync.
 #include "common.h"
@@ -150,6 +151,145 @@ __global__ __launch_bounds__(256) void kl_penalty_pg_kernel(const float* __restr
     loss[0] = l / n;
     kl_mean[0] = ksum / n;
   }
+}
+
+// ==============================================================================================
+// PPO (actor-critic) token objectives: the north-star "PPO RLHF (actor + critic + reward)"
+// configuration. The reference's train_rlhf.py:149-153 is the sequence-level REINFORCE special
+// case above (kl_penalty_pg); these run over [S, T] token grids.
+// ==============================================================================================
+
+// Generalised advantage estimation, one wave per sequence:
+//   A_t = m_t * (delta_t + gamma*lam*m_{t+1} * A_{t+1}),  delta_t = r_t + gamma*m_{t+1}*V_{t+1} - V_t
+// is the affine reverse recurrence x_t = a_t + c_t x_{t+1}. Lane l owns the contiguous segment
+// [l*L, (l+1)*L) (L = ceil(T/64)): pass 1 composes the segment's map x_{t0} = A + C x_{t1}, a
+// log2(64)-step shuffle scan composes the maps of lanes l..63 (so every lane learns the x
+// entering its segment from the right), pass 2 re-walks the segment writing A_t and the
+// returns R_t = A_t + V_t. No serial 1-thread-per-sequence loop over T.
+__global__ __launch_bounds__(64) void gae_kernel(const float* __restrict__ r, const float* __restrict__ v,
+                                                 const float* __restrict__ m, int T, float gamma,
+                                                 float lam, float* __restrict__ adv,
+                                                 float* __restrict__ ret) {
+  const int lane = threadIdx.x;
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * T;
+  const int L = (T + 63) / 64;
+  const int t0 = min(T, lane * L), t1 = min(T, t0 + L);
+  auto coef = [&](int t, float& a, float& c) {
+    const float mt = m[base + t];
+    const float mn = t + 1 < T ? m[base + t + 1] : 0.f;
+    const float vn = t + 1 < T ? v[base + t + 1] : 0.f;
+    a = mt * (r[base + t] + gamma * mn * vn - v[base + t]);
+    c = mt * gamma * lam * mn;
+  };
+  float A = 0.f, C = 1.f;  // identity map for an empty segment
+  for (int t = t1 - 1; t >= t0; --t) {
+    float a, c;
+    coef(t, a, c);
+    A = a + c * A;
+    C = c * C;
+  }
+  // (SA, SC): composition of the maps of lanes l .. min(63, l + 2^k - 1)
+  float SA = A, SC = C;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const float na = __shfl_down(SA, off, 64), nc = __shfl_down(SC, off, 64);
+    if (lane + off < 64) {
+      SA = SA + SC * na;
+      SC = SC * nc;
+    }
+  }
+  float x = __shfl_down(SA, 1, 64);  // x entering this segment from the right (x_T = 0)
+  if (lane == 63) x = 0.f;
+  for (int t = t1 - 1; t >= t0; --t) {
+    float a, c;
+    coef(t, a, c);
+    x = a + c * x;
+    adv[base + t] = x;
+    ret[base + t] = x + v[base + t];
+  }
+}
+
+// Clipped surrogate over masked tokens (fwd + bwd in one launch):
+//   rho = exp(lp - lp_old); loss = sum m * max(-A rho, -A clip(rho, 1-eps, 1+eps)) / sum m
+//   dlp = m * (-A rho if the unclipped branch is the max else 0) / sum m
+//   metrics: [0] clip fraction, [1] approx KL  mean((rho - 1) - log rho), [2] token count
+__global__ __launch_bounds__(1024) void ppo_policy_loss_kernel(
+    const float* __restrict__ lp, const float* __restrict__ old, const float* __restrict__ adv,
+    const float* __restrict__ m, int64_t n, float eps, float* __restrict__ loss,
+    float* __restrict__ dlp, float* __restrict__ metrics) {
+  __shared__ float scratch[16];
+  float cnt = 0.f, l = 0.f, cf = 0.f, kl = 0.f;
+  for (int64_t i = threadIdx.x; i < n; i += 1024) {
+    const float mi = m[i];
+    const float d = lp[i] - old[i];
+    const float rho = __expf(d), a = adv[i];
+    const float l1 = -a * rho, l2 = -a * fminf(fmaxf(rho, 1.f - eps), 1.f + eps);
+    l += mi * fmaxf(l1, l2);
+    cnt += mi;
+    cf += mi * (fabsf(rho - 1.f) > eps ? 1.f : 0.f);
+    kl += mi * ((rho - 1.f) - d);
+  }
+  cnt = block_sum<1024>(cnt, scratch);
+  l = block_sum<1024>(l, scratch);
+  cf = block_sum<1024>(cf, scratch);
+  kl = block_sum<1024>(kl, scratch);
+  const float inv = 1.f / fmaxf(cnt, 1.f);
+  for (int64_t i = threadIdx.x; i < n; i += 1024) {
+    const float d = lp[i] - old[i];
+    const float rho = __expf(d), a = adv[i];
+    const float l1 = -a * rho, l2 = -a * fminf(fmaxf(rho, 1.f - eps), 1.f + eps);
+    dlp[i] = l1 >= l2 ? m[i] * l1 * inv : 0.f;
+  }
+  if (threadIdx.x == 0) {
+    loss[0] = l * inv;
+    metrics[0] = cf * inv;
+    metrics[1] = kl * inv;
+    metrics[2] = cnt;
+  }
+}
+
+// Clipped value loss: 0.5 * sum m * max((V - R)^2, (Vc - R)^2) / sum m,
+// Vc = V_old + clamp(V - V_old, -c, c); dV through whichever branch is the max.
+__global__ __launch_bounds__(1024) void ppo_value_loss_kernel(
+    const float* __restrict__ val, const float* __restrict__ old, const float* __restrict__ ret,
+    const float* __restrict__ m, int64_t n, float clip, float* __restrict__ loss,
+    float* __restrict__ dval) {
+  __shared__ float scratch[16];
+  float cnt = 0.f, l = 0.f;
+  for (int64_t i = threadIdx.x; i < n; i += 1024) {
+    const float mi = m[i], v = val[i], o = old[i], R = ret[i];
+    const float vc = o + fminf(fmaxf(v - o, -clip), clip);
+    l += mi * 0.5f * fmaxf((v - R) * (v - R), (vc - R) * (vc - R));
+    cnt += mi;
+  }
+  cnt = block_sum<1024>(cnt, scratch);
+  l = block_sum<1024>(l, scratch);
+  const float inv = 1.f / fmaxf(cnt, 1.f);
+  for (int64_t i = threadIdx.x; i < n; i += 1024) {
+    const float mi = m[i], v = val[i], o = old[i], R = ret[i];
+    const float dv = v - o;
+    const float vc = o + fminf(fmaxf(dv, -clip), clip);
+    const float u1 = (v - R) * (v - R), u2 = (vc - R) * (vc - R);
+    const float g = u1 >= u2 ? (v - R) : (fabsf(dv) <= clip ? (vc - R) : 0.f);
+    dval[i] = mi * g * inv;
+  }
+  if (threadIdx.x == 0) loss[0] = l * inv;
+}
+
+// ----------------------------------------------------------------------------------------------
+void launch_gae(const float* r, const float* v, const float* m, int S, int T, float gamma,
+                float lam, float* adv, float* ret, hipStream_t st) {
+  if (S == 0 || T == 0) return;
+  gae_kernel<<<S, 64, 0, st>>>(r, v, m, T, gamma, lam, adv, ret);
+}
+void launch_ppo_policy_loss(const float* lp, const float* old, const float* adv, const float* m,
+                            int64_t n, float eps, float* loss, float* dlp, float* metrics,
+                            hipStream_t st) {
+  ppo_policy_loss_kernel<<<1, 1024, 0, st>>>(lp, old, adv, m, n, eps, loss, dlp, metrics);
+}
+void launch_ppo_value_loss(const float* val, const float* old, const float* ret, const float* m,
+                           int64_t n, float clip, float* loss, float* dval, hipStream_t st) {
+  ppo_value_loss_kernel<<<1, 1024, 0, st>>>(val, old, ret, m, n, clip, loss, dval);
 }
 
 // ----------------------------------------------------------------------------------------------

@@ -15,7 +15,7 @@ from typing import Any, Dict, Optional, Tuple
 import torch
 
 from .config import ModelConfig, get_config
-from .reward import RewardModel
+from .reward import RewardModel, ValueModel
 from .tokenizer import load_tokenizer
 from .transformer import CausalLM, build_model, default_dtype
 
@@ -90,6 +90,16 @@ def build_reward_model(base_model_name_or_path: str, pooling: str = "last_token"
     return rm, bundle.tokenizer
 
 
+def build_value_model(base_model_name_or_path: str, device=None, torch_dtype=None, seed: int = 0,
+                      gradient_checkpointing: bool = False) -> Tuple[ValueModel, Any]:
+    """PPO critic on the headless backbone of `base_model_name_or_path` (a preset, a local HF dir
+    or a reward-model `hf/` export: its backbone weights initialise the critic)."""
+    device = torch.device(device) if device is not None else default_device()
+    bundle = load_causal_lm(base_model_name_or_path, gradient_checkpointing=gradient_checkpointing,
+                            torch_dtype=torch_dtype, device=device, seed=seed, headless=True)
+    return ValueModel(bundle.model), bundle.tokenizer
+
+
 def load_reward_checkpoint(rm: RewardModel, path: str, model_index: Optional[int] = None):
     """Load a reward model from an accelerate-layout dir (`model.safetensors`, or
     `model_{i}.safetensors`), an `hf/` export, or `pytorch_model.bin`."""
@@ -133,7 +143,7 @@ def save_hf_pretrained(model, tokenizer, path: str):
 
     p = Path(path)
     p.mkdir(parents=True, exist_ok=True)
-    base = model.backbone if isinstance(model, RewardModel) else model
+    base = model.backbone if isinstance(model, (RewardModel, ValueModel)) else model
     (p / "config.json").write_text(json.dumps(base.cfg.to_hf(), indent=2))
     (p / "dla_config.json").write_text(json.dumps(base.cfg.to_dict(), indent=2))
     sd = {k: v.detach().contiguous().cpu() for k, v in model.hf_state_dict().items()}

@@ -68,3 +68,50 @@ class RewardModel(nn.Module):
         if strict and missing:
             raise KeyError(f"reward checkpoint missing keys: {missing[:8]}")
         return missing, unexpected
+
+
+class ValueModel(nn.Module):
+    """PPO critic: headless native decoder + per-token `Linear(H, 1)` value head. values[s, t]
+    estimates the return from the state that ends at token t (the same grid as the token
+    log-probs: position t scores the action that emits token t + 1). Checkpoint keys:
+    `backbone.*` + `v_head.weight` / `v_head.bias`. Not part of the reference (its RLHF loop is
+    critic-free REINFORCE); used by `ppo.algorithm: ppo`."""
+
+    def __init__(self, backbone: CausalLM):
+        super().__init__()
+        self.backbone = backbone
+        H = backbone.cfg.hidden_size
+        dev, dt = backbone.embed.device, backbone.embed.dtype
+        self.v_head = nn.Linear(H, 1, device=dev, dtype=dt)
+        with torch.no_grad():
+            nn.init.normal_(self.v_head.weight, std=1.0 / (H + 1) ** 0.5)
+            self.v_head.bias.zero_()
+
+    def forward(self, input_ids: torch.Tensor, attention_mask: torch.Tensor = None) -> torch.Tensor:
+        return self.v_head(self.backbone(input_ids, attention_mask)).squeeze(-1).float()
+
+    def hf_state_dict(self) -> Dict[str, torch.Tensor]:
+        from .hf_io import to_hf_state_dict
+
+        sd = {f"backbone.{k}": v for k, v in to_hf_state_dict(self.backbone, base=True).items()}
+        sd["v_head.weight"] = self.v_head.weight.detach()
+        sd["v_head.bias"] = self.v_head.bias.detach()
+        return sd
+
+    @torch.no_grad()
+    def load_hf_state_dict(self, sd: Dict[str, torch.Tensor], strict: bool = True):
+        from .hf_io import load_hf_state_dict
+
+        sd = {(k[len("module."):] if k.startswith("module.") else k): v for k, v in sd.items()}
+        bb = {k[len("backbone."):]: v for k, v in sd.items() if k.startswith("backbone.")}
+        missing, unexpected = load_hf_state_dict(self.backbone, bb, strict=False, base=True)
+        missing = [m for m in missing if not m.startswith("lm_head")]
+        for name in ("weight", "bias"):
+            key = f"v_head.{name}"
+            if key in sd:
+                getattr(self.v_head, name).copy_(sd[key].to(self.v_head.weight.dtype))
+            else:
+                missing.append(key)
+        if strict and missing:
+            raise KeyError(f"value-model checkpoint missing keys: {missing[:8]}")
+        return missing, unexpected

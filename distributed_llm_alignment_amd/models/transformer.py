@@ -310,6 +310,18 @@ class CausalLM(nn.Module):
         lp = self._token_logprob(h.reshape(S * T, H), tgt.reshape(-1)).view(S, T)
         return ops.seq_reduce(lp, mask, mean=(reduction == "mean"))
 
+    def token_logprobs(self, input_ids, attention_mask=None):
+        """[S, T] log p(x_{t+1} | x_<=t) at every scored position (0 elsewhere): the per-action
+        grid of token-level RL objectives (PPO)."""
+        h = self(input_ids, attention_mask)
+        S, T, H = h.shape
+        tgt, _ = ops.shifted_targets(input_ids, attention_mask)
+        if self.lm_head_bias is not None:
+            lg = self.logits(h).float()
+            lp = torch.log_softmax(lg, -1).gather(-1, tgt.clamp(min=0).unsqueeze(-1)).squeeze(-1)
+            return torch.where(tgt >= 0, lp, torch.zeros_like(lp))
+        return self._token_logprob(h.reshape(S * T, H), tgt.reshape(-1)).view(S, T)
+
     def causal_lm_loss(self, input_ids, labels, attention_mask=None):
         """HF ForCausalLMLoss (train_sft.py:145-146): mean token NLL over labels != -100."""
         h = self(input_ids, attention_mask)  # __call__: module hooks (param all-gather waits) run

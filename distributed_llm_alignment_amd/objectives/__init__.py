@@ -5,6 +5,8 @@ benchmarks and tests share one implementation.
   sft_loss         reference train_sft.py:145-146 (HF causal-LM CE, ignore -100)
   reward_loss      reference train_reward.py:139-148 (Bradley-Terry pairwise)
   rlhf_loss        reference train_rlhf.py:127-153 (REINFORCE with KL-shaped reward)
+  ppo_rollout_stats / ppo_loss  token-level actor-critic PPO (GAE, clipped surrogate + value
+                   loss) for `ppo.algorithm: ppo` (north-star config; not in the reference)
   distill_loss     reference train_distill.py:125-147 (CE on rollouts or ensemble forward KL)
 """
 from __future__ import annotations
@@ -77,6 +79,53 @@ def rlhf_loss(policy, ref, seqs, mask, rewards, kl_coef: float = 0.1):
         ref_lp = ref.sequence_logprob(seqs, mask, "mean")
     loss, kl_mean, adv = ops.kl_penalty_pg(pol, ref_lp, rewards, kl_coef)
     return loss, {"kl": kl_mean, "advantages": adv, "policy_logps": pol.detach()}
+
+
+def action_mask(mask: torch.Tensor, prompt_len: int) -> torch.Tensor:
+    """[S, T] fp32: 1 at grid positions t whose action (token t + 1) is a generated, valid token
+    (prompt tokens and padding after EOS are not actions)."""
+    S, T = mask.shape
+    act = torch.zeros((S, T), dtype=torch.float32, device=mask.device)
+    gen = (torch.arange(1, T, device=mask.device) >= prompt_len).float()
+    act[:, :-1] = mask[:, 1:].float() * gen
+    return act
+
+
+@torch.no_grad()
+def ppo_rollout_stats(policy, ref, critic, seqs, mask, prompt_len: int, scores, kl_coef: float = 0.1,
+                      gamma: float = 1.0, lam: float = 0.95, whiten: bool = True):
+    """Token-level PPO targets for one batch of rollouts (actor-critic; the north-star
+    "PPO RLHF (actor + critic + reward)" config). Per-token reward = -kl_coef * (logp - logp_ref)
+    on every action, plus the reward-model score on the last action; GAE(gamma, lam) over the
+    critic's values; advantages whitened over the action tokens."""
+    old_lp = policy.token_logprobs(seqs, mask)
+    ref_lp = ref.token_logprobs(seqs, mask)
+    values = critic(seqs, mask)
+    act = action_mask(mask, prompt_len)
+    kl = (old_lp - ref_lp) * act
+    rewards = -kl_coef * kl
+    S, T = act.shape
+    last = (act * torch.arange(T, device=act.device, dtype=act.dtype)).argmax(1)
+    has = act.sum(1) > 0
+    rewards[torch.arange(S, device=act.device), last] += torch.where(has, scores.float(), torch.zeros_like(scores.float()))
+    adv, ret = ops.gae(rewards, values, act, gamma, lam)
+    if whiten:
+        n = act.sum().clamp(min=1)
+        mu = (adv * act).sum() / n
+        var = (((adv - mu) ** 2) * act).sum() / n
+        adv = (adv - mu) * torch.rsqrt(var + 1e-8) * act
+    return {"old_logp": old_lp, "values": values, "advantages": adv, "returns": ret, "act": act,
+            "kl": kl.sum(1) / act.sum(1).clamp(min=1), "scores": scores.float()}
+
+
+def ppo_loss(policy, critic, seqs, mask, stats: Dict[str, torch.Tensor], clip_eps: float = 0.2,
+             value_clip: float = 0.2, vf_coef: float = 0.1):
+    """Clipped surrogate (HIP fused fwd+bwd) + vf_coef * clipped value loss on one minibatch."""
+    lp = policy.token_logprobs(seqs, mask)
+    pl, pm = ops.ppo_policy_loss(lp, stats["old_logp"], stats["advantages"], stats["act"], clip_eps)
+    v = critic(seqs, mask)
+    vl = ops.ppo_value_loss(v, stats["values"], stats["returns"], stats["act"], value_clip)
+    return pl + vf_coef * vl, {"policy_loss": pl.detach(), "value_loss": vl.detach(), **pm}
 
 
 def distill_loss(student, teachers: Sequence, batch, use_kl: bool):

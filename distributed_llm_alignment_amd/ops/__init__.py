@@ -5,12 +5,14 @@ from .activations import gelu_new, swiglu
 from .attention import RotaryCache, attention_core, qkv_attention, ref_attention
 from .linear import accumulate_weight_grad, linear
 from .logprob import linear_logprob, seq_reduce, sequence_logprob, shifted_targets, token_nll
-from .losses import dpo_loss, ensemble_kl, kl_penalty_pg, pairwise_loss
+from .losses import (dpo_loss, ensemble_kl, gae, kl_penalty_pg, pairwise_loss, ppo_policy_loss,
+                     ppo_value_loss)
 from .norm import add_norm, layer_norm, rms_norm
 
 __all__ = [
     "_ext", "decode", "moe", "gelu_new", "swiglu", "RotaryCache", "attention_core", "qkv_attention",
     "ref_attention", "linear_logprob", "seq_reduce", "sequence_logprob", "shifted_targets",
-    "token_nll", "dpo_loss", "ensemble_kl", "kl_penalty_pg", "pairwise_loss", "add_norm",
-    "layer_norm", "rms_norm", "linear", "accumulate_weight_grad",
+    "token_nll", "dpo_loss", "ensemble_kl", "kl_penalty_pg", "pairwise_loss", "gae",
+    "ppo_policy_loss", "ppo_value_loss", "add_norm", "layer_norm", "rms_norm", "linear",
+    "accumulate_weight_grad",
 ]

@@ -6,6 +6,8 @@ host sync); CPU paths are the literal reference formulas:
   * pairwise_loss   src/models/reward_model.py:67-68
   * kl_penalty_pg   src/training/train_rlhf.py:149-153
   * ensemble_kl     src/training/train_distill.py:127-144
+  * gae / ppo_policy_loss / ppo_value_loss: token-level actor-critic PPO (north-star config; the
+    reference's REINFORCE above stays the default RLHF algorithm)
 """
 from __future__ import annotations
 
@@ -147,3 +149,92 @@ def ensemble_kl(student_logits: torch.Tensor, teacher_logits: torch.Tensor) -> t
     logq = F.log_softmax(student_logits.float(), dim=-1)
     pbar = torch.softmax(teacher_logits.float(), dim=-1).mean(0)
     return F.kl_div(logq, pbar, reduction="none").sum(-1)
+
+
+# ------------------------------------------------------------- PPO (actor-critic) objectives
+# Token-level PPO for the north-star "PPO RLHF (actor + critic + reward)" configuration; the
+# reference's sequence-level REINFORCE (train_rlhf.py:149-153, `kl_penalty_pg` above) stays the
+# default algorithm. [S, T] fp32 grids; `mask` selects action tokens.
+def gae(rewards: torch.Tensor, values: torch.Tensor, mask: torch.Tensor, gamma: float = 1.0,
+        lam: float = 0.95):
+    """Generalised advantage estimation (no gradient):
+    A_t = m_t (delta_t + gamma lam m_{t+1} A_{t+1}), delta_t = r_t + gamma m_{t+1} V_{t+1} - V_t.
+    Returns (advantages, returns = A + V)."""
+    r = rewards.detach().float().contiguous()
+    v = values.detach().float().contiguous()
+    m = mask.detach().float().contiguous()
+    if _ext.use_native(r):
+        return _ext.require().gae(r, v, m, float(gamma), float(lam))
+    S, T = r.shape
+    adv = torch.zeros_like(r)
+    nxt = torch.zeros(S, dtype=r.dtype, device=r.device)
+    zero = torch.zeros_like(nxt)
+    for t in range(T - 1, -1, -1):
+        mn = m[:, t + 1] if t + 1 < T else zero
+        vn = v[:, t + 1] if t + 1 < T else zero
+        delta = r[:, t] + gamma * mn * vn - v[:, t]
+        nxt = m[:, t] * (delta + gamma * lam * mn * nxt)
+        adv[:, t] = nxt
+    return adv, adv + v
+
+
+class _PPOPolicyFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, lp, old, adv, mask, eps):
+        loss, dlp, metrics = _ext.require().ppo_policy_loss(lp, old, adv, mask, eps)
+        ctx.save_for_backward(dlp)
+        ctx.mark_non_differentiable(metrics)
+        return loss, metrics
+
+    @staticmethod
+    def backward(ctx, gloss, _gm):
+        (dlp,) = ctx.saved_tensors
+        return dlp * gloss, None, None, None, None
+
+
+def ppo_policy_loss(logp: torch.Tensor, old_logp: torch.Tensor, advantages: torch.Tensor,
+                    mask: torch.Tensor, clip_eps: float = 0.2):
+    """Clipped surrogate, mean over masked tokens of max(-A rho, -A clip(rho, 1 +- eps)),
+    rho = exp(logp - old_logp). Returns (loss, {clipfrac, approx_kl}) (device tensors)."""
+    lp = logp.float().contiguous()
+    old = old_logp.detach().float().contiguous()
+    a = advantages.detach().float().contiguous()
+    m = mask.detach().float().contiguous()
+    if _ext.use_native(lp):
+        loss, met = _PPOPolicyFn.apply(lp, old, a, m, float(clip_eps))
+        return loss, {"clipfrac": met[0], "approx_kl": met[1]}
+    n = m.sum().clamp(min=1)
+    rho = torch.exp(lp - old)
+    per = torch.maximum(-a * rho, -a * rho.clamp(1 - clip_eps, 1 + clip_eps))
+    loss = (per * m).sum() / n
+    with torch.no_grad():
+        clipfrac = (((rho - 1).abs() > clip_eps).float() * m).sum() / n
+        akl = (((rho - 1) - (lp - old)) * m).sum() / n
+    return loss, {"clipfrac": clipfrac, "approx_kl": akl}
+
+
+class _PPOValueFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, val, old, ret, mask, clip):
+        loss, dval = _ext.require().ppo_value_loss(val, old, ret, mask, clip)
+        ctx.save_for_backward(dval)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        (dval,) = ctx.saved_tensors
+        return dval * g, None, None, None, None
+
+
+def ppo_value_loss(values: torch.Tensor, old_values: torch.Tensor, returns: torch.Tensor,
+                   mask: torch.Tensor, clip: float = 0.2) -> torch.Tensor:
+    """0.5 * masked mean of max((V - R)^2, (V_clip - R)^2), V_clip = V_old + clamp(V - V_old, +-c)."""
+    v = values.float().contiguous()
+    old = old_values.detach().float().contiguous()
+    R = returns.detach().float().contiguous()
+    m = mask.detach().float().contiguous()
+    if _ext.use_native(v):
+        return _PPOValueFn.apply(v, old, R, m, float(clip))
+    n = m.sum().clamp(min=1)
+    vc = old + (v - old).clamp(-clip, clip)
+    return 0.5 * (torch.maximum((v - R) ** 2, (vc - R) ** 2) * m).sum() / n

@@ -230,9 +230,10 @@ def apply_tensor_parallel(model, group, tp_rank: Optional[int] = None, tp_size: 
     else:
         for p in vocab_params:
             p._dla_tp_replicated = True
-    if hasattr(model, "scorer"):
-        for p in model.scorer.parameters():
-            p._dla_tp_replicated = True
+    for head in ("scorer", "v_head"):  # reward / value heads are replicated across TP ranks
+        if hasattr(model, head):
+            for p in getattr(model, head).parameters():
+                p._dla_tp_replicated = True
     base.tp = group
     base.tp_size = tp
     base.tp_rank = r

@@ -11,6 +11,14 @@ fixes #8), then REINFORCE with a KL-shaped reward and a mean baseline:
 Overlap (BASELINE north star, `ppo.async_rollouts: true`, off by default since it changes the
 semantics to one-step-stale rollouts): step k+1's rollouts are generated while step k's gradient
 reduce-scatter is still in flight on RCCL's stream.
+
+`ppo.algorithm: ppo` (not in the reference, whose loop is critic-free) switches to token-level
+actor-critic PPO, the north-star "PPO RLHF (actor + critic + reward)" configuration: a critic
+(`ValueModel`, initialised from `critic.base_model_name_or_path` or the reward backbone) gives
+per-token values, the per-token reward is -kl_coef * (logp - logp_ref) plus the reward-model
+score on the last generated token, advantages are GAE(gamma, lam) (HIP wave-scan kernel),
+whitened; `ppo_epochs` x `num_minibatches` updates of the clipped surrogate + `vf_coef` x the
+clipped value loss (fused HIP fwd+bwd kernels), policy and critic each on their own engine.
 """
 from __future__ import annotations
 
@@ -22,8 +30,9 @@ from typing import Dict, List
 import torch
 
 from ..data import read_jsonl
-from ..models import build_reward_model, generate, load_causal_lm, load_reward_checkpoint
-from ..objectives import rlhf_loss
+from ..models import (build_reward_model, build_value_model, generate, load_causal_lm,
+                      load_reward_checkpoint)
+from ..objectives import ppo_loss, ppo_rollout_stats, rlhf_loss
 from ..parallel.dist import barrier, split_for_rank
 from ..utils.checkpoint import save_state
 from ..utils.config import add_config_args, config_from_args
@@ -103,6 +112,9 @@ def main(argv=None) -> int:
     gen_g.manual_seed(ctx.seed * 1000 + (ctx.mesh.dp_rank if ctx.mesh is not None else ctx.dist.rank))
     running = RunningLoss()
     log_every = (config.get("logging", {}) or {}).get("log_every_steps", 10)
+    algo = str(ppo.get("algorithm", "reinforce")).lower()
+    if algo not in ("reinforce", "ppo"):
+        raise ValueError(f"ppo.algorithm must be reinforce|ppo, got {algo!r}")
 
     def rollout():
         batch_prompts = rng.sample(prompts, k=min(batch_size, len(prompts)))
@@ -118,12 +130,14 @@ def main(argv=None) -> int:
         renc = rtok(fused, return_tensors="pt", padding=True, truncation=True, max_length=max_len)
         with torch.no_grad():
             scores = rm(renc["input_ids"].to(ctx.device), renc["attention_mask"].to(ctx.device))
-        return seqs, mask, scores
+        return seqs, mask, scores, ids.shape[1]
 
     policy.model.train()
+    if algo == "ppo":
+        return _ppo_loop(ctx, config, ppo, policy, ref, rm, rollout, engine, steps, kl_coef, log_every)
     pending = rollout()
     for step in range(steps):
-        seqs, mask, scores = pending
+        seqs, mask, scores, _ = pending
         loss, m = rlhf_loss(policy.model, ref.model, seqs, mask, scores, kl_coef)
         loss.backward()
         if ppo.get("async_rollouts", False) and step + 1 < steps:
@@ -144,6 +158,67 @@ def main(argv=None) -> int:
     barrier()
     save_state(config["logging"]["output_dir"], [policy.model, ref.model, rm], engine, None, steps, tok)
     ctx.log("RLHF PPO loop complete")
+    ctx.logger.close()
+    return 0
+
+
+def _ppo_loop(ctx, config, ppo, policy, ref, rm, rollout, engine, steps, kl_coef, log_every) -> int:
+    """Token-level actor-critic PPO (`ppo.algorithm: ppo`)."""
+    model_cfg = config["model"]
+    ccfg = config.get("critic", {}) or {}
+    rcfg = config.get("reward_model", {}) or {}
+    cbase = ccfg.get("base_model_name_or_path") or rcfg.get("base_model_name_or_path") \
+        or model_cfg["policy_model_name_or_path"]
+    critic, _ = build_value_model(cbase, device=ctx.device, seed=ctx.seed + 1,
+                                  gradient_checkpointing=ccfg.get("gradient_checkpointing",
+                                                                  model_cfg.get("gradient_checkpointing", True)))
+    parallelize(ctx, critic)
+    critic.train()
+    critic_engine = make_engine(ctx, critic, lr=ccfg.get("learning_rate", ppo.get("learning_rate", 1e-6)),
+                                betas=(0.9, 0.95), weight_decay=ppo.get("weight_decay", 0.01),
+                                max_grad_norm=ppo.get("max_grad_norm", 1.0))
+    gamma, lam = float(ppo.get("gamma", 1.0)), float(ppo.get("lam", 0.95))
+    clip, vclip = float(ppo.get("clip_range", 0.2)), float(ppo.get("value_clip_range", 0.2))
+    vf_coef = float(ppo.get("vf_coef", 0.1))
+    epochs, nmb = int(ppo.get("ppo_epochs", 1)), max(1, int(ppo.get("num_minibatches", 1)))
+    overlap = bool(ppo.get("async_rollouts", False))
+    running = RunningLoss()
+    pending = rollout()
+    for step in range(steps):
+        seqs, mask, scores, tp = pending
+        stats = ppo_rollout_stats(policy.model, ref.model, critic, seqs, mask, tp, scores, kl_coef,
+                                  gamma, lam)
+        S = seqs.shape[0]
+        bounds = [(i * S // nmb, (i + 1) * S // nmb) for i in range(nmb)]
+        for ep in range(epochs):
+            for mi, (a, b) in enumerate(bounds):
+                if b <= a:
+                    continue
+                mb = {k: v[a:b] for k, v in stats.items() if k in ("old_logp", "values", "advantages", "returns", "act")}
+                loss, m = ppo_loss(policy.model, critic, seqs[a:b], mask[a:b], mb, clip, vclip, vf_coef)
+                loss.backward()
+                last = ep == epochs - 1 and mi == len(bounds) - 1
+                if last and overlap and step + 1 < steps:
+                    pending = rollout()  # overlaps the in-flight gradient reduce-scatter
+                engine.step()
+                critic_engine.step()
+                running.update(loss.detach())
+        if not overlap and step + 1 < steps:
+            pending = rollout()
+        if (step + 1) % log_every == 0:
+            ctx.logger.log({"train/loss": running.average, "train/kl": stats["kl"].mean(),
+                            "train/reward_mean": stats["scores"].mean(),
+                            "train/policy_loss": m["policy_loss"], "train/value_loss": m["value_loss"],
+                            "train/clipfrac": m["clipfrac"], "train/approx_kl": m["approx_kl"],
+                            "train/grad_norm": engine.last_grad_norm}, step + 1)
+            running = RunningLoss()
+    barrier()
+    out = save_state(config["logging"]["output_dir"], [policy.model, ref.model, rm, critic], engine, None,
+                     steps, policy.tokenizer)
+    torch.save({k: (v.cpu() if isinstance(v, torch.Tensor) else v)
+                for k, v in critic_engine.optimizer_state().items()},
+               Path(out) / f"critic_optimizer_shard_{ctx.dist.rank}.pt")
+    ctx.log("RLHF PPO (actor-critic) loop complete")
     ctx.logger.close()
     return 0
 

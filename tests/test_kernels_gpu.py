@@ -286,6 +286,39 @@ def test_pairwise_and_kl_penalty_kernels():
     assert torch.allclose(lp.grad.cpu(), lp2.grad, atol=1e-6)
 
 
+@pytest.mark.parametrize("T", [37, 1280])
+def test_ppo_gae_and_clipped_loss_kernels(T):
+    """Wave-scan GAE and the fused clipped policy / value loss kernels vs the fp32 references."""
+    S = 6
+    r, v = torch.randn(S, T), torch.randn(S, T)
+    m = (torch.rand(S, T) > 0.2).float()
+    m[2] = 0
+    adv, ret = ops.gae(r.to(DEV), v.to(DEV), m.to(DEV), 0.99, 0.95)
+    adv2, ret2 = ops.gae(r, v, m, 0.99, 0.95)
+    assert torch.allclose(adv.cpu(), adv2, atol=1e-4, rtol=1e-4)
+    assert torch.allclose(ret.cpu(), ret2, atol=1e-4, rtol=1e-4)
+    lp = (torch.randn(S, T) * 0.3).to(DEV).requires_grad_()
+    old = lp.detach() + 0.3 * torch.randn(S, T, device=DEV)
+    a = torch.randn(S, T, device=DEV)
+    loss, met = ops.ppo_policy_loss(lp, old, a, m.to(DEV), 0.2)
+    loss.backward()
+    lp2 = lp.detach().cpu().requires_grad_()
+    loss2, met2 = ops.ppo_policy_loss(lp2, old.cpu(), a.cpu(), m, 0.2)
+    loss2.backward()
+    assert abs(loss.item() - loss2.item()) < 1e-4
+    assert abs(met["clipfrac"].item() - met2["clipfrac"].item()) < 1e-5
+    assert torch.allclose(lp.grad.cpu(), lp2.grad, atol=1e-6)
+    val = torch.randn(S, T, device=DEV).requires_grad_()
+    ov, R = val.detach() + 0.5 * torch.randn(S, T, device=DEV), torch.randn(S, T, device=DEV)
+    vl = ops.ppo_value_loss(val, ov, R, m.to(DEV), 0.2)
+    vl.backward()
+    val2 = val.detach().cpu().requires_grad_()
+    vl2 = ops.ppo_value_loss(val2, ov.cpu(), R.cpu(), m, 0.2)
+    vl2.backward()
+    assert abs(vl.item() - vl2.item()) < 1e-4
+    assert torch.allclose(val.grad.cpu(), val2.grad, atol=1e-6)
+
+
 def test_ensemble_kl_kernel():
     N, V, K = 33, 1000, 3
     s = bf(torch.randn(N, V)).requires_grad_()

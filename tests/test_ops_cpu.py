@@ -182,3 +182,50 @@ def test_clip_coefficient_matches_clip_grad_norm():
     tn = torch.nn.utils.clip_grad_norm_([p], 1.0)
     assert torch.allclose(norm, tn, atol=1e-4)
     assert torch.allclose(g * coef, p.grad, atol=1e-5)
+
+
+def test_gae_matches_per_sequence_loop():
+    from distributed_llm_alignment_amd.ops import gae
+
+    torch.manual_seed(0)
+    S, T, gamma, lam = 3, 37, 0.99, 0.9
+    r, v = torch.randn(S, T), torch.randn(S, T)
+    m = torch.zeros(S, T)
+    m[0, 5:30] = 1
+    m[1, :] = 1
+    m[2, 10:11] = 1
+    adv, ret = gae(r, v, m, gamma, lam)
+    for s in range(S):
+        a_next = 0.0
+        for t in range(T - 1, -1, -1):
+            mn = m[s, t + 1].item() if t + 1 < T else 0.0
+            vn = v[s, t + 1].item() if t + 1 < T else 0.0
+            delta = r[s, t].item() + gamma * mn * vn - v[s, t].item()
+            a = m[s, t].item() * (delta + gamma * lam * mn * a_next)
+            assert abs(adv[s, t].item() - a) < 1e-4
+            a_next = a
+    assert torch.allclose(ret, adv + v)
+
+
+def test_ppo_losses_match_clipped_formulas():
+    from distributed_llm_alignment_amd.ops import ppo_policy_loss, ppo_value_loss
+
+    torch.manual_seed(1)
+    N = 64
+    lp = torch.randn(N, dtype=torch.float64).mul(0.3).requires_grad_()
+    old = lp.detach() + torch.randn(N, dtype=torch.float64) * 0.3
+    adv, m = torch.randn(N, dtype=torch.float64), (torch.rand(N) > 0.3).double()
+    loss, met = ppo_policy_loss(lp, old, adv, m, 0.2)
+    loss.backward()
+    rho = torch.exp(lp.detach().float() - old.float())
+    per = torch.maximum(-adv.float() * rho, -adv.float() * rho.clamp(0.8, 1.2))
+    assert abs(loss.item() - ((per * m.float()).sum() / m.sum()).item()) < 1e-5
+    unclipped = (-adv.float() * rho) >= (-adv.float() * rho.clamp(0.8, 1.2))
+    g = torch.where(unclipped, -adv.float() * rho, torch.zeros_like(rho)) * m.float() / m.sum()
+    assert torch.allclose(lp.grad.float(), g, atol=1e-5)
+    v = torch.randn(N).requires_grad_()
+    ov, R = v.detach() + torch.randn(N) * 0.5, torch.randn(N)
+    vl = ppo_value_loss(v, ov, R, m.float(), 0.2)
+    vc = ov + (v.detach() - ov).clamp(-0.2, 0.2)
+    ref = 0.5 * (torch.maximum((v.detach() - R) ** 2, (vc - R) ** 2) * m.float()).sum() / m.sum()
+    assert abs(vl.item() - ref.item()) < 1e-5

@@ -241,3 +241,47 @@ def test_north_star_configs_run_scaled_down(tmp_path, cfg_name, ov):
         args += ["--override", o]
     assert train_dpo.main(args) == 0
     assert (tmp_path / "ck" / "final" / "model.safetensors").exists()
+
+
+def test_rlhf_ppo_actor_critic(tmp_path):
+    """`ppo.algorithm: ppo`: critic + GAE + clipped surrogate/value losses, 2 minibatches x
+    2 epochs, critic checkpoint as the 4th model."""
+    from distributed_llm_alignment_amd.training import train_rlhf
+
+    d = tmp_path
+    write_jsonl(d / "prompts.jsonl", synthetic_prompt_records(8, seed=4))
+    rl = {"seed": 5, "model": {"policy_model_name_or_path": "tiny-llama",
+                               "reference_model_name_or_path": "tiny-llama", "max_seq_length": 64},
+          "reward_model": {"base_model_name_or_path": "tiny-llama"},
+          "ppo": {"algorithm": "ppo", "batch_size": 4, "learning_rate": 1e-4, "kl_coef": 0.05,
+                  "steps": 3, "ppo_epochs": 2, "num_minibatches": 2, "gamma": 1.0, "lam": 0.95,
+                  "vf_coef": 0.1, "generation_params": {"max_new_tokens": 6, "temperature": 0.7,
+                                                        "top_p": 0.9}},
+          "sampling": {"source": "local", "prompt_path": str(d / "prompts.jsonl")},
+          "logging": {"output_dir": str(d / "ck" / "ppo"), "log_dir": str(d / "logs" / "ppo"),
+                      "log_every_steps": 1}}
+    assert train_rlhf.main(["--config", _cfg(d, "ppo", rl)]) == 0
+    m = _metrics(d / "logs" / "ppo")
+    for k in ("train/loss", "train/kl", "train/value_loss", "train/clipfrac", "train/approx_kl"):
+        assert k in m[-1], k
+    assert all(abs(r["train/loss"]) < 1e4 for r in m)
+    for f in ("model.safetensors", "model_3.safetensors", "critic_optimizer_shard_0.pt"):
+        assert (d / "ck" / "ppo" / f).exists(), f
+
+
+@pytest.mark.parametrize("cfg_name", ["rlhf_llama3_8b", "rlhf_ppo_llama3_8b"])
+def test_rlhf_north_star_configs_run_scaled_down(tmp_path, cfg_name):
+    """The shipped RLHF north-star configs (REINFORCE and actor-critic PPO) drive the trainer
+    with the architecture overridden to the tiny preset, world 1."""
+    from distributed_llm_alignment_amd.training import train_rlhf
+
+    root = Path(__file__).resolve().parents[1]
+    args = ["--config", str(root / "config" / f"{cfg_name}.yaml")]
+    for o in ["model.policy_model_name_or_path=tiny-llama", "model.reference_model_name_or_path=tiny-llama",
+              "reward_model.base_model_name_or_path=tiny-llama", "critic.base_model_name_or_path=tiny-llama",
+              "model.max_seq_length=48", "sampling.num_samples=8", "ppo.batch_size=4", "ppo.steps=2",
+              "ppo.generation_params.max_new_tokens=4", f"logging.output_dir={tmp_path / 'ck'}",
+              f"logging.log_dir={tmp_path / 'logs'}", "logging.log_every_steps=1"]:
+        args += ["--override", o]
+    assert train_rlhf.main(args) == 0
+    assert (tmp_path / "ck" / "model_2.safetensors").exists()
