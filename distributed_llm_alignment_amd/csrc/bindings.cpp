@@ -31,6 +31,8 @@ int norm_bwd_grid(int rows);
 int norm_wgrad_scratch_rows();
 void launch_swiglu_fwd(const bf16_t*, bf16_t*, int64_t, int, hipStream_t);
 void launch_swiglu_bwd(const bf16_t*, const bf16_t*, bf16_t*, int64_t, int, hipStream_t);
+void launch_swiglu_fwd_t(const bf16_t*, bf16_t*, bf16_t*, int64_t, int, hipStream_t);
+void launch_swiglu_bwd_t(const bf16_t*, const bf16_t*, bf16_t*, bf16_t*, int64_t, int, hipStream_t);
 void launch_gelu_fwd(const bf16_t*, bf16_t*, int64_t, hipStream_t);
 void launch_gelu_bwd(const bf16_t*, const bf16_t*, bf16_t*, int64_t, hipStream_t);
 void launch_rope_fwd(const bf16_t*, int64_t, bf16_t*, bf16_t*, const float*, const float*,
@@ -183,6 +185,33 @@ at::Tensor swiglu_bwd(const at::Tensor& gu, const at::Tensor& dout) {
   auto dgu = at::empty_like(gu);
   launch_swiglu_bwd(cbp(gu), cbp(dout), bp(dgu), rows, static_cast<int>(F), cur_stream(gu));
   return dgu;
+}
+
+// SwiGLU that also writes the transposed output ([F, rows]) for the TN weight-gradient GEMMs.
+std::tuple<at::Tensor, at::Tensor> swiglu_fwd_t(const at::Tensor& gu) {
+  check_bf16(gu, "gu");
+  TORCH_CHECK(gu.is_contiguous() && gu.dim() == 2, "gu: contiguous [rows, 2F]");
+  const int64_t rows = gu.size(0), F = gu.size(1) / 2;
+  TORCH_CHECK(gu.size(1) == 2 * F && F % 64 == 0, "F must be a multiple of 64");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(gu.device());
+  auto out = at::empty({rows, F}, gu.options());
+  auto outT = at::empty({F, rows}, gu.options());
+  launch_swiglu_fwd_t(cbp(gu), bp(out), bp(outT), rows, static_cast<int>(F), cur_stream(gu));
+  return {out, outT};
+}
+
+std::tuple<at::Tensor, at::Tensor> swiglu_bwd_t(const at::Tensor& gu, const at::Tensor& dout) {
+  check_bf16(gu, "gu");
+  check_bf16(dout, "dout");
+  TORCH_CHECK(gu.is_contiguous() && dout.is_contiguous() && gu.dim() == 2, "contiguous 2-D");
+  const int64_t rows = gu.size(0), F = gu.size(1) / 2;
+  TORCH_CHECK(gu.size(1) == 2 * F && F % 64 == 0 && dout.numel() == rows * F, "shapes");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(gu.device());
+  auto dgu = at::empty_like(gu);
+  auto dguT = at::empty({2 * F, rows}, gu.options());
+  launch_swiglu_bwd_t(cbp(gu), cbp(dout), bp(dgu), bp(dguT), rows, static_cast<int>(F),
+                      cur_stream(gu));
+  return {dgu, dguT};
 }
 
 at::Tensor gelu_fwd(const at::Tensor& x) {
@@ -751,6 +780,8 @@ TORCH_LIBRARY(dla, m) {
   m.def("norm_bwd(Tensor dy, Tensor s, Tensor w, Tensor rstd, Tensor? mean, Tensor? dres, bool has_bias, bool rms) -> (Tensor, Tensor, Tensor)");
   m.def("swiglu_fwd(Tensor gu) -> Tensor");
   m.def("swiglu_bwd(Tensor gu, Tensor dout) -> Tensor");
+  m.def("swiglu_fwd_t(Tensor gu) -> (Tensor, Tensor)");
+  m.def("swiglu_bwd_t(Tensor gu, Tensor dout) -> (Tensor, Tensor)");
   m.def("gelu_fwd(Tensor x) -> Tensor");
   m.def("gelu_bwd(Tensor x, Tensor dy) -> Tensor");
   m.def("rope_fwd(Tensor qkv, Tensor cos, Tensor sin, Tensor? pos, int Hq, int Hkv, int D, int rot, int T, int pos_offset) -> (Tensor, Tensor)");
@@ -780,6 +811,8 @@ TORCH_LIBRARY_IMPL(dla, CUDA, m) {
   m.impl("norm_bwd", &dla::norm_bwd);
   m.impl("swiglu_fwd", &dla::swiglu_fwd);
   m.impl("swiglu_bwd", &dla::swiglu_bwd);
+  m.impl("swiglu_fwd_t", &dla::swiglu_fwd_t);
+  m.impl("swiglu_bwd_t", &dla::swiglu_bwd_t);
   m.impl("gelu_fwd", &dla::gelu_fwd);
   m.impl("gelu_bwd", &dla::gelu_bwd);
   m.impl("rope_fwd", &dla::rope_fwd);

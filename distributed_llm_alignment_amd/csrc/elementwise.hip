@@ -52,6 +52,121 @@ __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const bf16_t* __restric
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// SwiGLU with a transposed second output, for the fused MLP autograd node (ops.swiglu_mlp).
+// The weight-gradient GEMMs run in the TN layout on transposed activations (ops/linear.py), so
+// the MLP backward needs m^T (down_proj) and dgu^T (gate|up proj): producing them here, from the
+// values already in registers, costs one extra write instead of a separate transpose pass
+// (read + write). 64 x 64 tiles: 256 threads, each owns 2 rows x 8 columns; the transposed copy
+// goes through a padded LDS tile (16-byte row stores on both sides).
+constexpr int kTT = 64, kTPad = 8;
+
+__global__ __launch_bounds__(256) void swiglu_fwd_t_kernel(const bf16_t* __restrict__ gu,
+                                                            bf16_t* __restrict__ out,
+                                                            bf16_t* __restrict__ outT,
+                                                            int64_t rows, int F) {
+  __shared__ bf16_t tile[kTT][kTT + kTPad];
+  const int64_t r0 = static_cast<int64_t>(blockIdx.y) * kTT;
+  const int c0 = blockIdx.x * kTT;
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int v = t + 256 * k;
+    const int rr = v >> 3, cv = (v & 7) * 8;
+    const int64_t r = r0 + rr;
+    bf16x8 o = {};
+    if (r < rows) {  // F % 64 == 0 is checked on the host
+      const bf16_t* row = gu + r * 2 * F;
+      const bf16x8 g = load_bf16x8(row + c0 + cv), u = load_bf16x8(row + F + c0 + cv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = f2bf(silu_f(bf2f(g[j])) * bf2f(u[j]));
+      store_bf16x8(out + r * F + c0 + cv, o);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) tile[rr][cv + j] = o[j];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {  // outT[c0 + cc][r0 + rv .. +8]
+    const int v = t + 256 * k;
+    const int cc = v >> 3, rv = (v & 7) * 8;
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = tile[rv + j][cc];
+    const int64_t oc = r0 + rv;
+    bf16_t* dst = outT + static_cast<int64_t>(c0 + cc) * rows + oc;
+    if (oc + 8 <= rows) {
+      store_bf16x8(dst, o);
+    } else {
+      for (int j = 0; j < 8; ++j)
+        if (oc + j < rows) dst[j] = o[j];
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void swiglu_bwd_t_kernel(const bf16_t* __restrict__ gu,
+                                                            const bf16_t* __restrict__ dout,
+                                                            bf16_t* __restrict__ dgu,
+                                                            bf16_t* __restrict__ dguT,
+                                                            int64_t rows, int F) {
+  __shared__ bf16_t tg[kTT][kTT + kTPad];
+  __shared__ bf16_t tu[kTT][kTT + kTPad];
+  const int64_t r0 = static_cast<int64_t>(blockIdx.y) * kTT;
+  const int c0 = blockIdx.x * kTT;
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int v = t + 256 * k;
+    const int rr = v >> 3, cv = (v & 7) * 8;
+    const int64_t r = r0 + rr;
+    bf16x8 dg = {}, du = {};
+    if (r < rows) {
+      const bf16_t* row = gu + r * 2 * F;
+      const bf16x8 g = load_bf16x8(row + c0 + cv), u = load_bf16x8(row + F + c0 + cv);
+      const bf16x8 d = load_bf16x8(dout + r * F + c0 + cv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float gf = bf2f(g[j]), uf = bf2f(u[j]), df = bf2f(d[j]);
+        const float sg = sigmoidf_(gf);
+        du[j] = f2bf(df * gf * sg);
+        dg[j] = f2bf(df * uf * sg * (1.f + gf * (1.f - sg)));
+      }
+      store_bf16x8(dgu + r * 2 * F + c0 + cv, dg);
+      store_bf16x8(dgu + r * 2 * F + F + c0 + cv, du);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      tg[rr][cv + j] = dg[j];
+      tu[rr][cv + j] = du[j];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {  // dguT[c0 + cc] (gate rows) and dguT[F + c0 + cc] (up rows)
+    const int v = t + 256 * k;
+    const int cc = v >> 3, rv = (v & 7) * 8;
+    bf16x8 a, b;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      a[j] = tg[rv + j][cc];
+      b[j] = tu[rv + j][cc];
+    }
+    const int64_t oc = r0 + rv;
+    bf16_t* da = dguT + static_cast<int64_t>(c0 + cc) * rows + oc;
+    bf16_t* db = dguT + static_cast<int64_t>(F + c0 + cc) * rows + oc;
+    if (oc + 8 <= rows) {
+      store_bf16x8(da, a);
+      store_bf16x8(db, b);
+    } else {
+      for (int j = 0; j < 8; ++j)
+        if (oc + j < rows) {
+          da[j] = a[j];
+          db[j] = b[j];
+        }
+    }
+  }
+}
+
 // gelu_new (tanh approximation), as used by GPT-2 and phi-2.
 __device__ __forceinline__ float gelu_tanh(float x, float* dgdx) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
@@ -98,6 +213,18 @@ void launch_swiglu_fwd(const bf16_t* gu, bf16_t* out, int64_t rows, int F, hipSt
 void launch_swiglu_bwd(const bf16_t* gu, const bf16_t* dout, bf16_t* dgu, int64_t rows, int F,
                        hipStream_t st) {
   swiglu_bwd_kernel<<<grid_for(rows * (F / 8)), 256, 0, st>>>(gu, dout, dgu, rows, F);
+}
+void launch_swiglu_fwd_t(const bf16_t* gu, bf16_t* out, bf16_t* outT, int64_t rows, int F,
+                         hipStream_t st) {
+  if (rows == 0) return;
+  const dim3 grid(F / kTT, static_cast<unsigned>((rows + kTT - 1) / kTT));
+  swiglu_fwd_t_kernel<<<grid, 256, 0, st>>>(gu, out, outT, rows, F);
+}
+void launch_swiglu_bwd_t(const bf16_t* gu, const bf16_t* dout, bf16_t* dgu, bf16_t* dguT,
+                         int64_t rows, int F, hipStream_t st) {
+  if (rows == 0) return;
+  const dim3 grid(F / kTT, static_cast<unsigned>((rows + kTT - 1) / kTT));
+  swiglu_bwd_t_kernel<<<grid, 256, 0, st>>>(gu, dout, dgu, dguT, rows, F);
 }
 void launch_gelu_fwd(const bf16_t* x, bf16_t* y, int64_t n, hipStream_t st) {
   gelu_fwd_kernel<<<grid_for(n / 8), 256, 0, st>>>(x, y, n / 8);

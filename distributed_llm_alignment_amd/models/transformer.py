@@ -100,6 +100,14 @@ class MLP(nn.Module):
             from ..parallel.tensor_parallel import tp_copy
 
             h = tp_copy(h, self.tp)
+        if (self.cfg.activation == "swiglu" and self.up_bias is None and self.down_bias is None
+                and ops.swiglu_mlp_ok(h, self.up_proj, self.down_proj)):
+            out = ops.swiglu_mlp(h, self.up_proj, self.down_proj)
+            if self.tp is None:
+                return out
+            from ..parallel.tensor_parallel import tp_reduce
+
+            return tp_reduce(out, self.tp)
         u = ops.linear(h, self.up_proj, self.up_bias)
         m = ops.swiglu(u) if self.cfg.activation == "swiglu" else ops.gelu_new(u)
         if self.tp is None:

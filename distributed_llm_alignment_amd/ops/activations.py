@@ -9,7 +9,12 @@ import math
 import torch
 import torch.nn.functional as F
 
+import os
+
 from . import _ext
+from .linear import accumulate_weight_grad, input_grad, uses_main_grad
+
+FUSED_MLP = os.environ.get("DLA_FUSED_MLP", "1") != "0"
 
 
 class _SwiGLUFn(torch.autograd.Function):
@@ -32,6 +37,51 @@ def swiglu(gu: torch.Tensor) -> torch.Tensor:
         return _SwiGLUFn.apply(gu)
     g, u = gu.float().chunk(2, dim=-1)
     return (F.silu(g) * u).to(gu.dtype)
+
+
+class _SwiGLUMLPFn(torch.autograd.Function):
+    """down(swiglu(h @ Wgu^T)) as ONE autograd node for weights that accumulate into the engine's
+    main_grad. The HIP SwiGLU kernels also emit m^T (forward) and dgu^T (backward), the operands
+    the TN weight-gradient GEMMs (ops/linear.py) would otherwise transpose in separate passes:
+    per Llama-3-8B layer and micro-batch that removes a read+write of [M, 3F] bf16."""
+
+    @staticmethod
+    def forward(ctx, h, w_up, w_down):
+        ops = _ext.require()
+        H = h.shape[-1]
+        h2 = h.reshape(-1, H)
+        u = F.linear(h2, w_up)
+        m, mt = ops.swiglu_fwd_t(u)
+        y = F.linear(m, w_down)
+        ctx.save_for_backward(h2, u, mt, w_up, w_down)
+        ctx.hshape = h.shape
+        return y.view(*h.shape[:-1], w_down.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        h2, u, mt, w_up, w_down = ctx.saved_tensors
+        ops = _ext.require()
+        dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
+        dm = input_grad(dy2, w_down)
+        accumulate_weight_grad(w_down, dy2, mt.t(), xt=mt)
+        del mt
+        du, dut = ops.swiglu_bwd_t(u, dm)
+        del dm
+        dh = input_grad(du, w_up) if ctx.needs_input_grad[0] else None
+        accumulate_weight_grad(w_up, du, h2, dyt=dut)
+        return (dh.view(ctx.hshape) if dh is not None else None), None, None
+
+
+def swiglu_mlp_ok(h: torch.Tensor, w_up: torch.Tensor, w_down: torch.Tensor) -> bool:
+    return (FUSED_MLP and _ext.use_native(h) and h.dtype == torch.bfloat16 and uses_main_grad(w_up)
+            and uses_main_grad(w_down) and w_up.shape[0] == 2 * w_down.shape[1]
+            and w_down.shape[1] % 64 == 0 and h.numel() // h.shape[-1] % 8 == 0)
+
+
+def swiglu_mlp(h: torch.Tensor, w_up: torch.Tensor, w_down: torch.Tensor) -> torch.Tensor:
+    """Bias-free SwiGLU MLP with main_grad weight accumulation (see _SwiGLUMLPFn); callers check
+    `swiglu_mlp_ok` first."""
+    return _SwiGLUMLPFn.apply(h, w_up, w_down)
 
 
 class _GeluFn(torch.autograd.Function):

@@ -56,32 +56,47 @@ TN_WGRAD = os.environ.get("DLA_TN_WGRAD", "1") != "0"
 TN_WGRAD_MIN_ELEMS = int(os.environ.get("DLA_TN_WGRAD_MIN", "0"))
 
 
-def _wgrad_accumulate(mg: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor) -> None:
+def _tn_ok(mg: torch.Tensor, M: int) -> bool:
     N, K = mg.shape
-    if (TN_WGRAD and N * K >= TN_WGRAD_MIN_ELEMS and mg.dtype == torch.bfloat16 and _ext.use_native(mg)
-            and dy2.is_contiguous() and x2.is_contiguous() and dy2.shape[0] % 8 == 0
-            and N % 8 == 0 and K % 8 == 0):
-        M = dy2.shape[0]
+    return (TN_WGRAD and N * K >= TN_WGRAD_MIN_ELEMS and mg.dtype == torch.bfloat16 and _ext.use_native(mg)
+            and M % 8 == 0 and N % 8 == 0 and K % 8 == 0)
+
+
+def _wgrad_accumulate(mg: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor,
+                      dyt: torch.Tensor = None, xt: torch.Tensor = None) -> None:
+    """mg += dy2^T x2. `dyt` / `xt` are optional already-transposed operands ([N, M] / [K, M]),
+    e.g. written by a producer kernel as a second output (ops.activations.swiglu_mlp)."""
+    N, K = mg.shape
+    M = dy2.shape[0]
+    if _tn_ok(mg, M) and (dyt is not None or dy2.is_contiguous()) and (xt is not None or x2.is_contiguous()):
         tr = _ext.require().transpose_bf16
-        dyt = torch.empty((N, M), dtype=dy2.dtype, device=dy2.device)
-        xt = torch.empty((K, M), dtype=x2.dtype, device=x2.device)
-        tr(dy2, dyt)
-        tr(x2, xt)
+        if dyt is None:
+            dyt = torch.empty((N, M), dtype=dy2.dtype, device=dy2.device)
+            tr(dy2, dyt)
+        if xt is None:
+            xt = torch.empty((K, M), dtype=x2.dtype, device=x2.device)
+            tr(x2, xt)
         mg.addmm_(dyt, xt.t())
         return
     mg.addmm_(dy2.t(), x2)
 
 
-def accumulate_weight_grad(weight: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor) -> bool:
+def accumulate_weight_grad(weight: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor,
+                           dyt: torch.Tensor = None, xt: torch.Tensor = None) -> bool:
     """main_grad += dy2^T @ x2 if the engine attached a main_grad; returns True if handled."""
     mg = getattr(weight, "main_grad", None)
     if mg is None or getattr(weight, "_dla_shared", False):
         return False
-    _wgrad_accumulate(mg, dy2, x2)
+    _wgrad_accumulate(mg, dy2, x2, dyt, xt)
     hook = getattr(weight, "_dla_grad_hook", None)
     if hook is not None:
         hook(weight)
     return True
+
+
+def uses_main_grad(weight: torch.Tensor) -> bool:
+    return (weight.requires_grad and torch.is_grad_enabled() and getattr(weight, "main_grad", None) is not None
+            and not getattr(weight, "_dla_shared", False))
 
 
 class _LinearMainGradFn(torch.autograd.Function):
@@ -107,7 +122,6 @@ class _LinearMainGradFn(torch.autograd.Function):
 
 
 def linear(x: torch.Tensor, weight: torch.Tensor, bias=None) -> torch.Tensor:
-    if (weight.requires_grad and torch.is_grad_enabled() and getattr(weight, "main_grad", None) is not None
-            and not getattr(weight, "_dla_shared", False)):
+    if uses_main_grad(weight):
         return _LinearMainGradFn.apply(x, weight, bias)
     return F.linear(x, weight, bias)
