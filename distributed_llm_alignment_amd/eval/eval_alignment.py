@@ -106,7 +106,8 @@ def main(argv=None) -> int:
     seed = cfg.get("seed", 0)
     results: Dict[str, Dict[str, Dict[str, float]]] = {}
     for name, path in cfg["models"].items():
-        bundle = load_causal_lm(path, gradient_checkpointing=False, seed=seed)
+        bundle = load_causal_lm(path, gradient_checkpointing=False, seed=seed,
+                                device_map=(cfg.get("hardware", {}) or {}).get("device_map"))
         bundle.model.eval()
         metrics = {}
         for bench, bcfg in cfg["benchmarks"].items():

@@ -77,7 +77,8 @@ def main(argv=None) -> int:
     lat = cfg["latency"]
     results: Dict[str, List[Dict[str, float]]] = {}
     for name, path in cfg["models"].items():
-        bundle = load_causal_lm(path, gradient_checkpointing=False, seed=cfg.get("seed", 0))
+        bundle = load_causal_lm(path, gradient_checkpointing=False, seed=cfg.get("seed", 0),
+                                device_map=(cfg.get("hardware", {}) or {}).get("device_map"))
         bundle.model.eval()
         results[name] = measure_model(bundle.model, lat["batch_sizes"], lat["seq_lengths"],
                                       lat.get("warmup_steps", 3), lat.get("measure_steps", 10),

@@ -32,8 +32,13 @@ class KVCache:
         L, Hkv, D = cfg.num_layers, model.layers[0].attn.kv_local, cfg.head_dim
         self.h_local, self.kv_local = model.layers[0].attn.h_local, Hkv
         self.cfg = cfg
-        self.k = torch.empty((L, batch, max_len, Hkv, D), device=dev, dtype=dt)
-        self.v = torch.empty((L, batch, max_len, Hkv, D), device=dev, dtype=dt)
+        self.split = model.layer_devices is not None
+        if self.split:  # layer-split model: each layer's K/V on that layer's device
+            self.k = [torch.empty((batch, max_len, Hkv, D), device=d, dtype=dt) for d in model.layer_devices]
+            self.v = [torch.empty((batch, max_len, Hkv, D), device=d, dtype=dt) for d in model.layer_devices]
+        else:
+            self.k = torch.empty((L, batch, max_len, Hkv, D), device=dev, dtype=dt)
+            self.v = torch.empty((L, batch, max_len, Hkv, D), device=dev, dtype=dt)
         self.max_len = max_len
         self.len = 0
         self.batch = batch
@@ -42,14 +47,14 @@ class KVCache:
         self.slot = torch.zeros(1, dtype=torch.long, device=dev)
         self.kv_len = torch.ones(1, dtype=torch.int32, device=dev)
         self.pos = torch.zeros((batch, 1), dtype=torch.int32, device=dev)
-        self.fast_decode = (dev.type == "cuda" and dt == torch.bfloat16
+        self.fast_decode = (not self.split and dev.type == "cuda" and dt == torch.bfloat16
                             and ops.decode.decode_supported(self.h_local, Hkv, D))
 
     def positions_for(self, T: int) -> torch.Tensor:
         if T == 1 and self.len > 0:
             self._pos = self.pos
             return self.pos
-        dev = self.k.device
+        dev = self.slot.device
         t = torch.arange(self.len, self.len + T, device=dev, dtype=torch.int32).unsqueeze(0)
         start = self.kv_start.unsqueeze(1) if self.kv_start is not None else 0
         self._pos = (t - start).clamp(min=0).expand(self.batch, T).contiguous()
@@ -76,14 +81,18 @@ class KVCache:
             o = ops.decode.decode_attention(q.reshape(B, self.h_local, D), self.k[layer],
                                             self.v[layer], self.kv_len, self.kv_start, window)
             return o.reshape(B, 1, self.h_local * D)
+        pos, kv_start = self._pos, self.kv_start
+        if self.split:
+            pos = pos.to(qkv.device) if pos is not None else None
+            kv_start = kv_start.to(qkv.device) if kv_start is not None else None
         q, k, v = ops.attention.rope_qk(qkv, rope, self.h_local, self.kv_local, cfg.head_dim,
-                                        positions=self._pos)
-        self.k[layer, :, self.len:self.len + T] = k
-        self.v[layer, :, self.len:self.len + T] = v
+                                        positions=pos)
+        self.k[layer][:, self.len:self.len + T] = k
+        self.v[layer][:, self.len:self.len + T] = v
         end = self.len + T
-        o = ops.attention_core(q.contiguous(), self.k[layer, :, :end], self.v[layer, :, :end],
+        o = ops.attention_core(q.contiguous(), self.k[layer][:, :end], self.v[layer][:, :end],
                                causal=True, causal_off=self.len, window=window,
-                               kv_start=self.kv_start, kv_end=None)
+                               kv_start=kv_start, kv_end=None)
         return o.reshape(B, T, self.h_local * cfg.head_dim)
 
     def advance(self, T: int):
@@ -143,7 +152,7 @@ def sample_next(logits: torch.Tensor, do_sample: bool, temperature: float, top_p
 
 def _graph_ok(model: CausalLM, cache: KVCache) -> bool:
     return (cache.fast_decode and model.tp_size == 1 and getattr(model, "_dla_fsdp", None) is None
-            and ops._ext.use_native(cache.k))
+            and not cache.split and ops._ext.use_native(cache.k))
 
 
 class _DecodeGraph:

@@ -59,19 +59,34 @@ def read_state_dict(path: Path) -> Dict[str, torch.Tensor]:
 
 def load_causal_lm(model_name_or_path: str, gradient_checkpointing: bool = True,
                    use_flash_attention: bool = False, torch_dtype: Optional[torch.dtype] = None,
-                   device=None, seed: int = 0, headless: bool = False) -> ModelBundle:
+                   device=None, seed: int = 0, headless: bool = False,
+                   device_map=None) -> ModelBundle:
     """Preset name / HF hub alias -> random init (seeded, identical on all ranks);
     local dir (config.json + safetensors) -> loaded weights. `use_flash_attention` is accepted
-    for config compatibility: the native model always runs the HIP flash-attention kernel."""
-    device = torch.device(device) if device is not None else default_device()
+    for config compatibility: the native model always runs the HIP flash-attention kernel.
+
+    `device_map` ("auto" or a device list) splits the layers over several devices in ONE process
+    (parallel.layer_split; the reference's device_map="auto", base_model.py:33). "auto" with a
+    single visible GPU is the plain one-device placement."""
+    from ..parallel.layer_split import dispatch_layers, resolve_devices
+
+    split = resolve_devices(device_map)
+    split = split if split is not None and len(split) > 1 else None
+    if split is not None:
+        dtype = torch_dtype or default_dtype(split[0])
+        device = torch.device("cpu")  # materialise on the host, then place layer ranges
+    else:
+        device = torch.device(device) if device is not None else default_device()
+        dtype = torch_dtype or default_dtype(device)
     cfg = get_config(model_name_or_path)
-    dtype = torch_dtype or default_dtype(device)
     p = Path(str(model_name_or_path))
     has_weights = p.is_dir() and bool(_weight_files(p))
     model = build_model(cfg, device=device, dtype=dtype, seed=seed, init=not has_weights, headless=headless)
     if has_weights:
         sd = read_state_dict(p)
         model.load_hf_state_dict(sd, strict=False)
+    if split is not None:
+        dispatch_layers(model, split)
     if gradient_checkpointing:
         model.gradient_checkpointing_enable()
     tok = load_tokenizer(model_name_or_path, cfg)

@@ -207,6 +207,7 @@ class CausalLM(nn.Module):
         self.tp_size = 1
         self.tp_rank = 0
         self.vocab_parallel = None  # (vocab offset, local vocab) when embed/head are vocab-sharded
+        self.layer_devices = None   # per-layer devices under parallel.layer_split (device_map)
         if self.lm_head is None and not headless:
             # tied input/output embedding: its gradient arrives from two ops, so it must go through
             # autograd's AccumulateGrad (one hook call) rather than the GEMM main-grad path
@@ -264,12 +265,17 @@ class CausalLM(nn.Module):
         kv_start, kv_end, positions = attention_layout(attention_mask)
         x = self.embed_tokens(input_ids, positions)
         resid = None
-        for layer in self.layers:
+        for i, layer in enumerate(self.layers):
+            if self.layer_devices is not None:
+                x, resid, kv_start, kv_end, positions = _hop(self.layer_devices[i], x, resid, kv_start,
+                                                             kv_end, positions)
             if self.gradient_checkpointing and self.training and torch.is_grad_enabled():
                 x, resid = checkpoint(layer, x, resid, self.rope, kv_start, kv_end, positions,
                                       use_reentrant=False)
             else:
                 x, resid = layer(x, resid, self.rope, kv_start, kv_end, positions)
+        if self.layer_devices is not None:
+            x, resid = _hop(self.norm_w.device, x, resid)
         h, _ = ops.add_norm(x, resid, self.norm_w, self.norm_b, self.cfg.norm_eps,
                             self.cfg.norm_type == "rms")
         return h
@@ -279,7 +285,11 @@ class CausalLM(nn.Module):
         x = self.embed_tokens(input_ids, positions)
         resid = None
         for i, layer in enumerate(self.layers):
+            if self.layer_devices is not None:
+                x, resid = _hop(self.layer_devices[i], x, resid)
             x, resid = layer(x, resid, self.rope, None, None, None, cache, i)
+        if self.layer_devices is not None:
+            x, resid = _hop(self.norm_w.device, x, resid)
         h, _ = ops.add_norm(x, resid, self.norm_w, self.norm_b, self.cfg.norm_eps,
                             self.cfg.norm_type == "rms")
         cache.step_done(input_ids.shape[1])
@@ -354,6 +364,11 @@ class CausalLM(nn.Module):
         from .hf_io import load_hf_state_dict
 
         return load_hf_state_dict(self, sd, strict=strict)
+
+
+def _hop(dev, *ts):
+    """Move activations to the next layer range's device (layer-split model parallel)."""
+    return tuple(t if (t is None or t.device == dev) else t.to(dev, non_blocking=True) for t in ts)
 
 
 def _chunked_randn(p: torch.Tensor, gen: torch.Generator, std: float) -> torch.Tensor:

@@ -35,6 +35,9 @@ def parse_args(argv=None) -> argparse.Namespace:
     p.add_argument("--temperature", type=float, default=0.7)
     p.add_argument("--top_p", type=float, default=0.9)
     p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--device_map", default=None,
+                   help="'auto': split the teacher's layers over all visible GPUs in this one process "
+                        "(reference behavior; only for models larger than one GPU's HBM)")
     return p.parse_args(argv)
 
 
@@ -46,7 +49,10 @@ def main(argv=None) -> int:
     args = parse_args(argv)
     st = init_distributed()
     torch.manual_seed(args.seed)
-    bundle = load_causal_lm(args.teacher, gradient_checkpointing=False, device=st.device, seed=args.seed)
+    if args.device_map and st.world_size > 1:
+        raise SystemExit("--device_map is a single-process mode; launch one process (or drop it)")
+    bundle = load_causal_lm(args.teacher, gradient_checkpointing=False, device=st.device, seed=args.seed,
+                            device_map=args.device_map)
     model, tok = bundle.model, bundle.tokenizer
     model.eval()
     rm = rtok = None

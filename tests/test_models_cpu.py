@@ -137,3 +137,42 @@ def test_byte_tokenizer_roundtrip_and_padding():
     t.padding_side = "left"
     enc = t(["a", "abc"], padding=True)
     assert enc["attention_mask"][0] == [0, 0, 1, 1]
+
+
+def test_layer_split_plan_balanced_and_contiguous():
+    from distributed_llm_alignment_amd.parallel.layer_split import plan_layer_split
+
+    assert plan_layer_split([1] * 32, 4) == [0] * 8 + [1] * 8 + [2] * 8 + [3] * 8
+    p = plan_layer_split([1] * 8, 3, first_extra=2)  # device 0 also holds embed/head
+    assert p == sorted(p) and set(p) == {0, 1, 2} and p.count(0) < p.count(2)
+    assert plan_layer_split([5, 5], 4) == [0, 1]  # never more devices than layers
+
+
+@pytest.mark.parametrize("name", ["tiny-llama", "tiny-gpt2"])
+def test_layer_split_model_matches_single_device(name):
+    """device_map-style layer split (reference base_model.py:33) is numerically the same model:
+    forward, backward and cached greedy generation match the one-device model."""
+    from distributed_llm_alignment_amd.parallel.layer_split import dispatch_layers
+
+    cfg = get_config(name)
+    a = build_model(cfg, device="cpu", seed=0)
+    b = build_model(cfg, device="cpu", seed=0)
+    devs = dispatch_layers(b, ["cpu", "cpu", "cpu"])
+    assert len(devs) == cfg.num_layers and b.layer_devices is devs
+    ids = torch.randint(3, cfg.vocab_size, (2, 10))
+    mask = torch.ones_like(ids)
+    mask[0, :3] = 0
+    la, lb = a.sequence_logprob(ids, mask), b.sequence_logprob(ids, mask)
+    assert torch.allclose(la, lb)
+    la.sum().backward()
+    lb.sum().backward()
+    for pa, pb in zip(a.parameters(), b.parameters()):
+        assert torch.allclose(pa.grad, pb.grad)
+    ga = generate(a, ids, mask, max_new_tokens=4, do_sample=False, eos_token_id=-1)
+    gb = generate(b, ids, mask, max_new_tokens=4, do_sample=False, eos_token_id=-1)
+    assert torch.equal(ga, gb)
+
+
+def test_load_causal_lm_device_map_single_device_is_plain():
+    b = load_causal_lm("tiny-llama", gradient_checkpointing=False, device="cpu", device_map="auto")
+    assert b.model.layer_devices is None
