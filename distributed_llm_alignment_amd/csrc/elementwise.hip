@@ -11,6 +11,18 @@ namespace dla {
 
 __device__ __forceinline__ float silu_f(float g) { return g * sigmoidf_(g); }
 
+// d/dg and d/du of silu(g) * u for 8 lanes; shared by both backward kernels so they agree bitwise
+__device__ __forceinline__ void swiglu_grad8(const bf16x8& g, const bf16x8& u, const bf16x8& d,
+                                             bf16x8& dg, bf16x8& du) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float gf = bf2f(g[j]), uf = bf2f(u[j]), df = bf2f(d[j]);
+    const float sg = sigmoidf_(gf);
+    du[j] = f2bf(df * (gf * sg));
+    dg[j] = f2bf(df * uf * sg * (1.f + gf * (1.f - sg)));
+  }
+}
+
 __global__ __launch_bounds__(256) void swiglu_fwd_kernel(const bf16_t* __restrict__ gu,
                                                           bf16_t* __restrict__ out, int64_t rows,
                                                           int F) {
@@ -39,14 +51,7 @@ __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const bf16_t* __restric
     const bf16_t* row = gu + r * 2 * F;
     bf16x8 g = load_bf16x8(row + c), u = load_bf16x8(row + F + c);
     bf16x8 d = load_bf16x8(dout + r * F + c), dg, du;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float gf = bf2f(g[j]), uf = bf2f(u[j]), df = bf2f(d[j]);
-      const float sg = sigmoidf_(gf);
-      const float sl = gf * sg;
-      du[j] = f2bf(df * sl);
-      dg[j] = f2bf(df * uf * sg * (1.f + gf * (1.f - sg)));
-    }
+    swiglu_grad8(g, u, d, dg, du);
     store_bf16x8(dgu + r * 2 * F + c, dg);
     store_bf16x8(dgu + r * 2 * F + F + c, du);
   }
@@ -124,13 +129,7 @@ __global__ __launch_bounds__(256) void swiglu_bwd_t_kernel(const bf16_t* __restr
       const bf16_t* row = gu + r * 2 * F;
       const bf16x8 g = load_bf16x8(row + c0 + cv), u = load_bf16x8(row + F + c0 + cv);
       const bf16x8 d = load_bf16x8(dout + r * F + c0 + cv);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float gf = bf2f(g[j]), uf = bf2f(u[j]), df = bf2f(d[j]);
-        const float sg = sigmoidf_(gf);
-        du[j] = f2bf(df * gf * sg);
-        dg[j] = f2bf(df * uf * sg * (1.f + gf * (1.f - sg)));
-      }
+      swiglu_grad8(g, u, d, dg, du);
       store_bf16x8(dgu + r * 2 * F + c0 + cv, dg);
       store_bf16x8(dgu + r * 2 * F + F + c0 + cv, du);
     }

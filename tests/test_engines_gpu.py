@@ -48,7 +48,7 @@ def test_fsdp_engine_matches_flat_engine_gpu(ckpt):
     assert a == pytest.approx(b, rel=2e-2, abs=1e-3), (a, b)
 
 
-@pytest.mark.parametrize("R,C", [(4096, 6144), (1000, 136), (64, 8)])
+@pytest.mark.parametrize("R,C", [(4096, 6144), (1000, 136), (64, 8), (8192, 14336), (72, 328)])
 def test_transpose_kernel(R, C):
     from distributed_llm_alignment_amd.ops import _ext
 
