@@ -61,6 +61,46 @@ def dpo_step_loss(policy, ref, batch, beta: float = 0.1, label_smoothing: float 
     return loss, metrics
 
 
+def ref_sequence_logps(ref, batch, reduction: str = "mean", pad_id: int = 0):
+    """The frozen reference's per-sequence log-probs for a preference batch ([2B]: chosen, rejected)."""
+    ids, mask, lm = concat_pair(batch, pad_id)
+    with torch.no_grad():
+        return sequence_logps(ref, ids, mask, reduction, lm)
+
+
+class RefLogpsStream:
+    """Runs the frozen reference forward on a second HIP stream so it overlaps the policy's
+    forward/backward on the main stream (the two are independent until the DPO loss). The ref
+    pass is GEMM-light relative to its memory-bound phases (attention, norms, SwiGLU) and the
+    policy's are the same: interleaving the two streams fills the gaps each leaves on the CUs.
+    `submit(batch)` returns a handle; `result(handle)` makes the main stream wait for it.
+    On CPU (or with enabled=False) it simply computes inline."""
+
+    def __init__(self, ref, reduction: str = "mean", pad_id: int = 0, enabled: bool = True):
+        self.ref, self.reduction, self.pad_id = ref, reduction, pad_id
+        dev = next(ref.parameters()).device
+        self.stream = torch.cuda.Stream(device=dev) if (enabled and dev.type == "cuda") else None
+
+    def submit(self, batch):
+        if self.stream is None:
+            return ref_sequence_logps(self.ref, batch, self.reduction, self.pad_id), None
+        main = torch.cuda.current_stream(self.stream.device)
+        self.stream.wait_stream(main)  # batch tensors were produced on the main stream
+        with torch.cuda.stream(self.stream):
+            lp = ref_sequence_logps(self.ref, batch, self.reduction, self.pad_id)
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+        return lp, ev
+
+    def result(self, handle):
+        lp, ev = handle
+        if ev is not None:
+            main = torch.cuda.current_stream(lp.device)
+            main.wait_event(ev)
+            lp.record_stream(main)
+        return lp
+
+
 def sft_loss(model, batch) -> torch.Tensor:
     return model.causal_lm_loss(batch["input_ids"], batch["labels"], batch.get("attention_mask"))
 
