@@ -156,6 +156,17 @@ __global__ __launch_bounds__(kFwdThreads) void attn_fwd_kernel(AttnParams p) {
   if (CAUSAL) kmax = min(kmax, blk_qmax + p.causal_off + 1);
   int kmin = kbeg;
   if (CAUSAL && p.window > 0) kmin = max(kmin, qb * BQ + p.causal_off - p.window + 1);
+  // packed sequences: query i sees keys >= seg_start[i]; seg_start is non-decreasing in i, so
+  // the block's first query bounds the key range from below and each wave's first / last query
+  // bound its activity / masking (wseg_* are 0 without segments: no effect)
+  const int* ss = p.seg_start ? p.seg_start + static_cast<int64_t>(b) * p.Tq : nullptr;
+  int wseg_lo = 0, wseg_hi = 0, qseg = 0;
+  if (ss) {
+    kmin = max(kmin, ss[qb * BQ]);
+    wseg_lo = __builtin_amdgcn_readfirstlane(ss[min(q0, p.Tq - 1)]);
+    wseg_hi = __builtin_amdgcn_readfirstlane(ss[min(q0 + 31, p.Tq - 1)]);
+    qseg = ss[min(qi, p.Tq - 1)];
+  }
   const int tile0 = (max(kmin, 0) / BK) * BK;
   const int ntiles = kmax > tile0 ? (kmax - tile0 + BK - 1) / BK : 0;
 
@@ -195,7 +206,7 @@ __global__ __launch_bounds__(kFwdThreads) void attn_fwd_kernel(AttnParams p) {
     const int kt = tile0 + t * BK;
     const bf16_t* Ks = Kb[t & 1];
     const bf16_t* Vs = Vb[t & 1];
-    bool active = q0 < p.Tq;
+    bool active = q0 < p.Tq && kt + BK > wseg_lo;
     if (CAUSAL) {
       active = active && (kt <= q0 + 31 + p.causal_off);
       if (p.window > 0) active = active && (kt + BK - 1 > q0 + p.causal_off - p.window);
@@ -212,7 +223,7 @@ __global__ __launch_bounds__(kFwdThreads) void attn_fwd_kernel(AttnParams p) {
         }
       }
       // mask only tiles that touch a boundary (kv range, causal diagonal, window edge)
-      bool need_mask = kt < kbeg || kt + BK > kend;
+      bool need_mask = kt < kbeg || kt + BK > kend || kt < wseg_hi;
       if (CAUSAL) {
         need_mask = need_mask || (kt + BK - 1 > q0 + p.causal_off);
         if (p.window > 0) need_mask = need_mask || (kt <= q0 + 31 + p.causal_off - p.window);
@@ -222,7 +233,7 @@ __global__ __launch_bounds__(kFwdThreads) void attn_fwd_kernel(AttnParams p) {
         // the visible keys of this lane's query are r in [lo, hi), tested as one unsigned
         // compare per score
         const int base = kt + 4 * h;
-        int lo = kbeg - base, hi = kend - base;
+        int lo = max(kbeg, qseg) - base, hi = kend - base;
         if (CAUSAL) {
           hi = min(hi, qi + p.causal_off + 1 - base);
           if (p.window > 0) lo = max(lo, qi + p.causal_off - p.window + 1 - base);
@@ -499,6 +510,21 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnBwdParams p) {
 #pragma unroll
   for (int g = 0; g < 4; ++g) woff[g] = ds_off(l32, 2 * g + h);
 
+  // packed sequences: key kj is seen only by queries < seg_end[kj] (non-decreasing in kj); per
+  // sub-tile j: this lane's bound and the wave-uniform bounds of its first / last key
+  const int* se = p.seg_end ? p.seg_end + static_cast<int64_t>(b) * p.Tk : nullptr;
+  int kse[2], kse_lo[2], kse_hi[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    kse[j] = kse_lo[j] = kse_hi[j] = 0x7fffffff;
+    if (se) {
+      const int kj0 = kw + 32 * j;
+      kse[j] = se[min(kj0 + l32, p.Tk - 1)];
+      kse_lo[j] = __builtin_amdgcn_readfirstlane(se[min(kj0, p.Tk - 1)]);
+      kse_hi[j] = __builtin_amdgcn_readfirstlane(se[min(kj0 + 31, p.Tk - 1)]);
+    }
+  }
+
   f32x16 dk[2][DT], dv[2][DT];
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
@@ -552,8 +578,8 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnBwdParams p) {
     for (int j = 0; j < 2; ++j) {
       const int kj0 = kw + 32 * j;
       // does this sub-tile see any query of the tile? which masks apply? (wave-uniform)
-      bool act = kj0 < kend && kj0 + 32 > kbeg;
-      bool need_mask = kj0 < kbeg || kj0 + 32 > kend || qt + BQ > p.Tq;
+      bool act = kj0 < kend && kj0 + 32 > kbeg && qt < kse_hi[j];
+      bool need_mask = kj0 < kbeg || kj0 + 32 > kend || qt + BQ > p.Tq || qt + BQ > kse_lo[j];
       if (CAUSAL) {
         act = act && kj0 <= qt + BQ - 1 + p.causal_off;
         need_mask = need_mask || (kj0 + 31 > qt + p.causal_off);
@@ -590,7 +616,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnBwdParams p) {
         // visible queries of this lane's key kj: accumulator rows rr = (i&3) + 8(i>>2) (query
         // qt + rr + 4h) in [lo, hi), one unsigned compare per element
         const int kj = kj0 + l32;
-        int lo = 0, hi = p.Tq - qt - 4 * h;
+        int lo = 0, hi = min(p.Tq, kse[j]) - qt - 4 * h;
         if (kj < kbeg || kj >= kend) hi = 0;
         if (CAUSAL) {
           const int dlt = kj - qt - p.causal_off - 4 * h;  // visible iff rr >= dlt

@@ -22,6 +22,7 @@ struct AttnParams {
   int window;       // >0: also require j > i + causal_off - window
   const int* kv_start;  // [B] or null
   const int* kv_end;    // [B] or null
+  const int* seg_start;  // [B, Tq] or null: packed sequences, query i sees keys >= seg_start[i]
 };
 
 // Backward geometry: one workgroup per (256-key block, GQA head subset, kv head, batch);
@@ -57,6 +58,7 @@ struct AttnBwdParams {
   int window;
   const int* kv_start;
   const int* kv_end;
+  const int* seg_end;  // [B, Tk] or null: packed sequences, key j is seen by queries < seg_end[j]
 };
 
 }  // namespace dla

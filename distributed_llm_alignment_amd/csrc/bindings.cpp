@@ -316,11 +316,24 @@ static void check_kv_range(const c10::optional<at::Tensor>& r, int64_t B, const 
   }
 }
 
+// packed-sequence bounds [2, B, T] int32 (seg_start; seg_end), causal self-attention only
+static const int* seg_ptr(const c10::optional<at::Tensor>& segs, int64_t B, int64_t Tq, int64_t Tk,
+                          bool causal, int64_t causal_off, const at::Tensor& q, int row) {
+  if (!segs || !segs->defined()) return nullptr;
+  TORCH_CHECK(segs->scalar_type() == at::kInt && segs->is_contiguous() && segs->dim() == 3 &&
+                  segs->size(0) == 2 && segs->size(1) == B && segs->size(2) == Tq,
+              "segs must be contiguous int32 [2, B, T]");
+  TORCH_CHECK(causal && causal_off == 0 && Tq == Tk, "packed sequences need causal self-attention");
+  same_device(q, *segs);
+  return segs->data_ptr<int>() + row * B * Tq;
+}
+
 std::tuple<at::Tensor, at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k,
                                             const at::Tensor& v, double scale, bool causal,
                                             int64_t causal_off, int64_t window,
                                             const c10::optional<at::Tensor>& kv_start,
-                                            const c10::optional<at::Tensor>& kv_end) {
+                                            const c10::optional<at::Tensor>& kv_end,
+                                            const c10::optional<at::Tensor>& segs) {
   check_bthd(q, "q");
   check_bthd(k, "k");
   check_bthd(v, "v");
@@ -354,6 +367,7 @@ std::tuple<at::Tensor, at::Tensor> attn_fwd(const at::Tensor& q, const at::Tenso
   p.window = static_cast<int>(window);
   p.kv_start = (kv_start && kv_start->defined()) ? kv_start->data_ptr<int>() : nullptr;
   p.kv_end = (kv_end && kv_end->defined()) ? kv_end->data_ptr<int>() : nullptr;
+  p.seg_start = seg_ptr(segs, B, Tq, Tk, causal, causal_off, q, 0);
   launch_attn_fwd(p, static_cast<int>(D), causal, cur_stream(q));
   return {o, lse2};
 }
@@ -391,7 +405,7 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k,
               const at::Tensor& v, const at::Tensor& o, const at::Tensor& lse2, at::Tensor& dq,
               at::Tensor& dk, at::Tensor& dv, double scale, bool causal, int64_t causal_off,
               int64_t window, const c10::optional<at::Tensor>& kv_start,
-              const c10::optional<at::Tensor>& kv_end) {
+              const c10::optional<at::Tensor>& kv_end, const c10::optional<at::Tensor>& segs) {
   check_bthd(dout, "dout");
   check_bthd(q, "q");
   check_bthd(k, "k");
@@ -451,6 +465,7 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k,
   p.window = static_cast<int>(window);
   p.kv_start = (kv_start && kv_start->defined()) ? kv_start->data_ptr<int>() : nullptr;
   p.kv_end = (kv_end && kv_end->defined()) ? kv_end->data_ptr<int>() : nullptr;
+  p.seg_end = seg_ptr(segs, B, Tq, Tk, causal, causal_off, q, 1);
   launch_attn_bwd(p, static_cast<int>(D), causal, st);
   launch_attn_dq_reduce(p.dq_slab, static_cast<int>(nkb), static_cast<int>(B), static_cast<int>(Tq),
                         p.slab_rows, static_cast<int>(Hq), static_cast<int>(D), causal, p.causal_off, p.window,
@@ -786,8 +801,8 @@ TORCH_LIBRARY(dla, m) {
   m.def("gelu_bwd(Tensor x, Tensor dy) -> Tensor");
   m.def("rope_fwd(Tensor qkv, Tensor cos, Tensor sin, Tensor? pos, int Hq, int Hkv, int D, int rot, int T, int pos_offset) -> (Tensor, Tensor)");
   m.def("rope_bwd(Tensor dq, Tensor dk, Tensor(a!) dqkv, Tensor cos, Tensor sin, Tensor? pos, int Hq, int Hkv, int D, int rot, int T, int pos_offset) -> ()");
-  m.def("attn_fwd(Tensor q, Tensor k, Tensor v, float scale, bool causal, int causal_off, int window, Tensor? kv_start, Tensor? kv_end) -> (Tensor, Tensor)");
-  m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse2, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, float scale, bool causal, int causal_off, int window, Tensor? kv_start, Tensor? kv_end) -> ()");
+  m.def("attn_fwd(Tensor q, Tensor k, Tensor v, float scale, bool causal, int causal_off, int window, Tensor? kv_start, Tensor? kv_end, Tensor? segs=None) -> (Tensor, Tensor)");
+  m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse2, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, float scale, bool causal, int causal_off, int window, Tensor? kv_start, Tensor? kv_end, Tensor? segs=None) -> ()");
   m.def("transpose_bf16(Tensor input, Tensor(a!) out) -> ()");
   m.def("logprob_fwd(Tensor logits, Tensor targets, int vocab_offset=0) -> (Tensor, Tensor)");
   m.def("logprob_bwd(Tensor(a!) logits, Tensor targets, Tensor lse, Tensor grad, int vocab_offset=0) -> ()");

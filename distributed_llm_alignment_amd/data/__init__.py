@@ -1,5 +1,5 @@
 """Data pipeline: reference-schema JSONL datasets, collation, HF/local/synthetic loaders."""
-from .datasets import (EvalPromptDataset, InstructionDataset, PreferenceDataset, Sample,
+from .datasets import (EvalPromptDataset, InstructionDataset, PackedDataset, PreferenceDataset, Sample,
                        TeacherRolloutDataset, build_instruction_dataset, build_preference_dataset,
                        load_instruction_records, load_preference_records, pad_batch, read_jsonl,
                        write_jsonl)
@@ -8,7 +8,7 @@ from .synthetic import (synthetic_instruction_records, synthetic_lm_batch, synth
                         synthetic_preference_records, synthetic_prompt_records)
 
 __all__ = [
-    "EvalPromptDataset", "InstructionDataset", "PreferenceDataset", "Sample", "TeacherRolloutDataset",
+    "EvalPromptDataset", "InstructionDataset", "PackedDataset", "PreferenceDataset", "Sample", "TeacherRolloutDataset",
     "build_instruction_dataset", "build_preference_dataset", "load_instruction_records",
     "load_preference_records", "pad_batch", "read_jsonl", "write_jsonl", "build_dataloader",
     "get_distributed_sampler", "synthetic_instruction_records", "synthetic_lm_batch",

@@ -97,6 +97,53 @@ class InstructionDataset(Dataset):
         return pad_batch(batch, _pad_id(self.tokenizer))
 
 
+class PackedDataset(Dataset):
+    """`data.packing: true` (a dead key in the reference, sft_config.yaml:16): SFT
+    examples concatenated into rows of at most `max_length` tokens, in order (greedy, a new row
+    when the next example does not fit). Each row carries `segment_ids` (1, 2, ... per example),
+    so the model runs block-diagonal causal attention with per-example positions
+    (models.transformer.packed_layout) — numerically the same as the examples run one by one,
+    without the padding FLOPs. Labels are -100 at each example's first token, so no example is
+    trained to predict the next one's start."""
+
+    def __init__(self, base: Dataset, max_length: int):
+        self.base = base
+        self.max_length = max_length
+        self.tokenizer = getattr(base, "tokenizer", None)
+        self.rows: List[List[int]] = []
+        cur: List[int] = []
+        used = 0
+        for i in range(len(base)):
+            n = min(int(base[i]["input_ids"].numel()), max_length)
+            if cur and used + n > max_length:
+                self.rows.append(cur)
+                cur, used = [], 0
+            cur.append(i)
+            used += n
+        if cur:
+            self.rows.append(cur)
+
+    def __len__(self) -> int:
+        return len(self.rows)
+
+    def __getitem__(self, idx: int) -> Dict[str, torch.Tensor]:
+        ids, labels, segs = [], [], []
+        for j, i in enumerate(self.rows[idx]):
+            ex = self.base[i]
+            x = ex["input_ids"][: self.max_length]
+            lab = ex["labels"][: self.max_length].clone()
+            lab[0] = -100
+            ids.append(x)
+            labels.append(lab)
+            segs.append(torch.full_like(x, j + 1))
+        input_ids = torch.cat(ids)
+        return {"input_ids": input_ids, "attention_mask": torch.ones_like(input_ids),
+                "labels": torch.cat(labels), "segment_ids": torch.cat(segs)}
+
+    def collate(self, batch):
+        return pad_batch(batch, _pad_id(self.tokenizer) if self.tokenizer is not None else 0)
+
+
 class PreferenceDataset(Dataset):
     """(prompt, chosen, rejected) triples for RM / DPO (reference datasets.py:86-152)."""
 
@@ -283,11 +330,12 @@ def load_preference_records(cfg: Dict[str, Any], split: str = "train") -> List[D
     return records
 
 
-def build_instruction_dataset(cfg: Dict[str, Any], tokenizer, split: str = "train") -> InstructionDataset:
-    return InstructionDataset(tokenizer=tokenizer,
-                              max_length=cfg.get("max_length", cfg.get("max_seq_length", 2048)),
-                              mask_prompt=cfg.get("mask_prompt", True),
-                              records=load_instruction_records(cfg, split=split))
+def build_instruction_dataset(cfg: Dict[str, Any], tokenizer, split: str = "train"):
+    max_length = cfg.get("max_length", cfg.get("max_seq_length", 2048))
+    ds = InstructionDataset(tokenizer=tokenizer, max_length=max_length,
+                            mask_prompt=cfg.get("mask_prompt", True),
+                            records=load_instruction_records(cfg, split=split))
+    return PackedDataset(ds, max_length) if cfg.get("packing", False) else ds
 
 
 def build_preference_dataset(cfg: Dict[str, Any], tokenizer, split: str = "train") -> PreferenceDataset:

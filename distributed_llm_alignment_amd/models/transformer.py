@@ -46,6 +46,26 @@ def attention_layout(attention_mask: Optional[torch.Tensor]):
     return first, end, pos
 
 
+def packed_layout(segment_ids: torch.Tensor):
+    """Packed rows: `segment_ids` [B, T] labels each token with its sequence (runs of equal ids,
+    e.g. 1, 1, 1, 2, 2, 0, 0 with 0 = trailing padding). Returns (positions [B, T] restarting at
+    0 in every run, segs [2, B, T] int32 = (first index of the token's run, one past its last)),
+    on device, no host sync. Attention is then block-diagonal causal: the packed sequences do
+    not see each other (makes `data.packing` real)."""
+    B, T = segment_ids.shape
+    dev = segment_ids.device
+    t = torch.arange(T, device=dev, dtype=torch.int64).expand(B, T)
+    new = torch.ones_like(segment_ids, dtype=torch.bool)
+    new[:, 1:] = segment_ids[:, 1:] != segment_ids[:, :-1]
+    start = torch.where(new, t, torch.zeros_like(t)).cummax(1).values
+    last = torch.ones_like(new)
+    last[:, :-1] = new[:, 1:]
+    end_at = torch.where(last, t + 1, torch.full_like(t, T))
+    end = end_at.flip(1).cummin(1).values.flip(1)
+    pos = (t - start).to(torch.int32)
+    return pos, torch.stack([start, end]).to(torch.int32).contiguous()
+
+
 class Attention(nn.Module):
     def __init__(self, cfg: ModelConfig, device=None, dtype=None):
         super().__init__()
@@ -59,7 +79,7 @@ class Attention(nn.Module):
         self.tp = None  # tensor-parallel group (parallel.tensor_parallel.apply_tensor_parallel)
         self.h_local, self.kv_local = cfg.num_heads, cfg.num_kv_heads
 
-    def forward(self, h, rope, kv_start, kv_end, positions, cache=None, layer_idx=0):
+    def forward(self, h, rope, kv_start, kv_end, positions, cache=None, layer_idx=0, segs=None):
         cfg = self.cfg
         if self.tp is not None:
             from ..parallel.tensor_parallel import tp_copy
@@ -70,7 +90,7 @@ class Attention(nn.Module):
         if cache is None:
             a = ops.qkv_attention(qkv, self.h_local, self.kv_local, cfg.head_dim, rope,
                                   causal=True, window=window, kv_start=kv_start, kv_end=kv_end,
-                                  positions=positions)
+                                  positions=positions, segs=segs)
         else:
             a = cache.attend(layer_idx, qkv, rope, window)
         if self.tp is None:
@@ -173,11 +193,11 @@ class DecoderLayer(nn.Module):
         self.attn = Attention(cfg, device, dtype)
         self.mlp = MoE(cfg, device, dtype) if cfg.is_moe else MLP(cfg, device, dtype)
 
-    def forward(self, x, resid, rope, kv_start, kv_end, positions, cache=None, layer_idx=0):
+    def forward(self, x, resid, rope, kv_start, kv_end, positions, cache=None, layer_idx=0, segs=None):
         cfg = self.cfg
         rms = cfg.norm_type == "rms"
         h, resid = ops.add_norm(x, resid, self.ln1_w, self.ln1_b, cfg.norm_eps, rms)
-        a = self.attn(h, rope, kv_start, kv_end, positions, cache, layer_idx)
+        a = self.attn(h, rope, kv_start, kv_end, positions, cache, layer_idx, segs)
         if cfg.parallel_block:
             return a + self.mlp(h), resid
         h, resid = ops.add_norm(a, resid, self.ln2_w, self.ln2_b, cfg.norm_eps, rms)
@@ -259,21 +279,25 @@ class CausalLM(nn.Module):
         return x
 
     def forward(self, input_ids: torch.Tensor, attention_mask: Optional[torch.Tensor] = None,
-                cache=None) -> torch.Tensor:
+                cache=None, segment_ids: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """`segment_ids` (optional, [B, T]): several sequences packed per row (see packed_layout)."""
         if cache is not None:
             return self._forward_cached(input_ids, attention_mask, cache)
         kv_start, kv_end, positions = attention_layout(attention_mask)
+        segs = None
+        if segment_ids is not None:
+            positions, segs = packed_layout(segment_ids)
         x = self.embed_tokens(input_ids, positions)
         resid = None
         for i, layer in enumerate(self.layers):
             if self.layer_devices is not None:
-                x, resid, kv_start, kv_end, positions = _hop(self.layer_devices[i], x, resid, kv_start,
-                                                             kv_end, positions)
+                x, resid, kv_start, kv_end, positions, segs = _hop(self.layer_devices[i], x, resid,
+                                                                   kv_start, kv_end, positions, segs)
             if self.gradient_checkpointing and self.training and torch.is_grad_enabled():
-                x, resid = checkpoint(layer, x, resid, self.rope, kv_start, kv_end, positions,
-                                      use_reentrant=False)
+                x, resid = checkpoint(layer, x, resid, self.rope, kv_start, kv_end, positions, None, 0,
+                                      segs, use_reentrant=False)
             else:
-                x, resid = layer(x, resid, self.rope, kv_start, kv_end, positions)
+                x, resid = layer(x, resid, self.rope, kv_start, kv_end, positions, segs=segs)
         if self.layer_devices is not None:
             x, resid = _hop(self.norm_w.device, x, resid)
         h, _ = ops.add_norm(x, resid, self.norm_w, self.norm_b, self.cfg.norm_eps,
@@ -340,9 +364,10 @@ class CausalLM(nn.Module):
             return torch.where(tgt >= 0, lp, torch.zeros_like(lp))
         return self._token_logprob(h.reshape(S * T, H), tgt.reshape(-1)).view(S, T)
 
-    def causal_lm_loss(self, input_ids, labels, attention_mask=None):
-        """HF ForCausalLMLoss (train_sft.py:145-146): mean token NLL over labels != -100."""
-        h = self(input_ids, attention_mask)  # __call__: module hooks (param all-gather waits) run
+    def causal_lm_loss(self, input_ids, labels, attention_mask=None, segment_ids=None):
+        """HF ForCausalLMLoss (train_sft.py:145-146): mean token NLL over labels != -100.
+        With `segment_ids` the rows hold packed sequences (labels -100 at each sequence start)."""
+        h = self(input_ids, attention_mask, segment_ids=segment_ids)  # __call__: module hooks run
         if self.lm_head_bias is not None:
             lg = self.logits(h).float()
             return F.cross_entropy(lg[:, :-1].reshape(-1, lg.shape[-1]), labels[:, 1:].reshape(-1),

@@ -102,7 +102,8 @@ class RefLogpsStream:
 
 
 def sft_loss(model, batch) -> torch.Tensor:
-    return model.causal_lm_loss(batch["input_ids"], batch["labels"], batch.get("attention_mask"))
+    return model.causal_lm_loss(batch["input_ids"], batch["labels"], batch.get("attention_mask"),
+                                batch.get("segment_ids"))
 
 
 def reward_loss(rm, batch, pad_id: int = 0):

@@ -80,10 +80,12 @@ def _ref_rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, pos: torch.
     return torch.cat([o1, o2, rest], dim=-1).to(x.dtype)
 
 
-def _visibility(B, Tq, Tk, causal, causal_off, window, kv_start, kv_end, device):
+def _visibility(B, Tq, Tk, causal, causal_off, window, kv_start, kv_end, device, segs=None):
     qi = torch.arange(Tq, device=device).view(1, Tq, 1)
     kj = torch.arange(Tk, device=device).view(1, 1, Tk)
     ok = torch.ones(B, Tq, Tk, dtype=torch.bool, device=device)
+    if segs is not None:  # packed sequences: query i sees keys >= seg_start[i] (block diagonal)
+        ok = ok & (kj >= segs[0].view(B, Tq, 1).to(device))
     if kv_start is not None:
         ok = ok & (kj >= kv_start.view(B, 1, 1).to(device))
     if kv_end is not None:
@@ -96,7 +98,7 @@ def _visibility(B, Tq, Tk, causal, causal_off, window, kv_start, kv_end, device)
 
 
 def ref_attention(q, k, v, scale, causal=True, causal_off=0, window=0, kv_start=None,
-                  kv_end=None) -> torch.Tensor:
+                  kv_end=None, segs=None) -> torch.Tensor:
     """q [B, Tq, Hq, D], k/v [B, Tk, Hkv, D] -> [B, Tq, Hq, D] (fp32 math)."""
     B, Tq, Hq, D = q.shape
     Tk, Hkv = k.shape[1], k.shape[2]
@@ -105,7 +107,7 @@ def ref_attention(q, k, v, scale, causal=True, causal_off=0, window=0, kv_start=
     kf = k.float().transpose(1, 2).repeat_interleave(rep, dim=1)
     vf = v.float().transpose(1, 2).repeat_interleave(rep, dim=1)
     s = torch.matmul(qf, kf.transpose(-1, -2)) * scale
-    ok = _visibility(B, Tq, Tk, causal, causal_off, window, kv_start, kv_end, q.device)
+    ok = _visibility(B, Tq, Tk, causal, causal_off, window, kv_start, kv_end, q.device, segs)
     s = s.masked_fill(~ok.unsqueeze(1), float("-inf"))
     p = torch.softmax(s, dim=-1)
     p = torch.nan_to_num(p, nan=0.0)
@@ -124,7 +126,8 @@ class _FusedQKVAttnFn(torch.autograd.Function):
     """qkv [B, T, C] -> o [B, T, Hq*D]; RoPE (optional) fused in; returns one dqkv."""
 
     @staticmethod
-    def forward(ctx, qkv, cos, sin, pos, Hq, Hkv, D, rot, scale, causal, window, kv_start, kv_end):
+    def forward(ctx, qkv, cos, sin, pos, Hq, Hkv, D, rot, scale, causal, window, kv_start, kv_end,
+                segs=None):
         ops = _ext.require()
         B, T, C = qkv.shape
         q2 = qkv.reshape(B * T, C)
@@ -136,16 +139,17 @@ class _FusedQKVAttnFn(torch.autograd.Function):
             q4 = qkv.as_strided((B, T, Hq, D), (T * C, C, D, 1), qkv.storage_offset())
             k4 = qkv.as_strided((B, T, Hkv, D), (T * C, C, D, 1), qkv.storage_offset() + Hq * D)
         v4 = qkv.as_strided((B, T, Hkv, D), (T * C, C, D, 1), qkv.storage_offset() + (Hq + Hkv) * D)
-        o, lse2 = ops.attn_fwd(q4, k4, v4, float(scale), bool(causal), 0, int(window), kv_start, kv_end)
+        o, lse2 = ops.attn_fwd(q4, k4, v4, float(scale), bool(causal), 0, int(window), kv_start, kv_end,
+                               segs)
         ctx.save_for_backward(qkv, q4 if rot > 0 else None, k4 if rot > 0 else None, o, lse2,
-                              cos, sin, pos, kv_start, kv_end)
+                              cos, sin, pos, kv_start, kv_end, segs)
         ctx.cfg = (B, T, C, Hq, Hkv, D, rot, scale, causal, window)
         return o.view(B, T, Hq * D)
 
     @staticmethod
     def backward(ctx, do):
         ops = _ext.require()
-        qkv, q4, k4, o, lse2, cos, sin, pos, kv_start, kv_end = ctx.saved_tensors
+        qkv, q4, k4, o, lse2, cos, sin, pos, kv_start, kv_end, segs = ctx.saved_tensors
         B, T, C, Hq, Hkv, D, rot, scale, causal, window = ctx.cfg
         off = qkv.storage_offset()
         if rot == 0:
@@ -162,36 +166,36 @@ class _FusedQKVAttnFn(torch.autograd.Function):
             dq = dqkv.as_strided((B, T, Hq, D), (T * C, C, D, 1), 0)
             dk = dqkv.as_strided((B, T, Hkv, D), (T * C, C, D, 1), Hq * D)
         ops.attn_bwd(do4, q4, k4, v4, o, lse2, dq, dk, dv, float(scale), bool(causal), 0,
-                     int(window), kv_start, kv_end)
+                     int(window), kv_start, kv_end, segs)
         if rot > 0:
             ops.rope_bwd(dq.view(B * T, Hq * D), dk.view(B * T, Hkv * D), dqkv.view(B * T, C),
                          cos, sin, pos, Hq, Hkv, D, rot, T, 0)
-        return dqkv, None, None, None, None, None, None, None, None, None, None, None, None
+        return dqkv, None, None, None, None, None, None, None, None, None, None, None, None, None
 
 
 class _AttnCoreFn(torch.autograd.Function):
     """[B, T, H, D] q/k/v -> o. Used for KV-cache decode and padded head dims."""
 
     @staticmethod
-    def forward(ctx, q, k, v, scale, causal, causal_off, window, kv_start, kv_end):
+    def forward(ctx, q, k, v, scale, causal, causal_off, window, kv_start, kv_end, segs=None):
         ops = _ext.require()
         o, lse2 = ops.attn_fwd(q, k, v, float(scale), bool(causal), int(causal_off), int(window),
-                               kv_start, kv_end)
-        ctx.save_for_backward(q, k, v, o, lse2, kv_start, kv_end)
+                               kv_start, kv_end, segs)
+        ctx.save_for_backward(q, k, v, o, lse2, kv_start, kv_end, segs)
         ctx.cfg = (scale, causal, causal_off, window)
         return o
 
     @staticmethod
     def backward(ctx, do):
         ops = _ext.require()
-        q, k, v, o, lse2, kv_start, kv_end = ctx.saved_tensors
+        q, k, v, o, lse2, kv_start, kv_end, segs = ctx.saved_tensors
         scale, causal, causal_off, window = ctx.cfg
         dq = torch.empty_like(q, memory_format=torch.contiguous_format)
         dk = torch.empty_like(k, memory_format=torch.contiguous_format)
         dv = torch.empty_like(v, memory_format=torch.contiguous_format)
         ops.attn_bwd(do.contiguous(), q, k, v, o, lse2, dq, dk, dv, float(scale), bool(causal),
-                     int(causal_off), int(window), kv_start, kv_end)
-        return dq, dk, dv, None, None, None, None, None, None
+                     int(causal_off), int(window), kv_start, kv_end, segs)
+        return dq, dk, dv, None, None, None, None, None, None, None
 
 
 def _pad_d(x: torch.Tensor, Dp: int) -> torch.Tensor:
@@ -199,20 +203,20 @@ def _pad_d(x: torch.Tensor, Dp: int) -> torch.Tensor:
 
 
 def attention_core(q, k, v, scale=None, causal=True, causal_off=None, window=0, kv_start=None,
-                   kv_end=None) -> torch.Tensor:
+                   kv_end=None, segs=None) -> torch.Tensor:
     """q [B, Tq, Hq, D], k/v [B, Tk, Hkv, D] (unit stride on D) -> [B, Tq, Hq, D]."""
     D = q.shape[-1]
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
     if causal_off is None:
         causal_off = k.shape[1] - q.shape[1]
     if not _ext.use_native(q):
-        return ref_attention(q, k, v, scale, causal, causal_off, window, kv_start, kv_end)
-    ks, ke = _i32(kv_start), _i32(kv_end)
+        return ref_attention(q, k, v, scale, causal, causal_off, window, kv_start, kv_end, segs)
+    ks, ke, sg = _i32(kv_start), _i32(kv_end), _i32(segs)
     if D in (64, 128):
-        return _AttnCoreFn.apply(q, k, v, scale, causal, causal_off, window, ks, ke)
+        return _AttnCoreFn.apply(q, k, v, scale, causal, causal_off, window, ks, ke, sg)
     Dp = 64 if D < 64 else 128
     o = _AttnCoreFn.apply(_pad_d(q, Dp), _pad_d(k, Dp), _pad_d(v, Dp), scale, causal, causal_off,
-                          window, ks, ke)
+                          window, ks, ke, sg)
     return o[..., :D]
 
 
@@ -224,9 +228,10 @@ def apply_rope(x: torch.Tensor, rope: RotaryCache, positions: torch.Tensor) -> t
 
 def qkv_attention(qkv: torch.Tensor, Hq: int, Hkv: int, D: int, rope: Optional[RotaryCache],
                   causal: bool = True, window: int = 0, kv_start=None, kv_end=None,
-                  positions: Optional[torch.Tensor] = None, scale: Optional[float] = None
-                  ) -> torch.Tensor:
-    """Fused QKV -> (RoPE) -> attention. qkv [B, T, (Hq+2Hkv)*D] -> [B, T, Hq*D]."""
+                  positions: Optional[torch.Tensor] = None, scale: Optional[float] = None,
+                  segs: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Fused QKV -> (RoPE) -> attention. qkv [B, T, (Hq+2Hkv)*D] -> [B, T, Hq*D].
+    `segs` [2, B, T] int32 (seg_start; seg_end): packed sequences, block-diagonal causal mask."""
     B, T, C = qkv.shape
     assert C == (Hq + 2 * Hkv) * D, "qkv width mismatch"
     if rope is not None and T > rope.max_pos:
@@ -241,9 +246,9 @@ def qkv_attention(qkv: torch.Tensor, Hq: int, Hkv: int, D: int, rope: Optional[R
             pos = positions if positions is not None else torch.arange(T, device=qkv.device).expand(B, T)
             q = apply_rope(q, rope, pos)
             k = apply_rope(k, rope, pos)
-        o = ref_attention(q, k, v, scale, causal, 0, window, kv_start, kv_end)
+        o = ref_attention(q, k, v, scale, causal, 0, window, kv_start, kv_end, segs)
         return o.reshape(B, T, Hq * D)
-    ks, ke = _i32(kv_start), _i32(kv_end)
+    ks, ke, sg = _i32(kv_start), _i32(kv_end), _i32(segs)
     pos32 = _i32(positions.reshape(-1)) if positions is not None else None
     if D in (64, 128):
         if rope is not None:
@@ -251,7 +256,7 @@ def qkv_attention(qkv: torch.Tensor, Hq: int, Hkv: int, D: int, rope: Optional[R
         else:
             cos = sin = torch.empty(0, device=qkv.device)
         return _FusedQKVAttnFn.apply(qkv.contiguous(), cos, sin, pos32, Hq, Hkv, D, rot, scale,
-                                     causal, window, ks, ke)
+                                     causal, window, ks, ke, sg)
     # odd head dims (e.g. phi-2 D=80): reference RoPE glue + padded native attention core
     q = qkv[..., : Hq * D].reshape(B, T, Hq, D)
     k = qkv[..., Hq * D:(Hq + Hkv) * D].reshape(B, T, Hkv, D)
@@ -260,7 +265,7 @@ def qkv_attention(qkv: torch.Tensor, Hq: int, Hkv: int, D: int, rope: Optional[R
         pos = positions if positions is not None else torch.arange(T, device=qkv.device).expand(B, T)
         q = apply_rope(q, rope, pos)
         k = apply_rope(k, rope, pos)
-    o = attention_core(q, k, v, scale, causal, 0, window, kv_start, kv_end)
+    o = attention_core(q, k, v, scale, causal, 0, window, kv_start, kv_end, segs)
     return o.reshape(B, T, Hq * D)
 
 

@@ -176,3 +176,69 @@ def test_layer_split_model_matches_single_device(name):
 def test_load_causal_lm_device_map_single_device_is_plain():
     b = load_causal_lm("tiny-llama", gradient_checkpointing=False, device="cpu", device_map="auto")
     assert b.model.layer_devices is None
+
+
+def test_packed_layout_runs():
+    from distributed_llm_alignment_amd.models.transformer import packed_layout
+
+    seg = torch.tensor([[1, 1, 1, 2, 2, 3, 0, 0], [1, 1, 1, 1, 1, 1, 1, 1]])
+    pos, segs = packed_layout(seg)
+    assert pos.tolist() == [[0, 1, 2, 0, 1, 0, 0, 1], list(range(8))]
+    assert segs[0].tolist() == [[0, 0, 0, 3, 3, 5, 6, 6], [0] * 8]
+    assert segs[1].tolist() == [[3, 3, 3, 5, 5, 6, 8, 8], [8] * 8]
+
+
+@pytest.mark.parametrize("name", ["tiny-llama", "tiny-mistral"])
+def test_packed_rows_match_separate_sequences(name):
+    """Block-diagonal packed attention: each packed sequence's hidden states and
+    loss equal those of the sequence run on its own."""
+    cfg = get_config(name)
+    m = build_model(cfg, device="cpu", seed=0)
+    lens = [5, 7, 3]
+    seqs = [torch.randint(3, cfg.vocab_size, (n,)) for n in lens]
+    T = sum(lens) + 2
+    ids = torch.zeros(1, T, dtype=torch.long)
+    ids[0, : sum(lens)] = torch.cat(seqs)
+    seg = torch.zeros(1, T, dtype=torch.long)
+    mask = torch.zeros(1, T, dtype=torch.long)
+    o = 0
+    for j, n in enumerate(lens):
+        seg[0, o:o + n] = j + 1
+        mask[0, o:o + n] = 1
+        o += n
+    hp = m(ids, mask, segment_ids=seg)
+    o = 0
+    for x in seqs:
+        hs = m(x.unsqueeze(0))
+        assert torch.allclose(hp[0, o:o + len(x)], hs[0], atol=1e-5), name
+        o += len(x)
+    # loss over the packed row == token-weighted mean of the separate losses
+    labels = ids.clone()
+    labels[mask == 0] = -100
+    o = 0
+    for n in lens:
+        labels[0, o] = -100
+        o += n
+    lp = m.causal_lm_loss(ids, labels, mask, segment_ids=seg)
+    tot = sum(m.causal_lm_loss(x.unsqueeze(0), x.unsqueeze(0)) * (len(x) - 1) for x in seqs)
+    assert torch.allclose(lp, tot / sum(n - 1 for n in lens), atol=1e-5)
+
+
+def test_packed_dataset_rows():
+    from distributed_llm_alignment_amd.data import InstructionDataset, PackedDataset
+
+    tok = ByteTokenizer()
+    recs = [{"prompt": "p" * a, "response": "r" * b} for a, b in [(3, 4), (2, 2), (10, 20), (1, 1)]]
+    base = InstructionDataset(tok, max_length=32, records=recs)
+    ds = PackedDataset(base, 32)
+    sizes = [base[i]["input_ids"].numel() for i in range(len(base))]
+    assert sum(len(r) for r in ds.rows) == len(base) and all(len(r) >= 1 for r in ds.rows)
+    for r in range(len(ds)):
+        row = ds[r]
+        n = row["input_ids"].numel()
+        assert n <= 32 and n == sum(sizes[i] for i in ds.rows[r])
+        starts = [0] + list(torch.cumsum(torch.tensor([sizes[i] for i in ds.rows[r]]), 0)[:-1])
+        assert all(row["labels"][int(s)] == -100 for s in starts)
+        assert row["segment_ids"].max().item() == len(ds.rows[r])
+    b = ds.collate([ds[0], ds[len(ds) - 1]])
+    assert set(b) == {"input_ids", "attention_mask", "labels", "segment_ids"}

@@ -153,15 +153,18 @@ def test_summarize_responses_keywords():
     assert m["avg_length"] == pytest.approx((3 + 3 + 2) / 3)
 
 
-def test_gpt2_cpu_plumbing_config(tmp_path, monkeypatch):
-    """BASELINE.json config 1 (GPT-2-small SFT, CPU, world_size=1, synthetic pairs)."""
+@pytest.mark.parametrize("packing", [False, True])
+def test_gpt2_cpu_plumbing_config(tmp_path, monkeypatch, packing):
+    """BASELINE.json config 1 (GPT-2-small SFT, CPU, world_size=1, synthetic pairs); also with
+    `data.packing: true` (packed rows, block-diagonal attention)."""
     from distributed_llm_alignment_amd.training import train_sft
 
     monkeypatch.chdir(tmp_path)
     root = Path(__file__).resolve().parent.parent
     rc = train_sft.main(["--config", str(root / "config" / "sft_gpt2_cpu.yaml"),
                          "--override", "optimization.max_train_steps=4", "--override", "logging.save_every_steps=0",
-                         "--override", "model.max_seq_length=64"])
+                         "--override", "model.max_seq_length=64",
+                         "--override", f"data.packing={str(packing).lower()}"])
     assert rc == 0
     m = _metrics(tmp_path / "logs" / "sft_gpt2_cpu")
     assert len(m) == 2 and all(r["train/loss"] == r["train/loss"] for r in m)
