@@ -38,6 +38,7 @@ def parse():
     ap.add_argument("--zero", type=int, default=None)
     ap.add_argument("--tp", type=int, default=1, help="tensor-parallel degree (dp = gpus / tp)")
     ap.add_argument("--ep", type=int, default=1, help="expert-parallel degree for MoE models")
+    ap.add_argument("--sp", type=int, default=1, help="Ulysses sequence-parallel degree (long context)")
     ap.add_argument("--fp8", action="store_true", help="MoE: e4m3 expert GEMMs in the forward")
     ap.add_argument("--grad-ckpt", action="store_true", help="activation checkpointing (policy)")
     ap.add_argument("--bucket-mb", type=float, default=256.0)
@@ -72,7 +73,7 @@ def main() -> int:
         _ext.require()
         gemm_mode = enable_gemm_tuning(dev.index)
     world = st.world_size
-    mesh = build_mesh(tp=args.tp, ep=args.ep)
+    mesh = build_mesh(tp=args.tp, ep=args.ep, sp=args.sp)
     overrides = {} if args.layers is None else {"num_layers": args.layers}
     cfg = get_config(args.model, **overrides)
     dtype = torch.bfloat16 if dev.type == "cuda" else torch.float32
@@ -85,6 +86,11 @@ def main() -> int:
     if mesh.tp > 1:
         apply_tensor_parallel(policy, mesh.tp_group)
         apply_tensor_parallel(ref, mesh.tp_group)
+    if mesh.sp > 1:
+        from distributed_llm_alignment_amd.parallel.sequence import apply_sequence_parallel
+
+        apply_sequence_parallel(policy, mesh.sp_group)
+        apply_sequence_parallel(ref, mesh.sp_group)
     if mesh.ep > 1:
         from distributed_llm_alignment_amd.parallel.expert import apply_expert_parallel
 
@@ -105,8 +111,9 @@ def main() -> int:
     else:
         engine = DataParallelEngine(policy, lr=1e-6, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01,
                                     max_grad_norm=1.0, zero_stage=args.zero, bucket_mb=args.bucket_mb,
-                                    group=mesh.dp_group, tp_group=mesh.tp_group,
-                                    expert_group=mesh.edp_group if mesh.ep > 1 else None)
+                                    group=mesh.grad_group, tp_group=mesh.tp_group,
+                                    expert_group=mesh.edp_group if mesh.ep > 1 else None,
+                                    sp_size=mesh.sp)
     policy.train()
 
     gen = torch.Generator().manual_seed(17 + mesh.dp_rank)  # TP ranks share a batch
@@ -117,7 +124,7 @@ def main() -> int:
 
     # only when the ref forward issues no collectives (TP / EP / ZeRO-3 gathers would race the
     # policy's on the same communicators from two streams)
-    ref_stream = bool(args.ref_stream) and args.tp == 1 and args.ep == 1 and args.zero != 3
+    ref_stream = bool(args.ref_stream) and args.tp == 1 and args.ep == 1 and args.sp == 1 and args.zero != 3
     refs = RefLogpsStream(ref, enabled=ref_stream)
     ref_stream = refs.stream is not None
 
@@ -204,7 +211,8 @@ def main() -> int:
                 "seq_len": args.seq_len,
                 "parallelism": f"dp{mesh.dp}" + (f"-tp{mesh.tp}" if mesh.tp > 1 else "")
                                + (f"-ep{mesh.ep}" if mesh.ep > 1 else "")
-                               + (f"-zero{engine.zero}" if mesh.dp > 1 or engine.zero == 3 else ""),
+                               + (f"-sp{mesh.sp}" if mesh.sp > 1 else "")
+                               + (f"-zero{engine.zero}" if mesh.dp * mesh.sp > 1 or engine.zero == 3 else ""),
                 "micro_batch_pairs": args.micro_pairs,
                 "grad_accum": args.accum,
                 "ref_model": "frozen, co-resident" + (", own HIP stream" if ref_stream else ""),

@@ -40,7 +40,9 @@ class RewardModel(nn.Module):
         return (hidden * m).sum(1) / attention_mask.sum(1, keepdim=True).clamp(min=1).to(hidden.dtype)
 
     def forward(self, input_ids: torch.Tensor, attention_mask: torch.Tensor = None) -> torch.Tensor:
-        h = self.backbone(input_ids, attention_mask)
+        from ..parallel.sequence import sp_full_hidden
+
+        h = sp_full_hidden(self.backbone, self.backbone(input_ids, attention_mask), input_ids.shape[1])
         return self.scorer(self.pool(h, attention_mask)).squeeze(-1).float()
 
     def hf_state_dict(self) -> Dict[str, torch.Tensor]:
@@ -88,7 +90,9 @@ class ValueModel(nn.Module):
             self.v_head.bias.zero_()
 
     def forward(self, input_ids: torch.Tensor, attention_mask: torch.Tensor = None) -> torch.Tensor:
-        return self.v_head(self.backbone(input_ids, attention_mask)).squeeze(-1).float()
+        v = self.v_head(self.backbone(input_ids, attention_mask)).squeeze(-1).float()
+        sp = getattr(self.backbone, "sp", None)
+        return v if sp is None else sp.gather(v, dim=1)[:, :input_ids.shape[1]]
 
     def hf_state_dict(self) -> Dict[str, torch.Tensor]:
         from .hf_io import to_hf_state_dict

@@ -77,6 +77,7 @@ class Attention(nn.Module):
         o_bias = cfg.attn_bias and cfg.arch in ("gpt2", "phi")
         self.o_bias = _param(H, device=device, dtype=dtype) if o_bias else None
         self.tp = None  # tensor-parallel group (parallel.tensor_parallel.apply_tensor_parallel)
+        self.sp = None  # Ulysses sequence parallel (parallel.sequence.apply_sequence_parallel)
         self.h_local, self.kv_local = cfg.num_heads, cfg.num_kv_heads
 
     def forward(self, h, rope, kv_start, kv_end, positions, cache=None, layer_idx=0, segs=None):
@@ -87,7 +88,14 @@ class Attention(nn.Module):
             h = tp_copy(h, self.tp)
         qkv = ops.linear(h, self.qkv_proj, self.qkv_bias)
         window = cfg.sliding_window if cfg.sliding_window else 0
-        if cache is None:
+        if cache is None and self.sp is not None:
+            # Ulysses: all-to-all to (all tokens, 1/P of the heads), attention, all-to-all back
+            a = self.sp.attention(
+                qkv, self.h_local, self.kv_local, cfg.head_dim,
+                lambda full, hq, hkv: ops.qkv_attention(full, hq, hkv, cfg.head_dim, rope, causal=True,
+                                                        window=window, kv_start=kv_start, kv_end=kv_end,
+                                                        positions=positions, segs=segs))
+        elif cache is None:
             a = ops.qkv_attention(qkv, self.h_local, self.kv_local, cfg.head_dim, rope,
                                   causal=True, window=window, kv_start=kv_start, kv_end=kv_end,
                                   positions=positions, segs=segs)
@@ -227,6 +235,7 @@ class CausalLM(nn.Module):
         self.tp_size = 1
         self.tp_rank = 0
         self.vocab_parallel = None  # (vocab offset, local vocab) when embed/head are vocab-sharded
+        self.sp = None              # parallel.sequence.SequenceParallel: this rank holds 1/P of T
         self.layer_devices = None   # per-layer devices under parallel.layer_split (device_map)
         if self.lm_head is None and not headless:
             # tied input/output embedding: its gradient arrives from two ops, so it must go through
@@ -283,11 +292,23 @@ class CausalLM(nn.Module):
         """`segment_ids` (optional, [B, T]): several sequences packed per row (see packed_layout)."""
         if cache is not None:
             return self._forward_cached(input_ids, attention_mask, cache)
+        sp = self.sp
+        if sp is not None:  # full (padded) masks / positions drive attention; tokens are sliced
+            from ..parallel.sequence import sp_shard_inputs
+
+            input_ids, attention_mask, segment_ids = sp_shard_inputs(sp, input_ids, attention_mask,
+                                                                     segment_ids)
         kv_start, kv_end, positions = attention_layout(attention_mask)
         segs = None
         if segment_ids is not None:
             positions, segs = packed_layout(segment_ids)
-        x = self.embed_tokens(input_ids, positions)
+        if sp is not None:
+            if positions is None:
+                B, T = input_ids.shape
+                positions = torch.arange(T, device=input_ids.device, dtype=torch.int32).expand(B, T)
+            x = self.embed_tokens(sp.local(input_ids), sp.local(positions))
+        else:
+            x = self.embed_tokens(input_ids, positions)
         resid = None
         for i, layer in enumerate(self.layers):
             if self.layer_devices is not None:
@@ -342,42 +363,53 @@ class CausalLM(nn.Module):
         return sum(terms) if terms else None
 
     # ----------------------------------------------------------------- objective helpers
-    def sequence_logprob(self, input_ids, attention_mask=None, reduction: str = "mean"):
-        """Reference `compute_logprobs` (train_dpo.py:31-39): masked mean log p per sequence."""
-        h = self(input_ids, attention_mask)  # __call__: module hooks (param all-gather waits) run
-        if self.lm_head_bias is not None:
-            return _biased_seq_logprob(self, h, input_ids, attention_mask, reduction)
-        S, T, H = h.shape
-        tgt, mask = ops.shifted_targets(input_ids, attention_mask)
-        lp = self._token_logprob(h.reshape(S * T, H), tgt.reshape(-1)).view(S, T)
-        return ops.seq_reduce(lp, mask, mean=(reduction == "mean"))
+    def _sp_targets(self, tgt: torch.Tensor, mask: Optional[torch.Tensor] = None):
+        """Full [S, T] targets / mask -> this rank's token slice (identity without SP)."""
+        sp = self.sp
+        if sp is None:
+            return tgt, mask
+        return sp.local(sp.pad(tgt, -100)), (None if mask is None else sp.local(sp.pad(mask, 0)))
 
-    def token_logprobs(self, input_ids, attention_mask=None):
-        """[S, T] log p(x_{t+1} | x_<=t) at every scored position (0 elsewhere): the per-action
-        grid of token-level RL objectives (PPO)."""
-        h = self(input_ids, attention_mask)
+    def _masked_token_logprob(self, h: torch.Tensor, tgt: torch.Tensor) -> torch.Tensor:
+        """[S, T', H] hidden + [S, T'] targets (-100 = ignore) -> [S, T'] fp32 log-probs (0 where
+        ignored); the LM-head bias models (phi-2) go through full logits."""
         S, T, H = h.shape
-        tgt, _ = ops.shifted_targets(input_ids, attention_mask)
         if self.lm_head_bias is not None:
             lg = self.logits(h).float()
             lp = torch.log_softmax(lg, -1).gather(-1, tgt.clamp(min=0).unsqueeze(-1)).squeeze(-1)
             return torch.where(tgt >= 0, lp, torch.zeros_like(lp))
         return self._token_logprob(h.reshape(S * T, H), tgt.reshape(-1)).view(S, T)
 
+    def sequence_logprob(self, input_ids, attention_mask=None, reduction: str = "mean"):
+        """Reference `compute_logprobs` (train_dpo.py:31-39): masked mean log p per sequence."""
+        h = self(input_ids, attention_mask)  # __call__: module hooks (param all-gather waits) run
+        tgt, mask = self._sp_targets(*ops.shifted_targets(input_ids, attention_mask))
+        lp = self._masked_token_logprob(h, tgt)
+        return sp_seq_reduce(self.sp, lp, mask, reduction == "mean")
+
+    def token_logprobs(self, input_ids, attention_mask=None):
+        """[S, T] log p(x_{t+1} | x_<=t) at every scored position (0 elsewhere): the per-action
+        grid of token-level RL objectives (PPO)."""
+        h = self(input_ids, attention_mask)
+        tgt, _ = self._sp_targets(ops.shifted_targets(input_ids, attention_mask)[0])
+        lp = self._masked_token_logprob(h, tgt)
+        if self.sp is not None:
+            lp = self.sp.gather(lp, dim=1)[:, :input_ids.shape[1]]
+        return lp
+
     def causal_lm_loss(self, input_ids, labels, attention_mask=None, segment_ids=None):
         """HF ForCausalLMLoss (train_sft.py:145-146): mean token NLL over labels != -100.
         With `segment_ids` the rows hold packed sequences (labels -100 at each sequence start)."""
         h = self(input_ids, attention_mask, segment_ids=segment_ids)  # __call__: module hooks run
-        if self.lm_head_bias is not None:
-            lg = self.logits(h).float()
-            return F.cross_entropy(lg[:, :-1].reshape(-1, lg.shape[-1]), labels[:, 1:].reshape(-1),
-                                   ignore_index=-100)
-        S, T, H = h.shape
         tgt = torch.full_like(labels, -100)
         tgt[:, :-1] = labels[:, 1:]
-        tgt = tgt.reshape(-1)
-        lp = self._token_logprob(h.reshape(S * T, H), tgt)
-        return -(lp.sum() / (tgt >= 0).sum().clamp(min=1))
+        tgt, _ = self._sp_targets(tgt)
+        lp = self._masked_token_logprob(h, tgt)
+        total, count = lp.sum(), (tgt >= 0).sum().float()
+        if self.sp is not None:
+            total = self.sp.reduce(total)
+            count = self.sp.reduce(count)
+        return -(total / count.clamp(min=1))
 
     # ----------------------------------------------------------------- HF key mapping
     def hf_state_dict(self) -> Dict[str, torch.Tensor]:
@@ -405,12 +437,16 @@ def _chunked_randn(p: torch.Tensor, gen: torch.Generator, std: float) -> torch.T
     return p
 
 
-def _biased_seq_logprob(model, h, input_ids, attention_mask, reduction):
-    lg = model.logits(h).float()
-    tgt, mask = ops.shifted_targets(input_ids, attention_mask)
-    lp = torch.log_softmax(lg, -1).gather(-1, tgt.clamp(min=0).unsqueeze(-1)).squeeze(-1)
-    lp = torch.where(tgt >= 0, lp, torch.zeros_like(lp))
-    return ops.seq_reduce(lp, mask, mean=(reduction == "mean"))
+def sp_seq_reduce(sp, lp: torch.Tensor, mask: torch.Tensor, mean: bool) -> torch.Tensor:
+    """Masked per-sequence sum / mean of token log-probs; under sequence parallelism the partial
+    sums and token counts of the local slices are all-reduced over the SP group."""
+    if sp is None:
+        return ops.seq_reduce(lp, mask, mean=mean)
+    s = sp.reduce(ops.seq_reduce(lp, mask, mean=False))
+    if not mean:
+        return s
+    n = sp.reduce(mask.float().sum(1))
+    return s / n.clamp(min=1)
 
 
 def default_dtype(device) -> torch.dtype:

@@ -40,11 +40,12 @@ def sequence_logps(model, ids, mask, reduction: str = "mean", loss_mask=None):
     """Per-sequence log-prob; `loss_mask` (optional) restricts scoring to response tokens."""
     if loss_mask is None:
         return model.sequence_logprob(ids, mask, reduction)
+    from ..models.transformer import sp_seq_reduce
+
     h = model(ids, mask)
-    tgt, m = ops.shifted_targets(ids, loss_mask)
-    S, T, H = h.shape
-    lp = ops.linear_logprob(h.reshape(S * T, H), model.head_weight, tgt.reshape(-1)).view(S, T)
-    return ops.seq_reduce(lp, m, mean=(reduction == "mean"))
+    tgt, m = model._sp_targets(*ops.shifted_targets(ids, loss_mask))
+    lp = model._masked_token_logprob(h, tgt)
+    return sp_seq_reduce(model.sp, lp, m, reduction == "mean")
 
 
 def dpo_step_loss(policy, ref, batch, beta: float = 0.1, label_smoothing: float = 0.0,
@@ -185,5 +186,9 @@ def distill_loss(student, teachers: Sequence, batch, use_kl: bool):
         t_logits = torch.stack([t.logits(t(ids, mask)) for t in teachers])
     S, T, V = s_logits.shape
     kl = ops.ensemble_kl(s_logits.reshape(S * T, V), t_logits.reshape(len(teachers), S * T, V)).view(S, T)
-    m = mask.float()
-    return (kl * m).sum() / m.sum()
+    sp = student.sp
+    if sp is None:
+        m = mask.float()
+        return (kl * m).sum() / m.sum()
+    m = sp.local(sp.pad(mask.float(), 0))  # sequence parallel: this rank's token slice
+    return sp.reduce((kl * m).sum()) / sp.reduce(m.sum())

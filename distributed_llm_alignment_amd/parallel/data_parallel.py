@@ -63,8 +63,12 @@ class DataParallelEngine:
                  weight_decay: float = 0.0, max_grad_norm: float = 1.0, zero_stage: Optional[int] = None,
                  bucket_mb: float = 256.0, master_weights: bool = True,
                  dist_st: Optional[DistState] = None, group=None, tp_group=None, expert_group=None,
-                 overlap_param_gather: bool = os.environ.get("DLA_OVERLAP_AG", "1") != "0"):
+                 overlap_param_gather: bool = os.environ.get("DLA_OVERLAP_AG", "1") != "0",
+                 sp_size: int = 1):
         self.module = module
+        # sequence parallel (parallel.sequence): `group` is DP x SP and the sp ranks of a replica
+        # hold partial (token-slice) gradients of one replicated loss -> sum over SP, mean over DP
+        self.sp_size = int(sp_size)
         self.dist = dist_st or dist_state()
         # tensor parallel: grads of TP-sharded params differ per TP rank; params marked
         # `_dla_tp_replicated` are identical across TP ranks (counted once in the clip norm)
@@ -286,8 +290,12 @@ class DataParallelEngine:
         self._seen = set()
 
     # ------------------------------------------------------------------------ step
+    @property
+    def grad_scale(self) -> float:
+        return self.sp_size / self.world
+
     def clip_and_norm(self):
-        gs = 1.0 / self.world
+        gs = self.grad_scale
         grad_sumsq(self.grad_shard, self._sumsq, accumulate=False)
         if self._repl_ranges:
             rep = sum(self.grad_shard[a:e].float().pow(2).sum() for a, e in self._repl_ranges)
@@ -329,7 +337,7 @@ class DataParallelEngine:
         self.step_count += 1
         adamw_update(self.param_shard, self.master, self.grad_shard, self.exp_avg, self.exp_avg_sq,
                      lr, self.betas[0], self.betas[1], self.eps, self.wd, self.step_count,
-                     clip=coef if self.max_grad_norm else None, grad_scale=1.0 / self.world)
+                     clip=coef if self.max_grad_norm else None, grad_scale=self.grad_scale)
         if self.zero:
             self.wait_params()
             for bi in reversed(range(len(self.buckets))):  # forward order

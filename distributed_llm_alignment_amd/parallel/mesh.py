@@ -5,6 +5,12 @@ contiguous rank blocks ([0..tp-1], ...), DP groups stride across them (ranks wit
 rank). On a fully connected xGMI mesh every placement has a dedicated link, so contiguous TP
 blocks are chosen for multi-node extension (TP stays intra-node). EP groups are carved from the
 DP dimension (experts sharded across data-parallel replicas, Switch/GShard style).
+
+Sequence parallelism (Ulysses, `parallel.sequence`) sits between DP and TP:
+rank = (dp_rank * sp + sp_rank) * tp + tp_rank. SP ranks share a batch (sequence slices of the
+same rows), so `dp` / `dp_rank` / `dp_group` still index *batch* replicas (what the sampler
+shards over), while gradients are reduced over `grad_group` = DP x SP (summed over SP, averaged
+over DP: `DataParallelEngine(sp_size=sp)`).
 """
 from __future__ import annotations
 
@@ -31,23 +37,52 @@ class Mesh:
     ep_group: Optional[object] = None        # ranks sharing one set of experts' tokens
     edp_group: Optional[object] = None       # ranks holding the SAME experts (grad reduction)
     world_group: Optional[object] = None
+    sp: int = 1
+    sp_rank: int = 0
+    sp_group: Optional[object] = None        # ranks holding slices of the same sequences
+    dpsp_group: Optional[object] = None      # DP x SP: gradient reduction when sp > 1
 
     @property
     def is_tp(self) -> bool:
         return self.tp > 1
 
+    @property
+    def grad_group(self):
+        """Group over which dense gradients are reduced (DP, or DP x SP under sequence parallel)."""
+        return self.dpsp_group if self.sp > 1 else self.dp_group
+
 
 _MESH: Optional[Mesh] = None
 
 
-def build_mesh(tp: int = 1, ep: int = 1) -> Mesh:
+def build_mesh(tp: int = 1, ep: int = 1, sp: int = 1) -> Mesh:
     """Create process groups (collective: every rank must call with the same arguments)."""
     global _MESH
     st = dist_state()
     world = st.world_size if st.initialized else 1
     rank = st.rank if st.initialized else 0
-    if world % tp:
-        raise ValueError(f"world {world} not divisible by tp {tp}")
+    if world % (tp * sp):
+        raise ValueError(f"world {world} not divisible by tp {tp} x sp {sp}")
+    if sp > 1 and (tp > 1 or ep > 1):
+        raise ValueError("sequence parallel composes with data parallel only (tp = ep = 1)")
+    if sp > 1:
+        dp = world // sp
+        mesh = Mesh(world=world, rank=rank, tp=1, dp=dp, ep=1, tp_rank=0, dp_rank=rank // sp,
+                    ep_rank=0, sp=sp, sp_rank=rank % sp)
+        mesh.world_group = dist.group.WORLD
+        mesh.dpsp_group = dist.group.WORLD
+        for d in range(dp):  # SP groups: contiguous blocks (one xGMI hop between any two)
+            ranks = [d * sp + s for s in range(sp)]
+            g = dist.new_group(ranks)
+            if rank in ranks:
+                mesh.sp_group = g
+        for s in range(sp):  # DP groups (batch replicas): same sp rank
+            ranks = [d * sp + s for d in range(dp)]
+            g = dist.new_group(ranks) if dp > 1 else None
+            if rank in ranks:
+                mesh.dp_group = g
+        _MESH = mesh
+        return mesh
     dp = world // tp
     if dp % ep:
         raise ValueError(f"dp {dp} not divisible by ep {ep}")

@@ -88,7 +88,7 @@ def setup(cfg: Dict[str, Any], stage: str, default_seed: int = 0) -> TrainContex
     hw = hardware_parallel(cfg)
     from ..parallel.mesh import build_mesh
 
-    mesh = build_mesh(tp=hw["tp_size"], ep=hw["ep_size"])  # collective; DP x TP x EP groups
+    mesh = build_mesh(tp=hw["tp_size"], ep=hw["ep_size"], sp=hw.get("sp_size", 1))  # collective
     return TrainContext(cfg=cfg, dist=st, device=st.device, logger=logger, hw=hw,
                         output_dir=out, log_dir=log_dir, seed=seed, stage=stage, mesh=mesh)
 
@@ -104,6 +104,10 @@ def parallelize(ctx: TrainContext, model):
         from ..parallel.tensor_parallel import apply_tensor_parallel
 
         apply_tensor_parallel(model, m.tp_group)
+    if m.sp > 1:
+        from ..parallel.sequence import apply_sequence_parallel
+
+        apply_sequence_parallel(model, m.sp_group)
     if m.ep > 1 and base.cfg.is_moe:
         from ..parallel.expert import apply_expert_parallel
 
@@ -128,21 +132,24 @@ def use_fsdp(ctx: TrainContext) -> bool:
 
 def make_engine(ctx: TrainContext, model, lr: float, betas=(0.9, 0.999), weight_decay: float = 0.0,
                 max_grad_norm: float = 1.0):
-    groups = dict(group=ctx.mesh.dp_group if ctx.mesh is not None else None,
+    groups = dict(group=ctx.mesh.grad_group if ctx.mesh is not None else None,
                   tp_group=ctx.mesh.tp_group if ctx.mesh is not None else None)
+    sp = ctx.mesh.sp if ctx.mesh is not None else 1
     if ctx.mesh is not None and ctx.mesh.ep > 1:
         groups["expert_group"] = ctx.mesh.edp_group
     if use_fsdp(ctx):
+        if sp > 1:
+            raise NotImplementedError("ZeRO-3 / FSDP with sequence parallel: use zero_stage <= 1")
         from ..parallel.fsdp import FullyShardedEngine
 
         return FullyShardedEngine(model, lr=lr, betas=betas, weight_decay=weight_decay,
                                   max_grad_norm=max_grad_norm,
-                                  master_weights=ctx.hw.get("master_weights", True), **groups)
+                                  master_weights=ctx.hw.get("master_weights", True), sp_size=sp, **groups)
     z = ctx.hw.get("zero_stage")
     return DataParallelEngine(model, lr=lr, betas=betas, weight_decay=weight_decay,
                               max_grad_norm=max_grad_norm, zero_stage=None if z is None else min(int(z), 1),
                               bucket_mb=ctx.hw.get("bucket_mb", 256.0),
-                              master_weights=ctx.hw.get("master_weights", True), **groups)
+                              master_weights=ctx.hw.get("master_weights", True), sp_size=sp, **groups)
 
 
 def effective_batch_msg(ctx: TrainContext, micro: int) -> str:
@@ -198,7 +205,7 @@ def train_loop(ctx: TrainContext, loader, sampler, engine: DataParallelEngine, s
                          enabled=ctx.is_main or bool(lg.get("profile_all_ranks", False)))
     faults = FaultInjector(dbg.get("fault_at_step"), dbg.get("fault_rank"))
     sync_every = int(dbg.get("check_sync_every", 0) or 0)
-    dp_group = ctx.mesh.dp_group if ctx.mesh is not None else None
+    dp_group = ctx.mesh.grad_group if ctx.mesh is not None else None  # params replicated over it
     running = RunningLoss()
     last_metrics: Dict[str, Any] = {}
     done = global_step >= total_steps

@@ -98,6 +98,7 @@ def hardware_parallel(cfg: Dict[str, Any]) -> Dict[str, Any]:
         "zero_stage": hw.get("zero_stage"),
         "tp_size": int(hw.get("tp_size", 1) or 1),
         "ep_size": int(hw.get("ep_size", 1) or 1),
+        "sp_size": int(hw.get("sp_size", 1) or 1),  # Ulysses sequence parallel (parallel.sequence)
         "bucket_mb": float(hw.get("bucket_mb", 256)),
         "master_weights": bool(hw.get("master_weights", True)),
         "fsdp": False,
