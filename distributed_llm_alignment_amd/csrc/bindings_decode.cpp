@@ -20,6 +20,44 @@ void launch_rope_cache(const bf16_t*, int64_t, bf16_t*, bf16_t*, bf16_t*, int64_
 void launch_sample(const void*, bool, int64_t, int64_t, int, float, int, float, bool,
                    const int64_t*, int64_t*, hipStream_t);
 
+int skinny_splits(int M, int N, int K);
+void launch_skinny_gemm(const bf16_t*, int64_t, const bf16_t*, int64_t, bf16_t*, int64_t, float*,
+                        unsigned*, int, int, int, int, bool, hipStream_t);
+
+// y[M, N] = x[M, K] @ w[N, K]^T for M <= 16 (decode). With `swiglu`, x is the fused gate|up
+// output gu[M, 2K] and the kernel applies silu(g) * u while staging it. `counters` (int32,
+// zero-initialised once, re-armed by the kernel) holds one split-K arrival counter per 64
+// output columns.
+at::Tensor skinny_gemm(const at::Tensor& x, const at::Tensor& w, at::Tensor& counters, bool swiglu) {
+  check_bf16(x, "x");
+  check_bf16(w, "w");
+  check_i32(counters, "counters");
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.stride(1) == 1 && w.stride(1) == 1,
+              "x [M, K] / w [N, K] with unit inner stride");
+  const int64_t M = x.size(0), N = w.size(0), K = w.size(1);
+  TORCH_CHECK(M >= 1 && M <= 16, "skinny GEMM: 1 <= M <= 16");
+  TORCH_CHECK(x.size(1) == (swiglu ? 2 * K : K), "x width must be K (2K with swiglu)");
+  TORCH_CHECK(K % 256 == 0 && N % 16 == 0, "skinny GEMM: K % 256 == 0 and N % 16 == 0");
+  TORCH_CHECK(x.stride(0) % 8 == 0 && w.stride(0) % 8 == 0, "16-byte aligned rows");
+  TORCH_CHECK(N < (1ll << 30) && K < (1ll << 30), "shape too large");
+  check_aligned16(x, "x");
+  check_aligned16(w, "w");
+  same_device(x, w);
+  same_device(x, counters);
+  const int64_t nb = (N + 63) / 64;
+  TORCH_CHECK(counters.is_contiguous() && counters.numel() >= nb, "counters: one per 64 columns");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  const int S = skinny_splits((int)M, (int)N, (int)K);
+  auto y = at::empty({M, N}, x.options());
+  at::Tensor ws;
+  if (S > 1) ws = at::empty({S, M, N}, x.options().dtype(at::kFloat));
+  launch_skinny_gemm(cbp(x), x.stride(0), cbp(w), w.stride(0), bp(y), y.stride(0),
+                     S > 1 ? ws.data_ptr<float>() : nullptr,
+                     reinterpret_cast<unsigned*>(counters.data_ptr<int>()), (int)M, (int)N, (int)K,
+                     S, swiglu, cur_stream(x));
+  return y;
+}
+
 at::Tensor decode_attn(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
                        const at::Tensor& kv_len, const c10::optional<at::Tensor>& kv_start,
                        int64_t window, double scale) {
@@ -128,10 +166,12 @@ TORCH_LIBRARY_FRAGMENT(dla, m) {
   m.def("decode_attn(Tensor q, Tensor k_cache, Tensor v_cache, Tensor kv_len, Tensor? kv_start, int window, float scale) -> Tensor");
   m.def("rope_cache_write(Tensor qkv, Tensor cos, Tensor sin, Tensor pos, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor slot, int Hq, int Hkv, int D, int rot) -> Tensor");
   m.def("sample_tokens(Tensor logits, float temperature, int top_k, float top_p, bool greedy, Tensor rng) -> Tensor");
+  m.def("skinny_gemm(Tensor x, Tensor w, Tensor(a!) counters, bool swiglu) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(dla, CUDA, m) {
   m.impl("decode_attn", &dla::decode_attn);
   m.impl("sample_tokens", &dla::sample_tokens);
   m.impl("rope_cache_write", &dla::rope_cache_write);
+  m.impl("skinny_gemm", &dla::skinny_gemm);
 }

@@ -86,7 +86,7 @@ class Attention(nn.Module):
             from ..parallel.tensor_parallel import tp_copy
 
             h = tp_copy(h, self.tp)
-        qkv = ops.linear(h, self.qkv_proj, self.qkv_bias)
+        qkv = _lin(h, self.qkv_proj, self.qkv_bias)
         window = cfg.sliding_window if cfg.sliding_window else 0
         if cache is None and self.sp is not None:
             # Ulysses: all-to-all to (all tokens, 1/P of the heads), attention, all-to-all back
@@ -102,7 +102,7 @@ class Attention(nn.Module):
         else:
             a = cache.attend(layer_idx, qkv, rope, window)
         if self.tp is None:
-            return ops.linear(a, self.o_proj, self.o_bias)
+            return _lin(a, self.o_proj, self.o_bias)
         from ..parallel.tensor_parallel import tp_reduce
 
         out = tp_reduce(ops.linear(a, self.o_proj, None), self.tp)
@@ -128,6 +128,13 @@ class MLP(nn.Module):
             from ..parallel.tensor_parallel import tp_copy
 
             h = tp_copy(h, self.tp)
+        if (self.cfg.activation == "swiglu" and self.up_bias is None and self.down_bias is None
+                and self.tp is None and ops.decode.skinny_ok(h, self.up_proj)):
+            # decode (<= 16 rows, no autograd): skinny GEMMs, SwiGLU fused into the down GEMM
+            u = ops.decode.skinny_linear(h, self.up_proj)
+            if u is not None:
+                y = ops.decode.skinny_linear(u, self.down_proj, swiglu=True)
+                return y if y is not None else ops.linear(ops.swiglu(u), self.down_proj)
         if (self.cfg.activation == "swiglu" and self.up_bias is None and self.down_bias is None
                 and ops.swiglu_mlp_ok(h, self.up_proj, self.down_proj)):
             out = ops.swiglu_mlp(h, self.up_proj, self.down_proj)
@@ -341,7 +348,11 @@ class CausalLM(nn.Module):
         return h
 
     def logits(self, hidden: torch.Tensor) -> torch.Tensor:
-        lg = F.linear(hidden, self.head_weight, self.lm_head_bias)
+        lg = None
+        if self.lm_head_bias is None:
+            lg = ops.decode.skinny_linear(hidden, self.head_weight)  # decode rows only
+        if lg is None:
+            lg = F.linear(hidden, self.head_weight, self.lm_head_bias)
         if self.vocab_parallel is not None:
             from ..parallel.tensor_parallel import tp_all_gather_last
 
@@ -421,6 +432,15 @@ class CausalLM(nn.Module):
         from .hf_io import load_hf_state_dict
 
         return load_hf_state_dict(self, sd, strict=strict)
+
+
+def _lin(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor]) -> torch.Tensor:
+    """ops.linear, with the decode skinny-GEMM kernel for <= 16 rows without autograd."""
+    if b is None:
+        y = ops.decode.skinny_linear(x, w)
+        if y is not None:
+            return y
+    return ops.linear(x, w, b)
 
 
 def _hop(dev, *ts):

@@ -7,6 +7,7 @@ be captured once in a hipGraph and replayed per token. CPU tensors use PyTorch r
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional
 
 import torch
@@ -59,3 +60,55 @@ def sample_tokens(logits: torch.Tensor, temperature: float, top_k: int, top_p: f
     from ..models.generation import sample_next
 
     return sample_next(logits.float(), not greedy, temperature, top_p, top_k, generator)
+
+
+# ------------------------------------------------------------------------- skinny GEMM (M <= 16)
+SKINNY = os.environ.get("DLA_SKINNY", "1") != "0"
+_COUNTERS = {}
+
+
+def _skinny_counters(dev: torch.device) -> Optional[torch.Tensor]:
+    """Per-device split-K arrival counters (zeroed once; the kernel re-arms them). Never created
+    inside a hipGraph capture (it would become a graph-pool allocation + memset node)."""
+    key = dev.index
+    c = _COUNTERS.get(key)
+    if c is None:
+        if torch.cuda.is_current_stream_capturing():
+            return None
+        c = torch.zeros(8192, dtype=torch.int32, device=dev)
+        _COUNTERS[key] = c
+    return c
+
+
+def skinny_ok(x: torch.Tensor, weight: torch.Tensor, swiglu: bool = False) -> bool:
+    """Inference-only decode GEMM: <= 16 rows, bf16, K % 256 == 0, N % 16 == 0, no autograd."""
+    if not (SKINNY and _ext.use_native(x)) or torch.is_grad_enabled() and (x.requires_grad or weight.requires_grad):
+        return False
+    rows = x.numel() // x.shape[-1] if x.dim() else 0
+    N, K = weight.shape if weight.dim() == 2 else (0, 0)
+    return (1 <= rows <= 16 and x.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16
+            and weight.dim() == 2 and weight.stride(1) == 1 and weight.stride(0) % 8 == 0
+            and x.shape[-1] == (2 * K if swiglu else K) and K % 256 == 0 and N % 16 == 0
+            and (N + 63) // 64 <= 8192 and x.device == weight.device)
+
+
+def skinny_linear(x: torch.Tensor, weight: torch.Tensor, swiglu: bool = False) -> Optional[torch.Tensor]:
+    """y = x @ weight^T (or swiglu(x) @ weight^T) with the decode skinny-GEMM kernel
+    (csrc/skinny.hip). Returns None when the shape/state is not eligible (caller falls back)."""
+    if not skinny_ok(x, weight, swiglu):
+        return None
+    cnt = _skinny_counters(x.device)
+    if cnt is None:
+        return None
+    x2 = x.reshape(-1, x.shape[-1])
+    if x2.stride(-1) != 1 or x2.stride(0) % 8 or x2.data_ptr() % 16:
+        x2 = x2.contiguous()
+    y = _ext.require().skinny_gemm(x2, weight, cnt, bool(swiglu))
+    return y.view(*x.shape[:-1], weight.shape[0])
+
+
+def ref_skinny_linear(x: torch.Tensor, weight: torch.Tensor, swiglu: bool = False) -> torch.Tensor:
+    if swiglu:
+        g, u = x.float().chunk(2, dim=-1)
+        x = (torch.nn.functional.silu(g) * u).to(x.dtype)
+    return (x.float() @ weight.float().t()).to(x.dtype)
