@@ -26,7 +26,7 @@ void launch_skinny_gemm(const bf16_t*, int64_t, const bf16_t*, int64_t, bf16_t*,
 
 // y[M, N] = x[M, K] @ w[N, K]^T for M <= 16 (decode). With `swiglu`, x is the fused gate|up
 // output gu[M, 2K] and the kernel applies silu(g) * u while staging it. `counters` (int32,
-// zero-initialised once, re-armed by the kernel) holds one split-K arrival counter per 64
+// zero-initialised once, re-armed by the kernel) holds one split-K arrival counter per 128
 // output columns.
 at::Tensor skinny_gemm(const at::Tensor& x, const at::Tensor& w, at::Tensor& counters, bool swiglu) {
   check_bf16(x, "x");
@@ -44,10 +44,11 @@ at::Tensor skinny_gemm(const at::Tensor& x, const at::Tensor& w, at::Tensor& cou
   check_aligned16(w, "w");
   same_device(x, w);
   same_device(x, counters);
-  const int64_t nb = (N + 63) / 64;
-  TORCH_CHECK(counters.is_contiguous() && counters.numel() >= nb, "counters: one per 64 columns");
+  const int64_t nb = (N + 127) / 128;
+  TORCH_CHECK(counters.is_contiguous() && counters.numel() >= nb, "counters: one per 128 columns");
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   const int S = skinny_splits((int)M, (int)N, (int)K);
+  TORCH_CHECK(M * (K / S + 8) * 2 <= 160 * 1024, "skinny GEMM: x slice exceeds LDS");
   auto y = at::empty({M, N}, x.options());
   at::Tensor ws;
   if (S > 1) ws = at::empty({S, M, N}, x.options().dtype(at::kFloat));

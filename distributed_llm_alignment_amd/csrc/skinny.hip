@@ -7,23 +7,27 @@
 // src/training/generate_teacher_data.py:60-80 runs these projections with a handful of rows.
 //
 // Why a hand-written kernel: at M <= 16 a GEMM is a weight stream (Llama-3-8B decode reads
-// ~16 GB of weights per token) and the library's tiles for it ran at 2.2-4.9 TB/s on MI355X
-// (profiles/r1_decode_v2_kernel_stats.md). The layout here is built for that stream:
+// ~16 GB of weights per token) and the library's tiles for it ran at 2.2-4.9 TB/s in a real
+// decode step on MI355X. The layout here is built for that stream (measured results and the
+// split-K caveat: profiles/r1_decode_skinny.md):
 //   * the workgroup stages its K-slice of x in LDS once (rows >= M are never read: those lanes
 //     feed zeros to the MFMA);
 //   * each wave owns 16 weight rows and walks its K-slice with 16-byte loads, 8 k-steps
 //     (8 x 16 B per lane) in flight ahead of the MFMAs (v_mfma_f32_16x16x32_bf16: B fragment =
 //     16 weight rows x 32 k, exactly what one 16-byte load per lane delivers);
 //   * split-K over workgroups fills the 256 CUs for N = 4096; partial tiles go to an fp32
-//     workspace and the last-arriving workgroup of a column (device-scope counter, reset by
-//     that workgroup: no memset, graph-capture safe) sums them in a FIXED order: deterministic.
+//     workspace and the last-arriving workgroup of a column (agent-scope release/acquire +
+//     ticket counter, re-armed by that workgroup: no memset, graph-capture safe) sums them in a
+//     FIXED order: deterministic.
 #include "common.h"
+
+#include <cstdlib>
 
 namespace dla {
 
 namespace {
 
-constexpr int kSkWaves = 4;           // waves per workgroup; each owns 16 output columns
+constexpr int kSkWaves = 8;           // waves per workgroup; each owns 16 output columns
 constexpr int kSkCols = 16 * kSkWaves;  // output columns (weight rows) per workgroup
 constexpr int kSkUnroll = 8;          // k-steps (32 each) of weight loads in flight per wave
 constexpr int kSkChunk = 32 * kSkUnroll;
@@ -36,10 +40,10 @@ __device__ __forceinline__ float silu_sk(float g) { return g * sigmoidf_(g); }
 
 }  // namespace
 
-// grid: (ceil(N / 64), S). LDS: M x (kc + 8) bf16 (row pad of 16 B keeps the 16-row fragment
+// grid: (ceil(N / 128), S), 8 waves. LDS: M x (kc + 8) bf16 (row pad of 16 B keeps the 16-row fragment
 // reads on distinct banks).
 template <bool SWIGLU>
-__global__ __launch_bounds__(256) void skinny_gemm_kernel(
+__global__ __launch_bounds__(64 * kSkWaves) void skinny_gemm_kernel(
     const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ W, int64_t ldw,
     bf16_t* __restrict__ y, int64_t ldy, float* __restrict__ ws, unsigned* __restrict__ counters,
     int M, int N, int K, int kc) {
@@ -50,52 +54,97 @@ __global__ __launch_bounds__(256) void skinny_gemm_kernel(
   const int klen = min(kc, K - k0);
   const int ldl = kc + 8;
 
-  // ---- stage x[:, k0:k0+klen] (or swiglu(gu) of it) into LDS, 16 B per thread-step
-  const int vecs = klen >> 3;
-  for (int i = threadIdx.x; i < M * vecs; i += blockDim.x) {
-    const int m = i / vecs, c = (i - m * vecs) << 3;
-    bf16x8 v;
-    if constexpr (SWIGLU) {
-      const bf16x8 g = load_bf16x8(x + m * ldx + k0 + c);
-      const bf16x8 u = load_bf16x8(x + m * ldx + K + k0 + c);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = f2bf(silu_sk(bf2f(g[j])) * bf2f(u[j]));
-    } else {
-      v = load_bf16x8(x + m * ldx + k0 + c);
-    }
-    store_bf16x8(xs + m * ldl + c, v);
-  }
-  __syncthreads();
-
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int n0 = blockIdx.x * kSkCols + wave * 16;
   const int r = lane & 15, q = lane >> 4;  // fragment row (m for A, n for B), k quarter
+  const bool active = n0 < N;
+  const bf16_t* wrow = W + static_cast<int64_t>(active ? n0 + r : 0) * ldw + k0 + q * 8;
+
+  // the first two weight chunks are in flight before x is staged (independent of LDS)
+  const int nchunks = klen / kSkChunk;
+  s16x8 b0[kSkUnroll], b1[kSkUnroll];
+  if (active) {
+#pragma unroll
+    for (int u = 0; u < kSkUnroll; ++u) b0[u] = __builtin_bit_cast(s16x8, load_bf16x8(wrow + u * 32));
+    if (nchunks > 1) {
+#pragma unroll
+      for (int u = 0; u < kSkUnroll; ++u)
+        b1[u] = __builtin_bit_cast(s16x8, load_bf16x8(wrow + kSkChunk + u * 32));
+    }
+  }
+
+  // ---- stage x[:, k0:k0+klen] (or swiglu(gu) of it) into LDS: 8 independent 16-byte loads per
+  // thread per pass (all issued before the first LDS store, so the pass costs one latency)
+  const int vecs = klen >> 3;
+  const int total = M * vecs;
+  constexpr int NT = 64 * kSkWaves;
+  for (int base = 0; base < total; base += 8 * NT) {
+    bf16x8 v[8];
+    if constexpr (SWIGLU) {
+      bf16x8 gg[8], uu[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = base + j * NT + threadIdx.x;
+        if (i < total) {
+          const int m = i / vecs, c = (i - m * vecs) << 3;
+          gg[j] = load_bf16x8(x + m * ldx + k0 + c);
+          uu[j] = load_bf16x8(x + m * ldx + K + k0 + c);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[j][e] = f2bf(silu_sk(bf2f(gg[j][e])) * bf2f(uu[j][e]));
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = base + j * NT + threadIdx.x;
+        if (i < total) {
+          const int m = i / vecs, c = (i - m * vecs) << 3;
+          v[j] = load_bf16x8(x + m * ldx + k0 + c);
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int i = base + j * NT + threadIdx.x;
+      if (i < total) {
+        const int m = i / vecs, c = (i - m * vecs) << 3;
+        store_bf16x8(xs + m * ldl + c, v[j]);
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- main loop: ping-pong register buffers, the next chunk's 8 loads stay in flight while
+  // the current chunk's 8 MFMAs run (no wait on the newest loads until they are consumed)
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  if (n0 < N) {
-    const bf16_t* wrow = W + static_cast<int64_t>(n0 + r) * ldw + k0 + q * 8;
+  if (active) {
     const bf16_t* xrow = xs + r * ldl + q * 8;
     const bool arow = r < M;
-    s16x8 b[kSkUnroll];
-#pragma unroll
-    for (int u = 0; u < kSkUnroll; ++u)
-      b[u] = __builtin_bit_cast(s16x8, load_bf16x8(wrow + u * 32));
-    for (int kk = 0; kk < klen; kk += kSkChunk) {
-      s16x8 nb[kSkUnroll];
-      const bool more = kk + kSkChunk < klen;
-      if (more) {
-#pragma unroll
-        for (int u = 0; u < kSkUnroll; ++u)
-          nb[u] = __builtin_bit_cast(s16x8, load_bf16x8(wrow + kk + kSkChunk + u * 32));
-      }
+    auto compute = [&](const s16x8* b, int kk) {
 #pragma unroll
       for (int u = 0; u < kSkUnroll; ++u) {
         s16x8 a = {0, 0, 0, 0, 0, 0, 0, 0};
         if (arow) a = __builtin_bit_cast(s16x8, load_bf16x8(xrow + kk + u * 32));
         acc = mfma16(a, b[u], acc);
       }
-      if (more) {
+    };
+    // two register sets in a ring: compute chunk c while chunk c+1 is in flight, then refill
+    for (int c = 0; c < nchunks; c += 2) {
+      compute(b0, c * kSkChunk);
+      if (c + 2 < nchunks) {
 #pragma unroll
-        for (int u = 0; u < kSkUnroll; ++u) b[u] = nb[u];
+        for (int u = 0; u < kSkUnroll; ++u)
+          b0[u] = __builtin_bit_cast(s16x8, load_bf16x8(wrow + (c + 2) * kSkChunk + u * 32));
+      }
+      if (c + 1 < nchunks) {
+        compute(b1, (c + 1) * kSkChunk);
+        if (c + 3 < nchunks) {
+#pragma unroll
+          for (int u = 0; u < kSkUnroll; ++u)
+            b1[u] = __builtin_bit_cast(s16x8, load_bf16x8(wrow + (c + 3) * kSkChunk + u * 32));
+        }
       }
     }
   }
@@ -112,7 +161,9 @@ __global__ __launch_bounds__(256) void skinny_gemm_kernel(
     }
     return;
   }
-  // split-K: partial tile -> ws[s][m][n]; the last workgroup of this column block reduces
+  // split-K: partial tile -> fp32 slab ws[s][m][n] (plain stores); then one agent-scope release
+  // + ticket per workgroup, and one acquire in the last arriver, which sums the S slabs of its 64
+  // columns in split order (fixed -> deterministic) with plain loads
   if (n < N) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -120,34 +171,47 @@ __global__ __launch_bounds__(256) void skinny_gemm_kernel(
       if (m < M) ws[(static_cast<int64_t>(s) * M + m) * N + n] = acc[i];
     }
   }
-  __threadfence();
-  __syncthreads();
-  __shared__ unsigned last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // every wave's slab stores are complete; the x image in LDS is dead
+  unsigned* flag = reinterpret_cast<unsigned*>(xs);
   if (threadIdx.x == 0) {
-    const unsigned prev = atomicAdd(&counters[blockIdx.x], 1u);
-    last = (prev == static_cast<unsigned>(S - 1));
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned prev = __hip_atomic_fetch_add(&counters[blockIdx.x], 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+    flag[0] = (prev == static_cast<unsigned>(S - 1)) ? 1u : 0u;
   }
   __syncthreads();
-  if (!last) return;
-  __threadfence();
-  // reduce this block's 64 columns x M rows in split order (fixed -> deterministic)
+  if (flag[0] == 0u) return;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    counters[blockIdx.x] = 0u;  // re-arm for the next launch (kernel boundary orders it)
+  }
+  __syncthreads();
   const int nb0 = blockIdx.x * kSkCols;
   for (int i = threadIdx.x; i < M * kSkCols; i += blockDim.x) {
     const int m = i / kSkCols, nn = nb0 + (i - m * kSkCols);
     if (nn >= N) continue;
+    const float* p = ws + static_cast<int64_t>(m) * N + nn;
+    const int64_t slab = static_cast<int64_t>(M) * N;
     float t = 0.f;
-    for (int ss = 0; ss < S; ++ss)
-      t += __hip_atomic_load(ws + (static_cast<int64_t>(ss) * M + m) * N + nn, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
+    for (int ss = 0; ss < S; ++ss) t += p[ss * slab];
     y[m * ldy + nn] = f2bf(t);
   }
-  if (threadIdx.x == 0) counters[blockIdx.x] = 0u;  // re-arm for the next launch
 }
 
 int skinny_splits(int M, int N, int K) {
-  // smallest split count (K-slices a multiple of kSkChunk) that gives >= 512 workgroups, with the
-  // x slice within 64 KB of LDS (two workgroups per CU)
+  // Column blocks >= 128 (8 waves each: >= 4 waves per CU): no split (an in-kernel split-K combine costs each
+  // workgroup an agent-scope release, measured 1.5-2x slower at 900-4000 workgroups). Otherwise
+  // the smallest split count (K-slices a multiple of kSkChunk) giving >= `target` workgroups
+  // (DLA_SKINNY_WG, default 256: one 8-wave workgroup per CU).
+  static const int target = [] {
+    const char* e = getenv("DLA_SKINNY_WG");
+    return e ? atoi(e) : 256;
+  }();
   const int nb = (N + kSkCols - 1) / kSkCols;
+  if (nb >= 128) return 1;
   const int chunks = K / kSkChunk;
   int best = chunks;
   for (int s = 1; s <= chunks; ++s) {
@@ -155,7 +219,7 @@ int skinny_splits(int M, int N, int K) {
     const int kc = K / s;
     if (static_cast<int64_t>(M) * (kc + 8) * 2 > 65536) continue;
     best = s;
-    if (static_cast<int64_t>(nb) * s >= 512) break;
+    if (static_cast<int64_t>(nb) * s >= target) break;
   }
   return best;
 }
@@ -168,6 +232,14 @@ void launch_skinny_gemm(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t l
   const int kc = K / S;
   dim3 grid((N + kSkCols - 1) / kSkCols, S);
   const size_t lds = skinny_lds_bytes(M, kc);
+  static bool attr_set = [] {  // S = 1 at K = 4096 stages up to 16 x 4104 bf16 (> 64 KB default)
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_gemm_kernel<false>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_gemm_kernel<true>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    return true;
+  }();
+  (void)attr_set;
   if (swiglu)
     skinny_gemm_kernel<true><<<grid, 64 * kSkWaves, lds, st>>>(x, ldx, W, ldw, y, ldy, ws,
                                                                 counters, M, N, K, kc);

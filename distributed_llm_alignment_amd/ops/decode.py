@@ -64,6 +64,11 @@ def sample_tokens(logits: torch.Tensor, temperature: float, top_k: int, top_p: f
 
 # ------------------------------------------------------------------------- skinny GEMM (M <= 16)
 SKINNY = os.environ.get("DLA_SKINNY", "1") != "0"
+# Only wide outputs (>= 128 column blocks of 128: no split-K) take the skinny kernel by default.
+# Narrow ones need split-K, and the in-kernel combine's agent-scope release fence made a real
+# decode step 1.66x slower on MI355X (dirty L2 from the KV-cache / activation writes), although
+# the isolated GEMMs measured fine (tools/skinny_bench.py; profiles/r1_decode_skinny.md).
+SKINNY_MIN_N = int(os.environ.get("DLA_SKINNY_MIN_N", "16384"))
 _COUNTERS = {}
 
 
@@ -86,10 +91,10 @@ def skinny_ok(x: torch.Tensor, weight: torch.Tensor, swiglu: bool = False) -> bo
         return False
     rows = x.numel() // x.shape[-1] if x.dim() else 0
     N, K = weight.shape if weight.dim() == 2 else (0, 0)
-    return (1 <= rows <= 16 and x.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16
+    return (1 <= rows <= 16 and N >= SKINNY_MIN_N and x.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16
             and weight.dim() == 2 and weight.stride(1) == 1 and weight.stride(0) % 8 == 0
             and x.shape[-1] == (2 * K if swiglu else K) and K % 256 == 0 and N % 16 == 0
-            and (N + 63) // 64 <= 8192 and x.device == weight.device)
+            and (N + 127) // 128 <= 8192 and x.device == weight.device)
 
 
 def skinny_linear(x: torch.Tensor, weight: torch.Tensor, swiglu: bool = False) -> Optional[torch.Tensor]:

@@ -5,9 +5,14 @@ hipBLASLt with the TunableOp table) at Llama-3-8B decode shapes, B = 8 rows.
 """
 import argparse
 import json
+import os
+import sys
 
 import torch
 import torch.nn.functional as F
+
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def timeit(fn, iters):
