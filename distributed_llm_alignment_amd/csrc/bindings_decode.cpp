@@ -21,6 +21,9 @@ void launch_sample(const void*, bool, int64_t, int64_t, int, float, int, float, 
                    const int64_t*, int64_t*, hipStream_t);
 
 int skinny_splits(int M, int N, int K);
+bool skinny_use_ksplit(int N, int K);
+void launch_skinny_ksplit(const bf16_t*, int64_t, const bf16_t*, int64_t, bf16_t*, int64_t, int,
+                          int, int, hipStream_t);
 void launch_skinny_gemm(const bf16_t*, int64_t, const bf16_t*, int64_t, bf16_t*, int64_t, float*,
                         unsigned*, int, int, int, int, bool, hipStream_t);
 
@@ -47,9 +50,14 @@ at::Tensor skinny_gemm(const at::Tensor& x, const at::Tensor& w, at::Tensor& cou
   const int64_t nb = (N + 127) / 128;
   TORCH_CHECK(counters.is_contiguous() && counters.numel() >= nb, "counters: one per 128 columns");
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  auto y = at::empty({M, N}, x.options());
+  if (!swiglu && skinny_use_ksplit((int)N, (int)K)) {  // narrow N: in-workgroup split-K
+    launch_skinny_ksplit(cbp(x), x.stride(0), cbp(w), w.stride(0), bp(y), y.stride(0), (int)M,
+                         (int)N, (int)K, cur_stream(x));
+    return y;
+  }
   const int S = skinny_splits((int)M, (int)N, (int)K);
   TORCH_CHECK(M * (K / S + 8) * 2 <= 160 * 1024, "skinny GEMM: x slice exceeds LDS");
-  auto y = at::empty({M, N}, x.options());
   at::Tensor ws;
   if (S > 1) ws = at::empty({S, M, N}, x.options().dtype(at::kFloat));
   launch_skinny_gemm(cbp(x), x.stride(0), cbp(w), w.stride(0), bp(y), y.stride(0),

@@ -248,4 +248,79 @@ void launch_skinny_gemm(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t l
                                                                  counters, M, N, K, kc);
 }
 
+// Narrow outputs (N <= ~16K: qkv, o, down at Llama-3-8B): ONE workgroup per 16 output columns,
+// its 8 waves split K among themselves (wave w: k in [w K/8, (w+1) K/8)) and reduce their
+// 16 x 16 accumulators through LDS. No cross-workgroup combine (whose agent-scope release made
+// the split-K form slow inside a real decode step), 8 waves per CU for N = 4096. x is read as
+// MFMA A fragments straight from global memory (tiny, L2-resident), in the same two-set ring as
+// the weights.
+constexpr int kKsUnroll = 4;  // k-steps per chunk (one 16-byte W and x load per lane each)
+constexpr int kKsChunk = 32 * kKsUnroll;
+
+template <int DEPTH>
+__global__ __launch_bounds__(512) void skinny_ksplit_kernel(
+    const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ W, int64_t ldw,
+    bf16_t* __restrict__ y, int64_t ldy, int M, int N, int K) {
+  __shared__ float red[8][4][64];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = lane & 15, q = lane >> 4;
+  const int n0 = blockIdx.x * 16;
+  const int kw = K >> 3;  // per-wave K slice (multiple of kKsChunk, checked on the host)
+  const int k0 = wave * kw;
+  const int nchunks = kw / kKsChunk;
+  const bool arow = r < M;
+  const bf16_t* wrow = W + static_cast<int64_t>(n0 + r) * ldw + k0 + q * 8;
+  const bf16_t* xrow = x + static_cast<int64_t>(arow ? r : 0) * ldx + k0 + q * 8;
+  // DEPTH chunks (W and x fragments) in flight: a ring of register sets, refilled as consumed
+  s16x8 b[DEPTH][kKsUnroll], a[DEPTH][kKsUnroll];
+  auto load = [&](int j, int c) {
+#pragma unroll
+    for (int u = 0; u < kKsUnroll; ++u)
+      b[j][u] = __builtin_bit_cast(s16x8, load_bf16x8(wrow + c * kKsChunk + u * 32));
+#pragma unroll
+    for (int u = 0; u < kKsUnroll; ++u) {
+      a[j][u] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (arow) a[j][u] = __builtin_bit_cast(s16x8, load_bf16x8(xrow + c * kKsChunk + u * 32));
+    }
+  };
+#pragma unroll
+  for (int j = 0; j < DEPTH; ++j)
+    if (j < nchunks) load(j, j);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int c0 = 0; c0 < nchunks; c0 += DEPTH) {
+#pragma unroll
+    for (int j = 0; j < DEPTH; ++j) {
+      const int c = c0 + j;
+      if (c < nchunks) {
+#pragma unroll
+        for (int u = 0; u < kKsUnroll; ++u) acc = mfma16(a[j][u], b[j][u], acc);
+        if (c + DEPTH < nchunks) load(j, c + DEPTH);
+      }
+    }
+  }
+  // lane holds C[m = 4q + i][n = n0 + r]; sum the 8 waves' tiles in wave order (deterministic)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) red[wave][i][lane] = acc[i];
+  __syncthreads();
+  if (threadIdx.x < 256) {
+    const int i = threadIdx.x >> 6, l = threadIdx.x & 63;
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) t += red[w][i][l];
+    const int m = 4 * (l >> 4) + i, n = n0 + (l & 15);
+    if (m < M) y[m * ldy + n] = f2bf(t);
+  }
+}
+
+bool skinny_use_ksplit(int N, int K) {
+  return (N + kSkCols - 1) / kSkCols < 128 && (K % (8 * kKsChunk)) == 0 && N % 16 == 0;
+}
+
+void launch_skinny_ksplit(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
+                          int64_t ldy, int M, int N, int K, hipStream_t st) {
+  // a 2-deep ring (84 VGPRs: 5-6 waves per SIMD, every qkv block resident in one round); a
+  // 4-deep ring (152 VGPRs) measured slower at qkv (16.0 vs 14.8 us in a decode step)
+  skinny_ksplit_kernel<2><<<N / 16, 512, 0, st>>>(x, ldx, W, ldw, y, ldy, M, N, K);
+}
+
 }  // namespace dla

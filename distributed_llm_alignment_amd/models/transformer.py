@@ -133,8 +133,10 @@ class MLP(nn.Module):
             # decode (<= 16 rows, no autograd): skinny GEMMs, SwiGLU fused into the down GEMM
             u = ops.decode.skinny_linear(h, self.up_proj)
             if u is not None:
-                y = ops.decode.skinny_linear(u, self.down_proj, swiglu=True)
-                return y if y is not None else ops.linear(ops.swiglu(u), self.down_proj)
+                # SwiGLU fused into the down GEMM only where that GEMM needs no split-K combine
+                y = (ops.decode.skinny_linear(u, self.down_proj, swiglu=True)
+                     if self.down_proj.shape[0] >= ops.decode.SKINNY_WIDE_N else None)
+                return y if y is not None else _lin(ops.swiglu(u), self.down_proj, None)
         if (self.cfg.activation == "swiglu" and self.up_bias is None and self.down_bias is None
                 and ops.swiglu_mlp_ok(h, self.up_proj, self.down_proj)):
             out = ops.swiglu_mlp(h, self.up_proj, self.down_proj)

@@ -64,11 +64,13 @@ def sample_tokens(logits: torch.Tensor, temperature: float, top_k: int, top_p: f
 
 # ------------------------------------------------------------------------- skinny GEMM (M <= 16)
 SKINNY = os.environ.get("DLA_SKINNY", "1") != "0"
-# Only wide outputs (>= 128 column blocks of 128: no split-K) take the skinny kernel by default.
-# Narrow ones need split-K, and the in-kernel combine's agent-scope release fence made a real
-# decode step 1.66x slower on MI355X (dirty L2 from the KV-cache / activation writes), although
-# the isolated GEMMs measured fine (tools/skinny_bench.py; profiles/r1_decode_skinny.md).
-SKINNY_MIN_N = int(os.environ.get("DLA_SKINNY_MIN_N", "16384"))
+# Every decode GEMM takes the skinny kernels: wide outputs (>= 128 column blocks) the LDS-staged
+# kernel without split-K, narrow ones the in-workgroup split-K kernel. The cross-workgroup
+# split-K form (agent-scope release per workgroup) stays only for shapes neither fits, since inside
+# a real decode step it was 1.66x slower (profiles/r1_decode_skinny.md). DLA_SKINNY_MIN_N raises
+# the width threshold for A/B runs.
+SKINNY_MIN_N = int(os.environ.get("DLA_SKINNY_MIN_N", "0"))
+SKINNY_WIDE_N = 128 * 128  # >= this many output columns: the kernel runs without any split-K
 _COUNTERS = {}
 
 
@@ -85,22 +87,24 @@ def _skinny_counters(dev: torch.device) -> Optional[torch.Tensor]:
     return c
 
 
-def skinny_ok(x: torch.Tensor, weight: torch.Tensor, swiglu: bool = False) -> bool:
+def skinny_ok(x: torch.Tensor, weight: torch.Tensor, swiglu: bool = False,
+              min_n: Optional[int] = None) -> bool:
     """Inference-only decode GEMM: <= 16 rows, bf16, K % 256 == 0, N % 16 == 0, no autograd."""
     if not (SKINNY and _ext.use_native(x)) or torch.is_grad_enabled() and (x.requires_grad or weight.requires_grad):
         return False
     rows = x.numel() // x.shape[-1] if x.dim() else 0
     N, K = weight.shape if weight.dim() == 2 else (0, 0)
-    return (1 <= rows <= 16 and N >= SKINNY_MIN_N and x.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16
+    return (1 <= rows <= 16 and N >= (SKINNY_MIN_N if min_n is None else min_n) and x.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16
             and weight.dim() == 2 and weight.stride(1) == 1 and weight.stride(0) % 8 == 0
             and x.shape[-1] == (2 * K if swiglu else K) and K % 256 == 0 and N % 16 == 0
             and (N + 127) // 128 <= 8192 and x.device == weight.device)
 
 
-def skinny_linear(x: torch.Tensor, weight: torch.Tensor, swiglu: bool = False) -> Optional[torch.Tensor]:
+def skinny_linear(x: torch.Tensor, weight: torch.Tensor, swiglu: bool = False,
+                  min_n: Optional[int] = None) -> Optional[torch.Tensor]:
     """y = x @ weight^T (or swiglu(x) @ weight^T) with the decode skinny-GEMM kernel
     (csrc/skinny.hip). Returns None when the shape/state is not eligible (caller falls back)."""
-    if not skinny_ok(x, weight, swiglu):
+    if not skinny_ok(x, weight, swiglu, min_n):
         return None
     cnt = _skinny_counters(x.device)
     if cnt is None:

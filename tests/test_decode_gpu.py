@@ -130,6 +130,7 @@ def test_layer_split_gpu_host_matches_single_gpu():
 
 @pytest.mark.parametrize("M", [1, 3, 8, 16])
 @pytest.mark.parametrize("N,K,swiglu", [(4096, 4096, False), (6144, 4096, False), (1040, 512, False),
+                                         (4096, 14336, False), (16, 2048, False),
                                          (4096, 14336, True), (28672, 4096, False), (2048, 768, True)])
 def test_skinny_gemm_matches_fp32(M, N, K, swiglu):
     """Decode skinny GEMM (csrc/skinny.hip) vs an fp32 PyTorch reference, split-K and not, with
@@ -140,12 +141,12 @@ def test_skinny_gemm_matches_fp32(M, N, K, swiglu):
     x = torch.randn(M, 2 * K if swiglu else K, device=DEV, generator=g).to(torch.bfloat16)
     w = (torch.randn(N, K, device=DEV, generator=g) * K ** -0.5).to(torch.bfloat16)
     with torch.no_grad():
-        y = decode.skinny_linear(x, w, swiglu=swiglu)
+        y = decode.skinny_linear(x, w, swiglu=swiglu, min_n=0)
         assert y is not None and y.shape == (M, N)
         r = decode.ref_skinny_linear(x, w, swiglu)
         err = (y.float() - r.float()).abs().max().item()
         assert err <= 2e-2 * max(1.0, r.float().abs().max().item()), err
-        y2 = decode.skinny_linear(x, w, swiglu=swiglu)  # counters re-armed, same bits
+        y2 = decode.skinny_linear(x, w, swiglu=swiglu, min_n=0)  # counters re-armed, same bits
         assert torch.equal(y, y2)
 
 
@@ -157,11 +158,12 @@ def test_skinny_gemm_strided_rows_and_eligibility():
     x = big[..., 1024:2048]                                     # [4, 1, 1024] row stride 3072
     w = torch.randn(512, 1024, device=DEV, generator=g).to(torch.bfloat16)
     with torch.no_grad():
-        y = decode.skinny_linear(x, w)
+        y = decode.skinny_linear(x, w, min_n=0)
         assert y.shape == (4, 1, 512)
         assert torch.allclose(y.float(), decode.ref_skinny_linear(x, w).float(), atol=0.25, rtol=2e-2)
-        assert decode.skinny_linear(torch.zeros(17, 1024, device=DEV, dtype=torch.bfloat16), w) is None
+        assert decode.skinny_linear(torch.zeros(17, 1024, device=DEV, dtype=torch.bfloat16), w, min_n=0) is None
         assert decode.skinny_linear(torch.zeros(2, 1000, device=DEV, dtype=torch.bfloat16),
-                                    torch.zeros(512, 1000, device=DEV, dtype=torch.bfloat16)) is None
+                                    torch.zeros(512, 1000, device=DEV, dtype=torch.bfloat16), min_n=0) is None
+        assert decode.skinny_linear(x, w, min_n=1 << 20) is None  # width threshold respected
     xg = x.detach().clone().requires_grad_(True)
-    assert decode.skinny_linear(xg, w) is None  # autograd: library GEMM path
+    assert decode.skinny_linear(xg, w, min_n=0) is None  # autograd: library GEMM path

@@ -50,7 +50,7 @@ def main():
                 lib = lambda: F.linear(decode._ext.require().swiglu_fwd(x), w)
             else:
                 lib = lambda: F.linear(x, w)
-            sk = lambda: decode.skinny_linear(x, w, swiglu=sw)
+            sk = lambda: decode.skinny_linear(x, w, swiglu=sw, min_n=0)
             t_lib, t_sk = timeit(lib, a.iters), timeit(sk, a.iters)
         gb = N * K * 2 / 1e9
         print(json.dumps({"gemm": name, "rows": a.rows, "N": N, "K": K, "library_us": round(t_lib, 1),
