@@ -71,6 +71,10 @@ SKINNY = os.environ.get("DLA_SKINNY", "1") != "0"
 # the width threshold for A/B runs.
 SKINNY_MIN_N = int(os.environ.get("DLA_SKINNY_MIN_N", "0"))
 SKINNY_WIDE_N = 128 * 128  # >= this many output columns: the kernel runs without any split-K
+# measured in a decode step (profiles/r1_decode_skinny.md): hipBLASLt stays ahead for the LM head
+# (N = 128256) and for the long-K narrow down projection (K = 14336), so those keep the library
+SKINNY_MAX_N = int(os.environ.get("DLA_SKINNY_MAX_N", "65536"))
+SKINNY_MAX_NARROW_K = int(os.environ.get("DLA_SKINNY_MAX_NARROW_K", "8192"))
 _COUNTERS = {}
 
 
@@ -94,6 +98,8 @@ def skinny_ok(x: torch.Tensor, weight: torch.Tensor, swiglu: bool = False,
         return False
     rows = x.numel() // x.shape[-1] if x.dim() else 0
     N, K = weight.shape if weight.dim() == 2 else (0, 0)
+    if min_n is None and (N > SKINNY_MAX_N or (N < SKINNY_WIDE_N and K > SKINNY_MAX_NARROW_K)):
+        return False
     return (1 <= rows <= 16 and N >= (SKINNY_MIN_N if min_n is None else min_n) and x.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16
             and weight.dim() == 2 and weight.stride(1) == 1 and weight.stride(0) % 8 == 0
             and x.shape[-1] == (2 * K if swiglu else K) and K % 256 == 0 and N % 16 == 0
