@@ -25,13 +25,14 @@ bool skinny_use_ksplit(int N, int K);
 void launch_skinny_ksplit(const bf16_t*, int64_t, const bf16_t*, int64_t, bf16_t*, int64_t, int,
                           int, int, hipStream_t);
 void launch_skinny_gemm(const bf16_t*, int64_t, const bf16_t*, int64_t, bf16_t*, int64_t, float*,
-                        unsigned*, int, int, int, int, bool, hipStream_t);
+                        unsigned*, int, int, int, int, bool, bool, hipStream_t);
 
 // y[M, N] = x[M, K] @ w[N, K]^T for M <= 16 (decode). With `swiglu`, x is the fused gate|up
 // output gu[M, 2K] and the kernel applies silu(g) * u while staging it. `counters` (int32,
 // zero-initialised once, re-armed by the kernel) holds one split-K arrival counter per 128
 // output columns.
-at::Tensor skinny_gemm(const at::Tensor& x, const at::Tensor& w, at::Tensor& counters, bool swiglu) {
+at::Tensor skinny_gemm(const at::Tensor& x, const at::Tensor& w, at::Tensor& counters, bool swiglu,
+                       bool glu_out) {
   check_bf16(x, "x");
   check_bf16(w, "w");
   check_i32(counters, "counters");
@@ -50,6 +51,15 @@ at::Tensor skinny_gemm(const at::Tensor& x, const at::Tensor& w, at::Tensor& cou
   const int64_t nb = (N + 127) / 128;
   TORCH_CHECK(counters.is_contiguous() && counters.numel() >= nb, "counters: one per 128 columns");
   c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  if (glu_out) {  // w = [gate; up] (2F rows) -> silu(x gate^T) * (x up^T) [M, F]
+    TORCH_CHECK(!swiglu && N % 128 == 0, "glu_out: 2F rows with F % 64 == 0, no swiglu input");
+    TORCH_CHECK(M * (K + 8) * 2 <= 152 * 1024, "skinny GEMM: x exceeds LDS");
+    auto m = at::empty({M, N / 2}, x.options());
+    launch_skinny_gemm(cbp(x), x.stride(0), cbp(w), w.stride(0), bp(m), m.stride(0), nullptr,
+                       reinterpret_cast<unsigned*>(counters.data_ptr<int>()), (int)M, (int)N,
+                       (int)K, 1, false, true, cur_stream(x));
+    return m;
+  }
   auto y = at::empty({M, N}, x.options());
   if (!swiglu && skinny_use_ksplit((int)N, (int)K)) {  // narrow N: in-workgroup split-K
     launch_skinny_ksplit(cbp(x), x.stride(0), cbp(w), w.stride(0), bp(y), y.stride(0), (int)M,
@@ -63,7 +73,7 @@ at::Tensor skinny_gemm(const at::Tensor& x, const at::Tensor& w, at::Tensor& cou
   launch_skinny_gemm(cbp(x), x.stride(0), cbp(w), w.stride(0), bp(y), y.stride(0),
                      S > 1 ? ws.data_ptr<float>() : nullptr,
                      reinterpret_cast<unsigned*>(counters.data_ptr<int>()), (int)M, (int)N, (int)K,
-                     S, swiglu, cur_stream(x));
+                     S, swiglu, false, cur_stream(x));
   return y;
 }
 
@@ -175,7 +185,7 @@ TORCH_LIBRARY_FRAGMENT(dla, m) {
   m.def("decode_attn(Tensor q, Tensor k_cache, Tensor v_cache, Tensor kv_len, Tensor? kv_start, int window, float scale) -> Tensor");
   m.def("rope_cache_write(Tensor qkv, Tensor cos, Tensor sin, Tensor pos, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor slot, int Hq, int Hkv, int D, int rot) -> Tensor");
   m.def("sample_tokens(Tensor logits, float temperature, int top_k, float top_p, bool greedy, Tensor rng) -> Tensor");
-  m.def("skinny_gemm(Tensor x, Tensor w, Tensor(a!) counters, bool swiglu) -> Tensor");
+  m.def("skinny_gemm(Tensor x, Tensor w, Tensor(a!) counters, bool swiglu, bool glu_out=False) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(dla, CUDA, m) {

@@ -42,7 +42,12 @@ __device__ __forceinline__ float silu_sk(float g) { return g * sigmoidf_(g); }
 
 // grid: (ceil(N / 128), S), 8 waves. LDS: M x (kc + 8) bf16 (row pad of 16 B keeps the 16-row fragment
 // reads on distinct banks).
-template <bool SWIGLU>
+// GLU_OUT (decode gate|up projection): W is [gate; up] (2F rows) and the output is
+// m = silu(gate) * up [M, F]. Block b's waves 0-3 take gate rows [64b, 64b + 64), waves 4-7 the
+// matching up rows F + [64b, 64b + 64); the tile is exchanged through LDS and SwiGLU applied in
+// the epilogue (after the same bf16 rounding of gate/up as the unfused path): no gu round trip,
+// no separate swiglu launch.
+template <bool SWIGLU, bool GLU_OUT = false>
 __global__ __launch_bounds__(64 * kSkWaves) void skinny_gemm_kernel(
     const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ W, int64_t ldw,
     bf16_t* __restrict__ y, int64_t ldy, float* __restrict__ ws, unsigned* __restrict__ counters,
@@ -55,7 +60,9 @@ __global__ __launch_bounds__(64 * kSkWaves) void skinny_gemm_kernel(
   const int ldl = kc + 8;
 
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int n0 = blockIdx.x * kSkCols + wave * 16;
+  const int F = N >> 1;
+  const int n0 = GLU_OUT ? (wave < 4 ? 0 : F) + blockIdx.x * 64 + (wave & 3) * 16
+                         : blockIdx.x * kSkCols + wave * 16;
   const int r = lane & 15, q = lane >> 4;  // fragment row (m for A, n for B), k quarter
   const bool active = n0 < N;
   const bf16_t* wrow = W + static_cast<int64_t>(active ? n0 + r : 0) * ldw + k0 + q * 8;
@@ -151,6 +158,18 @@ __global__ __launch_bounds__(64 * kSkWaves) void skinny_gemm_kernel(
 
   // ---- epilogue. Lane holds C[m = 4q + i][n = n0 + r], i = 0..3.
   const int n = n0 + r;
+  if constexpr (GLU_OUT) {
+    __shared__ float glu[2][16][64];  // [gate|up][m][column within the block]
+    const int half = wave >> 2, col = (wave & 3) * 16 + r;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) glu[half][4 * q + i][col] = bf2f(f2bf(acc[i]));
+    __syncthreads();
+    for (int i = threadIdx.x; i < M * 64; i += blockDim.x) {
+      const int m = i >> 6, c = i & 63, nn = blockIdx.x * 64 + c;
+      if (nn < F) y[m * ldy + nn] = f2bf(silu_sk(glu[0][m][c]) * glu[1][m][c]);
+    }
+    return;
+  }
   if (S == 1) {
     if (n < N) {
 #pragma unroll
@@ -228,7 +247,7 @@ size_t skinny_lds_bytes(int M, int kc) { return static_cast<size_t>(M) * (kc + 8
 
 void launch_skinny_gemm(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
                         int64_t ldy, float* ws, unsigned* counters, int M, int N, int K, int S,
-                        bool swiglu, hipStream_t st) {
+                        bool swiglu, bool glu_out, hipStream_t st) {
   const int kc = K / S;
   dim3 grid((N + kSkCols - 1) / kSkCols, S);
   const size_t lds = skinny_lds_bytes(M, kc);
@@ -237,9 +256,19 @@ void launch_skinny_gemm(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t l
                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_gemm_kernel<true>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    // the GLU variant also holds an 8 KB static exchange tile: dynamic + static <= 160 KB
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_gemm_kernel<false, true>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 152 * 1024);
+    (void)hipGetLastError();  // never leave a sticky error for the caller's next launch check
     return true;
   }();
   (void)attr_set;
+  if (glu_out) {  // N = 2F weight rows -> F outputs, 64 per block, never split
+    dim3 g2(N / 2 / 64, 1);
+    skinny_gemm_kernel<false, true><<<g2, 64 * kSkWaves, skinny_lds_bytes(M, K), st>>>(
+        x, ldx, W, ldw, y, ldy, ws, counters, M, N, K, K);
+    return;
+  }
   if (swiglu)
     skinny_gemm_kernel<true><<<grid, 64 * kSkWaves, lds, st>>>(x, ldx, W, ldw, y, ldy, ws,
                                                                 counters, M, N, K, kc);

@@ -131,6 +131,9 @@ class MLP(nn.Module):
         if (self.cfg.activation == "swiglu" and self.up_bias is None and self.down_bias is None
                 and self.tp is None and ops.decode.skinny_ok(h, self.up_proj)):
             # decode (<= 16 rows, no autograd): skinny GEMMs, SwiGLU fused into the down GEMM
+            m = ops.decode.skinny_glu(h, self.up_proj)  # gate|up GEMM with SwiGLU epilogue
+            if m is not None:
+                return _lin(m, self.down_proj, None)
             u = ops.decode.skinny_linear(h, self.up_proj)
             if u is not None:
                 # SwiGLU fused into the down GEMM only where that GEMM needs no split-K combine

@@ -122,6 +122,22 @@ def skinny_linear(x: torch.Tensor, weight: torch.Tensor, swiglu: bool = False,
     return y.view(*x.shape[:-1], weight.shape[0])
 
 
+def skinny_glu(x: torch.Tensor, weight: torch.Tensor) -> Optional[torch.Tensor]:
+    """Decode gate|up projection with SwiGLU in the epilogue: weight = [gate; up] (2F rows) ->
+    silu(x gate^T) * (x up^T) [.., F] in one kernel (csrc/skinny.hip GLU_OUT). None if the
+    shape/state is not eligible (the caller runs GEMM + swiglu)."""
+    if not skinny_ok(x, weight) or weight.shape[0] % 128 or x.shape[-1] * min(x.numel() // x.shape[-1], 16) > 80 * 1024:
+        return None
+    cnt = _skinny_counters(x.device)
+    if cnt is None:
+        return None
+    x2 = x.reshape(-1, x.shape[-1])
+    if x2.stride(-1) != 1 or x2.stride(0) % 8 or x2.data_ptr() % 16:
+        x2 = x2.contiguous()
+    m = _ext.require().skinny_gemm(x2, weight, cnt, False, True)
+    return m.view(*x.shape[:-1], weight.shape[0] // 2)
+
+
 def ref_skinny_linear(x: torch.Tensor, weight: torch.Tensor, swiglu: bool = False) -> torch.Tensor:
     if swiglu:
         g, u = x.float().chunk(2, dim=-1)

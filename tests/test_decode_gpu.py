@@ -167,3 +167,22 @@ def test_skinny_gemm_strided_rows_and_eligibility():
         assert decode.skinny_linear(x, w, min_n=1 << 20) is None  # width threshold respected
     xg = x.detach().clone().requires_grad_(True)
     assert decode.skinny_linear(xg, w, min_n=0) is None  # autograd: library GEMM path
+
+
+@pytest.mark.parametrize("M", [1, 8, 16])
+@pytest.mark.parametrize("F,K", [(14336, 4096), (192, 512)])
+def test_skinny_glu_epilogue_matches_unfused(M, F, K):
+    """gate|up skinny GEMM with the SwiGLU epilogue == swiglu(bf16 GEMM output), fp32 reference."""
+    from distributed_llm_alignment_amd.ops import decode
+
+    g = torch.Generator(device=DEV).manual_seed(M + F)
+    x = torch.randn(M, K, device=DEV, generator=g).to(torch.bfloat16)
+    w = (torch.randn(2 * F, K, device=DEV, generator=g) * K ** -0.5).to(torch.bfloat16)
+    with torch.no_grad():
+        m = decode.skinny_glu(x, w)
+        assert m is not None and m.shape == (M, F)
+        u = (x.float() @ w.float().t()).to(torch.bfloat16)
+        gg, uu = u.float().chunk(2, dim=-1)
+        r = (torch.nn.functional.silu(gg) * uu)
+        err = (m.float() - r).abs().max().item()
+        assert err <= 3e-2 * max(1.0, r.abs().max().item()), err

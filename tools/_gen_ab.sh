@@ -2,4 +2,5 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
-for v in "65536 8192" "999999999 999999" "65536 8192" "999999999 999999"; do set -- $v; echo "max_n=$1 max_narrow_k=$2"; DLA_SKINNY_MAX_N=$1 DLA_SKINNY_MAX_NARROW_K=$2 timeout -k 10 200 python -u tools/bench_generate.py --modes graph,eager --new 128 2>/dev/null | grep mode || exit 1; done
+timeout -k 10 300 python -u -m pytest tests/test_decode_gpu.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider 2>&1 | tail -2 || exit 1
+for i in 1 2; do timeout -k 10 200 python -u tools/bench_generate.py --modes graph,eager --new 128 2>/dev/null | grep mode || exit 1; done
