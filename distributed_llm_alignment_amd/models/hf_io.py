@@ -140,9 +140,38 @@ def to_hf_state_dict(model, base: bool = False) -> Dict[str, torch.Tensor]:
 
 
 @torch.no_grad()
+def _unfuse_moe_experts(sd: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+    """Newer transformers keep Mixtral experts fused in memory (`mlp.gate.weight`,
+    `mlp.experts.gate_up_proj` [E, 2F, H] = [w1; w3], `mlp.experts.down_proj` [E, H, F] = w2);
+    checkpoints on disk use the per-expert `block_sparse_moe.experts.{e}.w1/w3/w2` names the key
+    map speaks. Rewrite the fused form into the per-expert one."""
+    if not any(k.endswith("mlp.experts.gate_up_proj") for k in sd):
+        return sd
+    out = {}
+    for k, v in sd.items():
+        if k.endswith("mlp.experts.gate_up_proj"):
+            pre = k[: -len("mlp.experts.gate_up_proj")] + "block_sparse_moe.experts."
+            F = v.shape[1] // 2
+            for e in range(v.shape[0]):
+                out[f"{pre}{e}.w1.weight"] = v[e, :F]
+                out[f"{pre}{e}.w3.weight"] = v[e, F:]
+        elif k.endswith("mlp.experts.down_proj"):
+            pre = k[: -len("mlp.experts.down_proj")] + "block_sparse_moe.experts."
+            for e in range(v.shape[0]):
+                out[f"{pre}{e}.w2.weight"] = v[e]
+        elif k.endswith("mlp.gate.weight") and ".layers." in k:
+            out[k[: -len("mlp.gate.weight")] + "block_sparse_moe.gate.weight"] = v
+        else:
+            out[k] = v
+    return out
+
+
 def load_hf_state_dict(model, sd: Dict[str, torch.Tensor], strict: bool = True, base: bool = False):
-    """Copy HF tensors into the fused native parameters. Accepts `module.` prefixes (DDP)."""
+    """Copy HF tensors into the fused native parameters. Accepts `module.` prefixes (DDP) and the
+    fused in-memory Mixtral expert layout of newer transformers."""
     sd = {(k[len("module."):] if k.startswith("module.") else k): v for k, v in sd.items()}
+    if model.cfg.is_moe:
+        sd = _unfuse_moe_experts(sd)
     params = dict(model.named_parameters())
     used = set()
     missing = []

@@ -59,6 +59,32 @@ def test_transformers_llama_parity_if_available():
     assert torch.allclose(a, b, atol=2e-4), (a - b).abs().max()
 
 
+@pytest.mark.parametrize("name", ["tiny-llama", "tiny-mistral", "tiny-mixtral", "tiny-gpt2", "tiny-phi"])
+def test_transformers_parity_all_families_with_padding(name):
+    """Logits parity with the installed transformers model of every family (random tiny config,
+    eager attention, a right-padded row): Llama, Mistral (sliding window), Mixtral (top-2 MoE,
+    fused or per-expert HF key layout), GPT-2, Phi-2."""
+    transformers = pytest.importorskip("transformers")
+    cfg = get_config(name)
+    d = cfg.to_hf()
+    hc = transformers.AutoConfig.for_model(d["model_type"], **{k: v for k, v in d.items() if k not in
+                                                               ("architectures", "torch_dtype", "model_type")})
+    hc._attn_implementation = "eager"
+    torch.manual_seed(0)
+    hf = transformers.AutoModelForCausalLM.from_config(hc).eval()
+    mine = build_model(cfg, device="cpu", seed=1).eval()
+    missing, unexpected = mine.load_hf_state_dict(hf.state_dict(), strict=False)
+    assert not missing and not unexpected, (missing, unexpected)
+    ids = torch.randint(3, cfg.vocab_size, (2, 24))
+    am = torch.ones_like(ids)
+    am[1, 18:] = 0
+    with torch.no_grad():
+        a = hf(ids, attention_mask=am).logits
+        b = mine.logits(mine(ids, am))
+    m = am.bool()
+    assert torch.allclose(a[m], b[m], atol=2e-4), (a - b)[m].abs().max()
+
+
 def test_padding_invariance_left_and_right():
     cfg = get_config("tiny-llama")
     m = build_model(cfg, device="cpu", seed=0).eval()
