@@ -268,3 +268,30 @@ def test_packed_dataset_rows():
         assert row["segment_ids"].max().item() == len(ds.rows[r])
     b = ds.collate([ds[0], ds[len(ds) - 1]])
     assert set(b) == {"input_ids", "attention_mask", "labels", "segment_ids"}
+
+
+def test_greedy_generation_matches_transformers_generate():
+    """Left-padded greedy decoding (KV cache path) == HF `generate(do_sample=False)` — the call
+    the reference's RLHF / teacher-generation loops make (train_rlhf.py:115-121)."""
+    transformers = pytest.importorskip("transformers")
+    from distributed_llm_alignment_amd.models import generate
+
+    cfg = get_config("tiny-llama")
+    d = cfg.to_hf()
+    hc = transformers.AutoConfig.for_model(d["model_type"], **{k: v for k, v in d.items() if k not in
+                                                               ("architectures", "torch_dtype", "model_type")})
+    hc._attn_implementation = "eager"
+    torch.manual_seed(0)
+    hf = transformers.AutoModelForCausalLM.from_config(hc).eval()
+    mine = build_model(cfg, device="cpu", seed=1).eval()
+    mine.load_hf_state_dict(hf.state_dict(), strict=False)
+    g = torch.Generator().manual_seed(4)
+    ids = torch.randint(3, cfg.vocab_size, (2, 12), generator=g)
+    am = torch.ones_like(ids)
+    ids[1, :4] = 0
+    am[1, :4] = 0  # left padding, as the reference's generation pads
+    ours = generate(mine, ids, am, max_new_tokens=10, do_sample=False, eos_token_id=-1, pad_token_id=0)
+    with torch.no_grad():
+        theirs = hf.generate(ids, attention_mask=am, max_new_tokens=10, do_sample=False,
+                             eos_token_id=None, pad_token_id=0)
+    assert torch.equal(ours, theirs), (ours, theirs)
