@@ -19,6 +19,10 @@ void launch_rope_cache(const bf16_t*, int64_t, bf16_t*, bf16_t*, bf16_t*, int64_
                        int, int, int, hipStream_t);
 void launch_sample(const void*, bool, int64_t, int64_t, int, float, int, float, bool,
                    const int64_t*, int64_t*, hipStream_t);
+int sample_split_chunks(const void*, int64_t, int64_t, int, float, int, float, bool);
+size_t sample_workspace_bytes(int64_t, int);
+void launch_sample_split(const void*, bool, int64_t, int64_t, int, int, float, int, float,
+                         const int64_t*, int64_t*, void*, hipStream_t);
 
 int skinny_splits(int M, int N, int K);
 bool skinny_use_ksplit(int N, int K);
@@ -173,9 +177,19 @@ at::Tensor sample_tokens(const at::Tensor& logits, double temperature, int64_t t
   c10::hip::HIPGuardMasqueradingAsCUDA g(logits.device());
   auto out = at::empty({B}, logits.options().dtype(at::kLong));
   const float inv_t = temperature > 0.0 ? static_cast<float>(1.0 / temperature) : 0.f;
-  launch_sample(logits.data_ptr(), logits.scalar_type() == at::kBFloat16, logits.stride(0), B,
-                (int)V, inv_t, (int)top_k, static_cast<float>(top_p), greedy,
-                rng.data_ptr<int64_t>(), out.data_ptr<int64_t>(), cur_stream(logits));
+  const bool is_bf16 = logits.scalar_type() == at::kBFloat16;
+  const int G = sample_split_chunks(logits.data_ptr(), logits.stride(0), B, (int)V, inv_t,
+                                    (int)top_k, static_cast<float>(top_p), greedy);
+  if (G > 0) {  // top-k / top-p on a large vocabulary: row-split multi-launch sampler
+    auto ws = at::empty({(int64_t)sample_workspace_bytes(B, G)}, logits.options().dtype(at::kByte));
+    launch_sample_split(logits.data_ptr(), is_bf16, logits.stride(0), B, (int)V, G, inv_t,
+                        (int)top_k, static_cast<float>(top_p), rng.data_ptr<int64_t>(),
+                        out.data_ptr<int64_t>(), ws.data_ptr(), cur_stream(logits));
+    return out;
+  }
+  launch_sample(logits.data_ptr(), is_bf16, logits.stride(0), B, (int)V, inv_t, (int)top_k,
+                static_cast<float>(top_p), greedy, rng.data_ptr<int64_t>(),
+                out.data_ptr<int64_t>(), cur_stream(logits));
   return out;
 }
 

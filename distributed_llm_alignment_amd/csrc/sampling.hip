@@ -310,6 +310,420 @@ __global__ __launch_bounds__(kSampNT) void sample_kernel(const T* __restrict__ l
   if (tid == 0) out[r] = ans >= 0 ? ans : argmax;  // u on a rounding gap at the top: argmax
 }
 
+// ---------------------------------------------------------------------------------------------
+// Row-split sampler (plain / top-k / top-p draws) for large vocabularies. The single-block kernel above keeps
+// 8 of 256 CUs busy at B = 8 and spends ~90 us per histogram pass. Here every row is cut into G
+// chunks (G = 32 for V = 128256 -> B * 32 workgroups) and each pass is a separate launch:
+//   max     (B x G)  chunk max / argmax -> partials
+//   hist    (B x G)  chunk histogram in LDS over the pass's [lo, lo + w), z >= floor; occupied
+//                    bins added to the row histogram with global integer atomics (masses in
+//                    2^-40 fixed point, so the sums do not depend on workgroup order)
+//   resolve (B)      read + re-zero the row histogram, suffix scan, the same bin searches as
+//                    sample_kernel; writes the next pass's window / tau
+//   mass    (B x G)  kept mass of each chunk (z >= tau)
+//   pick    (B)      u ~ U(0, total) with the same Philox stream, chunk by prefix, token by a
+//                    block scan inside the chunk
+// Launch count is fixed by (top_k > 0, top_p < 1), so the sequence is hipGraph-capturable; rows
+// whose thresholds settle early skip the remaining passes on the device.
+constexpr int kSplitNT = 256;
+constexpr int kSplitG = 32;  // chunks per row (compile-time: the merge loops fully unroll)
+
+struct SplitState {  // per row, lives in the workspace between launches
+  float tau, lo, w, floor_z, above_m, target;
+  int phase, above_c;
+};
+enum : int { kDone = 0, kKCoarse = 1, kKFine = 2, kPCoarse = 3, kPFine = 4 };
+
+struct SplitWs {
+  float* pmax;        // [B, G]
+  int* parg;          // [B, G]
+  int* hc;                 // [B, kBins] row histogram counts (global atomics)
+  unsigned long long* hm;  // [B, kBins] row histogram masses, 2^-40 fixed point
+  SplitState* state;  // [B]
+  float* cmass;       // [B, G]
+};
+
+constexpr double kFix = 1099511627776.0;  // 2^40: integer mass sums are order-independent
+
+__host__ __device__ inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+__host__ __device__ inline SplitWs split_ws(void* base, int64_t B, int G) {
+  char* p = static_cast<char*>(base);
+  SplitWs w;
+  const size_t bg = size_t(B) * G;
+  w.pmax = reinterpret_cast<float*>(p); p += align256(bg * 4);
+  w.parg = reinterpret_cast<int*>(p); p += align256(bg * 4);
+  w.hc = reinterpret_cast<int*>(p); p += align256(size_t(B) * kBins * 4);
+  w.hm = reinterpret_cast<unsigned long long*>(p); p += align256(size_t(B) * kBins * 8);
+  w.state = reinterpret_cast<SplitState*>(p); p += align256(size_t(B) * sizeof(SplitState));
+  w.cmass = reinterpret_cast<float*>(p); p += align256(bg * 4);
+  return w;
+}
+inline size_t split_ws_bytes(int64_t B, int G) {
+  const size_t bg = size_t(B) * G;
+  return align256(bg * 4) * 3 + align256(size_t(B) * kBins * 4) + align256(size_t(B) * kBins * 8) +
+         align256(size_t(B) * sizeof(SplitState));
+}
+
+// chunk g of a row, in 8-element vectors: [v0, v1)
+__device__ __forceinline__ void chunk_range(int V, int G, int g, int& v0, int& v1) {
+  const int nv = V / 8, cv = (nv + G - 1) / G;
+  v0 = min(nv, g * cv);
+  v1 = min(nv, v0 + cv);
+}
+
+// row max (first index on ties) from the G chunk partials; every lane gets the result
+__device__ __forceinline__ void row_max(const float* pmax, const int* parg, int G, float& gmax,
+                                        int& argmax) {
+  float m[kSplitG];
+  int a[kSplitG];
+#pragma unroll
+  for (int g = 0; g < kSplitG; ++g) {  // all loads in flight before the compare chain
+    m[g] = pmax[g];
+    a[g] = parg[g];
+  }
+  gmax = -INFINITY;
+  argmax = 0x7fffffff;
+#pragma unroll
+  for (int g = 0; g < kSplitG; ++g)  // chunks are in index order: strict > keeps the first index
+    if (m[g] > gmax) {
+      gmax = m[g];
+      argmax = a[g];
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kSplitNT) void split_max_kernel(const T* __restrict__ logits,
+                                                             int64_t ld_, int V, int G, SplitWs ws) {
+  __shared__ float sm[kSplitNT / 64];
+  __shared__ int sa[kSplitNT / 64];
+  const int r = blockIdx.y, g = blockIdx.x, tid = threadIdx.x;
+  for (int i = g * (kBins / kSplitG) + tid; i < (g + 1) * (kBins / kSplitG); i += kSplitNT) {
+    ws.hc[int64_t(r) * kBins + i] = 0;  // the first histogram pass accumulates into zeros
+    ws.hm[int64_t(r) * kBins + i] = 0ull;
+  }
+  const T* row = logits + int64_t(r) * ld_;
+  int v0, v1;
+  chunk_range(V, G, g, v0, v1);
+  float m = -INFINITY;
+  int am = 0x7fffffff;
+  for (int i = v0 + tid; i < v1; i += kSplitNT) {
+    float x[8];
+    ld8(row, i, x);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (x[j] > m) {
+        m = x[j];
+        am = i * 8 + j;
+      }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(m, o, 64);
+    const int oa = __shfl_xor(am, o, 64);
+    if (om > m || (om == m && oa < am)) {
+      m = om;
+      am = oa;
+    }
+  }
+  if ((tid & 63) == 0) {
+    sm[tid >> 6] = m;
+    sa[tid >> 6] = am;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < kSplitNT / 64; ++w)
+      if (sm[w] > m || (sm[w] == m && sa[w] < am)) {
+        m = sm[w];
+        am = sa[w];
+      }
+    ws.pmax[r * G + g] = m;
+    ws.parg[r * G + g] = am;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kSplitNT) void split_hist_kernel(const T* __restrict__ logits,
+                                                              int64_t ld_, int V, int G,
+                                                              float inv_t, bool first, SplitWs ws) {
+  __shared__ int c[kBins];
+  __shared__ float m[kBins];
+  const int r = blockIdx.y, g = blockIdx.x, tid = threadIdx.x;
+  float lo = -kRange, w = kRange, floor_z = -INFINITY;
+  if (!first) {
+    const SplitState s = ws.state[r];
+    if (s.phase == kDone) return;
+    lo = s.lo;
+    w = s.w;
+    floor_z = s.floor_z;
+  }
+  float gmax;
+  int argmax;
+  row_max(ws.pmax + r * G, ws.parg + r * G, G, gmax, argmax);
+  for (int i = tid; i < kBins; i += kSplitNT) {
+    c[i] = 0;
+    m[i] = 0.f;
+  }
+  __syncthreads();
+  const T* row = logits + int64_t(r) * ld_;
+  int v0, v1;
+  chunk_range(V, G, g, v0, v1);
+  const float sc = kBins / w, hi = lo + w;
+  const bool top = hi >= 0.f;
+  for (int i = v0 + tid; i < v1; i += kSplitNT) {
+    float x[8];
+    ld8(row, i, x);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float z = (x[j] - gmax) * inv_t;
+      if (z >= lo && (z < hi || (top && z <= 0.f)) && z >= floor_z) {
+        const int b = min(kBins - 1, (int)((z - lo) * sc));
+        atomicAdd(&c[b], 1);
+        atomicAdd(&m[b], __expf(z));
+      }
+    }
+  }
+  __syncthreads();
+  int* oc = ws.hc + int64_t(r) * kBins;
+  unsigned long long* om = ws.hm + int64_t(r) * kBins;
+  for (int i = tid; i < kBins; i += kSplitNT)
+    if (c[i] > 0) {  // only occupied bins: few atomics for concentrated rows
+      atomicAdd(oc + i, c[i]);
+      atomicAdd(om + i, (unsigned long long)((double)m[i] * kFix));
+    }
+}
+
+__global__ __launch_bounds__(kSampNT) void split_resolve_kernel(int G, int top_k, float top_p,
+                                                                bool need_p, int first_phase,
+                                                                SplitWs ws) {
+  __shared__ int hc[kBins];
+  __shared__ float hm[kBins];
+  __shared__ int tc[kSampNT];
+  __shared__ float tm[kSampNT];
+  __shared__ int sel;
+  const int r = blockIdx.x, tid = threadIdx.x;
+  SplitState s;
+  if (first_phase != kDone) {  // first pass: fresh state
+    s.tau = -kRange;
+    s.lo = -kRange;
+    s.w = kRange;
+    s.floor_z = -INFINITY;
+    s.above_m = 0.f;
+    s.target = 0.f;
+    s.above_c = 0;
+    s.phase = first_phase;
+  } else {
+    s = ws.state[r];
+    if (s.phase == kDone) return;
+  }
+  for (int b = tid; b < kBins; b += kSampNT) {  // read the row histogram, re-zero it for the next pass
+    hc[b] = ws.hc[int64_t(r) * kBins + b];
+    hm[b] = (float)((double)ws.hm[int64_t(r) * kBins + b] * (1.0 / kFix));
+    ws.hc[int64_t(r) * kBins + b] = 0;
+    ws.hm[int64_t(r) * kBins + b] = 0ull;
+  }
+  __syncthreads();
+  suffix_scan(hc, hm, tc, tm);
+  const float W = kRange / kBins;
+  if (s.phase == kKCoarse) {
+    const int kbin = find_bin_count(hc, top_k, &sel);
+    s.above_c = kbin + 1 < kBins ? hc[kbin + 1] : 0;
+    s.above_m = kbin + 1 < kBins ? hm[kbin + 1] : 0.f;
+    s.lo = -kRange + kbin * W;
+    s.w = W;
+    s.floor_z = -INFINITY;
+    s.phase = kKFine;
+  } else if (s.phase == kKFine) {
+    const int sb = find_bin_count(hc, top_k - s.above_c, &sel);
+    s.tau = s.lo + sb * (W / kBins);
+    const float total = s.above_m + hm[sb];
+    s.phase = kDone;
+    if (need_p) {
+      const float target = top_p * total;
+      if (s.above_m < target) {  // nucleus edge inside this same coarse bin
+        const int sp = find_bin_mass(hm, target - s.above_m, &sel);
+        s.tau = fmaxf(s.tau, s.lo + sp * (W / kBins));
+      } else {  // edge in a higher coarse bin: coarse pass again above the top-k floor
+        s.target = target;
+        s.lo = -kRange;
+        s.w = kRange;
+        s.floor_z = s.tau;
+        s.phase = kPCoarse;
+      }
+    }
+  } else if (s.phase == kPCoarse) {
+    if (first_phase == kPCoarse) s.target = top_p * hm[0];  // no top-k: total = whole row
+    const int cb = find_bin_mass(hm, s.target, &sel);
+    s.above_m = cb + 1 < kBins ? hm[cb + 1] : 0.f;
+    s.lo = -kRange + cb * W;
+    s.w = W;
+    s.floor_z = s.tau;
+    s.phase = kPFine;
+  } else {  // kPFine
+    const int sp = find_bin_mass(hm, s.target - s.above_m, &sel);
+    s.tau = fmaxf(s.tau, s.lo + sp * (W / kBins));
+    s.phase = kDone;
+  }
+  __syncthreads();
+  if (tid == 0) ws.state[r] = s;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kSplitNT) void split_mass_kernel(const T* __restrict__ logits,
+                                                              int64_t ld_, int V, int G,
+                                                              float inv_t, bool has_tau,
+                                                              SplitWs ws) {
+  __shared__ float red[kSplitNT / 64];
+  const int r = blockIdx.y, g = blockIdx.x, tid = threadIdx.x;
+  float gmax;
+  int argmax;
+  row_max(ws.pmax + r * G, ws.parg + r * G, G, gmax, argmax);
+  const float tau = has_tau ? ws.state[r].tau : -kRange;
+  const T* row = logits + int64_t(r) * ld_;
+  int v0, v1;
+  chunk_range(V, G, g, v0, v1);
+  float acc = 0.f;
+  for (int i = v0 + tid; i < v1; i += kSplitNT) {
+    float x[8];
+    ld8(row, i, x);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float z = (x[j] - gmax) * inv_t;
+      acc += z >= tau ? __expf(z) : 0.f;
+    }
+  }
+  const float tot = block_sum<kSplitNT>(acc, red);
+  if (tid == 0) ws.cmass[r * G + g] = tot;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kSplitNT) void split_pick_kernel(const T* __restrict__ logits,
+                                                              int64_t ld_, int V, int G,
+                                                              float inv_t, bool has_tau,
+                                                              const int64_t* __restrict__ rng,
+                                                              SplitWs ws,
+                                                              int64_t* __restrict__ out) {
+  __shared__ float tm[kSplitNT];
+  __shared__ int ans;
+  const int r = blockIdx.x, tid = threadIdx.x;
+  float gmax;
+  int argmax;
+  row_max(ws.pmax + r * G, ws.parg + r * G, G, gmax, argmax);
+  const float tau = has_tau ? ws.state[r].tau : -kRange;
+  float cms[kSplitG];
+  float total = 0.f;
+#pragma unroll
+  for (int g = 0; g < kSplitG; ++g) {
+    cms[g] = ws.cmass[r * kSplitG + g];
+    total += cms[g];
+  }
+  const float u = philox_uniform((uint64_t)rng[0], (uint64_t)r, (uint64_t)rng[1]) * total;
+  // chunk holding u (every lane walks the G partials in the same order)
+  int cg = -1;
+  float base = 0.f, acc = 0.f;
+#pragma unroll
+  for (int g = 0; g < kSplitG; ++g) {
+    const float cm = cms[g];
+    if (cm > 0.f) {
+      if (u < acc + cm) {
+        cg = g;
+        base = acc;
+        break;
+      }
+      cg = g;  // u on a rounding gap past the last chunk: fall into the last non-empty one
+      base = acc;
+    }
+    acc += cm;
+  }
+  if (tid == 0) ans = -1;
+  const T* row = logits + int64_t(r) * ld_;
+  float mine = 0.f;
+  int s0 = 0, s1 = 0;
+  if (cg >= 0) {
+    int v0, v1;
+    chunk_range(V, G, cg, v0, v1);
+    const int n = (v1 - v0) * 8, per = (n + kSplitNT - 1) / kSplitNT;
+    s0 = min(n, tid * per) + v0 * 8;
+    s1 = min(n, tid * per + per) + v0 * 8;
+    for (int v = s0; v < s1; ++v) {
+      const float z = (ld(row, v) - gmax) * inv_t;
+      mine += z >= tau ? __expf(z) : 0.f;
+    }
+  }
+  tm[tid] = mine;
+  __syncthreads();
+  for (int o = 1; o < kSplitNT; o <<= 1) {
+    const float add = tid >= o ? tm[tid - o] : 0.f;
+    __syncthreads();
+    tm[tid] += add;
+    __syncthreads();
+  }
+  const float before = base + (tid > 0 ? tm[tid - 1] : 0.f);
+  if (mine > 0.f && u >= before && u < base + tm[tid]) {
+    float a = before;
+    int pick = -1;
+    for (int v = s0; v < s1; ++v) {
+      const float z = (ld(row, v) - gmax) * inv_t;
+      if (z >= tau) {
+        a += __expf(z);
+        pick = v;
+        if (u < a) break;
+      }
+    }
+    ans = pick;
+  }
+  __syncthreads();
+  if (tid == 0) out[r] = ans >= 0 ? ans : argmax;  // u on a rounding gap: argmax
+}
+
+static bool split_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("DLA_SAMPLER_SPLIT");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// chunks per row for the split sampler, 0 = use the single-block kernel
+int sample_split_chunks(const void* logits, int64_t ld_, int64_t rows, int V, float inv_temp,
+                        int top_k, float top_p, bool greedy) {
+  const bool vec = V % 8 == 0 && ld_ % 8 == 0 && reinterpret_cast<uintptr_t>(logits) % 16 == 0;
+  if (!split_enabled() || !vec || greedy || inv_temp <= 0.f || V < 32768 || rows > 65535)
+    return 0;
+  return kSplitG;
+}
+size_t sample_workspace_bytes(int64_t rows, int G) { return G > 0 ? split_ws_bytes(rows, G) : 0; }
+
+template <typename T>
+static void launch_split(const T* lg, int64_t ld_, int64_t rows, int V, int G, float inv_t,
+                         int top_k, float top_p, const int64_t* rng, int64_t* out, void* wsp,
+                         hipStream_t st) {
+  const SplitWs ws = split_ws(wsp, rows, G);
+  const dim3 grid(G, rows);
+  const bool need_k = top_k > 0 && top_k < V, need_p = top_p < 1.f;
+  split_max_kernel<T><<<grid, kSplitNT, 0, st>>>(lg, ld_, V, G, ws);
+  const int passes = (need_k ? 2 : 0) + (need_p ? 2 : 0);
+  for (int p = 0; p < passes; ++p) {
+    split_hist_kernel<T><<<grid, kSplitNT, 0, st>>>(lg, ld_, V, G, inv_t, p == 0, ws);
+    const int first_phase = p == 0 ? (need_k ? kKCoarse : kPCoarse) : kDone;
+    split_resolve_kernel<<<rows, kSampNT, 0, st>>>(G, top_k, top_p, need_p, first_phase, ws);
+  }
+  split_mass_kernel<T><<<grid, kSplitNT, 0, st>>>(lg, ld_, V, G, inv_t, passes > 0, ws);
+  split_pick_kernel<T><<<rows, kSplitNT, 0, st>>>(lg, ld_, V, G, inv_t, passes > 0, rng, ws, out);
+}
+
+void launch_sample_split(const void* logits, bool is_bf16, int64_t ld_, int64_t rows, int V,
+                         int G, float inv_temp, int top_k, float top_p, const int64_t* rng,
+                         int64_t* out, void* ws, hipStream_t st) {
+  if (rows == 0) return;
+  if (is_bf16)
+    launch_split(static_cast<const bf16_t*>(logits), ld_, rows, V, G, inv_temp, top_k, top_p, rng,
+                 out, ws, st);
+  else
+    launch_split(static_cast<const float*>(logits), ld_, rows, V, G, inv_temp, top_k, top_p, rng,
+                 out, ws, st);
+}
+
 void launch_sample(const void* logits, bool is_bf16, int64_t ld_, int64_t rows, int V,
                    float inv_temp, int top_k, float top_p, bool greedy, const int64_t* rng,
                    int64_t* out, hipStream_t st) {

@@ -81,6 +81,64 @@ def test_sampler_distribution(top_k, top_p):
     assert torch.allclose(freq, p, atol=0.015), (freq, p)
 
 
+@pytest.mark.parametrize("top_k,top_p", [(0, 1.0), (0, 0.8), (3, 1.0), (4, 0.7), (6, 0.5)])
+def test_split_sampler_distribution_large_vocab(top_k, top_p):
+    """Row-split sampler (V >= 32768 with top-k / top-p): 8 planted logits spread over
+    different chunks of a 128256 vocabulary, the rest far below the -64 z window."""
+    from distributed_llm_alignment_amd.ops import decode
+
+    V, rows, T = 128256, 12000, 0.9
+    base = torch.tensor([2.0, 1.5, 1.0, 0.5, 0.0, -0.5, -1.0, -3.0], device=DEV)
+    pos = torch.tensor([5, 17000, 33333, 50008, 70001, 90000, 110007, 128255], device=DEV)
+    logits = torch.full((rows, V), -100.0, device=DEV, dtype=torch.bfloat16)
+    logits[:, pos] = base.to(torch.bfloat16)
+    rng = torch.tensor([7, 11], dtype=torch.long, device=DEV)
+    tok = decode.sample_tokens(logits, T, top_k, top_p, False, rng)
+    assert bool(torch.isin(tok, pos).all())
+    freq = (tok.unsqueeze(1) == pos.unsqueeze(0)).float().mean(0)
+    z = base / T
+    if top_k:
+        z = torch.where(z >= torch.topk(z, top_k).values[-1], z, torch.tensor(float("-inf"), device=DEV))
+    p = torch.softmax(z, 0)
+    if top_p < 1.0:
+        sp, si = torch.sort(p, descending=True)
+        keep = (sp.cumsum(0) - sp) < top_p
+        p2 = torch.zeros_like(p)
+        p2[si[keep]] = sp[keep]
+        p = p2 / p2.sum()
+    assert torch.allclose(freq, p, atol=0.02), (freq, p)
+
+
+@pytest.mark.parametrize("top_k,top_p", [(50, 1.0), (0, 0.9), (50, 0.9)])
+def test_split_sampler_support_random_logits(top_k, top_p):
+    """Every draw of the row-split sampler lies inside the top-k set / the nucleus of a
+    plain fp32 reference, on dense random logits (the shape a decode step sees)."""
+    from distributed_llm_alignment_amd.ops import decode
+
+    g = torch.Generator(device=DEV).manual_seed(5)
+    B, V, T = 8, 128256, 0.7
+    logits = (torch.randn(B, V, device=DEV, generator=g) * 3.0).to(torch.bfloat16)
+    z = logits.float() / T
+    sz, _ = torch.sort(z, dim=-1, descending=True)
+    floor = torch.full((B,), -float("inf"), device=DEV)
+    if top_k:  # ties of the k-th value are kept, as in the kernel
+        floor = sz[:, top_k - 1]
+    if top_p < 1.0:
+        pz = torch.softmax(torch.where(sz >= floor[:, None] - 1e-4, sz,
+                                       torch.tensor(float("-inf"), device=DEV)), -1)
+        nucleus = (pz.cumsum(-1) - pz) < top_p + 1e-3
+        edge = torch.where(nucleus, sz, torch.tensor(float("inf"), device=DEV)).min(-1).values
+        floor = torch.maximum(floor, edge)
+    allowed = z >= floor[:, None] - 1e-4
+    seen = set()
+    for step in range(64):
+        rng = torch.tensor([3, step], dtype=torch.long, device=DEV)
+        tok = decode.sample_tokens(logits, T, top_k, top_p, False, rng)
+        assert bool(allowed.gather(1, tok[:, None]).all()), step
+        seen.update(tok.tolist())
+    assert len(seen) > 16  # it samples, not argmax
+
+
 def test_graph_generation_matches_eager_greedy():
     from distributed_llm_alignment_amd.models import build_model, generate, get_config
 
