@@ -161,6 +161,28 @@ def test_graph_generation_matches_eager_greedy():
     assert torch.equal(x[0, 20:28], a[0, 20:28])
 
 
+@pytest.mark.parametrize("top_k,top_p", [(0, 1.0), (50, 0.9)])
+def test_graph_generation_matches_eager_sampled_large_vocab(top_k, top_p):
+    """Sampled decoding with a 65536-token vocabulary takes the row-split sampler (several
+    launches + a workspace per step); a captured hipGraph replay draws the same tokens as eager
+    decoding for the same seed (device-side Philox counter, order-independent histograms)."""
+    import dataclasses
+
+    from distributed_llm_alignment_amd.models import build_model, generate, get_config
+
+    cfg = dataclasses.replace(get_config("tiny-llama-d128"), vocab_size=65536)
+    m = build_model(cfg, device=DEV, dtype=torch.bfloat16, seed=0)
+    g = torch.Generator(device=DEV).manual_seed(4)
+    ids = torch.randint(3, cfg.vocab_size, (4, 16), device=DEV, generator=g)
+    am = torch.ones_like(ids)
+    kw = dict(max_new_tokens=24, do_sample=True, temperature=0.8, top_k=top_k, top_p=top_p,
+              eos_token_id=-1, seed=11)
+    a = generate(m, ids, am, use_graph=False, **kw)
+    b = generate(m, ids, am, use_graph=True, **kw)
+    assert torch.equal(a, b), (a, b)
+    assert len(set(a[:, 16:].flatten().tolist())) > 24  # sampled, not a fixed point
+
+
 def test_layer_split_gpu_host_matches_single_gpu():
     """Layer-split model parallel (device_map, parallel/layer_split.py) with a real device hop:
     first half of the layers on the GPU (HIP kernels), second half on the host (reference ops),
