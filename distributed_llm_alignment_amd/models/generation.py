@@ -10,6 +10,8 @@ to the cache through the same kernel with causal offset.
 """
 from __future__ import annotations
 
+import os
+import weakref
 from dataclasses import dataclass
 from typing import Optional
 
@@ -42,13 +44,22 @@ class KVCache:
         self.max_len = max_len
         self.len = 0
         self.batch = batch
-        self.kv_start = kv_start.to(torch.int32) if kv_start is not None else None
+        self.kv_start = kv_start.to(torch.int32).clone() if kv_start is not None else None
         self._pos = None
         self.slot = torch.zeros(1, dtype=torch.long, device=dev)
         self.kv_len = torch.ones(1, dtype=torch.int32, device=dev)
         self.pos = torch.zeros((batch, 1), dtype=torch.int32, device=dev)
         self.fast_decode = (not self.split and dev.type == "cuda" and dt == torch.bfloat16
                             and ops.decode.decode_supported(self.h_local, Hkv, D))
+
+    def reset(self, kv_start: Optional[torch.Tensor]):
+        """Empty the cache for a new batch of the same shape, keeping every buffer (and so every
+        address a captured decode graph reads) in place."""
+        self.len = 0
+        self._pos = None
+        self.capturing = False
+        if kv_start is not None:
+            self.kv_start.copy_(kv_start.to(torch.int32))
 
     def positions_for(self, T: int) -> torch.Tensor:
         if T == 1 and self.len > 0:
@@ -188,6 +199,15 @@ class _DecodeGraph:
         self.col.add_(1)
         self.rng[1:].add_(1)
 
+    def reset(self, seed: int):
+        self.tok.zero_()
+        self.finished.zero_()
+        self.out.fill_(self.pad)
+        self.gen_mask.zero_()
+        self.col.zero_()
+        self.rng[0].fill_(seed)
+        self.rng[1].fill_(0)
+
     def capture(self):
         self.cache.capturing = True
         s = torch.cuda.Stream()
@@ -199,10 +219,27 @@ class _DecodeGraph:
             with torch.cuda.graph(self.graph, stream=s, capture_error_mode="thread_local"):
                 self._body()
         torch.cuda.current_stream().wait_stream(s)
+        self.model = None  # the graph holds the weight addresses; do not keep the module alive
 
     def replay(self):
         self.graph.replay()
         self.cache.len += 1
+
+
+# One captured decode step is kept per model and replayed by later generate() calls of the same
+# shape and sampling settings (RLHF generates every step at fixed shapes): no re-capture and no
+# new KV cache per call. The key includes every parameter/buffer address, so a module whose
+# weights moved (`.to()`, re-materialised shards) captures afresh. DLA_GRAPH_REUSE=0 disables.
+GRAPH_REUSE = os.environ.get("DLA_GRAPH_REUSE", "1") != "0"
+_GRAPH_SLOT: dict = {}  # id(model) -> (weakref(model), key, cache, decode graph)
+
+
+def clear_graph_cache() -> None:
+    _GRAPH_SLOT.clear()
+
+
+def _weights_key(model: CausalLM) -> tuple:
+    return tuple(t.data_ptr() for t in model.parameters()) + tuple(t.data_ptr() for t in model.buffers())
 
 
 @torch.no_grad()
@@ -228,21 +265,39 @@ def generate(model: CausalLM, input_ids: torch.Tensor, attention_mask: Optional[
     kv_start = None
     if attention_mask is not None:
         kv_start, _, _ = attention_layout(attention_mask)
-    cache = KVCache(model, B, Tp + max_new_tokens, kv_start)
-    h = model(input_ids, cache=cache)
     greedy = not do_sample or temperature <= 0
+    reuse_key, dg = None, None
+    if GRAPH_REUSE and use_graph is not False and max_new_tokens > 2 and input_ids.is_cuda:
+        reuse_key = (B, Tp, max_new_tokens, kv_start is None, greedy, float(temperature), int(top_k),
+                     float(top_p), eos, pad, input_ids.device, _weights_key(model))
+        hit = _GRAPH_SLOT.get(id(model))
+        if hit is not None and hit[0]() is model and hit[1] == reuse_key:
+            cache, dg = hit[2], hit[3]
+            cache.reset(kv_start)
+        else:
+            _GRAPH_SLOT.pop(id(model), None)  # free the old cache before sizing a new one
+    if dg is None:
+        cache = KVCache(model, B, Tp + max_new_tokens, kv_start)
+    h = model(input_ids, cache=cache)
     if seed is None:
         seed = int(torch.randint(0, 2 ** 62, (1,), generator=generator).item()) if generator is not None \
             and generator.device.type == "cpu" else int(torch.randint(0, 2 ** 62, (1,)).item())
     graph_ok = _graph_ok(model, cache) if use_graph is None else (use_graph and _graph_ok(model, cache))
     if graph_ok and max_new_tokens > 2:
-        dg = _DecodeGraph(model, cache, B, max_new_tokens, eos, pad, greedy, temperature, top_k, top_p, seed)
+        if dg is None:
+            dg = _DecodeGraph(model, cache, B, max_new_tokens, eos, pad, greedy, temperature, top_k,
+                              top_p, seed)
+        else:
+            dg.reset(seed)
         dg.sample(model.logits(h[:, -1]))  # token 1 from the prefill, eager
         h = model(dg.tok, cache=cache)  # token 2 eagerly: warms every decode-shape kernel/GEMM
         dg.sample(model.logits(h[:, -1]))
         n = 2
-        if n < max_new_tokens:
+        if n < max_new_tokens and dg.graph is None:
+            dg.model = model
             dg.capture()  # records (does not run) one decode step
+            if reuse_key is not None:
+                _GRAPH_SLOT[id(model)] = (weakref.ref(model), reuse_key, cache, dg)
         while n < max_new_tokens:
             dg.replay()
             n += 1
