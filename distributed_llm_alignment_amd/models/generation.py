@@ -231,6 +231,7 @@ class _DecodeGraph:
 # new KV cache per call. The key includes every parameter/buffer address, so a module whose
 # weights moved (`.to()`, re-materialised shards) captures afresh. DLA_GRAPH_REUSE=0 disables.
 GRAPH_REUSE = os.environ.get("DLA_GRAPH_REUSE", "1") != "0"
+PROMPT_BUCKET = 64
 _GRAPH_SLOT: dict = {}  # id(model) -> (weakref(model), key, cache, decode graph)
 
 
@@ -259,9 +260,19 @@ def generate(model: CausalLM, input_ids: torch.Tensor, attention_mask: Optional[
     all-finished check every 16 tokens). `use_graph=False` forces the eager per-op loop."""
     was_training = model.training
     model.eval()
-    B, Tp = input_ids.shape
     eos = eos_token_id if eos_token_id is not None else model.cfg.eos_token_id
     pad = pad_token_id if pad_token_id is not None else eos
+    extra = 0
+    if GRAPH_REUSE and input_ids.is_cuda and max_new_tokens > 2 and ops._ext.use_native(input_ids):
+        # left-pad the prompt to a multiple of PROMPT_BUCKET so batches whose longest prompt
+        # differs share one decode graph / KV cache (masked prefix: same tokens, stripped below)
+        extra = -input_ids.shape[1] % PROMPT_BUCKET
+        if extra:
+            fill = pad if pad is not None and 0 <= pad < model.cfg.vocab_size else 0
+            input_ids = torch.nn.functional.pad(input_ids, (extra, 0), value=fill)
+            am0 = attention_mask if attention_mask is not None else torch.ones_like(input_ids[:, extra:])
+            attention_mask = torch.nn.functional.pad(am0, (extra, 0), value=0)
+    B, Tp = input_ids.shape
     kv_start = None
     if attention_mask is not None:
         kv_start, _, _ = attention_layout(attention_mask)
@@ -334,7 +345,9 @@ def generate(model: CausalLM, input_ids: torch.Tensor, attention_mask: Optional[
         gm = torch.stack(gen_mask, 1)
     if was_training:
         model.train()
+    pm = attention_mask if attention_mask is not None else torch.ones_like(input_ids)
+    if extra:
+        seqs, pm = seqs[:, extra:].contiguous(), pm[:, extra:]
     if not return_mask:
         return seqs
-    pm = attention_mask if attention_mask is not None else torch.ones_like(input_ids)
     return seqs, torch.cat([pm.long(), gm], dim=1)
