@@ -10,12 +10,20 @@ reference fwd, fused DPO loss, bucketed RCCL reduce-scatter overlapped with back
 fused AdamW, all-gather. Data: synthetic token ids, random-init weights (no network).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
+
+Launch contract: under torchrun (WORLD_SIZE set) every process is one rank and the world size
+must equal --gpus. Invoked bare with --gpus N > 1, this process is only a launcher: it never
+initialises HIP (counting devices does not), starts `torch.distributed.run` with N ranks on
+127.0.0.1 as a CHILD process and exits with its return code (reference launch contract:
+config/accelerate_config.yaml:12, 8 processes on one node).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -23,11 +31,14 @@ import torch
 
 
 HF_STACK_PAIRS_PER_S_1GPU = 5.2648  # BASELINE.md, measured on MI355X
+PEAK_DENSE_BF16_TFLOPS = 2500.0     # MI355X dense bf16 MFMA peak (no sparsity)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--device", choices=("auto", "cpu"), default="auto",
+                    help="cpu: gloo ranks on the host (plumbing test of the launch path only)")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--model", default="llama3-8b")
@@ -49,11 +60,43 @@ def parse():
     ap.add_argument("--profile-dir", default=None, help="write a torch.profiler trace of 1 step")
     ap.add_argument("--layers", type=int, default=None, help="debug only: override layer count "
                     "(a reduced model is NOT the benchmark config)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
-def main() -> int:
-    args = parse()
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args, argv) -> int:
+    """Parent-side launcher for `--gpus N` without torchrun. Touches no GPU: device_count()
+    does not initialise HIP on this image, and the ranks run in a child process tree."""
+    if args.device != "cpu":
+        n_dev = torch.cuda.device_count()
+        if args.gpus > n_dev:
+            print(f"bench.py: --gpus {args.gpus} but only {n_dev} GPU(s) visible; refusing to "
+                  f"run fewer ranks than requested", file=sys.stderr, flush=True)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
+           f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "4")
+    return subprocess.call(cmd, env=env)
+
+
+def main(argv=None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = parse(argv)
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_ranks(args, argv)
+    env_world = int(os.environ.get("WORLD_SIZE", "1"))
+    if env_world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={env_world} but --gpus {args.gpus}")
     import distributed_llm_alignment_amd as dla  # noqa: F401  (loads the HIP extension)
     from distributed_llm_alignment_amd.data.synthetic import synthetic_preference_batch
     from distributed_llm_alignment_amd.models import build_model, get_config
@@ -66,8 +109,20 @@ def main() -> int:
 
     from distributed_llm_alignment_amd.utils.tuning import enable_gemm_tuning
 
-    st = init_distributed()
+    st = init_distributed(device="cpu" if args.device == "cpu" else None)
     dev = st.device
+    if st.world_size != args.gpus:
+        raise SystemExit(f"bench.py: running {st.world_size} rank(s) for --gpus {args.gpus}")
+    if st.world_size > 1:
+        import torch.distributed as dist
+
+        want = "gloo" if dev.type == "cpu" else "nccl"  # nccl == RCCL on ROCm
+        got = dist.get_backend()
+        if got != want or dist.get_world_size() != args.gpus:
+            raise SystemExit(f"bench.py: backend {got} world {dist.get_world_size()}, "
+                             f"expected {want} x {args.gpus}")
+    if args.device != "cpu" and not torch.cuda.is_available():
+        raise SystemExit("bench.py: no GPU visible (use --device cpu for the host plumbing run)")
     gemm_mode = "off"
     if dev.type == "cuda":
         _ext.require()
@@ -189,7 +244,7 @@ def main() -> int:
     tflops_gpu = value * flops_pair / world / 1e12
     if st.rank == 0:
         rec = {
-            "metric": "preference-samples/sec (whole node), Llama-3-8B DPO" if cfg.name == "llama3-8b"
+            "metric": "preference-samples/sec (whole node), Llama-3-8B DPO at 1/2/4/8 MI355X" if cfg.name == "llama3-8b"
                       else f"preference-samples/sec (whole node), {cfg.name} DPO",
             "value": round(value, 4),
             "unit": "preference_pairs/s",
@@ -217,6 +272,8 @@ def main() -> int:
                 "grad_accum": args.accum,
                 "ref_model": "frozen, co-resident" + (", own HIP stream" if ref_stream else ""),
                 "model_tflops_per_gpu": round(tflops_gpu, 1),
+                "mfu": round(tflops_gpu / PEAK_DENSE_BF16_TFLOPS, 4) if dev.type == "cuda" else None,
+                "backend": st.backend or "single-process",
                 "final_loss": round(float(state["loss"].item()), 5),
                 "gemm_selection": "tunableop:" + gemm_mode,
             },
