@@ -66,6 +66,7 @@ def main(argv=None) -> int:
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--backend", default=None)
+    ap.add_argument("--out", default=None, help="rank 0 also writes the rows (JSON lines) here")
     args = ap.parse_args(argv)
     gpu = torch.cuda.is_available() and args.backend != "gloo"
     backend = args.backend or ("nccl" if gpu else "gloo")
@@ -89,6 +90,9 @@ def main(argv=None) -> int:
     if dist.get_rank() == 0:
         for r in rows:
             print(json.dumps(r), flush=True)
+        if args.out:
+            Path(args.out).parent.mkdir(parents=True, exist_ok=True)
+            Path(args.out).write_text("".join(json.dumps(r) + "\n" for r in rows))
     dist.destroy_process_group()
     return 0
 
