@@ -21,6 +21,7 @@
 //   * XOR-swizzled LDS image usable both for row (ds_read_b128) and transposed reads.
 //   * query blocks are the slowest grid dimension, heaviest causal blocks first (LPT order).
 // Backward: see attn_bwd_kernel.
+#include <stdexcept>
 #include "common.h"
 #include "attn_params.h"
 
@@ -834,7 +835,8 @@ void launch_attn_fwd(const AttnParams& p, int D, bool causal, hipStream_t st) {
   if (p.B == 0 || p.Tq == 0) return;
   switch (D) {
     case 64: fwd_dispatch<64>(p, causal, st); break;
-    default: fwd_dispatch<128>(p, causal, st); break;
+    case 128: fwd_dispatch<128>(p, causal, st); break;
+    default: throw std::invalid_argument("attn_fwd: head_dim must be 64 or 128");
   }
 }
 
@@ -860,7 +862,8 @@ void launch_attn_bwd(const AttnBwdParams& p, int D, bool causal, hipStream_t st)
   if (p.B == 0 || p.Tq == 0 || p.Tk == 0) return;
   switch (D) {
     case 64: bwd_dispatch<64>(p, causal, st); break;
-    default: bwd_dispatch<128>(p, causal, st); break;
+    case 128: bwd_dispatch<128>(p, causal, st); break;
+    default: throw std::invalid_argument("attn_bwd: head_dim must be 64 or 128");
   }
 }
 

@@ -87,7 +87,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> norm_fwd(
   check_bf16(w, "w");
   TORCH_CHECK(x.is_contiguous(), "x must be contiguous");
   const int64_t H = x.size(-1);
-  TORCH_CHECK(H % 8 == 0 && H <= 16384, "hidden size must be a multiple of 8 and <= 16384");
+  // forward kernels cover H <= 8192 (wave per row, 16 x 8 columns per lane)
+  TORCH_CHECK(H % 8 == 0 && H <= 8192, "norm_fwd: hidden size must be a multiple of 8 and <= 8192");
   TORCH_CHECK(w.numel() == H && w.is_contiguous(), "w shape");
   const int64_t rows = x.numel() / H;
   TORCH_CHECK(rows < (1ll << 31), "too many rows");

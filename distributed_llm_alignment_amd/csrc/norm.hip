@@ -7,6 +7,7 @@
 // 16-byte chunks (8 bf16) of the row in registers, so the row is read exactly once per pass.
 // Residual fusion: s = bf16(x + r) is written out (the new residual stream) and normalised,
 // saving a separate elementwise pass in both directions.
+#include <stdexcept>
 #include "common.h"
 
 namespace dla {
@@ -355,6 +356,8 @@ void launch_norm_fwd(const bf16_t* x, const bf16_t* res, bf16_t* sum_out, const 
 #undef DLA_NORM_ROW
     return;
   }
+  // wave-per-row: 64 lanes x NC(<=16) x 8 columns covers H <= 8192 (binding enforces it)
+  if (H > 64 * 16 * 8) throw std::invalid_argument("norm_fwd: hidden size > 8192");
   const int nc = chunks_for(H, 64);
   dim3 grid((rows + 3) / 4);
   if (rms) {

@@ -52,6 +52,10 @@ class KVCache:
         self.fast_decode = (not self.split and dev.type == "cuda" and dt == torch.bfloat16
                             and ops.decode.decode_supported(self.h_local, Hkv, D))
 
+    def nbytes(self) -> int:
+        ks = self.k if isinstance(self.k, list) else [self.k]
+        return 2 * sum(t.numel() * t.element_size() for t in ks)
+
     def reset(self, kv_start: Optional[torch.Tensor]):
         """Empty the cache for a new batch of the same shape, keeping every buffer (and so every
         address a captured decode graph reads) in place."""
@@ -161,9 +165,18 @@ def sample_next(logits: torch.Tensor, do_sample: bool, temperature: float, top_p
     return torch.multinomial(probs, 1, generator=generator).squeeze(-1)
 
 
+def _graph_capable(model: CausalLM) -> bool:
+    """Model-level conditions for a captured decode step: single-device, unsharded, and no host
+    sync inside the forward (MoE routing still reads per-expert counts on the host unless the
+    device-driven grouped expert GEMM is active)."""
+    moe_host_sync = model.cfg.is_moe and not getattr(model, "moe_device_dispatch", False)
+    return (model.tp_size == 1 and getattr(model, "_dla_fsdp", None) is None
+            and model.layer_devices is None and not moe_host_sync)
+
+
 def _graph_ok(model: CausalLM, cache: KVCache) -> bool:
-    return (cache.fast_decode and model.tp_size == 1 and getattr(model, "_dla_fsdp", None) is None
-            and not cache.split and ops._ext.use_native(cache.k))
+    return (cache.fast_decode and _graph_capable(model) and not cache.split
+            and ops._ext.use_native(cache.k))
 
 
 class _DecodeGraph:
@@ -230,13 +243,34 @@ class _DecodeGraph:
 # shape and sampling settings (RLHF generates every step at fixed shapes): no re-capture and no
 # new KV cache per call. The key includes every parameter/buffer address, so a module whose
 # weights moved (`.to()`, re-materialised shards) captures afresh. DLA_GRAPH_REUSE=0 disables.
+# The cached KV cache + graph pool stay resident between calls (through the RLHF backward and
+# optimizer step); caches larger than DLA_GRAPH_REUSE_MAX_GB (default 24 GB, << 288 GB HBM) are
+# not kept, entries die with their model (weakref callback), and `release_graph_cache(model)`
+# frees one model's entry on demand.
 GRAPH_REUSE = os.environ.get("DLA_GRAPH_REUSE", "1") != "0"
+GRAPH_REUSE_MAX_BYTES = int(float(os.environ.get("DLA_GRAPH_REUSE_MAX_GB", "24")) * 2 ** 30)
 PROMPT_BUCKET = 64
 _GRAPH_SLOT: dict = {}  # id(model) -> (weakref(model), key, cache, decode graph)
 
 
 def clear_graph_cache() -> None:
     _GRAPH_SLOT.clear()
+
+
+def release_graph_cache(model: CausalLM) -> None:
+    """Drop the cached decode graph + KV cache of `model` (e.g. before a memory-heavy step)."""
+    _GRAPH_SLOT.pop(id(model), None)
+
+
+def graph_cache_bytes() -> int:
+    return sum(e[2].nbytes() for e in _GRAPH_SLOT.values())
+
+
+def _remember(model: CausalLM, key, cache, dg) -> None:
+    if cache.nbytes() > GRAPH_REUSE_MAX_BYTES:
+        return
+    mid = id(model)
+    _GRAPH_SLOT[mid] = (weakref.ref(model, lambda _r, mid=mid: _GRAPH_SLOT.pop(mid, None)), key, cache, dg)
 
 
 def _weights_key(model: CausalLM) -> tuple:
@@ -263,7 +297,8 @@ def generate(model: CausalLM, input_ids: torch.Tensor, attention_mask: Optional[
     eos = eos_token_id if eos_token_id is not None else model.cfg.eos_token_id
     pad = pad_token_id if pad_token_id is not None else eos
     extra = 0
-    if GRAPH_REUSE and input_ids.is_cuda and max_new_tokens > 2 and ops._ext.use_native(input_ids):
+    if (GRAPH_REUSE and use_graph is not False and input_ids.is_cuda and max_new_tokens > 2
+            and ops._ext.use_native(input_ids) and _graph_capable(model)):
         # left-pad the prompt to a multiple of PROMPT_BUCKET so batches whose longest prompt
         # differs share one decode graph / KV cache (masked prefix: same tokens, stripped below)
         extra = -input_ids.shape[1] % PROMPT_BUCKET
@@ -278,7 +313,8 @@ def generate(model: CausalLM, input_ids: torch.Tensor, attention_mask: Optional[
         kv_start, _, _ = attention_layout(attention_mask)
     greedy = not do_sample or temperature <= 0
     reuse_key, dg = None, None
-    if GRAPH_REUSE and use_graph is not False and max_new_tokens > 2 and input_ids.is_cuda:
+    if GRAPH_REUSE and use_graph is not False and max_new_tokens > 2 and input_ids.is_cuda \
+            and _graph_capable(model):
         reuse_key = (B, Tp, max_new_tokens, kv_start is None, greedy, float(temperature), int(top_k),
                      float(top_p), eos, pad, input_ids.device, _weights_key(model))
         hit = _GRAPH_SLOT.get(id(model))
@@ -308,7 +344,7 @@ def generate(model: CausalLM, input_ids: torch.Tensor, attention_mask: Optional[
             dg.model = model
             dg.capture()  # records (does not run) one decode step
             if reuse_key is not None:
-                _GRAPH_SLOT[id(model)] = (weakref.ref(model), reuse_key, cache, dg)
+                _remember(model, reuse_key, cache, dg)
         while n < max_new_tokens:
             dg.replay()
             n += 1

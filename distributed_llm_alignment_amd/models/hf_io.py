@@ -9,7 +9,8 @@ produces the headless `AutoModel` layout used under `backbone.` by the reward mo
 """
 from __future__ import annotations
 
-from typing import Dict, List, Tuple
+from collections.abc import Mapping
+from typing import Callable, Dict, Iterable, List, Optional, Set, Tuple
 
 import torch
 
@@ -124,11 +125,47 @@ def _slice(t: torch.Tensor, spec):
     return t[a:b]
 
 
-def to_hf_state_dict(model, base: bool = False) -> Dict[str, torch.Tensor]:
+class LazyTensors(Mapping):
+    """Read-on-access tensor mapping: keys are known up front, a tensor is materialised only when
+    indexed (safetensors files of a 70B checkpoint never have to sit in host memory at once)."""
+
+    def __init__(self, keys: Iterable[str], getter: Callable[[str], torch.Tensor]):
+        self._keys = list(keys)
+        self._set = set(self._keys)
+        self._get = getter
+
+    def __getitem__(self, k):
+        if k not in self._set:
+            raise KeyError(k)
+        return self._get(k)
+
+    def __iter__(self):
+        return iter(self._keys)
+
+    def __len__(self):
+        return len(self._keys)
+
+    def __contains__(self, k):
+        return k in self._set
+
+
+def renamed(sd: Mapping, fn: Callable[[str], Optional[str]]) -> LazyTensors:
+    """Lazy view of `sd` with keys mapped through `fn` (None drops a key); no tensor is read."""
+    m = {}
+    for k in sd:
+        nk = fn(k)
+        if nk is not None:
+            m[nk] = k
+    return LazyTensors(m.keys(), lambda k: sd[m[k]])
+
+
+def to_hf_state_dict(model, base: bool = False, only: Optional[Set[str]] = None) -> Dict[str, torch.Tensor]:
+    """HF-named views of the native parameters; `only` restricts to a set of native names (the
+    streamed checkpoint writer converts one FSDP unit / layer at a time)."""
     params = dict(model.named_parameters())
     out: Dict[str, torch.Tensor] = {}
     for native, hf, spec in key_map(model.cfg):
-        if native not in params:
+        if native not in params or (only is not None and native not in only):
             continue
         if base and hf.startswith("lm_head"):
             continue
@@ -166,17 +203,21 @@ def _unfuse_moe_experts(sd: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
     return out
 
 
-def load_hf_state_dict(model, sd: Dict[str, torch.Tensor], strict: bool = True, base: bool = False):
+def load_hf_state_dict(model, sd: Mapping, strict: bool = True, base: bool = False,
+                       only: Optional[Set[str]] = None, used_out: Optional[set] = None):
     """Copy HF tensors into the fused native parameters. Accepts `module.` prefixes (DDP) and the
-    fused in-memory Mixtral expert layout of newer transformers."""
-    sd = {(k[len("module."):] if k.startswith("module.") else k): v for k, v in sd.items()}
-    if model.cfg.is_moe:
-        sd = _unfuse_moe_experts(sd)
+    fused in-memory Mixtral expert layout of newer transformers. `sd` may be lazy (LazyTensors):
+    only the tensors of the parameters being loaded are read. With `only` (native names) the
+    other parameters are skipped and neither missing nor unexpected keys are judged here; the
+    keys consumed are added to `used_out`."""
+    sd = renamed(sd, lambda k: k[len("module."):] if k.startswith("module.") else k)
+    if model.cfg.is_moe and any(k.endswith("mlp.experts.gate_up_proj") for k in sd):
+        sd = _unfuse_moe_experts({k: sd[k] for k in sd})
     params = dict(model.named_parameters())
     used = set()
     missing = []
     for native, hf, spec in key_map(model.cfg):
-        if native not in params:
+        if native not in params or (only is not None and native not in only):
             continue
         key = hf
         if key not in sd:
@@ -197,6 +238,10 @@ def load_hf_state_dict(model, sd: Dict[str, torch.Tensor], strict: bool = True, 
             raise ValueError(f"shape mismatch for {hf}: ckpt {tuple(src.shape)} vs model {tuple(dst.shape)}")
         dst.copy_(src.to(dst.dtype))
         used.add(key)
+    if used_out is not None:
+        used_out.update(used)
+    if only is not None:
+        return missing, []
     unexpected = [k for k in sd if k not in used and not k.endswith("rotary_emb.inv_freq")
                   and not k.startswith("lm_head") and ".attn.bias" not in k and ".attn.masked_bias" not in k]
     if strict and (missing or unexpected):

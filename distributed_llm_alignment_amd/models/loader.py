@@ -35,26 +35,29 @@ def default_device() -> torch.device:
 
 
 def _weight_files(path: Path):
-    st = sorted(path.glob("model*.safetensors"))
     if (path / "model.safetensors").exists():
         return [path / "model.safetensors"]
-    if st:
-        return st
+    index = path / "model.safetensors.index.json"
+    if index.exists():  # HF index shards (model-0000k-of-0000n), never model_1* files
+        wm = json.loads(index.read_text())["weight_map"]
+        return [path / f for f in sorted(set(wm.values()))]
     if (path / "pytorch_model.bin").exists():
         return [path / "pytorch_model.bin"]
     return []
 
 
-def read_state_dict(path: Path) -> Dict[str, torch.Tensor]:
+def read_state_dict(path: Path):
+    """HF weights of a model directory as a lazy mapping (tensors are read on access)."""
+    from ..utils.sharded_io import open_consolidated
+    from .hf_io import LazyTensors
+
+    lazy = open_consolidated(path, "model")
+    if lazy is not None:
+        return lazy
     sd: Dict[str, torch.Tensor] = {}
     for f in _weight_files(Path(path)):
-        if f.suffix == ".safetensors":
-            from safetensors.torch import load_file
-
-            sd.update(load_file(str(f)))
-        else:
-            sd.update(torch.load(str(f), map_location="cpu", weights_only=True))
-    return sd
+        sd.update(torch.load(str(f), map_location="cpu", weights_only=True))
+    return LazyTensors(sd.keys(), sd.__getitem__)
 
 
 def load_causal_lm(model_name_or_path: str, gradient_checkpointing: bool = True,
@@ -118,24 +121,28 @@ def build_value_model(base_model_name_or_path: str, device=None, torch_dtype=Non
 def load_reward_checkpoint(rm: RewardModel, path: str, model_index: Optional[int] = None):
     """Load a reward model from an accelerate-layout dir (`model.safetensors`, or
     `model_{i}.safetensors`), an `hf/` export, or `pytorch_model.bin`."""
-    p = Path(path)
-    cand = []
-    if p.is_file():
-        cand = [p]
-    else:
-        if model_index:
-            cand.append(p / f"model_{model_index}.safetensors")
-        cand += [p / "model.safetensors", p / "hf" / "model.safetensors", p / "pytorch_model.bin"]
-    for f in cand:
-        if f.exists():
-            if f.suffix == ".safetensors":
-                from safetensors.torch import load_file
+    from ..utils.sharded_io import open_consolidated
 
-                sd = load_file(str(f))
-            else:
-                sd = torch.load(str(f), map_location="cpu", weights_only=True)
+    p = Path(path)
+    if p.is_file():
+        if p.suffix == ".safetensors":
+            from safetensors.torch import load_file
+
+            sd = load_file(str(p))
+        else:
+            sd = torch.load(str(p), map_location="cpu", weights_only=True)
+        rm.load_hf_state_dict(sd, strict=True)
+        return str(p)
+    cand = ([(p, f"model_{model_index}")] if model_index else []) + [(p, "model"), (p / "hf", "model")]
+    for d, stem in cand:
+        sd = open_consolidated(d, stem)  # single file or HF index shards, read lazily
+        if sd is not None:
             rm.load_hf_state_dict(sd, strict=True)
-            return str(f)
+            return str(d / stem)
+    if (p / "pytorch_model.bin").exists():
+        rm.load_hf_state_dict(torch.load(str(p / "pytorch_model.bin"), map_location="cpu",
+                                         weights_only=True), strict=True)
+        return str(p / "pytorch_model.bin")
     raise FileNotFoundError(f"no reward weights under {path}")
 
 
@@ -157,12 +164,18 @@ def save_hf_pretrained(model, tokenizer, path: str):
     from safetensors.torch import save_file
 
     p = Path(path)
+    save_hf_export_files(model, tokenizer, path)
+    sd = {k: v.detach().contiguous().cpu() for k, v in model.hf_state_dict().items()}
+    save_file(_dedupe(sd), str(p / "model.safetensors"))
+
+
+def save_hf_export_files(model, tokenizer, path: str):
+    """Everything of an HF export except the weights: config.json, dla_config.json, tokenizer."""
+    p = Path(path)
     p.mkdir(parents=True, exist_ok=True)
     base = model.backbone if isinstance(model, (RewardModel, ValueModel)) else model
     (p / "config.json").write_text(json.dumps(base.cfg.to_hf(), indent=2))
     (p / "dla_config.json").write_text(json.dumps(base.cfg.to_dict(), indent=2))
-    sd = {k: v.detach().contiguous().cpu() for k, v in model.hf_state_dict().items()}
-    save_file(_dedupe(sd), str(p / "model.safetensors"))
     if tokenizer is not None and hasattr(tokenizer, "save_pretrained"):
         tokenizer.save_pretrained(str(p))
 

@@ -45,24 +45,35 @@ class RewardModel(nn.Module):
         h = sp_full_hidden(self.backbone, self.backbone(input_ids, attention_mask), input_ids.shape[1])
         return self.scorer(self.pool(h, attention_mask)).squeeze(-1).float()
 
-    def hf_state_dict(self) -> Dict[str, torch.Tensor]:
+    def hf_state_dict(self, only=None) -> Dict[str, torch.Tensor]:
         from .hf_io import to_hf_state_dict
 
-        sd = {f"backbone.{k}": v for k, v in to_hf_state_dict(self.backbone, base=True).items()}
-        sd["scorer.1.weight"] = self.scorer[1].weight.detach()
-        sd["scorer.1.bias"] = self.scorer[1].bias.detach()
+        bb_only = None if only is None else {n[len("backbone."):] for n in only if n.startswith("backbone.")}
+        sd = {f"backbone.{k}": v for k, v in to_hf_state_dict(self.backbone, base=True, only=bb_only).items()}
+        for name in ("weight", "bias"):
+            if only is None or f"scorer.1.{name}" in only:
+                sd[f"scorer.1.{name}"] = getattr(self.scorer[1], name).detach()
         return sd
 
     @torch.no_grad()
-    def load_hf_state_dict(self, sd: Dict[str, torch.Tensor], strict: bool = True):
-        from .hf_io import load_hf_state_dict
+    def load_hf_state_dict(self, sd, strict: bool = True, only=None, used_out=None):
+        from .hf_io import load_hf_state_dict, renamed
 
-        sd = {(k[len("module."):] if k.startswith("module.") else k): v for k, v in sd.items()}
-        bb = {k[len("backbone."):]: v for k, v in sd.items() if k.startswith("backbone.")}
-        missing, unexpected = load_hf_state_dict(self.backbone, bb, strict=False, base=True)
+        sd = renamed(sd, lambda k: k[len("module."):] if k.startswith("module.") else k)
+        bb = renamed(sd, lambda k: k[len("backbone."):] if k.startswith("backbone.") else None)
+        bb_only = None if only is None else {n[len("backbone."):] for n in only if n.startswith("backbone.")}
+        bb_used = set()
+        missing, unexpected = load_hf_state_dict(self.backbone, bb, strict=False, base=True,
+                                                 only=bb_only, used_out=bb_used)
+        if used_out is not None:
+            used_out.update("backbone." + k for k in bb_used)
         missing = [m for m in missing if not m.startswith("lm_head")]
         for name in ("weight", "bias"):
             key = f"scorer.1.{name}"
+            if only is not None and key not in only:
+                continue
+            if used_out is not None and key in sd:
+                used_out.add(key)
             if key in sd:
                 getattr(self.scorer[1], name).copy_(sd[key].to(self.scorer[1].weight.dtype))
             else:
@@ -94,24 +105,35 @@ class ValueModel(nn.Module):
         sp = getattr(self.backbone, "sp", None)
         return v if sp is None else sp.gather(v, dim=1)[:, :input_ids.shape[1]]
 
-    def hf_state_dict(self) -> Dict[str, torch.Tensor]:
+    def hf_state_dict(self, only=None) -> Dict[str, torch.Tensor]:
         from .hf_io import to_hf_state_dict
 
-        sd = {f"backbone.{k}": v for k, v in to_hf_state_dict(self.backbone, base=True).items()}
-        sd["v_head.weight"] = self.v_head.weight.detach()
-        sd["v_head.bias"] = self.v_head.bias.detach()
+        bb_only = None if only is None else {n[len("backbone."):] for n in only if n.startswith("backbone.")}
+        sd = {f"backbone.{k}": v for k, v in to_hf_state_dict(self.backbone, base=True, only=bb_only).items()}
+        for name in ("weight", "bias"):
+            if only is None or f"v_head.{name}" in only:
+                sd[f"v_head.{name}"] = getattr(self.v_head, name).detach()
         return sd
 
     @torch.no_grad()
-    def load_hf_state_dict(self, sd: Dict[str, torch.Tensor], strict: bool = True):
-        from .hf_io import load_hf_state_dict
+    def load_hf_state_dict(self, sd, strict: bool = True, only=None, used_out=None):
+        from .hf_io import load_hf_state_dict, renamed
 
-        sd = {(k[len("module."):] if k.startswith("module.") else k): v for k, v in sd.items()}
-        bb = {k[len("backbone."):]: v for k, v in sd.items() if k.startswith("backbone.")}
-        missing, unexpected = load_hf_state_dict(self.backbone, bb, strict=False, base=True)
+        sd = renamed(sd, lambda k: k[len("module."):] if k.startswith("module.") else k)
+        bb = renamed(sd, lambda k: k[len("backbone."):] if k.startswith("backbone.") else None)
+        bb_only = None if only is None else {n[len("backbone."):] for n in only if n.startswith("backbone.")}
+        bb_used = set()
+        missing, unexpected = load_hf_state_dict(self.backbone, bb, strict=False, base=True,
+                                                 only=bb_only, used_out=bb_used)
+        if used_out is not None:
+            used_out.update("backbone." + k for k in bb_used)
         missing = [m for m in missing if not m.startswith("lm_head")]
         for name in ("weight", "bias"):
             key = f"v_head.{name}"
+            if only is not None and key not in only:
+                continue
+            if used_out is not None and key in sd:
+                used_out.add(key)
             if key in sd:
                 getattr(self.v_head, name).copy_(sd[key].to(self.v_head.weight.dtype))
             else:

@@ -428,15 +428,15 @@ class CausalLM(nn.Module):
         return -(total / count.clamp(min=1))
 
     # ----------------------------------------------------------------- HF key mapping
-    def hf_state_dict(self) -> Dict[str, torch.Tensor]:
+    def hf_state_dict(self, only=None) -> Dict[str, torch.Tensor]:
         from .hf_io import to_hf_state_dict
 
-        return to_hf_state_dict(self)
+        return to_hf_state_dict(self, only=only)
 
-    def load_hf_state_dict(self, sd: Dict[str, torch.Tensor], strict: bool = True):
+    def load_hf_state_dict(self, sd, strict: bool = True, only=None, used_out=None):
         from .hf_io import load_hf_state_dict
 
-        return load_hf_state_dict(self, sd, strict=strict)
+        return load_hf_state_dict(self, sd, strict=strict, only=only, used_out=used_out)
 
 
 def _lin(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor]) -> torch.Tensor:

@@ -96,8 +96,9 @@ def apply_expert_parallel(model, mesh):
         m = layer.mlp
         m.expert_up.data = m.expert_up.data[lo:hi].contiguous()
         m.expert_down.data = m.expert_down.data[lo:hi].contiguous()
-        m.expert_up._dla_expert = True
-        m.expert_down._dla_expert = True
+        for w in (m.expert_up, m.expert_down):
+            w._dla_expert = True
+            w._dla_ep = (mesh.ep_group, ep.rank, ep.ep)  # dim-0 slice rank/size (checkpoint I/O)
         m.ep = ep
     base.ep_size = ep.ep
     base.ep_rank = ep.rank

@@ -61,18 +61,33 @@ def _alloc(t: torch.Tensor) -> None:
         st.resize_(nbytes)
 
 
-def default_units(module: nn.Module) -> List[nn.Module]:
+def default_units(module: nn.Module, min_num_params: int = 0) -> List[List[nn.Module]]:
+    """Consecutive decoder layers grouped into FSDP units. `min_num_params` is the size-based wrap
+    policy of the reference's FSDP plugin (config/fsdp_config.yaml:9-10, accelerate
+    SIZE_BASED_WRAP): layers are merged until a unit holds at least that many parameters (every
+    Llama/Mistral layer is far above the reference's 1e6, so that gives one unit per layer)."""
     base = getattr(module, "backbone", module)
     layers = getattr(base, "layers", None)
     if layers is None:
         raise ValueError("cannot infer FSDP units: module has no `.layers`")
-    return list(layers)
+    units, cur, n = [], [], 0
+    for layer in layers:
+        cur.append(layer)
+        n += sum(p.numel() for p in layer.parameters())
+        if n >= min_num_params:
+            units.append(cur)
+            cur, n = [], 0
+    if cur:
+        units.append(cur)
+    return units
 
 
 class _Unit:
-    def __init__(self, idx: int, module: Optional[nn.Module], params: List[nn.Parameter], world: int):
+    def __init__(self, idx: int, modules: Optional[List[nn.Module]], params: List[nn.Parameter],
+                 world: int):
         self.idx = idx
-        self.module = module
+        self.modules = modules or []
+        self.module = self.modules[-1] if self.modules else None
         self.params = params
         self.offsets: Dict[int, int] = {}
         pos = 0
@@ -101,7 +116,7 @@ class _ShardedBase:
     trainable = False
 
     def _init_sharding(self, module: nn.Module, group, params: List[nn.Parameter], prefetch: bool,
-                       dist_st: Optional[DistState], single: bool = False):
+                       dist_st: Optional[DistState], single: bool = False, min_num_params: int = 0):
         self.module = module
         self.dist = dist_st or dist_state()
         self.group = group
@@ -114,14 +129,14 @@ class _ShardedBase:
         self.dtype = params[0].dtype
         self.device = params[0].device
         pset = {id(p) for p in params}
-        unit_mods = default_units(module)
+        unit_mods = default_units(module, min_num_params)
         owner: Dict[int, int] = {}
         units: List[_Unit] = []
-        for i, m in enumerate(unit_mods):
-            ps = [p for p in m.parameters() if id(p) in pset and id(p) not in owner]
+        for i, mods in enumerate(unit_mods):
+            ps = [p for m in mods for p in m.parameters() if id(p) in pset and id(p) not in owner]
             for p in ps:
                 owner[id(p)] = i
-            units.append(_Unit(i, m, ps, self.world))
+            units.append(_Unit(i, mods, ps, self.world))
         root = [p for p in params if id(p) not in owner]
         for p in root:
             owner[id(p)] = len(units)
@@ -146,10 +161,10 @@ class _ShardedBase:
                 self.param_shard[u.shard_off:u.shard_off + u.chunk].copy_(self._my_chunk(u.full, u))
         self._pending = []  # in-flight reduce-scatters: (handle, tmp, unit)
         self._seen = set()
-        for u in units:
-            if u.module is not None:
-                u.module.register_forward_pre_hook(self._make_pre_forward(u))
-                u.module.register_forward_hook(self._make_post_forward(u))
+        for u in units:  # gather before the unit's first layer, free after its last
+            if u.modules:
+                u.modules[0].register_forward_pre_hook(self._make_pre_forward(u))
+                u.modules[-1].register_forward_hook(self._make_post_forward(u))
         for u in units:
             if not u.is_root:
                 self._reshard(u)
@@ -223,9 +238,9 @@ class ShardedInference(_ShardedBase):
     each layer gathered just in time for its forward."""
 
     def __init__(self, module: nn.Module, group=None, prefetch: bool = True,
-                 dist_st: Optional[DistState] = None):
+                 dist_st: Optional[DistState] = None, min_num_params: int = 0):
         params = list(module.parameters())
-        self._init_sharding(module, group, params, prefetch, dist_st)
+        self._init_sharding(module, group, params, prefetch, dist_st, min_num_params=min_num_params)
         module._dla_fsdp = self
 
     @contextlib.contextmanager
@@ -252,7 +267,11 @@ class FullyShardedEngine(_ShardedBase):
     def __init__(self, module: nn.Module, lr: float = 1e-5, betas=(0.9, 0.999), eps: float = 1e-8,
                  weight_decay: float = 0.0, max_grad_norm: float = 1.0, master_weights: bool = True,
                  dist_st: Optional[DistState] = None, group=None, tp_group=None, prefetch: bool = True,
-                 **_unused):
+                 min_num_params: int = 0, cpu_offload: bool = False, **_unused):
+        if cpu_offload:
+            raise ValueError("FSDP parameter CPU offload is not supported: sharded weights, fp32 "
+                             "master and moments stay in HBM (288 GB per MI355X); set "
+                             "hardware.fsdp.offload_params: false")
         params = [p for p in module.parameters() if p.requires_grad]
         if not params:
             raise ValueError("no trainable parameters")
@@ -269,7 +288,8 @@ class FullyShardedEngine(_ShardedBase):
         if group is None and self.tp_size > 1 and self.tp_size != st.world_size:
             raise ValueError("pass the data-parallel group (mesh.dp_group) when tp < world")
         # TP spanning the whole world: dp = 1, nothing to shard over (kept for uniformity)
-        self._init_sharding(module, group, params, prefetch, st, single=group is None and self.tp_size > 1)
+        self._init_sharding(module, group, params, prefetch, st, single=group is None and self.tp_size > 1,
+                            min_num_params=min_num_params)
         self.zero = 3
         self.lr, self.betas, self.eps, self.wd = lr, tuple(betas), eps, weight_decay
         self.max_grad_norm = max_grad_norm

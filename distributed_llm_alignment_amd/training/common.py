@@ -119,7 +119,7 @@ def parallelize(ctx: TrainContext, model):
         # frozen reference / teachers are sharded too (C10): 1/dp of their weights resident
         from ..parallel.fsdp import ShardedInference
 
-        ShardedInference(model, group=m.dp_group)
+        ShardedInference(model, group=m.dp_group, min_num_params=ctx.hw.get("fsdp_min_num_params", 0))
     return model
 
 
@@ -144,7 +144,12 @@ def make_engine(ctx: TrainContext, model, lr: float, betas=(0.9, 0.999), weight_
 
         return FullyShardedEngine(model, lr=lr, betas=betas, weight_decay=weight_decay,
                                   max_grad_norm=max_grad_norm,
-                                  master_weights=ctx.hw.get("master_weights", True), sp_size=sp, **groups)
+                                  master_weights=ctx.hw.get("master_weights", True), sp_size=sp,
+                                  min_num_params=ctx.hw.get("fsdp_min_num_params", 0),
+                                  cpu_offload=ctx.hw.get("cpu_offload", False), **groups)
+    if ctx.hw.get("cpu_offload"):
+        raise ValueError("hardware.fsdp.offload_params / cpu_offload is not supported (weights and "
+                         "optimizer state stay in 288 GB HBM); set it to false")
     z = ctx.hw.get("zero_stage")
     return DataParallelEngine(model, lr=lr, betas=betas, weight_decay=weight_decay,
                               max_grad_norm=max_grad_norm, zero_stage=None if z is None else min(int(z), 1),

@@ -31,13 +31,13 @@ from ..parallel import dist as pdist
 CONSOLIDATE_MAX_NUMEL = 2_000_000_000  # gather a torch-format optimizer.bin up to ~2B params
 
 
-def _model_file(i: int) -> str:
-    return "model.safetensors" if i == 0 else f"model_{i}.safetensors"
-
-
 def _rng_state() -> Dict[str, Any]:
+    """Reference keys (accelerate random_states_{rank}.pkl), stored with tensors / tuples / ints
+    only so resuming loads them with torch.load(weights_only=True) (no pickle execution)."""
+    name, key, pos, has_gauss, cached = np.random.get_state()
     st = {"random_state": random.getstate(),
-          "numpy_random_seed": np.random.get_state(),
+          "numpy_random_seed": (name, torch.from_numpy(key.astype(np.int64)), int(pos),
+                                int(has_gauss), float(cached)),
           "torch_manual_seed": torch.get_rng_state()}
     if torch.cuda.is_available():
         st["torch_cuda_manual_seed"] = torch.cuda.get_rng_state_all()
@@ -45,28 +45,34 @@ def _rng_state() -> Dict[str, Any]:
 
 
 def _set_rng_state(st: Dict[str, Any]):
-    random.setstate(st["random_state"])
-    np.random.set_state(st["numpy_random_seed"])
+    v, internal, gauss = st["random_state"]
+    random.setstate((v, tuple(internal), gauss))
+    name, key, pos, has_gauss, cached = st["numpy_random_seed"]
+    np.random.set_state((name, np.asarray(key, dtype=np.int64).astype(np.uint32), pos, has_gauss, cached))
     torch.set_rng_state(st["torch_manual_seed"])
     if torch.cuda.is_available() and "torch_cuda_manual_seed" in st:
         torch.cuda.set_rng_state_all(st["torch_cuda_manual_seed"])
 
 
-def _state_dict_of(model) -> Dict[str, torch.Tensor]:
-    sd = model.hf_state_dict() if hasattr(model, "hf_state_dict") else model.state_dict()
-    out, seen = {}, {}
-    for k, v in sd.items():
-        t = v.detach().contiguous().cpu()
-        key = (v.data_ptr(), tuple(v.shape), tuple(v.stride()))
-        out[k] = t.clone() if key in seen else t
-        seen[key] = k
-    return out
+def _is_sharded(model) -> bool:
+    from ..parallel.tensor_parallel import is_tensor_parallel
+
+    return (getattr(model, "_dla_fsdp", None) is not None or is_tensor_parallel(model)
+            or any(getattr(p, "_dla_ep", None) is not None for p in model.parameters()))
+
+
+def _stem(i: int) -> str:
+    return "model" if i == 0 else f"model_{i}"
 
 
 def save_state(output_dir, models: Sequence, engine=None, scheduler=None, step: int = 0,
                tokenizer=None, hf_export: bool = True, keep_last: Optional[int] = None,
-               extra: Optional[Dict[str, Any]] = None) -> Path:
-    from safetensors.torch import save_file
+               extra: Optional[Dict[str, Any]] = None, weights: Optional[str] = None) -> Path:
+    """`weights`: "full" (HF-named, streamed one unit at a time), "sharded" (per-rank local
+    files only, no collective), "both", or None = DLA_CKPT_WEIGHTS / auto ("both" when a model is
+    sharded across ranks, else "full")."""
+    from ..models.loader import save_hf_export_files
+    from . import sharded_io
 
     out = Path(output_dir)
     st = pdist.state()
@@ -75,23 +81,23 @@ def save_state(output_dir, models: Sequence, engine=None, scheduler=None, step: 
     pdist.barrier()
     if engine is not None and hasattr(engine, "wait_params"):
         engine.wait_params()  # overlapped ZeRO-1 all-gathers must land before weights are read
-    from contextlib import ExitStack
-
-    from ..parallel.fsdp import fsdp_full_params
-    from ..parallel.tensor_parallel import is_tensor_parallel, tp_unsharded
+    from ..parallel.tensor_parallel import is_tensor_parallel
 
     tp = any(is_tensor_parallel(m) for m in models)
-    with ExitStack() as stack:
-        for m in models:  # sharded weights are gathered on every rank (collectives)
-            stack.enter_context(fsdp_full_params(m))
-            stack.enter_context(tp_unsharded(m))
-        if st.is_main:
-            for i, m in enumerate(models):
-                save_file(_state_dict_of(m), str(out / _model_file(i)), metadata={"format": "pt"})
-            if hf_export and models:
-                from ..models.loader import save_hf_pretrained
-
-                save_hf_pretrained(models[0], tokenizer, str(out / "hf"))
+    mode = weights or os.environ.get("DLA_CKPT_WEIGHTS") or "auto"
+    for i, m in enumerate(models):
+        m_mode = mode if mode != "auto" else ("both" if _is_sharded(m) else "full")
+        if m_mode in ("sharded", "both"):
+            sharded_io.save_rank_shards(m, out, _stem(i))
+        if m_mode in ("full", "both"):
+            files = sharded_io.save_consolidated(m, out, _stem(i), st.is_main)
+            if i == 0 and hf_export and st.is_main:
+                # the HF export shares the weight files (hard links: no second gather or copy)
+                hf = out / "hf"
+                hf.mkdir(parents=True, exist_ok=True)
+                for f in files + ([f"{_stem(i)}.safetensors.index.json"] if len(files) > 1 else []):
+                    _link_or_copy(out / f, hf / f)
+                save_hf_export_files(m, tokenizer, str(hf))
     if st.is_main and scheduler is not None:
         torch.save(scheduler.state_dict(), out / "scheduler.bin")
     if engine is not None:
@@ -100,13 +106,14 @@ def save_state(output_dir, models: Sequence, engine=None, scheduler=None, step: 
         if st.is_main and hasattr(engine, "layout"):
             (out / "dla_optimizer_layout.json").write_text(json.dumps(engine.layout()))
         if engine.numel <= CONSOLIDATE_MAX_NUMEL and not tp:
-            osd = engine.torch_optimizer_state_dict()  # collective under ZeRO
+            osd = engine.torch_optimizer_state_dict()  # collective under ZeRO (gathered per unit)
             if st.is_main:
                 torch.save(osd, out / "optimizer.bin")
     torch.save({"step": step, **_rng_state()}, out / f"random_states_{st.rank}.pkl")
     if st.is_main:
         meta = {"step": step, "world_size": st.world_size, "num_models": len(models),
-                "zero": getattr(engine, "zero", 0) if engine is not None else None, **(extra or {})}
+                "zero": getattr(engine, "zero", 0) if engine is not None else None,
+                "weights": mode, **(extra or {})}
         (out / "dla_state.json").write_text(json.dumps(meta, indent=2))
         if models:
             # self-describing root: the model-0 architecture + tokenizer, so a checkpoint dir can be
@@ -121,6 +128,15 @@ def save_state(output_dir, models: Sequence, engine=None, scheduler=None, step: 
             _rotate(out.parent, keep_last)
     pdist.barrier()
     return out
+
+
+def _link_or_copy(src: Path, dst: Path) -> None:
+    if dst.exists():
+        dst.unlink()
+    try:
+        os.link(src, dst)
+    except OSError:
+        shutil.copyfile(src, dst)
 
 
 def _update_latest(ckpt: Path):
@@ -156,26 +172,30 @@ def resolve_checkpoint(path) -> Optional[Path]:
     return p if p.exists() else None
 
 
+def _weights_present(d: Path, index: int) -> bool:
+    stem = _stem(index)
+    return ((d / f"{stem}.safetensors").exists() or (d / f"{stem}.safetensors.index.json").exists()
+            or (d / f"{stem}.shards.json").exists())
+
+
 def load_model_weights(model, ckpt_dir, index: int = 0, strict: bool = True):
-    from safetensors.torch import load_file
+    """Load model `index` of a checkpoint into a (possibly FSDP / TP / EP sharded) model.
+    Per-rank shard files are used when their layout matches (exact, no collective on the
+    weights); otherwise the HF-named files are streamed in one unit at a time."""
+    from . import sharded_io
+    from ..models.hf_io import LazyTensors
 
     d = Path(ckpt_dir)
-    f = d / _model_file(index)
-    if f.exists():
-        sd = load_file(str(f))
-    elif (d / "pytorch_model.bin").exists() and index == 0:
-        sd = torch.load(str(d / "pytorch_model.bin"), map_location="cpu", weights_only=True)
-    else:
+    stem = _stem(index)
+    if (d / f"{stem}.shards.json").exists() and sharded_io.load_rank_shards(model, d, stem):
+        return [], []
+    sd = sharded_io.open_consolidated(d, stem)
+    if sd is None and (d / "pytorch_model.bin").exists() and index == 0:
+        raw = torch.load(str(d / "pytorch_model.bin"), map_location="cpu", weights_only=True)
+        sd = LazyTensors(raw.keys(), raw.__getitem__)
+    if sd is None:
         raise FileNotFoundError(f"no weights for model {index} in {d}")
-    from ..parallel.fsdp import fsdp_full_params
-    from ..parallel.tensor_parallel import tp_unsharded
-
-    # full tensors in, re-sliced to this TP rank / FSDP shard
-    with fsdp_full_params(model, writeback=True), tp_unsharded(model, writeback=True):
-        if hasattr(model, "load_hf_state_dict"):
-            return model.load_hf_state_dict(sd, strict=strict)
-        sd = {(k[7:] if k.startswith("module.") else k): v for k, v in sd.items()}
-        return model.load_state_dict(sd, strict=strict)
+    return sharded_io.load_consolidated(model, sd, strict=strict)
 
 
 def load_state(ckpt_dir, models: Sequence, engine=None, scheduler=None, load_models: bool = True) -> int:
@@ -187,7 +207,7 @@ def load_state(ckpt_dir, models: Sequence, engine=None, scheduler=None, load_mod
     st = pdist.state()
     if load_models:
         for i, m in enumerate(models):
-            if (d / _model_file(i)).exists():
+            if _weights_present(d, i):
                 load_model_weights(m, d, i, strict=True)
     if engine is not None:
         shard = d / f"optimizer_shard_{st.rank}.pt"
@@ -204,9 +224,16 @@ def load_state(ckpt_dir, models: Sequence, engine=None, scheduler=None, load_mod
     rs = d / f"random_states_{st.rank}.pkl"
     step = 0
     if rs.exists():
-        rstate = torch.load(str(rs), weights_only=False)  # written by this framework (own file)
-        step = int(rstate.get("step", 0))
-        _set_rng_state(rstate)
+        try:
+            rstate = torch.load(str(rs), weights_only=True)  # never unpickles code
+        except Exception as e:  # e.g. a pre-r2 file holding numpy arrays: resume without RNG
+            import warnings
+
+            warnings.warn(f"RNG state {rs} not restored (not weights_only-loadable: {e})")
+            rstate = None
+        if rstate is not None:
+            step = int(rstate.get("step", 0))
+            _set_rng_state(rstate)
     meta = d / "dla_state.json"
     if meta.exists():
         step = int(json.loads(meta.read_text()).get("step", step))

@@ -47,10 +47,23 @@ def load_config(path, overlays: Optional[Iterable[str]] = None,
         cfg = yaml.safe_load(fh) or {}
     for ov in overlays or []:
         with open(ov, "r", encoding="utf-8") as fh:
-            cfg = deep_merge(cfg, yaml.safe_load(fh) or {})
+            cfg = deep_merge(cfg, _as_overlay(yaml.safe_load(fh) or {}))
     for o in overrides or []:
         cfg = apply_override(cfg, o)
     return cfg
+
+
+_TOP_LEVEL = {"model", "data", "optimization", "logging", "hardware", "distill", "ppo", "sampling",
+              "reward_model", "models", "benchmarks", "generation", "latency", "seed"}
+
+
+def _as_overlay(frag: Dict[str, Any]) -> Dict[str, Any]:
+    """The reference's data-source presets (config/data_sources/*.yaml) are FLAT fragments meant to
+    be pasted under `data:` (README.md:122-126) — or under `sampling:` for RLHF prompt sources
+    (they carry `prompt_key`). Wrap such a fragment so it can be passed as an overlay."""
+    if "source" in frag and not (set(frag) & _TOP_LEVEL):
+        return {"sampling" if "prompt_key" in frag else "data": frag}
+    return frag
 
 
 def flatten_dict(config: Dict[str, Any], parent_key: str = "", sep: str = ".") -> Dict[str, Any]:
@@ -108,8 +121,15 @@ def hardware_parallel(cfg: Dict[str, Any]) -> Dict[str, Any]:
         try:
             with open(ds, "r", encoding="utf-8") as fh:
                 ds_cfg = json.load(fh)
-            stage = int(ds_cfg.get("zero_optimization", {}).get("stage", 0))
-        except (OSError, ValueError):
+            zo = ds_cfg.get("zero_optimization", {}) or {}
+            stage = int(zo.get("stage", 0))
+            for k in ("offload_optimizer", "offload_param"):
+                if str((zo.get(k) or {}).get("device", "none")).lower() not in ("none", "null"):
+                    raise ValueError(f"{ds}: zero_optimization.{k} offload is not supported "
+                                     f"(state stays in 288 GB HBM per MI355X)")
+            if ds_cfg.get("gradient_clipping") is not None:
+                out["ds_gradient_clipping"] = float(ds_cfg["gradient_clipping"])
+        except (OSError, json.JSONDecodeError):
             stage = 3
         out["zero_stage"] = stage if out["zero_stage"] is None else out["zero_stage"]
         out["fsdp"] = stage >= 3

@@ -10,8 +10,23 @@ if [ "${DLA_DEBUG:-0}" = "1" ]; then   # serialised HIP + loud RCCL errors (SURV
 fi
 REPO="$(cd "$(dirname "${BASH_SOURCE[0]}")/.." && pwd)"
 export PYTHONPATH="$REPO${PYTHONPATH:+:$PYTHONPATH}"
-if [ -z "${NPROC:-}" ]; then
-  NPROC=$(python -c "import torch; print(max(1, torch.cuda.device_count()))")
+ACCEL_CFG="${ACCELERATE_CONFIG:-$REPO/config/accelerate_config.yaml}"
+if [ -z "${NPROC:-}" ] || [ -z "${MASTER_PORT:-}" ]; then
+  # reference contract: num_processes / main_process_port from the accelerate config, capped at
+  # the GPUs actually visible (device_count() does not initialise HIP)
+  read -r _NP _PORT < <(python - "$ACCEL_CFG" <<'PY'
+import sys, yaml, torch
+try:
+    c = yaml.safe_load(open(sys.argv[1])) or {}
+except OSError:
+    c = {}
+n = torch.cuda.device_count()
+want = int(c.get("num_processes", n or 1))
+print(max(1, min(want, n)) if n else 1, int(c.get("main_process_port", 29500)))
+PY
+)
+  NPROC=${NPROC:-$_NP}
+  MASTER_PORT=${MASTER_PORT:-$_PORT}
 fi
 dla_run() {  # dla_run <module> [args...]
   local mod="$1"; shift

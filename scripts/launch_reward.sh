@@ -1,5 +1,5 @@
 #!/usr/bin/env bash
 # reward stage on all GPUs of this node: scripts/launch_reward.sh [CONFIG] [--override k=v ...]
 source "$(dirname "${BASH_SOURCE[0]}")/_launch_common.sh"
-CONFIG=${1:-config/reward.yaml}; shift || true
+CONFIG=${1:-config/reward_config.yaml}; shift || true
 dla_run distributed_llm_alignment_amd.training.train_reward --config "$CONFIG" "$@"

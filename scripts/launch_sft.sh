@@ -1,5 +1,5 @@
 #!/usr/bin/env bash
 # sft stage on all GPUs of this node: scripts/launch_sft.sh [CONFIG] [--override k=v ...]
 source "$(dirname "${BASH_SOURCE[0]}")/_launch_common.sh"
-CONFIG=${1:-config/sft.yaml}; shift || true
+CONFIG=${1:-config/sft_config.yaml}; shift || true
 dla_run distributed_llm_alignment_amd.training.train_sft --config "$CONFIG" "$@"
