@@ -32,6 +32,8 @@ def parse_args(argv=None):
     p.add_argument("--config", required=True)
     p.add_argument("--max_prompts", type=int, default=None)
     p.add_argument("--batch_size", type=int, default=8)
+    p.add_argument("--overlay", action="append", default=[], help="YAML fragment merged over the config")
+    p.add_argument("--override", action="append", default=[], help="dotted key.path=value override")
     return p.parse_args(argv)
 
 
@@ -101,7 +103,7 @@ def write_outputs(results, output_path: str, table_path: str):
 
 def main(argv=None) -> int:
     args = parse_args(argv)
-    cfg = load_config(args.config)
+    cfg = load_config(args.config, args.overlay, args.override)
     gen = cfg.get("generation", {}) or {}
     seed = cfg.get("seed", 0)
     results: Dict[str, Dict[str, Dict[str, float]]] = {}

@@ -27,6 +27,8 @@ def parse_args(argv=None):
     p = argparse.ArgumentParser(description="Measure forward / decode latency")
     p.add_argument("--config", required=True)
     p.add_argument("--decode_tokens", type=int, default=32)
+    p.add_argument("--overlay", action="append", default=[], help="YAML fragment merged over the config")
+    p.add_argument("--override", action="append", default=[], help="dotted key.path=value override")
     return p.parse_args(argv)
 
 
@@ -73,7 +75,7 @@ def measure_model(model, batch_sizes: List[int], seq_lengths: List[int], warmup_
 
 def main(argv=None) -> int:
     args = parse_args(argv)
-    cfg = load_config(args.config)
+    cfg = load_config(args.config, args.overlay, args.override)
     lat = cfg["latency"]
     results: Dict[str, List[Dict[str, float]]] = {}
     for name, path in cfg["models"].items():
