@@ -297,7 +297,9 @@ def generate(model: CausalLM, input_ids: torch.Tensor, attention_mask: Optional[
     eos = eos_token_id if eos_token_id is not None else model.cfg.eos_token_id
     pad = pad_token_id if pad_token_id is not None else eos
     extra = 0
-    if (GRAPH_REUSE and use_graph is not False and input_ids.is_cuda and max_new_tokens > 2
+    # (gated on the model, not on use_graph: eager and graph decoding of a graph-capable model
+    # see the same padded prefill, so their outputs stay bitwise comparable)
+    if (GRAPH_REUSE and input_ids.is_cuda and max_new_tokens > 2
             and ops._ext.use_native(input_ids) and _graph_capable(model)):
         # left-pad the prompt to a multiple of PROMPT_BUCKET so batches whose longest prompt
         # differs share one decode graph / KV cache (masked prefix: same tokens, stripped below)
