@@ -5,6 +5,7 @@
 #include <tuple>
 
 #include "bind_util.h"
+#include "gg_params.h"
 
 namespace dla {
 
@@ -18,6 +19,170 @@ void launch_moe_combine_bwd(const bf16_t*, const bf16_t*, const int*, const floa
                             int, bf16_t*, float*, hipStream_t);
 
 void launch_quant_fp8_rows(const bf16_t*, int64_t, int64_t, int, uint8_t*, float*, hipStream_t);
+
+
+
+static void check_offs(const at::Tensor& offs, int64_t G) {
+  check_i32(offs, "offs");
+  TORCH_CHECK(offs.dim() == 1 && offs.is_contiguous() && offs.size(0) == G + 1,
+              "offs must be contiguous int32 [G + 1]");
+}
+
+static bool gg_is_fp8(const at::Tensor& t) { return t.scalar_type() == at::kFloat8_e4m3fn; }
+
+static void check_operand(const at::Tensor& t, const char* name, bool fp8) {
+  check_cuda(t, name);
+  TORCH_CHECK(fp8 ? gg_is_fp8(t) : t.scalar_type() == at::kBFloat16, name,
+              fp8 ? " must be float8_e4m3fn" : " must be bfloat16");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+  check_aligned16(t, name);
+}
+
+// Rows of A are the expert-sorted token rows; offs[g]..offs[g+1] are expert g's rows (device
+// array, never read on the host). The kernel trusts 0 = offs[0] <= ... <= offs[G] = rows.
+static GGParams gg_base(const at::Tensor& a, const at::Tensor& offs) {
+  GGParams p{};
+  p.A = reinterpret_cast<const uint8_t*>(a.data_ptr());
+  p.offs = offs.data_ptr<int>();
+  p.G = static_cast<int>(offs.size(0) - 1);
+  return p;
+}
+
+// y[M, N] = x[M, K] . w[g]^T per expert row range; fp8: x/w e4m3 with row scales sx [M, 1],
+// sw [G, N, 1]
+at::Tensor gg_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& offs,
+                  const c10::optional<at::Tensor>& sx, const c10::optional<at::Tensor>& sw) {
+  const bool fp8 = gg_is_fp8(x);
+  check_operand(x, "x", fp8);
+  check_operand(w, "w", fp8);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 3 && w.size(2) == x.size(1), "x [M, K], w [G, N, K]");
+  const int64_t M = x.size(0), K = x.size(1), G = w.size(0), N = w.size(1);
+  check_offs(offs, G);
+  TORCH_CHECK(K % (fp8 ? 16 : 8) == 0 && N % 8 == 0 && N < (1 << 30) && K < (1 << 30),
+              "K % 8 (bf16) / 16 (fp8) == 0 and N % 8 == 0");
+  c10::hip::HIPGuardMasqueradingAsCUDA gd(x.device());
+  auto y = at::empty({M, N}, x.options().dtype(at::kBFloat16));
+  if (M == 0) return y;
+  GGParams p = gg_base(x, offs);
+  p.B = reinterpret_cast<const uint8_t*>(w.data_ptr());
+  p.C = y.data_ptr();
+  p.lda = K; p.ldb = K; p.ldc = N; p.sBg = N * K;
+  p.N = (int)N; p.K = (int)K;
+  if (fp8) {
+    TORCH_CHECK(sx && sw && sx->numel() == M && sw->numel() == G * N, "fp8 needs sx [M, 1] and sw [G, N, 1]");
+    check_f32(*sx, "sx"); check_f32(*sw, "sw");
+    TORCH_CHECK(sx->is_contiguous() && sw->is_contiguous(), "scales contiguous");
+    p.sa = sx->data_ptr<float>(); p.sb = sw->data_ptr<float>(); p.sSg = N;
+  }
+  launch_grouped_gemm(p, 0, fp8, false, M, cur_stream(x));
+  return y;
+}
+
+// gate|up projection with the SwiGLU epilogue: w_up [G, 2F, K] = [gate; up] -> (gu [M, 2F], a [M, F])
+std::tuple<at::Tensor, at::Tensor> gg_fwd_swiglu(const at::Tensor& x, const at::Tensor& w,
+                                                 const at::Tensor& offs,
+                                                 const c10::optional<at::Tensor>& sx,
+                                                 const c10::optional<at::Tensor>& sw) {
+  const bool fp8 = gg_is_fp8(x);
+  check_operand(x, "x", fp8);
+  check_operand(w, "w_up", fp8);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 3 && w.size(2) == x.size(1) && w.size(1) % 2 == 0,
+              "x [M, K], w_up [G, 2F, K]");
+  const int64_t M = x.size(0), K = x.size(1), G = w.size(0), F = w.size(1) / 2;
+  check_offs(offs, G);
+  TORCH_CHECK(F % 128 == 0 && K % (fp8 ? 16 : 8) == 0, "F % 128 == 0, K % 8 (bf16) / 16 (fp8) == 0");
+  c10::hip::HIPGuardMasqueradingAsCUDA gd(x.device());
+  auto gu = at::empty({M, 2 * F}, x.options().dtype(at::kBFloat16));
+  auto a = at::empty({M, F}, x.options().dtype(at::kBFloat16));
+  if (M == 0) return {gu, a};
+  GGParams p = gg_base(x, offs);
+  p.B = reinterpret_cast<const uint8_t*>(w.data_ptr());
+  p.C = gu.data_ptr();
+  p.lda = K; p.ldb = K; p.ldc = 2 * F; p.sBg = 2 * F * K;
+  p.N = (int)F; p.K = (int)K; p.F = (int)F;
+  p.out2 = bp(a); p.ld_out2 = F;
+  if (fp8) {
+    TORCH_CHECK(sx && sw && sx->numel() == M && sw->numel() == G * 2 * F, "fp8 needs sx [M, 1] and sw [G, 2F, 1]");
+    check_f32(*sx, "sx"); check_f32(*sw, "sw");
+    TORCH_CHECK(sx->is_contiguous() && sw->is_contiguous(), "scales contiguous");
+    p.sa = sx->data_ptr<float>(); p.sb = sw->data_ptr<float>(); p.sSg = 2 * F;
+  }
+  launch_grouped_gemm(p, 1, fp8, false, M, cur_stream(x));
+  return {gu, a};
+}
+
+// input gradient: dx[M, K] = dy[M, N] . w[g] (w [G, N, K])
+at::Tensor gg_dgrad(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& offs) {
+  check_operand(dy, "dy", false);
+  check_operand(w, "w", false);
+  TORCH_CHECK(dy.dim() == 2 && w.dim() == 3 && w.size(1) == dy.size(1), "dy [M, N], w [G, N, K]");
+  const int64_t M = dy.size(0), N = dy.size(1), G = w.size(0), K = w.size(2);
+  check_offs(offs, G);
+  TORCH_CHECK(K % 8 == 0 && N % 8 == 0, "N % 8 == 0 and K % 8 == 0");
+  c10::hip::HIPGuardMasqueradingAsCUDA gd(dy.device());
+  auto dx = at::empty({M, K}, dy.options());
+  if (M == 0) return dx;
+  GGParams p = gg_base(dy, offs);
+  p.B = reinterpret_cast<const uint8_t*>(w.data_ptr());
+  p.C = dx.data_ptr();
+  p.lda = N; p.ldb = K; p.ldc = K; p.sBg = N * K;
+  p.N = (int)K; p.K = (int)N;
+  launch_grouped_gemm(p, 2, false, false, M, cur_stream(dy));
+  return dx;
+}
+
+// down projection input gradient fused with the SwiGLU backward: da = dy . w_down[g]
+// (w_down [G, H, F]) -> (dgu [M, 2F], a [M, F]) from gu [M, 2F]
+std::tuple<at::Tensor, at::Tensor> gg_dgrad_swiglu(const at::Tensor& dy, const at::Tensor& w,
+                                                   const at::Tensor& offs, const at::Tensor& gu) {
+  check_operand(dy, "dy", false);
+  check_operand(w, "w_down", false);
+  check_operand(gu, "gu", false);
+  TORCH_CHECK(dy.dim() == 2 && w.dim() == 3 && w.size(1) == dy.size(1), "dy [M, H], w_down [G, H, F]");
+  const int64_t M = dy.size(0), H = dy.size(1), G = w.size(0), F = w.size(2);
+  TORCH_CHECK(gu.dim() == 2 && gu.size(0) == M && gu.size(1) == 2 * F, "gu [M, 2F]");
+  check_offs(offs, G);
+  TORCH_CHECK(F % 8 == 0 && H % 8 == 0, "H % 8 == 0 and F % 8 == 0");
+  c10::hip::HIPGuardMasqueradingAsCUDA gd(dy.device());
+  auto dgu = at::empty({M, 2 * F}, dy.options());
+  auto a = at::empty({M, F}, dy.options());
+  if (M == 0) return {dgu, a};
+  GGParams p = gg_base(dy, offs);
+  p.B = reinterpret_cast<const uint8_t*>(w.data_ptr());
+  p.C = dgu.data_ptr();
+  p.lda = H; p.ldb = F; p.ldc = 2 * F; p.sBg = H * F;
+  p.N = (int)F; p.K = (int)H; p.F = (int)F;
+  p.aux = cbp(gu); p.ld_aux = 2 * F;
+  p.out2 = bp(a); p.ld_out2 = F;
+  launch_grouped_gemm(p, 3, false, false, M, cur_stream(dy));
+  return {dgu, a};
+}
+
+// weight gradient: out[g] (+)= dy[rows of g]^T . x[rows of g]; dy [M, N1], x [M, N2],
+// out [G, N1, N2] bf16 or fp32 (the fp32 main-grad buffer)
+void gg_wgrad(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& offs, at::Tensor out,
+              bool accumulate) {
+  check_operand(dy, "dy", false);
+  check_operand(x, "x", false);
+  TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && dy.size(0) == x.size(0), "dy [M, N1], x [M, N2]");
+  const int64_t N1 = dy.size(1), N2 = x.size(1);
+  check_cuda(out, "out");
+  TORCH_CHECK(out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kFloat, "out bf16 or fp32");
+  TORCH_CHECK(out.dim() == 3 && out.size(1) == N1 && out.size(2) == N2 && out.is_contiguous(),
+              "out [G, N1, N2] contiguous");
+  check_aligned16(out, "out");
+  const int64_t G = out.size(0);
+  check_offs(offs, G);
+  TORCH_CHECK(N1 % 8 == 0 && N2 % 8 == 0, "N1 % 8 == 0 and N2 % 8 == 0");
+  c10::hip::HIPGuardMasqueradingAsCUDA gd(dy.device());
+  GGParams p = gg_base(dy, offs);
+  p.B = reinterpret_cast<const uint8_t*>(x.data_ptr());
+  p.C = out.data_ptr();
+  p.lda = N1; p.ldb = N2; p.ldc = N2; p.sCg = N1 * N2;
+  p.M = (int)N1; p.N = (int)N2; p.K = 0;
+  p.accumulate = accumulate ? 1 : 0;
+  launch_grouped_gemm(p, 4, false, out.scalar_type() == at::kFloat, dy.size(0), cur_stream(dy));
+}
 
 // x [M, K] bf16 (unit column stride, 16-B aligned rows) -> (q [M, K] float8_e4m3fn, inv_scale [M, 1])
 std::tuple<at::Tensor, at::Tensor> quant_fp8_rows(const at::Tensor& x) {
@@ -136,6 +301,11 @@ TORCH_LIBRARY_FRAGMENT(dla, m) {
   m.def("moe_dispatch(Tensor x, Tensor pos) -> Tensor");
   m.def("moe_combine(Tensor ys, Tensor pos, Tensor? w) -> Tensor");
   m.def("moe_combine_bwd(Tensor dout, Tensor ys, Tensor pos, Tensor w) -> (Tensor, Tensor)");
+  m.def("gg_fwd(Tensor x, Tensor w, Tensor offs, Tensor? sx, Tensor? sw) -> Tensor");
+  m.def("gg_fwd_swiglu(Tensor x, Tensor w_up, Tensor offs, Tensor? sx, Tensor? sw) -> (Tensor, Tensor)");
+  m.def("gg_dgrad(Tensor dy, Tensor w, Tensor offs) -> Tensor");
+  m.def("gg_dgrad_swiglu(Tensor dy, Tensor w_down, Tensor offs, Tensor gu) -> (Tensor, Tensor)");
+  m.def("gg_wgrad(Tensor dy, Tensor x, Tensor offs, Tensor(a!) out, bool accumulate) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(dla, CUDA, m) {
@@ -145,4 +315,9 @@ TORCH_LIBRARY_IMPL(dla, CUDA, m) {
   m.impl("moe_dispatch", &dla::moe_dispatch);
   m.impl("moe_combine", &dla::moe_combine);
   m.impl("moe_combine_bwd", &dla::moe_combine_bwd);
+  m.impl("gg_fwd", &dla::gg_fwd);
+  m.impl("gg_fwd_swiglu", &dla::gg_fwd_swiglu);
+  m.impl("gg_dgrad", &dla::gg_dgrad);
+  m.impl("gg_dgrad_swiglu", &dla::gg_dgrad_swiglu);
+  m.impl("gg_wgrad", &dla::gg_wgrad);
 }

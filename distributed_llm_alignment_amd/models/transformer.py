@@ -160,7 +160,8 @@ class MLP(nn.Module):
 
 class MoE(nn.Module):
     """Top-k routed SwiGLU experts (Mixtral). Softmax router in fp32, top-k renormalised,
-    dropless token dispatch (sort by expert, one GEMM pair per expert, weighted scatter-add).
+    dropless token dispatch (sort by expert, one device-driven grouped GEMM per projection,
+    weighted gather-combine); no host sync in the local (non-EP) path.
     Under expert parallelism `ep_group` routes tokens with all-to-all (see parallel.expert)."""
 
     def __init__(self, cfg: ModelConfig, device=None, dtype=None):
@@ -195,7 +196,7 @@ class MoE(nn.Module):
             return out.view(shp)
         pos, counts = ops.moe.expert_positions(topi, self.cfg.num_experts)
         xs = ops.moe.dispatch(h2, pos)
-        ys = ops.moe.experts_swiglu(xs, self.expert_up, self.expert_down, counts.tolist(), fp8=self.fp8)
+        ys = ops.moe.experts_swiglu(xs, self.expert_up, self.expert_down, counts, fp8=self.fp8)
         return ops.moe.combine(ys, pos, topv).view(shp)
 
 
@@ -253,6 +254,18 @@ class CausalLM(nn.Module):
             # tied input/output embedding: its gradient arrives from two ops, so it must go through
             # autograd's AccumulateGrad (one hook call) rather than the GEMM main-grad path
             self.embed._dla_shared = True
+
+    @property
+    def moe_device_dispatch(self) -> bool:
+        """True when every MoE layer routes without a host sync (grouped GEMM path, no EP, no
+        cached fp8 expert copies that a captured graph could replay stale): the condition for a
+        hipGraph-captured MoE decode step."""
+        cfg = self.cfg
+        if not cfg.is_moe:
+            return True
+        return (ops.moe.grouped_gemm_enabled() and getattr(self, "ep_size", 1) == 1
+                and cfg.intermediate_size % 128 == 0 and cfg.hidden_size % 16 == 0
+                and not any(getattr(layer.mlp, "fp8", False) for layer in self.layers))
 
     # --------------------------------------------------------------------------------- init
     @torch.no_grad()

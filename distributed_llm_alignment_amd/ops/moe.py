@@ -7,16 +7,20 @@ with boolean masks, `index_add_` and a fresh weight-gradient tensor per expert. 
     and its analytic backward touching only k logits per token;
   * dispatch / combine: gather kernels over a token-slot -> expert-sorted-row map `pos`
     (deterministic, no atomics); combine's backward also returns the routing-weight grads;
-  * experts: one hipBLASLt GEMM pair per expert on contiguous row ranges of the expert-sorted
-    matrix (outputs written in place, no concatenation), SwiGLU via the fused HIP kernel, and
-    weight gradients accumulated straight into the engine's flat grad buffer (`main_grad`),
-    so an expert that received no tokens costs nothing;
-  * optional fp8 (e4m3, per-tensor scales) forward GEMMs (`fp8=True`), bf16 backward.
+  * experts: the device-driven grouped GEMM (csrc/grouped_gemm.hip): ONE launch per projection
+    covers every expert, the per-expert row ranges come from a device offsets array (no host
+    sync, no per-expert launch loop, hipGraph-capturable), SwiGLU is fused into the gate|up
+    epilogue and the SwiGLU backward into the down projection's input-gradient epilogue, and
+    weight gradients accumulate straight into the engine's grad buffer (`main_grad`, bf16 or
+    fp32). `DLA_MOE_GEMM=loop` selects the previous per-expert hipBLASLt loop (host counts);
+  * optional fp8 (e4m3, row-wise scales) forward GEMMs (`fp8=True`) on the block-scaled
+    16x16x128 MFMA, bf16 backward.
 CPU (and non-bf16) inputs use the PyTorch reference path with identical semantics.
 """
 from __future__ import annotations
 
-from typing import List, Optional, Sequence
+import os
+from typing import List, Optional, Sequence, Union
 
 import torch
 import torch.nn.functional as F
@@ -59,8 +63,17 @@ def expert_positions(topi: torch.Tensor, num_experts: int):
     order = torch.argsort(flat, stable=True)
     pos = torch.empty_like(order)
     pos[order] = torch.arange(order.numel(), device=order.device)
-    counts = torch.bincount(flat, minlength=num_experts)
+    # scatter_add histogram: unlike torch.bincount it never reads the max id on the host
+    counts = torch.zeros(num_experts, dtype=torch.long, device=flat.device)
+    counts.scatter_add_(0, flat, torch.ones_like(flat))
     return pos.view(topi.shape).to(torch.int32), counts
+
+
+def expert_offsets(counts: torch.Tensor) -> torch.Tensor:
+    """Per-expert counts [E] (device) -> exclusive row offsets [E + 1] int32 (device, no sync)."""
+    offs = torch.zeros(counts.numel() + 1, dtype=torch.int32, device=counts.device)
+    offs[1:] = torch.cumsum(counts, 0).to(torch.int32)
+    return offs
 
 
 # ------------------------------------------------------------------------------ dispatch
@@ -233,6 +246,63 @@ class _ExpertsFn(torch.autograd.Function):
         return dxs, outs[0], outs[1], None, None
 
 
+class _GroupedExpertsFn(torch.autograd.Function):
+    """Grouped SwiGLU experts on the device-driven grouped GEMM; offs [E+1] int32 on device."""
+
+    @staticmethod
+    def forward(ctx, xs, w_up, w_down, offs, fp8: bool):
+        C = _ext.require()
+        if fp8:
+            wu_q, wu_s = fp8_weight(w_up)
+            wd_q, wd_s = fp8_weight(w_down)
+            xq, xsc = quant_fp8_rows(xs)
+            gu, a = C.gg_fwd_swiglu(xq, wu_q, offs, xsc, wu_s)
+            aq, asc = quant_fp8_rows(a)
+            ys = C.gg_fwd(aq, wd_q, offs, asc, wd_s)
+        else:
+            gu, a = C.gg_fwd_swiglu(xs, w_up, offs, None, None)
+            ys = C.gg_fwd(a, w_down, offs, None, None)
+        ctx.save_for_backward(xs, gu, w_up, w_down, offs)
+        return ys
+
+    @staticmethod
+    def backward(ctx, dys):
+        xs, gu, w_up, w_down, offs = ctx.saved_tensors
+        C = _ext.require()
+        dys = dys.contiguous()
+        # da = dy . W_down fused with the SwiGLU backward -> dgu, plus the recomputed a
+        dgu, a = C.gg_dgrad_swiglu(dys, w_down, offs, gu)
+        outs = []
+        for w, dy, x, need in ((w_up, dgu, xs, ctx.needs_input_grad[1]),
+                               (w_down, dys, a, ctx.needs_input_grad[2])):
+            mg = getattr(w, "main_grad", None)
+            if mg is not None and mg.is_contiguous() and mg.dtype in (torch.bfloat16, torch.float32):
+                C.gg_wgrad(dy, x, offs, mg, True)
+                hook = getattr(w, "_dla_grad_hook", None)
+                if hook is not None:
+                    hook(w)
+                outs.append(None)
+            elif need:
+                gw = torch.empty_like(w)
+                C.gg_wgrad(dy, x, offs, gw, False)
+                outs.append(gw)
+            else:
+                outs.append(None)
+        dxs = C.gg_dgrad(dgu, w_up, offs) if ctx.needs_input_grad[0] else None
+        return dxs, outs[0], outs[1], None, None
+
+
+def grouped_gemm_enabled() -> bool:
+    return os.environ.get("DLA_MOE_GEMM", "grouped") != "loop"
+
+
+def _grouped_ok(xs, w_up, w_down) -> bool:
+    F2, H = w_up.shape[1], w_up.shape[2]
+    return (grouped_gemm_enabled() and _ext.use_native(xs) and xs.dtype == torch.bfloat16
+            and w_up.dtype == torch.bfloat16 and (F2 // 2) % 128 == 0 and H % 16 == 0
+            and w_down.shape[1] == H and w_down.shape[2] == F2 // 2)
+
+
 def _swiglu_bwd(gu, dout):
     if _ext.use_native(gu) and gu.dtype == torch.bfloat16:
         return _ext.require().swiglu_bwd(gu.contiguous(), dout.contiguous())
@@ -244,10 +314,21 @@ def _swiglu_bwd(gu, dout):
 
 
 def experts_swiglu(xs: torch.Tensor, w_up: torch.Tensor, w_down: torch.Tensor,
-                   counts: Sequence[int], fp8: bool = False) -> torch.Tensor:
-    """xs [M, H] expert-sorted rows, w_up [E, 2F, H] ([gate; up]), w_down [E, H, F]."""
+                   counts: Union[torch.Tensor, Sequence[int]], fp8: bool = False) -> torch.Tensor:
+    """xs [M, H] expert-sorted rows, w_up [E, 2F, H] ([gate; up]), w_down [E, H, F].
+    counts: per-expert row counts, a device tensor (grouped GEMM path: never read on the host)
+    or a host sequence."""
     if fp8 and not (xs.is_cuda and _FP8 is not None):
         fp8 = False
+    xs = xs.contiguous()
+    if _grouped_ok(xs, w_up, w_down):
+        if isinstance(counts, torch.Tensor):
+            offs = expert_offsets(counts.to(xs.device))
+        else:
+            offs = expert_offsets(torch.tensor(list(counts), device=xs.device))
+        return _GroupedExpertsFn.apply(xs, w_up, w_down, offs, bool(fp8))
+    if isinstance(counts, torch.Tensor):
+        counts = counts.tolist()  # host sync: per-expert loop path only
     return _ExpertsFn.apply(xs, w_up, w_down, [int(c) for c in counts], bool(fp8))
 
 
