@@ -11,6 +11,7 @@ benchmarks and tests share one implementation.
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -170,6 +171,41 @@ def ppo_loss(policy, critic, seqs, mask, stats: Dict[str, torch.Tensor], clip_ep
     return pl + vf_coef * vl, {"policy_loss": pl.detach(), "value_loss": vl.detach(), **pm}
 
 
+# Tokens per ensemble-KL chunk: (teachers + 1) x chunk x V bf16 logits exist at a time
+# (V = 51200, 2 teachers, 1024 tokens: 315 MB) instead of [K, S, T, V] for the whole batch.
+KL_CHUNK_TOKENS = int(os.environ.get("DLA_KL_CHUNK_TOKENS", "1024"))
+
+
+def _kl_chunk(student, teachers, hs_c, ths_c):
+    s_logits = student.logits(hs_c)
+    with torch.no_grad():
+        t_logits = torch.stack([t.logits(h) for t, h in zip(teachers, ths_c)])
+    return ops.ensemble_kl(s_logits, t_logits)
+
+
+def chunked_ensemble_kl(student, teachers: Sequence, hs: torch.Tensor, ths: Sequence[torch.Tensor],
+                        chunk: Optional[int] = None) -> torch.Tensor:
+    """Per-token forward KL(mean_k softmax(teacher_k) || softmax(student)) from final hidden rows
+    (student hs [N, H] with grad, teacher hidden [N, H] each), token-chunked: each chunk's
+    student and teacher logits are produced by the LM-head GEMMs, reduced by the fused HIP
+    ensemble-KL kernel and dropped; the backward recomputes the chunk (activation checkpoint), so
+    neither [K, N, V] teacher logits nor [N, V] student logits are ever materialised whole
+    (reference: src/training/train_distill.py:130-144 stacks all teacher logits)."""
+    from torch.utils.checkpoint import checkpoint
+
+    chunk = int(chunk or KL_CHUNK_TOKENS)
+    N = hs.shape[0]
+    outs = []
+    for i in range(0, N, chunk):
+        hs_c = hs[i:i + chunk]
+        ths_c = [h[i:i + chunk] for h in ths]
+        if torch.is_grad_enabled() and hs.requires_grad and N > chunk:
+            outs.append(checkpoint(_kl_chunk, student, teachers, hs_c, ths_c, use_reentrant=False))
+        else:
+            outs.append(_kl_chunk(student, teachers, hs_c, ths_c))
+    return outs[0] if len(outs) == 1 else torch.cat(outs)
+
+
 def distill_loss(student, teachers: Sequence, batch, use_kl: bool):
     """CE on teacher rollouts (labels = input_ids) or token-masked ensemble forward-KL. KL mode
     compares every position (unshifted), as the reference does (train_distill.py:140-144)."""
@@ -181,11 +217,11 @@ def distill_loss(student, teachers: Sequence, batch, use_kl: bool):
             raise ValueError("KL distillation requires teacher and student to share a vocabulary "
                              "(SURVEY Appendix A #15)")
     hs = student(ids, mask)
-    s_logits = student.logits(hs)
     with torch.no_grad():
-        t_logits = torch.stack([t.logits(t(ids, mask)) for t in teachers])
-    S, T, V = s_logits.shape
-    kl = ops.ensemble_kl(s_logits.reshape(S * T, V), t_logits.reshape(len(teachers), S * T, V)).view(S, T)
+        ths = [t(ids, mask) for t in teachers]  # teacher hidden states only: [S, T, H] each
+    S, T = hs.shape[0], hs.shape[1]
+    kl = chunked_ensemble_kl(student, teachers, hs.reshape(S * T, -1),
+                             [h.reshape(S * T, -1) for h in ths]).view(S, T)
     sp = student.sp
     if sp is None:
         m = mask.float()

@@ -1,5 +1,5 @@
 """Linear layer whose weight gradient is accumulated straight into the flat fp32/bf16 grad
-buffer by the GEMM itself (C = A^T B + C, beta = 1).
+buffer by the GEMM itself (C = A^T B + C, beta = 1; bf16 operands, bf16 or fp32 C).
 
 Eager autograd computes each weight gradient into a fresh tensor and then launches a separate
 elementwise add into `.grad` on every micro-batch (≈1.5 % of a Llama-3-8B DPO step on MI355X,
@@ -58,8 +58,28 @@ TN_WGRAD_MIN_ELEMS = int(os.environ.get("DLA_TN_WGRAD_MIN", "0"))
 
 def _tn_ok(mg: torch.Tensor, M: int) -> bool:
     N, K = mg.shape
-    return (TN_WGRAD and N * K >= TN_WGRAD_MIN_ELEMS and mg.dtype == torch.bfloat16 and _ext.use_native(mg)
-            and M % 8 == 0 and N % 8 == 0 and K % 8 == 0)
+    return (TN_WGRAD and N * K >= TN_WGRAD_MIN_ELEMS and mg.dtype in (torch.bfloat16, torch.float32)
+            and _ext.use_native(mg) and M % 8 == 0 and N % 8 == 0 and K % 8 == 0)
+
+
+_F32_ADDMM = {"ok": None}
+
+
+def addmm_into(mg: torch.Tensor, a: torch.Tensor, b: torch.Tensor) -> None:
+    """mg += a @ b with one rounding. bf16 operands into an fp32 main-grad buffer run as ONE
+    hipBLASLt GEMM with a bf16 x bf16 -> fp32 C (beta = 1) epilogue: the accumulation over
+    micro-batches happens in fp32 and no bf16 temporary exists."""
+    if mg.dtype == a.dtype:
+        mg.addmm_(a, b)
+        return
+    if mg.is_cuda and _F32_ADDMM["ok"] is not False:
+        try:
+            torch.addmm(mg, a, b, out_dtype=mg.dtype, out=mg)
+            _F32_ADDMM["ok"] = True
+            return
+        except (RuntimeError, TypeError):
+            _F32_ADDMM["ok"] = False
+    mg.add_(a.to(mg.dtype) @ b.to(mg.dtype))
 
 
 def _wgrad_accumulate(mg: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor,
@@ -76,9 +96,9 @@ def _wgrad_accumulate(mg: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor,
         if xt is None:
             xt = torch.empty((K, M), dtype=x2.dtype, device=x2.device)
             tr(x2, xt)
-        mg.addmm_(dyt, xt.t())
+        addmm_into(mg, dyt, xt.t())
         return
-    mg.addmm_(dy2.t(), x2)
+    addmm_into(mg, dy2.t(), x2)
 
 
 def accumulate_weight_grad(weight: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor,

@@ -27,6 +27,7 @@ import torch.nn.functional as F
 
 from . import _ext
 from .activations import swiglu
+from .linear import addmm_into
 
 
 # ------------------------------------------------------------------------------ router
@@ -227,12 +228,12 @@ class _ExpertsFn(torch.autograd.Function):
                 a = swiglu(g)
                 da = dy @ w_down[e]
                 if g_down is not None:
-                    g_down[e].addmm_(dy.t(), a)
+                    addmm_into(g_down[e], dy.t(), a)
                 dg = _swiglu_bwd(g, da)
                 if need_x:
                     torch.mm(dg, w_up[e], out=dxs[s:s + c])
                 if g_up is not None:
-                    g_up[e].addmm_(dg.t(), xs[s:s + c])
+                    addmm_into(g_up[e], dg.t(), xs[s:s + c])
             s += c
         outs = []
         for w, g, mg in ((w_up, g_up, mg_up), (w_down, g_down, mg_down)):

@@ -20,6 +20,14 @@ Replaces DDP / DeepSpeed ZeRO / FSDP as reached through accelerate in the refere
     is available for loaded checkpoints.
 Gradients are SUM-reduced; the 1/world mean is folded into the AdamW kernel's grad scale and the
 clip-norm computation (no extra pass over the gradients).
+
+fp32 gradient accumulation (`grad_dtype=torch.float32`, chosen automatically by the trainers for
+gradient_accumulation_steps >= 16, e.g. config/dpo_hh.yaml's 256): the flat grad buffer is fp32
+(`main_grad`), weight gradients are accumulated into it by the GEMMs themselves (hipBLASLt
+bf16 x bf16 -> fp32 C, beta = 1), the few autograd-produced grads (norm weights, embeddings)
+are folded in by the post-accumulate hook, and the fused AdamW reads fp32 grads. The bucket
+collectives reduce in fp32 (`reduce_dtype=torch.float32`) or, to halve xGMI bytes, in bf16
+(`reduce_dtype=torch.bfloat16`: the bucket is rounded once, after accumulation).
 """
 from __future__ import annotations
 
@@ -65,7 +73,8 @@ class DataParallelEngine:
                  dist_st: Optional[DistState] = None, group=None, tp_group=None, expert_group=None,
                  overlap_param_gather: bool = os.environ.get("DLA_OVERLAP_AG", "1") != "0",
                  sp_size: int = 1,
-                 overlap_optimizer: bool = os.environ.get("DLA_OVERLAP_OPT", "0") == "1"):
+                 overlap_optimizer: bool = os.environ.get("DLA_OVERLAP_OPT", "0") == "1",
+                 grad_dtype: Optional[torch.dtype] = None, reduce_dtype: Optional[torch.dtype] = None):
         self.module = module
         # sequence parallel (parallel.sequence): `group` is DP x SP and the sp ranks of a replica
         # hold partial (token-slice) gradients of one replicated loss -> sum over SP, mean over DP
@@ -105,6 +114,9 @@ class DataParallelEngine:
             raise ValueError(f"mixed parameter dtypes {dtypes}")
         self.dtype = params[0].dtype
         self.device = params[0].device
+        self.grad_dtype = grad_dtype or self.dtype
+        self.grad_fp32 = self.grad_dtype == torch.float32 and self.dtype != torch.float32
+        self.reduce_dtype = reduce_dtype or self.grad_dtype
         params = list(reversed(params))  # ~ the order gradients are produced in
         bucket_elems = max(ALIGN, int(bucket_mb * (1 << 20)) // params[0].element_size())
         # expert-parallel weights (parallel.expert) are reduced over the group of ranks holding
@@ -144,7 +156,7 @@ class DataParallelEngine:
         self._comm = self.world > 1
         # ---- flat storage (params re-pointed into it)
         self.param_buf = torch.zeros(self.numel, dtype=self.dtype, device=self.device)
-        self.grad_buf = torch.zeros(self.numel, dtype=self.dtype, device=self.device)
+        self.grad_buf = torch.zeros(self.numel, dtype=self.grad_dtype, device=self.device)
         self.params = params
         # weights change in place inside the flat buffer (fused AdamW, all-gathers): the
         # per-parameter _version does not move, so caches key on this shared epoch too
@@ -155,9 +167,15 @@ class DataParallelEngine:
                 view = self.param_buf[o:o + p.numel()].view_as(p)
                 view.copy_(p.data)
                 p.data = view
-                p.grad = self.grad_buf[o:o + p.numel()].view_as(p)
+                gview = self.grad_buf[o:o + p.numel()].view_as(p)
+                if self.grad_fp32:
+                    # autograd grads must match the param dtype: they arrive in p.grad (bf16) and
+                    # the post-accumulate hook folds them into the fp32 main_grad
+                    p.grad = None
+                else:
+                    p.grad = gview
                 # ops.linear / linear_logprob accumulate weight grads here inside the GEMM
-                p.main_grad = p.grad
+                p.main_grad = gview
                 p._dla_grad_hook = self._on_grad
                 # persistent W^T for the TN-layout input-gradient GEMM (ops.linear.input_grad)
                 p._dla_wt_ok = p.dim() == 2 and not getattr(p, "_dla_shared", False)
@@ -170,7 +188,7 @@ class DataParallelEngine:
             shard += b.size // b.world
         self.shard_numel = shard
         if self.zero:
-            self.grad_shard = torch.zeros(shard, dtype=self.dtype, device=self.device)
+            self.grad_shard = torch.zeros(shard, dtype=self.grad_dtype, device=self.device)
             self.param_shard = torch.empty(shard, dtype=self.dtype, device=self.device)
             src = torch.cat([self._chunk(self.param_buf, b) for b in self.buckets])
             self.param_shard.copy_(src)
@@ -276,6 +294,10 @@ class DataParallelEngine:
             self._sync = prev
 
     def _on_grad(self, p: nn.Parameter):
+        if self.grad_fp32 and p.grad is not None:
+            # an autograd-produced (bf16) grad: fold into the fp32 main_grad, every micro-step
+            p.main_grad.add_(p.grad)
+            p.grad = None
         if not self._sync or not self._comm:
             return
         # a main_grad (GEMM-accumulated) weight reports twice: from the GEMM epilogue and from
@@ -298,12 +320,24 @@ class DataParallelEngine:
             if self.zero:
                 self.grad_shard[b.shard_off:b.shard_off + b.size].copy_(g)
             return
+        if self.reduce_dtype != self.grad_dtype:
+            # reduce in the (narrower) communication dtype: round the accumulated bucket once
+            gc = g.to(self.reduce_dtype)
+            if self.zero:
+                oc = torch.empty(b.size // b.world, dtype=self.reduce_dtype, device=g.device)
+                h = dist.reduce_scatter_tensor(oc, gc, op=dist.ReduceOp.SUM, group=b.group, async_op=True)
+                dst = self.grad_shard[b.shard_off:b.shard_off + b.size // b.world]
+                self._handles.append((h, lambda oc=oc, dst=dst: dst.copy_(oc)))
+            else:
+                h = dist.all_reduce(gc, op=dist.ReduceOp.SUM, group=b.group, async_op=True)
+                self._handles.append((h, lambda gc=gc, g=g: g.copy_(gc)))
+            return
         if self.zero:
             out = self.grad_shard[b.shard_off:b.shard_off + b.size // b.world]
             h = dist.reduce_scatter_tensor(out, g, op=dist.ReduceOp.SUM, group=b.group, async_op=True)
         else:
             h = dist.all_reduce(g, op=dist.ReduceOp.SUM, group=b.group, async_op=True)
-        self._handles.append(h)
+        self._handles.append((h, None))
 
     def finish_grad_sync(self):
         """Launch buckets whose params got no gradient (unused params), then wait for all."""
@@ -311,8 +345,10 @@ class DataParallelEngine:
             while self._launched < len(self.buckets):
                 self._launch(self._launched)
                 self._launched += 1
-            for h in self._handles:
+            for h, post in self._handles:
                 h.wait()
+                if post is not None:
+                    post()
         self._handles = []
         self._launched = 0
         self._ready = [0] * len(self.buckets)
@@ -416,6 +452,9 @@ class DataParallelEngine:
     def zero_grad(self):
         self.wait_params()  # an overlapped optimizer step still owns the grad buffer
         self.grad_buf.zero_()
+        if self.grad_fp32:
+            for p in self.params:
+                p.grad = None
         if self.zero:
             self.grad_shard.zero_()
 

@@ -151,10 +151,34 @@ def make_engine(ctx: TrainContext, model, lr: float, betas=(0.9, 0.999), weight_
         raise ValueError("hardware.fsdp.offload_params / cpu_offload is not supported (weights and "
                          "optimizer state stay in 288 GB HBM); set it to false")
     z = ctx.hw.get("zero_stage")
+    gd, rd = grad_dtypes(ctx)
     return DataParallelEngine(model, lr=lr, betas=betas, weight_decay=weight_decay,
                               max_grad_norm=max_grad_norm, zero_stage=None if z is None else min(int(z), 1),
                               bucket_mb=ctx.hw.get("bucket_mb", 256.0),
-                              master_weights=ctx.hw.get("master_weights", True), sp_size=sp, **groups)
+                              master_weights=ctx.hw.get("master_weights", True), sp_size=sp,
+                              grad_dtype=gd, reduce_dtype=rd, **groups)
+
+
+_DTYPES = {"fp32": torch.float32, "float32": torch.float32, "bf16": torch.bfloat16,
+           "bfloat16": torch.bfloat16}
+
+
+def grad_dtypes(ctx: TrainContext):
+    """(grad accumulation dtype, reduce dtype) from hardware.grad_dtype / hardware.reduce_dtype.
+    grad_dtype "auto" (default): fp32 main grads once gradient_accumulation_steps >= 16 (bf16
+    accumulation of 16-256 micro-batch grads loses the small ones: config/dpo_hh.yaml uses 256),
+    else the parameter dtype. reduce_dtype defaults to the grad dtype."""
+    g = str(ctx.hw.get("grad_dtype", "auto")).lower()
+    if g == "auto":
+        gd = torch.float32 if int(ctx.hw.get("grad_accum", 1)) >= 16 else None
+    elif g in _DTYPES:
+        gd = _DTYPES[g]
+    else:
+        raise ValueError(f"hardware.grad_dtype must be auto / fp32 / bf16, got {g!r}")
+    r = ctx.hw.get("reduce_dtype")
+    if r is not None and str(r).lower() not in _DTYPES:
+        raise ValueError(f"hardware.reduce_dtype must be fp32 / bf16, got {r!r}")
+    return gd, (_DTYPES[str(r).lower()] if r is not None else None)
 
 
 def effective_batch_msg(ctx: TrainContext, micro: int) -> str:

@@ -114,6 +114,8 @@ def hardware_parallel(cfg: Dict[str, Any]) -> Dict[str, Any]:
         "sp_size": int(hw.get("sp_size", 1) or 1),  # Ulysses sequence parallel (parallel.sequence)
         "bucket_mb": float(hw.get("bucket_mb", 256)),
         "master_weights": bool(hw.get("master_weights", True)),
+        "grad_dtype": hw.get("grad_dtype", "auto"),      # fp32 main grads (auto: grad_accum >= 16)
+        "reduce_dtype": hw.get("reduce_dtype"),          # bucket collective dtype (default: grad)
         "fsdp": False,
     }
     ds = hw.get("deepspeed_config")

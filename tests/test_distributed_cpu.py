@@ -562,3 +562,76 @@ def test_consolidate_optimizer_shards_matches_gathered(tmp_path, fsdp):
     for i in want["state"]:
         for k in ("exp_avg", "exp_avg_sq"):
             assert torch.equal(got["state"][i][k], want["state"][i][k]), (i, k)
+
+
+# ------------------------------------------------------------------ fp32 gradient accumulation
+def _accum_grads(grad_dtype, reduce_dtype=None, n_micro=64, rank=0, world=1, zero=None):
+    from distributed_llm_alignment_amd.data.synthetic import synthetic_preference_batch
+    from distributed_llm_alignment_amd.models import build_model, get_config
+    from distributed_llm_alignment_amd.objectives import dpo_step_loss
+    from distributed_llm_alignment_amd.parallel.data_parallel import DataParallelEngine
+
+    cfg = get_config("tiny-llama")
+    pol = build_model(cfg, device="cpu", dtype=torch.bfloat16, seed=0)
+    ref = build_model(cfg, device="cpu", dtype=torch.bfloat16, seed=0).requires_grad_(False)
+    eng = DataParallelEngine(pol, lr=1e-2, max_grad_norm=0.0, bucket_mb=0.05, zero_stage=zero,
+                             grad_dtype=grad_dtype, reduce_dtype=reduce_dtype)
+    g = torch.Generator().manual_seed(5)
+    b = synthetic_preference_batch(2 * world, 16, cfg.vocab_size, generator=g)
+    mine = {s: {k: v[rank * 2:(rank + 1) * 2] for k, v in b[s].items()} for s in b}
+    for a in range(n_micro):
+        ctxm = eng.no_sync() if a < n_micro - 1 else _Null()
+        with ctxm:
+            loss, _ = dpo_step_loss(pol, ref, mine, beta=0.1)
+            (loss / n_micro).backward()
+    eng.finish_grad_sync()
+    if eng.zero:
+        return eng.grad_shard.float().clone(), [(b.start, b.end, b.shard_off) for b in eng.buckets]
+    return eng.grad_buf.float().clone()
+
+
+def test_fp32_main_grad_accumulation_is_exact_where_bf16_drifts():
+    """64 identical micro-batches of loss/64 must sum back to ONE micro-batch's gradient: with
+    fp32 main grads (GEMM bf16 x bf16 -> fp32 C accumulation + hook-folded autograd grads) it does
+    to fp32 rounding; bf16 accumulation stagnates (config/dpo_hh.yaml accumulates 256)."""
+    one = _accum_grads(torch.float32, n_micro=1)
+    f32 = _accum_grads(torch.float32, n_micro=64)
+    b16 = _accum_grads(None, n_micro=64)
+    rel = lambda x: ((x - one).norm() / one.norm()).item()  # noqa: E731
+    assert rel(f32) < 1e-4, rel(f32)
+    assert rel(b16) > 10 * rel(f32), (rel(b16), rel(f32))
+
+
+def _dp_fp32(rank, world, zero, reduce_bf16):
+    return _accum_grads(torch.float32, torch.bfloat16 if reduce_bf16 else None, n_micro=4,
+                        rank=rank, world=world, zero=zero)
+
+
+@pytest.mark.parametrize("zero,reduce_bf16", [(0, False), (1, False), (1, True)])
+def test_dp_fp32_grads_reduce_dtypes(zero, reduce_bf16):
+    res = run_ranks(_dp_fp32, 2, (zero, reduce_bf16))
+    if zero:  # reassemble the flat buffer from the two ranks' per-bucket chunks
+        layout = res[0][1]
+        full = torch.zeros(layout[-1][1])
+        for r in (0, 1):
+            sh = res[r][0]
+            for st, en, so in layout:
+                c = (en - st) // 2
+                full[st + r * c: st + (r + 1) * c] = sh[so:so + c]
+    else:
+        assert torch.equal(res[0], res[1])
+        full = res[0]
+    # single process over both ranks' rows (DP sums grads; the mean is applied in AdamW)
+    from distributed_llm_alignment_amd.parallel.data_parallel import DataParallelEngine  # noqa: F401
+
+    single = _single_fp32_sum()
+    n = min(full.numel(), single.numel())
+    rel = ((full[:n] - single[:n]).norm() / single[:n].norm()).item()
+    assert rel < (2e-2 if reduce_bf16 else 1e-2), rel
+
+
+def _single_fp32_sum():
+    # grads of rank 0's rows + rank 1's rows == sum-reduced DP grads
+    a = _accum_grads(torch.float32, n_micro=4, rank=0, world=2)
+    b = _accum_grads(torch.float32, n_micro=4, rank=1, world=2)
+    return a + b

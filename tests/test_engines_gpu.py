@@ -62,7 +62,9 @@ def test_transposed_dgrad_matches_nn_dgrad():
     """The engine's persistent-W^T input-gradient path and the transposed-activation TN weight
     gradient give the same steps as plain dY @ W / dY^T X, including the lazy W^T refresh after
     the optimizer updated W."""
-    from distributed_llm_alignment_amd.ops import linear as lin
+    import importlib
+
+    lin = importlib.import_module("distributed_llm_alignment_amd.ops.linear")
 
     try:
         lin.TRANSPOSED_DGRAD, lin.TN_WGRAD, lin.TN_WGRAD_MIN_ELEMS = True, True, 0
@@ -108,3 +110,40 @@ def test_overlapped_optimizer_bitwise_matches_serial():
     lb, pb = _dp_steps(False)
     assert la == lb
     assert torch.equal(pa, pb)
+
+
+def _accum_gpu(grad_dtype, n_micro):
+    from distributed_llm_alignment_amd.data.synthetic import synthetic_preference_batch
+    from distributed_llm_alignment_amd.models import build_model, get_config
+    from distributed_llm_alignment_amd.objectives import dpo_step_loss
+    from distributed_llm_alignment_amd.parallel.data_parallel import DataParallelEngine
+
+    dev = torch.device("cuda", 0)
+    cfg = get_config("tiny-llama-d128")
+    pol = build_model(cfg, device=dev, dtype=torch.bfloat16, seed=0)
+    ref = build_model(cfg, device=dev, dtype=torch.bfloat16, seed=0).requires_grad_(False)
+    eng = DataParallelEngine(pol, lr=1e-3, max_grad_norm=0.0, grad_dtype=grad_dtype)
+    g = torch.Generator().manual_seed(5)
+    b = synthetic_preference_batch(2, 128, cfg.vocab_size, device=dev, generator=g)
+    for _ in range(n_micro):
+        loss, _ = dpo_step_loss(pol, ref, b)
+        (loss / n_micro).backward()
+    torch.cuda.synchronize()
+    return eng.grad_buf.float().clone()
+
+
+def test_fp32_main_grad_accumulation_256_micro_batches():
+    """config/dpo_hh.yaml accumulates 256 micro-batches: with fp32 main grads (hipBLASLt
+    bf16 x bf16 -> fp32 C GEMM epilogue) 256 identical micro-batches of loss/256 sum back to one
+    micro-batch's gradient; bf16 accumulation drifts by orders of magnitude more."""
+    import importlib
+
+    lin = importlib.import_module("distributed_llm_alignment_amd.ops.linear")
+
+    one = _accum_gpu(torch.float32, 1)
+    f32 = _accum_gpu(torch.float32, 256)
+    assert lin._F32_ADDMM["ok"] is True, "fp32-C hipBLASLt GEMM path not taken"
+    b16 = _accum_gpu(None, 256)
+    rel = lambda x: ((x - one).norm() / one.norm()).item()  # noqa: E731
+    assert rel(f32) < 2e-4, rel(f32)
+    assert rel(b16) > 20 * rel(f32), (rel(b16), rel(f32))

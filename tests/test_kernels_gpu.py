@@ -520,3 +520,39 @@ def test_dpo_training_bitwise_deterministic_gpu():
     l2, p2 = run()
     assert torch.equal(l1, l2)
     assert torch.equal(p1, p2)
+
+
+def test_chunked_ensemble_kl_peak_memory_v51200():
+    """Distillation KL at the phi-2 vocabulary (V=51200): the token-chunked path never holds the
+    [K, S, T, V] teacher logits (839 MB here); values and student grads match the one-shot path."""
+    from distributed_llm_alignment_amd.models import build_model, get_config
+    from distributed_llm_alignment_amd.objectives import chunked_ensemble_kl
+
+    dev = torch.device("cuda", 0)
+    cfg = get_config("tiny-llama-d128", vocab_size=51200)
+    st = build_model(cfg, device=dev, dtype=torch.bfloat16, seed=0)
+    ts = [build_model(cfg, device=dev, dtype=torch.bfloat16, seed=s).requires_grad_(False) for s in (1, 2)]
+    g = torch.Generator(device=dev).manual_seed(0)
+    ids = torch.randint(0, 51200, (8, 512), device=dev, generator=g)
+    mask = torch.ones_like(ids)
+    N = ids.numel()
+    with torch.no_grad():
+        th = [t(ids, mask).reshape(N, -1) for t in ts]
+    full_bytes = 2 * N * 51200 * 2
+    res = []
+    for chunk in (256, N):
+        st.zero_grad(set_to_none=True)
+        hs = st(ids, mask).reshape(N, -1)
+        torch.cuda.synchronize()
+        torch.cuda.reset_peak_memory_stats(dev)
+        base = torch.cuda.memory_allocated(dev)
+        kl = chunked_ensemble_kl(st, ts, hs, th, chunk=chunk)
+        kl.float().sum().backward()
+        torch.cuda.synchronize()
+        peak = torch.cuda.max_memory_allocated(dev) - base
+        res.append((kl.detach().float(), st.head_weight.grad.float().clone(), peak))
+    (k1, g1, p1), (k2, g2, p2) = res
+    assert p1 < 0.5 * full_bytes and p1 < p2 / 4, (p1, p2, full_bytes)
+    assert p2 > full_bytes, "the one-shot path should materialise the teacher logits"
+    assert torch.allclose(k1, k2, atol=2e-3, rtol=1e-2)
+    assert ((g1 - g2).norm() / g2.norm()).item() < 2e-2
