@@ -267,7 +267,8 @@ class FullyShardedEngine(_ShardedBase):
     def __init__(self, module: nn.Module, lr: float = 1e-5, betas=(0.9, 0.999), eps: float = 1e-8,
                  weight_decay: float = 0.0, max_grad_norm: float = 1.0, master_weights: bool = True,
                  dist_st: Optional[DistState] = None, group=None, tp_group=None, prefetch: bool = True,
-                 min_num_params: int = 0, cpu_offload: bool = False, **_unused):
+                 min_num_params: int = 0, cpu_offload: bool = False,
+                 grad_dtype: Optional[torch.dtype] = None, **_unused):
         if cpu_offload:
             raise ValueError("FSDP parameter CPU offload is not supported: sharded weights, fp32 "
                              "master and moments stay in HBM (288 GB per MI355X); set "
@@ -296,7 +297,9 @@ class FullyShardedEngine(_ShardedBase):
         self.step_count = 0
         self.params = params
         n = self.shard_numel
-        self.grad_shard = torch.zeros(n, dtype=self.dtype, device=self.device)
+        # micro-batch grads are reduce-scattered per unit in the param dtype and accumulated here:
+        # fp32 (grad_dtype) keeps 16-256 micro-batch accumulations exact to fp32 rounding
+        self.grad_shard = torch.zeros(n, dtype=grad_dtype or self.dtype, device=self.device)
         self.master = self.param_shard.float().clone() if master_weights else None
         self.exp_avg = torch.zeros(n, dtype=torch.float32, device=self.device)
         self.exp_avg_sq = torch.zeros(n, dtype=torch.float32, device=self.device)

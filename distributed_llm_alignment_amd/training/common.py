@@ -143,7 +143,7 @@ def make_engine(ctx: TrainContext, model, lr: float, betas=(0.9, 0.999), weight_
         from ..parallel.fsdp import FullyShardedEngine
 
         return FullyShardedEngine(model, lr=lr, betas=betas, weight_decay=weight_decay,
-                                  max_grad_norm=max_grad_norm,
+                                  max_grad_norm=max_grad_norm, grad_dtype=grad_dtypes(ctx)[0],
                                   master_weights=ctx.hw.get("master_weights", True), sp_size=sp,
                                   min_num_params=ctx.hw.get("fsdp_min_num_params", 0),
                                   cpu_offload=ctx.hw.get("cpu_offload", False), **groups)
