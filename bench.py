@@ -48,6 +48,8 @@ def parse(argv=None):
     ap.add_argument("--beta", type=float, default=0.1)
     ap.add_argument("--zero", type=int, default=None)
     ap.add_argument("--tp", type=int, default=1, help="tensor-parallel degree (dp = gpus / tp)")
+    ap.add_argument("--tp-seq", action="store_true",
+                    help="Megatron sequence parallel inside the TP group (reduce-scatter/all-gather)")
     ap.add_argument("--ep", type=int, default=1, help="expert-parallel degree for MoE models")
     ap.add_argument("--sp", type=int, default=1, help="Ulysses sequence-parallel degree (long context)")
     ap.add_argument("--fp8", action="store_true", help="MoE: e4m3 expert GEMMs in the forward")
@@ -139,8 +141,8 @@ def main(argv=None) -> int:
     for p in ref.parameters():
         p.requires_grad_(False)
     if mesh.tp > 1:
-        apply_tensor_parallel(policy, mesh.tp_group)
-        apply_tensor_parallel(ref, mesh.tp_group)
+        apply_tensor_parallel(policy, mesh.tp_group, sequence_parallel=args.tp_seq)
+        apply_tensor_parallel(ref, mesh.tp_group, sequence_parallel=args.tp_seq)
     if mesh.sp > 1:
         from distributed_llm_alignment_amd.parallel.sequence import apply_sequence_parallel
 

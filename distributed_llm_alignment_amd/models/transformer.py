@@ -77,12 +77,19 @@ class Attention(nn.Module):
         o_bias = cfg.attn_bias and cfg.arch in ("gpt2", "phi")
         self.o_bias = _param(H, device=device, dtype=dtype) if o_bias else None
         self.tp = None  # tensor-parallel group (parallel.tensor_parallel.apply_tensor_parallel)
+        self.tp_seq = None  # Megatron sequence parallel over the TP group (token-sharded stream)
         self.sp = None  # Ulysses sequence parallel (parallel.sequence.apply_sequence_parallel)
         self.h_local, self.kv_local = cfg.num_heads, cfg.num_kv_heads
 
     def forward(self, h, rope, kv_start, kv_end, positions, cache=None, layer_idx=0, segs=None):
         cfg = self.cfg
-        if self.tp is not None:
+        seq = self.tp_seq if (h.dim() == 2 and cache is None) else None
+        if seq is not None:
+            from ..parallel.tensor_parallel import sp_gather
+
+            B, T = positions.shape
+            h = sp_gather(h, seq).view(B, T, -1)
+        elif self.tp is not None:
             from ..parallel.tensor_parallel import tp_copy
 
             h = tp_copy(h, self.tp)
@@ -103,8 +110,11 @@ class Attention(nn.Module):
             a = cache.attend(layer_idx, qkv, rope, window)
         if self.tp is None:
             return _lin(a, self.o_proj, self.o_bias)
-        from ..parallel.tensor_parallel import tp_reduce
+        from ..parallel.tensor_parallel import sp_reduce_scatter, tp_grad_sum, tp_reduce
 
+        if seq is not None:
+            out = sp_reduce_scatter(ops.linear(a, self.o_proj, None).reshape(-1, cfg.hidden_size), seq)
+            return out + tp_grad_sum(self.o_bias, seq) if self.o_bias is not None else out
         out = tp_reduce(ops.linear(a, self.o_proj, None), self.tp)
         return out + self.o_bias if self.o_bias is not None else out
 
@@ -122,9 +132,15 @@ class MLP(nn.Module):
         self.down_proj = _param(H, Fd, device=device, dtype=dtype)
         self.down_bias = _param(H, device=device, dtype=dtype) if cfg.mlp_bias else None
         self.tp = None
+        self.tp_seq = None
 
     def forward(self, h):
-        if self.tp is not None:
+        seq = self.tp_seq if h.dim() == 2 else None
+        if seq is not None:
+            from ..parallel.tensor_parallel import sp_gather
+
+            h = sp_gather(h, seq)
+        elif self.tp is not None:
             from ..parallel.tensor_parallel import tp_copy
 
             h = tp_copy(h, self.tp)
@@ -145,15 +161,18 @@ class MLP(nn.Module):
             out = ops.swiglu_mlp(h, self.up_proj, self.down_proj)
             if self.tp is None:
                 return out
-            from ..parallel.tensor_parallel import tp_reduce
+            from ..parallel.tensor_parallel import sp_reduce_scatter, tp_reduce
 
-            return tp_reduce(out, self.tp)
+            return sp_reduce_scatter(out, seq) if seq is not None else tp_reduce(out, self.tp)
         u = ops.linear(h, self.up_proj, self.up_bias)
         m = ops.swiglu(u) if self.cfg.activation == "swiglu" else ops.gelu_new(u)
         if self.tp is None:
             return ops.linear(m, self.down_proj, self.down_bias)
-        from ..parallel.tensor_parallel import tp_reduce
+        from ..parallel.tensor_parallel import sp_reduce_scatter, tp_grad_sum, tp_reduce
 
+        if seq is not None:
+            out = sp_reduce_scatter(ops.linear(m, self.down_proj, None), seq)
+            return out + tp_grad_sum(self.down_bias, seq) if self.down_bias is not None else out
         out = tp_reduce(ops.linear(m, self.down_proj, None), self.tp)
         return out + self.down_bias if self.down_bias is not None else out
 
@@ -213,16 +232,26 @@ class DecoderLayer(nn.Module):
             self.ln2_b = _param(H, device=device, dtype=dtype) if bias else None
         self.attn = Attention(cfg, device, dtype)
         self.mlp = MoE(cfg, device, dtype) if cfg.is_moe else MLP(cfg, device, dtype)
+        self.tp_seq = None  # Megatron-SP: x / resid are this rank's [N/tp, H] token rows
 
     def forward(self, x, resid, rope, kv_start, kv_end, positions, cache=None, layer_idx=0, segs=None):
         cfg = self.cfg
         rms = cfg.norm_type == "rms"
-        h, resid = ops.add_norm(x, resid, self.ln1_w, self.ln1_b, cfg.norm_eps, rms)
+        seq = self.tp_seq if x.dim() == 2 else None
+        if seq is not None:
+            from ..parallel.tensor_parallel import tp_grad_sum as w_
+        else:
+            w_ = _ident
+        h, resid = ops.add_norm(x, resid, w_(self.ln1_w, seq), w_(self.ln1_b, seq), cfg.norm_eps, rms)
         a = self.attn(h, rope, kv_start, kv_end, positions, cache, layer_idx, segs)
         if cfg.parallel_block:
             return a + self.mlp(h), resid
-        h, resid = ops.add_norm(a, resid, self.ln2_w, self.ln2_b, cfg.norm_eps, rms)
+        h, resid = ops.add_norm(a, resid, w_(self.ln2_w, seq), w_(self.ln2_b, seq), cfg.norm_eps, rms)
         return self.mlp(h), resid
+
+
+def _ident(w, _seq=None):
+    return w
 
 
 class CausalLM(nn.Module):
@@ -248,6 +277,7 @@ class CausalLM(nn.Module):
         self.tp_size = 1
         self.tp_rank = 0
         self.vocab_parallel = None  # (vocab offset, local vocab) when embed/head are vocab-sharded
+        self.tp_seq = None          # Megatron sequence parallel over the TP group
         self.sp = None              # parallel.sequence.SequenceParallel: this rank holds 1/P of T
         self.layer_devices = None   # per-layer devices under parallel.layer_split (device_map)
         if self.lm_head is None and not headless:
@@ -312,6 +342,25 @@ class CausalLM(nn.Module):
             x = x + F.embedding(pos, self.wpe)
         return x
 
+    def _embed_tp_seq(self, input_ids, positions):
+        """Megatron-SP entry: this rank's [N/tp, H] token rows of the embedding (vocab-parallel
+        partial sums reduce-scattered straight into the token shards)."""
+        from ..parallel.tensor_parallel import sp_reduce_scatter, tp_grad_sum
+
+        seq = self.tp_seq
+        H = self.cfg.hidden_size
+        if self.vocab_parallel is not None:
+            off, V_l = self.vocab_parallel
+            local = input_ids - off
+            own = (local >= 0) & (local < V_l)
+            xp = F.embedding(local.clamp(0, V_l - 1), self.embed) * own.unsqueeze(-1).to(self.embed.dtype)
+            x = sp_reduce_scatter(xp.reshape(-1, H), seq)
+        else:
+            x = seq.local(F.embedding(input_ids, tp_grad_sum(self.embed, seq)).reshape(-1, H))
+        if self.wpe is not None:
+            x = x + seq.local(F.embedding(positions.long(), tp_grad_sum(self.wpe, seq)).reshape(-1, H))
+        return x
+
     def forward(self, input_ids: torch.Tensor, attention_mask: Optional[torch.Tensor] = None,
                 cache=None, segment_ids: Optional[torch.Tensor] = None) -> torch.Tensor:
         """`segment_ids` (optional, [B, T]): several sequences packed per row (see packed_layout)."""
@@ -327,11 +376,16 @@ class CausalLM(nn.Module):
         segs = None
         if segment_ids is not None:
             positions, segs = packed_layout(segment_ids)
-        if sp is not None:
-            if positions is None:
+        tp_seq = self.tp_seq if (sp is None and self.tp_seq is not None
+                                 and input_ids.numel() % self.tp_seq.tp == 0) else None
+        if sp is not None or tp_seq is not None:
+            if positions is None:  # explicit [B, T] positions also carry the shape to the layers
                 B, T = input_ids.shape
                 positions = torch.arange(T, device=input_ids.device, dtype=torch.int32).expand(B, T)
+        if sp is not None:
             x = self.embed_tokens(sp.local(input_ids), sp.local(positions))
+        elif tp_seq is not None:
+            x = self._embed_tp_seq(input_ids, positions)
         else:
             x = self.embed_tokens(input_ids, positions)
         resid = None
@@ -346,6 +400,12 @@ class CausalLM(nn.Module):
                 x, resid = layer(x, resid, self.rope, kv_start, kv_end, positions, segs=segs)
         if self.layer_devices is not None:
             x, resid = _hop(self.norm_w.device, x, resid)
+        if tp_seq is not None:
+            from ..parallel.tensor_parallel import sp_gather_replicated_grad, tp_grad_sum
+
+            h, _ = ops.add_norm(x, resid, tp_grad_sum(self.norm_w, tp_seq), tp_grad_sum(self.norm_b, tp_seq),
+                                self.cfg.norm_eps, self.cfg.norm_type == "rms")
+            return sp_gather_replicated_grad(h, tp_seq).view(*input_ids.shape, -1)
         h, _ = ops.add_norm(x, resid, self.norm_w, self.norm_b, self.cfg.norm_eps,
                             self.cfg.norm_type == "rms")
         return h

@@ -103,7 +103,8 @@ def parallelize(ctx: TrainContext, model):
     if m.tp > 1:
         from ..parallel.tensor_parallel import apply_tensor_parallel
 
-        apply_tensor_parallel(model, m.tp_group)
+        apply_tensor_parallel(model, m.tp_group,
+                              sequence_parallel=bool(ctx.hw.get("tp_sequence_parallel", False)))
     if m.sp > 1:
         from ..parallel.sequence import apply_sequence_parallel
 

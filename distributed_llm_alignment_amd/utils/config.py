@@ -112,6 +112,8 @@ def hardware_parallel(cfg: Dict[str, Any]) -> Dict[str, Any]:
         "tp_size": int(hw.get("tp_size", 1) or 1),
         "ep_size": int(hw.get("ep_size", 1) or 1),
         "sp_size": int(hw.get("sp_size", 1) or 1),  # Ulysses sequence parallel (parallel.sequence)
+        # Megatron sequence parallel inside the TP group (reduce-scatter / all-gather, sharded norms)
+        "tp_sequence_parallel": bool(hw.get("tp_sequence_parallel", False)),
         "bucket_mb": float(hw.get("bucket_mb", 256)),
         "master_weights": bool(hw.get("master_weights", True)),
         "grad_dtype": hw.get("grad_dtype", "auto"),      # fp32 main grads (auto: grad_accum >= 16)

@@ -343,7 +343,8 @@ def _tp_trainers(rank, world, root, hw=None):
     return losses
 
 
-@pytest.mark.parametrize("hw", [None, {"zero_stage": 3, "gradient_accumulation_steps": 2}])
+@pytest.mark.parametrize("hw", [None, {"zero_stage": 3, "gradient_accumulation_steps": 2},
+                                {"tp_size": 2, "tp_sequence_parallel": True, "gradient_accumulation_steps": 1}])
 def test_trainers_with_tensor_parallel(tmp_path, hw):
     """SFT then DPO with hardware.tp_size=2 (or ZeRO-3) on 2 gloo ranks: checkpoints hold FULL
     (gathered) weights that load into an unsharded model, and the DPO loss starts at ln 2."""
@@ -635,3 +636,57 @@ def _single_fp32_sum():
     a = _accum_grads(torch.float32, n_micro=4, rank=0, world=2)
     b = _accum_grads(torch.float32, n_micro=4, rank=1, world=2)
     return a + b
+
+
+# ---------------------------------------------------------- Megatron sequence parallel (TP-SP)
+def _tp_seq_vs_tp(rank, world, name, ckpt):
+    import torch
+
+    from distributed_llm_alignment_amd.models import build_model, get_config
+    from distributed_llm_alignment_amd.parallel.mesh import build_mesh
+    from distributed_llm_alignment_amd.parallel.tensor_parallel import apply_tensor_parallel
+
+    mesh = build_mesh(tp=world)
+    cfg = get_config(name)
+    dense = build_model(cfg, device="cpu", seed=0)
+    tps = build_model(cfg, device="cpu", seed=0)
+    apply_tensor_parallel(tps, mesh.tp_group, sequence_parallel=True)
+    if ckpt:
+        tps.gradient_checkpointing_enable()
+        tps.train()
+    g = torch.Generator().manual_seed(5)
+    ids = torch.randint(3, cfg.vocab_size, (2, 12), generator=g)
+    mask = torch.ones_like(ids)
+    mask[1, 9:] = 0
+    a = dense.sequence_logprob(ids, mask)
+    b = tps.sequence_logprob(ids, mask)
+    a.sum().backward()
+    b.sum().backward()
+    D, hq = cfg.head_dim, cfg.num_heads // world
+    Fl = cfg.intermediate_size // world
+    out = [a, b,
+           (dense.layers[0].attn.qkv_proj.grad[rank * hq * D:(rank + 1) * hq * D]
+            - tps.layers[0].attn.qkv_proj.grad[: hq * D]).abs().max(),
+           (dense.layers[1].mlp.down_proj.grad[:, rank * Fl:(rank + 1) * Fl]
+            - tps.layers[1].mlp.down_proj.grad).abs().max(),
+           (dense.norm_w.grad - tps.norm_w.grad).abs().max(),
+           (dense.layers[1].ln1_w.grad - tps.layers[1].ln1_w.grad).abs().max()]
+    if tps.vocab_parallel is not None:
+        Vl = cfg.vocab_size // world
+        out.append((dense.embed.grad[rank * Vl:(rank + 1) * Vl] - tps.embed.grad).abs().max())
+    else:
+        out.append((dense.embed.grad - tps.embed.grad).abs().max())
+    if tps.wpe is not None:
+        out.append((dense.wpe.grad - tps.wpe.grad).abs().max())
+    return out
+
+
+@pytest.mark.parametrize("name,ckpt", [("tiny-llama", False), ("tiny-gpt2", False), ("tiny-llama", True)])
+def test_tp_sequence_parallel_matches_dense(name, ckpt):
+    """TP=2 with Megatron-SP (token-sharded residual stream, reduce-scatter/all-gather, TP-summed
+    norm/bias/wpe grads) == the unsharded model: log-probs and every gradient kind."""
+    res = run_ranks(_tp_seq_vs_tp, 2, (name, ckpt))
+    for r in (0, 1):
+        a, b, *errs = res[r]
+        assert torch.allclose(a, b, atol=1e-5), (a, b)
+        assert max(float(e) for e in errs) < 2e-5, errs

@@ -208,7 +208,7 @@ def test_rccl_fsdp_matches_zero1():
 def _pairs_mesh(kind):
     from distributed_llm_alignment_amd.parallel.mesh import build_mesh
 
-    return build_mesh(**{kind: 2})
+    return build_mesh(**{("tp" if kind == "tpseq" else kind): 2})
 
 
 def _logprob_vs_dense(rank, world, dev, kind):
@@ -221,10 +221,10 @@ def _logprob_vs_dense(rank, world, dev, kind):
     mesh = _pairs_mesh(kind)
     dense = build_model(cfg, device=dev, dtype=torch.bfloat16, seed=0)
     par = build_model(cfg, device=dev, dtype=torch.bfloat16, seed=0)
-    if kind == "tp":
+    if kind in ("tp", "tpseq"):
         from distributed_llm_alignment_amd.parallel.tensor_parallel import apply_tensor_parallel
 
-        apply_tensor_parallel(par, mesh.tp_group)
+        apply_tensor_parallel(par, mesh.tp_group, sequence_parallel=kind == "tpseq")
     elif kind == "sp":
         from distributed_llm_alignment_amd.parallel.sequence import apply_sequence_parallel
 
@@ -253,7 +253,7 @@ def _logprob_vs_dense(rank, world, dev, kind):
 
 
 @needs2
-@pytest.mark.parametrize("kind", ["tp", "sp", "ep"])
+@pytest.mark.parametrize("kind", ["tp", "tpseq", "sp", "ep"])
 def test_rccl_parallel_logprob_matches_dense(kind):
     import numpy as np
 
