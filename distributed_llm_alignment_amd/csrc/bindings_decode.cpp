@@ -10,9 +10,13 @@
 
 namespace dla {
 
-void launch_decode_attn(const bf16_t*, int64_t, int64_t, const bf16_t*, const bf16_t*, int64_t,
+void launch_decode_attn(const bf16_t*, int64_t, int64_t, bf16_t*, bf16_t*, int64_t,
                         int64_t, int64_t, const int*, const int*, int, float, int, int, int, int,
                         int, float*, float*, bf16_t*, int64_t, int64_t, hipStream_t);
+void launch_decode_attn_rope(const bf16_t*, int64_t, const float*, const float*, const int*,
+                             const int64_t*, int, bf16_t*, bf16_t*, int64_t, int64_t, int64_t,
+                             const int*, const int*, int, float, int, int, int, int, int, float*,
+                             float*, bf16_t*, int64_t, int64_t, hipStream_t);
 int decode_num_splits(int Tmax);
 void launch_rope_cache(const bf16_t*, int64_t, bf16_t*, bf16_t*, bf16_t*, int64_t, int64_t,
                        int64_t, const int64_t*, const float*, const float*, const int*, int, int,
@@ -118,7 +122,7 @@ at::Tensor decode_attn(const at::Tensor& q, const at::Tensor& k_cache, const at:
   auto part_o = at::empty({B, Hq, nsplit, D}, fopt);
   auto part_ml = at::empty({B, Hq, nsplit, 2}, fopt);
   auto out = at::empty({B, Hq, D}, q.options());
-  launch_decode_attn(cbp(q), q.stride(0), q.stride(1), cbp(k_cache), cbp(v_cache),
+  launch_decode_attn(cbp(q), q.stride(0), q.stride(1), bp(k_cache), bp(v_cache),
                      k_cache.stride(0), k_cache.stride(1), k_cache.stride(2),
                      kv_len.data_ptr<int>(), ks, static_cast<int>(window),
                      static_cast<float>(scale * 1.4426950408889634), (int)B, (int)Hq, (int)Hkv,
@@ -163,6 +167,66 @@ at::Tensor rope_cache_write(const at::Tensor& qkv, const at::Tensor& cos, const 
   return q;
 }
 
+// One decode step's attention with the rope + cache write of the newest token fused in (one
+// launch pair instead of rope_cache_write + decode_attn): qkv [B, 1, (Hq + 2 Hkv) D] raw row,
+// caches [B, Tmax, Hkv, D] (row `slot` is written), kv_len = slot + 1 (device).
+at::Tensor decode_attn_rope(const at::Tensor& qkv, const at::Tensor& cos, const at::Tensor& sin,
+                            const at::Tensor& pos, at::Tensor& k_cache, at::Tensor& v_cache,
+                            const at::Tensor& slot, const at::Tensor& kv_len,
+                            const c10::optional<at::Tensor>& kv_start, int64_t window, double scale,
+                            int64_t Hq, int64_t Hkv, int64_t D, int64_t rot) {
+  check_bf16(qkv, "qkv");
+  check_bf16(k_cache, "k_cache");
+  check_bf16(v_cache, "v_cache");
+  check_f32(cos, "cos");
+  check_f32(sin, "sin");
+  check_i32(pos, "pos");
+  check_i32(kv_len, "kv_len");
+  check_cuda(slot, "slot");
+  TORCH_CHECK(slot.scalar_type() == at::kLong && slot.numel() >= 1, "slot int64");
+  const int64_t B = qkv.size(0);
+  TORCH_CHECK(qkv.dim() == 3 && qkv.size(1) == 1 && qkv.size(2) == (Hq + 2 * Hkv) * D &&
+                  qkv.stride(2) == 1 && qkv.stride(0) % 8 == 0,
+              "qkv [B, 1, (Hq+2Hkv)D] with 16-byte aligned rows");
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(0) == B && k_cache.size(2) == Hkv &&
+                  k_cache.size(3) == D && k_cache.sizes() == v_cache.sizes() &&
+                  k_cache.strides() == v_cache.strides() && k_cache.stride(3) == 1,
+              "caches [B, Tmax, Hkv, D]");
+  TORCH_CHECK(D == 64 || D == 128, "decode attention supports head_dim 64 or 128");
+  TORCH_CHECK(Hq % Hkv == 0, "Hq % Hkv");
+  const int64_t G = Hq / Hkv;
+  TORCH_CHECK(G == 1 || G == 2 || G == 4 || G == 8, "GQA group size must be 1, 2, 4 or 8");
+  TORCH_CHECK(rot % 16 == 0 && rot <= D && rot > 0, "rot % 16 == 0, 0 < rot <= D");
+  TORCH_CHECK(cos.is_contiguous() && sin.is_contiguous() && cos.size(-1) == rot / 2, "rope tables");
+  TORCH_CHECK(pos.numel() == B && pos.is_contiguous(), "pos [B]");
+  TORCH_CHECK(k_cache.stride(1) % 8 == 0 && k_cache.stride(2) % 8 == 0 && k_cache.stride(0) % 8 == 0,
+              "16-byte aligned cache rows");
+  check_aligned16(qkv, "qkv");
+  check_aligned16(k_cache, "k_cache");
+  check_aligned16(v_cache, "v_cache");
+  const int* ks = nullptr;
+  if (kv_start && kv_start->defined()) {
+    check_i32(*kv_start, "kv_start");
+    TORCH_CHECK(kv_start->numel() == B && kv_start->is_contiguous(), "kv_start [B]");
+    ks = kv_start->data_ptr<int>();
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA g(qkv.device());
+  const int64_t Tmax = k_cache.size(1);
+  const int nsplit = decode_num_splits(static_cast<int>(Tmax));
+  auto fopt = qkv.options().dtype(at::kFloat);
+  auto part_o = at::empty({B, Hq, nsplit, D}, fopt);
+  auto part_ml = at::empty({B, Hq, nsplit, 2}, fopt);
+  auto out = at::empty({B, Hq, D}, qkv.options());
+  launch_decode_attn_rope(cbp(qkv), qkv.stride(0), cos.data_ptr<float>(), sin.data_ptr<float>(),
+                          pos.data_ptr<int>(), slot.data_ptr<int64_t>(), (int)rot, bp(k_cache),
+                          bp(v_cache), k_cache.stride(0), k_cache.stride(1), k_cache.stride(2),
+                          kv_len.data_ptr<int>(), ks, static_cast<int>(window),
+                          static_cast<float>(scale * 1.4426950408889634), (int)B, (int)Hq, (int)Hkv,
+                          (int)D, (int)Tmax, part_o.data_ptr<float>(), part_ml.data_ptr<float>(),
+                          bp(out), out.stride(0), out.stride(1), cur_stream(qkv));
+  return out;
+}
+
 at::Tensor sample_tokens(const at::Tensor& logits, double temperature, int64_t top_k,
                          double top_p, bool greedy, const at::Tensor& rng) {
   check_cuda(logits, "logits");
@@ -198,6 +262,7 @@ at::Tensor sample_tokens(const at::Tensor& logits, double temperature, int64_t t
 TORCH_LIBRARY_FRAGMENT(dla, m) {
   m.def("decode_attn(Tensor q, Tensor k_cache, Tensor v_cache, Tensor kv_len, Tensor? kv_start, int window, float scale) -> Tensor");
   m.def("rope_cache_write(Tensor qkv, Tensor cos, Tensor sin, Tensor pos, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor slot, int Hq, int Hkv, int D, int rot) -> Tensor");
+  m.def("decode_attn_rope(Tensor qkv, Tensor cos, Tensor sin, Tensor pos, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor slot, Tensor kv_len, Tensor? kv_start, int window, float scale, int Hq, int Hkv, int D, int rot) -> Tensor");
   m.def("sample_tokens(Tensor logits, float temperature, int top_k, float top_p, bool greedy, Tensor rng) -> Tensor");
   m.def("skinny_gemm(Tensor x, Tensor w, Tensor(a!) counters, bool swiglu, bool glu_out=False) -> Tensor");
 }
@@ -206,5 +271,6 @@ TORCH_LIBRARY_IMPL(dla, CUDA, m) {
   m.impl("decode_attn", &dla::decode_attn);
   m.impl("sample_tokens", &dla::sample_tokens);
   m.impl("rope_cache_write", &dla::rope_cache_write);
+  m.impl("decode_attn_rope", &dla::decode_attn_rope);
   m.impl("skinny_gemm", &dla::skinny_gemm);
 }

@@ -22,15 +22,50 @@ constexpr int kDecChunk = 128;  // keys per block (4 waves x 32)
 
 // Lanes cooperate on rows: LPK = D/8 lanes x 16 B cover one K/V row (coalesced 256-byte rows
 // for D = 128), KPI = 64/LPK rows per wave instruction.
-template <int D, int G>
+// Fused decode-step prologue (ROPE = true): instead of a separate rope + cache-write launch, the
+// kernel reads the raw qkv row of the newest token: every block rotates its G query heads while
+// filling `qs`; the newest key's K/V (rotated k, plain v) come from registers rather than the
+// cache, and the block whose split holds that key writes them into the cache slot for the next
+// steps. Rounding matches rope_cache_kernel + the unfused kernel (q and k rounded to bf16 after
+// the rotation), so fused and unfused decode agree bitwise.
+struct DecRope {
+  const bf16_t* qkv;  // [B, (Hq + 2 Hkv) * D] rows of the newest token
+  int64_t ld;
+  const float* cos_t;  // [P, rot/2]
+  const float* sin_t;
+  const int* pos;      // [B] rope position of the newest token
+  const int64_t* slot; // cache slot of the newest token (== kv_len - 1)
+  int rot;
+  int Hkv;
+};
+
+// 8 rotated dims [d0, d0 + 8) of one head (rotate-half over the first `rot` dims), rounded to bf16
+__device__ __forceinline__ bf16x8 dec_rope8(const bf16_t* src, int d0, int rot, const float* cs,
+                                            const float* sn) {
+  const bf16x8 x = load_bf16x8(src + d0);
+  if (d0 >= rot) return x;
+  const int half = rot >> 1;
+  const bool lo = d0 < half;
+  const bf16x8 y = load_bf16x8(src + (lo ? d0 + half : d0 - half));
+  const int c0 = lo ? d0 : d0 - half;
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float c = cs[c0 + j], s = sn[c0 + j], a = bf2f(x[j]), bb = bf2f(y[j]);
+    o[j] = f2bf(lo ? a * c - bb * s : a * c + bb * s);
+  }
+  return o;
+}
+
+template <int D, int G, bool ROPE>
 __global__ __launch_bounds__(256) void decode_attn_kernel(
     const bf16_t* __restrict__ q, int64_t q_sb, int64_t q_sh,     // q [B, Hq, D]
-    const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,  // [B, Tmax, Hkv, D]
+    bf16_t* __restrict__ kc, bf16_t* __restrict__ vc,              // [B, Tmax, Hkv, D]
     int64_t c_sb, int64_t c_st, int64_t c_sh, const int* __restrict__ kv_len,
     const int* __restrict__ kv_start, int window, float scale_log2, int nsplit,
     float* __restrict__ part_o,  // [B, Hq, nsplit, D]
     float* __restrict__ part_ml, // [B, Hq, nsplit, 2]
-    int Hq) {
+    int Hq, DecRope rp) {
   constexpr int LPK = D / 8, KPI = 64 / LPK, KPW = kDecChunk / 4;
   __shared__ float qs[G][D];
   __shared__ float ps[G][kDecChunk];
@@ -39,6 +74,23 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
   const int split = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int len = kv_len[0];
+  // fused prologue: the newest token's K / V slice of this lane (dims dl .. dl + 7)
+  bf16x8 knew = {}, vnew = {};
+  int newest = -1;
+  if constexpr (ROPE) {
+    newest = static_cast<int>(rp.slot[0]);
+    const int dl0 = (lane % LPK) * 8;
+    const bf16_t* row = rp.qkv + (int64_t)b * rp.ld;
+    const int half = rp.rot >> 1;
+    const float* cs = rp.cos_t + (int64_t)rp.pos[b] * half;
+    const float* sn = rp.sin_t + (int64_t)rp.pos[b] * half;
+    knew = dec_rope8(row + (int64_t)(Hq + hk) * D, dl0, rp.rot, cs, sn);
+    vnew = load_bf16x8(row + (int64_t)(Hq + rp.Hkv + hk) * D + dl0);
+    if (split == newest / kDecChunk && wv == 0 && lane < LPK) {  // cache write for later steps
+      store_bf16x8(kc + (int64_t)b * c_sb + (int64_t)newest * c_st + (int64_t)hk * c_sh + dl0, knew);
+      store_bf16x8(vc + (int64_t)b * c_sb + (int64_t)newest * c_st + (int64_t)hk * c_sh + dl0, vnew);
+    }
+  }
   int lo = kv_start ? kv_start[b] : 0;
   if (window > 0) lo = max(lo, len - window);
   const int base = split * kDecChunk;
@@ -51,9 +103,22 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
     }
     return;
   }
-  for (int i = tid; i < G * D; i += 256) {
-    const int g = i / D, d = i % D;
-    qs[g][d] = bf2f(q[(int64_t)b * q_sb + (int64_t)(hk * G + g) * q_sh + d]) * scale_log2;
+  if constexpr (ROPE) {
+    const bf16_t* row = rp.qkv + (int64_t)b * rp.ld;
+    const int half = rp.rot >> 1;
+    const float* cs = rp.cos_t + (int64_t)rp.pos[b] * half;
+    const float* sn = rp.sin_t + (int64_t)rp.pos[b] * half;
+    for (int i = tid; i < G * (D / 8); i += 256) {
+      const int g = i / (D / 8), d0 = (i % (D / 8)) * 8;
+      const bf16x8 qv = dec_rope8(row + (int64_t)(hk * G + g) * D, d0, rp.rot, cs, sn);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qs[g][d0 + j] = bf2f(qv[j]) * scale_log2;
+    }
+  } else {
+    for (int i = tid; i < G * D; i += 256) {
+      const int g = i / D, d = i % D;
+      qs[g][d] = bf2f(q[(int64_t)b * q_sb + (int64_t)(hk * G + g) * q_sh + d]) * scale_log2;
+    }
   }
   __syncthreads();
   const int sub = lane / LPK, dl = (lane % LPK) * 8;
@@ -73,6 +138,9 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
   for (int it = 0; it < NIT; ++it) {
     const int key = min(max(base + wv * KPW + it * KPI + sub, k0), k1 - 1);
     kvr[it] = load_bf16x8(kbase + (int64_t)key * c_st);
+    if constexpr (ROPE) {
+      if (key == newest) kvr[it] = knew;
+    }
   }
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
@@ -137,6 +205,9 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
   for (int it = 0; it < NIT; ++it) {
     const int key = min(max(base + wv * KPW + it * KPI + sub, k0), k1 - 1);
     vvr[it] = load_bf16x8(vbase + (int64_t)key * c_st);
+    if constexpr (ROPE) {
+      if (key == newest) vvr[it] = vnew;
+    }
   }
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
@@ -255,18 +326,27 @@ __global__ __launch_bounds__(64) void decode_combine_kernel(const float* __restr
 }
 
 template <int D>
-static void launch_decode_d(const bf16_t* q, int64_t q_sb, int64_t q_sh, const bf16_t* kc,
-                            const bf16_t* vc, int64_t c_sb, int64_t c_st, int64_t c_sh,
+static void launch_decode_d(const bf16_t* q, int64_t q_sb, int64_t q_sh, bf16_t* kc,
+                            bf16_t* vc, int64_t c_sb, int64_t c_st, int64_t c_sh,
                             const int* kv_len, const int* kv_start, int window, float scale_log2,
                             int B, int Hq, int Hkv, int Tmax, float* part_o, float* part_ml,
-                            bf16_t* out, int64_t o_sb, int64_t o_sh, hipStream_t st) {
+                            bf16_t* out, int64_t o_sb, int64_t o_sh, const DecRope* rp,
+                            hipStream_t st) {
   const int G = Hq / Hkv;
   const int nsplit = (Tmax + kDecChunk - 1) / kDecChunk;
   dim3 grid(nsplit, Hkv, B);
+  const DecRope r0 = rp ? *rp : DecRope{};
 #define DLA_DEC(GG)                                                                              \
-  decode_attn_kernel<D, GG><<<grid, 256, 0, st>>>(q, q_sb, q_sh, kc, vc, c_sb, c_st, c_sh,      \
-                                                   kv_len, kv_start, window, scale_log2, nsplit, \
-                                                   part_o, part_ml, Hq)
+  if (rp)                                                                                        \
+    decode_attn_kernel<D, GG, true><<<grid, 256, 0, st>>>(q, q_sb, q_sh, kc, vc, c_sb, c_st,    \
+                                                          c_sh, kv_len, kv_start, window,       \
+                                                          scale_log2, nsplit, part_o, part_ml,  \
+                                                          Hq, r0);                              \
+  else                                                                                           \
+    decode_attn_kernel<D, GG, false><<<grid, 256, 0, st>>>(q, q_sb, q_sh, kc, vc, c_sb, c_st,   \
+                                                           c_sh, kv_len, kv_start, window,      \
+                                                           scale_log2, nsplit, part_o, part_ml, \
+                                                           Hq, r0)
   switch (G) {
     case 1: DLA_DEC(1); break;
     case 2: DLA_DEC(2); break;
@@ -280,17 +360,33 @@ static void launch_decode_d(const bf16_t* q, int64_t q_sb, int64_t q_sh, const b
 
 int decode_num_splits(int Tmax) { return (Tmax + kDecChunk - 1) / kDecChunk; }
 
-void launch_decode_attn(const bf16_t* q, int64_t q_sb, int64_t q_sh, const bf16_t* kc,
-                        const bf16_t* vc, int64_t c_sb, int64_t c_st, int64_t c_sh,
+void launch_decode_attn(const bf16_t* q, int64_t q_sb, int64_t q_sh, bf16_t* kc,
+                        bf16_t* vc, int64_t c_sb, int64_t c_st, int64_t c_sh,
                         const int* kv_len, const int* kv_start, int window, float scale_log2, int B,
                         int Hq, int Hkv, int D, int Tmax, float* part_o, float* part_ml,
                         bf16_t* out, int64_t o_sb, int64_t o_sh, hipStream_t st) {
   if (D == 128)
     launch_decode_d<128>(q, q_sb, q_sh, kc, vc, c_sb, c_st, c_sh, kv_len, kv_start, window,
-                         scale_log2, B, Hq, Hkv, Tmax, part_o, part_ml, out, o_sb, o_sh, st);
+                         scale_log2, B, Hq, Hkv, Tmax, part_o, part_ml, out, o_sb, o_sh, nullptr, st);
   else
     launch_decode_d<64>(q, q_sb, q_sh, kc, vc, c_sb, c_st, c_sh, kv_len, kv_start, window,
-                        scale_log2, B, Hq, Hkv, Tmax, part_o, part_ml, out, o_sb, o_sh, st);
+                        scale_log2, B, Hq, Hkv, Tmax, part_o, part_ml, out, o_sb, o_sh, nullptr, st);
+}
+
+// rope + cache write of the newest token fused into the decode attention (see DecRope)
+void launch_decode_attn_rope(const bf16_t* qkv, int64_t ld, const float* cos_t, const float* sin_t,
+                             const int* pos, const int64_t* slot, int rot, bf16_t* kc, bf16_t* vc,
+                             int64_t c_sb, int64_t c_st, int64_t c_sh, const int* kv_len,
+                             const int* kv_start, int window, float scale_log2, int B, int Hq,
+                             int Hkv, int D, int Tmax, float* part_o, float* part_ml, bf16_t* out,
+                             int64_t o_sb, int64_t o_sh, hipStream_t st) {
+  const DecRope rp{qkv, ld, cos_t, sin_t, pos, slot, rot, Hkv};
+  if (D == 128)
+    launch_decode_d<128>(nullptr, 0, 0, kc, vc, c_sb, c_st, c_sh, kv_len, kv_start, window,
+                         scale_log2, B, Hq, Hkv, Tmax, part_o, part_ml, out, o_sb, o_sh, &rp, st);
+  else
+    launch_decode_d<64>(nullptr, 0, 0, kc, vc, c_sb, c_st, c_sh, kv_len, kv_start, window,
+                        scale_log2, B, Hq, Hkv, Tmax, part_o, part_ml, out, o_sb, o_sh, &rp, st);
 }
 
 }  // namespace dla

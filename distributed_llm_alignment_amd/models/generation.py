@@ -10,6 +10,7 @@ to the cache through the same kernel with causal offset.
 """
 from __future__ import annotations
 
+import math
 import os
 import weakref
 from dataclasses import dataclass
@@ -83,6 +84,14 @@ class KVCache:
         if T == 1 and self.len > 0 and self.fast_decode:
             # device-indexed cache write + split-KV decode kernel (graph-capturable)
             D = cfg.head_dim
+            if rope is not None and rope.rot_dim % 16 == 0 and FUSED_DECODE_ROPE:
+                # rope + cache write of the newest token fused into the attention launch
+                cos, sin = rope.tables(qkv.device)
+                o = ops._ext.require().decode_attn_rope(
+                    qkv, cos, sin, self.pos.view(-1), self.k[layer], self.v[layer], self.slot,
+                    self.kv_len, self.kv_start, window, 1.0 / math.sqrt(D), self.h_local, self.kv_local, D,
+                    rope.rot_dim)
+                return o.reshape(B, 1, self.h_local * D)
             if rope is not None and rope.rot_dim % 16 == 0:
                 cos, sin = rope.tables(qkv.device)
                 q = ops._ext.require().rope_cache_write(qkv, cos, sin, self.pos.view(-1), self.k[layer],
@@ -248,6 +257,8 @@ class _DecodeGraph:
 # not kept, entries die with their model (weakref callback), and `release_graph_cache(model)`
 # frees one model's entry on demand.
 GRAPH_REUSE = os.environ.get("DLA_GRAPH_REUSE", "1") != "0"
+# rope + KV-cache write of the newest token fused into the decode attention launch
+FUSED_DECODE_ROPE = os.environ.get("DLA_FUSED_DECODE_ROPE", "1") != "0"
 GRAPH_REUSE_MAX_BYTES = int(float(os.environ.get("DLA_GRAPH_REUSE_MAX_GB", "24")) * 2 ** 30)
 PROMPT_BUCKET = 64
 _GRAPH_SLOT: dict = {}  # id(model) -> (weakref(model), key, cache, decode graph)

@@ -302,3 +302,32 @@ def test_skinny_glu_epilogue_matches_unfused(M, F, K):
         r = (torch.nn.functional.silu(gg) * uu)
         err = (m.float() - r).abs().max().item()
         assert err <= 3e-2 * max(1.0, r.abs().max().item()), err
+
+
+@pytest.mark.parametrize("D,Hq,Hkv,rot", [(128, 32, 8, 128), (64, 8, 8, 32), (128, 8, 1, 64)])
+def test_fused_rope_decode_attention_matches_unfused(D, Hq, Hkv, rot):
+    """decode_attn_rope (rope + cache write of the newest token inside the attention launch) ==
+    rope_cache_write + decode_attn, bitwise: output and the written cache row."""
+    from distributed_llm_alignment_amd.ops import RotaryCache, _ext
+
+    C = _ext.require()
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(7)
+    B, Tmax, L = 3, 300, 257  # newest token at slot 256: first key of a fresh 128-key split
+    rope = RotaryCache(rot, 10000.0, 4096, None)
+    cos, sin = rope.tables(dev)
+    kc = torch.randn(B, Tmax, Hkv, D, device=dev, generator=g).to(torch.bfloat16)
+    vc = torch.randn(B, Tmax, Hkv, D, device=dev, generator=g).to(torch.bfloat16)
+    qkv = torch.randn(B, 1, (Hq + 2 * Hkv) * D, device=dev, generator=g).to(torch.bfloat16)
+    kv_start = torch.tensor([0, 5, 40], device=dev, dtype=torch.int32)
+    pos = (L - 1 - kv_start).to(torch.int32)
+    slot = torch.tensor([L - 1], device=dev, dtype=torch.long)
+    kv_len = torch.tensor([L], device=dev, dtype=torch.int32)
+    k1, v1 = kc.clone(), vc.clone()
+    q = C.rope_cache_write(qkv, cos, sin, pos, k1, v1, slot, Hq, Hkv, D, rot)
+    ref = C.decode_attn(q, k1, v1, kv_len, kv_start, 0, D ** -0.5)
+    k2, v2 = kc.clone(), vc.clone()
+    out = C.decode_attn_rope(qkv, cos, sin, pos, k2, v2, slot, kv_len, kv_start, 0, D ** -0.5, Hq, Hkv, D, rot)
+    torch.cuda.synchronize()
+    assert torch.equal(k1, k2) and torch.equal(v1, v2)
+    assert torch.equal(out, ref)
