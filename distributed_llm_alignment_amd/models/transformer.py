@@ -134,6 +134,18 @@ class MLP(nn.Module):
         self.tp = None
         self.tp_seq = None
 
+    def decode_norm_glu(self, a, resid, norm_w, eps):
+        """Decode rows: (mlp(RMSNorm(a + resid) * norm_w), a + resid) with the add + norm fused
+        into the skinny gate|up launch; None when not eligible."""
+        if (self.cfg.activation != "swiglu" or self.up_bias is not None or self.down_bias is not None
+                or self.tp is not None):
+            return None
+        r = ops.decode.skinny_glu_norm(a, resid, norm_w, eps, self.up_proj)
+        if r is None:
+            return None
+        m, s = r
+        return _lin(m, self.down_proj, None), s
+
     def forward(self, h):
         seq = self.tp_seq if h.dim() == 2 else None
         if seq is not None:
@@ -246,6 +258,10 @@ class DecoderLayer(nn.Module):
         a = self.attn(h, rope, kv_start, kv_end, positions, cache, layer_idx, segs)
         if cfg.parallel_block:
             return a + self.mlp(h), resid
+        if cache is not None and rms and self.ln2_b is None and isinstance(self.mlp, MLP):
+            fused = self.mlp.decode_norm_glu(a, resid, self.ln2_w, cfg.norm_eps)
+            if fused is not None:  # decode: residual add + RMSNorm inside the gate|up launch
+                return fused
         h, resid = ops.add_norm(a, resid, w_(self.ln2_w, seq), w_(self.ln2_b, seq), cfg.norm_eps, rms)
         return self.mlp(h), resid
 
