@@ -19,6 +19,49 @@ void launch_moe_combine_bwd(const bf16_t*, const bf16_t*, const int*, const floa
                             int, bf16_t*, float*, hipStream_t);
 
 void launch_quant_fp8_rows(const bf16_t*, int64_t, int64_t, int, uint8_t*, float*, hipStream_t);
+void launch_embed_fwd(const bf16_t*, int64_t, const int64_t*, int64_t, int, int64_t, bf16_t*, hipStream_t);
+void launch_embed_bwd(const int64_t*, const int64_t*, const bf16_t*, int64_t, int, float*, void*, bool,
+                      int64_t, hipStream_t);
+
+// token embedding gather: out[n] = w[ids[n]] (ids int64 [N], w [V, H] bf16)
+at::Tensor embed_fwd(const at::Tensor& w, const at::Tensor& ids) {
+  check_bf16(w, "w");
+  check_cuda(ids, "ids");
+  TORCH_CHECK(ids.scalar_type() == at::kLong && ids.dim() == 1 && ids.is_contiguous(), "ids int64 [N]");
+  TORCH_CHECK(w.dim() == 2 && w.stride(1) == 1 && w.stride(0) % 8 == 0 && w.size(1) % 8 == 0,
+              "w [V, H], H % 8 == 0, 16-byte aligned rows");
+  check_aligned16(w, "w");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(w.device());
+  auto out = at::empty({ids.size(0), w.size(1)}, w.options());
+  launch_embed_fwd(cbp(w), w.stride(0), ids.data_ptr<int64_t>(), ids.size(0), (int)w.size(1),
+                   w.size(0), bp(out), cur_stream(w));
+  return out;
+}
+
+// grad[sid[j]] += dy[perm[j]] for the sorted ids (deterministic run sums, no atomics), in place
+// into grad [V, H] (bf16 or fp32: the engine's main-grad view)
+void embed_bwd(const at::Tensor& sid, const at::Tensor& perm, const at::Tensor& dy, at::Tensor grad) {
+  check_cuda(sid, "sid");
+  check_cuda(perm, "perm");
+  check_bf16(dy, "dy");
+  check_cuda(grad, "grad");
+  TORCH_CHECK(sid.scalar_type() == at::kLong && perm.scalar_type() == at::kLong && sid.dim() == 1 &&
+                  sid.sizes() == perm.sizes() && sid.is_contiguous() && perm.is_contiguous(),
+              "sid / perm int64 [N]");
+  TORCH_CHECK(grad.scalar_type() == at::kBFloat16 || grad.scalar_type() == at::kFloat, "grad bf16 / fp32");
+  TORCH_CHECK(dy.dim() == 2 && dy.is_contiguous() && dy.size(0) == sid.size(0) && dy.size(1) % 8 == 0,
+              "dy [N, H] contiguous, H % 8 == 0");
+  TORCH_CHECK(grad.dim() == 2 && grad.size(1) == dy.size(1) && grad.stride(1) == 1 && grad.stride(0) % 8 == 0,
+              "grad [V, H] with 16-byte aligned rows");
+  check_aligned16(dy, "dy");
+  check_aligned16(grad, "grad");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(dy.device());
+  const int64_t N = sid.size(0);
+  auto scratch = at::empty({N, dy.size(1)}, dy.options().dtype(at::kFloat));
+  launch_embed_bwd(sid.data_ptr<int64_t>(), perm.data_ptr<int64_t>(), cbp(dy), N, (int)dy.size(1),
+                   scratch.data_ptr<float>(), grad.data_ptr(), grad.scalar_type() == at::kFloat,
+                   grad.stride(0), cur_stream(dy));
+}
 
 
 
@@ -297,6 +340,8 @@ std::tuple<at::Tensor, at::Tensor> moe_combine_bwd(const at::Tensor& dout, const
 TORCH_LIBRARY_FRAGMENT(dla, m) {
   m.def("moe_topk_fwd(Tensor logits, int k) -> (Tensor, Tensor)");
   m.def("quant_fp8_rows(Tensor x) -> (Tensor, Tensor)");
+  m.def("embed_fwd(Tensor w, Tensor ids) -> Tensor");
+  m.def("embed_bwd(Tensor sid, Tensor perm, Tensor dy, Tensor(a!) grad) -> ()");
   m.def("moe_topk_bwd(Tensor topv, Tensor topi, Tensor grad, int E) -> Tensor");
   m.def("moe_dispatch(Tensor x, Tensor pos) -> Tensor");
   m.def("moe_combine(Tensor ys, Tensor pos, Tensor? w) -> Tensor");
@@ -311,6 +356,8 @@ TORCH_LIBRARY_FRAGMENT(dla, m) {
 TORCH_LIBRARY_IMPL(dla, CUDA, m) {
   m.impl("moe_topk_fwd", &dla::moe_topk_fwd);
   m.impl("quant_fp8_rows", &dla::quant_fp8_rows);
+  m.impl("embed_fwd", &dla::embed_fwd);
+  m.impl("embed_bwd", &dla::embed_bwd);
   m.impl("moe_topk_bwd", &dla::moe_topk_bwd);
   m.impl("moe_dispatch", &dla::moe_dispatch);
   m.impl("moe_combine", &dla::moe_combine);

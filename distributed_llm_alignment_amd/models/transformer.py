@@ -351,7 +351,7 @@ class CausalLM(nn.Module):
 
             x = vocab_parallel_embedding(input_ids, self.embed, self.vocab_parallel[0], self.tp)
         else:
-            x = F.embedding(input_ids, self.embed)
+            x = ops.embedding(input_ids, self.embed)
         if self.wpe is not None:
             T = input_ids.shape[1]
             pos = positions.long() if positions is not None else torch.arange(T, device=input_ids.device)

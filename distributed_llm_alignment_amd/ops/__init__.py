@@ -1,6 +1,7 @@
 """gfx950 compute ops. GPU tensors run the in-tree HIP kernels (`torch.ops.dla.*`); CPU tensors
 run the pure-PyTorch references (test tier / numerics oracles)."""
 from . import _ext, decode, moe
+from .embedding import embedding
 from .activations import gelu_new, swiglu, swiglu_mlp, swiglu_mlp_ok
 from .attention import RotaryCache, attention_core, qkv_attention, ref_attention
 from .linear import accumulate_weight_grad, linear
@@ -10,6 +11,7 @@ from .losses import (dpo_loss, ensemble_kl, gae, kl_penalty_pg, pairwise_loss, p
 from .norm import add_norm, layer_norm, rms_norm
 
 __all__ = [
+    "embedding",
     "_ext", "decode", "moe", "gelu_new", "swiglu", "swiglu_mlp", "swiglu_mlp_ok", "RotaryCache", "attention_core", "qkv_attention",
     "ref_attention", "linear_logprob", "seq_reduce", "sequence_logprob", "shifted_targets",
     "token_nll", "dpo_loss", "ensemble_kl", "kl_penalty_pg", "pairwise_loss", "gae",

@@ -1,0 +1,57 @@
+"""Token embedding on the HIP gather / deterministic scatter-add kernels (csrc/embedding.hip,
+SURVEY K1).
+
+Forward gathers table rows with 16-byte loads. Backward sorts the token ids on the device
+(`torch.sort`, stable: no host sync) and sums every token's dY rows in sorted order straight into
+the engine's flat main-grad buffer (bf16 or fp32), instead of eager PyTorch's dense [V, H]
+gradient (zero-fill + segment sum) plus autograd's add into `.grad` -- two passes over V x H per
+micro-batch. Tied / shared tables (`_dla_shared`: the LM head also writes the gradient) get a
+dense gradient tensor through autograd as usual. CPU tensors use `F.embedding`.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.nn.functional as F
+
+from . import _ext
+
+
+class _EmbeddingFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ids, weight):
+        flat = ids.reshape(-1).to(torch.int64).contiguous()
+        out = _ext.require().embed_fwd(weight, flat)
+        ctx.save_for_backward(flat)
+        ctx.wshape = weight.shape
+        ctx.weight = weight
+        return out.view(*ids.shape, weight.shape[1])
+
+    @staticmethod
+    def backward(ctx, dy):
+        (flat,) = ctx.saved_tensors
+        weight = ctx.weight
+        sid, perm = torch.sort(flat, stable=True)
+        dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
+        mg = getattr(weight, "main_grad", None)
+        if mg is not None and not getattr(weight, "_dla_shared", False) and mg.is_contiguous():
+            _ext.require().embed_bwd(sid, perm, dy2, mg)
+            hook = getattr(weight, "_dla_grad_hook", None)
+            if hook is not None:
+                hook(weight)
+            return None, None
+        g = torch.zeros(ctx.wshape, dtype=torch.float32 if weight.dtype != torch.bfloat16 else weight.dtype,
+                        device=dy.device)
+        _ext.require().embed_bwd(sid, perm, dy2, g)
+        return None, g.to(weight.dtype)
+
+
+NATIVE_EMBEDDING = os.environ.get("DLA_EMBED_KERNEL", "1") != "0"
+
+
+def embedding(ids: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    if (NATIVE_EMBEDDING and _ext.use_native(weight) and weight.dtype == torch.bfloat16 and weight.dim() == 2
+            and weight.shape[1] % 8 == 0 and weight.stride(1) == 1 and weight.stride(0) % 8 == 0):
+        return _EmbeddingFn.apply(ids, weight)
+    return F.embedding(ids, weight)

@@ -556,3 +556,46 @@ def test_chunked_ensemble_kl_peak_memory_v51200():
     assert p2 > full_bytes, "the one-shot path should materialise the teacher logits"
     assert torch.allclose(k1, k2, atol=2e-3, rtol=1e-2)
     assert ((g1 - g2).norm() / g2.norm()).item() < 2e-2
+
+
+@pytest.mark.parametrize("gdtype", [torch.bfloat16, torch.float32, None])
+def test_embedding_gather_and_sorted_scatter_add(gdtype):
+    """HIP embedding: exact gather; backward = per-token sums of dY (hot token repeated across
+    many 16-position chunks, singletons, unused rows untouched) accumulated into a main-grad
+    buffer (bf16 / fp32) or returned densely; bitwise reproducible across runs."""
+    from distributed_llm_alignment_amd import ops
+
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(3)
+    V, H = 1000, 4096
+    w = torch.randn(V, H, device=dev, generator=g).to(torch.bfloat16).requires_grad_(True)
+    ids = torch.randint(0, V, (6, 211), device=dev, generator=g)
+    ids[:, :90] = 7  # a hot token: 540 occurrences
+    ids[2, 100:150] = 11
+    base = None
+    if gdtype is not None:
+        base = torch.randn(V, H, device=dev, generator=g).to(gdtype)
+        w.main_grad = base.clone()
+    out = ops.embedding(ids, w)
+    assert torch.equal(out, torch.nn.functional.embedding(ids, w.detach()))
+    dy = torch.randn(*out.shape, device=dev, generator=g).to(torch.bfloat16)
+    out.backward(dy)
+    ref = torch.zeros(V, H, device=dev, dtype=torch.float64)
+    ref.index_add_(0, ids.reshape(-1), dy.reshape(-1, H).double())
+    if gdtype is None:
+        got = w.grad.double()
+        tol = 1e-2
+    else:
+        assert w.grad is None
+        got = w.main_grad.double() - base.double()
+        tol = 1e-2 if gdtype == torch.bfloat16 else 1e-5
+    untouched = torch.ones(V, dtype=torch.bool, device=dev)
+    untouched[ids.reshape(-1)] = False
+    assert torch.equal(got[untouched], torch.zeros_like(got[untouched]))
+    rel = ((got - ref).norm() / ref.norm()).item()
+    assert rel < tol, rel
+    if gdtype is not None:  # bitwise reproducible
+        first = w.main_grad.clone()
+        w.main_grad = base.clone()
+        ops.embedding(ids, w).backward(dy)
+        assert torch.equal(w.main_grad, first)
