@@ -6,6 +6,7 @@
 
 #include "bind_util.h"
 #include "gg_params.h"
+#include "reward_head.h"
 
 namespace dla {
 
@@ -22,6 +23,80 @@ void launch_quant_fp8_rows(const bf16_t*, int64_t, int64_t, int, uint8_t*, float
 void launch_embed_fwd(const bf16_t*, int64_t, const int64_t*, int64_t, int, int64_t, bf16_t*, hipStream_t);
 void launch_embed_bwd(const int64_t*, const int64_t*, const bf16_t*, int64_t, int, float*, void*, bool,
                       int64_t, hipStream_t);
+
+static RHParams rh_params(const at::Tensor& hidden, const c10::optional<at::Tensor>& last,
+                          const c10::optional<at::Tensor>& mask, const at::Tensor& w,
+                          const c10::optional<at::Tensor>& bias, double p, int64_t seed) {
+  check_bf16(hidden, "hidden");
+  check_bf16(w, "w");
+  TORCH_CHECK(hidden.dim() == 3 && hidden.stride(2) == 1 && hidden.stride(1) % 8 == 0 &&
+                  hidden.stride(0) % 8 == 0 && hidden.size(2) % 8 == 0,
+              "hidden [B, T, H], H % 8 == 0, 16-byte aligned rows");
+  check_aligned16(hidden, "hidden");
+  const int64_t B = hidden.size(0), T = hidden.size(1), H = hidden.size(2);
+  TORCH_CHECK(w.numel() == H && w.is_contiguous(), "w [H] (Linear(H, 1).weight)");
+  check_aligned16(w, "w");
+  TORCH_CHECK(p >= 0.0 && p < 1.0, "dropout p in [0, 1)");
+  RHParams r{};
+  r.hidden = cbp(hidden);
+  r.sb = hidden.stride(0);
+  r.st = hidden.stride(1);
+  if (mask && mask->defined()) {
+    check_f32(*mask, "mask");
+    TORCH_CHECK(mask->dim() == 2 && mask->size(0) == B && mask->size(1) == T && mask->is_contiguous(),
+                "mask [B, T] fp32");
+    r.mask = mask->data_ptr<float>();
+  } else {
+    TORCH_CHECK(last && last->defined(), "last_token pooling needs `last`");
+    check_i32(*last, "last");
+    TORCH_CHECK(last->numel() == B && last->is_contiguous(), "last [B] int32");
+    r.last = last->data_ptr<int>();
+  }
+  r.w = cbp(w);
+  if (bias && bias->defined()) {
+    check_bf16(*bias, "bias");
+    r.bias = cbp(*bias);
+  }
+  r.B = (int)B;
+  r.T = (int)T;
+  r.H = (int)H;
+  r.p = static_cast<float>(p);
+  r.seed = static_cast<uint64_t>(seed);
+  return r;
+}
+
+// pooled (last valid token via `last`, or masked mean via `mask`) -> dropout -> . w + bias:
+// returns (score fp32 [B], dropped pooled rows fp32 [B, H])
+std::tuple<at::Tensor, at::Tensor> reward_head_fwd(const at::Tensor& hidden,
+                                                   const c10::optional<at::Tensor>& last,
+                                                   const c10::optional<at::Tensor>& mask,
+                                                   const at::Tensor& w,
+                                                   const c10::optional<at::Tensor>& bias, double p,
+                                                   int64_t seed) {
+  RHParams r = rh_params(hidden, last, mask, w, bias, p, seed);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(hidden.device());
+  auto score = at::empty({hidden.size(0)}, hidden.options().dtype(at::kFloat));
+  auto pooled = at::empty({hidden.size(0), hidden.size(2)}, hidden.options().dtype(at::kFloat));
+  r.score = score.data_ptr<float>();
+  r.pooled = pooled.data_ptr<float>();
+  launch_reward_head_fwd(r, cur_stream(hidden));
+  return {score, pooled};
+}
+
+// dHidden [B, T, H] (zero except the pooled positions), same mask regenerated from `seed`
+at::Tensor reward_head_bwd(const at::Tensor& dscore, const at::Tensor& hidden,
+                           const c10::optional<at::Tensor>& last, const c10::optional<at::Tensor>& mask,
+                           const at::Tensor& w, double p, int64_t seed) {
+  RHParams r = rh_params(hidden, last, mask, w, c10::nullopt, p, seed);
+  check_f32(dscore, "dscore");
+  TORCH_CHECK(dscore.numel() == hidden.size(0) && dscore.is_contiguous(), "dscore [B]");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(hidden.device());
+  auto dh = at::zeros({hidden.size(0), hidden.size(1), hidden.size(2)}, hidden.options());
+  r.dscore = dscore.data_ptr<float>();
+  r.dhidden = bp(dh);
+  launch_reward_head_bwd(r, cur_stream(hidden));
+  return dh;
+}
 
 // token embedding gather: out[n] = w[ids[n]] (ids int64 [N], w [V, H] bf16)
 at::Tensor embed_fwd(const at::Tensor& w, const at::Tensor& ids) {
@@ -341,6 +416,8 @@ TORCH_LIBRARY_FRAGMENT(dla, m) {
   m.def("moe_topk_fwd(Tensor logits, int k) -> (Tensor, Tensor)");
   m.def("quant_fp8_rows(Tensor x) -> (Tensor, Tensor)");
   m.def("embed_fwd(Tensor w, Tensor ids) -> Tensor");
+  m.def("reward_head_fwd(Tensor hidden, Tensor? last, Tensor? mask, Tensor w, Tensor? bias, float p, int seed) -> (Tensor, Tensor)");
+  m.def("reward_head_bwd(Tensor dscore, Tensor hidden, Tensor? last, Tensor? mask, Tensor w, float p, int seed) -> Tensor");
   m.def("embed_bwd(Tensor sid, Tensor perm, Tensor dy, Tensor(a!) grad) -> ()");
   m.def("moe_topk_bwd(Tensor topv, Tensor topi, Tensor grad, int E) -> Tensor");
   m.def("moe_dispatch(Tensor x, Tensor pos) -> Tensor");
@@ -357,6 +434,8 @@ TORCH_LIBRARY_IMPL(dla, CUDA, m) {
   m.impl("moe_topk_fwd", &dla::moe_topk_fwd);
   m.impl("quant_fp8_rows", &dla::quant_fp8_rows);
   m.impl("embed_fwd", &dla::embed_fwd);
+  m.impl("reward_head_fwd", &dla::reward_head_fwd);
+  m.impl("reward_head_bwd", &dla::reward_head_bwd);
   m.impl("embed_bwd", &dla::embed_bwd);
   m.impl("moe_topk_bwd", &dla::moe_topk_bwd);
   m.impl("moe_dispatch", &dla::moe_dispatch);

@@ -12,7 +12,31 @@ from typing import Dict
 import torch
 import torch.nn as nn
 
+from ..ops import _ext
 from .transformer import CausalLM, attention_layout
+
+
+class _RewardHeadFn(torch.autograd.Function):
+    """Fused pooling + dropout + Linear(H, 1) (csrc/reward_head.hip)."""
+
+    @staticmethod
+    def forward(ctx, hidden, w, b, last, mask, p: float, seed: int):
+        C = _ext.require()
+        score, pooled = C.reward_head_fwd(hidden, last, mask, w.reshape(-1), b, p, seed)
+        ctx.save_for_backward(hidden, w, last, mask, pooled)
+        ctx.p, ctx.seed, ctx.has_b = p, seed, b is not None
+        return score
+
+    @staticmethod
+    def backward(ctx, ds):
+        hidden, w, last, mask, pooled = ctx.saved_tensors
+        ds = ds.float().contiguous()
+        dh = None
+        if ctx.needs_input_grad[0]:
+            dh = _ext.require().reward_head_bwd(ds, hidden, last, mask, w.reshape(-1), ctx.p, ctx.seed)
+        dw = (ds.unsqueeze(1) * pooled).sum(0).to(w.dtype).view_as(w) if ctx.needs_input_grad[1] else None
+        db = ds.sum().to(w.dtype).reshape(1) if (ctx.has_b and ctx.needs_input_grad[2]) else None
+        return dh, dw, db, None, None, None, None
 
 
 class RewardModel(nn.Module):
@@ -43,7 +67,32 @@ class RewardModel(nn.Module):
         from ..parallel.sequence import sp_full_hidden
 
         h = sp_full_hidden(self.backbone, self.backbone(input_ids, attention_mask), input_ids.shape[1])
+        lin = self.scorer[1]
+        if (_ext.use_native(h) and h.dtype == torch.bfloat16 and lin.weight.dtype == torch.bfloat16
+                and h.shape[-1] % 8 == 0 and h.stride(-1) == 1):
+            return self._fused_head(h, attention_mask)
         return self.scorer(self.pool(h, attention_mask)).squeeze(-1).float()
+
+    def _fused_head(self, h: torch.Tensor, attention_mask) -> torch.Tensor:
+        B, T = h.shape[0], h.shape[1]
+        last = mask = None
+        if self.pooling == "last_token":
+            if attention_mask is None:
+                last = torch.full((B,), T - 1, dtype=torch.int32, device=h.device)
+            else:
+                _, end, _ = attention_layout(attention_mask)
+                last = (end - 1).clamp(min=0).to(torch.int32).contiguous()
+        else:
+            mask = (torch.ones((B, T), device=h.device) if attention_mask is None
+                    else attention_mask.float()).contiguous()
+        drop = self.scorer[0]
+        p = float(drop.p) if (self.training and drop.p > 0) else 0.0
+        # dropout seed from torch's host generator (torch.manual_seed reproducible, no GPU sync)
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if p > 0 else 0
+        if h.stride(1) % 8 or h.stride(0) % 8 or h.data_ptr() % 16:
+            h = h.contiguous()
+        lin = self.scorer[1]
+        return _RewardHeadFn.apply(h, lin.weight, lin.bias, last, mask, p, seed)
 
     def hf_state_dict(self, only=None) -> Dict[str, torch.Tensor]:
         from .hf_io import to_hf_state_dict

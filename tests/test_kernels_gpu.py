@@ -599,3 +599,52 @@ def test_embedding_gather_and_sorted_scatter_add(gdtype):
         w.main_grad = base.clone()
         ops.embedding(ids, w).backward(dy)
         assert torch.equal(w.main_grad, first)
+
+
+@pytest.mark.parametrize("pooling", ["last_token", "mean"])
+def test_fused_reward_head(pooling):
+    """Fused pool + dropout + Linear(H,1): eval == the PyTorch head (fp32 reference); train-mode
+    dropout has the right keep rate and its backward is the exact derivative of its own forward
+    (directional finite difference at a fixed seed)."""
+    from distributed_llm_alignment_amd.models import build_model, get_config
+    from distributed_llm_alignment_amd.models.reward import RewardModel
+
+    dev = torch.device("cuda", 0)
+    cfg = get_config("tiny-llama-d128")
+    rm = RewardModel(build_model(cfg, device=dev, dtype=torch.bfloat16, seed=0, headless=True),
+                     pooling=pooling)
+    g = torch.Generator(device=dev).manual_seed(2)
+    ids = torch.randint(3, cfg.vocab_size, (4, 96), device=dev, generator=g)
+    mask = torch.ones_like(ids)
+    mask[1, 70:] = 0
+    mask[2, :10] = 0
+    rm.eval()
+    s = rm(ids, mask)
+    with torch.no_grad():
+        h = rm.backbone(ids, mask)
+        ref = rm.scorer[1](rm.pool(h, mask)).squeeze(-1).float()
+    assert torch.allclose(s, ref, atol=2e-2, rtol=2e-2), (s, ref)
+    # train mode: directional derivative check of the fused head alone at a fixed seed
+    from distributed_llm_alignment_amd.models.reward import _RewardHeadFn
+    from distributed_llm_alignment_amd.models.transformer import attention_layout
+
+    hh = torch.randn(4, 96, cfg.hidden_size, device=dev, generator=g).to(torch.bfloat16)
+    _, end, _ = attention_layout(mask)
+    last = (end - 1).clamp(min=0).to(torch.int32).contiguous()
+    mk = mask.float().contiguous() if pooling == "mean" else None
+    lt = None if pooling == "mean" else last
+    w = rm.scorer[1].weight.detach().clone().requires_grad_(True)
+    hv = hh.clone().requires_grad_(True)
+    sc = _RewardHeadFn.apply(hv, w, None, lt, mk, 0.5, 1234)
+    sc.sum().backward()
+    dirn = torch.randn_like(w, dtype=torch.float32)
+    eps = 1e-2
+    sp = _RewardHeadFn.apply(hh, (w.detach().float() + eps * dirn).to(torch.bfloat16), None, lt, mk, 0.5, 1234)
+    sm = _RewardHeadFn.apply(hh, (w.detach().float() - eps * dirn).to(torch.bfloat16), None, lt, mk, 0.5, 1234)
+    fd = ((sp - sm).sum() / (2 * eps)).item()
+    an = (w.grad.float() * dirn).sum().item()
+    assert abs(fd - an) <= 5e-2 * max(1.0, abs(an)), (fd, an)
+    # keep rate of the hash dropout ~ 1 - p
+    _, pooled = torch.ops.dla.reward_head_fwd(hh, lt, mk, w.detach().reshape(-1), None, 0.5, 99)
+    kept = (pooled != 0).float().mean().item()
+    assert 0.45 < kept < 0.55, kept
