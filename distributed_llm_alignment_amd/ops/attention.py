@@ -257,16 +257,46 @@ def qkv_attention(qkv: torch.Tensor, Hq: int, Hkv: int, D: int, rope: Optional[R
             cos = sin = torch.empty(0, device=qkv.device)
         return _FusedQKVAttnFn.apply(qkv.contiguous(), cos, sin, pos32, Hq, Hkv, D, rot, scale,
                                      causal, window, ks, ke, sg)
-    # odd head dims (e.g. phi-2 D=80): reference RoPE glue + padded native attention core
-    q = qkv[..., : Hq * D].reshape(B, T, Hq, D)
-    k = qkv[..., Hq * D:(Hq + Hkv) * D].reshape(B, T, Hkv, D)
-    v = qkv[..., (Hq + Hkv) * D:].reshape(B, T, Hkv, D)
-    if rope is not None:
-        pos = positions if positions is not None else torch.arange(T, device=qkv.device).expand(B, T)
-        q = apply_rope(q, rope, pos)
-        k = apply_rope(k, rope, pos)
+    # odd head dims (e.g. phi-2 D=80, partial rotary 32): HIP RoPE forward/backward on the fused
+    # qkv buffer (the kernels take any D % 8 == 0), then the native attention core on head dims
+    # zero-padded to the next supported size
+    if rope is not None and D % 8 == 0 and rot % 16 == 0:
+        cos, sin = rope.tables(qkv.device)
+        q, k, v = _RopeQKFn.apply(qkv.contiguous(), cos, sin, pos32, Hq, Hkv, D, rot)
+    else:
+        q = qkv[..., : Hq * D].reshape(B, T, Hq, D)
+        k = qkv[..., Hq * D:(Hq + Hkv) * D].reshape(B, T, Hkv, D)
+        v = qkv[..., (Hq + Hkv) * D:].reshape(B, T, Hkv, D)
+        if rope is not None:
+            pos = positions if positions is not None else torch.arange(T, device=qkv.device).expand(B, T)
+            q = apply_rope(q, rope, pos)
+            k = apply_rope(k, rope, pos)
     o = attention_core(q, k, v, scale, causal, 0, window, kv_start, kv_end, segs)
     return o.reshape(B, T, Hq * D)
+
+
+class _RopeQKFn(torch.autograd.Function):
+    """qkv [B, T, (Hq+2Hkv)D] -> rotated q [B,T,Hq,D], k [B,T,Hkv,D] and v [B,T,Hkv,D] on the
+    HIP rope kernels (forward rope_fwd; backward rope_bwd un-rotates dq/dk straight into dqkv)."""
+
+    @staticmethod
+    def forward(ctx, qkv, cos, sin, pos32, Hq, Hkv, D, rot):
+        B, T, C = qkv.shape
+        q, k = _ext.require().rope_fwd(qkv.reshape(B * T, C), cos, sin, pos32, Hq, Hkv, D, rot, T, 0)
+        v = qkv[..., (Hq + Hkv) * D:].reshape(B, T, Hkv, D)
+        ctx.save_for_backward(cos, sin, pos32)
+        ctx.cfg = (B, T, C, Hq, Hkv, D, rot)
+        return q.view(B, T, Hq, D), k.view(B, T, Hkv, D), v
+
+    @staticmethod
+    def backward(ctx, dq, dk, dv):
+        cos, sin, pos32 = ctx.saved_tensors
+        B, T, C, Hq, Hkv, D, rot = ctx.cfg
+        dqkv = torch.empty((B, T, C), dtype=dq.dtype, device=dq.device)
+        _ext.require().rope_bwd(dq.contiguous().view(B * T, Hq * D), dk.contiguous().view(B * T, Hkv * D),
+                                dqkv.view(B * T, C), cos, sin, pos32, Hq, Hkv, D, rot, T, 0)
+        dqkv[..., (Hq + Hkv) * D:] = dv.reshape(B, T, Hkv * D)
+        return dqkv, None, None, None, None, None, None, None
 
 
 def rope_qk(qkv: torch.Tensor, rope: Optional[RotaryCache], Hq: int, Hkv: int, D: int,

@@ -648,3 +648,33 @@ def test_fused_reward_head(pooling):
     _, pooled = torch.ops.dla.reward_head_fwd(hh, lt, mk, w.detach().reshape(-1), None, 0.5, 99)
     kept = (pooled != 0).float().mean().item()
     assert 0.45 < kept < 0.55, kept
+
+
+def test_odd_head_dim_partial_rotary_attention_fwd_bwd():
+    """phi-2 geometry (head_dim 80, rotary 32 of 80 dims): HIP RoPE autograd + padded native
+    attention core vs the fp32 PyTorch reference, forward and backward through the fused qkv."""
+    from distributed_llm_alignment_amd import ops
+
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(4)
+    B, T, Hq, Hkv, D, rot = 2, 200, 4, 4, 80, 32
+    rope = ops.RotaryCache(rot, 10000.0, 2048, None)
+    qkv = torch.randn(B, T, (Hq + 2 * Hkv) * D, device=dev, generator=g).to(torch.bfloat16).requires_grad_(True)
+    mask = torch.ones(B, T, dtype=torch.long, device=dev)
+    mask[1, :30] = 0
+    from distributed_llm_alignment_amd.models.transformer import attention_layout
+
+    ks, ke, pos = attention_layout(mask)
+    o = ops.qkv_attention(qkv, Hq, Hkv, D, rope, kv_start=ks, kv_end=ke, positions=pos)
+    qf = qkv.detach().float().cpu().requires_grad_(True)
+    ocpu = ops.qkv_attention(qf, Hq, Hkv, D, rope, kv_start=ks.cpu() if ks is not None else None,
+                             kv_end=ke.cpu() if ke is not None else None,
+                             positions=pos.cpu() if pos is not None else None)
+    valid = mask.bool().unsqueeze(-1).cpu()
+    err = ((o.float().cpu() - ocpu) * valid).abs().max().item()
+    assert err < 3e-2, err
+    do = torch.randn(*o.shape, device=dev, generator=g).to(torch.bfloat16) * mask.unsqueeze(-1)
+    (dg,) = torch.autograd.grad(o, qkv, do)
+    (dr,) = torch.autograd.grad(ocpu, qf, do.float().cpu())
+    rel = ((dg.float().cpu() - dr).norm() / dr.norm()).item()
+    assert rel < 3e-2, rel
