@@ -122,12 +122,18 @@ __device__ void suffix_scan(int* c, float* m, int* tc, float* tm) {
 
 // Histogram of the row's z over [lo, lo + w) into kBins bins (counts + exp masses), optionally
 // restricted to z >= floor_z.
+// Bin masses are summed as 2^-40 fixed-point integers (each exp(z) <= 1 rounded once), so the
+// histogram -- and with it every threshold and the sampled token -- does not depend on the order
+// in which the lanes' atomics land (a float LDS atomicAdd sum does, in its last bits).
+constexpr float kHistFix = 1099511627776.0f;  // 2^40
+
 template <bool VEC, typename T>
 __device__ void histogram(const T* row, int V, float gmax, float inv_t, float lo, float w,
                           float floor_z, int* c, float* m) {
+  __shared__ unsigned long long mfix[kBins];
   for (int i = threadIdx.x; i < kBins; i += kSampNT) {
     c[i] = 0;
-    m[i] = 0.f;
+    mfix[i] = 0ull;
   }
   __syncthreads();
   const float sc = kBins / w;
@@ -138,9 +144,12 @@ __device__ void histogram(const T* row, int V, float gmax, float inv_t, float lo
     if (z >= lo && (z < hi || (top && z <= 0.f)) && z >= floor_z) {
       const int b = min(kBins - 1, (int)((z - lo) * sc));
       atomicAdd(&c[b], 1);
-      atomicAdd(&m[b], __expf(z));
+      atomicAdd(&mfix[b], static_cast<unsigned long long>(__expf(z) * kHistFix));
     }
   });
+  __syncthreads();
+  for (int i = threadIdx.x; i < kBins; i += kSampNT)
+    m[i] = static_cast<float>(static_cast<double>(mfix[i]) * (1.0 / 1099511627776.0));
   __syncthreads();
 }
 
@@ -447,7 +456,7 @@ __global__ __launch_bounds__(kSplitNT) void split_hist_kernel(const T* __restric
                                                               int64_t ld_, int V, int G,
                                                               float inv_t, bool first, SplitWs ws) {
   __shared__ int c[kBins];
-  __shared__ float m[kBins];
+  __shared__ unsigned long long m[kBins];  // 2^-40 fixed point: order-independent sums
   const int r = blockIdx.y, g = blockIdx.x, tid = threadIdx.x;
   float lo = -kRange, w = kRange, floor_z = -INFINITY;
   if (!first) {
@@ -462,7 +471,7 @@ __global__ __launch_bounds__(kSplitNT) void split_hist_kernel(const T* __restric
   row_max(ws.pmax + r * G, ws.parg + r * G, G, gmax, argmax);
   for (int i = tid; i < kBins; i += kSplitNT) {
     c[i] = 0;
-    m[i] = 0.f;
+    m[i] = 0ull;
   }
   __syncthreads();
   const T* row = logits + int64_t(r) * ld_;
@@ -479,7 +488,7 @@ __global__ __launch_bounds__(kSplitNT) void split_hist_kernel(const T* __restric
       if (z >= lo && (z < hi || (top && z <= 0.f)) && z >= floor_z) {
         const int b = min(kBins - 1, (int)((z - lo) * sc));
         atomicAdd(&c[b], 1);
-        atomicAdd(&m[b], __expf(z));
+        atomicAdd(&m[b], static_cast<unsigned long long>(__expf(z) * kHistFix));
       }
     }
   }
@@ -489,7 +498,7 @@ __global__ __launch_bounds__(kSplitNT) void split_hist_kernel(const T* __restric
   for (int i = tid; i < kBins; i += kSplitNT)
     if (c[i] > 0) {  // only occupied bins: few atomics for concentrated rows
       atomicAdd(oc + i, c[i]);
-      atomicAdd(om + i, (unsigned long long)((double)m[i] * kFix));
+      atomicAdd(om + i, m[i]);  // same 2^-40 scale as kFix
     }
 }
 
