@@ -20,6 +20,9 @@
 //     costs one barrier; all 256 queries of the workgroup share each K/V tile.
 //   * XOR-swizzled LDS image usable both for row (ds_read_b128) and transposed reads.
 //   * query blocks are the slowest grid dimension, heaviest causal blocks first (LPT order).
+//   * widened store tail (T21): O leaves as 8 x 16 B per lane after a permlane32 swap instead
+//     of 16 x 8 B (the per-lane row stores are issue-bound): 141 -> 121 us causal T = 1024,
+//     190 -> 170 us non-causal (tools/attn_bench.py --ab, one box).
 // Backward: see attn_bwd_kernel.
 #include <stdexcept>
 #include "common.h"
@@ -96,13 +99,12 @@ __device__ __forceinline__ s16x8 tr_frag_nat(const bf16_t* img, int r0, int c0, 
 // ==============================================================================================
 // forward
 // ==============================================================================================
-constexpr int kFwdThreads = 512;  // 8 waves
-constexpr int kFwdRows = 256;     // queries per workgroup
 constexpr int kFwdKeys = 64;      // keys per K/V tile
 
-template <int D, bool CAUSAL>
-__global__ __launch_bounds__(kFwdThreads) void attn_fwd_kernel(AttnParams p) {
-  constexpr int NT = kFwdThreads, BQ = kFwdRows, BK = kFwdKeys;
+// NW waves per workgroup, 32 queries each (NT = 64 NW threads, BQ = 32 NW queries)
+template <int D, bool CAUSAL, int NW>
+__global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
+  constexpr int NT = 64 * NW, BQ = 32 * NW, BK = kFwdKeys;
   constexpr int NCH = D / 8;
   constexpr int KS = D / 16;
   constexpr int DT = D / 32;
@@ -128,22 +130,6 @@ __global__ __launch_bounds__(kFwdThreads) void attn_fwd_kernel(AttnParams p) {
   const bf16_t* qp = p.q + b * p.q_sb + static_cast<int64_t>(hq) * p.q_sh;
   const bf16_t* kp = p.k + b * p.k_sb + static_cast<int64_t>(hk) * p.k_sh;
   const bf16_t* vp = p.v + b * p.v_sb + static_cast<int64_t>(hk) * p.v_sh;
-
-  // Q fragments stay in registers, pre-scaled by softmax_scale*log2(e) so the scores come
-  // out of the MFMA already in the exp2 domain (no per-score multiply).
-  s16x8 qf[KS];
-#pragma unroll
-  for (int s = 0; s < KS; ++s) {
-    if (qi < p.Tq) {
-      const bf16x8 raw = load_bf16x8(qp + qi * p.q_st + 16 * s + 8 * h);
-      float t[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) t[j] = bf2f(raw[j]) * p.scale2;
-      qf[s] = __builtin_bit_cast(s16x8, pack_bf16x8(t));
-    } else {
-      qf[s] = s16x8{};
-    }
-  }
 
   f32x16 o[DT];
 #pragma unroll
@@ -197,6 +183,22 @@ __global__ __launch_bounds__(kFwdThreads) void attn_fwd_kernel(AttnParams p) {
     }
   };
 
+  // Q fragments stay in registers, pre-scaled by softmax_scale*log2(e) so the scores come
+  // out of the MFMA already in the exp2 domain (no per-score multiply). (Issuing the K/V tile-0
+  // loads ahead of the Q loads measured -2.5 % .. +3 % by shape: kept in this order.)
+  s16x8 qf[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    if (qi < p.Tq) {
+      const bf16x8 raw = load_bf16x8(qp + qi * p.q_st + 16 * s + 8 * h);
+      float t[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) t[j] = bf2f(raw[j]) * p.scale2;
+      qf[s] = __builtin_bit_cast(s16x8, pack_bf16x8(t));
+    } else {
+      qf[s] = s16x8{};
+    }
+  }
   if (ntiles > 0) {
     gload(tile0);
     lwrite(0);
@@ -305,15 +307,22 @@ __global__ __launch_bounds__(kFwdThreads) void attn_fwd_kernel(AttnParams p) {
   if (qi < p.Tq) {
     const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
     bf16_t* op = p.o + b * p.o_sb + qi * p.o_st + static_cast<int64_t>(hq) * p.o_sh;
+    // widened store tail (cdna guide T21): lane half h holds columns 8k + 4h .. +3 of each 8-column
+    // group k; one v_permlane32_swap per dword pairs groups k, k+1 so that each lane owns 8
+    // contiguous columns (8k + 8h ..) and stores 16 B: 8 x dwordx4 per lane instead of 16 x dwordx2
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) {
 #pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int d = 32 * dt + 8 * g4 + 4 * h;
-        uint2 pk;
-        pk.x = pack2bf(o[dt][4 * g4 + 0] * inv, o[dt][4 * g4 + 1] * inv);
-        pk.y = pack2bf(o[dt][4 * g4 + 2] * inv, o[dt][4 * g4 + 3] * inv);
-        *reinterpret_cast<uint2*>(op + d) = pk;
+      for (int g4 = 0; g4 < 4; g4 += 2) {
+        uint2 a, c;
+        a.x = pack2bf(o[dt][4 * g4 + 0] * inv, o[dt][4 * g4 + 1] * inv);
+        a.y = pack2bf(o[dt][4 * g4 + 2] * inv, o[dt][4 * g4 + 3] * inv);
+        c.x = pack2bf(o[dt][4 * g4 + 4] * inv, o[dt][4 * g4 + 5] * inv);
+        c.y = pack2bf(o[dt][4 * g4 + 6] * inv, o[dt][4 * g4 + 7] * inv);
+        const auto rx = __builtin_amdgcn_permlane32_swap(a.x, c.x, false, false);
+        const auto ry = __builtin_amdgcn_permlane32_swap(a.y, c.y, false, false);
+        const int d = 32 * dt + 8 * g4 + 8 * h;
+        *reinterpret_cast<uint4*>(op + d) = make_uint4(rx[0], ry[0], rx[1], ry[1]);
       }
     }
     if (h == 0) {
@@ -711,19 +720,24 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnBwdParams p) {
     if (p.hsplit == 1) {
       bf16_t* dkp = p.dk + b * p.dk_sb + kj * p.dk_st + static_cast<int64_t>(hk) * p.dk_sh;
       bf16_t* dvp = p.dv + b * p.dv_sb + kj * p.dv_st + static_cast<int64_t>(hk) * p.dv_sh;
+      // widened stores (T21, as the forward's O): permlane32_swap pairs 8-column groups so
+      // each lane writes 16 contiguous bytes
+      auto store_row = [&](bf16_t* dst, const f32x16& x, float sc, int dt) {
+#pragma unroll
+        for (int g4 = 0; g4 < 4; g4 += 2) {
+          const uint32_t a0 = pack2bf(x[4 * g4] * sc, x[4 * g4 + 1] * sc);
+          const uint32_t a1 = pack2bf(x[4 * g4 + 2] * sc, x[4 * g4 + 3] * sc);
+          const uint32_t c0 = pack2bf(x[4 * g4 + 4] * sc, x[4 * g4 + 5] * sc);
+          const uint32_t c1 = pack2bf(x[4 * g4 + 6] * sc, x[4 * g4 + 7] * sc);
+          const auto r0 = __builtin_amdgcn_permlane32_swap(a0, c0, false, false);
+          const auto r1 = __builtin_amdgcn_permlane32_swap(a1, c1, false, false);
+          *reinterpret_cast<uint4*>(dst + 32 * dt + 8 * g4 + 8 * h) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
+        }
+      };
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          const int d = 32 * dt + 8 * g4 + 4 * h;
-          uint2 a, c;
-          a.x = pack2bf(dk[j][dt][4 * g4] * p.scale, dk[j][dt][4 * g4 + 1] * p.scale);
-          a.y = pack2bf(dk[j][dt][4 * g4 + 2] * p.scale, dk[j][dt][4 * g4 + 3] * p.scale);
-          c.x = pack2bf(dv[j][dt][4 * g4], dv[j][dt][4 * g4 + 1]);
-          c.y = pack2bf(dv[j][dt][4 * g4 + 2], dv[j][dt][4 * g4 + 3]);
-          *reinterpret_cast<uint2*>(dkp + d) = a;
-          *reinterpret_cast<uint2*>(dvp + d) = c;
-        }
+        store_row(dkp, dk[j][dt], p.scale, dt);
+        store_row(dvp, dv[j][dt], 1.f, dt);
       }
     } else {  // fp32 partials of this head subset, summed by attn_dkv_reduce_kernel
       const int64_t off = ((static_cast<int64_t>(sidx) * p.B + b) * p.Tk + kj) * p.Hkv * D +
@@ -766,15 +780,39 @@ __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(
     const int kbeg = kv_start ? kv_start[b] : 0;
     const int kend = kv_end ? kv_end[b] : Tk;
     const float* src = slab + (static_cast<int64_t>(b) * slab_rows + t) * rs + static_cast<int64_t>(hq) * D + c * 8;
-    f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+    // the key blocks that wrote row t form one contiguous range [lo, hi) (kv range: an
+    // interval; causal: a prefix; window: a suffix): find it with ALU only, then sum the slabs
+    // in kb order with 4 blocks' loads in flight at a time (same order as one at a time: the
+    // sum is bitwise unchanged)
+    int lo = nkb, hi = 0;
     for (int kb = 0; kb < nkb; ++kb) {
       const int k0 = kb * kAttnBwdKeys;
       int qt0, qend;
       bwd_q_range<CAUSAL>(k0, Tq, causal_off, window, qt0, qend);
       if (k0 >= kend || k0 + kAttnBwdKeys <= kbeg || t < qt0 || t >= qend) continue;
+      lo = min(lo, kb);
+      hi = kb + 1;
+    }
+    f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+    int kb = lo;
+    for (; kb + 4 <= hi; kb += 4) {
+      f32x4 x[4][2];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const f32x4* sv = reinterpret_cast<const f32x4*>(src + (kb + u) * slab_stride);
+        x[u][0] = __builtin_nontemporal_load(sv);
+        x[u][1] = __builtin_nontemporal_load(sv + 1);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a0 += x[u][0];
+        a1 += x[u][1];
+      }
+    }
+    for (; kb < hi; ++kb) {
       const f32x4* sv = reinterpret_cast<const f32x4*>(src + kb * slab_stride);
-      a0 += sv[0];
-      a1 += sv[1];
+      a0 += __builtin_nontemporal_load(sv);
+      a1 += __builtin_nontemporal_load(sv + 1);
     }
     const float v[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
     store_bf16x8(dst + b * d_sb + t * d_st + hq * d_sh + c * 8, pack_bf16x8(v));
@@ -823,12 +861,15 @@ static inline unsigned stream_grid(int64_t work) {
   return static_cast<unsigned>(g < 1 ? 1 : g);
 }
 
+// Forward: 8 waves (256 queries) per workgroup. A 4-wave / 128-query variant (two independent
+// workgroups per CU, unaligned barriers) measured 31-35 % slower at T = 1024 and 4096.
 template <int D>
 static void fwd_dispatch(const AttnParams& p, bool causal, hipStream_t st) {
-  const int nqb = (p.Tq + kFwdRows - 1) / kFwdRows;
+  constexpr int NW = 8;
+  const int nqb = (p.Tq + 32 * NW - 1) / (32 * NW);
   const dim3 grid(nqb * p.Hq * p.B);
-  if (causal) attn_fwd_kernel<D, true><<<grid, kFwdThreads, 0, st>>>(p);
-  else attn_fwd_kernel<D, false><<<grid, kFwdThreads, 0, st>>>(p);
+  if (causal) attn_fwd_kernel<D, true, NW><<<grid, 64 * NW, 0, st>>>(p);
+  else attn_fwd_kernel<D, false, NW><<<grid, 64 * NW, 0, st>>>(p);
 }
 
 void launch_attn_fwd(const AttnParams& p, int D, bool causal, hipStream_t st) {

@@ -21,7 +21,7 @@ def main() -> int:
     ap.add_argument("--D", type=int, default=128)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--noncausal", action="store_true")
-    ap.add_argument("--ab", default="", help="env var to A/B (0 vs 1) on the forward, interleaved")
+    ap.add_argument("--ab", default="", help="NAME[=v0,v1]: env var to A/B on the forward, interleaved")
     ap.add_argument("--rounds", type=int, default=3)
     a = ap.parse_args()
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -50,10 +50,12 @@ def main() -> int:
     tb = (time.perf_counter() - t0) / a.iters
     if a.ab:
         # interleaved rounds in one process (cdna guide §5.4 rule 24): min per setting
+        name, _, vals = a.ab.partition("=")
+        vals = tuple(vals.split(",")) if vals else ("0", "1")
         best, outs = {}, {}
         for _ in range(a.rounds):
-            for val in ("0", "1"):
-                os.environ[a.ab] = val
+            for val in vals:
+                os.environ[name] = val
                 outs[val] = ops.attention_core(q, k, v, causal=causal)
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
@@ -61,10 +63,10 @@ def main() -> int:
                     ops.attention_core(q, k, v, causal=causal)
                 torch.cuda.synchronize()
                 best[val] = min(best.get(val, 1e9), (time.perf_counter() - t0) / a.iters)
-        os.environ.pop(a.ab)
-        diff = (outs["0"].float() - outs["1"].float()).abs().max().item()
-        for val in ("0", "1"):
-            print(f"[attn-ab] {a.ab}={val} fwd {best[val]*1e6:.1f} us ({flops_fwd/best[val]/1e12:.0f} TF/s)",
+        os.environ.pop(name)
+        diff = (outs[vals[0]].float() - outs[vals[1]].float()).abs().max().item()
+        for val in vals:
+            print(f"[attn-ab] {name}={val} fwd {best[val]*1e6:.1f} us ({flops_fwd/best[val]/1e12:.0f} TF/s)",
                   flush=True)
         print(f"[attn-ab] max |o0 - o1| = {diff:.3e}", flush=True)
     print(f"[attn] B={a.B} T={a.T} Hq={a.Hq} causal={causal} fwd {tf*1e6:.1f} us ({flops_fwd/tf/1e12:.0f} TF/s)  bwd(all kernels) {tb*1e6:.1f} us "
