@@ -5,10 +5,9 @@
 // Decode is bandwidth bound: each step streams the whole KV cache once. Design:
 //   * split-KV (flash-decoding): grid = (splits, Hkv, B); a block owns one KV head, ALL its
 //     G = Hq/Hkv query heads (GQA: the K/V rows are read once, not G times) and a 128-key chunk;
-//   * rows are read cooperatively: D/8 lanes x 16 B per K/V row (one 256-byte row per 16 lanes
-//     for D = 128, 4 rows per wave instruction, fully coalesced); each lane keeps its 8-dim slice
-//     of the G query vectors in registers; dot products reduce across the row's lanes by
-//     shuffles; P.V accumulates per lane and reduces across row groups, then across waves;
+//   * each wave takes 32 keys of the chunk: S^T = K q^T on MFMA (K rows as A fragments), a
+//     wave-local softmax, P.V on the VALU over V rows read coalesced (D/8 lanes x 16 B per row);
+//     the 4 waves merge once at the end (see decode_attn_kernel);
 //   * partial (m, l, o) per split in fp32, merged by `decode_combine_kernel`.
 // Lengths are DEVICE values (kv_len scalar, per-row kv_start for left padding), so the same
 // launch replays inside a captured hipGraph while the cache grows; splits beyond kv_len exit.
@@ -57,6 +56,17 @@ __device__ __forceinline__ bf16x8 dec_rope8(const bf16_t* src, int d0, int rot, 
   return o;
 }
 
+// The four waves of a block work independently until one final merge.
+//   * every load is issued up front, one memory round trip: the wave's 32 K rows as MFMA A
+//     fragments (lane = key, 16 B of its row per k-step), its 32 V rows in the coalesced row
+//     layout, and q as the B fragment (lane = query head);
+//   * S^T = K q^T with v_mfma_f32_16x16x32_bf16 (no cross-lane dot-product reductions); the
+//     lane holding (head g, 8 keys) runs a wave-local online softmax with 2 cross-lane steps;
+//   * P^T goes to the V row layout through a wave-private LDS slice, P.V on the VALU, and the 4
+//     waves' (m, l, o) are merged after the block's single barrier.
+// The previous version (one block-wide softmax: 6 barriers, the V loads behind the scores):
+// 17.3 -> 16.4 us per layer in a Llama-3-8B B=8 decode step. Neither the grid order (kv head
+// fastest) nor a head-major cache layout changed the time (tools/decode_attn_bench.py).
 template <int D, int G, bool ROPE>
 __global__ __launch_bounds__(256) void decode_attn_kernel(
     const bf16_t* __restrict__ q, int64_t q_sb, int64_t q_sh,     // q [B, Hq, D]
@@ -66,29 +76,32 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
     float* __restrict__ part_o,  // [B, Hq, nsplit, D]
     float* __restrict__ part_ml, // [B, Hq, nsplit, 2]
     int Hq, DecRope rp) {
-  constexpr int LPK = D / 8, KPI = 64 / LPK, KPW = kDecChunk / 4;
-  __shared__ float qs[G][D];
-  __shared__ float ps[G][kDecChunk];
-  __shared__ float red[G][4];
+  constexpr int LPK = D / 8, KPI = 64 / LPK, KPW = kDecChunk / 4, NIT = KPW / KPI;
+  constexpr int KST = D / 32;  // MFMA k-steps over the head dim
+  static_assert(G <= 16 && KPW == 32, "decode tile geometry");
+  __shared__ float pex[4][KPW][G];
   __shared__ float acc_s[4][G][D];
+  __shared__ float mls[4][G][2];
   const int split = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int len = kv_len[0];
-  // fused prologue: the newest token's K / V slice of this lane (dims dl .. dl + 7)
-  bf16x8 knew = {}, vnew = {};
+  const int sub = lane / LPK, dl = (lane % LPK) * 8;  // V row layout
+  const int r16 = lane & 15, kg = lane >> 4;           // MFMA fragment layout
+  bf16x8 vnew = {};
   int newest = -1;
+  const bf16_t* qrow = nullptr;
+  const float *cs = nullptr, *sn = nullptr;
   if constexpr (ROPE) {
     newest = static_cast<int>(rp.slot[0]);
-    const int dl0 = (lane % LPK) * 8;
-    const bf16_t* row = rp.qkv + (int64_t)b * rp.ld;
+    qrow = rp.qkv + (int64_t)b * rp.ld;
     const int half = rp.rot >> 1;
-    const float* cs = rp.cos_t + (int64_t)rp.pos[b] * half;
-    const float* sn = rp.sin_t + (int64_t)rp.pos[b] * half;
-    knew = dec_rope8(row + (int64_t)(Hq + hk) * D, dl0, rp.rot, cs, sn);
-    vnew = load_bf16x8(row + (int64_t)(Hq + rp.Hkv + hk) * D + dl0);
+    cs = rp.cos_t + (int64_t)rp.pos[b] * half;
+    sn = rp.sin_t + (int64_t)rp.pos[b] * half;
+    vnew = load_bf16x8(qrow + (int64_t)(Hq + rp.Hkv + hk) * D + dl);
     if (split == newest / kDecChunk && wv == 0 && lane < LPK) {  // cache write for later steps
-      store_bf16x8(kc + (int64_t)b * c_sb + (int64_t)newest * c_st + (int64_t)hk * c_sh + dl0, knew);
-      store_bf16x8(vc + (int64_t)b * c_sb + (int64_t)newest * c_st + (int64_t)hk * c_sh + dl0, vnew);
+      const bf16x8 knew = dec_rope8(qrow + (int64_t)(Hq + hk) * D, dl, rp.rot, cs, sn);
+      store_bf16x8(kc + (int64_t)b * c_sb + (int64_t)newest * c_st + (int64_t)hk * c_sh + dl, knew);
+      store_bf16x8(vc + (int64_t)b * c_sb + (int64_t)newest * c_st + (int64_t)hk * c_sh + dl, vnew);
     }
   }
   int lo = kv_start ? kv_start[b] : 0;
@@ -103,123 +116,97 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
     }
     return;
   }
-  if constexpr (ROPE) {
-    const bf16_t* row = rp.qkv + (int64_t)b * rp.ld;
-    const int half = rp.rot >> 1;
-    const float* cs = rp.cos_t + (int64_t)rp.pos[b] * half;
-    const float* sn = rp.sin_t + (int64_t)rp.pos[b] * half;
-    for (int i = tid; i < G * (D / 8); i += 256) {
-      const int g = i / (D / 8), d0 = (i % (D / 8)) * 8;
-      const bf16x8 qv = dec_rope8(row + (int64_t)(hk * G + g) * D, d0, rp.rot, cs, sn);
+  const int kw0 = base + wv * KPW;  // this wave's first key
+  const bf16_t* kb0 = kc + (int64_t)b * c_sb + (int64_t)hk * c_sh;
+  const bf16_t* vb0 = vc + (int64_t)b * c_sb + (int64_t)hk * c_sh + dl;
+  // ---- all loads up front (keys clamped into [k0, k1): unconditional, masked later)
+  s16x8 kf[2][KST];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) qs[g][d0 + j] = bf2f(qv[j]) * scale_log2;
-    }
-  } else {
-    for (int i = tid; i < G * D; i += 256) {
-      const int g = i / D, d = i % D;
-      qs[g][d] = bf2f(q[(int64_t)b * q_sb + (int64_t)(hk * G + g) * q_sh + d]) * scale_log2;
-    }
-  }
-  __syncthreads();
-  const int sub = lane / LPK, dl = (lane % LPK) * 8;
-  const bf16_t* kbase = kc + (int64_t)b * c_sb + (int64_t)hk * c_sh + dl;
-  const bf16_t* vbase = vc + (int64_t)b * c_sb + (int64_t)hk * c_sh + dl;
-  float qr[G][8];
+  for (int t = 0; t < 2; ++t) {
+    const int key = kw0 + 16 * t + r16;
+    const int kcl = min(max(key, k0), k1 - 1);
 #pragma unroll
-  for (int g = 0; g < G; ++g)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) qr[g][j] = qs[g][dl + j];
-  // ---- phase 1: scores (log2 domain). All of the wave's K rows are loaded up front
-  // (unconditional loads at clamped keys, so the NIT 16-byte loads issue back to back and the
-  // wave has them all in flight), then consumed.
-  constexpr int NIT = KPW / KPI;
-  bf16x8 kvr[NIT];
-#pragma unroll
-  for (int it = 0; it < NIT; ++it) {
-    const int key = min(max(base + wv * KPW + it * KPI + sub, k0), k1 - 1);
-    kvr[it] = load_bf16x8(kbase + (int64_t)key * c_st);
+    for (int s = 0; s < KST; ++s)
+      kf[t][s] = __builtin_bit_cast(s16x8, load_bf16x8(kb0 + (int64_t)kcl * c_st + 32 * s + 8 * kg));
     if constexpr (ROPE) {
-      if (key == newest) kvr[it] = knew;
-    }
-  }
+      if (key == newest) {
 #pragma unroll
-  for (int it = 0; it < NIT; ++it) {
-    const int kl = wv * KPW + it * KPI + sub;  // key within the chunk
-    const int key = base + kl;
-    const bool ok = key >= k0 && key < k1;
-    float s[G];
-#pragma unroll
-    for (int g = 0; g < G; ++g) s[g] = 0.f;
-    {
-      const bf16x8 kv = kvr[it];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float kf = bf2f(kv[j]);
-#pragma unroll
-        for (int g = 0; g < G; ++g) s[g] += qr[g][j] * kf;
+        for (int s = 0; s < KST; ++s)
+          kf[t][s] = __builtin_bit_cast(s16x8, dec_rope8(qrow + (int64_t)(Hq + hk) * D, 32 * s + 8 * kg, rp.rot, cs, sn));
       }
     }
+  }
+  bf16x8 vvr[NIT];
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-#pragma unroll
-      for (int o = 1; o < LPK; o <<= 1) s[g] += __shfl_xor(s[g], o, 64);
-    }
-    if ((lane % LPK) == 0) {
-#pragma unroll
-      for (int g = 0; g < G; ++g) ps[g][kl] = ok ? s[g] : -INFINITY;
+  for (int it = 0; it < NIT; ++it) {
+    const int key = min(max(kw0 + it * KPI + sub, k0), k1 - 1);
+    vvr[it] = load_bf16x8(vb0 + (int64_t)key * c_st);
+    if constexpr (ROPE) {
+      if (key == newest) vvr[it] = vnew;
     }
   }
-  __syncthreads();
-  // ---- softmax over the chunk: thread t < 128 owns key t for every head
-  float mg[G];
+  s16x8 qf[KST];
 #pragma unroll
-  for (int g = 0; g < G; ++g) {
-    const float v = tid < kDecChunk ? ps[g][tid] : -INFINITY;
-    const float m = wave_max(v);
-    if (lane == 0) red[g][wv] = m;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int g = 0; g < G; ++g) mg[g] = fmaxf(fmaxf(red[g][0], red[g][1]), fmaxf(red[g][2], red[g][3]));
-  __syncthreads();
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-    float p = 0.f;
-    if (tid < kDecChunk) {
-      const float sv = ps[g][tid];
-      p = sv == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(sv - mg[g]);
-      ps[g][tid] = p;
+  for (int s = 0; s < KST; ++s) {
+    qf[s] = s16x8{};
+    if (r16 < G) {
+      if constexpr (ROPE)
+        qf[s] = __builtin_bit_cast(s16x8, dec_rope8(qrow + (int64_t)(hk * G + r16) * D, 32 * s + 8 * kg, rp.rot, cs, sn));
+      else
+        qf[s] = __builtin_bit_cast(s16x8, load_bf16x8(q + (int64_t)b * q_sb + (int64_t)(hk * G + r16) * q_sh + 32 * s + 8 * kg));
     }
-    const float l = wave_sum(p);
-    if (lane == 0) red[g][wv] = l;
   }
-  __syncthreads();
-  // ---- phase 2: o[g][d] = sum_key p[g][key] v[key][d]; wave wv owns keys [wv*KPW, wv*KPW+KPW)
+  // ---- S^T[key][g]: lane holds keys kw0 + 16t + 4kg + i (i < 4) of head g = r16
+  f32x4 sacc[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    sacc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KST; ++s) sacc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[t][s], qf[s], sacc[t], 0, 0, 0);
+  }
+  float sc[2][4];
+  float m = -INFINITY;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int key = kw0 + 16 * t + 4 * kg + i;
+      sc[t][i] = (key >= k0 && key < k1) ? sacc[t][i] * scale_log2 : -INFINITY;
+      m = fmaxf(m, sc[t][i]);
+    }
+  m = fmaxf(m, __shfl_xor(m, 16, 64));
+  m = fmaxf(m, __shfl_xor(m, 32, 64));
+  const float muse = m == -INFINITY ? 0.f : m;
+  float l = 0.f;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float p = __builtin_amdgcn_exp2f(sc[t][i] - muse);  // exp2(-inf) = 0 for masked keys
+      l += p;
+      if (r16 < G) pex[wv][16 * t + 4 * kg + i][r16] = p;
+    }
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  // wave-private exchange: this wave's LDS writes complete before its reads (in-order LDS queue)
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  // ---- P.V in the row layout: lane (sub, dl) owns keys it * KPI + sub of the wave's 32
   float o[G][8];
 #pragma unroll
   for (int g = 0; g < G; ++g)
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[g][j] = 0.f;
-  bf16x8 vvr[NIT];
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
-    const int key = min(max(base + wv * KPW + it * KPI + sub, k0), k1 - 1);
-    vvr[it] = load_bf16x8(vbase + (int64_t)key * c_st);
-    if constexpr (ROPE) {
-      if (key == newest) vvr[it] = vnew;
-    }
-  }
-#pragma unroll
-  for (int it = 0; it < NIT; ++it) {
-    const int kl = wv * KPW + it * KPI + sub;  // p = 0 outside [k0, k1) (set above)
+    const int kl = it * KPI + sub;
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      const float p = ps[g][kl];
+      const float p = pex[wv][kl][g];
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[g][j] += p * bf2f(vvr[it][j]);
     }
   }
-  // reduce the KPI key sub-groups of the wave (lanes sharing dl)
 #pragma unroll
   for (int g = 0; g < G; ++g)
 #pragma unroll
@@ -232,15 +219,32 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc_s[wv][g][dl + j] = o[g][j];
   }
+  if (kg == 0 && r16 < G) {
+    mls[wv][r16][0] = m;
+    mls[wv][r16][1] = l;
+  }
   __syncthreads();
+  // ---- merge the 4 waves (fixed order) into this split's partial
   for (int i = tid; i < G * D; i += 256) {
     const int g = i / D, d = i % D;
-    const float v = acc_s[0][g][d] + acc_s[1][g][d] + acc_s[2][g][d] + acc_s[3][g][d];
+    float mm = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) mm = fmaxf(mm, mls[w][g][0]);
+    float v = 0.f, ll = 0.f;
+    if (mm != -INFINITY) {
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const float mw = mls[w][g][0];
+        const float c = mw == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(mw - mm);
+        v += c * acc_s[w][g][d];
+        ll += c * mls[w][g][1];
+      }
+    }
     part_o[(pbase + (int64_t)g * nsplit) * D + d] = v;
-  }
-  if (tid < G) {
-    part_ml[(pbase + (int64_t)tid * nsplit) * 2 + 0] = mg[tid];
-    part_ml[(pbase + (int64_t)tid * nsplit) * 2 + 1] = red[tid][0] + red[tid][1] + red[tid][2] + red[tid][3];
+    if (d == 0) {
+      part_ml[(pbase + (int64_t)g * nsplit) * 2 + 0] = mm;
+      part_ml[(pbase + (int64_t)g * nsplit) * 2 + 1] = ll;
+    }
   }
 }
 
@@ -294,35 +298,67 @@ void launch_rope_cache(const bf16_t* qkv, int64_t ld, bf16_t* q_out, bf16_t* kc,
                                           sin_t, pos, B, Hq, Hkv, D, rot);
 }
 
-// one block per (b, h): merge the splits (log2-domain running max)
+// one 64-thread block per (b, h): merge the splits (log2-domain running max). The split
+// statistics are read in parallel (one split per lane, 64 at a time) and the per-split weights
+// go through LDS, so the output pass issues its part_o loads 8 splits at a time instead of one
+// dependent load chain per split (which made this launch grow by ~0.5 us per split).
 template <int D>
 __global__ __launch_bounds__(64) void decode_combine_kernel(const float* __restrict__ part_o,
                                                              const float* __restrict__ part_ml,
                                                              int nsplit, bf16_t* __restrict__ out,
                                                              int64_t o_sb, int64_t o_sh, int Hq) {
-  const int bh = blockIdx.x;
+  __shared__ float wsp[64];
+  const int bh = blockIdx.x, lane = threadIdx.x;
   const int b = bh / Hq, h = bh % Hq;
   const float* ml = part_ml + (int64_t)bh * nsplit * 2;
+  const float* po = part_o + (int64_t)bh * nsplit * D;
   float m = -INFINITY;
-  for (int s = 0; s < nsplit; ++s) m = fmaxf(m, ml[2 * s]);
+  for (int s = lane; s < nsplit; s += 64) m = fmaxf(m, ml[2 * s]);
+  m = wave_max(m);
   constexpr int DPT = D / 64;
   float acc[DPT] = {};
   float l = 0.f;
   if (m != -INFINITY) {
-    for (int s = 0; s < nsplit; ++s) {
-      const float ms = ml[2 * s];
-      if (ms == -INFINITY) continue;
-      const float c = __builtin_amdgcn_exp2f(ms - m);
-      l += c * ml[2 * s + 1];
+    for (int s0 = 0; s0 < nsplit; s0 += 64) {
+      const int s = s0 + lane;
+      float c = 0.f;
+      if (s < nsplit) {
+        const float ms = ml[2 * s];
+        c = ms == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(ms - m);
+        l += c * ml[2 * s + 1];
+      }
+      wsp[lane] = c;
+      __syncthreads();
+      const int n = min(64, nsplit - s0);
+      int j = 0;
+      for (; j + 8 <= n; j += 8) {
+        float v[8][DPT];
 #pragma unroll
-      for (int j = 0; j < DPT; ++j)
-        acc[j] += c * part_o[((int64_t)bh * nsplit + s) * D + threadIdx.x * DPT + j];
+        for (int u = 0; u < 8; ++u)
+#pragma unroll
+          for (int t = 0; t < DPT; ++t) v[u][t] = po[(int64_t)(s0 + j + u) * D + lane * DPT + t];
+        // an empty split never wrote its part_o row (uninitialised memory): weight 0 selects 0
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const float w = wsp[j + u];
+#pragma unroll
+          for (int t = 0; t < DPT; ++t) acc[t] += w == 0.f ? 0.f : w * v[u][t];
+        }
+      }
+      for (; j < n; ++j) {
+        const float w = wsp[j];
+#pragma unroll
+        for (int t = 0; t < DPT; ++t)
+          acc[t] += w == 0.f ? 0.f : w * po[(int64_t)(s0 + j) * D + lane * DPT + t];
+      }
+      __syncthreads();
     }
+    l = wave_sum(l);
   }
   const float inv = l > 0.f ? 1.f / l : 0.f;
 #pragma unroll
   for (int j = 0; j < DPT; ++j)
-    out[(int64_t)b * o_sb + (int64_t)h * o_sh + threadIdx.x * DPT + j] = f2bf(acc[j] * inv);
+    out[(int64_t)b * o_sb + (int64_t)h * o_sh + lane * DPT + j] = f2bf(acc[j] * inv);
 }
 
 template <int D>
