@@ -605,7 +605,7 @@ def test_embedding_gather_and_sorted_scatter_add(gdtype):
 def test_fused_reward_head(pooling):
     """Fused pool + dropout + Linear(H,1): eval == the PyTorch head (fp32 reference); train-mode
     dropout has the right keep rate and its backward is the exact derivative of its own forward
-    (directional finite difference at a fixed seed)."""
+    at a fixed seed (gradients checked against the dropped pooled rows the forward returns)."""
     from distributed_llm_alignment_amd.models import build_model, get_config
     from distributed_llm_alignment_amd.models.reward import RewardModel
 
@@ -624,7 +624,10 @@ def test_fused_reward_head(pooling):
         h = rm.backbone(ids, mask)
         ref = rm.scorer[1](rm.pool(h, mask)).squeeze(-1).float()
     assert torch.allclose(s, ref, atol=2e-2, rtol=2e-2), (s, ref)
-    # train mode: directional derivative check of the fused head alone at a fixed seed
+    # train mode: the backward is the exact derivative of the forward at the same seed. score_b =
+    # <pooled_b, w> + bias with pooled_b the dropped (and 1/(1-p)-scaled) pooled row that the
+    # forward returns, so dL/dw = sum_b pooled_b, and dL/dhidden routes w * keep * scale to the
+    # pooled positions (last token, or every valid token / count for mean pooling)
     from distributed_llm_alignment_amd.models.reward import _RewardHeadFn
     from distributed_llm_alignment_amd.models.transformer import attention_layout
 
@@ -637,13 +640,19 @@ def test_fused_reward_head(pooling):
     hv = hh.clone().requires_grad_(True)
     sc = _RewardHeadFn.apply(hv, w, None, lt, mk, 0.5, 1234)
     sc.sum().backward()
-    dirn = torch.randn_like(w, dtype=torch.float32)
-    eps = 1e-2
-    sp = _RewardHeadFn.apply(hh, (w.detach().float() + eps * dirn).to(torch.bfloat16), None, lt, mk, 0.5, 1234)
-    sm = _RewardHeadFn.apply(hh, (w.detach().float() - eps * dirn).to(torch.bfloat16), None, lt, mk, 0.5, 1234)
-    fd = ((sp - sm).sum() / (2 * eps)).item()
-    an = (w.grad.float() * dirn).sum().item()
-    assert abs(fd - an) <= 5e-2 * max(1.0, abs(an)), (fd, an)
+    _, pooled = torch.ops.dla.reward_head_fwd(hh, lt, mk, w.detach().reshape(-1), None, 0.5, 1234)
+    assert torch.allclose(sc.float(), pooled @ w.detach().float().reshape(-1), atol=1e-2, rtol=1e-2)
+    gw = pooled.sum(0)
+    assert torch.allclose(w.grad.float().reshape(-1), gw, atol=1e-2 * gw.abs().max().item(), rtol=1e-2)
+    keep = (pooled != 0).float() * 2.0  # 1 / (1 - p) on kept columns
+    wk = keep * w.detach().float().reshape(1, -1)  # [B, H]
+    if pooling == "mean":
+        cnt = mask.float().sum(1, keepdim=True).clamp_min(1.0)
+        ref_g = mask.float().unsqueeze(-1) * (wk / cnt).unsqueeze(1)
+    else:
+        ref_g = torch.zeros_like(hv, dtype=torch.float32)
+        ref_g[torch.arange(4, device=dev), last.long()] = wk
+    assert torch.allclose(hv.grad.float(), ref_g, atol=2e-3, rtol=1e-2)
     # keep rate of the hash dropout ~ 1 - p
     _, pooled = torch.ops.dla.reward_head_fwd(hh, lt, mk, w.detach().reshape(-1), None, 0.5, 99)
     kept = (pooled != 0).float().mean().item()
