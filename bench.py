@@ -210,6 +210,7 @@ def main(argv=None) -> int:
     sync()
     barrier()
     sync()
+    engine.comm_timer.reset()
     t0 = time.perf_counter()
     if args.profile_dir:
         from torch.profiler import ProfilerActivity, profile
@@ -231,6 +232,12 @@ def main(argv=None) -> int:
 
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
     elapsed = float(t_max.item())
+    # gradient-comm time the step did NOT hide: the compute stream's wait on RCCL at the step
+    # boundary (0 without collectives), averaged over the timed steps, max over ranks
+    exposed = torch.tensor([engine.comm_timer.total_ms() / args.steps], dtype=torch.float64, device=dev)
+    if st.initialized:
+        dist.all_reduce(exposed, op=dist.ReduceOp.MAX)
+    exposed_ms = float(exposed.item())
     if args.profile_dir and st.rank == 0:
         os.makedirs(args.profile_dir, exist_ok=True)
         prof.export_chrome_trace(os.path.join(args.profile_dir, "trace.json"))
@@ -277,6 +284,7 @@ def main(argv=None) -> int:
                 "mfu": round(tflops_gpu / PEAK_DENSE_BF16_TFLOPS, 4) if dev.type == "cuda" else None,
                 "backend": st.backend or "single-process",
                 "final_loss": round(float(state["loss"].item()), 5),
+                "comm_exposed_ms_per_step": round(exposed_ms, 2),
                 "gemm_selection": "tunableop:" + gemm_mode,
             },
         }

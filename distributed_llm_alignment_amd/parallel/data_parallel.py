@@ -41,7 +41,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from ..optim.adamw import adamw_update, clip_coefficient, grad_sumsq
-from .dist import DistState, state as dist_state
+from .dist import DistState, ExposedCommTimer, state as dist_state
 
 ALIGN = 64  # elements; keeps every param view 128-byte aligned for 16-byte vector kernels
 
@@ -114,6 +114,7 @@ class DataParallelEngine:
             raise ValueError(f"mixed parameter dtypes {dtypes}")
         self.dtype = params[0].dtype
         self.device = params[0].device
+        self.comm_timer = ExposedCommTimer(self.device)  # exposed gradient-comm wait per step
         self.grad_dtype = grad_dtype or self.dtype
         self.grad_fp32 = self.grad_dtype == torch.float32 and self.dtype != torch.float32
         self.reduce_dtype = reduce_dtype or self.grad_dtype
@@ -345,10 +346,12 @@ class DataParallelEngine:
             while self._launched < len(self.buckets):
                 self._launch(self._launched)
                 self._launched += 1
+            self.comm_timer.begin()
             for h, post in self._handles:
                 h.wait()
                 if post is not None:
                     post()
+            self.comm_timer.end()
         self._handles = []
         self._launched = 0
         self._ready = [0] * len(self.buckets)

@@ -139,3 +139,63 @@ def split_for_rank(items: list, rank: Optional[int] = None, world: Optional[int]
     per, extra = divmod(n, world)
     start = rank * per + min(rank, extra)
     return items[start:start + per + (1 if rank < extra else 0)]
+
+
+class ExposedCommTimer:
+    """Time the training step spends waiting for its gradient collectives at the step boundary
+    (`finish_grad_sync`): the part of the reduce-scatter / all-reduce that nothing overlapped.
+
+    On a GPU, events go on the compute stream around the waits. `Work.wait()` makes that stream
+    wait for RCCL's stream, so the device time between the two events is exactly the stall. It is
+    about 0 when the collectives finished behind earlier work (backward compute, the next RLHF
+    rollout), and the whole tail of the reduce otherwise. On the CPU (gloo) `wait()` blocks the
+    host, and host time is measured. `last_ms()` reads the most recent interval; it synchronises
+    on the end event, so call it at logging time, not inside the step."""
+
+    def __init__(self, device: torch.device):
+        self.cuda = device.type == "cuda"
+        self._a = self._b = None
+        self._t0 = self._host_ms = 0.0
+        self._hist: list = []  # every interval since reset(): (start, end) events or host ms
+
+    def begin(self):
+        if self.cuda:
+            self._a = torch.cuda.Event(enable_timing=True)
+            self._a.record()
+        else:
+            import time
+
+            self._t0 = time.perf_counter()
+
+    def end(self):
+        if self.cuda:
+            self._b = torch.cuda.Event(enable_timing=True)
+            self._b.record()
+            self._hist.append((self._a, self._b))
+        else:
+            import time
+
+            self._host_ms = (time.perf_counter() - self._t0) * 1e3
+            self._hist.append(self._host_ms)
+        if len(self._hist) > 4096:
+            del self._hist[:2048]
+
+    def reset(self):
+        self._hist = []
+
+    def total_ms(self) -> float:
+        """Sum over every interval since reset() (synchronises on the last one)."""
+        if self.cuda:
+            if self._hist:
+                self._hist[-1][1].synchronize()
+            return float(sum(a.elapsed_time(b) for a, b in self._hist))
+        return float(sum(self._hist))
+
+    def last_ms(self) -> float:
+        if self.cuda:
+            if self._b is None:
+                return 0.0
+            self._b.synchronize()
+            return float(self._a.elapsed_time(self._b))
+        return self._host_ms
+

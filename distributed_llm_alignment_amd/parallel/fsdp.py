@@ -39,7 +39,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from ..optim.adamw import adamw_update, clip_coefficient, grad_sumsq
-from .dist import DistState, state as dist_state
+from .dist import DistState, ExposedCommTimer, state as dist_state
 
 ALIGN = 64
 
@@ -160,6 +160,7 @@ class _ShardedBase:
                     p.data = view
                 self.param_shard[u.shard_off:u.shard_off + u.chunk].copy_(self._my_chunk(u.full, u))
         self._pending = []  # in-flight reduce-scatters: (handle, tmp, unit)
+        self.comm_timer = ExposedCommTimer(self.device)  # exposed gradient-comm wait per step
         self._seen = set()
         for u in units:  # gather before the unit's first layer, free after its last
             if u.modules:
@@ -384,8 +385,10 @@ class FullyShardedEngine(_ShardedBase):
         for u in sorted(self.units, key=lambda x: -x.idx):
             if not u.reduced and (u.ready > 0 or u.in_backward or u.is_root):
                 self._reduce(u)
+        self.comm_timer.begin()
         while self._pending:
             self._drain_one()
+        self.comm_timer.end()
         self._seen = set()
         for u in self.units:
             u.ready = 0

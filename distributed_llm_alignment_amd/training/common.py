@@ -275,7 +275,8 @@ def train_loop(ctx: TrainContext, loader, sampler, engine: DataParallelEngine, s
             last_metrics = metrics
             global_step += 1
             if log_every and global_step % log_every == 0:
-                rec = {"train/loss": running.average, "train/grad_norm": engine.last_grad_norm}
+                rec = {"train/loss": running.average, "train/grad_norm": engine.last_grad_norm,
+                       "train/comm_exposed_ms": engine.comm_timer.last_ms()}
                 if scheduler is not None:
                     rec["train/lr"] = scheduler.lr(global_step)
                 if extra_log_fn is not None:

@@ -10,7 +10,9 @@ fixes #8), then REINFORCE with a KL-shaped reward and a mean baseline:
 
 Overlap (BASELINE north star, `ppo.async_rollouts: true`, off by default since it changes the
 semantics to one-step-stale rollouts): step k+1's rollouts are generated while step k's gradient
-reduce-scatter is still in flight on RCCL's stream.
+reduce-scatter is still in flight on RCCL's stream. `train/comm_exposed_ms` logs the part of the
+gradient collectives the step did not hide (the compute stream's wait at `engine.step`;
+parallel/dist.py ExposedCommTimer); tests/test_distributed_cpu.py measures it with 2 gloo ranks.
 
 `ppo.algorithm: ppo` (not in the reference, whose loop is critic-free) switches to token-level
 actor-critic PPO, the north-star "PPO RLHF (actor + critic + reward)" configuration: a critic
@@ -152,7 +154,8 @@ def main(argv=None) -> int:
         running.update(loss.detach())
         if (step + 1) % log_every == 0:
             ctx.logger.log({"train/loss": running.average, "train/kl": m["kl"],
-                            "train/reward_mean": scores.mean(), "train/grad_norm": engine.last_grad_norm},
+                            "train/reward_mean": scores.mean(), "train/grad_norm": engine.last_grad_norm,
+                            "train/comm_exposed_ms": engine.comm_timer.last_ms()},
                            step + 1)
             running = RunningLoss()
     barrier()
@@ -210,7 +213,8 @@ def _ppo_loop(ctx, config, ppo, policy, ref, rm, rollout, engine, steps, kl_coef
                             "train/reward_mean": stats["scores"].mean(),
                             "train/policy_loss": m["policy_loss"], "train/value_loss": m["value_loss"],
                             "train/clipfrac": m["clipfrac"], "train/approx_kl": m["approx_kl"],
-                            "train/grad_norm": engine.last_grad_norm}, step + 1)
+                            "train/grad_norm": engine.last_grad_norm,
+                            "train/comm_exposed_ms": engine.comm_timer.last_ms()}, step + 1)
             running = RunningLoss()
     barrier()
     out = save_state(config["logging"]["output_dir"], [policy.model, ref.model, rm, critic], engine, None,

@@ -183,6 +183,34 @@ def test_graph_generation_matches_eager_sampled_large_vocab(top_k, top_p):
     assert len(set(a[:, 16:].flatten().tolist())) > 24  # sampled, not a fixed point
 
 
+@pytest.mark.parametrize("fp8", [False, True])
+def test_moe_generation_graph_matches_eager(fp8):
+    """Mixtral-style policy: routing + device-driven grouped expert GEMMs (no host sync) inside
+    the captured decode step give the same greedy tokens as eager decoding and the graph is
+    actually used. With fp8 experts (quantised weight copies cached outside the graph) capture
+    is refused and use_graph=True falls back to eager decoding, still with the same tokens."""
+    from distributed_llm_alignment_amd.models import build_model, generate, get_config
+    from distributed_llm_alignment_amd.models import generation as gen
+
+    gen.clear_graph_cache()
+    cfg = get_config("tiny-mixtral", hidden_size=256, intermediate_size=512, num_experts=8)
+    m = build_model(cfg, device=DEV, dtype=torch.bfloat16, seed=3)
+    for layer in m.layers:
+        layer.mlp.fp8 = fp8
+    assert gen._graph_capable(m) == (not fp8)
+    g = torch.Generator(device=DEV).manual_seed(6)
+    ids = torch.randint(3, cfg.vocab_size, (3, 17), device=DEV, generator=g)
+    am = torch.ones_like(ids)
+    am[2, :4] = 0
+    ids[2, :4] = 0
+    a = generate(m, ids, am, max_new_tokens=16, do_sample=False, eos_token_id=-1, use_graph=False)
+    b = generate(m, ids, am, max_new_tokens=16, do_sample=False, eos_token_id=-1, use_graph=True)
+    assert torch.equal(a, b), (a, b)
+    captured = id(m) in gen._GRAPH_SLOT and gen._GRAPH_SLOT[id(m)][3].graph is not None
+    assert captured == (not fp8)
+    gen.clear_graph_cache()
+
+
 def test_decode_graph_reused_across_generate_calls():
     """The second generate() of the same shape replays the first call's captured decode step
     (no new KV cache, no re-capture) and still matches eager decoding on new prompts and new
