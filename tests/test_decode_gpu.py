@@ -193,7 +193,7 @@ def test_moe_generation_graph_matches_eager(fp8):
     from distributed_llm_alignment_amd.models import generation as gen
 
     gen.clear_graph_cache()
-    cfg = get_config("tiny-mixtral", hidden_size=256, intermediate_size=512, num_experts=8)
+    cfg = get_config("tiny-mixtral", hidden_size=256, head_dim=64, intermediate_size=512, num_experts=8)
     m = build_model(cfg, device=DEV, dtype=torch.bfloat16, seed=3)
     for layer in m.layers:
         layer.mlp.fp8 = fp8
