@@ -545,9 +545,44 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnBwdParams p) {
     }
   }
 
+  // Row constants (log2-domain LSE, delta) of this lane's 16 accumulator rows
+  // r = (i&3) + 8(i>>2) + 4h = four runs of 4 consecutive rows: 4 + 4 dwordx4 loads, issued in
+  // phase B of the previous tile so that no memory wait sits in front of the MFMA chains (one
+  // dword load per row, issued at the top of the tile, cost a full round trip per tile).
+  f32x4 lr4[4], dl4[4];
+  const bool rows_vec = (p.Tq & 3) == 0;
+  auto load_rows = [&](int it) {
+    const int hq = hq0 + it / nqt;
+    const int qt = qt0 + (it % nqt) * BQ;
+    const int64_t rb = (static_cast<int64_t>(b) * p.Hq + hq) * p.Tq;
+    if (rows_vec && qt + BQ <= p.Tq) {  // full tile (wave-uniform), 16-B aligned runs
+      const float* lp = p.lse2 + rb + qt + 4 * h;
+      const float* dp = p.delta + rb + qt + 4 * h;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        lr4[g] = *reinterpret_cast<const f32x4*>(lp + 8 * g);
+        dl4[g] = *reinterpret_cast<const f32x4*>(dp + 8 * g);
+      }
+    } else {  // partial tile / odd Tq: clamped unpredicated loads, rows past Tq masked (p = 0)
+      const int rlim = p.Tq - qt - 4 * h;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int r = 8 * g + e;
+          const int64_t ri = rb + min(qt + 4 * h + r, p.Tq - 1);
+          const float a = p.lse2[ri], c = p.delta[ri];
+          lr4[g][e] = r < rlim ? a : INFINITY;
+          dl4[g][e] = r < rlim ? c : 0.f;
+        }
+      }
+    }
+  };
+
   if (n_iter > 0) {
     prefetch(0);
     stage();
+    load_rows(0);
     if (n_iter > 1) prefetch(1);
   }
   __syncthreads();
@@ -556,55 +591,35 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnBwdParams p) {
     const int hq = hq0 + it / nqt;
     const int qt = qt0 + (it % nqt) * BQ;
 
-    // row constants of this lane's 16 accumulator rows r = (i&3) + 8(i>>2) + 4h, from L2; they
-    // are first needed after the sub-tile-0 MFMA chains
-    float lr[16], dl[16];
-    {
-      const int64_t rb = (static_cast<int64_t>(b) * p.Hq + hq) * p.Tq;
-      if (qt + BQ <= p.Tq) {  // full tile (wave-uniform): one base, immediate offsets
-        const float* lp = p.lse2 + rb + qt + 4 * h;
-        const float* dp = p.delta + rb + qt + 4 * h;
+    // which of the two 32-key sub-tiles see a query of the tile, which need masks (wave-uniform)
+    bool act[2], need_mask[2];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int r = (i & 3) + 8 * (i >> 2);
-          lr[i] = lp[r];
-          dl[i] = dp[r];
-        }
-      } else {  // last partial tile: clamped unpredicated loads, rows past Tq masked (p = 0)
-        const int rlim = p.Tq - qt - 4 * h;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int r = (i & 3) + 8 * (i >> 2);
-          const int64_t ri = rb + min(qt + 4 * h + r, p.Tq - 1);
-          const float a = p.lse2[ri], c = p.delta[ri];
-          lr[i] = r < rlim ? a : INFINITY;
-          dl[i] = r < rlim ? c : 0.f;
+    for (int j = 0; j < 2; ++j) {
+      const int kj0 = kw + 32 * j;
+      act[j] = kj0 < kend && kj0 + 32 > kbeg && qt < kse_hi[j];
+      need_mask[j] = kj0 < kbeg || kj0 + 32 > kend || qt + BQ > p.Tq || qt + BQ > kse_lo[j];
+      if (CAUSAL) {
+        act[j] = act[j] && kj0 <= qt + BQ - 1 + p.causal_off;
+        need_mask[j] = need_mask[j] || (kj0 + 31 > qt + p.causal_off);
+        if (p.window > 0) {
+          act[j] = act[j] && (kj0 + 31 > qt + p.causal_off - p.window);
+          need_mask[j] = need_mask[j] || (kj0 <= qt + BQ - 1 + p.causal_off - p.window);
         }
       }
     }
 
-    // ---------------------------------------------------------------- phase A (per sub-tile)
+    // ---------------------------------------------------------------- phase A
+    // per sub-tile: S = Q K^T and dP = dO V^T (key on the lane), two MFMA chains; every
+    // fragment is read one k-step ahead and sched_barriers pin that order: at one wave per
+    // SIMD, a read the compiler sinks onto its MFMA stalls the matrix pipe for the whole LDS
+    // latency. Then P and dS (zero for an inactive sub-tile), packed as the bf16 B operands of
+    // the dV / dK products. (Both sub-tiles' chains at once need 64 accumulators on top of the
+    // 256 dK / dV ones: the compiler then spills.)
+    s16x8 pb0[2], pb1[2], sb0[2], sb1[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int kj0 = kw + 32 * j;
-      // does this sub-tile see any query of the tile? which masks apply? (wave-uniform)
-      bool act = kj0 < kend && kj0 + 32 > kbeg && qt < kse_hi[j];
-      bool need_mask = kj0 < kbeg || kj0 + 32 > kend || qt + BQ > p.Tq || qt + BQ > kse_lo[j];
-      if (CAUSAL) {
-        act = act && kj0 <= qt + BQ - 1 + p.causal_off;
-        need_mask = need_mask || (kj0 + 31 > qt + p.causal_off);
-        if (p.window > 0) {
-          act = act && (kj0 + 31 > qt + p.causal_off - p.window);
-          need_mask = need_mask || (kj0 <= qt + BQ - 1 + p.causal_off - p.window);
-        }
-      }
-      // P / dS fragments (zero for an inactive sub-tile). Only these cross the branch: the dK / dV
-      // MFMAs below run unconditionally, since accumulators updated under a branch get phi
-      // copies, which for 256 accumulator registers means spilling every iteration.
-      s16x8 pb0 = {}, pb1 = {}, sb0 = {}, sb1 = {};
-      if (act) {
-        // S (rows = queries, cols = this sub-tile's keys) and dP = dO V^T; operand fragments
-        // double-buffered one k-step ahead
+      pb0[j] = pb1[j] = sb0[j] = sb1[j] = s16x8{};
+      if (act[j]) {
         f32x16 sacc = f32x16{}, dpacc = f32x16{};
         const bf16_t* Kj = Ks + (64 * w + 32 * j) * D;
         const bf16_t* Vj = Vs + (64 * w + 32 * j) * D;
@@ -619,13 +634,14 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnBwdParams p) {
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
           if (s + 1 < KS) ld_sdp(s + 1, (s + 1) & 1);
+          __builtin_amdgcn_sched_barrier(0);
           sacc = mfma32(fa[s & 1], fb[s & 1], sacc);
           dpacc = mfma32(fc[s & 1], fd[s & 1], dpacc);
+          __builtin_amdgcn_sched_barrier(0);
         }
-        // P and dS; masking is branch-free: per lane, key kj vs query qt + rr + 4h
-        // visible queries of this lane's key kj: accumulator rows rr = (i&3) + 8(i>>2) (query
-        // qt + rr + 4h) in [lo, hi), one unsigned compare per element
-        const int kj = kj0 + l32;
+        // masking is branch-free per lane: key kj vs query qt + rr + 4h, visible iff rr in
+        // [lo, hi), one unsigned compare per element
+        const int kj = kw + 32 * j + l32;
         int lo = 0, hi = min(p.Tq, kse[j]) - qt - 4 * h;
         if (kj < kbeg || kj >= kend) hi = 0;
         if (CAUSAL) {
@@ -637,39 +653,53 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnBwdParams p) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int rr = (i & 3) + 8 * (i >> 2);
-          float pv = ex2(fmaf(sacc[i], p.scale2, -lr[i]));
-          if (need_mask) pv = static_cast<unsigned>(rr - lo) < span ? pv : 0.f;
+          float pv = ex2(fmaf(sacc[i], p.scale2, -lr4[i >> 2][i & 3]));
+          if (need_mask[j]) pv = static_cast<unsigned>(rr - lo) < span ? pv : 0.f;
           sacc[i] = pv;
-          dpacc[i] = pv * (dpacc[i] - dl[i]);
+          dpacc[i] = pv * (dpacc[i] - dl4[i >> 2][i & 3]);
         }
-        pb0 = pack8(sacc, 0);
-        pb1 = pack8(sacc, 8);
-        sb0 = pack8(dpacc, 0);
-        sb1 = pack8(dpacc, 8);
+        pb0[j] = pack8(sacc, 0);
+        pb1[j] = pack8(sacc, 8);
+        sb0[j] = pack8(dpacc, 0);
+        sb1[j] = pack8(dpacc, 8);
       }
-      {
-        // dV^T += dO^T P ; dK^T += Q^T dS   (k = query in the accumulator's permuted row order);
-        // the four transposed fragments of tile dt+1 are read while tile dt's MFMAs run
-        s16x8 ta[2], tb[2], tc[2], td[2];
-        auto ld_kv = [&](int dt, int sl) {  // tr_frag_perm of rows 4h.. / 16+4h.., column tile dt
-          ta[sl] = cat4(tr_read(dOs + toff[dt][0]), tr_read(dOs + toff[dt][1]));
-          tb[sl] = cat4(tr_read(dOs + 16 * D + toff[dt][0]), tr_read(dOs + 16 * D + toff[dt][1]));
-          tc[sl] = cat4(tr_read(Qs + toff[dt][0]), tr_read(Qs + toff[dt][1]));
-          td[sl] = cat4(tr_read(Qs + 16 * D + toff[dt][0]), tr_read(Qs + 16 * D + toff[dt][1]));
-        };
-        ld_kv(0, 0);
+    }
+
+    // transposed dO / Q fragments of column tile dt (A operands of dV^T += dO^T P and
+    // dK^T += Q^T dS, k = query in the accumulator's permuted row order), shared by both
+    // sub-tiles
+    s16x8 ta[2], tb[2], tc[2], td[2];
+    auto ld_kv = [&](int dt, int sl) {
+      ta[sl] = cat4(tr_read(dOs + toff[dt][0]), tr_read(dOs + toff[dt][1]));
+      tb[sl] = cat4(tr_read(dOs + 16 * D + toff[dt][0]), tr_read(dOs + 16 * D + toff[dt][1]));
+      tc[sl] = cat4(tr_read(Qs + toff[dt][0]), tr_read(Qs + toff[dt][1]));
+      td[sl] = cat4(tr_read(Qs + 16 * D + toff[dt][0]), tr_read(Qs + 16 * D + toff[dt][1]));
+    };
+    ld_kv(0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+
+    // dV^T += dO^T P ; dK^T += Q^T dS for both sub-tiles; the four transposed fragments of
+    // column tile dt+1 are read while tile dt's eight MFMAs run. The MFMAs run unconditionally
+    // (zero P / dS when inactive): accumulators updated under a branch get phi copies, which
+    // for 256 accumulator registers means spilling every iteration.
 #pragma unroll
-        for (int dt = 0; dt < DT; ++dt) {
-          if (dt + 1 < DT) ld_kv(dt + 1, (dt + 1) & 1);
-          dv[j][dt] = mfma32(ta[dt & 1], pb0, dv[j][dt]);
-          dv[j][dt] = mfma32(tb[dt & 1], pb1, dv[j][dt]);
-          dk[j][dt] = mfma32(tc[dt & 1], sb0, dk[j][dt]);
-          dk[j][dt] = mfma32(td[dt & 1], sb1, dk[j][dt]);
-        }
+    for (int dt = 0; dt < DT; ++dt) {
+      if (dt + 1 < DT) ld_kv(dt + 1, (dt + 1) & 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        dv[j][dt] = mfma32(ta[dt & 1], pb0[j], dv[j][dt]);
+        dv[j][dt] = mfma32(tb[dt & 1], pb1[j], dv[j][dt]);
+        dk[j][dt] = mfma32(tc[dt & 1], sb0[j], dk[j][dt]);
+        dk[j][dt] = mfma32(td[dt & 1], sb1[j], dk[j][dt]);
       }
-      // dS^T rows of this sub-tile -> [key][32 queries] image: accumulator rows 4g..4g+3 are
-      // queries 8g + 4h + 0..3, i.e. 8-byte unit 2g + h of the key's row
-      const u32x4 ds0 = __builtin_bit_cast(u32x4, sb0), ds1 = __builtin_bit_cast(u32x4, sb1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // dS^T rows -> [key][32 queries] image: accumulator rows 4g..4g+3 are queries 8g + 4h + 0..3,
+    // i.e. 8-byte unit 2g + h of the key's row
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const u32x4 ds0 = __builtin_bit_cast(u32x4, sb0[j]), ds1 = __builtin_bit_cast(u32x4, sb1[j]);
       bf16_t* dSw = dSs + (64 * w + 32 * j) * 32;
       *reinterpret_cast<uint2*>(dSw + woff[0]) = make_uint2(ds0[0], ds0[1]);
       *reinterpret_cast<uint2*>(dSw + woff[1]) = make_uint2(ds0[2], ds0[3]);
@@ -679,9 +709,10 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnBwdParams p) {
     __syncthreads();  // dS visible; every wave is done reading this Q / dO tile
 
     // ---------------------------------------------------------------- phase B
-    if (it + 1 < n_iter) {  // stage the next tile, prefetch the one after it
+    if (it + 1 < n_iter) {  // stage the next tile, prefetch the one after it + next row constants
       stage();
       if (it + 2 < n_iter) prefetch(it + 2);
+      load_rows(it + 1);
     }
     if (w < DT) {  // dQ partial; D = 64: waves 2, 3 have no column slice
       const int dt = w;
@@ -696,7 +727,9 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnBwdParams p) {
 #pragma unroll
       for (int s = 0; s < BKV / 16; ++s) {
         if (s + 1 < BKV / 16) ld_dq(s + 1, (s + 1) & 1);
+        __builtin_amdgcn_sched_barrier(0);
         acc = mfma32(qa[s & 1], qb[s & 1], acc);
+        __builtin_amdgcn_sched_barrier(0);
       }
       // lane holds column d = 32dt + l32, rows q = qt + (i&3) + 8(i>>2) + 4h (128-B row segments)
       // (slab rows are padded to a multiple of 32: every store is in bounds, none predicated)
