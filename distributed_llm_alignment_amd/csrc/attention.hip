@@ -20,10 +20,14 @@
 //     costs one barrier; all 256 queries of the workgroup share each K/V tile.
 //   * XOR-swizzled LDS image usable both for row (ds_read_b128) and transposed reads.
 //   * query blocks are the slowest grid dimension, heaviest causal blocks first (LPT order).
+//   * HP query heads of one GQA group share a workgroup (and so every K/V tile in LDS): the
+//     per-head query block shrinks to 256 / HP rows, which narrows the causal diagonal band where
+//     part of the waves idle (see fwd_dispatch).
 //   * widened store tail (T21): O leaves as 8 x 16 B per lane after a permlane32 swap instead
 //     of 16 x 8 B (the per-lane row stores are issue-bound): 141 -> 121 us causal T = 1024,
 //     190 -> 170 us non-causal (tools/attn_bench.py --ab, one box).
 // Backward: see attn_bwd_kernel.
+#include <cstdlib>
 #include <stdexcept>
 #include "common.h"
 #include "attn_params.h"
@@ -101,10 +105,14 @@ __device__ __forceinline__ s16x8 tr_frag_nat(const bf16_t* img, int r0, int c0, 
 // ==============================================================================================
 constexpr int kFwdKeys = 64;      // keys per K/V tile
 
-// NW waves per workgroup, 32 queries each (NT = 64 NW threads, BQ = 32 NW queries)
-template <int D, bool CAUSAL, int NW>
+// NW waves per workgroup, 32 queries each (NT = 64 NW threads). HP query heads of one GQA group
+// per workgroup (HP = 2: waves 0..NW/2-1 take head 2p, the rest head 2p+1): every K/V tile staged
+// in LDS still feeds 32 NW query rows, but a head's query block is only BQ = 32 NW / HP rows, so
+// the causal diagonal (whose tiles run with part of the waves idle) is HP times narrower.
+template <int D, bool CAUSAL, int NW, int HP>
 __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
-  constexpr int NT = 64 * NW, BQ = 32 * NW, BK = kFwdKeys;
+  constexpr int NT = 64 * NW, BQ = 32 * NW / HP, BK = kFwdKeys;
+  constexpr int WPH = NW / HP;  // waves per head
   constexpr int NCH = D / 8;
   constexpr int KS = D / 16;
   constexpr int DT = D / 32;
@@ -118,13 +126,14 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l32 = lane & 31, h = lane >> 5;
   const int nqb = (p.Tq + BQ - 1) / BQ;
-  const int nbh = p.Hq * p.B;
+  const int nhb = p.Hq / HP;  // head blocks
+  const int nbh = nhb * p.B;
   const int bid = blockIdx.x;
   const int qb = CAUSAL ? nqb - 1 - bid / nbh : bid / nbh;
   const int rest = bid % nbh;
-  const int hq = rest % p.Hq, b = rest / p.Hq;
-  const int hk = hq / (p.Hq / p.Hkv);
-  const int q0 = qb * BQ + w * 32;
+  const int hq = (rest % nhb) * HP + w / WPH, b = rest / nhb;
+  const int hk = hq / (p.Hq / p.Hkv);  // the same for the HP heads (host: group % HP == 0)
+  const int q0 = qb * BQ + (w % WPH) * 32;
   const int qi = q0 + l32;
 
   const bf16_t* qp = p.q + b * p.q_sb + static_cast<int64_t>(hq) * p.q_sh;
@@ -896,13 +905,30 @@ static inline unsigned stream_grid(int64_t work) {
 
 // Forward: 8 waves (256 queries) per workgroup. A 4-wave / 128-query variant (two independent
 // workgroups per CU, unaligned barriers) measured 31-35 % slower at T = 1024 and 4096.
+// HP GQA heads per workgroup: 4 (64-query blocks, 2 waves per head) when the group size allows
+// it, else 2, else 1; DLA_ATTN_FWD_HP=1|2|4 caps it for A/B runs. Same-box A/B (B8 T1024 Hq32
+// Hkv8 D128, tools/gpu_attn_env_ab.sh): causal 140-148 / 131-133 / 124-129 us for HP 1 / 2 / 4,
+// non-causal 217 -> 205-209 us, T = 4096 unchanged (366-379 us).
+template <int D, int HP>
+static void fwd_launch(const AttnParams& p, bool causal, hipStream_t st) {
+  constexpr int NW = 8, BQ = 32 * NW / HP;
+  const int nqb = (p.Tq + BQ - 1) / BQ;
+  const dim3 grid(nqb * (p.Hq / HP) * p.B);
+  if (causal) attn_fwd_kernel<D, true, NW, HP><<<grid, 64 * NW, 0, st>>>(p);
+  else attn_fwd_kernel<D, false, NW, HP><<<grid, 64 * NW, 0, st>>>(p);
+}
+
 template <int D>
 static void fwd_dispatch(const AttnParams& p, bool causal, hipStream_t st) {
-  constexpr int NW = 8;
-  const int nqb = (p.Tq + 32 * NW - 1) / (32 * NW);
-  const dim3 grid(nqb * p.Hq * p.B);
-  if (causal) attn_fwd_kernel<D, true, NW><<<grid, 64 * NW, 0, st>>>(p);
-  else attn_fwd_kernel<D, false, NW><<<grid, 64 * NW, 0, st>>>(p);
+  static const int forced = [] {
+    const char* e = std::getenv("DLA_ATTN_FWD_HP");
+    return e ? std::atoi(e) : 0;
+  }();
+  const int group = p.Hq / p.Hkv;
+  const int want = forced > 0 ? forced : 4;
+  if (want >= 4 && group % 4 == 0) fwd_launch<D, 4>(p, causal, st);
+  else if (want >= 2 && group % 2 == 0) fwd_launch<D, 2>(p, causal, st);
+  else fwd_launch<D, 1>(p, causal, st);
 }
 
 void launch_attn_fwd(const AttnParams& p, int D, bool causal, hipStream_t st) {
