@@ -53,7 +53,8 @@ def parse(argv=None):
     ap.add_argument("--ep", type=int, default=1, help="expert-parallel degree for MoE models")
     ap.add_argument("--sp", type=int, default=1, help="Ulysses sequence-parallel degree (long context)")
     ap.add_argument("--fp8", action="store_true", help="MoE: e4m3 expert GEMMs in the forward")
-    ap.add_argument("--grad-ckpt", action="store_true", help="activation checkpointing (policy)")
+    ap.add_argument("--grad-ckpt", nargs="?", const="full", default=None, choices=("full", "mlp", "attention"),
+                    help="activation recompute on the policy: full layers (bare flag) or selective")
     ap.add_argument("--bucket-mb", type=float, default=256.0)
     ap.add_argument("--ref-stream", type=int, default=0,
                     help="1: frozen reference forward on a second HIP stream, overlapping the policy "
@@ -158,7 +159,7 @@ def main(argv=None) -> int:
             for layer in m.layers:
                 layer.mlp.fp8 = True
     if args.grad_ckpt:
-        policy.gradient_checkpointing_enable()
+        policy.gradient_checkpointing_enable(args.grad_ckpt)
     if args.zero == 3:  # ZeRO-3 / FSDP: per-layer gather, sharded frozen reference
         from distributed_llm_alignment_amd.parallel.fsdp import FullyShardedEngine, ShardedInference
 

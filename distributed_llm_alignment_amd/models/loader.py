@@ -90,8 +90,8 @@ def load_causal_lm(model_name_or_path: str, gradient_checkpointing: bool = True,
         model.load_hf_state_dict(sd, strict=False)
     if split is not None:
         dispatch_layers(model, split)
-    if gradient_checkpointing:
-        model.gradient_checkpointing_enable()
+    if gradient_checkpointing:  # True / "full", or a selective policy ("mlp", "attention")
+        model.gradient_checkpointing_enable(gradient_checkpointing)
     tok = load_tokenizer(model_name_or_path, cfg)
     return ModelBundle(model=model, tokenizer=tok)
 

@@ -245,6 +245,7 @@ class DecoderLayer(nn.Module):
         self.attn = Attention(cfg, device, dtype)
         self.mlp = MoE(cfg, device, dtype) if cfg.is_moe else MLP(cfg, device, dtype)
         self.tp_seq = None  # Megatron-SP: x / resid are this rank's [N/tp, H] token rows
+        self.recompute = None  # selective activation recompute: None | "attention" | "mlp"
 
     def forward(self, x, resid, rope, kv_start, kv_end, positions, cache=None, layer_idx=0, segs=None):
         cfg = self.cfg
@@ -254,16 +255,22 @@ class DecoderLayer(nn.Module):
             from ..parallel.tensor_parallel import tp_grad_sum as w_
         else:
             w_ = _ident
+        rc = self.recompute if (cache is None and self.training and torch.is_grad_enabled()) else None
         h, resid = ops.add_norm(x, resid, w_(self.ln1_w, seq), w_(self.ln1_b, seq), cfg.norm_eps, rms)
-        a = self.attn(h, rope, kv_start, kv_end, positions, cache, layer_idx, segs)
+        if rc == "attention":  # keep h; drop q/k/v, O and the LSE; recompute them in backward
+            a = checkpoint(self.attn, h, rope, kv_start, kv_end, positions, None, layer_idx, segs,
+                           use_reentrant=False)
+        else:
+            a = self.attn(h, rope, kv_start, kv_end, positions, cache, layer_idx, segs)
+        mlp = (lambda t: checkpoint(self.mlp, t, use_reentrant=False)) if rc == "mlp" else self.mlp
         if cfg.parallel_block:
-            return a + self.mlp(h), resid
+            return a + mlp(h), resid
         if cache is not None and rms and self.ln2_b is None and isinstance(self.mlp, MLP):
             fused = self.mlp.decode_norm_glu(a, resid, self.ln2_w, cfg.norm_eps)
             if fused is not None:  # decode: residual add + RMSNorm inside the gate|up launch
                 return fused
         h, resid = ops.add_norm(a, resid, w_(self.ln2_w, seq), w_(self.ln2_b, seq), cfg.norm_eps, rms)
-        return self.mlp(h), resid
+        return mlp(h), resid
 
 
 def _ident(w, _seq=None):
@@ -334,11 +341,31 @@ class CausalLM(nn.Module):
                         if p.numel() < (1 << 26) else _chunked_randn(p, gen, s))
         return self
 
-    def gradient_checkpointing_enable(self):
-        self.gradient_checkpointing = True
+    # Activation recompute policies. "full" (= True, the reference's HF
+    # gradient checkpointing): every decoder layer keeps only its input and is re-run in
+    # backward. Selective: "mlp" re-runs only the MLP block (gate|up GEMM, SwiGLU, down GEMM), so
+    # its [T, 2F] / [T, F] intermediates — the largest activations of a Llama layer — are never
+    # kept; "attention" re-runs only the attention block (qkv GEMM, RoPE, flash attention, o
+    # GEMM). With 288 GB of HBM the 8B DPO bench needs none; they serve long context and 70B.
+    RECOMPUTE_POLICIES = ("full", "mlp", "attention")
+
+    def gradient_checkpointing_enable(self, policy="full", gradient_checkpointing_kwargs=None):
+        if policy is True or policy is None:
+            policy = "full"
+        policy = str(policy).lower()
+        if policy not in self.RECOMPUTE_POLICIES:
+            raise ValueError(f"gradient checkpointing policy must be one of {self.RECOMPUTE_POLICIES}, "
+                             f"got {policy!r}")
+        self.gradient_checkpointing = policy == "full"
+        for layer in self.layers:
+            layer.recompute = None if policy == "full" else policy
+        self.recompute_policy = policy
 
     def gradient_checkpointing_disable(self):
         self.gradient_checkpointing = False
+        for layer in self.layers:
+            layer.recompute = None
+        self.recompute_policy = None
 
     # ------------------------------------------------------------------------------ forward
     @property

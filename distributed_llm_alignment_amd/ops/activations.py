@@ -53,13 +53,16 @@ class _SwiGLUMLPFn(torch.autograd.Function):
         u = F.linear(h2, w_up)
         m, mt = ops.swiglu_fwd_t(u)
         y = F.linear(m, w_down)
-        ctx.save_for_backward(h2, u, mt, w_up, w_down)
+        # (weights on ctx: see ops.linear._LinearMainGradFn)
+        ctx.save_for_backward(h2, u, mt)
+        ctx.w_up, ctx.w_down = w_up, w_down
         ctx.hshape = h.shape
         return y.view(*h.shape[:-1], w_down.shape[0])
 
     @staticmethod
     def backward(ctx, dy):
-        h2, u, mt, w_up, w_down = ctx.saved_tensors
+        h2, u, mt = ctx.saved_tensors
+        w_up, w_down = ctx.w_up, ctx.w_down
         ops = _ext.require()
         dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
         dm = input_grad(dy2, w_down)

@@ -122,13 +122,18 @@ def uses_main_grad(weight: torch.Tensor) -> bool:
 class _LinearMainGradFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias):
-        ctx.save_for_backward(x, weight)
+        # weights ride on ctx, not save_for_backward: under activation recompute
+        # (torch.utils.checkpoint) saved tensors come back as detached aliases without the
+        # engine's attributes (main_grad, the cached W^T), and the grads would be lost
+        ctx.save_for_backward(x)
+        ctx.weight = weight
         ctx.has_bias = bias is not None
         return F.linear(x, weight, bias)
 
     @staticmethod
     def backward(ctx, dy):
-        x, weight = ctx.saved_tensors
+        (x,) = ctx.saved_tensors
+        weight = ctx.weight
         K, N = x.shape[-1], dy.shape[-1]
         dy2 = dy.reshape(-1, N)
         dx = input_grad(dy2, weight).view(x.shape) if ctx.needs_input_grad[0] else None

@@ -44,7 +44,8 @@ class _LinearLogprobFn(torch.autograd.Function):
         if need_grad:
             logits = F.linear(hidden, weight)
             logp, lse = ops.logprob_fwd(logits, targets)
-            ctx.save_for_backward(hidden, weight, targets, lse, logits)
+            ctx.save_for_backward(hidden, targets, lse, logits)
+            ctx.weight = weight  # (on ctx: see ops.linear._LinearMainGradFn)
             return logp
         logp = torch.empty(N, dtype=torch.float32, device=hidden.device)
         for s in range(0, N, _NO_GRAD_CHUNK):
@@ -57,7 +58,8 @@ class _LinearLogprobFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         ops = _ext.require()
-        hidden, weight, targets, lse, logits = ctx.saved_tensors
+        hidden, targets, lse, logits = ctx.saved_tensors
+        weight = ctx.weight
         ops.logprob_bwd(logits, targets, lse, g.float().contiguous())
         dlogits = logits  # rewritten in place
         dh = input_grad(dlogits, weight) if ctx.needs_input_grad[0] else None

@@ -206,13 +206,15 @@ class _ExpertsFn(torch.autograd.Function):
                     torch.mm(xs[s:s + c], w_up[e].t(), out=gu[s:s + c])
                     torch.mm(swiglu(gu[s:s + c]), w_down[e].t(), out=ys[s:s + c])
                 s += c
-        ctx.save_for_backward(xs, gu, w_up, w_down)
+        ctx.save_for_backward(xs, gu)
+        ctx.w_up, ctx.w_down = w_up, w_down  # (on ctx: see ops.linear._LinearMainGradFn)
         ctx.counts = list(counts)
         return ys
 
     @staticmethod
     def backward(ctx, dys):
-        xs, gu, w_up, w_down = ctx.saved_tensors
+        xs, gu = ctx.saved_tensors
+        w_up, w_down = ctx.w_up, ctx.w_down
         dys = dys.contiguous()
         need_x = ctx.needs_input_grad[0]
         dxs = torch.zeros_like(xs) if need_x else None
@@ -263,12 +265,14 @@ class _GroupedExpertsFn(torch.autograd.Function):
         else:
             gu, a = C.gg_fwd_swiglu(xs, w_up, offs, None, None)
             ys = C.gg_fwd(a, w_down, offs, None, None)
-        ctx.save_for_backward(xs, gu, w_up, w_down, offs)
+        ctx.save_for_backward(xs, gu, offs)
+        ctx.w_up, ctx.w_down = w_up, w_down  # (on ctx: see ops.linear._LinearMainGradFn)
         return ys
 
     @staticmethod
     def backward(ctx, dys):
-        xs, gu, w_up, w_down, offs = ctx.saved_tensors
+        xs, gu, offs = ctx.saved_tensors
+        w_up, w_down = ctx.w_up, ctx.w_down
         C = _ext.require()
         dys = dys.contiguous()
         # da = dy . W_down fused with the SwiGLU backward -> dgu, plus the recomputed a

@@ -234,13 +234,15 @@ class _VPLogprobFn(torch.autograd.Function):
         tl = torch.where(own, logp_l + lse_l, torch.zeros_like(logp_l))
         dist.all_reduce(tl, group=group)
         logp = torch.where(targets >= 0, tl - lse, torch.zeros_like(tl))
-        ctx.save_for_backward(hidden, weight_l, targets, lse, logits_l)
+        ctx.save_for_backward(hidden, targets, lse, logits_l)
+        ctx.weight_l = weight_l  # (on ctx: see ops.linear._LinearMainGradFn)
         ctx.off, ctx.group = off, group
         return logp
 
     @staticmethod
     def backward(ctx, g):
-        hidden, weight_l, targets, lse, logits_l = ctx.saved_tensors
+        hidden, targets, lse, logits_l = ctx.saved_tensors
+        weight_l = ctx.weight_l
         dlog = _local_bwd(logits_l, targets, lse, g, ctx.off)
         dh = None
         if ctx.needs_input_grad[0]:

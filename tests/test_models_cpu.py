@@ -295,3 +295,30 @@ def test_greedy_generation_matches_transformers_generate():
         theirs = hf.generate(ids, attention_mask=am, max_new_tokens=10, do_sample=False,
                              eos_token_id=None, pad_token_id=0)
     assert torch.equal(ours, theirs), (ours, theirs)
+
+
+@pytest.mark.parametrize("name", ["tiny-llama", "tiny-phi", "tiny-mixtral"])
+@pytest.mark.parametrize("policy", ["full", "mlp", "attention"])
+def test_recompute_policies_match_no_recompute(name, policy):
+    """Selective activation recompute: re-running the MLP or the attention block in
+    backward gives the same loss and gradients as keeping every activation."""
+    cfg = get_config(name)
+    ids = torch.randint(3, cfg.vocab_size, (2, 16), generator=torch.Generator().manual_seed(1))
+    am = torch.ones_like(ids)
+    am[1, :3] = 0
+    grads = []
+    for pol in (None, policy):
+        m = build_model(cfg, device="cpu", seed=4).train()
+        if pol is not None:
+            m.gradient_checkpointing_enable(pol)
+        lp = m.sequence_logprob(ids, am)
+        lp.sum().backward()
+        grads.append([p.grad.clone() for p in m.parameters() if p.requires_grad])
+    for a, b in zip(*grads):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+
+
+def test_recompute_policy_rejects_unknown():
+    m = build_model(get_config("tiny-llama"), device="cpu")
+    with pytest.raises(ValueError):
+        m.gradient_checkpointing_enable("everything")
