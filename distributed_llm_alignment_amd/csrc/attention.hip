@@ -759,6 +759,27 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnBwdParams p) {
   for (int j = 0; j < 2; ++j) {
     const int kj = kw + 32 * j + l32;
     if (kj >= p.Tk) continue;
+    if (p.hsplit == 1 && p.rope_cos != nullptr) {
+      // fused RoPE backward: column d < D/2 pairs with d + D/2, i.e. the same register of
+      // column tile dt + DT/2, both in this lane (un-rotation: lo = a c + b s, hi = b c - a s)
+      const int pos = p.rope_pos ? p.rope_pos[static_cast<int64_t>(b) * p.Tk + kj] : kj;
+      const float* cp = p.rope_cos + static_cast<int64_t>(pos) * (D / 2) + 4 * h;
+      const float* sp = p.rope_sin + static_cast<int64_t>(pos) * (D / 2) + 4 * h;
+#pragma unroll
+      for (int dt = 0; dt < DT / 2; ++dt) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 c4 = *reinterpret_cast<const f32x4*>(cp + 32 * dt + 8 * g);
+          const f32x4 s4 = *reinterpret_cast<const f32x4*>(sp + 32 * dt + 8 * g);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float a = dk[j][dt][4 * g + e], bb = dk[j][dt + DT / 2][4 * g + e];
+            dk[j][dt][4 * g + e] = a * c4[e] + bb * s4[e];
+            dk[j][dt + DT / 2][4 * g + e] = bb * c4[e] - a * s4[e];
+          }
+        }
+      }
+    }
     if (p.hsplit == 1) {
       bf16_t* dkp = p.dk + b * p.dk_sb + kj * p.dk_st + static_cast<int64_t>(hk) * p.dk_sh;
       bf16_t* dvp = p.dv + b * p.dv_sb + kj * p.dv_st + static_cast<int64_t>(hk) * p.dv_sh;
@@ -801,14 +822,56 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnBwdParams p) {
   }
 }
 
+// Sum of the 8-column chunk at `src` over key blocks [lo, hi) of the slab (fixed kb order, 4
+// blocks' loads in flight at a time: bitwise the same as one at a time).
+__device__ __forceinline__ void slab_sum8(const float* src, int64_t slab_stride, int lo, int hi,
+                                          f32x4& a0, f32x4& a1) {
+  a0 = f32x4{0.f, 0.f, 0.f, 0.f};
+  a1 = a0;
+  int kb = lo;
+  for (; kb + 4 <= hi; kb += 4) {
+    f32x4 x[4][2];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const f32x4* sv = reinterpret_cast<const f32x4*>(src + (kb + u) * slab_stride);
+      x[u][0] = __builtin_nontemporal_load(sv);
+      x[u][1] = __builtin_nontemporal_load(sv + 1);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      a0 += x[u][0];
+      a1 += x[u][1];
+    }
+  }
+  for (; kb < hi; ++kb) {
+    const f32x4* sv = reinterpret_cast<const f32x4*>(src + kb * slab_stride);
+    a0 += __builtin_nontemporal_load(sv);
+    a1 += __builtin_nontemporal_load(sv + 1);
+  }
+}
+
+// un-rotate one pair of 8-column chunks (d and d + D/2) with the position's cos/sin
+__device__ __forceinline__ void rope_unrotate8(const float* cp, const float* sp, float (&lo)[8],
+                                               float (&hi)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float c = cp[j], s = sp[j], a = lo[j], b = hi[j];
+    lo[j] = a * c + b * s;
+    hi[j] = b * c - a * s;
+  }
+}
+
 // dQ[b, t, h, :] = sum over the key blocks whose workgroups swept row t (fixed kb order)
-// -> bf16 into a strided destination. One thread per 8 columns.
+// -> bf16 into a strided destination. One thread per 8 columns, or with the fused RoPE backward
+// (rcos != null) per pair of 8-column chunks d, d + D/2.
 template <bool CAUSAL>
 __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(
     const float* __restrict__ slab, int nkb, int B, int Tq, int slab_rows, int Hq, int D,
     int causal_off, int window, const int* __restrict__ kv_start, const int* __restrict__ kv_end,
-    int Tk, bf16_t* __restrict__ dst, int64_t d_sb, int64_t d_st, int64_t d_sh) {
-  const int cv = D / 8;
+    int Tk, bf16_t* __restrict__ dst, int64_t d_sb, int64_t d_st, int64_t d_sh,
+    const float* __restrict__ rcos, const float* __restrict__ rsin, const int* __restrict__ rpos) {
+  const int hv = D / 16;
+  const int cv = rcos ? hv : D / 8;  // work items per row
   const int64_t total = static_cast<int64_t>(B) * Tq * Hq * cv;
   const int64_t rs = static_cast<int64_t>(Hq) * D;
   const int64_t slab_stride = static_cast<int64_t>(B) * slab_rows * rs;
@@ -835,38 +898,42 @@ __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(
       lo = min(lo, kb);
       hi = kb + 1;
     }
-    f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
-    int kb = lo;
-    for (; kb + 4 <= hi; kb += 4) {
-      f32x4 x[4][2];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const f32x4* sv = reinterpret_cast<const f32x4*>(src + (kb + u) * slab_stride);
-        x[u][0] = __builtin_nontemporal_load(sv);
-        x[u][1] = __builtin_nontemporal_load(sv + 1);
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        a0 += x[u][0];
-        a1 += x[u][1];
-      }
+    f32x4 a0, a1;
+    slab_sum8(src, slab_stride, lo, hi, a0, a1);
+    float v[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+    bf16_t* out = dst + b * d_sb + t * d_st + hq * d_sh + c * 8;
+    if (rcos) {
+      f32x4 b0, b1;
+      slab_sum8(src + hv * 8, slab_stride, lo, hi, b0, b1);
+      float w[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+      const int pos = rpos ? rpos[static_cast<int64_t>(b) * Tq + t] : t;
+      rope_unrotate8(rcos + static_cast<int64_t>(pos) * (D / 2) + c * 8,
+                     rsin + static_cast<int64_t>(pos) * (D / 2) + c * 8, v, w);
+      store_bf16x8(out + hv * 8, pack_bf16x8(w));
     }
-    for (; kb < hi; ++kb) {
-      const f32x4* sv = reinterpret_cast<const f32x4*>(src + kb * slab_stride);
-      a0 += __builtin_nontemporal_load(sv);
-      a1 += __builtin_nontemporal_load(sv + 1);
-    }
-    const float v[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
-    store_bf16x8(dst + b * d_sb + t * d_st + hq * d_sh + c * 8, pack_bf16x8(v));
+    store_bf16x8(out, pack_bf16x8(v));
   }
 }
 
-// dK = scale * sum_s dk_part[s], dV = sum_s dv_part[s] -> bf16 strided (head-split workgroups)
+// dK = scale * sum_s dk_part[s], dV = sum_s dv_part[s] -> bf16 strided (head-split workgroups).
+// With the fused RoPE backward (rcos != null) a work item is the chunk pair d, d + D/2.
+__device__ __forceinline__ void part_sum8(const float* p, int64_t pstride, int hs, f32x4& a0, f32x4& a1) {
+  a0 = f32x4{0.f, 0.f, 0.f, 0.f};
+  a1 = a0;
+  for (int s = 0; s < hs; ++s) {
+    const f32x4* v = reinterpret_cast<const f32x4*>(p + s * pstride);
+    a0 += v[0];
+    a1 += v[1];
+  }
+}
+
 __global__ __launch_bounds__(256) void attn_dkv_reduce_kernel(
     const float* __restrict__ dkp, const float* __restrict__ dvp, int hs, int B, int Tk, int Hkv,
     int D, float scale, bf16_t* __restrict__ dk, int64_t dk_sb, int64_t dk_st, int64_t dk_sh,
-    bf16_t* __restrict__ dv, int64_t dv_sb, int64_t dv_st, int64_t dv_sh) {
-  const int cv = D / 8;
+    bf16_t* __restrict__ dv, int64_t dv_sb, int64_t dv_st, int64_t dv_sh,
+    const float* __restrict__ rcos, const float* __restrict__ rsin, const int* __restrict__ rpos) {
+  const int hv = D / 16;
+  const int cv = rcos ? hv : D / 8;
   const int64_t total = static_cast<int64_t>(B) * Tk * Hkv * cv;
   const int64_t pstride = static_cast<int64_t>(B) * Tk * Hkv * D;
   for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += static_cast<int64_t>(gridDim.x) * 256) {
@@ -877,20 +944,28 @@ __global__ __launch_bounds__(256) void attn_dkv_reduce_kernel(
     const int t = static_cast<int>(r % Tk);
     const int b = static_cast<int>(r / Tk);
     const int64_t off = ((static_cast<int64_t>(b) * Tk + t) * Hkv + hk) * D + c * 8;
-    f32x4 k0 = {0.f, 0.f, 0.f, 0.f}, k1 = k0, v0 = k0, v1 = k0;
-    for (int s = 0; s < hs; ++s) {
-      const f32x4* ks = reinterpret_cast<const f32x4*>(dkp + s * pstride + off);
-      const f32x4* vs = reinterpret_cast<const f32x4*>(dvp + s * pstride + off);
-      k0 += ks[0];
-      k1 += ks[1];
-      v0 += vs[0];
-      v1 += vs[1];
-    }
-    const float kf[8] = {k0[0] * scale, k0[1] * scale, k0[2] * scale, k0[3] * scale,
-                         k1[0] * scale, k1[1] * scale, k1[2] * scale, k1[3] * scale};
+    f32x4 k0, k1, v0, v1;
+    part_sum8(dkp + off, pstride, hs, k0, k1);
+    part_sum8(dvp + off, pstride, hs, v0, v1);
+    float kf[8] = {k0[0] * scale, k0[1] * scale, k0[2] * scale, k0[3] * scale,
+                   k1[0] * scale, k1[1] * scale, k1[2] * scale, k1[3] * scale};
     const float vf[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-    store_bf16x8(dk + b * dk_sb + t * dk_st + hk * dk_sh + c * 8, pack_bf16x8(kf));
-    store_bf16x8(dv + b * dv_sb + t * dv_st + hk * dv_sh + c * 8, pack_bf16x8(vf));
+    bf16_t* kout = dk + b * dk_sb + t * dk_st + hk * dk_sh + c * 8;
+    bf16_t* vout = dv + b * dv_sb + t * dv_st + hk * dv_sh + c * 8;
+    if (rcos) {  // partner chunk c + D/16: dV copied through, dK un-rotated with its pair
+      part_sum8(dkp + off + hv * 8, pstride, hs, k0, k1);
+      part_sum8(dvp + off + hv * 8, pstride, hs, v0, v1);
+      float kw[8] = {k0[0] * scale, k0[1] * scale, k0[2] * scale, k0[3] * scale,
+                     k1[0] * scale, k1[1] * scale, k1[2] * scale, k1[3] * scale};
+      const float vw[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+      const int pos = rpos ? rpos[static_cast<int64_t>(b) * Tk + t] : t;
+      rope_unrotate8(rcos + static_cast<int64_t>(pos) * (D / 2) + c * 8,
+                     rsin + static_cast<int64_t>(pos) * (D / 2) + c * 8, kf, kw);
+      store_bf16x8(kout + hv * 8, pack_bf16x8(kw));
+      store_bf16x8(vout + hv * 8, pack_bf16x8(vw));
+    }
+    store_bf16x8(kout, pack_bf16x8(kf));
+    store_bf16x8(vout, pack_bf16x8(vf));
   }
 }
 
@@ -970,26 +1045,30 @@ void launch_attn_bwd(const AttnBwdParams& p, int D, bool causal, hipStream_t st)
 void launch_attn_dq_reduce(const float* slab, int nkb, int B, int Tq, int slab_rows, int Hq, int D,
                            bool causal, int causal_off, int window, const int* kv_start,
                            const int* kv_end, int Tk, bf16_t* dst, int64_t d_sb, int64_t d_st,
-                           int64_t d_sh, hipStream_t st) {
-  const int64_t work = static_cast<int64_t>(B) * Tq * Hq * (D / 8);
+                           int64_t d_sh, const float* rcos, const float* rsin, const int* rpos,
+                           hipStream_t st) {
+  const int64_t work = static_cast<int64_t>(B) * Tq * Hq * (rcos ? D / 16 : D / 8);
   if (work == 0) return;
   if (causal)
     attn_dq_reduce_kernel<true><<<stream_grid(work), 256, 0, st>>>(
-        slab, nkb, B, Tq, slab_rows, Hq, D, causal_off, window, kv_start, kv_end, Tk, dst, d_sb, d_st, d_sh);
+        slab, nkb, B, Tq, slab_rows, Hq, D, causal_off, window, kv_start, kv_end, Tk, dst, d_sb, d_st, d_sh,
+        rcos, rsin, rpos);
   else
     attn_dq_reduce_kernel<false><<<stream_grid(work), 256, 0, st>>>(
-        slab, nkb, B, Tq, slab_rows, Hq, D, causal_off, window, kv_start, kv_end, Tk, dst, d_sb, d_st, d_sh);
+        slab, nkb, B, Tq, slab_rows, Hq, D, causal_off, window, kv_start, kv_end, Tk, dst, d_sb, d_st, d_sh,
+        rcos, rsin, rpos);
 }
 
 void launch_attn_dkv_reduce(const float* dkp, const float* dvp, int hs, int B, int Tk, int Hkv,
                             int D, float scale, bf16_t* dk, int64_t dk_sb, int64_t dk_st,
                             int64_t dk_sh, bf16_t* dv, int64_t dv_sb, int64_t dv_st,
-                            int64_t dv_sh, hipStream_t st) {
-  const int64_t work = static_cast<int64_t>(B) * Tk * Hkv * (D / 8);
+                            int64_t dv_sh, const float* rcos, const float* rsin, const int* rpos,
+                            hipStream_t st) {
+  const int64_t work = static_cast<int64_t>(B) * Tk * Hkv * (rcos ? D / 16 : D / 8);
   if (work == 0) return;
   attn_dkv_reduce_kernel<<<stream_grid(work), 256, 0, st>>>(dkp, dvp, hs, B, Tk, Hkv, D, scale, dk,
                                                             dk_sb, dk_st, dk_sh, dv, dv_sb, dv_st,
-                                                            dv_sh);
+                                                            dv_sh, rcos, rsin, rpos);
 }
 
 }  // namespace dla

@@ -59,6 +59,12 @@ struct AttnBwdParams {
   const int* kv_start;
   const int* kv_end;
   const int* seg_end;  // [B, Tk] or null: packed sequences, key j is seen by queries < seg_end[j]
+  // fused RoPE backward (full rotary, rot = D, self-attention Tq = Tk): dQ / dK leave the
+  // kernels un-rotated (the transpose of the rotation applied in the forward), written straight
+  // into the q / k column slices of the fused dqkv buffer; null = no rotation
+  const float* rope_cos;  // [max_pos, D/2] fp32
+  const float* rope_sin;
+  const int* rope_pos;    // [B * T] token positions, or null: position = t
 };
 
 }  // namespace dla

@@ -73,10 +73,10 @@ void launch_attn_bwd_delta(const bf16_t*, const bf16_t*, int64_t, int64_t, int64
 void launch_attn_bwd(const AttnBwdParams&, int, bool, hipStream_t);
 void launch_attn_dq_reduce(const float*, int, int, int, int, int, int, bool, int, int,
                            const int*, const int*, int, bf16_t*, int64_t, int64_t, int64_t,
-                           hipStream_t);
+                           const float*, const float*, const int*, hipStream_t);
 void launch_attn_dkv_reduce(const float*, const float*, int, int, int, int, int, float, bf16_t*,
                             int64_t, int64_t, int64_t, bf16_t*, int64_t, int64_t, int64_t,
-                            hipStream_t);
+                            const float*, const float*, const int*, hipStream_t);
 void launch_transpose_bf16(const bf16_t*, int64_t, int64_t, int64_t, bf16_t*, int64_t, hipStream_t);
 
 // ================================= norms ======================================================
@@ -406,7 +406,9 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k,
               const at::Tensor& v, const at::Tensor& o, const at::Tensor& lse2, at::Tensor& dq,
               at::Tensor& dk, at::Tensor& dv, double scale, bool causal, int64_t causal_off,
               int64_t window, const c10::optional<at::Tensor>& kv_start,
-              const c10::optional<at::Tensor>& kv_end, const c10::optional<at::Tensor>& segs) {
+              const c10::optional<at::Tensor>& kv_end, const c10::optional<at::Tensor>& segs,
+              const c10::optional<at::Tensor>& rope_cos, const c10::optional<at::Tensor>& rope_sin,
+              const c10::optional<at::Tensor>& rope_pos) {
   check_bthd(dout, "dout");
   check_bthd(q, "q");
   check_bthd(k, "k");
@@ -467,16 +469,37 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k,
   p.kv_start = (kv_start && kv_start->defined()) ? kv_start->data_ptr<int>() : nullptr;
   p.kv_end = (kv_end && kv_end->defined()) ? kv_end->data_ptr<int>() : nullptr;
   p.seg_end = seg_ptr(segs, B, Tq, Tk, causal, causal_off, q, 1);
+  // fused RoPE backward: dq / dk receive the un-rotated gradients (full rotary only)
+  const bool rope = rope_cos && rope_cos->defined();
+  if (rope) {
+    TORCH_CHECK(rope_sin && rope_sin->defined(), "rope_sin missing");
+    for (const at::Tensor* t : {&*rope_cos, &*rope_sin}) {
+      TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous() && t->dim() == 2 &&
+                      t->size(1) == D / 2, "rope cos/sin must be contiguous fp32 [max_pos, head_dim/2]");
+      same_device(q, *t);
+    }
+    TORCH_CHECK(Tq == Tk && causal_off == 0, "fused RoPE backward needs self-attention");
+    if (rope_pos && rope_pos->defined()) {
+      TORCH_CHECK(rope_pos->scalar_type() == at::kInt && rope_pos->is_contiguous() &&
+                      rope_pos->numel() == B * Tq, "rope_pos must be contiguous int32 [B*T]");
+      same_device(q, *rope_pos);
+    } else {
+      TORCH_CHECK(Tq <= rope_cos->size(0), "positions exceed the rotary table");
+    }
+    p.rope_cos = rope_cos->data_ptr<float>();
+    p.rope_sin = rope_sin->data_ptr<float>();
+    p.rope_pos = (rope_pos && rope_pos->defined()) ? rope_pos->data_ptr<int>() : nullptr;
+  }
   launch_attn_bwd(p, static_cast<int>(D), causal, st);
   launch_attn_dq_reduce(p.dq_slab, static_cast<int>(nkb), static_cast<int>(B), static_cast<int>(Tq),
                         p.slab_rows, static_cast<int>(Hq), static_cast<int>(D), causal, p.causal_off, p.window,
                         p.kv_start, p.kv_end, static_cast<int>(Tk), bp(dq), dq.stride(0),
-                        dq.stride(1), dq.stride(2), st);
+                        dq.stride(1), dq.stride(2), p.rope_cos, p.rope_sin, p.rope_pos, st);
   if (hs > 1) {
     launch_attn_dkv_reduce(p.dk_part, p.dv_part, hs, static_cast<int>(B), static_cast<int>(Tk),
                            static_cast<int>(Hkv), static_cast<int>(D), p.scale, bp(dk),
                            dk.stride(0), dk.stride(1), dk.stride(2), bp(dv), dv.stride(0),
-                           dv.stride(1), dv.stride(2), st);
+                           dv.stride(1), dv.stride(2), p.rope_cos, p.rope_sin, p.rope_pos, st);
   }
 }
 
@@ -803,7 +826,7 @@ TORCH_LIBRARY(dla, m) {
   m.def("rope_fwd(Tensor qkv, Tensor cos, Tensor sin, Tensor? pos, int Hq, int Hkv, int D, int rot, int T, int pos_offset) -> (Tensor, Tensor)");
   m.def("rope_bwd(Tensor dq, Tensor dk, Tensor(a!) dqkv, Tensor cos, Tensor sin, Tensor? pos, int Hq, int Hkv, int D, int rot, int T, int pos_offset) -> ()");
   m.def("attn_fwd(Tensor q, Tensor k, Tensor v, float scale, bool causal, int causal_off, int window, Tensor? kv_start, Tensor? kv_end, Tensor? segs=None) -> (Tensor, Tensor)");
-  m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse2, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, float scale, bool causal, int causal_off, int window, Tensor? kv_start, Tensor? kv_end, Tensor? segs=None) -> ()");
+  m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse2, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, float scale, bool causal, int causal_off, int window, Tensor? kv_start, Tensor? kv_end, Tensor? segs=None, Tensor? rope_cos=None, Tensor? rope_sin=None, Tensor? rope_pos=None) -> ()");
   m.def("transpose_bf16(Tensor input, Tensor(a!) out) -> ()");
   m.def("logprob_fwd(Tensor logits, Tensor targets, int vocab_offset=0) -> (Tensor, Tensor)");
   m.def("logprob_bwd(Tensor(a!) logits, Tensor targets, Tensor lse, Tensor grad, int vocab_offset=0) -> ()");

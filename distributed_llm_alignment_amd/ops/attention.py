@@ -18,6 +18,7 @@ Fully-masked query rows produce zeros.
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, Optional
 
 import torch
@@ -122,6 +123,12 @@ def _i32(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
     return None if t is None else t.to(dtype=torch.int32).contiguous()
 
 
+# Full-rotary RoPE backward folded into the attention backward's dQ reduce / dK-dV passes (no
+# separate rope_bwd launch, no rotated-space dq/dk temporaries); DLA_FUSED_ROPE_BWD=0 restores
+# the separate kernel for A/B runs.
+FUSED_ROPE_BWD = os.environ.get("DLA_FUSED_ROPE_BWD", "1") != "0"
+
+
 class _FusedQKVAttnFn(torch.autograd.Function):
     """qkv [B, T, C] -> o [B, T, Hq*D]; RoPE (optional) fused in; returns one dqkv."""
 
@@ -159,15 +166,20 @@ class _FusedQKVAttnFn(torch.autograd.Function):
         do4 = do.contiguous().view(B, T, Hq, D)
         dqkv = torch.empty((B, T, C), dtype=qkv.dtype, device=qkv.device)
         dv = dqkv.as_strided((B, T, Hkv, D), (T * C, C, D, 1), (Hq + Hkv) * D)
-        if rot > 0:  # rotated-space dq / dk, un-rotated into dqkv by the RoPE backward
+        fused_rope = rot == D and FUSED_ROPE_BWD
+        if rot > 0 and not fused_rope:  # rotated-space dq / dk, un-rotated by the RoPE backward
             dq = torch.empty((B, T, Hq, D), dtype=qkv.dtype, device=qkv.device)
             dk = torch.empty((B, T, Hkv, D), dtype=qkv.dtype, device=qkv.device)
-        else:  # written straight into the fused dqkv buffer
+        else:  # written straight into the fused dqkv buffer (un-rotated in the attention passes)
             dq = dqkv.as_strided((B, T, Hq, D), (T * C, C, D, 1), 0)
             dk = dqkv.as_strided((B, T, Hkv, D), (T * C, C, D, 1), Hq * D)
-        ops.attn_bwd(do4, q4, k4, v4, o, lse2, dq, dk, dv, float(scale), bool(causal), 0,
-                     int(window), kv_start, kv_end, segs)
-        if rot > 0:
+        if fused_rope:
+            ops.attn_bwd(do4, q4, k4, v4, o, lse2, dq, dk, dv, float(scale), bool(causal), 0,
+                         int(window), kv_start, kv_end, segs, cos, sin, pos)
+        else:
+            ops.attn_bwd(do4, q4, k4, v4, o, lse2, dq, dk, dv, float(scale), bool(causal), 0,
+                         int(window), kv_start, kv_end, segs)
+        if rot > 0 and not fused_rope:
             ops.rope_bwd(dq.view(B * T, Hq * D), dk.view(B * T, Hkv * D), dqkv.view(B * T, C),
                          cos, sin, pos, Hq, Hkv, D, rot, T, 0)
         return dqkv, None, None, None, None, None, None, None, None, None, None, None, None, None

@@ -309,6 +309,44 @@ def test_attention_long_seq_grad_llama_shape():
     assert rel_err(qkv.grad, qr.grad) < 3e-2
 
 
+@pytest.mark.parametrize("leftpad", [False, True])
+def test_attention_fused_rope_bwd_unsplit_grid(leftpad):
+    """Full-rotary RoPE backward folded into the attention backward at a shape whose grid needs
+    no GQA head split (B*Hkv*key blocks >= the CU count, non-causal): dK is un-rotated in the main
+    kernel's epilogue (partner column tile in the same lane), dQ in the slab reduce; explicit
+    positions (left padding) exercise rope_pos."""
+    B, T, Hq, Hkv, D = 4, 2048, 32, 8, 128
+    C = (Hq + 2 * Hkv) * D
+    qkv = bf(torch.randn(B, T, C)).requires_grad_()
+    rope = RotaryCache(D, 500000.0, 8192)
+    kv_start = kv_end = positions = None
+    if leftpad:
+        kv_start = torch.tensor([0, 300, 0, 1000], device=DEV, dtype=torch.int32)
+        kv_end = torch.full((B,), T, device=DEV, dtype=torch.int32)
+        positions = (torch.arange(T, device=DEV).unsqueeze(0) - kv_start.unsqueeze(1)).clamp(min=0).int()
+    o = ops.qkv_attention(qkv, Hq, Hkv, D, rope, False, 0, kv_start, kv_end, positions)
+    go = bf(torch.randn_like(o.float()))
+    (o.float() * go.float()).sum().backward()
+    qr = qkv.detach().float().requires_grad_()
+    orf = _qkv_ref_nc(qr, Hq, Hkv, D, rope, kv_start, kv_end, positions)
+    (orf * go.float()).sum().backward()
+    assert rel_err(o, orf) < 2e-2
+    assert rel_err(qkv.grad, qr.grad) < 3e-2
+
+
+def _qkv_ref_nc(qkv, Hq, Hkv, D, rope, kv_start, kv_end, positions):
+    B, T, _ = qkv.shape
+    q = qkv[..., : Hq * D].reshape(B, T, Hq, D)
+    k = qkv[..., Hq * D:(Hq + Hkv) * D].reshape(B, T, Hkv, D)
+    v = qkv[..., (Hq + Hkv) * D:].reshape(B, T, Hkv, D)
+    cos, sin = rope.tables(qkv.device)
+    pos = positions.long() if positions is not None else torch.arange(T, device=qkv.device).expand(B, T)
+    q = _ref_rope(q, cos, sin, pos, rope.rot_dim)
+    k = _ref_rope(k, cos, sin, pos, rope.rot_dim)
+    out = ref_attention(q, k, v, 1.0 / math.sqrt(D), causal=False, kv_start=kv_start, kv_end=kv_end)
+    return out.float().reshape(B, T, Hq * D)
+
+
 # ------------------------------------------------------------------------------- logprob
 @pytest.mark.parametrize("V", [32000, 50257])
 def test_linear_logprob(V):
