@@ -108,3 +108,32 @@ def test_fp8_rowwise_quant_kernel_and_moe_layer():
     moe.fp8 = True
     out = moe(h).float()
     assert (out - ref).norm() / ref.norm() < 0.08
+
+
+@pytest.mark.parametrize("policy", ["full", "mlp"])
+def test_moe_recompute_keeps_expert_grads(policy):
+    """Expert weights accumulate into the engine's main_grad from the grouped-GEMM autograd node;
+    under activation recompute (whole layer or MLP block) that node must still see the real
+    parameters (weights ride on ctx): one DPO step's gradients equal the no-recompute step's."""
+    from distributed_llm_alignment_amd.data.synthetic import synthetic_preference_batch
+    from distributed_llm_alignment_amd.models import build_model, get_config
+    from distributed_llm_alignment_amd.objectives import dpo_step_loss
+    from distributed_llm_alignment_amd.parallel.data_parallel import DataParallelEngine
+
+    cfg = get_config("tiny-mixtral", hidden_size=256, head_dim=64, intermediate_size=512, num_experts=8)
+    grads = []
+    for pol in (None, policy):
+        m = build_model(cfg, device=DEV, dtype=torch.bfloat16, seed=3)
+        ref = build_model(cfg, device=DEV, dtype=torch.bfloat16, seed=3).requires_grad_(False)
+        if pol is not None:
+            m.gradient_checkpointing_enable(pol)
+        eng = DataParallelEngine(m, lr=1e-3, weight_decay=0.0, max_grad_norm=1.0)
+        b = synthetic_preference_batch(2, 128, cfg.vocab_size, device=DEV, generator=torch.Generator().manual_seed(1))
+        loss, _ = dpo_step_loss(m, ref, b)
+        loss.backward()
+        eng.finish_grad_sync()
+        grads.append({n: (p.main_grad if getattr(p, "main_grad", None) is not None else p.grad).float().clone()
+                      for n, p in m.named_parameters()})
+    for n, a in grads[0].items():
+        assert a.abs().max() > 0, n
+        torch.testing.assert_close(grads[1][n], a, rtol=2e-2, atol=2e-4, msg=n)
