@@ -71,6 +71,38 @@ __device__ __forceinline__ s16x8 pack8(const f32x16& x, int base) {
 
 __device__ __forceinline__ float ex2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// RoPE on load (full rotary, rotate-half): rotates the 16-byte chunk `ch` (of NCH per row) of
+// token `t` of a sequence (position pos_t[pidx], or t without a position table). Column d < D/2 pairs with d + D/2, i.e. chunk ch ^ NCH/2,
+// which the staging layouts below always hold in lane ^ NCH/2 of the same wave: one xor-shuffle
+// per dword fetches it. Every lane must call this (the shuffle); `valid` = the row exists.
+template <int NCH>
+__device__ __forceinline__ bf16x8 rope_rot_chunk(bf16x8 v, int ch, bool valid, int64_t pidx, int t,
+                                                 const float* __restrict__ cos_t,
+                                                 const float* __restrict__ sin_t,
+                                                 const int* __restrict__ pos_t) {
+  const u32x4 w = __builtin_bit_cast(u32x4, v);
+  u32x4 o;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) o[i] = __shfl_xor(w[i], NCH / 2, 64);
+  if (!valid) return v;
+  const bf16x8 partner = __builtin_bit_cast(bf16x8, o);
+  const bool lo = ch < NCH / 2;
+  const int d0 = (lo ? ch : ch - NCH / 2) * 8;
+  const int pos = pos_t ? pos_t[pidx] : t;
+  const float* cp = cos_t + static_cast<int64_t>(pos) * (NCH * 4) + d0;
+  const float* sp = sin_t + static_cast<int64_t>(pos) * (NCH * 4) + d0;
+  const f32x4 c0 = *reinterpret_cast<const f32x4*>(cp), c1 = *reinterpret_cast<const f32x4*>(cp + 4);
+  const f32x4 s0 = *reinterpret_cast<const f32x4*>(sp), s1 = *reinterpret_cast<const f32x4*>(sp + 4);
+  float r[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float c = j < 4 ? c0[j] : c1[j - 4], s = j < 4 ? s0[j] : s1[j - 4];
+    const float a = bf2f(v[j]), q = bf2f(partner[j]);
+    r[j] = lo ? a * c - q * s : a * c + q * s;
+  }
+  return pack_bf16x8(r);
+}
+
 // Deferred-max threshold (cdna guide T13, log2 units): the running max is only raised when a
 // tile's max exceeds it by more than this, so most tiles skip the O rescale. P <= 2^8.
 constexpr float kRescaleThr = 8.0f;
@@ -182,12 +214,17 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
       }
     }
   };
-  auto lwrite = [&](int buf) {
+  const bool rope = p.rope_cos != nullptr;  // kernel-uniform
+  auto lwrite = [&](int buf, int kt) {
 #pragma unroll
     for (int c = 0; c < CPT; ++c) {
       const int ci = tid + NT * c;
       const int row = ci / NCH, ch = ci % NCH;
-      store_bf16x8(&Kb[buf][swz<D>(row, ch)], kreg[c]);
+      bf16x8 kv = kreg[c];
+      if (rope)
+        kv = rope_rot_chunk<NCH>(kv, ch, kt + row < p.Tk, static_cast<int64_t>(b) * p.Tk + kt + row,
+                                 kt + row, p.rope_cos, p.rope_sin, p.rope_pos);
+      store_bf16x8(&Kb[buf][swz<D>(row, ch)], kv);
       store_bf16x8(&Vb[buf][swz<D>(row, ch)], vreg[c]);
     }
   };
@@ -196,21 +233,47 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
   // out of the MFMA already in the exp2 domain (no per-score multiply). (Issuing the K/V tile-0
   // loads ahead of the Q loads measured -2.5 % .. +3 % by shape: kept in this order.)
   s16x8 qf[KS];
+  {
+    float qv[KS][8];
 #pragma unroll
-  for (int s = 0; s < KS; ++s) {
-    if (qi < p.Tq) {
-      const bf16x8 raw = load_bf16x8(qp + qi * p.q_st + 16 * s + 8 * h);
+    for (int s = 0; s < KS; ++s) {
+      const bf16x8 raw = qi < p.Tq ? load_bf16x8(qp + qi * p.q_st + 16 * s + 8 * h) : bf16x8{};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qv[s][j] = bf2f(raw[j]);
+    }
+    if (rope && qi < p.Tq) {
+      // RoPE on load: fragment s (columns 16s + 8h + j) pairs with fragment s + KS/2 (+ D/2)
+      const int pos = p.rope_pos ? p.rope_pos[static_cast<int64_t>(b) * p.Tq + qi] : qi;
+      const float* cp = p.rope_cos + static_cast<int64_t>(pos) * (D / 2) + 8 * h;
+      const float* sp = p.rope_sin + static_cast<int64_t>(pos) * (D / 2) + 8 * h;
+#pragma unroll
+      for (int s = 0; s < KS / 2; ++s) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float c = cp[16 * s + j], sn = sp[16 * s + j];
+          const float a = qv[s][j], bb = qv[s + KS / 2][j];
+          qv[s][j] = a * c - bb * sn;
+          qv[s + KS / 2][j] = bb * c + a * sn;
+        }
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
       float t[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) t[j] = bf2f(raw[j]) * p.scale2;
+      for (int j = 0; j < 8; ++j) t[j] = qv[s][j] * p.scale2;
       qf[s] = __builtin_bit_cast(s16x8, pack_bf16x8(t));
-    } else {
-      qf[s] = s16x8{};
+    }
+    // the rotated (unscaled) Q rows for the backward; the HP heads' waves write disjoint rows
+    if (rope && p.q_rot != nullptr && qi < p.Tq) {
+      bf16_t* qo = p.q_rot + b * p.qr_sb + qi * p.qr_st + static_cast<int64_t>(hq) * p.qr_sh + 8 * h;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) store_bf16x8(qo + 16 * s, pack_bf16x8(qv[s]));
     }
   }
   if (ntiles > 0) {
     gload(tile0);
-    lwrite(0);
+    lwrite(0, tile0);
     if (ntiles > 1) gload(tile0 + BK);
   }
   __syncthreads();
@@ -306,7 +369,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
       }
     }
     if (t + 1 < ntiles) {  // stage tile t+1 into the other buffer, prefetch tile t+2
-      lwrite((t + 1) & 1);
+      lwrite((t + 1) & 1, kt + BK);
       if (t + 2 < ntiles) gload(kt + 2 * BK);
     }
     __syncthreads();
@@ -442,7 +505,9 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnBwdParams p) {
   const int kbeg = p.kv_start ? p.kv_start[b] : 0;
   const int kend = p.kv_end ? p.kv_end[b] : p.Tk;
 
-  {  // K and V blocks -> LDS (rows past Tk zeroed)
+  // kernel-uniform: k arrives un-rotated (q comes pre-rotated: the forward's q_rot output)
+  const bool rope_in = p.rope_inputs != 0;
+  {  // K and V blocks -> LDS (rows past Tk zeroed; K rotated on the way with RoPE on load)
     const bf16_t* kp = p.k + b * p.k_sb + static_cast<int64_t>(hk) * p.k_sh;
     const bf16_t* vp = p.v + b * p.v_sb + static_cast<int64_t>(hk) * p.v_sh;
 #pragma unroll 4
@@ -451,7 +516,11 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnBwdParams p) {
       const int row = ci / NCH, ch = ci % NCH;
       const int key = k0 + row;
       const bool in = key < p.Tk;
-      store_bf16x8(Ks + swz<D>(row, ch), in ? load_bf16x8(kp + key * p.k_st + ch * 8) : bf16x8{});
+      bf16x8 kv = in ? load_bf16x8(kp + key * p.k_st + ch * 8) : bf16x8{};
+      if (rope_in)
+        kv = rope_rot_chunk<NCH>(kv, ch, in, static_cast<int64_t>(b) * p.Tk + key, key, p.rope_cos,
+                                 p.rope_sin, p.rope_pos);
+      store_bf16x8(Ks + swz<D>(row, ch), kv);
       store_bf16x8(Vs + swz<D>(row, ch), in ? load_bf16x8(vp + key * p.v_st + ch * 8) : bf16x8{});
     }
   }
@@ -759,33 +828,12 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnBwdParams p) {
   for (int j = 0; j < 2; ++j) {
     const int kj = kw + 32 * j + l32;
     if (kj >= p.Tk) continue;
-    if (p.hsplit == 1 && p.rope_cos != nullptr) {
-      // fused RoPE backward: column d < D/2 pairs with d + D/2, i.e. the same register of
-      // column tile dt + DT/2, both in this lane (un-rotation: lo = a c + b s, hi = b c - a s)
-      const int pos = p.rope_pos ? p.rope_pos[static_cast<int64_t>(b) * p.Tk + kj] : kj;
-      const float* cp = p.rope_cos + static_cast<int64_t>(pos) * (D / 2) + 4 * h;
-      const float* sp = p.rope_sin + static_cast<int64_t>(pos) * (D / 2) + 4 * h;
-#pragma unroll
-      for (int dt = 0; dt < DT / 2; ++dt) {
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const f32x4 c4 = *reinterpret_cast<const f32x4*>(cp + 32 * dt + 8 * g);
-          const f32x4 s4 = *reinterpret_cast<const f32x4*>(sp + 32 * dt + 8 * g);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float a = dk[j][dt][4 * g + e], bb = dk[j][dt + DT / 2][4 * g + e];
-            dk[j][dt][4 * g + e] = a * c4[e] + bb * s4[e];
-            dk[j][dt + DT / 2][4 * g + e] = bb * c4[e] - a * s4[e];
-          }
-        }
-      }
-    }
     if (p.hsplit == 1) {
       bf16_t* dkp = p.dk + b * p.dk_sb + kj * p.dk_st + static_cast<int64_t>(hk) * p.dk_sh;
       bf16_t* dvp = p.dv + b * p.dv_sb + kj * p.dv_st + static_cast<int64_t>(hk) * p.dv_sh;
       // widened stores (T21, as the forward's O): permlane32_swap pairs 8-column groups so
       // each lane writes 16 contiguous bytes
-      auto store_row = [&](bf16_t* dst, const f32x16& x, float sc, int dt) {
+      auto store_row = [&](bf16_t* dst, f32x16 x, float sc, int dt) {
 #pragma unroll
         for (int g4 = 0; g4 < 4; g4 += 2) {
           const uint32_t a0 = pack2bf(x[4 * g4] * sc, x[4 * g4 + 1] * sc);
@@ -797,11 +845,36 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnBwdParams p) {
           *reinterpret_cast<uint4*>(dst + 32 * dt + 8 * g4 + 8 * h) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
         }
       };
+      if (p.rope_cos != nullptr) {
+        // fused RoPE backward: column d < D/2 pairs with d + D/2 = the same register of column
+        // tile dt + DT/2 in this lane (un-rotation: lo = a c + b s, hi = b c - a s), applied to
+        // register copies on the way out (writing the accumulators back spilled in the loop)
+        const int pos = p.rope_pos ? p.rope_pos[static_cast<int64_t>(b) * p.Tk + kj] : kj;
+        const float* cp = p.rope_cos + static_cast<int64_t>(pos) * (D / 2) + 4 * h;
+        const float* sp = p.rope_sin + static_cast<int64_t>(pos) * (D / 2) + 4 * h;
 #pragma unroll
-      for (int dt = 0; dt < DT; ++dt) {
-        store_row(dkp, dk[j][dt], p.scale, dt);
-        store_row(dvp, dv[j][dt], 1.f, dt);
+        for (int dt = 0; dt < DT / 2; ++dt) {
+          f32x16 lo = dk[j][dt], hi = dk[j][dt + DT / 2];
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const f32x4 c4 = *reinterpret_cast<const f32x4*>(cp + 32 * dt + 8 * g);
+            const f32x4 s4 = *reinterpret_cast<const f32x4*>(sp + 32 * dt + 8 * g);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float a = lo[4 * g + e], bb = hi[4 * g + e];
+              lo[4 * g + e] = a * c4[e] + bb * s4[e];
+              hi[4 * g + e] = bb * c4[e] - a * s4[e];
+            }
+          }
+          store_row(dkp, lo, p.scale, dt);
+          store_row(dkp, hi, p.scale, dt + DT / 2);
+        }
+      } else {
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) store_row(dkp, dk[j][dt], p.scale, dt);
       }
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) store_row(dvp, dv[j][dt], 1.f, dt);
     } else {  // fp32 partials of this head subset, summed by attn_dkv_reduce_kernel
       const int64_t off = ((static_cast<int64_t>(sidx) * p.B + b) * p.Tk + kj) * p.Hkv * D +
                           static_cast<int64_t>(hk) * D;

@@ -23,6 +23,13 @@ struct AttnParams {
   const int* kv_start;  // [B] or null
   const int* kv_end;    // [B] or null
   const int* seg_start;  // [B, Tq] or null: packed sequences, query i sees keys >= seg_start[i]
+  // RoPE on load (full rotary, self-attention): q / k are the un-rotated projections; the kernel
+  // rotates Q in registers and every K row as it is staged into LDS; null = inputs pre-rotated
+  const float* rope_cos;  // [max_pos, D/2] fp32
+  const float* rope_sin;
+  const int* rope_pos;    // [B * T] token positions, or null: position = t
+  bf16_t* q_rot;          // optional [B, T, Hq, D] out: the rotated Q (what the backward reads)
+  int64_t qr_sb, qr_st, qr_sh;
 };
 
 // Backward geometry: one workgroup per (256-key block, GQA head subset, kv head, batch);
@@ -65,6 +72,8 @@ struct AttnBwdParams {
   const float* rope_cos;  // [max_pos, D/2] fp32
   const float* rope_sin;
   const int* rope_pos;    // [B * T] token positions, or null: position = t
+  int rope_inputs;        // 1: k arrives un-rotated and is rotated as it is staged (q is the
+                          // forward's q_rot output)
 };
 
 }  // namespace dla

@@ -329,12 +329,44 @@ static const int* seg_ptr(const c10::optional<at::Tensor>& segs, int64_t B, int6
   return segs->data_ptr<int>() + row * B * Tq;
 }
 
+// rotary tables for the fused RoPE paths: contiguous fp32 [max_pos, D/2] cos / sin, optional
+// int32 [B*T] positions (else position = t); full rotary, self-attention only
+static void rope_args(const c10::optional<at::Tensor>& rope_cos, const c10::optional<at::Tensor>& rope_sin,
+                      const c10::optional<at::Tensor>& rope_pos, const at::Tensor& q, int64_t B,
+                      int64_t Tq, int64_t Tk, int64_t D, int64_t causal_off, const float** cos_p,
+                      const float** sin_p, const int** pos_p) {
+  *cos_p = *sin_p = nullptr;
+  *pos_p = nullptr;
+  if (!rope_cos || !rope_cos->defined()) return;
+  TORCH_CHECK(rope_sin && rope_sin->defined(), "rope_sin missing");
+  for (const at::Tensor* t : {&*rope_cos, &*rope_sin}) {
+    TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous() && t->dim() == 2 &&
+                    t->size(1) == D / 2, "rope cos/sin must be contiguous fp32 [max_pos, head_dim/2]");
+    same_device(q, *t);
+  }
+  TORCH_CHECK(Tq == Tk && causal_off == 0, "fused RoPE needs self-attention");
+  if (rope_pos && rope_pos->defined()) {
+    TORCH_CHECK(rope_pos->scalar_type() == at::kInt && rope_pos->is_contiguous() &&
+                    rope_pos->numel() == B * Tq, "rope_pos must be contiguous int32 [B*T]");
+    same_device(q, *rope_pos);
+    *pos_p = rope_pos->data_ptr<int>();
+  } else {
+    TORCH_CHECK(Tq <= rope_cos->size(0), "positions exceed the rotary table");
+  }
+  *cos_p = rope_cos->data_ptr<float>();
+  *sin_p = rope_sin->data_ptr<float>();
+}
+
 std::tuple<at::Tensor, at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k,
                                             const at::Tensor& v, double scale, bool causal,
                                             int64_t causal_off, int64_t window,
                                             const c10::optional<at::Tensor>& kv_start,
                                             const c10::optional<at::Tensor>& kv_end,
-                                            const c10::optional<at::Tensor>& segs) {
+                                            const c10::optional<at::Tensor>& segs,
+                                            const c10::optional<at::Tensor>& rope_cos,
+                                            const c10::optional<at::Tensor>& rope_sin,
+                                            const c10::optional<at::Tensor>& rope_pos,
+                                            const c10::optional<at::Tensor>& q_rot) {
   check_bthd(q, "q");
   check_bthd(k, "k");
   check_bthd(v, "v");
@@ -369,6 +401,16 @@ std::tuple<at::Tensor, at::Tensor> attn_fwd(const at::Tensor& q, const at::Tenso
   p.kv_start = (kv_start && kv_start->defined()) ? kv_start->data_ptr<int>() : nullptr;
   p.kv_end = (kv_end && kv_end->defined()) ? kv_end->data_ptr<int>() : nullptr;
   p.seg_start = seg_ptr(segs, B, Tq, Tk, causal, causal_off, q, 0);
+  rope_args(rope_cos, rope_sin, rope_pos, q, B, Tq, Tk, D, causal_off, &p.rope_cos, &p.rope_sin,
+            &p.rope_pos);
+  if (q_rot && q_rot->defined()) {
+    TORCH_CHECK(p.rope_cos != nullptr, "q_rot needs the rotary tables");
+    check_bthd(*q_rot, "q_rot");
+    TORCH_CHECK(q_rot->sizes() == q.sizes(), "q_rot shape");
+    same_device(q, *q_rot);
+    p.q_rot = bp(*q_rot);
+    p.qr_sb = q_rot->stride(0); p.qr_st = q_rot->stride(1); p.qr_sh = q_rot->stride(2);
+  }
   launch_attn_fwd(p, static_cast<int>(D), causal, cur_stream(q));
   return {o, lse2};
 }
@@ -408,7 +450,7 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k,
               int64_t window, const c10::optional<at::Tensor>& kv_start,
               const c10::optional<at::Tensor>& kv_end, const c10::optional<at::Tensor>& segs,
               const c10::optional<at::Tensor>& rope_cos, const c10::optional<at::Tensor>& rope_sin,
-              const c10::optional<at::Tensor>& rope_pos) {
+              const c10::optional<at::Tensor>& rope_pos, bool rope_inputs) {
   check_bthd(dout, "dout");
   check_bthd(q, "q");
   check_bthd(k, "k");
@@ -469,27 +511,12 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k,
   p.kv_start = (kv_start && kv_start->defined()) ? kv_start->data_ptr<int>() : nullptr;
   p.kv_end = (kv_end && kv_end->defined()) ? kv_end->data_ptr<int>() : nullptr;
   p.seg_end = seg_ptr(segs, B, Tq, Tk, causal, causal_off, q, 1);
-  // fused RoPE backward: dq / dk receive the un-rotated gradients (full rotary only)
-  const bool rope = rope_cos && rope_cos->defined();
-  if (rope) {
-    TORCH_CHECK(rope_sin && rope_sin->defined(), "rope_sin missing");
-    for (const at::Tensor* t : {&*rope_cos, &*rope_sin}) {
-      TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous() && t->dim() == 2 &&
-                      t->size(1) == D / 2, "rope cos/sin must be contiguous fp32 [max_pos, head_dim/2]");
-      same_device(q, *t);
-    }
-    TORCH_CHECK(Tq == Tk && causal_off == 0, "fused RoPE backward needs self-attention");
-    if (rope_pos && rope_pos->defined()) {
-      TORCH_CHECK(rope_pos->scalar_type() == at::kInt && rope_pos->is_contiguous() &&
-                      rope_pos->numel() == B * Tq, "rope_pos must be contiguous int32 [B*T]");
-      same_device(q, *rope_pos);
-    } else {
-      TORCH_CHECK(Tq <= rope_cos->size(0), "positions exceed the rotary table");
-    }
-    p.rope_cos = rope_cos->data_ptr<float>();
-    p.rope_sin = rope_sin->data_ptr<float>();
-    p.rope_pos = (rope_pos && rope_pos->defined()) ? rope_pos->data_ptr<int>() : nullptr;
-  }
+  // fused RoPE backward: dq / dk receive the un-rotated gradients (full rotary only); with
+  // rope_inputs q / k are also un-rotated and get rotated as they are staged
+  rope_args(rope_cos, rope_sin, rope_pos, q, B, Tq, Tk, D, causal_off, &p.rope_cos, &p.rope_sin,
+            &p.rope_pos);
+  TORCH_CHECK(!rope_inputs || p.rope_cos != nullptr, "rope_inputs needs the rotary tables");
+  p.rope_inputs = rope_inputs ? 1 : 0;
   launch_attn_bwd(p, static_cast<int>(D), causal, st);
   launch_attn_dq_reduce(p.dq_slab, static_cast<int>(nkb), static_cast<int>(B), static_cast<int>(Tq),
                         p.slab_rows, static_cast<int>(Hq), static_cast<int>(D), causal, p.causal_off, p.window,
@@ -825,8 +852,8 @@ TORCH_LIBRARY(dla, m) {
   m.def("gelu_bwd(Tensor x, Tensor dy) -> Tensor");
   m.def("rope_fwd(Tensor qkv, Tensor cos, Tensor sin, Tensor? pos, int Hq, int Hkv, int D, int rot, int T, int pos_offset) -> (Tensor, Tensor)");
   m.def("rope_bwd(Tensor dq, Tensor dk, Tensor(a!) dqkv, Tensor cos, Tensor sin, Tensor? pos, int Hq, int Hkv, int D, int rot, int T, int pos_offset) -> ()");
-  m.def("attn_fwd(Tensor q, Tensor k, Tensor v, float scale, bool causal, int causal_off, int window, Tensor? kv_start, Tensor? kv_end, Tensor? segs=None) -> (Tensor, Tensor)");
-  m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse2, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, float scale, bool causal, int causal_off, int window, Tensor? kv_start, Tensor? kv_end, Tensor? segs=None, Tensor? rope_cos=None, Tensor? rope_sin=None, Tensor? rope_pos=None) -> ()");
+  m.def("attn_fwd(Tensor q, Tensor k, Tensor v, float scale, bool causal, int causal_off, int window, Tensor? kv_start, Tensor? kv_end, Tensor? segs=None, Tensor? rope_cos=None, Tensor? rope_sin=None, Tensor? rope_pos=None, Tensor(a!)? q_rot=None) -> (Tensor, Tensor)");
+  m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse2, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, float scale, bool causal, int causal_off, int window, Tensor? kv_start, Tensor? kv_end, Tensor? segs=None, Tensor? rope_cos=None, Tensor? rope_sin=None, Tensor? rope_pos=None, bool rope_inputs=False) -> ()");
   m.def("transpose_bf16(Tensor input, Tensor(a!) out) -> ()");
   m.def("logprob_fwd(Tensor logits, Tensor targets, int vocab_offset=0) -> (Tensor, Tensor)");
   m.def("logprob_bwd(Tensor(a!) logits, Tensor targets, Tensor lse, Tensor grad, int vocab_offset=0) -> ()");

@@ -127,6 +127,12 @@ def _i32(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
 # separate rope_bwd launch, no rotated-space dq/dk temporaries); DLA_FUSED_ROPE_BWD=0 restores
 # the separate kernel for A/B runs.
 FUSED_ROPE_BWD = os.environ.get("DLA_FUSED_ROPE_BWD", "1") != "0"
+# Full-rotary RoPE forward folded into the attention kernels ("RoPE on load": no rope_fwd launch,
+# no rotated K copy; the forward writes the rotated Q only when a backward needs it). Off by
+# default: same-box A/B on the Llama-3-8B DPO step 1611-1613 (on) vs 1608-1609 ms (off) — every
+# forward workgroup re-rotates each K tile it stages (16 query blocks per sequence at T = 1024),
+# which costs more than the one 40 us rope pass it replaces. DLA_FUSED_ROPE_FWD=1 enables it.
+FUSED_ROPE_FWD = os.environ.get("DLA_FUSED_ROPE_FWD", "0") == "1"
 
 
 class _FusedQKVAttnFn(torch.autograd.Function):
@@ -138,18 +144,32 @@ class _FusedQKVAttnFn(torch.autograd.Function):
         ops = _ext.require()
         B, T, C = qkv.shape
         q2 = qkv.reshape(B * T, C)
-        if rot > 0:
-            q_r, k_r = ops.rope_fwd(q2, cos, sin, pos, Hq, Hkv, D, rot, T, 0)
-            q4 = q_r.view(B, T, Hq, D)
-            k4 = k_r.view(B, T, Hkv, D)
+        off = qkv.storage_offset()
+        v4 = qkv.as_strided((B, T, Hkv, D), (T * C, C, D, 1), off + (Hq + Hkv) * D)
+        on_load = rot == D and FUSED_ROPE_FWD
+        if on_load:
+            # RoPE on load: the kernel rotates Q in registers and K as it stages it; the rotated
+            # Q leaves as a side output only when a backward will read it
+            q4 = qkv.as_strided((B, T, Hq, D), (T * C, C, D, 1), off)
+            k4 = qkv.as_strided((B, T, Hkv, D), (T * C, C, D, 1), off + Hq * D)
+            q_rot = torch.empty((B, T, Hq, D), dtype=qkv.dtype, device=qkv.device) \
+                if ctx.needs_input_grad[0] else None
+            o, lse2 = ops.attn_fwd(q4, k4, v4, float(scale), bool(causal), 0, int(window), kv_start,
+                                   kv_end, segs, cos, sin, pos, q_rot)
+            ctx.save_for_backward(qkv, q_rot, None, o, lse2, cos, sin, pos, kv_start, kv_end, segs)
         else:
-            q4 = qkv.as_strided((B, T, Hq, D), (T * C, C, D, 1), qkv.storage_offset())
-            k4 = qkv.as_strided((B, T, Hkv, D), (T * C, C, D, 1), qkv.storage_offset() + Hq * D)
-        v4 = qkv.as_strided((B, T, Hkv, D), (T * C, C, D, 1), qkv.storage_offset() + (Hq + Hkv) * D)
-        o, lse2 = ops.attn_fwd(q4, k4, v4, float(scale), bool(causal), 0, int(window), kv_start, kv_end,
-                               segs)
-        ctx.save_for_backward(qkv, q4 if rot > 0 else None, k4 if rot > 0 else None, o, lse2,
-                              cos, sin, pos, kv_start, kv_end, segs)
+            if rot > 0:
+                q_r, k_r = ops.rope_fwd(q2, cos, sin, pos, Hq, Hkv, D, rot, T, 0)
+                q4 = q_r.view(B, T, Hq, D)
+                k4 = k_r.view(B, T, Hkv, D)
+            else:
+                q4 = qkv.as_strided((B, T, Hq, D), (T * C, C, D, 1), off)
+                k4 = qkv.as_strided((B, T, Hkv, D), (T * C, C, D, 1), off + Hq * D)
+            o, lse2 = ops.attn_fwd(q4, k4, v4, float(scale), bool(causal), 0, int(window), kv_start,
+                                   kv_end, segs)
+            ctx.save_for_backward(qkv, q4 if rot > 0 else None, k4 if rot > 0 else None, o, lse2,
+                                  cos, sin, pos, kv_start, kv_end, segs)
+        ctx.on_load = on_load
         ctx.cfg = (B, T, C, Hq, Hkv, D, rot, scale, causal, window)
         return o.view(B, T, Hq * D)
 
@@ -159,14 +179,16 @@ class _FusedQKVAttnFn(torch.autograd.Function):
         qkv, q4, k4, o, lse2, cos, sin, pos, kv_start, kv_end, segs = ctx.saved_tensors
         B, T, C, Hq, Hkv, D, rot, scale, causal, window = ctx.cfg
         off = qkv.storage_offset()
-        if rot == 0:
+        if ctx.on_load:  # q4 = the forward's rotated Q; K is rotated again as it is staged
+            k4 = qkv.as_strided((B, T, Hkv, D), (T * C, C, D, 1), off + Hq * D)
+        elif rot == 0:
             q4 = qkv.as_strided((B, T, Hq, D), (T * C, C, D, 1), off)
             k4 = qkv.as_strided((B, T, Hkv, D), (T * C, C, D, 1), off + Hq * D)
         v4 = qkv.as_strided((B, T, Hkv, D), (T * C, C, D, 1), off + (Hq + Hkv) * D)
         do4 = do.contiguous().view(B, T, Hq, D)
         dqkv = torch.empty((B, T, C), dtype=qkv.dtype, device=qkv.device)
         dv = dqkv.as_strided((B, T, Hkv, D), (T * C, C, D, 1), (Hq + Hkv) * D)
-        fused_rope = rot == D and FUSED_ROPE_BWD
+        fused_rope = rot == D and (FUSED_ROPE_BWD or ctx.on_load)
         if rot > 0 and not fused_rope:  # rotated-space dq / dk, un-rotated by the RoPE backward
             dq = torch.empty((B, T, Hq, D), dtype=qkv.dtype, device=qkv.device)
             dk = torch.empty((B, T, Hkv, D), dtype=qkv.dtype, device=qkv.device)
@@ -175,7 +197,7 @@ class _FusedQKVAttnFn(torch.autograd.Function):
             dk = dqkv.as_strided((B, T, Hkv, D), (T * C, C, D, 1), Hq * D)
         if fused_rope:
             ops.attn_bwd(do4, q4, k4, v4, o, lse2, dq, dk, dv, float(scale), bool(causal), 0,
-                         int(window), kv_start, kv_end, segs, cos, sin, pos)
+                         int(window), kv_start, kv_end, segs, cos, sin, pos, bool(ctx.on_load))
         else:
             ops.attn_bwd(do4, q4, k4, v4, o, lse2, dq, dk, dv, float(scale), bool(causal), 0,
                          int(window), kv_start, kv_end, segs)
