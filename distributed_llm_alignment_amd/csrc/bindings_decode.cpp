@@ -37,6 +37,32 @@ void launch_skinny_gemm(const bf16_t*, int64_t, const bf16_t*, int64_t, bf16_t*,
                         unsigned*, int, int, int, int, bool, bool, hipStream_t);
 void launch_skinny_glu_norm(const bf16_t*, const bf16_t*, const bf16_t*, bf16_t*, float, int64_t,
                             const bf16_t*, int64_t, bf16_t*, int64_t, int, int, int, hipStream_t);
+bool skinny_glu_ks_ok(int N, int K);
+void launch_skinny_glu_ks(const bf16_t*, int64_t, const bf16_t*, int64_t, bf16_t*, int64_t, int,
+                          int, int, hipStream_t);
+
+// Decode gate|up with the SwiGLU epilogue on the in-workgroup split-K kernel: w = [gate; up]
+// (2F rows) -> m = silu(x gate^T) * (x up^T) [M, F], one workgroup per 16 features.
+at::Tensor skinny_glu_ks(const at::Tensor& x, const at::Tensor& w) {
+  check_bf16(x, "x");
+  check_bf16(w, "w");
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.stride(1) == 1 && w.stride(1) == 1,
+              "x [M, K] / w [2F, K] with unit inner stride");
+  const int64_t M = x.size(0), N = w.size(0), K = w.size(1);
+  TORCH_CHECK(M >= 1 && M <= 16, "skinny GLU: 1 <= M <= 16");
+  TORCH_CHECK(x.size(1) == K, "x width must be K");
+  TORCH_CHECK(N < (1ll << 30) && K < (1ll << 30) && skinny_glu_ks_ok((int)N, (int)K),
+              "skinny GLU: K % 512 == 0 and 2F % 32 == 0");
+  TORCH_CHECK(x.stride(0) % 8 == 0 && w.stride(0) % 8 == 0, "16-byte aligned rows");
+  check_aligned16(x, "x");
+  check_aligned16(w, "w");
+  same_device(x, w);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  auto m = at::empty({M, N / 2}, x.options());
+  launch_skinny_glu_ks(cbp(x), x.stride(0), cbp(w), w.stride(0), bp(m), m.stride(0), (int)M,
+                       (int)N, (int)K, cur_stream(x));
+  return m;
+}
 
 // Decode MLP entry with the residual add + RMSNorm fused in: s = x + res (returned: the next
 // residual), m = swiglu(RMSNorm(s) * norm_w @ w_up^T) with w_up = [gate; up] (2F rows).
@@ -300,6 +326,7 @@ TORCH_LIBRARY_FRAGMENT(dla, m) {
   m.def("sample_tokens(Tensor logits, float temperature, int top_k, float top_p, bool greedy, Tensor rng) -> Tensor");
   m.def("skinny_gemm(Tensor x, Tensor w, Tensor(a!) counters, bool swiglu, bool glu_out=False) -> Tensor");
   m.def("skinny_glu_norm(Tensor x, Tensor res, Tensor norm_w, float eps, Tensor w) -> (Tensor, Tensor)");
+  m.def("skinny_glu_ks(Tensor x, Tensor w) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(dla, CUDA, m) {
@@ -309,4 +336,5 @@ TORCH_LIBRARY_IMPL(dla, CUDA, m) {
   m.impl("decode_attn_rope", &dla::decode_attn_rope);
   m.impl("skinny_gemm", &dla::skinny_gemm);
   m.impl("skinny_glu_norm", &dla::skinny_glu_norm);
+  m.impl("skinny_glu_ks", &dla::skinny_glu_ks);
 }

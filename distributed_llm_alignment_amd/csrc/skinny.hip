@@ -38,6 +38,25 @@ __device__ __forceinline__ f32x4 mfma16(s16x8 a, s16x8 b, f32x4 c) {
 
 __device__ __forceinline__ float silu_sk(float g) { return g * sigmoidf_(g); }
 
+// Weight-stream load: with NT the 16-byte load carries the non-temporal hint (each weight byte is
+// read once per decode step by one CU; MI355X_MICROARCH.md "nt-weights").
+template <bool NT>
+__device__ __forceinline__ s16x8 load_w(const bf16_t* p) {
+  if constexpr (NT)
+    return __builtin_bit_cast(s16x8, __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(p)));
+  else
+    return __builtin_bit_cast(s16x8, load_bf16x8(p));
+}
+
+// DLA_SKINNY_NT=1: non-temporal weight loads in every skinny kernel (read once per process)
+bool skinny_nt() {
+  static const bool nt = [] {
+    const char* e = getenv("DLA_SKINNY_NT");
+    return e != nullptr && atoi(e) != 0;
+  }();
+  return nt;
+}
+
 }  // namespace
 
 // grid: (ceil(N / 128), S), 8 waves. LDS: M x (kc + 8) bf16 (row pad of 16 B keeps the 16-row fragment
@@ -59,7 +78,7 @@ struct SkNorm {
   float eps;
 };
 
-template <bool SWIGLU, bool GLU_OUT = false, bool NORM = false>
+template <bool SWIGLU, bool GLU_OUT = false, bool NORM = false, bool NTW = false>
 __global__ __launch_bounds__(64 * kSkWaves) void skinny_gemm_kernel(
     const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ W, int64_t ldw,
     bf16_t* __restrict__ y, int64_t ldy, float* __restrict__ ws, unsigned* __restrict__ counters,
@@ -86,11 +105,10 @@ __global__ __launch_bounds__(64 * kSkWaves) void skinny_gemm_kernel(
   s16x8 b0[kSkUnroll], b1[kSkUnroll];
   if (active) {
 #pragma unroll
-    for (int u = 0; u < kSkUnroll; ++u) b0[u] = __builtin_bit_cast(s16x8, load_bf16x8(wrow + u * 32));
+    for (int u = 0; u < kSkUnroll; ++u) b0[u] = load_w<NTW>(wrow + u * 32);
     if (nchunks > 1) {
 #pragma unroll
-      for (int u = 0; u < kSkUnroll; ++u)
-        b1[u] = __builtin_bit_cast(s16x8, load_bf16x8(wrow + kSkChunk + u * 32));
+      for (int u = 0; u < kSkUnroll; ++u) b1[u] = load_w<NTW>(wrow + kSkChunk + u * 32);
     }
   }
 
@@ -205,14 +223,14 @@ __global__ __launch_bounds__(64 * kSkWaves) void skinny_gemm_kernel(
       if (c + 2 < nchunks) {
 #pragma unroll
         for (int u = 0; u < kSkUnroll; ++u)
-          b0[u] = __builtin_bit_cast(s16x8, load_bf16x8(wrow + (c + 2) * kSkChunk + u * 32));
+          b0[u] = load_w<NTW>(wrow + (c + 2) * kSkChunk + u * 32);
       }
       if (c + 1 < nchunks) {
         compute(b1, (c + 1) * kSkChunk);
         if (c + 3 < nchunks) {
 #pragma unroll
           for (int u = 0; u < kSkUnroll; ++u)
-            b1[u] = __builtin_bit_cast(s16x8, load_bf16x8(wrow + (c + 3) * kSkChunk + u * 32));
+            b1[u] = load_w<NTW>(wrow + (c + 3) * kSkChunk + u * 32);
         }
       }
     }
@@ -324,19 +342,20 @@ void launch_skinny_glu_norm(const bf16_t* x, const bf16_t* res, const bf16_t* nw
       x, ldx, W, ldw, y, ldy, nullptr, nullptr, M, N, K, K, SkNorm{res, nw, sum_out, eps});
 }
 
-void launch_skinny_gemm(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
-                        int64_t ldy, float* ws, unsigned* counters, int M, int N, int K, int S,
-                        bool swiglu, bool glu_out, hipStream_t st) {
+template <bool NT>
+void launch_skinny_gemm_t(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
+                          int64_t ldy, float* ws, unsigned* counters, int M, int N, int K, int S,
+                          bool swiglu, bool glu_out, hipStream_t st) {
   const int kc = K / S;
   dim3 grid((N + kSkCols - 1) / kSkCols, S);
   const size_t lds = skinny_lds_bytes(M, kc);
   static bool attr_set = [] {  // S = 1 at K = 4096 stages up to 16 x 4104 bf16 (> 64 KB default)
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_gemm_kernel<false>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_gemm_kernel<false, false, false, NT>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_gemm_kernel<true>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_gemm_kernel<true, false, false, NT>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     // the GLU variant also holds an 8 KB static exchange tile: dynamic + static <= 160 KB
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_gemm_kernel<false, true>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_gemm_kernel<false, true, false, NT>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, 152 * 1024);
     (void)hipGetLastError();  // never leave a sticky error for the caller's next launch check
     return true;
@@ -344,16 +363,25 @@ void launch_skinny_gemm(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t l
   (void)attr_set;
   if (glu_out) {  // N = 2F weight rows -> F outputs, 64 per block, never split
     dim3 g2(N / 2 / 64, 1);
-    skinny_gemm_kernel<false, true><<<g2, 64 * kSkWaves, skinny_lds_bytes(M, K), st>>>(
+    skinny_gemm_kernel<false, true, false, NT><<<g2, 64 * kSkWaves, skinny_lds_bytes(M, K), st>>>(
         x, ldx, W, ldw, y, ldy, ws, counters, M, N, K, K);
     return;
   }
   if (swiglu)
-    skinny_gemm_kernel<true><<<grid, 64 * kSkWaves, lds, st>>>(x, ldx, W, ldw, y, ldy, ws,
-                                                                counters, M, N, K, kc);
+    skinny_gemm_kernel<true, false, false, NT><<<grid, 64 * kSkWaves, lds, st>>>(
+        x, ldx, W, ldw, y, ldy, ws, counters, M, N, K, kc);
   else
-    skinny_gemm_kernel<false><<<grid, 64 * kSkWaves, lds, st>>>(x, ldx, W, ldw, y, ldy, ws,
-                                                                 counters, M, N, K, kc);
+    skinny_gemm_kernel<false, false, false, NT><<<grid, 64 * kSkWaves, lds, st>>>(
+        x, ldx, W, ldw, y, ldy, ws, counters, M, N, K, kc);
+}
+
+void launch_skinny_gemm(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
+                        int64_t ldy, float* ws, unsigned* counters, int M, int N, int K, int S,
+                        bool swiglu, bool glu_out, hipStream_t st) {
+  if (skinny_nt())
+    launch_skinny_gemm_t<true>(x, ldx, W, ldw, y, ldy, ws, counters, M, N, K, S, swiglu, glu_out, st);
+  else
+    launch_skinny_gemm_t<false>(x, ldx, W, ldw, y, ldy, ws, counters, M, N, K, S, swiglu, glu_out, st);
 }
 
 // Narrow outputs (N <= ~16K: qkv, o, down at Llama-3-8B): ONE workgroup per 16 output columns,
@@ -365,16 +393,21 @@ void launch_skinny_gemm(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t l
 constexpr int kKsUnroll = 4;  // k-steps per chunk (one 16-byte W and x load per lane each)
 constexpr int kKsChunk = 32 * kKsUnroll;
 
-template <int DEPTH>
+// GLU (decode gate|up with the SwiGLU epilogue, W = [gate; up], 2F rows -> m [M, F]): the
+// workgroup owns 16 features; waves 0-3 take the gate rows, waves 4-7 the matching up rows, each
+// over a quarter of K. F / 16 workgroups (896 at Llama-3-8B) instead of the LDS-staged kernel's
+// F / 64 = 224, which leaves 32 of the 256 CUs without a weight stream.
+template <int DEPTH, bool NT, bool GLU>
 __global__ __launch_bounds__(512) void skinny_ksplit_kernel(
     const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ W, int64_t ldw,
     bf16_t* __restrict__ y, int64_t ldy, int M, int N, int K) {
   __shared__ float red[8][4][64];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = lane & 15, q = lane >> 4;
-  const int n0 = blockIdx.x * 16;
-  const int kw = K >> 3;  // per-wave K slice (multiple of kKsChunk, checked on the host)
-  const int k0 = wave * kw;
+  const int n0 = GLU ? (wave < 4 ? 0 : N >> 1) + blockIdx.x * 16 : blockIdx.x * 16;
+  // per-wave K slice (multiple of kKsChunk, checked on the host)
+  const int kw = GLU ? K >> 2 : K >> 3;
+  const int k0 = (GLU ? (wave & 3) : wave) * kw;
   const int nchunks = kw / kKsChunk;
   const bool arow = r < M;
   const bf16_t* wrow = W + static_cast<int64_t>(n0 + r) * ldw + k0 + q * 8;
@@ -383,8 +416,7 @@ __global__ __launch_bounds__(512) void skinny_ksplit_kernel(
   s16x8 b[DEPTH][kKsUnroll], a[DEPTH][kKsUnroll];
   auto load = [&](int j, int c) {
 #pragma unroll
-    for (int u = 0; u < kKsUnroll; ++u)
-      b[j][u] = __builtin_bit_cast(s16x8, load_bf16x8(wrow + c * kKsChunk + u * 32));
+    for (int u = 0; u < kKsUnroll; ++u) b[j][u] = load_w<NT>(wrow + c * kKsChunk + u * 32);
 #pragma unroll
     for (int u = 0; u < kKsUnroll; ++u) {
       a[j][u] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
@@ -406,17 +438,29 @@ __global__ __launch_bounds__(512) void skinny_ksplit_kernel(
       }
     }
   }
-  // lane holds C[m = 4q + i][n = n0 + r]; sum the 8 waves' tiles in wave order (deterministic)
+  // lane holds C[m = 4q + i][n = n0 + r]; sum the waves' tiles in wave order (deterministic)
 #pragma unroll
   for (int i = 0; i < 4; ++i) red[wave][i][lane] = acc[i];
   __syncthreads();
   if (threadIdx.x < 256) {
     const int i = threadIdx.x >> 6, l = threadIdx.x & 63;
-    float t = 0.f;
+    const int m = 4 * (l >> 4) + i, n = blockIdx.x * 16 + (l & 15);
+    if constexpr (GLU) {
+      float g = 0.f, u = 0.f;
 #pragma unroll
-    for (int w = 0; w < 8; ++w) t += red[w][i][l];
-    const int m = 4 * (l >> 4) + i, n = n0 + (l & 15);
-    if (m < M) y[m * ldy + n] = f2bf(t);
+      for (int w = 0; w < 4; ++w) g += red[w][i][l];
+#pragma unroll
+      for (int w = 4; w < 8; ++w) u += red[w][i][l];
+      // gate / up rounded to bf16 first, exactly as the unfused GEMM + swiglu pair
+      g = bf2f(f2bf(g));
+      u = bf2f(f2bf(u));
+      if (m < M) y[m * ldy + n] = f2bf(silu_sk(g) * u);
+    } else {
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) t += red[w][i][l];
+      if (m < M) y[m * ldy + n] = f2bf(t);
+    }
   }
 }
 
@@ -424,11 +468,26 @@ bool skinny_use_ksplit(int N, int K) {
   return (N + kSkCols - 1) / kSkCols < 128 && (K % (8 * kKsChunk)) == 0 && N % 16 == 0;
 }
 
+bool skinny_glu_ks_ok(int N, int K) { return (K % (4 * kKsChunk)) == 0 && N % 32 == 0; }
+
 void launch_skinny_ksplit(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
                           int64_t ldy, int M, int N, int K, hipStream_t st) {
   // a 2-deep ring (84 VGPRs: 5-6 waves per SIMD, every qkv block resident in one round); a
   // 4-deep ring (152 VGPRs) measured slower at qkv (16.0 vs 14.8 us in a decode step)
-  skinny_ksplit_kernel<2><<<N / 16, 512, 0, st>>>(x, ldx, W, ldw, y, ldy, M, N, K);
+  if (skinny_nt())
+    skinny_ksplit_kernel<2, true, false><<<N / 16, 512, 0, st>>>(x, ldx, W, ldw, y, ldy, M, N, K);
+  else
+    skinny_ksplit_kernel<2, false, false><<<N / 16, 512, 0, st>>>(x, ldx, W, ldw, y, ldy, M, N, K);
+}
+
+// gate|up (N = 2F weight rows) -> m = silu(gate) * up [M, F], F / 16 workgroups
+void launch_skinny_glu_ks(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
+                          int64_t ldy, int M, int N, int K, hipStream_t st) {
+  const int nb = N / 32;
+  if (skinny_nt())
+    skinny_ksplit_kernel<2, true, true><<<nb, 512, 0, st>>>(x, ldx, W, ldw, y, ldy, M, N, K);
+  else
+    skinny_ksplit_kernel<2, false, true><<<nb, 512, 0, st>>>(x, ldx, W, ldw, y, ldy, M, N, K);
 }
 
 }  // namespace dla

@@ -122,11 +122,23 @@ def skinny_linear(x: torch.Tensor, weight: torch.Tensor, swiglu: bool = False,
     return y.view(*x.shape[:-1], weight.shape[0])
 
 
-def skinny_glu(x: torch.Tensor, weight: torch.Tensor) -> Optional[torch.Tensor]:
+# gate|up kernel: "ks" = in-workgroup split-K (F / 16 workgroups, 4 waves per gate / up K
+# quarter), "lds" = x staged in LDS, one wave per 16 rows over all of K (F / 64 workgroups)
+SKINNY_GLU = os.environ.get("DLA_SKINNY_GLU", "lds")
+
+
+def skinny_glu(x: torch.Tensor, weight: torch.Tensor, mode: Optional[str] = None) -> Optional[torch.Tensor]:
     """Decode gate|up projection with SwiGLU in the epilogue: weight = [gate; up] (2F rows) ->
-    silu(x gate^T) * (x up^T) [.., F] in one kernel (csrc/skinny.hip GLU_OUT). None if the
+    silu(x gate^T) * (x up^T) [.., F] in one kernel (csrc/skinny.hip). None if the
     shape/state is not eligible (the caller runs GEMM + swiglu)."""
-    if not skinny_ok(x, weight) or weight.shape[0] % 128 or x.shape[-1] * min(x.numel() // x.shape[-1], 16) > 80 * 1024:
+    if not skinny_ok(x, weight):
+        return None
+    if (mode or SKINNY_GLU) == "ks" and x.shape[-1] % 512 == 0 and weight.shape[0] % 32 == 0:
+        x2 = x.reshape(-1, x.shape[-1])
+        if x2.stride(-1) != 1 or x2.stride(0) % 8 or x2.data_ptr() % 16:
+            x2 = x2.contiguous()
+        return _ext.require().skinny_glu_ks(x2, weight).view(*x.shape[:-1], weight.shape[0] // 2)
+    if weight.shape[0] % 128 or x.shape[-1] * min(x.numel() // x.shape[-1], 16) > 80 * 1024:
         return None
     cnt = _skinny_counters(x.device)
     if cnt is None:

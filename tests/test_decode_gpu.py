@@ -313,17 +313,19 @@ def test_skinny_gemm_strided_rows_and_eligibility():
     assert decode.skinny_linear(xg, w, min_n=0) is None  # autograd: library GEMM path
 
 
+@pytest.mark.parametrize("mode", ["lds", "ks"])
 @pytest.mark.parametrize("M", [1, 8, 16])
 @pytest.mark.parametrize("F,K", [(14336, 4096), (192, 512)])
-def test_skinny_glu_epilogue_matches_unfused(M, F, K):
-    """gate|up skinny GEMM with the SwiGLU epilogue == swiglu(bf16 GEMM output), fp32 reference."""
+def test_skinny_glu_epilogue_matches_unfused(M, F, K, mode):
+    """gate|up skinny GEMM with the SwiGLU epilogue == swiglu(bf16 GEMM output), fp32 reference;
+    both gate|up kernels (LDS-staged and in-workgroup split-K)."""
     from distributed_llm_alignment_amd.ops import decode
 
     g = torch.Generator(device=DEV).manual_seed(M + F)
     x = torch.randn(M, K, device=DEV, generator=g).to(torch.bfloat16)
     w = (torch.randn(2 * F, K, device=DEV, generator=g) * K ** -0.5).to(torch.bfloat16)
     with torch.no_grad():
-        m = decode.skinny_glu(x, w)
+        m = decode.skinny_glu(x, w, mode=mode)
         assert m is not None and m.shape == (M, F)
         u = (x.float() @ w.float().t()).to(torch.bfloat16)
         gg, uu = u.float().chunk(2, dim=-1)
@@ -375,7 +377,7 @@ def test_fused_norm_glu_matches_add_norm_then_glu(M, K, F):
     w = (torch.randn(2 * F, K, device=dev, generator=g) * 0.02).to(torch.bfloat16)
     with torch.no_grad():
         h, s_ref = ops.add_norm(a, r, nw, None, 1e-5, True)
-        m_ref = ops.decode.skinny_glu(h, w)
+        m_ref = ops.decode.skinny_glu(h, w, mode="lds")  # the kernel it stages the norm into
         m, s = ops._ext.require().skinny_glu_norm(a, r, nw, 1e-5, w)
     torch.cuda.synchronize()
     assert torch.equal(s, s_ref)
