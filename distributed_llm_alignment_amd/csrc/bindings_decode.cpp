@@ -49,7 +49,7 @@ at::Tensor skinny_glu_ks(const at::Tensor& x, const at::Tensor& w) {
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.stride(1) == 1 && w.stride(1) == 1,
               "x [M, K] / w [2F, K] with unit inner stride");
   const int64_t M = x.size(0), N = w.size(0), K = w.size(1);
-  TORCH_CHECK(M >= 1 && M <= 16, "skinny GLU: 1 <= M <= 16");
+  TORCH_CHECK(M >= 1 && M <= 64, "skinny GLU: 1 <= M <= 64");
   TORCH_CHECK(x.size(1) == K, "x width must be K");
   TORCH_CHECK(N < (1ll << 30) && K < (1ll << 30) && skinny_glu_ks_ok((int)N, (int)K),
               "skinny GLU: K % 512 == 0 and 2F % 32 == 0");
@@ -107,7 +107,9 @@ at::Tensor skinny_gemm(const at::Tensor& x, const at::Tensor& w, at::Tensor& cou
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.stride(1) == 1 && w.stride(1) == 1,
               "x [M, K] / w [N, K] with unit inner stride");
   const int64_t M = x.size(0), N = w.size(0), K = w.size(1);
-  TORCH_CHECK(M >= 1 && M <= 16, "skinny GEMM: 1 <= M <= 16");
+  // 17..64 rows: only the in-workgroup split-K kernel (narrow N, no fused swiglu input)
+  TORCH_CHECK(M >= 1 && (M <= 16 || (M <= 64 && !swiglu && !glu_out && skinny_use_ksplit((int)N, (int)K))),
+              "skinny GEMM: 1 <= M <= 16 (<= 64 on the split-K path: N < 16384, K % 1024 == 0)");
   TORCH_CHECK(x.size(1) == (swiglu ? 2 * K : K), "x width must be K (2K with swiglu)");
   TORCH_CHECK(K % 256 == 0 && N % 16 == 0, "skinny GEMM: K % 256 == 0 and N % 16 == 0");
   TORCH_CHECK(x.stride(0) % 8 == 0 && w.stride(0) % 8 == 0, "16-byte aligned rows");

@@ -395,62 +395,79 @@ constexpr int kKsChunk = 32 * kKsUnroll;
 
 // GLU (decode gate|up with the SwiGLU epilogue, W = [gate; up], 2F rows -> m [M, F]): the
 // workgroup owns 16 features; waves 0-3 take the gate rows, waves 4-7 the matching up rows, each
-// over a quarter of K. F / 16 workgroups (896 at Llama-3-8B) instead of the LDS-staged kernel's
-// F / 64 = 224, which leaves 32 of the 256 CUs without a weight stream.
-template <int DEPTH, bool NT, bool GLU>
+// over a quarter of K (F / 16 workgroups).
+// MT = row tiles of 16 (M <= 16 MT): every weight fragment feeds MT MFMAs, one per 16 rows of x
+// (larger decode batches, e.g. the reference's 64 rollouts per RLHF step on one GPU); UNR k-steps
+// per ring slot (4 at MT = 1; 2 above, which keeps the x fragments at ~110 VGPRs for MT = 4, four
+// waves per SIMD).
+template <int DEPTH, bool NT, bool GLU, int MT = 1, int UNR = kKsUnroll>
 __global__ __launch_bounds__(512) void skinny_ksplit_kernel(
     const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ W, int64_t ldw,
     bf16_t* __restrict__ y, int64_t ldy, int M, int N, int K) {
-  __shared__ float red[8][4][64];
+  constexpr int CH = 32 * UNR;  // k per ring slot
+  __shared__ float red[8][4 * MT][64];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = lane & 15, q = lane >> 4;
   const int n0 = GLU ? (wave < 4 ? 0 : N >> 1) + blockIdx.x * 16 : blockIdx.x * 16;
   // per-wave K slice (multiple of kKsChunk, checked on the host)
   const int kw = GLU ? K >> 2 : K >> 3;
   const int k0 = (GLU ? (wave & 3) : wave) * kw;
-  const int nchunks = kw / kKsChunk;
-  const bool arow = r < M;
+  const int nchunks = kw / CH;
   const bf16_t* wrow = W + static_cast<int64_t>(n0 + r) * ldw + k0 + q * 8;
-  const bf16_t* xrow = x + static_cast<int64_t>(arow ? r : 0) * ldx + k0 + q * 8;
+  bool arow[MT];
+  const bf16_t* xrow[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t) {
+    arow[t] = 16 * t + r < M;
+    xrow[t] = x + static_cast<int64_t>(arow[t] ? 16 * t + r : 0) * ldx + k0 + q * 8;
+  }
   // DEPTH chunks (W and x fragments) in flight: a ring of register sets, refilled as consumed
-  s16x8 b[DEPTH][kKsUnroll], a[DEPTH][kKsUnroll];
+  s16x8 b[DEPTH][UNR], a[DEPTH][UNR][MT];
   auto load = [&](int j, int c) {
 #pragma unroll
-    for (int u = 0; u < kKsUnroll; ++u) b[j][u] = load_w<NT>(wrow + c * kKsChunk + u * 32);
+    for (int u = 0; u < UNR; ++u) b[j][u] = load_w<NT>(wrow + c * CH + u * 32);
 #pragma unroll
-    for (int u = 0; u < kKsUnroll; ++u) {
-      a[j][u] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      if (arow) a[j][u] = __builtin_bit_cast(s16x8, load_bf16x8(xrow + c * kKsChunk + u * 32));
-    }
+    for (int u = 0; u < UNR; ++u)
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        a[j][u][t] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        if (arow[t]) a[j][u][t] = __builtin_bit_cast(s16x8, load_bf16x8(xrow[t] + c * CH + u * 32));
+      }
   };
 #pragma unroll
   for (int j = 0; j < DEPTH; ++j)
     if (j < nchunks) load(j, j);
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  f32x4 acc[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int c0 = 0; c0 < nchunks; c0 += DEPTH) {
 #pragma unroll
     for (int j = 0; j < DEPTH; ++j) {
       const int c = c0 + j;
       if (c < nchunks) {
 #pragma unroll
-        for (int u = 0; u < kKsUnroll; ++u) acc = mfma16(a[j][u], b[j][u], acc);
+        for (int u = 0; u < UNR; ++u)
+#pragma unroll
+          for (int t = 0; t < MT; ++t) acc[t] = mfma16(a[j][u][t], b[j][u], acc[t]);
         if (c + DEPTH < nchunks) load(j, c + DEPTH);
       }
     }
   }
-  // lane holds C[m = 4q + i][n = n0 + r]; sum the waves' tiles in wave order (deterministic)
+  // lane holds C[m = 16 t + 4q + i][n = n0 + r]; sum the waves' tiles in wave order (deterministic)
 #pragma unroll
-  for (int i = 0; i < 4; ++i) red[wave][i][lane] = acc[i];
+  for (int t = 0; t < MT; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) red[wave][4 * t + i][lane] = acc[t][i];
   __syncthreads();
-  if (threadIdx.x < 256) {
-    const int i = threadIdx.x >> 6, l = threadIdx.x & 63;
-    const int m = 4 * (l >> 4) + i, n = blockIdx.x * 16 + (l & 15);
+  for (int e = threadIdx.x; e < 256 * MT; e += 512) {
+    const int ti = e >> 6, l = e & 63;  // ti = 4 t + i
+    const int m = 16 * (ti >> 2) + 4 * (l >> 4) + (ti & 3), n = blockIdx.x * 16 + (l & 15);
     if constexpr (GLU) {
       float g = 0.f, u = 0.f;
 #pragma unroll
-      for (int w = 0; w < 4; ++w) g += red[w][i][l];
+      for (int w = 0; w < 4; ++w) g += red[w][ti][l];
 #pragma unroll
-      for (int w = 4; w < 8; ++w) u += red[w][i][l];
+      for (int w = 4; w < 8; ++w) u += red[w][ti][l];
       // gate / up rounded to bf16 first, exactly as the unfused GEMM + swiglu pair
       g = bf2f(f2bf(g));
       u = bf2f(f2bf(u));
@@ -458,7 +475,7 @@ __global__ __launch_bounds__(512) void skinny_ksplit_kernel(
     } else {
       float t = 0.f;
 #pragma unroll
-      for (int w = 0; w < 8; ++w) t += red[w][i][l];
+      for (int w = 0; w < 8; ++w) t += red[w][ti][l];
       if (m < M) y[m * ldy + n] = f2bf(t);
     }
   }
@@ -470,24 +487,34 @@ bool skinny_use_ksplit(int N, int K) {
 
 bool skinny_glu_ks_ok(int N, int K) { return (K % (4 * kKsChunk)) == 0 && N % 32 == 0; }
 
+template <bool NT, bool GLU>
+static void launch_ks(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
+                      int64_t ldy, int M, int N, int K, int nb, hipStream_t st) {
+  // M <= 16: a 2-deep ring (84 VGPRs: 5-6 waves per SIMD, every qkv block resident in one round);
+  // a 4-deep ring (152 VGPRs) measured slower at qkv (16.0 vs 14.8 us in a decode step)
+  if (M <= 16)
+    skinny_ksplit_kernel<2, NT, GLU, 1><<<nb, 512, 0, st>>>(x, ldx, W, ldw, y, ldy, M, N, K);
+  else if (M <= 32)
+    skinny_ksplit_kernel<2, NT, GLU, 2, 2><<<nb, 512, 0, st>>>(x, ldx, W, ldw, y, ldy, M, N, K);
+  else
+    skinny_ksplit_kernel<2, NT, GLU, 4, 2><<<nb, 512, 0, st>>>(x, ldx, W, ldw, y, ldy, M, N, K);
+}
+
 void launch_skinny_ksplit(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
                           int64_t ldy, int M, int N, int K, hipStream_t st) {
-  // a 2-deep ring (84 VGPRs: 5-6 waves per SIMD, every qkv block resident in one round); a
-  // 4-deep ring (152 VGPRs) measured slower at qkv (16.0 vs 14.8 us in a decode step)
   if (skinny_nt())
-    skinny_ksplit_kernel<2, true, false><<<N / 16, 512, 0, st>>>(x, ldx, W, ldw, y, ldy, M, N, K);
+    launch_ks<true, false>(x, ldx, W, ldw, y, ldy, M, N, K, N / 16, st);
   else
-    skinny_ksplit_kernel<2, false, false><<<N / 16, 512, 0, st>>>(x, ldx, W, ldw, y, ldy, M, N, K);
+    launch_ks<false, false>(x, ldx, W, ldw, y, ldy, M, N, K, N / 16, st);
 }
 
 // gate|up (N = 2F weight rows) -> m = silu(gate) * up [M, F], F / 16 workgroups
 void launch_skinny_glu_ks(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
                           int64_t ldy, int M, int N, int K, hipStream_t st) {
-  const int nb = N / 32;
   if (skinny_nt())
-    skinny_ksplit_kernel<2, true, true><<<nb, 512, 0, st>>>(x, ldx, W, ldw, y, ldy, M, N, K);
+    launch_ks<true, true>(x, ldx, W, ldw, y, ldy, M, N, K, N / 32, st);
   else
-    skinny_ksplit_kernel<2, false, true><<<nb, 512, 0, st>>>(x, ldx, W, ldw, y, ldy, M, N, K);
+    launch_ks<false, true>(x, ldx, W, ldw, y, ldy, M, N, K, N / 32, st);
 }
 
 }  // namespace dla

@@ -157,7 +157,7 @@ class MLP(nn.Module):
 
             h = tp_copy(h, self.tp)
         if (self.cfg.activation == "swiglu" and self.up_bias is None and self.down_bias is None
-                and self.tp is None and ops.decode.skinny_ok(h, self.up_proj)):
+                and self.tp is None and ops.decode.skinny_ok(h, self.up_proj, glu=True)):
             # decode (<= 16 rows, no autograd): skinny GEMMs, SwiGLU fused into the down GEMM
             m = ops.decode.skinny_glu(h, self.up_proj)  # gate|up GEMM with SwiGLU epilogue
             if m is not None:

@@ -91,16 +91,37 @@ def _skinny_counters(dev: torch.device) -> Optional[torch.Tensor]:
     return c
 
 
+# 17..64 decode rows can run on the split-K kernels with 2 or 4 row tiles per weight fragment
+# (narrow outputs N < 16384 with K % 1024 == 0, and the gate|up GLU kernel; DLA_SKINNY_MAX_ROWS=64).
+# Off by default: measured on 1x MI355X (Llama-3-8B, prompt 512, graph decode) 11.57 vs 6.11
+# ms/token at 64 rows and 7.12 vs 5.09 at 32 -- every workgroup re-reads all of x for its 16
+# output columns (~1.7 GB of L2 -> CU traffic per layer at 64 rows), which costs more than the
+# weight stream it shares; hipBLASLt's 16-64 x 64 tiles keep 17+ rows.
+SKINNY_MAX_ROWS = int(os.environ.get("DLA_SKINNY_MAX_ROWS", "16"))
+SKINNY_KS_MAX_K = int(os.environ.get("DLA_SKINNY_KS_MAX_K", str(1 << 20)))  # A/B: long-K down on hipBLASLt
+
+
+def _ks_rows_ok(rows: int, N: int, K: int, glu: bool) -> bool:
+    if glu:
+        return rows <= SKINNY_MAX_ROWS and K % 512 == 0 and N % 32 == 0
+    return (rows <= SKINNY_MAX_ROWS and N < SKINNY_WIDE_N and K % 1024 == 0 and N % 16 == 0
+            and K <= SKINNY_KS_MAX_K)
+
+
 def skinny_ok(x: torch.Tensor, weight: torch.Tensor, swiglu: bool = False,
-              min_n: Optional[int] = None) -> bool:
-    """Inference-only decode GEMM: <= 16 rows, bf16, K % 256 == 0, N % 16 == 0, no autograd."""
+              min_n: Optional[int] = None, glu: bool = False) -> bool:
+    """Inference-only decode GEMM: <= 16 rows (<= 64 on the split-K kernels), bf16,
+    K % 256 == 0, N % 16 == 0, no autograd. `glu`: the gate|up GEMM with the SwiGLU epilogue."""
     if not (SKINNY and _ext.use_native(x)) or torch.is_grad_enabled() and (x.requires_grad or weight.requires_grad):
         return False
     rows = x.numel() // x.shape[-1] if x.dim() else 0
     N, K = weight.shape if weight.dim() == 2 else (0, 0)
-    if min_n is None and (N > SKINNY_MAX_N or (N < SKINNY_WIDE_N and K > SKINNY_MAX_NARROW_K)):
+    if rows > 16:
+        if swiglu or not _ks_rows_ok(rows, N, K, glu):
+            return False
+    elif min_n is None and (N > SKINNY_MAX_N or (N < SKINNY_WIDE_N and K > SKINNY_MAX_NARROW_K)):
         return False
-    return (1 <= rows <= 16 and N >= (SKINNY_MIN_N if min_n is None else min_n) and x.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16
+    return (1 <= rows <= 64 and N >= (SKINNY_MIN_N if min_n is None else min_n) and x.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16
             and weight.dim() == 2 and weight.stride(1) == 1 and weight.stride(0) % 8 == 0
             and x.shape[-1] == (2 * K if swiglu else K) and K % 256 == 0 and N % 16 == 0
             and (N + 127) // 128 <= 8192 and x.device == weight.device)
@@ -131,9 +152,10 @@ def skinny_glu(x: torch.Tensor, weight: torch.Tensor, mode: Optional[str] = None
     """Decode gate|up projection with SwiGLU in the epilogue: weight = [gate; up] (2F rows) ->
     silu(x gate^T) * (x up^T) [.., F] in one kernel (csrc/skinny.hip). None if the
     shape/state is not eligible (the caller runs GEMM + swiglu)."""
-    if not skinny_ok(x, weight):
+    if not skinny_ok(x, weight, glu=True):
         return None
-    if (mode or SKINNY_GLU) == "ks" and x.shape[-1] % 512 == 0 and weight.shape[0] % 32 == 0:
+    rows = x.numel() // x.shape[-1]
+    if ((mode or SKINNY_GLU) == "ks" or rows > 16) and x.shape[-1] % 512 == 0 and weight.shape[0] % 32 == 0:
         x2 = x.reshape(-1, x.shape[-1])
         if x2.stride(-1) != 1 or x2.stride(0) % 8 or x2.data_ptr() % 16:
             x2 = x2.contiguous()

@@ -23,6 +23,8 @@ def main() -> int:
     ap.add_argument("--new", type=int, default=256)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--grad-ckpt", default="", help="policy activation recompute: full|mlp|attention "
+                    "(the reference's rlhf_config batch of 64 rollouts on one GPU needs mlp)")
     a = ap.parse_args()
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from distributed_llm_alignment_amd.models import build_model, generate, get_config
@@ -40,6 +42,8 @@ def main() -> int:
     ref = build_model(cfg, device=dev, dtype=torch.bfloat16, seed=1).requires_grad_(False).eval()
     rm = RewardModel(build_model(cfg, device=dev, dtype=torch.bfloat16, seed=2, headless=True)).to(dev, torch.bfloat16)
     rm.eval().requires_grad_(False)
+    if a.grad_ckpt:
+        pol.gradient_checkpointing_enable(a.grad_ckpt)
     eng = DataParallelEngine(pol, lr=1e-6, betas=(0.9, 0.95), weight_decay=0.01, max_grad_norm=1.0)
     g = torch.Generator(device=dev).manual_seed(0)
     phases = {"generate": 0.0, "score": 0.0, "train": 0.0}
@@ -75,6 +79,7 @@ def main() -> int:
         step(True)
     dt = sync() - t
     print(json.dumps({"bench": "rlhf_step", "model": cfg.name, "rollouts_per_step": a.batch,
+                      "grad_ckpt": a.grad_ckpt or "none",
                       "prompt": a.prompt, "new_tokens": a.new, "s_per_step": round(dt / a.steps, 3),
                       "rollouts_per_s": round(a.batch * a.steps / dt, 3),
                       **{f"{k}_s": round(v / a.steps, 3) for k, v in phases.items()}}), flush=True)
