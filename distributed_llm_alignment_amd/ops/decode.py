@@ -101,9 +101,12 @@ SKINNY_MAX_ROWS = int(os.environ.get("DLA_SKINNY_MAX_ROWS", "16"))
 SKINNY_KS_MAX_K = int(os.environ.get("DLA_SKINNY_KS_MAX_K", str(1 << 20)))  # A/B: long-K down on hipBLASLt
 
 
+SKINNY_GLU_MAX_ROWS = int(os.environ.get("DLA_SKINNY_GLU_MAX_ROWS", "64"))
+
+
 def _ks_rows_ok(rows: int, N: int, K: int, glu: bool) -> bool:
     if glu:
-        return rows <= SKINNY_MAX_ROWS and K % 512 == 0 and N % 32 == 0
+        return rows <= min(SKINNY_MAX_ROWS, SKINNY_GLU_MAX_ROWS) and K % 512 == 0 and N % 32 == 0
     return (rows <= SKINNY_MAX_ROWS and N < SKINNY_WIDE_N and K % 1024 == 0 and N % 16 == 0
             and K <= SKINNY_KS_MAX_K)
 
