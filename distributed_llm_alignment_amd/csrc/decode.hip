@@ -115,6 +115,9 @@ __global__ __launch_bounds__(256, 3) void decode_attn_kernel(
   const int split = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int len = kv_len[0];
+  // the row's first visible key, loaded together with kv_len ahead of the newest-token prologue
+  // (one scalar round trip before the bulk K / V loads; measured neutral vs after the prologue)
+  int lo = kv_start ? kv_start[b] : 0;
   const int sub = lane / LPK, dl = (lane % LPK) * 8;  // V row layout
   const int r16 = lane & 15, kg = lane >> 4;           // MFMA fragment layout
   bf16x8 vnew = {};
@@ -134,7 +137,6 @@ __global__ __launch_bounds__(256, 3) void decode_attn_kernel(
       store_bf16x8(vc + (int64_t)b * c_sb + (int64_t)newest * c_st + (int64_t)hk * c_sh + dl, vnew);
     }
   }
-  int lo = kv_start ? kv_start[b] : 0;
   if (window > 0) lo = max(lo, len - window);
   const int base = split * kDecChunk;
   const int k0 = max(base, lo), k1 = min(base + kDecChunk, len);
@@ -149,31 +151,35 @@ __global__ __launch_bounds__(256, 3) void decode_attn_kernel(
   const int kw0 = base + wv * KPW;  // this wave's first key
   const bf16_t* kb0 = kc + (int64_t)b * c_sb + (int64_t)hk * c_sh;
   const bf16_t* vb0 = vc + (int64_t)b * c_sb + (int64_t)hk * c_sh + dl;
-  // ---- all loads up front (keys clamped into [k0, k1): unconditional, masked later)
+  // ---- all loads up front (keys clamped into [k0, k1): unconditional, masked later). The bulk
+  // K / V loads go out before anything that waits on memory: the newest key's rotated K / raw V
+  // (a dependent chain through pos -> cos / sin) replace their registers only afterwards.
   s16x8 kf[2][KST];
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
-    const int key = kw0 + 16 * t + r16;
-    const int kcl = min(max(key, k0), k1 - 1);
+    const int kcl = min(max(kw0 + 16 * t + r16, k0), k1 - 1);
 #pragma unroll
     for (int s = 0; s < KST; ++s)
       kf[t][s] = __builtin_bit_cast(s16x8, load_bf16x8(kb0 + (int64_t)kcl * c_st + 32 * s + 8 * kg));
-    if constexpr (ROPE) {
-      if (key == newest) {
-#pragma unroll
-        for (int s = 0; s < KST; ++s)
-          kf[t][s] = __builtin_bit_cast(s16x8, dec_rope8(qrow + (int64_t)(Hq + hk) * D, 32 * s + 8 * kg, rp.rot, cs, sn));
-      }
-    }
   }
   bf16x8 vvr[NIT];
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
     const int key = min(max(kw0 + it * KPI + sub, k0), k1 - 1);
     vvr[it] = load_bf16x8(vb0 + (int64_t)key * c_st);
-    if constexpr (ROPE) {
-      if (key == newest) vvr[it] = vnew;
+  }
+  if constexpr (ROPE) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      if (min(max(kw0 + 16 * t + r16, k0), k1 - 1) == newest) {
+#pragma unroll
+        for (int s = 0; s < KST; ++s)
+          kf[t][s] = __builtin_bit_cast(s16x8, dec_rope8(qrow + (int64_t)(Hq + hk) * D, 32 * s + 8 * kg, rp.rot, cs, sn));
+      }
     }
+#pragma unroll
+    for (int it = 0; it < NIT; ++it)
+      if (min(max(kw0 + it * KPI + sub, k0), k1 - 1) == newest) vvr[it] = vnew;
   }
   s16x8 qf[KST];
 #pragma unroll
