@@ -492,7 +492,15 @@ static void launch_ks(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw
                       int64_t ldy, int M, int N, int K, int nb, hipStream_t st) {
   // M <= 16: a 2-deep ring (84 VGPRs: 5-6 waves per SIMD, every qkv block resident in one round);
   // a 4-deep ring (152 VGPRs) measured slower at qkv (16.0 vs 14.8 us in a decode step)
-  if (M <= 16)
+  // long K (the 14336-deep down projection: 14 ring slots per wave, one workgroup per CU) keeps
+  // a 4-deep ring in flight (DLA_SKINNY_DEEP_K, default 8192: K at or above it)
+  static const int deep_k = [] {
+    const char* e = getenv("DLA_SKINNY_DEEP_K");
+    return e ? atoi(e) : 8192;
+  }();
+  if (M <= 16 && !GLU && K >= deep_k)
+    skinny_ksplit_kernel<4, NT, GLU, 1><<<nb, 512, 0, st>>>(x, ldx, W, ldw, y, ldy, M, N, K);
+  else if (M <= 16)
     skinny_ksplit_kernel<2, NT, GLU, 1><<<nb, 512, 0, st>>>(x, ldx, W, ldw, y, ldy, M, N, K);
   else if (M <= 32)
     skinny_ksplit_kernel<2, NT, GLU, 2, 2><<<nb, 512, 0, st>>>(x, ldx, W, ldw, y, ldy, M, N, K);
