@@ -76,7 +76,9 @@ class ExpertParallel:
         inv = torch.empty_like(perm)
         inv[perm] = torch.arange(perm.numel(), device=dev)
         xe = xr.index_select(0, perm)
-        counts_local = recv.view(ep, El).sum(0)  # device: the grouped expert GEMM reads it there
+        # per-local-expert row counts from the host copy this layer already synced (the expert
+        # GEMM, grouped or per-expert loop, then needs no further host round trip)
+        counts_local = [sum(rc[s * El + e] for s in range(ep)) for e in range(El)]
         ye = ops.moe.experts_swiglu(xe, moe.expert_up, moe.expert_down, counts_local, fp8=moe.fp8)
         yr = ye.index_select(0, inv)
         ys = all_to_all(yr, send_splits, recv_splits, self.group)

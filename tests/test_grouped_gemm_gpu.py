@@ -174,9 +174,13 @@ def test_moe_layer_grouped_matches_loop_and_captures():
     moe = m.layers[0].mlp
     g = torch.Generator(device=DEV).manual_seed(5)
     h = _rand(4, 200, cfg.hidden_size, g=g).requires_grad_(True)
-    out = moe(h)
-    go = _rand(*out.shape, g=g)
-    grads = torch.autograd.grad(out, [h, moe.router, moe.expert_up, moe.expert_down], go)
+    os.environ["DLA_MOE_GEMM"] = "grouped"  # auto would take the loop for bf16 training
+    try:
+        out = moe(h)
+        go = _rand(*out.shape, g=g)
+        grads = torch.autograd.grad(out, [h, moe.router, moe.expert_up, moe.expert_down], go)
+    finally:
+        os.environ.pop("DLA_MOE_GEMM")
     os.environ["DLA_MOE_GEMM"] = "loop"
     try:
         out_l = moe(h)

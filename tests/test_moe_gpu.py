@@ -110,11 +110,14 @@ def test_fp8_rowwise_quant_kernel_and_moe_layer():
     assert (out - ref).norm() / ref.norm() < 0.08
 
 
+@pytest.mark.parametrize("gemm", ["grouped", "auto"])
 @pytest.mark.parametrize("policy", ["full", "mlp"])
-def test_moe_recompute_keeps_expert_grads(policy):
-    """Expert weights accumulate into the engine's main_grad from the grouped-GEMM autograd node;
-    under activation recompute (whole layer or MLP block) that node must still see the real
-    parameters (weights ride on ctx): one DPO step's gradients equal the no-recompute step's."""
+def test_moe_recompute_keeps_expert_grads(policy, gemm, monkeypatch):
+    """Expert weights accumulate into the engine's main_grad from the expert autograd node
+    (grouped GEMM, or the per-expert loop that `auto` takes for bf16 training); under activation
+    recompute (whole layer or MLP block) that node must still see the real parameters (weights
+    ride on ctx): one DPO step's gradients equal the no-recompute step's."""
+    monkeypatch.setenv("DLA_MOE_GEMM", gemm)
     from distributed_llm_alignment_amd.data.synthetic import synthetic_preference_batch
     from distributed_llm_alignment_amd.models import build_model, get_config
     from distributed_llm_alignment_amd.objectives import dpo_step_loss
