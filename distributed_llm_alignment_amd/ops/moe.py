@@ -218,39 +218,45 @@ class _ExpertsFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dys):
         xs, gu = ctx.saved_tensors
-        w_up, w_down = ctx.w_up, ctx.w_down
-        dys = dys.contiguous()
-        need_x = ctx.needs_input_grad[0]
-        dxs = torch.zeros_like(xs) if need_x else None
-        mg_up = getattr(w_up, "main_grad", None)
-        mg_down = getattr(w_down, "main_grad", None)
-        g_up = mg_up if mg_up is not None else (torch.zeros_like(w_up) if ctx.needs_input_grad[1] else None)
-        g_down = mg_down if mg_down is not None else (torch.zeros_like(w_down) if ctx.needs_input_grad[2] else None)
-        s = 0
-        for e, c in enumerate(ctx.counts):
-            if c:
-                dy = dys[s:s + c]
-                g = gu[s:s + c]
-                a = swiglu(g)
-                da = dy @ w_down[e]
-                if g_down is not None:
-                    addmm_into(g_down[e], dy.t(), a)
-                dg = _swiglu_bwd(g, da)
-                if need_x:
-                    torch.mm(dg, w_up[e], out=dxs[s:s + c])
-                if g_up is not None:
-                    addmm_into(g_up[e], dg.t(), xs[s:s + c])
-            s += c
-        outs = []
-        for w, g, mg in ((w_up, g_up, mg_up), (w_down, g_down, mg_down)):
-            if mg is not None:
-                hook = getattr(w, "_dla_grad_hook", None)
-                if hook is not None:
-                    hook(w)
-                outs.append(None)
-            else:
-                outs.append(g)
-        return dxs, outs[0], outs[1], None, None
+        return _loop_experts_backward(dys, xs, gu, ctx.w_up, ctx.w_down, ctx.counts,
+                                      ctx.needs_input_grad) + (None, None)
+
+
+def _loop_experts_backward(dys, xs, gu, w_up, w_down, counts, needs):
+    """Per-expert hipBLASLt backward of the SwiGLU experts (host counts): (dxs, d_up, d_down),
+    weight grads accumulated into main_grad where the engine attached one."""
+    dys = dys.contiguous()
+    need_x = needs[0]
+    dxs = torch.zeros_like(xs) if need_x else None
+    mg_up = getattr(w_up, "main_grad", None)
+    mg_down = getattr(w_down, "main_grad", None)
+    g_up = mg_up if mg_up is not None else (torch.zeros_like(w_up) if needs[1] else None)
+    g_down = mg_down if mg_down is not None else (torch.zeros_like(w_down) if needs[2] else None)
+    s = 0
+    for e, c in enumerate(counts):
+        if c:
+            dy = dys[s:s + c]
+            g = gu[s:s + c]
+            a = swiglu(g)
+            da = dy @ w_down[e]
+            if g_down is not None:
+                addmm_into(g_down[e], dy.t(), a)
+            dg = _swiglu_bwd(g, da)
+            if need_x:
+                torch.mm(dg, w_up[e], out=dxs[s:s + c])
+            if g_up is not None:
+                addmm_into(g_up[e], dg.t(), xs[s:s + c])
+        s += c
+    outs = []
+    for w, g, mg in ((w_up, g_up, mg_up), (w_down, g_down, mg_down)):
+        if mg is not None:
+            hook = getattr(w, "_dla_grad_hook", None)
+            if hook is not None:
+                hook(w)
+            outs.append(None)
+        else:
+            outs.append(g)
+    return dxs, outs[0], outs[1]
 
 
 class _GroupedExpertsFn(torch.autograd.Function):
@@ -277,6 +283,13 @@ class _GroupedExpertsFn(torch.autograd.Function):
     def backward(ctx, dys):
         xs, gu, offs = ctx.saved_tensors
         w_up, w_down = ctx.w_up, ctx.w_down
+        if _loop_backward_ok():
+            # fp8 forward on the grouped kernel, bf16 backward on the per-expert hipBLASLt loop
+            # (faster there; one host read of the offsets, outside any capture)
+            o = offs.tolist()
+            counts = [o[e + 1] - o[e] for e in range(len(o) - 1)]
+            return _loop_experts_backward(dys, xs, gu, w_up, w_down, counts,
+                                          ctx.needs_input_grad) + (None, None)
         C = _ext.require()
         dys = dys.contiguous()
         # da = dy . W_down fused with the SwiGLU backward -> dgu, plus the recomputed a
@@ -304,6 +317,13 @@ class _GroupedExpertsFn(torch.autograd.Function):
 def grouped_gemm_enabled() -> bool:
     """The grouped GEMM may be used (the condition for a host-sync-free, capturable MoE layer)."""
     return os.environ.get("DLA_MOE_GEMM", "auto") != "loop"
+
+
+def _loop_backward_ok() -> bool:
+    """auto: the grouped node's backward (fp8-forward experts under autograd) runs the per-expert
+    loop (DLA_MOE_BWD=grouped keeps the grouped dgrad / wgrad kernels)."""
+    return (os.environ.get("DLA_MOE_GEMM", "auto") == "auto" and os.environ.get("DLA_MOE_BWD", "auto") != "grouped"
+            and not torch.cuda.is_current_stream_capturing())
 
 
 def _use_grouped(fp8: bool) -> bool:
