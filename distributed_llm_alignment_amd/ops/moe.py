@@ -326,11 +326,19 @@ def _loop_backward_ok() -> bool:
             and not torch.cuda.is_current_stream_capturing())
 
 
-def _use_grouped(fp8: bool) -> bool:
+# auto: below this many expert rows a no-grad call (decode steps, eager or captured) stays on the
+# grouped GEMM, so eager and hipGraph decoding run the same kernels; larger no-grad calls (the
+# frozen reference forward, prefill) take the loop like training
+MOE_LOOP_MIN_ROWS = int(os.environ.get("DLA_MOE_LOOP_MIN_ROWS", "1024"))
+
+
+def _use_grouped(fp8: bool, rows: int = 0) -> bool:
     mode = os.environ.get("DLA_MOE_GEMM", "auto")
     if mode != "auto":
         return mode != "loop"
-    return fp8 or not torch.is_grad_enabled() or torch.cuda.is_current_stream_capturing()
+    if fp8 or torch.cuda.is_current_stream_capturing():
+        return True
+    return not torch.is_grad_enabled() and rows < MOE_LOOP_MIN_ROWS
 
 
 def _grouped_ok(xs, w_up, w_down) -> bool:
@@ -358,7 +366,7 @@ def experts_swiglu(xs: torch.Tensor, w_up: torch.Tensor, w_down: torch.Tensor,
     if fp8 and not (xs.is_cuda and _FP8 is not None):
         fp8 = False
     xs = xs.contiguous()
-    if _grouped_ok(xs, w_up, w_down) and _use_grouped(fp8):
+    if _grouped_ok(xs, w_up, w_down) and _use_grouped(fp8, xs.shape[0]):
         if isinstance(counts, torch.Tensor):
             offs = expert_offsets(counts.to(xs.device))
         else:
