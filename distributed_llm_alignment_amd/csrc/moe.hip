@@ -12,6 +12,8 @@
 //   combine_bwd: dys[pos[t,j]] = w[t,j] * dout[t],  dw[t,j] = <dout[t], ys[pos[t,j]]>
 // Router: the renormalised top-k softmax equals a softmax over the selected logits, so the
 // forward needs one pass over E logits per token and the backward touches only k of them.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace dla {
@@ -181,10 +183,71 @@ __global__ __launch_bounds__(256) void quant_fp8_rows_kernel(const bf16_t* __res
   }
 }
 
+// Single-pass form for rows of <= 256 * 8 * NV elements: the row stays in registers between the
+// amax reduction and the conversion (the two-pass kernel above re-reads it), all NV loads of a
+// thread in flight at once. Same arithmetic and reduction, so the same bits.
+template <int NV>
+__global__ __launch_bounds__(256) void quant_fp8_rows_reg_kernel(const bf16_t* __restrict__ x,
+                                                                 int64_t ld, int K,
+                                                                 uint8_t* __restrict__ q,
+                                                                 float* __restrict__ inv) {
+  __shared__ float red[4];
+  const int64_t r = blockIdx.x;
+  const bf16_t* row = x + r * ld;
+  const int nv = K / 8;
+  bf16x8 a[NV];
+#pragma unroll
+  for (int u = 0; u < NV; ++u) {
+    const int i = threadIdx.x + u * 256;
+    if (i < nv) a[u] = load_bf16x8(row + i * 8);
+  }
+  float m = 0.f;
+#pragma unroll
+  for (int u = 0; u < NV; ++u) {
+    const int i = threadIdx.x + u * 256;
+    if (i < nv) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(bf2f(a[u][j])));
+    }
+  }
+  m = block_max<256>(m, red);
+  const float amax = fmaxf(m, 1e-12f);
+  const float sc = 448.f / amax;
+  if (threadIdx.x == 0) inv[r] = amax / 448.f;
+  uint8_t* qrow = q + r * (int64_t)K;
+#pragma unroll
+  for (int u = 0; u < NV; ++u) {
+    const int i = threadIdx.x + u * 256;
+    if (i < nv) {
+      uint32_t lo = 0, hi = 0;
+      lo = __builtin_amdgcn_cvt_pk_fp8_f32(bf2f(a[u][0]) * sc, bf2f(a[u][1]) * sc, lo, false);
+      lo = __builtin_amdgcn_cvt_pk_fp8_f32(bf2f(a[u][2]) * sc, bf2f(a[u][3]) * sc, lo, true);
+      hi = __builtin_amdgcn_cvt_pk_fp8_f32(bf2f(a[u][4]) * sc, bf2f(a[u][5]) * sc, hi, false);
+      hi = __builtin_amdgcn_cvt_pk_fp8_f32(bf2f(a[u][6]) * sc, bf2f(a[u][7]) * sc, hi, true);
+      *reinterpret_cast<uint2*>(qrow + i * 8) = make_uint2(lo, hi);
+    }
+  }
+}
+
 void launch_quant_fp8_rows(const bf16_t* x, int64_t ld, int64_t rows, int K, uint8_t* q, float* inv,
                            hipStream_t st) {
   if (rows == 0) return;
-  quant_fp8_rows_kernel<<<rows, 256, 0, st>>>(x, ld, K, q, inv);
+  // DLA_FP8_QUANT_2PASS=1: the two-pass kernel (A/B)
+  static const bool two_pass = [] {
+    const char* e = getenv("DLA_FP8_QUANT_2PASS");
+    return e != nullptr && e[0] == '1';
+  }();
+  const int nv = K / 8;
+  if (!two_pass && nv <= 256)
+    quant_fp8_rows_reg_kernel<1><<<rows, 256, 0, st>>>(x, ld, K, q, inv);
+  else if (!two_pass && nv <= 512)
+    quant_fp8_rows_reg_kernel<2><<<rows, 256, 0, st>>>(x, ld, K, q, inv);
+  else if (!two_pass && nv <= 1024)
+    quant_fp8_rows_reg_kernel<4><<<rows, 256, 0, st>>>(x, ld, K, q, inv);
+  else if (!two_pass && nv <= 2048)
+    quant_fp8_rows_reg_kernel<8><<<rows, 256, 0, st>>>(x, ld, K, q, inv);
+  else
+    quant_fp8_rows_kernel<<<rows, 256, 0, st>>>(x, ld, K, q, inv);
 }
 
 // ----------------------------------------------------------------------------------------------

@@ -162,3 +162,21 @@ def test_moe_fp8_hybrid_backward_matches_grouped(monkeypatch):
             t.float() for t in torch.autograd.grad(out, [h, moe.expert_up, moe.expert_down], go))
     for a, b in zip(res["auto"], res["grouped"]):
         assert (a - b).norm() / b.norm().clamp(min=1e-6) < 2e-2
+
+
+@pytest.mark.parametrize("K", [1024, 4096, 14336, 20480])
+def test_fp8_row_quant_matches_torch_conversion(K):
+    """Row-wise e4m3 quantiser (single-pass register form up to K = 16384, two-pass above):
+    scale = amax / 448, codes equal torch's float8_e4m3fn conversion of x * 448 / amax (up to
+    the last bits of the kernel's scale and the hardware conversion: ~0.2 % of codes one step away)."""
+    from distributed_llm_alignment_amd import ops
+
+    g = torch.Generator(device=DEV).manual_seed(K)
+    x = (torch.randn(67, K, device=DEV, generator=g) * 2).to(torch.bfloat16)
+    q, inv = ops.moe.quant_fp8_rows(x)
+    amax = x.float().abs().amax(1, keepdim=True).clamp(min=1e-12)
+    assert torch.allclose(inv, amax / 448.0, rtol=1e-6, atol=0)
+    ref = (x.float() * (448.0 / amax)).to(torch.float8_e4m3fn)
+    a, b = q.view(torch.uint8).int(), ref.view(torch.uint8).int()
+    diff = (a - b).abs()
+    assert int(diff.max()) <= 1 and float((diff > 0).float().mean()) < 1e-2
