@@ -222,10 +222,42 @@ class _ExpertsFn(torch.autograd.Function):
                                       ctx.needs_input_grad) + (None, None)
 
 
+# The per-expert input-gradient GEMMs dA = dY W are NN-layout; hipBLASLt's default heuristic
+# (used for these routing-dependent row counts, which no TunableOp table can list) picks a
+# depth-32 tile for them. They run in the forward's TN layout through a transposed expert-weight
+# copy made once per optimizer step by the HIP tiled transpose (HBM cost: one more copy of the
+# expert weights). Mixtral 2-layer DPO, same box, two rounds: bf16 60.2-60.6 vs 59.6-59.8 pairs/s,
+# fp8 forward 67.3-67.7 vs 66.9-67.0 (a torch strided transpose-copy instead lost 2-3 %).
+# DLA_MOE_TRANSPOSED_DGRAD=0 keeps the NN layout.
+MOE_TRANSPOSED_DGRAD = os.environ.get("DLA_MOE_TRANSPOSED_DGRAD", "1") != "0"
+
+
+def transposed_experts(w: torch.Tensor) -> torch.Tensor:
+    """Cached [E, K, N] copy of expert weights [E, N, K], re-made when the weight's version
+    counter or its engine's weight epoch moved (once per optimizer step)."""
+    ep = getattr(w, "_dla_epoch", None)
+    key = (w._version, ep[0] if ep is not None else 0)
+    c = getattr(w, "_dla_wT", None)
+    if c is None or c[0] != key:
+        with torch.no_grad():
+            t = c[1] if c is not None else torch.empty((w.shape[0], w.shape[2], w.shape[1]),
+                                                         dtype=w.dtype, device=w.device)
+            tr = _ext.require().transpose_bf16
+            for e in range(w.shape[0]):
+                tr(w.detach()[e], t[e])
+        c = (key, t)
+        w._dla_wT = c
+    return c[1]
+
+
 def _loop_experts_backward(dys, xs, gu, w_up, w_down, counts, needs):
     """Per-expert hipBLASLt backward of the SwiGLU experts (host counts): (dxs, d_up, d_down),
     weight grads accumulated into main_grad where the engine attached one."""
     dys = dys.contiguous()
+    tdg = (MOE_TRANSPOSED_DGRAD and _ext.use_native(dys) and w_up.dtype == torch.bfloat16
+           and w_up.shape[1] % 8 == 0 and w_up.shape[2] % 8 == 0)
+    wdT = transposed_experts(w_down) if tdg else None  # [E, F, H]
+    wuT = transposed_experts(w_up) if tdg and needs[0] else None  # [E, H, 2F]
     need_x = needs[0]
     dxs = torch.zeros_like(xs) if need_x else None
     mg_up = getattr(w_up, "main_grad", None)
@@ -238,12 +270,12 @@ def _loop_experts_backward(dys, xs, gu, w_up, w_down, counts, needs):
             dy = dys[s:s + c]
             g = gu[s:s + c]
             a = swiglu(g)
-            da = dy @ w_down[e]
+            da = F.linear(dy, wdT[e]) if tdg else dy @ w_down[e]
             if g_down is not None:
                 addmm_into(g_down[e], dy.t(), a)
             dg = _swiglu_bwd(g, da)
             if need_x:
-                torch.mm(dg, w_up[e], out=dxs[s:s + c])
+                torch.mm(dg, wuT[e].t() if tdg else w_up[e], out=dxs[s:s + c])
             if g_up is not None:
                 addmm_into(g_up[e], dg.t(), xs[s:s + c])
         s += c

@@ -1,10 +1,11 @@
 #!/bin/bash
-# MoE per-expert backward: input-gradient GEMMs through transposed expert weights (TN) vs NN.
+# MoE per-expert backward: input-gradient GEMMs through transposed expert weights (TN, copy by
+# the HIP tiled transpose once per step) vs the NN layout.
 set -o pipefail
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest tests/test_moe_gpu.py tests/test_grouped_gemm_gpu.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/moe_tests4.log 2>&1 || { tail -40 gpurun_out/moe_tests4.log; exit 1; }
-tail -1 gpurun_out/moe_tests4.log
+DLA_MOE_TRANSPOSED_DGRAD=1 timeout -k 10 400 python -u -m pytest tests/test_moe_gpu.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/moe_tests5.log 2>&1 || { tail -40 gpurun_out/moe_tests5.log; exit 1; }
+tail -1 gpurun_out/moe_tests5.log
 run() {  # label, env, args...
   local lab=$1; shift
   env $1 timeout -k 10 400 python -u bench.py --model mixtral-8x7b --layers 2 --steps 4 --warmup 2 ${@:2} > gpurun_out/mix_$lab.log 2>&1 || { tail -20 gpurun_out/mix_$lab.log; exit 1; }
