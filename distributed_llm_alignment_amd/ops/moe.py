@@ -254,7 +254,11 @@ def _loop_experts_backward(dys, xs, gu, w_up, w_down, counts, needs):
     """Per-expert hipBLASLt backward of the SwiGLU experts (host counts): (dxs, d_up, d_down),
     weight grads accumulated into main_grad where the engine attached one."""
     dys = dys.contiguous()
+    # only for weights whose updates the flat-buffer engine announces through its weight epoch
+    # (in-place kernel updates move no version counter; FSDP re-gathers storage): as ops.linear
     tdg = (MOE_TRANSPOSED_DGRAD and _ext.use_native(dys) and w_up.dtype == torch.bfloat16
+           and getattr(w_up, "_dla_epoch", None) is not None
+           and getattr(w_down, "_dla_epoch", None) is not None
            and w_up.shape[1] % 8 == 0 and w_up.shape[2] % 8 == 0)
     wdT = transposed_experts(w_down) if tdg else None  # [E, F, H]
     wuT = transposed_experts(w_up) if tdg and needs[0] else None  # [E, H, 2F]

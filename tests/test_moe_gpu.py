@@ -180,3 +180,35 @@ def test_fp8_row_quant_matches_torch_conversion(K):
     a, b = q.view(torch.uint8).int(), ref.view(torch.uint8).int()
     diff = (a - b).abs()
     assert int(diff.max()) <= 1 and float((diff > 0).float().mean()) < 1e-2
+
+
+def test_moe_transposed_dgrad_matches_nn_and_follows_steps(monkeypatch):
+    """Per-expert backward through the cached transposed expert weights (TN input-gradient GEMMs)
+    equals the NN-layout backward, also after the weights changed (the copy is re-made)."""
+    from distributed_llm_alignment_amd import ops
+    from distributed_llm_alignment_amd.models import build_model, get_config
+    from distributed_llm_alignment_amd.parallel.data_parallel import DataParallelEngine
+
+    monkeypatch.setenv("DLA_MOE_GEMM", "loop")
+    cfg = get_config("tiny-mixtral", hidden_size=256, intermediate_size=512, num_experts=8)
+    m = build_model(cfg, device=DEV, dtype=torch.bfloat16, seed=6)
+    eng = DataParallelEngine(m, lr=1e-2, weight_decay=0.0, max_grad_norm=1.0)
+    moe = m.layers[0].mlp
+    g = torch.Generator(device=DEV).manual_seed(2)
+    h = torch.randn(2, 150, cfg.hidden_size, device=DEV, generator=g).to(torch.bfloat16)
+    go = torch.randn(2, 150, cfg.hidden_size, device=DEV, generator=g).to(torch.bfloat16)
+    for step in range(2):
+        res = {}
+        for tn in (True, False):
+            monkeypatch.setattr(ops.moe, "MOE_TRANSPOSED_DGRAD", tn)
+            for p in (moe.expert_up, moe.expert_down):
+                p.main_grad.zero_()
+            x = h.clone().requires_grad_(True)
+            moe(x).backward(go)
+            res[tn] = [x.grad.float()] + [p.main_grad.float().clone() for p in (moe.expert_up, moe.expert_down)]
+        for a, b in zip(res[True], res[False]):
+            assert (a - b).norm() / b.norm().clamp(min=1e-6) < 1e-2, step
+        with torch.no_grad():  # new weights: the cached transposes must follow
+            moe.expert_up.mul_(1.25)
+            moe.expert_down.mul_(0.8)
+    assert eng is not None
