@@ -13,10 +13,11 @@ with boolean masks, `index_add_` and a fresh weight-gradient tensor per expert. 
     epilogue and the SwiGLU backward into the down projection's input-gradient epilogue, and
     weight gradients accumulate straight into the engine's grad buffer (`main_grad`, bf16 or
     fp32). `DLA_MOE_GEMM=loop|grouped` forces the per-expert hipBLASLt loop (host counts) or the
-    grouped GEMM; the default `auto` takes the loop only for bf16 experts with autograd recording
-    outside a hipGraph capture (training fwd+bwd: the loop's hipBLASLt tiles are faster there, 59.1
-    vs 55.1 pairs/s on the Mixtral 2-layer DPO bench, same box) and the grouped GEMM everywhere else
-    (inference / decode, captures, fp8: 63.6 vs 63.3);
+    grouped GEMM; the default `auto` takes the loop for bf16 experts outside a hipGraph capture
+    when autograd records or the call has >= 1024 rows (training fwd+bwd, the frozen reference
+    forward, prefill: the loop's hipBLASLt tiles are faster there, 59.5 vs 55.4 pairs/s on the
+    Mixtral 2-layer DPO bench, same box), and the grouped GEMM for decode-sized calls, captures and
+    the fp8 forward, whose backward then runs on the per-expert loop (67.4-67.7 vs 64.1-64.5);
   * optional fp8 (e4m3, row-wise scales) forward GEMMs (`fp8=True`) on the block-scaled
     16x16x128 MFMA, bf16 backward.
 CPU (and non-bf16) inputs use the PyTorch reference path with identical semantics.
