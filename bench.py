@@ -72,11 +72,56 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
+def _visible_list(n_phys: int):
+    """Apply ROCR/HIP/CUDA_VISIBLE_DEVICES (innermost wins the count) to n_phys devices."""
+    n = n_phys
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip() != ""]))
+    return n
+
+
+def visible_gpu_count() -> int:
+    """GPUs this process could use, WITHOUT initialising HIP in this process (the launcher later
+    forks/execs torchrun, which must never happen from a HIP-initialised process): KFD topology
+    nodes with SIMDs whose DRM render node exists and is accessible here, narrowed by the
+    *_VISIBLE_DEVICES variables. If sysfs cannot be read, a throw-away child process counts."""
+    root = "/sys/class/kfd/kfd/topology/nodes"
+    try:
+        nodes = os.listdir(root)
+    except OSError:
+        nodes = None
+    if nodes is not None:
+        n = 0
+        for nd in nodes:
+            try:
+                with open(os.path.join(root, nd, "properties")) as fh:
+                    props = dict(ln.split(None, 1) for ln in fh.read().splitlines() if " " in ln)
+            except OSError:
+                continue
+            if int(props.get("simd_count", "0")) <= 0:
+                continue  # CPU node
+            minor = props.get("drm_render_minor", "").strip()
+            dev = f"/dev/dri/renderD{minor}"
+            if minor and os.path.exists(dev) and os.access(dev, os.R_OK | os.W_OK):
+                n += 1
+        return _visible_list(n)
+    code = "import torch; print(torch.cuda.device_count())"
+    try:
+        out = subprocess.run([sys.executable, "-c", code], stdout=subprocess.PIPE,
+                             stderr=subprocess.DEVNULL, text=True, timeout=300)
+        return int(out.stdout.strip().splitlines()[-1])
+    except Exception:
+        return 0
+
+
 def launch_ranks(args, argv) -> int:
-    """Parent-side launcher for `--gpus N` without torchrun. Touches no GPU: device_count()
-    does not initialise HIP on this image, and the ranks run in a child process tree."""
+    """Parent-side launcher for `--gpus N` without torchrun. Touches no GPU (device count from
+    sysfs or a child process), and the ranks run in a child process tree: torchrun tears every
+    rank down as soon as one exits non-zero, and its exit code is returned."""
     if args.device != "cpu":
-        n_dev = torch.cuda.device_count()
+        n_dev = visible_gpu_count()
         if args.gpus > n_dev:
             print(f"bench.py: --gpus {args.gpus} but only {n_dev} GPU(s) visible; refusing to "
                   f"run fewer ranks than requested", file=sys.stderr, flush=True)
@@ -88,6 +133,44 @@ def launch_ranks(args, argv) -> int:
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     env.setdefault("OMP_NUM_THREADS", "4")
     return subprocess.call(cmd, env=env)
+
+
+def preflight(st, dev) -> None:
+    """Per-rank first-contact check before anything is timed (stderr, one line per rank): rank,
+    device, RCCL version, world, and a 16 MB all-reduce of known values verified element-wise.
+    A wrong sum or a hang (collective timeout) ends the run before the benchmark starts."""
+    import torch.distributed as dist
+
+    name = torch.cuda.get_device_name(dev) if dev.type == "cuda" else "cpu"
+    try:
+        rccl = ".".join(map(str, torch.cuda.nccl.version())) if dev.type == "cuda" else "-"
+    except Exception:  # pragma: no cover - version query unsupported
+        rccl = "?"
+    n = 4 * 1024 * 1024  # 16 MB of fp32
+    x = torch.full((n,), float(st.rank + 1), dtype=torch.float32, device=dev)
+    t0 = time.perf_counter()
+    if st.initialized:
+        dist.all_reduce(x)
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    want = st.world_size * (st.world_size + 1) / 2
+    ok = bool(torch.all(x == want).item())
+    sys.stderr.write(f"[preflight] rank {st.rank}/{st.world_size} local {st.local_rank} device {dev} "
+                     f"({name}) backend {st.backend or 'single-process'} rccl {rccl} all_reduce16MB "
+                     f"{'ok' if ok else 'WRONG'} {dt * 1e3:.1f} ms\n")  # one write: no interleaving
+    sys.stderr.flush()
+    if not ok:
+        raise SystemExit(f"bench.py: preflight all-reduce returned wrong values on rank {st.rank}")
+
+
+def _maybe_fail(step: int, rank: int) -> None:
+    """Fault injection for the launcher test: DLA_BENCH_FAIL_RANK / DLA_BENCH_FAIL_STEP make that
+    rank die abruptly (no cleanup) at that step; the whole command must still exit non-zero."""
+    r = os.environ.get("DLA_BENCH_FAIL_RANK")
+    if r is not None and int(r) == rank and step == int(os.environ.get("DLA_BENCH_FAIL_STEP", "0")):
+        print(f"bench.py: injected failure on rank {rank} at step {step}", file=sys.stderr, flush=True)
+        os._exit(17)
 
 
 def main(argv=None) -> int:
@@ -112,7 +195,9 @@ def main(argv=None) -> int:
 
     from distributed_llm_alignment_amd.utils.tuning import enable_gemm_tuning
 
-    st = init_distributed(device="cpu" if args.device == "cpu" else None)
+    # a dead peer must end the run in bounded time, not after the 30 min default
+    st = init_distributed(device="cpu" if args.device == "cpu" else None,
+                          timeout_s=int(os.environ.get("DLA_BENCH_COLLECTIVE_TIMEOUT_S", "300")))
     dev = st.device
     if st.world_size != args.gpus:
         raise SystemExit(f"bench.py: running {st.world_size} rank(s) for --gpus {args.gpus}")
@@ -130,6 +215,8 @@ def main(argv=None) -> int:
     if dev.type == "cuda":
         _ext.require()
         gemm_mode = enable_gemm_tuning(dev.index)
+    if st.world_size > 1 or os.environ.get("DLA_BENCH_PREFLIGHT") == "1":
+        preflight(st, dev)
     world = st.world_size
     mesh = build_mesh(tp=args.tp, ep=args.ep, sp=args.sp)
     overrides = {} if args.layers is None else {"num_layers": args.layers}
@@ -178,7 +265,7 @@ def main(argv=None) -> int:
     n_batches = 4
     batches = [synthetic_preference_batch(args.micro_pairs, args.seq_len, cfg.vocab_size, device=dev,
                                           generator=gen) for _ in range(n_batches)]
-    state = {"i": 0, "loss": None}
+    state = {"i": 0, "loss": None, "step": 0}
 
     # only when the ref forward issues no collectives (TP / EP / ZeRO-3 gathers would race the
     # policy's on the same communicators from two streams)
@@ -189,6 +276,8 @@ def main(argv=None) -> int:
     def train_step():
         # the ref pass of micro-batch a+1 is queued on its own stream before micro-batch a's
         # backward, so it runs alongside the policy backward
+        _maybe_fail(state["step"], st.rank)
+        state["step"] += 1
         pending = refs.submit(batches[state["i"] % n_batches])
         for a in range(args.accum):
             b = batches[state["i"] % n_batches]
@@ -290,6 +379,11 @@ def main(argv=None) -> int:
             },
         }
         print(json.dumps(rec), flush=True)
+    if st.initialized:  # orderly teardown: no communicator threads left running at exit
+        barrier()
+        from distributed_llm_alignment_amd.parallel.dist import destroy
+
+        destroy()
     return 0
 
 

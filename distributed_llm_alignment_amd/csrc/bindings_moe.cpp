@@ -20,9 +20,9 @@ void launch_moe_combine_bwd(const bf16_t*, const bf16_t*, const int*, const floa
                             int, bf16_t*, float*, hipStream_t);
 
 void launch_quant_fp8_rows(const bf16_t*, int64_t, int64_t, int, uint8_t*, float*, hipStream_t);
-void launch_embed_fwd(const bf16_t*, int64_t, const int64_t*, int64_t, int, int64_t, bf16_t*, hipStream_t);
-void launch_embed_bwd(const int64_t*, const int64_t*, const bf16_t*, int64_t, int, float*, void*, bool,
-                      int64_t, hipStream_t);
+void launch_embed_fwd(const bf16_t*, int64_t, const int64_t*, int64_t, int, int64_t, bf16_t*, int*, hipStream_t);
+void launch_embed_bwd(const int64_t*, const int64_t*, const bf16_t*, int64_t, int, int64_t, float*, void*,
+                      bool, int64_t, hipStream_t);
 
 static RHParams rh_params(const at::Tensor& hidden, const c10::optional<at::Tensor>& last,
                           const c10::optional<at::Tensor>& mask, const at::Tensor& w,
@@ -98,10 +98,14 @@ at::Tensor reward_head_bwd(const at::Tensor& dscore, const at::Tensor& hidden,
   return dh;
 }
 
-// token embedding gather: out[n] = w[ids[n]] (ids int64 [N], w [V, H] bf16)
-at::Tensor embed_fwd(const at::Tensor& w, const at::Tensor& ids) {
+// token embedding gather: out[n] = w[ids[n]] (ids int64 [N], w [V, H] bf16). An id outside
+// [0, V) gives a zero row and sets bad[0] = 1 (int32 [1], sticky, checked by the caller at its
+// next host sync): no device assert, no host sync here.
+at::Tensor embed_fwd(const at::Tensor& w, const at::Tensor& ids, at::Tensor bad) {
   check_bf16(w, "w");
   check_cuda(ids, "ids");
+  check_i32(bad, "bad");
+  TORCH_CHECK(bad.numel() >= 1 && bad.device() == w.device(), "bad: int32 [1] on the table's device");
   TORCH_CHECK(ids.scalar_type() == at::kLong && ids.dim() == 1 && ids.is_contiguous(), "ids int64 [N]");
   TORCH_CHECK(w.dim() == 2 && w.stride(1) == 1 && w.stride(0) % 8 == 0 && w.size(1) % 8 == 0,
               "w [V, H], H % 8 == 0, 16-byte aligned rows");
@@ -109,7 +113,7 @@ at::Tensor embed_fwd(const at::Tensor& w, const at::Tensor& ids) {
   c10::hip::HIPGuardMasqueradingAsCUDA g(w.device());
   auto out = at::empty({ids.size(0), w.size(1)}, w.options());
   launch_embed_fwd(cbp(w), w.stride(0), ids.data_ptr<int64_t>(), ids.size(0), (int)w.size(1),
-                   w.size(0), bp(out), cur_stream(w));
+                   w.size(0), bp(out), bad.data_ptr<int>(), cur_stream(w));
   return out;
 }
 
@@ -134,7 +138,7 @@ void embed_bwd(const at::Tensor& sid, const at::Tensor& perm, const at::Tensor& 
   const int64_t N = sid.size(0);
   auto scratch = at::empty({N, dy.size(1)}, dy.options().dtype(at::kFloat));
   launch_embed_bwd(sid.data_ptr<int64_t>(), perm.data_ptr<int64_t>(), cbp(dy), N, (int)dy.size(1),
-                   scratch.data_ptr<float>(), grad.data_ptr(), grad.scalar_type() == at::kFloat,
+                   grad.size(0), scratch.data_ptr<float>(), grad.data_ptr(), grad.scalar_type() == at::kFloat,
                    grad.stride(0), cur_stream(dy));
 }
 
@@ -415,7 +419,7 @@ std::tuple<at::Tensor, at::Tensor> moe_combine_bwd(const at::Tensor& dout, const
 TORCH_LIBRARY_FRAGMENT(dla, m) {
   m.def("moe_topk_fwd(Tensor logits, int k) -> (Tensor, Tensor)");
   m.def("quant_fp8_rows(Tensor x) -> (Tensor, Tensor)");
-  m.def("embed_fwd(Tensor w, Tensor ids) -> Tensor");
+  m.def("embed_fwd(Tensor w, Tensor ids, Tensor(a!) bad) -> Tensor");
   m.def("reward_head_fwd(Tensor hidden, Tensor? last, Tensor? mask, Tensor w, Tensor? bias, float p, int seed) -> (Tensor, Tensor)");
   m.def("reward_head_bwd(Tensor dscore, Tensor hidden, Tensor? last, Tensor? mask, Tensor w, float p, int seed) -> Tensor");
   m.def("embed_bwd(Tensor sid, Tensor perm, Tensor dy, Tensor(a!) grad) -> ()");

@@ -22,14 +22,21 @@ constexpr int kEmbChunk = 16;  // sorted positions per backward wave
 
 __global__ __launch_bounds__(256) void embed_fwd_kernel(const bf16_t* __restrict__ w, int64_t ldw,
                                                         const int64_t* __restrict__ ids, int64_t N,
-                                                        int H, int64_t V, bf16_t* __restrict__ out) {
+                                                        int H, int64_t V, bf16_t* __restrict__ out,
+                                                        int* __restrict__ bad) {
   const int64_t row = blockIdx.x * 4ll + (threadIdx.x >> 6);
   if (row >= N) return;
   const int lane = threadIdx.x & 63;
-  int64_t id = ids[row];
-  id = id < 0 ? 0 : (id >= V ? V - 1 : id);  // the binding rejects out-of-range ids; never fault
-  const bf16_t* src = w + id * ldw;
+  const int64_t id = ids[row];
   bf16_t* dst = out + row * static_cast<int64_t>(H);
+  if (id < 0 || id >= V) {
+    // out-of-range id: never read outside the table. The row is zeros and the sticky error word
+    // is set (vector store from lane 0); ops/embedding.py raises on it at the next host sync.
+    for (int c = lane * 8; c < H; c += 512) store_bf16x8(dst + c, bf16x8{});
+    if (lane == 0) bad[0] = 1;
+    return;
+  }
+  const bf16_t* src = w + id * ldw;
   for (int c = lane * 8; c < H; c += 512) store_bf16x8(dst + c, load_bf16x8(src + c));
 }
 
@@ -56,7 +63,7 @@ __device__ __forceinline__ void emb_add_row(G* g, int c, const float* a) {
 template <typename G>
 __global__ __launch_bounds__(256) void embed_bwd_partial_kernel(
     const int64_t* __restrict__ sid, const int64_t* __restrict__ perm, const bf16_t* __restrict__ dy,
-    int64_t N, int H, float* __restrict__ scratch, G* __restrict__ grad, int64_t ldg) {
+    int64_t N, int H, int64_t V, float* __restrict__ scratch, G* __restrict__ grad, int64_t ldg) {
   const int64_t chunk = blockIdx.x * 4ll + (threadIdx.x >> 6);
   const int64_t p0 = chunk * kEmbChunk;
   if (p0 >= N) return;
@@ -68,6 +75,10 @@ __global__ __launch_bounds__(256) void embed_bwd_partial_kernel(
     int64_t q = p + 1;
     while (q < p1 && sid[q] == id) ++q;
     const bool whole = (p == 0 || sid[p - 1] != id) && (q == N || sid[q] != id);
+    if (id < 0 || id >= V) {  // out-of-range ids (flagged by the forward) touch no gradient row
+      p = q;
+      continue;
+    }
     for (int c = lane * 8; c < H; c += 512) {
       float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       for (int64_t j = p; j < q; ++j) {
@@ -92,13 +103,14 @@ __global__ __launch_bounds__(256) void embed_bwd_partial_kernel(
 // add into grad[id].
 template <typename G>
 __global__ __launch_bounds__(256) void embed_bwd_fold_kernel(const int64_t* __restrict__ sid,
-                                                             int64_t N, int H,
+                                                             int64_t N, int H, int64_t V,
                                                              const float* __restrict__ scratch,
                                                              G* __restrict__ grad, int64_t ldg) {
   const int64_t p = blockIdx.x * 4ll + (threadIdx.x >> 6);
   if (p >= N) return;
   const int64_t id = sid[p];
   if (p > 0 && sid[p - 1] == id) return;  // not a run head
+  if (id < 0 || id >= V) return;
   int64_t end = p + 1;
   while (end < N && sid[end] == id) ++end;
   if (p / kEmbChunk == (end - 1) / kEmbChunk) return;  // whole run inside one chunk: pass 1 did it
@@ -117,22 +129,22 @@ __global__ __launch_bounds__(256) void embed_bwd_fold_kernel(const int64_t* __re
 }
 
 void launch_embed_fwd(const bf16_t* w, int64_t ldw, const int64_t* ids, int64_t N, int H, int64_t V,
-                      bf16_t* out, hipStream_t st) {
+                      bf16_t* out, int* bad, hipStream_t st) {
   if (N == 0) return;
-  embed_fwd_kernel<<<static_cast<unsigned>((N + 3) / 4), 256, 0, st>>>(w, ldw, ids, N, H, V, out);
+  embed_fwd_kernel<<<static_cast<unsigned>((N + 3) / 4), 256, 0, st>>>(w, ldw, ids, N, H, V, out, bad);
 }
 
 void launch_embed_bwd(const int64_t* sid, const int64_t* perm, const bf16_t* dy, int64_t N, int H,
-                      float* scratch, void* grad, bool grad_f32, int64_t ldg, hipStream_t st) {
+                      int64_t V, float* scratch, void* grad, bool grad_f32, int64_t ldg, hipStream_t st) {
   if (N == 0) return;
   const int64_t chunks = (N + kEmbChunk - 1) / kEmbChunk;
   const unsigned g1 = static_cast<unsigned>((chunks + 3) / 4), g2 = static_cast<unsigned>((N + 3) / 4);
   if (grad_f32) {
-    embed_bwd_partial_kernel<float><<<g1, 256, 0, st>>>(sid, perm, dy, N, H, scratch, static_cast<float*>(grad), ldg);
-    embed_bwd_fold_kernel<float><<<g2, 256, 0, st>>>(sid, N, H, scratch, static_cast<float*>(grad), ldg);
+    embed_bwd_partial_kernel<float><<<g1, 256, 0, st>>>(sid, perm, dy, N, H, V, scratch, static_cast<float*>(grad), ldg);
+    embed_bwd_fold_kernel<float><<<g2, 256, 0, st>>>(sid, N, H, V, scratch, static_cast<float*>(grad), ldg);
   } else {
-    embed_bwd_partial_kernel<bf16_t><<<g1, 256, 0, st>>>(sid, perm, dy, N, H, scratch, static_cast<bf16_t*>(grad), ldg);
-    embed_bwd_fold_kernel<bf16_t><<<g2, 256, 0, st>>>(sid, N, H, scratch, static_cast<bf16_t*>(grad), ldg);
+    embed_bwd_partial_kernel<bf16_t><<<g1, 256, 0, st>>>(sid, perm, dy, N, H, V, scratch, static_cast<bf16_t*>(grad), ldg);
+    embed_bwd_fold_kernel<bf16_t><<<g2, 256, 0, st>>>(sid, N, H, V, scratch, static_cast<bf16_t*>(grad), ldg);
   }
 }
 

@@ -7,6 +7,12 @@ the engine's flat main-grad buffer (bf16 or fp32), instead of eager PyTorch's de
 gradient (zero-fill + segment sum) plus autograd's add into `.grad` -- two passes over V x H per
 micro-batch. Tied / shared tables (`_dla_shared`: the LM head also writes the gradient) get a
 dense gradient tensor through autograd as usual. CPU tensors use `F.embedding`.
+
+Out-of-range ids: `F.embedding` raises on them. Checking on the host would cost a sync per
+forward, and a device assert aborts the whole process, so the kernel instead writes a zero row,
+never touches memory outside the table (forward and backward) and sets a sticky per-device error
+word. `check_ids()` raises on it; the trainer calls it at every logging step (where it syncs
+anyway), and DLA_EMBED_CHECK=1 checks after every forward (debug).
 """
 from __future__ import annotations
 
@@ -18,11 +24,35 @@ import torch.nn.functional as F
 from . import _ext
 
 
+_BAD = {}  # device -> int32 [1] sticky out-of-range-id word
+_CHECK_EVERY = os.environ.get("DLA_EMBED_CHECK", "0") == "1"
+
+
+def _bad_word(device: torch.device) -> torch.Tensor:
+    w = _BAD.get(device)
+    if w is None:
+        w = _BAD[device] = torch.zeros(1, dtype=torch.int32, device=device)
+    return w
+
+
+def check_ids(reset: bool = True) -> None:
+    """Raise if any native embedding forward since the last check saw an id outside [0, V)
+    (one host sync per device that ran the kernel)."""
+    for dev, w in list(_BAD.items()):
+        if int(w.item()) != 0:
+            if reset:
+                w.zero_()
+            raise IndexError(f"embedding: token id out of range [0, vocab) on {dev} (the rows were "
+                             "zero-filled and got no gradient); check the tokenizer / vocab_size")
+
+
 class _EmbeddingFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, ids, weight):
         flat = ids.reshape(-1).to(torch.int64).contiguous()
-        out = _ext.require().embed_fwd(weight, flat)
+        out = _ext.require().embed_fwd(weight, flat, _bad_word(weight.device))
+        if _CHECK_EVERY:
+            check_ids()
         ctx.save_for_backward(flat)
         ctx.wshape = weight.shape
         ctx.weight = weight

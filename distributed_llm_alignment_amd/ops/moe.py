@@ -225,12 +225,37 @@ class _ExpertsFn(torch.autograd.Function):
 
 # The per-expert input-gradient GEMMs dA = dY W are NN-layout; hipBLASLt's default heuristic
 # (used for these routing-dependent row counts, which no TunableOp table can list) picks a
-# depth-32 tile for them. They run in the forward's TN layout through a transposed expert-weight
-# copy made once per optimizer step by the HIP tiled transpose (HBM cost: one more copy of the
-# expert weights). Mixtral 2-layer DPO, same box, two rounds: bf16 60.2-60.6 vs 59.6-59.8 pairs/s,
-# fp8 forward 67.3-67.7 vs 66.9-67.0 (a torch strided transpose-copy instead lost 2-3 %).
-# DLA_MOE_TRANSPOSED_DGRAD=0 keeps the NN layout.
-MOE_TRANSPOSED_DGRAD = os.environ.get("DLA_MOE_TRANSPOSED_DGRAD", "1") != "0"
+# depth-32 tile for them. They can run in the forward's TN layout through a transposed expert-weight
+# copy made once per optimizer step by the HIP tiled transpose. Mixtral 2-layer DPO, same box, two
+# rounds: bf16 60.2-60.6 vs 59.6-59.8 pairs/s, fp8 forward 67.3-67.7 vs 66.9-67.0 (~1 %). The copy
+# costs one more copy of the local expert weights (~90 GB per rank for Mixtral-8x7B without EP), so
+# it is budgeted: DLA_MOE_TRANSPOSED_DGRAD=auto (default) makes copies only while the total stays
+# within DLA_MOE_TDGRAD_BUDGET_GB (default 4 GB per process; e.g. small local expert stacks under
+# EP, or debug-depth models), =1 always, =0 never. `free_transposed_experts` drops the copies.
+MOE_TRANSPOSED_DGRAD = os.environ.get("DLA_MOE_TRANSPOSED_DGRAD", "auto").lower()
+_TDG_BUDGET = int(float(os.environ.get("DLA_MOE_TDGRAD_BUDGET_GB", "4")) * 2 ** 30)
+_TDG_BYTES = [0]  # bytes currently held by transposed copies in this process
+
+
+def _tdgrad_allowed(*ws: torch.Tensor) -> bool:
+    if MOE_TRANSPOSED_DGRAD in ("0", "off", "false"):
+        return False
+    if MOE_TRANSPOSED_DGRAD in ("1", "on", "true"):
+        return True
+    need = sum(w.numel() * w.element_size() for w in ws if getattr(w, "_dla_wT", None) is None)
+    return _TDG_BYTES[0] + need <= _TDG_BUDGET
+
+
+def free_transposed_experts(module) -> int:
+    """Drop the cached transposed expert copies of every parameter of `module` (engine teardown,
+    re-sharding). Returns the bytes released."""
+    freed = 0
+    for p in module.parameters():
+        c = p.__dict__.pop("_dla_wT", None)
+        if c is not None:
+            freed += c[1].numel() * c[1].element_size()
+    _TDG_BYTES[0] = max(0, _TDG_BYTES[0] - freed)
+    return freed
 
 
 def transposed_experts(w: torch.Tensor) -> torch.Tensor:
@@ -241,8 +266,11 @@ def transposed_experts(w: torch.Tensor) -> torch.Tensor:
     c = getattr(w, "_dla_wT", None)
     if c is None or c[0] != key:
         with torch.no_grad():
-            t = c[1] if c is not None else torch.empty((w.shape[0], w.shape[2], w.shape[1]),
-                                                         dtype=w.dtype, device=w.device)
+            if c is not None:
+                t = c[1]
+            else:
+                t = torch.empty((w.shape[0], w.shape[2], w.shape[1]), dtype=w.dtype, device=w.device)
+                _TDG_BYTES[0] += t.numel() * t.element_size()
             tr = _ext.require().transpose_bf16
             for e in range(w.shape[0]):
                 tr(w.detach()[e], t[e])
@@ -257,10 +285,11 @@ def _loop_experts_backward(dys, xs, gu, w_up, w_down, counts, needs):
     dys = dys.contiguous()
     # only for weights whose updates the flat-buffer engine announces through its weight epoch
     # (in-place kernel updates move no version counter; FSDP re-gathers storage): as ops.linear
-    tdg = (MOE_TRANSPOSED_DGRAD and _ext.use_native(dys) and w_up.dtype == torch.bfloat16
+    tdg = (_ext.use_native(dys) and w_up.dtype == torch.bfloat16
            and getattr(w_up, "_dla_epoch", None) is not None
            and getattr(w_down, "_dla_epoch", None) is not None
-           and w_up.shape[1] % 8 == 0 and w_up.shape[2] % 8 == 0)
+           and w_up.shape[1] % 8 == 0 and w_up.shape[2] % 8 == 0
+           and _tdgrad_allowed(w_down, *((w_up,) if needs[0] else ())))
     wdT = transposed_experts(w_down) if tdg else None  # [E, F, H]
     wuT = transposed_experts(w_up) if tdg and needs[0] else None  # [E, H, 2F]
     need_x = needs[0]

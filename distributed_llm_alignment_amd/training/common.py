@@ -275,6 +275,9 @@ def train_loop(ctx: TrainContext, loader, sampler, engine: DataParallelEngine, s
             last_metrics = metrics
             global_step += 1
             if log_every and global_step % log_every == 0:
+                from ..ops.embedding import check_ids
+
+                check_ids()  # out-of-range token ids since the last log (sticky device word)
                 rec = {"train/loss": running.average, "train/grad_norm": engine.last_grad_norm,
                        "train/comm_exposed_ms": engine.comm_timer.last_ms()}
                 if scheduler is not None:

@@ -219,9 +219,13 @@ def _ppo_loop(ctx, config, ppo, policy, ref, rm, rollout, engine, steps, kl_coef
     barrier()
     out = save_state(config["logging"]["output_dir"], [policy.model, ref.model, rm, critic], engine, None,
                      steps, policy.tokenizer)
-    torch.save({k: (v.cpu() if isinstance(v, torch.Tensor) else v)
-                for k, v in critic_engine.optimizer_state().items()},
-               Path(out) / f"critic_optimizer_shard_{ctx.dist.rank}.pt")
+    from ..utils.stream_st import save_streamed
+
+    cst = critic_engine.optimizer_state()
+    save_streamed(Path(out) / f"critic_optimizer_shard_{ctx.dist.rank}.safetensors",
+                  {k: v for k, v in cst.items() if isinstance(v, torch.Tensor) or v is None},
+                  {k: (list(v) if isinstance(v, tuple) else v) for k, v in cst.items()
+                   if not (isinstance(v, torch.Tensor) or v is None)})
     ctx.log("RLHF PPO (actor-critic) loop complete")
     ctx.logger.close()
     return 0

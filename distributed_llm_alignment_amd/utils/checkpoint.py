@@ -8,8 +8,9 @@
   optimizer.bin                                  torch AdamW-format state dict (consolidated)
   scheduler.bin                                  only when a scheduler is given
   random_states_{rank}.pkl                       step + python / numpy / torch / cuda RNG
-Extras the reference lacks (Appendix A #6, §5.4 gaps): `optimizer_shard_{rank}.pt` (exact
-ZeRO-sharded state for fast resume), `dla_state.json` (step, layout), an `hf/` export of model 0
+Extras the reference lacks (Appendix A #6, §5.4 gaps): `optimizer_shard_{rank}.safetensors`
+(exact ZeRO-sharded state for fast resume, streamed from the device through one pinned buffer:
+host RSS stays bounded however large the shard, utils/stream_st.py), `dla_state.json` (step, layout), an `hf/` export of model 0
 (config.json + model.safetensors + tokenizer, `from_pretrained`-style so stages chain), a
 `latest` pointer next to the step dirs, and keep-last-N rotation. `load_state` resumes; model
 loading tolerates `module.` prefixes and `pytorch_model.bin`.
@@ -28,7 +29,12 @@ import torch
 
 from ..parallel import dist as pdist
 
-CONSOLIDATE_MAX_NUMEL = 2_000_000_000  # gather a torch-format optimizer.bin up to ~2B params
+CONSOLIDATE_MAX_NUMEL = 2_000_000_000  # in-memory gather of optimizer.bin up to ~2B params
+# Above that, optimizer.bin is consolidated by rank 0 from the page-cache mapped shard files
+# (tools/consolidate_checkpoint.py; no host copy of the whole state) up to this many params
+# (DLA_OPTIMIZER_BIN_MAX_NUMEL; 0 disables): Llama-3-8B is written by default, 70B is not (a
+# 560 GB file from one rank) and stays consolidatable offline with the same tool.
+STREAM_CONSOLIDATE_MAX_NUMEL = int(float(os.environ.get("DLA_OPTIMIZER_BIN_MAX_NUMEL", "1.6e10")))
 
 
 def _rng_state() -> Dict[str, Any]:
@@ -101,14 +107,24 @@ def save_state(output_dir, models: Sequence, engine=None, scheduler=None, step: 
     if st.is_main and scheduler is not None:
         torch.save(scheduler.state_dict(), out / "scheduler.bin")
     if engine is not None:
-        torch.save({k: (v.cpu() if isinstance(v, torch.Tensor) else v)
-                    for k, v in engine.optimizer_state().items()}, out / f"optimizer_shard_{st.rank}.pt")
+        from .stream_st import save_streamed
+
+        osd_local = engine.optimizer_state()
+        tens = {k: v for k, v in osd_local.items() if isinstance(v, torch.Tensor) or v is None}
+        meta = {k: (list(v) if isinstance(v, tuple) else v) for k, v in osd_local.items() if k not in tens}
+        save_streamed(out / f"optimizer_shard_{st.rank}.safetensors", tens, meta)
         if st.is_main and hasattr(engine, "layout"):
             (out / "dla_optimizer_layout.json").write_text(json.dumps(engine.layout()))
         if engine.numel <= CONSOLIDATE_MAX_NUMEL and not tp:
             osd = engine.torch_optimizer_state_dict()  # collective under ZeRO (gathered per unit)
             if st.is_main:
                 torch.save(osd, out / "optimizer.bin")
+        elif not tp and engine.numel <= STREAM_CONSOLIDATE_MAX_NUMEL and hasattr(engine, "layout"):
+            pdist.barrier()  # every rank's shard is on disk
+            if st.is_main:
+                from .consolidate import consolidate_optimizer as consolidate
+
+                consolidate(out, out / "optimizer.bin")
     torch.save({"step": step, **_rng_state()}, out / f"random_states_{st.rank}.pkl")
     if st.is_main:
         meta = {"step": step, "world_size": st.world_size, "num_models": len(models),
@@ -210,9 +226,18 @@ def load_state(ckpt_dir, models: Sequence, engine=None, scheduler=None, load_mod
             if _weights_present(d, i):
                 load_model_weights(m, d, i, strict=True)
     if engine is not None:
-        shard = d / f"optimizer_shard_{st.rank}.pt"
+        shard = d / f"optimizer_shard_{st.rank}.safetensors"
+        legacy = d / f"optimizer_shard_{st.rank}.pt"
         if shard.exists():
-            sd = torch.load(str(shard), map_location="cpu", weights_only=True)
+            from .stream_st import mmap_tensor, read_header
+
+            hdr = read_header(shard)
+            sd = dict(hdr[2])
+            sd.update({k: mmap_tensor(shard, k, hdr) for k in hdr[0]})  # copied chunk-free by .copy_
+            sd.setdefault("master", None)
+            engine.load_optimizer_state(sd)
+        elif legacy.exists():
+            sd = torch.load(str(legacy), map_location="cpu", weights_only=True)
             engine.load_optimizer_state({k: (v.to(engine.device) if isinstance(v, torch.Tensor) else v)
                                          for k, v in sd.items()})
         else:
@@ -237,4 +262,21 @@ def load_state(ckpt_dir, models: Sequence, engine=None, scheduler=None, load_mod
     meta = d / "dla_state.json"
     if meta.exists():
         step = int(json.loads(meta.read_text()).get("step", step))
+    # weight-derived caches (W^T for the TN dgrad, fp8 / transposed expert copies) were keyed on
+    # versions the in-place loads above did not move: drop them so nothing stale is read
+    for m in models:
+        invalidate_weight_caches(m)
+    if engine is not None and hasattr(engine, "_wt_epoch"):
+        engine._wt_epoch[0] += 1
     return step
+
+
+def invalidate_weight_caches(model) -> None:
+    """Drop every cache derived from a parameter's values (ops.linear `_dla_wt`, ops.moe
+    `_dla_fp8` / `_dla_wT`): the next use rebuilds it from the current weights."""
+    from ..ops.moe import free_transposed_experts
+
+    free_transposed_experts(model)
+    for p in model.parameters():
+        for k in ("_dla_wt_ver", "_dla_fp8"):
+            p.__dict__.pop(k, None)

@@ -357,6 +357,18 @@ def load_rank_shards(model, d, stem: str) -> bool:
     ok = (f.exists() and int(lay["tp_size"]) == getattr(base, "tp_size", 1)
           and int(lay["fsdp_world"]) == (eng.world if eng is not None else 1))
     in_fsdp = {id(p) for u in eng.units for p in u.params} if eng is not None else set()
+    if ok and eng is not None:
+        # the flat shard is only meaningful under the SAME unit grouping: a different
+        # fsdp_min_num_params can keep the total length and still move every element
+        names = {id(p): n for n, p in model.named_parameters()}
+        saved = lay.get("fsdp_units") or []
+        now = [{"numel": u.numel, "chunk": u.chunk, "shard_off": u.shard_off,
+                "params": sorted((names[id(p)], u.offsets[id(p)]) for p in u.params)} for u in eng.units]
+        ok = len(saved) == len(now) and all(
+            int(a["numel"]) == b["numel"] and int(a["chunk"]) == b["chunk"]
+            and int(a["shard_off"]) == b["shard_off"]
+            and sorted((q["name"], int(q["offset"])) for q in a["params"]) == b["params"]
+            for a, b in zip(saved, now))
     if ok:
         with safe_open(str(f), framework="pt") as h:
             keys = set(h.keys())

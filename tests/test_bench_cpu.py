@@ -54,3 +54,50 @@ def _has_gpu():
     import torch
 
     return torch.cuda.device_count() > 0
+
+
+def test_bench_rank_failure_ends_the_whole_run_fast():
+    """One rank dying mid-step (no cleanup) must make the whole command exit non-zero quickly:
+    torchrun tears down the surviving rank, which is otherwise blocked in a collective."""
+    import time
+
+    t0 = time.perf_counter()
+    p = _run(["--gpus", "2", "--device", "cpu", "--model", "tiny-llama", "--steps", "50",
+              "--warmup", "1", "--seq-len", "64", "--micro-pairs", "2", "--accum", "2"],
+             env_extra={"DLA_BENCH_FAIL_RANK": "1", "DLA_BENCH_FAIL_STEP": "2"}, timeout=240)
+    dt = time.perf_counter() - t0
+    assert p.returncode != 0
+    assert "injected failure on rank 1" in p.stderr
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert dt < 90, dt  # includes two interpreter + torch start-ups
+
+
+def test_bench_preflight_line_per_rank():
+    p = _run(["--gpus", "2", "--device", "cpu", "--model", "tiny-llama", "--steps", "1",
+              "--warmup", "0", "--seq-len", "64", "--micro-pairs", "2", "--accum", "1"])
+    assert p.returncode == 0, p.stderr[-3000:]
+    import re
+
+    ranks = sorted(int(m) for m in re.findall(r"\[preflight\] rank (\d+)/2 .*?all_reduce16MB ok", p.stderr))
+    assert ranks == [0, 1], p.stderr[-2000:]
+
+
+def test_launcher_counts_gpus_without_hip(monkeypatch):
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("benchmod", os.path.join(ROOT, "bench.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,1,2")
+    assert mod._visible_list(8) == 3
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", "")
+    assert mod._visible_list(8) == 0
+    monkeypatch.delenv("ROCR_VISIBLE_DEVICES")
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES")
+    monkeypatch.delenv("CUDA_VISIBLE_DEVICES", raising=False)
+    assert mod._visible_list(4) == 4
+    import torch
+
+    n = mod.visible_gpu_count()  # sysfs here (or the child-process count): never HIP in-process
+    assert n >= 0
+    assert not torch.cuda.is_initialized()

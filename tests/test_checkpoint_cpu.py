@@ -174,3 +174,38 @@ def test_rng_state_is_weights_only_loadable(tmp_path):
     torch.manual_seed(0)
     assert load_state(tmp_path / "ck", [m]) == 7
     assert (random.random(), float(np.random.rand()), float(torch.rand(1))) == want
+
+
+def _fsdp_regroup(rank, world, root):
+    from distributed_llm_alignment_amd.models import build_model, get_config
+    from distributed_llm_alignment_amd.parallel.fsdp import FullyShardedEngine, fsdp_full_params
+    from distributed_llm_alignment_amd.utils import sharded_io
+    from distributed_llm_alignment_amd.utils.checkpoint import load_model_weights, save_state
+
+    cfg = get_config("tiny-llama")
+    pol = build_model(cfg, device="cpu", seed=0)
+    with torch.no_grad():
+        for i, p in enumerate(pol.parameters()):
+            p.add_(0.001 * (i + 1))
+    eng = FullyShardedEngine(pol, lr=1e-2)
+    save_state(f"{root}/ck", [pol], eng, step=1, weights="both")
+    with fsdp_full_params(pol):
+        want = [p.detach().clone() for p in pol.parameters()]
+    # same world, different unit grouping (fsdp_min_num_params): the flat shards must be refused
+    pol2 = build_model(cfg, device="cpu", seed=5)
+    eng2 = FullyShardedEngine(pol2, lr=1e-2, min_num_params=10 ** 9)
+    regrouped = len(eng2.units) != len(eng.units)
+    took_shards = sharded_io.load_rank_shards(pol2, f"{root}/ck", "model")
+    load_model_weights(pol2, f"{root}/ck", 0)  # falls back to the HF-named files
+    with fsdp_full_params(pol2):
+        same = all(torch.equal(a, b) for a, b in zip(want, pol2.parameters()))
+    return regrouped, took_shards, same
+
+
+def test_fsdp_shards_refused_when_unit_grouping_changes(tmp_path):
+    """a flat FSDP shard saved under one unit grouping must not be loaded under
+    another even when the total length matches; the HF-named weights load instead, exactly."""
+    res = run_ranks(_fsdp_regroup, 2, (str(tmp_path),))
+    for r in (0, 1):
+        regrouped, took, same = res[r]
+        assert regrouped and not took and same

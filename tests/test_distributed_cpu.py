@@ -199,7 +199,7 @@ def test_checkpoint_resume_exact_zero1():
         assert same
     files = set(os.listdir(os.path.join(d, "step_2")))
     for f in ("model.safetensors", "model_1.safetensors", "optimizer.bin", "random_states_0.pkl",
-              "random_states_1.pkl", "optimizer_shard_0.pt", "optimizer_shard_1.pt"):
+              "random_states_1.pkl", "optimizer_shard_0.safetensors", "optimizer_shard_1.safetensors"):
         assert f in files, f
 
 
@@ -525,8 +525,13 @@ def test_replica_divergence_detector():
     assert res[0] == "caught" and res[1] == "caught"
 
 
-def _ckpt_for_consolidation(rank, world, root, fsdp):
+def _ckpt_for_consolidation(rank, world, root, fsdp, stream=False):
     import torch
+
+    from distributed_llm_alignment_amd.utils import checkpoint as ckmod
+
+    if stream:  # force save_state's page-cache consolidation path (the >2B-param route)
+        ckmod.CONSOLIDATE_MAX_NUMEL = 0
 
     from distributed_llm_alignment_amd.data.synthetic import synthetic_preference_batch
     from distributed_llm_alignment_amd.models import build_model, get_config
@@ -543,6 +548,9 @@ def _ckpt_for_consolidation(rank, world, root, fsdp):
     dpo_step_loss(pol, ref, b)[0].backward()
     eng.step()
     save_state(f"{root}/ck", [pol], eng, step=1, hf_export=False)
+    want = eng.torch_optimizer_state_dict()  # collective (gathered)
+    if rank == 0:
+        torch.save(want, f"{root}/want.bin")
     return 0
 
 
@@ -563,6 +571,42 @@ def test_consolidate_optimizer_shards_matches_gathered(tmp_path, fsdp):
     for i in want["state"]:
         for k in ("exp_avg", "exp_avg_sq"):
             assert torch.equal(got["state"][i][k], want["state"][i][k]), (i, k)
+
+
+@pytest.mark.parametrize("fsdp", [False, True])
+def test_save_state_streams_optimizer_bin_above_gather_limit(tmp_path, fsdp):
+    """Above the in-memory gather limit save_state still writes optimizer.bin (accelerate layout,
+    reference src/training/utils.py:99-102) by consolidating the streamed shard files; it equals
+    the engine's gathered state dict, and resume from the .safetensors shards is exact."""
+    run_ranks(_ckpt_for_consolidation, 2, (str(tmp_path), fsdp, True))
+    ck = tmp_path / "ck"
+    got = torch.load(str(ck / "optimizer.bin"), weights_only=True)
+    want = torch.load(str(tmp_path / "want.bin"), weights_only=True)
+    assert sorted(got["state"]) == sorted(want["state"])
+    for i in want["state"]:
+        for k in ("exp_avg", "exp_avg_sq"):
+            assert torch.equal(got["state"][i][k], want["state"][i][k]), (i, k)
+    assert got["param_groups"][0]["lr"] == want["param_groups"][0]["lr"]
+
+
+def test_stream_st_roundtrip_bounded_host_buffer(tmp_path):
+    """utils/stream_st.py: the file is standard safetensors (safe_open reads it), meta survives,
+    and the mapped read-back equals the input for every dtype used by the engines."""
+    from safetensors import safe_open
+
+    from distributed_llm_alignment_amd.utils.stream_st import load_streamed, save_streamed
+
+    g = torch.Generator().manual_seed(0)
+    t = {"a": torch.randn(1000, 3, generator=g), "b": torch.randn(77, generator=g).to(torch.bfloat16),
+         "c": torch.arange(5, dtype=torch.int64), "none": None, "empty": torch.empty(0)}
+    f = save_streamed(tmp_path / "x.safetensors", t, {"step": 3, "betas": [0.9, 0.95]}, chunk_mb=1)
+    with safe_open(str(f), framework="pt") as h:
+        assert torch.equal(h.get_tensor("a"), t["a"]) and torch.equal(h.get_tensor("b"), t["b"])
+    back, meta = load_streamed(f)
+    assert meta == {"step": 3, "betas": [0.9, 0.95]}
+    assert set(back) == {"a", "b", "c", "empty"}
+    for k in ("a", "b", "c"):
+        assert torch.equal(back[k], t[k])
 
 
 # ------------------------------------------------------------------ fp32 gradient accumulation

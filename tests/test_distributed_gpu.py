@@ -20,7 +20,10 @@ import pytest
 import torch
 import torch.multiprocessing as mp
 
-pytestmark = pytest.mark.gpu
+# per-test wall budget: a first-contact RCCL hang costs at most this, not the driver's round
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(120, method="thread")]
+_INIT_TIMEOUT_S = 90  # collective / rendezvous timeout inside each rank
+_RANK_DEADLINE_S = 110  # the parent waits at most this long for ALL ranks of one test
 
 
 # DLA_RANKS_ON_CPU=N: host dry run of this file's rank logic on N gloo ranks (torch fallbacks
@@ -54,10 +57,10 @@ def _worker(rank, world, port, fn, args, q):
         from distributed_llm_alignment_amd.parallel.dist import destroy, init_distributed
 
         if _CPU_RANKS:
-            st = init_distributed(backend="gloo", device="cpu", timeout_s=240)
+            st = init_distributed(backend="gloo", device="cpu", timeout_s=_INIT_TIMEOUT_S)
         else:
             _ext.require()
-            st = init_distributed(timeout_s=240)
+            st = init_distributed(timeout_s=_INIT_TIMEOUT_S)
             if world > 1:
                 assert dist.get_backend() == "nccl", dist.get_backend()
         res = fn(rank, world, st.device, *args)
@@ -89,15 +92,18 @@ def run_ranks(fn, world, args=()):
     for p in procs:
         p.start()
     out = {}
+    import time
+
+    deadline = time.monotonic() + _RANK_DEADLINE_S
     try:
         for _ in procs:
-            rank, status, res = q.get(timeout=240)
+            rank, status, res = q.get(timeout=max(1.0, deadline - time.monotonic()))
             if status != "ok":
                 raise AssertionError(f"rank {rank} failed:\n{res}")
             out[rank] = res
     finally:
         for p in procs:
-            p.join(30)
+            p.join(max(1.0, min(15.0, deadline + 15 - time.monotonic())))
             if p.is_alive():
                 p.kill()
     return out
@@ -321,7 +327,7 @@ def test_rccl_bus_bandwidth_recorded():
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
            os.path.join(root, "tools", "comm_bench.py"), "--sizes-mb", "16,64,256", "--out", out]
     p = subprocess.run(cmd, cwd=root, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
-                       timeout=200)
+                       timeout=100)
     assert p.returncode == 0, p.stdout[-3000:]
     rows = [json.loads(ln) for ln in open(out)]
     assert {r["op"] for r in rows} == {"all_reduce", "reduce_scatter", "all_gather", "all_to_all"}

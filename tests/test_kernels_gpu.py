@@ -639,6 +639,38 @@ def test_embedding_gather_and_sorted_scatter_add(gdtype):
         assert torch.equal(w.main_grad, first)
 
 
+def test_embedding_out_of_range_ids_are_contained():
+    """An id outside [0, V) (negative or >= V): the forward writes a zero row and never reads
+    outside the table, the backward skips it (no write outside the main-grad rows: a guard band
+    around the table view stays untouched), and `check_ids` raises once, then resets."""
+    from distributed_llm_alignment_amd import ops
+    from distributed_llm_alignment_amd.ops.embedding import check_ids
+
+    dev = torch.device("cuda", 0)
+    check_ids()  # clean slate
+    V, H = 64, 256
+    g = torch.Generator(device=dev).manual_seed(5)
+    w = torch.randn(V, H, device=dev, generator=g).to(torch.bfloat16).requires_grad_(True)
+    flat = torch.zeros((V + 2 * 512) * H, device=dev, dtype=torch.float32)  # guard bands
+    w.main_grad = flat[512 * H:(512 + V) * H].view(V, H)
+    ids = torch.tensor([[1, -1, 5, V, 5, V + 300, -200, 2]], device=dev)
+    out = ops.embedding(ids, w)
+    bad = (ids < 0) | (ids >= V)
+    assert torch.equal(out[bad], torch.zeros_like(out[bad]))
+    good = ids[~bad]
+    assert torch.equal(out[~bad], w.detach()[good])
+    dy = torch.ones_like(out)
+    out.backward(dy)
+    torch.cuda.synchronize()
+    assert torch.count_nonzero(flat[:512 * H]) == 0 and torch.count_nonzero(flat[(512 + V) * H:]) == 0
+    ref = torch.zeros(V, H, device=dev)
+    ref.index_add_(0, good, torch.ones(good.numel(), H, device=dev))
+    assert torch.equal(w.main_grad, ref)
+    with pytest.raises(IndexError):
+        check_ids()
+    check_ids()  # reset after raising
+
+
 @pytest.mark.parametrize("pooling", ["last_token", "mean"])
 def test_fused_reward_head(pooling):
     """Fused pool + dropout + Linear(H,1): eval == the PyTorch head (fp32 reference); train-mode

@@ -268,7 +268,7 @@ def test_rlhf_ppo_actor_critic(tmp_path):
     for k in ("train/loss", "train/kl", "train/value_loss", "train/clipfrac", "train/approx_kl"):
         assert k in m[-1], k
     assert all(abs(r["train/loss"]) < 1e4 for r in m)
-    for f in ("model.safetensors", "model_3.safetensors", "critic_optimizer_shard_0.pt"):
+    for f in ("model.safetensors", "model_3.safetensors", "critic_optimizer_shard_0.safetensors"):
         assert (d / "ck" / "ppo" / f).exists(), f
 
 
