@@ -61,6 +61,12 @@ def parse(argv=None):
                          "(measured 1.2 %% slower on 1x MI355X: the GEMMs are power-bound, so the "
                          "two streams only contend)")
     ap.add_argument("--profile-dir", default=None, help="write a torch.profiler trace of 1 step")
+    ap.add_argument("--tp-shape", type=int, default=1,
+                    help="debug: time ONE tensor-parallel rank's compute at world 1 (the model's "
+                         "per-rank shard shapes, models.config.tp_shard_config; no TP collectives)")
+    ap.add_argument("--sharded-init", choices=("auto", "on", "off"), default="auto",
+                    help="build on the meta device and materialise only this rank's TP / FSDP "
+                         "shards (auto: with --tp > 1 or --zero 3)")
     ap.add_argument("--layers", type=int, default=None, help="debug only: override layer count "
                     "(a reduced model is NOT the benchmark config)")
     return ap.parse_args(argv)
@@ -220,11 +226,17 @@ def main(argv=None) -> int:
     world = st.world_size
     mesh = build_mesh(tp=args.tp, ep=args.ep, sp=args.sp)
     overrides = {} if args.layers is None else {"num_layers": args.layers}
-    cfg = get_config(args.model, **overrides)
+    if args.tp_shape > 1:
+        if world != 1 or args.tp != 1:
+            raise SystemExit("bench.py: --tp-shape is a one-GPU debug mode (world 1, --tp 1)")
+        cfg = get_config(f"{args.model}@tp{args.tp_shape}", **overrides)
+    else:
+        cfg = get_config(args.model, **overrides)
     dtype = torch.bfloat16 if dev.type == "cuda" else torch.float32
 
-    policy = build_model(cfg, device=dev, dtype=dtype, seed=1234)
-    ref = build_model(cfg, device=dev, dtype=dtype, seed=1234)
+    meta = args.sharded_init == "on" or (args.sharded_init == "auto" and (args.tp > 1 or args.zero == 3))
+    policy = build_model(cfg, device=dev, dtype=dtype, seed=1234, meta=meta)
+    ref = build_model(cfg, device=dev, dtype=dtype, seed=1234, meta=meta)
     ref.eval()
     for p in ref.parameters():
         p.requires_grad_(False)
@@ -252,8 +264,13 @@ def main(argv=None) -> int:
 
         engine = FullyShardedEngine(policy, lr=1e-6, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01,
                                     max_grad_norm=1.0, group=mesh.dp_group, tp_group=mesh.tp_group)
-        ShardedInference(ref, group=mesh.dp_group)
+        ShardedInference(ref, group=mesh.dp_group)  # (materialises the meta ref unit by unit)
     else:
+        if meta:  # this rank's TP / EP shards only, one parameter at a time
+            from distributed_llm_alignment_amd.models.materialize import materialize
+
+            materialize(policy, dev)
+            materialize(ref, dev)
         engine = DataParallelEngine(policy, lr=1e-6, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01,
                                     max_grad_norm=1.0, zero_stage=args.zero, bucket_mb=args.bucket_mb,
                                     group=mesh.grad_group, tp_group=mesh.tp_group,
@@ -360,7 +377,8 @@ def main(argv=None) -> int:
             "dtype": "bf16" if dtype == torch.bfloat16 else "fp32",
             "data": "synthetic preference pairs (random token ids), random-init weights",
             "config": {
-                "model": cfg.name if args.layers is None else f"{cfg.name}-L{args.layers}(debug)",
+                "model": (cfg.name if args.layers is None else f"{cfg.name}-L{args.layers}(debug)")
+                         + ("(per-TP-rank shapes, debug)" if args.tp_shape > 1 else ""),
                 "global_batch": pairs_per_step,
                 "seq_len": args.seq_len,
                 "parallelism": f"dp{mesh.dp}" + (f"-tp{mesh.tp}" if mesh.tp > 1 else "")

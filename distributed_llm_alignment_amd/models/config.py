@@ -254,8 +254,30 @@ HUB_ALIASES = {
 }
 
 
+def tp_shard_config(cfg: ModelConfig, tp: int) -> ModelConfig:
+    """The per-rank shapes of `cfg` under tensor parallelism of degree `tp` as a standalone
+    (world-1) model: heads, KV heads, FFN width and vocabulary divided by tp, hidden size and
+    depth kept. Used by `bench.py --tp-shape` to time one TP rank's real GEMM / attention / norm
+    shapes on one GPU (e.g. Llama-3-70B at tp 8: 8 q heads / 1 kv head, FFN 3584, vocab 16032)."""
+    if cfg.num_heads % tp or cfg.num_kv_heads % tp or cfg.intermediate_size % tp or cfg.vocab_size % tp:
+        raise ValueError(f"{cfg.name}: heads / kv heads / FFN / vocab must divide tp={tp}")
+    d = cfg.to_dict()
+    d.update(num_heads=cfg.num_heads // tp, num_kv_heads=cfg.num_kv_heads // tp,
+             intermediate_size=cfg.intermediate_size // tp, vocab_size=cfg.vocab_size // tp,
+             name=f"{cfg.name}@tp{tp}")
+    return ModelConfig.from_dict(d)
+
+
 def get_config(name_or_path: str, **overrides) -> ModelConfig:
-    """Resolve a preset / HF directory / hub alias into a ModelConfig."""
+    """Resolve a preset / HF directory / hub alias into a ModelConfig. `<preset>@tp<N>` gives the
+    per-rank shard shapes of that preset under TP degree N (tp_shard_config)."""
+    name = str(name_or_path)
+    if "@tp" in name and not Path(name).is_dir():
+        base, tp = name.rsplit("@tp", 1)
+        cfg = tp_shard_config(get_config(base), int(tp))
+        for k, v in overrides.items():
+            setattr(cfg, k, v)
+        return cfg
     p = Path(str(name_or_path))
     if p.is_dir():
         if (p / "dla_config.json").exists():

@@ -63,7 +63,7 @@ def read_state_dict(path: Path):
 def load_causal_lm(model_name_or_path: str, gradient_checkpointing: bool = True,
                    use_flash_attention: bool = False, torch_dtype: Optional[torch.dtype] = None,
                    device=None, seed: int = 0, headless: bool = False,
-                   device_map=None) -> ModelBundle:
+                   device_map=None, meta_init: bool = False) -> ModelBundle:
     """Preset name / HF hub alias -> random init (seeded, identical on all ranks);
     local dir (config.json + safetensors) -> loaded weights. `use_flash_attention` is accepted
     for config compatibility: the native model always runs the HIP flash-attention kernel.
@@ -84,10 +84,19 @@ def load_causal_lm(model_name_or_path: str, gradient_checkpointing: bool = True,
     cfg = get_config(model_name_or_path)
     p = Path(str(model_name_or_path))
     has_weights = p.is_dir() and bool(_weight_files(p))
-    model = build_model(cfg, device=device, dtype=dtype, seed=seed, init=not has_weights, headless=headless)
-    if has_weights:
-        sd = read_state_dict(p)
-        model.load_hf_state_dict(sd, strict=False)
+    if meta_init and split is None:
+        # memory-bounded construction: shapes only now; values (seeded init or the lazily read
+        # checkpoint) are produced per parameter / FSDP unit after parallelize() has sharded the
+        # shapes (models/materialize.py)
+        from .materialize import build_meta
+
+        model = build_meta(cfg, dtype, seed=seed, headless=headless,
+                           state_dict=read_state_dict(p) if has_weights else None)
+    else:
+        model = build_model(cfg, device=device, dtype=dtype, seed=seed, init=not has_weights, headless=headless)
+        if has_weights:
+            sd = read_state_dict(p)
+            model.load_hf_state_dict(sd, strict=False)
     if split is not None:
         dispatch_layers(model, split)
     if gradient_checkpointing:  # True / "full", or a selective policy ("mlp", "attention")

@@ -89,11 +89,12 @@ class Attention(nn.Module):
 
             B, T = positions.shape
             h = sp_gather(h, seq).view(B, T, -1)
-        elif self.tp is not None:
-            from ..parallel.tensor_parallel import tp_copy
+        if seq is None and self.tp is not None and torch.is_grad_enabled():
+            from ..parallel.tensor_parallel import col_parallel_linear
 
-            h = tp_copy(h, self.tp)
-        qkv = _lin(h, self.qkv_proj, self.qkv_bias)
+            qkv = col_parallel_linear(h, self.qkv_proj, self.qkv_bias, self.tp)
+        else:  # (no autograd: the TP input copy is the identity; decode keeps the skinny GEMMs)
+            qkv = _lin(h, self.qkv_proj, self.qkv_bias)
         window = cfg.sliding_window if cfg.sliding_window else 0
         if cache is None and self.sp is not None:
             # Ulysses: all-to-all to (all tokens, 1/P of the heads), attention, all-to-all back
@@ -115,7 +116,9 @@ class Attention(nn.Module):
         if seq is not None:
             out = sp_reduce_scatter(ops.linear(a, self.o_proj, None).reshape(-1, cfg.hidden_size), seq)
             return out + tp_grad_sum(self.o_bias, seq) if self.o_bias is not None else out
-        out = tp_reduce(ops.linear(a, self.o_proj, None), self.tp)
+        from ..parallel.tensor_parallel import row_parallel_linear
+
+        out = row_parallel_linear(a, self.o_proj, self.tp)
         return out + self.o_bias if self.o_bias is not None else out
 
 
@@ -153,9 +156,19 @@ class MLP(nn.Module):
 
             h = sp_gather(h, seq)
         elif self.tp is not None:
-            from ..parallel.tensor_parallel import tp_copy
+            from ..parallel import tensor_parallel as tpm
 
-            h = tp_copy(h, self.tp)
+            if (tpm.TP_OVERLAP and self.cfg.activation == "swiglu" and self.up_bias is None
+                    and self.down_bias is None and ops.swiglu_mlp_ok(h, self.up_proj, self.down_proj)):
+                # the whole Megatron MLP as one node, collectives overlapped (ops.activations)
+                return ops.swiglu_mlp(h, self.up_proj, self.down_proj, tp_group=self.tp,
+                                      chunks=tpm.TP_CHUNKS)
+            if tpm.TP_OVERLAP:
+                u = tpm.col_parallel_linear(h, self.up_proj, self.up_bias, self.tp)
+                m = ops.swiglu(u) if self.cfg.activation == "swiglu" else ops.gelu_new(u)
+                out = tpm.row_parallel_linear(m, self.down_proj, self.tp)
+                return out + self.down_bias if self.down_bias is not None else out
+            h = tpm.tp_copy(h, self.tp)
         if (self.cfg.activation == "swiglu" and self.up_bias is None and self.down_bias is None
                 and self.tp is None and ops.decode.skinny_ok(h, self.up_proj, glu=True)):
             # decode (<= 16 rows, no autograd): skinny GEMMs, SwiGLU fused into the down GEMM
@@ -323,22 +336,13 @@ class CausalLM(nn.Module):
     # --------------------------------------------------------------------------------- init
     @torch.no_grad()
     def init_weights(self, seed: int = 0):
-        """Deterministic random init (identical on every rank -> no broadcast needed)."""
-        dev = self.embed.device
-        gen = torch.Generator(device=dev)
-        gen.manual_seed(seed)
-        std = self.cfg.init_std
-        out_std = std / math.sqrt(2 * self.cfg.num_layers)
-        for name, p in self.named_parameters():
-            if p.dim() == 1:
-                if name.endswith(("ln1_w", "ln2_w", "norm_w")):
-                    p.fill_(1.0)
-                else:
-                    p.zero_()
-            else:
-                s = out_std if name.endswith(("o_proj", "down_proj", "expert_down")) else std
-                p.copy_(torch.randn(p.shape, generator=gen, device=dev, dtype=torch.float32).mul_(s).to(p.dtype)
-                        if p.numel() < (1 << 26) else _chunked_randn(p, gen, s))
+        """Deterministic random init, identical on every rank (no broadcast needed). Each
+        parameter draws from its own generator seeded by (seed, parameter index), so any subset
+        can be produced alone and in any order: the memory-bounded construction path
+        (models/materialize.py) materialises one parameter / FSDP unit at a time and gets
+        bitwise the same weights as this whole-model init."""
+        for idx, (name, p) in enumerate(self.named_parameters()):
+            p.copy_(init_param_tensor(self.cfg, name, idx, tuple(p.shape), seed, p.device, p.dtype))
         return self
 
     # Activation recompute policies (SURVEY K23 / P5). "full" (= True, the reference's HF
@@ -578,6 +582,30 @@ def _chunked_randn(p: torch.Tensor, gen: torch.Generator, std: float) -> torch.T
     return p
 
 
+def _param_seed(seed: int, idx: int) -> int:
+    return (int(seed) * 1_000_003 + int(idx) * 7_919 + 17) % (2 ** 62)
+
+
+def init_param_tensor(cfg: ModelConfig, name: str, idx: int, shape, seed: int, device, dtype) -> torch.Tensor:
+    """The init value of parameter `name` (index `idx` in named_parameters order) as a fresh
+    tensor: norm weights 1, other vectors 0, matrices N(0, init_std) with the GPT-2 style
+    1/sqrt(2L) scaling on the residual-output projections."""
+    device = torch.device(device)
+    if len(shape) == 1:
+        val = 1.0 if name.endswith(("ln1_w", "ln2_w", "norm_w")) else 0.0
+        return torch.full(shape, val, device=device, dtype=dtype)
+    std = cfg.init_std
+    if name.endswith(("o_proj", "down_proj", "expert_down")):
+        std = std / math.sqrt(2 * cfg.num_layers)
+    gen = torch.Generator(device=device)
+    gen.manual_seed(_param_seed(seed, idx))
+    t = torch.empty(shape, device=device, dtype=dtype)
+    if t.numel() < (1 << 26):
+        t.copy_(torch.randn(shape, generator=gen, device=device, dtype=torch.float32).mul_(std))
+        return t
+    return _chunked_randn(t, gen, std)
+
+
 def sp_seq_reduce(sp, lp: torch.Tensor, mask: torch.Tensor, mean: bool) -> torch.Tensor:
     """Masked per-sequence sum / mean of token log-probs; under sequence parallelism the partial
     sums and token counts of the local slices are all-reduced over the SP group."""
@@ -596,8 +624,14 @@ def default_dtype(device) -> torch.dtype:
 
 
 def build_model(cfg: ModelConfig, device=None, dtype=None, seed: int = 0, init: bool = True,
-                headless: bool = False) -> CausalLM:
+                headless: bool = False, meta: bool = False) -> CausalLM:
+    """`meta=True`: parameters on the meta device, values produced later and only for this rank's
+    shard (models/materialize.py; memory-bounded construction for 70B-class models)."""
     dtype = dtype or default_dtype(device)
+    if meta:
+        from .materialize import build_meta
+
+        return build_meta(cfg, dtype, seed=seed, headless=headless)
     model = CausalLM(cfg, device=device, dtype=dtype, headless=headless)
     if init:
         model.init_weights(seed)

@@ -46,17 +46,33 @@ class _SwiGLUMLPFn(torch.autograd.Function):
     per Llama-3-8B layer and micro-batch that removes a read+write of [M, 3F] bf16."""
 
     @staticmethod
-    def forward(ctx, h, w_up, w_down):
+    def forward(ctx, h, w_up, w_down, tp_group=None, chunks=1):
         ops = _ext.require()
         H = h.shape[-1]
         h2 = h.reshape(-1, H)
         u = F.linear(h2, w_up)
         m, mt = ops.swiglu_fwd_t(u)
-        y = F.linear(m, w_down)
+        if tp_group is None:
+            y = F.linear(m, w_down)
+        else:
+            # tensor parallel (gate|up column-, down row-parallel): the down GEMM runs in token
+            # chunks, each chunk's all-reduce launched async behind the next chunk's GEMM
+            import torch.distributed as dist
+
+            from ..parallel.tensor_parallel import _chunk_bounds
+
+            y = torch.empty((m.shape[0], w_down.shape[0]), dtype=m.dtype, device=m.device)
+            works = []
+            for a, b in _chunk_bounds(m.shape[0], chunks):
+                torch.mm(m[a:b], w_down.t(), out=y[a:b])
+                works.append(dist.all_reduce(y[a:b], group=tp_group, async_op=True))
+            for w in works:
+                w.wait()
         # (weights on ctx: see ops.linear._LinearMainGradFn)
         ctx.save_for_backward(h2, u, mt)
         ctx.w_up, ctx.w_down = w_up, w_down
         ctx.hshape = h.shape
+        ctx.tp_group = tp_group
         return y.view(*h.shape[:-1], w_down.shape[0])
 
     @staticmethod
@@ -71,8 +87,17 @@ class _SwiGLUMLPFn(torch.autograd.Function):
         du, dut = ops.swiglu_bwd_t(u, dm)
         del dm
         dh = input_grad(du, w_up) if ctx.needs_input_grad[0] else None
+        work = None
+        if dh is not None and ctx.tp_group is not None:
+            # column-parallel input grad: all-reduce in flight during the gate|up weight grad
+            import torch.distributed as dist
+
+            dh = dh.contiguous()
+            work = dist.all_reduce(dh, group=ctx.tp_group, async_op=True)
         accumulate_weight_grad(w_up, du, h2, dyt=dut)
-        return (dh.view(ctx.hshape) if dh is not None else None), None, None
+        if work is not None:
+            work.wait()
+        return (dh.view(ctx.hshape) if dh is not None else None), None, None, None, None
 
 
 def swiglu_mlp_ok(h: torch.Tensor, w_up: torch.Tensor, w_down: torch.Tensor) -> bool:
@@ -81,10 +106,12 @@ def swiglu_mlp_ok(h: torch.Tensor, w_up: torch.Tensor, w_down: torch.Tensor) -> 
             and w_down.shape[1] % 64 == 0 and h.numel() // h.shape[-1] % 8 == 0)
 
 
-def swiglu_mlp(h: torch.Tensor, w_up: torch.Tensor, w_down: torch.Tensor) -> torch.Tensor:
+def swiglu_mlp(h: torch.Tensor, w_up: torch.Tensor, w_down: torch.Tensor, tp_group=None,
+               chunks: int = 1) -> torch.Tensor:
     """Bias-free SwiGLU MLP with main_grad weight accumulation (see _SwiGLUMLPFn); callers check
-    `swiglu_mlp_ok` first."""
-    return _SwiGLUMLPFn.apply(h, w_up, w_down)
+    `swiglu_mlp_ok` first. With `tp_group` the node is the whole Megatron TP MLP (input
+    replicated, output all-reduced) with its collectives overlapped."""
+    return _SwiGLUMLPFn.apply(h, w_up, w_down, tp_group, chunks)
 
 
 class _GeluFn(torch.autograd.Function):

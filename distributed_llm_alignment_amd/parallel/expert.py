@@ -94,10 +94,18 @@ def apply_expert_parallel(model, mesh):
         return model
     ep = ExpertParallel(mesh.ep_group, cfg.num_experts)
     lo, hi = ep.rank * ep.El, (ep.rank + 1) * ep.El
+    owners = None
     for layer in base.layers:
         m = layer.mlp
-        m.expert_up.data = m.expert_up.data[lo:hi].contiguous()
-        m.expert_down.data = m.expert_down.data[lo:hi].contiguous()
+        for nm in ("expert_up", "expert_down"):
+            w = getattr(m, nm)
+            if w.is_meta:  # memory-bounded construction: local rows now, values later
+                from ..models.materialize import _owners, reshape_meta
+
+                owners = owners if owners is not None else _owners(model)
+                reshape_meta(model, w, (hi - lo,) + tuple(w.shape[1:]), owners, _dla_ep_rows=(lo, hi))
+            else:
+                w.data = w.data[lo:hi].contiguous()
         for w in (m.expert_up, m.expert_down):
             w._dla_expert = True
             w._dla_ep = (mesh.ep_group, ep.rank, ep.ep)  # dim-0 slice rank/size (checkpoint I/O)

@@ -127,7 +127,10 @@ class _ShardedBase:
             self.world, self.rank = 1, 0
         self.prefetch = prefetch
         self.dtype = params[0].dtype
-        self.device = params[0].device
+        # meta parameters (models/materialize.py): values are produced unit by unit below, on
+        # this rank's device, and never exist for the whole model at once
+        meta = any(p.is_meta for p in params)
+        self.device = self.dist.device if meta else params[0].device
         pset = {id(p) for p in params}
         unit_mods = default_units(module, min_num_params)
         owner: Dict[int, int] = {}
@@ -150,15 +153,38 @@ class _ShardedBase:
         self.shard_numel = shard
         self.numel = sum(u.numel for u in units)
         self.param_shard = torch.empty(shard, dtype=self.dtype, device=self.device)
+        if meta:
+            from ..models.materialize import _account, _owners, local_value, replace_param
+
+            owners_map = _owners(module)
+            esz = torch.empty(0, dtype=self.dtype).element_size()
+            _account(shard * esz)  # this rank's shards, kept
         with torch.no_grad():
             for u in units:
                 u.full = torch.zeros(u.numel, dtype=self.dtype, device=self.device)
-                for p in u.params:
+                if meta:
+                    _account(u.numel * esz)
+                for i, p in enumerate(u.params):
                     o = u.offsets[id(p)]
-                    view = u.full[o:o + p.numel()].view_as(p)
-                    view.copy_(p.data)
-                    p.data = view
+                    view = u.full[o:o + p.numel()].view(p.shape)
+                    if p.is_meta:
+                        val = local_value(module, p, self.device)
+                        view.copy_(val)
+                        _account(-val.numel() * val.element_size())  # lives on in the unit buffer
+                        del val
+                        newp = replace_param(module, p, view, owners_map)
+                        u.offsets[id(newp)] = u.offsets.pop(id(p))
+                        owner[id(newp)] = owner.pop(id(p))
+                        u.params[i] = newp
+                    else:
+                        view.copy_(p.data)
+                        p.data = view
                 self.param_shard[u.shard_off:u.shard_off + u.chunk].copy_(self._my_chunk(u.full, u))
+                if not u.is_root:  # one full unit at a time: bounded construction peak
+                    _free(u.full)
+                    u.resident = False
+                    if meta:
+                        _account(-u.numel * esz)
         self._pending = []  # in-flight reduce-scatters: (handle, tmp, unit)
         self.comm_timer = ExposedCommTimer(self.device)  # exposed gradient-comm wait per step
         self._seen = set()
@@ -166,9 +192,6 @@ class _ShardedBase:
             if u.modules:
                 u.modules[0].register_forward_pre_hook(self._make_pre_forward(u))
                 u.modules[-1].register_forward_hook(self._make_post_forward(u))
-        for u in units:
-            if not u.is_root:
-                self._reshard(u)
 
     # ------------------------------------------------------------------ gather / free
     def _my_chunk(self, buf: torch.Tensor, u: _Unit) -> torch.Tensor:
@@ -296,7 +319,7 @@ class FullyShardedEngine(_ShardedBase):
         self.lr, self.betas, self.eps, self.wd = lr, tuple(betas), eps, weight_decay
         self.max_grad_norm = max_grad_norm
         self.step_count = 0
-        self.params = params
+        self.params = [p for p in module.parameters() if p.requires_grad]  # (meta ones replaced)
         n = self.shard_numel
         # micro-batch grads are reduce-scattered per unit in the param dtype and accumulated here:
         # fp32 (grad_dtype) keeps 16-256 micro-batch accumulations exact to fp32 rounding

@@ -24,6 +24,7 @@ grads per rank; `tp_grad_sum` all-reduces those over the TP group in backward.
 """
 from __future__ import annotations
 
+import os
 from contextlib import contextmanager
 from typing import Optional
 
@@ -175,6 +176,112 @@ def tp_reduce(x, group):
     return _ReduceFromTP.apply(x, group)
 
 
+# ------------------------------------------------------------ overlapped TP linear layers
+# The plain TP layer issues every collective synchronously on the critical path: per layer and
+# micro-batch, 2 forward all-reduces of the [B*T, H] row-parallel outputs and 2 backward
+# all-reduces of the column-parallel input grads (Llama-3-70B at TP 8: 64 MB each at 4k tokens,
+# about as long as the layer's GEMMs on one rank). With DLA_TP_OVERLAP (default on):
+#   * row-parallel (o_proj, down_proj) forward: the GEMM runs in DLA_TP_CHUNKS token chunks and
+#     chunk c's all-reduce is launched async (RCCL's stream) as soon as its rows exist, so it
+#     overlaps the GEMM of chunk c+1; the layer waits once, before the residual add;
+#   * column-parallel (qkv, gate|up) backward: dX = dY W is computed first, its all-reduce
+#     launched async, THEN the weight-gradient GEMM runs (independent of it) while the
+#     collective is in flight.
+TP_OVERLAP = os.environ.get("DLA_TP_OVERLAP", "1") != "0"
+TP_CHUNKS = max(1, int(os.environ.get("DLA_TP_CHUNKS", "4")))
+
+
+def _chunk_bounds(M: int, chunks: int):
+    """Row ranges of `chunks` near-equal pieces, each a multiple of 8 rows (GEMM-friendly)."""
+    step = max(8, ((M + chunks - 1) // chunks + 7) // 8 * 8)
+    return [(a, min(M, a + step)) for a in range(0, M, step)]
+
+
+def _linear_backward(ctx, dy2, x2, weight, async_group=None):
+    """dX (optionally all-reduced async over `async_group`, overlapped with the weight grad), dW."""
+    from ..ops.linear import accumulate_weight_grad, input_grad
+
+    dx, work = None, None
+    if ctx.needs_input_grad[0]:
+        dx = input_grad(dy2, weight)
+        if async_group is not None:
+            dx = dx.contiguous()
+            work = dist.all_reduce(dx, group=async_group, async_op=True)
+    dw = None
+    if ctx.needs_input_grad[1] and not accumulate_weight_grad(weight, dy2, x2):
+        dw = dy2.t() @ x2
+    if work is not None:
+        work.wait()
+    return dx, dw
+
+
+class _ColParallelLinearFn(torch.autograd.Function):
+    """y = x W^T (+ b), x replicated over the TP group (Megatron's f operator folded in): the
+    backward all-reduces dX asynchronously behind the weight-gradient GEMM."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, group):
+        ctx.save_for_backward(x)
+        ctx.weight, ctx.group, ctx.has_bias = weight, group, bias is not None
+        return F.linear(x, weight, bias)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        dx, dw = _linear_backward(ctx, dy2, x.reshape(-1, x.shape[-1]), ctx.weight, ctx.group)
+        db = dy2.sum(0) if (ctx.has_bias and ctx.needs_input_grad[2]) else None
+        return (dx.view(x.shape) if dx is not None else None), dw, db, None
+
+
+class _RowParallelLinearFn(torch.autograd.Function):
+    """y = all_reduce(x W^T) over the TP group (Megatron's g operator folded in), the forward
+    GEMM + all-reduce pipelined over token chunks; backward = the plain linear backward."""
+
+    @staticmethod
+    def forward(ctx, x, weight, group, chunks):
+        K = x.shape[-1]
+        x2 = x.reshape(-1, K)
+        if not x2.is_contiguous():
+            x2 = x2.contiguous()
+        M, N = x2.shape[0], weight.shape[0]
+        y = torch.empty((M, N), dtype=x.dtype, device=x.device)
+        works = []
+        for a, b in _chunk_bounds(M, chunks):
+            torch.mm(x2[a:b], weight.t(), out=y[a:b])
+            works.append(dist.all_reduce(y[a:b], group=group, async_op=True))
+        for w in works:
+            w.wait()
+        ctx.save_for_backward(x)
+        ctx.weight = weight
+        return y.view(*x.shape[:-1], N)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        dx, dw = _linear_backward(ctx, dy2, x.reshape(-1, x.shape[-1]), ctx.weight)
+        return (dx.view(x.shape) if dx is not None else None), dw, None, None
+
+
+def col_parallel_linear(x, weight, bias, group):
+    """Column-parallel linear on a TP-replicated input (tp_copy + linear, overlapped backward)."""
+    if not TP_OVERLAP:
+        from ..ops.linear import linear
+
+        return linear(tp_copy(x, group), weight, bias)
+    return _ColParallelLinearFn.apply(x, weight, bias, group)
+
+
+def row_parallel_linear(x, weight, group, chunks: Optional[int] = None):
+    """Row-parallel linear summed over TP (linear + tp_reduce, chunk-pipelined forward)."""
+    if not TP_OVERLAP:
+        from ..ops.linear import linear
+
+        return tp_reduce(linear(x, weight, None), group)
+    return _RowParallelLinearFn.apply(x, weight, group, chunks or TP_CHUNKS)
+
+
 def tp_all_gather_last(x: torch.Tensor, group) -> torch.Tensor:
     """Concatenate per-rank shards along the last dim (inference only, e.g. full logits)."""
     ws = dist.get_world_size(group)
@@ -317,8 +424,19 @@ def apply_tensor_parallel(model, group, tp_rank: Optional[int] = None, tp_size: 
         raise ValueError(f"heads ({cfg.num_heads}/{cfg.num_kv_heads}) and FFN ({cfg.intermediate_size}) "
                          f"must divide tp={tp}")
     specs, vocab = _tp_specs(cfg, tp)
+    owners = None
 
     def shard(p, spec):
+        nonlocal owners
+        if p.is_meta:  # memory-bounded construction: local shape now, values later
+            from ..models.materialize import _owners, reshape_meta
+
+            owners = owners if owners is not None else _owners(model)
+            dim, segs = spec
+            shape = list(p.shape)
+            shape[dim] = sum(n // tp for n in segs)
+            reshape_meta(model, p, shape, owners, _dla_tp_spec=spec)
+            return
         p.data = shard_tensor(p.data, spec, r, tp)
         p._dla_tp_spec = spec
 

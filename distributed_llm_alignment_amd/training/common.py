@@ -116,12 +116,28 @@ def parallelize(ctx: TrainContext, model):
     if base.cfg.is_moe and (ctx.cfg.get("model", {}) or {}).get("moe_fp8", False):
         for layer in base.layers:  # e4m3 expert GEMMs in the forward (bf16 backward)
             layer.mlp.fp8 = True
-    if use_fsdp(ctx) and not any(p.requires_grad for p in model.parameters()):
+    trainable = any(p.requires_grad for p in model.parameters())
+    if use_fsdp(ctx) and not trainable:
         # frozen reference / teachers are sharded too (C10): 1/dp of their weights resident
         from ..parallel.fsdp import ShardedInference
 
         ShardedInference(model, group=m.dp_group, min_num_params=ctx.hw.get("fsdp_min_num_params", 0))
+    from ..models.materialize import has_meta_params, materialize
+
+    if has_meta_params(model) and not (use_fsdp(ctx) and trainable):
+        # memory-bounded construction (meta_init): this rank's TP / EP shards only, one parameter
+        # at a time; a trainable FSDP model is materialised unit by unit by its engine instead
+        materialize(model, ctx.device)
     return model
+
+
+def meta_init(ctx: TrainContext) -> bool:
+    """hardware.sharded_init: build models on the meta device and materialise only this rank's
+    shards (auto: whenever tensor parallelism or ZeRO-3 / FSDP shards the weights)."""
+    v = ctx.hw.get("sharded_init", "auto")
+    if isinstance(v, str) and v.lower() == "auto":
+        return (ctx.mesh is not None and ctx.mesh.tp > 1) or bool(use_fsdp(ctx))
+    return bool(v)
 
 
 def use_fsdp(ctx: TrainContext) -> bool:
@@ -151,6 +167,10 @@ def make_engine(ctx: TrainContext, model, lr: float, betas=(0.9, 0.999), weight_
     if ctx.hw.get("cpu_offload"):
         raise ValueError("hardware.fsdp.offload_params / cpu_offload is not supported (weights and "
                          "optimizer state stay in 288 GB HBM); set it to false")
+    from ..models.materialize import has_meta_params, materialize
+
+    if has_meta_params(model):
+        materialize(model, ctx.device)
     z = ctx.hw.get("zero_stage")
     gd, rd = grad_dtypes(ctx)
     return DataParallelEngine(model, lr=lr, betas=betas, weight_decay=weight_decay,

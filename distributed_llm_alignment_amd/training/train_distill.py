@@ -16,7 +16,7 @@ from ..data import TeacherRolloutDataset, build_dataloader
 from ..models import load_causal_lm
 from ..objectives import distill_loss
 from ..utils.config import add_config_args, config_from_args
-from .common import effective_batch_msg, make_engine, parallelize, setup, train_loop
+from .common import meta_init, effective_batch_msg, make_engine, parallelize, setup, train_loop
 
 
 def parse_args(argv=None) -> argparse.Namespace:
@@ -31,7 +31,7 @@ def main(argv=None) -> int:
     dcfg: Dict = config.get("distill", {}) or {}
     student = load_causal_lm(model_cfg["student_model_name_or_path"],
                              gradient_checkpointing=model_cfg.get("gradient_checkpointing", True),
-                             device=ctx.device, seed=ctx.seed)
+                             device=ctx.device, seed=ctx.seed, meta_init=meta_init(ctx))
     use_kl = bool(dcfg.get("use_kl", False) and dcfg.get("on_policy", False))
     teachers: List = []
     if use_kl:
@@ -42,7 +42,8 @@ def main(argv=None) -> int:
         if not paths:
             raise ValueError("KL distillation requested but no teacher model path provided")
         for i, tp in enumerate(paths):
-            tb = load_causal_lm(tp, gradient_checkpointing=False, device=ctx.device, seed=ctx.seed + 1 + i)
+            tb = load_causal_lm(tp, gradient_checkpointing=False, device=ctx.device, seed=ctx.seed + 1 + i,
+                                 meta_init=meta_init(ctx))
             tb.model.eval().requires_grad_(False)
             teachers.append(tb.model)
     parallelize(ctx, student.model)

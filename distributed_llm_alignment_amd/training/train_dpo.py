@@ -25,7 +25,7 @@ from ..models import load_causal_lm
 from ..objectives import dpo_step_loss
 from ..optim.scheduler import LRSchedule
 from ..utils.config import add_config_args, config_from_args
-from .common import effective_batch_msg, make_engine, parallelize, setup, train_loop
+from .common import meta_init, effective_batch_msg, make_engine, parallelize, setup, train_loop
 
 
 def parse_args(argv=None) -> argparse.Namespace:
@@ -39,9 +39,9 @@ def main(argv=None) -> int:
     model_cfg: Dict = config["model"]
     policy = load_causal_lm(model_cfg["policy_model_name_or_path"],
                             gradient_checkpointing=model_cfg.get("gradient_checkpointing", True),
-                            device=ctx.device, seed=ctx.seed)
+                            device=ctx.device, seed=ctx.seed, meta_init=meta_init(ctx))
     ref = load_causal_lm(model_cfg["reference_model_name_or_path"], gradient_checkpointing=False,
-                         device=ctx.device, seed=ctx.seed)
+                         device=ctx.device, seed=ctx.seed, meta_init=meta_init(ctx))
     ref.model.eval()
     ref.model.requires_grad_(False)
     parallelize(ctx, policy.model)

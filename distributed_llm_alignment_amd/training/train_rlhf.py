@@ -118,6 +118,15 @@ def main(argv=None) -> int:
     if algo not in ("reinforce", "ppo"):
         raise ValueError(f"ppo.algorithm must be reinforce|ppo, got {algo!r}")
 
+    # reward inputs built on the device when the reward tokenizer equals the policy's (no
+    # decode / re-tokenise round trip through the host; training/handoff.py), else the
+    # reference's text path (src/training/train_rlhf.py:131-147)
+    from .handoff import RewardHandoff
+
+    handoff = RewardHandoff(tok, rtok, policy.model.cfg.vocab_size, ctx.device, max_len,
+                            ppo.get("reward_handoff", "auto"))
+    ctx.log(f"reward hand-off: {'device ids' if handoff.device_path else 'decode + re-tokenise'}")
+
     def rollout():
         batch_prompts = rng.sample(prompts, k=min(batch_size, len(prompts)))
         mine = split_for_rank(batch_prompts)
@@ -127,11 +136,9 @@ def main(argv=None) -> int:
                               top_p=gen.get("top_p", 1.0), top_k=gen.get("top_k", 0),
                               pad_token_id=tok.pad_token_id, eos_token_id=getattr(tok, "eos_token_id", None),
                               generator=gen_g, return_mask=True)
-        responses = tok.batch_decode(seqs[:, ids.shape[1]:], skip_special_tokens=True)
-        fused = [f"{p}\n\n{r}" for p, r in zip(mine, responses)]
-        renc = rtok(fused, return_tensors="pt", padding=True, truncation=True, max_length=max_len)
+        r_ids, r_mask = handoff(mine, ids, am, seqs, mask)
         with torch.no_grad():
-            scores = rm(renc["input_ids"].to(ctx.device), renc["attention_mask"].to(ctx.device))
+            scores = rm(r_ids, r_mask)
         return seqs, mask, scores, ids.shape[1]
 
     policy.model.train()

@@ -19,7 +19,7 @@ from ..objectives import sft_loss
 from ..optim.scheduler import LRSchedule
 from ..parallel.dist import all_gather_tensor
 from ..utils.config import add_config_args, config_from_args
-from .common import effective_batch_msg, make_engine, move_to, parallelize, setup, train_loop
+from .common import meta_init, effective_batch_msg, make_engine, move_to, parallelize, setup, train_loop
 
 
 def parse_args(argv=None) -> argparse.Namespace:
@@ -51,7 +51,7 @@ def main(argv=None) -> int:
     bundle = load_causal_lm(model_cfg["model_name_or_path"],
                             gradient_checkpointing=model_cfg.get("gradient_checkpointing", True),
                             use_flash_attention=model_cfg.get("use_flash_attention", False),
-                            device=ctx.device, seed=ctx.seed)
+                            device=ctx.device, seed=ctx.seed, meta_init=meta_init(ctx))
     model, tok = bundle.model, bundle.tokenizer
     parallelize(ctx, model)
     data_cfg = dict(config["data"])

@@ -118,6 +118,8 @@ def hardware_parallel(cfg: Dict[str, Any]) -> Dict[str, Any]:
         "master_weights": bool(hw.get("master_weights", True)),
         "grad_dtype": hw.get("grad_dtype", "auto"),      # fp32 main grads (auto: grad_accum >= 16)
         "reduce_dtype": hw.get("reduce_dtype"),          # bucket collective dtype (default: grad)
+        # build on the meta device, materialise only this rank's shards (auto: TP or FSDP)
+        "sharded_init": hw.get("sharded_init", "auto"),
         "fsdp": False,
     }
     ds = hw.get("deepspeed_config")

@@ -269,6 +269,54 @@ def test_rccl_parallel_logprob_matches_dense(kind):
         assert err_g < 5e-2, (r, err_g)
 
 
+def _tp_fused_mlp(rank, world, dev):
+    """The fused Megatron MLP node with overlapped collectives (chunked row-parallel forward,
+    async column-parallel input-grad all-reduce behind the weight-grad GEMM) == the dense MLP."""
+    import torch.distributed as dist
+
+    from distributed_llm_alignment_amd import ops
+    from distributed_llm_alignment_amd.parallel.tensor_parallel import shard_tensor
+
+    if not dist.is_initialized():  # world 1: a one-rank RCCL group still runs the async path
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    group = dist.group.WORLD
+    H, F_, M = 256, 512, 264
+    g = torch.Generator().manual_seed(1)
+    h = (torch.randn(M, H, generator=g) * 0.5).to(dev, torch.bfloat16)
+    w_up = (torch.randn(2 * F_, H, generator=g) / H ** 0.5).to(dev, torch.bfloat16)
+    w_dn = (torch.randn(H, F_, generator=g) / F_ ** 0.5).to(dev, torch.bfloat16)
+    gy = torch.randn(M, H, generator=g).to(dev, torch.bfloat16)
+    out = {}
+    for name, (wu, wd, grp) in {
+        "dense": (w_up, w_dn, None),
+        "tp": (shard_tensor(w_up, (0, [F_, F_]), rank, world), shard_tensor(w_dn, (1, [F_]), rank, world), group),
+    }.items():
+        wu = wu.clone().requires_grad_(True)
+        wd = wd.clone().requires_grad_(True)
+        for w in (wu, wd):
+            w.main_grad = torch.zeros(w.shape, dtype=torch.float32, device=dev)
+        x = h.clone().requires_grad_(True)
+        assert ops.swiglu_mlp_ok(x, wu, wd)
+        y = ops.swiglu_mlp(x, wu, wd, tp_group=grp, chunks=3)
+        y.backward(gy)
+        torch.cuda.synchronize()
+        out[name] = (y.float(), x.grad.float(), wu.main_grad, wd.main_grad)
+    d, t = out["dense"], out["tp"]
+    err = lambda a, b: float((a - b).norm() / (b.norm() + 1e-12))
+    wu_full = shard_tensor(d[2], (0, [F_, F_]), rank, world)
+    wd_full = shard_tensor(d[3], (1, [F_]), rank, world)
+    return err(t[0], d[0]), err(t[1], d[1]), err(t[2], wu_full), err(t[3], wd_full)
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_rccl_tp_fused_mlp_overlapped_collectives(world):
+    if world > _n_gpus() or _CPU_RANKS:
+        pytest.skip("needs that many GPUs (the fused node is GPU-only)")
+    res = run_ranks(_tp_fused_mlp, world)
+    for r, errs in res.items():
+        assert max(errs) < 2e-2, (r, errs)
+
+
 # ------------------------------------------------------------------------------ overlap + graphs
 def _overlap_then_generate(rank, world, dev):
     from distributed_llm_alignment_amd.data.synthetic import synthetic_preference_batch

@@ -23,6 +23,9 @@ def main() -> int:
     ap.add_argument("--new", type=int, default=256)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--handoff", choices=("device", "text", "none"), default="device",
+                    help="reward inputs: device-built ids (training/handoff.py), the reference's "
+                         "decode + re-tokenise text path (byte tokenizer), or the raw sequences")
     ap.add_argument("--grad-ckpt", default="", help="policy activation recompute: full|mlp|attention "
                     "(the reference's rlhf_config batch of 64 rollouts on one GPU needs mlp)")
     a = ap.parse_args()
@@ -46,6 +49,13 @@ def main() -> int:
         pol.gradient_checkpointing_enable(a.grad_ckpt)
     eng = DataParallelEngine(pol, lr=1e-6, betas=(0.9, 0.95), weight_decay=0.01, max_grad_norm=1.0)
     g = torch.Generator(device=dev).manual_seed(0)
+    from distributed_llm_alignment_amd.models.tokenizer import ByteTokenizer
+    from distributed_llm_alignment_amd.training.handoff import RewardHandoff
+
+    tok = ByteTokenizer(vocab_size=cfg.vocab_size)
+    handoff = RewardHandoff(tok, tok, cfg.vocab_size, dev, a.prompt + a.new + 8,
+                            "text" if a.handoff == "text" else "device")
+    prompts = ["synthetic prompt"] * a.batch
     phases = {"generate": 0.0, "score": 0.0, "train": 0.0}
 
     def sync():
@@ -60,7 +70,11 @@ def main() -> int:
                               top_p=0.9, eos_token_id=-1, return_mask=True, seed=3)
         t1 = sync()
         with torch.no_grad():
-            scores = rm(seqs, mask)
+            if a.handoff == "none":
+                scores = rm(seqs, mask)
+            else:
+                r_ids, r_mask = handoff(prompts, ids, am, seqs, mask)
+                scores = rm(r_ids, r_mask)
         t2 = sync()
         pol.train()
         loss, _ = rlhf_loss(pol, ref, seqs, mask, scores.float(), 0.1)
@@ -79,7 +93,7 @@ def main() -> int:
         step(True)
     dt = sync() - t
     print(json.dumps({"bench": "rlhf_step", "model": cfg.name, "rollouts_per_step": a.batch,
-                      "grad_ckpt": a.grad_ckpt or "none",
+                      "grad_ckpt": a.grad_ckpt or "none", "handoff": a.handoff,
                       "prompt": a.prompt, "new_tokens": a.new, "s_per_step": round(dt / a.steps, 3),
                       "rollouts_per_s": round(a.batch * a.steps / dt, 3),
                       **{f"{k}_s": round(v / a.steps, 3) for k, v in phases.items()}}), flush=True)
