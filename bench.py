@@ -51,6 +51,8 @@ def parse(argv=None):
     ap.add_argument("--tp-seq", action="store_true",
                     help="Megatron sequence parallel inside the TP group (reduce-scatter/all-gather)")
     ap.add_argument("--ep", type=int, default=1, help="expert-parallel degree for MoE models")
+    ap.add_argument("--ep-capacity", type=float, default=2.0,
+                    help="EP dispatch capacity factor (sync-free fixed blocks); 0 = exact, host splits")
     ap.add_argument("--sp", type=int, default=1, help="Ulysses sequence-parallel degree (long context)")
     ap.add_argument("--fp8", action="store_true", help="MoE: e4m3 expert GEMMs in the forward")
     ap.add_argument("--grad-ckpt", nargs="?", const="full", default=None, choices=("full", "mlp", "attention"),
@@ -251,8 +253,8 @@ def main(argv=None) -> int:
     if mesh.ep > 1:
         from distributed_llm_alignment_amd.parallel.expert import apply_expert_parallel
 
-        apply_expert_parallel(policy, mesh)
-        apply_expert_parallel(ref, mesh)
+        apply_expert_parallel(policy, mesh, capacity_factor=args.ep_capacity)
+        apply_expert_parallel(ref, mesh, capacity_factor=args.ep_capacity)
     if cfg.is_moe and args.fp8:
         for m in (policy, ref):
             for layer in m.layers:

@@ -36,15 +36,22 @@ namespace dla {
 
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
-// Element offset of 16-byte chunk `ch` of row `row` in a [rows][D] bf16 LDS image. The XOR
-// keeps both ds_read_b128 row reads and ds_read_b64_tr_b16 column reads spread over banks
-// (cdna guide T10 "one image for row reads AND transposed reads", layout (b)).
+// LDS row width (elements) of head dim D: a multiple of 32 (the 32-column MFMA output tiles).
+// D = 80 (phi-2) uses 96-wide images: the 16 pad columns are zero, so Q.K^T runs over exactly
+// D/16 = 5 k-steps and only the P.V / dK / dV column tiles carry the 96/80 pad.
 template <int D>
+constexpr int attn_dp() { return (D + 31) / 32 * 32; }
+
+// Element offset of 16-byte chunk `ch` of row `row` in a [rows][W] bf16 LDS image. The XOR
+// keeps both ds_read_b128 row reads and ds_read_b64_tr_b16 column reads spread over banks
+// (cdna guide T10 "one image for row reads AND transposed reads", layout (b)). Rows of a
+// non-power-of-two chunk count (W = 96: 12 chunks) XOR inside aligned groups of 4 chunks.
+template <int W>
 __device__ __forceinline__ int swz(int row, int ch) {
-  constexpr int NCH = D / 8;
-  static_assert((NCH & (NCH - 1)) == 0, "power-of-two chunks per row");
-  const int f = (((row & 3) << 2) | ((row >> 2) & 3)) & (NCH - 1);
-  return row * D + ((ch ^ f) << 3);
+  constexpr int NCH = W / 8;
+  constexpr int MASK = (NCH & (NCH - 1)) == 0 ? NCH - 1 : 3;
+  const int f = (((row & 3) << 2) | ((row >> 2) & 3)) & MASK;
+  return row * W + ((ch ^ f) << 3);
 }
 
 // dS^T image [keys][32 queries] bf16 (64-B rows): 8-byte unit c4 of row `row`, XOR-swizzled
@@ -145,13 +152,16 @@ template <int D, bool CAUSAL, int NW, int HP>
 __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
   constexpr int NT = 64 * NW, BQ = 32 * NW / HP, BK = kFwdKeys;
   constexpr int WPH = NW / HP;  // waves per head
-  constexpr int NCH = D / 8;
+  constexpr int DP = attn_dp<D>();  // LDS row width (D + zero pad to the 32-column tiles)
+  constexpr int NCH = DP / 8;       // 16-B chunks per LDS row
+  constexpr int NCHL = D / 8;       // of which loaded from memory
   constexpr int KS = D / 16;
-  constexpr int DT = D / 32;
-  constexpr int CPT = BK * NCH / NT;  // 16-B chunks per thread per K (or V) tile
+  constexpr int DT = DP / 32;
+  constexpr int CPT = (BK * NCH + NT - 1) / NT;  // 16-B chunks per thread per K (or V) tile
+  constexpr bool CPT_EXACT = (BK * NCH) % NT == 0;
   static_assert(CPT >= 1, "K/V tile smaller than the workgroup");
-  __shared__ __attribute__((aligned(16))) bf16_t Kb[2][BK * D];
-  __shared__ __attribute__((aligned(16))) bf16_t Vb[2][BK * D];
+  __shared__ __attribute__((aligned(16))) bf16_t Kb[2][BK * DP];
+  __shared__ __attribute__((aligned(16))) bf16_t Vb[2][BK * DP];
 
   // readfirstlane: the wave index is wave-uniform, so everything derived from it (key / query
   // ranges, activity and mask flags) stays in SGPRs and its branches are scalar
@@ -205,7 +215,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
       const int ci = tid + NT * c;
       const int row = ci / NCH, ch = ci % NCH;
       const int key = kt + row;
-      if (key < p.Tk) {
+      if (key < p.Tk && ch < NCHL && (CPT_EXACT || ci < BK * NCH)) {
         kreg[c] = load_bf16x8(kp + key * p.k_st + ch * 8);
         vreg[c] = load_bf16x8(vp + key * p.v_st + ch * 8);
       } else {
@@ -219,13 +229,16 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
 #pragma unroll
     for (int c = 0; c < CPT; ++c) {
       const int ci = tid + NT * c;
+      if (!CPT_EXACT && ci >= BK * NCH) continue;
       const int row = ci / NCH, ch = ci % NCH;
       bf16x8 kv = kreg[c];
-      if (rope)
-        kv = rope_rot_chunk<NCH>(kv, ch, kt + row < p.Tk, static_cast<int64_t>(b) * p.Tk + kt + row,
-                                 kt + row, p.rope_cos, p.rope_sin, p.rope_pos);
-      store_bf16x8(&Kb[buf][swz<D>(row, ch)], kv);
-      store_bf16x8(&Vb[buf][swz<D>(row, ch)], vreg[c]);
+      if constexpr (DP == D) {  // RoPE on load: full rotary only (the host checks rot == D)
+        if (rope)
+          kv = rope_rot_chunk<NCH>(kv, ch, kt + row < p.Tk, static_cast<int64_t>(b) * p.Tk + kt + row,
+                                   kt + row, p.rope_cos, p.rope_sin, p.rope_pos);
+      }
+      store_bf16x8(&Kb[buf][swz<DP>(row, ch)], kv);
+      store_bf16x8(&Vb[buf][swz<DP>(row, ch)], vreg[c]);
     }
   };
 
@@ -241,7 +254,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) qv[s][j] = bf2f(raw[j]);
     }
-    if (rope && qi < p.Tq) {
+    if (DP == D && rope && qi < p.Tq) {
       // RoPE on load: fragment s (columns 16s + 8h + j) pairs with fragment s + KS/2 (+ D/2)
       const int pos = p.rope_pos ? p.rope_pos[static_cast<int64_t>(b) * p.Tq + qi] : qi;
       const float* cp = p.rope_cos + static_cast<int64_t>(pos) * (D / 2) + 8 * h;
@@ -293,7 +306,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
         sacc[st] = f32x16{};
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
-          const s16x8 a = *reinterpret_cast<const s16x8*>(Ks + swz<D>(32 * st + l32, 2 * s + h));
+          const s16x8 a = *reinterpret_cast<const s16x8*>(Ks + swz<DP>(32 * st + l32, 2 * s + h));
           sacc[st] = mfma32(a, qf[s], sacc[st]);
         }
       }
@@ -362,7 +375,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
         for (int st = 0; st < 2; ++st) {
 #pragma unroll
           for (int s = 0; s < 2; ++s) {
-            const s16x8 a = tr_frag_perm<D>(Vs, 32 * st + 16 * s + 4 * h, c0, lane);
+            const s16x8 a = tr_frag_perm<DP>(Vs, 32 * st + 16 * s + 4 * h, c0, lane);
             o[dt] = mfma32(a, pf[st][s], o[dt]);
           }
         }
@@ -394,7 +407,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
         const auto rx = __builtin_amdgcn_permlane32_swap(a.x, c.x, false, false);
         const auto ry = __builtin_amdgcn_permlane32_swap(a.y, c.y, false, false);
         const int d = 32 * dt + 8 * g4 + 8 * h;
-        *reinterpret_cast<uint4*>(op + d) = make_uint4(rx[0], ry[0], rx[1], ry[1]);
+        if (d < D) *reinterpret_cast<uint4*>(op + d) = make_uint4(rx[0], ry[0], rx[1], ry[1]);
       }
     }
     if (h == 0) {
@@ -416,13 +429,13 @@ __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(const bf16_t* __res
                                                               float* __restrict__ delta) {
   // delta[row] = <O[row], dO[row]>: D/8 lanes x 16-B loads per row (16 lanes at D = 128),
   // 64 / (D/8) rows per wave, shuffle reduction inside the lane group
-  const int lpr = D >> 3;  // lanes per row (power of two: 8 or 16)
+  const int lpr = D <= 64 ? 8 : 16;  // lanes per row (power of two; D = 80: 10 of 16 load)
   const int lane = threadIdx.x & 63;
   const int64_t row = (blockIdx.x * 4ll + (threadIdx.x >> 6)) * (64 / lpr) + lane / lpr;
   const int c = (lane % lpr) * 8;
   float acc = 0.f;
   const bool ok = row < static_cast<int64_t>(B) * H * T;
-  if (ok) {
+  if (ok && c < D) {
     const int t = static_cast<int>(row % T);
     const int64_t bh = row / T;
     const int hh = static_cast<int>(bh % H), b = static_cast<int>(bh / H);
@@ -477,15 +490,18 @@ __device__ __forceinline__ void bwd_q_range(int k0, int Tq, int causal_off, int 
 template <int D, bool CAUSAL>
 __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnBwdParams p) {
   constexpr int BKV = kAttnBwdKeys, BQ = kAttnBwdQRows;
-  constexpr int NCH = D / 8;
+  constexpr int DP = attn_dp<D>();  // LDS row width (zero-padded to the 32-column tiles)
+  constexpr int NCH = DP / 8;
+  constexpr int NCHL = D / 8;       // chunks loaded from memory
   constexpr int KS = D / 16;
-  constexpr int DT = D / 32;
-  constexpr int QCPT = BQ * NCH / 256;  // 16-B chunks per thread per [32][D] tile
+  constexpr int DT = DP / 32;
+  constexpr int QCPT = (BQ * NCH + 255) / 256;  // 16-B chunks per thread per [32][DP] tile
+  constexpr bool Q_EXACT = (BQ * NCH) % 256 == 0;
   static_assert(QCPT >= 1 && BKV == 256 && BQ == 32, "tile geometry");
-  __shared__ __attribute__((aligned(16))) bf16_t Ks[BKV * D];
-  __shared__ __attribute__((aligned(16))) bf16_t Vs[BKV * D];
-  __shared__ __attribute__((aligned(16))) bf16_t Qs[BQ * D];
-  __shared__ __attribute__((aligned(16))) bf16_t dOs[BQ * D];
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[BKV * DP];
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[BKV * DP];
+  __shared__ __attribute__((aligned(16))) bf16_t Qs[BQ * DP];
+  __shared__ __attribute__((aligned(16))) bf16_t dOs[BQ * DP];
   __shared__ __attribute__((aligned(16))) bf16_t dSs[BKV * BQ];
 
   // readfirstlane: the wave index is wave-uniform, so everything derived from it (key / query
@@ -515,13 +531,15 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnBwdParams p) {
       const int ci = tid + 256 * c;
       const int row = ci / NCH, ch = ci % NCH;
       const int key = k0 + row;
-      const bool in = key < p.Tk;
+      const bool in = key < p.Tk && ch < NCHL;
       bf16x8 kv = in ? load_bf16x8(kp + key * p.k_st + ch * 8) : bf16x8{};
-      if (rope_in)
-        kv = rope_rot_chunk<NCH>(kv, ch, in, static_cast<int64_t>(b) * p.Tk + key, key, p.rope_cos,
-                                 p.rope_sin, p.rope_pos);
-      store_bf16x8(Ks + swz<D>(row, ch), kv);
-      store_bf16x8(Vs + swz<D>(row, ch), in ? load_bf16x8(vp + key * p.v_st + ch * 8) : bf16x8{});
+      if constexpr (DP == D) {
+        if (rope_in)
+          kv = rope_rot_chunk<NCH>(kv, ch, in, static_cast<int64_t>(b) * p.Tk + key, key, p.rope_cos,
+                                   p.rope_sin, p.rope_pos);
+      }
+      store_bf16x8(Ks + swz<DP>(row, ch), kv);
+      store_bf16x8(Vs + swz<DP>(row, ch), in ? load_bf16x8(vp + key * p.v_st + ch * 8) : bf16x8{});
     }
   }
 
@@ -543,7 +561,10 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnBwdParams p) {
     for (int c = 0; c < QCPT; ++c) {
       const int ci = tid + 256 * c;
       const int row = ci / NCH, ch = ci % NCH;
-      if (qt + BQ <= p.Tq) {  // full tile (wave-uniform)
+      if ((!Q_EXACT && ci >= BQ * NCH) || ch >= NCHL) {  // pad columns (D = 80): zero
+        qreg[c] = bf16x8{};
+        dreg[c] = bf16x8{};
+      } else if (qt + BQ <= p.Tq) {  // full tile (wave-uniform)
         qreg[c] = load_bf16x8(qp + (qt + row) * p.q_st + ch * 8);
         dreg[c] = load_bf16x8(dop + (qt + row) * p.do_st + ch * 8);
       } else {  // rows past Tq: loaded clamped (unpredicated), zeroed
@@ -560,9 +581,10 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnBwdParams p) {
 #pragma unroll
     for (int c = 0; c < QCPT; ++c) {
       const int ci = tid + 256 * c;
+      if (!Q_EXACT && ci >= BQ * NCH) continue;
       const int row = ci / NCH, ch = ci % NCH;
-      store_bf16x8(Qs + swz<D>(row, ch), qreg[c]);
-      store_bf16x8(dOs + swz<D>(row, ch), dreg[c]);
+      store_bf16x8(Qs + swz<DP>(row, ch), qreg[c]);
+      store_bf16x8(dOs + swz<DP>(row, ch), dreg[c]);
     }
   };
 
@@ -571,19 +593,19 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnBwdParams p) {
   const int i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3, half16 = (lane >> 4) & 1;
   int roff[KS];  // row reads: row l32 (+16k), chunk 2s + h
 #pragma unroll
-  for (int s = 0; s < KS; ++s) roff[s] = swz<D>(l32, 2 * s + h);
+  for (int s = 0; s < KS; ++s) roff[s] = swz<DP>(l32, 2 * s + h);
   int toff[DT][2];  // tr_frag_perm: rows 4h + qq and 4h + 8 + qq (+16k), columns 32dt + 16*half16
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt) {
     const int ch = 4 * dt + 2 * half16 + (pp >> 1), sub = (pp & 1) * 4;
-    toff[dt][0] = swz<D>(4 * h + qq, ch) + sub;
-    toff[dt][1] = swz<D>(4 * h + 8 + qq, ch) + sub;
+    toff[dt][0] = swz<DP>(4 * h + qq, ch) + sub;
+    toff[dt][1] = swz<DP>(4 * h + 8 + qq, ch) + sub;
   }
   int noff[2];  // phase B K reads (tr_frag_nat): rows 8h + qq and 8h + 4 + qq (+16s), dt = w
   {
     const int ch = 4 * (w % DT) + 2 * half16 + (pp >> 1), sub = (pp & 1) * 4;
-    noff[0] = swz<D>(8 * h + qq, ch) + sub;
-    noff[1] = swz<D>(8 * h + 4 + qq, ch) + sub;
+    noff[0] = swz<DP>(8 * h + qq, ch) + sub;
+    noff[1] = swz<DP>(8 * h + 4 + qq, ch) + sub;
   }
   int doff[2][2];  // phase B dS^T reads: rows 16*par + 8h + qq (+4) (+32k), query unit colc4
   {
@@ -699,8 +721,8 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnBwdParams p) {
       pb0[j] = pb1[j] = sb0[j] = sb1[j] = s16x8{};
       if (act[j]) {
         f32x16 sacc = f32x16{}, dpacc = f32x16{};
-        const bf16_t* Kj = Ks + (64 * w + 32 * j) * D;
-        const bf16_t* Vj = Vs + (64 * w + 32 * j) * D;
+        const bf16_t* Kj = Ks + (64 * w + 32 * j) * DP;
+        const bf16_t* Vj = Vs + (64 * w + 32 * j) * DP;
         s16x8 fa[2], fb[2], fc[2], fd[2];
         auto ld_sdp = [&](int s, int sl) {
           fa[sl] = *reinterpret_cast<const s16x8*>(Qs + roff[s]);
@@ -749,9 +771,9 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnBwdParams p) {
     s16x8 ta[2], tb[2], tc[2], td[2];
     auto ld_kv = [&](int dt, int sl) {
       ta[sl] = cat4(tr_read(dOs + toff[dt][0]), tr_read(dOs + toff[dt][1]));
-      tb[sl] = cat4(tr_read(dOs + 16 * D + toff[dt][0]), tr_read(dOs + 16 * D + toff[dt][1]));
+      tb[sl] = cat4(tr_read(dOs + 16 * DP + toff[dt][0]), tr_read(dOs + 16 * DP + toff[dt][1]));
       tc[sl] = cat4(tr_read(Qs + toff[dt][0]), tr_read(Qs + toff[dt][1]));
-      td[sl] = cat4(tr_read(Qs + 16 * D + toff[dt][0]), tr_read(Qs + 16 * D + toff[dt][1]));
+      td[sl] = cat4(tr_read(Qs + 16 * DP + toff[dt][0]), tr_read(Qs + 16 * DP + toff[dt][1]));
     };
     ld_kv(0, 0);
     __builtin_amdgcn_sched_barrier(0);
@@ -792,14 +814,14 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnBwdParams p) {
       if (it + 2 < n_iter) prefetch(it + 2);
       load_rows(it + 1);
     }
-    if (w < DT) {  // dQ partial; D = 64: waves 2, 3 have no column slice
+    if (w < DT) {  // dQ partial; D = 64: waves 2, 3 have no column slice (D = 80: wave 3)
       const int dt = w;
       f32x16 acc = f32x16{};
       s16x8 qa[2], qb[2];
       auto ld_dq = [&](int s, int sl) {  // A = dS (rows 16s + 8h..), B = K (rows 16s + 8h..)
         const bf16_t* dsr = dSs + (s >> 1) * 32 * 32;
         qa[sl] = cat4(tr_read(dsr + doff[s & 1][0]), tr_read(dsr + doff[s & 1][1]));
-        qb[sl] = cat4(tr_read(Ks + 16 * s * D + noff[0]), tr_read(Ks + 16 * s * D + noff[1]));
+        qb[sl] = cat4(tr_read(Ks + 16 * s * DP + noff[0]), tr_read(Ks + 16 * s * DP + noff[1]));
       };
       ld_dq(0, 0);
 #pragma unroll
@@ -814,10 +836,12 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnBwdParams p) {
       const int64_t rs = static_cast<int64_t>(p.Hq) * D;
       float* sp = p.dq_slab + ((static_cast<int64_t>(kb) * p.B + b) * p.slab_rows + qt) * rs +
                   static_cast<int64_t>(hq) * D + 32 * dt + l32;
+      if (32 * dt + l32 < D) {  // (the pad columns of D = 80 are not stored)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int r = (i & 3) + 8 * (i >> 2) + 4 * h;
-        sp[r * rs] = acc[i] * p.scale;
+        for (int i = 0; i < 16; ++i) {
+          const int r = (i & 3) + 8 * (i >> 2) + 4 * h;
+          sp[r * rs] = acc[i] * p.scale;
+        }
       }
     }
     __syncthreads();  // next Q / dO tile visible; every wave is done reading dS
@@ -842,10 +866,11 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnBwdParams p) {
           const uint32_t c1 = pack2bf(x[4 * g4 + 6] * sc, x[4 * g4 + 7] * sc);
           const auto r0 = __builtin_amdgcn_permlane32_swap(a0, c0, false, false);
           const auto r1 = __builtin_amdgcn_permlane32_swap(a1, c1, false, false);
-          *reinterpret_cast<uint4*>(dst + 32 * dt + 8 * g4 + 8 * h) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
+          if (32 * dt + 8 * g4 + 8 * h < D)
+            *reinterpret_cast<uint4*>(dst + 32 * dt + 8 * g4 + 8 * h) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
         }
       };
-      if (p.rope_cos != nullptr) {
+      if (DP == D && p.rope_cos != nullptr) {
         // fused RoPE backward: column d < D/2 pairs with d + D/2 = the same register of column
         // tile dt + DT/2 in this lane (un-rotation: lo = a c + b s, hi = b c - a s), applied to
         // register copies on the way out (writing the accumulators back spilled in the loop)
@@ -885,6 +910,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnBwdParams p) {
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
           const int d = 32 * dt + 8 * g4 + 4 * h;
+          if (d >= D) continue;
           *reinterpret_cast<f32x4*>(dkp + d) = f32x4{dk[j][dt][4 * g4], dk[j][dt][4 * g4 + 1],
                                                      dk[j][dt][4 * g4 + 2], dk[j][dt][4 * g4 + 3]};
           *reinterpret_cast<f32x4*>(dvp + d) = f32x4{dv[j][dt][4 * g4], dv[j][dt][4 * g4 + 1],
@@ -1083,8 +1109,9 @@ void launch_attn_fwd(const AttnParams& p, int D, bool causal, hipStream_t st) {
   if (p.B == 0 || p.Tq == 0) return;
   switch (D) {
     case 64: fwd_dispatch<64>(p, causal, st); break;
+    case 80: fwd_dispatch<80>(p, causal, st); break;
     case 128: fwd_dispatch<128>(p, causal, st); break;
-    default: throw std::invalid_argument("attn_fwd: head_dim must be 64 or 128");
+    default: throw std::invalid_argument("attn_fwd: head_dim must be 64, 80 or 128");
   }
 }
 
@@ -1093,7 +1120,7 @@ void launch_attn_bwd_delta(const bf16_t* o, const bf16_t* dout, int64_t o_sb, in
                            int H, int T, int D, float* delta, hipStream_t st) {
   const int64_t rows = static_cast<int64_t>(B) * H * T;
   if (rows == 0) return;
-  const int64_t rows_per_block = 4 * (64 / (D / 8));
+  const int64_t rows_per_block = 4 * (64 / (D <= 64 ? 8 : 16));  // as attn_bwd_delta_kernel
   attn_bwd_delta_kernel<<<static_cast<unsigned>((rows + rows_per_block - 1) / rows_per_block), 256, 0, st>>>(
       o, dout, o_sb, o_st, o_sh, do_sb, do_st, do_sh, B, H, T, D, delta);
 }
@@ -1110,8 +1137,9 @@ void launch_attn_bwd(const AttnBwdParams& p, int D, bool causal, hipStream_t st)
   if (p.B == 0 || p.Tq == 0 || p.Tk == 0) return;
   switch (D) {
     case 64: bwd_dispatch<64>(p, causal, st); break;
+    case 80: bwd_dispatch<80>(p, causal, st); break;
     case 128: bwd_dispatch<128>(p, causal, st); break;
-    default: throw std::invalid_argument("attn_bwd: head_dim must be 64 or 128");
+    default: throw std::invalid_argument("attn_bwd: head_dim must be 64, 80 or 128");
   }
 }
 

@@ -374,7 +374,7 @@ std::tuple<at::Tensor, at::Tensor> attn_fwd(const at::Tensor& q, const at::Tenso
   same_device(q, v);
   const int64_t B = q.size(0), Tq = q.size(1), Hq = q.size(2), D = q.size(3);
   const int64_t Tk = k.size(1), Hkv = k.size(2);
-  TORCH_CHECK(D == 64 || D == 128, "head_dim must be 64 or 128 (pad others)");
+  TORCH_CHECK(D == 64 || D == 80 || D == 128, "head_dim must be 64, 80 or 128 (pad others)");
   TORCH_CHECK(k.size(0) == B && v.size(0) == B && k.size(3) == D && v.size(3) == D &&
                   v.size(1) == Tk && v.size(2) == Hkv,
               "k/v shapes");
@@ -403,6 +403,7 @@ std::tuple<at::Tensor, at::Tensor> attn_fwd(const at::Tensor& q, const at::Tenso
   p.seg_start = seg_ptr(segs, B, Tq, Tk, causal, causal_off, q, 0);
   rope_args(rope_cos, rope_sin, rope_pos, q, B, Tq, Tk, D, causal_off, &p.rope_cos, &p.rope_sin,
             &p.rope_pos);
+  TORCH_CHECK(p.rope_cos == nullptr || D != 80, "RoPE on load: full-rotary head dims 64 / 128 only");
   if (q_rot && q_rot->defined()) {
     TORCH_CHECK(p.rope_cos != nullptr, "q_rot needs the rotary tables");
     check_bthd(*q_rot, "q_rot");
@@ -462,7 +463,7 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k,
   check_f32(lse2, "lse2");
   const int64_t B = q.size(0), Tq = q.size(1), Hq = q.size(2), D = q.size(3);
   const int64_t Tk = k.size(1), Hkv = k.size(2);
-  TORCH_CHECK(D == 64 || D == 128, "head_dim must be 64 or 128");
+  TORCH_CHECK(D == 64 || D == 80 || D == 128, "head_dim must be 64, 80 or 128");
   TORCH_CHECK(dout.sizes() == q.sizes() && o.sizes() == q.sizes() && dq.sizes() == q.sizes(),
               "dout/o/dq shape");
   TORCH_CHECK(dk.sizes() == k.sizes() && dv.sizes() == v.sizes(), "dk/dv shape");
@@ -516,6 +517,7 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k,
   rope_args(rope_cos, rope_sin, rope_pos, q, B, Tq, Tk, D, causal_off, &p.rope_cos, &p.rope_sin,
             &p.rope_pos);
   TORCH_CHECK(!rope_inputs || p.rope_cos != nullptr, "rope_inputs needs the rotary tables");
+  TORCH_CHECK(p.rope_cos == nullptr || D != 80, "fused RoPE backward: full-rotary head dims 64 / 128 only");
   p.rope_inputs = rope_inputs ? 1 : 0;
   launch_attn_bwd(p, static_cast<int>(D), causal, st);
   launch_attn_dq_reduce(p.dq_slab, static_cast<int>(nkb), static_cast<int>(B), static_cast<int>(Tq),

@@ -8,6 +8,7 @@
 #include <tuple>
 
 #include "bind_util.h"
+#include "skinny_params.h"
 
 namespace dla {
 
@@ -40,6 +41,73 @@ void launch_skinny_glu_norm(const bf16_t*, const bf16_t*, const bf16_t*, bf16_t*
 bool skinny_glu_ks_ok(int N, int K);
 void launch_skinny_glu_ks(const bf16_t*, int64_t, const bf16_t*, int64_t, bf16_t*, int64_t, int,
                           int, int, hipStream_t);
+
+void launch_skinny_ks_fused(const bf16_t*, int64_t, const bf16_t*, int64_t, bf16_t*, int64_t, int,
+                            int, int, const KsFuse&, bool, bool, hipStream_t);
+void launch_skinny_glu_normin(const bf16_t*, int64_t, const bf16_t*, int64_t, bf16_t*, int64_t, int,
+                              int, int, const KsFuse&, hipStream_t);
+
+// Fused decode-layer projection (M <= 16, skinny.hip KsFuse):
+//   * res given: returns (s = bf16(bf16(x w^T) + res) [M, N], ssq [16, N/16] fp32 partial sums of
+//     s^2 per (row, 16-column workgroup)) -- the o / down projection producing the residual;
+//   * ssq_in given: x is a residual stream s and w a weight with the RMSNorm weight folded in
+//     (w o norm_w, ops/decode.py): returns rstd[m] * (s w^T), rstd = rsqrt(sum(ssq_in[m]) / K +
+//     eps) -- RMSNorm(s) @ W^T without a norm launch: the qkv projection, or with `glu` the
+//     gate|up projection with the SwiGLU epilogue (w = [gate; up], output [M, F]).
+std::tuple<at::Tensor, at::Tensor> skinny_fused(const at::Tensor& x, const at::Tensor& w,
+                                                const c10::optional<at::Tensor>& res,
+                                                const c10::optional<at::Tensor>& ssq_in, double eps,
+                                                bool glu) {
+  check_bf16(x, "x");
+  check_bf16(w, "w");
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.stride(1) == 1 && w.stride(1) == 1 &&
+                  x.stride(0) % 8 == 0 && w.stride(0) % 8 == 0,
+              "x [M, K] / w [N, K]: unit inner stride, 16-byte aligned rows");
+  const int64_t M = x.size(0), N = w.size(0), K = w.size(1);
+  TORCH_CHECK(M >= 1 && M <= 16 && x.size(1) == K, "fused skinny: 1 <= M <= 16, x [M, K]");
+  TORCH_CHECK(N < (1ll << 30) && K < (1ll << 30), "shape too large");
+  check_aligned16(x, "x");
+  check_aligned16(w, "w");
+  same_device(x, w);
+  const bool nin = ssq_in.has_value();
+  KsFuse fz{};
+  if (nin) {
+    const at::Tensor& sq = *ssq_in;
+    check_cuda(sq, "ssq_in");
+    TORCH_CHECK(sq.scalar_type() == at::kFloat && sq.dim() == 2 && sq.size(0) == 16 && sq.is_contiguous() &&
+                    sq.size(1) >= 1 && sq.size(1) <= 512,
+                "ssq_in fp32 [16, nbp <= 512] contiguous");
+    same_device(x, sq);
+    fz.ssq_in = sq.data_ptr<float>();
+    fz.nbp = static_cast<int>(sq.size(1));
+    fz.eps = static_cast<float>(eps);
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  if (glu) {
+    TORCH_CHECK(nin && !res.has_value(), "glu: normalised input, no residual");
+    TORCH_CHECK(N % 128 == 0 && M * (K + 8) * 2 <= 148 * 1024, "glu: 2F % 128 == 0, x fits LDS");
+    auto m = at::empty({M, N / 2}, x.options());
+    launch_skinny_glu_normin(cbp(x), x.stride(0), cbp(w), w.stride(0), bp(m), m.stride(0), (int)M,
+                             (int)N, (int)K, fz, cur_stream(x));
+    return {m, at::Tensor()};
+  }
+  TORCH_CHECK(skinny_use_ksplit((int)N, (int)K), "fused skinny: N < 16384, N % 16 == 0, K % 1024 == 0");
+  auto y = at::empty({M, N}, x.options());
+  at::Tensor ssq;
+  if (res.has_value()) {
+    const at::Tensor& r = *res;
+    check_bf16(r, "res");
+    TORCH_CHECK(r.dim() == 2 && r.size(0) == M && r.size(1) == N && r.stride(1) == 1, "res [M, N]");
+    same_device(x, r);
+    fz.res = cbp(r);
+    fz.ldr = r.stride(0);
+    ssq = at::empty({16, N / 16}, x.options().dtype(at::kFloat));
+    fz.ssq_out = ssq.data_ptr<float>();
+  }
+  launch_skinny_ks_fused(cbp(x), x.stride(0), cbp(w), w.stride(0), bp(y), y.stride(0), (int)M,
+                         (int)N, (int)K, fz, res.has_value(), nin, cur_stream(x));
+  return {y, ssq};
+}
 
 // Decode gate|up with the SwiGLU epilogue on the in-workgroup split-K kernel: w = [gate; up]
 // (2F rows) -> m = silu(x gate^T) * (x up^T) [M, F], one workgroup per 16 features.
@@ -329,6 +397,7 @@ TORCH_LIBRARY_FRAGMENT(dla, m) {
   m.def("skinny_gemm(Tensor x, Tensor w, Tensor(a!) counters, bool swiglu, bool glu_out=False) -> Tensor");
   m.def("skinny_glu_norm(Tensor x, Tensor res, Tensor norm_w, float eps, Tensor w) -> (Tensor, Tensor)");
   m.def("skinny_glu_ks(Tensor x, Tensor w) -> Tensor");
+  m.def("skinny_fused(Tensor x, Tensor w, Tensor? res, Tensor? ssq_in, float eps, bool glu) -> (Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(dla, CUDA, m) {
@@ -339,4 +408,5 @@ TORCH_LIBRARY_IMPL(dla, CUDA, m) {
   m.impl("skinny_gemm", &dla::skinny_gemm);
   m.impl("skinny_glu_norm", &dla::skinny_glu_norm);
   m.impl("skinny_glu_ks", &dla::skinny_glu_ks);
+  m.impl("skinny_fused", &dla::skinny_fused);
 }

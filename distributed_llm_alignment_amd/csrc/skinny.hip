@@ -20,6 +20,7 @@
 //     ticket counter, re-armed by that workgroup: no memset, graph-capture safe) sums them in a
 //     FIXED order: deterministic.
 #include "common.h"
+#include "skinny_params.h"
 
 #include <cstdlib>
 
@@ -78,14 +79,63 @@ struct SkNorm {
   float eps;
 };
 
-template <bool SWIGLU, bool GLU_OUT = false, bool NORM = false, bool NTW = false>
+// Decode-layer fusion of the residual add + RMSNorm across two launches (no norm launch):
+//   RES (producer, the o / down projections): the epilogue writes the new residual stream
+//       s = bf16(bf16(x W^T) + res) instead of the projection, plus per-(row, workgroup) partial
+//       sums of s^2 over the workgroup's 16 columns (fixed order) into ssq_out [16][gridDim.x];
+//   NIN (consumer, the qkv / gate|up projections of the next sublayer): RMSNorm(s) W^T =
+//       rstd[m] * (s (W o w)^T) -- the per-row rsqrt(mean(s^2) + eps) factors out of the GEMM and
+//       the norm weight w is folded into a cached copy of W (ops/decode.py). So the consumer is a
+//       plain GEMM on s whose epilogue scales row m by rstd[m], computed from the producer's
+//       partials (prefetched at kernel start, reduced in fixed order at the end): the weight
+//       stream starts at once, and no per-element normalisation is needed.
+// Deterministic (eager == graph); the rounding differs from the separate-norm path (h is never
+// rounded to bf16; W o w is), so the two agree to bf16 accuracy, not bitwise.
+
+// prefetch (kernel start) of this wave's two rows' partial sums of squares: lane-strided, up to
+// 8 values per row (nbp <= 512)
+struct KsPart {
+  float v[2][8];
+};
+
+__device__ __forceinline__ KsPart ks_part_load(const KsFuse& fz, int M, int wave, int lane) {
+  KsPart p;
+#pragma unroll
+  for (int rr = 0; rr < 2; ++rr) {
+    const int m = 2 * wave + rr;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int i = lane + 64 * j;
+      p.v[rr][j] = (m < M && i < fz.nbp) ? fz.ssq_in[m * fz.nbp + i] : 0.f;
+    }
+  }
+  return p;
+}
+
+// rows 2w, 2w+1 per wave: rstd = rsqrt(sum / K + eps) (in-lane sum in order, then butterfly)
+__device__ __forceinline__ void ks_rstd(const KsPart& p, const KsFuse& fz, int M, int K, int wave,
+                                        int lane, float* rstd_s) {
+#pragma unroll
+  for (int rr = 0; rr < 2; ++rr) {
+    const int m = 2 * wave + rr;
+    float t = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) t += p.v[rr][j];
+    t = wave_sum(t);
+    if (lane == 0 && m < M) rstd_s[m] = rsqrtf(t / static_cast<float>(K) + fz.eps);
+  }
+}
+
+template <bool SWIGLU, bool GLU_OUT = false, bool NORM = false, bool NTW = false, bool NPRE = false>
 __global__ __launch_bounds__(64 * kSkWaves) void skinny_gemm_kernel(
     const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ W, int64_t ldw,
     bf16_t* __restrict__ y, int64_t ldy, float* __restrict__ ws, unsigned* __restrict__ counters,
-    int M, int N, int K, int kc, SkNorm nrm = SkNorm{}) {
+    int M, int N, int K, int kc, SkNorm nrm = SkNorm{}, KsFuse fz = KsFuse{}) {
   extern __shared__ __attribute__((aligned(16))) bf16_t xs[];
   // NORM statistics (512 B, a multiple of 16 so the dynamic LDS base stays 16-byte aligned)
   __shared__ __attribute__((aligned(16))) float nred[16][8];
+  // NPRE: per-row rstd from the producer's partial sums (see KsFuse)
+  __shared__ __attribute__((aligned(16))) float rstd_p[16];
   const int S = gridDim.y;
   const int s = blockIdx.y;
   const int k0 = s * kc;
@@ -112,6 +162,8 @@ __global__ __launch_bounds__(64 * kSkWaves) void skinny_gemm_kernel(
     }
   }
 
+  KsPart part{};
+  if constexpr (NPRE) part = ks_part_load(fz, M, wave, lane);  // reduced in the epilogue
   // ---- stage x[:, k0:k0+klen] (or swiglu(gu) of it) into LDS: 8 independent 16-byte loads per
   // thread per pass (all issued before the first LDS store, so the pass costs one latency)
   const int vecs = klen >> 3;
@@ -241,6 +293,12 @@ __global__ __launch_bounds__(64 * kSkWaves) void skinny_gemm_kernel(
   if constexpr (GLU_OUT) {
     __shared__ float glu[2][16][64];  // [gate|up][m][column within the block]
     const int half = wave >> 2, col = (wave & 3) * 16 + r;
+    if constexpr (NPRE) {  // RMSNorm row factor of the folded-weight GEMM (see KsFuse)
+      ks_rstd(part, fz, M, K, wave, lane, rstd_p);
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i] *= (4 * q + i < M) ? rstd_p[4 * q + i] : 0.f;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) glu[half][4 * q + i][col] = bf2f(f2bf(acc[i]));
     __syncthreads();
@@ -400,12 +458,15 @@ constexpr int kKsChunk = 32 * kKsUnroll;
 // (larger decode batches, e.g. the reference's 64 rollouts per RLHF step on one GPU); UNR k-steps
 // per ring slot (4 at MT = 1; 2 above, which keeps the x fragments at ~110 VGPRs for MT = 4, four
 // waves per SIMD).
-template <int DEPTH, bool NT, bool GLU, int MT = 1, int UNR = kKsUnroll>
+template <int DEPTH, bool NT, bool GLU, int MT = 1, int UNR = kKsUnroll, bool RES = false, bool NIN = false>
 __global__ __launch_bounds__(512) void skinny_ksplit_kernel(
     const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ W, int64_t ldw,
-    bf16_t* __restrict__ y, int64_t ldy, int M, int N, int K) {
+    bf16_t* __restrict__ y, int64_t ldy, int M, int N, int K, KsFuse fz = KsFuse{}) {
   constexpr int CH = 32 * UNR;  // k per ring slot
+  static_assert(!(RES || NIN) || (MT == 1 && !GLU), "fused residual / norm: M <= 16, plain output");
   __shared__ float red[8][4 * MT][64];
+  __shared__ float rstd_s[16];
+  __shared__ float sqs[16][16];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = lane & 15, q = lane >> 4;
   const int n0 = GLU ? (wave < 4 ? 0 : N >> 1) + blockIdx.x * 16 : blockIdx.x * 16;
@@ -437,6 +498,8 @@ __global__ __launch_bounds__(512) void skinny_ksplit_kernel(
 #pragma unroll
   for (int j = 0; j < DEPTH; ++j)
     if (j < nchunks) load(j, j);
+  KsPart part{};
+  if constexpr (NIN) part = ks_part_load(fz, M, wave, lane);  // reduced in the epilogue
   f32x4 acc[MT];
 #pragma unroll
   for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -458,6 +521,7 @@ __global__ __launch_bounds__(512) void skinny_ksplit_kernel(
   for (int t = 0; t < MT; ++t)
 #pragma unroll
     for (int i = 0; i < 4; ++i) red[wave][4 * t + i][lane] = acc[t][i];
+  if constexpr (NIN) ks_rstd(part, fz, M, K, wave, lane, rstd_s);
   __syncthreads();
   for (int e = threadIdx.x; e < 256 * MT; e += 512) {
     const int ti = e >> 6, l = e & 63;  // ti = 4 t + i
@@ -476,9 +540,66 @@ __global__ __launch_bounds__(512) void skinny_ksplit_kernel(
       float t = 0.f;
 #pragma unroll
       for (int w = 0; w < 8; ++w) t += red[w][ti][l];
-      if (m < M) y[m * ldy + n] = f2bf(t);
+      if constexpr (NIN) t *= m < M ? rstd_s[m] : 0.f;
+      if constexpr (RES) {
+        if (m < M) {
+          const float sv = bf2f(f2bf(bf2f(f2bf(t)) + bf2f(static_cast<bf16_t>(fz.res[m * fz.ldr + n]))));
+          y[m * ldy + n] = f2bf(sv);
+          sqs[m][l & 15] = sv * sv;
+        }
+      } else {
+        if (m < M) y[m * ldy + n] = f2bf(t);
+      }
     }
   }
+  if constexpr (RES) {  // per-row partial sum of squares over this workgroup's 16 columns
+    __syncthreads();
+    if (threadIdx.x < M) {
+      float t = 0.f;
+#pragma unroll
+      for (int c = 0; c < 16; ++c) t += sqs[threadIdx.x][c];
+      fz.ssq_out[threadIdx.x * gridDim.x + blockIdx.x] = t;
+    }
+  }
+}
+
+// fused decode-layer launches (KsFuse): the residual-producing projection and the
+// norm-consuming qkv projection on the in-workgroup split-K kernel, the gate|up GLU on the LDS
+// kernel. M <= 16.
+void launch_skinny_ks_fused(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
+                            int64_t ldy, int M, int N, int K, const KsFuse& fz, bool res, bool nin,
+                            hipStream_t st) {
+  static const int deep_k = [] {
+    const char* e = getenv("DLA_SKINNY_DEEP_K");
+    return e ? atoi(e) : 8192;
+  }();
+  const int nb = N / 16;
+  const bool deep = K >= deep_k;
+#define DLA_KSF(D, R, NI) skinny_ksplit_kernel<D, false, false, 1, kKsUnroll, R, NI><<<nb, 512, 0, st>>>(x, ldx, W, ldw, y, ldy, M, N, K, fz)
+  if (res && nin) {
+    if (deep) DLA_KSF(4, true, true); else DLA_KSF(2, true, true);
+  } else if (res) {
+    if (deep) DLA_KSF(4, true, false); else DLA_KSF(2, true, false);
+  } else if (nin) {
+    if (deep) DLA_KSF(4, false, true); else DLA_KSF(2, false, true);
+  } else {
+    if (deep) DLA_KSF(4, false, false); else DLA_KSF(2, false, false);
+  }
+#undef DLA_KSF
+}
+
+void launch_skinny_glu_normin(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
+                              int64_t ldy, int M, int N, int K, const KsFuse& fz, hipStream_t st) {
+  static bool attr_set = [] {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_gemm_kernel<false, true, false, false, true>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+    (void)hipGetLastError();
+    return true;
+  }();
+  (void)attr_set;
+  dim3 g2(N / 2 / 64, 1);
+  skinny_gemm_kernel<false, true, false, false, true><<<g2, 64 * kSkWaves, skinny_lds_bytes(M, K), st>>>(
+      x, ldx, W, ldw, y, ldy, nullptr, nullptr, M, N, K, K, SkNorm{}, fz);
 }
 
 bool skinny_use_ksplit(int N, int K) {

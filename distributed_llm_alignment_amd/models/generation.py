@@ -338,6 +338,9 @@ def generate(model: CausalLM, input_ids: torch.Tensor, attention_mask: Optional[
             _GRAPH_SLOT.pop(id(model), None)  # free the old cache before sizing a new one
     if dg is None:
         cache = KVCache(model, B, Tp + max_new_tokens, kv_start)
+    # folded RMSNorm weights of the fused decode layer are refreshed in place (never inside the
+    # captured step): a cached graph replays the same buffers with the current weights
+    ops.decode.refresh_folded_weights(model)
     h = model(input_ids, cache=cache)
     if seed is None:
         seed = int(torch.randint(0, 2 ** 62, (1,), generator=generator).item()) if generator is not None \

@@ -260,6 +260,31 @@ class DecoderLayer(nn.Module):
         self.tp_seq = None  # Megatron-SP: x / resid are this rank's [N/tp, H] token rows
         self.recompute = None  # selective activation recompute: None | "attention" | "mlp"
 
+    def decode_fused_ok(self, x) -> bool:
+        """This layer's decode step can run on the fused residual/norm kernels."""
+        cfg, at, mlp = self.cfg, self.attn, self.mlp
+        return (cfg.norm_type == "rms" and not cfg.parallel_block and isinstance(mlp, MLP)
+                and cfg.activation == "swiglu" and mlp.up_bias is None and mlp.down_bias is None
+                and at.qkv_bias is None and at.o_bias is None and at.tp is None and mlp.tp is None
+                and at.sp is None and self.ln1_b is None and self.ln2_b is None
+                and ops.decode.fused_layer_ok(x, cfg.hidden_size, at.qkv_proj, at.o_proj,
+                                              mlp.up_proj, mlp.down_proj))
+
+    def decode_fused(self, s, ssq, rope, cache, layer_idx):
+        """One decode step of the layer with no norm launch (ops.decode fused layer): `s` is the
+        residual stream after the previous layer and `ssq` its row-norm partials (None for the
+        first layer). Returns the next (s, ssq)."""
+        cfg, at, mlp = self.cfg, self.attn, self.mlp
+        if ssq is None:
+            h, _ = ops.add_norm(s, None, self.ln1_w, None, cfg.norm_eps, True)
+            qkv = _lin(h, at.qkv_proj, None)
+        else:
+            qkv = ops.decode.skinny_normed(s, ssq, self.ln1_w, cfg.norm_eps, at.qkv_proj)
+        a = cache.attend(layer_idx, qkv, rope, cfg.sliding_window if cfg.sliding_window else 0)
+        s2, ssq2 = ops.decode.skinny_residual(a, at.o_proj, s)
+        m = ops.decode.skinny_normed(s2, ssq2, self.ln2_w, cfg.norm_eps, mlp.up_proj, glu=True)
+        return ops.decode.skinny_residual(m, mlp.down_proj, s2)
+
     def forward(self, x, resid, rope, kv_start, kv_end, positions, cache=None, layer_idx=0, segs=None):
         cfg = self.cfg
         rms = cfg.norm_type == "rms"
@@ -460,6 +485,15 @@ class CausalLM(nn.Module):
     def _forward_cached(self, input_ids, attention_mask, cache):
         positions = cache.positions_for(input_ids.shape[1])
         x = self.embed_tokens(input_ids, positions)
+        if (input_ids.shape[1] == 1 and self.layer_devices is None and self.layers
+                and self.layers[0].decode_fused_ok(x)):
+            # decode step: residual add + RMSNorm folded into the neighbouring projections
+            s, ssq = x, None
+            for i, layer in enumerate(self.layers):
+                s, ssq = layer.decode_fused(s, ssq, self.rope, cache, i)
+            h, _ = ops.add_norm(s, None, self.norm_w, self.norm_b, self.cfg.norm_eps, True)
+            cache.step_done(1)
+            return h
         resid = None
         for i, layer in enumerate(self.layers):
             if self.layer_devices is not None:

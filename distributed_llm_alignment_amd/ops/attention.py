@@ -146,7 +146,7 @@ class _FusedQKVAttnFn(torch.autograd.Function):
         q2 = qkv.reshape(B * T, C)
         off = qkv.storage_offset()
         v4 = qkv.as_strided((B, T, Hkv, D), (T * C, C, D, 1), off + (Hq + Hkv) * D)
-        on_load = rot == D and FUSED_ROPE_FWD
+        on_load = rot == D and D in (64, 128) and FUSED_ROPE_FWD
         if on_load:
             # RoPE on load: the kernel rotates Q in registers and K as it stages it; the rotated
             # Q leaves as a side output only when a backward will read it
@@ -188,7 +188,7 @@ class _FusedQKVAttnFn(torch.autograd.Function):
         do4 = do.contiguous().view(B, T, Hq, D)
         dqkv = torch.empty((B, T, C), dtype=qkv.dtype, device=qkv.device)
         dv = dqkv.as_strided((B, T, Hkv, D), (T * C, C, D, 1), (Hq + Hkv) * D)
-        fused_rope = rot == D and (FUSED_ROPE_BWD or ctx.on_load)
+        fused_rope = rot == D and D in (64, 128) and (FUSED_ROPE_BWD or ctx.on_load)
         if rot > 0 and not fused_rope:  # rotated-space dq / dk, un-rotated by the RoPE backward
             dq = torch.empty((B, T, Hq, D), dtype=qkv.dtype, device=qkv.device)
             dk = torch.empty((B, T, Hkv, D), dtype=qkv.dtype, device=qkv.device)
@@ -232,6 +232,12 @@ class _AttnCoreFn(torch.autograd.Function):
         return dq, dk, dv, None, None, None, None, None, None, None
 
 
+# head dims with a native kernel tile: 64 / 128, and 80 (phi-2: Q.K^T over exactly 5 MFMA k-steps,
+# 96-wide LDS images whose 16 zero pad columns cost only the P.V / dK / dV tiles; csrc/attention.hip
+# attn_dp). Others are zero-padded to the next native size. DLA_ATTN_D80=0 pads D = 80 to 128.
+NATIVE_HEAD_DIMS = (64, 80, 128) if os.environ.get("DLA_ATTN_D80", "1") != "0" else (64, 128)
+
+
 def _pad_d(x: torch.Tensor, Dp: int) -> torch.Tensor:
     return F.pad(x, (0, Dp - x.shape[-1]))
 
@@ -246,7 +252,7 @@ def attention_core(q, k, v, scale=None, causal=True, causal_off=None, window=0, 
     if not _ext.use_native(q):
         return ref_attention(q, k, v, scale, causal, causal_off, window, kv_start, kv_end, segs)
     ks, ke, sg = _i32(kv_start), _i32(kv_end), _i32(segs)
-    if D in (64, 128):
+    if D in NATIVE_HEAD_DIMS:
         return _AttnCoreFn.apply(q, k, v, scale, causal, causal_off, window, ks, ke, sg)
     Dp = 64 if D < 64 else 128
     o = _AttnCoreFn.apply(_pad_d(q, Dp), _pad_d(k, Dp), _pad_d(v, Dp), scale, causal, causal_off,
@@ -284,14 +290,14 @@ def qkv_attention(qkv: torch.Tensor, Hq: int, Hkv: int, D: int, rope: Optional[R
         return o.reshape(B, T, Hq * D)
     ks, ke, sg = _i32(kv_start), _i32(kv_end), _i32(segs)
     pos32 = _i32(positions.reshape(-1)) if positions is not None else None
-    if D in (64, 128):
+    if D in NATIVE_HEAD_DIMS:
         if rope is not None:
             cos, sin = rope.tables(qkv.device)
         else:
             cos = sin = torch.empty(0, device=qkv.device)
         return _FusedQKVAttnFn.apply(qkv.contiguous(), cos, sin, pos32, Hq, Hkv, D, rot, scale,
                                      causal, window, ks, ke, sg)
-    # odd head dims (e.g. phi-2 D=80, partial rotary 32): HIP RoPE forward/backward on the fused
+    # other head dims (e.g. 96, 256): HIP RoPE forward/backward on the fused
     # qkv buffer (the kernels take any D % 8 == 0), then the native attention core on head dims
     # zero-padded to the next supported size
     if rope is not None and D % 8 == 0 and rot % 16 == 0:

@@ -204,3 +204,86 @@ def ref_skinny_linear(x: torch.Tensor, weight: torch.Tensor, swiglu: bool = Fals
         g, u = x.float().chunk(2, dim=-1)
         x = (torch.nn.functional.silu(g) * u).to(x.dtype)
     return (x.float() @ weight.float().t()).to(x.dtype)
+
+
+# ------------------------------------------------------- fused decode layer (residual + norm)
+# Each decode layer's two residual-add + RMSNorm launches (4.8 us each at Llama-3-8B B=8,
+# profiles/r2_decode.md: pure launch ramp / latency on 64 KB) are split across the neighbouring
+# projections instead (csrc/skinny.hip KsFuse): the o and down projections write the new
+# residual stream s = x + y plus per-(row, 16 columns) partial sums of s^2, and the next
+# projection (gate|up, or the next layer's qkv) computes RMSNorm(s) W^T = rstd * (s (W o w)^T):
+# a plain GEMM on s against a cached copy of W with the norm weight w folded into its columns,
+# whose epilogue scales each row by rstd (from the producer's partials). DLA_DECODE_FUSED_NORM=0
+# keeps the separate norm launches.
+DECODE_FUSED_NORM = os.environ.get("DLA_DECODE_FUSED_NORM", "1") != "0"
+
+
+def fused_layer_ok(x: torch.Tensor, H: int, qkv_w: torch.Tensor, o_w: torch.Tensor,
+                   up_w: torch.Tensor, down_w: torch.Tensor) -> bool:
+    """Shapes / state the fused decode layer supports (M <= 16 bf16 rows, no autograd)."""
+    if not (DECODE_FUSED_NORM and SKINNY and _ext.use_native(x)) or torch.is_grad_enabled():
+        return False
+    rows = x.numel() // x.shape[-1]
+    if not (1 <= rows <= 16 and x.dtype == torch.bfloat16 and x.shape[-1] == H):
+        return False
+    F2 = up_w.shape[0]
+    ok = (H % 1024 == 0 and H < 16384 and H // 16 <= 512 and qkv_w.shape == (qkv_w.shape[0], H)
+          and qkv_w.shape[0] < 16384 and qkv_w.shape[0] % 16 == 0 and o_w.shape[0] == H
+          and o_w.shape[1] % 1024 == 0 and down_w.shape == (H, F2 // 2) and (F2 // 2) % 1024 == 0
+          and F2 % 128 == 0 and rows * (H + 8) * 2 <= 148 * 1024)
+    return ok and all(w.dtype == torch.bfloat16 and w.stride(-1) == 1 and w.stride(0) % 8 == 0
+                      for w in (qkv_w, o_w, up_w, down_w))
+
+
+def _rows(t: torch.Tensor) -> torch.Tensor:
+    t2 = t.reshape(-1, t.shape[-1])
+    if t2.stride(-1) != 1 or t2.stride(0) % 8 or t2.data_ptr() % 16:
+        t2 = t2.contiguous()
+    return t2
+
+
+def _wkey(t: torch.Tensor):
+    ep = getattr(t, "_dla_epoch", None)
+    return (t.data_ptr(), t._version, ep[0] if ep is not None else 0)
+
+
+def folded_weight(w: torch.Tensor, norm_w: torch.Tensor) -> torch.Tensor:
+    """Cached W o norm_w (the RMSNorm weight folded into W's input columns), refreshed IN PLACE
+    when either tensor changed (version counter / engine weight epoch): a captured decode graph
+    keeps reading the same storage. Never re-made inside a capture (call
+    `refresh_folded_weights` before capturing / replaying)."""
+    key = (_wkey(w), _wkey(norm_w))
+    c = getattr(w, "_dla_fold", None)
+    if c is None or c[0] != key:
+        if torch.cuda.is_current_stream_capturing():
+            if c is None:
+                raise RuntimeError("folded decode weight first requested inside a graph capture")
+            return c[1]
+        with torch.no_grad():
+            t = c[1] if c is not None else torch.empty_like(w, memory_format=torch.contiguous_format)
+            torch.mul(w.detach(), norm_w.detach().view(1, -1), out=t)
+        c = (key, t)
+        w._dla_fold = c
+    return c[1]
+
+
+def refresh_folded_weights(model) -> None:
+    """Bring every folded decode weight of `model` up to date (before a graph replay)."""
+    for layer in getattr(model, "layers", []):
+        for w, nw in ((getattr(layer.attn, "qkv_proj", None), getattr(layer, "ln1_w", None)),
+                      (getattr(layer.mlp, "up_proj", None), getattr(layer, "ln2_w", None))):
+            if w is not None and nw is not None and getattr(w, "_dla_fold", None) is not None:
+                folded_weight(w, nw)
+
+
+def skinny_residual(x: torch.Tensor, w: torch.Tensor, res: torch.Tensor):
+    """s = res + x @ w^T (bf16 rounding as linear + add), plus the row-norm partials of s."""
+    s, ssq = _ext.require().skinny_fused(_rows(x), w, _rows(res), None, 0.0, False)
+    return s.view(*res.shape[:-1], w.shape[0]), ssq
+
+
+def skinny_normed(s: torch.Tensor, ssq: torch.Tensor, norm_w: torch.Tensor, eps: float,
+                  w: torch.Tensor, glu: bool = False) -> torch.Tensor:
+    """RMSNorm(s) * norm_w @ w^T from the producer's partials (glu: gate|up + SwiGLU epilogue)."""
+    y, _ = _ext.require().skinny_fused(_rows(s), folded_weight(w, norm_w), None, ssq, float(eps), bool(glu))
+    return y.view(*s.shape[:-1], y.shape[-1])

@@ -326,10 +326,11 @@ def _loop_experts_backward(dys, xs, gu, w_up, w_down, counts, needs):
 
 
 class _GroupedExpertsFn(torch.autograd.Function):
-    """Grouped SwiGLU experts on the device-driven grouped GEMM; offs [E+1] int32 on device."""
+    """Grouped SwiGLU experts on the device-driven grouped GEMM; offs [E+1] int32 on device.
+    `sync_free`: the backward also stays on the grouped kernels (never reads offs on the host)."""
 
     @staticmethod
-    def forward(ctx, xs, w_up, w_down, offs, fp8: bool):
+    def forward(ctx, xs, w_up, w_down, offs, fp8: bool, sync_free: bool = False):
         C = _ext.require()
         if fp8:
             wu_q, wu_s = fp8_weight(w_up)
@@ -343,13 +344,14 @@ class _GroupedExpertsFn(torch.autograd.Function):
             ys = C.gg_fwd(a, w_down, offs, None, None)
         ctx.save_for_backward(xs, gu, offs)
         ctx.w_up, ctx.w_down = w_up, w_down  # (on ctx: see ops.linear._LinearMainGradFn)
+        ctx.sync_free = sync_free
         return ys
 
     @staticmethod
     def backward(ctx, dys):
         xs, gu, offs = ctx.saved_tensors
         w_up, w_down = ctx.w_up, ctx.w_down
-        if _loop_backward_ok():
+        if not ctx.sync_free and _loop_backward_ok():
             # fp8 forward on the grouped kernel, bf16 backward on the per-expert hipBLASLt loop
             # (faster there; one host read of the offsets, outside any capture)
             o = offs.tolist()
@@ -377,7 +379,11 @@ class _GroupedExpertsFn(torch.autograd.Function):
             else:
                 outs.append(None)
         dxs = C.gg_dgrad(dgu, w_up, offs) if ctx.needs_input_grad[0] else None
-        return dxs, outs[0], outs[1], None, None
+        if dxs is not None and dxs.shape[0] > 0:
+            # rows past offs[-1] (padding of a capacity buffer) are never written by the kernel
+            tail = torch.arange(dxs.shape[0], device=dxs.device) >= offs[-1].long()
+            dxs = dxs.masked_fill(tail.unsqueeze(-1), 0)
+        return dxs, outs[0], outs[1], None, None, None
 
 
 def grouped_gemm_enabled() -> bool:
@@ -441,6 +447,34 @@ def experts_swiglu(xs: torch.Tensor, w_up: torch.Tensor, w_down: torch.Tensor,
     if isinstance(counts, torch.Tensor):
         counts = counts.tolist()  # host sync: per-expert loop path only
     return _ExpertsFn.apply(xs, w_up, w_down, [int(c) for c in counts], bool(fp8))
+
+
+def _ref_grouped_experts(xs, w_up, w_down, offs):
+    """Static-shape reference of the grouped experts for a device offsets array (no host read):
+    every expert runs over all rows and keeps its [offs[e], offs[e+1]) range; rows past offs[-1]
+    are zero. CPU / non-native path of `experts_swiglu_offsets`."""
+    rows = torch.arange(xs.shape[0], device=xs.device).view(-1, 1)
+    o = offs.to(xs.device).long()
+    out = xs.new_zeros((xs.shape[0], w_down.shape[1]))
+    for e in range(w_up.shape[0]):
+        y = F.linear(swiglu(F.linear(xs, w_up[e])), w_down[e])
+        out = torch.where((rows >= o[e]) & (rows < o[e + 1]), y, out)
+    return out
+
+
+def experts_swiglu_offsets(xs: torch.Tensor, w_up: torch.Tensor, w_down: torch.Tensor,
+                           offs: torch.Tensor, fp8: bool = False) -> torch.Tensor:
+    """Grouped experts over rows whose per-expert ranges are given ONLY as a device offsets array
+    offs [E+1] (rows past offs[-1] are padding: ignored, zero output and gradient). Never reads
+    the offsets on the host, forward or backward: the sync-free expert-parallel path."""
+    xs = xs.contiguous()
+    if _grouped_ok(xs, w_up, w_down):
+        if fp8 and _FP8 is None:
+            fp8 = False
+        ys = _GroupedExpertsFn.apply(xs, w_up, w_down, offs.to(torch.int32), bool(fp8), True)
+        tail = torch.arange(ys.shape[0], device=ys.device) >= offs[-1].long()
+        return ys.masked_fill(tail.unsqueeze(-1), 0)
+    return _ref_grouped_experts(xs, w_up, w_down, offs)
 
 
 def ref_moe(h2, router, w_up, w_down, k):

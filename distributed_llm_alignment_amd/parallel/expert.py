@@ -2,18 +2,26 @@
 (north-star "Mixtral 8x7B DPO with expert-parallel all-to-all").
 
 Each rank of an EP group of size ep owns E/ep consecutive experts (`expert_up/down` sliced in
-place, identical seeded init everywhere -> no broadcast). Per MoE layer:
-  1. route locally (HIP top-k kernel), order token slots expert-major (experts of one destination
-     rank are contiguous), `moe_dispatch` gathers the rows;
-  2. exchange the per-(rank, expert) counts with one tiny all-to-all, one host sync for the split
-     sizes (the same sync the dropless local path needs for its GEMM loop);
-  3. `all_to_all_single` of the token rows (xGMI is a full mesh on one MI355X node: every pair of
-     ranks has its own link, so all-to-all runs at full per-link bandwidth);
-  4. regroup source-major -> expert-major rows, grouped expert SwiGLU;
-  5. the inverse all-to-all and the weighted `moe_combine`.
-Backward mirrors it (all-to-all is its own adjoint with the splits swapped). Expert weights are
-marked `_dla_expert`: the data-parallel engine reduces their grads over the expert-data-parallel
-group (replicas holding the same experts) instead of the full DP group.
+place, identical seeded init everywhere -> no broadcast). Two dispatch modes:
+
+* `capacity` (default; `hardware.ep_capacity_factor` > 0): NO host synchronisation anywhere in
+  the layer, forward or backward. Every (source, destination) pair exchanges a fixed block of
+  C = capacity_factor * N * k / ep rows (multiple of 8), so the all-to-all split sizes are known
+  on the host without reading the routing: token slots are ordered expert-major on the device,
+  each destination's slots beyond C are dropped (their combine weight becomes 0, the GShard /
+  Switch convention; `dropped_slots()` reports the count lazily), the per-(destination, local
+  expert) counts travel in one small device-side all-to-all, and the receiver builds the
+  expert-major row order and the grouped-GEMM offsets on the device. The grouped expert GEMM
+  (csrc/grouped_gemm.hip) then runs over the padded [ep*C] buffer, touching only the valid rows.
+  The tokens are processed in `chunks` (default 2) pipelined pieces: chunk c+1's dispatch
+  all-to-all is in flight on RCCL's stream while chunk c's expert GEMMs run, and chunk c's
+  return all-to-all overlaps chunk c+1's experts. With a capacity large enough that nothing is
+  dropped the result equals the exact path (the MoE layer is per-token).
+* `exact` (capacity factor 0): dropless with host-known splits: the per-(rank, expert) counts
+  are read on the host once per layer and `all_to_all_single` moves exactly the routed rows.
+
+Expert weights are marked `_dla_expert`: the data-parallel engine reduces their grads over the
+expert-data-parallel group (replicas holding the same experts) instead of the full DP group.
 """
 from __future__ import annotations
 
@@ -46,8 +54,45 @@ def all_to_all(x, out_splits, in_splits, group):
     return _AllToAll.apply(x, list(out_splits), list(in_splits), group)
 
 
+class _A2AStart(torch.autograd.Function):
+    """Equal-split all-to-all launched asynchronously; `_A2AWait` completes it. Backward: the
+    adjoint all-to-all (synchronous)."""
+
+    @staticmethod
+    def forward(ctx, x, group, holder):
+        ctx.group = group
+        x = x.contiguous()
+        out = torch.empty_like(x)
+        holder.append(dist.all_to_all_single(out, x, group=group, async_op=True))
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        dx = torch.empty_like(g)
+        dist.all_to_all_single(dx, g.contiguous(), group=ctx.group)
+        return dx, None, None
+
+
+class _A2AWait(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, out, holder):
+        holder.pop(0).wait()
+        return out.view_as(out)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, None
+
+
+def _gather_rows(x: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
+    """out[i] = x[idx[i]] (idx < 0 -> zero row). Static shapes, no host sync; the backward is the
+    matching scatter (idx is injective on its valid entries)."""
+    valid = (idx >= 0).unsqueeze(-1)
+    return torch.where(valid, x.index_select(0, idx.clamp(min=0)), torch.zeros((), dtype=x.dtype, device=x.device))
+
+
 class ExpertParallel:
-    def __init__(self, group, num_experts: int):
+    def __init__(self, group, num_experts: int, capacity_factor: float = 2.0, chunks: int = 2):
         self.group = group
         self.ep = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
@@ -55,8 +100,119 @@ class ExpertParallel:
             raise ValueError(f"num_experts {num_experts} not divisible by ep {self.ep}")
         self.E = num_experts
         self.El = num_experts // self.ep
+        self.capacity_factor = float(capacity_factor)
+        self.chunks = max(1, int(chunks))
+        self._dropped = None  # device int64 counter of dropped token slots (capacity mode)
+
+    def dropped_slots(self, reset: bool = True) -> int:
+        """Token slots dropped by the capacity limit since the last call (one host read)."""
+        if self._dropped is None:
+            return 0
+        n = int(self._dropped.item())
+        if reset:
+            self._dropped.zero_()
+        return n
 
     def dispatch_combine(self, moe, h2: torch.Tensor, topv: torch.Tensor, topi: torch.Tensor):
+        if self.capacity_factor > 0:
+            return self._capacity(moe, h2, topv, topi)
+        return self._exact(moe, h2, topv, topi)
+
+    # ------------------------------------------------------------------ capacity (sync-free)
+    def capacity(self, n_tokens: int, k: int) -> int:
+        c = int(self.capacity_factor * n_tokens * k / self.ep + 0.999999)
+        return max(8, (c + 7) // 8 * 8)
+
+    def _route_chunk(self, topi: torch.Tensor, C: int):
+        """Device-side slot placement for one token chunk: (send_src [ep*C] token index or -1,
+        slot_pos [n, k] row of each slot in the send buffer or ep*C when dropped, send counts
+        [ep, El] int32, dropped count)."""
+        ep, El, E = self.ep, self.El, self.E
+        n, k = topi.shape
+        dev = topi.device
+        flat = topi.reshape(-1).long()
+        order = torch.argsort(flat, stable=True)
+        rank_sorted = torch.empty_like(order)
+        rank_sorted[order] = torch.arange(order.numel(), device=dev)
+        counts = torch.zeros(E, dtype=torch.long, device=dev).scatter_add_(0, flat, torch.ones_like(flat))
+        cum = torch.cumsum(counts, 0)
+        dstart = (cum - counts).view(ep, El)[:, 0]  # first expert-major slot of each destination
+        dest = flat // El
+        off = rank_sorted - dstart[dest]  # slot's rank inside its destination block
+        keep = off < C
+        pos = torch.where(keep, dest * C + off, torch.full_like(off, ep * C))
+        send_src = torch.full((ep * C + 1,), -1, dtype=torch.long, device=dev)
+        send_src.scatter_(0, pos, torch.where(keep, torch.arange(n * k, device=dev) // k, -1))
+        # per (destination, local expert) rows actually sent: the first C of the block in order
+        cnt = counts.view(ep, El)
+        before = torch.cumsum(cnt, 1) - cnt
+        sent = torch.clamp(torch.clamp(C - before, min=0), max=cnt)
+        return send_src[:ep * C], pos.view(n, k), sent.to(torch.int32), (~keep).sum()
+
+    def _expert_order(self, rc: torch.Tensor, C: int):
+        """Receiver side: rows [src s][j < sum_e rc[s, e]] (local-expert sorted per source) ->
+        expert-major order. Returns (xe_src [ep*C] recv row or -1, inv [ep*C] expert-major position
+        of every recv row or -1, grouped-GEMM offsets [El+1] int32)."""
+        ep, El = self.ep, self.El
+        dev = rc.device
+        rc = rc.long()
+        tot_s = rc.sum(1)  # rows received from each source
+        cum_s = torch.cumsum(rc, 1)  # [ep, El] inclusive, per source
+        r = torch.arange(C, device=dev).view(1, C).expand(ep, C)  # row within the source block
+        e = (r.unsqueeze(-1) >= cum_s.unsqueeze(1)).sum(-1)  # local expert of the row (El: padding)
+        valid = r < tot_s.view(ep, 1)
+        e_c = e.clamp(max=El - 1)
+        j = r - torch.gather(cum_s - rc, 1, e_c)  # index inside its (source, expert) run
+        per_e = rc.sum(0)  # [El] rows per local expert
+        starts_es = (torch.cumsum(rc.t().reshape(-1), 0) - rc.t().reshape(-1)).view(El, ep)  # (e, s)
+        q = starts_es[e_c, torch.arange(ep, device=dev).view(ep, 1).expand(ep, C)] + j
+        inv = torch.where(valid, q, torch.full_like(q, -1)).reshape(-1)
+        xe_src = torch.full((ep * C + 1,), -1, dtype=torch.long, device=dev)
+        xe_src.scatter_(0, torch.where(valid.reshape(-1), inv, torch.full_like(inv, ep * C)),
+                        torch.arange(ep * C, device=dev))
+        offs = torch.zeros(El + 1, dtype=torch.int32, device=dev)
+        offs[1:] = torch.cumsum(per_e, 0).to(torch.int32)
+        return xe_src[:ep * C], inv, offs
+
+    def _capacity(self, moe, h2: torch.Tensor, topv: torch.Tensor, topi: torch.Tensor):
+        N, H = h2.shape
+        k = topi.shape[1]
+        nch = self.chunks if N >= 8 * self.chunks else 1
+        bounds = [(N * c // nch, N * (c + 1) // nch) for c in range(nch)]
+        holder: list = []
+        stage = []
+        # 1) route every chunk and launch its dispatch all-to-alls (rows + counts) async
+        for a, b in bounds:
+            C = self.capacity(b - a, k)
+            send_src, pos, sent, ndrop = self._route_chunk(topi[a:b], C)
+            if self._dropped is None:
+                self._dropped = torch.zeros((), dtype=torch.long, device=h2.device)
+            self._dropped += ndrop
+            rc = torch.empty_like(sent)
+            w = dist.all_to_all_single(rc, sent.contiguous(), group=self.group, async_op=True)
+            xs = _gather_rows(h2[a:b], send_src)
+            xr = _A2AStart.apply(xs, self.group, holder)
+            stage.append((C, pos, w, rc, xr))
+        # 2) per chunk: wait for its rows, experts on the device-built order, return all-to-all
+        back = []
+        for C, pos, w, rc, xr in stage:
+            w.wait()
+            xr = _A2AWait.apply(xr, holder)
+            xe_src, inv, offs = self._expert_order(rc, C)
+            xe = _gather_rows(xr, xe_src)
+            ye = ops.moe.experts_swiglu_offsets(xe, moe.expert_up, moe.expert_down, offs, fp8=moe.fp8)
+            yr = _gather_rows(ye, inv)
+            back.append((pos, _A2AStart.apply(yr, self.group, holder)))
+        # 3) combine each chunk (dropped slots read the appended zero row)
+        outs = []
+        for (a, b), (pos, ys) in zip(bounds, back):
+            ys = _A2AWait.apply(ys, holder)
+            ys = torch.cat([ys, ys.new_zeros(1, H)], 0)
+            outs.append(ops.moe.combine(ys, pos.to(torch.int32), topv[a:b]))
+        return outs[0] if len(outs) == 1 else torch.cat(outs, 0)
+
+    # ------------------------------------------------------------------ exact (host splits)
+    def _exact(self, moe, h2: torch.Tensor, topv: torch.Tensor, topi: torch.Tensor):
         ep, El = self.ep, self.El
         pos, counts = ops.moe.expert_positions(topi, self.E)
         recv = torch.empty_like(counts)
@@ -86,13 +242,14 @@ class ExpertParallel:
 
 
 @torch.no_grad()
-def apply_expert_parallel(model, mesh):
-    """Keep this rank's E/ep experts of every MoE layer and attach the all-to-all router."""
+def apply_expert_parallel(model, mesh, capacity_factor: float = 2.0, chunks: int = 2):
+    """Keep this rank's E/ep experts of every MoE layer and attach the all-to-all router
+    (`capacity_factor` 0: exact dropless dispatch with one host read per layer)."""
     base = getattr(model, "backbone", model)
     cfg = base.cfg
     if mesh.ep <= 1 or not cfg.is_moe:
         return model
-    ep = ExpertParallel(mesh.ep_group, cfg.num_experts)
+    ep = ExpertParallel(mesh.ep_group, cfg.num_experts, capacity_factor=capacity_factor, chunks=chunks)
     lo, hi = ep.rank * ep.El, (ep.rank + 1) * ep.El
     owners = None
     for layer in base.layers:

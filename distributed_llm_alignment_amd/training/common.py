@@ -112,7 +112,8 @@ def parallelize(ctx: TrainContext, model):
     if m.ep > 1 and base.cfg.is_moe:
         from ..parallel.expert import apply_expert_parallel
 
-        apply_expert_parallel(model, m)
+        apply_expert_parallel(model, m, capacity_factor=ctx.hw.get("ep_capacity_factor", 2.0),
+                              chunks=ctx.hw.get("ep_chunks", 2))
     if base.cfg.is_moe and (ctx.cfg.get("model", {}) or {}).get("moe_fp8", False):
         for layer in base.layers:  # e4m3 expert GEMMs in the forward (bf16 backward)
             layer.mlp.fp8 = True

@@ -280,3 +280,6 @@ def invalidate_weight_caches(model) -> None:
     for p in model.parameters():
         for k in ("_dla_wt_ver", "_dla_fp8"):
             p.__dict__.pop(k, None)
+        fold = p.__dict__.get("_dla_fold")
+        if fold is not None:  # keep the buffer (a captured decode graph reads it), mark stale
+            p._dla_fold = (None, fold[1])

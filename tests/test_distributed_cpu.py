@@ -456,7 +456,7 @@ def test_fsdp_checkpoint_resume(tmp_path):
 
 
 # ------------------------------------------------------------------------------ expert parallel
-def _ep_step(rank, world, ep, zero):
+def _ep_step(rank, world, ep, zero, cf=None, nosync=False):
     import torch
 
     from distributed_llm_alignment_amd.data.synthetic import synthetic_preference_batch
@@ -470,28 +470,124 @@ def _ep_step(rank, world, ep, zero):
     cfg = get_config("tiny-mixtral")
     pol = build_model(cfg, device="cpu", seed=0)
     ref = build_model(cfg, device="cpu", seed=0).requires_grad_(False)
-    apply_expert_parallel(pol, mesh)
-    apply_expert_parallel(ref, mesh)
+    # capacity factor ep: a destination block holds every slot a source can send (no drops)
+    cf = float(ep) if cf is None else cf
+    apply_expert_parallel(pol, mesh, capacity_factor=cf)
+    apply_expert_parallel(ref, mesh, capacity_factor=cf)
     eng = DataParallelEngine(pol, lr=1e-2, weight_decay=0.01, max_grad_norm=0.05, zero_stage=zero,
                              group=mesh.dp_group, expert_group=mesh.edp_group, bucket_mb=0.05)
     g = torch.Generator().manual_seed(21 + rank)
     b = synthetic_preference_batch(2, 16, cfg.vocab_size, generator=g)
     out = []
     for _ in range(2):
-        loss, _ = dpo_step_loss(pol, ref, b)
-        loss.backward()
+        if nosync and ep > 1:
+            # the sync-free EP layer must never read a device value on the host: any
+            # .item() / .tolist() / bool() inside the MoE forward or backward raises
+            from distributed_llm_alignment_amd.models.transformer import MoE
+
+            with _forbid_host_reads(MoE) as guard:
+                loss, _ = dpo_step_loss(pol, ref, b)
+                guard.flag["on"] = True  # the whole backward pass, MoE layers included
+                try:
+                    loss.backward()
+                finally:
+                    guard.flag["on"] = False
+        else:
+            loss, _ = dpo_step_loss(pol, ref, b)
+            loss.backward()
         out.append(float(eng.step()))
     out.append(float(dpo_step_loss(pol, ref, b)[0].detach()))
     return out
 
 
+class _forbid_host_reads:
+    """Inside MoE.forward (and the backward of what it recorded) Tensor.item / tolist / __bool__ /
+    __int__ / __float__ raise."""
+
+    def __init__(self, moe_cls):
+        self.moe_cls = moe_cls
+
+    def __enter__(self):
+        import torch
+
+        self.saved = {n: getattr(torch.Tensor, n) for n in ("item", "tolist", "__bool__", "__int__", "__float__")}
+        self.fwd = self.moe_cls.forward
+        flag = {"on": False}
+        self.flag = flag
+
+        def guard(name):
+            orig = self.saved[name]
+
+            def f(t, *a, **k):
+                if flag["on"]:
+                    raise AssertionError(f"host read Tensor.{name} in the sync-free EP path")
+                return orig(t, *a, **k)
+            return f
+
+        for n in self.saved:
+            setattr(torch.Tensor, n, guard(n))
+        fwd = self.fwd
+
+        def moe_forward(mod, *a, **k):
+            flag["on"] = True
+            try:
+                return fwd(mod, *a, **k)
+            finally:
+                flag["on"] = False
+        self.moe_cls.forward = moe_forward
+        return self
+
+    def __exit__(self, *exc):
+        import torch
+
+        for n, f in self.saved.items():
+            setattr(torch.Tensor, n, f)
+        self.moe_cls.forward = self.fwd
+        return False
+
+
 @pytest.mark.parametrize("zero", [0, 1])
-def test_expert_parallel_matches_replicated_experts(zero):
-    """EP=2 (all-to-all token routing, expert grads local) == DP=2 with replicated experts."""
+@pytest.mark.parametrize("mode", ["capacity", "exact"])
+def test_expert_parallel_matches_replicated_experts(zero, mode):
+    """EP=2 (all-to-all token routing, expert grads local) == DP=2 with replicated experts, for
+    the sync-free fixed-capacity dispatch (chunk-pipelined) and the exact host-split one."""
     a = run_ranks(_ep_step, 2, (1, zero))
-    b = run_ranks(_ep_step, 2, (2, zero))
+    b = run_ranks(_ep_step, 2, (2, zero, None if mode == "capacity" else 0.0))
     for r in (0, 1):
         assert a[r] == pytest.approx(b[r], rel=1e-4, abs=1e-6), (a[r], b[r])
+
+
+def test_expert_parallel_forward_backward_issue_no_host_sync():
+    """The capacity dispatch never reads a device value on the host (forward and backward of
+    every MoE layer), and still matches the replicated-expert run."""
+    a = run_ranks(_ep_step, 2, (1, 1))
+    b = run_ranks(_ep_step, 2, (2, 1, None, True))
+    for r in (0, 1):
+        assert a[r] == pytest.approx(b[r], rel=1e-4, abs=1e-6), (a[r], b[r])
+
+
+def _ep_drop(rank, world):
+    import torch
+
+    from distributed_llm_alignment_amd.models import build_model, get_config
+    from distributed_llm_alignment_amd.parallel.expert import apply_expert_parallel
+    from distributed_llm_alignment_amd.parallel.mesh import build_mesh
+
+    mesh = build_mesh(ep=2)
+    cfg = get_config("tiny-mixtral")
+    m = build_model(cfg, device="cpu", seed=0)
+    apply_expert_parallel(m, mesh, capacity_factor=0.25)  # far too small: slots get dropped
+    ids = torch.randint(3, cfg.vocab_size, (2, 32), generator=torch.Generator().manual_seed(rank))
+    lp = m.sequence_logprob(ids)
+    ep = m.layers[0].mlp.ep
+    return bool(torch.isfinite(lp).all()), ep.dropped_slots()
+
+
+def test_expert_parallel_capacity_overflow_is_counted():
+    res = run_ranks(_ep_drop, 2)
+    for r in (0, 1):
+        finite, dropped = res[r]
+        assert finite and dropped > 0
 
 
 def test_expert_parallel_world4_edp2():
@@ -753,7 +849,9 @@ def _exposed_comm(rank, world, zero):
     for mode in ("sync", "overlap", "sync", "overlap", "sync", "overlap"):
         net(x).square().mean().backward()
         if mode == "overlap":
-            time.sleep(0.25)
+            # the stand-in rollout outlasts the collectives even on a loaded host: 3x the
+            # slowest sync-mode exposure seen so far (at least 250 ms)
+            time.sleep(max(0.25, 3e-3 * max(out.get("sync", [0.0]))))
         eng.step()
         out.setdefault(mode, []).append(eng.comm_timer.last_ms())
     return {k: statistics.median(v) for k, v in out.items()}

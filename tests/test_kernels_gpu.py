@@ -830,3 +830,42 @@ def test_odd_head_dim_partial_rotary_attention_fwd_bwd():
     (dr,) = torch.autograd.grad(ocpu, qf, do.float().cpu())
     rel = ((dg.float().cpu() - dr).norm() / dr.norm()).item()
     assert rel < 3e-2, rel
+
+
+@pytest.mark.parametrize("case", ["causal_mha", "causal_gqa_leftpad", "noncausal_window"])
+def test_attention_head_dim_80_native(case):
+    """Native D = 80 tiles (phi-2, the reference's distill student: 96-wide LDS images, 5 MFMA
+    k-steps, pad columns never stored) over several 256-key backward blocks, GQA, padding and
+    a window, against fp32; and equal to the padded-to-128 path to bf16 accuracy."""
+    from distributed_llm_alignment_amd.ops import attention as A
+
+    assert 80 in A.NATIVE_HEAD_DIMS
+    B, T, D = 2, 600, 80
+    Hq, Hkv = (4, 4) if case == "causal_mha" else (8, 2)
+    causal, window, ks, ke = True, 0, None, None
+    if case == "causal_gqa_leftpad":
+        ks = torch.tensor([0, 90], device=DEV, dtype=torch.int32)
+    if case == "noncausal_window":
+        causal = False
+        ke = torch.tensor([T, 377], device=DEV, dtype=torch.int32)
+    q = bf(torch.randn(B, T, Hq, D)).requires_grad_()
+    k = bf(torch.randn(B, T, Hkv, D)).requires_grad_()
+    v = bf(torch.randn(B, T, Hkv, D)).requires_grad_()
+    o = ops.attention_core(q, k, v, causal=causal, window=window, kv_start=ks, kv_end=ke)
+    go = bf(torch.randn_like(o.float()))
+    gq, gk, gv = torch.autograd.grad(o, [q, k, v], go)
+    qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
+    orf = ref_attention(qr, kr, vr, 1 / math.sqrt(D), causal, 0, window, ks, ke)
+    rq, rk, rv = torch.autograd.grad(orf, [qr, kr, vr], go.float())
+    valid = torch.ones(B, T, 1, 1, dtype=torch.bool, device=DEV)
+    if ks is not None:
+        valid[1, :90] = False
+    assert rel_err(o * valid, orf * valid) < 2e-2, "forward"
+    assert rel_err(gq * valid, rq * valid) < 3e-2, "dq"
+    assert rel_err(gk, rk) < 3e-2, "dk"
+    assert rel_err(gv, rv) < 3e-2, "dv"
+    # the padded-to-128 path (what D = 80 ran on before): same result to bf16 accuracy
+    pad = lambda t: torch.nn.functional.pad(t.detach(), (0, 48))
+    op = ops.attention_core(pad(q), pad(k), pad(v), scale=1 / math.sqrt(D), causal=causal,
+                            window=window, kv_start=ks, kv_end=ke)[..., :D]
+    assert rel_err(o * valid, op * valid) < 1e-2
