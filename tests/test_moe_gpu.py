@@ -212,3 +212,61 @@ def test_moe_transposed_dgrad_matches_nn_and_follows_steps(monkeypatch):
             moe.expert_up.mul_(1.25)
             moe.expert_down.mul_(0.8)
     assert eng is not None
+
+
+def test_mixtral_layer_fwd_bwd_graph_captured_matches_fp32():
+    """The whole Mixtral MoE layer -- router top-k, device-side expert offsets, dispatch, grouped
+    expert GEMMs (SwiGLU fused), combine -- forward AND backward captured in ONE hipGraph (no host
+    sync anywhere) and replayed; outputs and every gradient against an fp32 autograd reference
+    (HF Mixtral semantics, ops.moe.ref_moe) on the same bf16 weights; a second replay with new
+    inputs written into the static buffers follows them."""
+    from distributed_llm_alignment_amd import ops
+    from distributed_llm_alignment_amd.models import build_model, get_config
+
+    cfg = get_config("tiny-mixtral", hidden_size=256, intermediate_size=512, num_experts=8)
+    moe = build_model(cfg, device=DEV, dtype=torch.bfloat16, seed=5).layers[0].mlp
+    g = torch.Generator(device=DEV).manual_seed(9)
+    x = torch.randn(512, cfg.hidden_size, device=DEV, generator=g).to(torch.bfloat16).requires_grad_(True)
+    gy = torch.randn(512, cfg.hidden_size, device=DEV, generator=g).to(torch.bfloat16)
+    params = [x, moe.router, moe.expert_up, moe.expert_down]
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):  # warm-up: allocates .grad and every lazily created buffer
+        for _ in range(2):
+            moe(x).backward(gy)
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        y = moe(x)
+        y.backward(gy)
+
+    def check():
+        for p in params:
+            p.grad.zero_()
+        graph.replay()
+        torch.cuda.synchronize()
+        xr, rr, ur, dr = (p.detach().float().requires_grad_(True) for p in params)
+        # fp32 Mixtral math with the routing the bf16 router logits select (as the kernel does:
+        # near-ties between experts may order differently in fp32)
+        with torch.no_grad():
+            topi = torch.topk(torch.nn.functional.linear(x.detach(), moe.router.detach()).float(),
+                              cfg.num_experts_per_tok, -1).indices
+        logits = xr @ rr.t()
+        w = torch.softmax(logits.gather(1, topi), -1)
+        yr = torch.zeros_like(xr)
+        for j in range(topi.shape[1]):
+            for e in range(cfg.num_experts):
+                sel = topi[:, j] == e
+                gu = xr[sel] @ ur[e].t()
+                a = torch.nn.functional.silu(gu[:, :gu.shape[1] // 2]) * gu[:, gu.shape[1] // 2:]
+                yr = yr.index_add(0, sel.nonzero().squeeze(1), w[sel, j:j + 1] * (a @ dr[e].t()))
+        yr.backward(gy.float())
+        err = lambda a, b: float((a.float() - b).norm() / (b.norm() + 1e-12))
+        assert err(y, yr) < 2e-2
+        for p, r in zip(params, (xr, rr, ur, dr)):
+            assert err(p.grad, r.grad) < 5e-2, (p.shape, err(p.grad, r.grad))
+
+    check()
+    with torch.no_grad():  # new routing: the captured graph must follow the device-side offsets
+        x.copy_(torch.randn(x.shape, device=DEV, generator=g).to(torch.bfloat16))
+    check()
