@@ -55,10 +55,14 @@ __device__ __forceinline__ int swz(int row, int ch) {
 }
 
 // dS^T image [keys][32 queries] bf16 (64-B rows): 8-byte unit c4 of row `row`, XOR-swizzled
-// with row bits 2..4 so the 32 key rows written by a half-wave land on 32 distinct bank pairs
-// (unswizzled: 16-bank row stride -> 8-way conflicts; the swizzle is a per-row permutation, so
-// the ds_read_b64_tr_b16 reads of the dQ MFMA stay conflict-free).
-__device__ __forceinline__ int ds_off(int row, int c4) { return row * 32 + ((c4 ^ ((row >> 2) & 7)) << 2); }
+// with row bits 1..3. ds_write_b64 banks 16-lane groups over 32 banks: 16 consecutive key rows
+// (one unit each) cover (row parity, unit ^ (row>>1)&7) = all 16 bank pairs. The transposed dQ
+// reads stay conflict-free: attn_bwd_kernel's 32-lane groups read rows r..r+3 (x 8 units), and
+// attn_bwd8_kernel's read rows r..r+3 with units 4t..4t+3 beside rows r+8..r+11, whose XOR
+// differs in bit 2 and so moves them to the other four units. (Row bits 2..4 left the latter
+// 2-way conflicted on every read: SQ_LDS_BANK_CONFLICT 1.3e7 per call at B8 T1024.)
+__device__ __forceinline__ int ds_swz(int row) { return (row >> 1) & 7; }
+__device__ __forceinline__ int ds_off(int row, int c4) { return row * 32 + ((c4 ^ ds_swz(row)) << 2); }
 
 __device__ __forceinline__ s16x4 tr_read(const bf16_t* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
@@ -921,6 +925,455 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnBwdParams p) {
   }
 }
 
+// ----------------------------------------------------------------------------------------------
+// backward, 8-wave variant (two waves per SIMD)
+// ----------------------------------------------------------------------------------------------
+// Same workgroup geometry, LDS images, slab and partial outputs as attn_bwd_kernel (256 keys per
+// workgroup, 32-query tiles, 160 KB LDS), but 8 waves of ONE 32-key sub-tile each: dK^T / dV^T of
+// a wave are 128 accumulators at D = 128, so two waves fit one SIMD's register file and each
+// hides the other's LDS / memory latency (attn_bwd_kernel, one wave per SIMD, exposes it: ~25 %
+// MFMA busy). To fit 256 registers:
+//   * the row constants (LSE, delta) are loaded straight into the score / dP accumulators, which
+//     then start at -lse2/scale2 and -delta (S - lse and dP - delta come out of the MFMA chains);
+//   * fragment reads are single-buffered: the other wave of the SIMD fills the gaps;
+//   * dQ uses 16x16x32 MFMAs over 16-column slices of d (wave w: columns 16w..16w+15, both
+//     16-query halves), so a wave holds 8 dQ accumulators.
+// Causal sub-tiles that see no query of a tile skip all their MFMAs (wave-uniform branch).
+// Phase timestamps for one workgroup (tools/attn_bwd_probe.hip builds with DLA_BWD_TRACE; the
+// extension never defines it): s_memtime per (wave, tile, point), vector-stored by lane 0.
+#ifdef DLA_BWD_TRACE
+__device__ long long g_bwd_trace[8 * 64 * 8];
+#define BWD_TS(k)                                                                         \
+  do {                                                                                    \
+    if (blockIdx.x == DLA_BWD_TRACE && lane == 0 && it < 64)                              \
+      g_bwd_trace[(w * 64 + it) * 8 + (k)] = static_cast<long long>(__builtin_amdgcn_s_memtime()); \
+  } while (0)
+#else
+#define BWD_TS(k) \
+  do {            \
+  } while (0)
+#endif
+
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(512) void attn_bwd8_kernel(AttnBwdParams p) {
+  constexpr int BKV = kAttnBwdKeys, BQ = kAttnBwdQRows, NT = 512;
+  constexpr int DP = attn_dp<D>();
+  constexpr int NCH = DP / 8;
+  constexpr int NCHL = D / 8;
+  constexpr int KS = D / 16;
+  constexpr int DT = DP / 32;
+  constexpr int NDS = D / 16;  // 16-column dQ slices: 8 (D = 128), 5 (80), 4 (64)
+  constexpr bool Q_EXACT = BQ * NCH == NT;
+  static_assert(BQ * NCH <= NT && (BKV * NCH) % NT == 0 && BKV == 256 && BQ == 32, "tile geometry");
+  // one array, small images first: Q / dO / dS addresses stay inside the 16-bit ds_read
+  // immediate of one base register (Q and dO reads share an address VGPR, +8 KB)
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * BQ * DP + BKV * BQ + 2 * BKV * DP];
+  bf16_t* const Qs = lds;
+  bf16_t* const dOs = lds + BQ * DP;
+  bf16_t* const dSs = lds + 2 * BQ * DP;
+  bf16_t* const Ks = dSs + BKV * BQ;
+  bf16_t* const Vs = Ks + BKV * DP;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l32 = lane & 31, h = lane >> 5;
+  const int group = p.Hq / p.Hkv;
+  const int hpb = group / p.hsplit;
+  const int nrest = p.Hkv * p.B * p.hsplit;
+  const int kb = static_cast<int>(blockIdx.x) / nrest;
+  int rest = static_cast<int>(blockIdx.x) - kb * nrest;
+  const int sidx = rest % p.hsplit;
+  rest /= p.hsplit;
+  const int hk = rest % p.Hkv, b = rest / p.Hkv;
+  const int k0 = kb * BKV;
+  const int kw = k0 + 32 * w;  // this wave's 32 keys
+  const int kbeg = p.kv_start ? p.kv_start[b] : 0;
+  const int kend = p.kv_end ? p.kv_end[b] : p.Tk;
+
+  const bool rope_in = p.rope_inputs != 0;
+  {  // K and V blocks -> LDS (as attn_bwd_kernel; 16 consecutive lanes hold one row)
+    const bf16_t* kp = p.k + b * p.k_sb + static_cast<int64_t>(hk) * p.k_sh;
+    const bf16_t* vp = p.v + b * p.v_sb + static_cast<int64_t>(hk) * p.v_sh;
+#pragma unroll 2
+    for (int c = 0; c < BKV * NCH / NT; ++c) {
+      const int ci = tid + NT * c;
+      const int row = ci / NCH, ch = ci % NCH;
+      const int key = k0 + row;
+      const bool in = key < p.Tk && ch < NCHL;
+      bf16x8 kv = in ? load_bf16x8(kp + key * p.k_st + ch * 8) : bf16x8{};
+      if constexpr (DP == D) {
+        if (rope_in)
+          kv = rope_rot_chunk<NCH>(kv, ch, in, static_cast<int64_t>(b) * p.Tk + key, key, p.rope_cos,
+                                   p.rope_sin, p.rope_pos);
+      }
+      store_bf16x8(Ks + swz<DP>(row, ch), kv);
+      store_bf16x8(Vs + swz<DP>(row, ch), in ? load_bf16x8(vp + key * p.v_st + ch * 8) : bf16x8{});
+    }
+  }
+
+  int qt0, qend;
+  bwd_q_range<CAUSAL>(k0, p.Tq, p.causal_off, p.window, qt0, qend);
+  const int nqt = (qend - qt0 + BQ - 1) / BQ;
+  const bool block_has_keys = k0 < kend && k0 + BKV > kbeg;
+  const int n_iter = block_has_keys ? hpb * nqt : 0;
+  const int hq0 = hk * group + sidx * hpb;
+
+  // register prefetch of the next (head, q-tile)'s Q and dO rows: one 16-B chunk per thread.
+  // Global addresses in the loop are a wave-uniform (SGPR) base + a 32-bit lane byte offset
+  // (SGPR-base addressing): per-lane 64-bit pointers cost two registers each and spilled.
+  const int qrow = tid / NCH, qch = tid % NCH;
+  const bool qslot = (Q_EXACT || tid < BQ * NCH) && qch < NCHL;
+  const uint32_t qlo = static_cast<uint32_t>(qrow * p.q_st + qch * 8) * 2u;
+  const uint32_t dlo = static_cast<uint32_t>(qrow * p.do_st + qch * 8) * 2u;
+  bf16x8 qreg, dreg;
+  auto gld = [](const bf16_t* base, uint32_t off) {
+    return load_bf16x8(reinterpret_cast<const bf16_t*>(reinterpret_cast<const char*>(base) + off));
+  };
+  // (head, q-tile) of a tile index, advanced incrementally (no per-tile integer division):
+  // heads outer, tiles inner
+  const int qtend = qt0 + nqt * BQ;
+  auto advance = [&](int& hq, int& qt) {
+    qt += BQ;
+    if (qt >= qtend) {
+      qt = qt0;
+      ++hq;
+    }
+  };
+  auto prefetch = [&](int hq, int qt) {
+    const bf16_t* qp = p.q + b * p.q_sb + static_cast<int64_t>(hq) * p.q_sh;
+    const bf16_t* dop = p.dout + b * p.do_sb + static_cast<int64_t>(hq) * p.do_sh;
+    if (!qslot) {
+      qreg = bf16x8{};
+      dreg = bf16x8{};
+    } else if (qt + BQ <= p.Tq) {
+      qreg = gld(qp + static_cast<int64_t>(qt) * p.q_st, qlo);
+      dreg = gld(dop + static_cast<int64_t>(qt) * p.do_st, dlo);
+    } else {
+      const int qq = min(qt + qrow, p.Tq - 1);
+      const bf16x8 a = load_bf16x8(qp + qq * p.q_st + qch * 8);
+      const bf16x8 g = load_bf16x8(dop + qq * p.do_st + qch * 8);
+      const bool in = qt + qrow < p.Tq;
+      qreg = in ? a : bf16x8{};
+      dreg = in ? g : bf16x8{};
+    }
+  };
+  auto stage = [&]() {
+    if (Q_EXACT || tid < BQ * NCH) {
+      store_bf16x8(Qs + swz<DP>(qrow, qch), qreg);
+      store_bf16x8(dOs + swz<DP>(qrow, qch), dreg);
+    }
+  };
+
+  const int i16 = lane & 15, qq = i16 >> 2, pp = i16 & 3, half16 = (lane >> 4) & 1, g4l = lane >> 4;
+  // Lane constants of the LDS addresses. Every swizzled address is base + ((k ^ x) << 3) with a
+  // compile-time k (the chunk index minus the bits the XOR never touches), so a handful of
+  // bases replace one address register per (image, k-step); they are made opaque at the top of
+  // every tile (asm barrier) so the derived addresses are formed next to their reads instead of
+  // being hoisted out of the loop (which costs a register each and spilled).
+  constexpr int FMASK = (NCH & (NCH - 1)) == 0 ? NCH - 1 : 3;  // as swz<DP>
+  auto swzf = [](int row) { return (((row & 3) << 2) | ((row >> 2) & 3)) & FMASK; };
+  // row reads (row l32, chunk 2s + h): swz<DP>(l32, 2s + h) = rq + ((2s ^ rx) << 3)
+  int rq = l32 * DP, rx = h ^ swzf(l32);
+  // transposed Q / dO reads (rows 4h + qq, 4h + 8 + qq; chunk 4dt + c1, c1 < 4)
+  const int c1 = 2 * half16 + (pp >> 1);
+  int tq0 = (4 * h + qq) * DP + (pp & 1) * 4, tx0 = c1 ^ swzf(4 * h + qq);
+  int tq1 = (4 * h + 8 + qq) * DP + (pp & 1) * 4, tx1 = c1 ^ swzf(4 * h + 8 + qq);
+  // dS^T writes: ds_off(l32, 2g + h) = wq + ((2g ^ wx) << 2)
+  int wq = l32 * 32, wx = h ^ ds_swz(l32);
+  // phase B (16x16x32 dQ): A = dS rows (keys) 8*g4l + qq (+4) of query columns 16t + i16,
+  // B = K rows 8*g4l + qq (+4) of d columns 16*slice + i16; both + 32 keys per k-step
+  constexpr int DQT = NDS == 4 ? 1 : 2;  // query halves per wave (D = 64: 8 waves x 1 half)
+  const int dslice = NDS == 4 ? (w & 3) : w;
+  const int dthalf = NDS == 4 ? (w >> 2) : 0;
+  int qoff[DQT][2], koff[2];
+#pragma unroll
+  for (int t = 0; t < DQT; ++t) {
+    const int tt = NDS == 4 ? dthalf : t;
+    qoff[t][0] = ds_off(8 * g4l + qq, 4 * tt + pp);
+    qoff[t][1] = ds_off(8 * g4l + 4 + qq, 4 * tt + pp);
+  }
+  {
+    const int ch = 2 * dslice + (pp >> 1), sub = (pp & 1) * 4;
+    koff[0] = swz<DP>(8 * g4l + qq, ch) + sub;
+    koff[1] = swz<DP>(8 * g4l + 4 + qq, ch) + sub;
+  }
+
+  const int* se = p.seg_end ? p.seg_end + static_cast<int64_t>(b) * p.Tk : nullptr;
+  int kse = 0x7fffffff, kse_lo = 0x7fffffff, kse_hi = 0x7fffffff;
+  if (se) {
+    kse = se[min(kw + l32, p.Tk - 1)];
+    kse_lo = __builtin_amdgcn_readfirstlane(se[min(kw, p.Tk - 1)]);
+    kse_hi = __builtin_amdgcn_readfirstlane(se[min(kw + 31, p.Tk - 1)]);
+  }
+
+  f32x16 dk[DT], dv[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) {
+    dk[dt] = f32x16{};
+    dv[dt] = f32x16{};
+  }
+
+  // Row constants enter through the MFMA chains: one extra k-step per chain whose A fragment
+  // holds this lane's query row's -lse2/scale2 (resp. -delta) split into bf16 hi + lo in k slots
+  // 0, 1 (lanes h = 0; zero elsewhere) against a B fragment of ones in the same slots, so the
+  // fp32 accumulators come out as S - lse2/scale2 and dP - delta. Per tile a wave loads 2
+  // dwords per lane (its own query row) instead of the 16 + 16 accumulator-row constants
+  // (8 dwordx4 loads per lane of data every lane holds 32-fold: the texture path, not the
+  // bytes, cost ~900 cycles per tile) and spends no VALU on accumulator initialisation.
+  float rlse = 0.f, rdel = 0.f;  // next tile's values for query row qt + l32
+  auto load_rows = [&](int hq, int qt) {
+    const int64_t rb = (static_cast<int64_t>(b) * p.Hq + hq) * p.Tq;
+    const int r = min(qt + l32, p.Tq - 1);
+    rlse = p.lse2[rb + r];
+    rdel = p.delta[rb + r];
+  };
+  typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+  const s16x8 ones = __builtin_bit_cast(s16x8, u32x4v{h ? 0u : 0x3F803F80u, 0u, 0u, 0u});
+  const float inv_s2 = 1.f / p.scale2;
+
+  int hq = hq0, qt = qt0;        // tile it
+  int hq_r = hq0, qt_r = qt0;    // tile it + 1 (row constants)
+  int hq_p = hq0, qt_p = qt0;    // tile it + 2 (Q / dO prefetch)
+  if (n_iter > 0) {
+    prefetch(hq_p, qt_p);
+    stage();
+    load_rows(hq_r, qt_r);
+    advance(hq_p, qt_p);
+    if (n_iter > 1) prefetch(hq_p, qt_p);
+    advance(hq_p, qt_p);
+  }
+  __syncthreads();
+
+  // static priority for the second-dispatched half (waves 4-7 share SIMDs with 0-3 and lose
+  // every VALU arbitration by age otherwise; MI355X_MICROARCH "Two waves per SIMD" item 4)
+  if (w >= 4) __builtin_amdgcn_s_setprio(1);
+  for (int it = 0; it < n_iter; ++it) {
+    advance(hq_r, qt_r);
+    asm volatile("" : "+v"(rq), "+v"(rx), "+v"(tq0), "+v"(tx0), "+v"(tq1), "+v"(tx1), "+v"(wq), "+v"(wx));
+    auto roff = [&](int s) { return rq + (((2 * s) ^ rx) << 3); };
+    auto toff = [&](int dt, int r) { return r ? tq1 + (((4 * dt) ^ tx1) << 3) : tq0 + (((4 * dt) ^ tx0) << 3); };
+    BWD_TS(0);
+
+    bool act = kw < kend && kw + 32 > kbeg && qt < kse_hi;
+    bool need_mask = kw < kbeg || kw + 32 > kend || qt + BQ > p.Tq || qt + BQ > kse_lo;
+    if (CAUSAL) {
+      act = act && kw <= qt + BQ - 1 + p.causal_off;
+      need_mask = need_mask || (kw + 31 > qt + p.causal_off);
+      if (p.window > 0) {
+        act = act && (kw + 31 > qt + p.causal_off - p.window);
+        need_mask = need_mask || (kw <= qt + BQ - 1 + p.causal_off - p.window);
+      }
+    }
+
+    // ---------------------------------------------------------------- phase A
+    s16x8 sb0 = s16x8{}, sb1 = s16x8{};
+    if (act) {
+      f32x16 sacc = f32x16{}, dpacc = f32x16{};
+      const bf16_t* Kw = Ks + 32 * w * DP;
+      const bf16_t* Vw = Vs + 32 * w * DP;
+      // S chain, then dP chain: fragments one k-step ahead, the order pinned by sched_barriers
+      // (left free, the scheduler hoists all KS steps' reads and spills; both chains at once
+      // need twice the fragment registers)
+      s16x8 fa[2], fb[2];
+      auto chain = [&](const bf16_t* A, const bf16_t* Bm, f32x16& acc) {
+        fa[0] = *reinterpret_cast<const s16x8*>(A + roff(0));
+        fb[0] = *reinterpret_cast<const s16x8*>(Bm + roff(0));
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          if (s + 1 < KS) {
+            fa[(s + 1) & 1] = *reinterpret_cast<const s16x8*>(A + roff(s + 1));
+            fb[(s + 1) & 1] = *reinterpret_cast<const s16x8*>(Bm + roff(s + 1));
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          acc = mfma32(fa[s & 1], fb[s & 1], acc);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      };
+      chain(Qs, Kw, sacc);
+      chain(dOs, Vw, dpacc);
+      {  // + the row-constant k-step (last: its loads get the whole chains as slack)
+        const bool rv = qt + l32 < p.Tq;
+        float x = -rlse * inv_s2;
+        x = (rv && __builtin_isfinite(x)) ? x : -1e30f;  // rows past Tq / without keys: p = 0
+        const float y = rv ? -rdel : 0.f;
+        const float xh = bf2f(static_cast<bf16_t>(pack2bf(x, 0.f) & 0xffffu));
+        const float yh = bf2f(static_cast<bf16_t>(pack2bf(y, 0.f) & 0xffffu));
+        const s16x8 ax = __builtin_bit_cast(s16x8, u32x4v{h ? 0u : pack2bf(x, x - xh), 0u, 0u, 0u});
+        const s16x8 ay = __builtin_bit_cast(s16x8, u32x4v{h ? 0u : pack2bf(y, y - yh), 0u, 0u, 0u});
+        sacc = mfma32(ax, ones, sacc);
+        dpacc = mfma32(ay, ones, dpacc);
+      }
+      BWD_TS(1);
+      const int kj = kw + l32;
+      int lo = 0, hi = min(p.Tq, kse) - qt - 4 * h;
+      if (kj < kbeg || kj >= kend) hi = 0;
+      if (CAUSAL) {
+        const int dlt = kj - qt - p.causal_off - 4 * h;
+        lo = max(lo, dlt);
+        if (p.window > 0) hi = min(hi, dlt + p.window);
+      }
+      const unsigned span = hi > lo ? static_cast<unsigned>(hi - lo) : 0u;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int rr = (i & 3) + 8 * (i >> 2);
+        float pv = ex2(sacc[i] * p.scale2);
+        if (need_mask) pv = static_cast<unsigned>(rr - lo) < span ? pv : 0.f;
+        sacc[i] = pv;
+        dpacc[i] = pv * dpacc[i];
+      }
+      const s16x8 pb0 = pack8(sacc, 0), pb1 = pack8(sacc, 8);
+      sb0 = pack8(dpacc, 0);
+      sb1 = pack8(dpacc, 8);
+      BWD_TS(2);
+      // dV^T += dO^T P ; dK^T += Q^T dS (transposed fragments of column tile dt+1 read while
+      // tile dt's four MFMAs run)
+      s16x8 ta[2], tb[2], tc[2], td[2];
+      auto ld_kv = [&](int dt, int sl) {
+        const int o0 = toff(dt, 0), o1 = toff(dt, 1);
+        ta[sl] = cat4(tr_read(dOs + o0), tr_read(dOs + o1));
+        tb[sl] = cat4(tr_read(dOs + 16 * DP + o0), tr_read(dOs + 16 * DP + o1));
+        tc[sl] = cat4(tr_read(Qs + o0), tr_read(Qs + o1));
+        td[sl] = cat4(tr_read(Qs + 16 * DP + o0), tr_read(Qs + 16 * DP + o1));
+      };
+      ld_kv(0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        if (dt + 1 < DT) ld_kv(dt + 1, (dt + 1) & 1);
+        __builtin_amdgcn_sched_barrier(0);
+        // alternating accumulators: no MFMA waits on the one just issued
+        dv[dt] = mfma32(ta[dt & 1], pb0, dv[dt]);
+        dk[dt] = mfma32(tc[dt & 1], sb0, dk[dt]);
+        dv[dt] = mfma32(tb[dt & 1], pb1, dv[dt]);
+        dk[dt] = mfma32(td[dt & 1], sb1, dk[dt]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      BWD_TS(3);
+    }
+    {  // dS^T rows -> [key][32 queries] image (zero for an inactive sub-tile)
+      const u32x4 ds0 = __builtin_bit_cast(u32x4, sb0), ds1 = __builtin_bit_cast(u32x4, sb1);
+      bf16_t* dSw = dSs + 32 * w * 32;
+      *reinterpret_cast<uint2*>(dSw + wq + ((0 ^ wx) << 2)) = make_uint2(ds0[0], ds0[1]);
+      *reinterpret_cast<uint2*>(dSw + wq + ((2 ^ wx) << 2)) = make_uint2(ds0[2], ds0[3]);
+      *reinterpret_cast<uint2*>(dSw + wq + ((4 ^ wx) << 2)) = make_uint2(ds1[0], ds1[1]);
+      *reinterpret_cast<uint2*>(dSw + wq + ((6 ^ wx) << 2)) = make_uint2(ds1[2], ds1[3]);
+    }
+    BWD_TS(4);
+    __syncthreads();
+    BWD_TS(5);
+
+    // ---------------------------------------------------------------- phase B
+    if (it + 1 < n_iter) {
+      stage();
+      if (it + 2 < n_iter) prefetch(hq_p, qt_p);
+      load_rows(hq_r, qt_r);
+    }
+    BWD_TS(6);
+    if (w < NDS || NDS == 4) {
+      f32x4 acc[DQT];
+#pragma unroll
+      for (int t = 0; t < DQT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      // fragments two k-steps ahead (phase B has the registers: the score accumulators are dead)
+      constexpr int NB = 3, NKS = BKV / 32;
+      s16x8 kf[NB], af[NB][DQT];
+      auto ld_dq = [&](int ks, int sl) {
+        kf[sl] = cat4(tr_read(Ks + 32 * ks * DP + koff[0]), tr_read(Ks + 32 * ks * DP + koff[1]));
+#pragma unroll
+        for (int t = 0; t < DQT; ++t)
+          af[sl][t] = cat4(tr_read(dSs + 32 * ks * 32 + qoff[t][0]), tr_read(dSs + 32 * ks * 32 + qoff[t][1]));
+      };
+      ld_dq(0, 0);
+      ld_dq(1, 1);
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+        if (ks + 2 < NKS) ld_dq(ks + 2, (ks + 2) % NB);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int t = 0; t < DQT; ++t)
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks % NB][t], kf[ks % NB], acc[t], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // lane holds d = 16*slice + i16 of query rows 16t + 4*g4l + e (64-B row segments)
+      const int64_t rs = static_cast<int64_t>(p.Hq) * D;
+      char* sp = reinterpret_cast<char*>(p.dq_slab + ((static_cast<int64_t>(kb) * p.B + b) * p.slab_rows + qt) * rs +
+                                         static_cast<int64_t>(hq) * D + 16 * dslice);
+      const uint32_t so = static_cast<uint32_t>(4 * g4l * rs + i16) * 4u;
+#pragma unroll
+      for (int t = 0; t < DQT; ++t) {
+        const int tt = NDS == 4 ? dthalf : t;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          *reinterpret_cast<float*>(sp + (16 * tt + e) * rs * 4 + so) = acc[t][e] * p.scale;
+      }
+    }
+    BWD_TS(7);
+    __syncthreads();
+    advance(hq, qt);
+    advance(hq_p, qt_p);
+  }
+
+  const int kj = kw + l32;
+  if (kj >= p.Tk) return;
+  if (p.hsplit == 1) {
+    bf16_t* dkp = p.dk + b * p.dk_sb + kj * p.dk_st + static_cast<int64_t>(hk) * p.dk_sh;
+    bf16_t* dvp = p.dv + b * p.dv_sb + kj * p.dv_st + static_cast<int64_t>(hk) * p.dv_sh;
+    auto store_row = [&](bf16_t* dst, f32x16 x, float sc, int dt) {
+#pragma unroll
+      for (int g4 = 0; g4 < 4; g4 += 2) {
+        const uint32_t a0 = pack2bf(x[4 * g4] * sc, x[4 * g4 + 1] * sc);
+        const uint32_t a1 = pack2bf(x[4 * g4 + 2] * sc, x[4 * g4 + 3] * sc);
+        const uint32_t c0 = pack2bf(x[4 * g4 + 4] * sc, x[4 * g4 + 5] * sc);
+        const uint32_t c1 = pack2bf(x[4 * g4 + 6] * sc, x[4 * g4 + 7] * sc);
+        const auto r0 = __builtin_amdgcn_permlane32_swap(a0, c0, false, false);
+        const auto r1 = __builtin_amdgcn_permlane32_swap(a1, c1, false, false);
+        if (32 * dt + 8 * g4 + 8 * h < D)
+          *reinterpret_cast<uint4*>(dst + 32 * dt + 8 * g4 + 8 * h) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
+      }
+    };
+    if (DP == D && p.rope_cos != nullptr) {
+      const int pos = p.rope_pos ? p.rope_pos[static_cast<int64_t>(b) * p.Tk + kj] : kj;
+      const float* cp = p.rope_cos + static_cast<int64_t>(pos) * (D / 2) + 4 * h;
+      const float* sp = p.rope_sin + static_cast<int64_t>(pos) * (D / 2) + 4 * h;
+#pragma unroll
+      for (int dt = 0; dt < DT / 2; ++dt) {
+        f32x16 lo = dk[dt], hi = dk[dt + DT / 2];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 c4 = *reinterpret_cast<const f32x4*>(cp + 32 * dt + 8 * g);
+          const f32x4 s4 = *reinterpret_cast<const f32x4*>(sp + 32 * dt + 8 * g);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float a = lo[4 * g + e], bb = hi[4 * g + e];
+            lo[4 * g + e] = a * c4[e] + bb * s4[e];
+            hi[4 * g + e] = bb * c4[e] - a * s4[e];
+          }
+        }
+        store_row(dkp, lo, p.scale, dt);
+        store_row(dkp, hi, p.scale, dt + DT / 2);
+      }
+    } else {
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) store_row(dkp, dk[dt], p.scale, dt);
+    }
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) store_row(dvp, dv[dt], 1.f, dt);
+  } else {
+    const int64_t off = ((static_cast<int64_t>(sidx) * p.B + b) * p.Tk + kj) * p.Hkv * D +
+                        static_cast<int64_t>(hk) * D;
+    float* dkp = p.dk_part + off;
+    float* dvp = p.dv_part + off;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d = 32 * dt + 8 * g4 + 4 * h;
+        if (d >= D) continue;
+        *reinterpret_cast<f32x4*>(dkp + d) = f32x4{dk[dt][4 * g4], dk[dt][4 * g4 + 1], dk[dt][4 * g4 + 2], dk[dt][4 * g4 + 3]};
+        *reinterpret_cast<f32x4*>(dvp + d) = f32x4{dv[dt][4 * g4], dv[dt][4 * g4 + 1], dv[dt][4 * g4 + 2], dv[dt][4 * g4 + 3]};
+      }
+    }
+  }
+}
+
 // Sum of the 8-column chunk at `src` over key blocks [lo, hi) of the slab (fixed kb order, 4
 // blocks' loads in flight at a time: bitwise the same as one at a time).
 __device__ __forceinline__ void slab_sum8(const float* src, int64_t slab_stride, int lo, int hi,
@@ -1125,10 +1578,22 @@ void launch_attn_bwd_delta(const bf16_t* o, const bf16_t* dout, int64_t o_sb, in
       o, dout, o_sb, o_st, o_sh, do_sb, do_st, do_sh, B, H, T, D, delta);
 }
 
+// Backward main kernel: DLA_ATTN_BWD_WAVES=8 (attn_bwd8_kernel) or 4 (attn_bwd_kernel).
+// Read per call (not cached) so one process can A/B both.
+static int attn_bwd_waves() {
+  const char* e = std::getenv("DLA_ATTN_BWD_WAVES");
+  return (e && std::atoi(e) == 8) ? 8 : 4;
+}
+
 template <int D>
 static void bwd_dispatch(const AttnBwdParams& p, bool causal, hipStream_t st) {
   const int nkb = (p.Tk + kAttnBwdKeys - 1) / kAttnBwdKeys;
   const dim3 grid(nkb * p.Hkv * p.B * p.hsplit);
+  if (attn_bwd_waves() == 8) {
+    if (causal) attn_bwd8_kernel<D, true><<<grid, 512, 0, st>>>(p);
+    else attn_bwd8_kernel<D, false><<<grid, 512, 0, st>>>(p);
+    return;
+  }
   if (causal) attn_bwd_kernel<D, true><<<grid, 256, 0, st>>>(p);
   else attn_bwd_kernel<D, false><<<grid, 256, 0, st>>>(p);
 }

@@ -124,6 +124,14 @@ def test_fused_swiglu_mlp_main_grad():
 
 
 # ------------------------------------------------------------------------------- attention
+@pytest.fixture(params=["4", "8"], ids=["bwd4", "bwd8"])
+def bwd_waves(request, monkeypatch):
+    """Run an attention-backward test on both main kernels: attn_bwd_kernel (4 waves, one per
+    SIMD) and attn_bwd8_kernel (8 waves); the launcher reads DLA_ATTN_BWD_WAVES per call."""
+    monkeypatch.setenv("DLA_ATTN_BWD_WAVES", request.param)
+    return request.param
+
+
 def _qkv_ref(qkv, Hq, Hkv, D, rope, kv_start, kv_end, window, positions):
     B, T, _ = qkv.shape
     q = qkv[..., : Hq * D].reshape(B, T, Hq, D)
@@ -140,7 +148,7 @@ def _qkv_ref(qkv, Hq, Hkv, D, rope, kv_start, kv_end, window, positions):
 
 @pytest.mark.parametrize("D", [128, 64])
 @pytest.mark.parametrize("case", ["plain", "rightpad", "leftpad", "window", "norope"])
-def test_qkv_attention_fwd_bwd(D, case):
+def test_qkv_attention_fwd_bwd(D, case, bwd_waves):
     B, T, Hq, Hkv = 2, 200, 8, 2
     C = (Hq + 2 * Hkv) * D
     qkv = bf(torch.randn(B, T, C)).requires_grad_()
@@ -185,7 +193,7 @@ def test_attention_core_decode_offset():
 
 
 @pytest.mark.parametrize("case", ["causal_gqa", "leftpad_window", "noncausal_rightpad", "mha"])
-def test_attention_multi_keyblock_bwd(case):
+def test_attention_multi_keyblock_bwd(case, bwd_waves):
     """T spans several 256-key backward workgroups: per-key-block dQ slabs + ordered reduce,
     head-split dK/dV partials (GQA) and the single-split path (MHA)."""
     B, T, Hq, Hkv, D = 2, 600, 8, 2, 128
@@ -217,7 +225,7 @@ def test_attention_multi_keyblock_bwd(case):
 
 
 @pytest.mark.parametrize("Hq,Hkv", [(8, 1), (64, 8), (16, 2)])
-def test_attention_gqa8_llama70b_shapes(Hq, Hkv):
+def test_attention_gqa8_llama70b_shapes(Hq, Hkv, bwd_waves):
     """Llama-3-70B's GQA 8:1 through the fused QKV path: (8, 1) is one tensor-parallel rank at
     TP=8 (a single KV head: every query head of the workgroup shares it), (64, 8) the whole
     layer; T spans several backward key blocks. fp32 reference on the same bf16 inputs."""
@@ -290,7 +298,7 @@ def _fp32_forward(model, ids):
 
 
 @pytest.mark.parametrize("window", [0, 200])
-def test_attention_packed_segments(window):
+def test_attention_packed_segments(window, bwd_waves):
     """Packed sequences (block-diagonal causal mask via [2, B, T] segment bounds) over several
     256-key backward workgroups and 256-query forward blocks, GQA, with trailing padding."""
     from distributed_llm_alignment_amd.models.transformer import packed_layout
@@ -337,7 +345,7 @@ def test_packed_model_matches_separate_gpu():
         o += len(x)
 
 
-def test_attention_bwd_deterministic():
+def test_attention_bwd_deterministic(bwd_waves):
     """dQ is summed from per-key-block slabs in a fixed order (no float atomics): bitwise
     reproducible gradients."""
     B, T, Hq, Hkv, D = 2, 700, 8, 2, 128
@@ -367,7 +375,7 @@ def test_attention_fwd_forced_rescale():
     assert (o[0, 310, 0].float() - r[0, 310, 0]).abs().max().item() < 5e-2
 
 
-def test_attention_long_seq_grad_llama_shape():
+def test_attention_long_seq_grad_llama_shape(bwd_waves):
     B, T, Hq, Hkv, D = 1, 1024, 32, 8, 128
     C = (Hq + 2 * Hkv) * D
     qkv = bf(torch.randn(B, T, C)).requires_grad_()
@@ -383,7 +391,7 @@ def test_attention_long_seq_grad_llama_shape():
 
 
 @pytest.mark.parametrize("leftpad", [False, True])
-def test_attention_fused_rope_bwd_unsplit_grid(leftpad):
+def test_attention_fused_rope_bwd_unsplit_grid(leftpad, bwd_waves):
     """Full-rotary RoPE backward folded into the attention backward at a shape whose grid needs
     no GQA head split (B*Hkv*key blocks >= the CU count, non-causal): dK is un-rotated in the main
     kernel's epilogue (partner column tile in the same lane), dQ in the slab reduce; explicit
@@ -833,7 +841,7 @@ def test_odd_head_dim_partial_rotary_attention_fwd_bwd():
 
 
 @pytest.mark.parametrize("case", ["causal_mha", "causal_gqa_leftpad", "noncausal_window"])
-def test_attention_head_dim_80_native(case):
+def test_attention_head_dim_80_native(case, bwd_waves):
     """Native D = 80 tiles (phi-2, the reference's distill student: 96-wide LDS images, 5 MFMA
     k-steps, pad columns never stored) over several 256-key backward blocks, GQA, padding and
     a window, against fp32; and equal to the padded-to-128 path to bf16 accuracy."""

@@ -1,11 +1,10 @@
+#!/bin/bash
 set -o pipefail
 mkdir -p gpurun_out
-export PYTHONUNBUFFERED=1 TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/r3_gpu_tests3.log 2>&1
-rc=$?; tail -3 gpurun_out/r3_gpu_tests3.log; [ $rc -eq 0 ] || { grep -E "FAIL|Error|assert" gpurun_out/r3_gpu_tests3.log | head -30; exit $rc; }
-timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 > gpurun_out/r3_bench1.log 2>&1 || { tail -5 gpurun_out/r3_bench1.log; exit 1; }
-tail -1 gpurun_out/r3_bench1.log
-timeout -k 10 120 python -u tools/bench_handoff.py > gpurun_out/r3_handoff.log 2>&1 || exit 1
-cat gpurun_out/r3_handoff.log
-timeout -k 10 300 python -u tools/bench_generate.py --modes graph --new 128 --batch 64 --prompt 512 > gpurun_out/r3_gen64.log 2>&1 || exit 1
-tail -1 gpurun_out/r3_gen64.log
+timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -m gpu -x -q -k "attention or qkv" --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/r3_attn_tests.log 2>&1 || { tail -30 gpurun_out/r3_attn_tests.log; exit 1; }
+tail -1 gpurun_out/r3_attn_tests.log
+timeout -k 10 60 tools/attn_bwd_probe.bin 8 > gpurun_out/probe.log 2>&1 || { cat gpurun_out/probe.log; exit 1; }
+grep -v "tile 10" gpurun_out/probe.log
+timeout -k 10 200 python -u tools/attn_bench.py --ab DLA_ATTN_BWD_WAVES=4,8 --rounds 3 > gpurun_out/r3_attn_ab.log 2>&1 || { tail -20 gpurun_out/r3_attn_ab.log; exit 1; }
+for hs in 1 2 4; do DLA_ATTN_BWD_WAVES=8 DLA_ATTN_BWD_HSPLIT=$hs timeout -k 10 100 python -u tools/attn_bench.py >> gpurun_out/r3_attn_ab.log 2>&1 || exit 1; done
+grep attn gpurun_out/r3_attn_ab.log

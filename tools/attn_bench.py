@@ -21,7 +21,7 @@ def main() -> int:
     ap.add_argument("--D", type=int, default=128)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--noncausal", action="store_true")
-    ap.add_argument("--ab", default="", help="NAME[=v0,v1]: env var to A/B on the forward, interleaved")
+    ap.add_argument("--ab", default="", help="NAME[=v0,v1]: env var to A/B (forward and backward), interleaved")
     ap.add_argument("--rounds", type=int, default=3)
     a = ap.parse_args()
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -63,12 +63,25 @@ def main() -> int:
                     ops.attention_core(q, k, v, causal=causal)
                 torch.cuda.synchronize()
                 best[val] = min(best.get(val, 1e9), (time.perf_counter() - t0) / a.iters)
+        # backward (all kernels: delta, main, dQ reduce, dK/dV reduce), same interleaving
+        bbest, gouts = {}, {}
+        for _ in range(a.rounds):
+            for val in vals:
+                os.environ[name] = val
+                gouts[val] = torch.autograd.grad(o, [q, k, v], do, retain_graph=True)
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for _ in range(a.iters):
+                    torch.autograd.grad(o, [q, k, v], do, retain_graph=True)
+                torch.cuda.synchronize()
+                bbest[val] = min(bbest.get(val, 1e9), (time.perf_counter() - t0) / a.iters)
         os.environ.pop(name)
         diff = (outs[vals[0]].float() - outs[vals[1]].float()).abs().max().item()
+        gdiff = max((x.float() - y.float()).abs().max().item() for x, y in zip(gouts[vals[0]], gouts[vals[1]]))
         for val in vals:
-            print(f"[attn-ab] {name}={val} fwd {best[val]*1e6:.1f} us ({flops_fwd/best[val]/1e12:.0f} TF/s)",
-                  flush=True)
-        print(f"[attn-ab] max |o0 - o1| = {diff:.3e}", flush=True)
+            print(f"[attn-ab] {name}={val} fwd {best[val]*1e6:.1f} us ({flops_fwd/best[val]/1e12:.0f} TF/s) "
+                  f"bwd {bbest[val]*1e6:.1f} us ({2.5*flops_fwd/bbest[val]/1e12:.0f} TF/s)", flush=True)
+        print(f"[attn-ab] max |o0 - o1| = {diff:.3e}  max |grad0 - grad1| = {gdiff:.3e}", flush=True)
     print(f"[attn] B={a.B} T={a.T} Hq={a.Hq} causal={causal} fwd {tf*1e6:.1f} us ({flops_fwd/tf/1e12:.0f} TF/s)  bwd(all kernels) {tb*1e6:.1f} us "
           f"({2.5*flops_fwd/tb/1e12:.0f} TF/s)", flush=True)
     return 0
