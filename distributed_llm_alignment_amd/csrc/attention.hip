@@ -143,6 +143,25 @@ __device__ __forceinline__ s16x8 tr_frag_nat(const bf16_t* img, int r0, int c0, 
   return cat4(a, b);
 }
 
+// Partial-rotary backward (phi-2: rot = 32 at D = 80): in the dK^T accumulator tile 0 (lane =
+// key, register i = column d = (i&3) + 8(i>>2) + 4h), column d < 16 pairs with d + 16 =
+// register i + 8 of the same lane; un-rotate (lo = a c + b s, hi = b c - a s) with
+// cp / sp = cos / sin + pos * 16 + 4h.
+__device__ __forceinline__ f32x16 unrotate_tile0_rot32(f32x16 x, const float* cp, const float* sp) {
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    const f32x4 c4 = *reinterpret_cast<const f32x4*>(cp + 8 * g);
+    const f32x4 s4 = *reinterpret_cast<const f32x4*>(sp + 8 * g);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float a = x[4 * g + e], bb = x[4 * g + e + 8];
+      x[4 * g + e] = a * c4[e] + bb * s4[e];
+      x[4 * g + e + 8] = bb * c4[e] - a * s4[e];
+    }
+  }
+  return x;
+}
+
 // ==============================================================================================
 // forward
 // ==============================================================================================
@@ -874,7 +893,14 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_kernel(AttnBwdParams p) {
             *reinterpret_cast<uint4*>(dst + 32 * dt + 8 * g4 + 8 * h) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
         }
       };
-      if (DP == D && p.rope_cos != nullptr) {
+      if (D == 80 && p.rope_cos != nullptr) {  // partial rotary (rot = 32): column tile 0 only
+        const int pos = p.rope_pos ? p.rope_pos[static_cast<int64_t>(b) * p.Tk + kj] : kj;
+        store_row(dkp, unrotate_tile0_rot32(dk[j][0], p.rope_cos + static_cast<int64_t>(pos) * 16 + 4 * h,
+                                            p.rope_sin + static_cast<int64_t>(pos) * 16 + 4 * h),
+                  p.scale, 0);
+#pragma unroll
+        for (int dt = 1; dt < DT; ++dt) store_row(dkp, dk[j][dt], p.scale, dt);
+      } else if (DP == D && p.rope_cos != nullptr) {
         // fused RoPE backward: column d < D/2 pairs with d + D/2 = the same register of column
         // tile dt + DT/2 in this lane (un-rotation: lo = a c + b s, hi = b c - a s), applied to
         // register copies on the way out (writing the accumulators back spilled in the loop)
@@ -1329,7 +1355,14 @@ __global__ __launch_bounds__(512) void attn_bwd8_kernel(AttnBwdParams p) {
           *reinterpret_cast<uint4*>(dst + 32 * dt + 8 * g4 + 8 * h) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
       }
     };
-    if (DP == D && p.rope_cos != nullptr) {
+    if (D == 80 && p.rope_cos != nullptr) {  // partial rotary (rot = 32): column tile 0 only
+      const int pos = p.rope_pos ? p.rope_pos[static_cast<int64_t>(b) * p.Tk + kj] : kj;
+      store_row(dkp, unrotate_tile0_rot32(dk[0], p.rope_cos + static_cast<int64_t>(pos) * 16 + 4 * h,
+                                          p.rope_sin + static_cast<int64_t>(pos) * 16 + 4 * h),
+                p.scale, 0);
+#pragma unroll
+      for (int dt = 1; dt < DT; ++dt) store_row(dkp, dk[dt], p.scale, dt);
+    } else if (DP == D && p.rope_cos != nullptr) {
       const int pos = p.rope_pos ? p.rope_pos[static_cast<int64_t>(b) * p.Tk + kj] : kj;
       const float* cp = p.rope_cos + static_cast<int64_t>(pos) * (D / 2) + 4 * h;
       const float* sp = p.rope_sin + static_cast<int64_t>(pos) * (D / 2) + 4 * h;
@@ -1421,9 +1454,12 @@ __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(
     const float* __restrict__ slab, int nkb, int B, int Tq, int slab_rows, int Hq, int D,
     int causal_off, int window, const int* __restrict__ kv_start, const int* __restrict__ kv_end,
     int Tk, bf16_t* __restrict__ dst, int64_t d_sb, int64_t d_st, int64_t d_sh,
-    const float* __restrict__ rcos, const float* __restrict__ rsin, const int* __restrict__ rpos) {
-  const int hv = D / 16;
-  const int cv = rcos ? hv : D / 8;  // work items per row
+    const float* __restrict__ rcos, const float* __restrict__ rsin, const int* __restrict__ rpos,
+    int rot) {
+  // work items per row: without RoPE one per 8 columns; with it one per rotary chunk pair
+  // (c, c + rot/16) plus one per 8 columns past the rotary dims (partial rotary, D = 80)
+  const int hv = rot / 16;
+  const int cv = rcos ? hv + (D - rot) / 8 : D / 8;
   const int64_t total = static_cast<int64_t>(B) * Tq * Hq * cv;
   const int64_t rs = static_cast<int64_t>(Hq) * D;
   const int64_t slab_stride = static_cast<int64_t>(B) * slab_rows * rs;
@@ -1436,7 +1472,9 @@ __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(
     const int b = static_cast<int>(r / Tq);
     const int kbeg = kv_start ? kv_start[b] : 0;
     const int kend = kv_end ? kv_end[b] : Tk;
-    const float* src = slab + (static_cast<int64_t>(b) * slab_rows + t) * rs + static_cast<int64_t>(hq) * D + c * 8;
+    const bool pair = rcos && c < hv;
+    const int col = (rcos && !pair) ? rot + (c - hv) * 8 : c * 8;
+    const float* src = slab + (static_cast<int64_t>(b) * slab_rows + t) * rs + static_cast<int64_t>(hq) * D + col;
     // the key blocks that wrote row t form one contiguous range [lo, hi) (kv range: an
     // interval; causal: a prefix; window: a suffix): find it with ALU only, then sum the slabs
     // in kb order with 4 blocks' loads in flight at a time (same order as one at a time: the
@@ -1453,14 +1491,14 @@ __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(
     f32x4 a0, a1;
     slab_sum8(src, slab_stride, lo, hi, a0, a1);
     float v[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
-    bf16_t* out = dst + b * d_sb + t * d_st + hq * d_sh + c * 8;
-    if (rcos) {
+    bf16_t* out = dst + b * d_sb + t * d_st + hq * d_sh + col;
+    if (pair) {
       f32x4 b0, b1;
       slab_sum8(src + hv * 8, slab_stride, lo, hi, b0, b1);
       float w[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
       const int pos = rpos ? rpos[static_cast<int64_t>(b) * Tq + t] : t;
-      rope_unrotate8(rcos + static_cast<int64_t>(pos) * (D / 2) + c * 8,
-                     rsin + static_cast<int64_t>(pos) * (D / 2) + c * 8, v, w);
+      rope_unrotate8(rcos + static_cast<int64_t>(pos) * (rot / 2) + c * 8,
+                     rsin + static_cast<int64_t>(pos) * (rot / 2) + c * 8, v, w);
       store_bf16x8(out + hv * 8, pack_bf16x8(w));
     }
     store_bf16x8(out, pack_bf16x8(v));
@@ -1483,9 +1521,10 @@ __global__ __launch_bounds__(256) void attn_dkv_reduce_kernel(
     const float* __restrict__ dkp, const float* __restrict__ dvp, int hs, int B, int Tk, int Hkv,
     int D, float scale, bf16_t* __restrict__ dk, int64_t dk_sb, int64_t dk_st, int64_t dk_sh,
     bf16_t* __restrict__ dv, int64_t dv_sb, int64_t dv_st, int64_t dv_sh,
-    const float* __restrict__ rcos, const float* __restrict__ rsin, const int* __restrict__ rpos) {
-  const int hv = D / 16;
-  const int cv = rcos ? hv : D / 8;
+    const float* __restrict__ rcos, const float* __restrict__ rsin, const int* __restrict__ rpos,
+    int rot) {
+  const int hv = rot / 16;  // work items as attn_dq_reduce_kernel
+  const int cv = rcos ? hv + (D - rot) / 8 : D / 8;
   const int64_t total = static_cast<int64_t>(B) * Tk * Hkv * cv;
   const int64_t pstride = static_cast<int64_t>(B) * Tk * Hkv * D;
   for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += static_cast<int64_t>(gridDim.x) * 256) {
@@ -1495,24 +1534,26 @@ __global__ __launch_bounds__(256) void attn_dkv_reduce_kernel(
     r /= Hkv;
     const int t = static_cast<int>(r % Tk);
     const int b = static_cast<int>(r / Tk);
-    const int64_t off = ((static_cast<int64_t>(b) * Tk + t) * Hkv + hk) * D + c * 8;
+    const bool pair = rcos && c < hv;
+    const int col = (rcos && !pair) ? rot + (c - hv) * 8 : c * 8;
+    const int64_t off = ((static_cast<int64_t>(b) * Tk + t) * Hkv + hk) * D + col;
     f32x4 k0, k1, v0, v1;
     part_sum8(dkp + off, pstride, hs, k0, k1);
     part_sum8(dvp + off, pstride, hs, v0, v1);
     float kf[8] = {k0[0] * scale, k0[1] * scale, k0[2] * scale, k0[3] * scale,
                    k1[0] * scale, k1[1] * scale, k1[2] * scale, k1[3] * scale};
     const float vf[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-    bf16_t* kout = dk + b * dk_sb + t * dk_st + hk * dk_sh + c * 8;
-    bf16_t* vout = dv + b * dv_sb + t * dv_st + hk * dv_sh + c * 8;
-    if (rcos) {  // partner chunk c + D/16: dV copied through, dK un-rotated with its pair
+    bf16_t* kout = dk + b * dk_sb + t * dk_st + hk * dk_sh + col;
+    bf16_t* vout = dv + b * dv_sb + t * dv_st + hk * dv_sh + col;
+    if (pair) {  // partner chunk c + rot/16: dV copied through, dK un-rotated with its pair
       part_sum8(dkp + off + hv * 8, pstride, hs, k0, k1);
       part_sum8(dvp + off + hv * 8, pstride, hs, v0, v1);
       float kw[8] = {k0[0] * scale, k0[1] * scale, k0[2] * scale, k0[3] * scale,
                      k1[0] * scale, k1[1] * scale, k1[2] * scale, k1[3] * scale};
       const float vw[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
       const int pos = rpos ? rpos[static_cast<int64_t>(b) * Tk + t] : t;
-      rope_unrotate8(rcos + static_cast<int64_t>(pos) * (D / 2) + c * 8,
-                     rsin + static_cast<int64_t>(pos) * (D / 2) + c * 8, kf, kw);
+      rope_unrotate8(rcos + static_cast<int64_t>(pos) * (rot / 2) + c * 8,
+                     rsin + static_cast<int64_t>(pos) * (rot / 2) + c * 8, kf, kw);
       store_bf16x8(kout + hv * 8, pack_bf16x8(kw));
       store_bf16x8(vout + hv * 8, pack_bf16x8(vw));
     }
@@ -1578,11 +1619,13 @@ void launch_attn_bwd_delta(const bf16_t* o, const bf16_t* dout, int64_t o_sb, in
       o, dout, o_sb, o_st, o_sh, do_sb, do_st, do_sh, B, H, T, D, delta);
 }
 
-// Backward main kernel: DLA_ATTN_BWD_WAVES=8 (attn_bwd8_kernel) or 4 (attn_bwd_kernel).
-// Read per call (not cached) so one process can A/B both.
+// Backward main kernel: attn_bwd8_kernel (8 waves, default) or attn_bwd_kernel
+// (DLA_ATTN_BWD_WAVES=4). Same-box A/B, B8 T1024 Hq32 Hkv8 D128 causal, all backward passes:
+// 489 -> 410 us; non-causal 624 -> 549 us (profiles/r3_attention_bwd.md). Read per call (not
+// cached) so one process can A/B both.
 static int attn_bwd_waves() {
   const char* e = std::getenv("DLA_ATTN_BWD_WAVES");
-  return (e && std::atoi(e) == 8) ? 8 : 4;
+  return (e && std::atoi(e) == 4) ? 4 : 8;
 }
 
 template <int D>
@@ -1612,29 +1655,29 @@ void launch_attn_dq_reduce(const float* slab, int nkb, int B, int Tq, int slab_r
                            bool causal, int causal_off, int window, const int* kv_start,
                            const int* kv_end, int Tk, bf16_t* dst, int64_t d_sb, int64_t d_st,
                            int64_t d_sh, const float* rcos, const float* rsin, const int* rpos,
-                           hipStream_t st) {
-  const int64_t work = static_cast<int64_t>(B) * Tq * Hq * (rcos ? D / 16 : D / 8);
+                           int rot, hipStream_t st) {
+  const int64_t work = static_cast<int64_t>(B) * Tq * Hq * (rcos ? rot / 16 + (D - rot) / 8 : D / 8);
   if (work == 0) return;
   if (causal)
     attn_dq_reduce_kernel<true><<<stream_grid(work), 256, 0, st>>>(
         slab, nkb, B, Tq, slab_rows, Hq, D, causal_off, window, kv_start, kv_end, Tk, dst, d_sb, d_st, d_sh,
-        rcos, rsin, rpos);
+        rcos, rsin, rpos, rot);
   else
     attn_dq_reduce_kernel<false><<<stream_grid(work), 256, 0, st>>>(
         slab, nkb, B, Tq, slab_rows, Hq, D, causal_off, window, kv_start, kv_end, Tk, dst, d_sb, d_st, d_sh,
-        rcos, rsin, rpos);
+        rcos, rsin, rpos, rot);
 }
 
 void launch_attn_dkv_reduce(const float* dkp, const float* dvp, int hs, int B, int Tk, int Hkv,
                             int D, float scale, bf16_t* dk, int64_t dk_sb, int64_t dk_st,
                             int64_t dk_sh, bf16_t* dv, int64_t dv_sb, int64_t dv_st,
                             int64_t dv_sh, const float* rcos, const float* rsin, const int* rpos,
-                            hipStream_t st) {
-  const int64_t work = static_cast<int64_t>(B) * Tk * Hkv * (rcos ? D / 16 : D / 8);
+                            int rot, hipStream_t st) {
+  const int64_t work = static_cast<int64_t>(B) * Tk * Hkv * (rcos ? rot / 16 + (D - rot) / 8 : D / 8);
   if (work == 0) return;
   attn_dkv_reduce_kernel<<<stream_grid(work), 256, 0, st>>>(dkp, dvp, hs, B, Tk, Hkv, D, scale, dk,
                                                             dk_sb, dk_st, dk_sh, dv, dv_sb, dv_st,
-                                                            dv_sh, rcos, rsin, rpos);
+                                                            dv_sh, rcos, rsin, rpos, rot);
 }
 
 }  // namespace dla

@@ -74,6 +74,8 @@ struct AttnBwdParams {
   const int* rope_pos;    // [B * T] token positions, or null: position = t
   int rope_inputs;        // 1: k arrives un-rotated and is rotated as it is staged (q is the
                           // forward's q_rot output)
+  int rope_rot;           // rotary dims: D (full), or 32 at D = 80 (phi-2's partial rotary:
+                          // only dims [0, 32) rotate, d < 16 pairing with d + 16)
 };
 
 }  // namespace dla

@@ -73,10 +73,10 @@ void launch_attn_bwd_delta(const bf16_t*, const bf16_t*, int64_t, int64_t, int64
 void launch_attn_bwd(const AttnBwdParams&, int, bool, hipStream_t);
 void launch_attn_dq_reduce(const float*, int, int, int, int, int, int, bool, int, int,
                            const int*, const int*, int, bf16_t*, int64_t, int64_t, int64_t,
-                           const float*, const float*, const int*, hipStream_t);
+                           const float*, const float*, const int*, int, hipStream_t);
 void launch_attn_dkv_reduce(const float*, const float*, int, int, int, int, int, float, bf16_t*,
                             int64_t, int64_t, int64_t, bf16_t*, int64_t, int64_t, int64_t,
-                            const float*, const float*, const int*, hipStream_t);
+                            const float*, const float*, const int*, int, hipStream_t);
 void launch_transpose_bf16(const bf16_t*, int64_t, int64_t, int64_t, bf16_t*, int64_t, hipStream_t);
 
 // ================================= norms ======================================================
@@ -334,16 +334,23 @@ static const int* seg_ptr(const c10::optional<at::Tensor>& segs, int64_t B, int6
 static void rope_args(const c10::optional<at::Tensor>& rope_cos, const c10::optional<at::Tensor>& rope_sin,
                       const c10::optional<at::Tensor>& rope_pos, const at::Tensor& q, int64_t B,
                       int64_t Tq, int64_t Tk, int64_t D, int64_t causal_off, const float** cos_p,
-                      const float** sin_p, const int** pos_p) {
+                      const float** sin_p, const int** pos_p, int* rot_p = nullptr) {
   *cos_p = *sin_p = nullptr;
   *pos_p = nullptr;
+  if (rot_p) *rot_p = 0;
   if (!rope_cos || !rope_cos->defined()) return;
   TORCH_CHECK(rope_sin && rope_sin->defined(), "rope_sin missing");
+  // full rotary, or (backward only: rot_p given) phi-2's partial rotary, 32 of D = 80 dims
+  const int64_t half = rope_cos->dim() == 2 ? rope_cos->size(1) : -1;
+  const bool partial_ok = rot_p != nullptr && D == 80 && half == 16;
   for (const at::Tensor* t : {&*rope_cos, &*rope_sin}) {
     TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous() && t->dim() == 2 &&
-                    t->size(1) == D / 2, "rope cos/sin must be contiguous fp32 [max_pos, head_dim/2]");
+                    (t->size(1) == D / 2 || (partial_ok && t->size(1) == 16)),
+                "rope cos/sin must be contiguous fp32 [max_pos, head_dim/2] (or [max_pos, 16] at "
+                "head_dim 80 in the backward)");
     same_device(q, *t);
   }
+  if (rot_p) *rot_p = static_cast<int>(2 * half);
   TORCH_CHECK(Tq == Tk && causal_off == 0, "fused RoPE needs self-attention");
   if (rope_pos && rope_pos->defined()) {
     TORCH_CHECK(rope_pos->scalar_type() == at::kInt && rope_pos->is_contiguous() &&
@@ -515,20 +522,20 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k,
   // fused RoPE backward: dq / dk receive the un-rotated gradients (full rotary only); with
   // rope_inputs q / k are also un-rotated and get rotated as they are staged
   rope_args(rope_cos, rope_sin, rope_pos, q, B, Tq, Tk, D, causal_off, &p.rope_cos, &p.rope_sin,
-            &p.rope_pos);
+            &p.rope_pos, &p.rope_rot);
   TORCH_CHECK(!rope_inputs || p.rope_cos != nullptr, "rope_inputs needs the rotary tables");
-  TORCH_CHECK(p.rope_cos == nullptr || D != 80, "fused RoPE backward: full-rotary head dims 64 / 128 only");
+  TORCH_CHECK(!rope_inputs || p.rope_rot == D, "rope_inputs (RoPE on load): full rotary only");
   p.rope_inputs = rope_inputs ? 1 : 0;
   launch_attn_bwd(p, static_cast<int>(D), causal, st);
   launch_attn_dq_reduce(p.dq_slab, static_cast<int>(nkb), static_cast<int>(B), static_cast<int>(Tq),
                         p.slab_rows, static_cast<int>(Hq), static_cast<int>(D), causal, p.causal_off, p.window,
                         p.kv_start, p.kv_end, static_cast<int>(Tk), bp(dq), dq.stride(0),
-                        dq.stride(1), dq.stride(2), p.rope_cos, p.rope_sin, p.rope_pos, st);
+                        dq.stride(1), dq.stride(2), p.rope_cos, p.rope_sin, p.rope_pos, p.rope_rot, st);
   if (hs > 1) {
     launch_attn_dkv_reduce(p.dk_part, p.dv_part, hs, static_cast<int>(B), static_cast<int>(Tk),
                            static_cast<int>(Hkv), static_cast<int>(D), p.scale, bp(dk),
                            dk.stride(0), dk.stride(1), dk.stride(2), bp(dv), dv.stride(0),
-                           dv.stride(1), dv.stride(2), p.rope_cos, p.rope_sin, p.rope_pos, st);
+                           dv.stride(1), dv.stride(2), p.rope_cos, p.rope_sin, p.rope_pos, p.rope_rot, st);
   }
 }
 

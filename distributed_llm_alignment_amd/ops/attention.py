@@ -188,7 +188,10 @@ class _FusedQKVAttnFn(torch.autograd.Function):
         do4 = do.contiguous().view(B, T, Hq, D)
         dqkv = torch.empty((B, T, C), dtype=qkv.dtype, device=qkv.device)
         dv = dqkv.as_strided((B, T, Hkv, D), (T * C, C, D, 1), (Hq + Hkv) * D)
-        fused_rope = rot == D and D in (64, 128) and (FUSED_ROPE_BWD or ctx.on_load)
+        # full rotary at D 64 / 128, or phi-2's partial rotary (32 of D = 80 dims: the dK
+        # epilogue un-rotates column tile 0, the reduce passes the rotary chunk pairs)
+        fused_rope = (rot == D and D in (64, 128) or (D == 80 and rot == 32)) and \
+            (FUSED_ROPE_BWD or ctx.on_load)
         if rot > 0 and not fused_rope:  # rotated-space dq / dk, un-rotated by the RoPE backward
             dq = torch.empty((B, T, Hq, D), dtype=qkv.dtype, device=qkv.device)
             dk = torch.empty((B, T, Hkv, D), dtype=qkv.dtype, device=qkv.device)

@@ -877,3 +877,35 @@ def test_attention_head_dim_80_native(case, bwd_waves):
     op = ops.attention_core(pad(q), pad(k), pad(v), scale=1 / math.sqrt(D), causal=causal,
                             window=window, kv_start=ks, kv_end=ke)[..., :D]
     assert rel_err(o * valid, op * valid) < 1e-2
+
+
+@pytest.mark.parametrize("case", ["mha", "gqa_leftpad"])
+def test_attention_partial_rotary_d80_fused_bwd(case, bwd_waves):
+    """phi-2's partial rotary (32 of D = 80 dims) folded into the attention backward: dK
+    un-rotated in the main kernels' epilogue (column tile 0, registers i <-> i + 8), dQ and the
+    head-split dK/dV partials in the reduce passes (rotary chunk pairs + pass-through chunks);
+    fp32 reference with HF-style partial RoPE on the same bf16 inputs."""
+    B, T, D, rot = 2, 600, 80, 32
+    Hq, Hkv = (4, 4) if case == "mha" else (8, 2)
+    C = (Hq + 2 * Hkv) * D
+    qkv = bf(torch.randn(B, T, C)).requires_grad_()
+    rope = RotaryCache(rot, 10000.0, 2048)
+    kv_start = kv_end = positions = None
+    if case == "gqa_leftpad":
+        kv_start = torch.tensor([0, 70], device=DEV, dtype=torch.int32)
+        kv_end = torch.full((B,), T, device=DEV, dtype=torch.int32)
+        positions = (torch.arange(T, device=DEV).unsqueeze(0) - kv_start.unsqueeze(1)).clamp(min=0).int()
+    o = ops.qkv_attention(qkv, Hq, Hkv, D, rope, True, 0, kv_start, kv_end, positions)
+    go = bf(torch.randn_like(o.float()))
+    (o.float() * go.float()).sum().backward()
+    qr = qkv.detach().float().requires_grad_()
+    orf = _qkv_ref(qr, Hq, Hkv, D, rope, kv_start, kv_end, 0, positions)
+    (orf * go.float()).sum().backward()
+    valid = torch.ones(B, T, 1, dtype=torch.bool, device=DEV)
+    if kv_start is not None:
+        valid[1, :70] = False
+    assert rel_err(o * valid, orf * valid) < 2e-2, "forward"
+    g, r = qkv.grad.float() * valid, qr.grad * valid
+    assert rel_err(g[..., :Hq * D], r[..., :Hq * D]) < 3e-2, "dq"
+    assert rel_err(g[..., Hq * D:(Hq + Hkv) * D], r[..., Hq * D:(Hq + Hkv) * D]) < 3e-2, "dk"
+    assert rel_err(g[..., (Hq + Hkv) * D:], r[..., (Hq + Hkv) * D:]) < 3e-2, "dv"
