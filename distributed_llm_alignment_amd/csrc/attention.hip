@@ -1152,8 +1152,7 @@ __global__ __launch_bounds__(512) void attn_bwd8_kernel(AttnBwdParams p) {
     rlse = p.lse2[rb + r];
     rdel = p.delta[rb + r];
   };
-  typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
-  const s16x8 ones = __builtin_bit_cast(s16x8, u32x4v{h ? 0u : 0x3F803F80u, 0u, 0u, 0u});
+  const s16x8 ones = __builtin_bit_cast(s16x8, u32x4{h ? 0u : 0x3F803F80u, 0u, 0u, 0u});
   const float inv_s2 = 1.f / p.scale2;
 
   int hq = hq0, qt = qt0;        // tile it
@@ -1223,8 +1222,8 @@ __global__ __launch_bounds__(512) void attn_bwd8_kernel(AttnBwdParams p) {
         const float y = rv ? -rdel : 0.f;
         const float xh = bf2f(static_cast<bf16_t>(pack2bf(x, 0.f) & 0xffffu));
         const float yh = bf2f(static_cast<bf16_t>(pack2bf(y, 0.f) & 0xffffu));
-        const s16x8 ax = __builtin_bit_cast(s16x8, u32x4v{h ? 0u : pack2bf(x, x - xh), 0u, 0u, 0u});
-        const s16x8 ay = __builtin_bit_cast(s16x8, u32x4v{h ? 0u : pack2bf(y, y - yh), 0u, 0u, 0u});
+        const s16x8 ax = __builtin_bit_cast(s16x8, u32x4{h ? 0u : pack2bf(x, x - xh), 0u, 0u, 0u});
+        const s16x8 ay = __builtin_bit_cast(s16x8, u32x4{h ? 0u : pack2bf(y, y - yh), 0u, 0u, 0u});
         sacc = mfma32(ax, ones, sacc);
         dpacc = mfma32(ay, ones, dpacc);
       }

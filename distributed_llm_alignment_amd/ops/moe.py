@@ -230,11 +230,22 @@ class _ExpertsFn(torch.autograd.Function):
 # rounds: bf16 60.2-60.6 vs 59.6-59.8 pairs/s, fp8 forward 67.3-67.7 vs 66.9-67.0 (~1 %). The copy
 # costs one more copy of the local expert weights (~90 GB per rank for Mixtral-8x7B without EP), so
 # it is budgeted: DLA_MOE_TRANSPOSED_DGRAD=auto (default) makes copies only while the total stays
-# within DLA_MOE_TDGRAD_BUDGET_GB (default 4 GB per process; e.g. small local expert stacks under
-# EP, or debug-depth models), =1 always, =0 never. `free_transposed_experts` drops the copies.
+# within the budget below, =1 always, =0 never. `free_transposed_experts` drops the copies.
 MOE_TRANSPOSED_DGRAD = os.environ.get("DLA_MOE_TRANSPOSED_DGRAD", "auto").lower()
-_TDG_BUDGET = int(float(os.environ.get("DLA_MOE_TDGRAD_BUDGET_GB", "4")) * 2 ** 30)
+# Default budget: 8 % of the device's memory (~23 GB on a 288 GB MI355X): the local expert stacks
+# of Mixtral-8x7B under EP=8 (~11 GB) or a debug-depth model fit, the 90 GB of all experts on one
+# rank do not. DLA_MOE_TDGRAD_BUDGET_GB overrides it.
+_TDG_BUDGET_ENV = os.environ.get("DLA_MOE_TDGRAD_BUDGET_GB")
+_TDG_FRACTION = 0.08
 _TDG_BYTES = [0]  # bytes currently held by transposed copies in this process
+
+
+def _tdgrad_budget(w: torch.Tensor) -> int:
+    if _TDG_BUDGET_ENV is not None:
+        return int(float(_TDG_BUDGET_ENV) * 2 ** 30)
+    if w.device.type != "cuda":
+        return 0
+    return int(_TDG_FRACTION * torch.cuda.get_device_properties(w.device).total_memory)
 
 
 def _tdgrad_allowed(*ws: torch.Tensor) -> bool:
@@ -243,7 +254,7 @@ def _tdgrad_allowed(*ws: torch.Tensor) -> bool:
     if MOE_TRANSPOSED_DGRAD in ("1", "on", "true"):
         return True
     need = sum(w.numel() * w.element_size() for w in ws if getattr(w, "_dla_wT", None) is None)
-    return _TDG_BYTES[0] + need <= _TDG_BUDGET
+    return bool(ws) and _TDG_BYTES[0] + need <= _tdgrad_budget(ws[0])
 
 
 def free_transposed_experts(module) -> int:
