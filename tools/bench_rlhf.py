@@ -3,7 +3,13 @@
 generate B rollouts (prompt T_p, up to N new tokens, hipGraph decode + fused sampler), score
 them with a Llama-3-8B-backbone reward model, compute policy / reference sequence log-probs and
 the KL-penalised policy-gradient loss (fused HIP kernel), backward and fused AdamW. Random init,
-synthetic prompts. Prints one JSON line (rollouts/s and the phase split)."""
+synthetic prompts. Prints one JSON line (rollouts/s and the phase split).
+
+--overlap: one-step-stale rollouts (`ppo.async_rollouts`) overlapped on ONE GPU. A snapshot copy of
+the policy generates and scores step k+1's rollouts on a side stream, from a helper thread, while
+the main thread trains on step k's. Generation is bound by HBM bandwidth (B=8 weight streaming)
+and the update by MFMA, so the two share the chip. The snapshot is refreshed from the policy
+after each update: rollouts come from the weights one update behind."""
 from __future__ import annotations
 
 import argparse
@@ -26,6 +32,8 @@ def main() -> int:
     ap.add_argument("--handoff", choices=("device", "text", "none"), default="device",
                     help="reward inputs: device-built ids (training/handoff.py), the reference's "
                          "decode + re-tokenise text path (byte tokenizer), or the raw sequences")
+    ap.add_argument("--overlap", action="store_true",
+                    help="generate step k+1's rollouts (policy snapshot, side stream) during step k's update")
     ap.add_argument("--grad-ckpt", default="", help="policy activation recompute: full|mlp|attention "
                     "(the reference's rlhf_config batch of 64 rollouts on one GPU needs mlp)")
     a = ap.parse_args()
@@ -86,14 +94,87 @@ def main() -> int:
             phases["score"] += t2 - t1
             phases["train"] += t3 - t2
 
-    for _ in range(a.warmup):
-        step(False)
-    t = sync()
-    for _ in range(a.steps):
-        step(True)
-    dt = sync() - t
+    if a.overlap:
+        import threading
+
+        snap = build_model(cfg, device=dev, dtype=torch.bfloat16, seed=1).requires_grad_(False).eval()
+        snap_params = list(snap.parameters())
+
+        @torch.no_grad()
+        def refresh():  # snapshot <- policy (main stream, after the update)
+            for d, s_ in zip(snap_params, pol.parameters()):
+                d.copy_(s_.detach())
+
+        side = torch.cuda.Stream(device=dev)
+
+        def rollout():
+            ids = torch.randint(3, cfg.vocab_size, (a.batch, a.prompt), device=dev, generator=g)
+            am = torch.ones_like(ids)
+            seqs, mask = generate(snap, ids, am, max_new_tokens=a.new, do_sample=True, temperature=0.7,
+                                  top_p=0.9, eos_token_id=-1, return_mask=True, seed=3)
+            with torch.no_grad():
+                if a.handoff == "none":
+                    scores = rm(seqs, mask)
+                else:
+                    r_ids, r_mask = handoff(prompts, ids, am, seqs, mask)
+                    scores = rm(r_ids, r_mask)
+            return seqs, mask, scores
+
+        def train(ro):
+            seqs, mask, scores = ro
+            pol.train()
+            loss, _ = rlhf_loss(pol, ref, seqs, mask, scores.float(), 0.1)
+            loss.backward()
+            eng.step()
+
+        refresh()
+        pending = rollout()  # also captures the snapshot's decode graph (serially)
+
+        def ostep(record):
+            nonlocal pending
+            out = {}
+            main = torch.cuda.current_stream(dev)
+            side.wait_stream(main)  # the refreshed snapshot
+
+            def job():
+                with torch.cuda.stream(side):
+                    t0 = time.perf_counter()
+                    out["ro"] = rollout()
+                    side.synchronize()
+                    out["t"] = time.perf_counter() - t0
+
+            th = threading.Thread(target=job)
+            t0 = time.perf_counter()
+            th.start()
+            train(pending)
+            main.synchronize()
+            t_train = time.perf_counter() - t0
+            th.join()
+            main.wait_stream(side)
+            for x in out["ro"]:
+                x.record_stream(main)
+            refresh()
+            pending = out["ro"]
+            if record:
+                phases["generate"] += out["t"]
+                phases["train"] += t_train
+
+        for _ in range(a.warmup):
+            ostep(False)
+        t = sync()
+        for _ in range(a.steps):
+            ostep(True)
+        dt = sync() - t
+    else:
+        for _ in range(a.warmup):
+            step(False)
+        t = sync()
+        for _ in range(a.steps):
+            step(True)
+        dt = sync() - t
     print(json.dumps({"bench": "rlhf_step", "model": cfg.name, "rollouts_per_step": a.batch,
                       "grad_ckpt": a.grad_ckpt or "none", "handoff": a.handoff,
+                      "overlap": bool(a.overlap),
                       "prompt": a.prompt, "new_tokens": a.new, "s_per_step": round(dt / a.steps, 3),
                       "rollouts_per_s": round(a.batch * a.steps / dt, 3),
                       **{f"{k}_s": round(v / a.steps, 3) for k, v in phases.items()}}), flush=True)
