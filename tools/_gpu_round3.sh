@@ -1,9 +1,7 @@
 #!/bin/bash
 set -o pipefail
 mkdir -p gpurun_out
-: > gpurun_out/probe_var.log
-for r in 1 2; do for b in attn_bwd_probe attn_bwd_probe_v1 attn_bwd_probe_v2; do
-  echo "== $b" >> gpurun_out/probe_var.log
-  timeout -k 10 60 tools/$b.bin 8 >> gpurun_out/probe_var.log 2>&1 || exit 1
-done; done
-grep -E "==|main kernel|ticks|chains|dV/dK" gpurun_out/probe_var.log
+timeout -k 10 400 python -u tools/bench_rlhf.py --steps 3 --warmup 1 > gpurun_out/r3_rlhf_serial.log 2>&1 || { tail -20 gpurun_out/r3_rlhf_serial.log; exit 1; }
+tail -1 gpurun_out/r3_rlhf_serial.log
+timeout -k 10 400 python -u tools/bench_rlhf.py --steps 3 --warmup 1 --overlap > gpurun_out/r3_rlhf_overlap.log 2>&1 || { tail -20 gpurun_out/r3_rlhf_overlap.log; exit 1; }
+tail -1 gpurun_out/r3_rlhf_overlap.log
