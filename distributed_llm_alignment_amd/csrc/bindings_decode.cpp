@@ -47,6 +47,84 @@ void launch_skinny_ks_fused(const bf16_t*, int64_t, const bf16_t*, int64_t, bf16
 void launch_skinny_glu_normin(const bf16_t*, int64_t, const bf16_t*, int64_t, bf16_t*, int64_t, int,
                               int, int, const KsFuse&, hipStream_t);
 
+int m64_splits(int N, int K);
+bool m64_shape_ok(int N, int K, bool glu);
+void launch_m64_gemm(const bf16_t*, int64_t, const bf16_t*, int64_t, bf16_t*, int64_t, float*, int,
+                     int, int, int, bool, const float*, int, float, hipStream_t);
+void launch_m64_reduce(const float*, int, int, int, bf16_t*, int64_t, const bf16_t*, int64_t,
+                       const float*, int, int, float, float*, hipStream_t);
+
+// Decode projection at 17..64 rows (skinny64.hip), the same fused-layer contract as
+// skinny_fused below with row-norm partials per (row, 1024 columns):
+//   * plain: y = x w^T;
+//   * res given: (s = bf16(bf16(x w^T) + res), ssq [M, ceil(N / 1024)]);
+//   * ssq_in given ([M, nbp], nbp <= 8): y = rstd[m] * (x w^T), w with the norm weight folded in;
+//     with `glu` the gate|up projection + SwiGLU epilogue (w = [gate; up], output [M, F]).
+std::tuple<at::Tensor, at::Tensor> skinny64(const at::Tensor& x, const at::Tensor& w,
+                                            const c10::optional<at::Tensor>& res,
+                                            const c10::optional<at::Tensor>& ssq_in, double eps,
+                                            bool glu) {
+  check_bf16(x, "x");
+  check_bf16(w, "w");
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.stride(1) == 1 && w.stride(1) == 1 &&
+                  x.stride(0) % 8 == 0 && w.stride(0) % 8 == 0,
+              "x [M, K] / w [N, K]: unit inner stride, 16-byte aligned rows");
+  const int64_t M = x.size(0), N = w.size(0), K = w.size(1);
+  TORCH_CHECK(M >= 1 && M <= 64 && x.size(1) == K, "skinny64: 1 <= M <= 64, x [M, K]");
+  TORCH_CHECK(N < (1ll << 30) && K < (1ll << 30), "shape too large");
+  TORCH_CHECK(m64_shape_ok((int)N, (int)K, glu),
+              "skinny64: K % 256 == 0 and N % 128 == 0");
+  check_aligned16(x, "x");
+  check_aligned16(w, "w");
+  same_device(x, w);
+  const float* sq = nullptr;
+  int nbp = 0;
+  if (ssq_in.has_value()) {
+    const at::Tensor& t = *ssq_in;
+    check_cuda(t, "ssq_in");
+    TORCH_CHECK(t.scalar_type() == at::kFloat && t.dim() == 2 && t.size(0) == M && t.is_contiguous() &&
+                    t.size(1) >= 1 && t.size(1) <= 8,
+                "ssq_in fp32 [M, nbp <= 8] contiguous");
+    same_device(x, t);
+    sq = t.data_ptr<float>();
+    nbp = static_cast<int>(t.size(1));
+  }
+  TORCH_CHECK(!(res.has_value() && (sq || glu)), "skinny64: residual output takes a plain input");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  auto st = cur_stream(x);
+  if (glu) {
+    auto m = at::empty({M, N / 2}, x.options());
+    launch_m64_gemm(cbp(x), x.stride(0), cbp(w), w.stride(0), bp(m), m.stride(0), nullptr, (int)M,
+                    (int)N, (int)K, 1, true, sq, nbp, static_cast<float>(eps), st);
+    return {m, at::Tensor()};
+  }
+  const int S = m64_splits((int)N, (int)K);
+  TORCH_CHECK(S > 1 || !(sq || res.has_value()),
+              "skinny64: the residual / normalised-input epilogue needs a split-K shape");
+  auto y = at::empty({M, N}, x.options());
+  at::Tensor ws;
+  if (S > 1) ws = at::empty({S, M, N}, x.options().dtype(at::kFloat));
+  launch_m64_gemm(cbp(x), x.stride(0), cbp(w), w.stride(0), bp(y), y.stride(0),
+                  S > 1 ? ws.data_ptr<float>() : nullptr, (int)M, (int)N, (int)K, S, false, nullptr, 0,
+                  0.f, st);
+  const bf16_t* rp = nullptr;
+  int64_t ldr = 0;
+  at::Tensor ssq;
+  if (res.has_value()) {
+    const at::Tensor& r = *res;
+    check_bf16(r, "res");
+    TORCH_CHECK(r.dim() == 2 && r.size(0) == M && r.size(1) == N && r.stride(1) == 1, "res [M, N]");
+    same_device(x, r);
+    rp = cbp(r);
+    ldr = r.stride(0);
+    ssq = at::empty({M, (N + 1023) / 1024}, x.options().dtype(at::kFloat));
+  }
+  if (S > 1)
+    launch_m64_reduce(ws.data_ptr<float>(), S, (int)M, (int)N, bp(y), y.stride(0), rp, ldr, sq, nbp,
+                      (int)K, static_cast<float>(eps), ssq.defined() ? ssq.data_ptr<float>() : nullptr, st);
+  return {y, ssq};
+}
+
 // Fused decode-layer projection (M <= 16, skinny.hip KsFuse):
 //   * res given: returns (s = bf16(bf16(x w^T) + res) [M, N], ssq [16, N/16] fp32 partial sums of
 //     s^2 per (row, 16-column workgroup)) -- the o / down projection producing the residual;
@@ -398,6 +476,7 @@ TORCH_LIBRARY_FRAGMENT(dla, m) {
   m.def("skinny_glu_norm(Tensor x, Tensor res, Tensor norm_w, float eps, Tensor w) -> (Tensor, Tensor)");
   m.def("skinny_glu_ks(Tensor x, Tensor w) -> Tensor");
   m.def("skinny_fused(Tensor x, Tensor w, Tensor? res, Tensor? ssq_in, float eps, bool glu) -> (Tensor, Tensor)");
+  m.def("skinny64(Tensor x, Tensor w, Tensor? res, Tensor? ssq_in, float eps, bool glu) -> (Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(dla, CUDA, m) {
@@ -409,4 +488,5 @@ TORCH_LIBRARY_IMPL(dla, CUDA, m) {
   m.impl("skinny_glu_norm", &dla::skinny_glu_norm);
   m.impl("skinny_glu_ks", &dla::skinny_glu_ks);
   m.impl("skinny_fused", &dla::skinny_fused);
+  m.impl("skinny64", &dla::skinny64);
 }

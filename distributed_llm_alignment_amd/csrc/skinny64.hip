@@ -1,0 +1,328 @@
+// Decode GEMMs at 17..64 rows: y[M, N] = x[M, K] @ W[N, K]^T, bf16 in/out, fp32 accumulate.
+//
+// Reference: the rollout batch of src/training/train_rlhf.py:115-124 (config/rlhf_config.yaml:
+// 64 prompts per step) runs every projection of every generated token at 64 rows.
+//
+// Why a separate kernel from skinny.hip (M <= 16): there every workgroup holds ALL of x for its
+// K-slice in LDS (16 x 4096 bf16 = 128 KB), or re-reads x fragments per 16 output columns from
+// L2. At 64 rows x is 512 KB: it does not fit, and per-16-column re-reads cost ~1.7 GB of L2
+// traffic per layer (README "Tried": 11.6 vs 6.1 ms/token). hipBLASLt's 64-row tiles run the
+// narrow projections at 2.2-3.0 TB/s (profiles/r3_decode.md, B = 64). Layout here:
+//   * a workgroup owns 128 output columns (8 waves x 16; GLU: 64 gate + the matching 64 up
+//     columns) and a K-slice; x streams through a 2-slot LDS ring in 256-deep chunks shared by
+//     the 8 waves (x traffic from L2 = 1/8 of the per-16-column form);
+//   * each wave streams its 16 weight rows with 16-byte loads straight into registers (two
+//     256-deep ring slots = 16 loads in flight per lane), B fragments of
+//     v_mfma_f32_16x16x32_bf16; every weight fragment feeds MT = M/16 MFMAs (one per 16 rows);
+//   * narrow outputs split K over workgroups (>= 256 workgroups) into fp32 slabs, reduced in a
+//     FIXED order by a second small launch that also applies the decode-layer epilogue
+//     (residual add + row sum of squares, or the RMSNorm row factor) -- no inter-workgroup
+//     hand-off, deterministic, graph-capture safe;
+//   * the gate|up projection (wide, no split) applies RMSNorm's row factor and SwiGLU in its
+//     own epilogue.
+#include "common.h"
+
+#include <cstdlib>
+
+namespace dla {
+
+namespace {
+
+constexpr int kM64Waves = 8;
+constexpr int kM64Ck = 256;             // k per x chunk and per weight ring slot
+constexpr int kM64Steps = kM64Ck / 32;  // MFMA k-steps per chunk
+constexpr int kM64Ld = kM64Ck + 8;      // LDS row stride in bf16 (16-byte pad)
+constexpr int kM64MaxNbp = 8;           // row-norm partials per row (N / 1024 <= 8)
+
+__device__ __forceinline__ f32x4 mfma16(s16x8 a, s16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+template <bool NT>
+__device__ __forceinline__ s16x8 load_w(const bf16_t* p) {
+  if constexpr (NT)
+    return __builtin_bit_cast(s16x8, __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(p)));
+  else
+    return __builtin_bit_cast(s16x8, load_bf16x8(p));
+}
+
+bool m64_nt() {
+  static const bool nt = [] {
+    const char* e = getenv("DLA_SKINNY_NT");
+    return e != nullptr && atoi(e) != 0;
+  }();
+  return nt;
+}
+
+}  // namespace
+
+// grid (N / 128 [GLU: F / 64], S), 512 threads. LDS: 2 x 16 MT x kM64Ld bf16.
+// GLU: W = [gate; up] (2F rows), output m = silu(rstd * g) * (rstd * u) [M, F] where rstd comes
+// from ssq_in (the producer's row partial sums, [M][nbp]) when NIN, else 1; gate / up are
+// rounded to bf16 before SwiGLU exactly as the unfused GEMM + swiglu pair.
+// Otherwise S == 1 writes y = bf16(x W^T); S > 1 writes fp32 slab ws[s][m][n].
+template <int MT, bool GLU, bool NIN, bool NT>
+__global__ __launch_bounds__(512) void m64_gemm_kernel(
+    const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ W, int64_t ldw,
+    bf16_t* __restrict__ y, int64_t ldy, float* __restrict__ ws, int M, int N, int K, int kc,
+    const float* __restrict__ ssq_in, int nbp, float eps) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t xs[];
+  __shared__ float rstd_s[64];
+  constexpr int RB = 16 * MT * kM64Ld;  // one ring slot
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63;
+  const int r = lane & 15, q = lane >> 4;
+  const int F = N >> 1;
+  const int n0 = GLU ? (wave < 4 ? 0 : F) + blockIdx.x * 64 + (wave & 3) * 16
+                     : blockIdx.x * (16 * kM64Waves) + wave * 16;
+  const int s = blockIdx.y;
+  const int k0 = s * kc;
+  const int nch = kc / kM64Ck;
+  const bf16_t* wrow = W + static_cast<int64_t>(n0 + r) * ldw + k0 + q * 8;
+
+  // weight ring: chunks 0 and 1 in flight before anything else
+  s16x8 b0[kM64Steps], b1[kM64Steps];
+#pragma unroll
+  for (int u = 0; u < kM64Steps; ++u) b0[u] = load_w<NT>(wrow + u * 32);
+  if (nch > 1) {
+#pragma unroll
+    for (int u = 0; u < kM64Steps; ++u) b1[u] = load_w<NT>(wrow + kM64Ck + u * 32);
+  }
+  // NIN: this row's producer partials, reduced in the epilogue (thread m < M holds row m)
+  float pv[kM64MaxNbp];
+  if constexpr (NIN) {
+#pragma unroll
+    for (int j = 0; j < kM64MaxNbp; ++j) pv[j] = (tid < M && j < nbp) ? ssq_in[tid * nbp + j] : 0.f;
+  }
+
+  // x chunk staging: thread -> (row 16 j + tid / 32, 8 columns at 8 (tid % 32)); rows >= M are
+  // stored as zeros so the A fragments need no row test
+  const int xm = tid >> 5, xc = (tid & 31) * 8;
+  bf16x8 xr[MT];
+  auto xload = [&](int c) {
+#pragma unroll
+    for (int j = 0; j < MT; ++j) {
+      const int m = xm + 16 * j;
+      xr[j] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (m < M) xr[j] = load_bf16x8(x + static_cast<int64_t>(m) * ldx + k0 + c * kM64Ck + xc);
+    }
+  };
+  auto xstore = [&](int slot) {
+#pragma unroll
+    for (int j = 0; j < MT; ++j) store_bf16x8(xs + slot * RB + (xm + 16 * j) * kM64Ld + xc, xr[j]);
+  };
+  xload(0);
+  xstore(0);
+  __syncthreads();
+
+  f32x4 acc[MT];
+#pragma unroll
+  for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int aoff = r * kM64Ld + q * 8;
+  auto step = [&](s16x8* b, int c) {
+    if (c + 1 < nch) xload(c + 1);
+    const bf16_t* xb = xs + (c & 1) * RB + aoff;
+#pragma unroll
+    for (int u = 0; u < kM64Steps; ++u) {
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        const s16x8 a = __builtin_bit_cast(s16x8, *reinterpret_cast<const bf16x8*>(xb + t * 16 * kM64Ld + u * 32));
+        acc[t] = mfma16(a, b[u], acc[t]);
+      }
+    }
+    if (c + 2 < nch) {
+#pragma unroll
+      for (int u = 0; u < kM64Steps; ++u) b[u] = load_w<NT>(wrow + (c + 2) * kM64Ck + u * 32);
+    }
+    if (c + 1 < nch) xstore((c + 1) & 1);
+    __syncthreads();
+  };
+  for (int c = 0; c < nch; c += 2) {
+    step(b0, c);
+    if (c + 1 < nch) step(b1, c + 1);
+  }
+
+  // lane holds C[m = 16 t + 4 q + i][n = n0 + r]
+  if constexpr (GLU) {
+    if constexpr (NIN) {
+      if (tid < M) {
+        float t = 0.f;
+#pragma unroll
+        for (int j = 0; j < kM64MaxNbp; ++j) t += pv[j];
+        rstd_s[tid] = rsqrtf(t / static_cast<float>(K) + eps);
+      }
+    }
+    // the ring is dead after the loop's last barrier: exchange the gate / up tiles through it
+    float* glu = reinterpret_cast<float*>(xs);  // [2][64][64]
+    const int half = wave >> 2, col = (wave & 3) * 16 + r;
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = 16 * t + 4 * q + i;
+        float v = acc[t][i];
+        if constexpr (NIN) v *= m < M ? rstd_s[m] : 0.f;
+        glu[(half * 64 + m) * 64 + col] = bf2f(f2bf(v));
+      }
+    __syncthreads();
+    // 8 consecutive features of one row per thread, one 16-byte store
+    for (int e = tid; e < M * 8; e += 512) {
+      const int m = e >> 3, c8 = (e & 7) * 8;
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float g = glu[m * 64 + c8 + j], u = glu[(64 + m) * 64 + c8 + j];
+        o[j] = g / (1.f + __expf(-g)) * u;
+      }
+      store_bf16x8(y + static_cast<int64_t>(m) * ldy + blockIdx.x * 64 + c8, pack_bf16x8(o));
+    }
+    return;
+  }
+  const int n = n0 + r;
+  if (gridDim.y == 1) {
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = 16 * t + 4 * q + i;
+        if (m < M) y[static_cast<int64_t>(m) * ldy + n] = f2bf(acc[t][i]);
+      }
+    return;
+  }
+  float* slab = ws + static_cast<int64_t>(s) * M * N;
+#pragma unroll
+  for (int t = 0; t < MT; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = 16 * t + 4 * q + i;
+      if (m < M) slab[static_cast<int64_t>(m) * N + n] = acc[t][i];
+    }
+}
+
+// Split-K reduce + decode-layer epilogue. grid (ceil(N / 1024), M), 256 threads x 4 columns.
+//   MODE 0: y = bf16(sum_s ws[s])
+//   MODE 1 (NIN): y = bf16(rstd[m] * sum), rstd = rsqrt(sum_j ssq_in[m][j] / N_norm + eps)
+//   MODE 2 (RES): y = s = bf16(bf16(sum) + res) and ssq_out[m][blockIdx.x] = sum over the
+//                 block's 1024 columns of s^2 (fixed order) -- the next NIN consumer's partials
+template <int MODE>
+__global__ __launch_bounds__(256) void m64_reduce_kernel(const float* __restrict__ ws, int S, int M,
+                                                         int N, bf16_t* __restrict__ y, int64_t ldy,
+                                                         const bf16_t* __restrict__ res, int64_t ldr,
+                                                         const float* __restrict__ ssq_in, int nbp,
+                                                         int knorm, float eps, float* __restrict__ ssq_out) {
+  __shared__ float red[4];
+  const int m = blockIdx.y;
+  const int n = blockIdx.x * 1024 + threadIdx.x * 4;
+  const float* p = ws + static_cast<int64_t>(m) * N + n;
+  const int64_t slab = static_cast<int64_t>(M) * N;
+  const bool live = n < N;  // N % 128 == 0: a thread's 4 columns are all in or all out
+  f32x4 t = {0.f, 0.f, 0.f, 0.f};
+  if (live)
+    for (int s = 0; s < S; ++s) t += *reinterpret_cast<const f32x4*>(p + s * slab);
+  if constexpr (MODE == 1) {
+    float a = 0.f;
+    for (int j = 0; j < nbp; ++j) a += ssq_in[m * nbp + j];
+    t *= rsqrtf(a / static_cast<float>(knorm) + eps);
+  }
+  bf16x4 o;
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (!live) break;
+    if constexpr (MODE == 2) {
+      const float v = bf2f(f2bf(bf2f(f2bf(t[i])) + bf2f(res[static_cast<int64_t>(m) * ldr + n + i])));
+      o[i] = f2bf(v);
+      ss += v * v;
+    } else {
+      o[i] = f2bf(t[i]);
+    }
+  }
+  if (live) *reinterpret_cast<bf16x4*>(y + static_cast<int64_t>(m) * ldy + n) = o;
+  if constexpr (MODE == 2) {
+    ss = wave_sum(ss);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+    __syncthreads();
+    if (threadIdx.x == 0) ssq_out[m * gridDim.x + blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
+  }
+}
+
+int m64_splits(int N, int K) {
+  static const int target = [] {
+    const char* e = getenv("DLA_M64_WG");
+    return e ? atoi(e) : 256;
+  }();
+  const int nb = N / (16 * kM64Waves);
+  const int chunks = K / kM64Ck;
+  for (int s = 1; s <= chunks; ++s) {
+    if (chunks % s) continue;
+    if (nb * s >= target) return s;
+  }
+  return chunks;
+}
+
+bool m64_shape_ok(int N, int K, bool glu) {
+  return K % kM64Ck == 0 && N % 128 == 0;
+}
+
+size_t m64_lds_bytes(int M) {
+  const int mt = M <= 32 ? 2 : 4;
+  return static_cast<size_t>(2 * 16 * mt * kM64Ld) * sizeof(bf16_t);
+}
+
+template <int MT, bool GLU, bool NIN, bool NT>
+static void m64_launch(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
+                       int64_t ldy, float* ws, int M, int N, int K, int S, const float* ssq_in,
+                       int nbp, float eps, hipStream_t st) {
+  const size_t lds = static_cast<size_t>(2 * 16 * MT * kM64Ld) * sizeof(bf16_t);
+  static bool attr = [&] {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&m64_gemm_kernel<MT, GLU, NIN, NT>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+    (void)hipGetLastError();
+    return true;
+  }();
+  (void)attr;
+  dim3 grid(GLU ? N / 128 : N / (16 * kM64Waves), S);
+  m64_gemm_kernel<MT, GLU, NIN, NT><<<grid, 512, lds, st>>>(x, ldx, W, ldw, y, ldy, ws, M, N, K,
+                                                             K / S, ssq_in, nbp, eps);
+}
+
+template <int MT, bool NT>
+static void m64_dispatch(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
+                         int64_t ldy, float* ws, int M, int N, int K, int S, bool glu,
+                         const float* ssq_in, int nbp, float eps, hipStream_t st) {
+  if (glu && ssq_in)
+    m64_launch<MT, true, true, NT>(x, ldx, W, ldw, y, ldy, ws, M, N, K, 1, ssq_in, nbp, eps, st);
+  else if (glu)
+    m64_launch<MT, true, false, NT>(x, ldx, W, ldw, y, ldy, ws, M, N, K, 1, nullptr, 0, 0.f, st);
+  else
+    m64_launch<MT, false, false, NT>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, nullptr, 0, 0.f, st);
+}
+
+// GEMM (S > 1: fp32 slabs into ws) -- the reduce is a separate launch (launch_m64_reduce)
+void launch_m64_gemm(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
+                     int64_t ldy, float* ws, int M, int N, int K, int S, bool glu,
+                     const float* ssq_in, int nbp, float eps, hipStream_t st) {
+  const bool nt = m64_nt();
+  if (M <= 32) {
+    if (nt) m64_dispatch<2, true>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, glu, ssq_in, nbp, eps, st);
+    else m64_dispatch<2, false>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, glu, ssq_in, nbp, eps, st);
+  } else {
+    if (nt) m64_dispatch<4, true>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, glu, ssq_in, nbp, eps, st);
+    else m64_dispatch<4, false>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, glu, ssq_in, nbp, eps, st);
+  }
+}
+
+void launch_m64_reduce(const float* ws, int S, int M, int N, bf16_t* y, int64_t ldy, const bf16_t* res,
+                       int64_t ldr, const float* ssq_in, int nbp, int knorm, float eps, float* ssq_out,
+                       hipStream_t st) {
+  dim3 grid((N + 1023) / 1024, M);
+  if (res)
+    m64_reduce_kernel<2><<<grid, 256, 0, st>>>(ws, S, M, N, y, ldy, res, ldr, nullptr, 0, 0, 0.f, ssq_out);
+  else if (ssq_in)
+    m64_reduce_kernel<1><<<grid, 256, 0, st>>>(ws, S, M, N, y, ldy, nullptr, 0, ssq_in, nbp, knorm, eps, nullptr);
+  else
+    m64_reduce_kernel<0><<<grid, 256, 0, st>>>(ws, S, M, N, y, ldy, nullptr, 0, nullptr, 0, 0, 0.f, nullptr);
+}
+
+}  // namespace dla

@@ -218,14 +218,33 @@ def ref_skinny_linear(x: torch.Tensor, weight: torch.Tensor, swiglu: bool = Fals
 DECODE_FUSED_NORM = os.environ.get("DLA_DECODE_FUSED_NORM", "1") != "0"
 
 
+# 17..64 decode rows (the reference's 64-rollout RLHF batch): the fused layer runs on the
+# csrc/skinny64.hip kernels -- x streamed through an LDS ring shared by 8 waves x 16 columns,
+# split-K slabs reduced by a second launch that applies the residual / norm epilogue.
+# DLA_DECODE_M64=0 keeps those rows on hipBLASLt + separate norm / SwiGLU launches.
+DECODE_M64 = os.environ.get("DLA_DECODE_M64", "1") != "0"
+
+
+def _m64_layer_ok(H: int, qkv_w, o_w, up_w, down_w) -> bool:
+    F2 = up_w.shape[0]
+    return (H % 256 == 0 and H <= 8192 and qkv_w.shape[0] % 128 == 0 and o_w.shape[0] == H
+            and H % 128 == 0 and o_w.shape[1] % 256 == 0 and F2 % 128 == 0
+            and down_w.shape == (H, F2 // 2) and (F2 // 2) % 256 == 0)
+
+
 def fused_layer_ok(x: torch.Tensor, H: int, qkv_w: torch.Tensor, o_w: torch.Tensor,
                    up_w: torch.Tensor, down_w: torch.Tensor) -> bool:
-    """Shapes / state the fused decode layer supports (M <= 16 bf16 rows, no autograd)."""
+    """Shapes / state the fused decode layer supports (M <= 16 bf16 rows on csrc/skinny.hip,
+    17..64 on csrc/skinny64.hip; no autograd)."""
     if not (DECODE_FUSED_NORM and SKINNY and _ext.use_native(x)) or torch.is_grad_enabled():
         return False
     rows = x.numel() // x.shape[-1]
-    if not (1 <= rows <= 16 and x.dtype == torch.bfloat16 and x.shape[-1] == H):
+    if not (1 <= rows <= 64 and x.dtype == torch.bfloat16 and x.shape[-1] == H):
         return False
+    if rows > 16:
+        return (DECODE_M64 and _m64_layer_ok(H, qkv_w, o_w, up_w, down_w)
+                and all(w.dtype == torch.bfloat16 and w.stride(-1) == 1 and w.stride(0) % 8 == 0
+                        for w in (qkv_w, o_w, up_w, down_w)))
     F2 = up_w.shape[0]
     ok = (H % 1024 == 0 and H < 16384 and H // 16 <= 512 and qkv_w.shape == (qkv_w.shape[0], H)
           and qkv_w.shape[0] < 16384 and qkv_w.shape[0] % 16 == 0 and o_w.shape[0] == H
@@ -276,14 +295,27 @@ def refresh_folded_weights(model) -> None:
                 folded_weight(w, nw)
 
 
+def _fused_op(rows: int):
+    return _ext.require().skinny64 if rows > 16 else _ext.require().skinny_fused
+
+
 def skinny_residual(x: torch.Tensor, w: torch.Tensor, res: torch.Tensor):
     """s = res + x @ w^T (bf16 rounding as linear + add), plus the row-norm partials of s."""
-    s, ssq = _ext.require().skinny_fused(_rows(x), w, _rows(res), None, 0.0, False)
+    x2 = _rows(x)
+    s, ssq = _fused_op(x2.shape[0])(x2, w, _rows(res), None, 0.0, False)
     return s.view(*res.shape[:-1], w.shape[0]), ssq
 
 
 def skinny_normed(s: torch.Tensor, ssq: torch.Tensor, norm_w: torch.Tensor, eps: float,
                   w: torch.Tensor, glu: bool = False) -> torch.Tensor:
     """RMSNorm(s) * norm_w @ w^T from the producer's partials (glu: gate|up + SwiGLU epilogue)."""
-    y, _ = _ext.require().skinny_fused(_rows(s), folded_weight(w, norm_w), None, ssq, float(eps), bool(glu))
+    s2 = _rows(s)
+    y, _ = _fused_op(s2.shape[0])(s2, folded_weight(w, norm_w), None, ssq, float(eps), bool(glu))
     return y.view(*s.shape[:-1], y.shape[-1])
+
+
+def skinny64_linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """y = x @ w^T at 17..64 rows on csrc/skinny64.hip (tests / A/B)."""
+    x2 = _rows(x)
+    y, _ = _ext.require().skinny64(x2, w, None, None, 0.0, False)
+    return y.view(*x.shape[:-1], w.shape[0])

@@ -461,7 +461,7 @@ def _fused_cfg():
                       intermediate_size=2048, num_layers=3, vocab_size=4096)
 
 
-@pytest.mark.parametrize("B", [1, 5, 16])
+@pytest.mark.parametrize("B", [1, 5, 16, 24, 64])
 def test_fused_decode_layer_matches_unfused(B, monkeypatch):
     """Decode step with the residual add + RMSNorm folded into the projections (producer row
     partials, consumer-side normalisation; ops.decode fused layer) against the separate-norm
@@ -522,3 +522,40 @@ def test_fused_decode_projection_kernels_match_fp32():
     gu = h_ref @ wgu.float().t()
     m_ref = torch.nn.functional.silu(gu[:, :F]) * gu[:, F:]
     assert float((mm.float() - m_ref).norm() / m_ref.norm()) < 1e-2
+
+
+@pytest.mark.parametrize("M", [17, 32, 33, 64])
+def test_skinny64_kernels_match_fp32(M):
+    """csrc/skinny64.hip (17..64 decode rows): plain split-K GEMMs at the Llama-3-8B projection
+    shapes and a no-split wide shape, the residual producer (s, row partials of s^2 per 1024
+    columns), and the norm-on-input consumers (qkv via the reduce, gate|up via the GLU
+    epilogue), each against fp32 math on the same bf16 data."""
+    from distributed_llm_alignment_amd import ops
+    from distributed_llm_alignment_amd.ops.norm import _ref_norm
+
+    g = torch.Generator(device=DEV).manual_seed(M)
+    rel = lambda a, b: float((a.float() - b).norm() / b.norm())
+    for N, K in ((6144, 4096), (4096, 14336), (32768, 512), (1152, 1024)):
+        x = torch.randn(M, K, device=DEV, generator=g).to(torch.bfloat16)
+        w = (torch.randn(N, K, device=DEV, generator=g) * K ** -0.5).to(torch.bfloat16)
+        y = ops.decode.skinny64_linear(x, w)
+        assert y.shape == (M, N)
+        assert rel(y, x.float() @ w.float().t()) < 5e-3, (N, K)
+    H, F = 4096, 14336
+    x = torch.randn(M, F, device=DEV, generator=g).to(torch.bfloat16)
+    w = (torch.randn(H, F, device=DEV, generator=g) * F ** -0.5).to(torch.bfloat16)
+    res = torch.randn(M, H, device=DEV, generator=g).to(torch.bfloat16)
+    s, ssq = ops.decode.skinny_residual(x, w, res)
+    assert ssq.shape == (M, H // 1024)
+    s_ref = (x.float() @ w.float().t()).to(torch.bfloat16).float() + res.float()
+    assert float((s.float() - s_ref).abs().max()) < 0.05
+    assert torch.allclose(ssq.sum(1), (s.float() ** 2).sum(1), rtol=1e-4)
+    nw = (1 + 0.1 * torch.randn(H, device=DEV, generator=g)).to(torch.bfloat16)
+    h_ref = _ref_norm(s.float(), nw.float(), None, 1e-5, True)
+    wq = (torch.randn(6144, H, device=DEV, generator=g) * H ** -0.5).to(torch.bfloat16)
+    y = ops.decode.skinny_normed(s, ssq, nw, 1e-5, wq)
+    assert rel(y, h_ref @ wq.float().t()) < 1e-2
+    wgu = (torch.randn(2 * F, H, device=DEV, generator=g) * H ** -0.5).to(torch.bfloat16)
+    mm = ops.decode.skinny_normed(s, ssq, nw, 1e-5, wgu, glu=True)
+    gu = h_ref @ wgu.float().t()
+    assert rel(mm, torch.nn.functional.silu(gu[:, :F]) * gu[:, F:]) < 1e-2
