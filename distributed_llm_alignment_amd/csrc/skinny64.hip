@@ -23,6 +23,7 @@
 #include "common.h"
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace dla {
 
@@ -61,7 +62,7 @@ bool m64_nt() {
 // from ssq_in (the producer's row partial sums, [M][nbp]) when NIN, else 1; gate / up are
 // rounded to bf16 before SwiGLU exactly as the unfused GEMM + swiglu pair.
 // Otherwise S == 1 writes y = bf16(x W^T); S > 1 writes fp32 slab ws[s][m][n].
-template <int MT, bool GLU, bool NIN, bool NT>
+template <int MT, bool GLU, bool NIN, bool NT, int DEPTH>
 __global__ __launch_bounds__(512) void m64_gemm_kernel(
     const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ W, int64_t ldw,
     bf16_t* __restrict__ y, int64_t ldy, float* __restrict__ ws, int M, int N, int K, int kc,
@@ -80,14 +81,6 @@ __global__ __launch_bounds__(512) void m64_gemm_kernel(
   const int nch = kc / kM64Ck;
   const bf16_t* wrow = W + static_cast<int64_t>(n0 + r) * ldw + k0 + q * 8;
 
-  // weight ring: chunks 0 and 1 in flight before anything else
-  s16x8 b0[kM64Steps], b1[kM64Steps];
-#pragma unroll
-  for (int u = 0; u < kM64Steps; ++u) b0[u] = load_w<NT>(wrow + u * 32);
-  if (nch > 1) {
-#pragma unroll
-    for (int u = 0; u < kM64Steps; ++u) b1[u] = load_w<NT>(wrow + kM64Ck + u * 32);
-  }
   // NIN: this row's producer partials, reduced in the epilogue (thread m < M holds row m)
   float pv[kM64MaxNbp];
   if constexpr (NIN) {
@@ -95,51 +88,70 @@ __global__ __launch_bounds__(512) void m64_gemm_kernel(
     for (int j = 0; j < kM64MaxNbp; ++j) pv[j] = (tid < M && j < nbp) ? ssq_in[tid * nbp + j] : 0.f;
   }
 
-  // x chunk staging: thread -> (row 16 j + tid / 32, 8 columns at 8 (tid % 32)); rows >= M are
-  // stored as zeros so the A fragments need no row test
+  // Pipeline: chunk j = x(j) (this thread's 16-byte pieces of 16 MT rows, into register set
+  // j % DEPTH) followed by W(j) (8 loads per lane into ring slot j % DEPTH) -- ALWAYS in that
+  // issue order, because s_waitcnt vmcnt is in-order: storing x(c + 1) into LDS waits only for
+  // loads older than it, so W(c + 1) stays in flight (loading x after W made every step wait a
+  // full HBM round trip for the next weight chunk). DEPTH chunks are in flight; x rows >= M are
+  // zeros so the A fragments need no row test.
   const int xm = tid >> 5, xc = (tid & 31) * 8;
-  bf16x8 xr[MT];
-  auto xload = [&](int c) {
+  bf16x8 xr[DEPTH][MT];
+  s16x8 b[DEPTH][kM64Steps];
+  auto issue = [&](auto J, int c) {
+    constexpr int j = decltype(J)::value;
 #pragma unroll
-    for (int j = 0; j < MT; ++j) {
-      const int m = xm + 16 * j;
-      xr[j] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      if (m < M) xr[j] = load_bf16x8(x + static_cast<int64_t>(m) * ldx + k0 + c * kM64Ck + xc);
+    for (int t = 0; t < MT; ++t) {
+      const int m = xm + 16 * t;
+      xr[j][t] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (m < M) xr[j][t] = load_bf16x8(x + static_cast<int64_t>(m) * ldx + k0 + c * kM64Ck + xc);
     }
-  };
-  auto xstore = [&](int slot) {
 #pragma unroll
-    for (int j = 0; j < MT; ++j) store_bf16x8(xs + slot * RB + (xm + 16 * j) * kM64Ld + xc, xr[j]);
+    for (int u = 0; u < kM64Steps; ++u) b[j][u] = load_w<NT>(wrow + c * kM64Ck + u * 32);
   };
-  xload(0);
-  xstore(0);
+  auto xstore = [&](auto J, int slot) {
+    constexpr int j = decltype(J)::value;
+#pragma unroll
+    for (int t = 0; t < MT; ++t) store_bf16x8(xs + slot * RB + (xm + 16 * t) * kM64Ld + xc, xr[j][t]);
+  };
+  issue(std::integral_constant<int, 0>{}, 0);
+  if (1 < nch) issue(std::integral_constant<int, 1>{}, 1);
+  if constexpr (DEPTH > 2) {
+    if (2 < nch) issue(std::integral_constant<int, 2>{}, 2);
+  }
+  if constexpr (DEPTH > 3) {
+    if (3 < nch) issue(std::integral_constant<int, 3>{}, 3);
+  }
+  xstore(std::integral_constant<int, 0>{}, 0);
   __syncthreads();
 
   f32x4 acc[MT];
 #pragma unroll
   for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int aoff = r * kM64Ld + q * 8;
-  auto step = [&](s16x8* b, int c) {
-    if (c + 1 < nch) xload(c + 1);
+  auto step = [&](auto J, int c) {
+    constexpr int j = decltype(J)::value;
     const bf16_t* xb = xs + (c & 1) * RB + aoff;
 #pragma unroll
     for (int u = 0; u < kM64Steps; ++u) {
 #pragma unroll
       for (int t = 0; t < MT; ++t) {
         const s16x8 a = __builtin_bit_cast(s16x8, *reinterpret_cast<const bf16x8*>(xb + t * 16 * kM64Ld + u * 32));
-        acc[t] = mfma16(a, b[u], acc[t]);
+        acc[t] = mfma16(a, b[j][u], acc[t]);
       }
     }
-    if (c + 2 < nch) {
-#pragma unroll
-      for (int u = 0; u < kM64Steps; ++u) b[u] = load_w<NT>(wrow + (c + 2) * kM64Ck + u * 32);
-    }
-    if (c + 1 < nch) xstore((c + 1) & 1);
+    if (c + 1 < nch) xstore(std::integral_constant<int, (j + 1) % DEPTH>{}, (c + 1) & 1);
     __syncthreads();
+    if (c + DEPTH < nch) issue(J, c + DEPTH);
   };
-  for (int c = 0; c < nch; c += 2) {
-    step(b0, c);
-    if (c + 1 < nch) step(b1, c + 1);
+  for (int c = 0; c < nch; c += DEPTH) {
+    step(std::integral_constant<int, 0>{}, c);
+    if (c + 1 < nch) step(std::integral_constant<int, 1>{}, c + 1);
+    if constexpr (DEPTH > 2) {
+      if (c + 2 < nch) step(std::integral_constant<int, 2>{}, c + 2);
+    }
+    if constexpr (DEPTH > 3) {
+      if (c + 3 < nch) step(std::integral_constant<int, 3>{}, c + 3);
+    }
   }
 
   // lane holds C[m = 16 t + 4 q + i][n = n0 + r]
@@ -196,7 +208,10 @@ __global__ __launch_bounds__(512) void m64_gemm_kernel(
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int m = 16 * t + 4 * q + i;
-      if (m < M) slab[static_cast<int64_t>(m) * N + n] = acc[t][i];
+      if (m < M) {
+        if constexpr (NT) __builtin_nontemporal_store(acc[t][i], slab + static_cast<int64_t>(m) * N + n);
+        else slab[static_cast<int64_t>(m) * N + n] = acc[t][i];
+      }
     }
 }
 
@@ -205,8 +220,8 @@ __global__ __launch_bounds__(512) void m64_gemm_kernel(
 //   MODE 1 (NIN): y = bf16(rstd[m] * sum), rstd = rsqrt(sum_j ssq_in[m][j] / N_norm + eps)
 //   MODE 2 (RES): y = s = bf16(bf16(sum) + res) and ssq_out[m][blockIdx.x] = sum over the
 //                 block's 1024 columns of s^2 (fixed order) -- the next NIN consumer's partials
-template <int MODE>
-__global__ __launch_bounds__(256) void m64_reduce_kernel(const float* __restrict__ ws, int S, int M,
+template <int MODE, int S>
+__global__ __launch_bounds__(256) void m64_reduce_kernel(const float* __restrict__ ws, int M,
                                                          int N, bf16_t* __restrict__ y, int64_t ldy,
                                                          const bf16_t* __restrict__ res, int64_t ldr,
                                                          const float* __restrict__ ssq_in, int nbp,
@@ -217,9 +232,17 @@ __global__ __launch_bounds__(256) void m64_reduce_kernel(const float* __restrict
   const float* p = ws + static_cast<int64_t>(m) * N + n;
   const int64_t slab = static_cast<int64_t>(M) * N;
   const bool live = n < N;  // N % 128 == 0: a thread's 4 columns are all in or all out
+  // all S slab loads in flight at once (compile-time count), summed in split order
+  f32x4 v[S];
+  if (live) {
+#pragma unroll
+    for (int s = 0; s < S; ++s) v[s] = *reinterpret_cast<const f32x4*>(p + s * slab);
+  }
   f32x4 t = {0.f, 0.f, 0.f, 0.f};
-  if (live)
-    for (int s = 0; s < S; ++s) t += *reinterpret_cast<const f32x4*>(p + s * slab);
+  if (live) {
+#pragma unroll
+    for (int s = 0; s < S; ++s) t += v[s];
+  }
   if constexpr (MODE == 1) {
     float a = 0.f;
     for (int j = 0; j < nbp; ++j) a += ssq_in[m * nbp + j];
@@ -254,11 +277,13 @@ int m64_splits(int N, int K) {
   }();
   const int nb = N / (16 * kM64Waves);
   const int chunks = K / kM64Ck;
-  for (int s = 1; s <= chunks; ++s) {
+  // split counts the reduce kernel is instantiated for
+  for (int s : {1, 2, 4, 7, 8, 14, 16}) {
     if (chunks % s) continue;
     if (nb * s >= target) return s;
   }
-  return chunks;
+  for (int s : {16, 14, 8, 7, 4, 2}) if (chunks % s == 0) return s;
+  return 1;
 }
 
 bool m64_shape_ok(int N, int K, bool glu) {
@@ -270,21 +295,41 @@ size_t m64_lds_bytes(int M) {
   return static_cast<size_t>(2 * 16 * mt * kM64Ld) * sizeof(bf16_t);
 }
 
-template <int MT, bool GLU, bool NIN, bool NT>
-static void m64_launch(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
-                       int64_t ldy, float* ws, int M, int N, int K, int S, const float* ssq_in,
-                       int nbp, float eps, hipStream_t st) {
+static int m64_depth() {
+  static const int d = [] {
+    const char* e = getenv("DLA_M64_DEPTH");
+    const int v = e ? atoi(e) : 2;
+    return v < 2 ? 2 : (v > 4 ? 4 : v);
+  }();
+  return d;
+}
+
+template <int MT, bool GLU, bool NIN, bool NT, int DEPTH>
+static void m64_launch_d(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
+                         int64_t ldy, float* ws, int M, int N, int K, int S, const float* ssq_in,
+                         int nbp, float eps, hipStream_t st) {
   const size_t lds = static_cast<size_t>(2 * 16 * MT * kM64Ld) * sizeof(bf16_t);
-  static bool attr = [&] {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&m64_gemm_kernel<MT, GLU, NIN, NT>),
+  static bool attr = [] {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&m64_gemm_kernel<MT, GLU, NIN, NT, DEPTH>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
     (void)hipGetLastError();
     return true;
   }();
   (void)attr;
   dim3 grid(GLU ? N / 128 : N / (16 * kM64Waves), S);
-  m64_gemm_kernel<MT, GLU, NIN, NT><<<grid, 512, lds, st>>>(x, ldx, W, ldw, y, ldy, ws, M, N, K,
-                                                             K / S, ssq_in, nbp, eps);
+  m64_gemm_kernel<MT, GLU, NIN, NT, DEPTH><<<grid, 512, lds, st>>>(x, ldx, W, ldw, y, ldy, ws, M, N,
+                                                                    K, K / S, ssq_in, nbp, eps);
+}
+
+template <int MT, bool GLU, bool NIN, bool NT>
+static void m64_launch(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
+                       int64_t ldy, float* ws, int M, int N, int K, int S, const float* ssq_in,
+                       int nbp, float eps, hipStream_t st) {
+  switch (m64_depth()) {
+    case 2: m64_launch_d<MT, GLU, NIN, NT, 2>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, ssq_in, nbp, eps, st); break;
+    case 4: m64_launch_d<MT, GLU, NIN, NT, 4>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, ssq_in, nbp, eps, st); break;
+    default: m64_launch_d<MT, GLU, NIN, NT, 3>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, ssq_in, nbp, eps, st); break;
+  }
 }
 
 template <int MT, bool NT>
@@ -313,16 +358,34 @@ void launch_m64_gemm(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw,
   }
 }
 
+template <int MODE>
+static void m64_reduce_s(const float* ws, int S, int M, int N, bf16_t* y, int64_t ldy, const bf16_t* res,
+                         int64_t ldr, const float* ssq_in, int nbp, int knorm, float eps, float* ssq_out,
+                         hipStream_t st) {
+  dim3 grid((N + 1023) / 1024, M);
+#define DLA_M64R(SS) \
+  m64_reduce_kernel<MODE, SS><<<grid, 256, 0, st>>>(ws, M, N, y, ldy, res, ldr, ssq_in, nbp, knorm, eps, ssq_out)
+  switch (S) {
+    case 2: DLA_M64R(2); break;
+    case 4: DLA_M64R(4); break;
+    case 7: DLA_M64R(7); break;
+    case 8: DLA_M64R(8); break;
+    case 14: DLA_M64R(14); break;
+    case 16: DLA_M64R(16); break;
+    default: DLA_M64R(1); break;  // S == 1 never reaches the reduce (checked by the caller)
+  }
+#undef DLA_M64R
+}
+
 void launch_m64_reduce(const float* ws, int S, int M, int N, bf16_t* y, int64_t ldy, const bf16_t* res,
                        int64_t ldr, const float* ssq_in, int nbp, int knorm, float eps, float* ssq_out,
                        hipStream_t st) {
-  dim3 grid((N + 1023) / 1024, M);
   if (res)
-    m64_reduce_kernel<2><<<grid, 256, 0, st>>>(ws, S, M, N, y, ldy, res, ldr, nullptr, 0, 0, 0.f, ssq_out);
+    m64_reduce_s<2>(ws, S, M, N, y, ldy, res, ldr, nullptr, 0, 0, 0.f, ssq_out, st);
   else if (ssq_in)
-    m64_reduce_kernel<1><<<grid, 256, 0, st>>>(ws, S, M, N, y, ldy, nullptr, 0, ssq_in, nbp, knorm, eps, nullptr);
+    m64_reduce_s<1>(ws, S, M, N, y, ldy, nullptr, 0, ssq_in, nbp, knorm, eps, nullptr, st);
   else
-    m64_reduce_kernel<0><<<grid, 256, 0, st>>>(ws, S, M, N, y, ldy, nullptr, 0, nullptr, 0, 0, 0.f, nullptr);
+    m64_reduce_s<0>(ws, S, M, N, y, ldy, nullptr, 0, nullptr, 0, 0, 0.f, nullptr, st);
 }
 
 }  // namespace dla

@@ -222,7 +222,7 @@ DECODE_FUSED_NORM = os.environ.get("DLA_DECODE_FUSED_NORM", "1") != "0"
 # csrc/skinny64.hip kernels -- x streamed through an LDS ring shared by 8 waves x 16 columns,
 # split-K slabs reduced by a second launch that applies the residual / norm epilogue.
 # DLA_DECODE_M64=0 keeps those rows on hipBLASLt + separate norm / SwiGLU launches.
-DECODE_M64 = os.environ.get("DLA_DECODE_M64", "1") != "0"
+DECODE_M64 = os.environ.get("DLA_DECODE_M64", "1") != "0"  # A/B: profiles/r3_decode_b64.md
 
 
 def _m64_layer_ok(H: int, qkv_w, o_w, up_w, down_w) -> bool:
