@@ -19,7 +19,7 @@ void launch_decode_attn_rope(const bf16_t*, int64_t, const float*, const float*,
                              const int64_t*, int, bf16_t*, bf16_t*, int64_t, int64_t, int64_t,
                              const int*, const int*, int, float, int, int, int, int, int, float*,
                              float*, bf16_t*, int64_t, int64_t, hipStream_t);
-int decode_num_splits(int Tmax);
+int decode_num_splits(int Tmax, int B, int Hkv);
 void launch_rope_cache(const bf16_t*, int64_t, bf16_t*, bf16_t*, bf16_t*, int64_t, int64_t,
                        int64_t, const int64_t*, const float*, const float*, const int*, int, int,
                        int, int, int, hipStream_t);
@@ -325,7 +325,7 @@ at::Tensor decode_attn(const at::Tensor& q, const at::Tensor& k_cache, const at:
     ks = kv_start->data_ptr<int>();
   }
   c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
-  const int nsplit = decode_num_splits(static_cast<int>(Tmax));
+  const int nsplit = decode_num_splits(static_cast<int>(Tmax), static_cast<int>(B), static_cast<int>(Hkv));
   auto fopt = q.options().dtype(at::kFloat);
   auto part_o = at::empty({B, Hq, nsplit, D}, fopt);
   auto part_ml = at::empty({B, Hq, nsplit, 2}, fopt);
@@ -420,7 +420,7 @@ at::Tensor decode_attn_rope(const at::Tensor& qkv, const at::Tensor& cos, const 
   }
   c10::hip::HIPGuardMasqueradingAsCUDA g(qkv.device());
   const int64_t Tmax = k_cache.size(1);
-  const int nsplit = decode_num_splits(static_cast<int>(Tmax));
+  const int nsplit = decode_num_splits(static_cast<int>(Tmax), static_cast<int>(B), static_cast<int>(Hkv));
   auto fopt = qkv.options().dtype(at::kFloat);
   auto part_o = at::empty({B, Hq, nsplit, D}, fopt);
   auto part_ml = at::empty({B, Hq, nsplit, 2}, fopt);

@@ -323,6 +323,257 @@ __global__ __launch_bounds__(256, 3) void decode_attn_kernel(
   }
 }
 
+// Multi-chunk form (the default): grid (nsplit, Hkv, B) with each block looping over `cpb`
+// consecutive 128-key chunks of its (b, kv head), chunk c + 2's K / V loads in flight while chunk
+// c is computed (a 2-slot register ring), and a per-wave online softmax across the chunks. The
+// host picks cpb so the grid fits in ~one round of resident blocks: at B = 64 (the reference's
+// RLHF rollout batch) the one-chunk-per-block grid ran 2560 blocks in ~3.3 rounds, each block
+// paying its own dependent round trips (scalars -> K/V -> merge); here 512 blocks stream ~4.5
+// chunks each and the per-block prologue / merge is paid once. Numerics: the same masked
+// exp2-domain softmax and P.V MFMA as decode_attn_kernel<PVM>, with the running max rescale
+// applied between chunks; partials (m, l, o) per split as before.
+__device__ __forceinline__ void dec_glds16(const void* src, void* lds_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
+}
+
+template <int D, int G, bool ROPE>
+__global__ __launch_bounds__(256, 2) void decode_attn_loop_kernel(
+    const bf16_t* __restrict__ q, int64_t q_sb, int64_t q_sh,
+    bf16_t* __restrict__ kc, bf16_t* __restrict__ vc,
+    int64_t c_sb, int64_t c_st, int64_t c_sh, const int* __restrict__ kv_len,
+    const int* __restrict__ kv_start, int window, float scale_log2, int nsplit, int cpb,
+    float* __restrict__ part_o, float* __restrict__ part_ml, int Hq, DecRope rp,
+    bf16_t* __restrict__ out, int64_t o_sb, int64_t o_sh) {
+  // out != nullptr (one split per sequence): the block writes the normalised bf16 output itself
+  // and the combine launch is skipped
+  constexpr int LPK = D / 8, KPI = 64 / LPK, KPW = kDecChunk / 4, NIT = KPW / KPI;
+  constexpr int KST = D / 32;
+  static_assert(G <= 16 && KPW == 32, "decode tile geometry");
+  static_assert(G * D * 4 <= KPW * D * 2, "acc_s aliases one V image slot");
+  // per wave: 2 V image slots (LDS-DMA ring), the first re-used for the wave's partial O
+  __shared__ __attribute__((aligned(16))) bf16_t vimg[4][2][KPW * D];
+  __shared__ float mls[4][G][2];
+  const int split = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int len = kv_len[0];
+  int lo = kv_start ? kv_start[b] : 0;
+  const int sub = lane / LPK, dl = (lane % LPK) * 8;
+  const int r16 = lane & 15, kg = lane >> 4;
+  int newest = -1;
+  const bf16_t* qrow = nullptr;
+  const float *cs = nullptr, *sn = nullptr;
+  const int cfirst = split * cpb;
+  if constexpr (ROPE) {
+    newest = static_cast<int>(rp.slot[0]);
+    qrow = rp.qkv + (int64_t)b * rp.ld;
+    const int half = rp.rot >> 1;
+    cs = rp.cos_t + (int64_t)rp.pos[b] * half;
+    sn = rp.sin_t + (int64_t)rp.pos[b] * half;
+    const int cn = newest / kDecChunk;
+    if (cn >= cfirst && cn < cfirst + cpb && wv == 0 && lane < LPK) {  // cache write for later steps
+      const bf16x8 vnew = load_bf16x8(qrow + (int64_t)(Hq + rp.Hkv + hk) * D + dl);
+      const bf16x8 knew = dec_rope8(qrow + (int64_t)(Hq + hk) * D, dl, rp.rot, cs, sn);
+      store_bf16x8(kc + (int64_t)b * c_sb + (int64_t)newest * c_st + (int64_t)hk * c_sh + dl, knew);
+      store_bf16x8(vc + (int64_t)b * c_sb + (int64_t)newest * c_st + (int64_t)hk * c_sh + dl, vnew);
+    }
+  }
+  if (window > 0) lo = max(lo, len - window);
+  // chunks [cbeg, cend) of this split that hold visible keys
+  const int cbeg = max(cfirst, lo / kDecChunk);
+  const int cend = min(cfirst + cpb, (len + kDecChunk - 1) / kDecChunk);
+  const int64_t pbase = ((int64_t)b * Hq + (int64_t)hk * G) * nsplit + split;
+  if (cbeg >= cend || max(cbeg * kDecChunk, lo) >= len) {
+    if (out != nullptr) {  // no visible key: zeros, as the combine writes for an all-empty row
+      for (int i = tid; i < G * D; i += 256)
+        out[(int64_t)b * o_sb + (int64_t)(hk * G + i / D) * o_sh + i % D] = 0;
+    } else if (tid < G) {
+      part_ml[(pbase + (int64_t)tid * nsplit) * 2 + 0] = -INFINITY;
+      part_ml[(pbase + (int64_t)tid * nsplit) * 2 + 1] = 0.f;
+    }
+    return;
+  }
+  // q fragments first (the oldest loads: S of chunk 0 waits for them and K(0) only)
+  s16x8 qf[KST];
+#pragma unroll
+  for (int s = 0; s < KST; ++s) {
+    qf[s] = s16x8{};
+    if (r16 < G) {
+      if constexpr (ROPE)
+        qf[s] = __builtin_bit_cast(s16x8, dec_rope8(qrow + (int64_t)(hk * G + r16) * D, 32 * s + 8 * kg, rp.rot, cs, sn));
+      else
+        qf[s] = __builtin_bit_cast(s16x8, load_bf16x8(q + (int64_t)b * q_sb + (int64_t)(hk * G + r16) * q_sh + 32 * s + 8 * kg));
+    }
+  }
+  const bf16_t* kb0 = kc + (int64_t)b * c_sb + (int64_t)hk * c_sh;
+  const bf16_t* vb0 = vc + (int64_t)b * c_sb + (int64_t)hk * c_sh;
+  // 2-slot ring: K as MFMA A fragments in registers, V by LDS-DMA straight into the wave's
+  // swizzled image (lane-linear destination, the swizzle applied on the per-lane SOURCE chunk:
+  // image row it * KPI + sub, position dl / 8 holds logical chunk (dl / 8) ^ f(row)); keys
+  // clamped into the chunk's visible range. Issue order per chunk: K then V.
+  s16x8 kf[2][2][KST];
+  auto load = [&](auto J, int c) {
+    constexpr int j = decltype(J)::value;
+    const int base = c * kDecChunk, k0 = max(base, lo), k1 = min(base + kDecChunk, len);
+    const int kw0 = base + wv * KPW;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int kcl = min(max(kw0 + 16 * t + r16, k0), k1 - 1);
+#pragma unroll
+      for (int s = 0; s < KST; ++s)
+        kf[j][t][s] = __builtin_bit_cast(s16x8, load_bf16x8(kb0 + (int64_t)kcl * c_st + 32 * s + 8 * kg));
+    }
+    bf16_t* img = &vimg[wv][j][0];
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int row = it * KPI + sub;
+      const int key = min(max(kw0 + row, k0), k1 - 1);
+      const int ch = (dec_swz<D>(row, dl >> 3) - row * D) >> 3;  // position dl/8 <-> chunk ch
+      dec_glds16(vb0 + (int64_t)key * c_st + ch * 8, img + it * 512);
+    }
+  };
+  float m_run = -INFINITY, l_run = 0.f;
+  f32x4 oacc[D / 16];
+#pragma unroll
+  for (int dt = 0; dt < D / 16; ++dt) oacc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto step = [&](auto J, int c) {
+    constexpr int j = decltype(J)::value;
+    const int base = c * kDecChunk, k0 = max(base, lo), k1 = min(base + kDecChunk, len);
+    const int kw0 = base + wv * KPW;
+    const bool newest_here = ROPE && newest >= kw0 && newest < kw0 + KPW;
+    if constexpr (ROPE) {  // the newest key's K comes from registers (its cache row is being written)
+      if (newest_here) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          if (min(max(kw0 + 16 * t + r16, k0), k1 - 1) == newest) {
+#pragma unroll
+            for (int s = 0; s < KST; ++s)
+              kf[j][t][s] = __builtin_bit_cast(s16x8, dec_rope8(qrow + (int64_t)(Hq + hk) * D, 32 * s + 8 * kg, rp.rot, cs, sn));
+          }
+        }
+      }
+    }
+    f32x4 sacc[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      sacc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < KST; ++s) sacc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[j][t][s], qf[s], sacc[t], 0, 0, 0);
+    }
+    float sc[2][4];
+    float mc = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int key = kw0 + 16 * t + 4 * kg + i;
+        sc[t][i] = (key >= k0 && key < k1) ? sacc[t][i] * scale_log2 : -INFINITY;
+        mc = fmaxf(mc, sc[t][i]);
+      }
+    mc = fmaxf(mc, __shfl_xor(mc, 16, 64));
+    mc = fmaxf(mc, __shfl_xor(mc, 32, 64));
+    const float mnew = fmaxf(m_run, mc);
+    const float alpha = m_run == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m_run - mnew);
+    const float muse = mnew == -INFINITY ? 0.f : mnew;
+    float pf[2][4], ls = 0.f;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float p = __builtin_amdgcn_exp2f(sc[t][i] - muse);
+        ls += p;
+        pf[t][i] = r16 < G ? p : 0.f;
+      }
+    ls += __shfl_xor(ls, 16, 64);
+    ls += __shfl_xor(ls, 32, 64);
+    l_run = l_run * alpha + ls;
+    m_run = mnew;
+    const float pv8[8] = {pf[0][0], pf[0][1], pf[0][2], pf[0][3], pf[1][0], pf[1][1], pf[1][2], pf[1][3]};
+    const s16x8 pa = __builtin_bit_cast(s16x8, pack_bf16x8(pv8));
+    float ai[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ai[i] = __shfl(alpha, 4 * kg + i, 64);
+    // V(c) has landed once every VMEM op but the next chunk's (2 KST K loads + NIT V pieces,
+    // issued after it) is done; the compiler does not see the DMA -> LDS dependence
+    if (c + 1 < cend) {
+      if constexpr (2 * KST + NIT == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      else if constexpr (2 * KST + NIT == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    bf16_t* vw = &vimg[wv][j][0];
+    if constexpr (ROPE) {  // the newest key's V row from the qkv row (not the cache) into the image
+      if (newest_here) {
+        const int rown = newest - kw0;
+        if (sub == (rown % KPI))
+          store_bf16x8(vw + dec_swz<D>(rown, dl >> 3), load_bf16x8(qrow + (int64_t)(Hq + rp.Hkv + hk) * D + dl));
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int dt = 0; dt < D / 16; ++dt) {
+      const s16x4 v0 = dec_tr_read<D>(vw, 4 * kg, 16 * dt, lane);
+      const s16x4 v1 = dec_tr_read<D>(vw, 16 + 4 * kg, 16 * dt, lane);
+      const s16x8 vb = s16x8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+      f32x4 o = oacc[dt];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[i] *= ai[i];
+      oacc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vb, o, 0, 0, 0);
+    }
+    if (c + 2 < cend) {
+      // WAR: this slot's transposed reads are complete before the DMA refill is issued
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      load(J, c + 2);
+    }
+  };
+  load(std::integral_constant<int, 0>{}, cbeg);
+  if (cbeg + 1 < cend) load(std::integral_constant<int, 1>{}, cbeg + 1);
+  for (int c = cbeg; c < cend; c += 2) {
+    step(std::integral_constant<int, 0>{}, c);
+    if (c + 1 < cend) step(std::integral_constant<int, 1>{}, c + 1);
+  }
+  // this wave's partial O into its own (dead) first image slot
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  float* acc_w = reinterpret_cast<float*>(&vimg[wv][0][0]);
+#pragma unroll
+  for (int dt = 0; dt < D / 16; ++dt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (4 * kg + i < G) acc_w[(4 * kg + i) * D + 16 * dt + r16] = oacc[dt][i];
+  if (kg == 0 && r16 < G) {
+    mls[wv][r16][0] = m_run;
+    mls[wv][r16][1] = l_run;
+  }
+  __syncthreads();
+  for (int i = tid; i < G * D; i += 256) {
+    const int g = i / D, d = i % D;
+    float mm = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) mm = fmaxf(mm, mls[w][g][0]);
+    float v = 0.f, ll = 0.f;
+    if (mm != -INFINITY) {
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const float mw = mls[w][g][0];
+        const float cc = mw == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(mw - mm);
+        v += cc * reinterpret_cast<const float*>(&vimg[w][0][0])[g * D + d];
+        ll += cc * mls[w][g][1];
+      }
+    }
+    if (out != nullptr) {
+      out[(int64_t)b * o_sb + (int64_t)(hk * G + g) * o_sh + d] = f2bf(ll > 0.f ? v * (1.f / ll) : 0.f);
+      continue;
+    }
+    part_o[(pbase + (int64_t)g * nsplit) * D + d] = v;
+    if (d == 0) {
+      part_ml[(pbase + (int64_t)g * nsplit) * 2 + 0] = mm;
+      part_ml[(pbase + (int64_t)g * nsplit) * 2 + 1] = ll;
+    }
+  }
+}
+
 // Decode-step prologue: rotate q (-> q_out [B, Hq, D]) and k of the newest token and write k and
 // v straight into the cache slot `*slot` (device value), replacing rope + two index_copy
 // launches. qkv [B, (Hq + 2 Hkv) * D] rows; same rotate-half math as rope.hip.
@@ -445,6 +696,9 @@ static bool decode_pv_mfma() {
   return v;
 }
 
+static int decode_cpb(int Tmax, int B, int Hkv);
+int decode_num_splits(int Tmax, int B, int Hkv);
+
 template <int D>
 static void launch_decode_d(const bf16_t* q, int64_t q_sb, int64_t q_sh, bf16_t* kc,
                             bf16_t* vc, int64_t c_sb, int64_t c_st, int64_t c_sh,
@@ -453,9 +707,35 @@ static void launch_decode_d(const bf16_t* q, int64_t q_sb, int64_t q_sh, bf16_t*
                             bf16_t* out, int64_t o_sb, int64_t o_sh, const DecRope* rp,
                             hipStream_t st) {
   const int G = Hq / Hkv;
-  const int nsplit = (Tmax + kDecChunk - 1) / kDecChunk;
+  const int cpb = decode_cpb(Tmax, B, Hkv);
+  const int nsplit = decode_num_splits(Tmax, B, Hkv);
   dim3 grid(nsplit, Hkv, B);
   const DecRope r0 = rp ? *rp : DecRope{};
+  if (cpb > 0) {
+    bf16_t* fin = nsplit == 1 ? out : nullptr;  // one split per sequence: no combine launch
+#define DLA_DECL(GG)                                                                                    \
+  if (rp)                                                                                               \
+    decode_attn_loop_kernel<D, GG, true><<<grid, 256, 0, st>>>(q, q_sb, q_sh, kc, vc, c_sb, c_st, c_sh, \
+                                                               kv_len, kv_start, window, scale_log2,    \
+                                                               nsplit, cpb, part_o, part_ml, Hq, r0,    \
+                                                               fin, o_sb, o_sh);                        \
+  else                                                                                                  \
+    decode_attn_loop_kernel<D, GG, false><<<grid, 256, 0, st>>>(q, q_sb, q_sh, kc, vc, c_sb, c_st, c_sh, \
+                                                                kv_len, kv_start, window, scale_log2,   \
+                                                                nsplit, cpb, part_o, part_ml, Hq, r0,   \
+                                                                fin, o_sb, o_sh)
+    switch (G) {
+      case 1: DLA_DECL(1); break;
+      case 2: DLA_DECL(2); break;
+      case 4: DLA_DECL(4); break;
+      case 8: DLA_DECL(8); break;
+      default: break;
+    }
+#undef DLA_DECL
+    if (fin == nullptr)
+      decode_combine_kernel<D><<<B * Hq, 64, 0, st>>>(part_o, part_ml, nsplit, out, o_sb, o_sh, Hq);
+    return;
+  }
 #define DLA_DEC2(GG, PV)                                                                         \
   if (rp)                                                                                        \
     decode_attn_kernel<D, GG, true, PV><<<grid, 256, 0, st>>>(q, q_sb, q_sh, kc, vc, c_sb, c_st, \
@@ -485,7 +765,28 @@ static void launch_decode_d(const bf16_t* q, int64_t q_sb, int64_t q_sh, bf16_t*
   decode_combine_kernel<D><<<B * Hq, 64, 0, st>>>(part_o, part_ml, nsplit, out, o_sb, o_sh, Hq);
 }
 
-int decode_num_splits(int Tmax) { return (Tmax + kDecChunk - 1) / kDecChunk; }
+// DLA_DECODE_LOOP=0: one 128-key chunk per block (decode_attn_kernel); otherwise blocks loop over
+// chunks so that B x Hkv x splits stays near DLA_DECODE_BLOCKS (default 512 = two resident
+// 256-thread blocks per CU at the loop kernel's register budget)
+static int decode_cpb(int Tmax, int B, int Hkv) {
+  // read per call (cheap next to a launch) so a test can force the loop kernel at small shapes
+  const char* e = getenv("DLA_DECODE_LOOP");
+  const char* tb = getenv("DLA_DECODE_BLOCKS");
+  const int target = (e != nullptr && atoi(e) == 0) ? 0 : (tb ? atoi(tb) : 512);
+  const int nch = (Tmax + kDecChunk - 1) / kDecChunk;
+  if (target <= 0) return 0;
+  const int64_t blocks = static_cast<int64_t>(B) * Hkv * nch;
+  const int cpb = static_cast<int>((blocks + target - 1) / target);
+  // at <= 2 chunks per block the one-chunk kernel (3 blocks per CU) measured faster
+  // (B = 8, 1152 keys: 4.05 vs 4.12 ms/token)
+  return cpb <= 2 ? 0 : std::min(cpb, nch);
+}
+
+int decode_num_splits(int Tmax, int B, int Hkv) {
+  const int nch = (Tmax + kDecChunk - 1) / kDecChunk;
+  const int cpb = decode_cpb(Tmax, B, Hkv);
+  return cpb == 0 ? nch : (nch + cpb - 1) / cpb;
+}
 
 void launch_decode_attn(const bf16_t* q, int64_t q_sb, int64_t q_sh, bf16_t* kc,
                         bf16_t* vc, int64_t c_sb, int64_t c_st, int64_t c_sh,

@@ -16,9 +16,15 @@ def _native():
     _ext.require()
 
 
+@pytest.mark.parametrize("blocks", [None, "16", "60"])
 @pytest.mark.parametrize("D,Hq,Hkv,window", [(128, 32, 8, 0), (64, 8, 8, 0), (128, 16, 2, 300), (64, 16, 8, 0)])
-def test_decode_attention_matches_reference(D, Hq, Hkv, window):
+def test_decode_attention_matches_reference(D, Hq, Hkv, window, blocks, monkeypatch):
+    """blocks: DLA_DECODE_BLOCKS target -- None keeps the default (one 128-key chunk per block
+    at this size), 16 / 60 force the multi-chunk loop kernel with 1 / 2 splits per sequence."""
     from distributed_llm_alignment_amd.ops import decode
+
+    if blocks is not None:
+        monkeypatch.setenv("DLA_DECODE_BLOCKS", blocks)
 
     g = torch.Generator(device=DEV).manual_seed(0)
     B, Tmax, L = 5, 1100, 777
@@ -139,8 +145,12 @@ def test_split_sampler_support_random_logits(top_k, top_p):
     assert len(seen) > 16  # it samples, not argmax
 
 
-def test_graph_generation_matches_eager_greedy():
+@pytest.mark.parametrize("blocks", [None, "2"])
+def test_graph_generation_matches_eager_greedy(blocks, monkeypatch):
     from distributed_llm_alignment_amd.models import build_model, generate, get_config
+
+    if blocks is not None:  # the multi-chunk decode attention kernel inside the captured graph
+        monkeypatch.setenv("DLA_DECODE_BLOCKS", blocks)
 
     cfg = get_config("tiny-llama-d128")
     m = build_model(cfg, device=DEV, dtype=torch.bfloat16, seed=0)
@@ -335,10 +345,15 @@ def test_skinny_glu_epilogue_matches_unfused(M, F, K, mode):
 
 
 @pytest.mark.parametrize("D,Hq,Hkv,rot", [(128, 32, 8, 128), (64, 8, 8, 32), (128, 8, 1, 64)])
-def test_fused_rope_decode_attention_matches_unfused(D, Hq, Hkv, rot):
+@pytest.mark.parametrize("blocks", [None, "4"])
+def test_fused_rope_decode_attention_matches_unfused(D, Hq, Hkv, rot, blocks, monkeypatch):
     """decode_attn_rope (rope + cache write of the newest token inside the attention launch) ==
-    rope_cache_write + decode_attn, bitwise: output and the written cache row."""
+    rope_cache_write + decode_attn, bitwise: output and the written cache row (blocks = 4: both
+    on the multi-chunk loop kernel, the newest key's V patched into the DMA'd LDS image)."""
     from distributed_llm_alignment_amd.ops import RotaryCache, _ext
+
+    if blocks is not None:
+        monkeypatch.setenv("DLA_DECODE_BLOCKS", blocks)
 
     C = _ext.require()
     dev = torch.device("cuda", 0)
