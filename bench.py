@@ -172,6 +172,38 @@ def preflight(st, dev) -> None:
         raise SystemExit(f"bench.py: preflight all-reduce returned wrong values on rank {st.rank}")
 
 
+def collective_bandwidth(st, dev, mb: int = 256, iters: int = 5) -> dict:
+    """RCCL bus bandwidth over this run's ranks, measured before the timed window: a `mb` MB bf16
+    all-reduce and reduce-scatter (the collectives of the DDP / ZeRO-1 gradient sync), 2 warm-up +
+    `iters` timed calls each, slowest rank's time (nccl-tests' busbw convention:
+    all-reduce algbw x 2(n-1)/n, reduce-scatter algbw x (n-1)/n). Recorded in the result line so a
+    multi-GPU run carries its own xGMI evidence."""
+    import torch.distributed as dist
+
+    n = st.world_size
+    if n < 2 or not st.initialized:
+        return {}
+    numel = mb * 1024 * 1024 // 2
+    x = torch.ones(numel, dtype=torch.bfloat16, device=dev)
+    out = torch.empty(numel // n, dtype=torch.bfloat16, device=dev)
+    res = {}
+    for name, fn, factor in (("allreduce", lambda: dist.all_reduce(x), 2 * (n - 1) / n),
+                             ("reduce_scatter", lambda: dist.reduce_scatter_tensor(out, x), (n - 1) / n)):
+        for _ in range(2):
+            fn()
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            fn()
+        torch.cuda.synchronize(dev)
+        dt = torch.tensor([(time.perf_counter() - t0) / iters], dtype=torch.float64, device=dev)
+        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+        res[f"{name}_{mb}MB_busbw_GBps"] = round(mb * 2 ** 20 / float(dt.item()) * factor / 1e9, 1)
+    del x, out
+    return res
+
+
 def _maybe_fail(step: int, rank: int) -> None:
     """Fault injection for the launcher test: DLA_BENCH_FAIL_RANK / DLA_BENCH_FAIL_STEP make that
     rank die abruptly (no cleanup) at that step; the whole command must still exit non-zero."""
@@ -223,8 +255,11 @@ def main(argv=None) -> int:
     if dev.type == "cuda":
         _ext.require()
         gemm_mode = enable_gemm_tuning(dev.index)
+    coll_bw = {}
     if st.world_size > 1 or os.environ.get("DLA_BENCH_PREFLIGHT") == "1":
         preflight(st, dev)
+        if dev.type == "cuda":
+            coll_bw = collective_bandwidth(st, dev)
     world = st.world_size
     mesh = build_mesh(tp=args.tp, ep=args.ep, sp=args.sp)
     overrides = {} if args.layers is None else {"num_layers": args.layers}
@@ -396,6 +431,7 @@ def main(argv=None) -> int:
                 "final_loss": round(float(state["loss"].item()), 5),
                 "comm_exposed_ms_per_step": round(exposed_ms, 2),
                 "gemm_selection": "tunableop:" + gemm_mode,
+                **({"rccl": coll_bw} if coll_bw else {}),
             },
         }
         print(json.dumps(rec), flush=True)

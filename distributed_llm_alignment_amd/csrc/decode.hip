@@ -766,20 +766,23 @@ static void launch_decode_d(const bf16_t* q, int64_t q_sb, int64_t q_sh, bf16_t*
 }
 
 // DLA_DECODE_LOOP=0: one 128-key chunk per block (decode_attn_kernel); otherwise blocks loop over
-// chunks so that B x Hkv x splits stays near DLA_DECODE_BLOCKS (default 512 = two resident
-// 256-thread blocks per CU at the loop kernel's register budget)
+// chunks so that B x Hkv x splits stays near DLA_DECODE_BLOCKS (default 256; same-box graph decode:
+// B = 8 / 1152 keys 3 chunks per block 3.98-4.00 vs 4.02 ms/token one-chunk, 2 chunks 4.03-4.06,
+// 9 chunks (no combine) 4.25; B = 64 / ~576 keys: one split per sequence)
 static int decode_cpb(int Tmax, int B, int Hkv) {
   // read per call (cheap next to a launch) so a test can force the loop kernel at small shapes
   const char* e = getenv("DLA_DECODE_LOOP");
   const char* tb = getenv("DLA_DECODE_BLOCKS");
-  const int target = (e != nullptr && atoi(e) == 0) ? 0 : (tb ? atoi(tb) : 512);
+  const int target = (e != nullptr && atoi(e) == 0) ? 0 : (tb ? atoi(tb) : 256);
   const int nch = (Tmax + kDecChunk - 1) / kDecChunk;
   if (target <= 0) return 0;
   const int64_t blocks = static_cast<int64_t>(B) * Hkv * nch;
   const int cpb = static_cast<int>((blocks + target - 1) / target);
-  // at <= 2 chunks per block the one-chunk kernel (3 blocks per CU) measured faster
-  // (B = 8, 1152 keys: 4.05 vs 4.12 ms/token)
-  return cpb <= 2 ? 0 : std::min(cpb, nch);
+  // below DLA_DECODE_LOOP_MIN (default 3) chunks per block the one-chunk kernel (3 blocks per CU)
+  // measured faster (B = 8, 1152 keys: 4.05 vs 4.12 ms/token)
+  const char* mn = getenv("DLA_DECODE_LOOP_MIN");
+  const int min_cpb = mn ? atoi(mn) : 3;
+  return cpb < min_cpb ? 0 : std::min(cpb, nch);
 }
 
 int decode_num_splits(int Tmax, int B, int Hkv) {
