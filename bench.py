@@ -189,19 +189,30 @@ def collective_bandwidth(st, dev, mb: int = 256, iters: int = 5) -> dict:
     res = {}
     for name, fn, factor in (("allreduce", lambda: dist.all_reduce(x), 2 * (n - 1) / n),
                              ("reduce_scatter", lambda: dist.reduce_scatter_tensor(out, x), (n - 1) / n)):
-        for _ in range(2):
-            fn()
-        torch.cuda.synchronize(dev)
-        dist.barrier()
-        t0 = time.perf_counter()
-        for _ in range(iters):
-            fn()
-        torch.cuda.synchronize(dev)
-        dt = torch.tensor([(time.perf_counter() - t0) / iters], dtype=torch.float64, device=dev)
-        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
-        res[f"{name}_{mb}MB_busbw_GBps"] = round(mb * 2 ** 20 / float(dt.item()) * factor / 1e9, 1)
+        try:
+            res[f"{name}_{mb}MB_busbw_GBps"] = _time_collective(st, dev, fn, mb, iters, factor)
+        except Exception as e:  # informational only: never fails the benchmark (gloo has no RS)
+            sys.stderr.write(f"[preflight] {name} bandwidth probe skipped: {e}\n")
     del x, out
     return res
+
+
+def _time_collective(st, dev, fn, mb: int, iters: int, factor: float) -> float:
+    import torch.distributed as dist
+
+    for _ in range(2):
+        fn()
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        fn()
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    dt = torch.tensor([(time.perf_counter() - t0) / iters], dtype=torch.float64, device=dev)
+    dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    return round(mb * 2 ** 20 / float(dt.item()) * factor / 1e9, 1)
 
 
 def _maybe_fail(step: int, rank: int) -> None:
@@ -258,8 +269,8 @@ def main(argv=None) -> int:
     coll_bw = {}
     if st.world_size > 1 or os.environ.get("DLA_BENCH_PREFLIGHT") == "1":
         preflight(st, dev)
-        if dev.type == "cuda":
-            coll_bw = collective_bandwidth(st, dev)
+        if dev.type == "cuda" or os.environ.get("DLA_BENCH_COLLBW") == "1":
+            coll_bw = collective_bandwidth(st, dev, mb=int(os.environ.get("DLA_BENCH_COLLBW_MB", "256")))
     world = st.world_size
     mesh = build_mesh(tp=args.tp, ep=args.ep, sp=args.sp)
     overrides = {} if args.layers is None else {"num_layers": args.layers}

@@ -101,3 +101,17 @@ def test_launcher_counts_gpus_without_hip(monkeypatch):
     n = mod.visible_gpu_count()  # sysfs here (or the child-process count): never HIP in-process
     assert n >= 0
     assert not torch.cuda.is_initialized()
+
+
+def test_bench_records_collective_bandwidth():
+    """Multi-rank result lines carry the run's own collective bus bandwidth (`config.rccl`,
+    measured before the timed window; on the GPU node RCCL all-reduce and reduce-scatter over
+    xGMI). Here on gloo: the all-reduce is measured; gloo's missing reduce-scatter is skipped
+    without failing the run."""
+    p = _run(["--gpus", "2", "--device", "cpu", "--model", "tiny-llama", "--steps", "1",
+              "--warmup", "0", "--seq-len", "64", "--micro-pairs", "2", "--accum", "1"],
+             {"DLA_BENCH_COLLBW": "1", "DLA_BENCH_COLLBW_MB": "2"})
+    assert p.returncode == 0, p.stderr[-3000:]
+    rec = _record(p.stdout)
+    bw = rec["config"]["rccl"]
+    assert bw["allreduce_2MB_busbw_GBps"] > 0, bw
