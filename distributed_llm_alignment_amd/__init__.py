@@ -8,6 +8,11 @@ scaling runs RCCL collectives over xGMI (`parallel/`).
 """
 __version__ = "0.1.0"
 
+import os as _os
+
 from .ops import _ext as _ext  # noqa: F401  (loads csrc/_C.so when present)
 
-_ext.load()
+# DLA_SKIP_EXT_LOAD=1: do not load _C.so at import (the build entry sets it, so a stale library
+# from an older source tree -- whose op schemas no longer match -- is rebuilt, never loaded first)
+if _os.environ.get("DLA_SKIP_EXT_LOAD") != "1":
+    _ext.load()

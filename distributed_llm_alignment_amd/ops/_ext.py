@@ -51,7 +51,8 @@ def require():
     if not available():
         raise RuntimeError(
             "distributed_llm_alignment_amd HIP extension is not loaded "
-            f"({_STATE['error']!r}). Build it with: python -m distributed_llm_alignment_amd._build"
+            f"({_STATE['error']!r}). Build it with: "
+            "DLA_SKIP_EXT_LOAD=1 python -m distributed_llm_alignment_amd._build"
         )
     return torch.ops.dla
 
