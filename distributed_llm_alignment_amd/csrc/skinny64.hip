@@ -57,25 +57,28 @@ bool m64_nt() {
 
 }  // namespace
 
-// grid (N / 128 [GLU: F / 64], S), 512 threads. LDS: 2 x 16 MT x kM64Ld bf16.
+// grid (N / 16 NW [GLU: F / 8 NW], S), 64 NW threads. LDS: 2 x 16 MT x kM64Ld bf16.
 // GLU: W = [gate; up] (2F rows), output m = silu(rstd * g) * (rstd * u) [M, F] where rstd comes
 // from ssq_in (the producer's row partial sums, [M][nbp]) when NIN, else 1; gate / up are
 // rounded to bf16 before SwiGLU exactly as the unfused GEMM + swiglu pair.
 // Otherwise S == 1 writes y = bf16(x W^T); S > 1 writes fp32 slab ws[s][m][n].
-template <int MT, bool GLU, bool NIN, bool NT, int DEPTH>
-__global__ __launch_bounds__(512) void m64_gemm_kernel(
+template <int MT, bool GLU, bool NIN, bool NT, int DEPTH, int NW = kM64Waves>
+__global__ __launch_bounds__(64 * NW) void m64_gemm_kernel(
     const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ W, int64_t ldw,
     bf16_t* __restrict__ y, int64_t ldy, float* __restrict__ ws, int M, int N, int K, int kc,
     const float* __restrict__ ssq_in, int nbp, float eps) {
   extern __shared__ __attribute__((aligned(16))) bf16_t xs[];
   __shared__ float rstd_s[64];
   constexpr int RB = 16 * MT * kM64Ld;  // one ring slot
+  constexpr int NTH = 64 * NW;
+  constexpr int XPASS = 16 * MT * 32 / NTH;  // x staging passes (32 threads per 256-deep row)
+  constexpr int FPW = 8 * NW;                // GLU: features per workgroup
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63;
   const int r = lane & 15, q = lane >> 4;
   const int F = N >> 1;
-  const int n0 = GLU ? (wave < 4 ? 0 : F) + blockIdx.x * 64 + (wave & 3) * 16
-                     : blockIdx.x * (16 * kM64Waves) + wave * 16;
+  const int n0 = GLU ? (wave < NW / 2 ? 0 : F) + blockIdx.x * FPW + (wave % (NW / 2)) * 16
+                     : blockIdx.x * (16 * NW) + wave * 16;
   const int s = blockIdx.y;
   const int k0 = s * kc;
   const int nch = kc / kM64Ck;
@@ -95,13 +98,13 @@ __global__ __launch_bounds__(512) void m64_gemm_kernel(
   // full HBM round trip for the next weight chunk). DEPTH chunks are in flight; x rows >= M are
   // zeros so the A fragments need no row test.
   const int xm = tid >> 5, xc = (tid & 31) * 8;
-  bf16x8 xr[DEPTH][MT];
+  bf16x8 xr[DEPTH][XPASS];
   s16x8 b[DEPTH][kM64Steps];
   auto issue = [&](auto J, int c) {
     constexpr int j = decltype(J)::value;
 #pragma unroll
-    for (int t = 0; t < MT; ++t) {
-      const int m = xm + 16 * t;
+    for (int t = 0; t < XPASS; ++t) {
+      const int m = xm + (NTH / 32) * t;
       xr[j][t] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
       if (m < M) xr[j][t] = load_bf16x8(x + static_cast<int64_t>(m) * ldx + k0 + c * kM64Ck + xc);
     }
@@ -111,7 +114,7 @@ __global__ __launch_bounds__(512) void m64_gemm_kernel(
   auto xstore = [&](auto J, int slot) {
     constexpr int j = decltype(J)::value;
 #pragma unroll
-    for (int t = 0; t < MT; ++t) store_bf16x8(xs + slot * RB + (xm + 16 * t) * kM64Ld + xc, xr[j][t]);
+    for (int t = 0; t < XPASS; ++t) store_bf16x8(xs + slot * RB + (xm + (NTH / 32) * t) * kM64Ld + xc, xr[j][t]);
   };
   issue(std::integral_constant<int, 0>{}, 0);
   if (1 < nch) issue(std::integral_constant<int, 1>{}, 1);
@@ -165,8 +168,8 @@ __global__ __launch_bounds__(512) void m64_gemm_kernel(
       }
     }
     // the ring is dead after the loop's last barrier: exchange the gate / up tiles through it
-    float* glu = reinterpret_cast<float*>(xs);  // [2][64][64]
-    const int half = wave >> 2, col = (wave & 3) * 16 + r;
+    float* glu = reinterpret_cast<float*>(xs);  // [2][64][FPW]
+    const int half = wave / (NW / 2), col = (wave % (NW / 2)) * 16 + r;
     __syncthreads();
 #pragma unroll
     for (int t = 0; t < MT; ++t)
@@ -175,19 +178,19 @@ __global__ __launch_bounds__(512) void m64_gemm_kernel(
         const int m = 16 * t + 4 * q + i;
         float v = acc[t][i];
         if constexpr (NIN) v *= m < M ? rstd_s[m] : 0.f;
-        glu[(half * 64 + m) * 64 + col] = bf2f(f2bf(v));
+        glu[(half * 64 + m) * FPW + col] = bf2f(f2bf(v));
       }
     __syncthreads();
     // 8 consecutive features of one row per thread, one 16-byte store
-    for (int e = tid; e < M * 8; e += 512) {
-      const int m = e >> 3, c8 = (e & 7) * 8;
+    for (int e = tid; e < M * (FPW / 8); e += NTH) {
+      const int m = e / (FPW / 8), c8 = (e % (FPW / 8)) * 8;
       float o[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float g = glu[m * 64 + c8 + j], u = glu[(64 + m) * 64 + c8 + j];
+        const float g = glu[m * FPW + c8 + j], u = glu[(64 + m) * FPW + c8 + j];
         o[j] = g / (1.f + __expf(-g)) * u;
       }
-      store_bf16x8(y + static_cast<int64_t>(m) * ldy + blockIdx.x * 64 + c8, pack_bf16x8(o));
+      store_bf16x8(y + static_cast<int64_t>(m) * ldy + blockIdx.x * FPW + c8, pack_bf16x8(o));
     }
     return;
   }
@@ -295,41 +298,30 @@ size_t m64_lds_bytes(int M) {
   return static_cast<size_t>(2 * 16 * mt * kM64Ld) * sizeof(bf16_t);
 }
 
-static int m64_depth() {
-  static const int d = [] {
-    const char* e = getenv("DLA_M64_DEPTH");
-    const int v = e ? atoi(e) : 2;
-    return v < 2 ? 2 : (v > 4 ? 4 : v);
-  }();
-  return d;
-}
-
-template <int MT, bool GLU, bool NIN, bool NT, int DEPTH>
-static void m64_launch_d(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
+template <int MT, bool GLU, bool NIN, bool NT, int NW>
+static void m64_launch_w(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
                          int64_t ldy, float* ws, int M, int N, int K, int S, const float* ssq_in,
                          int nbp, float eps, hipStream_t st) {
   const size_t lds = static_cast<size_t>(2 * 16 * MT * kM64Ld) * sizeof(bf16_t);
   static bool attr = [] {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&m64_gemm_kernel<MT, GLU, NIN, NT, DEPTH>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&m64_gemm_kernel<MT, GLU, NIN, NT, 2, NW>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
     (void)hipGetLastError();
     return true;
   }();
   (void)attr;
-  dim3 grid(GLU ? N / 128 : N / (16 * kM64Waves), S);
-  m64_gemm_kernel<MT, GLU, NIN, NT, DEPTH><<<grid, 512, lds, st>>>(x, ldx, W, ldw, y, ldy, ws, M, N,
-                                                                    K, K / S, ssq_in, nbp, eps);
+  dim3 grid(GLU ? N / 2 / (8 * NW) : N / (16 * NW), S);
+  m64_gemm_kernel<MT, GLU, NIN, NT, 2, NW><<<grid, 64 * NW, lds, st>>>(x, ldx, W, ldw, y, ldy, ws, M, N,
+                                                                       K, K / S, ssq_in, nbp, eps);
 }
 
+// NW = 8 waves per workgroup (gate|up: 64 features per workgroup). 4 waves (448 gate|up
+// workgroups at Llama-3-8B, two per CU) measured 55.0 vs 53.2 us: README "Tried".
 template <int MT, bool GLU, bool NIN, bool NT>
 static void m64_launch(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
                        int64_t ldy, float* ws, int M, int N, int K, int S, const float* ssq_in,
                        int nbp, float eps, hipStream_t st) {
-  switch (m64_depth()) {
-    case 2: m64_launch_d<MT, GLU, NIN, NT, 2>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, ssq_in, nbp, eps, st); break;
-    case 4: m64_launch_d<MT, GLU, NIN, NT, 4>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, ssq_in, nbp, eps, st); break;
-    default: m64_launch_d<MT, GLU, NIN, NT, 3>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, ssq_in, nbp, eps, st); break;
-  }
+  m64_launch_w<MT, GLU, NIN, NT, kM64Waves>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, ssq_in, nbp, eps, st);
 }
 
 template <int MT, bool NT>
