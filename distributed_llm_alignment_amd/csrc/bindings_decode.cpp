@@ -5,6 +5,9 @@
 #include <torch/library.h>
 
 #include <cmath>
+#include <cstdlib>
+#include <map>
+#include <mutex>
 #include <tuple>
 
 #include "bind_util.h"
@@ -14,11 +17,11 @@ namespace dla {
 
 void launch_decode_attn(const bf16_t*, int64_t, int64_t, bf16_t*, bf16_t*, int64_t,
                         int64_t, int64_t, const int*, const int*, int, float, int, int, int, int,
-                        int, float*, float*, bf16_t*, int64_t, int64_t, hipStream_t);
+                        int, float*, float*, bf16_t*, int64_t, int64_t, int*, hipStream_t);
 void launch_decode_attn_rope(const bf16_t*, int64_t, const float*, const float*, const int*,
                              const int64_t*, int, bf16_t*, bf16_t*, int64_t, int64_t, int64_t,
                              const int*, const int*, int, float, int, int, int, int, int, float*,
-                             float*, bf16_t*, int64_t, int64_t, hipStream_t);
+                             float*, bf16_t*, int64_t, int64_t, int*, hipStream_t);
 int decode_num_splits(int Tmax, int B, int Hkv);
 void launch_rope_cache(const bf16_t*, int64_t, bf16_t*, bf16_t*, bf16_t*, int64_t, int64_t,
                        int64_t, const int64_t*, const float*, const float*, const int*, int, int,
@@ -293,6 +296,32 @@ at::Tensor skinny_gemm(const at::Tensor& x, const at::Tensor& w, at::Tensor& cou
   return y;
 }
 
+// Per-device arrival counters of the in-kernel split combine (decode.hip dec_arrive_combine):
+// zeroed once here, re-armed to 0 by the block that combines. Created only outside a stream
+// capture (generation runs an eager decode step before capturing); nullptr -> the combine launch.
+// One buffer per device: two decode attention kernels must not run concurrently on one device.
+// DLA_DECODE_FUSED_COMBINE=0 keeps the separate combine launch.
+constexpr int64_t kDecCounters = 4096;
+static int* decode_counters(const at::Tensor& like, int64_t n) {
+  static const bool on = [] {
+    const char* e = std::getenv("DLA_DECODE_FUSED_COMBINE");
+    return !(e != nullptr && std::atoi(e) == 0);
+  }();
+  if (!on || n > kDecCounters) return nullptr;
+  static auto* bufs = new std::map<int, at::Tensor>();  // never destroyed (outlives the allocator)
+  static std::mutex mu;
+  std::lock_guard<std::mutex> lk(mu);
+  const int dev = like.get_device();
+  auto it = bufs->find(dev);
+  if (it != bufs->end()) return it->second.data_ptr<int>();
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(cur_stream(like), &cs) != hipSuccess || cs != hipStreamCaptureStatusNone)
+    return nullptr;
+  auto t = at::zeros({kDecCounters}, like.options().dtype(at::kInt));
+  bufs->emplace(dev, t);
+  return t.data_ptr<int>();
+}
+
 at::Tensor decode_attn(const at::Tensor& q, const at::Tensor& k_cache, const at::Tensor& v_cache,
                        const at::Tensor& kv_len, const c10::optional<at::Tensor>& kv_start,
                        int64_t window, double scale) {
@@ -335,7 +364,7 @@ at::Tensor decode_attn(const at::Tensor& q, const at::Tensor& k_cache, const at:
                      kv_len.data_ptr<int>(), ks, static_cast<int>(window),
                      static_cast<float>(scale * 1.4426950408889634), (int)B, (int)Hq, (int)Hkv,
                      (int)D, (int)Tmax, part_o.data_ptr<float>(), part_ml.data_ptr<float>(),
-                     bp(out), out.stride(0), out.stride(1), cur_stream(q));
+                     bp(out), out.stride(0), out.stride(1), decode_counters(q, B * Hkv), cur_stream(q));
   return out;
 }
 
@@ -431,7 +460,8 @@ at::Tensor decode_attn_rope(const at::Tensor& qkv, const at::Tensor& cos, const 
                           kv_len.data_ptr<int>(), ks, static_cast<int>(window),
                           static_cast<float>(scale * 1.4426950408889634), (int)B, (int)Hq, (int)Hkv,
                           (int)D, (int)Tmax, part_o.data_ptr<float>(), part_ml.data_ptr<float>(),
-                          bp(out), out.stride(0), out.stride(1), cur_stream(qkv));
+                          bp(out), out.stride(0), out.stride(1), decode_counters(qkv, B * Hkv),
+                          cur_stream(qkv));
   return out;
 }
 

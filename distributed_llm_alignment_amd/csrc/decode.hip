@@ -323,6 +323,84 @@ __global__ __launch_bounds__(256, 3) void decode_attn_kernel(
   }
 }
 
+// In-kernel split combine (decode_attn_loop_kernel with `cnt`): every block publishes its
+// partial (m, l, o) with write-through (sc1) stores, waits for them (vmcnt(0) in every wave), and
+// one lane adds to the (b, kv head) arrival counter; the block whose add returns nsplit - 1 re-arms
+// the counter, takes ONE agent-scope acquire and merges the nsplit partials into the normalised
+// bf16 output -- the decode_combine_kernel launch and its kernel boundary are gone. No block waits
+// on another (no polling), so a late or empty split cannot stall the grid. Hand-off form:
+// MI355X_MICROARCH "Valid forms" (sc1 stores + drained vmcnt + agent atomic; consumer acquire).
+__device__ __forceinline__ void dec_pub(float* p, float v, bool wt) {
+  if (wt) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+
+constexpr int kDecMaxFuse = 8;  // most splits the in-kernel combine merges
+
+template <int D, int G>
+__device__ __forceinline__ void dec_arrive_combine(int* __restrict__ cnt, const float* part_o,
+                                                   const float* part_ml, int64_t pbase0, int nsplit,
+                                                   bf16_t* __restrict__ out, int64_t o_base,
+                                                   int64_t o_sh) {
+  __shared__ int last_s;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == nsplit - 1;
+    if (last) {
+      __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    last_s = last;
+  }
+  __syncthreads();
+  if (!last_s) return;
+  // same merge as decode_combine_kernel (log2-domain running max, splits in ascending order),
+  // every load of the (<= kDecMaxFuse) splits issued before any use: one round trip after the acquire
+  constexpr int EPT = (G * D + 255) / 256;
+  float mv[EPT][kDecMaxFuse], lv[EPT][kDecMaxFuse], ov[EPT][kDecMaxFuse];
+#pragma unroll
+  for (int e = 0; e < EPT; ++e) {
+    const int i = threadIdx.x + 256 * e;
+    const int g = min(i, G * D - 1) / D, d = i % D;
+    const float* ml = part_ml + (pbase0 + (int64_t)g * nsplit) * 2;
+    const float* po = part_o + (pbase0 + (int64_t)g * nsplit) * D + d;
+#pragma unroll
+    for (int s = 0; s < kDecMaxFuse; ++s) {
+      if (s < nsplit) {
+        mv[e][s] = ml[2 * s];
+        lv[e][s] = ml[2 * s + 1];
+        ov[e][s] = po[(int64_t)s * D];
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < EPT; ++e) {
+    const int i = threadIdx.x + 256 * e;
+    if (i >= G * D) break;
+    const int g = i / D, d = i % D;
+    float m = -INFINITY;
+#pragma unroll
+    for (int s = 0; s < kDecMaxFuse; ++s)
+      if (s < nsplit) m = fmaxf(m, mv[e][s]);
+    float acc = 0.f, l = 0.f;
+    if (m != -INFINITY) {
+#pragma unroll
+      for (int s = 0; s < kDecMaxFuse; ++s) {
+        if (s < nsplit) {
+          const float c = mv[e][s] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(mv[e][s] - m);
+          l += c * lv[e][s];
+          acc += c == 0.f ? 0.f : c * ov[e][s];  // an empty split never wrote its o row
+        }
+      }
+    }
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    out[o_base + (int64_t)g * o_sh + d] = f2bf(acc * inv);
+  }
+}
+
 // Multi-chunk form (the default): grid (nsplit, Hkv, B) with each block looping over `cpb`
 // consecutive 128-key chunks of its (b, kv head), chunk c + 2's K / V loads in flight while chunk
 // c is computed (a 2-slot register ring), and a per-wave online softmax across the chunks. The
@@ -344,9 +422,10 @@ __global__ __launch_bounds__(256, 2) void decode_attn_loop_kernel(
     int64_t c_sb, int64_t c_st, int64_t c_sh, const int* __restrict__ kv_len,
     const int* __restrict__ kv_start, int window, float scale_log2, int nsplit, int cpb,
     float* __restrict__ part_o, float* __restrict__ part_ml, int Hq, DecRope rp,
-    bf16_t* __restrict__ out, int64_t o_sb, int64_t o_sh) {
-  // out != nullptr (one split per sequence): the block writes the normalised bf16 output itself
-  // and the combine launch is skipped
+    bf16_t* __restrict__ out, int64_t o_sb, int64_t o_sh, int* __restrict__ cnt) {
+  // out != nullptr, cnt == nullptr (one split per sequence): the block writes the normalised bf16
+  // output itself; out and cnt (nsplit > 1): partials + in-kernel combine (dec_arrive_combine).
+  // Either way the combine launch is skipped.
   constexpr int LPK = D / 8, KPI = 64 / LPK, KPW = kDecChunk / 4, NIT = KPW / KPI;
   constexpr int KST = D / 32;
   static_assert(G <= 16 && KPW == 32, "decode tile geometry");
@@ -383,14 +462,21 @@ __global__ __launch_bounds__(256, 2) void decode_attn_loop_kernel(
   const int cbeg = max(cfirst, lo / kDecChunk);
   const int cend = min(cfirst + cpb, (len + kDecChunk - 1) / kDecChunk);
   const int64_t pbase = ((int64_t)b * Hq + (int64_t)hk * G) * nsplit + split;
+  const bool fuse = cnt != nullptr;
+  int* const cslot = fuse ? cnt + (int64_t)b * gridDim.y + hk : nullptr;
+  const int64_t pbase0 = ((int64_t)b * Hq + (int64_t)hk * G) * nsplit;
+  const int64_t obase = (int64_t)b * o_sb + (int64_t)hk * G * o_sh;
   if (cbeg >= cend || max(cbeg * kDecChunk, lo) >= len) {
-    if (out != nullptr) {  // no visible key: zeros, as the combine writes for an all-empty row
+    if (out != nullptr && !fuse) {  // no visible key: zeros, as the combine writes for an all-empty row
       for (int i = tid; i < G * D; i += 256)
         out[(int64_t)b * o_sb + (int64_t)(hk * G + i / D) * o_sh + i % D] = 0;
-    } else if (tid < G) {
-      part_ml[(pbase + (int64_t)tid * nsplit) * 2 + 0] = -INFINITY;
-      part_ml[(pbase + (int64_t)tid * nsplit) * 2 + 1] = 0.f;
+      return;
     }
+    if (tid < G) {
+      dec_pub(&part_ml[(pbase + (int64_t)tid * nsplit) * 2 + 0], -INFINITY, fuse);
+      dec_pub(&part_ml[(pbase + (int64_t)tid * nsplit) * 2 + 1], 0.f, fuse);
+    }
+    if (fuse) dec_arrive_combine<D, G>(cslot, part_o, part_ml, pbase0, nsplit, out, obase, o_sh);
     return;
   }
   // q fragments first (the oldest loads: S of chunk 0 waits for them and K(0) only)
@@ -562,16 +648,17 @@ __global__ __launch_bounds__(256, 2) void decode_attn_loop_kernel(
         ll += cc * mls[w][g][1];
       }
     }
-    if (out != nullptr) {
+    if (out != nullptr && !fuse) {
       out[(int64_t)b * o_sb + (int64_t)(hk * G + g) * o_sh + d] = f2bf(ll > 0.f ? v * (1.f / ll) : 0.f);
       continue;
     }
-    part_o[(pbase + (int64_t)g * nsplit) * D + d] = v;
+    dec_pub(&part_o[(pbase + (int64_t)g * nsplit) * D + d], v, fuse);
     if (d == 0) {
-      part_ml[(pbase + (int64_t)g * nsplit) * 2 + 0] = mm;
-      part_ml[(pbase + (int64_t)g * nsplit) * 2 + 1] = ll;
+      dec_pub(&part_ml[(pbase + (int64_t)g * nsplit) * 2 + 0], mm, fuse);
+      dec_pub(&part_ml[(pbase + (int64_t)g * nsplit) * 2 + 1], ll, fuse);
     }
   }
+  if (fuse) dec_arrive_combine<D, G>(cslot, part_o, part_ml, pbase0, nsplit, out, obase, o_sh);
 }
 
 // Decode-step prologue: rotate q (-> q_out [B, Hq, D]) and k of the newest token and write k and
@@ -705,25 +792,27 @@ static void launch_decode_d(const bf16_t* q, int64_t q_sb, int64_t q_sh, bf16_t*
                             const int* kv_len, const int* kv_start, int window, float scale_log2,
                             int B, int Hq, int Hkv, int Tmax, float* part_o, float* part_ml,
                             bf16_t* out, int64_t o_sb, int64_t o_sh, const DecRope* rp,
-                            hipStream_t st) {
+                            int* cnt, hipStream_t st) {
   const int G = Hq / Hkv;
   const int cpb = decode_cpb(Tmax, B, Hkv);
   const int nsplit = decode_num_splits(Tmax, B, Hkv);
   dim3 grid(nsplit, Hkv, B);
   const DecRope r0 = rp ? *rp : DecRope{};
   if (cpb > 0) {
-    bf16_t* fin = nsplit == 1 ? out : nullptr;  // one split per sequence: no combine launch
+    // one split per sequence, or the in-kernel combine (arrival counters given): no combine launch
+    int* const cn = (nsplit > 1 && nsplit <= kDecMaxFuse) ? cnt : nullptr;
+    bf16_t* fin = (nsplit == 1 || cn != nullptr) ? out : nullptr;
 #define DLA_DECL(GG)                                                                                    \
   if (rp)                                                                                               \
     decode_attn_loop_kernel<D, GG, true><<<grid, 256, 0, st>>>(q, q_sb, q_sh, kc, vc, c_sb, c_st, c_sh, \
                                                                kv_len, kv_start, window, scale_log2,    \
                                                                nsplit, cpb, part_o, part_ml, Hq, r0,    \
-                                                               fin, o_sb, o_sh);                        \
+                                                               fin, o_sb, o_sh, cn);                    \
   else                                                                                                  \
     decode_attn_loop_kernel<D, GG, false><<<grid, 256, 0, st>>>(q, q_sb, q_sh, kc, vc, c_sb, c_st, c_sh, \
                                                                 kv_len, kv_start, window, scale_log2,   \
                                                                 nsplit, cpb, part_o, part_ml, Hq, r0,   \
-                                                                fin, o_sb, o_sh)
+                                                                fin, o_sb, o_sh, cn)
     switch (G) {
       case 1: DLA_DECL(1); break;
       case 2: DLA_DECL(2); break;
@@ -795,13 +884,13 @@ void launch_decode_attn(const bf16_t* q, int64_t q_sb, int64_t q_sh, bf16_t* kc,
                         bf16_t* vc, int64_t c_sb, int64_t c_st, int64_t c_sh,
                         const int* kv_len, const int* kv_start, int window, float scale_log2, int B,
                         int Hq, int Hkv, int D, int Tmax, float* part_o, float* part_ml,
-                        bf16_t* out, int64_t o_sb, int64_t o_sh, hipStream_t st) {
+                        bf16_t* out, int64_t o_sb, int64_t o_sh, int* cnt, hipStream_t st) {
   if (D == 128)
     launch_decode_d<128>(q, q_sb, q_sh, kc, vc, c_sb, c_st, c_sh, kv_len, kv_start, window,
-                         scale_log2, B, Hq, Hkv, Tmax, part_o, part_ml, out, o_sb, o_sh, nullptr, st);
+                         scale_log2, B, Hq, Hkv, Tmax, part_o, part_ml, out, o_sb, o_sh, nullptr, cnt, st);
   else
     launch_decode_d<64>(q, q_sb, q_sh, kc, vc, c_sb, c_st, c_sh, kv_len, kv_start, window,
-                        scale_log2, B, Hq, Hkv, Tmax, part_o, part_ml, out, o_sb, o_sh, nullptr, st);
+                        scale_log2, B, Hq, Hkv, Tmax, part_o, part_ml, out, o_sb, o_sh, nullptr, cnt, st);
 }
 
 // rope + cache write of the newest token fused into the decode attention (see DecRope)
@@ -810,14 +899,14 @@ void launch_decode_attn_rope(const bf16_t* qkv, int64_t ld, const float* cos_t, 
                              int64_t c_sb, int64_t c_st, int64_t c_sh, const int* kv_len,
                              const int* kv_start, int window, float scale_log2, int B, int Hq,
                              int Hkv, int D, int Tmax, float* part_o, float* part_ml, bf16_t* out,
-                             int64_t o_sb, int64_t o_sh, hipStream_t st) {
+                             int64_t o_sb, int64_t o_sh, int* cnt, hipStream_t st) {
   const DecRope rp{qkv, ld, cos_t, sin_t, pos, slot, rot, Hkv};
   if (D == 128)
     launch_decode_d<128>(nullptr, 0, 0, kc, vc, c_sb, c_st, c_sh, kv_len, kv_start, window,
-                         scale_log2, B, Hq, Hkv, Tmax, part_o, part_ml, out, o_sb, o_sh, &rp, st);
+                         scale_log2, B, Hq, Hkv, Tmax, part_o, part_ml, out, o_sb, o_sh, &rp, cnt, st);
   else
     launch_decode_d<64>(nullptr, 0, 0, kc, vc, c_sb, c_st, c_sh, kv_len, kv_start, window,
-                        scale_log2, B, Hq, Hkv, Tmax, part_o, part_ml, out, o_sb, o_sh, &rp, st);
+                        scale_log2, B, Hq, Hkv, Tmax, part_o, part_ml, out, o_sb, o_sh, &rp, cnt, st);
 }
 
 }  // namespace dla
