@@ -46,14 +46,14 @@ void launch_skinny_glu_ks(const bf16_t*, int64_t, const bf16_t*, int64_t, bf16_t
                           int, int, hipStream_t);
 
 void launch_skinny_ks_fused(const bf16_t*, int64_t, const bf16_t*, int64_t, bf16_t*, int64_t, int,
-                            int, int, const KsFuse&, bool, bool, hipStream_t);
+                            int, int, const KsFuse&, bool, bool, bool, hipStream_t);
 void launch_skinny_glu_normin(const bf16_t*, int64_t, const bf16_t*, int64_t, bf16_t*, int64_t, int,
-                              int, int, const KsFuse&, hipStream_t);
+                              int, int, const KsFuse&, bool, hipStream_t);
 
 int m64_splits(int N, int K);
 bool m64_shape_ok(int N, int K, bool glu);
 void launch_m64_gemm(const bf16_t*, int64_t, const bf16_t*, int64_t, bf16_t*, int64_t, float*, int,
-                     int, int, int, bool, const float*, int, float, hipStream_t);
+                     int, int, int, bool, const float*, int, float, bool, hipStream_t);
 void launch_m64_reduce(const float*, int, int, int, bf16_t*, int64_t, const bf16_t*, int64_t,
                        const float*, int, int, float, float*, hipStream_t);
 
@@ -69,10 +69,13 @@ std::tuple<at::Tensor, at::Tensor> skinny64(const at::Tensor& x, const at::Tenso
                                             bool glu) {
   check_bf16(x, "x");
   check_bf16(w, "w");
-  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.stride(1) == 1 && w.stride(1) == 1 &&
-                  x.stride(0) % 8 == 0 && w.stride(0) % 8 == 0,
-              "x [M, K] / w [N, K]: unit inner stride, 16-byte aligned rows");
-  const int64_t M = x.size(0), N = w.size(0), K = w.size(1);
+  // w: [N, K] row-major, or the tiled layout [N / 16, K / 32, 4, 16, 8] (skinny64.hip TW)
+  const bool tiled = w.dim() == 5;
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0 &&
+                  (tiled ? (w.size(2) == 4 && w.size(3) == 16 && w.size(4) == 8 && w.is_contiguous())
+                         : (w.dim() == 2 && w.stride(1) == 1 && w.stride(0) % 8 == 0)),
+              "x [M, K] / w [N, K] (unit inner stride, 16-byte aligned rows) or tiled [N/16, K/32, 4, 16, 8]");
+  const int64_t M = x.size(0), N = tiled ? w.size(0) * 16 : w.size(0), K = tiled ? w.size(1) * 32 : w.size(1);
   TORCH_CHECK(M >= 1 && M <= 64 && x.size(1) == K, "skinny64: 1 <= M <= 64, x [M, K]");
   TORCH_CHECK(N < (1ll << 30) && K < (1ll << 30), "shape too large");
   TORCH_CHECK(m64_shape_ok((int)N, (int)K, glu),
@@ -97,8 +100,8 @@ std::tuple<at::Tensor, at::Tensor> skinny64(const at::Tensor& x, const at::Tenso
   auto st = cur_stream(x);
   if (glu) {
     auto m = at::empty({M, N / 2}, x.options());
-    launch_m64_gemm(cbp(x), x.stride(0), cbp(w), w.stride(0), bp(m), m.stride(0), nullptr, (int)M,
-                    (int)N, (int)K, 1, true, sq, nbp, static_cast<float>(eps), st);
+    launch_m64_gemm(cbp(x), x.stride(0), cbp(w), tiled ? K : w.stride(0), bp(m), m.stride(0), nullptr,
+                    (int)M, (int)N, (int)K, 1, true, sq, nbp, static_cast<float>(eps), tiled, st);
     return {m, at::Tensor()};
   }
   const int S = m64_splits((int)N, (int)K);
@@ -107,9 +110,9 @@ std::tuple<at::Tensor, at::Tensor> skinny64(const at::Tensor& x, const at::Tenso
   auto y = at::empty({M, N}, x.options());
   at::Tensor ws;
   if (S > 1) ws = at::empty({S, M, N}, x.options().dtype(at::kFloat));
-  launch_m64_gemm(cbp(x), x.stride(0), cbp(w), w.stride(0), bp(y), y.stride(0),
+  launch_m64_gemm(cbp(x), x.stride(0), cbp(w), tiled ? K : w.stride(0), bp(y), y.stride(0),
                   S > 1 ? ws.data_ptr<float>() : nullptr, (int)M, (int)N, (int)K, S, false, nullptr, 0,
-                  0.f, st);
+                  0.f, tiled, st);
   const bf16_t* rp = nullptr;
   int64_t ldr = 0;
   at::Tensor ssq;
@@ -141,10 +144,13 @@ std::tuple<at::Tensor, at::Tensor> skinny_fused(const at::Tensor& x, const at::T
                                                 bool glu) {
   check_bf16(x, "x");
   check_bf16(w, "w");
-  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.stride(1) == 1 && w.stride(1) == 1 &&
-                  x.stride(0) % 8 == 0 && w.stride(0) % 8 == 0,
-              "x [M, K] / w [N, K]: unit inner stride, 16-byte aligned rows");
-  const int64_t M = x.size(0), N = w.size(0), K = w.size(1);
+  // w: [N, K] row-major, or the tiled layout [N / 16, K / 32, 4, 16, 8] (skinny64.hip TW)
+  const bool tiled = w.dim() == 5;
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0 &&
+                  (tiled ? (w.size(2) == 4 && w.size(3) == 16 && w.size(4) == 8 && w.is_contiguous())
+                         : (w.dim() == 2 && w.stride(1) == 1 && w.stride(0) % 8 == 0)),
+              "x [M, K] / w [N, K] (unit inner stride, 16-byte aligned rows) or tiled [N/16, K/32, 4, 16, 8]");
+  const int64_t M = x.size(0), N = tiled ? w.size(0) * 16 : w.size(0), K = tiled ? w.size(1) * 32 : w.size(1);
   TORCH_CHECK(M >= 1 && M <= 16 && x.size(1) == K, "fused skinny: 1 <= M <= 16, x [M, K]");
   TORCH_CHECK(N < (1ll << 30) && K < (1ll << 30), "shape too large");
   check_aligned16(x, "x");
@@ -168,8 +174,8 @@ std::tuple<at::Tensor, at::Tensor> skinny_fused(const at::Tensor& x, const at::T
     TORCH_CHECK(nin && !res.has_value(), "glu: normalised input, no residual");
     TORCH_CHECK(N % 128 == 0 && M * (K + 8) * 2 <= 148 * 1024, "glu: 2F % 128 == 0, x fits LDS");
     auto m = at::empty({M, N / 2}, x.options());
-    launch_skinny_glu_normin(cbp(x), x.stride(0), cbp(w), w.stride(0), bp(m), m.stride(0), (int)M,
-                             (int)N, (int)K, fz, cur_stream(x));
+    launch_skinny_glu_normin(cbp(x), x.stride(0), cbp(w), tiled ? K : w.stride(0), bp(m), m.stride(0),
+                             (int)M, (int)N, (int)K, fz, tiled, cur_stream(x));
     return {m, at::Tensor()};
   }
   TORCH_CHECK(skinny_use_ksplit((int)N, (int)K), "fused skinny: N < 16384, N % 16 == 0, K % 1024 == 0");
@@ -185,8 +191,8 @@ std::tuple<at::Tensor, at::Tensor> skinny_fused(const at::Tensor& x, const at::T
     ssq = at::empty({16, N / 16}, x.options().dtype(at::kFloat));
     fz.ssq_out = ssq.data_ptr<float>();
   }
-  launch_skinny_ks_fused(cbp(x), x.stride(0), cbp(w), w.stride(0), bp(y), y.stride(0), (int)M,
-                         (int)N, (int)K, fz, res.has_value(), nin, cur_stream(x));
+  launch_skinny_ks_fused(cbp(x), x.stride(0), cbp(w), tiled ? K : w.stride(0), bp(y), y.stride(0),
+                         (int)M, (int)N, (int)K, fz, res.has_value(), nin, tiled, cur_stream(x));
   return {y, ssq};
 }
 

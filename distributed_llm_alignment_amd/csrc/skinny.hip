@@ -126,7 +126,8 @@ __device__ __forceinline__ void ks_rstd(const KsPart& p, const KsFuse& fz, int M
   }
 }
 
-template <bool SWIGLU, bool GLU_OUT = false, bool NORM = false, bool NTW = false, bool NPRE = false>
+template <bool SWIGLU, bool GLU_OUT = false, bool NORM = false, bool NTW = false, bool NPRE = false,
+          bool TW = false>
 __global__ __launch_bounds__(64 * kSkWaves) void skinny_gemm_kernel(
     const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ W, int64_t ldw,
     bf16_t* __restrict__ y, int64_t ldy, float* __restrict__ ws, unsigned* __restrict__ counters,
@@ -148,17 +149,20 @@ __global__ __launch_bounds__(64 * kSkWaves) void skinny_gemm_kernel(
                          : blockIdx.x * kSkCols + wave * 16;
   const int r = lane & 15, q = lane >> 4;  // fragment row (m for A, n for B), k quarter
   const bool active = n0 < N;
-  const bf16_t* wrow = W + static_cast<int64_t>(active ? n0 + r : 0) * ldw + k0 + q * 8;
+  // TW: W in the tiled layout [N/16, K/32, 4, 16, 8] (skinny64.hip): wp(k) = k-offset k of this lane
+  const bf16_t* wrow = TW ? W + static_cast<int64_t>(active ? n0 >> 4 : 0) * 16 * K + (k0 >> 5) * 512 + lane * 8
+                          : W + static_cast<int64_t>(active ? n0 + r : 0) * ldw + k0 + q * 8;
+  auto wp = [&](int kk) { return TW ? wrow + (kk >> 5) * 512 : wrow + kk; };
 
   // the first two weight chunks are in flight before x is staged (independent of LDS)
   const int nchunks = klen / kSkChunk;
   s16x8 b0[kSkUnroll], b1[kSkUnroll];
   if (active) {
 #pragma unroll
-    for (int u = 0; u < kSkUnroll; ++u) b0[u] = load_w<NTW>(wrow + u * 32);
+    for (int u = 0; u < kSkUnroll; ++u) b0[u] = load_w<NTW>(wp(u * 32));
     if (nchunks > 1) {
 #pragma unroll
-      for (int u = 0; u < kSkUnroll; ++u) b1[u] = load_w<NTW>(wrow + kSkChunk + u * 32);
+      for (int u = 0; u < kSkUnroll; ++u) b1[u] = load_w<NTW>(wp(kSkChunk + u * 32));
     }
   }
 
@@ -275,14 +279,14 @@ __global__ __launch_bounds__(64 * kSkWaves) void skinny_gemm_kernel(
       if (c + 2 < nchunks) {
 #pragma unroll
         for (int u = 0; u < kSkUnroll; ++u)
-          b0[u] = load_w<NTW>(wrow + (c + 2) * kSkChunk + u * 32);
+          b0[u] = load_w<NTW>(wp((c + 2) * kSkChunk + u * 32));
       }
       if (c + 1 < nchunks) {
         compute(b1, (c + 1) * kSkChunk);
         if (c + 3 < nchunks) {
 #pragma unroll
           for (int u = 0; u < kSkUnroll; ++u)
-            b1[u] = load_w<NTW>(wrow + (c + 3) * kSkChunk + u * 32);
+            b1[u] = load_w<NTW>(wp((c + 3) * kSkChunk + u * 32));
         }
       }
     }
@@ -458,7 +462,8 @@ constexpr int kKsChunk = 32 * kKsUnroll;
 // (larger decode batches, e.g. the reference's 64 rollouts per RLHF step on one GPU); UNR k-steps
 // per ring slot (4 at MT = 1; 2 above, which keeps the x fragments at ~110 VGPRs for MT = 4, four
 // waves per SIMD).
-template <int DEPTH, bool NT, bool GLU, int MT = 1, int UNR = kKsUnroll, bool RES = false, bool NIN = false>
+template <int DEPTH, bool NT, bool GLU, int MT = 1, int UNR = kKsUnroll, bool RES = false, bool NIN = false,
+          bool TW = false>
 __global__ __launch_bounds__(512) void skinny_ksplit_kernel(
     const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ W, int64_t ldw,
     bf16_t* __restrict__ y, int64_t ldy, int M, int N, int K, KsFuse fz = KsFuse{}) {
@@ -474,7 +479,9 @@ __global__ __launch_bounds__(512) void skinny_ksplit_kernel(
   const int kw = GLU ? K >> 2 : K >> 3;
   const int k0 = (GLU ? (wave & 3) : wave) * kw;
   const int nchunks = kw / CH;
-  const bf16_t* wrow = W + static_cast<int64_t>(n0 + r) * ldw + k0 + q * 8;
+  // TW: tiled weight layout (see skinny_gemm_kernel)
+  const bf16_t* wrow = TW ? W + static_cast<int64_t>(n0 >> 4) * 16 * K + (k0 >> 5) * 512 + lane * 8
+                          : W + static_cast<int64_t>(n0 + r) * ldw + k0 + q * 8;
   bool arow[MT];
   const bf16_t* xrow[MT];
 #pragma unroll
@@ -486,7 +493,7 @@ __global__ __launch_bounds__(512) void skinny_ksplit_kernel(
   s16x8 b[DEPTH][UNR], a[DEPTH][UNR][MT];
   auto load = [&](int j, int c) {
 #pragma unroll
-    for (int u = 0; u < UNR; ++u) b[j][u] = load_w<NT>(wrow + c * CH + u * 32);
+    for (int u = 0; u < UNR; ++u) b[j][u] = load_w<NT>(TW ? wrow + (c * UNR + u) * 512 : wrow + c * CH + u * 32);
 #pragma unroll
     for (int u = 0; u < UNR; ++u)
 #pragma unroll
@@ -566,16 +573,17 @@ __global__ __launch_bounds__(512) void skinny_ksplit_kernel(
 // fused decode-layer launches (KsFuse): the residual-producing projection and the
 // norm-consuming qkv projection on the in-workgroup split-K kernel, the gate|up GLU on the LDS
 // kernel. M <= 16.
-void launch_skinny_ks_fused(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
-                            int64_t ldy, int M, int N, int K, const KsFuse& fz, bool res, bool nin,
-                            hipStream_t st) {
+template <bool TW>
+static void launch_ks_fused_t(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
+                              int64_t ldy, int M, int N, int K, const KsFuse& fz, bool res, bool nin,
+                              hipStream_t st) {
   static const int deep_k = [] {
     const char* e = getenv("DLA_SKINNY_DEEP_K");
     return e ? atoi(e) : 8192;
   }();
   const int nb = N / 16;
   const bool deep = K >= deep_k;
-#define DLA_KSF(D, R, NI) skinny_ksplit_kernel<D, false, false, 1, kKsUnroll, R, NI><<<nb, 512, 0, st>>>(x, ldx, W, ldw, y, ldy, M, N, K, fz)
+#define DLA_KSF(D, R, NI) skinny_ksplit_kernel<D, false, false, 1, kKsUnroll, R, NI, TW><<<nb, 512, 0, st>>>(x, ldx, W, ldw, y, ldy, M, N, K, fz)
   if (res && nin) {
     if (deep) DLA_KSF(4, true, true); else DLA_KSF(2, true, true);
   } else if (res) {
@@ -588,18 +596,34 @@ void launch_skinny_ks_fused(const bf16_t* x, int64_t ldx, const bf16_t* W, int64
 #undef DLA_KSF
 }
 
-void launch_skinny_glu_normin(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
-                              int64_t ldy, int M, int N, int K, const KsFuse& fz, hipStream_t st) {
+// tiled: W in the tiled layout (ldw unused)
+void launch_skinny_ks_fused(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
+                            int64_t ldy, int M, int N, int K, const KsFuse& fz, bool res, bool nin,
+                            bool tiled, hipStream_t st) {
+  if (tiled) launch_ks_fused_t<true>(x, ldx, W, ldw, y, ldy, M, N, K, fz, res, nin, st);
+  else launch_ks_fused_t<false>(x, ldx, W, ldw, y, ldy, M, N, K, fz, res, nin, st);
+}
+
+template <bool TW>
+static void launch_glu_normin_t(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
+                                int64_t ldy, int M, int N, int K, const KsFuse& fz, hipStream_t st) {
   static bool attr_set = [] {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_gemm_kernel<false, true, false, false, true>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_gemm_kernel<false, true, false, false, true, TW>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
     (void)hipGetLastError();
     return true;
   }();
   (void)attr_set;
   dim3 g2(N / 2 / 64, 1);
-  skinny_gemm_kernel<false, true, false, false, true><<<g2, 64 * kSkWaves, skinny_lds_bytes(M, K), st>>>(
+  skinny_gemm_kernel<false, true, false, false, true, TW><<<g2, 64 * kSkWaves, skinny_lds_bytes(M, K), st>>>(
       x, ldx, W, ldw, y, ldy, nullptr, nullptr, M, N, K, K, SkNorm{}, fz);
+}
+
+void launch_skinny_glu_normin(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
+                              int64_t ldy, int M, int N, int K, const KsFuse& fz, bool tiled,
+                              hipStream_t st) {
+  if (tiled) launch_glu_normin_t<true>(x, ldx, W, ldw, y, ldy, M, N, K, fz, st);
+  else launch_glu_normin_t<false>(x, ldx, W, ldw, y, ldy, M, N, K, fz, st);
 }
 
 bool skinny_use_ksplit(int N, int K) {

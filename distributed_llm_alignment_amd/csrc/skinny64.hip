@@ -39,22 +39,11 @@ __device__ __forceinline__ f32x4 mfma16(s16x8 a, s16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
-template <bool NT>
-__device__ __forceinline__ s16x8 load_w(const bf16_t* p) {
-  if constexpr (NT)
-    return __builtin_bit_cast(s16x8, __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(p)));
-  else
-    return __builtin_bit_cast(s16x8, load_bf16x8(p));
-}
-
-bool m64_nt() {
-  static const bool nt = [] {
-    const char* e = getenv("DLA_SKINNY_NT");
-    return e != nullptr && atoi(e) != 0;
-  }();
-  return nt;
-}
-
+// Weight layouts: row-major W [N, K], or TW (tiled, ops/decode.py `tiled_weight`):
+// Wt[N / 16][K / 32][4][16][8] with Wt[t][kk][q][r][e] = W[16 t + r][32 kk + 8 q + e], i.e. the
+// 16-byte pieces in the order lane (r = lane & 15, q = lane >> 4) of an MFMA B fragment reads them:
+// one weight load instruction is 1 KB contiguous and a wave's 256-deep chunk 8 KB, instead of 16
+// rows x 64 B at an 8 KB (K = 4096) stride.
 }  // namespace
 
 // grid (N / 16 NW [GLU: F / 8 NW], S), 64 NW threads. LDS: 2 x 16 MT x kM64Ld bf16.
@@ -62,7 +51,7 @@ bool m64_nt() {
 // from ssq_in (the producer's row partial sums, [M][nbp]) when NIN, else 1; gate / up are
 // rounded to bf16 before SwiGLU exactly as the unfused GEMM + swiglu pair.
 // Otherwise S == 1 writes y = bf16(x W^T); S > 1 writes fp32 slab ws[s][m][n].
-template <int MT, bool GLU, bool NIN, bool NT, int DEPTH, int NW = kM64Waves>
+template <int MT, bool GLU, bool NIN, bool TW, int DEPTH, int NW = kM64Waves>
 __global__ __launch_bounds__(64 * NW) void m64_gemm_kernel(
     const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ W, int64_t ldw,
     bf16_t* __restrict__ y, int64_t ldy, float* __restrict__ ws, int M, int N, int K, int kc,
@@ -82,7 +71,8 @@ __global__ __launch_bounds__(64 * NW) void m64_gemm_kernel(
   const int s = blockIdx.y;
   const int k0 = s * kc;
   const int nch = kc / kM64Ck;
-  const bf16_t* wrow = W + static_cast<int64_t>(n0 + r) * ldw + k0 + q * 8;
+  const bf16_t* wrow = TW ? W + static_cast<int64_t>(n0 >> 4) * 16 * K + (k0 >> 5) * 512 + lane * 8
+                         : W + static_cast<int64_t>(n0 + r) * ldw + k0 + q * 8;
 
   // NIN: this row's producer partials, reduced in the epilogue (thread m < M holds row m)
   float pv[kM64MaxNbp];
@@ -109,7 +99,8 @@ __global__ __launch_bounds__(64 * NW) void m64_gemm_kernel(
       if (m < M) xr[j][t] = load_bf16x8(x + static_cast<int64_t>(m) * ldx + k0 + c * kM64Ck + xc);
     }
 #pragma unroll
-    for (int u = 0; u < kM64Steps; ++u) b[j][u] = load_w<NT>(wrow + c * kM64Ck + u * 32);
+    for (int u = 0; u < kM64Steps; ++u)
+      b[j][u] = __builtin_bit_cast(s16x8, load_bf16x8(TW ? wrow + (c * kM64Steps + u) * 512 : wrow + c * kM64Ck + u * 32));
   };
   auto xstore = [&](auto J, int slot) {
     constexpr int j = decltype(J)::value;
@@ -212,8 +203,7 @@ __global__ __launch_bounds__(64 * NW) void m64_gemm_kernel(
     for (int i = 0; i < 4; ++i) {
       const int m = 16 * t + 4 * q + i;
       if (m < M) {
-        if constexpr (NT) __builtin_nontemporal_store(acc[t][i], slab + static_cast<int64_t>(m) * N + n);
-        else slab[static_cast<int64_t>(m) * N + n] = acc[t][i];
+        slab[static_cast<int64_t>(m) * N + n] = acc[t][i];
       }
     }
 }
@@ -298,54 +288,54 @@ size_t m64_lds_bytes(int M) {
   return static_cast<size_t>(2 * 16 * mt * kM64Ld) * sizeof(bf16_t);
 }
 
-template <int MT, bool GLU, bool NIN, bool NT, int NW>
+template <int MT, bool GLU, bool NIN, bool TW, int NW>
 static void m64_launch_w(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
                          int64_t ldy, float* ws, int M, int N, int K, int S, const float* ssq_in,
                          int nbp, float eps, hipStream_t st) {
   const size_t lds = static_cast<size_t>(2 * 16 * MT * kM64Ld) * sizeof(bf16_t);
   static bool attr = [] {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&m64_gemm_kernel<MT, GLU, NIN, NT, 2, NW>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&m64_gemm_kernel<MT, GLU, NIN, TW, 2, NW>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
     (void)hipGetLastError();
     return true;
   }();
   (void)attr;
   dim3 grid(GLU ? N / 2 / (8 * NW) : N / (16 * NW), S);
-  m64_gemm_kernel<MT, GLU, NIN, NT, 2, NW><<<grid, 64 * NW, lds, st>>>(x, ldx, W, ldw, y, ldy, ws, M, N,
+  m64_gemm_kernel<MT, GLU, NIN, TW, 2, NW><<<grid, 64 * NW, lds, st>>>(x, ldx, W, ldw, y, ldy, ws, M, N,
                                                                        K, K / S, ssq_in, nbp, eps);
 }
 
 // NW = 8 waves per workgroup (gate|up: 64 features per workgroup). 4 waves (448 gate|up
 // workgroups at Llama-3-8B, two per CU) measured 55.0 vs 53.2 us: README "Tried".
-template <int MT, bool GLU, bool NIN, bool NT>
+template <int MT, bool GLU, bool NIN, bool TW>
 static void m64_launch(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
                        int64_t ldy, float* ws, int M, int N, int K, int S, const float* ssq_in,
                        int nbp, float eps, hipStream_t st) {
-  m64_launch_w<MT, GLU, NIN, NT, kM64Waves>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, ssq_in, nbp, eps, st);
+  m64_launch_w<MT, GLU, NIN, TW, kM64Waves>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, ssq_in, nbp, eps, st);
 }
 
-template <int MT, bool NT>
+template <int MT, bool TW>
 static void m64_dispatch(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
                          int64_t ldy, float* ws, int M, int N, int K, int S, bool glu,
                          const float* ssq_in, int nbp, float eps, hipStream_t st) {
   if (glu && ssq_in)
-    m64_launch<MT, true, true, NT>(x, ldx, W, ldw, y, ldy, ws, M, N, K, 1, ssq_in, nbp, eps, st);
+    m64_launch<MT, true, true, TW>(x, ldx, W, ldw, y, ldy, ws, M, N, K, 1, ssq_in, nbp, eps, st);
   else if (glu)
-    m64_launch<MT, true, false, NT>(x, ldx, W, ldw, y, ldy, ws, M, N, K, 1, nullptr, 0, 0.f, st);
+    m64_launch<MT, true, false, TW>(x, ldx, W, ldw, y, ldy, ws, M, N, K, 1, nullptr, 0, 0.f, st);
   else
-    m64_launch<MT, false, false, NT>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, nullptr, 0, 0.f, st);
+    m64_launch<MT, false, false, TW>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, nullptr, 0, 0.f, st);
 }
 
-// GEMM (S > 1: fp32 slabs into ws) -- the reduce is a separate launch (launch_m64_reduce)
+// GEMM (S > 1: fp32 slabs into ws) -- the reduce is a separate launch (launch_m64_reduce).
+// tiled: W is the tiled layout (ldw unused).
 void launch_m64_gemm(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
                      int64_t ldy, float* ws, int M, int N, int K, int S, bool glu,
-                     const float* ssq_in, int nbp, float eps, hipStream_t st) {
-  const bool nt = m64_nt();
+                     const float* ssq_in, int nbp, float eps, bool tiled, hipStream_t st) {
   if (M <= 32) {
-    if (nt) m64_dispatch<2, true>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, glu, ssq_in, nbp, eps, st);
+    if (tiled) m64_dispatch<2, true>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, glu, ssq_in, nbp, eps, st);
     else m64_dispatch<2, false>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, glu, ssq_in, nbp, eps, st);
   } else {
-    if (nt) m64_dispatch<4, true>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, glu, ssq_in, nbp, eps, st);
+    if (tiled) m64_dispatch<4, true>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, glu, ssq_in, nbp, eps, st);
     else m64_dispatch<4, false>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, glu, ssq_in, nbp, eps, st);
   }
 }

@@ -266,33 +266,80 @@ def _wkey(t: torch.Tensor):
     return (t.data_ptr(), t._version, ep[0] if ep is not None else 0)
 
 
-def folded_weight(w: torch.Tensor, norm_w: torch.Tensor) -> torch.Tensor:
-    """Cached W o norm_w (the RMSNorm weight folded into W's input columns), refreshed IN PLACE
-    when either tensor changed (version counter / engine weight epoch): a captured decode graph
-    keeps reading the same storage. Never re-made inside a capture (call
+# The fused decode layer's kernels read their weights in a tiled layout (csrc/skinny64.hip TW:
+# [N/16, K/32, 4, 16, 8], each weight load 1 KB contiguous instead of 16 rows x 64 B at a K-row
+# stride). DLA_DECODE_TILED: 1 = the folded qkv / gate|up copies (which exist anyway) are kept
+# tiled; 2 (default) = also tiled copies of o / down (one extra copy of those two weights, ~4.8 GB
+# for Llama-3-8B, made the first time the fused decode layer runs); 0 = row-major.
+DECODE_TILED = int(os.environ.get("DLA_DECODE_TILED", "2"))
+
+
+def _tile_into(t: torch.Tensor, w: torch.Tensor) -> None:
+    N, K = w.shape
+    t.copy_(w.view(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4))
+
+
+def _cached(w: torch.Tensor, attr: str, key, make) -> torch.Tensor:
+    """Weight-derived cache on `w` (attr), refreshed IN PLACE when `key` moved: a captured decode
+    graph keeps reading the same storage. Never made inside a capture (call
     `refresh_folded_weights` before capturing / replaying)."""
-    key = (_wkey(w), _wkey(norm_w))
-    c = getattr(w, "_dla_fold", None)
+    c = getattr(w, attr, None)
     if c is None or c[0] != key:
         if torch.cuda.is_current_stream_capturing():
             if c is None:
-                raise RuntimeError("folded decode weight first requested inside a graph capture")
+                raise RuntimeError("derived decode weight first requested inside a graph capture")
             return c[1]
         with torch.no_grad():
-            t = c[1] if c is not None else torch.empty_like(w, memory_format=torch.contiguous_format)
-            torch.mul(w.detach(), norm_w.detach().view(1, -1), out=t)
+            t = make(c[1] if c is not None else None)
         c = (key, t)
-        w._dla_fold = c
+        setattr(w, attr, c)
     return c[1]
 
 
+def folded_weight(w: torch.Tensor, norm_w: torch.Tensor, tiled: bool = False) -> torch.Tensor:
+    """Cached W o norm_w (the RMSNorm weight folded into W's input columns; `tiled`: in the
+    skinny64 tiled layout), refreshed in place when either tensor changed (version counter /
+    engine weight epoch)."""
+    N, K = w.shape
+
+    def make(t):
+        if not tiled:
+            t = t if t is not None else torch.empty_like(w, memory_format=torch.contiguous_format)
+            torch.mul(w.detach(), norm_w.detach().view(1, -1), out=t)
+            return t
+        t = t if t is not None else torch.empty((N // 16, K // 32, 4, 16, 8), dtype=w.dtype, device=w.device)
+        _tile_into(t, w.detach() * norm_w.detach().view(1, -1))
+        return t
+
+    return _cached(w, "_dla_fold_t" if tiled else "_dla_fold", (_wkey(w), _wkey(norm_w)), make)
+
+
+def tiled_weight(w: torch.Tensor) -> torch.Tensor:
+    """Cached copy of W in the skinny64 tiled layout (refreshed like `folded_weight`)."""
+    N, K = w.shape
+
+    def make(t):
+        t = t if t is not None else torch.empty((N // 16, K // 32, 4, 16, 8), dtype=w.dtype, device=w.device)
+        _tile_into(t, w.detach())
+        return t
+
+    return _cached(w, "_dla_tile", _wkey(w), make)
+
+
 def refresh_folded_weights(model) -> None:
-    """Bring every folded decode weight of `model` up to date (before a graph replay)."""
+    """Bring every derived decode weight of `model` up to date (before a graph replay)."""
     for layer in getattr(model, "layers", []):
         for w, nw in ((getattr(layer.attn, "qkv_proj", None), getattr(layer, "ln1_w", None)),
                       (getattr(layer.mlp, "up_proj", None), getattr(layer, "ln2_w", None))):
-            if w is not None and nw is not None and getattr(w, "_dla_fold", None) is not None:
+            if w is None or nw is None:
+                continue
+            if getattr(w, "_dla_fold", None) is not None:
                 folded_weight(w, nw)
+            if getattr(w, "_dla_fold_t", None) is not None:
+                folded_weight(w, nw, tiled=True)
+        for w in (getattr(layer.attn, "o_proj", None), getattr(layer.mlp, "down_proj", None)):
+            if w is not None and getattr(w, "_dla_tile", None) is not None:
+                tiled_weight(w)
 
 
 def _fused_op(rows: int):
@@ -302,7 +349,8 @@ def _fused_op(rows: int):
 def skinny_residual(x: torch.Tensor, w: torch.Tensor, res: torch.Tensor):
     """s = res + x @ w^T (bf16 rounding as linear + add), plus the row-norm partials of s."""
     x2 = _rows(x)
-    s, ssq = _fused_op(x2.shape[0])(x2, w, _rows(res), None, 0.0, False)
+    wk = tiled_weight(w) if DECODE_TILED >= 2 else w
+    s, ssq = _fused_op(x2.shape[0])(x2, wk, _rows(res), None, 0.0, False)
     return s.view(*res.shape[:-1], w.shape[0]), ssq
 
 
@@ -310,12 +358,14 @@ def skinny_normed(s: torch.Tensor, ssq: torch.Tensor, norm_w: torch.Tensor, eps:
                   w: torch.Tensor, glu: bool = False) -> torch.Tensor:
     """RMSNorm(s) * norm_w @ w^T from the producer's partials (glu: gate|up + SwiGLU epilogue)."""
     s2 = _rows(s)
-    y, _ = _fused_op(s2.shape[0])(s2, folded_weight(w, norm_w), None, ssq, float(eps), bool(glu))
+    wf = folded_weight(w, norm_w, tiled=DECODE_TILED >= 1)
+    y, _ = _fused_op(s2.shape[0])(s2, wf, None, ssq, float(eps), bool(glu))
     return y.view(*s.shape[:-1], y.shape[-1])
 
 
-def skinny64_linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-    """y = x @ w^T at 17..64 rows on csrc/skinny64.hip (tests / A/B)."""
+def skinny64_linear(x: torch.Tensor, w: torch.Tensor, tiled: bool = False) -> torch.Tensor:
+    """y = x @ w^T at 17..64 rows on csrc/skinny64.hip (tests / A/B; `tiled`: through the
+    tiled-layout copy of w)."""
     x2 = _rows(x)
-    y, _ = _ext.require().skinny64(x2, w, None, None, 0.0, False)
+    y, _ = _ext.require().skinny64(x2, tiled_weight(w) if tiled else w, None, None, 0.0, False)
     return y.view(*x.shape[:-1], w.shape[0])

@@ -280,6 +280,7 @@ def invalidate_weight_caches(model) -> None:
     for p in model.parameters():
         for k in ("_dla_wt_ver", "_dla_fp8"):
             p.__dict__.pop(k, None)
-        fold = p.__dict__.get("_dla_fold")
-        if fold is not None:  # keep the buffer (a captured decode graph reads it), mark stale
-            p._dla_fold = (None, fold[1])
+        for k in ("_dla_fold", "_dla_fold_t", "_dla_tile"):  # ops.decode derived weights
+            c = p.__dict__.get(k)
+            if c is not None:  # keep the buffer (a captured decode graph reads it), mark stale
+                setattr(p, k, (None, c[1]))

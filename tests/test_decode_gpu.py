@@ -537,6 +537,16 @@ def test_fused_decode_projection_kernels_match_fp32():
     gu = h_ref @ wgu.float().t()
     m_ref = torch.nn.functional.silu(gu[:, :F]) * gu[:, F:]
     assert float((mm.float() - m_ref).norm() / m_ref.norm()) < 1e-2
+    # tiled weight layout (the default, DLA_DECODE_TILED) == row-major weights, bitwise
+    C = ops._ext.require()
+    s_rm, ssq_rm = C.skinny_fused(x, w, res, None, 0.0, False)
+    assert torch.equal(s_rm, s) and torch.equal(ssq_rm[:M], ssq[:M])  # rows >= M are not written
+    s_t, _ = C.skinny_fused(x, ops.decode.tiled_weight(w), res, None, 0.0, False)
+    assert torch.equal(s_t, s)
+    y_rm, _ = C.skinny_fused(s, ops.decode.folded_weight(wq, nw), None, ssq, 1e-5, False)
+    assert torch.equal(y_rm, y)
+    mm_rm, _ = C.skinny_fused(s, ops.decode.folded_weight(wgu, nw), None, ssq, 1e-5, True)
+    assert torch.equal(mm_rm, mm)
 
 
 @pytest.mark.parametrize("M", [17, 32, 33, 64])
@@ -556,6 +566,8 @@ def test_skinny64_kernels_match_fp32(M):
         y = ops.decode.skinny64_linear(x, w)
         assert y.shape == (M, N)
         assert rel(y, x.float() @ w.float().t()) < 5e-3, (N, K)
+        # the tiled weight layout is only a different load order: bitwise the same result
+        assert torch.equal(ops.decode.skinny64_linear(x, w, tiled=True), y), (N, K)
     H, F = 4096, 14336
     x = torch.randn(M, F, device=DEV, generator=g).to(torch.bfloat16)
     w = (torch.randn(H, F, device=DEV, generator=g) * F ** -0.5).to(torch.bfloat16)
@@ -565,6 +577,8 @@ def test_skinny64_kernels_match_fp32(M):
     s_ref = (x.float() @ w.float().t()).to(torch.bfloat16).float() + res.float()
     assert float((s.float() - s_ref).abs().max()) < 0.05
     assert torch.allclose(ssq.sum(1), (s.float() ** 2).sum(1), rtol=1e-4)
+    s_t, ssq_t = ops._ext.require().skinny64(x, ops.decode.tiled_weight(w), res, None, 0.0, False)
+    assert torch.equal(s_t, s) and torch.equal(ssq_t, ssq)
     nw = (1 + 0.1 * torch.randn(H, device=DEV, generator=g)).to(torch.bfloat16)
     h_ref = _ref_norm(s.float(), nw.float(), None, 1e-5, True)
     wq = (torch.randn(6144, H, device=DEV, generator=g) * H ** -0.5).to(torch.bfloat16)
@@ -574,3 +588,6 @@ def test_skinny64_kernels_match_fp32(M):
     mm = ops.decode.skinny_normed(s, ssq, nw, 1e-5, wgu, glu=True)
     gu = h_ref @ wgu.float().t()
     assert rel(mm, torch.nn.functional.silu(gu[:, :F]) * gu[:, F:]) < 1e-2
+    # row-major folded weight (DLA_M64_TILED=0) == the tiled default, bitwise
+    mm_rm, _ = ops._ext.require().skinny64(s, ops.decode.folded_weight(wgu, nw), None, ssq, 1e-5, True)
+    assert torch.equal(mm_rm, mm)
