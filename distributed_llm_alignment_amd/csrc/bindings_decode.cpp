@@ -51,6 +51,7 @@ void launch_skinny_glu_normin(const bf16_t*, int64_t, const bf16_t*, int64_t, bf
                               int, int, const KsFuse&, bool, hipStream_t);
 
 int m64_splits(int N, int K);
+void launch_tile_weight(const bf16_t*, int64_t, const bf16_t*, bf16_t*, int, int, hipStream_t);
 bool m64_shape_ok(int N, int K, bool glu);
 void launch_m64_gemm(const bf16_t*, int64_t, const bf16_t*, int64_t, bf16_t*, int64_t, float*, int,
                      int, int, int, bool, const float*, int, float, bool, hipStream_t);
@@ -129,6 +130,32 @@ std::tuple<at::Tensor, at::Tensor> skinny64(const at::Tensor& x, const at::Tenso
     launch_m64_reduce(ws.data_ptr<float>(), S, (int)M, (int)N, bp(y), y.stride(0), rp, ldr, sq, nbp,
                       (int)K, static_cast<float>(eps), ssq.defined() ? ssq.data_ptr<float>() : nullptr, st);
   return {y, ssq};
+}
+
+// out <- w [N, K] in the tiled decode layout [N/16, K/32, 4, 16, 8] (nw given: bf16(w * nw), the
+// RMSNorm weight folded into the input columns)
+void tile_weight(const at::Tensor& w, const c10::optional<at::Tensor>& nw, at::Tensor& out) {
+  check_bf16(w, "w");
+  check_bf16(out, "out");
+  TORCH_CHECK(w.dim() == 2 && w.stride(1) == 1 && w.stride(0) % 8 == 0, "w [N, K], unit inner stride");
+  const int64_t N = w.size(0), K = w.size(1);
+  TORCH_CHECK(N % 16 == 0 && K % 32 == 0 && N < (1ll << 30) && K < (1ll << 30), "N % 16 == 0, K % 32 == 0");
+  TORCH_CHECK(out.dim() == 5 && out.size(0) == N / 16 && out.size(1) == K / 32 && out.size(2) == 4 &&
+                  out.size(3) == 16 && out.size(4) == 8 && out.is_contiguous(),
+              "out [N/16, K/32, 4, 16, 8] contiguous");
+  check_aligned16(w, "w");
+  check_aligned16(out, "out");
+  same_device(w, out);
+  const bf16_t* np = nullptr;
+  if (nw.has_value()) {
+    check_bf16(*nw, "nw");
+    TORCH_CHECK(nw->dim() == 1 && nw->size(0) == K && nw->is_contiguous(), "nw [K]");
+    check_aligned16(*nw, "nw");
+    same_device(w, *nw);
+    np = cbp(*nw);
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA g(w.device());
+  launch_tile_weight(cbp(w), w.stride(0), np, bp(out), (int)N, (int)K, cur_stream(w));
 }
 
 // Fused decode-layer projection (M <= 16, skinny.hip KsFuse):
@@ -513,6 +540,7 @@ TORCH_LIBRARY_FRAGMENT(dla, m) {
   m.def("skinny_glu_ks(Tensor x, Tensor w) -> Tensor");
   m.def("skinny_fused(Tensor x, Tensor w, Tensor? res, Tensor? ssq_in, float eps, bool glu) -> (Tensor, Tensor)");
   m.def("skinny64(Tensor x, Tensor w, Tensor? res, Tensor? ssq_in, float eps, bool glu) -> (Tensor, Tensor)");
+  m.def("tile_weight(Tensor w, Tensor? nw, Tensor(a!) out) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(dla, CUDA, m) {
@@ -525,4 +553,5 @@ TORCH_LIBRARY_IMPL(dla, CUDA, m) {
   m.impl("skinny_glu_ks", &dla::skinny_glu_ks);
   m.impl("skinny_fused", &dla::skinny_fused);
   m.impl("skinny64", &dla::skinny64);
+  m.impl("tile_weight", &dla::tile_weight);
 }

@@ -274,9 +274,14 @@ def _wkey(t: torch.Tensor):
 DECODE_TILED = int(os.environ.get("DLA_DECODE_TILED", "2"))
 
 
-def _tile_into(t: torch.Tensor, w: torch.Tensor) -> None:
+def _tile_into(t: torch.Tensor, w: torch.Tensor, norm_w: Optional[torch.Tensor] = None) -> None:
+    """t <- w (with norm_w: bf16(w * norm_w)) in the tiled layout: one HIP pass on the GPU."""
     N, K = w.shape
-    t.copy_(w.view(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4))
+    if _ext.use_native(w) and w.stride(-1) == 1 and w.stride(0) % 8 == 0:
+        _ext.require().tile_weight(w, norm_w.contiguous() if norm_w is not None else None, t)
+        return
+    src = w * norm_w.view(1, -1) if norm_w is not None else w
+    t.copy_(src.reshape(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4))
 
 
 def _cached(w: torch.Tensor, attr: str, key, make) -> torch.Tensor:
@@ -285,7 +290,7 @@ def _cached(w: torch.Tensor, attr: str, key, make) -> torch.Tensor:
     `refresh_folded_weights` before capturing / replaying)."""
     c = getattr(w, attr, None)
     if c is None or c[0] != key:
-        if torch.cuda.is_current_stream_capturing():
+        if w.is_cuda and torch.cuda.is_current_stream_capturing():
             if c is None:
                 raise RuntimeError("derived decode weight first requested inside a graph capture")
             return c[1]
@@ -308,7 +313,7 @@ def folded_weight(w: torch.Tensor, norm_w: torch.Tensor, tiled: bool = False) ->
             torch.mul(w.detach(), norm_w.detach().view(1, -1), out=t)
             return t
         t = t if t is not None else torch.empty((N // 16, K // 32, 4, 16, 8), dtype=w.dtype, device=w.device)
-        _tile_into(t, w.detach() * norm_w.detach().view(1, -1))
+        _tile_into(t, w.detach(), norm_w.detach())
         return t
 
     return _cached(w, "_dla_fold_t" if tiled else "_dla_fold", (_wkey(w), _wkey(norm_w)), make)

@@ -549,6 +549,23 @@ def test_fused_decode_projection_kernels_match_fp32():
     assert torch.equal(mm_rm, mm)
 
 
+def test_tile_weight_kernel_matches_permute():
+    """csrc/skinny64.hip tile_weight_kernel == the torch permute definition of the tiled layout,
+    bitwise, plain and with the RMSNorm weight folded in (torch.mul rounding)."""
+    from distributed_llm_alignment_amd import ops
+
+    g = torch.Generator(device=DEV).manual_seed(3)
+    N, K = 6144, 4096
+    w = torch.randn(N, K, device=DEV, generator=g).to(torch.bfloat16)
+    nw = (1 + 0.1 * torch.randn(K, device=DEV, generator=g)).to(torch.bfloat16)
+    for norm in (None, nw):
+        out = torch.empty((N // 16, K // 32, 4, 16, 8), dtype=torch.bfloat16, device=DEV)
+        ops._ext.require().tile_weight(w, norm, out)
+        src = w if norm is None else w * norm.view(1, -1)
+        ref = src.view(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4)
+        assert torch.equal(out, ref)
+
+
 @pytest.mark.parametrize("M", [17, 32, 33, 64])
 def test_skinny64_kernels_match_fp32(M):
     """csrc/skinny64.hip (17..64 decode rows): plain split-K GEMMs at the Llama-3-8B projection
