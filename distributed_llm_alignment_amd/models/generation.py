@@ -39,6 +39,12 @@ class KVCache:
         if self.split:  # layer-split model: each layer's K/V on that layer's device
             self.k = [torch.empty((batch, max_len, Hkv, D), device=d, dtype=dt) for d in model.layer_devices]
             self.v = [torch.empty((batch, max_len, Hkv, D), device=d, dtype=dt) for d in model.layer_devices]
+        elif KV_HEAD_MAJOR:
+            # storage [L, B, Hkv, T_max, D] (a head's keys contiguous: one 128-key decode chunk is
+            # 32 KB in one run), seen through a [L, B, T_max, Hkv, D] view: every consumer is
+            # stride-generic
+            self.k = torch.empty((L, batch, Hkv, max_len, D), device=dev, dtype=dt).transpose(2, 3)
+            self.v = torch.empty((L, batch, Hkv, max_len, D), device=dev, dtype=dt).transpose(2, 3)
         else:
             self.k = torch.empty((L, batch, max_len, Hkv, D), device=dev, dtype=dt)
             self.v = torch.empty((L, batch, max_len, Hkv, D), device=dev, dtype=dt)
@@ -261,6 +267,8 @@ GRAPH_REUSE = os.environ.get("DLA_GRAPH_REUSE", "1") != "0"
 FUSED_DECODE_ROPE = os.environ.get("DLA_FUSED_DECODE_ROPE", "1") != "0"
 GRAPH_REUSE_MAX_BYTES = int(float(os.environ.get("DLA_GRAPH_REUSE_MAX_GB", "24")) * 2 ** 30)
 PROMPT_BUCKET = 64
+# KV cache storage head-major ([L, B, Hkv, T_max, D] behind the usual view), A/B: DLA_KV_HEAD_MAJOR
+KV_HEAD_MAJOR = os.environ.get("DLA_KV_HEAD_MAJOR", "0") != "0"
 _GRAPH_SLOT: dict = {}  # id(model) -> (weakref(model), key, cache, decode graph)
 
 
