@@ -51,7 +51,9 @@ void launch_skinny_glu_normin(const bf16_t*, int64_t, const bf16_t*, int64_t, bf
                               int, int, const KsFuse&, bool, hipStream_t);
 
 int m64_splits(int N, int K);
-void launch_tile_weight(const bf16_t*, int64_t, const bf16_t*, bf16_t*, int, int, hipStream_t);
+void launch_tile_weight(const bf16_t*, int64_t, const bf16_t*, bf16_t*, int, int, bool, hipStream_t);
+void launch_skinny_glu_il(const bf16_t*, int64_t, const bf16_t*, bf16_t*, int64_t, int, int, int,
+                          const KsFuse&, hipStream_t);
 bool m64_shape_ok(int N, int K, bool glu);
 void launch_m64_gemm(const bf16_t*, int64_t, const bf16_t*, int64_t, bf16_t*, int64_t, float*, int,
                      int, int, int, bool, const float*, int, float, bool, hipStream_t);
@@ -134,12 +136,13 @@ std::tuple<at::Tensor, at::Tensor> skinny64(const at::Tensor& x, const at::Tenso
 
 // out <- w [N, K] in the tiled decode layout [N/16, K/32, 4, 16, 8] (nw given: bf16(w * nw), the
 // RMSNorm weight folded into the input columns)
-void tile_weight(const at::Tensor& w, const c10::optional<at::Tensor>& nw, at::Tensor& out) {
+void tile_weight(const at::Tensor& w, const c10::optional<at::Tensor>& nw, at::Tensor& out, bool glu_il) {
   check_bf16(w, "w");
   check_bf16(out, "out");
   TORCH_CHECK(w.dim() == 2 && w.stride(1) == 1 && w.stride(0) % 8 == 0, "w [N, K], unit inner stride");
   const int64_t N = w.size(0), K = w.size(1);
   TORCH_CHECK(N % 16 == 0 && K % 32 == 0 && N < (1ll << 30) && K < (1ll << 30), "N % 16 == 0, K % 32 == 0");
+  TORCH_CHECK(!glu_il || N % 32 == 0, "glu_il: N = 2F, F % 16 == 0");
   TORCH_CHECK(out.dim() == 5 && out.size(0) == N / 16 && out.size(1) == K / 32 && out.size(2) == 4 &&
                   out.size(3) == 16 && out.size(4) == 8 && out.is_contiguous(),
               "out [N/16, K/32, 4, 16, 8] contiguous");
@@ -155,7 +158,38 @@ void tile_weight(const at::Tensor& w, const c10::optional<at::Tensor>& nw, at::T
     np = cbp(*nw);
   }
   c10::hip::HIPGuardMasqueradingAsCUDA g(w.device());
-  launch_tile_weight(cbp(w), w.stride(0), np, bp(out), (int)N, (int)K, cur_stream(w));
+  launch_tile_weight(cbp(w), w.stride(0), np, bp(out), (int)N, (int)K, glu_il, cur_stream(w));
+}
+
+// Decode gate|up + SwiGLU at M <= 16 over the interleaved tiled weight (tile_weight glu_il, norm
+// folded) from the producer's row-norm partials: [M, F] = silu(rstd * g) * (rstd * u)
+at::Tensor skinny_glu_il(const at::Tensor& x, const at::Tensor& wt, const at::Tensor& ssq_in, double eps) {
+  check_bf16(x, "x");
+  check_bf16(wt, "wt");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0, "x [M, K]");
+  TORCH_CHECK(wt.dim() == 5 && wt.size(2) == 4 && wt.size(3) == 16 && wt.size(4) == 8 && wt.is_contiguous(),
+              "wt [2F/16, K/32, 4, 16, 8] contiguous");
+  const int64_t M = x.size(0), N = wt.size(0) * 16, K = wt.size(1) * 32;
+  TORCH_CHECK(M >= 1 && M <= 16 && x.size(1) == K, "skinny_glu_il: 1 <= M <= 16, x [M, K]");
+  TORCH_CHECK(K % 512 == 0 && N < (1ll << 30) && K < (1ll << 30) && M * (K + 8) * 2 <= 148 * 1024,
+              "K % 512 == 0, x fits LDS");
+  check_cuda(ssq_in, "ssq_in");
+  TORCH_CHECK(ssq_in.scalar_type() == at::kFloat && ssq_in.dim() == 2 && ssq_in.size(0) == 16 &&
+                  ssq_in.is_contiguous() && ssq_in.size(1) >= 1 && ssq_in.size(1) <= 512,
+              "ssq_in fp32 [16, nbp <= 512] contiguous");
+  check_aligned16(x, "x");
+  check_aligned16(wt, "wt");
+  same_device(x, wt);
+  same_device(x, ssq_in);
+  KsFuse fz{};
+  fz.ssq_in = ssq_in.data_ptr<float>();
+  fz.nbp = static_cast<int>(ssq_in.size(1));
+  fz.eps = static_cast<float>(eps);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  auto m = at::empty({M, N / 2}, x.options());
+  launch_skinny_glu_il(cbp(x), x.stride(0), cbp(wt), bp(m), m.stride(0), (int)M, (int)N, (int)K, fz,
+                       cur_stream(x));
+  return m;
 }
 
 // Fused decode-layer projection (M <= 16, skinny.hip KsFuse):
@@ -540,7 +574,8 @@ TORCH_LIBRARY_FRAGMENT(dla, m) {
   m.def("skinny_glu_ks(Tensor x, Tensor w) -> Tensor");
   m.def("skinny_fused(Tensor x, Tensor w, Tensor? res, Tensor? ssq_in, float eps, bool glu) -> (Tensor, Tensor)");
   m.def("skinny64(Tensor x, Tensor w, Tensor? res, Tensor? ssq_in, float eps, bool glu) -> (Tensor, Tensor)");
-  m.def("tile_weight(Tensor w, Tensor? nw, Tensor(a!) out) -> ()");
+  m.def("tile_weight(Tensor w, Tensor? nw, Tensor(a!) out, bool glu_il=False) -> ()");
+  m.def("skinny_glu_il(Tensor x, Tensor wt, Tensor ssq_in, float eps) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(dla, CUDA, m) {
@@ -554,4 +589,5 @@ TORCH_LIBRARY_IMPL(dla, CUDA, m) {
   m.impl("skinny_fused", &dla::skinny_fused);
   m.impl("skinny64", &dla::skinny64);
   m.impl("tile_weight", &dla::tile_weight);
+  m.impl("skinny_glu_il", &dla::skinny_glu_il);
 }

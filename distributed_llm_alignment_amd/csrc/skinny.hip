@@ -626,6 +626,162 @@ void launch_skinny_glu_normin(const bf16_t* x, int64_t ldx, const bf16_t* W, int
   else launch_glu_normin_t<false>(x, ldx, W, ldw, y, ldy, M, N, K, fz, st);
 }
 
+// Decode gate|up (M <= 16) over an INTERLEAVED tiled weight (ops/decode.py `glu_weight`): tile t
+// (16 rows) holds gate rows 8t .. 8t+7 (r < 8) and the matching up rows F + 8t .. (r >= 8), the RMSNorm
+// weight folded in. One wave per tile, so a lane's gate and up sums meet by one lane swap
+// (lane ^ 8) -- no LDS exchange -- and the workgroup size is free: 7 waves give exactly 256
+// workgroups at Llama-3-8B (F = 14336: 1792 tiles), where the 8-wave gate|up kernel
+// (skinny_gemm_kernel GLU_OUT) runs 224 and leaves 32 CUs idle. Same K order, rstd and bf16
+// rounding as that kernel: bitwise the same output.
+template <int DEPTH>
+__global__ __launch_bounds__(512) void skinny_glu_il_kernel(const bf16_t* __restrict__ x, int64_t ldx,
+                                                           const bf16_t* __restrict__ Wt,
+                                                           bf16_t* __restrict__ y, int64_t ldy, int M,
+                                                           int ntiles, int K, KsFuse fz) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t xs[];
+  __shared__ float rstd_s[16];
+  const int nwv = blockDim.x >> 6;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = lane & 15, q = lane >> 4;
+  const int t = blockIdx.x * nwv + wave;
+  const bool active = t < ntiles;
+  const int ldl = K + 8;
+  const bf16_t* wrow = Wt + static_cast<int64_t>(active ? t : 0) * 16 * K + lane * 8;
+  const int nchunks = K / kSkChunk;
+  // DEPTH chunks of kSkUnroll 1 KB wave loads in flight (a ring of register sets)
+  s16x8 b[DEPTH][kSkUnroll];
+  if (active) {
+#pragma unroll
+    for (int j = 0; j < DEPTH; ++j)
+      if (j < nchunks) {
+#pragma unroll
+        for (int u = 0; u < kSkUnroll; ++u)
+          b[j][u] = __builtin_bit_cast(s16x8, load_bf16x8(wrow + (j * kSkUnroll + u) * 512));
+      }
+  }
+  // this wave's rows' norm partials (rows wave, wave + nwv, ...: 4 cover M <= 16 at >= 4 waves),
+  // reduced after the main loop
+  float pv[4][8];
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const int m = wave + rr * nwv;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int i = lane + 64 * j;
+      pv[rr][j] = (m < M && i < fz.nbp) ? fz.ssq_in[m * fz.nbp + i] : 0.f;
+    }
+  }
+  // stage x [M, K] into LDS, 4 independent 16-byte loads per thread per pass
+  const int vecs = K >> 3, total = M * vecs, nthr = blockDim.x;
+  for (int base = 0; base < total; base += 4 * nthr) {
+    bf16x8 v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = base + j * nthr + threadIdx.x;
+      if (i < total) {
+        const int m = i / vecs, c = (i - m * vecs) << 3;
+        v[j] = load_bf16x8(x + m * ldx + c);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = base + j * nthr + threadIdx.x;
+      if (i < total) {
+        const int m = i / vecs, c = (i - m * vecs) << 3;
+        store_bf16x8(xs + m * ldl + c, v[j]);
+      }
+    }
+  }
+  __syncthreads();
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (active) {
+    const bf16_t* xrow = xs + r * ldl + q * 8;
+    const bool arow = r < M;
+    auto compute = [&](const s16x8* b, int kk) {
+#pragma unroll
+      for (int u = 0; u < kSkUnroll; ++u) {
+        s16x8 a = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (arow) a = __builtin_bit_cast(s16x8, load_bf16x8(xrow + kk + u * 32));
+        acc = mfma16(a, b[u], acc);
+      }
+    };
+    for (int c0 = 0; c0 < nchunks; c0 += DEPTH) {
+#pragma unroll
+      for (int j = 0; j < DEPTH; ++j) {
+        const int c = c0 + j;
+        if (c < nchunks) {
+          compute(b[j], c * kSkChunk);
+          if (c + DEPTH < nchunks) {
+#pragma unroll
+            for (int u = 0; u < kSkUnroll; ++u)
+              b[j][u] = __builtin_bit_cast(s16x8, load_bf16x8(wrow + ((c + DEPTH) * kSkUnroll + u) * 512));
+          }
+        }
+      }
+    }
+  }
+  // rstd per row: in-lane sum in order, then the butterfly (as ks_rstd)
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    const int m = wave + rr * nwv;
+    float tt = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) tt += pv[rr][j];
+    tt = wave_sum(tt);
+    if (lane == 0 && m < M && m < 16) rstd_s[m] = rsqrtf(tt / static_cast<float>(K) + fz.eps);
+  }
+  __syncthreads();
+  if (!active) return;
+  // lane holds C[m = 4q + i][row r of the tile]: gate (r < 8) and up (r >= 8) of feature 8t + (r & 7)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = 4 * q + i;
+    const float v = bf2f(f2bf(acc[i] * (m < M ? rstd_s[m] : 0.f)));
+    const float o = __shfl_xor(v, 8, 64);
+    if (r < 8 && m < M) y[m * ldy + 8 * t + r] = f2bf(silu_sk(v) * o);
+  }
+}
+
+// gate|up over the interleaved tiled weight (2F rows -> [M, F]); waves per workgroup: the largest
+// of 8..4 dividing the tile count with >= 256 workgroups, else 8
+template <int DEPTH>
+static void launch_glu_il_d(const bf16_t* x, int64_t ldx, const bf16_t* Wt, bf16_t* y, int64_t ldy, int M,
+                            int ntiles, int K, const KsFuse& fz, int w, hipStream_t st) {
+  static bool attr_set = [] {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_glu_il_kernel<DEPTH>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+    (void)hipGetLastError();
+    return true;
+  }();
+  (void)attr_set;
+  skinny_glu_il_kernel<DEPTH><<<(ntiles + w - 1) / w, 64 * w, skinny_lds_bytes(M, K), st>>>(x, ldx, Wt, y, ldy,
+                                                                                          M, ntiles, K, fz);
+}
+
+void launch_skinny_glu_il(const bf16_t* x, int64_t ldx, const bf16_t* Wt, bf16_t* y, int64_t ldy, int M,
+                          int N, int K, const KsFuse& fz, hipStream_t st) {
+  // DLA_GLU_IL_DEPTH (2, 3 or 4) and DLA_GLU_IL_WAVES (0 = auto) for A/B runs
+  static const int depth = [] {
+    const char* e = getenv("DLA_GLU_IL_DEPTH");
+    const int d = e ? atoi(e) : 2;
+    return d < 2 ? 2 : (d > 4 ? 4 : d);
+  }();
+  static const int waves = [] {
+    const char* e = getenv("DLA_GLU_IL_WAVES");
+    const int v = e ? atoi(e) : 0;
+    return (v >= 1 && v <= 8) ? v : 0;
+  }();
+  const int ntiles = N / 16;
+  int w = 8;
+  for (int c : {8, 7, 6, 5, 4}) {
+    if (ntiles % c == 0 && ntiles / c >= 256) { w = c; break; }
+  }
+  if (waves > 0 && M <= 4 * waves) w = waves;  // the rstd waves cover 4 rows each
+  if (depth == 4) launch_glu_il_d<4>(x, ldx, Wt, y, ldy, M, ntiles, K, fz, w, st);
+  else if (depth == 3) launch_glu_il_d<3>(x, ldx, Wt, y, ldy, M, ntiles, K, fz, w, st);
+  else launch_glu_il_d<2>(x, ldx, Wt, y, ldy, M, ntiles, K, fz, w, st);
+}
+
 bool skinny_use_ksplit(int N, int K) {
   return (N + kSkCols - 1) / kSkCols < 128 && (K % (8 * kKsChunk)) == 0 && N % 16 == 0;
 }

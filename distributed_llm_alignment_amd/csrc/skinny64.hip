@@ -370,14 +370,15 @@ void launch_m64_reduce(const float* ws, int S, int M, int N, bf16_t* y, int64_t 
     m64_reduce_s<0>(ws, S, M, N, y, ldy, nullptr, 0, nullptr, 0, 0, 0.f, nullptr, st);
 }
 
-// W [N, K] (row stride ldw) -> the tiled layout [N/16, K/32, 4, 16, 8] (see TW above), with nw
+// W [N, K] (row stride ldw) -> the tiled layout [N/16, K/32, 4, 16, 8] (see TW above; glu_il: gate /
+// up rows interleaved 8 + 8 per tile, skinny.hip skinny_glu_il_kernel), with nw
 // the RMSNorm weight folded in (bf16(W * nw), torch.mul's rounding). One 16-byte output piece per
 // thread: a wave writes 1 KB contiguous and reads 16 rows x 64 B. Rebuilt whenever the weights
 // moved (every RLHF step): one pass instead of mul + a strided permute copy.
 __global__ __launch_bounds__(256) void tile_weight_kernel(const bf16_t* __restrict__ W, int64_t ldw,
                                                           const bf16_t* __restrict__ nw,
                                                           bf16_t* __restrict__ out, int K,
-                                                          int64_t total) {
+                                                          int64_t total, int glu_f) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
   if (i >= total) return;
   const int lane = static_cast<int>(i & 63);
@@ -386,7 +387,10 @@ __global__ __launch_bounds__(256) void tile_weight_kernel(const bf16_t* __restri
   const int64_t t = blk / kb;
   const int kk = static_cast<int>(blk - t * kb);
   const int col = kk * 32 + (lane >> 4) * 8;
-  bf16x8 v = load_bf16x8(W + (t * 16 + (lane & 15)) * ldw + col);
+  // glu_f > 0 (gate|up, F = glu_f): tile t row r < 8 is gate row 8t + r, r >= 8 up row F + 8t + r - 8
+  const int r = lane & 15;
+  const int64_t row = glu_f > 0 ? (r < 8 ? 8 * t + r : glu_f + 8 * t + r - 8) : t * 16 + r;
+  bf16x8 v = load_bf16x8(W + row * ldw + col);
   if (nw != nullptr) {
     const bf16x8 g = load_bf16x8(nw + col);
 #pragma unroll
@@ -396,9 +400,10 @@ __global__ __launch_bounds__(256) void tile_weight_kernel(const bf16_t* __restri
 }
 
 void launch_tile_weight(const bf16_t* W, int64_t ldw, const bf16_t* nw, bf16_t* out, int N, int K,
-                        hipStream_t st) {
+                        bool glu_il, hipStream_t st) {
   const int64_t total = static_cast<int64_t>(N) * K / 8;
-  tile_weight_kernel<<<static_cast<unsigned>((total + 255) / 256), 256, 0, st>>>(W, ldw, nw, out, K, total);
+  tile_weight_kernel<<<static_cast<unsigned>((total + 255) / 256), 256, 0, st>>>(W, ldw, nw, out, K, total,
+                                                                                 glu_il ? N / 2 : 0);
 }
 
 }  // namespace dla

@@ -274,13 +274,32 @@ def _wkey(t: torch.Tensor):
 DECODE_TILED = int(os.environ.get("DLA_DECODE_TILED", "2"))
 
 
-def _tile_into(t: torch.Tensor, w: torch.Tensor, norm_w: Optional[torch.Tensor] = None) -> None:
-    """t <- w (with norm_w: bf16(w * norm_w)) in the tiled layout: one HIP pass on the GPU."""
+# B <= 16 gate|up, opt-in (DLA_DECODE_GLU_IL=1): one wave per 16-row tile holding 8 gate + the
+# matching 8 up rows (interleaved tiled copy), SwiGLU by a lane swap, 7 waves per workgroup =
+# exactly 256 workgroups at Llama-3-8B (csrc/skinny.hip skinny_glu_il_kernel). Bitwise equal to the
+# default 8-wave kernel (224 workgroups) and no faster: 3.72 vs 3.72 ms/token, 47.0 vs 46.6 us per
+# layer (same box), 3.69-3.70 with a 3- or 4-deep ring (DLA_GLU_IL_DEPTH) -- the gate|up stream is
+# HBM-bound at ~5 TB/s, not short of CUs.
+DECODE_GLU_IL = os.environ.get("DLA_DECODE_GLU_IL", "0") != "0"
+
+
+def _glu_interleave(w: torch.Tensor) -> torch.Tensor:
+    """[gate; up] rows (2F) -> row order gate 8t..8t+7, up 8t..8t+7 per 16-row tile."""
+    F = w.shape[0] // 2
+    return torch.stack((w[:F].reshape(F // 8, 8, -1), w[F:].reshape(F // 8, 8, -1)), 1).reshape(2 * F, -1)
+
+
+def _tile_into(t: torch.Tensor, w: torch.Tensor, norm_w: Optional[torch.Tensor] = None,
+               glu_il: bool = False) -> None:
+    """t <- w (with norm_w: bf16(w * norm_w); glu_il: gate / up rows interleaved 8 + 8 per tile) in
+    the tiled layout: one HIP pass on the GPU."""
     N, K = w.shape
     if _ext.use_native(w) and w.stride(-1) == 1 and w.stride(0) % 8 == 0:
-        _ext.require().tile_weight(w, norm_w.contiguous() if norm_w is not None else None, t)
+        _ext.require().tile_weight(w, norm_w.contiguous() if norm_w is not None else None, t, bool(glu_il))
         return
     src = w * norm_w.view(1, -1) if norm_w is not None else w
+    if glu_il:
+        src = _glu_interleave(src)
     t.copy_(src.reshape(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4))
 
 
@@ -301,10 +320,11 @@ def _cached(w: torch.Tensor, attr: str, key, make) -> torch.Tensor:
     return c[1]
 
 
-def folded_weight(w: torch.Tensor, norm_w: torch.Tensor, tiled: bool = False) -> torch.Tensor:
+def folded_weight(w: torch.Tensor, norm_w: torch.Tensor, tiled: bool = False,
+                  glu_il: bool = False) -> torch.Tensor:
     """Cached W o norm_w (the RMSNorm weight folded into W's input columns; `tiled`: in the
-    skinny64 tiled layout), refreshed in place when either tensor changed (version counter /
-    engine weight epoch)."""
+    skinny64 tiled layout, `glu_il`: tiled with gate / up rows interleaved), refreshed in place
+    when either tensor changed (version counter / engine weight epoch)."""
     N, K = w.shape
 
     def make(t):
@@ -313,10 +333,11 @@ def folded_weight(w: torch.Tensor, norm_w: torch.Tensor, tiled: bool = False) ->
             torch.mul(w.detach(), norm_w.detach().view(1, -1), out=t)
             return t
         t = t if t is not None else torch.empty((N // 16, K // 32, 4, 16, 8), dtype=w.dtype, device=w.device)
-        _tile_into(t, w.detach(), norm_w.detach())
+        _tile_into(t, w.detach(), norm_w.detach(), glu_il)
         return t
 
-    return _cached(w, "_dla_fold_t" if tiled else "_dla_fold", (_wkey(w), _wkey(norm_w)), make)
+    attr = "_dla_fold_g" if glu_il else ("_dla_fold_t" if tiled else "_dla_fold")
+    return _cached(w, attr, (_wkey(w), _wkey(norm_w)), make)
 
 
 def tiled_weight(w: torch.Tensor) -> torch.Tensor:
@@ -342,6 +363,8 @@ def refresh_folded_weights(model) -> None:
                 folded_weight(w, nw)
             if getattr(w, "_dla_fold_t", None) is not None:
                 folded_weight(w, nw, tiled=True)
+            if getattr(w, "_dla_fold_g", None) is not None:
+                folded_weight(w, nw, tiled=True, glu_il=True)
         for w in (getattr(layer.attn, "o_proj", None), getattr(layer.mlp, "down_proj", None)):
             if w is not None and getattr(w, "_dla_tile", None) is not None:
                 tiled_weight(w)
@@ -363,6 +386,10 @@ def skinny_normed(s: torch.Tensor, ssq: torch.Tensor, norm_w: torch.Tensor, eps:
                   w: torch.Tensor, glu: bool = False) -> torch.Tensor:
     """RMSNorm(s) * norm_w @ w^T from the producer's partials (glu: gate|up + SwiGLU epilogue)."""
     s2 = _rows(s)
+    if (glu and DECODE_GLU_IL and DECODE_TILED >= 1 and s2.shape[0] <= 16 and w.shape[0] % 32 == 0
+            and w.shape[1] % 512 == 0):
+        m = _ext.require().skinny_glu_il(s2, folded_weight(w, norm_w, tiled=True, glu_il=True), ssq, float(eps))
+        return m.view(*s.shape[:-1], m.shape[-1])
     wf = folded_weight(w, norm_w, tiled=DECODE_TILED >= 1)
     y, _ = _fused_op(s2.shape[0])(s2, wf, None, ssq, float(eps), bool(glu))
     return y.view(*s.shape[:-1], y.shape[-1])

@@ -280,7 +280,7 @@ def invalidate_weight_caches(model) -> None:
     for p in model.parameters():
         for k in ("_dla_wt_ver", "_dla_fp8"):
             p.__dict__.pop(k, None)
-        for k in ("_dla_fold", "_dla_fold_t", "_dla_tile"):  # ops.decode derived weights
+        for k in ("_dla_fold", "_dla_fold_t", "_dla_fold_g", "_dla_tile"):  # ops.decode derived weights
             c = p.__dict__.get(k)
             if c is not None:  # keep the buffer (a captured decode graph reads it), mark stale
                 setattr(p, k, (None, c[1]))

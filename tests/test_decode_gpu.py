@@ -547,6 +547,17 @@ def test_fused_decode_projection_kernels_match_fp32():
     assert torch.equal(y_rm, y)
     mm_rm, _ = C.skinny_fused(s, ops.decode.folded_weight(wgu, nw), None, ssq, 1e-5, True)
     assert torch.equal(mm_rm, mm)
+    # the interleaved-tile gate|up kernel (7 waves per workgroup) == the 8-wave LDS-exchange kernel
+    mm_t, _ = C.skinny_fused(s, ops.decode.folded_weight(wgu, nw, tiled=True), None, ssq, 1e-5, True)
+    mm_il = C.skinny_glu_il(s, ops.decode.folded_weight(wgu, nw, tiled=True, glu_il=True), ssq, 1e-5)
+    assert torch.equal(mm_il, mm_t)
+    for Mx in (1, 15, 16):  # every row count the rstd waves cover
+        sx = torch.randn(Mx, H, device=DEV, generator=g).to(torch.bfloat16)
+        sq = torch.zeros(16, H // 16, device=DEV)
+        sq[:Mx] = (sx.float() ** 2).view(Mx, H // 16, 16).sum(-1)
+        a, _ = C.skinny_fused(sx, ops.decode.folded_weight(wgu, nw, tiled=True), None, sq, 1e-5, True)
+        b = C.skinny_glu_il(sx, ops.decode.folded_weight(wgu, nw, tiled=True, glu_il=True), sq, 1e-5)
+        assert torch.equal(a, b), Mx
 
 
 def test_tile_weight_kernel_matches_permute():
@@ -559,11 +570,14 @@ def test_tile_weight_kernel_matches_permute():
     w = torch.randn(N, K, device=DEV, generator=g).to(torch.bfloat16)
     nw = (1 + 0.1 * torch.randn(K, device=DEV, generator=g)).to(torch.bfloat16)
     for norm in (None, nw):
-        out = torch.empty((N // 16, K // 32, 4, 16, 8), dtype=torch.bfloat16, device=DEV)
-        ops._ext.require().tile_weight(w, norm, out)
-        src = w if norm is None else w * norm.view(1, -1)
-        ref = src.view(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4)
-        assert torch.equal(out, ref)
+        for il in (False, True):
+            out = torch.empty((N // 16, K // 32, 4, 16, 8), dtype=torch.bfloat16, device=DEV)
+            ops._ext.require().tile_weight(w, norm, out, il)
+            src = w if norm is None else w * norm.view(1, -1)
+            if il:
+                src = ops.decode._glu_interleave(src)
+            ref = src.reshape(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4)
+            assert torch.equal(out, ref)
 
 
 @pytest.mark.parametrize("M", [17, 32, 33, 64])

@@ -35,3 +35,16 @@ def test_folded_tiled_weight_refreshes_in_place():
     t2 = decode.folded_weight(w, nw, tiled=True)
     assert t2.data_ptr() == ptr
     assert torch.equal(t2, (w * nw.view(1, -1)).view(1, 16, 1, 4, 8).permute(0, 2, 3, 1, 4))
+
+
+def test_glu_interleave_row_order():
+    F, K = 32, 32
+    w = torch.arange(2 * F, dtype=torch.float32).view(-1, 1).expand(2 * F, K).contiguous()
+    il = decode._glu_interleave(w)[:, 0].long().tolist()
+    # tile t: gate rows 8t .. 8t+7, then up rows F + 8t .. F + 8t + 7
+    assert il[:16] == list(range(8)) + list(range(F, F + 8))
+    assert il[16:32] == list(range(8, 16)) + list(range(F + 8, F + 16))
+    t = decode.folded_weight(w.to(torch.bfloat16), torch.ones(K, dtype=torch.bfloat16), tiled=True, glu_il=True)
+    assert t.shape == (2 * F // 16, 1, 4, 16, 8)
+    # tile 1, lane r = 9 holds up row F + 8 + 1
+    assert float(t[1, 0, 0, 9, 0]) == F + 9
