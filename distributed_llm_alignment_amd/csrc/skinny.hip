@@ -58,6 +58,17 @@ bool skinny_nt() {
   return nt;
 }
 
+// Non-temporal loads on the TILED decode weight streams (each byte read once per step by one CU):
+// 3.54 vs 3.70 ms/token at B=8 (profiles/r3_decode_tiled.md). On the row-major layout nt lost
+// (DLA_SKINNY_NT above). DLA_DECODE_NT=0 turns it off.
+static bool decode_nt() {
+  static const bool nt = [] {
+    const char* e = getenv("DLA_DECODE_NT");
+    return !(e != nullptr && atoi(e) == 0);
+  }();
+  return nt;
+}
+
 }  // namespace
 
 // grid: (ceil(N / 128), S), 8 waves. LDS: M x (kc + 8) bf16 (row pad of 16 B keeps the 16-row fragment
@@ -573,7 +584,7 @@ __global__ __launch_bounds__(512) void skinny_ksplit_kernel(
 // fused decode-layer launches (KsFuse): the residual-producing projection and the
 // norm-consuming qkv projection on the in-workgroup split-K kernel, the gate|up GLU on the LDS
 // kernel. M <= 16.
-template <bool TW>
+template <bool TW, bool NT>
 static void launch_ks_fused_t(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
                               int64_t ldy, int M, int N, int K, const KsFuse& fz, bool res, bool nin,
                               hipStream_t st) {
@@ -583,7 +594,7 @@ static void launch_ks_fused_t(const bf16_t* x, int64_t ldx, const bf16_t* W, int
   }();
   const int nb = N / 16;
   const bool deep = K >= deep_k;
-#define DLA_KSF(D, R, NI) skinny_ksplit_kernel<D, false, false, 1, kKsUnroll, R, NI, TW><<<nb, 512, 0, st>>>(x, ldx, W, ldw, y, ldy, M, N, K, fz)
+#define DLA_KSF(D, R, NI) skinny_ksplit_kernel<D, NT, false, 1, kKsUnroll, R, NI, TW><<<nb, 512, 0, st>>>(x, ldx, W, ldw, y, ldy, M, N, K, fz)
   if (res && nin) {
     if (deep) DLA_KSF(4, true, true); else DLA_KSF(2, true, true);
   } else if (res) {
@@ -600,30 +611,33 @@ static void launch_ks_fused_t(const bf16_t* x, int64_t ldx, const bf16_t* W, int
 void launch_skinny_ks_fused(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
                             int64_t ldy, int M, int N, int K, const KsFuse& fz, bool res, bool nin,
                             bool tiled, hipStream_t st) {
-  if (tiled) launch_ks_fused_t<true>(x, ldx, W, ldw, y, ldy, M, N, K, fz, res, nin, st);
-  else launch_ks_fused_t<false>(x, ldx, W, ldw, y, ldy, M, N, K, fz, res, nin, st);
+  // DLA_DECODE_NT=1: non-temporal weight loads on the tiled stream (A/B)
+  if (tiled && decode_nt()) launch_ks_fused_t<true, true>(x, ldx, W, ldw, y, ldy, M, N, K, fz, res, nin, st);
+  else if (tiled) launch_ks_fused_t<true, false>(x, ldx, W, ldw, y, ldy, M, N, K, fz, res, nin, st);
+  else launch_ks_fused_t<false, false>(x, ldx, W, ldw, y, ldy, M, N, K, fz, res, nin, st);
 }
 
-template <bool TW>
+template <bool TW, bool NT>
 static void launch_glu_normin_t(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
                                 int64_t ldy, int M, int N, int K, const KsFuse& fz, hipStream_t st) {
   static bool attr_set = [] {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_gemm_kernel<false, true, false, false, true, TW>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_gemm_kernel<false, true, false, NT, true, TW>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
     (void)hipGetLastError();
     return true;
   }();
   (void)attr_set;
   dim3 g2(N / 2 / 64, 1);
-  skinny_gemm_kernel<false, true, false, false, true, TW><<<g2, 64 * kSkWaves, skinny_lds_bytes(M, K), st>>>(
+  skinny_gemm_kernel<false, true, false, NT, true, TW><<<g2, 64 * kSkWaves, skinny_lds_bytes(M, K), st>>>(
       x, ldx, W, ldw, y, ldy, nullptr, nullptr, M, N, K, K, SkNorm{}, fz);
 }
 
 void launch_skinny_glu_normin(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
                               int64_t ldy, int M, int N, int K, const KsFuse& fz, bool tiled,
                               hipStream_t st) {
-  if (tiled) launch_glu_normin_t<true>(x, ldx, W, ldw, y, ldy, M, N, K, fz, st);
-  else launch_glu_normin_t<false>(x, ldx, W, ldw, y, ldy, M, N, K, fz, st);
+  if (tiled && decode_nt()) launch_glu_normin_t<true, true>(x, ldx, W, ldw, y, ldy, M, N, K, fz, st);
+  else if (tiled) launch_glu_normin_t<true, false>(x, ldx, W, ldw, y, ldy, M, N, K, fz, st);
+  else launch_glu_normin_t<false, false>(x, ldx, W, ldw, y, ldy, M, N, K, fz, st);
 }
 
 // Decode gate|up (M <= 16) over an INTERLEAVED tiled weight (ops/decode.py `glu_weight`): tile t

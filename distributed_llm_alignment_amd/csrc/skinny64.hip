@@ -51,7 +51,7 @@ __device__ __forceinline__ f32x4 mfma16(s16x8 a, s16x8 b, f32x4 c) {
 // from ssq_in (the producer's row partial sums, [M][nbp]) when NIN, else 1; gate / up are
 // rounded to bf16 before SwiGLU exactly as the unfused GEMM + swiglu pair.
 // Otherwise S == 1 writes y = bf16(x W^T); S > 1 writes fp32 slab ws[s][m][n].
-template <int MT, bool GLU, bool NIN, bool TW, int DEPTH, int NW = kM64Waves>
+template <int MT, bool GLU, bool NIN, bool TW, int DEPTH, int NW = kM64Waves, bool NTL = false>
 __global__ __launch_bounds__(64 * NW) void m64_gemm_kernel(
     const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ W, int64_t ldw,
     bf16_t* __restrict__ y, int64_t ldy, float* __restrict__ ws, int M, int N, int K, int kc,
@@ -100,7 +100,9 @@ __global__ __launch_bounds__(64 * NW) void m64_gemm_kernel(
     }
 #pragma unroll
     for (int u = 0; u < kM64Steps; ++u)
-      b[j][u] = __builtin_bit_cast(s16x8, load_bf16x8(TW ? wrow + (c * kM64Steps + u) * 512 : wrow + c * kM64Ck + u * 32));
+      b[j][u] = NTL ? __builtin_bit_cast(s16x8, __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(
+                          TW ? wrow + (c * kM64Steps + u) * 512 : wrow + c * kM64Ck + u * 32)))
+                    : __builtin_bit_cast(s16x8, load_bf16x8(TW ? wrow + (c * kM64Steps + u) * 512 : wrow + c * kM64Ck + u * 32));
   };
   auto xstore = [&](auto J, int slot) {
     constexpr int j = decltype(J)::value;
@@ -288,20 +290,20 @@ size_t m64_lds_bytes(int M) {
   return static_cast<size_t>(2 * 16 * mt * kM64Ld) * sizeof(bf16_t);
 }
 
-template <int MT, bool GLU, bool NIN, bool TW, int NW>
+template <int MT, bool GLU, bool NIN, bool TW, int NW, bool NTL>
 static void m64_launch_w(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
                          int64_t ldy, float* ws, int M, int N, int K, int S, const float* ssq_in,
                          int nbp, float eps, hipStream_t st) {
   const size_t lds = static_cast<size_t>(2 * 16 * MT * kM64Ld) * sizeof(bf16_t);
   static bool attr = [] {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&m64_gemm_kernel<MT, GLU, NIN, TW, 2, NW>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&m64_gemm_kernel<MT, GLU, NIN, TW, 2, NW, NTL>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
     (void)hipGetLastError();
     return true;
   }();
   (void)attr;
   dim3 grid(GLU ? N / 2 / (8 * NW) : N / (16 * NW), S);
-  m64_gemm_kernel<MT, GLU, NIN, TW, 2, NW><<<grid, 64 * NW, lds, st>>>(x, ldx, W, ldw, y, ldy, ws, M, N,
+  m64_gemm_kernel<MT, GLU, NIN, TW, 2, NW, NTL><<<grid, 64 * NW, lds, st>>>(x, ldx, W, ldw, y, ldy, ws, M, N,
                                                                        K, K / S, ssq_in, nbp, eps);
 }
 
@@ -311,7 +313,15 @@ template <int MT, bool GLU, bool NIN, bool TW>
 static void m64_launch(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
                        int64_t ldy, float* ws, int M, int N, int K, int S, const float* ssq_in,
                        int nbp, float eps, hipStream_t st) {
-  m64_launch_w<MT, GLU, NIN, TW, kM64Waves>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, ssq_in, nbp, eps, st);
+  // non-temporal loads on the tiled weight stream (DLA_DECODE_NT, default on; see skinny.hip decode_nt)
+  static const bool nt = [] {
+    const char* e = getenv("DLA_DECODE_NT");
+    return !(e != nullptr && atoi(e) == 0);
+  }();
+  if (TW && nt)
+    m64_launch_w<MT, GLU, NIN, TW, kM64Waves, true>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, ssq_in, nbp, eps, st);
+  else
+    m64_launch_w<MT, GLU, NIN, TW, kM64Waves, false>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, ssq_in, nbp, eps, st);
 }
 
 template <int MT, bool TW>
