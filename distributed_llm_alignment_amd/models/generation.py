@@ -185,7 +185,7 @@ def _graph_capable(model: CausalLM) -> bool:
     sync inside the forward (MoE routing still reads per-expert counts on the host unless the
     device-driven grouped expert GEMM is active)."""
     moe_host_sync = model.cfg.is_moe and not getattr(model, "moe_device_dispatch", False)
-    return (model.tp_size == 1 and getattr(model, "_dla_fsdp", None) is None
+    return (model.tp_size == 1 and not model.layers_sharded()
             and model.layer_devices is None and not moe_host_sync)
 
 

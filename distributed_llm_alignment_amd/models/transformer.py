@@ -482,11 +482,18 @@ class CausalLM(nn.Module):
                             self.cfg.norm_type == "rms")
         return h
 
+    def layers_sharded(self) -> bool:
+        """Some decoder layer's weights are ZeRO-3 shards gathered only inside its forward."""
+        return getattr(self, "_dla_fsdp", None) is not None or any(
+            getattr(l, "_dla_sharded", False) for l in self.layers)
+
     def _forward_cached(self, input_ids, attention_mask, cache):
         positions = cache.positions_for(input_ids.shape[1])
         x = self.embed_tokens(input_ids, positions)
+        # decode_fused calls the layers' kernels directly, skipping Module.__call__: a ZeRO-3
+        # policy's layers are gathered by forward hooks, so sharded layers take the hooked path
         if (input_ids.shape[1] == 1 and self.layer_devices is None and self.layers
-                and self.layers[0].decode_fused_ok(x)):
+                and not self.layers_sharded() and self.layers[0].decode_fused_ok(x)):
             # decode step: residual add + RMSNorm folded into the neighbouring projections
             s, ssq = x, None
             for i, layer in enumerate(self.layers):

@@ -35,10 +35,33 @@ def _bad_word(device: torch.device) -> torch.Tensor:
     return w
 
 
-def check_ids(reset: bool = True) -> None:
+def check_ids(reset: bool = True, group=None, collective: bool = False) -> None:
     """Raise if any native embedding forward since the last check saw an id outside [0, V)
-    (one host sync per device that ran the kernel)."""
-    for dev, w in list(_BAD.items()):
+    (one host sync per device that ran the kernel).
+
+    `collective=True` (the trainers' logging step, reached by every rank together): the sticky
+    words are max-reduced over `group` first, so every rank raises at the same step instead of the
+    ranks that saw no bad id blocking in their next collective until the RCCL timeout."""
+    import torch.distributed as dist
+
+    words = list(_BAD.items())
+    if collective and dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        dev = words[0][0] if words else (torch.device("cuda", torch.cuda.current_device())
+                                         if dist.get_backend(group) == "nccl" else torch.device("cpu"))
+        flag = torch.zeros(1, dtype=torch.int32, device=dev)
+        for _, w in words:
+            flag = torch.maximum(flag, (w != 0).int().to(dev))
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+        if int(flag.item()) != 0:
+            local = [str(d) for d, w in words if int(w.item()) != 0]
+            if reset:
+                for _, w in words:
+                    w.zero_()
+            raise IndexError("embedding: token id out of range [0, vocab) on "
+                             f"{', '.join(local) if local else 'another rank'} (the rows were "
+                             "zero-filled and got no gradient); check the tokenizer / vocab_size")
+        return
+    for dev, w in words:
         if int(w.item()) != 0:
             if reset:
                 w.zero_()

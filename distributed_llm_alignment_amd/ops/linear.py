@@ -51,7 +51,7 @@ def input_grad(dy2: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
 # Weight gradient dW += dY^T X reduces over the token dim, which is the slow dim of both
 # operands (NT layout). For the large FFN weights it is faster to transpose both activations
 # with the HIP tiled transpose and run the TN GEMM: Llama-3-8B up 1.66 -> 1.22 + 0.24 ms,
-# down 0.95 -> 0.68 + 0.14 ms; no gain for qkv / o (tools/_probe_dw_tn.py, MI355X).
+# down 0.95 -> 0.68 + 0.14 ms; no gain for qkv / o (one-off layout probe, MI355X).
 TN_WGRAD = os.environ.get("DLA_TN_WGRAD", "1") != "0"
 TN_WGRAD_MIN_ELEMS = int(os.environ.get("DLA_TN_WGRAD_MIN", "0"))
 

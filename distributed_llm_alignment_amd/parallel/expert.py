@@ -4,12 +4,14 @@
 Each rank of an EP group of size ep owns E/ep consecutive experts (`expert_up/down` sliced in
 place, identical seeded init everywhere -> no broadcast). Two dispatch modes:
 
-* `capacity` (default; `hardware.ep_capacity_factor` > 0): NO host synchronisation anywhere in
+* `capacity` (`hardware.ep_capacity_factor` > 0, e.g. 2.0; `bench.py --ep-capacity`): NO host
+  synchronisation anywhere in
   the layer, forward or backward. Every (source, destination) pair exchanges a fixed block of
   C = capacity_factor * N * k / ep rows (multiple of 8), so the all-to-all split sizes are known
   on the host without reading the routing: token slots are ordered expert-major on the device,
   each destination's slots beyond C are dropped (their combine weight becomes 0, the GShard /
-  Switch convention; `dropped_slots()` reports the count lazily), the per-(destination, local
+  Switch convention; `dropped_slots()` reports the count lazily and the trainers log it as
+  `moe/dropped_slots`, warning when nonzero), the per-(destination, local
   expert) counts travel in one small device-side all-to-all, and the receiver builds the
   expert-major row order and the grouped-GEMM offsets on the device. The grouped expert GEMM
   (csrc/grouped_gemm.hip) then runs over the padded [ep*C] buffer, touching only the valid rows.
@@ -17,7 +19,8 @@ place, identical seeded init everywhere -> no broadcast). Two dispatch modes:
   all-to-all is in flight on RCCL's stream while chunk c's expert GEMMs run, and chunk c's
   return all-to-all overlaps chunk c+1's experts. With a capacity large enough that nothing is
   dropped the result equals the exact path (the MoE layer is per-token).
-* `exact` (capacity factor 0): dropless with host-known splits: the per-(rank, expert) counts
+* `exact` (capacity factor 0, the trainers' default: HF Mixtral, which the reference runs, is
+  dropless): dropless with host-known splits: the per-(rank, expert) counts
   are read on the host once per layer and `all_to_all_single` moves exactly the routed rows.
 
 Expert weights are marked `_dla_expert`: the data-parallel engine reduces their grads over the

@@ -189,6 +189,8 @@ class _ShardedBase:
         self.comm_timer = ExposedCommTimer(self.device)  # exposed gradient-comm wait per step
         self._seen = set()
         for u in units:  # gather before the unit's first layer, free after its last
+            for m in u.modules:  # callers that bypass Module.__call__ (fused decode) check this
+                m._dla_sharded = True
             if u.modules:
                 u.modules[0].register_forward_pre_hook(self._make_pre_forward(u))
                 u.modules[-1].register_forward_hook(self._make_post_forward(u))

@@ -112,7 +112,7 @@ def parallelize(ctx: TrainContext, model):
     if m.ep > 1 and base.cfg.is_moe:
         from ..parallel.expert import apply_expert_parallel
 
-        apply_expert_parallel(model, m, capacity_factor=ctx.hw.get("ep_capacity_factor", 2.0),
+        apply_expert_parallel(model, m, capacity_factor=ctx.hw.get("ep_capacity_factor", 0.0),
                               chunks=ctx.hw.get("ep_chunks", 2))
     if base.cfg.is_moe and (ctx.cfg.get("model", {}) or {}).get("moe_fp8", False):
         for layer in base.layers:  # e4m3 expert GEMMs in the forward (bf16 backward)
@@ -237,6 +237,19 @@ def _batch_rows(batch) -> int:
 StepFn = Callable[[Any], Tuple[torch.Tensor, Dict[str, Any]]]
 
 
+def _moe_dropped_slots(model) -> Optional[int]:
+    """Token slots the capacity-bounded EP dispatch dropped since the last call (None: no EP)."""
+    from ..parallel.expert import ExpertParallel
+
+    seen, total = set(), None
+    for m in model.modules():
+        ep = getattr(m, "ep", None)
+        if isinstance(ep, ExpertParallel) and id(ep) not in seen:
+            seen.add(id(ep))
+            total = (total or 0) + ep.dropped_slots()
+    return total
+
+
 def train_loop(ctx: TrainContext, loader, sampler, engine: DataParallelEngine, step_fn: StepFn,
                total_steps: int, models_to_save: List[Any], tokenizer=None,
                scheduler: Optional[LRSchedule] = None, log_every: int = 10, eval_every: int = 0,
@@ -298,9 +311,16 @@ def train_loop(ctx: TrainContext, loader, sampler, engine: DataParallelEngine, s
             if log_every and global_step % log_every == 0:
                 from ..ops.embedding import check_ids
 
-                check_ids()  # out-of-range token ids since the last log (sticky device word)
+                # out-of-range token ids since the last log (sticky device word), on every rank
+                check_ids(collective=True)
                 rec = {"train/loss": running.average, "train/grad_norm": engine.last_grad_norm,
                        "train/comm_exposed_ms": engine.comm_timer.last_ms()}
+                dropped = _moe_dropped_slots(models_to_save[0])
+                if dropped is not None:
+                    rec["moe/dropped_slots"] = dropped
+                    if dropped:
+                        ctx.log(f"WARNING: expert-parallel capacity dropped {dropped} token slots "
+                                f"since the last log (hardware.ep_capacity_factor; 0 = dropless)")
                 if scheduler is not None:
                     rec["train/lr"] = scheduler.lr(global_step)
                 if extra_log_fn is not None:

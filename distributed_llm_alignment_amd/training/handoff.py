@@ -15,7 +15,11 @@ Equality with the text path holds whenever re-tokenising the decoded text reprod
 when the sampled ids are the canonical tokenization and no merge crosses the "\\n\\n"
 boundary). Where it does not, the device path scores exactly the tokens the policy generated,
 which is what the log-probs in the loss are computed over. `ppo.reward_handoff: text` keeps the
-reference behaviour; `auto` (default) takes the device path when the tokenizers match.
+reference behaviour; `device` forces the device path. `auto` (default) takes the device path when
+the tokenizers match, and for non-byte (BPE) tokenizers first checks it on the first batch: both
+paths are built once, and if the ids differ (a merge across the boundary, a non-canonical sample)
+the hand-off falls back to `text` for the rest of the run, so the default scores what the
+reference scores.
 """
 from __future__ import annotations
 
@@ -121,6 +125,10 @@ class RewardHandoff:
             raise ValueError("ppo.reward_handoff=device needs the reward tokenizer to equal the policy's")
         self.device_path = match and mode != "text"
         self.ptok, self.rtok, self.max_length = policy_tok, reward_tok, int(max_length)
+        from ..models.tokenizer import ByteTokenizer
+
+        # auto + BPE: validate the device ids against the text round trip on the first batch
+        self._validate = self.device_path and mode == "auto" and not isinstance(reward_tok, ByteTokenizer)
         if self.device_path:
             self.special = special_token_table(reward_tok, vocab_size, device)
             self.sep = separator_ids(reward_tok).to(device)
@@ -128,8 +136,27 @@ class RewardHandoff:
 
     def __call__(self, prompts, ids, am, seqs, gen_mask=None):
         if self.device_path:
-            return device_reward_inputs(ids, am, seqs, self.sep, self.special, self.pad,
-                                        self.max_length, gen_mask)
+            out = device_reward_inputs(ids, am, seqs, self.sep, self.special, self.pad,
+                                       self.max_length, gen_mask)
+            if not self._validate:
+                return out
+            self._validate = False
+            ref = self._text(prompts, ids, seqs)
+            if self._same(out, ref):
+                return out
+            self.device_path = False  # the tokenizer does not round-trip these ids: text from now on
+            return ref
+        return self._text(prompts, ids, seqs)
+
+    @staticmethod
+    def _same(a, b) -> bool:
+        (ia, ma), (ib, mb) = a, b
+        n = max(ia.shape[1], ib.shape[1])
+        pad = lambda t: torch.nn.functional.pad(t, (0, n - t.shape[1]))  # noqa: E731
+        ma, mb = pad(ma.long()), pad(mb.long())
+        return bool(torch.equal(ma, mb) and torch.equal(pad(ia) * ma, pad(ib) * mb))
+
+    def _text(self, prompts, ids, seqs):
         responses = self.ptok.batch_decode(seqs[:, ids.shape[1]:], skip_special_tokens=True)
         fused = [f"{p}\n\n{r}" for p, r in zip(prompts, responses)]
         enc = self.rtok(fused, return_tensors="pt", padding=True, truncation=True, max_length=self.max_length)

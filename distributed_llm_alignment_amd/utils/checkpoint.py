@@ -115,11 +115,17 @@ def save_state(output_dir, models: Sequence, engine=None, scheduler=None, step: 
         save_streamed(out / f"optimizer_shard_{st.rank}.safetensors", tens, meta)
         if st.is_main and hasattr(engine, "layout"):
             (out / "dla_optimizer_layout.json").write_text(json.dumps(engine.layout()))
-        if engine.numel <= CONSOLIDATE_MAX_NUMEL and not tp:
+        # expert-parallel state: each EP rank holds different experts under local indices, and the
+        # expert buckets are sharded over the expert-DP group, not the global ranks -- one flat
+        # optimizer.bin cannot be assembled from rank-local layouts (the per-rank shards are the
+        # checkpoint; like TP, consolidation is refused rather than written partially)
+        ep = bool(getattr(engine, "has_experts", False))
+        if engine.numel <= CONSOLIDATE_MAX_NUMEL and not tp and not ep:
             osd = engine.torch_optimizer_state_dict()  # collective under ZeRO (gathered per unit)
             if st.is_main:
                 torch.save(osd, out / "optimizer.bin")
-        elif not tp and engine.numel <= STREAM_CONSOLIDATE_MAX_NUMEL and hasattr(engine, "layout"):
+        elif (not tp and not ep and engine.numel <= STREAM_CONSOLIDATE_MAX_NUMEL
+              and hasattr(engine, "layout")):
             pdist.barrier()  # every rank's shard is on disk
             if st.is_main:
                 from .consolidate import consolidate_optimizer as consolidate

@@ -113,7 +113,7 @@ def hardware_parallel(cfg: Dict[str, Any]) -> Dict[str, Any]:
         "ep_size": int(hw.get("ep_size", 1) or 1),
         "sp_size": int(hw.get("sp_size", 1) or 1),  # Ulysses sequence parallel (parallel.sequence)
         # expert parallel dispatch: fixed-capacity blocks (no host sync; 0 = exact, host splits)
-        "ep_capacity_factor": float(hw.get("ep_capacity_factor", 2.0)),
+        "ep_capacity_factor": float(hw.get("ep_capacity_factor", 0.0)),
         "ep_chunks": int(hw.get("ep_chunks", 2) or 1),
         # Megatron sequence parallel inside the TP group (reduce-scatter / all-gather, sharded norms)
         "tp_sequence_parallel": bool(hw.get("tp_sequence_parallel", False)),

@@ -11,7 +11,8 @@ ranks: bounded by one parameter). Host memory therefore stays at ~one parameter 
 model, which is what lets `save_state` write optimizer.bin at 7B/8B scale in-line (rank 0, after
 the shard barrier) and `tools/consolidate_checkpoint.py` do it offline for anything. Legacy
 `optimizer_shard_{rank}.pt` files are read with `torch.load(mmap=True, weights_only=True)`.
-Tensor-parallel checkpoints are refused: their shards are TP slices, not one flat state.
+Tensor-parallel and expert-parallel checkpoints are refused: their shards are TP slices / per-EP-rank
+experts, not one flat state.
 """
 from __future__ import annotations
 
@@ -99,6 +100,11 @@ def consolidate_optimizer(ckpt, out=None) -> Path:
     lay = json.loads((ckpt / "dla_optimizer_layout.json").read_text())
     if int(lay.get("tp_size", 1)) > 1:
         raise ValueError("tensor-parallel optimizer shards are TP slices; consolidate per TP rank")
+    if any(b.get("expert") for b in lay.get("buckets", [])):
+        # expert buckets: world = expert-DP size, rank = expert-DP rank, indices local to one
+        # EP rank's experts; the layout (written by rank 0) does not describe the other experts
+        raise ValueError("expert-parallel optimizer shards hold per-EP-rank experts; a flat "
+                         "optimizer.bin cannot be built from them (resume from the shards)")
     world = int(lay["world"])
     n_ranks = world if (lay["kind"] != "flat" or lay["zero"]) else 1
     shards = [_open_shard(ckpt, r) for r in range(n_ranks)]
