@@ -74,7 +74,14 @@ class DataParallelEngine:
                  overlap_param_gather: bool = os.environ.get("DLA_OVERLAP_AG", "1") != "0",
                  sp_size: int = 1,
                  overlap_optimizer: bool = os.environ.get("DLA_OVERLAP_OPT", "0") == "1",
-                 grad_dtype: Optional[torch.dtype] = None, reduce_dtype: Optional[torch.dtype] = None):
+                 grad_dtype: Optional[torch.dtype] = None, reduce_dtype: Optional[torch.dtype] = None,
+                 shape_world: int = 1):
+        """`shape_world` > 1 (debug / benchmarking, one process only): lay the engine out as rank 0
+        of a ZeRO-1 group of that size without any process group -- fp32 master weights and Adam
+        moments exist (and are updated) only for this rank's 1/shape_world chunk of every bucket,
+        the reduce-scatter becomes a local copy of that chunk and the all-gather a copy back.
+        The memory and per-rank optimizer work are those of one rank of the N-GPU job; the
+        communication is not run (tools/bench_rlhf.py --zero-shape, like bench.py --tp-shape)."""
         self.module = module
         # sequence parallel (parallel.sequence): `group` is DP x SP and the sp ranks of a replica
         # hold partial (token-slice) gradients of one replicated loss -> sum over SP, mean over DP
@@ -96,6 +103,11 @@ class DataParallelEngine:
                 self.world, self.rank = self.dist.world_size, self.dist.rank
         else:
             self.world, self.rank = 1, 0
+        self.shape_only = int(shape_world) > 1
+        if self.shape_only:
+            if self.world != 1:
+                raise ValueError("shape_world is a single-process mode (no data-parallel group)")
+            self.world, self.rank = int(shape_world), 0
         self.group = group
         self.zero = (1 if self.world > 1 else 0) if zero_stage is None else (zero_stage if self.world > 1 else 0)
         self.lr, self.betas, self.eps, self.wd = lr, tuple(betas), eps, weight_decay
@@ -154,7 +166,7 @@ class DataParallelEngine:
         self.numel = cur.end
         self.has_experts = any(b.expert for b in self.buckets)
         # communication needed at all? (ZeRO with a 1-rank expert group still copies shards)
-        self._comm = self.world > 1
+        self._comm = self.world > 1 and not self.shape_only
         # ---- flat storage (params re-pointed into it)
         self.param_buf = torch.zeros(self.numel, dtype=self.dtype, device=self.device)
         self.grad_buf = torch.zeros(self.numel, dtype=self.grad_dtype, device=self.device)
@@ -342,6 +354,10 @@ class DataParallelEngine:
 
     def finish_grad_sync(self):
         """Launch buckets whose params got no gradient (unused params), then wait for all."""
+        if self.shape_only and self._sync:  # the reduce-scatter's output: this rank's chunks
+            for b in self.buckets:
+                c = b.size // b.world
+                self.grad_shard[b.shard_off:b.shard_off + c].copy_(self._chunk(self.grad_buf, b))
         if self._comm:
             while self._launched < len(self.buckets):
                 self._launch(self._launched)
@@ -360,6 +376,8 @@ class DataParallelEngine:
     # ------------------------------------------------------------------------ step
     @property
     def grad_scale(self) -> float:
+        if self.shape_only:  # local gradients, nothing summed over ranks
+            return float(self.sp_size)
         return self.sp_size / self.world
 
     def clip_and_norm(self):
@@ -368,7 +386,7 @@ class DataParallelEngine:
         if self._repl_ranges:
             rep = sum(self.grad_shard[a:e].float().pow(2).sum() for a, e in self._repl_ranges)
             self._sumsq -= (1.0 - 1.0 / self.tp_size) * rep
-        if self.has_experts and self.world > 1:
+        if self.has_experts and self._comm:
             # weight every element by 1/(#ranks holding it) and sum over the DP group: dense
             # grads are replicated dp times (ZeRO-0) or unique (ZeRO-1); expert grads are
             # replicated over the expert-DP group (ZeRO-0) or unique, and differ across EP ranks
@@ -387,7 +405,7 @@ class DataParallelEngine:
                 ew = self.buckets[[b.expert for b in self.buckets].index(True)].world
                 self._sumsq = dense / self.world + self._esumsq / ew
             dist.all_reduce(self._sumsq, op=dist.ReduceOp.SUM, group=self.group)
-        elif self.zero and self.world > 1:
+        elif self.zero and self._comm:
             dist.all_reduce(self._sumsq, op=dist.ReduceOp.SUM, group=self.group)
         if self.tp_size > 1:
             dist.all_reduce(self._sumsq, op=dist.ReduceOp.SUM, group=self.tp_group)
@@ -417,6 +435,8 @@ class DataParallelEngine:
                 c = b.size // b.world
                 if b.world == 1:
                     self.param_buf[b.start:b.end].copy_(self.param_shard[b.shard_off:b.shard_off + c])
+                elif self.shape_only:  # the all-gather's local part
+                    self._chunk(self.param_buf, b).copy_(self.param_shard[b.shard_off:b.shard_off + c])
                 else:
                     h = dist.all_gather_into_tensor(self.param_buf[b.start:b.end],
                                                     self.param_shard[b.shard_off:b.shard_off + c],
@@ -487,6 +507,9 @@ class DataParallelEngine:
     # ------------------------------------------------------------------------ state
     def optimizer_state(self) -> Dict[str, object]:
         """Local (possibly sharded) optimizer state."""
+        if self.shape_only:
+            raise RuntimeError("a shape_world engine holds one rank's optimizer shard of a job that "
+                               "does not exist: it has no checkpointable state")
         self.wait_params()
         return {"step": self.step_count, "lr": self.lr, "betas": self.betas, "eps": self.eps,
                 "weight_decay": self.wd, "world": self.world, "zero": self.zero,

@@ -9,7 +9,16 @@ synthetic prompts. Prints one JSON line (rollouts/s and the phase split).
 the policy generates and scores step k+1's rollouts on a side stream, from a helper thread, while
 the main thread trains on step k's. Generation is bound by HBM bandwidth (B=8 weight streaming)
 and the update by MFMA, so the two share the chip. The snapshot is refreshed from the policy
-after each update: rollouts come from the weights one update behind."""
+after each update: rollouts come from the weights one update behind.
+
+--algorithm ppo: BASELINE config 3 as specified, token-level actor-critic PPO (`ppo.algorithm: ppo`,
+config/rlhf_ppo_llama3_8b.yaml): policy + frozen reference + reward model + critic (a Llama-3-8B
+backbone with a value head), each step generate -> score -> stats (policy / reference log-probs
+and critic values, GAE) -> `--ppo-epochs` x `--minibatches` clipped-surrogate + value updates on
+two engines. `--zero-shape N` lays both engines out as rank 0 of an N-rank ZeRO-1 job (fp32 master
+and moments for 1/N of each model, no collectives), so the memory and per-rank work are those of
+one GPU of the N-GPU node (reference: config/rlhf_config.yaml:13 batch 64 over 8 processes = 8
+rollouts per rank). Prints the phase split and a per-rank memory plan."""
 from __future__ import annotations
 
 import argparse
@@ -36,7 +45,14 @@ def main() -> int:
                     help="generate step k+1's rollouts (policy snapshot, side stream) during step k's update")
     ap.add_argument("--grad-ckpt", default="", help="policy activation recompute: full|mlp|attention "
                     "(the reference's rlhf_config batch of 64 rollouts on one GPU needs mlp)")
+    ap.add_argument("--algorithm", choices=("reinforce", "ppo"), default="reinforce")
+    ap.add_argument("--zero-shape", type=int, default=1,
+                    help="engines laid out as rank 0 of an N-rank ZeRO-1 job (1/N optimizer state)")
+    ap.add_argument("--ppo-epochs", type=int, default=2)
+    ap.add_argument("--minibatches", type=int, default=2)
     a = ap.parse_args()
+    if a.algorithm == "ppo":
+        return ppo_main(a)
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from distributed_llm_alignment_amd.models import build_model, generate, get_config
     from distributed_llm_alignment_amd.models.reward import RewardModel
@@ -178,6 +194,121 @@ def main() -> int:
                       "prompt": a.prompt, "new_tokens": a.new, "s_per_step": round(dt / a.steps, 3),
                       "rollouts_per_s": round(a.batch * a.steps / dt, 3),
                       **{f"{k}_s": round(v / a.steps, 3) for k, v in phases.items()}}), flush=True)
+    return 0
+
+
+def ppo_main(a) -> int:
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from distributed_llm_alignment_amd.models import build_model, generate, get_config
+    from distributed_llm_alignment_amd.models.reward import RewardModel, ValueModel
+    from distributed_llm_alignment_amd.models.tokenizer import ByteTokenizer
+    from distributed_llm_alignment_amd.objectives import ppo_loss, ppo_rollout_stats
+    from distributed_llm_alignment_amd.ops import _ext
+    from distributed_llm_alignment_amd.parallel.data_parallel import DataParallelEngine
+    from distributed_llm_alignment_amd.training.handoff import RewardHandoff
+    from distributed_llm_alignment_amd.utils.tuning import enable_gemm_tuning
+
+    dev = torch.device("cuda", 0)
+    _ext.require()
+    enable_gemm_tuning(0)
+    cfg = get_config(a.model)
+    gib = 2.0 ** 30
+    mem = {}
+
+    def note(k):
+        torch.cuda.synchronize()
+        mem[k] = round(torch.cuda.memory_allocated(dev) / gib, 2)
+
+    note("start")
+    pol = build_model(cfg, device=dev, dtype=torch.bfloat16, seed=1)
+    note("policy")
+    ref = build_model(cfg, device=dev, dtype=torch.bfloat16, seed=1).requires_grad_(False).eval()
+    note("reference")
+    rm = RewardModel(build_model(cfg, device=dev, dtype=torch.bfloat16, seed=2, headless=True)).to(dev, torch.bfloat16)
+    rm.eval().requires_grad_(False)
+    note("reward")
+    critic = ValueModel(build_model(cfg, device=dev, dtype=torch.bfloat16, seed=3, headless=True))
+    note("critic")
+    if a.grad_ckpt:
+        pol.gradient_checkpointing_enable(a.grad_ckpt)
+        critic.backbone.gradient_checkpointing_enable(a.grad_ckpt)
+    kw = dict(betas=(0.9, 0.95), weight_decay=0.01, max_grad_norm=1.0, shape_world=a.zero_shape)
+    eng = DataParallelEngine(pol, lr=1e-6, **kw)
+    note("policy_engine")
+    ceng = DataParallelEngine(critic, lr=5e-6, **kw)
+    note("critic_engine")
+    g = torch.Generator(device=dev).manual_seed(0)
+    tok = ByteTokenizer(vocab_size=cfg.vocab_size)
+    handoff = RewardHandoff(tok, tok, cfg.vocab_size, dev, a.prompt + a.new + 8, "device")
+    prompts = ["synthetic prompt"] * a.batch
+    phases = {"generate": 0.0, "score": 0.0, "stats": 0.0, "update": 0.0}
+    peaks = {}
+
+    def sync():
+        torch.cuda.synchronize()
+        return time.perf_counter()
+
+    def phase_peak(name):
+        torch.cuda.synchronize()
+        peaks[name] = max(peaks.get(name, 0.0), round(torch.cuda.max_memory_allocated(dev) / gib, 2))
+        torch.cuda.reset_peak_memory_stats(dev)
+
+    def step(record):
+        ids = torch.randint(3, cfg.vocab_size, (a.batch, a.prompt), device=dev, generator=g)
+        am = torch.ones_like(ids)
+        torch.cuda.reset_peak_memory_stats(dev)
+        t0 = sync()
+        seqs, mask = generate(pol, ids, am, max_new_tokens=a.new, do_sample=True, temperature=0.7,
+                              top_p=0.9, eos_token_id=-1, return_mask=True, seed=3)
+        t1 = sync()
+        phase_peak("generate")
+        with torch.no_grad():
+            r_ids, r_mask = handoff(prompts, ids, am, seqs, mask)
+            scores = rm(r_ids, r_mask)
+        t2 = sync()
+        phase_peak("score")
+        stats = ppo_rollout_stats(pol, ref, critic, seqs, mask, a.prompt, scores, 0.05, 1.0, 0.95)
+        t3 = sync()
+        phase_peak("stats")
+        S = seqs.shape[0]
+        nmb = max(1, a.minibatches)
+        bounds = [(i * S // nmb, (i + 1) * S // nmb) for i in range(nmb)]
+        pol.train()
+        critic.train()
+        for _ in range(a.ppo_epochs):
+            for lo, hi in bounds:
+                mb = {k: v[lo:hi] for k, v in stats.items() if k in ("old_logp", "values", "advantages", "returns", "act")}
+                loss, m = ppo_loss(pol, critic, seqs[lo:hi], mask[lo:hi], mb, 0.2, 0.2, 0.1)
+                loss.backward()
+                eng.step()
+                ceng.step()
+        t4 = sync()
+        phase_peak("update")
+        if record:
+            phases["generate"] += t1 - t0
+            phases["score"] += t2 - t1
+            phases["stats"] += t3 - t2
+            phases["update"] += t4 - t3
+        return loss, m
+
+    for _ in range(a.warmup):
+        step(False)
+    t = sync()
+    for _ in range(a.steps):
+        loss, m = step(True)
+    dt = sync() - t
+    # the update moved both models (finite, nonzero grad norms)
+    health = {"loss": round(float(loss), 5), "policy_grad_norm": round(float(eng.last_grad_norm), 5),
+              "critic_grad_norm": round(float(ceng.last_grad_norm), 5),
+              "clipfrac": round(float(m["clipfrac"]), 4)}
+    print(json.dumps({"bench": "ppo_step", "model": cfg.name, "rollouts_per_step": a.batch,
+                      "zero_shape": a.zero_shape, "ppo_epochs": a.ppo_epochs, "minibatches": a.minibatches,
+                      "grad_ckpt": a.grad_ckpt or "none", "prompt": a.prompt, "new_tokens": a.new,
+                      "s_per_step": round(dt / a.steps, 3), "rollouts_per_s": round(a.batch * a.steps / dt, 3),
+                      **{f"{k}_s": round(v / a.steps, 3) for k, v in phases.items()},
+                      "mem_after_gib": mem, "peak_gib_by_phase": peaks,
+                      "device_total_gib": round(torch.cuda.get_device_properties(dev).total_memory / gib, 1),
+                      **health}), flush=True)
     return 0
 
 
