@@ -66,6 +66,10 @@ def parse(argv=None):
     ap.add_argument("--tp-shape", type=int, default=1,
                     help="debug: time ONE tensor-parallel rank's compute at world 1 (the model's "
                          "per-rank shard shapes, models.config.tp_shard_config; no TP collectives)")
+    ap.add_argument("--ep-shape", type=int, default=1,
+                    help="debug: time ONE expert-parallel rank of an N-GPU MoE job at world 1: E/N "
+                         "local experts per layer, the capacity-padded sync-free dispatch with the "
+                         "all-to-alls as local copies, ZeRO-1 optimizer state of one of N ranks")
     ap.add_argument("--sharded-init", choices=("auto", "on", "off"), default="auto",
                     help="build on the meta device and materialise only this rank's TP / FSDP "
                          "shards (auto: with --tp > 1 or --zero 3)")
@@ -301,6 +305,13 @@ def main(argv=None) -> int:
 
         apply_expert_parallel(policy, mesh, capacity_factor=args.ep_capacity)
         apply_expert_parallel(ref, mesh, capacity_factor=args.ep_capacity)
+    if args.ep_shape > 1:
+        if world != 1 or args.ep != 1 or not cfg.is_moe:
+            raise SystemExit("bench.py: --ep-shape is a one-GPU debug mode for MoE models (world 1, --ep 1)")
+        from distributed_llm_alignment_amd.parallel.expert import apply_expert_parallel
+
+        for m in (policy, ref):
+            apply_expert_parallel(m, None, capacity_factor=args.ep_capacity or 2.0, shape_ep=args.ep_shape)
     if cfg.is_moe and args.fp8:
         for m in (policy, ref):
             for layer in m.layers:
@@ -323,7 +334,7 @@ def main(argv=None) -> int:
                                     max_grad_norm=1.0, zero_stage=args.zero, bucket_mb=args.bucket_mb,
                                     group=mesh.grad_group, tp_group=mesh.tp_group,
                                     expert_group=mesh.edp_group if mesh.ep > 1 else None,
-                                    sp_size=mesh.sp)
+                                    sp_size=mesh.sp, shape_world=args.ep_shape)
     policy.train()
 
     gen = torch.Generator().manual_seed(17 + mesh.dp_rank)  # TP ranks share a batch
@@ -426,7 +437,9 @@ def main(argv=None) -> int:
             "data": "synthetic preference pairs (random token ids), random-init weights",
             "config": {
                 "model": (cfg.name if args.layers is None else f"{cfg.name}-L{args.layers}(debug)")
-                         + ("(per-TP-rank shapes, debug)" if args.tp_shape > 1 else ""),
+                         + ("(per-TP-rank shapes, debug)" if args.tp_shape > 1 else "")
+                         + (f"(one EP rank of ep{args.ep_shape}: {cfg.num_experts // args.ep_shape} "
+                            "local experts/layer, a2a as local copies, debug)" if args.ep_shape > 1 else ""),
                 "global_batch": pairs_per_step,
                 "seq_len": args.seq_len,
                 "parallelism": f"dp{mesh.dp}" + (f"-tp{mesh.tp}" if mesh.tp > 1 else "")

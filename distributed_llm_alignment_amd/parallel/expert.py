@@ -58,32 +58,56 @@ def all_to_all(x, out_splits, in_splits, group):
 
 
 class _A2AStart(torch.autograd.Function):
-    """Equal-split all-to-all launched asynchronously; `_A2AWait` completes it. Backward: the
-    adjoint all-to-all (synchronous)."""
+    """Equal-split all-to-all launched asynchronously; `_A2AWait` completes it. The backward is
+    split the same way: `_A2AWait.backward` (which autograd reaches first) launches the adjoint
+    all-to-all asynchronously and `_A2AStart.backward` waits for it, so with several chunks the
+    gradient exchange of one chunk overlaps the expert backward of another. `group=None` is the
+    one-process shape mode (ExpertParallel(shape_ep=N)): the exchange is the identity."""
 
     @staticmethod
     def forward(ctx, x, group, holder):
-        ctx.group = group
+        ctx.link = link = {"group": group}
         x = x.contiguous()
+        if group is None:
+            holder.append((None, link))
+            return x.view_as(x)
         out = torch.empty_like(x)
-        holder.append(dist.all_to_all_single(out, x, group=group, async_op=True))
+        holder.append((dist.all_to_all_single(out, x, group=group, async_op=True), link))
         return out
 
     @staticmethod
     def backward(ctx, g):
-        dx = torch.empty_like(g)
-        dist.all_to_all_single(dx, g.contiguous(), group=ctx.group)
+        link = ctx.link
+        if link.get("h") is not None:
+            link.pop("h").wait()
+        dx = link.pop("dx", None)
+        if dx is None:  # the wait node's backward did not run first: exchange here
+            if link["group"] is None:
+                return g, None, None
+            dx = torch.empty_like(g)
+            dist.all_to_all_single(dx, g.contiguous(), group=link["group"])
         return dx, None, None
 
 
 class _A2AWait(torch.autograd.Function):
     @staticmethod
     def forward(ctx, out, holder):
-        holder.pop(0).wait()
+        h, link = holder.pop(0)
+        if h is not None:
+            h.wait()
+        ctx.link = link
         return out.view_as(out)
 
     @staticmethod
     def backward(ctx, g):
+        link = ctx.link
+        g = g.contiguous()
+        if link["group"] is None:
+            link["dx"] = g
+        else:
+            dx = torch.empty_like(g)
+            link["h"] = dist.all_to_all_single(dx, g, group=link["group"], async_op=True)
+            link["dx"] = dx
         return g, None
 
 
@@ -95,10 +119,19 @@ def _gather_rows(x: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
 
 
 class ExpertParallel:
-    def __init__(self, group, num_experts: int, capacity_factor: float = 2.0, chunks: int = 2):
-        self.group = group
-        self.ep = dist.get_world_size(group)
-        self.rank = dist.get_rank(group)
+    def __init__(self, group, num_experts: int, capacity_factor: float = 2.0, chunks: int = 2,
+                 shape_ep: int = 1):
+        """`shape_ep` > 1 (one process, no group; bench.py --ep-shape): rank 0 of an EP group of
+        that size. It keeps E/shape_ep experts and runs the capacity-padded, sync-free dispatch with
+        every all-to-all replaced by the identity: the rows this rank would send to destination r
+        stand in for the rows it would receive from source r. Under balanced routing that is the
+        per-rank expert load of the real job (k x N slots into E/ep experts), so the timing is one
+        EP rank's compute; the numerics are not the full model's (every slot meets the local
+        experts)."""
+        self.shape = int(shape_ep) > 1
+        self.group = None if self.shape else group
+        self.ep = int(shape_ep) if self.shape else dist.get_world_size(group)
+        self.rank = 0 if self.shape else dist.get_rank(group)
         if num_experts % self.ep:
             raise ValueError(f"num_experts {num_experts} not divisible by ep {self.ep}")
         self.E = num_experts
@@ -119,6 +152,8 @@ class ExpertParallel:
     def dispatch_combine(self, moe, h2: torch.Tensor, topv: torch.Tensor, topi: torch.Tensor):
         if self.capacity_factor > 0:
             return self._capacity(moe, h2, topv, topi)
+        if self.shape:
+            raise ValueError("the EP shape mode runs the capacity dispatch (capacity_factor > 0)")
         return self._exact(moe, h2, topv, topi)
 
     # ------------------------------------------------------------------ capacity (sync-free)
@@ -191,15 +226,19 @@ class ExpertParallel:
             if self._dropped is None:
                 self._dropped = torch.zeros((), dtype=torch.long, device=h2.device)
             self._dropped += ndrop
-            rc = torch.empty_like(sent)
-            w = dist.all_to_all_single(rc, sent.contiguous(), group=self.group, async_op=True)
+            if self.shape:
+                rc, w = sent, None
+            else:
+                rc = torch.empty_like(sent)
+                w = dist.all_to_all_single(rc, sent.contiguous(), group=self.group, async_op=True)
             xs = _gather_rows(h2[a:b], send_src)
             xr = _A2AStart.apply(xs, self.group, holder)
             stage.append((C, pos, w, rc, xr))
         # 2) per chunk: wait for its rows, experts on the device-built order, return all-to-all
         back = []
         for C, pos, w, rc, xr in stage:
-            w.wait()
+            if w is not None:
+                w.wait()
             xr = _A2AWait.apply(xr, holder)
             xe_src, inv, offs = self._expert_order(rc, C)
             xe = _gather_rows(xr, xe_src)
@@ -245,11 +284,29 @@ class ExpertParallel:
 
 
 @torch.no_grad()
-def apply_expert_parallel(model, mesh, capacity_factor: float = 2.0, chunks: int = 2):
+def apply_expert_parallel(model, mesh, capacity_factor: float = 2.0, chunks: int = 2,
+                          shape_ep: int = 1):
     """Keep this rank's E/ep experts of every MoE layer and attach the all-to-all router
-    (`capacity_factor` 0: exact dropless dispatch with one host read per layer)."""
+    (`capacity_factor` 0: exact dropless dispatch with one host read per layer). `shape_ep` > 1
+    with `mesh=None`: the one-process shape mode of ExpertParallel (bench.py --ep-shape)."""
     base = getattr(model, "backbone", model)
     cfg = base.cfg
+    if shape_ep > 1:
+        if mesh is not None and mesh.ep > 1:
+            raise ValueError("shape_ep is a one-process mode; it does not combine with a real EP group")
+        if not cfg.is_moe:
+            return model
+        ep = ExpertParallel(None, cfg.num_experts, capacity_factor=capacity_factor, chunks=chunks,
+                            shape_ep=shape_ep)
+        for layer in base.layers:
+            m = layer.mlp
+            for nm in ("expert_up", "expert_down"):
+                w = getattr(m, nm)
+                w.data = w.data[:ep.El].contiguous()
+                w._dla_expert = True  # its optimizer state is not sharded over the DP ranks
+            m.ep = ep
+        base.ep_size = ep.ep
+        return model
     if mesh.ep <= 1 or not cfg.is_moe:
         return model
     ep = ExpertParallel(mesh.ep_group, cfg.num_experts, capacity_factor=capacity_factor, chunks=chunks)

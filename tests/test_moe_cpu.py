@@ -68,3 +68,31 @@ def test_mixtral_dpo_step_runs_with_engine():
     l0.backward()
     assert float(eng.step()) > 0
     assert pol.layers[0].mlp.expert_up.grad.abs().sum() == 0  # grads zeroed after step
+
+
+def test_expert_parallel_shape_mode_one_rank():
+    """bench.py --ep-shape: one EP rank's experts (E / N per layer) behind the capacity dispatch
+    with identity all-to-alls; expert buckets keep unsharded optimizer state while the dense ones
+    are laid out as 1 of N ZeRO-1 ranks, and a DPO step trains the local experts."""
+    from distributed_llm_alignment_amd.data.synthetic import synthetic_preference_batch
+    from distributed_llm_alignment_amd.objectives import dpo_step_loss
+    from distributed_llm_alignment_amd.parallel.data_parallel import DataParallelEngine
+    from distributed_llm_alignment_amd.parallel.expert import apply_expert_parallel
+
+    cfg = get_config("tiny-mixtral")
+    N = cfg.num_experts // 2
+    pol = build_model(cfg, device="cpu", seed=0)
+    ref = build_model(cfg, device="cpu", seed=0).requires_grad_(False)
+    for m in (pol, ref):
+        apply_expert_parallel(m, None, capacity_factor=2.0, shape_ep=N)
+    mlp = pol.layers[0].mlp
+    assert mlp.expert_up.shape[0] == 2 and mlp.ep.shape and mlp.ep.ep == N
+    eng = DataParallelEngine(pol, lr=1e-2, shape_world=N)
+    assert any(b.expert and b.world == 1 for b in eng.buckets)
+    assert any(not b.expert and b.world == N for b in eng.buckets)
+    w0 = mlp.expert_up.detach().clone()
+    b = synthetic_preference_batch(2, 16, cfg.vocab_size, generator=torch.Generator().manual_seed(0))
+    loss, _ = dpo_step_loss(pol, ref, b)
+    loss.backward()
+    assert torch.isfinite(loss) and float(eng.step()) > 0
+    assert not torch.equal(w0, mlp.expert_up.detach())
