@@ -84,12 +84,18 @@ class Attention(nn.Module):
     def forward(self, h, rope, kv_start, kv_end, positions, cache=None, layer_idx=0, segs=None):
         cfg = self.cfg
         seq = self.tp_seq if (h.dim() == 2 and cache is None) else None
-        if seq is not None:
-            from ..parallel.tensor_parallel import sp_gather
+        from ..parallel import tensor_parallel as tpm
 
+        sp_overlap = seq is not None and tpm.TP_OVERLAP and self.qkv_bias is None
+        if sp_overlap:  # gather chunk-pipelined under the qkv GEMM
             B, T = positions.shape
-            h = sp_gather(h, seq).view(B, T, -1)
-        if seq is None and self.tp is not None and torch.is_grad_enabled():
+            qkv = tpm.sp_gather_linear(h, self.qkv_proj, seq).view(B, T, -1)
+        elif seq is not None:
+            B, T = positions.shape
+            h = tpm.sp_gather(h, seq).view(B, T, -1)
+        if sp_overlap:
+            pass
+        elif seq is None and self.tp is not None and torch.is_grad_enabled():
             from ..parallel.tensor_parallel import col_parallel_linear
 
             qkv = col_parallel_linear(h, self.qkv_proj, self.qkv_bias, self.tp)
@@ -114,7 +120,10 @@ class Attention(nn.Module):
         from ..parallel.tensor_parallel import sp_reduce_scatter, tp_grad_sum, tp_reduce
 
         if seq is not None:
-            out = sp_reduce_scatter(ops.linear(a, self.o_proj, None).reshape(-1, cfg.hidden_size), seq)
+            if tpm.TP_OVERLAP:  # reduce-scatter chunk-pipelined behind the o GEMM
+                out = tpm.sp_linear_reduce_scatter(a.reshape(-1, a.shape[-1]), self.o_proj, seq)
+            else:
+                out = sp_reduce_scatter(ops.linear(a, self.o_proj, None).reshape(-1, cfg.hidden_size), seq)
             return out + tp_grad_sum(self.o_bias, seq) if self.o_bias is not None else out
         from ..parallel.tensor_parallel import row_parallel_linear
 
@@ -152,9 +161,15 @@ class MLP(nn.Module):
     def forward(self, h):
         seq = self.tp_seq if h.dim() == 2 else None
         if seq is not None:
-            from ..parallel.tensor_parallel import sp_gather
+            from ..parallel import tensor_parallel as tpm
 
-            h = sp_gather(h, seq)
+            if tpm.TP_OVERLAP and self.up_bias is None and self.down_bias is None:
+                # Megatron-SP MLP in chunk-major token order (per-token block): the all-gather
+                # pipelined under gate|up, the reduce-scatter behind the down GEMM chunks
+                u = tpm.sp_gather_linear(h, self.up_proj, seq, token_order=False)
+                m = ops.swiglu(u) if self.cfg.activation == "swiglu" else ops.gelu_new(u)
+                return tpm.sp_linear_reduce_scatter(m, self.down_proj, seq, token_order=False)
+            h = tpm.sp_gather(h, seq)
         elif self.tp is not None:
             from ..parallel import tensor_parallel as tpm
 

@@ -153,6 +153,166 @@ class _TPGradSum(torch.autograd.Function):
         return g, None
 
 
+# ------------------------------------------ Megatron-SP collectives overlapped with the GEMMs
+# With DLA_TP_OVERLAP, the sequence-parallel gather -> column-parallel GEMM and row-parallel GEMM
+# -> reduce-scatter pairs run chunk-pipelined instead of as one blocking collective each. The
+# local rows [n, H] are cut into C chunks of m rows; chunk c of EVERY rank is gathered by one
+# async all-gather into a [tp*m, H] block (rows (r, j) = token r*n + c*m + j), so the gathered
+# tensor is "chunk-major" [C][tp][m]. The GEMM of block c runs while block c+1 is in flight; on
+# the way out, the row-parallel GEMM of block c is reduce-scattered (async) straight into this
+# rank's local rows [c*m, (c+1)*m) while block c+1 is multiplied. Per-token ops (the MLP) stay
+# in chunk-major order end to end; attention needs token order, so its qkv output and O input are
+# permuted (one copy of the small per-rank [N, q_l + 2 kv_l] / [N, q_l] tensors). The backward
+# mirrors it: the adjoint all-gathers of dY are issued async up front and consumed chunk by chunk,
+# the adjoint reduce-scatters are launched per chunk and overlap the weight-gradient GEMM.
+def _sp_chunks(n: int, chunks: int) -> int:
+    c = max(1, int(chunks))
+    while c > 1 and (n % c or (n // c) % 8):
+        c -= 1
+    return c
+
+
+def _sp_gather_async(x_local: torch.Tensor, seq: TPSeq, C: int):
+    """x_local [n, K] -> (chunk-major [C*tp*m, K] buffer, per-chunk async all-gather works)."""
+    n, K = x_local.shape
+    m = n // C
+    out = x_local.new_empty((n * seq.tp, K))
+    works = []
+    for c in range(C):
+        works.append(dist.all_gather_into_tensor(out[c * seq.tp * m:(c + 1) * seq.tp * m],
+                                                 x_local[c * m:(c + 1) * m].contiguous(),
+                                                 group=seq.group, async_op=True))
+    return out, works
+
+
+def _to_token_order(t: torch.Tensor, tp: int, C: int) -> torch.Tensor:
+    """chunk-major rows (c, r, j) -> token order (r, c, j)."""
+    M, K = t.shape
+    return t.view(C, tp, M // (C * tp), K).transpose(0, 1).reshape(M, K)
+
+
+def _to_chunk_major(t: torch.Tensor, tp: int, C: int) -> torch.Tensor:
+    M, K = t.shape
+    return t.view(tp, C, M // (C * tp), K).transpose(0, 1).reshape(M, K)
+
+
+def _dgrad_into(dy: torch.Tensor, weight: torch.Tensor, out: torch.Tensor) -> None:
+    """out = dy @ weight through the cached W^T (TN layout) when the engine allows it."""
+    from ..ops.linear import TRANSPOSED_DGRAD, transposed_weight
+
+    if (TRANSPOSED_DGRAD and getattr(weight, "_dla_wt_ok", False) and weight.dtype == torch.bfloat16
+            and _ext.use_native(weight) and weight.shape[0] % 8 == 0 and weight.shape[1] % 8 == 0):
+        torch.mm(dy, transposed_weight(weight).t(), out=out)
+    else:
+        torch.mm(dy, weight, out=out)
+
+
+def _wgrad(ctx_needs: bool, weight: torch.Tensor, dy2: torch.Tensor, x2: torch.Tensor):
+    from ..ops.linear import accumulate_weight_grad
+
+    if not ctx_needs or accumulate_weight_grad(weight, dy2, x2):
+        return None
+    return dy2.t() @ x2
+
+
+class _SPGatherLinearFn(torch.autograd.Function):
+    """y = gather_SP(x) W^T with the all-gather chunk-pipelined under the GEMM; `token_order`
+    False keeps y chunk-major (per-token consumers)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, seq, chunks, token_order):
+        x2 = x.reshape(-1, x.shape[-1])
+        n = x2.shape[0]
+        C = _sp_chunks(n, chunks)
+        xg, works = _sp_gather_async(x2, seq, C)
+        blk = seq.tp * (n // C)
+        y = x2.new_empty((n * seq.tp, weight.shape[0]))
+        for c, w in enumerate(works):
+            w.wait()
+            torch.mm(xg[c * blk:(c + 1) * blk], weight.t(), out=y[c * blk:(c + 1) * blk])
+        ctx.save_for_backward(xg)
+        ctx.weight, ctx.seq, ctx.C, ctx.token_order, ctx.n = weight, seq, C, token_order, n
+        return _to_token_order(y, seq.tp, C) if token_order else y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (xg,) = ctx.saved_tensors
+        seq, C, n, weight = ctx.seq, ctx.C, ctx.n, ctx.weight
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        dy2 = _to_chunk_major(dy2, seq.tp, C) if ctx.token_order else dy2.contiguous()
+        m, blk = n // C, seq.tp * (n // C)
+        dx, works, parts = None, [], []
+        if ctx.needs_input_grad[0]:
+            dx = dy2.new_empty((n, xg.shape[1]))
+            for c in range(C):
+                part = dy2.new_empty((blk, xg.shape[1]))
+                _dgrad_into(dy2[c * blk:(c + 1) * blk], weight, part)
+                parts.append(part)
+                works.append(dist.reduce_scatter_tensor(dx[c * m:(c + 1) * m], part, group=seq.group,
+                                                        async_op=True))
+        dw = _wgrad(ctx.needs_input_grad[1], weight, dy2, xg)  # overlaps the reduce-scatters
+        for w in works:
+            w.wait()
+        return dx, dw, None, None, None
+
+
+class _SPLinearReduceScatterFn(torch.autograd.Function):
+    """reduce_scatter_SP(a W^T) -> this rank's [n, N] rows, the reduce-scatter of token chunk c
+    launched as soon as its GEMM finished; `token_order` False: `a` is already chunk-major."""
+
+    @staticmethod
+    def forward(ctx, a, weight, seq, chunks, token_order):
+        a2 = a.reshape(-1, a.shape[-1])
+        M = a2.shape[0]
+        n = M // seq.tp
+        C = _sp_chunks(n, chunks)
+        a_cm = _to_chunk_major(a2, seq.tp, C) if token_order else a2.contiguous()
+        m, blk = n // C, seq.tp * (n // C)
+        y = a2.new_empty((n, weight.shape[0]))
+        works, parts = [], []
+        for c in range(C):
+            part = torch.mm(a_cm[c * blk:(c + 1) * blk], weight.t())
+            parts.append(part)
+            works.append(dist.reduce_scatter_tensor(y[c * m:(c + 1) * m], part, group=seq.group,
+                                                    async_op=True))
+        for w in works:
+            w.wait()
+        ctx.save_for_backward(a_cm)
+        ctx.weight, ctx.seq, ctx.C, ctx.token_order, ctx.ashape = weight, seq, C, token_order, a.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (a_cm,) = ctx.saved_tensors
+        seq, C, weight = ctx.seq, ctx.C, ctx.weight
+        dyg, works = _sp_gather_async(dy.reshape(-1, dy.shape[-1]).contiguous(), seq, C)
+        blk = dyg.shape[0] // C
+        da = None
+        if ctx.needs_input_grad[0]:
+            da = a_cm.new_empty(a_cm.shape)
+            for c, w in enumerate(works):
+                w.wait()
+                _dgrad_into(dyg[c * blk:(c + 1) * blk], weight, da[c * blk:(c + 1) * blk])
+            if ctx.token_order:
+                da = _to_token_order(da, seq.tp, C)
+            da = da.view(ctx.ashape)
+        else:
+            for w in works:
+                w.wait()
+        dw = _wgrad(ctx.needs_input_grad[1], weight, dyg, a_cm)
+        return da, dw, None, None, None
+
+
+def sp_gather_linear(x, weight, seq: TPSeq, chunks: Optional[int] = None, token_order: bool = True):
+    """Column-parallel GEMM on the SP-gathered input, gather chunk-pipelined (see above)."""
+    return _SPGatherLinearFn.apply(x, weight, seq, chunks or TP_CHUNKS, token_order)
+
+
+def sp_linear_reduce_scatter(a, weight, seq: TPSeq, chunks: Optional[int] = None, token_order: bool = True):
+    """Row-parallel GEMM reduce-scattered over SP, chunk-pipelined (see above)."""
+    return _SPLinearReduceScatterFn.apply(a, weight, seq, chunks or TP_CHUNKS, token_order)
+
+
 def sp_gather(x, seq: TPSeq):
     return _SPGather.apply(x, seq)
 
@@ -330,16 +490,20 @@ class _VPLogprobFn(torch.autograd.Function):
     def forward(ctx, hidden, weight_l, targets, off, group):
         logits_l = F.linear(hidden, weight_l)
         logp_l, lse_l = _local_fwd(logits_l, targets, off)
-        m = lse_l.clone()
-        dist.all_reduce(m, op=dist.ReduceOp.MAX, group=group)
-        se = torch.exp(lse_l - m)
-        dist.all_reduce(se, group=group)
-        lse = m + torch.log(se)
         V_l = weight_l.shape[0]
         t = targets - off
         own = (targets >= 0) & (t >= 0) & (t < V_l)
-        tl = torch.where(own, logp_l + lse_l, torch.zeros_like(logp_l))
-        dist.all_reduce(tl, group=group)
+        tl_l = torch.where(own, logp_l + lse_l, torch.zeros_like(logp_l))
+        # ONE latency-bound collective instead of three (max, sum-exp, target logit all-reduces):
+        # every rank gathers all shards' (lse_r, target logit_r) and reduces them locally in a
+        # fixed rank order (identical result on every rank)
+        tp = dist.get_world_size(group)
+        pair = torch.stack([lse_l.float(), tl_l.float()])
+        allp = pair.new_empty((tp * 2,) + tuple(pair.shape[1:]))
+        dist.all_gather_into_tensor(allp, pair.contiguous(), group=group)
+        allp = allp.view((tp,) + tuple(pair.shape))
+        lse = torch.logsumexp(allp[:, 0], dim=0)
+        tl = allp[:, 1].sum(0)
         logp = torch.where(targets >= 0, tl - lse, torch.zeros_like(tl))
         ctx.save_for_backward(hidden, targets, lse, logits_l)
         ctx.weight_l = weight_l  # (on ctx: see ops.linear._LinearMainGradFn)
@@ -351,18 +515,21 @@ class _VPLogprobFn(torch.autograd.Function):
         hidden, targets, lse, logits_l = ctx.saved_tensors
         weight_l = ctx.weight_l
         dlog = _local_bwd(logits_l, targets, lse, g, ctx.off)
-        dh = None
+        dh, work = None, None
         if ctx.needs_input_grad[0]:
             from ..ops.linear import input_grad
 
             dh = input_grad(dlog, weight_l).contiguous()
-            dist.all_reduce(dh, group=ctx.group)
+            # in flight on RCCL's stream while the (vocab-shard) weight-gradient GEMM runs
+            work = dist.all_reduce(dh, group=ctx.group, async_op=True)
         dw = None
         if ctx.needs_input_grad[1]:
             from ..ops.linear import accumulate_weight_grad
 
             if not accumulate_weight_grad(weight_l, dlog, hidden):
                 dw = dlog.t() @ hidden
+        if work is not None:
+            work.wait()
         return dh, dw, None, None, None
 
 

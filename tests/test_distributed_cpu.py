@@ -779,7 +779,7 @@ def _single_fp32_sum():
 
 
 # ---------------------------------------------------------- Megatron sequence parallel (TP-SP)
-def _tp_seq_vs_tp(rank, world, name, ckpt):
+def _tp_seq_vs_tp(rank, world, name, ckpt, T=12):
     import torch
 
     from distributed_llm_alignment_amd.models import build_model, get_config
@@ -795,9 +795,9 @@ def _tp_seq_vs_tp(rank, world, name, ckpt):
         tps.gradient_checkpointing_enable()
         tps.train()
     g = torch.Generator().manual_seed(5)
-    ids = torch.randint(3, cfg.vocab_size, (2, 12), generator=g)
+    ids = torch.randint(3, cfg.vocab_size, (2, T), generator=g)
     mask = torch.ones_like(ids)
-    mask[1, 9:] = 0
+    mask[1, T - 3:] = 0
     a = dense.sequence_logprob(ids, mask)
     b = tps.sequence_logprob(ids, mask)
     a.sum().backward()
@@ -821,11 +821,17 @@ def _tp_seq_vs_tp(rank, world, name, ckpt):
     return out
 
 
-@pytest.mark.parametrize("name,ckpt", [("tiny-llama", False), ("tiny-gpt2", False), ("tiny-llama", True)])
-def test_tp_sequence_parallel_matches_dense(name, ckpt):
+@pytest.mark.parametrize("name,ckpt,T", [("tiny-llama", False, 12), ("tiny-gpt2", False, 12),
+                                          ("tiny-llama", True, 12), ("tiny-llama", False, 32),
+                                          ("tiny-llama", True, 32)])
+def test_tp_sequence_parallel_matches_dense(name, ckpt, T):
     """TP=2 with Megatron-SP (token-sharded residual stream, reduce-scatter/all-gather, TP-summed
-    norm/bias/wpe grads) == the unsharded model: log-probs and every gradient kind."""
-    res = run_ranks(_tp_seq_vs_tp, 2, (name, ckpt))
+    norm/bias/wpe grads) == the unsharded model: log-probs and every gradient kind. T=32 gives 32
+    local rows per rank, so the overlapped SP GEMMs run 4 chunk-major chunks of 8 rows."""
+    from distributed_llm_alignment_amd.parallel.tensor_parallel import _sp_chunks
+
+    assert _sp_chunks(T * 2 // 2, 4) == (4 if T == 32 else 1)
+    res = run_ranks(_tp_seq_vs_tp, 2, (name, ckpt, T))
     for r in (0, 1):
         a, b, *errs = res[r]
         assert torch.allclose(a, b, atol=1e-5), (a, b)
