@@ -23,6 +23,12 @@ void launch_decode_attn_rope(const bf16_t*, int64_t, const float*, const float*,
                              const int*, const int*, int, float, int, int, int, int, int, float*,
                              float*, bf16_t*, int64_t, int64_t, int*, hipStream_t);
 int decode_num_splits(int Tmax, int B, int Hkv);
+int decode_qkv_attn_splits(int Tmax, int B, int Hkv);
+bool launch_decode_qkv_attn(const bf16_t*, int64_t, const bf16_t*, bf16_t*, int64_t, int, int, int,
+                            const KsFuse&, const float*, const float*, const int*, const int64_t*, int,
+                            bf16_t*, bf16_t*, int64_t, int64_t, int64_t, const int*, const int*, int,
+                            float, int, int, int, int, float*, float*, bf16_t*, int64_t, int64_t, int*,
+                            int*, const int*, int*, hipStream_t);
 void launch_rope_cache(const bf16_t*, int64_t, bf16_t*, bf16_t*, bf16_t*, int64_t, int64_t,
                        int64_t, const int64_t*, const float*, const float*, const int*, int, int,
                        int, int, int, hipStream_t);
@@ -532,6 +538,93 @@ at::Tensor decode_attn_rope(const at::Tensor& qkv, const at::Tensor& cos, const 
   return out;
 }
 
+// Fused decode qkv projection + attention (decode.hip decode_qkv_attn_kernel, B <= 16): s [B, H]
+// the residual stream, ssq [16, nbp] its row-norm partials, wt the tiled qkv weight with the
+// RMSNorm weight folded in ([N/16, H/32, 4, 16, 8]); then the decode attention of the newest token
+// with its rope + cache write. sync_cnt: this layer's arrival counter (int32, zeroed by the cache
+// at prefill), len_first: kv_len of the first decode step, err: sticky wait-timeout word.
+// Returns the attention output [B, Hq, D], or an undefined tensor when the shape is outside the
+// fused kernel (the caller runs the two launches).
+at::Tensor decode_qkv_attn(const at::Tensor& s, const at::Tensor& ssq, const at::Tensor& wt, double eps,
+                           const at::Tensor& cos, const at::Tensor& sin, const at::Tensor& pos,
+                           at::Tensor& k_cache, at::Tensor& v_cache, const at::Tensor& slot,
+                           const at::Tensor& kv_len, const c10::optional<at::Tensor>& kv_start,
+                           int64_t window, double scale, int64_t Hq, int64_t Hkv, int64_t D, int64_t rot,
+                           at::Tensor& sync_cnt, const at::Tensor& len_first, at::Tensor& err) {
+  check_bf16(s, "s");
+  check_bf16(wt, "wt");
+  check_bf16(k_cache, "k_cache");
+  check_bf16(v_cache, "v_cache");
+  check_f32(cos, "cos");
+  check_f32(sin, "sin");
+  check_i32(pos, "pos");
+  check_i32(kv_len, "kv_len");
+  check_i32(sync_cnt, "sync_cnt");
+  check_i32(len_first, "len_first");
+  check_i32(err, "err");
+  check_cuda(slot, "slot");
+  TORCH_CHECK(slot.scalar_type() == at::kLong && slot.numel() >= 1, "slot int64");
+  TORCH_CHECK(ssq.scalar_type() == at::kFloat && ssq.dim() == 2 && ssq.size(0) == 16 && ssq.is_contiguous() &&
+                  ssq.size(1) >= 1 && ssq.size(1) <= 512,
+              "ssq fp32 [16, nbp <= 512] contiguous");
+  TORCH_CHECK(wt.dim() == 5 && wt.size(2) == 4 && wt.size(3) == 16 && wt.size(4) == 8 && wt.is_contiguous(),
+              "wt tiled [N/16, K/32, 4, 16, 8]");
+  const int64_t M = s.size(0), N = wt.size(0) * 16, K = wt.size(1) * 32;
+  TORCH_CHECK(s.dim() == 2 && s.size(1) == K && s.stride(1) == 1 && s.stride(0) % 8 == 0 && M >= 1 && M <= 16,
+              "s [B <= 16, K] with 16-byte aligned rows");
+  TORCH_CHECK(N == (Hq + 2 * Hkv) * D, "qkv weight rows must be (Hq + 2 Hkv) * D");
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(0) == M && k_cache.size(2) == Hkv && k_cache.size(3) == D &&
+                  k_cache.sizes() == v_cache.sizes() && k_cache.strides() == v_cache.strides() &&
+                  k_cache.stride(3) == 1 && k_cache.stride(1) % 8 == 0 && k_cache.stride(2) % 8 == 0 &&
+                  k_cache.stride(0) % 8 == 0,
+              "caches [B, Tmax, Hkv, D], 16-byte aligned rows");
+  TORCH_CHECK(rot % 16 == 0 && rot <= D && rot > 0, "rot % 16 == 0, 0 < rot <= D");
+  TORCH_CHECK(cos.is_contiguous() && sin.is_contiguous() && cos.size(-1) == rot / 2, "rope tables");
+  TORCH_CHECK(pos.numel() == M && pos.is_contiguous(), "pos [B]");
+  TORCH_CHECK(sync_cnt.numel() >= 1 && len_first.numel() >= 1 && err.numel() >= 1, "sync words");
+  check_aligned16(s, "s");
+  check_aligned16(wt, "wt");
+  check_aligned16(k_cache, "k_cache");
+  check_aligned16(v_cache, "v_cache");
+  const int* ks = nullptr;
+  if (kv_start && kv_start->defined()) {
+    check_i32(*kv_start, "kv_start");
+    TORCH_CHECK(kv_start->numel() == M && kv_start->is_contiguous(), "kv_start [B]");
+    ks = kv_start->data_ptr<int>();
+  }
+  const int64_t G = Hq / Hkv;
+  TORCH_CHECK(skinny_use_ksplit((int)N, (int)K) && Hq % Hkv == 0 && (G == 1 || G == 2 || G == 4 || G == 8) &&
+                  (D == 64 || D == 128),
+              "decode_qkv_attn: N < 16384, N % 16 == 0, K % 1024 == 0, GQA group 1/2/4/8, head_dim 64/128");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(s.device());
+  const int64_t Tmax = k_cache.size(1);
+  const int nsplit = decode_qkv_attn_splits((int)Tmax, (int)M, (int)Hkv);
+  TORCH_CHECK(nsplit <= 8, "decode_qkv_attn: more than 8 key splits (use the two-launch path)");
+  int* ccnt = nsplit > 1 ? decode_counters(s, M * Hkv) : nullptr;
+  TORCH_CHECK(nsplit == 1 || ccnt != nullptr,
+              "decode_qkv_attn: split-combine counters unavailable (first call inside a capture, or "
+              "DLA_DECODE_FUSED_COMBINE=0)");
+  KsFuse fz{};
+  fz.ssq_in = ssq.data_ptr<float>();
+  fz.nbp = static_cast<int>(ssq.size(1));
+  fz.eps = static_cast<float>(eps);
+  auto qkv = at::empty({M, N}, s.options());
+  auto fopt = s.options().dtype(at::kFloat);
+  auto part_o = at::empty({M, Hq, nsplit, D}, fopt);
+  auto part_ml = at::empty({M, Hq, nsplit, 2}, fopt);
+  auto out = at::empty({M, Hq, D}, s.options());
+  const bool ok = launch_decode_qkv_attn(
+      cbp(s), s.stride(0), cbp(wt), bp(qkv), qkv.stride(0), (int)M, (int)N, (int)K, fz,
+      cos.data_ptr<float>(), sin.data_ptr<float>(), pos.data_ptr<int>(), slot.data_ptr<int64_t>(), (int)rot,
+      bp(k_cache), bp(v_cache), k_cache.stride(0), k_cache.stride(1), k_cache.stride(2),
+      kv_len.data_ptr<int>(), ks, static_cast<int>(window), static_cast<float>(scale * 1.4426950408889634),
+      (int)Hq, (int)Hkv, (int)D, (int)Tmax, part_o.data_ptr<float>(), part_ml.data_ptr<float>(), bp(out),
+      out.stride(0), out.stride(1), ccnt, sync_cnt.data_ptr<int>(), len_first.data_ptr<int>(),
+      err.data_ptr<int>(), cur_stream(s));
+  TORCH_CHECK(ok, "decode_qkv_attn: shape outside the fused kernel");
+  return out;
+}
+
 at::Tensor sample_tokens(const at::Tensor& logits, double temperature, int64_t top_k,
                          double top_p, bool greedy, const at::Tensor& rng) {
   check_cuda(logits, "logits");
@@ -568,6 +661,7 @@ TORCH_LIBRARY_FRAGMENT(dla, m) {
   m.def("decode_attn(Tensor q, Tensor k_cache, Tensor v_cache, Tensor kv_len, Tensor? kv_start, int window, float scale) -> Tensor");
   m.def("rope_cache_write(Tensor qkv, Tensor cos, Tensor sin, Tensor pos, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor slot, int Hq, int Hkv, int D, int rot) -> Tensor");
   m.def("decode_attn_rope(Tensor qkv, Tensor cos, Tensor sin, Tensor pos, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor slot, Tensor kv_len, Tensor? kv_start, int window, float scale, int Hq, int Hkv, int D, int rot) -> Tensor");
+  m.def("decode_qkv_attn(Tensor s, Tensor ssq, Tensor wt, float eps, Tensor cos, Tensor sin, Tensor pos, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor slot, Tensor kv_len, Tensor? kv_start, int window, float scale, int Hq, int Hkv, int D, int rot, Tensor(c!) sync_cnt, Tensor len_first, Tensor(d!) err) -> Tensor");
   m.def("sample_tokens(Tensor logits, float temperature, int top_k, float top_p, bool greedy, Tensor rng) -> Tensor");
   m.def("skinny_gemm(Tensor x, Tensor w, Tensor(a!) counters, bool swiglu, bool glu_out=False) -> Tensor");
   m.def("skinny_glu_norm(Tensor x, Tensor res, Tensor norm_w, float eps, Tensor w) -> (Tensor, Tensor)");
@@ -581,6 +675,7 @@ TORCH_LIBRARY_FRAGMENT(dla, m) {
 TORCH_LIBRARY_IMPL(dla, CUDA, m) {
   m.impl("decode_attn", &dla::decode_attn);
   m.impl("sample_tokens", &dla::sample_tokens);
+  m.impl("decode_qkv_attn", &dla::decode_qkv_attn);
   m.impl("rope_cache_write", &dla::rope_cache_write);
   m.impl("decode_attn_rope", &dla::decode_attn_rope);
   m.impl("skinny_gemm", &dla::skinny_gemm);

@@ -15,6 +15,7 @@
 #include <cstdlib>
 
 #include "common.h"
+#include "skinny_ks.h"
 
 namespace dla {
 
@@ -104,7 +105,7 @@ __global__ __launch_bounds__(256, 3) void decode_attn_kernel(
     const int* __restrict__ kv_start, int window, float scale_log2, int nsplit,
     float* __restrict__ part_o,  // [B, Hq, nsplit, D]
     float* __restrict__ part_ml, // [B, Hq, nsplit, 2]
-    int Hq, DecRope rp) {
+    int Hq, DecRope rp, int Tcap) {
   constexpr int LPK = D / 8, KPI = 64 / LPK, KPW = kDecChunk / 4, NIT = KPW / KPI;
   constexpr int KST = D / 32;  // MFMA k-steps over the head dim
   static_assert(G <= 16 && KPW == 32, "decode tile geometry");
@@ -137,8 +138,24 @@ __global__ __launch_bounds__(256, 3) void decode_attn_kernel(
       store_bf16x8(vc + (int64_t)b * c_sb + (int64_t)newest * c_st + (int64_t)hk * c_sh + dl, vnew);
     }
   }
-  if (window > 0) lo = max(lo, len - window);
   const int base = split * kDecChunk;
+  const int kw0 = base + wv * KPW;  // this wave's first key
+  const bf16_t* kb0 = kc + (int64_t)b * c_sb + (int64_t)hk * c_sh;
+  const bf16_t* vb0 = vc + (int64_t)b * c_sb + (int64_t)hk * c_sh + dl;
+  // ---- all loads up front. K rows are clamped only into the cache capacity, so they leave at
+  // kernel start without waiting for kv_len / kv_start (rows outside [k0, k1) are masked out of
+  // the scores: whatever they hold is discarded); V rows are clamped into [k0, k1) (a masked
+  // key's weight is 0 and its row must be finite). The newest key's rotated K / raw V (a
+  // dependent chain through pos -> cos / sin) replace their registers only afterwards.
+  s16x8 kf[2][KST];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int kcl = min(kw0 + 16 * t + r16, Tcap - 1);
+#pragma unroll
+    for (int s = 0; s < KST; ++s)
+      kf[t][s] = __builtin_bit_cast(s16x8, load_bf16x8(kb0 + (int64_t)kcl * c_st + 32 * s + 8 * kg));
+  }
+  if (window > 0) lo = max(lo, len - window);
   const int k0 = max(base, lo), k1 = min(base + kDecChunk, len);
   const int64_t pbase = ((int64_t)b * Hq + (int64_t)hk * G) * nsplit + split;
   if (k0 >= k1) {  // empty split (beyond the current length or fully masked)
@@ -147,20 +164,6 @@ __global__ __launch_bounds__(256, 3) void decode_attn_kernel(
       part_ml[(pbase + (int64_t)tid * nsplit) * 2 + 1] = 0.f;
     }
     return;
-  }
-  const int kw0 = base + wv * KPW;  // this wave's first key
-  const bf16_t* kb0 = kc + (int64_t)b * c_sb + (int64_t)hk * c_sh;
-  const bf16_t* vb0 = vc + (int64_t)b * c_sb + (int64_t)hk * c_sh + dl;
-  // ---- all loads up front (keys clamped into [k0, k1): unconditional, masked later). The bulk
-  // K / V loads go out before anything that waits on memory: the newest key's rotated K / raw V
-  // (a dependent chain through pos -> cos / sin) replace their registers only afterwards.
-  s16x8 kf[2][KST];
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int kcl = min(max(kw0 + 16 * t + r16, k0), k1 - 1);
-#pragma unroll
-    for (int s = 0; s < KST; ++s)
-      kf[t][s] = __builtin_bit_cast(s16x8, load_bf16x8(kb0 + (int64_t)kcl * c_st + 32 * s + 8 * kg));
   }
   bf16x8 vvr[NIT];
 #pragma unroll
@@ -171,7 +174,7 @@ __global__ __launch_bounds__(256, 3) void decode_attn_kernel(
   if constexpr (ROPE) {
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      if (min(max(kw0 + 16 * t + r16, k0), k1 - 1) == newest) {
+      if (min(kw0 + 16 * t + r16, Tcap - 1) == newest) {
 #pragma unroll
         for (int s = 0; s < KST; ++s)
           kf[t][s] = __builtin_bit_cast(s16x8, dec_rope8(qrow + (int64_t)(Hq + hk) * D, 32 * s + 8 * kg, rp.rot, cs, sn));
@@ -415,14 +418,20 @@ __device__ __forceinline__ void dec_glds16(const void* src, void* lds_base) {
                                    (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
 }
 
-template <int D, int G, bool ROPE>
-__global__ __launch_bounds__(256, 2) void decode_attn_loop_kernel(
+// The loop kernel's body, shared with the fused qkv-projection + attention kernel below. WAITQ:
+// the qkv row of the newest token (q, k, v) is produced by other workgroups of the same launch;
+// the body issues every load that does not depend on it (the first two chunks' K / V), then
+// calls wait() and only then reads q and writes the newest K / V into the cache.
+template <int D, int G, bool ROPE, bool WAITQ = false, int RD = 2, class Wait>
+__device__ __forceinline__ void dec_loop_body(
+    const int split, const int hk, const int b, const int Hkv_grid,
     const bf16_t* __restrict__ q, int64_t q_sb, int64_t q_sh,
     bf16_t* __restrict__ kc, bf16_t* __restrict__ vc,
     int64_t c_sb, int64_t c_st, int64_t c_sh, const int* __restrict__ kv_len,
     const int* __restrict__ kv_start, int window, float scale_log2, int nsplit, int cpb,
-    float* __restrict__ part_o, float* __restrict__ part_ml, int Hq, DecRope rp,
-    bf16_t* __restrict__ out, int64_t o_sb, int64_t o_sh, int* __restrict__ cnt) {
+    float* __restrict__ part_o, float* __restrict__ part_ml, int Hq, const DecRope& rp,
+    bf16_t* __restrict__ out, int64_t o_sb, int64_t o_sh, int* __restrict__ cnt, int Tcap,
+    Wait&& wait) {
   // out != nullptr, cnt == nullptr (one split per sequence): the block writes the normalised bf16
   // output itself; out and cnt (nsplit > 1): partials + in-kernel combine (dec_arrive_combine).
   // Either way the combine launch is skipped.
@@ -430,10 +439,11 @@ __global__ __launch_bounds__(256, 2) void decode_attn_loop_kernel(
   constexpr int KST = D / 32;
   static_assert(G <= 16 && KPW == 32, "decode tile geometry");
   static_assert(G * D * 4 <= KPW * D * 2, "acc_s aliases one V image slot");
+  static_assert(!WAITQ || ROPE, "the fused qkv form reads the raw qkv row");
   // per wave: 2 V image slots (LDS-DMA ring), the first re-used for the wave's partial O
-  __shared__ __attribute__((aligned(16))) bf16_t vimg[4][2][KPW * D];
+  static_assert(RD == 1 || RD == 2, "ring depth");
+  __shared__ __attribute__((aligned(16))) bf16_t vimg[4][RD][KPW * D];
   __shared__ float mls[4][G][2];
-  const int split = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int len = kv_len[0];
   int lo = kv_start ? kv_start[b] : 0;
@@ -443,30 +453,58 @@ __global__ __launch_bounds__(256, 2) void decode_attn_loop_kernel(
   const bf16_t* qrow = nullptr;
   const float *cs = nullptr, *sn = nullptr;
   const int cfirst = split * cpb;
+  auto cache_write = [&]() {  // the newest key's rotated K / raw V into its cache slot
+    if constexpr (ROPE) {
+      const int cn = newest / kDecChunk;
+      if (cn >= cfirst && cn < cfirst + cpb && wv == 0 && lane < LPK) {
+        const bf16x8 vnew = load_bf16x8(qrow + (int64_t)(Hq + rp.Hkv + hk) * D + dl);
+        const bf16x8 knew = dec_rope8(qrow + (int64_t)(Hq + hk) * D, dl, rp.rot, cs, sn);
+        store_bf16x8(kc + (int64_t)b * c_sb + (int64_t)newest * c_st + (int64_t)hk * c_sh + dl, knew);
+        store_bf16x8(vc + (int64_t)b * c_sb + (int64_t)newest * c_st + (int64_t)hk * c_sh + dl, vnew);
+      }
+    }
+  };
   if constexpr (ROPE) {
     newest = static_cast<int>(rp.slot[0]);
     qrow = rp.qkv + (int64_t)b * rp.ld;
     const int half = rp.rot >> 1;
     cs = rp.cos_t + (int64_t)rp.pos[b] * half;
     sn = rp.sin_t + (int64_t)rp.pos[b] * half;
-    const int cn = newest / kDecChunk;
-    if (cn >= cfirst && cn < cfirst + cpb && wv == 0 && lane < LPK) {  // cache write for later steps
-      const bf16x8 vnew = load_bf16x8(qrow + (int64_t)(Hq + rp.Hkv + hk) * D + dl);
-      const bf16x8 knew = dec_rope8(qrow + (int64_t)(Hq + hk) * D, dl, rp.rot, cs, sn);
-      store_bf16x8(kc + (int64_t)b * c_sb + (int64_t)newest * c_st + (int64_t)hk * c_sh + dl, knew);
-      store_bf16x8(vc + (int64_t)b * c_sb + (int64_t)newest * c_st + (int64_t)hk * c_sh + dl, vnew);
-    }
+    if constexpr (!WAITQ) cache_write();
   }
+  const bf16_t* kb0 = kc + (int64_t)b * c_sb + (int64_t)hk * c_sh;
+  const bf16_t* vb0 = vc + (int64_t)b * c_sb + (int64_t)hk * c_sh;
+  // 2-slot ring: K as MFMA A fragments in registers, V by LDS-DMA straight into the wave's
+  // swizzled image (lane-linear destination, the swizzle applied on the per-lane SOURCE chunk:
+  // image row it * KPI + sub, position dl / 8 holds logical chunk (dl / 8) ^ f(row)). K rows are
+  // clamped only into the chunk and the cache capacity (no kv_len / kv_start dependence: the
+  // first chunk's K loads leave at kernel start, beside the scalar length loads; rows outside
+  // the visible range are masked out of the scores, so whatever they hold is discarded); V rows
+  // are clamped into the visible range (a masked key's weight is 0 and its V row must be finite).
+  s16x8 kf[RD][2][KST];
+  auto loadK = [&](auto J, int c) {
+    constexpr int j = decltype(J)::value;
+    const int kw0 = c * kDecChunk + wv * KPW;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int kcl = min(kw0 + 16 * t + r16, Tcap - 1);
+#pragma unroll
+      for (int s = 0; s < KST; ++s)
+        kf[j][t][s] = __builtin_bit_cast(s16x8, load_bf16x8(kb0 + (int64_t)kcl * c_st + 32 * s + 8 * kg));
+    }
+  };
+  loadK(std::integral_constant<int, 0>{}, cfirst);  // speculative: the split's first chunk
   if (window > 0) lo = max(lo, len - window);
   // chunks [cbeg, cend) of this split that hold visible keys
   const int cbeg = max(cfirst, lo / kDecChunk);
   const int cend = min(cfirst + cpb, (len + kDecChunk - 1) / kDecChunk);
   const int64_t pbase = ((int64_t)b * Hq + (int64_t)hk * G) * nsplit + split;
   const bool fuse = cnt != nullptr;
-  int* const cslot = fuse ? cnt + (int64_t)b * gridDim.y + hk : nullptr;
+  int* const cslot = fuse ? cnt + (int64_t)b * Hkv_grid + hk : nullptr;
   const int64_t pbase0 = ((int64_t)b * Hq + (int64_t)hk * G) * nsplit;
   const int64_t obase = (int64_t)b * o_sb + (int64_t)hk * G * o_sh;
   if (cbeg >= cend || max(cbeg * kDecChunk, lo) >= len) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the speculative K loads
     if (out != nullptr && !fuse) {  // no visible key: zeros, as the combine writes for an all-empty row
       for (int i = tid; i < G * D; i += 256)
         out[(int64_t)b * o_sb + (int64_t)(hk * G + i / D) * o_sh + i % D] = 0;
@@ -479,36 +517,26 @@ __global__ __launch_bounds__(256, 2) void decode_attn_loop_kernel(
     if (fuse) dec_arrive_combine<D, G>(cslot, part_o, part_ml, pbase0, nsplit, out, obase, o_sh);
     return;
   }
-  // q fragments first (the oldest loads: S of chunk 0 waits for them and K(0) only)
+  // q fragments (unfused: first, the oldest loads: S of chunk 0 waits for them and K(0) only;
+  // WAITQ: after the chunk prefetch and the wait)
   s16x8 qf[KST];
+  auto load_q = [&]() {
 #pragma unroll
-  for (int s = 0; s < KST; ++s) {
-    qf[s] = s16x8{};
-    if (r16 < G) {
-      if constexpr (ROPE)
-        qf[s] = __builtin_bit_cast(s16x8, dec_rope8(qrow + (int64_t)(hk * G + r16) * D, 32 * s + 8 * kg, rp.rot, cs, sn));
-      else
-        qf[s] = __builtin_bit_cast(s16x8, load_bf16x8(q + (int64_t)b * q_sb + (int64_t)(hk * G + r16) * q_sh + 32 * s + 8 * kg));
+    for (int s = 0; s < KST; ++s) {
+      qf[s] = s16x8{};
+      if (r16 < G) {
+        if constexpr (ROPE)
+          qf[s] = __builtin_bit_cast(s16x8, dec_rope8(qrow + (int64_t)(hk * G + r16) * D, 32 * s + 8 * kg, rp.rot, cs, sn));
+        else
+          qf[s] = __builtin_bit_cast(s16x8, load_bf16x8(q + (int64_t)b * q_sb + (int64_t)(hk * G + r16) * q_sh + 32 * s + 8 * kg));
+      }
     }
-  }
-  const bf16_t* kb0 = kc + (int64_t)b * c_sb + (int64_t)hk * c_sh;
-  const bf16_t* vb0 = vc + (int64_t)b * c_sb + (int64_t)hk * c_sh;
-  // 2-slot ring: K as MFMA A fragments in registers, V by LDS-DMA straight into the wave's
-  // swizzled image (lane-linear destination, the swizzle applied on the per-lane SOURCE chunk:
-  // image row it * KPI + sub, position dl / 8 holds logical chunk (dl / 8) ^ f(row)); keys
-  // clamped into the chunk's visible range. Issue order per chunk: K then V.
-  s16x8 kf[2][2][KST];
-  auto load = [&](auto J, int c) {
+  };
+  if constexpr (!WAITQ) load_q();
+  auto loadV = [&](auto J, int c) {
     constexpr int j = decltype(J)::value;
     const int base = c * kDecChunk, k0 = max(base, lo), k1 = min(base + kDecChunk, len);
     const int kw0 = base + wv * KPW;
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const int kcl = min(max(kw0 + 16 * t + r16, k0), k1 - 1);
-#pragma unroll
-      for (int s = 0; s < KST; ++s)
-        kf[j][t][s] = __builtin_bit_cast(s16x8, load_bf16x8(kb0 + (int64_t)kcl * c_st + 32 * s + 8 * kg));
-    }
     bf16_t* img = &vimg[wv][j][0];
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
@@ -517,6 +545,10 @@ __global__ __launch_bounds__(256, 2) void decode_attn_loop_kernel(
       const int ch = (dec_swz<D>(row, dl >> 3) - row * D) >> 3;  // position dl/8 <-> chunk ch
       dec_glds16(vb0 + (int64_t)key * c_st + ch * 8, img + it * 512);
     }
+  };
+  auto load = [&](auto J, int c) {  // issue order per chunk: K then V
+    loadK(J, c);
+    loadV(J, c);
   };
   float m_run = -INFINITY, l_run = 0.f;
   f32x4 oacc[D / 16];
@@ -531,7 +563,7 @@ __global__ __launch_bounds__(256, 2) void decode_attn_loop_kernel(
       if (newest_here) {
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
-          if (min(max(kw0 + 16 * t + r16, k0), k1 - 1) == newest) {
+          if (min(kw0 + 16 * t + r16, Tcap - 1) == newest) {
 #pragma unroll
             for (int s = 0; s < KST; ++s)
               kf[j][t][s] = __builtin_bit_cast(s16x8, dec_rope8(qrow + (int64_t)(Hq + hk) * D, 32 * s + 8 * kg, rp.rot, cs, sn));
@@ -581,7 +613,7 @@ __global__ __launch_bounds__(256, 2) void decode_attn_loop_kernel(
     for (int i = 0; i < 4; ++i) ai[i] = __shfl(alpha, 4 * kg + i, 64);
     // V(c) has landed once every VMEM op but the next chunk's (2 KST K loads + NIT V pieces,
     // issued after it) is done; the compiler does not see the DMA -> LDS dependence
-    if (c + 1 < cend) {
+    if (RD == 2 && c + 1 < cend) {
       if constexpr (2 * KST + NIT == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
       else if constexpr (2 * KST + NIT == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -608,17 +640,25 @@ __global__ __launch_bounds__(256, 2) void decode_attn_loop_kernel(
       for (int i = 0; i < 4; ++i) o[i] *= ai[i];
       oacc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vb, o, 0, 0, 0);
     }
-    if (c + 2 < cend) {
+    if (c + RD < cend) {
       // WAR: this slot's transposed reads are complete before the DMA refill is issued
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      load(J, c + 2);
+      load(J, c + RD);
     }
   };
-  load(std::integral_constant<int, 0>{}, cbeg);
-  if (cbeg + 1 < cend) load(std::integral_constant<int, 1>{}, cbeg + 1);
-  for (int c = cbeg; c < cend; c += 2) {
+  if (cbeg != cfirst) loadK(std::integral_constant<int, 0>{}, cbeg);  // left padding: the guess was wrong
+  loadV(std::integral_constant<int, 0>{}, cbeg);
+  if constexpr (RD == 2)
+    if (cbeg + 1 < cend) load(std::integral_constant<int, RD - 1>{}, cbeg + 1);
+  if constexpr (WAITQ) {  // every load above is independent of this step's qkv row
+    wait();
+    cache_write();
+    load_q();
+  }
+  for (int c = cbeg; c < cend; c += RD) {
     step(std::integral_constant<int, 0>{}, c);
-    if (c + 1 < cend) step(std::integral_constant<int, 1>{}, c + 1);
+    if constexpr (RD == 2)
+      if (c + 1 < cend) step(std::integral_constant<int, RD - 1>{}, c + 1);
   }
   // this wave's partial O into its own (dead) first image slot
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -659,6 +699,145 @@ __global__ __launch_bounds__(256, 2) void decode_attn_loop_kernel(
     }
   }
   if (fuse) dec_arrive_combine<D, G>(cslot, part_o, part_ml, pbase0, nsplit, out, obase, o_sh);
+}
+
+template <int D, int G, bool ROPE>
+__global__ __launch_bounds__(256, 2) void decode_attn_loop_kernel(
+    const bf16_t* __restrict__ q, int64_t q_sb, int64_t q_sh,
+    bf16_t* __restrict__ kc, bf16_t* __restrict__ vc,
+    int64_t c_sb, int64_t c_st, int64_t c_sh, const int* __restrict__ kv_len,
+    const int* __restrict__ kv_start, int window, float scale_log2, int nsplit, int cpb,
+    float* __restrict__ part_o, float* __restrict__ part_ml, int Hq, DecRope rp,
+    bf16_t* __restrict__ out, int64_t o_sb, int64_t o_sh, int* __restrict__ cnt, int Tcap) {
+  dec_loop_body<D, G, ROPE>(blockIdx.x, blockIdx.y, blockIdx.z, gridDim.y, q, q_sb, q_sh, kc, vc,
+                            c_sb, c_st, c_sh, kv_len, kv_start, window, scale_log2, nsplit, cpb, part_o,
+                            part_ml, Hq, rp, out, o_sb, o_sh, cnt, Tcap, [] {});
+}
+
+// ---------------------------------------------------------------------------------------------
+// Fused decode qkv projection + attention (B <= 16, the fused decode layer; ops/decode.py
+// `qkv_attend`). One launch holds two roles:
+//   * blocks [0, nq): the qkv projection (skinny_ks.h body: RMSNorm folded into the tiled weight,
+//     the row factor from the producer's partials, non-temporal weight stream) -- each block
+//     stores its 16 columns, releases them (agent-scope release fence) and adds 1 to a per-layer
+//     arrival counter;
+//   * blocks [nq, nq + nsplit * Hkv * B): the multi-chunk decode attention (dec_loop_body). A
+//     block first issues everything that does not depend on this token's q / k / v -- the first
+//     two 128-key chunks of its K (registers) and V (LDS-DMA) -- then waits until the counter
+//     shows every qkv block of this step (one lane polls with s_sleep, then one agent-scope
+//     acquire), and only then reads q, rotates it and writes the newest K / V into the cache.
+// So the KV-cache stream of the attention overlaps the qkv weight stream instead of following it
+// (two dependent launches and their ramp / tail become one), and the attention blocks fill the
+// CUs the 1.5 qkv blocks per CU leave uneven. The counter is monotonic within a generation: step
+// k of the decode (kv_len = len_first + k - 1) waits for nq * k arrivals; the cache zeroes it and
+// sets len_first when a prompt is prefilled. No block of the qkv role ever waits, so the launch
+// cannot deadlock whatever the dispatch order; a wait that exceeds ~2^22 polls (far beyond any
+// real step) sets `err` and proceeds instead of hanging the GPU.
+struct DecQkvSync {
+  int* cnt;              // this layer's arrival counter (monotonic within a generation)
+  const int* len_first;  // kv_len of the first decode step since the counter was zeroed
+  int nq;                // qkv-role blocks in the launch
+  int* err;              // sticky: a wait timed out
+};
+
+template <int D, int G>
+__global__ __launch_bounds__(512) void decode_qkv_attn_kernel(
+    const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ Wt,
+    bf16_t* __restrict__ qkv, int64_t ldq, int M, int N, int K, KsFuse fz, int Hkv,
+    bf16_t* __restrict__ kc, bf16_t* __restrict__ vc, int64_t c_sb, int64_t c_st, int64_t c_sh,
+    const int* __restrict__ kv_len, const int* __restrict__ kv_start, int window,
+    float scale_log2, int nsplit, int cpb, float* __restrict__ part_o, float* __restrict__ part_ml,
+    int Hq, DecRope rp, bf16_t* __restrict__ out, int64_t o_sb, int64_t o_sh,
+    int* __restrict__ ccnt, int Tcap, DecQkvSync sy) {
+  const int bid = blockIdx.x;
+  if (bid < sy.nq) {
+    ks_body<2, true, false, 1, kKsUnroll, false, true, true>(bid, sy.nq, x, ldx, Wt, K, qkv, ldq, M, N, K, fz);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave's own stores
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the release's write-back before the add)
+      __hip_atomic_fetch_add(sy.cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
+  if (threadIdx.x >= 256) return;  // the attention role runs on waves 0-3
+  const int a = bid - sy.nq;
+  const int split = a % nsplit, r = a / nsplit, hk = r % Hkv, b = r / Hkv;
+  auto wait = [&]() {
+    if (threadIdx.x == 0) {
+      const int target = sy.nq * (kv_len[0] - sy.len_first[0] + 1);
+      int spins = 0;
+      while (__hip_atomic_load(sy.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > (1 << 22)) {
+          __hip_atomic_store(sy.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+  };
+  dec_loop_body<D, G, true, true, 2>(split, hk, b, Hkv, nullptr, 0, 0, kc, vc, c_sb, c_st, c_sh, kv_len,
+                                  kv_start, window, scale_log2, nsplit, cpb, part_o, part_ml, Hq, rp,
+                                  out, o_sb, o_sh, ccnt, Tcap, wait);
+}
+
+// splits of the fused kernel's attention role: ~256 attention blocks, in-kernel combine (<= 8)
+int decode_qkv_attn_splits(int Tmax, int B, int Hkv) {
+  const int nch = (Tmax + kDecChunk - 1) / kDecChunk;
+  const int64_t blocks = static_cast<int64_t>(B) * Hkv * nch;
+  const int cpb = std::max(1, static_cast<int>((blocks + 255) / 256));
+  return (nch + cpb - 1) / cpb;
+}
+
+// returns false (nothing launched) when the shape is outside the fused kernel's range
+bool launch_decode_qkv_attn(const bf16_t* x, int64_t ldx, const bf16_t* Wt, bf16_t* qkv, int64_t ldq,
+                            int M, int N, int K, const KsFuse& fz, const float* cos_t,
+                            const float* sin_t, const int* pos, const int64_t* slot, int rot,
+                            bf16_t* kc, bf16_t* vc, int64_t c_sb, int64_t c_st, int64_t c_sh,
+                            const int* kv_len, const int* kv_start, int window, float scale_log2,
+                            int Hq, int Hkv, int D, int Tmax, float* part_o, float* part_ml,
+                            bf16_t* out, int64_t o_sb, int64_t o_sh, int* ccnt, int* sync_cnt,
+                            const int* len_first, int* err, hipStream_t st) {
+  const int B = M, G = Hq / Hkv;
+  const int nch = (Tmax + kDecChunk - 1) / kDecChunk;
+  const int nsplit = decode_qkv_attn_splits(Tmax, B, Hkv);
+  const int cpb = (nch + nsplit - 1) / nsplit;
+  if (nsplit > kDecMaxFuse || N % 16 != 0) return false;
+  const int nq = N / 16;
+  const DecRope rp{qkv, ldq, cos_t, sin_t, pos, slot, rot, Hkv};
+  const DecQkvSync sy{sync_cnt, len_first, nq, err};
+  int* const cn = nsplit > 1 ? ccnt : nullptr;
+  const dim3 grid(nq + nsplit * Hkv * B);
+#define DLA_QA(DD, GG)                                                                                 \
+  decode_qkv_attn_kernel<DD, GG><<<grid, 512, 0, st>>>(x, ldx, Wt, qkv, ldq, M, N, K, fz, Hkv, kc, vc, \
+                                                        c_sb, c_st, c_sh, kv_len, kv_start, window,     \
+                                                        scale_log2, nsplit, cpb, part_o, part_ml, Hq,   \
+                                                        rp, out, o_sb, o_sh, cn, Tmax, sy)
+  if (D == 128) {
+    switch (G) {
+      case 1: DLA_QA(128, 1); break;
+      case 2: DLA_QA(128, 2); break;
+      case 4: DLA_QA(128, 4); break;
+      case 8: DLA_QA(128, 8); break;
+      default: return false;
+    }
+  } else if (D == 64) {
+    switch (G) {
+      case 1: DLA_QA(64, 1); break;
+      case 2: DLA_QA(64, 2); break;
+      case 4: DLA_QA(64, 4); break;
+      case 8: DLA_QA(64, 8); break;
+      default: return false;
+    }
+  } else {
+    return false;
+  }
+#undef DLA_QA
+  return true;
 }
 
 // Decode-step prologue: rotate q (-> q_out [B, Hq, D]) and k of the newest token and write k and
@@ -807,12 +986,12 @@ static void launch_decode_d(const bf16_t* q, int64_t q_sb, int64_t q_sh, bf16_t*
     decode_attn_loop_kernel<D, GG, true><<<grid, 256, 0, st>>>(q, q_sb, q_sh, kc, vc, c_sb, c_st, c_sh, \
                                                                kv_len, kv_start, window, scale_log2,    \
                                                                nsplit, cpb, part_o, part_ml, Hq, r0,    \
-                                                               fin, o_sb, o_sh, cn);                    \
+                                                               fin, o_sb, o_sh, cn, Tmax);              \
   else                                                                                                  \
     decode_attn_loop_kernel<D, GG, false><<<grid, 256, 0, st>>>(q, q_sb, q_sh, kc, vc, c_sb, c_st, c_sh, \
                                                                 kv_len, kv_start, window, scale_log2,   \
                                                                 nsplit, cpb, part_o, part_ml, Hq, r0,   \
-                                                                fin, o_sb, o_sh, cn)
+                                                                fin, o_sb, o_sh, cn, Tmax)
     switch (G) {
       case 1: DLA_DECL(1); break;
       case 2: DLA_DECL(2); break;
@@ -830,12 +1009,12 @@ static void launch_decode_d(const bf16_t* q, int64_t q_sb, int64_t q_sh, bf16_t*
     decode_attn_kernel<D, GG, true, PV><<<grid, 256, 0, st>>>(q, q_sb, q_sh, kc, vc, c_sb, c_st, \
                                                               c_sh, kv_len, kv_start, window,    \
                                                               scale_log2, nsplit, part_o,        \
-                                                              part_ml, Hq, r0);                  \
+                                                              part_ml, Hq, r0, Tmax);            \
   else                                                                                           \
     decode_attn_kernel<D, GG, false, PV><<<grid, 256, 0, st>>>(q, q_sb, q_sh, kc, vc, c_sb,      \
                                                                c_st, c_sh, kv_len, kv_start,     \
                                                                window, scale_log2, nsplit,       \
-                                                               part_o, part_ml, Hq, r0)
+                                                               part_o, part_ml, Hq, r0, Tmax)
 #define DLA_DEC(GG)           \
   if (decode_pv_mfma()) {     \
     DLA_DEC2(GG, true);       \

@@ -21,6 +21,7 @@
 //     FIXED order: deterministic.
 #include "common.h"
 #include "skinny_params.h"
+#include "skinny_ks.h"
 
 #include <cstdlib>
 
@@ -32,22 +33,6 @@ constexpr int kSkWaves = 8;           // waves per workgroup; each owns 16 outpu
 constexpr int kSkCols = 16 * kSkWaves;  // output columns (weight rows) per workgroup
 constexpr int kSkUnroll = 8;          // k-steps (32 each) of weight loads in flight per wave
 constexpr int kSkChunk = 32 * kSkUnroll;
-
-__device__ __forceinline__ f32x4 mfma16(s16x8 a, s16x8 b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-}
-
-__device__ __forceinline__ float silu_sk(float g) { return g * sigmoidf_(g); }
-
-// Weight-stream load: with NT the 16-byte load carries the non-temporal hint (each weight byte is
-// read once per decode step by one CU; MI355X_MICROARCH.md "nt-weights").
-template <bool NT>
-__device__ __forceinline__ s16x8 load_w(const bf16_t* p) {
-  if constexpr (NT)
-    return __builtin_bit_cast(s16x8, __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(p)));
-  else
-    return __builtin_bit_cast(s16x8, load_bf16x8(p));
-}
 
 // DLA_SKINNY_NT=1: non-temporal weight loads in every skinny kernel (read once per process)
 bool skinny_nt() {
@@ -102,40 +87,6 @@ struct SkNorm {
 //       stream starts at once, and no per-element normalisation is needed.
 // Deterministic (eager == graph); the rounding differs from the separate-norm path (h is never
 // rounded to bf16; W o w is), so the two agree to bf16 accuracy, not bitwise.
-
-// prefetch (kernel start) of this wave's two rows' partial sums of squares: lane-strided, up to
-// 8 values per row (nbp <= 512)
-struct KsPart {
-  float v[2][8];
-};
-
-__device__ __forceinline__ KsPart ks_part_load(const KsFuse& fz, int M, int wave, int lane) {
-  KsPart p;
-#pragma unroll
-  for (int rr = 0; rr < 2; ++rr) {
-    const int m = 2 * wave + rr;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int i = lane + 64 * j;
-      p.v[rr][j] = (m < M && i < fz.nbp) ? fz.ssq_in[m * fz.nbp + i] : 0.f;
-    }
-  }
-  return p;
-}
-
-// rows 2w, 2w+1 per wave: rstd = rsqrt(sum / K + eps) (in-lane sum in order, then butterfly)
-__device__ __forceinline__ void ks_rstd(const KsPart& p, const KsFuse& fz, int M, int K, int wave,
-                                        int lane, float* rstd_s) {
-#pragma unroll
-  for (int rr = 0; rr < 2; ++rr) {
-    const int m = 2 * wave + rr;
-    float t = 0.f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) t += p.v[rr][j];
-    t = wave_sum(t);
-    if (lane == 0 && m < M) rstd_s[m] = rsqrtf(t / static_cast<float>(K) + fz.eps);
-  }
-}
 
 template <bool SWIGLU, bool GLU_OUT = false, bool NORM = false, bool NTW = false, bool NPRE = false,
           bool TW = false>
@@ -463,9 +414,6 @@ void launch_skinny_gemm(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t l
 // the split-K form slow inside a real decode step), 8 waves per CU for N = 4096. x is read as
 // MFMA A fragments straight from global memory (tiny, L2-resident), in the same two-set ring as
 // the weights.
-constexpr int kKsUnroll = 4;  // k-steps per chunk (one 16-byte W and x load per lane each)
-constexpr int kKsChunk = 32 * kKsUnroll;
-
 // GLU (decode gate|up with the SwiGLU epilogue, W = [gate; up], 2F rows -> m [M, F]): the
 // workgroup owns 16 features; waves 0-3 take the gate rows, waves 4-7 the matching up rows, each
 // over a quarter of K (F / 16 workgroups).
@@ -478,107 +426,7 @@ template <int DEPTH, bool NT, bool GLU, int MT = 1, int UNR = kKsUnroll, bool RE
 __global__ __launch_bounds__(512) void skinny_ksplit_kernel(
     const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ W, int64_t ldw,
     bf16_t* __restrict__ y, int64_t ldy, int M, int N, int K, KsFuse fz = KsFuse{}) {
-  constexpr int CH = 32 * UNR;  // k per ring slot
-  static_assert(!(RES || NIN) || (MT == 1 && !GLU), "fused residual / norm: M <= 16, plain output");
-  __shared__ float red[8][4 * MT][64];
-  __shared__ float rstd_s[16];
-  __shared__ float sqs[16][16];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int r = lane & 15, q = lane >> 4;
-  const int n0 = GLU ? (wave < 4 ? 0 : N >> 1) + blockIdx.x * 16 : blockIdx.x * 16;
-  // per-wave K slice (multiple of kKsChunk, checked on the host)
-  const int kw = GLU ? K >> 2 : K >> 3;
-  const int k0 = (GLU ? (wave & 3) : wave) * kw;
-  const int nchunks = kw / CH;
-  // TW: tiled weight layout (see skinny_gemm_kernel)
-  const bf16_t* wrow = TW ? W + static_cast<int64_t>(n0 >> 4) * 16 * K + (k0 >> 5) * 512 + lane * 8
-                          : W + static_cast<int64_t>(n0 + r) * ldw + k0 + q * 8;
-  bool arow[MT];
-  const bf16_t* xrow[MT];
-#pragma unroll
-  for (int t = 0; t < MT; ++t) {
-    arow[t] = 16 * t + r < M;
-    xrow[t] = x + static_cast<int64_t>(arow[t] ? 16 * t + r : 0) * ldx + k0 + q * 8;
-  }
-  // DEPTH chunks (W and x fragments) in flight: a ring of register sets, refilled as consumed
-  s16x8 b[DEPTH][UNR], a[DEPTH][UNR][MT];
-  auto load = [&](int j, int c) {
-#pragma unroll
-    for (int u = 0; u < UNR; ++u) b[j][u] = load_w<NT>(TW ? wrow + (c * UNR + u) * 512 : wrow + c * CH + u * 32);
-#pragma unroll
-    for (int u = 0; u < UNR; ++u)
-#pragma unroll
-      for (int t = 0; t < MT; ++t) {
-        a[j][u][t] = s16x8{0, 0, 0, 0, 0, 0, 0, 0};
-        if (arow[t]) a[j][u][t] = __builtin_bit_cast(s16x8, load_bf16x8(xrow[t] + c * CH + u * 32));
-      }
-  };
-#pragma unroll
-  for (int j = 0; j < DEPTH; ++j)
-    if (j < nchunks) load(j, j);
-  KsPart part{};
-  if constexpr (NIN) part = ks_part_load(fz, M, wave, lane);  // reduced in the epilogue
-  f32x4 acc[MT];
-#pragma unroll
-  for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int c0 = 0; c0 < nchunks; c0 += DEPTH) {
-#pragma unroll
-    for (int j = 0; j < DEPTH; ++j) {
-      const int c = c0 + j;
-      if (c < nchunks) {
-#pragma unroll
-        for (int u = 0; u < UNR; ++u)
-#pragma unroll
-          for (int t = 0; t < MT; ++t) acc[t] = mfma16(a[j][u][t], b[j][u], acc[t]);
-        if (c + DEPTH < nchunks) load(j, c + DEPTH);
-      }
-    }
-  }
-  // lane holds C[m = 16 t + 4q + i][n = n0 + r]; sum the waves' tiles in wave order (deterministic)
-#pragma unroll
-  for (int t = 0; t < MT; ++t)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) red[wave][4 * t + i][lane] = acc[t][i];
-  if constexpr (NIN) ks_rstd(part, fz, M, K, wave, lane, rstd_s);
-  __syncthreads();
-  for (int e = threadIdx.x; e < 256 * MT; e += 512) {
-    const int ti = e >> 6, l = e & 63;  // ti = 4 t + i
-    const int m = 16 * (ti >> 2) + 4 * (l >> 4) + (ti & 3), n = blockIdx.x * 16 + (l & 15);
-    if constexpr (GLU) {
-      float g = 0.f, u = 0.f;
-#pragma unroll
-      for (int w = 0; w < 4; ++w) g += red[w][ti][l];
-#pragma unroll
-      for (int w = 4; w < 8; ++w) u += red[w][ti][l];
-      // gate / up rounded to bf16 first, exactly as the unfused GEMM + swiglu pair
-      g = bf2f(f2bf(g));
-      u = bf2f(f2bf(u));
-      if (m < M) y[m * ldy + n] = f2bf(silu_sk(g) * u);
-    } else {
-      float t = 0.f;
-#pragma unroll
-      for (int w = 0; w < 8; ++w) t += red[w][ti][l];
-      if constexpr (NIN) t *= m < M ? rstd_s[m] : 0.f;
-      if constexpr (RES) {
-        if (m < M) {
-          const float sv = bf2f(f2bf(bf2f(f2bf(t)) + bf2f(static_cast<bf16_t>(fz.res[m * fz.ldr + n]))));
-          y[m * ldy + n] = f2bf(sv);
-          sqs[m][l & 15] = sv * sv;
-        }
-      } else {
-        if (m < M) y[m * ldy + n] = f2bf(t);
-      }
-    }
-  }
-  if constexpr (RES) {  // per-row partial sum of squares over this workgroup's 16 columns
-    __syncthreads();
-    if (threadIdx.x < M) {
-      float t = 0.f;
-#pragma unroll
-      for (int c = 0; c < 16; ++c) t += sqs[threadIdx.x][c];
-      fz.ssq_out[threadIdx.x * gridDim.x + blockIdx.x] = t;
-    }
-  }
+  ks_body<DEPTH, NT, GLU, MT, UNR, RES, NIN, TW>(blockIdx.x, gridDim.x, x, ldx, W, ldw, y, ldy, M, N, K, fz);
 }
 
 // fused decode-layer launches (KsFuse): the residual-producing projection and the

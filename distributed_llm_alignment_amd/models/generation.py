@@ -55,6 +55,12 @@ class KVCache:
         self._pos = None
         self.slot = torch.zeros(1, dtype=torch.long, device=dev)
         self.kv_len = torch.ones(1, dtype=torch.int32, device=dev)
+        # fused qkv + attention decode kernel (ops.decode.qkv_attend): per-layer arrival counters
+        # of its qkv blocks (monotonic within a generation, zeroed at every prefill), the kv_len of
+        # the first decode step, and a sticky wait-timeout word
+        self.sync = torch.zeros(L, dtype=torch.int32, device=dev)
+        self.len_first = torch.ones(1, dtype=torch.int32, device=dev)
+        self.sync_err = torch.zeros(1, dtype=torch.int32, device=dev)
         self.pos = torch.zeros((batch, 1), dtype=torch.int32, device=dev)
         self.fast_decode = (not self.split and dev.type == "cuda" and dt == torch.bfloat16
                             and ops.decode.decode_supported(self.h_local, Hkv, D))
@@ -125,9 +131,29 @@ class KVCache:
                                kv_start=kv_start, kv_end=None)
         return o.reshape(B, T, self.h_local * cfg.head_dim)
 
+    def attend_fused(self, layer: int, s: torch.Tensor, ssq: torch.Tensor, wt: torch.Tensor, eps: float,
+                     rope, window: int) -> Optional[torch.Tensor]:
+        """One decode step's qkv projection (RMSNorm folded into the tiled weight `wt`, the row
+        factor from the producer's partials `ssq`) and attention in ONE launch (csrc/decode.hip
+        decode_qkv_attn_kernel). None when the step or shape is not eligible."""
+        B = s.shape[0]
+        if not (self.len > 0 and self.len + 1 <= self.max_len and self.fast_decode and rope is not None
+                and rope.rot_dim % 16 == 0 and FUSED_DECODE_ROPE and s.dim() == 2 and B <= 16):
+            return None
+        D = self.cfg.head_dim
+        cos, sin = rope.tables(s.device)
+        o = ops._ext.require().decode_qkv_attn(
+            s, ssq, wt, float(eps), cos, sin, self.pos.view(-1), self.k[layer], self.v[layer], self.slot,
+            self.kv_len, self.kv_start, window, 1.0 / math.sqrt(D), self.h_local, self.kv_local, D,
+            rope.rot_dim, self.sync[layer:layer + 1], self.len_first, self.sync_err)
+        return o.reshape(B, 1, self.h_local * D)
+
     def advance(self, T: int):
         """Host-driven advance (prefill / eager decode) keeping the device state in step."""
         self.len += T
+        if T > 1:  # a (new) prompt: the fused decode kernel's counters start over
+            self.sync.zero_()
+            self.len_first.fill_(self.len + 1)
         self.slot.fill_(self.len)
         self.kv_len.fill_(self.len + 1)
         start = self.kv_start.view(-1, 1) if self.kv_start is not None else 0

@@ -293,9 +293,15 @@ class DecoderLayer(nn.Module):
         if ssq is None:
             h, _ = ops.add_norm(s, None, self.ln1_w, None, cfg.norm_eps, True)
             qkv = _lin(h, at.qkv_proj, None)
+            a = cache.attend(layer_idx, qkv, rope, cfg.sliding_window if cfg.sliding_window else 0)
         else:
-            qkv = ops.decode.skinny_normed(s, ssq, self.ln1_w, cfg.norm_eps, at.qkv_proj)
-        a = cache.attend(layer_idx, qkv, rope, cfg.sliding_window if cfg.sliding_window else 0)
+            window = cfg.sliding_window if cfg.sliding_window else 0
+            # qkv projection + attention in one launch (ops.decode.qkv_attend), else two
+            a = ops.decode.qkv_attend(s, ssq, self.ln1_w, cfg.norm_eps, at.qkv_proj, cache, layer_idx,
+                                      rope, window)
+            if a is None:
+                qkv = ops.decode.skinny_normed(s, ssq, self.ln1_w, cfg.norm_eps, at.qkv_proj)
+                a = cache.attend(layer_idx, qkv, rope, window)
         s2, ssq2 = ops.decode.skinny_residual(a, at.o_proj, s)
         m = ops.decode.skinny_normed(s2, ssq2, self.ln2_w, cfg.norm_eps, mlp.up_proj, glu=True)
         return ops.decode.skinny_residual(m, mlp.down_proj, s2)

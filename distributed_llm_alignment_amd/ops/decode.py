@@ -395,6 +395,40 @@ def skinny_normed(s: torch.Tensor, ssq: torch.Tensor, norm_w: torch.Tensor, eps:
     return y.view(*s.shape[:-1], y.shape[-1])
 
 
+# Fused decode qkv projection + attention (csrc/decode.hip decode_qkv_attn_kernel, B <= 16): the
+# attention blocks prefetch their first KV chunks while the qkv blocks of the same launch stream
+# the qkv weight, then wait on a device counter for this step's q / k / v. DLA_DECODE_QKV_ATTN=0
+# keeps the two launches (skinny_normed + the rope-fused decode attention).
+DECODE_QKV_ATTN = os.environ.get("DLA_DECODE_QKV_ATTN", "1") != "0"
+_DECODE_NT = os.environ.get("DLA_DECODE_NT", "1") != "0"  # the fused kernel streams with nt loads
+
+
+_COMBINE_ON = os.environ.get("DLA_DECODE_FUSED_COMBINE", "1") != "0"
+
+
+def qkv_attn_splits(Tmax: int, B: int, Hkv: int) -> int:
+    """Key splits of the fused kernel's attention role (csrc/decode.hip decode_qkv_attn_splits)."""
+    nch = (Tmax + 127) // 128
+    cpb = max(1, (B * Hkv * nch + 255) // 256)
+    return (nch + cpb - 1) // cpb
+
+
+def qkv_attend(s: torch.Tensor, ssq: torch.Tensor, norm_w: torch.Tensor, eps: float, w: torch.Tensor,
+               cache, layer: int, rope, window: int) -> Optional[torch.Tensor]:
+    """attention(RMSNorm(s) * norm_w @ w^T) for one decode step in one launch, or None."""
+    if not (DECODE_QKV_ATTN and _DECODE_NT and DECODE_TILED >= 1 and getattr(cache, "sync", None) is not None
+            and not isinstance(cache.k, list)):
+        return None
+    s2 = _rows(s)
+    B, K = s2.shape
+    N = w.shape[0]
+    nsplit = qkv_attn_splits(cache.max_len, B, cache.kv_local)
+    if not (B <= 16 and N < 16384 and N % 16 == 0 and K % 1024 == 0 and nsplit <= 8
+            and (nsplit == 1 or _COMBINE_ON)):
+        return None
+    return cache.attend_fused(layer, s2, ssq, folded_weight(w, norm_w, tiled=True), eps, rope, window)
+
+
 def skinny64_linear(x: torch.Tensor, w: torch.Tensor, tiled: bool = False) -> torch.Tensor:
     """y = x @ w^T at 17..64 rows on csrc/skinny64.hip (tests / A/B; `tiled`: through the
     tiled-layout copy of w)."""

@@ -510,6 +510,57 @@ def test_fused_decode_layer_matches_unfused(B, monkeypatch):
     assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("B,T,pad", [(1, 40, False), (5, 300, True), (8, 40, False), (16, 200, True)])
+def test_fused_qkv_attention_matches_two_launches(B, T, pad, monkeypatch):
+    """Decode steps with the qkv projection and the attention in ONE launch (csrc/decode.hip
+    decode_qkv_attn_kernel: attention blocks prefetch KV while the qkv blocks run, then wait on a
+    device counter) against the two-launch path and an fp32 full forward; graph == eager on the
+    fused kernel; the counter reached every step and no wait timed out."""
+    from distributed_llm_alignment_amd import ops
+    from distributed_llm_alignment_amd.models import build_model, generate
+    from distributed_llm_alignment_amd.models.generation import KVCache, clear_graph_cache
+
+    cfg = _fused_cfg()
+    m = build_model(cfg, device=DEV, dtype=torch.bfloat16, seed=4).eval()
+    g = torch.Generator(device=DEV).manual_seed(11)
+    ids = torch.randint(3, cfg.vocab_size, (B, T), device=DEV, generator=g)
+    am = torch.ones_like(ids)
+    if pad:  # left padding: per-row kv_start
+        for r in range(B):
+            am[r, :(7 * r) % 33] = 0
+    steps = [torch.randint(3, cfg.vocab_size, (B, 1), device=DEV, generator=g) for _ in range(3)]
+    outs, caches = {}, {}
+    from distributed_llm_alignment_amd.models.transformer import attention_layout
+
+    kv_start = attention_layout(am)[0] if pad else None
+    with torch.no_grad():
+        for fused in (False, True):
+            monkeypatch.setattr(ops.decode, "DECODE_QKV_ATTN", fused)
+            cache = KVCache(m, B, T + 8, kv_start)
+            m(ids, am if pad else None, cache=cache)
+            outs[fused] = [m(nx, cache=cache).float() for nx in steps]
+            caches[fused] = cache
+        full = torch.cat([ids] + steps, 1)
+        fam = torch.cat([am, torch.ones(B, len(steps), dtype=am.dtype, device=DEV)], 1)
+        ref = m(full, fam if pad else None)[:, -len(steps):].float()
+    cf = caches[True]
+    torch.cuda.synchronize()
+    assert int(cf.sync_err.item()) == 0
+    n_q = m.layers[1].attn.qkv_proj.shape[0] // 16
+    assert int(cf.sync[1].item()) == n_q * len(steps)  # layer 1 ran the fused kernel every step
+    assert int(caches[False].sync[1].item()) == 0
+    err = lambda a, b: float((a - b).norm() / b.norm())  # noqa: E731
+    for k in range(len(steps)):
+        assert err(outs[True][k], outs[False][k]) < 1e-2, k
+        assert err(outs[True][k][:, 0], ref[:, k]) < 3e-2, k
+    monkeypatch.setattr(ops.decode, "DECODE_QKV_ATTN", True)
+    clear_graph_cache()
+    a = generate(m, ids, am, max_new_tokens=12, do_sample=False, eos_token_id=-1, use_graph=False)
+    b = generate(m, ids, am, max_new_tokens=12, do_sample=False, eos_token_id=-1, use_graph=True)
+    clear_graph_cache()
+    assert torch.equal(a, b)
+
+
 def test_fsdp_sharded_policy_generation_matches_unsharded(monkeypatch):
     """A ZeRO-3 policy (layers gathered by forward hooks, freed after each layer) must not take
     the fused decode path, which calls the kernels without Module.__call__ and would read freed
