@@ -621,7 +621,8 @@ at::Tensor decode_qkv_attn(const at::Tensor& s, const at::Tensor& ssq, const at:
       (int)Hq, (int)Hkv, (int)D, (int)Tmax, part_o.data_ptr<float>(), part_ml.data_ptr<float>(), bp(out),
       out.stride(0), out.stride(1), ccnt, sync_cnt.data_ptr<int>(), len_first.data_ptr<int>(),
       err.data_ptr<int>(), cur_stream(s));
-  TORCH_CHECK(ok, "decode_qkv_attn: shape outside the fused kernel");
+  TORCH_CHECK(ok, "decode_qkv_attn: shape outside the fused kernel (more attention units than "
+                  "resident workgroups)");
   return out;
 }
 

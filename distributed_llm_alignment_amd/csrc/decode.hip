@@ -505,6 +505,7 @@ __device__ __forceinline__ void dec_loop_body(
   const int64_t obase = (int64_t)b * o_sb + (int64_t)hk * G * o_sh;
   if (cbeg >= cend || max(cbeg * kDecChunk, lo) >= len) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the speculative K loads
+    if constexpr (WAITQ) wait();  // once on every path, before any other barrier of the block
     if (out != nullptr && !fuse) {  // no visible key: zeros, as the combine writes for an all-empty row
       for (int i = tid; i < G * D; i += 256)
         out[(int64_t)b * o_sb + (int64_t)(hk * G + i / D) * o_sh + i % D] = 0;
@@ -716,27 +717,32 @@ __global__ __launch_bounds__(256, 2) void decode_attn_loop_kernel(
 
 // ---------------------------------------------------------------------------------------------
 // Fused decode qkv projection + attention (B <= 16, the fused decode layer; ops/decode.py
-// `qkv_attend`). One launch holds two roles:
-//   * blocks [0, nq): the qkv projection (skinny_ks.h body: RMSNorm folded into the tiled weight,
-//     the row factor from the producer's partials, non-temporal weight stream) -- each block
-//     stores its 16 columns, releases them (agent-scope release fence) and adds 1 to a per-layer
-//     arrival counter;
-//   * blocks [nq, nq + nsplit * Hkv * B): the multi-chunk decode attention (dec_loop_body). A
-//     block first issues everything that does not depend on this token's q / k / v -- the first
-//     two 128-key chunks of its K (registers) and V (LDS-DMA) -- then waits until the counter
-//     shows every qkv block of this step (one lane polls with s_sleep, then one agent-scope
-//     acquire), and only then reads q, rotates it and writes the newest K / V into the cache.
-// So the KV-cache stream of the attention overlaps the qkv weight stream instead of following it
-// (two dependent launches and their ramp / tail become one), and the attention blocks fill the
-// CUs the 1.5 qkv blocks per CU leave uneven. The counter is monotonic within a generation: step
-// k of the decode (kv_len = len_first + k - 1) waits for nq * k arrivals; the cache zeroes it and
-// sets len_first when a prompt is prefilled. No block of the qkv role ever waits, so the launch
-// cannot deadlock whatever the dispatch order; a wait that exceeds ~2^22 polls (far beyond any
-// real step) sets `err` and proceeds instead of hanging the GPU.
+// `qkv_attend`): ONE launch of exactly as many 512-thread workgroups as fit on the chip at once
+// (one per CU: the host checks the occupancy), each doing two phases:
+//   1. the qkv projection of its share of the 16-column tiles (skinny_ks.h body: RMSNorm folded
+//      into the tiled weight, the row factor from the producer's partials, non-temporal weight
+//      stream), then one agent-scope release and an add of its tile count to a per-layer counter;
+//   2. workgroups [0, na) then run one attention unit each on waves 0-3 (dec_loop_body, a
+//      (split, kv head, sequence) of the multi-chunk decode attention with the in-kernel split
+//      combine). Before phase 1 such a workgroup issues every load that does not depend on this
+//      step's q / k / v -- the first two 128-key chunks of its K (registers) and V (LDS-DMA) --
+//      so the KV-cache stream overlaps the qkv weight stream; after phase 1 one lane polls the
+//      counter (s_sleep) until every tile of this step has arrived, takes one agent-scope acquire,
+//      and only then are q read (rotated) and the newest K / V written into the cache.
+// The tiles are dealt so the work evens out: an attention workgroup takes `ta` tiles, the others
+// `tn`. Two dependent launches with their ramp / tail become one, and no CU idles behind an
+// uneven tile count. The counter is monotonic within a generation: step k of the decode
+// (kv_len = len_first + k - 1) waits for nq * k arrivals; the cache zeroes it and sets len_first
+// when a prompt is prefilled. Every workgroup is resident at once (one per CU), so the waits
+// cannot deadlock; a wait beyond ~2^22 polls (far past any real step) sets `err` and proceeds
+// rather than hanging the GPU. Barrier discipline: phase 1 runs on all 8 waves with the same
+// barrier sequence whichever call site reaches it, and waves 4-7 exit only after it.
 struct DecQkvSync {
   int* cnt;              // this layer's arrival counter (monotonic within a generation)
   const int* len_first;  // kv_len of the first decode step since the counter was zeroed
-  int nq;                // qkv-role blocks in the launch
+  int nq;                // qkv tiles (16 columns each)
+  int na;                // attention units = workgroups [0, na)
+  int ta, tn;            // tiles per attention workgroup / per other workgroup
   int* err;              // sticky: a wait timed out
 };
 
@@ -749,22 +755,30 @@ __global__ __launch_bounds__(512) void decode_qkv_attn_kernel(
     float scale_log2, int nsplit, int cpb, float* __restrict__ part_o, float* __restrict__ part_ml,
     int Hq, DecRope rp, bf16_t* __restrict__ out, int64_t o_sb, int64_t o_sh,
     int* __restrict__ ccnt, int Tcap, DecQkvSync sy) {
-  const int bid = blockIdx.x;
-  if (bid < sy.nq) {
-    ks_body<2, true, false, 1, kKsUnroll, false, true, true>(bid, sy.nq, x, ldx, Wt, K, qkv, ldq, M, N, K, fz);
+  const int bid = blockIdx.x, wave = threadIdx.x >> 6;
+  const bool attn = bid < sy.na;
+  const int t0 = attn ? bid * sy.ta : sy.na * sy.ta + (bid - sy.na) * sy.tn;
+  const int t1 = min(sy.nq, t0 + (attn ? sy.ta : sy.tn));
+  auto qkv_phase = [&]() {  // all 8 waves
+    for (int t = t0; t < t1; ++t) {
+      ks_body<2, true, false, 1, kKsUnroll, false, true, true>(t, sy.nq, x, ldx, Wt, K, qkv, ldq, M, N, K, fz);
+      __syncthreads();  // the reduction buffer is reused by the next tile
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave's own stores
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (threadIdx.x == 0 && t1 > t0) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the release's write-back before the add)
-      __hip_atomic_fetch_add(sy.cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(sy.cnt, t1 - t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+  };
+  if (!attn || wave >= 4) {
+    qkv_phase();
     return;
   }
-  if (threadIdx.x >= 256) return;  // the attention role runs on waves 0-3
-  const int a = bid - sy.nq;
-  const int split = a % nsplit, r = a / nsplit, hk = r % Hkv, b = r / Hkv;
+  const int split = bid % nsplit, r = bid / nsplit, hk = r % Hkv, b = r / Hkv;
   auto wait = [&]() {
+    qkv_phase();
     if (threadIdx.x == 0) {
       const int target = sy.nq * (kv_len[0] - sy.len_first[0] + 1);
       int spins = 0;
@@ -778,19 +792,33 @@ __global__ __launch_bounds__(512) void decode_qkv_attn_kernel(
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    __syncthreads();
+    __syncthreads();  // (waves 4-7 have ended: the barrier counts waves 0-3)
   };
   dec_loop_body<D, G, true, true, 2>(split, hk, b, Hkv, nullptr, 0, 0, kc, vc, c_sb, c_st, c_sh, kv_len,
-                                  kv_start, window, scale_log2, nsplit, cpb, part_o, part_ml, Hq, rp,
-                                  out, o_sb, o_sh, ccnt, Tcap, wait);
+                                     kv_start, window, scale_log2, nsplit, cpb, part_o, part_ml, Hq, rp,
+                                     out, o_sb, o_sh, ccnt, Tcap, wait);
 }
 
-// splits of the fused kernel's attention role: ~256 attention blocks, in-kernel combine (<= 8)
+// splits of the fused kernel's attention units: ~256 units, in-kernel combine (<= 8 splits)
 int decode_qkv_attn_splits(int Tmax, int B, int Hkv) {
   const int nch = (Tmax + kDecChunk - 1) / kDecChunk;
   const int64_t blocks = static_cast<int64_t>(B) * Hkv * nch;
-  const int cpb = std::max(1, static_cast<int>((blocks + 255) / 256));
+  const int cpb = std::max({1, static_cast<int>((blocks + 255) / 256), (nch + kDecMaxFuse - 1) / kDecMaxFuse});
   return (nch + cpb - 1) / cpb;
+}
+
+// workgroups that are resident at once (occupancy x CUs), per instantiation
+template <int D, int G>
+static int qkv_attn_capacity() {
+  static const int cap = [] {
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, decode_qkv_attn_kernel<D, G>, 512, 0) != hipSuccess)
+      return 0;
+    return cus * per;
+  }();
+  return cap;
 }
 
 // returns false (nothing launched) when the shape is outside the fused kernel's range
@@ -807,11 +835,45 @@ bool launch_decode_qkv_attn(const bf16_t* x, int64_t ldx, const bf16_t* Wt, bf16
   const int nsplit = decode_qkv_attn_splits(Tmax, B, Hkv);
   const int cpb = (nch + nsplit - 1) / nsplit;
   if (nsplit > kDecMaxFuse || N % 16 != 0) return false;
-  const int nq = N / 16;
+  int cap = 0;
+  if (D == 128) {
+    switch (G) {
+      case 1: cap = qkv_attn_capacity<128, 1>(); break;
+      case 2: cap = qkv_attn_capacity<128, 2>(); break;
+      case 4: cap = qkv_attn_capacity<128, 4>(); break;
+      case 8: cap = qkv_attn_capacity<128, 8>(); break;
+      default: return false;
+    }
+  } else if (D == 64) {
+    switch (G) {
+      case 1: cap = qkv_attn_capacity<64, 1>(); break;
+      case 2: cap = qkv_attn_capacity<64, 2>(); break;
+      case 4: cap = qkv_attn_capacity<64, 4>(); break;
+      case 8: cap = qkv_attn_capacity<64, 8>(); break;
+      default: return false;
+    }
+  } else {
+    return false;
+  }
+  const int nq = N / 16, na = nsplit * Hkv * B;
+  if (cap <= 0 || na > cap) return false;
+  const int grid = cap;
+  // even the work out: tile bytes 16 K bf16, attention unit bytes cpb chunks of K + V
+  const double wq = 32.0 * K, wa = 2.0 * cpb * kDecChunk * D * 2;
+  const double per = (nq * wq + na * wa) / grid;
+  int ta, tn;
+  if (na >= grid) {
+    ta = (nq + grid - 1) / grid;
+    tn = 0;
+  } else {
+    ta = std::max(0, static_cast<int>((per - wa) / wq + 0.5));
+    ta = std::min(ta, nq / std::max(na, 1));
+    tn = (nq - na * ta + (grid - na) - 1) / (grid - na);
+  }
+  if (static_cast<int64_t>(na) * ta + static_cast<int64_t>(grid - na) * tn < nq) return false;
   const DecRope rp{qkv, ldq, cos_t, sin_t, pos, slot, rot, Hkv};
-  const DecQkvSync sy{sync_cnt, len_first, nq, err};
+  const DecQkvSync sy{sync_cnt, len_first, nq, na, ta, tn, err};
   int* const cn = nsplit > 1 ? ccnt : nullptr;
-  const dim3 grid(nq + nsplit * Hkv * B);
 #define DLA_QA(DD, GG)                                                                                 \
   decode_qkv_attn_kernel<DD, GG><<<grid, 512, 0, st>>>(x, ldx, Wt, qkv, ldq, M, N, K, fz, Hkv, kc, vc, \
                                                         c_sb, c_st, c_sh, kv_len, kv_start, window,     \
@@ -822,19 +884,15 @@ bool launch_decode_qkv_attn(const bf16_t* x, int64_t ldx, const bf16_t* Wt, bf16
       case 1: DLA_QA(128, 1); break;
       case 2: DLA_QA(128, 2); break;
       case 4: DLA_QA(128, 4); break;
-      case 8: DLA_QA(128, 8); break;
-      default: return false;
+      default: DLA_QA(128, 8); break;
     }
-  } else if (D == 64) {
+  } else {
     switch (G) {
       case 1: DLA_QA(64, 1); break;
       case 2: DLA_QA(64, 2); break;
       case 4: DLA_QA(64, 4); break;
-      case 8: DLA_QA(64, 8); break;
-      default: return false;
+      default: DLA_QA(64, 8); break;
     }
-  } else {
-    return false;
   }
 #undef DLA_QA
   return true;

@@ -406,10 +406,20 @@ _DECODE_NT = os.environ.get("DLA_DECODE_NT", "1") != "0"  # the fused kernel str
 _COMBINE_ON = os.environ.get("DLA_DECODE_FUSED_COMBINE", "1") != "0"
 
 
+_CUS = {}
+
+
+def _cu_count(dev: torch.device) -> int:
+    n = _CUS.get(dev.index)
+    if n is None:
+        n = _CUS[dev.index] = torch.cuda.get_device_properties(dev).multi_processor_count
+    return n
+
+
 def qkv_attn_splits(Tmax: int, B: int, Hkv: int) -> int:
     """Key splits of the fused kernel's attention role (csrc/decode.hip decode_qkv_attn_splits)."""
     nch = (Tmax + 127) // 128
-    cpb = max(1, (B * Hkv * nch + 255) // 256)
+    cpb = max(1, (B * Hkv * nch + 255) // 256, (nch + 7) // 8)
     return (nch + cpb - 1) // cpb
 
 
@@ -423,7 +433,9 @@ def qkv_attend(s: torch.Tensor, ssq: torch.Tensor, norm_w: torch.Tensor, eps: fl
     B, K = s2.shape
     N = w.shape[0]
     nsplit = qkv_attn_splits(cache.max_len, B, cache.kv_local)
-    if not (B <= 16 and N < 16384 and N % 16 == 0 and K % 1024 == 0 and nsplit <= 8
+    # one attention unit per resident workgroup (one 512-thread workgroup per CU)
+    cus = _cu_count(s2.device)
+    if not (B <= 16 and N < 16384 and N % 16 == 0 and K % 1024 == 0 and nsplit * cache.kv_local * B <= cus
             and (nsplit == 1 or _COMBINE_ON)):
         return None
     return cache.attend_fused(layer, s2, ssq, folded_weight(w, norm_w, tiled=True), eps, rope, window)
