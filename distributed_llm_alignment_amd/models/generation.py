@@ -291,6 +291,9 @@ class _DecodeGraph:
 GRAPH_REUSE = os.environ.get("DLA_GRAPH_REUSE", "1") != "0"
 # rope + KV-cache write of the newest token fused into the decode attention launch
 FUSED_DECODE_ROPE = os.environ.get("DLA_FUSED_DECODE_ROPE", "1") != "0"
+# ZeRO-3 (FSDP) policies are gathered once per generate() call (DLA_DECODE_GATHER=0: per-layer
+# gathers inside every decode step, eager only)
+DECODE_GATHER = os.environ.get("DLA_DECODE_GATHER", "1") != "0"
 GRAPH_REUSE_MAX_BYTES = int(float(os.environ.get("DLA_GRAPH_REUSE_MAX_GB", "24")) * 2 ** 30)
 PROMPT_BUCKET = 64
 # KV cache storage head-major ([L, B, Hkv, T_max, D] behind the usual view), A/B: DLA_KV_HEAD_MAJOR
@@ -337,6 +340,16 @@ def generate(model: CausalLM, input_ids: torch.Tensor, attention_mask: Optional[
     On MI355X the prompt is prefilled with the flash-attention kernel, then every new token is
     ONE replay of a captured hipGraph (decode kernel + fused sampler, no host sync except an
     all-finished check every 16 tokens). `use_graph=False` forces the eager per-op loop."""
+    if DECODE_GATHER and model.layers_sharded():
+        # ZeRO-3 policy: gather it once for the whole rollout (fused decode kernels + captured
+        # graph) instead of an all-gather per layer per token
+        import contextlib
+
+        with contextlib.ExitStack() as stack:
+            for eng in model.sharding_engines():
+                stack.enter_context(eng.gathered_for_inference())
+            return generate(model, input_ids, attention_mask, max_new_tokens, do_sample, temperature,
+                            top_p, top_k, eos_token_id, pad_token_id, generator, return_mask, use_graph, seed)
     was_training = model.training
     model.eval()
     eos = eos_token_id if eos_token_id is not None else model.cfg.eos_token_id

@@ -503,10 +503,18 @@ class CausalLM(nn.Module):
                             self.cfg.norm_type == "rms")
         return h
 
+    def sharding_engines(self) -> list:
+        """The ZeRO-3 engines whose shards some of this model's layers live in."""
+        out = []
+        for e in [getattr(self, "_dla_fsdp", None)] + [getattr(l, "_dla_sharded", None) for l in self.layers]:
+            if e is not None and all(e is not o for o in out):
+                out.append(e)
+        return out
+
     def layers_sharded(self) -> bool:
-        """Some decoder layer's weights are ZeRO-3 shards gathered only inside its forward."""
-        return getattr(self, "_dla_fsdp", None) is not None or any(
-            getattr(l, "_dla_sharded", False) for l in self.layers)
+        """Some decoder layer's weights are ZeRO-3 shards gathered only inside its forward (not
+        pinned resident by `gathered_for_inference`)."""
+        return any(not getattr(e, "_pinned", False) for e in self.sharding_engines())
 
     def _forward_cached(self, input_ids, attention_mask, cache):
         positions = cache.positions_for(input_ids.shape[1])

@@ -190,7 +190,7 @@ class _ShardedBase:
         self._seen = set()
         for u in units:  # gather before the unit's first layer, free after its last
             for m in u.modules:  # callers that bypass Module.__call__ (fused decode) check this
-                m._dla_sharded = True
+                m._dla_sharded = self
             if u.modules:
                 u.modules[0].register_forward_pre_hook(self._make_pre_forward(u))
                 u.modules[-1].register_forward_hook(self._make_post_forward(u))
@@ -219,14 +219,36 @@ class _ShardedBase:
             h.wait()
             u.handle = None
 
+    _pinned = False  # gathered_for_inference(): every unit stays resident
+
     def _reshard(self, u: _Unit):
-        if u.is_root:
+        if u.is_root or self._pinned:
             return
         if u.handle is not None:
             u.handle.wait()
             u.handle = None
         _free(u.full)
         u.resident = False
+
+    @contextlib.contextmanager
+    def gathered_for_inference(self):
+        """Every unit gathered once and kept resident (the forward hooks neither re-gather nor
+        free) for the duration: rollout generation of a ZeRO-3 policy then runs like an unsharded
+        model -- the fused decode kernels and the captured decode graph -- instead of one
+        all-gather per layer per generated token ("hybrid engine"). Costs the full weights of the
+        model on every rank while inside."""
+        if self._pinned:
+            yield
+            return
+        for u in self.units:
+            self._gather(u)
+        self._pinned = True
+        try:
+            yield
+        finally:
+            self._pinned = False
+            for u in self.units:
+                self._reshard(u)
 
     # ------------------------------------------------------------------ hooks
     def _make_pre_forward(self, u: _Unit):

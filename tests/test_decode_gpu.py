@@ -562,28 +562,36 @@ def test_fused_qkv_attention_matches_two_launches(B, T, pad, monkeypatch):
 
 
 def test_fsdp_sharded_policy_generation_matches_unsharded(monkeypatch):
-    """A ZeRO-3 policy (layers gathered by forward hooks, freed after each layer) must not take
-    the fused decode path, which calls the kernels without Module.__call__ and would read freed
-    unit storage: its greedy rollouts equal the unsharded model's on the per-layer path."""
+    """A ZeRO-3 policy: generate() gathers it once for the rollout (gathered_for_inference: the
+    fused decode kernels and the captured graph on resident weights) and its greedy rollouts equal
+    the unsharded model's bitwise; with DLA_DECODE_GATHER off the decode steps take the per-layer
+    hooked path (never the fused kernels, which would read freed unit storage) and equal the
+    unsharded model on that same path. The units are resharded afterwards."""
     from distributed_llm_alignment_amd import ops
-    from distributed_llm_alignment_amd.models import build_model, generate
+    from distributed_llm_alignment_amd.models import build_model, generate, generation
     from distributed_llm_alignment_amd.models.generation import PROMPT_BUCKET, clear_graph_cache
     from distributed_llm_alignment_amd.parallel.fsdp import FullyShardedEngine
 
     cfg = _fused_cfg()
     a_m = build_model(cfg, device=DEV, dtype=torch.bfloat16, seed=2).eval()
     b_m = build_model(cfg, device=DEV, dtype=torch.bfloat16, seed=2)
-    FullyShardedEngine(b_m, lr=1e-3)
+    eng = FullyShardedEngine(b_m, lr=1e-3)
     b_m.eval()
     assert b_m.layers_sharded() and not a_m.layers_sharded()
     ids = torch.randint(3, cfg.vocab_size, (4, PROMPT_BUCKET), device=DEV,
                         generator=torch.Generator(device=DEV).manual_seed(3))
     clear_graph_cache()
-    b = generate(b_m, ids, max_new_tokens=10, do_sample=False, eos_token_id=-1)
-    monkeypatch.setattr(ops.decode, "DECODE_FUSED_NORM", False)  # same per-layer kernels
     a = generate(a_m, ids, max_new_tokens=10, do_sample=False, eos_token_id=-1, use_graph=False)
+    b = generate(b_m, ids, max_new_tokens=10, do_sample=False, eos_token_id=-1)
     clear_graph_cache()
     assert torch.equal(a, b)
+    assert b_m.layers_sharded() and not any(u.resident for u in eng.units if not u.is_root)
+    monkeypatch.setattr(generation, "DECODE_GATHER", False)
+    b2 = generate(b_m, ids, max_new_tokens=10, do_sample=False, eos_token_id=-1)
+    monkeypatch.setattr(ops.decode, "DECODE_FUSED_NORM", False)  # same per-layer kernels
+    a2 = generate(a_m, ids, max_new_tokens=10, do_sample=False, eos_token_id=-1, use_graph=False)
+    clear_graph_cache()
+    assert torch.equal(a2, b2)
 
 
 def test_fused_decode_projection_kernels_match_fp32():

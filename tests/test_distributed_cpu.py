@@ -873,3 +873,33 @@ def test_async_rollout_order_hides_gradient_comm(zero):
         print(f"rank {r} zero{zero}: exposed comm sync {d['sync']:.1f} ms, overlapped {d['overlap']:.1f} ms")
         assert d["sync"] > 1.0, d  # the collectives take measurable time on this host
         assert d["overlap"] < 0.35 * d["sync"], d
+
+
+def _fsdp_generate(rank, world, gather):
+    import torch
+
+    from distributed_llm_alignment_amd.models import build_model, generate, generation, get_config
+    from distributed_llm_alignment_amd.parallel.fsdp import FullyShardedEngine
+
+    generation.DECODE_GATHER = gather
+    cfg = get_config("tiny-llama")
+    full = build_model(cfg, device="cpu", seed=0).eval()
+    pol = build_model(cfg, device="cpu", seed=0)
+    eng = FullyShardedEngine(pol, lr=1e-2)
+    pol.eval()
+    g = torch.Generator().manual_seed(1 + rank)  # ranks generate different prompts
+    ids = torch.randint(3, cfg.vocab_size, (2, 9), generator=g)
+    a = generate(full, ids, max_new_tokens=6, do_sample=False, eos_token_id=-1)
+    b = generate(pol, ids, max_new_tokens=6, do_sample=False, eos_token_id=-1)
+    resharded = not any(u.resident for u in eng.units if not u.is_root)
+    return [bool(torch.equal(a, b)), resharded, pol.layers_sharded()]
+
+
+@pytest.mark.parametrize("gather", [True, False])
+def test_fsdp_policy_generation_gloo(gather):
+    """ZeRO-3 policy rollouts on 2 gloo ranks (each rank its own prompts): gathered once for the
+    rollout (hybrid engine) or per layer per step, the tokens equal the unsharded model's and
+    the units are freed afterwards."""
+    res = run_ranks(_fsdp_generate, 2, (gather,))
+    for r in (0, 1):
+        assert list(res[r]) == [True, True, True], res[r]
