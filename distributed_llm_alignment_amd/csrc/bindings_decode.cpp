@@ -24,6 +24,11 @@ void launch_decode_attn_rope(const bf16_t*, int64_t, const float*, const float*,
                              float*, bf16_t*, int64_t, int64_t, int*, hipStream_t);
 int decode_num_splits(int Tmax, int B, int Hkv);
 int decode_qkv_attn_splits(int Tmax, int B, int Hkv);
+int decode_attn_slab_splits(int Tmax, int B, int Hkv);
+void launch_decode_attn_slab(const float*, int, int, const float*, int, int, float, const float*,
+                             const float*, const int*, const int64_t*, int, bf16_t*, bf16_t*, int64_t,
+                             int64_t, int64_t, const int*, const int*, int, float, int, int, int, int, int,
+                             float*, float*, bf16_t*, int64_t, int64_t, int*, hipStream_t);
 bool launch_decode_qkv_attn(const bf16_t*, int64_t, const bf16_t*, bf16_t*, int64_t, int, int, int,
                             const KsFuse&, const float*, const float*, const int*, const int64_t*, int,
                             bf16_t*, bf16_t*, int64_t, int64_t, int64_t, const int*, const int*, int,
@@ -626,6 +631,90 @@ at::Tensor decode_qkv_attn(const at::Tensor& s, const at::Tensor& ssq, const at:
   return out;
 }
 
+// 17..64 decode rows: the qkv projection's split-K slabs (no reduce launch) ...
+at::Tensor skinny64_slabs(const at::Tensor& x, const at::Tensor& w) {
+  check_bf16(x, "x");
+  check_bf16(w, "w");
+  TORCH_CHECK(w.dim() == 5 && w.size(2) == 4 && w.size(3) == 16 && w.size(4) == 8 && w.is_contiguous(),
+              "w tiled [N/16, K/32, 4, 16, 8]");
+  const int64_t M = x.size(0), N = w.size(0) * 16, K = w.size(1) * 32;
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0 && x.size(1) == K && M >= 1 && M <= 64,
+              "x [M <= 64, K]");
+  TORCH_CHECK(m64_shape_ok((int)N, (int)K, false), "skinny64: K % 256 == 0 and N % 128 == 0");
+  check_aligned16(x, "x");
+  check_aligned16(w, "w");
+  same_device(x, w);
+  const int S = m64_splits((int)N, (int)K);
+  TORCH_CHECK(S > 1, "skinny64_slabs: the shape has no split-K");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  auto ws = at::empty({S, M, N}, x.options().dtype(at::kFloat));
+  launch_m64_gemm(cbp(x), x.stride(0), cbp(w), K, nullptr, 0, ws.data_ptr<float>(), (int)M, (int)N, (int)K, S,
+                  false, nullptr, 0, 0.f, true, cur_stream(x));
+  return ws;
+}
+
+// ... reduced (rstd x sum in split order, exactly the reduce launch's arithmetic) inside the
+// decode attention launch (decode.hip decode_attn_slab_kernel), rope + cache write fused as in
+// decode_attn_rope. ws [S, B, (Hq + 2 Hkv) D], ssq [B, nbp] the input rows' partials.
+at::Tensor decode_attn_rope_slab(const at::Tensor& ws, const at::Tensor& ssq, double eps, int64_t knorm,
+                                 const at::Tensor& cos,
+                                 const at::Tensor& sin, const at::Tensor& pos, at::Tensor& k_cache,
+                                 at::Tensor& v_cache, const at::Tensor& slot, const at::Tensor& kv_len,
+                                 const c10::optional<at::Tensor>& kv_start, int64_t window, double scale,
+                                 int64_t Hq, int64_t Hkv, int64_t D, int64_t rot) {
+  check_f32(ws, "ws");
+  check_f32(ssq, "ssq");
+  check_bf16(k_cache, "k_cache");
+  check_bf16(v_cache, "v_cache");
+  check_f32(cos, "cos");
+  check_f32(sin, "sin");
+  check_i32(pos, "pos");
+  check_i32(kv_len, "kv_len");
+  check_cuda(slot, "slot");
+  TORCH_CHECK(slot.scalar_type() == at::kLong && slot.numel() >= 1, "slot int64");
+  TORCH_CHECK(ws.dim() == 3 && ws.is_contiguous(), "ws [S, B, N] contiguous");
+  const int64_t S = ws.size(0), B = ws.size(1), N = ws.size(2);
+  TORCH_CHECK(N == (Hq + 2 * Hkv) * D, "ws width must be (Hq + 2 Hkv) * D");
+  TORCH_CHECK(ssq.dim() == 2 && ssq.size(0) == B && ssq.is_contiguous() && ssq.size(1) >= 1, "ssq [B, nbp]");
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(0) == B && k_cache.size(2) == Hkv && k_cache.size(3) == D &&
+                  k_cache.sizes() == v_cache.sizes() && k_cache.strides() == v_cache.strides() &&
+                  k_cache.stride(3) == 1 && k_cache.stride(1) % 8 == 0 && k_cache.stride(2) % 8 == 0 &&
+                  k_cache.stride(0) % 8 == 0,
+              "caches [B, Tmax, Hkv, D], 16-byte aligned rows");
+  TORCH_CHECK(D == 64 || D == 128, "decode attention supports head_dim 64 or 128");
+  TORCH_CHECK(Hq % Hkv == 0, "Hq % Hkv");
+  const int64_t G = Hq / Hkv;
+  TORCH_CHECK(G == 1 || G == 2 || G == 4 || G == 8, "GQA group size must be 1, 2, 4 or 8");
+  TORCH_CHECK(rot % 16 == 0 && rot <= D && rot > 0, "rot % 16 == 0, 0 < rot <= D");
+  TORCH_CHECK(cos.is_contiguous() && sin.is_contiguous() && cos.size(-1) == rot / 2, "rope tables");
+  TORCH_CHECK(pos.numel() == B && pos.is_contiguous(), "pos [B]");
+  check_aligned16(k_cache, "k_cache");
+  check_aligned16(v_cache, "v_cache");
+  const int* ks = nullptr;
+  if (kv_start && kv_start->defined()) {
+    check_i32(*kv_start, "kv_start");
+    TORCH_CHECK(kv_start->numel() == B && kv_start->is_contiguous(), "kv_start [B]");
+    ks = kv_start->data_ptr<int>();
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA g(ws.device());
+  const int64_t Tmax = k_cache.size(1);
+  const int nsplit = decode_attn_slab_splits((int)Tmax, (int)B, (int)Hkv);
+  auto fopt = ws.options();
+  auto part_o = at::empty({B, Hq, nsplit, D}, fopt);
+  auto part_ml = at::empty({B, Hq, nsplit, 2}, fopt);
+  auto out = at::empty({B, Hq, D}, k_cache.options());
+  launch_decode_attn_slab(ws.data_ptr<float>(), (int)S, (int)N, ssq.data_ptr<float>(), (int)ssq.size(1),
+                          (int)knorm, static_cast<float>(eps),
+                          cos.data_ptr<float>(), sin.data_ptr<float>(), pos.data_ptr<int>(),
+                          slot.data_ptr<int64_t>(), (int)rot, bp(k_cache), bp(v_cache), k_cache.stride(0),
+                          k_cache.stride(1), k_cache.stride(2), kv_len.data_ptr<int>(), ks,
+                          static_cast<int>(window), static_cast<float>(scale * 1.4426950408889634), (int)B,
+                          (int)Hq, (int)Hkv, (int)D, (int)Tmax, part_o.data_ptr<float>(),
+                          part_ml.data_ptr<float>(), bp(out), out.stride(0), out.stride(1),
+                          decode_counters(ws, B * Hkv), cur_stream(ws));
+  return out;
+}
+
 at::Tensor sample_tokens(const at::Tensor& logits, double temperature, int64_t top_k,
                          double top_p, bool greedy, const at::Tensor& rng) {
   check_cuda(logits, "logits");
@@ -663,6 +752,8 @@ TORCH_LIBRARY_FRAGMENT(dla, m) {
   m.def("rope_cache_write(Tensor qkv, Tensor cos, Tensor sin, Tensor pos, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor slot, int Hq, int Hkv, int D, int rot) -> Tensor");
   m.def("decode_attn_rope(Tensor qkv, Tensor cos, Tensor sin, Tensor pos, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor slot, Tensor kv_len, Tensor? kv_start, int window, float scale, int Hq, int Hkv, int D, int rot) -> Tensor");
   m.def("decode_qkv_attn(Tensor s, Tensor ssq, Tensor wt, float eps, Tensor cos, Tensor sin, Tensor pos, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor slot, Tensor kv_len, Tensor? kv_start, int window, float scale, int Hq, int Hkv, int D, int rot, Tensor(c!) sync_cnt, Tensor len_first, Tensor(d!) err) -> Tensor");
+  m.def("skinny64_slabs(Tensor x, Tensor w) -> Tensor");
+  m.def("decode_attn_rope_slab(Tensor ws, Tensor ssq, float eps, int knorm, Tensor cos, Tensor sin, Tensor pos, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor slot, Tensor kv_len, Tensor? kv_start, int window, float scale, int Hq, int Hkv, int D, int rot) -> Tensor");
   m.def("sample_tokens(Tensor logits, float temperature, int top_k, float top_p, bool greedy, Tensor rng) -> Tensor");
   m.def("skinny_gemm(Tensor x, Tensor w, Tensor(a!) counters, bool swiglu, bool glu_out=False) -> Tensor");
   m.def("skinny_glu_norm(Tensor x, Tensor res, Tensor norm_w, float eps, Tensor w) -> (Tensor, Tensor)");
@@ -677,6 +768,8 @@ TORCH_LIBRARY_IMPL(dla, CUDA, m) {
   m.impl("decode_attn", &dla::decode_attn);
   m.impl("sample_tokens", &dla::sample_tokens);
   m.impl("decode_qkv_attn", &dla::decode_qkv_attn);
+  m.impl("skinny64_slabs", &dla::skinny64_slabs);
+  m.impl("decode_attn_rope_slab", &dla::decode_attn_rope_slab);
   m.impl("rope_cache_write", &dla::rope_cache_write);
   m.impl("decode_attn_rope", &dla::decode_attn_rope);
   m.impl("skinny_gemm", &dla::skinny_gemm);

@@ -431,7 +431,7 @@ __device__ __forceinline__ void dec_loop_body(
     const int* __restrict__ kv_start, int window, float scale_log2, int nsplit, int cpb,
     float* __restrict__ part_o, float* __restrict__ part_ml, int Hq, const DecRope& rp,
     bf16_t* __restrict__ out, int64_t o_sb, int64_t o_sh, int* __restrict__ cnt, int Tcap,
-    Wait&& wait) {
+    Wait&& wait, const bf16_t* qkv_lds = nullptr) {
   // out != nullptr, cnt == nullptr (one split per sequence): the block writes the normalised bf16
   // output itself; out and cnt (nsplit > 1): partials + in-kernel combine (dec_arrive_combine).
   // Either way the combine launch is skipped.
@@ -450,15 +450,17 @@ __device__ __forceinline__ void dec_loop_body(
   const int sub = lane / LPK, dl = (lane % LPK) * 8;
   const int r16 = lane & 15, kg = lane >> 4;
   int newest = -1;
-  const bf16_t* qrow = nullptr;
+  // this block's q heads, k and v of the newest token: a row of the qkv projection, or (qkv_lds)
+  // the block's [G + 2][D] slice staged in LDS by wait()
+  const bf16_t *qh = nullptr, *kh = nullptr, *vh = nullptr;
   const float *cs = nullptr, *sn = nullptr;
   const int cfirst = split * cpb;
   auto cache_write = [&]() {  // the newest key's rotated K / raw V into its cache slot
     if constexpr (ROPE) {
       const int cn = newest / kDecChunk;
       if (cn >= cfirst && cn < cfirst + cpb && wv == 0 && lane < LPK) {
-        const bf16x8 vnew = load_bf16x8(qrow + (int64_t)(Hq + rp.Hkv + hk) * D + dl);
-        const bf16x8 knew = dec_rope8(qrow + (int64_t)(Hq + hk) * D, dl, rp.rot, cs, sn);
+        const bf16x8 vnew = load_bf16x8(vh + dl);
+        const bf16x8 knew = dec_rope8(kh, dl, rp.rot, cs, sn);
         store_bf16x8(kc + (int64_t)b * c_sb + (int64_t)newest * c_st + (int64_t)hk * c_sh + dl, knew);
         store_bf16x8(vc + (int64_t)b * c_sb + (int64_t)newest * c_st + (int64_t)hk * c_sh + dl, vnew);
       }
@@ -466,7 +468,16 @@ __device__ __forceinline__ void dec_loop_body(
   };
   if constexpr (ROPE) {
     newest = static_cast<int>(rp.slot[0]);
-    qrow = rp.qkv + (int64_t)b * rp.ld;
+    if (qkv_lds != nullptr) {
+      qh = qkv_lds;
+      kh = qkv_lds + G * D;
+      vh = qkv_lds + (G + 1) * D;
+    } else {
+      const bf16_t* qrow = rp.qkv + (int64_t)b * rp.ld;
+      qh = qrow + (int64_t)(hk * G) * D;
+      kh = qrow + (int64_t)(Hq + hk) * D;
+      vh = qrow + (int64_t)(Hq + rp.Hkv + hk) * D;
+    }
     const int half = rp.rot >> 1;
     cs = rp.cos_t + (int64_t)rp.pos[b] * half;
     sn = rp.sin_t + (int64_t)rp.pos[b] * half;
@@ -527,7 +538,7 @@ __device__ __forceinline__ void dec_loop_body(
       qf[s] = s16x8{};
       if (r16 < G) {
         if constexpr (ROPE)
-          qf[s] = __builtin_bit_cast(s16x8, dec_rope8(qrow + (int64_t)(hk * G + r16) * D, 32 * s + 8 * kg, rp.rot, cs, sn));
+          qf[s] = __builtin_bit_cast(s16x8, dec_rope8(qh + (int64_t)r16 * D, 32 * s + 8 * kg, rp.rot, cs, sn));
         else
           qf[s] = __builtin_bit_cast(s16x8, load_bf16x8(q + (int64_t)b * q_sb + (int64_t)(hk * G + r16) * q_sh + 32 * s + 8 * kg));
       }
@@ -567,7 +578,7 @@ __device__ __forceinline__ void dec_loop_body(
           if (min(kw0 + 16 * t + r16, Tcap - 1) == newest) {
 #pragma unroll
             for (int s = 0; s < KST; ++s)
-              kf[j][t][s] = __builtin_bit_cast(s16x8, dec_rope8(qrow + (int64_t)(Hq + hk) * D, 32 * s + 8 * kg, rp.rot, cs, sn));
+              kf[j][t][s] = __builtin_bit_cast(s16x8, dec_rope8(kh, 32 * s + 8 * kg, rp.rot, cs, sn));
           }
         }
       }
@@ -626,7 +637,7 @@ __device__ __forceinline__ void dec_loop_body(
       if (newest_here) {
         const int rown = newest - kw0;
         if (sub == (rown % KPI))
-          store_bf16x8(vw + dec_swz<D>(rown, dl >> 3), load_bf16x8(qrow + (int64_t)(Hq + rp.Hkv + hk) * D + dl));
+          store_bf16x8(vw + dec_swz<D>(rown, dl >> 3), load_bf16x8(vh + dl));
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       }
     }
@@ -1144,6 +1155,97 @@ void launch_decode_attn_rope(const bf16_t* qkv, int64_t ld, const float* cos_t, 
   else
     launch_decode_d<64>(nullptr, 0, 0, kc, vc, c_sb, c_st, c_sh, kv_len, kv_start, window,
                         scale_log2, B, Hq, Hkv, Tmax, part_o, part_ml, out, o_sb, o_sh, &rp, cnt, st);
+}
+
+// 17..64 decode rows (csrc/skinny64.hip): the qkv projection leaves S fp32 split-K slabs whose
+// reduce launch (m64_reduce_kernel MODE 1: y = bf16(rstd * sum_s slab_s)) is folded into this
+// attention launch instead. A block issues its first chunks' K / V loads, then reduces exactly the
+// (G + 2) x D values it reads -- its q heads, k and v of row b -- into LDS with the same
+// arithmetic and order as the reduce kernel (slabs summed in split order, rstd from the row's
+// partials in order), so the output equals the two-launch path bitwise; one launch and one
+// kernel boundary per layer fewer.
+struct DecSlab {
+  const float* ws;   // [S][M][N] fp32 slabs of the qkv projection
+  int S, M, N;
+  const float* ssq;  // [M][nbp] partial sums of squares of the input rows
+  int nbp, knorm;
+  float eps;
+};
+
+template <int D, int G>
+__global__ __launch_bounds__(256, 2) void decode_attn_slab_kernel(
+    bf16_t* __restrict__ kc, bf16_t* __restrict__ vc, int64_t c_sb, int64_t c_st, int64_t c_sh,
+    const int* __restrict__ kv_len, const int* __restrict__ kv_start, int window, float scale_log2,
+    int nsplit, int cpb, float* __restrict__ part_o, float* __restrict__ part_ml, int Hq, DecRope rp,
+    bf16_t* __restrict__ out, int64_t o_sb, int64_t o_sh, int* __restrict__ cnt, int Tcap, DecSlab sl) {
+  __shared__ __attribute__((aligned(16))) bf16_t qkv_s[(G + 2) * D];
+  const int split = blockIdx.x, hk = blockIdx.y, b = blockIdx.z, Hkv = gridDim.y;
+  auto stage = [&]() {
+    float a = 0.f;
+    for (int j = 0; j < sl.nbp; ++j) a += sl.ssq[b * sl.nbp + j];
+    const float rstd = rsqrtf(a / static_cast<float>(sl.knorm) + sl.eps);
+    const int64_t slab = static_cast<int64_t>(sl.M) * sl.N;
+    const float* row = sl.ws + static_cast<int64_t>(b) * sl.N;
+    for (int i = threadIdx.x; i < (G + 2) * D; i += 256) {
+      const int col = i < G * D ? hk * G * D + i
+                                : (i < (G + 1) * D ? Hq * D + hk * D + (i - G * D)
+                                                   : (Hq + Hkv) * D + hk * D + (i - (G + 1) * D));
+      float t = 0.f;
+      for (int sp = 0; sp < sl.S; ++sp) t += row[sp * slab + col];
+      qkv_s[i] = f2bf(t * rstd);
+    }
+    __syncthreads();
+  };
+  dec_loop_body<D, G, true, true, 2>(split, hk, b, Hkv, nullptr, 0, 0, kc, vc, c_sb, c_st, c_sh, kv_len,
+                                     kv_start, window, scale_log2, nsplit, cpb, part_o, part_ml, Hq, rp,
+                                     out, o_sb, o_sh, cnt, Tcap, stage, qkv_s);
+}
+
+void launch_decode_attn_slab(const float* ws, int S, int N, const float* ssq, int nbp, int knorm, float eps,
+                             const float* cos_t, const float* sin_t, const int* pos, const int64_t* slot,
+                             int rot, bf16_t* kc, bf16_t* vc, int64_t c_sb, int64_t c_st, int64_t c_sh,
+                             const int* kv_len, const int* kv_start, int window, float scale_log2, int B,
+                             int Hq, int Hkv, int D, int Tmax, float* part_o, float* part_ml, bf16_t* out,
+                             int64_t o_sb, int64_t o_sh, int* cnt, hipStream_t st) {
+  const int G = Hq / Hkv;
+  const int nch = (Tmax + kDecChunk - 1) / kDecChunk;
+  const int cpb = std::max(1, decode_cpb(Tmax, B, Hkv));
+  const int nsplit = (nch + cpb - 1) / cpb;
+  const DecRope rp{nullptr, 0, cos_t, sin_t, pos, slot, rot, Hkv};
+  const DecSlab sl{ws, S, B, N, ssq, nbp, knorm, eps};
+  int* const cn = (nsplit > 1 && nsplit <= kDecMaxFuse) ? cnt : nullptr;
+  bf16_t* fin = (nsplit == 1 || cn != nullptr) ? out : nullptr;
+  dim3 grid(nsplit, Hkv, B);
+#define DLA_SL(DD, GG)                                                                                   \
+  decode_attn_slab_kernel<DD, GG><<<grid, 256, 0, st>>>(kc, vc, c_sb, c_st, c_sh, kv_len, kv_start,      \
+                                                         window, scale_log2, nsplit, cpb, part_o, part_ml, \
+                                                         Hq, rp, fin, o_sb, o_sh, cn, Tmax, sl)
+  if (D == 128) {
+    switch (G) {
+      case 1: DLA_SL(128, 1); break;
+      case 2: DLA_SL(128, 2); break;
+      case 4: DLA_SL(128, 4); break;
+      default: DLA_SL(128, 8); break;
+    }
+  } else {
+    switch (G) {
+      case 1: DLA_SL(64, 1); break;
+      case 2: DLA_SL(64, 2); break;
+      case 4: DLA_SL(64, 4); break;
+      default: DLA_SL(64, 8); break;
+    }
+  }
+#undef DLA_SL
+  if (fin == nullptr)
+    (D == 128 ? decode_combine_kernel<128> : decode_combine_kernel<64>)<<<B * Hq, 64, 0, st>>>(
+        part_o, part_ml, nsplit, out, o_sb, o_sh, Hq);
+}
+
+// splits of the slab attention launch (host mirror for the partial buffers)
+int decode_attn_slab_splits(int Tmax, int B, int Hkv) {
+  const int nch = (Tmax + kDecChunk - 1) / kDecChunk;
+  const int cpb = std::max(1, decode_cpb(Tmax, B, Hkv));
+  return (nch + cpb - 1) / cpb;
 }
 
 }  // namespace dla

@@ -148,6 +148,24 @@ class KVCache:
             rope.rot_dim, self.sync[layer:layer + 1], self.len_first, self.sync_err)
         return o.reshape(B, 1, self.h_local * D)
 
+    def attend_slab(self, layer: int, s: torch.Tensor, ssq: torch.Tensor, wt: torch.Tensor, eps: float,
+                    rope, window: int) -> Optional[torch.Tensor]:
+        """17..64 decode rows: the qkv projection as split-K slabs (csrc/skinny64.hip, no reduce
+        launch) and the attention launch reducing the slabs it reads (csrc/decode.hip
+        decode_attn_slab_kernel). None when not eligible."""
+        B = s.shape[0]
+        if not (self.len > 0 and self.len + 1 <= self.max_len and self.fast_decode and rope is not None
+                and rope.rot_dim % 16 == 0 and FUSED_DECODE_ROPE and s.dim() == 2 and 16 < B <= 64):
+            return None
+        D = self.cfg.head_dim
+        ext = ops._ext.require()
+        ws = ext.skinny64_slabs(s, wt)
+        cos, sin = rope.tables(s.device)
+        o = ext.decode_attn_rope_slab(ws, ssq, float(eps), s.shape[1], cos, sin, self.pos.view(-1), self.k[layer],
+                                      self.v[layer], self.slot, self.kv_len, self.kv_start, window,
+                                      1.0 / math.sqrt(D), self.h_local, self.kv_local, D, rope.rot_dim)
+        return o.reshape(B, 1, self.h_local * D)
+
     def advance(self, T: int):
         """Host-driven advance (prefill / eager decode) keeping the device state in step."""
         self.len += T

@@ -423,14 +423,27 @@ def qkv_attn_splits(Tmax: int, B: int, Hkv: int) -> int:
     return (nch + cpb - 1) // cpb
 
 
+# 17..64 rows: the qkv split-K slabs are reduced inside the attention launch (csrc/decode.hip
+# decode_attn_slab_kernel) instead of by a separate reduce launch. DLA_DECODE_SLAB_ATTN=0 keeps it.
+DECODE_SLAB_ATTN = os.environ.get("DLA_DECODE_SLAB_ATTN", "1") != "0"
+
+
 def qkv_attend(s: torch.Tensor, ssq: torch.Tensor, norm_w: torch.Tensor, eps: float, w: torch.Tensor,
                cache, layer: int, rope, window: int) -> Optional[torch.Tensor]:
-    """attention(RMSNorm(s) * norm_w @ w^T) for one decode step in one launch, or None."""
-    if not (DECODE_QKV_ATTN and _DECODE_NT and DECODE_TILED >= 1 and getattr(cache, "sync", None) is not None
-            and not isinstance(cache.k, list)):
+    """attention(RMSNorm(s) * norm_w @ w^T) for one decode step with fewer launches, or None:
+    <= 16 rows the qkv projection and the attention in ONE launch, 17..64 rows the qkv reduce
+    folded into the attention launch."""
+    if getattr(cache, "sync", None) is None or isinstance(cache.k, list):
         return None
     s2 = _rows(s)
     B, K = s2.shape
+    if B > 16:
+        if not (DECODE_SLAB_ATTN and DECODE_M64 and DECODE_TILED >= 1 and B <= 64 and K % 256 == 0
+                and w.shape[0] % 128 == 0):
+            return None
+        return cache.attend_slab(layer, s2, ssq, folded_weight(w, norm_w, tiled=True), eps, rope, window)
+    if not (DECODE_QKV_ATTN and _DECODE_NT and DECODE_TILED >= 1):
+        return None
     N = w.shape[0]
     nsplit = qkv_attn_splits(cache.max_len, B, cache.kv_local)
     # one attention unit per resident workgroup (one 512-thread workgroup per CU)
