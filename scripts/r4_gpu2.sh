@@ -18,6 +18,10 @@ for arm in 1 0 1 0; do
   DLA_DECODE_QKV_ATTN=$arm timeout -k 10 300 python -u tools/bench_generate.py --modes graph --new 128 > gpurun_out/r4b/gen_b8_qa$arm.log 2>&1 || exit 1
   echo "qkv_attn=$arm $(tail -1 gpurun_out/r4b/gen_b8_qa$arm.log)"
 done
+for arm in 1 0; do
+  DLA_DECODE_SLAB_ATTN=$arm timeout -k 10 300 python -u tools/bench_generate.py --modes graph --new 128 --batch 64 --prompt 512 > gpurun_out/r4b/gen_b64_sl$arm.log 2>&1 || exit 1
+  echo "b64 slab_attn=$arm $(tail -1 gpurun_out/r4b/gen_b64_sl$arm.log)"
+done
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/pdec -o run -- python3 $R/tools/bench_generate.py --modes graph --new 128 > $R/gpurun_out/r4b/prof_dec.log 2>&1 || exit 1
 summ /tmp/pdec $R/gpurun_out/r4b/prof_dec_fused.md --by-grid --top 25 --per 4096
