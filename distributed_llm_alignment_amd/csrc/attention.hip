@@ -1319,15 +1319,26 @@ __global__ __launch_bounds__(512) void attn_bwd8_kernel(AttnBwdParams p) {
       }
       // lane holds d = 16*slice + i16 of query rows 16t + 4*g4l + e (64-B row segments)
       const int64_t rs = static_cast<int64_t>(p.Hq) * D;
-      char* sp = reinterpret_cast<char*>(p.dq_slab + ((static_cast<int64_t>(kb) * p.B + b) * p.slab_rows + qt) * rs +
-                                         static_cast<int64_t>(hq) * D + 16 * dslice);
-      const uint32_t so = static_cast<uint32_t>(4 * g4l * rs + i16) * 4u;
+      const int64_t sbase = ((static_cast<int64_t>(kb) * p.B + b) * p.slab_rows + qt) * rs +
+                            static_cast<int64_t>(hq) * D + 16 * dslice;
+      const uint32_t so = static_cast<uint32_t>(4 * g4l * rs + i16);
+      if (p.dq_slab16 != nullptr) {  // bf16 partials (32-B row segments)
+        bf16_t* sp = p.dq_slab16 + sbase;
 #pragma unroll
-      for (int t = 0; t < DQT; ++t) {
-        const int tt = NDS == 4 ? dthalf : t;
+        for (int t = 0; t < DQT; ++t) {
+          const int tt = NDS == 4 ? dthalf : t;
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-          *reinterpret_cast<float*>(sp + (16 * tt + e) * rs * 4 + so) = acc[t][e] * p.scale;
+          for (int e = 0; e < 4; ++e) sp[(16 * tt + e) * rs + so] = f2bf(acc[t][e] * p.scale);
+        }
+      } else {
+        char* sp = reinterpret_cast<char*>(p.dq_slab + sbase);
+#pragma unroll
+        for (int t = 0; t < DQT; ++t) {
+          const int tt = NDS == 4 ? dthalf : t;
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            *reinterpret_cast<float*>(sp + ((16 * tt + e) * rs + so) * 4u) = acc[t][e] * p.scale;
+        }
       }
     }
     BWD_TS(7);
@@ -1434,6 +1445,30 @@ __device__ __forceinline__ void slab_sum8(const float* src, int64_t slab_stride,
   }
 }
 
+// bf16 slabs: the same sum over the key blocks (fp32 accumulation in kb order)
+__device__ __forceinline__ void slab_sum8(const bf16_t* src, int64_t slab_stride, int lo, int hi,
+                                          f32x4& a0, f32x4& a1) {
+  a0 = f32x4{0.f, 0.f, 0.f, 0.f};
+  a1 = a0;
+  int kb = lo;
+  for (; kb + 4 <= hi; kb += 4) {
+    bf16x8 x[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      x[u] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(src + (kb + u) * slab_stride));
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      a0 += f32x4{bf2f(x[u][0]), bf2f(x[u][1]), bf2f(x[u][2]), bf2f(x[u][3])};
+      a1 += f32x4{bf2f(x[u][4]), bf2f(x[u][5]), bf2f(x[u][6]), bf2f(x[u][7])};
+    }
+  }
+  for (; kb < hi; ++kb) {
+    const bf16x8 x = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(src + kb * slab_stride));
+    a0 += f32x4{bf2f(x[0]), bf2f(x[1]), bf2f(x[2]), bf2f(x[3])};
+    a1 += f32x4{bf2f(x[4]), bf2f(x[5]), bf2f(x[6]), bf2f(x[7])};
+  }
+}
+
 // un-rotate one pair of 8-column chunks (d and d + D/2) with the position's cos/sin
 __device__ __forceinline__ void rope_unrotate8(const float* cp, const float* sp, float (&lo)[8],
                                                float (&hi)[8]) {
@@ -1448,9 +1483,9 @@ __device__ __forceinline__ void rope_unrotate8(const float* cp, const float* sp,
 // dQ[b, t, h, :] = sum over the key blocks whose workgroups swept row t (fixed kb order)
 // -> bf16 into a strided destination. One thread per 8 columns, or with the fused RoPE backward
 // (rcos != null) per pair of 8-column chunks d, d + D/2.
-template <bool CAUSAL>
+template <bool CAUSAL, typename ST = float>
 __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(
-    const float* __restrict__ slab, int nkb, int B, int Tq, int slab_rows, int Hq, int D,
+    const ST* __restrict__ slab, int nkb, int B, int Tq, int slab_rows, int Hq, int D,
     int causal_off, int window, const int* __restrict__ kv_start, const int* __restrict__ kv_end,
     int Tk, bf16_t* __restrict__ dst, int64_t d_sb, int64_t d_st, int64_t d_sh,
     const float* __restrict__ rcos, const float* __restrict__ rsin, const int* __restrict__ rpos,
@@ -1473,7 +1508,7 @@ __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(
     const int kend = kv_end ? kv_end[b] : Tk;
     const bool pair = rcos && c < hv;
     const int col = (rcos && !pair) ? rot + (c - hv) * 8 : c * 8;
-    const float* src = slab + (static_cast<int64_t>(b) * slab_rows + t) * rs + static_cast<int64_t>(hq) * D + col;
+    const ST* src = slab + (static_cast<int64_t>(b) * slab_rows + t) * rs + static_cast<int64_t>(hq) * D + col;
     // the key blocks that wrote row t form one contiguous range [lo, hi) (kv range: an
     // interval; causal: a prefix; window: a suffix): find it with ALU only, then sum the slabs
     // in kb order with 4 blocks' loads in flight at a time (same order as one at a time: the
@@ -1627,6 +1662,12 @@ static int attn_bwd_waves() {
   return (e && std::atoi(e) == 4) ? 4 : 8;
 }
 
+// bf16 dQ slabs (8-wave kernel; DLA_ATTN_DQ_BF16=0 keeps fp32). Read per call, like the wave count.
+bool attn_dq_slab_bf16() {
+  const char* e = std::getenv("DLA_ATTN_DQ_BF16");
+  return attn_bwd_waves() == 8 && !(e && std::atoi(e) == 0);
+}
+
 template <int D>
 static void bwd_dispatch(const AttnBwdParams& p, bool causal, hipStream_t st) {
   const int nkb = (p.Tk + kAttnBwdKeys - 1) / kAttnBwdKeys;
@@ -1654,9 +1695,20 @@ void launch_attn_dq_reduce(const float* slab, int nkb, int B, int Tq, int slab_r
                            bool causal, int causal_off, int window, const int* kv_start,
                            const int* kv_end, int Tk, bf16_t* dst, int64_t d_sb, int64_t d_st,
                            int64_t d_sh, const float* rcos, const float* rsin, const int* rpos,
-                           int rot, hipStream_t st) {
+                           int rot, hipStream_t st, const bf16_t* slab16) {
   const int64_t work = static_cast<int64_t>(B) * Tq * Hq * (rcos ? rot / 16 + (D - rot) / 8 : D / 8);
   if (work == 0) return;
+  if (slab16 != nullptr) {
+    if (causal)
+      attn_dq_reduce_kernel<true, bf16_t><<<stream_grid(work), 256, 0, st>>>(
+          slab16, nkb, B, Tq, slab_rows, Hq, D, causal_off, window, kv_start, kv_end, Tk, dst, d_sb, d_st, d_sh,
+          rcos, rsin, rpos, rot);
+    else
+      attn_dq_reduce_kernel<false, bf16_t><<<stream_grid(work), 256, 0, st>>>(
+          slab16, nkb, B, Tq, slab_rows, Hq, D, causal_off, window, kv_start, kv_end, Tk, dst, d_sb, d_st, d_sh,
+          rcos, rsin, rpos, rot);
+    return;
+  }
   if (causal)
     attn_dq_reduce_kernel<true><<<stream_grid(work), 256, 0, st>>>(
         slab, nkb, B, Tq, slab_rows, Hq, D, causal_off, window, kv_start, kv_end, Tk, dst, d_sb, d_st, d_sh,

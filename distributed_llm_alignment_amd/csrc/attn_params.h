@@ -46,6 +46,8 @@ struct AttnBwdParams {
   const float* delta;  // [B, Hq, Tq] = rowsum(dO * O)
   float* dq_slab;      // [nkb, B, slab_rows, Hq, D] fp32: one dQ partial per 256-key block (plain
                        // stores, no atomics), summed in key-block order by the reduce pass
+  bf16_t* dq_slab16;   // the same slabs in bf16 (8-wave kernel, DLA_ATTN_DQ_BF16): each partial
+                       // rounded once, summed in fp32 by the reduce -- half the slab traffic
   float* dk_part;      // [hsplit, B, Tk, Hkv, D] fp32 partials (hsplit > 1 only)
   float* dv_part;
   bf16_t* dk;          // strided like k (hsplit == 1)

@@ -71,9 +71,10 @@ void launch_attn_fwd(const AttnParams&, int, bool, hipStream_t);
 void launch_attn_bwd_delta(const bf16_t*, const bf16_t*, int64_t, int64_t, int64_t, int64_t,
                            int64_t, int64_t, int, int, int, int, float*, hipStream_t);
 void launch_attn_bwd(const AttnBwdParams&, int, bool, hipStream_t);
+bool attn_dq_slab_bf16();
 void launch_attn_dq_reduce(const float*, int, int, int, int, int, int, bool, int, int,
                            const int*, const int*, int, bf16_t*, int64_t, int64_t, int64_t,
-                           const float*, const float*, const int*, int, hipStream_t);
+                           const float*, const float*, const int*, int, hipStream_t, const bf16_t*);
 void launch_attn_dkv_reduce(const float*, const float*, int, int, int, int, int, float, bf16_t*,
                             int64_t, int64_t, int64_t, bf16_t*, int64_t, int64_t, int64_t,
                             const float*, const float*, const int*, int, hipStream_t);
@@ -489,7 +490,8 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k,
   // one fp32 dQ partial per key block (no zero fill: the reduce pass reads exactly the rows
   // each key block's workgroups wrote)
   const int64_t slab_rows = (Tq + kAttnBwdQRows - 1) / kAttnBwdQRows * kAttnBwdQRows;
-  auto slab = at::empty({std::max<int64_t>(nkb, 1), B, slab_rows, Hq, D}, fopt);
+  const bool slab16 = attn_dq_slab_bf16();
+  auto slab = at::empty({std::max<int64_t>(nkb, 1), B, slab_rows, Hq, D}, slab16 ? q.options() : fopt);
   const int hs = attn_bwd_hsplit(nkb, Hkv, B, Hq / Hkv, causal, device_cus(q.get_device()));
   at::Tensor dkp, dvp;
   if (hs > 1) {
@@ -499,7 +501,8 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k,
   AttnBwdParams p{};
   p.q = cbp(q); p.k = cbp(k); p.v = cbp(v); p.dout = cbp(dout);
   p.lse2 = lse2.data_ptr<float>(); p.delta = delta.data_ptr<float>();
-  p.dq_slab = slab.data_ptr<float>();
+  p.dq_slab = slab16 ? nullptr : slab.data_ptr<float>();
+  p.dq_slab16 = slab16 ? bp(slab) : nullptr;
   p.dk_part = hs > 1 ? dkp.data_ptr<float>() : nullptr;
   p.dv_part = hs > 1 ? dvp.data_ptr<float>() : nullptr;
   p.dk = bp(dk); p.dv = bp(dv);
@@ -530,7 +533,8 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k,
   launch_attn_dq_reduce(p.dq_slab, static_cast<int>(nkb), static_cast<int>(B), static_cast<int>(Tq),
                         p.slab_rows, static_cast<int>(Hq), static_cast<int>(D), causal, p.causal_off, p.window,
                         p.kv_start, p.kv_end, static_cast<int>(Tk), bp(dq), dq.stride(0),
-                        dq.stride(1), dq.stride(2), p.rope_cos, p.rope_sin, p.rope_pos, p.rope_rot, st);
+                        dq.stride(1), dq.stride(2), p.rope_cos, p.rope_sin, p.rope_pos, p.rope_rot, st,
+                        p.dq_slab16);
   if (hs > 1) {
     launch_attn_dkv_reduce(p.dk_part, p.dv_part, hs, static_cast<int>(B), static_cast<int>(Tk),
                            static_cast<int>(Hkv), static_cast<int>(D), p.scale, bp(dk),

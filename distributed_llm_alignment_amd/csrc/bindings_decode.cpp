@@ -628,6 +628,8 @@ at::Tensor decode_qkv_attn(const at::Tensor& s, const at::Tensor& ssq, const at:
       err.data_ptr<int>(), cur_stream(s));
   TORCH_CHECK(ok, "decode_qkv_attn: shape outside the fused kernel (more attention units than "
                   "resident workgroups)");
+  const hipError_t le = hipGetLastError();
+  TORCH_CHECK(le == hipSuccess, "decode_qkv_attn launch: ", hipGetErrorString(le));
   return out;
 }
 
@@ -650,6 +652,8 @@ at::Tensor skinny64_slabs(const at::Tensor& x, const at::Tensor& w) {
   auto ws = at::empty({S, M, N}, x.options().dtype(at::kFloat));
   launch_m64_gemm(cbp(x), x.stride(0), cbp(w), K, nullptr, 0, ws.data_ptr<float>(), (int)M, (int)N, (int)K, S,
                   false, nullptr, 0, 0.f, true, cur_stream(x));
+  const hipError_t le = hipGetLastError();
+  TORCH_CHECK(le == hipSuccess, "skinny64_slabs launch: ", hipGetErrorString(le));
   return ws;
 }
 
@@ -712,6 +716,8 @@ at::Tensor decode_attn_rope_slab(const at::Tensor& ws, const at::Tensor& ssq, do
                           (int)Hq, (int)Hkv, (int)D, (int)Tmax, part_o.data_ptr<float>(),
                           part_ml.data_ptr<float>(), bp(out), out.stride(0), out.stride(1),
                           decode_counters(ws, B * Hkv), cur_stream(ws));
+  const hipError_t le = hipGetLastError();
+  TORCH_CHECK(le == hipSuccess, "decode_attn_rope_slab launch: ", hipGetErrorString(le));
   return out;
 }
 

@@ -633,11 +633,18 @@ __device__ __forceinline__ void dec_loop_body(
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     bf16_t* vw = &vimg[wv][j][0];
-    if constexpr (ROPE) {  // the newest key's V row from the qkv row (not the cache) into the image
-      if (newest_here) {
-        const int rown = newest - kw0;
-        if (sub == (rown % KPI))
-          store_bf16x8(vw + dec_swz<D>(rown, dl >> 3), load_bf16x8(vh + dl));
+    if constexpr (ROPE) {
+      // Every image row whose clamped key is the newest one -- its own row, and the rows past
+      // the visible range that loadV clamped onto it (a wave beyond kv_len has only those) --
+      // takes the V row from the qkv row: the cache slot is written by this launch, so the DMA
+      // read stale or never-written bytes there, and a NaN in a masked row still poisons P.V.
+      if (newest >= k0 && newest < k1) {
+        const bf16x8 vn = load_bf16x8(vh + dl);
+#pragma unroll
+        for (int it = 0; it < NIT; ++it) {
+          const int row = it * KPI + sub;
+          if (min(max(kw0 + row, k0), k1 - 1) == newest) store_bf16x8(vw + dec_swz<D>(row, dl >> 3), vn);
+        }
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       }
     }

@@ -12,8 +12,14 @@ summ() {  # dir out args...
   local tr=$(find "$1" -name '*kernel_trace.csv' | head -1)
   python3 $R/scripts/prof_window.py "$tr" "${@:3}" > "$2" && rm -rf "$1"
 }
-timeout -k 10 300 python -u -m pytest tests/test_decode_gpu.py -x -q --timeout 120 --timeout-method thread -k "fused_qkv or fsdp or fused_decode or graph" > gpurun_out/r4b/dec_tests.log 2>&1 || { echo TESTS_FAILED; tail -40 gpurun_out/r4b/dec_tests.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_decode_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/r4b/dec_tests.log 2>&1 || { echo TESTS_FAILED; tail -40 gpurun_out/r4b/dec_tests.log; exit 1; }
 tail -2 gpurun_out/r4b/dec_tests.log
+timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread -k "attn or attention or flash" > gpurun_out/r4b/attn_tests.log 2>&1 || { echo ATTN_TESTS_FAILED; tail -40 gpurun_out/r4b/attn_tests.log; exit 1; }
+tail -2 gpurun_out/r4b/attn_tests.log
+for arm in 1 0; do
+  DLA_ATTN_DQ_BF16=$arm timeout -k 10 400 python -u bench.py --steps 4 --warmup 2 > gpurun_out/r4b/dpo_dq$arm.log 2>&1 || exit 1
+  echo "dq_bf16=$arm $(tail -1 gpurun_out/r4b/dpo_dq$arm.log)"
+done
 for arm in 1 0 1 0; do
   DLA_DECODE_QKV_ATTN=$arm timeout -k 10 300 python -u tools/bench_generate.py --modes graph --new 128 > gpurun_out/r4b/gen_b8_qa$arm.log 2>&1 || exit 1
   echo "qkv_attn=$arm $(tail -1 gpurun_out/r4b/gen_b8_qa$arm.log)"
