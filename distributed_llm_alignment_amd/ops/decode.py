@@ -353,7 +353,12 @@ def tiled_weight(w: torch.Tensor) -> torch.Tensor:
 
 
 def refresh_folded_weights(model) -> None:
-    """Bring every derived decode weight of `model` up to date (before a graph replay)."""
+    """Bring every derived decode weight of `model` up to date (before a graph replay). A model
+    whose layers are ZeRO-3 sharded right now is skipped: its weights are not resident (the
+    per-layer decode path does not use these copies), and they refresh once it is gathered."""
+    ls = getattr(model, "layers_sharded", None)
+    if ls is not None and ls():
+        return
     for layer in getattr(model, "layers", []):
         for w, nw in ((getattr(layer.attn, "qkv_proj", None), getattr(layer, "ln1_w", None)),
                       (getattr(layer.mlp, "up_proj", None), getattr(layer, "ln2_w", None))):

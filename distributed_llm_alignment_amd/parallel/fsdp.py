@@ -185,6 +185,13 @@ class _ShardedBase:
                     u.resident = False
                     if meta:
                         _account(-u.numel * esz)
+        # weight epoch: bumped whenever the shards change (step / load / writeback). Gathers keep
+        # the params' version counters untouched, so caches derived from weights (the decode
+        # kernels' folded / tiled copies, ops.decode._wkey) key on this instead
+        self._wt_epoch = [0]
+        for u in units:
+            for p in u.params:
+                p._dla_epoch = self._wt_epoch
         self._pending = []  # in-flight reduce-scatters: (handle, tmp, unit)
         self.comm_timer = ExposedCommTimer(self.device)  # exposed gradient-comm wait per step
         self._seen = set()
@@ -302,6 +309,7 @@ class ShardedInference(_ShardedBase):
                 with torch.no_grad():
                     for u in self.units:
                         self.param_shard[u.shard_off:u.shard_off + u.chunk].copy_(self._my_chunk(u.full, u))
+                self._wt_epoch[0] += 1
             for u in self.units:
                 self._reshard(u)
 
@@ -468,6 +476,7 @@ class FullyShardedEngine(_ShardedBase):
         lr = self.lr if lr is None else lr
         coef = self.clip_and_norm()
         self.step_count += 1
+        self._wt_epoch[0] += 1
         adamw_update(self.param_shard, self.master, self.grad_shard, self.exp_avg, self.exp_avg_sq,
                      lr, self.betas[0], self.betas[1], self.eps, self.wd, self.step_count,
                      clip=coef if self.max_grad_norm else None, grad_scale=1.0 / self.world)
@@ -498,6 +507,7 @@ class FullyShardedEngine(_ShardedBase):
     def _shards_from_full(self):
         for u in self.units:
             self.param_shard[u.shard_off:u.shard_off + u.chunk].copy_(self._my_chunk(u.full, u))
+        self._wt_epoch[0] += 1
         if self.master is not None:
             self.master.copy_(self.param_shard.float())
 
@@ -530,6 +540,7 @@ class FullyShardedEngine(_ShardedBase):
         if self.master is not None and sd.get("master") is not None:
             self.master.copy_(sd["master"])
             self.param_shard.copy_(self.master.to(self.dtype))
+            self._wt_epoch[0] += 1
 
     def _gather_unit(self, shard: torch.Tensor, u: _Unit) -> torch.Tensor:
         out = torch.empty(u.numel, dtype=shard.dtype, device=shard.device)

@@ -209,3 +209,30 @@ def test_fsdp_shards_refused_when_unit_grouping_changes(tmp_path):
     for r in (0, 1):
         regrouped, took, same = res[r]
         assert regrouped and not took and same
+
+
+def test_fsdp_weight_epoch_moves_with_the_shards():
+    """Gathers preserve the params' version counters, so weight-derived caches (the decode
+    kernels' folded / tiled copies, keyed by ops.decode._wkey) key on the engine's weight epoch:
+    it must move on every optimizer step and state writeback, and refresh_folded_weights must
+    leave a sharded model alone (its weights are not resident)."""
+    from distributed_llm_alignment_amd import ops
+    from distributed_llm_alignment_amd.models import build_model, get_config
+    from distributed_llm_alignment_amd.parallel.fsdp import FullyShardedEngine
+
+    cfg = get_config("tiny-llama")
+    pol = build_model(cfg, device="cpu", seed=0)
+    eng = FullyShardedEngine(pol, lr=1e-2)
+    w = pol.layers[0].attn.qkv_proj
+    k0 = ops.decode._wkey(w)
+    ids = torch.randint(3, cfg.vocab_size, (2, 16), generator=torch.Generator().manual_seed(0))
+    pol(ids).float().pow(2).mean().backward()
+    eng.step()
+    k1 = ops.decode._wkey(w)
+    assert k1[2] != k0[2]
+    with eng.summon_full_params(writeback=True):
+        pass
+    assert ops.decode._wkey(w)[2] != k1[2]
+    assert pol.layers_sharded()
+    ops.decode.refresh_folded_weights(pol)  # no-op while sharded
+    assert getattr(w, "_dla_fold", None) is None
