@@ -328,9 +328,10 @@ static void check_pos(const at::Tensor& pos, int64_t N, int64_t k) {
   TORCH_CHECK(k >= 1 && k <= 8, "top-k must be in [1, 8]");
 }
 
-// The kernels trust pos[] to be a permutation of [0, N*k): verified cheaply on the device side
-// by the caller's construction (ops/moe.py builds it from an argsort); rows are bounds-checked
-// here through the output allocation size.
+// The kernels trust pos[] to index rows of ys / xs: a permutation of [0, N*k) on the exact path
+// (ops/moe.py builds it from an argsort), or slots of a capacity-padded buffer with dropped slots
+// all pointing at one appended zero row (parallel/expert.py, rows >= N*k there); the caller's
+// construction is the bound, row counts are checked against the allocations here.
 std::tuple<at::Tensor, at::Tensor> moe_topk_fwd(const at::Tensor& logits, int64_t k) {
   check_bf16(logits, "logits");
   TORCH_CHECK(logits.dim() == 2 && logits.is_contiguous(), "logits [N, E] contiguous");
@@ -379,7 +380,7 @@ at::Tensor moe_combine(const at::Tensor& ys, const at::Tensor& pos,
   TORCH_CHECK(ys.dim() == 2 && ys.is_contiguous() && ys.size(1) % 8 == 0, "ys [M, H], H % 8 == 0");
   const int64_t N = pos.size(0), k = pos.size(-1), H = ys.size(1);
   check_pos(pos, N, k);
-  TORCH_CHECK(ys.size(0) == N * k, "ys rows must equal N * k");
+  TORCH_CHECK(ys.size(0) >= 1, "ys has no rows");  // pos rows index ys (exact: N*k, capacity: any)
   const float* wp = nullptr;
   if (w && w->defined()) {
     check_f32(*w, "w");
@@ -402,12 +403,14 @@ std::tuple<at::Tensor, at::Tensor> moe_combine_bwd(const at::Tensor& dout, const
   check_pos(pos, N, k);
   TORCH_CHECK(dout.dim() == 2 && dout.size(0) == N && dout.size(1) == H && dout.is_contiguous(),
               "dout [N, H]");
-  TORCH_CHECK(ys.dim() == 2 && ys.size(0) == N * k && ys.is_contiguous() && H % 8 == 0, "ys [N*k, H]");
+  TORCH_CHECK(ys.dim() == 2 && ys.size(0) >= 1 && ys.is_contiguous() && H % 8 == 0, "ys [R, H]");
   TORCH_CHECK(w.sizes() == pos.sizes() && w.is_contiguous(), "w [N, k]");
   check_aligned16(ys, "ys");
   check_aligned16(dout, "dout");
   c10::hip::HIPGuardMasqueradingAsCUDA g(ys.device());
-  auto dys = at::empty_like(ys);
+  // not a permutation (capacity buffer): rows no slot reads get a zero gradient; the appended
+  // zero row shared by the dropped slots receives racing writes, and its gradient is discarded
+  auto dys = ys.size(0) == N * k ? at::empty_like(ys) : at::zeros_like(ys);
   auto dw = at::empty({N, k}, w.options());
   launch_moe_combine_bwd(cbp(dout), cbp(ys), pos.data_ptr<int>(), w.data_ptr<float>(), N, (int)H,
                          (int)k, bp(dys), dw.data_ptr<float>(), cur_stream(ys));

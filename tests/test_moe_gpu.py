@@ -58,6 +58,58 @@ def test_dispatch_combine_kernels(N, H, k, E):
     assert torch.allclose(dw, rdw, atol=1e-1, rtol=1e-2)
 
 
+def test_combine_capacity_layout_kernels():
+    """The EP capacity path combines from a padded slot buffer (parallel/expert.py): pos indexes a
+    [R, H] buffer with R > N*k, unused rows, and every dropped slot on one appended zero row."""
+    from distributed_llm_alignment_amd import ops
+
+    g = torch.Generator(device=DEV).manual_seed(4)
+    N, k, H, R = 300, 2, 512, 1000
+    pos = torch.randperm(R - 1, device=DEV, generator=g)[:N * k].view(N, k).to(torch.int32)
+    pos[::7, 1] = R - 1  # dropped slots
+    ys = torch.randn(R, H, device=DEV, generator=g).to(torch.bfloat16)
+    ys[-1] = 0
+    ys.requires_grad_(True)
+    w = torch.rand(N, k, device=DEV, generator=g).requires_grad_(True)
+    out = ops.moe.combine(ys, pos, w)
+    ysf = ys.detach().float().requires_grad_(True)
+    wf = w.detach().clone().requires_grad_(True)
+    ref = ops.moe._ref_combine(ysf, pos, wf)
+    assert torch.allclose(out.float(), ref, atol=2e-2, rtol=1e-2)
+    go = torch.randn(N, H, device=DEV, generator=g).to(torch.bfloat16)
+    dys, dw = torch.autograd.grad(out, [ys, w], go)
+    rdys, rdw = torch.autograd.grad(ref, [ysf, wf], go.float())
+    assert torch.allclose(dys[:-1].float(), rdys[:-1], atol=2e-2, rtol=1e-2)  # unread rows: zero
+    assert torch.allclose(dw, rdw, atol=1e-1, rtol=1e-2)
+
+
+def test_expert_parallel_shape_mode_layer_matches_fp32():
+    """bench.py --ep-shape on the GPU: the capacity dispatch (identity all-to-alls, device-built
+    expert order, grouped expert kernels, padded combine) of one EP rank's experts, forward and
+    backward, against the same layer in fp32 on the CPU."""
+    import copy
+
+    from distributed_llm_alignment_amd.models import build_model, get_config
+    from distributed_llm_alignment_amd.parallel.expert import apply_expert_parallel
+
+    cfg = get_config("tiny-mixtral", hidden_size=256, intermediate_size=512, num_experts=8)
+    m = build_model(cfg, device="cpu", dtype=torch.float32, seed=2)
+    apply_expert_parallel(m, None, capacity_factor=2.0, shape_ep=4)
+    mg = copy.deepcopy(m).to(DEV, torch.bfloat16)
+    g = torch.Generator().manual_seed(5)
+    h = torch.randn(2, 256, cfg.hidden_size, generator=g)
+    outs = []
+    for mod, x in ((m.layers[0].mlp, h.clone()), (mg.layers[0].mlp, h.to(DEV, torch.bfloat16))):
+        x.requires_grad_(True)
+        y = mod(x)
+        y.float().pow(2).sum().backward()
+        outs.append((y.detach().float().cpu(), x.grad.float().cpu(), mod.expert_up.grad.float().cpu()))
+    (y0, dx0, du0), (y1, dx1, du1) = outs
+    for a, b in ((y0, y1), (dx0, dx1), (du0, du1)):
+        assert torch.isfinite(b).all()
+        assert (a - b).abs().max() / a.abs().max() < 5e-2
+
+
 def test_mixtral_layer_bf16_vs_fp32_reference():
     from distributed_llm_alignment_amd import ops
     from distributed_llm_alignment_amd.models import build_model, get_config
