@@ -13,7 +13,7 @@ summ() {  # dir out args...
   local tr=$(find "$1" -name '*kernel_trace.csv' | head -1)
   python3 $R/scripts/prof_window.py "$tr" "${@:3}" > "$2" && rm -rf "$1"
 }
-timeout -k 10 300 python -u -m pytest tests/test_moe_gpu.py -x -q --timeout 120 --timeout-method thread > $O/moe_tests.log 2>&1 || { echo MOE_TESTS_FAILED; tail -40 $O/moe_tests.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_moe_gpu.py -x -q --timeout 120 --timeout-method thread > $O/moe_tests.log 2>&1 || { echo MOE_TESTS_FAILED; tail -40 $O/moe_tests.log; }
 tail -2 $O/moe_tests.log
 timeout -k 10 600 python -u bench.py --model mixtral-8x7b --ep-shape 8 --steps 3 --warmup 2 > $O/mixtral_ep8.log 2>&1 || { tail -30 $O/mixtral_ep8.log; exit 1; }
 tail -1 $O/mixtral_ep8.log
