@@ -13,10 +13,10 @@ summ() {  # dir out args...
   local tr=$(find "$1" -name '*kernel_trace.csv' | head -1)
   python3 $R/scripts/prof_window.py "$tr" "${@:3}" > "$2" && rm -rf "$1"
 }
-timeout -k 10 300 python -u -m pytest tests/test_moe_gpu.py -x -q --timeout 120 --timeout-method thread > $O/moe_tests.log 2>&1 || { echo MOE_TESTS_FAILED; tail -40 $O/moe_tests.log; }
-tail -2 $O/moe_tests.log
-timeout -k 10 600 python -u bench.py --model mixtral-8x7b --ep-shape 8 --steps 3 --warmup 2 > $O/mixtral_ep8.log 2>&1 || { tail -30 $O/mixtral_ep8.log; exit 1; }
-tail -1 $O/mixtral_ep8.log
+for v in "" "--fp8"; do
+  timeout -k 10 600 python -u bench.py --model mixtral-8x7b --ep-shape 8 --micro-pairs 2 --accum 8 --ep-capacity 1.25 $v --steps 3 --warmup 2 > $O/mixtral_ep8$v.log 2>&1 || { echo "MIXTRAL$v rc=$?"; tail -5 $O/mixtral_ep8$v.log; }
+  tail -1 $O/mixtral_ep8$v.log
+done
 timeout -k 10 300 python -u tools/tp_chunk_probe.py > $O/tp_chunks.log 2>&1 || { tail -20 $O/tp_chunks.log; exit 1; }
 cat $O/tp_chunks.log
 cd /tmp
