@@ -402,9 +402,11 @@ def skinny_normed(s: torch.Tensor, ssq: torch.Tensor, norm_w: torch.Tensor, eps:
 
 # Fused decode qkv projection + attention (csrc/decode.hip decode_qkv_attn_kernel, B <= 16): the
 # attention blocks prefetch their first KV chunks while the qkv blocks of the same launch stream
-# the qkv weight, then wait on a device counter for this step's q / k / v. DLA_DECODE_QKV_ATTN=0
-# keeps the two launches (skinny_normed + the rope-fused decode attention).
-DECODE_QKV_ATTN = os.environ.get("DLA_DECODE_QKV_ATTN", "1") != "0"
+# the qkv weight, then wait on a device counter for this step's q / k / v. Off by default
+# (DLA_DECODE_QKV_ATTN=1 turns it on): measured slower in a real graph decode on 1x MI355X,
+# Llama-3-8B B=8 prompt 1024: 4.16 / 4.05 vs 3.58 / 3.57 ms/token for the two launches
+# (skinny_normed + the rope-fused decode attention); profiles/r4_decode.md.
+DECODE_QKV_ATTN = os.environ.get("DLA_DECODE_QKV_ATTN", "0") == "1"
 _DECODE_NT = os.environ.get("DLA_DECODE_NT", "1") != "0"  # the fused kernel streams with nt loads
 
 
@@ -429,8 +431,9 @@ def qkv_attn_splits(Tmax: int, B: int, Hkv: int) -> int:
 
 
 # 17..64 rows: the qkv split-K slabs are reduced inside the attention launch (csrc/decode.hip
-# decode_attn_slab_kernel) instead of by a separate reduce launch. DLA_DECODE_SLAB_ATTN=0 keeps it.
-DECODE_SLAB_ATTN = os.environ.get("DLA_DECODE_SLAB_ATTN", "1") != "0"
+# decode_attn_slab_kernel) instead of by a separate reduce launch. Off by default
+# (DLA_DECODE_SLAB_ATTN=1): a wash at B=64 prompt 512 (5.161 vs 5.143 ms/token, same box).
+DECODE_SLAB_ATTN = os.environ.get("DLA_DECODE_SLAB_ATTN", "0") == "1"
 
 
 def qkv_attend(s: torch.Tensor, ssq: torch.Tensor, norm_w: torch.Tensor, eps: float, w: torch.Tensor,
