@@ -586,7 +586,9 @@ at::Tensor decode_qkv_attn(const at::Tensor& s, const at::Tensor& ssq, const at:
   TORCH_CHECK(rot % 16 == 0 && rot <= D && rot > 0, "rot % 16 == 0, 0 < rot <= D");
   TORCH_CHECK(cos.is_contiguous() && sin.is_contiguous() && cos.size(-1) == rot / 2, "rope tables");
   TORCH_CHECK(pos.numel() == M && pos.is_contiguous(), "pos [B]");
-  TORCH_CHECK(sync_cnt.numel() >= 1 && len_first.numel() >= 1 && err.numel() >= 1, "sync words");
+  TORCH_CHECK(sync_cnt.numel() >= 8 * 32 && sync_cnt.is_contiguous() && len_first.numel() >= 1 &&
+                  err.numel() >= 1,
+              "sync words (sync_cnt: 8 counter replicas x 32 ints)");
   check_aligned16(s, "s");
   check_aligned16(wt, "wt");
   check_aligned16(k_cache, "k_cache");

@@ -755,8 +755,20 @@ __global__ __launch_bounds__(256, 2) void decode_attn_loop_kernel(
 // cannot deadlock; a wait beyond ~2^22 polls (far past any real step) sets `err` and proceeds
 // rather than hanging the GPU. Barrier discipline: phase 1 runs on all 8 waves with the same
 // barrier sequence whichever call site reaches it, and waves 4-7 exit only after it.
+constexpr int kQaRep = 8;       // arrival-counter replicas (pollers per cache line / 8)
+constexpr int kQaRepStride = 32;  // ints between replicas: one 128-byte line each
+
+// 16-byte load that bypasses the CU's vector L1 and reads device-coherent data (`sc1`): the
+// consumer side of the write-through hand-off (global_, never flat_; waits for itself)
+__device__ __forceinline__ bf16x8 load_sc1_16(const bf16_t* p) {
+  typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+  u32x4v v;
+  asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
+  return __builtin_bit_cast(bf16x8, v);
+}
+
 struct DecQkvSync {
-  int* cnt;              // this layer's arrival counter (monotonic within a generation)
+  int* cnt;              // this layer's arrival counter, kQaRep replicas kQaRepStride ints apart
   const int* len_first;  // kv_len of the first decode step since the counter was zeroed
   int nq;                // qkv tiles (16 columns each)
   int na;                // attention units = workgroups [0, na)
@@ -777,18 +789,23 @@ __global__ __launch_bounds__(512) void decode_qkv_attn_kernel(
   const bool attn = bid < sy.na;
   const int t0 = attn ? bid * sy.ta : sy.na * sy.ta + (bid - sy.na) * sy.tn;
   const int t1 = min(sy.nq, t0 + (attn ? sy.ta : sy.tn));
+  __shared__ __attribute__((aligned(16))) bf16_t qkv_s[(G + 2) * D];
+  // Hand-off without release / acquire fences (an agent release writes back the XCD's L2, ~1.7 us
+  // per workgroup; an acquire ~1.7 us per consumer): every qkv byte is stored write-through (`sc1`)
+  // and drained by its storing wave before the workgroup's counter add, and every consumer load
+  // of it is an `sc1` load after the poll. The counter is replicated on kQaRep lines (one add per
+  // replica, one wave instruction) so the ~200 pollers spread over 8 lines.
   auto qkv_phase = [&]() {  // all 8 waves
     for (int t = t0; t < t1; ++t) {
-      ks_body<2, true, false, 1, kKsUnroll, false, true, true>(t, sy.nq, x, ldx, Wt, K, qkv, ldq, M, N, K, fz);
+      ks_body<2, true, false, 1, kKsUnroll, false, true, true, true>(t, sy.nq, x, ldx, Wt, K, qkv, ldq, M, N,
+                                                                       K, fz);
       __syncthreads();  // the reduction buffer is reused by the next tile
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave's own stores
     __syncthreads();
-    if (threadIdx.x == 0 && t1 > t0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the release's write-back before the add)
-      __hip_atomic_fetch_add(sy.cnt, t1 - t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (threadIdx.x < kQaRep && t1 > t0)
+      __hip_atomic_fetch_add(sy.cnt + threadIdx.x * kQaRepStride, t1 - t0, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
   };
   if (!attn || wave >= 4) {
     qkv_phase();
@@ -799,22 +816,31 @@ __global__ __launch_bounds__(512) void decode_qkv_attn_kernel(
     qkv_phase();
     if (threadIdx.x == 0) {
       const int target = sy.nq * (kv_len[0] - sy.len_first[0] + 1);
+      const int* rep = sy.cnt + (bid % kQaRep) * kQaRepStride;
       int spins = 0;
-      while (__hip_atomic_load(sy.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-        __builtin_amdgcn_s_sleep(2);
-        if (++spins > (1 << 22)) {
+      while (__hip_atomic_load(rep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        __builtin_amdgcn_s_sleep(4);
+        if (++spins > (1 << 21)) {
           __hip_atomic_store(sy.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
         }
       }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();  // (waves 4-7 have ended: the barrier counts waves 0-3)
+    // this block's q heads, k and v of the newest token into LDS, by `sc1` loads
+    const bf16_t* row = qkv + (int64_t)b * ldq;
+    for (int i = threadIdx.x; i < (G + 2) * D / 8; i += 256) {
+      const int e = i * 8;
+      const int col = e < G * D ? hk * G * D + e
+                                : (e < (G + 1) * D ? Hq * D + hk * D + (e - G * D)
+                                                   : (Hq + Hkv) * D + hk * D + (e - (G + 1) * D));
+      *reinterpret_cast<bf16x8*>(&qkv_s[e]) = load_sc1_16(row + col);
+    }
+    __syncthreads();
   };
   dec_loop_body<D, G, true, true, 2>(split, hk, b, Hkv, nullptr, 0, 0, kc, vc, c_sb, c_st, c_sh, kv_len,
                                      kv_start, window, scale_log2, nsplit, cpb, part_o, part_ml, Hq, rp,
-                                     out, o_sb, o_sh, ccnt, Tcap, wait);
+                                     out, o_sb, o_sh, ccnt, Tcap, wait, qkv_s);
 }
 
 // splits of the fused kernel's attention units: ~256 units, in-kernel combine (<= 8 splits)

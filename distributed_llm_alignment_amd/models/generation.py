@@ -57,8 +57,9 @@ class KVCache:
         self.kv_len = torch.ones(1, dtype=torch.int32, device=dev)
         # fused qkv + attention decode kernel (ops.decode.qkv_attend): per-layer arrival counters
         # of its qkv blocks (monotonic within a generation, zeroed at every prefill), the kv_len of
-        # the first decode step, and a sticky wait-timeout word
-        self.sync = torch.zeros(L, dtype=torch.int32, device=dev)
+        # the first decode step, and a sticky wait-timeout word. Each layer's counter is kept in 8
+        # replicas on 128-byte lines of their own (csrc/decode.hip kQaRep / kQaRepStride)
+        self.sync = torch.zeros((L, 8, 32), dtype=torch.int32, device=dev)
         self.len_first = torch.ones(1, dtype=torch.int32, device=dev)
         self.sync_err = torch.zeros(1, dtype=torch.int32, device=dev)
         self.pos = torch.zeros((batch, 1), dtype=torch.int32, device=dev)
@@ -145,7 +146,7 @@ class KVCache:
         o = ops._ext.require().decode_qkv_attn(
             s, ssq, wt, float(eps), cos, sin, self.pos.view(-1), self.k[layer], self.v[layer], self.slot,
             self.kv_len, self.kv_start, window, 1.0 / math.sqrt(D), self.h_local, self.kv_local, D,
-            rope.rot_dim, self.sync[layer:layer + 1], self.len_first, self.sync_err)
+            rope.rot_dim, self.sync[layer], self.len_first, self.sync_err)
         return o.reshape(B, 1, self.h_local * D)
 
     def attend_slab(self, layer: int, s: torch.Tensor, ssq: torch.Tensor, wt: torch.Tensor, eps: float,
