@@ -26,4 +26,12 @@ timeout -k 10 400 python -u tools/bench_rlhf.py --batch 8 > $O/rlhf_b8.log 2>&1 
 tail -1 $O/rlhf_b8.log
 timeout -k 10 600 python -u tools/bench_rlhf.py --algorithm ppo --zero-shape 8 --batch 8 > $O/ppo_z8_nockpt.log 2>&1 || { echo "PPO_NOCKPT rc=$?"; tail -3 $O/ppo_z8_nockpt.log; }
 tail -1 $O/ppo_z8_nockpt.log
+timeout -k 10 300 python -u tools/grouped_gemm_bench.py --scheds 0,3 --rounds 2 > $O/gg_bench.log 2>&1 || { echo "GG rc=$?"; tail -3 $O/gg_bench.log; }
+grep '^{' $O/gg_bench.log | tail -12
+cd /tmp
+timeout -k 10 420 rocprofv3 --kernel-trace --output-format csv -d /tmp/pmx -o run -- python3 $R/bench.py --model mixtral-8x7b --ep-shape 8 --micro-pairs 2 --accum 8 --ep-capacity 1.25 --steps 2 --warmup 1 > $R/$O/prof_mixtral.log 2>&1 || exit 1
+tr=$(find /tmp/pmx -name '*kernel_trace.csv' | head -1)
+python3 $R/scripts/step_breakdown.py "$tr" > $R/$O/mixtral_breakdown.md
+python3 $R/scripts/prof_window.py "$tr" --window adamw --top 45 > $R/$O/mixtral_top.md
+rm -rf /tmp/pmx
 echo ALL_DONE
