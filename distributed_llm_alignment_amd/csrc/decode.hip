@@ -906,11 +906,17 @@ bool launch_decode_qkv_attn(const bf16_t* x, int64_t ldx, const bf16_t* Wt, bf16
   const double wq = 32.0 * K, wa = 2.0 * cpb * kDecChunk * D * 2;
   const double per = (nq * wq + na * wa) / grid;
   int ta, tn;
+  // DLA_QA_TA (A/B knob): qkv tiles per attention workgroup; the rest are dealt to the others
+  static const int ta_env = [] {
+    const char* e = std::getenv("DLA_QA_TA");
+    return e ? std::atoi(e) : -1;
+  }();
   if (na >= grid) {
     ta = (nq + grid - 1) / grid;
     tn = 0;
   } else {
     ta = std::max(0, static_cast<int>((per - wa) / wq + 0.5));
+    if (ta_env >= 0) ta = ta_env;
     ta = std::min(ta, nq / std::max(na, 1));
     tn = (nq - na * ta + (grid - na) - 1) / (grid - na);
   }
