@@ -336,6 +336,35 @@ def _loop_experts_backward(dys, xs, gu, w_up, w_down, counts, needs):
     return dxs, outs[0], outs[1]
 
 
+# One local expert (EP with E / ep = 1, e.g. Mixtral at ep 8): the group is the whole padded
+# capacity buffer, so the down projection forward and the gate|up input gradient run as plain
+# hipBLASLt GEMMs over its static row count (row-independent: the unwritten padding rows only
+# produce output rows nobody reads, and the input gradient's are zeroed below). Measured in the
+# Mixtral --ep-shape 8 step: the grouped kernel ran those two at 670 / 534 TFLOP/s at 4096 rows
+# per call (one 256-row tile per CU over a 14336- / 28672-deep K). DLA_MOE_SINGLE_LIB=0: grouped.
+MOE_SINGLE_LIB = os.environ.get("DLA_MOE_SINGLE_LIB", "1") != "0"
+
+
+def _expert0_t(w: torch.Tensor) -> torch.Tensor:
+    """Cached transposed copy of expert 0's weight w[0] ([N, K] -> [K, N]), refreshed when the
+    weight's version counter or its engine's weight epoch moved."""
+    ep = getattr(w, "_dla_epoch", None)
+    key = (w._version, ep[0] if ep is not None else 0)
+    c = getattr(w, "_dla_wt0", None)
+    if c is None or c[0] != key:
+        with torch.no_grad():
+            t = c[1] if c is not None else torch.empty((w.shape[2], w.shape[1]), dtype=w.dtype, device=w.device)
+            _ext.require().transpose_bf16(w.detach()[0], t)
+        c = (key, t)
+        w._dla_wt0 = c
+    return c[1]
+
+
+def _single_lib(offs: torch.Tensor, w: torch.Tensor, rows: int) -> bool:
+    return (MOE_SINGLE_LIB and offs.numel() == 2 and w.shape[0] == 1 and w.dtype == torch.bfloat16
+            and rows >= 256)
+
+
 class _GroupedExpertsFn(torch.autograd.Function):
     """Grouped SwiGLU experts on the device-driven grouped GEMM; offs [E+1] int32 on device.
     `sync_free`: the backward also stays on the grouped kernels (never reads offs on the host)."""
@@ -352,7 +381,10 @@ class _GroupedExpertsFn(torch.autograd.Function):
             ys = C.gg_fwd(aq, wd_q, offs, asc, wd_s)
         else:
             gu, a = C.gg_fwd_swiglu(xs, w_up, offs, None, None)
-            ys = C.gg_fwd(a, w_down, offs, None, None)
+            if _single_lib(offs, w_down, a.shape[0]):
+                ys = F.linear(a, w_down.detach()[0])
+            else:
+                ys = C.gg_fwd(a, w_down, offs, None, None)
         ctx.save_for_backward(xs, gu, offs)
         ctx.w_up, ctx.w_down = w_up, w_down  # (on ctx: see ops.linear._LinearMainGradFn)
         ctx.sync_free = sync_free
@@ -389,7 +421,12 @@ class _GroupedExpertsFn(torch.autograd.Function):
                 outs.append(gw)
             else:
                 outs.append(None)
-        dxs = C.gg_dgrad(dgu, w_up, offs) if ctx.needs_input_grad[0] else None
+        dxs = None
+        if ctx.needs_input_grad[0]:
+            if _single_lib(offs, w_up, dgu.shape[0]):
+                dxs = F.linear(dgu, _expert0_t(w_up))  # dgu [M, 2F] . W_up[0] [2F, H], TN layout
+            else:
+                dxs = C.gg_dgrad(dgu, w_up, offs)
         if dxs is not None and dxs.shape[0] > 0:
             # rows past offs[-1] (padding of a capacity buffer) are never written by the kernel
             tail = torch.arange(dxs.shape[0], device=dxs.device) >= offs[-1].long()

@@ -83,7 +83,8 @@ def test_combine_capacity_layout_kernels():
     assert torch.allclose(dw, rdw, atol=1e-1, rtol=1e-2)
 
 
-def test_expert_parallel_shape_mode_layer_matches_fp32():
+@pytest.mark.parametrize("shape_ep", [4, 8])  # 2 local experts: grouped kernels; 1: the hipBLASLt path
+def test_expert_parallel_shape_mode_layer_matches_fp32(shape_ep):
     """bench.py --ep-shape on the GPU: the capacity dispatch (identity all-to-alls, device-built
     expert order, grouped expert kernels, padded combine) of one EP rank's experts, forward and
     backward, against the same layer in fp32 on the CPU."""
@@ -94,7 +95,7 @@ def test_expert_parallel_shape_mode_layer_matches_fp32():
 
     cfg = get_config("tiny-mixtral", hidden_size=256, intermediate_size=512, num_experts=8)
     m = build_model(cfg, device="cpu", dtype=torch.float32, seed=2)
-    apply_expert_parallel(m, None, capacity_factor=2.0, shape_ep=4)
+    apply_expert_parallel(m, None, capacity_factor=2.0, shape_ep=shape_ep)
     mg = copy.deepcopy(m).to(DEV, torch.bfloat16)
     m = m.to(torch.bfloat16).to(torch.float32)  # the reference sees the same (rounded) weights
     g = torch.Generator().manual_seed(5)
