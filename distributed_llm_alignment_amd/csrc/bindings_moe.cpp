@@ -16,6 +16,7 @@ void launch_moe_topk_bwd(const float*, const int*, const float*, int64_t, int, i
 void launch_moe_dispatch(const bf16_t*, const int*, int64_t, int, int, bf16_t*, hipStream_t);
 void launch_moe_combine(const bf16_t*, const int*, const float*, int64_t, int, int, bf16_t*,
                         hipStream_t);
+void launch_zero_rows_from(bf16_t*, int64_t, int, int64_t, const int*, hipStream_t);
 void launch_moe_combine_bwd(const bf16_t*, const bf16_t*, const int*, const float*, int64_t, int,
                             int, bf16_t*, float*, hipStream_t);
 
@@ -394,6 +395,18 @@ at::Tensor moe_combine(const at::Tensor& ys, const at::Tensor& pos,
   return out;
 }
 
+// x[r] = 0 for r >= from[0] (device scalar: e.g. offs[-1] of a capacity buffer); no host sync
+void zero_rows_from(at::Tensor& x, const at::Tensor& from) {
+  check_bf16(x, "x");
+  check_i32(from, "from");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0 && x.size(1) % 8 == 0,
+              "x [R, C], C % 8 == 0, 16-byte aligned rows");
+  check_aligned16(x, "x");
+  TORCH_CHECK(from.numel() >= 1, "from: one int32 on the device");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  launch_zero_rows_from(bp(x), x.size(0), (int)x.size(1), x.stride(0), from.data_ptr<int>(), cur_stream(x));
+}
+
 std::tuple<at::Tensor, at::Tensor> moe_combine_bwd(const at::Tensor& dout, const at::Tensor& ys,
                                                    const at::Tensor& pos, const at::Tensor& w) {
   check_bf16(dout, "dout");
@@ -430,6 +443,7 @@ TORCH_LIBRARY_FRAGMENT(dla, m) {
   m.def("moe_dispatch(Tensor x, Tensor pos) -> Tensor");
   m.def("moe_combine(Tensor ys, Tensor pos, Tensor? w) -> Tensor");
   m.def("moe_combine_bwd(Tensor dout, Tensor ys, Tensor pos, Tensor w) -> (Tensor, Tensor)");
+  m.def("zero_rows_from(Tensor(a!) x, Tensor from) -> ()");
   m.def("gg_fwd(Tensor x, Tensor w, Tensor offs, Tensor? sx, Tensor? sw) -> Tensor");
   m.def("gg_fwd_swiglu(Tensor x, Tensor w_up, Tensor offs, Tensor? sx, Tensor? sw) -> (Tensor, Tensor)");
   m.def("gg_dgrad(Tensor dy, Tensor w, Tensor offs) -> Tensor");
@@ -448,6 +462,7 @@ TORCH_LIBRARY_IMPL(dla, CUDA, m) {
   m.impl("moe_dispatch", &dla::moe_dispatch);
   m.impl("moe_combine", &dla::moe_combine);
   m.impl("moe_combine_bwd", &dla::moe_combine_bwd);
+  m.impl("zero_rows_from", &dla::zero_rows_from);
   m.impl("gg_fwd", &dla::gg_fwd);
   m.impl("gg_fwd_swiglu", &dla::gg_fwd_swiglu);
   m.impl("gg_dgrad", &dla::gg_dgrad);

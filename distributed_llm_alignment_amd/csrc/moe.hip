@@ -266,6 +266,25 @@ void launch_moe_dispatch(const bf16_t* x, const int* pos, int64_t N, int H, int 
   if (N == 0) return;
   moe_dispatch_kernel<<<N, 256, 0, st>>>(x, pos, N, H, k, xs);
 }
+// zero rows [*from, R) of a [R, C] bf16 tensor (C % 8 == 0), the row bound read on the device:
+// the unwritten padding rows of a capacity buffer before a GEMM reduces over them
+__global__ __launch_bounds__(256) void zero_rows_from_kernel(bf16_t* __restrict__ x, int64_t R, int C,
+                                                             int64_t ld, const int* __restrict__ from) {
+  const int64_t r0 = from[0];
+  const int64_t per_row = C / 8;
+  const int64_t n = (R - r0) * per_row;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * 256) {
+    const int64_t r = r0 + i / per_row, c = (i % per_row) * 8;
+    store_bf16x8(x + r * ld + c, bf16x8{0, 0, 0, 0, 0, 0, 0, 0});
+  }
+}
+
+void launch_zero_rows_from(bf16_t* x, int64_t R, int C, int64_t ld, const int* from, hipStream_t st) {
+  if (R == 0 || C == 0) return;
+  zero_rows_from_kernel<<<1024, 256, 0, st>>>(x, R, C, ld, from);
+}
+
 void launch_moe_combine(const bf16_t* ys, const int* pos, const float* w, int64_t N, int H, int k,
                         bf16_t* out, hipStream_t st) {
   if (N == 0) return;

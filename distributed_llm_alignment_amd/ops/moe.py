@@ -32,7 +32,7 @@ import torch.nn.functional as F
 
 from . import _ext
 from .activations import swiglu
-from .linear import addmm_into
+from .linear import _wgrad_accumulate, addmm_into
 
 
 # ------------------------------------------------------------------------------ router
@@ -405,11 +405,23 @@ class _GroupedExpertsFn(torch.autograd.Function):
         dys = dys.contiguous()
         # da = dy . W_down fused with the SwiGLU backward -> dgu, plus the recomputed a
         dgu, a = C.gg_dgrad_swiglu(dys, w_down, offs, gu)
+        single = _single_lib(offs, w_up, dgu.shape[0])
+        if single:
+            # the weight gradients reduce over the rows: the padding rows the grouped kernel left
+            # unwritten must be zero (xs's and dys's already are)
+            C.zero_rows_from(dgu, offs[1:])
+            C.zero_rows_from(a, offs[1:])
         outs = []
         for w, dy, x, need in ((w_up, dgu, xs, ctx.needs_input_grad[1]),
                                (w_down, dys, a, ctx.needs_input_grad[2])):
             mg = getattr(w, "main_grad", None)
-            if mg is not None and mg.is_contiguous() and mg.dtype in (torch.bfloat16, torch.float32):
+            if single and mg is not None and mg.is_contiguous() and mg.dtype in (torch.bfloat16, torch.float32):
+                _wgrad_accumulate(mg[0], dy, x)
+                hook = getattr(w, "_dla_grad_hook", None)
+                if hook is not None:
+                    hook(w)
+                outs.append(None)
+            elif mg is not None and mg.is_contiguous() and mg.dtype in (torch.bfloat16, torch.float32):
                 C.gg_wgrad(dy, x, offs, mg, True)
                 hook = getattr(w, "_dla_grad_hook", None)
                 if hook is not None:

@@ -98,6 +98,8 @@ def test_expert_parallel_shape_mode_layer_matches_fp32(shape_ep):
     apply_expert_parallel(m, None, capacity_factor=2.0, shape_ep=shape_ep)
     mg = copy.deepcopy(m).to(DEV, torch.bfloat16)
     m = m.to(torch.bfloat16).to(torch.float32)  # the reference sees the same (rounded) weights
+    for w in (mg.layers[0].mlp.expert_up, mg.layers[0].mlp.expert_down):  # as a training engine does
+        w.main_grad = torch.zeros(w.shape, dtype=torch.float32, device=DEV)
     g = torch.Generator().manual_seed(5)
     h = torch.randn(2, 256, cfg.hidden_size, generator=g).to(torch.bfloat16).float()
     outs = []
@@ -105,7 +107,8 @@ def test_expert_parallel_shape_mode_layer_matches_fp32(shape_ep):
         x.requires_grad_(True)
         y = mod(x)
         y.float().pow(2).sum().backward()
-        outs.append((y.detach().float().cpu(), x.grad.float().cpu(), mod.expert_up.grad.float().cpu()))
+        gu = mod.expert_up.main_grad if x.is_cuda else mod.expert_up.grad
+        outs.append((y.detach().float().cpu(), x.grad.float().cpu(), gu.float().cpu()))
     (y0, dx0, du0), (y1, dx1, du1) = outs
     # a token whose top-2 router logits nearly tie may pick another expert in bf16 than in fp32:
     # per-token rows are compared with a small allowance for such flips, the expert grads as a whole
