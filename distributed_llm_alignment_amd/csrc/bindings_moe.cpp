@@ -17,6 +17,9 @@ void launch_moe_dispatch(const bf16_t*, const int*, int64_t, int, int, bf16_t*, 
 void launch_moe_combine(const bf16_t*, const int*, const float*, int64_t, int, int, bf16_t*,
                         hipStream_t);
 void launch_zero_rows_from(bf16_t*, int64_t, int, int64_t, const int*, hipStream_t);
+void launch_ep_route(const void*, bool, int, int, int, int, int, int, int64_t*, int*, int*, int64_t*,
+                     hipStream_t);
+void launch_ep_expert_order(const int*, int, int, int, int64_t*, int64_t*, int*, hipStream_t);
 void launch_moe_combine_bwd(const bf16_t*, const bf16_t*, const int*, const float*, int64_t, int,
                             int, bf16_t*, float*, hipStream_t);
 
@@ -395,6 +398,45 @@ at::Tensor moe_combine(const at::Tensor& ys, const at::Tensor& pos,
   return out;
 }
 
+// Expert-parallel capacity routing of one token chunk (parallel/expert.py _route_chunk):
+// topi [n, k] int32/int64 -> (send_src [ep*C] int64, pos [n, k] int32, sent [ep, El] int32);
+// the dropped-slot count is added to `dropped` (int64 [1] on the device).
+std::tuple<at::Tensor, at::Tensor, at::Tensor> ep_route(const at::Tensor& topi, int64_t E, int64_t ep,
+                                                        int64_t C, at::Tensor& dropped) {
+  check_cuda(topi, "topi");
+  TORCH_CHECK(topi.dim() == 2 && topi.is_contiguous() &&
+                  (topi.scalar_type() == at::kInt || topi.scalar_type() == at::kLong),
+              "topi [n, k] int32/int64 contiguous");
+  TORCH_CHECK(dropped.scalar_type() == at::kLong && dropped.numel() >= 1 && dropped.device() == topi.device(),
+              "dropped: int64 counter on the device");
+  const int64_t n = topi.size(0), k = topi.size(1), S = n * k;
+  TORCH_CHECK(E >= 1 && E <= 64 && ep >= 1 && E % ep == 0 && C >= 1, "1 <= E <= 64, ep | E");
+  TORCH_CHECK(S <= 256 * 64, "ep_route: at most 16384 slots per chunk");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(topi.device());
+  auto send_src = at::empty({ep * C}, topi.options().dtype(at::kLong));
+  auto pos = at::empty({n, k}, topi.options().dtype(at::kInt));
+  auto sent = at::empty({ep, E / ep}, topi.options().dtype(at::kInt));
+  launch_ep_route(topi.data_ptr(), topi.scalar_type() == at::kLong, (int)S, (int)k, (int)E, (int)(E / ep),
+                  (int)ep, (int)C, send_src.data_ptr<int64_t>(), pos.data_ptr<int>(), sent.data_ptr<int>(),
+                  dropped.data_ptr<int64_t>(), cur_stream(topi));
+  return {send_src, pos, sent};
+}
+
+// Receiver side (_expert_order): rc [ep, El] int32 -> (xe_src [ep*C], inv [ep*C] int64, offs [El+1] int32)
+std::tuple<at::Tensor, at::Tensor, at::Tensor> ep_expert_order(const at::Tensor& rc, int64_t C) {
+  check_i32(rc, "rc");
+  TORCH_CHECK(rc.dim() == 2 && rc.is_contiguous() && rc.size(0) <= 64 && rc.size(1) <= 64 && C >= 1,
+              "rc [ep <= 64, El <= 64] contiguous");
+  const int64_t ep = rc.size(0), El = rc.size(1);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(rc.device());
+  auto xe_src = at::empty({ep * C}, rc.options().dtype(at::kLong));
+  auto inv = at::empty({ep * C}, rc.options().dtype(at::kLong));
+  auto offs = at::empty({El + 1}, rc.options());
+  launch_ep_expert_order(rc.data_ptr<int>(), (int)ep, (int)El, (int)C, xe_src.data_ptr<int64_t>(),
+                         inv.data_ptr<int64_t>(), offs.data_ptr<int>(), cur_stream(rc));
+  return {xe_src, inv, offs};
+}
+
 // x[r] = 0 for r >= from[0] (device scalar: e.g. offs[-1] of a capacity buffer); no host sync
 void zero_rows_from(at::Tensor& x, const at::Tensor& from) {
   check_bf16(x, "x");
@@ -444,6 +486,8 @@ TORCH_LIBRARY_FRAGMENT(dla, m) {
   m.def("moe_combine(Tensor ys, Tensor pos, Tensor? w) -> Tensor");
   m.def("moe_combine_bwd(Tensor dout, Tensor ys, Tensor pos, Tensor w) -> (Tensor, Tensor)");
   m.def("zero_rows_from(Tensor(a!) x, Tensor from) -> ()");
+  m.def("ep_route(Tensor topi, int E, int ep, int C, Tensor(a!) dropped) -> (Tensor, Tensor, Tensor)");
+  m.def("ep_expert_order(Tensor rc, int C) -> (Tensor, Tensor, Tensor)");
   m.def("gg_fwd(Tensor x, Tensor w, Tensor offs, Tensor? sx, Tensor? sw) -> Tensor");
   m.def("gg_fwd_swiglu(Tensor x, Tensor w_up, Tensor offs, Tensor? sx, Tensor? sw) -> (Tensor, Tensor)");
   m.def("gg_dgrad(Tensor dy, Tensor w, Tensor offs) -> Tensor");
@@ -463,6 +507,8 @@ TORCH_LIBRARY_IMPL(dla, CUDA, m) {
   m.impl("moe_combine", &dla::moe_combine);
   m.impl("moe_combine_bwd", &dla::moe_combine_bwd);
   m.impl("zero_rows_from", &dla::zero_rows_from);
+  m.impl("ep_route", &dla::ep_route);
+  m.impl("ep_expert_order", &dla::ep_expert_order);
   m.impl("gg_fwd", &dla::gg_fwd);
   m.impl("gg_fwd_swiglu", &dla::gg_fwd_swiglu);
   m.impl("gg_dgrad", &dla::gg_dgrad);

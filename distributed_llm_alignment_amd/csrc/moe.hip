@@ -266,6 +266,161 @@ void launch_moe_dispatch(const bf16_t* x, const int* pos, int64_t N, int H, int 
   if (N == 0) return;
   moe_dispatch_kernel<<<N, 256, 0, st>>>(x, pos, N, H, k, xs);
 }
+// ---------------------------------------------------------------------------------------------
+// Expert-parallel capacity routing (parallel/expert.py `_route_chunk` / `_expert_order`), each
+// as ONE single-workgroup launch instead of ~20 small torch ops (argsort, scatters, cumsums):
+// the EP step launched ~160 kernels per layer and pass, most of them these.
+//
+// ep_route: slot s = (token t, choice j) of expert e = topi[t, j], destination d = e / El.
+// Ranks are stable (slot order) within each expert: slots go through in 64-slot batches, one
+// ballot per expert per batch; pass 1 counts per (batch, expert) into LDS, a per-expert scan over
+// the batches gives each batch's base, pass 2 ranks. Then, as the torch form: the slot's offset
+// in its destination's expert-sorted block, kept if < C, its send row d * C + off (else the
+// dropped row ep * C), send_src[row] = t (-1 where empty), the rows actually sent per
+// (destination, local expert), and the dropped count added to a device counter.
+constexpr int kRouteThreads = 1024;
+constexpr int kRouteMaxE = 64;
+constexpr int kRouteMaxBatches = 256;  // 16384 slots per chunk (host-checked)
+
+template <typename TI>
+__global__ __launch_bounds__(kRouteThreads) void ep_route_kernel(
+    const TI* __restrict__ topi, int S, int k, int E, int El, int ep, int C,
+    int64_t* __restrict__ send_src, int* __restrict__ pos, int* __restrict__ sent,
+    int64_t* __restrict__ dropped) {
+  __shared__ int bcnt[kRouteMaxBatches][kRouteMaxE];  // (batch, expert) counts -> bases
+  __shared__ int ecnt[kRouteMaxE], ecum[kRouteMaxE + 1];
+  __shared__ int ndrop;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = kRouteThreads / 64;
+  const int nb = (S + 63) / 64;
+  for (int i = tid; i < ep * C; i += kRouteThreads) send_src[i] = -1;
+  if (tid == 0) ndrop = 0;
+  // pass 1: per-batch counts
+  for (int b = wv; b < nb; b += nw) {
+    const int s = b * 64 + lane;
+    const int e = s < S ? static_cast<int>(topi[s]) : -1;
+    for (int x = 0; x < E; ++x) {
+      const uint64_t m = __ballot(e == x);
+      if (lane == 0) bcnt[b][x] = __popcll(m);
+    }
+  }
+  __syncthreads();
+  // per-expert exclusive scan over the batches (one thread per expert)
+  if (tid < E) {
+    int run = 0;
+    for (int b = 0; b < nb; ++b) {
+      const int c = bcnt[b][tid];
+      bcnt[b][tid] = run;
+      run += c;
+    }
+    ecnt[tid] = run;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int run = 0;
+    for (int x = 0; x < E; ++x) {
+      ecum[x] = run;
+      run += ecnt[x];
+    }
+    ecum[E] = run;
+  }
+  __syncthreads();
+  // sent rows per (destination, local expert): the first C of each destination block in order
+  for (int i = tid; i < E; i += kRouteThreads) {
+    const int d = i / El;
+    const int before = ecum[i] - ecum[d * El];
+    sent[i] = min(max(C - before, 0), ecnt[i]);
+  }
+  // pass 2: ranks -> positions
+  for (int b = wv; b < nb; b += nw) {
+    const int s = b * 64 + lane;
+    const int e = s < S ? static_cast<int>(topi[s]) : -1;
+    int rank = 0;
+    for (int x = 0; x < E; ++x) {
+      const uint64_t m = __ballot(e == x);
+      if (e == x) rank = bcnt[b][x] + __popcll(m & ((1ull << lane) - 1ull));
+    }
+    if (s < S) {
+      const int d = e / El;
+      const int off = ecum[e] + rank - ecum[d * El];
+      int p;
+      if (off < C) {
+        p = d * C + off;
+        send_src[p] = s / k;
+      } else {
+        p = ep * C;
+        atomicAdd(&ndrop, 1);
+      }
+      pos[s] = p;
+    }
+  }
+  __syncthreads();
+  if (tid == 0 && ndrop > 0) dropped[0] += ndrop;
+}
+
+// ep_expert_order (receiver): rc [ep, El] rows received per (source, local expert), each source's
+// block local-expert sorted. Row j < C of source s: its local expert e (first with j < the
+// inclusive prefix of rc[s]), its index in that run, and its expert-major position q = (rows of
+// experts < e over all sources) + (rows of expert e from sources < s) + index. Outputs
+// xe_src[q] = s * C + j (-1 where no row), inv[s * C + j] = q (-1 past the source's rows), and
+// the grouped-GEMM offsets offs[El + 1].
+__global__ __launch_bounds__(kRouteThreads) void ep_expert_order_kernel(
+    const int* __restrict__ rc, int ep, int El, int C, int64_t* __restrict__ xe_src,
+    int64_t* __restrict__ inv, int* __restrict__ offs) {
+  __shared__ int cum_s[64][kRouteMaxE + 1];  // per source: exclusive prefix over local experts
+  __shared__ int start_es[kRouteMaxE][64];   // expert-major start of (e, s)
+  __shared__ int tot_s[64];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < ep * C; i += kRouteThreads) xe_src[i] = -1;
+  if (tid < ep) {
+    int run = 0;
+    for (int e = 0; e < El; ++e) {
+      cum_s[tid][e] = run;
+      run += rc[tid * El + e];
+    }
+    cum_s[tid][El] = run;
+    tot_s[tid] = run;
+  }
+  if (tid == 0) {
+    int run = 0;
+    offs[0] = 0;
+    for (int e = 0; e < El; ++e) {
+      for (int s2 = 0; s2 < ep; ++s2) {
+        start_es[e][s2] = run;
+        run += rc[s2 * El + e];
+      }
+      offs[e + 1] = run;
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < ep * C; i += kRouteThreads) {
+    const int s2 = i / C, j = i % C;
+    if (j >= tot_s[s2]) {
+      inv[i] = -1;
+      continue;
+    }
+    int e = 0;
+    while (e + 1 < El && j >= cum_s[s2][e + 1]) ++e;
+    const int q = start_es[e][s2] + (j - cum_s[s2][e]);
+    inv[i] = q;
+    xe_src[q] = i;
+  }
+}
+
+void launch_ep_route(const void* topi, bool i64, int S, int k, int E, int El, int ep, int C,
+                     int64_t* send_src, int* pos, int* sent, int64_t* dropped, hipStream_t st) {
+  if (i64)
+    ep_route_kernel<int64_t><<<1, kRouteThreads, 0, st>>>(static_cast<const int64_t*>(topi), S, k, E, El, ep,
+                                                          C, send_src, pos, sent, dropped);
+  else
+    ep_route_kernel<int><<<1, kRouteThreads, 0, st>>>(static_cast<const int*>(topi), S, k, E, El, ep, C,
+                                                      send_src, pos, sent, dropped);
+}
+
+void launch_ep_expert_order(const int* rc, int ep, int El, int C, int64_t* xe_src, int64_t* inv, int* offs,
+                            hipStream_t st) {
+  ep_expert_order_kernel<<<1, kRouteThreads, 0, st>>>(rc, ep, El, C, xe_src, inv, offs);
+}
+
 // zero rows [*from, R) of a [R, C] bf16 tensor (C % 8 == 0), the row bound read on the device:
 // the unwritten padding rows of a capacity buffer before a GEMM reduces over them
 __global__ __launch_bounds__(256) void zero_rows_from_kernel(bf16_t* __restrict__ x, int64_t R, int C,

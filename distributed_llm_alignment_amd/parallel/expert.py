@@ -28,6 +28,7 @@ expert-data-parallel group (replicas holding the same experts) instead of the fu
 """
 from __future__ import annotations
 
+import os
 from typing import List
 
 import torch
@@ -111,6 +112,15 @@ class _A2AWait(torch.autograd.Function):
         return g, None
 
 
+# the capacity routing's slot placement and receiver order as one HIP launch each
+# (csrc/moe.hip ep_route / ep_expert_order) instead of ~20 torch ops; DLA_EP_NATIVE_ROUTE=0: torch
+_NATIVE_ROUTE = os.environ.get("DLA_EP_NATIVE_ROUTE", "1") != "0"
+
+
+def _native_route(topi: torch.Tensor, E: int, ep: int, slots: int) -> bool:
+    return _NATIVE_ROUTE and topi.is_cuda and E <= 64 and slots <= 16384 and topi.dtype in (torch.int32, torch.int64)
+
+
 def _gather_rows(x: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
     """out[i] = x[idx[i]] (idx < 0 -> zero row). Static shapes, no host sync; the backward is the
     matching scatter (idx is injective on its valid entries)."""
@@ -168,6 +178,11 @@ class ExpertParallel:
         ep, El, E = self.ep, self.El, self.E
         n, k = topi.shape
         dev = topi.device
+        if _native_route(topi, E, ep, n * k):
+            if self._dropped is None:
+                self._dropped = torch.zeros((), dtype=torch.long, device=dev)
+            send_src, pos, sent = ops._ext.require().ep_route(topi.contiguous(), E, ep, C, self._dropped.view(1))
+            return send_src, pos, sent, None  # (dropped slots counted by the kernel)
         flat = topi.reshape(-1).long()
         order = torch.argsort(flat, stable=True)
         rank_sorted = torch.empty_like(order)
@@ -193,6 +208,8 @@ class ExpertParallel:
         of every recv row or -1, grouped-GEMM offsets [El+1] int32)."""
         ep, El = self.ep, self.El
         dev = rc.device
+        if rc.is_cuda and ep <= 64 and El <= 64 and _NATIVE_ROUTE:
+            return ops._ext.require().ep_expert_order(rc.to(torch.int32).contiguous(), C)
         rc = rc.long()
         tot_s = rc.sum(1)  # rows received from each source
         cum_s = torch.cumsum(rc, 1)  # [ep, El] inclusive, per source
@@ -223,9 +240,10 @@ class ExpertParallel:
         for a, b in bounds:
             C = self.capacity(b - a, k)
             send_src, pos, sent, ndrop = self._route_chunk(topi[a:b], C)
-            if self._dropped is None:
-                self._dropped = torch.zeros((), dtype=torch.long, device=h2.device)
-            self._dropped += ndrop
+            if ndrop is not None:
+                if self._dropped is None:
+                    self._dropped = torch.zeros((), dtype=torch.long, device=h2.device)
+                self._dropped += ndrop
             if self.shape:
                 rc, w = sent, None
             else:

@@ -333,3 +333,41 @@ def test_mixtral_layer_fwd_bwd_graph_captured_matches_fp32():
     with torch.no_grad():  # new routing: the captured graph must follow the device-side offsets
         x.copy_(torch.randn(x.shape, device=DEV, generator=g).to(torch.bfloat16))
     check()
+
+
+@pytest.mark.parametrize("E,ep,n,k,cf", [(8, 8, 2048, 2, 1.25), (8, 4, 1000, 2, 1.0), (8, 2, 777, 2, 0.6),
+                                         (16, 8, 4096, 2, 2.0), (64, 8, 333, 4, 1.0), (8, 1, 64, 1, 1.0)])
+def test_native_ep_route_matches_torch(E, ep, n, k, cf, monkeypatch):
+    """csrc/moe.hip ep_route / ep_expert_order == parallel/expert.py's torch forms, bit for bit:
+    send rows, slot positions, sent counts, dropped slots (capacity factors that drop), and the
+    receiver's expert-major order and offsets."""
+    from distributed_llm_alignment_amd.parallel import expert as epm
+
+    g = torch.Generator(device=DEV).manual_seed(E * 131 + ep + n)
+    # skewed routing so some destinations overflow their capacity
+    w = torch.rand(E, device=DEV, generator=g) ** 3 + 0.05
+    topi = torch.multinomial(w.expand(n, E), k, replacement=False, generator=g).to(torch.int32)
+    xp = epm.ExpertParallel(None, E, capacity_factor=cf, shape_ep=ep) if ep > 1 else None
+    if xp is None:  # ep == 1: shape mode needs ep > 1; build the object by hand
+        xp = epm.ExpertParallel.__new__(epm.ExpertParallel)
+        xp.shape, xp.group, xp.ep, xp.rank, xp.E, xp.El = True, None, 1, 0, E, E
+        xp.capacity_factor, xp.chunks, xp._dropped = cf, 1, None
+    C = xp.capacity(n, k)
+    got = xp._route_chunk(topi, C)
+    nd_native = int(xp._dropped.item())
+    monkeypatch.setattr(epm, "_NATIVE_ROUTE", False)
+    want = xp._route_chunk(topi, C)
+    assert torch.equal(got[0], want[0])
+    assert torch.equal(got[1].long(), want[1].long())
+    assert torch.equal(got[2].long(), want[2].long())
+    assert nd_native == int(want[3].item())
+    # receiver order for a few received-count patterns (the shape mode's rc = sent)
+    for rc in (want[2].to(torch.int32), torch.randint(0, C // max(1, E // ep) + 1, (ep, E // ep), device=DEV,
+                                                       generator=g).to(torch.int32)):
+        rc = torch.minimum(rc, torch.full_like(rc, C // (E // ep)))
+        ref = xp._expert_order(rc, C)
+        monkeypatch.setattr(epm, "_NATIVE_ROUTE", True)
+        nat = xp._expert_order(rc, C)
+        monkeypatch.setattr(epm, "_NATIVE_ROUTE", False)
+        for a, b in zip(nat, ref):
+            assert torch.equal(a.long(), b.long())
