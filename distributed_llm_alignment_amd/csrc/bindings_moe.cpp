@@ -14,14 +14,14 @@ void launch_moe_topk_fwd(const bf16_t*, int64_t, int, int, float*, int*, hipStre
 void launch_moe_topk_bwd(const float*, const int*, const float*, int64_t, int, int, bf16_t*,
                          hipStream_t);
 void launch_moe_dispatch(const bf16_t*, const int*, int64_t, int, int, bf16_t*, hipStream_t);
-void launch_moe_combine(const bf16_t*, const int*, const float*, int64_t, int, int, bf16_t*,
+void launch_moe_combine(const bf16_t*, const int*, const float*, int64_t, int, int, int64_t, bf16_t*,
                         hipStream_t);
 void launch_zero_rows_from(bf16_t*, int64_t, int, int64_t, const int*, hipStream_t);
 void launch_ep_route(const void*, bool, int, int, int, int, int, int, int64_t*, int*, int*, int64_t*,
                      hipStream_t);
 void launch_ep_expert_order(const int*, int, int, int, int64_t*, int64_t*, int*, hipStream_t);
 void launch_moe_combine_bwd(const bf16_t*, const bf16_t*, const int*, const float*, int64_t, int,
-                            int, bf16_t*, float*, hipStream_t);
+                            int, int64_t, bf16_t*, float*, hipStream_t);
 
 void launch_quant_fp8_rows(const bf16_t*, int64_t, int64_t, int, uint8_t*, float*, hipStream_t);
 void launch_embed_fwd(const bf16_t*, int64_t, const int64_t*, int64_t, int, int64_t, bf16_t*, int*, hipStream_t);
@@ -333,9 +333,9 @@ static void check_pos(const at::Tensor& pos, int64_t N, int64_t k) {
 }
 
 // The kernels trust pos[] to index rows of ys / xs: a permutation of [0, N*k) on the exact path
-// (ops/moe.py builds it from an argsort), or slots of a capacity-padded buffer with dropped slots
-// all pointing at one appended zero row (parallel/expert.py, rows >= N*k there); the caller's
-// construction is the bound, row counts are checked against the allocations here.
+// (ops/moe.py builds it from an argsort), or slots of a capacity-padded buffer (parallel/expert.py)
+// whose dropped slots point one past its last row -- the combine kernels read pos >= rows as a
+// zero row (no gradient, zero weight gradient); the caller's construction is the bound.
 std::tuple<at::Tensor, at::Tensor> moe_topk_fwd(const at::Tensor& logits, int64_t k) {
   check_bf16(logits, "logits");
   TORCH_CHECK(logits.dim() == 2 && logits.is_contiguous(), "logits [N, E] contiguous");
@@ -394,7 +394,7 @@ at::Tensor moe_combine(const at::Tensor& ys, const at::Tensor& pos,
   check_aligned16(ys, "ys");
   c10::hip::HIPGuardMasqueradingAsCUDA g(ys.device());
   auto out = at::empty({N, H}, ys.options());
-  launch_moe_combine(cbp(ys), pos.data_ptr<int>(), wp, N, (int)H, (int)k, bp(out), cur_stream(ys));
+  launch_moe_combine(cbp(ys), pos.data_ptr<int>(), wp, N, (int)H, (int)k, ys.size(0), bp(out), cur_stream(ys));
   return out;
 }
 
@@ -468,7 +468,7 @@ std::tuple<at::Tensor, at::Tensor> moe_combine_bwd(const at::Tensor& dout, const
   auto dys = ys.size(0) == N * k ? at::empty_like(ys) : at::zeros_like(ys);
   auto dw = at::empty({N, k}, w.options());
   launch_moe_combine_bwd(cbp(dout), cbp(ys), pos.data_ptr<int>(), w.data_ptr<float>(), N, (int)H,
-                         (int)k, bp(dys), dw.data_ptr<float>(), cur_stream(ys));
+                         (int)k, ys.size(0), bp(dys), dw.data_ptr<float>(), cur_stream(ys));
   return {dys, dw};
 }
 

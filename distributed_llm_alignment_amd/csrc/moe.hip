@@ -100,8 +100,9 @@ template <bool HAS_W>
 __global__ __launch_bounds__(256) void moe_combine_kernel(const bf16_t* __restrict__ ys,
                                                            const int* __restrict__ pos,
                                                            const float* __restrict__ w,
-                                                           int64_t N, int H, int k,
+                                                           int64_t N, int H, int k, int64_t R,
                                                            bf16_t* __restrict__ out) {
+  // rows p >= R read as zero (dropped slots of a capacity buffer: no appended zero row needed)
   const int64_t t = blockIdx.x;
   int p[kMaxK];
   float wt[kMaxK];
@@ -112,6 +113,7 @@ __global__ __launch_bounds__(256) void moe_combine_kernel(const bf16_t* __restri
   for (int i = threadIdx.x; i < H / 8; i += 256) {
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int j = 0; j < k; ++j) {
+      if (p[j] >= R) continue;
       const bf16x8 a = load_bf16x8(ys + (int64_t)p[j] * H + i * 8);
 #pragma unroll
       for (int q = 0; q < 8; ++q) acc[q] += wt[j] * bf2f(a[q]);
@@ -124,7 +126,7 @@ __global__ __launch_bounds__(256) void moe_combine_bwd_kernel(const bf16_t* __re
                                                                const bf16_t* __restrict__ ys,
                                                                const int* __restrict__ pos,
                                                                const float* __restrict__ w,
-                                                               int64_t N, int H, int k,
+                                                               int64_t N, int H, int k, int64_t R,
                                                                bf16_t* __restrict__ dys,
                                                                float* __restrict__ dw) {
   __shared__ float red[4];
@@ -132,6 +134,10 @@ __global__ __launch_bounds__(256) void moe_combine_bwd_kernel(const bf16_t* __re
   for (int j = 0; j < k; ++j) {
     const int64_t p = pos[t * k + j];
     const float wt = w[t * k + j];
+    if (p >= R) {  // a dropped slot (block-uniform): no row, zero weight gradient
+      if (threadIdx.x == 0) dw[t * k + j] = 0.f;
+      continue;
+    }
     float dot = 0.f;
     for (int i = threadIdx.x; i < H / 8; i += 256) {
       const bf16x8 g = load_bf16x8(dout + t * H + i * 8);
@@ -441,15 +447,15 @@ void launch_zero_rows_from(bf16_t* x, int64_t R, int C, int64_t ld, const int* f
 }
 
 void launch_moe_combine(const bf16_t* ys, const int* pos, const float* w, int64_t N, int H, int k,
-                        bf16_t* out, hipStream_t st) {
+                        int64_t R, bf16_t* out, hipStream_t st) {
   if (N == 0) return;
-  if (w) moe_combine_kernel<true><<<N, 256, 0, st>>>(ys, pos, w, N, H, k, out);
-  else moe_combine_kernel<false><<<N, 256, 0, st>>>(ys, pos, w, N, H, k, out);
+  if (w) moe_combine_kernel<true><<<N, 256, 0, st>>>(ys, pos, w, N, H, k, R, out);
+  else moe_combine_kernel<false><<<N, 256, 0, st>>>(ys, pos, w, N, H, k, R, out);
 }
 void launch_moe_combine_bwd(const bf16_t* dout, const bf16_t* ys, const int* pos, const float* w,
-                            int64_t N, int H, int k, bf16_t* dys, float* dw, hipStream_t st) {
+                            int64_t N, int H, int k, int64_t R, bf16_t* dys, float* dw, hipStream_t st) {
   if (N == 0) return;
-  moe_combine_bwd_kernel<<<N, 256, 0, st>>>(dout, ys, pos, w, N, H, k, dys, dw);
+  moe_combine_bwd_kernel<<<N, 256, 0, st>>>(dout, ys, pos, w, N, H, k, R, dys, dw);
 }
 
 }  // namespace dla

@@ -263,11 +263,13 @@ class ExpertParallel:
             ye = ops.moe.experts_swiglu_offsets(xe, moe.expert_up, moe.expert_down, offs, fp8=moe.fp8)
             yr = _gather_rows(ye, inv)
             back.append((pos, _A2AStart.apply(yr, self.group, holder)))
-        # 3) combine each chunk (dropped slots read the appended zero row)
+        # 3) combine each chunk (dropped slots point one past the buffer: the native combine reads
+        # them as zero; the CPU reference gets an appended zero row)
         outs = []
         for (a, b), (pos, ys) in zip(bounds, back):
             ys = _A2AWait.apply(ys, holder)
-            ys = torch.cat([ys, ys.new_zeros(1, H)], 0)
+            if not ys.is_cuda:
+                ys = torch.cat([ys, ys.new_zeros(1, H)], 0)
             outs.append(ops.moe.combine(ys, pos.to(torch.int32), topv[a:b]))
         return outs[0] if len(outs) == 1 else torch.cat(outs, 0)
 

@@ -66,7 +66,8 @@ def test_combine_capacity_layout_kernels():
     g = torch.Generator(device=DEV).manual_seed(4)
     N, k, H, R = 300, 2, 512, 1000
     pos = torch.randperm(R - 1, device=DEV, generator=g)[:N * k].view(N, k).to(torch.int32)
-    pos[::7, 1] = R - 1  # dropped slots
+    pos[::7, 1] = R - 1  # dropped slots on an explicit zero row
+    pos[3::11, 0] = R  # and one past the buffer (read as zero by the kernels)
     ys = torch.randn(R, H, device=DEV, generator=g).to(torch.bfloat16)
     ys[-1] = 0
     ys.requires_grad_(True)
@@ -74,7 +75,7 @@ def test_combine_capacity_layout_kernels():
     out = ops.moe.combine(ys, pos, w)
     ysf = ys.detach().float().requires_grad_(True)
     wf = w.detach().clone().requires_grad_(True)
-    ref = ops.moe._ref_combine(ysf, pos, wf)
+    ref = ops.moe._ref_combine(torch.cat([ysf, ysf.new_zeros(1, H)]), pos, wf)
     assert torch.allclose(out.float(), ref, atol=2e-2, rtol=1e-2)
     go = torch.randn(N, H, device=DEV, generator=g).to(torch.bfloat16)
     dys, dw = torch.autograd.grad(out, [ys, w], go)
