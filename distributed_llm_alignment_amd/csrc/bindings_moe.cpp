@@ -20,6 +20,8 @@ void launch_zero_rows_from(bf16_t*, int64_t, int, int64_t, const int*, hipStream
 void launch_ep_route(const void*, bool, int, int, int, int, int, int, int64_t*, int*, int*, int64_t*,
                      hipStream_t);
 void launch_ep_expert_order(const int*, int, int, int, int64_t*, int64_t*, int*, hipStream_t);
+void launch_gather_rows(const bf16_t*, int64_t, const int64_t*, int64_t, int, bf16_t*, hipStream_t);
+void launch_scatter_rows(const bf16_t*, const int64_t*, int64_t, int, bf16_t*, hipStream_t);
 void launch_moe_combine_bwd(const bf16_t*, const bf16_t*, const int*, const float*, int64_t, int,
                             int, int64_t, bf16_t*, float*, hipStream_t);
 
@@ -437,6 +439,36 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> ep_expert_order(const at::Tensor&
   return {xe_src, inv, offs};
 }
 
+// out[i] = idx[i] >= 0 ? x[idx[i]] : 0 (idx int64 [n], x [R, H] bf16 with unit column stride);
+// the caller guarantees idx < R
+at::Tensor gather_rows(const at::Tensor& x, const at::Tensor& idx) {
+  check_bf16(x, "x");
+  check_cuda(idx, "idx");
+  TORCH_CHECK(idx.scalar_type() == at::kLong && idx.dim() == 1 && idx.is_contiguous(), "idx int64 [n]");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0 && x.size(1) % 8 == 0,
+              "x [R, H], H % 8 == 0, 16-byte aligned rows");
+  check_aligned16(x, "x");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  auto out = at::empty({idx.size(0), x.size(1)}, x.options());
+  launch_gather_rows(cbp(x), x.stride(0), idx.data_ptr<int64_t>(), idx.size(0), (int)x.size(1), bp(out),
+                     cur_stream(x));
+  return out;
+}
+
+// dx[idx[i]] = g[i] for idx[i] >= 0 (idx injective on those), other rows of dx zero; dx [R, H]
+at::Tensor scatter_rows(const at::Tensor& gr, const at::Tensor& idx, int64_t R) {
+  check_bf16(gr, "g");
+  check_cuda(idx, "idx");
+  TORCH_CHECK(idx.scalar_type() == at::kLong && idx.dim() == 1 && idx.is_contiguous(), "idx int64 [n]");
+  TORCH_CHECK(gr.dim() == 2 && gr.is_contiguous() && gr.size(0) == idx.size(0) && gr.size(1) % 8 == 0,
+              "g [n, H] contiguous, H % 8 == 0");
+  check_aligned16(gr, "g");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(gr.device());
+  auto dx = at::zeros({R, gr.size(1)}, gr.options());
+  launch_scatter_rows(cbp(gr), idx.data_ptr<int64_t>(), idx.size(0), (int)gr.size(1), bp(dx), cur_stream(gr));
+  return dx;
+}
+
 // x[r] = 0 for r >= from[0] (device scalar: e.g. offs[-1] of a capacity buffer); no host sync
 void zero_rows_from(at::Tensor& x, const at::Tensor& from) {
   check_bf16(x, "x");
@@ -488,6 +520,8 @@ TORCH_LIBRARY_FRAGMENT(dla, m) {
   m.def("zero_rows_from(Tensor(a!) x, Tensor from) -> ()");
   m.def("ep_route(Tensor topi, int E, int ep, int C, Tensor(a!) dropped) -> (Tensor, Tensor, Tensor)");
   m.def("ep_expert_order(Tensor rc, int C) -> (Tensor, Tensor, Tensor)");
+  m.def("gather_rows(Tensor x, Tensor idx) -> Tensor");
+  m.def("scatter_rows(Tensor g, Tensor idx, int R) -> Tensor");
   m.def("gg_fwd(Tensor x, Tensor w, Tensor offs, Tensor? sx, Tensor? sw) -> Tensor");
   m.def("gg_fwd_swiglu(Tensor x, Tensor w_up, Tensor offs, Tensor? sx, Tensor? sw) -> (Tensor, Tensor)");
   m.def("gg_dgrad(Tensor dy, Tensor w, Tensor offs) -> Tensor");
@@ -509,6 +543,8 @@ TORCH_LIBRARY_IMPL(dla, CUDA, m) {
   m.impl("zero_rows_from", &dla::zero_rows_from);
   m.impl("ep_route", &dla::ep_route);
   m.impl("ep_expert_order", &dla::ep_expert_order);
+  m.impl("gather_rows", &dla::gather_rows);
+  m.impl("scatter_rows", &dla::scatter_rows);
   m.impl("gg_fwd", &dla::gg_fwd);
   m.impl("gg_fwd_swiglu", &dla::gg_fwd_swiglu);
   m.impl("gg_dgrad", &dla::gg_dgrad);

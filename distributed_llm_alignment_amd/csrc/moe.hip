@@ -427,6 +427,40 @@ void launch_ep_expert_order(const int* rc, int ep, int El, int C, int64_t* xe_sr
   ep_expert_order_kernel<<<1, kRouteThreads, 0, st>>>(rc, ep, El, C, xe_src, inv, offs);
 }
 
+// Row gather with holes (parallel/expert.py `_gather_rows`): out[i] = idx[i] >= 0 ? x[idx[i]] : 0,
+// and its adjoint for an idx injective on its valid entries: dx[idx[i]] = g[i] (dx pre-zeroed).
+// One launch each instead of clamp + index_select + where (+ index_add in the backward).
+__global__ __launch_bounds__(256) void gather_rows_kernel(const bf16_t* __restrict__ x, int64_t ldx,
+                                                          const int64_t* __restrict__ idx, int H,
+                                                          bf16_t* __restrict__ out) {
+  const int64_t r = blockIdx.x;
+  const int64_t i = idx[r];
+  for (int c = threadIdx.x; c < H / 8; c += 256) {
+    const bf16x8 v = i >= 0 ? load_bf16x8(x + i * ldx + c * 8) : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    store_bf16x8(out + r * H + c * 8, v);
+  }
+}
+
+__global__ __launch_bounds__(256) void scatter_rows_kernel(const bf16_t* __restrict__ g,
+                                                           const int64_t* __restrict__ idx, int H,
+                                                           bf16_t* __restrict__ dx) {
+  const int64_t r = blockIdx.x;
+  const int64_t i = idx[r];
+  if (i < 0) return;
+  for (int c = threadIdx.x; c < H / 8; c += 256) store_bf16x8(dx + i * H + c * 8, load_bf16x8(g + r * H + c * 8));
+}
+
+void launch_gather_rows(const bf16_t* x, int64_t ldx, const int64_t* idx, int64_t n, int H, bf16_t* out,
+                        hipStream_t st) {
+  if (n == 0) return;
+  gather_rows_kernel<<<n, 256, 0, st>>>(x, ldx, idx, H, out);
+}
+
+void launch_scatter_rows(const bf16_t* g, const int64_t* idx, int64_t n, int H, bf16_t* dx, hipStream_t st) {
+  if (n == 0) return;
+  scatter_rows_kernel<<<n, 256, 0, st>>>(g, idx, H, dx);
+}
+
 // zero rows [*from, R) of a [R, C] bf16 tensor (C % 8 == 0), the row bound read on the device:
 // the unwritten padding rows of a capacity buffer before a GEMM reduces over them
 __global__ __launch_bounds__(256) void zero_rows_from_kernel(bf16_t* __restrict__ x, int64_t R, int C,

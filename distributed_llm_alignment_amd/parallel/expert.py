@@ -121,9 +121,26 @@ def _native_route(topi: torch.Tensor, E: int, ep: int, slots: int) -> bool:
     return _NATIVE_ROUTE and topi.is_cuda and E <= 64 and slots <= 16384 and topi.dtype in (torch.int32, torch.int64)
 
 
+class _GatherRowsFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, idx):
+        ctx.save_for_backward(idx)
+        ctx.R = x.shape[0]
+        return ops._ext.require().gather_rows(x, idx)
+
+    @staticmethod
+    def backward(ctx, g):
+        (idx,) = ctx.saved_tensors
+        return ops._ext.require().scatter_rows(g.contiguous(), idx, ctx.R), None
+
+
 def _gather_rows(x: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
     """out[i] = x[idx[i]] (idx < 0 -> zero row). Static shapes, no host sync; the backward is the
-    matching scatter (idx is injective on its valid entries)."""
+    matching scatter (idx is injective on its valid entries). On the GPU one HIP launch each way
+    (csrc/moe.hip gather_rows / scatter_rows)."""
+    if (_NATIVE_ROUTE and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 2 and x.shape[1] % 8 == 0
+            and x.stride(1) == 1 and x.stride(0) % 8 == 0 and idx.dtype == torch.int64):
+        return _GatherRowsFn.apply(x, idx.contiguous())
     valid = (idx >= 0).unsqueeze(-1)
     return torch.where(valid, x.index_select(0, idx.clamp(min=0)), torch.zeros((), dtype=x.dtype, device=x.device))
 

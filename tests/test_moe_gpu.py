@@ -372,3 +372,26 @@ def test_native_ep_route_matches_torch(E, ep, n, k, cf, monkeypatch):
         monkeypatch.setattr(epm, "_NATIVE_ROUTE", False)
         for a, b in zip(nat, ref):
             assert torch.equal(a.long(), b.long())
+
+
+def test_native_gather_rows_fwd_bwd(monkeypatch):
+    """parallel/expert.py _gather_rows on the HIP kernels (gather with holes, adjoint scatter)
+    equals its torch form forward and backward, bitwise."""
+    from distributed_llm_alignment_amd.parallel import expert as epm
+
+    g = torch.Generator(device=DEV).manual_seed(9)
+    R, n, H = 300, 500, 264
+    x = torch.randn(R, H, device=DEV, generator=g).to(torch.bfloat16)
+    idx = torch.full((n,), -1, dtype=torch.long, device=DEV)
+    sel = torch.randperm(n, device=DEV, generator=g)[:R - 20]
+    idx[sel] = torch.randperm(R, device=DEV, generator=g)[:R - 20]  # injective, some rows unread
+    go = torch.randn(n, H, device=DEV, generator=g).to(torch.bfloat16)
+    res = []
+    for native in (True, False):
+        monkeypatch.setattr(epm, "_NATIVE_ROUTE", native)
+        xx = x.clone().requires_grad_(True)
+        y = epm._gather_rows(xx, idx)
+        (dx,) = torch.autograd.grad(y, [xx], go)
+        res.append((y, dx))
+    assert torch.equal(res[0][0], res[1][0])
+    assert torch.equal(res[0][1], res[1][1])
