@@ -92,9 +92,12 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False,
     out_so = SAN_SO if san else OUT_SO
     obj_dir.mkdir(parents=True, exist_ok=True)
     hsan = [f"-Xarch_host -fsanitize={x}".split() for x in san]
-    # vptr checks need the clang UBSan C++ runtime, which the g++-built bindings do not link
+    # vptr checks need the clang UBSan C++ runtime, which the g++-built bindings do not link; so
+    # does clang's indirect-call type check (-fsanitize=function: __ubsan_handle_function_type_mismatch
+    # is missing from g++'s libubsan, which is what the loader preloads)
     extra = ["-fno-omit-frame-pointer"] + (["-fno-sanitize=vptr"] if "undefined" in san else [])
-    hsan = [a for pair in hsan for a in pair] + [a for x in extra for a in ("-Xarch_host", x)] if san else []
+    hextra = ["-fno-sanitize=function"] if "undefined" in san else []
+    hsan = [a for pair in hsan for a in pair] + [a for x in extra + hextra for a in ("-Xarch_host", x)] if san else []
     gsan = [f"-fsanitize={x}" for x in san] + extra if san else []
     hips, bindings = _sources()
     headers = _headers()
