@@ -123,24 +123,31 @@ def _native_route(topi: torch.Tensor, E: int, ep: int, slots: int) -> bool:
 
 class _GatherRowsFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, idx):
+    def forward(ctx, x, idx, injective):
         ctx.save_for_backward(idx)
-        ctx.R = x.shape[0]
+        ctx.R, ctx.injective = x.shape[0], injective
         return ops._ext.require().gather_rows(x, idx)
 
     @staticmethod
     def backward(ctx, g):
         (idx,) = ctx.saved_tensors
-        return ops._ext.require().scatter_rows(g.contiguous(), idx, ctx.R), None
+        if ctx.injective:  # one HIP scatter, no accumulation needed
+            return ops._ext.require().scatter_rows(g.contiguous(), idx, ctx.R), None, None
+        # a row read by several slots (a token's k choices): accumulate
+        valid = (idx >= 0).unsqueeze(-1)
+        dx = torch.zeros((ctx.R, g.shape[1]), dtype=g.dtype, device=g.device)
+        dx.index_add_(0, idx.clamp(min=0), torch.where(valid, g, torch.zeros((), dtype=g.dtype, device=g.device)))
+        return dx, None, None
 
 
-def _gather_rows(x: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
+def _gather_rows(x: torch.Tensor, idx: torch.Tensor, injective: bool = True) -> torch.Tensor:
     """out[i] = x[idx[i]] (idx < 0 -> zero row). Static shapes, no host sync; the backward is the
-    matching scatter (idx is injective on its valid entries). On the GPU one HIP launch each way
+    matching scatter, or (`injective` False: a row read by several entries, e.g. a token's k
+    slots) a scatter-add. On the GPU the forward (and the injective backward) is one HIP launch
     (csrc/moe.hip gather_rows / scatter_rows)."""
     if (_NATIVE_ROUTE and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 2 and x.shape[1] % 8 == 0
             and x.stride(1) == 1 and x.stride(0) % 8 == 0 and idx.dtype == torch.int64):
-        return _GatherRowsFn.apply(x, idx.contiguous())
+        return _GatherRowsFn.apply(x, idx.contiguous(), injective)
     valid = (idx >= 0).unsqueeze(-1)
     return torch.where(valid, x.index_select(0, idx.clamp(min=0)), torch.zeros((), dtype=x.dtype, device=x.device))
 
@@ -266,7 +273,7 @@ class ExpertParallel:
             else:
                 rc = torch.empty_like(sent)
                 w = dist.all_to_all_single(rc, sent.contiguous(), group=self.group, async_op=True)
-            xs = _gather_rows(h2[a:b], send_src)
+            xs = _gather_rows(h2[a:b], send_src, injective=False)  # a token fills up to k slots
             xr = _A2AStart.apply(xs, self.group, holder)
             stage.append((C, pos, w, rc, xr))
         # 2) per chunk: wait for its rows, experts on the device-built order, return all-to-all

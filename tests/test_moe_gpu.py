@@ -113,11 +113,11 @@ def test_expert_parallel_shape_mode_layer_matches_fp32(shape_ep):
     (y0, dx0, du0), (y1, dx1, du1) = outs
     # a token whose top-2 router logits nearly tie may pick another expert in bf16 than in fp32:
     # per-token rows are compared with a small allowance for such flips, the expert grads as a whole
-    for a, b in ((y0, y1), (dx0, dx1)):
-        assert torch.isfinite(b).all()
+    for name, a, b in (("y", y0, y1), ("dx", dx0, dx1)):
+        assert torch.isfinite(b).all(), name
         a2, b2 = a.reshape(-1, a.shape[-1]), b.reshape(-1, b.shape[-1])
         rel = (a2 - b2).norm(dim=-1) / a2.norm(dim=-1).clamp_min(1e-12)
-        assert (rel > 3e-2).float().mean() < 0.03, rel.sort().values[-20:]
+        assert (rel > 3e-2).float().mean() < 0.03, (name, rel.sort().values[-20:])
     assert torch.isfinite(du1).all()
     assert (du0 - du1).norm() / du0.norm() < 5e-2
 
@@ -386,12 +386,15 @@ def test_native_gather_rows_fwd_bwd(monkeypatch):
     sel = torch.randperm(n, device=DEV, generator=g)[:R - 20]
     idx[sel] = torch.randperm(R, device=DEV, generator=g)[:R - 20]  # injective, some rows unread
     go = torch.randn(n, H, device=DEV, generator=g).to(torch.bfloat16)
-    res = []
-    for native in (True, False):
-        monkeypatch.setattr(epm, "_NATIVE_ROUTE", native)
-        xx = x.clone().requires_grad_(True)
-        y = epm._gather_rows(xx, idx)
-        (dx,) = torch.autograd.grad(y, [xx], go)
-        res.append((y, dx))
-    assert torch.equal(res[0][0], res[1][0])
-    assert torch.equal(res[0][1], res[1][1])
+    dup = idx.clone()
+    dup[: n // 2] = torch.randint(0, R, (n // 2,), device=DEV, generator=g)  # rows read twice or more
+    for ix, inj in ((idx, True), (dup, False)):
+        res = []
+        for native in (True, False):
+            monkeypatch.setattr(epm, "_NATIVE_ROUTE", native)
+            xx = x.clone().requires_grad_(True)
+            y = epm._gather_rows(xx, ix, injective=inj)
+            (dx,) = torch.autograd.grad(y, [xx], go)
+            res.append((y, dx.float()))
+        assert torch.equal(res[0][0], res[1][0])
+        assert torch.allclose(res[0][1], res[1][1], atol=1e-2, rtol=1e-2)  # (bf16 sums: order)
