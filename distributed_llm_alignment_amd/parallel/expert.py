@@ -133,11 +133,11 @@ class _GatherRowsFn(torch.autograd.Function):
         (idx,) = ctx.saved_tensors
         if ctx.injective:  # one HIP scatter, no accumulation needed
             return ops._ext.require().scatter_rows(g.contiguous(), idx, ctx.R), None, None
-        # a row read by several slots (a token's k choices): accumulate
+        # a row read by several slots (a token's k choices): accumulate, in fp32
         valid = (idx >= 0).unsqueeze(-1)
-        dx = torch.zeros((ctx.R, g.shape[1]), dtype=g.dtype, device=g.device)
-        dx.index_add_(0, idx.clamp(min=0), torch.where(valid, g, torch.zeros((), dtype=g.dtype, device=g.device)))
-        return dx, None, None
+        dx = torch.zeros((ctx.R, g.shape[1]), dtype=torch.float32, device=g.device)
+        dx.index_add_(0, idx.clamp(min=0), torch.where(valid, g.float(), torch.zeros((), device=g.device)))
+        return dx.to(g.dtype), None, None
 
 
 def _gather_rows(x: torch.Tensor, idx: torch.Tensor, injective: bool = True) -> torch.Tensor:

@@ -397,4 +397,8 @@ def test_native_gather_rows_fwd_bwd(monkeypatch):
             (dx,) = torch.autograd.grad(y, [xx], go)
             res.append((y, dx.float()))
         assert torch.equal(res[0][0], res[1][0])
-        assert torch.allclose(res[0][1], res[1][1], atol=1e-2, rtol=1e-2)  # (bf16 sums: order)
+        # the adjoint against an fp32 scatter-add (the torch form sums in bf16)
+        ref = torch.zeros(R, H, device=DEV).index_add_(0, ix.clamp(min=0), go.float() * (ix >= 0).unsqueeze(-1))
+        if inj:
+            assert torch.equal(res[0][1], res[1][1])
+        assert (res[0][1] - ref).abs().max() <= 1e-2 * ref.abs().max()
