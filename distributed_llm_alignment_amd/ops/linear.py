@@ -54,11 +54,14 @@ def input_grad(dy2: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
 # down 0.95 -> 0.68 + 0.14 ms; no gain for qkv / o (one-off layout probe, MI355X).
 TN_WGRAD = os.environ.get("DLA_TN_WGRAD", "1") != "0"
 TN_WGRAD_MIN_ELEMS = int(os.environ.get("DLA_TN_WGRAD_MIN", "0"))
+# upper bound (A/B knob): the LM head's dY is the [tokens, vocab] logit gradient, whose transpose
+# alone moves 2 x 2.1 GB per micro-batch at Llama-3 vocab
+TN_WGRAD_MAX_ELEMS = int(os.environ.get("DLA_TN_WGRAD_MAX", str(1 << 62)))
 
 
 def _tn_ok(mg: torch.Tensor, M: int) -> bool:
     N, K = mg.shape
-    return (TN_WGRAD and N * K >= TN_WGRAD_MIN_ELEMS and mg.dtype in (torch.bfloat16, torch.float32)
+    return (TN_WGRAD and TN_WGRAD_MIN_ELEMS <= N * K <= TN_WGRAD_MAX_ELEMS and mg.dtype in (torch.bfloat16, torch.float32)
             and _ext.use_native(mg) and M % 8 == 0 and N % 8 == 0 and K % 8 == 0)
 
 
