@@ -441,7 +441,7 @@ __device__ __forceinline__ void dec_loop_body(
   static_assert(G * D * 4 <= KPW * D * 2, "acc_s aliases one V image slot");
   static_assert(!WAITQ || ROPE, "the fused qkv form reads the raw qkv row");
   // per wave: 2 V image slots (LDS-DMA ring), the first re-used for the wave's partial O
-  static_assert(RD == 1 || RD == 2, "ring depth");
+  static_assert(RD >= 1 && RD <= 3, "ring depth");
   __shared__ __attribute__((aligned(16))) bf16_t vimg[4][RD][KPW * D];
   __shared__ float mls[4][G][2];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -625,9 +625,16 @@ __device__ __forceinline__ void dec_loop_body(
     for (int i = 0; i < 4; ++i) ai[i] = __shfl(alpha, 4 * kg + i, 64);
     // V(c) has landed once every VMEM op but the next chunk's (2 KST K loads + NIT V pieces,
     // issued after it) is done; the compiler does not see the DMA -> LDS dependence
-    if (RD == 2 && c + 1 < cend) {
-      if constexpr (2 * KST + NIT == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-      else if constexpr (2 * KST + NIT == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    // (chunks issued after c: min(RD - 1, cend - 1 - c); the refill of c + RD comes after this)
+    constexpr int PER = 2 * KST + NIT;
+    const int nlater = min(RD - 1, cend - 1 - c);
+    if (nlater >= 2) {
+      if constexpr (PER == 16) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+      else if constexpr (PER == 8) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if (nlater == 1) {
+      if constexpr (PER == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      else if constexpr (PER == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -667,8 +674,10 @@ __device__ __forceinline__ void dec_loop_body(
   };
   if (cbeg != cfirst) loadK(std::integral_constant<int, 0>{}, cbeg);  // left padding: the guess was wrong
   loadV(std::integral_constant<int, 0>{}, cbeg);
-  if constexpr (RD == 2)
-    if (cbeg + 1 < cend) load(std::integral_constant<int, RD - 1>{}, cbeg + 1);
+  if constexpr (RD >= 2)
+    if (cbeg + 1 < cend) load(std::integral_constant<int, 1>{}, cbeg + 1);
+  if constexpr (RD >= 3)
+    if (cbeg + 2 < cend) load(std::integral_constant<int, 2>{}, cbeg + 2);
   if constexpr (WAITQ) {  // every load above is independent of this step's qkv row
     wait();
     cache_write();
@@ -676,8 +685,10 @@ __device__ __forceinline__ void dec_loop_body(
   }
   for (int c = cbeg; c < cend; c += RD) {
     step(std::integral_constant<int, 0>{}, c);
-    if constexpr (RD == 2)
-      if (c + 1 < cend) step(std::integral_constant<int, RD - 1>{}, c + 1);
+    if constexpr (RD >= 2)
+      if (c + 1 < cend) step(std::integral_constant<int, 1>{}, c + 1);
+    if constexpr (RD >= 3)
+      if (c + 2 < cend) step(std::integral_constant<int, 2>{}, c + 2);
   }
   // this wave's partial O into its own (dead) first image slot
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -720,7 +731,7 @@ __device__ __forceinline__ void dec_loop_body(
   if (fuse) dec_arrive_combine<D, G>(cslot, part_o, part_ml, pbase0, nsplit, out, obase, o_sh);
 }
 
-template <int D, int G, bool ROPE>
+template <int D, int G, bool ROPE, int RD = 2>
 __global__ __launch_bounds__(256, 2) void decode_attn_loop_kernel(
     const bf16_t* __restrict__ q, int64_t q_sb, int64_t q_sh,
     bf16_t* __restrict__ kc, bf16_t* __restrict__ vc,
@@ -728,7 +739,7 @@ __global__ __launch_bounds__(256, 2) void decode_attn_loop_kernel(
     const int* __restrict__ kv_start, int window, float scale_log2, int nsplit, int cpb,
     float* __restrict__ part_o, float* __restrict__ part_ml, int Hq, DecRope rp,
     bf16_t* __restrict__ out, int64_t o_sb, int64_t o_sh, int* __restrict__ cnt, int Tcap) {
-  dec_loop_body<D, G, ROPE>(blockIdx.x, blockIdx.y, blockIdx.z, gridDim.y, q, q_sb, q_sh, kc, vc,
+  dec_loop_body<D, G, ROPE, false, RD>(blockIdx.x, blockIdx.y, blockIdx.z, gridDim.y, q, q_sb, q_sh, kc, vc,
                             c_sb, c_st, c_sh, kv_len, kv_start, window, scale_log2, nsplit, cpb, part_o,
                             part_ml, Hq, rp, out, o_sb, o_sh, cnt, Tcap, [] {});
 }
@@ -1089,8 +1100,21 @@ static void launch_decode_d(const bf16_t* q, int64_t q_sb, int64_t q_sh, bf16_t*
     // one split per sequence, or the in-kernel combine (arrival counters given): no combine launch
     int* const cn = (nsplit > 1 && nsplit <= kDecMaxFuse) ? cnt : nullptr;
     bf16_t* fin = (nsplit == 1 || cn != nullptr) ? out : nullptr;
+    // DLA_DECODE_RING=3 (A/B): all of a block's chunks in flight at once when it has >= 3 and the
+    // grid fits one block per CU (96 KB of V image per block)
+    static const int ring = [] {
+      const char* e = std::getenv("DLA_DECODE_RING");
+      return e ? std::atoi(e) : 2;
+    }();
+    const bool ring3 = ring == 3 && cpb >= 3 && (int64_t)nsplit * Hkv * B <= 256;
 #define DLA_DECL(GG)                                                                                    \
-  if (rp)                                                                                               \
+  if (rp && ring3)                                                                                      \
+    decode_attn_loop_kernel<D, GG, true, 3><<<grid, 256, 0, st>>>(q, q_sb, q_sh, kc, vc, c_sb, c_st,    \
+                                                                  c_sh, kv_len, kv_start, window,       \
+                                                                  scale_log2, nsplit, cpb, part_o,      \
+                                                                  part_ml, Hq, r0, fin, o_sb, o_sh, cn, \
+                                                                  Tmax);                                \
+  else if (rp)                                                                                          \
     decode_attn_loop_kernel<D, GG, true><<<grid, 256, 0, st>>>(q, q_sb, q_sh, kc, vc, c_sb, c_st, c_sh, \
                                                                kv_len, kv_start, window, scale_log2,    \
                                                                nsplit, cpb, part_o, part_ml, Hq, r0,    \
