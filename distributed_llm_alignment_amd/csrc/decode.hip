@@ -422,7 +422,9 @@ __device__ __forceinline__ void dec_glds16(const void* src, void* lds_base) {
 // the qkv row of the newest token (q, k, v) is produced by other workgroups of the same launch;
 // the body issues every load that does not depend on it (the first two chunks' K / V), then
 // calls wait() and only then reads q and writes the newest K / V into the cache.
-template <int D, int G, bool ROPE, bool WAITQ = false, int RD = 2, class Wait>
+// EARLYK: chunk c + RD's K loads leave right after chunk c's scores (the registers they refill are
+// free from there) instead of with its V refill after P.V
+template <int D, int G, bool ROPE, bool WAITQ = false, int RD = 2, bool EARLYK = false, class Wait>
 __device__ __forceinline__ void dec_loop_body(
     const int split, const int hk, const int b, const int Hkv_grid,
     const bf16_t* __restrict__ q, int64_t q_sb, int64_t q_sh,
@@ -590,6 +592,8 @@ __device__ __forceinline__ void dec_loop_body(
 #pragma unroll
       for (int s = 0; s < KST; ++s) sacc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[j][t][s], qf[s], sacc[t], 0, 0, 0);
     }
+    const bool kearly = EARLYK && c + RD < cend;
+    if (kearly) loadK(J, c + RD);
     float sc[2][4];
     float mc = -INFINITY;
 #pragma unroll
@@ -628,7 +632,11 @@ __device__ __forceinline__ void dec_loop_body(
     // (chunks issued after c: min(RD - 1, cend - 1 - c); the refill of c + RD comes after this)
     constexpr int PER = 2 * KST + NIT;
     const int nlater = min(RD - 1, cend - 1 - c);
-    if (nlater >= 2) {
+    if (kearly && nlater == 1) {  // K(c + 1), V(c + 1), then K(c + 2) behind V(c)
+      if constexpr (PER == 16) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+      else if constexpr (PER == 8) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if (nlater >= 2) {
       if constexpr (PER == 16) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
       else if constexpr (PER == 8) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -669,7 +677,8 @@ __device__ __forceinline__ void dec_loop_body(
     if (c + RD < cend) {
       // WAR: this slot's transposed reads are complete before the DMA refill is issued
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      load(J, c + RD);
+      if (kearly) loadV(J, c + RD);
+      else load(J, c + RD);
     }
   };
   if (cbeg != cfirst) loadK(std::integral_constant<int, 0>{}, cbeg);  // left padding: the guess was wrong
@@ -731,7 +740,7 @@ __device__ __forceinline__ void dec_loop_body(
   if (fuse) dec_arrive_combine<D, G>(cslot, part_o, part_ml, pbase0, nsplit, out, obase, o_sh);
 }
 
-template <int D, int G, bool ROPE, int RD = 2>
+template <int D, int G, bool ROPE, int RD = 2, bool EARLYK = false>
 __global__ __launch_bounds__(256, 2) void decode_attn_loop_kernel(
     const bf16_t* __restrict__ q, int64_t q_sb, int64_t q_sh,
     bf16_t* __restrict__ kc, bf16_t* __restrict__ vc,
@@ -739,7 +748,7 @@ __global__ __launch_bounds__(256, 2) void decode_attn_loop_kernel(
     const int* __restrict__ kv_start, int window, float scale_log2, int nsplit, int cpb,
     float* __restrict__ part_o, float* __restrict__ part_ml, int Hq, DecRope rp,
     bf16_t* __restrict__ out, int64_t o_sb, int64_t o_sh, int* __restrict__ cnt, int Tcap) {
-  dec_loop_body<D, G, ROPE, false, RD>(blockIdx.x, blockIdx.y, blockIdx.z, gridDim.y, q, q_sb, q_sh, kc, vc,
+  dec_loop_body<D, G, ROPE, false, RD, EARLYK>(blockIdx.x, blockIdx.y, blockIdx.z, gridDim.y, q, q_sb, q_sh, kc, vc,
                             c_sb, c_st, c_sh, kv_len, kv_start, window, scale_log2, nsplit, cpb, part_o,
                             part_ml, Hq, rp, out, o_sb, o_sh, cnt, Tcap, [] {});
 }
@@ -1107,8 +1116,18 @@ static void launch_decode_d(const bf16_t* q, int64_t q_sb, int64_t q_sh, bf16_t*
       return e ? std::atoi(e) : 2;
     }();
     const bool ring3 = ring == 3 && cpb >= 3 && (int64_t)nsplit * Hkv * B <= 256;
+    static const bool earlyk = [] {  // DLA_DECODE_EARLYK=1 (A/B)
+      const char* e = std::getenv("DLA_DECODE_EARLYK");
+      return e != nullptr && std::atoi(e) == 1;
+    }();
 #define DLA_DECL(GG)                                                                                    \
-  if (rp && ring3)                                                                                      \
+  if (rp && earlyk && !ring3)                                                                           \
+    decode_attn_loop_kernel<D, GG, true, 2, true><<<grid, 256, 0, st>>>(q, q_sb, q_sh, kc, vc, c_sb,    \
+                                                                        c_st, c_sh, kv_len, kv_start,   \
+                                                                        window, scale_log2, nsplit, cpb, \
+                                                                        part_o, part_ml, Hq, r0, fin,   \
+                                                                        o_sb, o_sh, cn, Tmax);          \
+  else if (rp && ring3)                                                                                 \
     decode_attn_loop_kernel<D, GG, true, 3><<<grid, 256, 0, st>>>(q, q_sb, q_sh, kc, vc, c_sb, c_st,    \
                                                                   c_sh, kv_len, kv_start, window,       \
                                                                   scale_log2, nsplit, cpb, part_o,      \
