@@ -376,8 +376,6 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
         for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
       }
       const float muse = m == -INFINITY ? 0.f : m;
-      // key sub-tile outer: sub-tile 0's P.V MFMAs are in flight while sub-tile 1's scores are
-      // exponentiated (VALU beside MFMA in one wave); the sums into O and lsum keep their order
 #pragma unroll
       for (int st = 0; st < 2; ++st) {
 #pragma unroll
@@ -386,12 +384,23 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
           sacc[st][i] = pv;
           lsum += pv;
         }
-        const s16x8 pf0 = pack8(sacc[st], 0), pf1 = pack8(sacc[st], 8);
+      }
+      s16x8 pf[2][2];
 #pragma unroll
-        for (int dt = 0; dt < DT; ++dt) {
-          const int c0 = 32 * dt + 16 * ((lane >> 4) & 1);
-          o[dt] = mfma32(tr_frag_perm<DP>(Vs, 32 * st + 4 * h, c0, lane), pf0, o[dt]);
-          o[dt] = mfma32(tr_frag_perm<DP>(Vs, 32 * st + 16 + 4 * h, c0, lane), pf1, o[dt]);
+      for (int st = 0; st < 2; ++st) {
+        pf[st][0] = pack8(sacc[st], 0);
+        pf[st][1] = pack8(sacc[st], 8);
+      }
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        const int c0 = 32 * dt + 16 * ((lane >> 4) & 1);
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            const s16x8 a = tr_frag_perm<DP>(Vs, 32 * st + 16 * s + 4 * h, c0, lane);
+            o[dt] = mfma32(a, pf[st][s], o[dt]);
+          }
         }
       }
     }
