@@ -203,8 +203,7 @@ class DataParallelEngine:
         if self.zero:
             self.grad_shard = torch.zeros(shard, dtype=self.grad_dtype, device=self.device)
             self.param_shard = torch.empty(shard, dtype=self.dtype, device=self.device)
-            src = torch.cat([self._chunk(self.param_buf, b) for b in self.buckets])
-            self.param_shard.copy_(src)
+            torch.cat([self._chunk(self.param_buf, b) for b in self.buckets], out=self.param_shard)
         else:
             self.grad_shard = self.grad_buf
             self.param_shard = self.param_buf
@@ -222,7 +221,7 @@ class DataParallelEngine:
                         if a < e:
                             self._repl_ranges.append((a + base, e + base))
         n_state = self.param_shard.numel()
-        self.master = self.param_shard.float().clone() if master_weights else None
+        self.master = self.param_shard.to(torch.float32, copy=True) if master_weights else None  # one allocation (.float().clone() made two)
         self.exp_avg = torch.zeros(n_state, dtype=torch.float32, device=self.device)
         self.exp_avg_sq = torch.zeros(n_state, dtype=torch.float32, device=self.device)
         self._sumsq = torch.zeros(1, dtype=torch.float32, device=self.device)
@@ -491,18 +490,18 @@ class DataParallelEngine:
                     gsrc = dist.get_global_rank(b.group, src) if b.group is not None else src
                     dist.broadcast(self.param_buf[b.start:b.end], src=gsrc, group=b.group)
             if self.zero:
-                self.param_shard.copy_(torch.cat([self._chunk(self.param_buf, b) for b in self.buckets]))
+                torch.cat([self._chunk(self.param_buf, b) for b in self.buckets], out=self.param_shard)
             if self.master is not None:
-                self.master.copy_(self.param_shard.float())
+                self.master.copy_(self.param_shard)  # (copy_ converts in place: no fp32 temporary)
 
     @torch.no_grad()
     def sync_master_from_params(self):
         self.wait_params()
         self._wt_epoch[0] += 1
         if self.zero:
-            self.param_shard.copy_(torch.cat([self._chunk(self.param_buf, b) for b in self.buckets]))
+            torch.cat([self._chunk(self.param_buf, b) for b in self.buckets], out=self.param_shard)
         if self.master is not None:
-            self.master.copy_(self.param_shard.float())
+            self.master.copy_(self.param_shard)  # (copy_ converts in place: no fp32 temporary)
 
     # ------------------------------------------------------------------------ state
     def optimizer_state(self) -> Dict[str, object]:

@@ -356,7 +356,7 @@ class FullyShardedEngine(_ShardedBase):
         # micro-batch grads are reduce-scattered per unit in the param dtype and accumulated here:
         # fp32 (grad_dtype) keeps 16-256 micro-batch accumulations exact to fp32 rounding
         self.grad_shard = torch.zeros(n, dtype=grad_dtype or self.dtype, device=self.device)
-        self.master = self.param_shard.float().clone() if master_weights else None
+        self.master = self.param_shard.to(torch.float32, copy=True) if master_weights else None  # one allocation (.float().clone() made two)
         self.exp_avg = torch.zeros(n, dtype=torch.float32, device=self.device)
         self.exp_avg_sq = torch.zeros(n, dtype=torch.float32, device=self.device)
         self._sumsq = torch.zeros(1, dtype=torch.float32, device=self.device)
@@ -509,7 +509,7 @@ class FullyShardedEngine(_ShardedBase):
             self.param_shard[u.shard_off:u.shard_off + u.chunk].copy_(self._my_chunk(u.full, u))
         self._wt_epoch[0] += 1
         if self.master is not None:
-            self.master.copy_(self.param_shard.float())
+            self.master.copy_(self.param_shard)  # (copy_ converts in place: no fp32 temporary)
 
     @torch.no_grad()
     def broadcast_params(self, src: int = 0):
@@ -522,7 +522,7 @@ class FullyShardedEngine(_ShardedBase):
     @torch.no_grad()
     def sync_master_from_params(self):
         if self.master is not None:
-            self.master.copy_(self.param_shard.float())
+            self.master.copy_(self.param_shard)  # (copy_ converts in place: no fp32 temporary)
 
     def optimizer_state(self) -> Dict[str, object]:
         return {"step": self.step_count, "lr": self.lr, "betas": self.betas, "eps": self.eps,
