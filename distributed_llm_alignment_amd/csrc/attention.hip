@@ -27,7 +27,6 @@
 //     of 16 x 8 B (the per-lane row stores are issue-bound): 141 -> 121 us causal T = 1024,
 //     190 -> 170 us non-causal (tools/attn_bench.py --ab, one box).
 // Backward: see attn_bwd_kernel.
-#include <algorithm>
 #include <cstdlib>
 #include <stdexcept>
 #include "common.h"
@@ -438,280 +437,6 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
       p.lse2[(static_cast<int64_t>(b) * p.Hq + hq) * p.Tq + qi] =
           lsum > 0.f ? m + __log2f(lsum) : INFINITY;
     }
-  }
-}
-
-// ----------------------------------------------------------------------------------------------
-// Persistent forward (DLA_ATTN_FWD_PERSIST=1; D = 128, no packing / window / fused RoPE): one
-// workgroup per CU walks its (q block, head block, batch) list in snake LPT order, and the K/V
-// tile pipeline runs on across block boundaries (the next block's first tiles are staged during
-// the current block's last ones) while the next block's Q arrives by LDS-DMA into a per-wave slot
-// (source-swizzled: position c of row r holds chunk c ^ (r & 15)). A block boundary then no
-// longer exposes the Q / first-tile load latency that a fresh workgroup pays (at one 8-wave
-// workgroup per CU nothing else hides it). Per-tile math, masks and outputs are exactly
-// attn_fwd_kernel's.
-template <int D, bool CAUSAL, int NW, int HP>
-__global__ __launch_bounds__(64 * NW) void attn_fwd_pkernel(AttnParams p, int nblocks) {
-  constexpr int NT = 64 * NW, BQ = 32 * NW / HP, BK = kFwdKeys;
-  constexpr int WPH = NW / HP;
-  constexpr int DP = D, NCH = DP / 8, KS = D / 16, DT = DP / 32;
-  constexpr int CPT = (BK * NCH) / NT;
-  static_assert(D == 128 && (BK * NCH) % NT == 0, "persistent forward: D = 128");
-  __shared__ __attribute__((aligned(16))) bf16_t Kb[2][BK * DP];
-  __shared__ __attribute__((aligned(16))) bf16_t Vb[2][BK * DP];
-  __shared__ __attribute__((aligned(16))) bf16_t Qs[NW][32 * D];
-
-  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int l32 = lane & 31, h = lane >> 5;
-  const int nqb = (p.Tq + BQ - 1) / BQ;
-  const int nhb = p.Hq / HP;
-  const int nbh = nhb * p.B;
-  const int G = gridDim.x, g = blockIdx.x;
-
-  struct Blk {
-    int qb, hq, b, hk, q0, kbeg, kend, tile0, ntiles;
-  };
-  auto blk_at = [&](int j, Blk& bk) -> bool {  // the j-th block of this workgroup, snake order
-    const int idx = (j & 1) ? j * G + (G - 1 - g) : j * G + g;
-    if (idx >= nblocks) return false;
-    bk.qb = CAUSAL ? nqb - 1 - idx / nbh : idx / nbh;
-    const int rest = idx % nbh;
-    bk.hq = (rest % nhb) * HP + w / WPH;
-    bk.b = rest / nhb;
-    bk.hk = bk.hq / (p.Hq / p.Hkv);
-    bk.q0 = bk.qb * BQ + (w % WPH) * 32;
-    bk.kbeg = p.kv_start ? p.kv_start[bk.b] : 0;
-    bk.kend = p.kv_end ? p.kv_end[bk.b] : p.Tk;
-    int kmax = bk.kend;
-    if (CAUSAL) kmax = min(kmax, min(p.Tq, bk.qb * BQ + BQ) - 1 + p.causal_off + 1);
-    bk.tile0 = (max(bk.kbeg, 0) / BK) * BK;
-    bk.ntiles = kmax > bk.tile0 ? (kmax - bk.tile0 + BK - 1) / BK : 0;
-    return true;
-  };
-  // staging cursor over the workgroup's tile sequence (blocks without tiles are skipped)
-  struct Cur {
-    int j, t;
-    bool valid;
-    Blk bk;
-  };
-  auto cur_seek = [&](Cur& c) {
-    c.valid = false;
-    while (blk_at(c.j, c.bk)) {
-      if (c.bk.ntiles > 0) {
-        c.valid = true;
-        return;
-      }
-      ++c.j;
-    }
-  };
-  auto cur_next = [&](Cur& c) {
-    if (!c.valid) return;
-    if (++c.t < c.bk.ntiles) return;
-    ++c.j;
-    c.t = 0;
-    cur_seek(c);
-  };
-  bf16x8 kreg[CPT], vreg[CPT];
-  auto gload = [&](const Cur& c) {
-    const bf16_t* kp = p.k + c.bk.b * p.k_sb + static_cast<int64_t>(c.bk.hk) * p.k_sh;
-    const bf16_t* vp = p.v + c.bk.b * p.v_sb + static_cast<int64_t>(c.bk.hk) * p.v_sh;
-    const int kt = c.bk.tile0 + c.t * BK;
-#pragma unroll
-    for (int cc = 0; cc < CPT; ++cc) {
-      const int ci = tid + NT * cc;
-      const int row = ci / NCH, ch = ci % NCH;
-      const int key = kt + row;
-      if (key < p.Tk) {
-        kreg[cc] = load_bf16x8(kp + key * p.k_st + ch * 8);
-        vreg[cc] = load_bf16x8(vp + key * p.v_st + ch * 8);
-      } else {
-        kreg[cc] = bf16x8{};
-        vreg[cc] = bf16x8{};
-      }
-    }
-  };
-  auto lwrite = [&](int buf) {
-#pragma unroll
-    for (int cc = 0; cc < CPT; ++cc) {
-      const int ci = tid + NT * cc;
-      const int row = ci / NCH, ch = ci % NCH;
-      store_bf16x8(&Kb[buf][swz<DP>(row, ch)], kreg[cc]);
-      store_bf16x8(&Vb[buf][swz<DP>(row, ch)], vreg[cc]);
-    }
-  };
-  // this wave's 32 query rows of block bk -> Qs[w] (8 x 1 KB LDS-DMA pieces; rows past Tq read
-  // row Tq - 1: never stored)
-  auto qdma = [&](const Blk& bk) {
-    const bf16_t* qp = p.q + bk.b * p.q_sb + static_cast<int64_t>(bk.hq) * p.q_sh;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int pos = i * 64 + lane, r = pos >> 4, c = (pos & 15) ^ (r & 15);
-      const int qrow = min(bk.q0 + r, p.Tq - 1);
-      __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void*)(qp + static_cast<int64_t>(qrow) * p.q_st + c * 8),
-          (__attribute__((address_space(3))) void*)(&Qs[w][i * 512]), 16, 0, 0);
-    }
-  };
-
-  Blk cur;
-  if (!blk_at(0, cur)) return;
-  qdma(cur);
-  Cur sc{0, 0, false, Blk{}};
-  cur_seek(sc);
-  bool pending = false;  // kreg / vreg hold a tile not yet written to LDS
-  if (sc.valid) {
-    gload(sc);
-    lwrite(0);
-    cur_next(sc);
-    if (sc.valid) {
-      gload(sc);
-      pending = true;
-      cur_next(sc);
-    }
-  }
-  __syncthreads();
-  int gt = 0;  // tiles consumed so far (LDS buffer parity)
-  for (int j = 0;; ++j) {
-    if (j > 0 && !blk_at(j, cur)) break;
-    Blk nxt;
-    const bool have_next = blk_at(j + 1, nxt);
-    // Q of this block: this wave's own DMA (vmcnt), then rows from the swizzled slot
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int qi = cur.q0 + l32;
-    s16x8 qf[KS];
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      const int pos = (2 * s + h) ^ (l32 & 15);
-      const bf16x8 raw = *reinterpret_cast<const bf16x8*>(&Qs[w][l32 * D + pos * 8]);
-      float t8[8];
-#pragma unroll
-      for (int jj = 0; jj < 8; ++jj) t8[jj] = qi < p.Tq ? bf2f(raw[jj]) * p.scale2 : 0.f;
-      qf[s] = __builtin_bit_cast(s16x8, pack_bf16x8(t8));
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (WAR: the slot is refilled next)
-    if (have_next) qdma(nxt);
-
-    f32x16 o[DT];
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) o[dt] = f32x16{};
-    float m = -INFINITY, lsum = 0.f;
-    const int q0 = cur.q0, kbeg = cur.kbeg, kend = cur.kend;
-    for (int t = 0; t < cur.ntiles; ++t, ++gt) {
-      const int kt = cur.tile0 + t * BK;
-      const bf16_t* Ks = Kb[gt & 1];
-      const bf16_t* Vs = Vb[gt & 1];
-      bool active = q0 < p.Tq;
-      if (CAUSAL) active = active && (kt <= q0 + 31 + p.causal_off);
-      if (active) {  // wave-uniform
-        f32x16 sacc[2];
-#pragma unroll
-        for (int st = 0; st < 2; ++st) {
-          sacc[st] = f32x16{};
-#pragma unroll
-          for (int s = 0; s < KS; ++s) {
-            const s16x8 a = *reinterpret_cast<const s16x8*>(Ks + swz<DP>(32 * st + l32, 2 * s + h));
-            sacc[st] = mfma32(a, qf[s], sacc[st]);
-          }
-        }
-        bool need_mask = kt < kbeg || kt + BK > kend;
-        if (CAUSAL) need_mask = need_mask || (kt + BK - 1 > q0 + p.causal_off);
-        if (need_mask) {
-          const int base = kt + 4 * h;
-          int lo = kbeg - base, hi = kend - base;
-          if (CAUSAL) hi = min(hi, qi + p.causal_off + 1 - base);
-          const unsigned span = hi > lo ? static_cast<unsigned>(hi - lo) : 0u;
-#pragma unroll
-          for (int st = 0; st < 2; ++st) {
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-              const int r = 32 * st + (i & 3) + 8 * (i >> 2);
-              sacc[st][i] = static_cast<unsigned>(r - lo) < span ? sacc[st][i] : -INFINITY;
-            }
-          }
-        }
-        float mloc = -INFINITY;
-#pragma unroll
-        for (int st = 0; st < 2; ++st)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) mloc = fmaxf(mloc, sacc[st][i]);
-        mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
-        if (!__all(mloc <= m + kRescaleThr)) {
-          const float mnew = fmaxf(m, mloc);
-          const float alpha = ex2(m - (mnew == -INFINITY ? 0.f : mnew));
-          m = mnew;
-          lsum *= alpha;
-#pragma unroll
-          for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
-        }
-        const float muse = m == -INFINITY ? 0.f : m;
-#pragma unroll
-        for (int st = 0; st < 2; ++st) {
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const float pv = ex2(sacc[st][i] - muse);
-            sacc[st][i] = pv;
-            lsum += pv;
-          }
-        }
-        s16x8 pf[2][2];
-#pragma unroll
-        for (int st = 0; st < 2; ++st) {
-          pf[st][0] = pack8(sacc[st], 0);
-          pf[st][1] = pack8(sacc[st], 8);
-        }
-#pragma unroll
-        for (int dt = 0; dt < DT; ++dt) {
-          const int c0 = 32 * dt + 16 * ((lane >> 4) & 1);
-#pragma unroll
-          for (int st = 0; st < 2; ++st) {
-#pragma unroll
-            for (int s = 0; s < 2; ++s) {
-              const s16x8 a = tr_frag_perm<DP>(Vs, 32 * st + 16 * s + 4 * h, c0, lane);
-              o[dt] = mfma32(a, pf[st][s], o[dt]);
-            }
-          }
-        }
-      }
-      // next tile of the workgroup's sequence (this block's or the next one's) into the other
-      // buffer, and the one after it into registers
-      if (pending) {
-        lwrite((gt + 1) & 1);
-        pending = false;
-        if (sc.valid) {
-          gload(sc);
-          pending = true;
-          cur_next(sc);
-        }
-      }
-      __syncthreads();
-    }
-
-    lsum += __shfl_xor(lsum, 32, 64);
-    if (qi < p.Tq) {
-      const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
-      bf16_t* op = p.o + cur.b * p.o_sb + qi * p.o_st + static_cast<int64_t>(cur.hq) * p.o_sh;
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt) {
-#pragma unroll
-        for (int g4 = 0; g4 < 4; g4 += 2) {
-          uint2 a, c;
-          a.x = pack2bf(o[dt][4 * g4 + 0] * inv, o[dt][4 * g4 + 1] * inv);
-          a.y = pack2bf(o[dt][4 * g4 + 2] * inv, o[dt][4 * g4 + 3] * inv);
-          c.x = pack2bf(o[dt][4 * g4 + 4] * inv, o[dt][4 * g4 + 5] * inv);
-          c.y = pack2bf(o[dt][4 * g4 + 6] * inv, o[dt][4 * g4 + 7] * inv);
-          const auto rx = __builtin_amdgcn_permlane32_swap(a.x, c.x, false, false);
-          const auto ry = __builtin_amdgcn_permlane32_swap(a.y, c.y, false, false);
-          const int d = 32 * dt + 8 * g4 + 8 * h;
-          *reinterpret_cast<uint4*>(op + d) = make_uint4(rx[0], ry[0], rx[1], ry[1]);
-        }
-      }
-      if (h == 0) {
-        p.lse2[(static_cast<int64_t>(cur.b) * p.Hq + cur.hq) * p.Tq + qi] =
-            lsum > 0.f ? m + __log2f(lsum) : INFINITY;
-      }
-    }
-    if (!have_next) break;
-    cur = nxt;
   }
 }
 
@@ -1901,28 +1626,6 @@ static void fwd_dispatch(const AttnParams& p, bool causal, hipStream_t st) {
     const char* e = std::getenv("DLA_ATTN_FWD_HP");
     return e ? std::atoi(e) : 0;
   }();
-  static const bool persist = [] {
-    const char* e = std::getenv("DLA_ATTN_FWD_PERSIST");
-    return e != nullptr && std::atoi(e) == 1;
-  }();
-  if constexpr (D == 128) {
-    if (persist && forced == 0 && (p.Hq / p.Hkv) % 4 == 0 && p.seg_start == nullptr && p.window <= 0 &&
-        p.rope_cos == nullptr) {
-      constexpr int NW = 8, HP = 4, BQ = 32 * NW / HP;
-      const int nblocks = ((p.Tq + BQ - 1) / BQ) * (p.Hq / HP) * p.B;
-      static const int cus = [] {
-        int dev = 0, n = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-          n = 256;
-        return n;
-      }();
-      const dim3 grid(static_cast<unsigned>(std::min(nblocks, cus)));
-      if (causal) attn_fwd_pkernel<D, true, NW, HP><<<grid, 64 * NW, 0, st>>>(p, nblocks);
-      else attn_fwd_pkernel<D, false, NW, HP><<<grid, 64 * NW, 0, st>>>(p, nblocks);
-      return;
-    }
-  }
   const int group = p.Hq / p.Hkv;
   const int want = forced > 0 ? forced : 4;
   if (want >= 4 && group % 4 == 0) fwd_launch<D, 4>(p, causal, st);
