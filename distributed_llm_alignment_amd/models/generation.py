@@ -463,6 +463,11 @@ def generate(model: CausalLM, input_ids: torch.Tensor, attention_mask: Optional[
         gm = torch.stack(gen_mask, 1)
     if was_training:
         model.train()
+    if ops.decode.DECODE_QKV_ATTN and cache.fast_decode and int(cache.sync_err.item()) != 0:
+        # the fused qkv + attention kernel's counter wait timed out (it proceeds rather than hang
+        # the GPU): the step's attention read an incomplete q / k / v row
+        raise RuntimeError("decode_qkv_attn: a workgroup's wait for the qkv tiles timed out "
+                           "(DLA_DECODE_QKV_ATTN=0 runs the two-launch path)")
     pm = attention_mask if attention_mask is not None else torch.ones_like(input_ids)
     if extra:
         seqs, pm = seqs[:, extra:].contiguous(), pm[:, extra:]
