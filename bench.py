@@ -43,16 +43,20 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--model", default="llama3-8b")
     ap.add_argument("--seq-len", type=int, default=1024)
-    ap.add_argument("--micro-pairs", type=int, default=4)
-    ap.add_argument("--accum", type=int, default=4)
+    ap.add_argument("--micro-pairs", type=int, default=None,
+                    help="pairs per micro-batch (default 4; 2 with --ep-shape, whose capacity-padded "
+                         "expert activations do not fit 4 at full depth)")
+    ap.add_argument("--accum", type=int, default=None,
+                    help="micro-batches per step (default: 16 pairs per step in total)")
     ap.add_argument("--beta", type=float, default=0.1)
     ap.add_argument("--zero", type=int, default=None)
     ap.add_argument("--tp", type=int, default=1, help="tensor-parallel degree (dp = gpus / tp)")
     ap.add_argument("--tp-seq", action="store_true",
                     help="Megatron sequence parallel inside the TP group (reduce-scatter/all-gather)")
     ap.add_argument("--ep", type=int, default=1, help="expert-parallel degree for MoE models")
-    ap.add_argument("--ep-capacity", type=float, default=2.0,
-                    help="EP dispatch capacity factor (sync-free fixed blocks); 0 = exact, host splits")
+    ap.add_argument("--ep-capacity", type=float, default=None,
+                    help="EP dispatch capacity factor (sync-free fixed blocks); 0 = exact, host splits "
+                         "(default 2.0; 1.25 with --ep-shape)")
     ap.add_argument("--sp", type=int, default=1, help="Ulysses sequence-parallel degree (long context)")
     ap.add_argument("--fp8", action="store_true", help="MoE: e4m3 expert GEMMs in the forward")
     ap.add_argument("--grad-ckpt", nargs="?", const="full", default=None, choices=("full", "mlp", "attention"),
@@ -75,7 +79,15 @@ def parse(argv=None):
                          "shards (auto: with --tp > 1 or --zero 3)")
     ap.add_argument("--layers", type=int, default=None, help="debug only: override layer count "
                     "(a reduced model is NOT the benchmark config)")
-    return ap.parse_args(argv)
+    a = ap.parse_args(argv)
+    shape = a.ep_shape > 1
+    if a.micro_pairs is None:
+        a.micro_pairs = 2 if shape else 4
+    if a.accum is None:
+        a.accum = max(1, 16 // a.micro_pairs)
+    if a.ep_capacity is None:
+        a.ep_capacity = 1.25 if shape else 2.0
+    return a
 
 
 def _free_port() -> int:
