@@ -265,20 +265,41 @@ __global__ __launch_bounds__(256) void m64_reduce_kernel(const float* __restrict
   }
 }
 
+// Split-K count: the most splits that keep the grid within one workgroup per CU. A grid of 1.5
+// workgroups per CU (the qkv projection at Llama-3-8B: 48 column blocks x 8 splits = 384) leaves
+// half the CUs streaming twice the bytes of the rest; 48 x 4 = 192 workgroups ran the same GEMM +
+// reduce in 21.4 vs 26.9 us (B = 64, tools/m64_probe.py). DLA_M64_WG=n (A/B) restores the
+// round-3 rule: the fewest splits whose grid reaches n workgroups.
 int m64_splits(int N, int K) {
   static const int target = [] {
     const char* e = getenv("DLA_M64_WG");
-    return e ? atoi(e) : 256;
+    return e ? atoi(e) : 0;
+  }();
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    (void)hipGetLastError();
+    return n;
   }();
   const int nb = N / (16 * kM64Waves);
   const int chunks = K / kM64Ck;
   // split counts the reduce kernel is instantiated for
-  for (int s : {1, 2, 4, 7, 8, 14, 16}) {
-    if (chunks % s) continue;
-    if (nb * s >= target) return s;
+  if (target > 0) {
+    for (int s : {1, 2, 4, 7, 8, 14, 16}) {
+      if (chunks % s) continue;
+      if (nb * s >= target) return s;
+    }
+    for (int s : {16, 14, 8, 7, 4, 2}) if (chunks % s == 0) return s;
+    return 1;
   }
-  for (int s : {16, 14, 8, 7, 4, 2}) if (chunks % s == 0) return s;
-  return 1;
+  // (a grid of fewer column blocks than CUs always splits at least once, as the round-3 rule did:
+  // the residual / norm epilogues live in the reduce launch)
+  int best = 1;
+  for (int s : {2, 4, 7, 8, 14, 16})
+    if (chunks % s == 0 && (nb * s <= cus || (best == 1 && nb < cus))) best = s;
+  return best;
 }
 
 bool m64_shape_ok(int N, int K, bool glu) {

@@ -1,6 +1,7 @@
 """Decode projections at 17..64 rows (csrc/skinny64.hip m64 kernels + split-K reduce) timed one by
 one at Llama-3-8B shapes, weights rotated over >= 1 GB so every call streams from HBM. The split
-count follows DLA_M64_WG (workgroup target, read once per process), so A/B it across processes:
+count is the most that keep the grid within one workgroup per CU; DLA_M64_WG=n (read once per
+process) restores the round-3 rule (fewest splits reaching n workgroups), so A/B across processes:
 
     DLA_M64_WG=512 python tools/m64_probe.py [--rows 64]
 """
@@ -25,7 +26,7 @@ def main():
 
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
-    out = {"rows": a.rows, "m64_wg": os.environ.get("DLA_M64_WG", "256")}
+    out = {"rows": a.rows, "m64_wg": os.environ.get("DLA_M64_WG", "auto")}
     with torch.no_grad():
         for name, N, K in (("qkv", 6144, 4096), ("o", 4096, 4096), ("down", 4096, 14336)):
             ncopy = max(2, -(-(1 << 30) // (N * K * 2)))
