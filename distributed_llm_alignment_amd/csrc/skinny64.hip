@@ -311,21 +311,21 @@ size_t m64_lds_bytes(int M) {
   return static_cast<size_t>(2 * 16 * mt * kM64Ld) * sizeof(bf16_t);
 }
 
-template <int MT, bool GLU, bool NIN, bool TW, int NW, bool NTL>
+template <int MT, bool GLU, bool NIN, bool TW, int NW, bool NTL, int DEPTH = 2>
 static void m64_launch_w(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
                          int64_t ldy, float* ws, int M, int N, int K, int S, const float* ssq_in,
                          int nbp, float eps, hipStream_t st) {
   const size_t lds = static_cast<size_t>(2 * 16 * MT * kM64Ld) * sizeof(bf16_t);
   static bool attr = [] {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&m64_gemm_kernel<MT, GLU, NIN, TW, 2, NW, NTL>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&m64_gemm_kernel<MT, GLU, NIN, TW, DEPTH, NW, NTL>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
     (void)hipGetLastError();
     return true;
   }();
   (void)attr;
   dim3 grid(GLU ? N / 2 / (8 * NW) : N / (16 * NW), S);
-  m64_gemm_kernel<MT, GLU, NIN, TW, 2, NW, NTL><<<grid, 64 * NW, lds, st>>>(x, ldx, W, ldw, y, ldy, ws, M, N,
-                                                                       K, K / S, ssq_in, nbp, eps);
+  m64_gemm_kernel<MT, GLU, NIN, TW, DEPTH, NW, NTL><<<grid, 64 * NW, lds, st>>>(x, ldx, W, ldw, y, ldy, ws, M,
+                                                                           N, K, K / S, ssq_in, nbp, eps);
 }
 
 // NW = 8 waves per workgroup (gate|up: 64 features per workgroup). 4 waves (448 gate|up
@@ -339,10 +339,24 @@ static void m64_launch(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ld
     const char* e = getenv("DLA_DECODE_NT");
     return !(e != nullptr && atoi(e) == 0);
   }();
-  if (TW && nt)
-    m64_launch_w<MT, GLU, NIN, TW, kM64Waves, true>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, ssq_in, nbp, eps, st);
-  else
-    m64_launch_w<MT, GLU, NIN, TW, kM64Waves, false>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, ssq_in, nbp, eps, st);
+  // DLA_M64_DEPTH (A/B): weight chunks in flight per wave on the tiled nt stream (2, 3 or 4)
+  static const int depth = [] {
+    const char* e = getenv("DLA_M64_DEPTH");
+    const int d = e ? atoi(e) : 2;
+    return d >= 2 && d <= 4 ? d : 2;
+  }();
+  if constexpr (TW) {
+    if (nt) {
+      if (depth == 3)
+        m64_launch_w<MT, GLU, NIN, TW, kM64Waves, true, 3>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, ssq_in, nbp, eps, st);
+      else if (depth == 4)
+        m64_launch_w<MT, GLU, NIN, TW, kM64Waves, true, 4>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, ssq_in, nbp, eps, st);
+      else
+        m64_launch_w<MT, GLU, NIN, TW, kM64Waves, true>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, ssq_in, nbp, eps, st);
+      return;
+    }
+  }
+  m64_launch_w<MT, GLU, NIN, TW, kM64Waves, false>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, ssq_in, nbp, eps, st);
 }
 
 template <int MT, bool TW>
