@@ -20,8 +20,10 @@ timeout -k 10 300 python -u tools/bench_generate.py --modes graph --new 128 --ba
 tail -1 $O/gen64.log
 timeout -k 10 400 python -u tools/bench_rlhf.py --batch 8 > $O/rlhf8.log 2>&1 || exit 1
 tail -1 $O/rlhf8.log
+timeout -k 10 600 python -u tools/bench_rlhf.py --batch 64 --grad-ckpt full > $O/rlhf64.log 2>&1 || exit 1
+tail -1 $O/rlhf64.log
 timeout -k 10 600 python -u tools/bench_rlhf.py --algorithm ppo --zero-shape 8 --batch 8 > $O/ppo.log 2>&1 || exit 1
 tail -1 $O/ppo.log | cut -c1-300
-timeout -k 10 600 python -u bench.py --model mixtral-8x7b --ep-shape 8 --micro-pairs 2 --accum 8 --ep-capacity 1.25 --steps 3 --warmup 2 > $O/mixtral.log 2>&1 || exit 1
+timeout -k 10 600 python -u bench.py --model mixtral-8x7b --ep-shape 8 --steps 3 --warmup 2 > $O/mixtral.log 2>&1 || exit 1
 tail -1 $O/mixtral.log | cut -c1-300
 echo ALL_DONE
