@@ -1399,6 +1399,23 @@ __global__ __launch_bounds__(512) void attn_bwd8_kernel(AttnBwdParams p) {
     }
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) store_row(dvp, dv[dt], 1.f, dt);
+  } else if (p.dk_part16 != nullptr) {  // bf16 partials: each rounded once, summed in fp32
+    const int64_t off = ((static_cast<int64_t>(sidx) * p.B + b) * p.Tk + kj) * p.Hkv * D +
+                        static_cast<int64_t>(hk) * D;
+    bf16_t* dkp = p.dk_part16 + off;
+    bf16_t* dvp = p.dv_part16 + off;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d = 32 * dt + 8 * g4 + 4 * h;
+        if (d >= D) continue;
+        *reinterpret_cast<uint2*>(dkp + d) = make_uint2(pack2bf(dk[dt][4 * g4], dk[dt][4 * g4 + 1]),
+                                                        pack2bf(dk[dt][4 * g4 + 2], dk[dt][4 * g4 + 3]));
+        *reinterpret_cast<uint2*>(dvp + d) = make_uint2(pack2bf(dv[dt][4 * g4], dv[dt][4 * g4 + 1]),
+                                                        pack2bf(dv[dt][4 * g4 + 2], dv[dt][4 * g4 + 3]));
+      }
+    }
   } else {
     const int64_t off = ((static_cast<int64_t>(sidx) * p.B + b) * p.Tk + kj) * p.Hkv * D +
                         static_cast<int64_t>(hk) * D;
@@ -1551,8 +1568,19 @@ __device__ __forceinline__ void part_sum8(const float* p, int64_t pstride, int h
   }
 }
 
+__device__ __forceinline__ void part_sum8(const bf16_t* p, int64_t pstride, int hs, f32x4& a0, f32x4& a1) {
+  a0 = f32x4{0.f, 0.f, 0.f, 0.f};
+  a1 = a0;
+  for (int s = 0; s < hs; ++s) {
+    const bf16x8 x = load_bf16x8(p + s * pstride);
+    a0 += f32x4{bf2f(x[0]), bf2f(x[1]), bf2f(x[2]), bf2f(x[3])};
+    a1 += f32x4{bf2f(x[4]), bf2f(x[5]), bf2f(x[6]), bf2f(x[7])};
+  }
+}
+
+template <typename PT>
 __global__ __launch_bounds__(256) void attn_dkv_reduce_kernel(
-    const float* __restrict__ dkp, const float* __restrict__ dvp, int hs, int B, int Tk, int Hkv,
+    const PT* __restrict__ dkp, const PT* __restrict__ dvp, int hs, int B, int Tk, int Hkv,
     int D, float scale, bf16_t* __restrict__ dk, int64_t dk_sb, int64_t dk_st, int64_t dk_sh,
     bf16_t* __restrict__ dv, int64_t dv_sb, int64_t dv_st, int64_t dv_sh,
     const float* __restrict__ rcos, const float* __restrict__ rsin, const int* __restrict__ rpos,
@@ -1668,6 +1696,12 @@ bool attn_dq_slab_bf16() {
   return attn_bwd_waves() == 8 && !(e && std::atoi(e) == 0);
 }
 
+// bf16 dK / dV head-split partials (8-wave kernel; DLA_ATTN_DKV_BF16=0 keeps fp32), read per call
+bool attn_dkv_part_bf16() {
+  const char* e = std::getenv("DLA_ATTN_DKV_BF16");
+  return attn_bwd_waves() == 8 && !(e && std::atoi(e) == 0);
+}
+
 template <int D>
 static void bwd_dispatch(const AttnBwdParams& p, bool causal, hipStream_t st) {
   const int nkb = (p.Tk + kAttnBwdKeys - 1) / kAttnBwdKeys;
@@ -1723,12 +1757,18 @@ void launch_attn_dkv_reduce(const float* dkp, const float* dvp, int hs, int B, i
                             int D, float scale, bf16_t* dk, int64_t dk_sb, int64_t dk_st,
                             int64_t dk_sh, bf16_t* dv, int64_t dv_sb, int64_t dv_st,
                             int64_t dv_sh, const float* rcos, const float* rsin, const int* rpos,
-                            int rot, hipStream_t st) {
+                            int rot, hipStream_t st, const bf16_t* dkp16, const bf16_t* dvp16) {
   const int64_t work = static_cast<int64_t>(B) * Tk * Hkv * (rcos ? rot / 16 + (D - rot) / 8 : D / 8);
   if (work == 0) return;
-  attn_dkv_reduce_kernel<<<stream_grid(work), 256, 0, st>>>(dkp, dvp, hs, B, Tk, Hkv, D, scale, dk,
-                                                            dk_sb, dk_st, dk_sh, dv, dv_sb, dv_st,
-                                                            dv_sh, rcos, rsin, rpos, rot);
+  if (dkp16 != nullptr) {
+    attn_dkv_reduce_kernel<bf16_t><<<stream_grid(work), 256, 0, st>>>(
+        dkp16, dvp16, hs, B, Tk, Hkv, D, scale, dk, dk_sb, dk_st, dk_sh, dv, dv_sb, dv_st, dv_sh, rcos, rsin,
+        rpos, rot);
+    return;
+  }
+  attn_dkv_reduce_kernel<float><<<stream_grid(work), 256, 0, st>>>(dkp, dvp, hs, B, Tk, Hkv, D, scale, dk,
+                                                                   dk_sb, dk_st, dk_sh, dv, dv_sb, dv_st,
+                                                                   dv_sh, rcos, rsin, rpos, rot);
 }
 
 }  // namespace dla

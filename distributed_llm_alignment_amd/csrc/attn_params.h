@@ -50,6 +50,8 @@ struct AttnBwdParams {
                        // rounded once, summed in fp32 by the reduce -- half the slab traffic
   float* dk_part;      // [hsplit, B, Tk, Hkv, D] fp32 partials (hsplit > 1 only)
   float* dv_part;
+  bf16_t* dk_part16;   // the same partials in bf16 (8-wave kernel, DLA_ATTN_DKV_BF16): summed in
+  bf16_t* dv_part16;   // fp32 by the reduce -- half the partial traffic, as dq_slab16
   bf16_t* dk;          // strided like k (hsplit == 1)
   bf16_t* dv;          // strided like v (hsplit == 1)
   int hsplit;          // GQA group split across workgroups (balances causal key blocks)

@@ -71,13 +71,15 @@ void launch_attn_fwd(const AttnParams&, int, bool, hipStream_t);
 void launch_attn_bwd_delta(const bf16_t*, const bf16_t*, int64_t, int64_t, int64_t, int64_t,
                            int64_t, int64_t, int, int, int, int, float*, hipStream_t);
 void launch_attn_bwd(const AttnBwdParams&, int, bool, hipStream_t);
+bool attn_dkv_part_bf16();
 bool attn_dq_slab_bf16();
 void launch_attn_dq_reduce(const float*, int, int, int, int, int, int, bool, int, int,
                            const int*, const int*, int, bf16_t*, int64_t, int64_t, int64_t,
                            const float*, const float*, const int*, int, hipStream_t, const bf16_t*);
 void launch_attn_dkv_reduce(const float*, const float*, int, int, int, int, int, float, bf16_t*,
                             int64_t, int64_t, int64_t, bf16_t*, int64_t, int64_t, int64_t,
-                            const float*, const float*, const int*, int, hipStream_t);
+                            const float*, const float*, const int*, int, hipStream_t, const bf16_t*,
+                            const bf16_t*);
 void launch_transpose_bf16(const bf16_t*, int64_t, int64_t, int64_t, bf16_t*, int64_t, hipStream_t);
 
 // ================================= norms ======================================================
@@ -494,17 +496,20 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k,
   auto slab = at::empty({std::max<int64_t>(nkb, 1), B, slab_rows, Hq, D}, slab16 ? q.options() : fopt);
   const int hs = attn_bwd_hsplit(nkb, Hkv, B, Hq / Hkv, causal, device_cus(q.get_device()));
   at::Tensor dkp, dvp;
+  const bool part16 = hs > 1 && attn_dkv_part_bf16();
   if (hs > 1) {
-    dkp = at::empty({hs, B, Tk, Hkv, D}, fopt);
-    dvp = at::empty({hs, B, Tk, Hkv, D}, fopt);
+    dkp = at::empty({hs, B, Tk, Hkv, D}, part16 ? q.options() : fopt);
+    dvp = at::empty({hs, B, Tk, Hkv, D}, part16 ? q.options() : fopt);
   }
   AttnBwdParams p{};
   p.q = cbp(q); p.k = cbp(k); p.v = cbp(v); p.dout = cbp(dout);
   p.lse2 = lse2.data_ptr<float>(); p.delta = delta.data_ptr<float>();
   p.dq_slab = slab16 ? nullptr : slab.data_ptr<float>();
   p.dq_slab16 = slab16 ? bp(slab) : nullptr;
-  p.dk_part = hs > 1 ? dkp.data_ptr<float>() : nullptr;
-  p.dv_part = hs > 1 ? dvp.data_ptr<float>() : nullptr;
+  p.dk_part = hs > 1 && !part16 ? dkp.data_ptr<float>() : nullptr;
+  p.dv_part = hs > 1 && !part16 ? dvp.data_ptr<float>() : nullptr;
+  p.dk_part16 = part16 ? bp(dkp) : nullptr;
+  p.dv_part16 = part16 ? bp(dvp) : nullptr;
   p.dk = bp(dk); p.dv = bp(dv);
   p.hsplit = hs;
   p.slab_rows = static_cast<int>(slab_rows);
@@ -539,7 +544,8 @@ void attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k,
     launch_attn_dkv_reduce(p.dk_part, p.dv_part, hs, static_cast<int>(B), static_cast<int>(Tk),
                            static_cast<int>(Hkv), static_cast<int>(D), p.scale, bp(dk),
                            dk.stride(0), dk.stride(1), dk.stride(2), bp(dv), dv.stride(0),
-                           dv.stride(1), dv.stride(2), p.rope_cos, p.rope_sin, p.rope_pos, p.rope_rot, st);
+                           dv.stride(1), dv.stride(2), p.rope_cos, p.rope_sin, p.rope_pos, p.rope_rot, st,
+                           p.dk_part16, p.dv_part16);
   }
 }
 
