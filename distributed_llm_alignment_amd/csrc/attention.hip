@@ -1628,8 +1628,14 @@ __global__ __launch_bounds__(256) void attn_dkv_reduce_kernel(
 // launchers
 // ----------------------------------------------------------------------------------------------
 static inline unsigned stream_grid(int64_t work) {
+  // grid-stride cap of the reduce passes (DLA_ATTN_REDUCE_GRID, A/B; default 2048 workgroups)
+  static const int64_t cap = [] {
+    const char* e = std::getenv("DLA_ATTN_REDUCE_GRID");
+    const int64_t v = e ? std::atoll(e) : 2048;
+    return v > 0 ? v : 2048;
+  }();
   int64_t g = (work + 255) / 256;
-  if (g > 2048) g = 2048;
+  if (g > cap) g = cap;
   return static_cast<unsigned>(g < 1 ? 1 : g);
 }
 
