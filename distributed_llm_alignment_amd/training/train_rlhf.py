@@ -6,7 +6,9 @@ attention over the cache), score `prompt\\n\\nresponse` with the reward model (e
 fixes #8), then REINFORCE with a KL-shaped reward and a mean baseline:
     kl = logp_pi - logp_ref ;  r' = r - kl_coef*kl ;  A = r' - mean(r') ;  loss = -mean(A * logp_pi)
 (fused HIP kernel). The log-prob mask covers prompt + generated tokens up to and including EOS
-(fixes #10). `generation_params.do_sample` defaults to True (#9).
+(fixes #10). `generation_params.do_sample` defaults to True (#9). `ppo.update_micro_batch: m`
+runs the update as gradient-accumulated micro-batches of m rollouts with a baseline each, the
+per-process semantics of the reference's multi-process run (`reinforce_update`).
 
 Overlap (BASELINE north star, `ppo.async_rollouts: true`, off by default since it changes the
 semantics to one-step-stale rollouts): step k+1's rollouts are generated while step k's gradient
@@ -25,6 +27,7 @@ clipped value loss (fused HIP fwd+bwd kernels), policy and critic each on their 
 from __future__ import annotations
 
 import argparse
+import contextlib
 import random
 from pathlib import Path
 from typing import Dict, List
@@ -144,11 +147,11 @@ def main(argv=None) -> int:
     policy.model.train()
     if algo == "ppo":
         return _ppo_loop(ctx, config, ppo, policy, ref, rm, rollout, engine, steps, kl_coef, log_every)
+    micro = int(ppo.get("update_micro_batch", 0) or 0)
     pending = rollout()
     for step in range(steps):
         seqs, mask, scores, _ = pending
-        loss, m = rlhf_loss(policy.model, ref.model, seqs, mask, scores, kl_coef)
-        loss.backward()
+        loss, m = reinforce_update(policy.model, ref.model, engine, seqs, mask, scores, kl_coef, micro)
         if ppo.get("async_rollouts", False) and step + 1 < steps:
             # the bucketed reduce-scatter launched by the backward hooks is in flight on RCCL's
             # stream; generating the next rollouts (pre-update weights) overlaps it
@@ -170,6 +173,34 @@ def main(argv=None) -> int:
     ctx.log("RLHF PPO loop complete")
     ctx.logger.close()
     return 0
+
+
+def reinforce_update(policy, ref, engine, seqs, mask, scores, kl_coef: float, micro: int = 0):
+    """Backward of the KL-penalised policy-gradient loss over this rank's rollouts.
+
+    micro > 0 (`ppo.update_micro_batch`): gradient-accumulated micro-batches of `micro` rollouts,
+    each with its own mean baseline and weighted by its share of the rollouts -- the gradient of
+    a job with that many rollouts per process (the reference splits `ppo.batch_size` across
+    processes and takes `rewards.mean()` per process, src/training/train_rlhf.py:114,151, then
+    DDP averages), and no activation recompute is needed for a large one-GPU batch.
+    Returns (loss, metrics) like `rlhf_loss`."""
+    n = seqs.shape[0]
+    if micro <= 0 or micro >= n:
+        loss, m = rlhf_loss(policy, ref, seqs, mask, scores, kl_coef)
+        loss.backward()
+        return loss, m
+    starts = list(range(0, n, micro))
+    tot, kl = 0.0, 0.0
+    for i, s0 in enumerate(starts):
+        sl = slice(s0, min(n, s0 + micro))
+        w = (sl.stop - sl.start) / n
+        ctx = engine.no_sync() if i < len(starts) - 1 else contextlib.nullcontext()
+        with ctx:
+            loss, m = rlhf_loss(policy, ref, seqs[sl], mask[sl], scores[sl], kl_coef)
+            (loss * w).backward()
+        tot = tot + loss.detach() * w
+        kl = kl + m["kl"] * w
+    return tot, {"kl": kl}
 
 
 def _ppo_loop(ctx, config, ppo, policy, ref, rm, rollout, engine, steps, kl_coef, log_every) -> int:

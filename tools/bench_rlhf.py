@@ -45,12 +45,19 @@ def main() -> int:
                     help="generate step k+1's rollouts (policy snapshot, side stream) during step k's update")
     ap.add_argument("--grad-ckpt", default="", help="policy activation recompute: full|mlp|attention "
                     "(the reference's rlhf_config batch of 64 rollouts on one GPU needs mlp)")
+    ap.add_argument("--micro", type=int, default=0,
+                    help="reinforce: run the policy update as batch/micro gradient-accumulated "
+                         "micro-batches, each with its own advantage baseline -- one rank's share of "
+                         "a batch/micro-rank DDP job (the reference splits the batch across processes "
+                         "and takes rewards.mean() per process), so no activation recompute is needed")
     ap.add_argument("--algorithm", choices=("reinforce", "ppo"), default="reinforce")
     ap.add_argument("--zero-shape", type=int, default=1,
                     help="engines laid out as rank 0 of an N-rank ZeRO-1 job (1/N optimizer state)")
     ap.add_argument("--ppo-epochs", type=int, default=2)
     ap.add_argument("--minibatches", type=int, default=2)
     a = ap.parse_args()
+    if a.micro and a.batch % a.micro:
+        ap.error("--batch must be a multiple of --micro")
     if a.algorithm == "ppo":
         return ppo_main(a)
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -58,6 +65,7 @@ def main() -> int:
     from distributed_llm_alignment_amd.models.reward import RewardModel
     from distributed_llm_alignment_amd.objectives import rlhf_loss
     from distributed_llm_alignment_amd.ops import _ext
+    from distributed_llm_alignment_amd.training.train_rlhf import reinforce_update
     from distributed_llm_alignment_amd.parallel.data_parallel import DataParallelEngine
     from distributed_llm_alignment_amd.utils.tuning import enable_gemm_tuning
 
@@ -101,8 +109,7 @@ def main() -> int:
                 scores = rm(r_ids, r_mask)
         t2 = sync()
         pol.train()
-        loss, _ = rlhf_loss(pol, ref, seqs, mask, scores.float(), 0.1)
-        loss.backward()
+        reinforce_update(pol, ref, eng, seqs, mask, scores.float(), 0.1, a.micro)
         eng.step()
         t3 = sync()
         if record:
@@ -190,7 +197,8 @@ def main() -> int:
         dt = sync() - t
     print(json.dumps({"bench": "rlhf_step", "model": cfg.name, "rollouts_per_step": a.batch,
                       "grad_ckpt": a.grad_ckpt or "none", "handoff": a.handoff,
-                      "overlap": bool(a.overlap),
+                      "overlap": bool(a.overlap), "update_micro": a.micro or a.batch,
+                      "peak_gib": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1),
                       "prompt": a.prompt, "new_tokens": a.new, "s_per_step": round(dt / a.steps, 3),
                       "rollouts_per_s": round(a.batch * a.steps / dt, 3),
                       **{f"{k}_s": round(v / a.steps, 3) for k, v in phases.items()}}), flush=True)
