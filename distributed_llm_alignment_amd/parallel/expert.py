@@ -29,7 +29,7 @@ expert-data-parallel group (replicas holding the same experts) instead of the fu
 from __future__ import annotations
 
 import os
-from typing import List
+from typing import List, Optional
 
 import torch
 import torch.distributed as dist
@@ -117,37 +117,52 @@ class _A2AWait(torch.autograd.Function):
 _NATIVE_ROUTE = os.environ.get("DLA_EP_NATIVE_ROUTE", "1") != "0"
 
 
+# The token -> slot gather's backward as a per-token gather-sum through the slot positions (the
+# combine kernel with unit weights) instead of an fp32 index_add + bf16 cast (Mixtral EP shape:
+# 41 + 11 ms/step); DLA_EP_GATHER_BWD_COMBINE=0 keeps the index_add for A/B.
+GATHER_BWD_COMBINE = os.environ.get("DLA_EP_GATHER_BWD_COMBINE", "1") != "0"
+
+
 def _native_route(topi: torch.Tensor, E: int, ep: int, slots: int) -> bool:
     return _NATIVE_ROUTE and topi.is_cuda and E <= 64 and slots <= 16384 and topi.dtype in (torch.int32, torch.int64)
 
 
 class _GatherRowsFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, idx, injective):
-        ctx.save_for_backward(idx)
+    def forward(ctx, x, idx, injective, inv):
+        ctx.save_for_backward(idx, inv)
         ctx.R, ctx.injective = x.shape[0], injective
         return ops._ext.require().gather_rows(x, idx)
 
     @staticmethod
     def backward(ctx, g):
-        (idx,) = ctx.saved_tensors
+        idx, inv = ctx.saved_tensors
         if ctx.injective:  # one HIP scatter, no accumulation needed
-            return ops._ext.require().scatter_rows(g.contiguous(), idx, ctx.R), None, None
+            return ops._ext.require().scatter_rows(g.contiguous(), idx, ctx.R), None, None, None
+        if inv is not None:
+            # the inverse map given (row r of x read by entries inv[r, :], >= len(g) = none): a
+            # gather-sum per row, fp32 in j order -- the MoE combine kernel with unit weights
+            return ops._ext.require().moe_combine(g.contiguous(), inv, None), None, None, None
         # a row read by several slots (a token's k choices): accumulate, in fp32
         valid = (idx >= 0).unsqueeze(-1)
         dx = torch.zeros((ctx.R, g.shape[1]), dtype=torch.float32, device=g.device)
         dx.index_add_(0, idx.clamp(min=0), torch.where(valid, g.float(), torch.zeros((), device=g.device)))
-        return dx.to(g.dtype), None, None
+        return dx.to(g.dtype), None, None, None
 
 
-def _gather_rows(x: torch.Tensor, idx: torch.Tensor, injective: bool = True) -> torch.Tensor:
+def _gather_rows(x: torch.Tensor, idx: torch.Tensor, injective: bool = True,
+                 inv: Optional[torch.Tensor] = None) -> torch.Tensor:
     """out[i] = x[idx[i]] (idx < 0 -> zero row). Static shapes, no host sync; the backward is the
     matching scatter, or (`injective` False: a row read by several entries, e.g. a token's k
-    slots) a scatter-add. On the GPU the forward (and the injective backward) is one HIP launch
-    (csrc/moe.hip gather_rows / scatter_rows)."""
+    slots) a scatter-add -- with `inv` ([rows of x, k] int32: the entries that read each row,
+    values >= len(idx) for none) a gather-sum instead. On the GPU the forward and both backward
+    forms are one HIP launch each (csrc/moe.hip gather_rows / scatter_rows / moe_combine)."""
     if (_NATIVE_ROUTE and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 2 and x.shape[1] % 8 == 0
             and x.stride(1) == 1 and x.stride(0) % 8 == 0 and idx.dtype == torch.int64):
-        return _GatherRowsFn.apply(x, idx.contiguous(), injective)
+        if inv is not None and not (GATHER_BWD_COMBINE and inv.shape[0] == x.shape[0] and inv.shape[1] <= 8):
+            inv = None
+        return _GatherRowsFn.apply(x, idx.contiguous(), injective,
+                                   inv.to(torch.int32).contiguous() if inv is not None else None)
     valid = (idx >= 0).unsqueeze(-1)
     return torch.where(valid, x.index_select(0, idx.clamp(min=0)), torch.zeros((), dtype=x.dtype, device=x.device))
 
@@ -273,7 +288,8 @@ class ExpertParallel:
             else:
                 rc = torch.empty_like(sent)
                 w = dist.all_to_all_single(rc, sent.contiguous(), group=self.group, async_op=True)
-            xs = _gather_rows(h2[a:b], send_src, injective=False)  # a token fills up to k slots
+            # a token fills up to k slots: its gradient is the sum of theirs, gathered through pos
+            xs = _gather_rows(h2[a:b], send_src, injective=False, inv=pos)
             xr = _A2AStart.apply(xs, self.group, holder)
             stage.append((C, pos, w, rc, xr))
         # 2) per chunk: wait for its rows, experts on the device-built order, return all-to-all

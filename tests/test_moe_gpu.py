@@ -402,3 +402,32 @@ def test_native_gather_rows_fwd_bwd(monkeypatch):
         if inj:
             assert torch.equal(res[0][1], res[1][1])
         assert (res[0][1] - ref).abs().max() <= 1e-2 * ref.abs().max()
+
+
+@pytest.mark.gpu
+def test_native_gather_rows_bwd_through_inverse_map():
+    """The token -> slot gather's backward as a gather-sum through the slot positions (the
+    combine kernel with unit weights, parallel/expert.py `inv`) equals the fp32 scatter-add,
+    including tokens with dropped slots (position >= the slot count)."""
+    from distributed_llm_alignment_amd.parallel import expert as epm
+
+    g = torch.Generator(device=DEV).manual_seed(11)
+    N, k, H, S = 257, 2, 264, 400  # tokens, top-k, width, slots (some tokens' slots dropped)
+    x = torch.randn(N, H, device=DEV, generator=g).to(torch.bfloat16)
+    perm = torch.randperm(N * k, device=DEV, generator=g)
+    pos = torch.full((N * k,), S, dtype=torch.long, device=DEV)
+    pos[perm[:S]] = torch.arange(S, device=DEV)  # slot s <- (token, choice) perm[s]
+    src = torch.full((S,), -1, dtype=torch.long, device=DEV)
+    src[pos[pos < S]] = (torch.arange(N * k, device=DEV) // k)[pos < S]
+    pos = pos.view(N, k)
+    go = torch.randn(S, H, device=DEV, generator=g).to(torch.bfloat16)
+    out = []
+    for inv in (pos, None):
+        xx = x.clone().requires_grad_(True)
+        y = epm._gather_rows(xx, src, injective=False, inv=inv)
+        (dx,) = torch.autograd.grad(y, [xx], go)
+        out.append((y, dx))
+    assert torch.equal(out[0][0], out[1][0])
+    ref = torch.zeros(N, H, device=DEV).index_add_(0, src.clamp(min=0), go.float() * (src >= 0).unsqueeze(-1))
+    assert torch.equal(out[0][1], ref.to(torch.bfloat16))  # k = 2: both sums are exact-order fp32
+    assert torch.equal(out[0][1], out[1][1])
