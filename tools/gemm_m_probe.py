@@ -1,0 +1,66 @@
+"""Per-layout GEMM rates of the dense projections at several token counts M, through the shipped
+TunableOp table in read mode exactly as bench.py loads it (shapes missing from the table fall to
+the library heuristic): forward Y = X W^T, input grad through the cached W^T (TN), weight grad TN.
+
+    python tools/gemm_m_probe.py [--model mixtral-8x7b] [--ms 4096,8192]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+import torch
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def timeit(fn, iters=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(iters)]
+    for s, e in ev:
+        s.record()
+        fn()
+        e.record()
+    torch.cuda.synchronize()
+    return statistics.median(s.elapsed_time(e) for s, e in ev) * 1e3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="mixtral-8x7b")
+    ap.add_argument("--ms", default="4096,8192")
+    a = ap.parse_args()
+    from distributed_llm_alignment_amd.models import get_config
+    from distributed_llm_alignment_amd.utils.tuning import enable_gemm_tuning
+
+    mode = enable_gemm_tuning(0)
+    cfg = get_config(a.model)
+    H = cfg.hidden_size
+    dev = torch.device("cuda", 0)
+    shapes = [("qkv", cfg.q_size + 2 * cfg.kv_size, H), ("o", H, cfg.q_size)]
+    for M in [int(x) for x in a.ms.split(",")]:
+        for name, N, K in shapes:
+            W = torch.randn(N, K, device=dev, dtype=torch.bfloat16) * 0.02
+            Wt = W.t().contiguous()
+            X = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+            dY = torch.randn(M, N, device=dev, dtype=torch.bfloat16)
+            dYt, Xt = dY.t().contiguous(), X.t().contiguous()
+            G = torch.zeros(N, K, device=dev, dtype=torch.float32)
+            fl = 2.0 * M * N * K
+            r = {"model": a.model, "gemm": name, "M": M, "N": N, "K": K, "tuning": mode}
+            for tag, fn in (("fwd", lambda: F.linear(X, W)), ("dgrad_tn", lambda: F.linear(dY, Wt)),
+                            ("wgrad_tn_f32", lambda: torch.addmm(G, dYt, Xt.t(), out_dtype=torch.float32, out=G))):
+                us = timeit(fn)
+                r[f"{tag}_us"] = round(us, 1)
+                r[f"{tag}_TFs"] = round(fl / us / 1e6, 0)
+            print(json.dumps(r), flush=True)
+            del W, Wt, X, dY, dYt, Xt, G
+            torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
