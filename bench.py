@@ -393,7 +393,7 @@ def main(argv=None) -> int:
     if args.profile_dir:
         from torch.profiler import ProfilerActivity, profile
 
-        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
             for _ in range(args.steps):
                 train_step()
             sync()
@@ -421,6 +421,10 @@ def main(argv=None) -> int:
         prof.export_chrome_trace(os.path.join(args.profile_dir, "trace.json"))
         with open(os.path.join(args.profile_dir, "kernels.txt"), "w") as fh:
             fh.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=60))
+        with open(os.path.join(args.profile_dir, "ops_by_shape.txt"), "w") as fh:
+            fh.write(prof.key_averages(group_by_input_shape=True).table(sort_by="cuda_time_total",
+                                                                         row_limit=100, max_name_column_width=60,
+                                                                         max_shapes_column_width=120))
 
     pairs_per_step = args.micro_pairs * args.accum * mesh.dp
     ms = elapsed / args.steps * 1000.0

@@ -365,6 +365,12 @@ def _single_lib(offs: torch.Tensor, w: torch.Tensor, rows: int) -> bool:
             and rows >= 256)
 
 
+# Capacity-buffer padding rows (past offs[-1]) zeroed in place on the node's own outputs instead of
+# by out-of-place masked_fills (a clone + fill of the [rows, H] buffer each way; Mixtral EP shape:
+# ~70 ms per step). DLA_MOE_TAIL_INPLACE=0 restores the masked_fills for A/B.
+_TAIL_INPLACE = os.environ.get("DLA_MOE_TAIL_INPLACE", "1") != "0"
+
+
 class _GroupedExpertsFn(torch.autograd.Function):
     """Grouped SwiGLU experts on the device-driven grouped GEMM; offs [E+1] int32 on device.
     `sync_free`: the backward also stays on the grouped kernels (never reads offs on the host)."""
@@ -385,6 +391,10 @@ class _GroupedExpertsFn(torch.autograd.Function):
                 ys = F.linear(a, w_down.detach()[0])
             else:
                 ys = C.gg_fwd(a, w_down, offs, None, None)
+        if sync_free and ys.shape[0] > 0 and _TAIL_INPLACE:
+            # capacity buffer (experts_swiglu_offsets): rows past offs[-1] are zero, in place on
+            # the fresh output (an out-of-place masked_fill cost a clone + fill per call)
+            C.zero_rows_from(ys, offs[-1:])
         ctx.save_for_backward(xs, gu, offs)
         ctx.w_up, ctx.w_down = w_up, w_down  # (on ctx: see ops.linear._LinearMainGradFn)
         ctx.sync_free = sync_free
@@ -439,10 +449,13 @@ class _GroupedExpertsFn(torch.autograd.Function):
                 dxs = F.linear(dgu, _expert0_t(w_up))  # dgu [M, 2F] . W_up[0] [2F, H], TN layout
             else:
                 dxs = C.gg_dgrad(dgu, w_up, offs)
-        if dxs is not None and dxs.shape[0] > 0:
-            # rows past offs[-1] (padding of a capacity buffer) are never written by the kernel
+        if dxs is not None and dxs.shape[0] > 0 and not _TAIL_INPLACE:
             tail = torch.arange(dxs.shape[0], device=dxs.device) >= offs[-1].long()
             dxs = dxs.masked_fill(tail.unsqueeze(-1), 0)
+        elif dxs is not None and dxs.shape[0] > 0 and not single:
+            # rows past offs[-1] (padding of a capacity buffer) are never written by the grouped
+            # kernel (single: dgu's padding rows are zero, so dxs's are too)
+            C.zero_rows_from(dxs, offs[-1:])
         return dxs, outs[0], outs[1], None, None, None
 
 
@@ -531,9 +544,12 @@ def experts_swiglu_offsets(xs: torch.Tensor, w_up: torch.Tensor, w_down: torch.T
     if _grouped_ok(xs, w_up, w_down):
         if fp8 and _FP8 is None:
             fp8 = False
+        # rows past offs[-1] come back zero (zeroed in place inside the node)
         ys = _GroupedExpertsFn.apply(xs, w_up, w_down, offs.to(torch.int32), bool(fp8), True)
-        tail = torch.arange(ys.shape[0], device=ys.device) >= offs[-1].long()
-        return ys.masked_fill(tail.unsqueeze(-1), 0)
+        if not _TAIL_INPLACE:
+            tail = torch.arange(ys.shape[0], device=ys.device) >= offs[-1].long()
+            ys = ys.masked_fill(tail.unsqueeze(-1), 0)
+        return ys
     return _ref_grouped_experts(xs, w_up, w_down, offs)
 
 
