@@ -26,4 +26,8 @@ timeout -k 10 600 python -u tools/bench_rlhf.py --algorithm ppo --zero-shape 8 -
 tail -1 $O/ppo.log | cut -c1-300
 timeout -k 10 600 python -u bench.py --model mixtral-8x7b --ep-shape 8 --steps 3 --warmup 2 > $O/mixtral.log 2>&1 || exit 1
 tail -1 $O/mixtral.log | cut -c1-300
+timeout -k 10 600 python -u bench.py --model mixtral-8x7b --ep-shape 8 --fp8 --steps 3 --warmup 2 > $O/mixtral_fp8.log 2>&1 || exit 1
+tail -1 $O/mixtral_fp8.log | cut -c1-300
+timeout -k 10 600 python -u tools/bench_rlhf.py --batch 64 --micro 8 > $O/rlhf64_micro8.log 2>&1 || exit 1
+tail -1 $O/rlhf64_micro8.log
 echo ALL_DONE
