@@ -275,8 +275,12 @@ class ExpertParallel:
         bounds = [(N * c // nch, N * (c + 1) // nch) for c in range(nch)]
         holder: list = []
         stage = []
+        # chunk views by one split (its backward is one cat; per-chunk slices each build a zero
+        # [N, H] gradient and add it)
+        h2c = torch.split(h2, [b - a for a, b in bounds])
+        topvc = torch.split(topv, [b - a for a, b in bounds])
         # 1) route every chunk and launch its dispatch all-to-alls (rows + counts) async
-        for a, b in bounds:
+        for ci, (a, b) in enumerate(bounds):
             C = self.capacity(b - a, k)
             send_src, pos, sent, ndrop = self._route_chunk(topi[a:b], C)
             if ndrop is not None:
@@ -289,7 +293,7 @@ class ExpertParallel:
                 rc = torch.empty_like(sent)
                 w = dist.all_to_all_single(rc, sent.contiguous(), group=self.group, async_op=True)
             # a token fills up to k slots: its gradient is the sum of theirs, gathered through pos
-            xs = _gather_rows(h2[a:b], send_src, injective=False, inv=pos)
+            xs = _gather_rows(h2c[ci], send_src, injective=False, inv=pos)
             xr = _A2AStart.apply(xs, self.group, holder)
             stage.append((C, pos, w, rc, xr))
         # 2) per chunk: wait for its rows, experts on the device-built order, return all-to-all
@@ -306,11 +310,11 @@ class ExpertParallel:
         # 3) combine each chunk (dropped slots point one past the buffer: the native combine reads
         # them as zero; the CPU reference gets an appended zero row)
         outs = []
-        for (a, b), (pos, ys) in zip(bounds, back):
+        for ci, (pos, ys) in enumerate(back):
             ys = _A2AWait.apply(ys, holder)
             if not ys.is_cuda:
                 ys = torch.cat([ys, ys.new_zeros(1, H)], 0)
-            outs.append(ops.moe.combine(ys, pos.to(torch.int32), topv[a:b]))
+            outs.append(ops.moe.combine(ys, pos.to(torch.int32), topvc[ci]))
         return outs[0] if len(outs) == 1 else torch.cat(outs, 0)
 
     # ------------------------------------------------------------------ exact (host splits)
