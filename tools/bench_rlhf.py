@@ -58,6 +58,8 @@ def main() -> int:
     a = ap.parse_args()
     if a.micro and a.batch % a.micro:
         ap.error("--batch must be a multiple of --micro")
+    if a.micro and (a.overlap or a.algorithm == "ppo"):
+        ap.error("--micro applies to the synchronous reinforce update only")
     if a.algorithm == "ppo":
         return ppo_main(a)
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
