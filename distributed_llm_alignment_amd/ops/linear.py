@@ -53,7 +53,9 @@ def input_grad(dy2: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
 # with the HIP tiled transpose and run the TN GEMM: Llama-3-8B up 1.66 -> 1.22 + 0.24 ms,
 # down 0.95 -> 0.68 + 0.14 ms; no gain for qkv / o (one-off layout probe, MI355X).
 TN_WGRAD = os.environ.get("DLA_TN_WGRAD", "1") != "0"
-TN_WGRAD_MIN_ELEMS = int(os.environ.get("DLA_TN_WGRAD_MIN", "0"))
+# lower bound: a small weight (the MoE router, [E, H]) is not worth transposing its [tokens, H]
+# input for (Mixtral EP shape: 15 ms per step of [4096, 4096] transposes for an [8, 4096] gradient)
+TN_WGRAD_MIN_ELEMS = int(float(os.environ.get("DLA_TN_WGRAD_MIN", str(1 << 20))))
 # upper bound (A/B knob): the LM head's dY is the [tokens, vocab] logit gradient, whose transpose
 # alone moves 2 x 2.1 GB per micro-batch at Llama-3 vocab
 TN_WGRAD_MAX_ELEMS = int(os.environ.get("DLA_TN_WGRAD_MAX", str(1 << 62)))

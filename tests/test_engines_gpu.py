@@ -66,13 +66,14 @@ def test_transposed_dgrad_matches_nn_dgrad():
 
     lin = importlib.import_module("distributed_llm_alignment_amd.ops.linear")
 
+    saved = (lin.TRANSPOSED_DGRAD, lin.TN_WGRAD, lin.TN_WGRAD_MIN_ELEMS)
     try:
         lin.TRANSPOSED_DGRAD, lin.TN_WGRAD, lin.TN_WGRAD_MIN_ELEMS = True, True, 0
         a = _run("dp", False)
         lin.TRANSPOSED_DGRAD, lin.TN_WGRAD = False, False
         b = _run("dp", False)
     finally:
-        lin.TRANSPOSED_DGRAD, lin.TN_WGRAD, lin.TN_WGRAD_MIN_ELEMS = True, True, 0
+        lin.TRANSPOSED_DGRAD, lin.TN_WGRAD, lin.TN_WGRAD_MIN_ELEMS = saved
     assert a == pytest.approx(b, rel=1e-2, abs=1e-3), (a, b)
 
 
