@@ -77,6 +77,10 @@ def parse(argv=None):
     ap.add_argument("--sharded-init", choices=("auto", "on", "off"), default="auto",
                     help="build on the meta device and materialise only this rank's TP / FSDP "
                          "shards (auto: with --tp > 1 or --zero 3)")
+    ap.add_argument("--force-pg", action="store_true",
+                    help="one GPU: create a real ONE-rank RCCL process group before any GPU work and "
+                         "run the N-GPU engine path on it (ZeRO-1 bucket hooks, reduce-scatter on "
+                         "RCCL's stream during backward, shard AdamW, overlapped all-gather)")
     ap.add_argument("--layers", type=int, default=None, help="debug only: override layer count "
                     "(a reduced model is NOT the benchmark config)")
     a = ap.parse_args(argv)
@@ -264,7 +268,10 @@ def main(argv=None) -> int:
 
     # a dead peer must end the run in bounded time, not after the 30 min default
     st = init_distributed(device="cpu" if args.device == "cpu" else None,
-                          timeout_s=int(os.environ.get("DLA_BENCH_COLLECTIVE_TIMEOUT_S", "300")))
+                          timeout_s=int(os.environ.get("DLA_BENCH_COLLECTIVE_TIMEOUT_S", "300")),
+                          force_pg=args.force_pg)
+    if args.force_pg and not st.forced and st.world_size == 1:
+        raise SystemExit("bench.py: --force-pg could not create the one-rank process group")
     dev = st.device
     if st.world_size != args.gpus:
         raise SystemExit(f"bench.py: running {st.world_size} rank(s) for --gpus {args.gpus}")
@@ -283,7 +290,7 @@ def main(argv=None) -> int:
         _ext.require()
         gemm_mode = enable_gemm_tuning(dev.index)
     coll_bw = {}
-    if st.world_size > 1 or os.environ.get("DLA_BENCH_PREFLIGHT") == "1":
+    if st.world_size > 1 or st.forced or os.environ.get("DLA_BENCH_PREFLIGHT") == "1":
         preflight(st, dev)
         if dev.type == "cuda" or os.environ.get("DLA_BENCH_COLLBW") == "1":
             coll_bw = collective_bandwidth(st, dev, mb=int(os.environ.get("DLA_BENCH_COLLBW_MB", "256")))
@@ -461,7 +468,9 @@ def main(argv=None) -> int:
                 "parallelism": f"dp{mesh.dp}" + (f"-tp{mesh.tp}" if mesh.tp > 1 else "")
                                + (f"-ep{mesh.ep}" if mesh.ep > 1 else "")
                                + (f"-sp{mesh.sp}" if mesh.sp > 1 else "")
-                               + (f"-zero{engine.zero}" if mesh.dp * mesh.sp > 1 or engine.zero == 3 else ""),
+                               + (f"-zero{engine.zero}" if mesh.dp * mesh.sp > 1 or engine.zero == 3
+                                  or st.forced else "")
+                               + ("(one-rank RCCL group, forced comm)" if st.forced else ""),
                 "micro_batch_pairs": args.micro_pairs,
                 "grad_accum": args.accum,
                 "ref_model": "frozen, co-resident" + (", own HIP stream" if ref_stream else ""),

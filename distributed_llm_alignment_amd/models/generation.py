@@ -366,11 +366,19 @@ def generate(model: CausalLM, input_ids: torch.Tensor, attention_mask: Optional[
         # graph) instead of an all-gather per layer per token
         import contextlib
 
-        with contextlib.ExitStack() as stack:
-            for eng in model.sharding_engines():
-                stack.enter_context(eng.gathered_for_inference())
-            return generate(model, input_ids, attention_mask, max_new_tokens, do_sample, temperature,
-                            top_p, top_k, eos_token_id, pad_token_id, generator, return_mask, use_graph, seed)
+        try:
+            with contextlib.ExitStack() as stack:
+                for eng in model.sharding_engines():
+                    stack.enter_context(eng.gathered_for_inference())
+                return generate(model, input_ids, attention_mask, max_new_tokens, do_sample, temperature,
+                                top_p, top_k, eos_token_id, pad_token_id, generator, return_mask, use_graph,
+                                seed)
+        finally:
+            # the gathered units are freed on exit: the captured graph (it reads their addresses),
+            # its KV cache and the derived decode weight copies (a second full set of layer
+            # weights) go with them, so between rollouts each rank holds only its shards
+            release_graph_cache(model)
+            ops.decode.drop_derived_weights(model)
     was_training = model.training
     model.eval()
     eos = eos_token_id if eos_token_id is not None else model.cfg.eos_token_id

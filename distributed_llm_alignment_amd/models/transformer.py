@@ -376,6 +376,7 @@ class CausalLM(nn.Module):
         if not cfg.is_moe:
             return True
         return (ops.moe.grouped_gemm_enabled() and getattr(self, "ep_size", 1) == 1
+                and all(getattr(layer.mlp, "ep", None) is None for layer in self.layers)
                 and cfg.intermediate_size % 128 == 0 and cfg.hidden_size % 16 == 0
                 and not any(getattr(layer.mlp, "fp8", False) for layer in self.layers))
 

@@ -352,6 +352,23 @@ def tiled_weight(w: torch.Tensor) -> torch.Tensor:
     return _cached(w, "_dla_tile", _wkey(w), make)
 
 
+DERIVED_ATTRS = ("_dla_fold", "_dla_fold_t", "_dla_fold_g", "_dla_tile")
+
+
+def drop_derived_weights(model) -> int:
+    """Free every derived decode weight copy (folded / tiled qkv, gate|up, o, down) held on the
+    parameters of `model`; returns the bytes released. A ZeRO-3 policy gathered for one rollout
+    (`gathered_for_inference`) calls this on exit: the copies are a second full-model-sized set of
+    layer weights, and keeping them would defeat the sharding for the rest of training."""
+    freed = 0
+    for p in model.parameters():
+        for k in DERIVED_ATTRS:
+            c = p.__dict__.pop(k, None)
+            if c is not None and isinstance(c[1], torch.Tensor):
+                freed += c[1].numel() * c[1].element_size()
+    return freed
+
+
 def refresh_folded_weights(model) -> None:
     """Bring every derived decode weight of `model` up to date (before a graph replay). A model
     whose layers are ZeRO-3 sharded right now is skipped: its weights are not resident (the

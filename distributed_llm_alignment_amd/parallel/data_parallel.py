@@ -75,13 +75,19 @@ class DataParallelEngine:
                  sp_size: int = 1,
                  overlap_optimizer: bool = os.environ.get("DLA_OVERLAP_OPT", "0") == "1",
                  grad_dtype: Optional[torch.dtype] = None, reduce_dtype: Optional[torch.dtype] = None,
-                 shape_world: int = 1):
+                 shape_world: int = 1, force_comm: Optional[bool] = None):
         """`shape_world` > 1 (debug / benchmarking, one process only): lay the engine out as rank 0
         of a ZeRO-1 group of that size without any process group -- fp32 master weights and Adam
         moments exist (and are updated) only for this rank's 1/shape_world chunk of every bucket,
         the reduce-scatter becomes a local copy of that chunk and the all-gather a copy back.
         The memory and per-rank optimizer work are those of one rank of the N-GPU job; the
-        communication is not run (tools/bench_rlhf.py --zero-shape, like bench.py --tp-shape)."""
+        communication is not run (tools/bench_rlhf.py --zero-shape, like bench.py --tp-shape).
+
+        `force_comm` (default: the process group was created with `force_pg`, or env
+        DLA_FORCE_COMM=1) with a ONE-rank group: run the multi-rank code path anyway -- ZeRO-1
+        layout, grad-ready bucket hooks, async reduce-scatters on RCCL's stream during backward,
+        the shard AdamW and the overlapped all-gathers -- so every line the N-GPU job runs
+        executes on one GPU (bench.py --force-pg, tests/test_force_comm_gpu.py)."""
         self.module = module
         # sequence parallel (parallel.sequence): `group` is DP x SP and the sp ranks of a replica
         # hold partial (token-slice) gradients of one replicated loss -> sum over SP, mean over DP
@@ -109,7 +115,13 @@ class DataParallelEngine:
                 raise ValueError("shape_world is a single-process mode (no data-parallel group)")
             self.world, self.rank = int(shape_world), 0
         self.group = group
-        self.zero = (1 if self.world > 1 else 0) if zero_stage is None else (zero_stage if self.world > 1 else 0)
+        if force_comm is None:
+            force_comm = self.dist.forced or os.environ.get("DLA_FORCE_COMM", "0") == "1"
+        # a one-rank group driven like an N-rank one (needs an initialised process group)
+        self.force_comm = bool(force_comm) and not self.shape_only and dist.is_available() \
+            and dist.is_initialized()
+        multi = self.world > 1 or self.force_comm
+        self.zero = (1 if multi else 0) if zero_stage is None else (zero_stage if multi else 0)
         self.lr, self.betas, self.eps, self.wd = lr, tuple(betas), eps, weight_decay
         self.max_grad_norm = max_grad_norm
         self.step_count = 0
@@ -117,6 +129,8 @@ class DataParallelEngine:
         self._handles = []
         self._launched = 0
         self._seen = set()
+        self._pass_armed = False  # an end-of-backward callback is queued for this sync pass
+        self._pass_launched = False  # every bucket of the accumulated grads is in flight
 
         params = [p for p in module.parameters() if p.requires_grad]
         if not params:
@@ -135,7 +149,7 @@ class DataParallelEngine:
         # expert-parallel weights (parallel.expert) are reduced over the group of ranks holding
         # the SAME experts; dense weights over the data-parallel group
         self.expert_group = expert_group
-        if expert_group is not None and self.dist.initialized:
+        if expert_group is not None and (self.dist.initialized or self.force_comm):
             ew, er = dist.get_world_size(expert_group), dist.get_rank(expert_group)
         else:
             ew, er = 1, 0
@@ -166,7 +180,8 @@ class DataParallelEngine:
         self.numel = cur.end
         self.has_experts = any(b.expert for b in self.buckets)
         # communication needed at all? (ZeRO with a 1-rank expert group still copies shards)
-        self._comm = self.world > 1 and not self.shape_only
+        self._comm = multi and not self.shape_only
+        self.comm_ops = 0  # collectives issued by this engine (tests check the comm path ran)
         # ---- flat storage (params re-pointed into it)
         self.param_buf = torch.zeros(self.numel, dtype=self.dtype, device=self.device)
         self.grad_buf = torch.zeros(self.numel, dtype=self.grad_dtype, device=self.device)
@@ -316,6 +331,8 @@ class DataParallelEngine:
         # its AccumulateGrad node (which still runs with an undefined grad) -> count once
         if id(p) in self._seen:
             return
+        if not self._pass_armed:
+            self._begin_sync_pass()
         self._seen.add(id(p))
         bi = self._bucket_of[id(p)]
         self._ready[bi] += 1
@@ -325,13 +342,38 @@ class DataParallelEngine:
             self._launch(self._launched)
             self._launched += 1
 
+    def _begin_sync_pass(self):
+        """First gradient of a synchronising backward pass: queue `_end_sync_pass` for the end of
+        this pass. A second sync pass before step() (backward called twice without no_sync)
+        re-launches every bucket: ZeRO-1's reduce-scatter reads the locally accumulated buffer
+        and overwrites the shard (in order on RCCL's stream), so the sum over both passes lands;
+        ZeRO-0's in-place all-reduce would sum the first pass's already-summed values again, so
+        that case is refused."""
+        if self._pass_launched and not self.zero:
+            raise RuntimeError("a second synchronising backward before step() under ZeRO-0: wrap the "
+                               "accumulation micro-batches in engine.no_sync()")
+        self._pass_armed = True
+        torch.autograd.Variable._execution_engine.queue_callback(self._end_sync_pass)
+
+    def _end_sync_pass(self):
+        # buckets whose params got no gradient this pass (unused params), in bucket order
+        while self._launched < len(self.buckets):
+            self._launch(self._launched)
+            self._launched += 1
+        self._launched = 0
+        self._ready = [0] * len(self.buckets)
+        self._seen = set()
+        self._pass_armed = False
+        self._pass_launched = True
+
     def _launch(self, bi: int):
         b = self.buckets[bi]
         g = self.grad_buf[b.start:b.end]
-        if b.world == 1:  # expert bucket whose experts live on this rank only
+        if b.world == 1 and not self.force_comm:  # expert bucket whose experts live here only
             if self.zero:
                 self.grad_shard[b.shard_off:b.shard_off + b.size].copy_(g)
             return
+        self.comm_ops += 1
         if self.reduce_dtype != self.grad_dtype:
             # reduce in the (narrower) communication dtype: round the accumulated bucket once
             gc = g.to(self.reduce_dtype)
@@ -358,9 +400,10 @@ class DataParallelEngine:
                 c = b.size // b.world
                 self.grad_shard[b.shard_off:b.shard_off + c].copy_(self._chunk(self.grad_buf, b))
         if self._comm:
-            while self._launched < len(self.buckets):
-                self._launch(self._launched)
-                self._launched += 1
+            if not self._pass_launched:  # no synchronising backward since the last step
+                while self._launched < len(self.buckets):
+                    self._launch(self._launched)
+                    self._launched += 1
             self.comm_timer.begin()
             for h, post in self._handles:
                 h.wait()
@@ -371,6 +414,7 @@ class DataParallelEngine:
         self._launched = 0
         self._ready = [0] * len(self.buckets)
         self._seen = set()
+        self._pass_launched = False
 
     # ------------------------------------------------------------------------ step
     @property
@@ -432,11 +476,12 @@ class DataParallelEngine:
             for bi in reversed(range(len(self.buckets))):  # forward order
                 b = self.buckets[bi]
                 c = b.size // b.world
-                if b.world == 1:
+                if b.world == 1 and not self.force_comm:
                     self.param_buf[b.start:b.end].copy_(self.param_shard[b.shard_off:b.shard_off + c])
                 elif self.shape_only:  # the all-gather's local part
                     self._chunk(self.param_buf, b).copy_(self.param_shard[b.shard_off:b.shard_off + c])
                 else:
+                    self.comm_ops += 1
                     h = dist.all_gather_into_tensor(self.param_buf[b.start:b.end],
                                                     self.param_shard[b.shard_off:b.shard_off + c],
                                                     group=b.group, async_op=self.overlap_param_gather)

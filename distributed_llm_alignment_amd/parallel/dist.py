@@ -24,6 +24,9 @@ class DistState:
     local_rank: int = 0
     device: torch.device = torch.device("cpu")
     backend: Optional[str] = None
+    # a ONE-rank process group that the engines drive like a real one (force_pg): every bucket
+    # hook, reduce-scatter, all-gather and all-to-all is issued on the communicator
+    forced: bool = False
 
     @property
     def is_main(self) -> bool:
@@ -31,19 +34,28 @@ class DistState:
 
     @property
     def initialized(self) -> bool:
-        return self.world_size > 1 and dist.is_available() and dist.is_initialized()
+        return (self.world_size > 1 or self.forced) and dist.is_available() and dist.is_initialized()
 
 
 _STATE = DistState()
 
 
 def init_distributed(backend: Optional[str] = None, timeout_s: int = 1800,
-                     device: Optional[str] = None) -> DistState:
-    """Initialise (idempotent). backend defaults to nccl(=RCCL) on GPU, gloo on CPU."""
+                     device: Optional[str] = None, force_pg: Optional[bool] = None) -> DistState:
+    """Initialise (idempotent). backend defaults to nccl(=RCCL) on GPU, gloo on CPU.
+
+    `force_pg` (default: env DLA_FORCE_PG=1) with a single process: create a real 1-rank
+    process group anyway and mark the state `forced`, so the communication engines run their
+    collective code paths (hooks, async works, RCCL's stream and events) on one GPU -- the same
+    code the N-GPU job runs, exercised where there is only one device (bench.py --force-pg,
+    tests/test_force_comm_gpu.py)."""
     global _STATE
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if force_pg is None:
+        force_pg = os.environ.get("DLA_FORCE_PG", "0") == "1"
+    forced = bool(force_pg) and world == 1
     use_gpu = torch.cuda.is_available() and device != "cpu"
     if use_gpu:
         n = torch.cuda.device_count()
@@ -56,16 +68,23 @@ def init_distributed(backend: Optional[str] = None, timeout_s: int = 1800,
     # blocking the job forever; DLA_COLLECTIVE_TIMEOUT_S overrides the timeout
     os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
     timeout_s = int(os.environ.get("DLA_COLLECTIVE_TIMEOUT_S", timeout_s))
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or forced) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if forced and "MASTER_PORT" not in os.environ:
+            import socket
+
+            with socket.socket() as s:  # a private rendezvous port for the one-rank group
+                s.bind(("127.0.0.1", 0))
+                os.environ["MASTER_PORT"] = str(s.getsockname()[1])
         os.environ.setdefault("MASTER_PORT", "29500")
         kwargs = dict(backend=be, rank=rank, world_size=world,
                       timeout=datetime.timedelta(seconds=timeout_s))
         if be == "nccl":
             kwargs["device_id"] = dev
         dist.init_process_group(**kwargs)
+    forced = forced and dist.is_initialized()
     _STATE = DistState(rank=rank, world_size=world, local_rank=local, device=dev,
-                       backend=be if world > 1 else None)
+                       backend=be if (world > 1 or forced) else None, forced=forced)
     return _STATE
 
 

@@ -349,10 +349,12 @@ class ExpertParallel:
 
 @torch.no_grad()
 def apply_expert_parallel(model, mesh, capacity_factor: float = 2.0, chunks: int = 2,
-                          shape_ep: int = 1):
+                          shape_ep: int = 1, force: bool = False):
     """Keep this rank's E/ep experts of every MoE layer and attach the all-to-all router
     (`capacity_factor` 0: exact dropless dispatch with one host read per layer). `shape_ep` > 1
-    with `mesh=None`: the one-process shape mode of ExpertParallel (bench.py --ep-shape)."""
+    with `mesh=None`: the one-process shape mode of ExpertParallel (bench.py --ep-shape).
+    `force`: attach the router even for a ONE-rank `mesh.ep_group` (init_distributed(force_pg)):
+    every all-to-all of the dispatch then runs on the communicator, on one GPU."""
     base = getattr(model, "backbone", model)
     cfg = base.cfg
     if shape_ep > 1:
@@ -371,7 +373,7 @@ def apply_expert_parallel(model, mesh, capacity_factor: float = 2.0, chunks: int
             m.ep = ep
         base.ep_size = ep.ep
         return model
-    if mesh.ep <= 1 or not cfg.is_moe:
+    if (mesh.ep <= 1 and not (force and mesh.ep_group is not None)) or not cfg.is_moe:
         return model
     ep = ExpertParallel(mesh.ep_group, cfg.num_experts, capacity_factor=capacity_factor, chunks=chunks)
     lo, hi = ep.rank * ep.El, (ep.rank + 1) * ep.El

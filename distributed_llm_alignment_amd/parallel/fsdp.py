@@ -32,6 +32,7 @@ layout as unsharded training.
 from __future__ import annotations
 
 import contextlib
+import os
 from typing import Dict, List, Optional
 
 import torch
@@ -116,15 +117,23 @@ class _ShardedBase:
     trainable = False
 
     def _init_sharding(self, module: nn.Module, group, params: List[nn.Parameter], prefetch: bool,
-                       dist_st: Optional[DistState], single: bool = False, min_num_params: int = 0):
+                       dist_st: Optional[DistState], single: bool = False, min_num_params: int = 0,
+                       force_comm: Optional[bool] = None):
         self.module = module
         self.dist = dist_st or dist_state()
         self.group = group
         if self.dist.initialized and not single:
-            self.world = dist.get_world_size(group) if group is not None else self.dist.world_size
-            self.rank = dist.get_rank(group) if group is not None else self.dist.rank
+            self.world = dist.get_world_size(group) if group is not None else dist.get_world_size()
+            self.rank = dist.get_rank(group) if group is not None else dist.get_rank()
         else:
             self.world, self.rank = 1, 0
+        if force_comm is None:
+            force_comm = self.dist.forced or os.environ.get("DLA_FORCE_COMM", "0") == "1"
+        # `_comm`: gathers / reduce-scatters go through the communicator. A one-rank group with
+        # force_comm runs them too (the N-GPU code path on one GPU, tests/test_force_comm_gpu.py)
+        self._comm = self.world > 1 or (bool(force_comm) and not single and dist.is_available()
+                                         and dist.is_initialized())
+        self.comm_ops = 0  # collectives issued (tests check that the comm path ran)
         self.prefetch = prefetch
         self.dtype = params[0].dtype
         # meta parameters (models/materialize.py): values are produced unit by unit below, on
@@ -215,7 +224,8 @@ class _ShardedBase:
         _alloc(u.full)
         src = self.param_shard[u.shard_off:u.shard_off + u.chunk]
         with torch.autograd._unsafe_preserve_version_counter(u.full):
-            if self.world > 1:
+            if self._comm:
+                self.comm_ops += 1
                 h = dist.all_gather_into_tensor(u.full, src, group=self.group, async_op=True)
             else:
                 u.full.copy_(src)
@@ -293,9 +303,11 @@ class ShardedInference(_ShardedBase):
     each layer gathered just in time for its forward."""
 
     def __init__(self, module: nn.Module, group=None, prefetch: bool = True,
-                 dist_st: Optional[DistState] = None, min_num_params: int = 0):
+                 dist_st: Optional[DistState] = None, min_num_params: int = 0,
+                 force_comm: Optional[bool] = None):
         params = list(module.parameters())
-        self._init_sharding(module, group, params, prefetch, dist_st, min_num_params=min_num_params)
+        self._init_sharding(module, group, params, prefetch, dist_st, min_num_params=min_num_params,
+                            force_comm=force_comm)
         module._dla_fsdp = self
 
     @contextlib.contextmanager
@@ -324,7 +336,7 @@ class FullyShardedEngine(_ShardedBase):
                  weight_decay: float = 0.0, max_grad_norm: float = 1.0, master_weights: bool = True,
                  dist_st: Optional[DistState] = None, group=None, tp_group=None, prefetch: bool = True,
                  min_num_params: int = 0, cpu_offload: bool = False,
-                 grad_dtype: Optional[torch.dtype] = None, **_unused):
+                 grad_dtype: Optional[torch.dtype] = None, force_comm: Optional[bool] = None, **_unused):
         if cpu_offload:
             raise ValueError("FSDP parameter CPU offload is not supported: sharded weights, fp32 "
                              "master and moments stay in HBM (288 GB per MI355X); set "
@@ -346,12 +358,13 @@ class FullyShardedEngine(_ShardedBase):
             raise ValueError("pass the data-parallel group (mesh.dp_group) when tp < world")
         # TP spanning the whole world: dp = 1, nothing to shard over (kept for uniformity)
         self._init_sharding(module, group, params, prefetch, st, single=group is None and self.tp_size > 1,
-                            min_num_params=min_num_params)
+                            min_num_params=min_num_params, force_comm=force_comm)
         self.zero = 3
         self.lr, self.betas, self.eps, self.wd = lr, tuple(betas), eps, weight_decay
         self.max_grad_norm = max_grad_norm
         self.step_count = 0
         self.params = [p for p in module.parameters() if p.requires_grad]  # (meta ones replaced)
+        self._cb_armed = False
         n = self.shard_numel
         # micro-batch grads are reduce-scattered per unit in the param dtype and accumulated here:
         # fp32 (grad_dtype) keeps 16-256 micro-batch accumulations exact to fp32 rounding
@@ -386,9 +399,26 @@ class FullyShardedEngine(_ShardedBase):
         module._dla_fsdp = self
 
     # ------------------------------------------------------------------ backward
+    def _arm_post_backward(self):
+        """Queue `_post_backward` to run when the current backward pass ends (once per pass)."""
+        if not self._cb_armed:
+            self._cb_armed = True
+            torch.autograd.Variable._execution_engine.queue_callback(self._post_backward)
+
+    def _post_backward(self):
+        """End of one backward pass (one micro-batch): reduce-scatter the units whose grads are
+        complete but not yet launched (the root), drain every pending reduce-scatter into the
+        grad shard and reset the per-pass state, so the next micro-batch's backward re-arms every
+        unit. Without this, a second micro-batch before step() found every parameter already
+        `seen` and every unit `reduced`: its gradients were never reduced (and a unit buffer still
+        pending from the first pass was zeroed under it)."""
+        self._cb_armed = False
+        self.finish_grad_sync()
+
     def _pre_backward(self, u: _Unit):
         if u.in_backward:
             return
+        self._arm_post_backward()
         u.in_backward = True
         self._gather(u)
         if not u.is_root:
@@ -400,6 +430,7 @@ class FullyShardedEngine(_ShardedBase):
     def _on_grad(self, p: nn.Parameter):
         if id(p) in self._seen:  # GEMM-epilogue + AccumulateGrad report the same grad
             return
+        self._arm_post_backward()
         self._seen.add(id(p))
         u = self.units[self.unit_of[id(p)]]
         u.ready += 1
@@ -413,7 +444,8 @@ class FullyShardedEngine(_ShardedBase):
         if not u.is_root and u.gfull.untyped_storage().size() == 0:  # unit saw no backward
             _alloc(u.gfull)
             u.gfull.zero_()
-        if self.world > 1:
+        if self._comm:
+            self.comm_ops += 1
             tmp = torch.empty(u.chunk, dtype=self.dtype, device=self.device)
             h = dist.reduce_scatter_tensor(tmp, u.gfull, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         else:
@@ -435,15 +467,18 @@ class FullyShardedEngine(_ShardedBase):
         else:
             _free(u.gfull)
 
-    def finish_grad_sync(self):
+    def finish_grad_sync(self, timed: bool = True):
         # identical order on every rank: layer units as they completed, then the rest by index
-        for u in sorted(self.units, key=lambda x: -x.idx):
-            if not u.reduced and (u.ready > 0 or u.in_backward or u.is_root):
-                self._reduce(u)
-        self.comm_timer.begin()
+        if self._seen or any(u.in_backward for u in self.units):
+            for u in sorted(self.units, key=lambda x: -x.idx):
+                if not u.reduced and (u.ready > 0 or u.in_backward or u.is_root):
+                    self._reduce(u)
+        if timed:
+            self.comm_timer.begin()
         while self._pending:
             self._drain_one()
-        self.comm_timer.end()
+        if timed:
+            self.comm_timer.end()
         self._seen = set()
         for u in self.units:
             u.ready = 0
@@ -463,7 +498,7 @@ class FullyShardedEngine(_ShardedBase):
         if self._repl_ranges:
             rep = sum(self.grad_shard[a:e].float().pow(2).sum() for a, e in self._repl_ranges)
             self._sumsq -= (1.0 - 1.0 / self.tp_size) * rep
-        if self.world > 1:
+        if self._comm:
             dist.all_reduce(self._sumsq, op=dist.ReduceOp.SUM, group=self.group)
         if self.tp_size > 1:
             dist.all_reduce(self._sumsq, op=dist.ReduceOp.SUM, group=self.tp_group)
@@ -545,7 +580,7 @@ class FullyShardedEngine(_ShardedBase):
     def _gather_unit(self, shard: torch.Tensor, u: _Unit) -> torch.Tensor:
         out = torch.empty(u.numel, dtype=shard.dtype, device=shard.device)
         src = shard[u.shard_off:u.shard_off + u.chunk].contiguous()
-        if self.world > 1:
+        if self._comm:
             dist.all_gather_into_tensor(out, src, group=self.group)
         else:
             out.copy_(src)

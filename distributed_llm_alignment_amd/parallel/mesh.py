@@ -90,6 +90,10 @@ def build_mesh(tp: int = 1, ep: int = 1, sp: int = 1) -> Mesh:
     mesh = Mesh(world=world, rank=rank, tp=tp, dp=dp, ep=ep, tp_rank=tp_rank, dp_rank=dp_rank,
                 ep_rank=dp_rank % ep)
     if world == 1:
+        if st.forced:  # one-rank process group (init_distributed(force_pg=True)): every group
+            # is the one-rank WORLD group, so the engines issue their collectives on RCCL
+            w = dist.group.WORLD
+            mesh.world_group = mesh.tp_group = mesh.dp_group = mesh.ep_group = mesh.edp_group = w
         _MESH = mesh
         return mesh
     mesh.world_group = dist.group.WORLD

@@ -140,10 +140,11 @@ class SequenceParallel:
         return a.permute(1, 2, 0, 3).reshape(B, Tl, Hq * D)
 
 
-def apply_sequence_parallel(model, group) -> Optional[SequenceParallel]:
+def apply_sequence_parallel(model, group, force: bool = False) -> Optional[SequenceParallel]:
     """Attach Ulysses SP over `group` to a CausalLM (or a wrapper with `.backbone`). Weights are
-    unchanged (replicated on the SP ranks); returns the handle (None for a 1-rank group)."""
-    if group is None or dist.get_world_size(group) == 1:
+    unchanged (replicated on the SP ranks); returns the handle (None for a 1-rank group unless
+    `force`: then the head/sequence all-to-alls run on the one-rank communicator)."""
+    if group is None or (dist.get_world_size(group) == 1 and not force):
         return None
     base = getattr(model, "backbone", model)
     sp = SequenceParallel(group)

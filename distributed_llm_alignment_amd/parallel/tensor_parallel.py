@@ -575,15 +575,17 @@ def _tp_specs(cfg, tp: int):
 
 @torch.no_grad()
 def apply_tensor_parallel(model, group, tp_rank: Optional[int] = None, tp_size: Optional[int] = None,
-                          sequence_parallel: bool = False):
+                          sequence_parallel: bool = False, force: bool = False):
     """Shard a CausalLM (or RewardModel backbone) in place for this TP rank; `sequence_parallel`
     additionally shards the residual stream over tokens (Megatron-SP: reduce-scatter / all-gather
-    instead of all-reduce)."""
+    instead of all-reduce). `force` with a ONE-rank group: install the TP layers anyway (identity
+    shards), so the column / row-parallel GEMMs, the SP gather-linear / reduce-scatter pipeline and
+    the vocab-parallel log-prob issue their collectives on the communicator, on one GPU."""
     base = getattr(model, "backbone", model)
     cfg = base.cfg
     tp = tp_size or dist.get_world_size(group)
     r = dist.get_rank(group) if tp_rank is None else tp_rank
-    if tp == 1:
+    if tp == 1 and not (force and group is not None):
         return model
     if cfg.is_moe:
         raise NotImplementedError("MoE layers use expert parallelism (parallel.expert), not TP")

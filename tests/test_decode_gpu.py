@@ -626,7 +626,16 @@ def test_fsdp_sharded_policy_generation_matches_unsharded(monkeypatch):
                         generator=torch.Generator(device=DEV).manual_seed(3))
     clear_graph_cache()
     a = generate(a_m, ids, max_new_tokens=10, do_sample=False, eos_token_id=-1, use_graph=False)
+    torch.cuda.synchronize()
+    mem0 = torch.cuda.memory_allocated(DEV)
     b = generate(b_m, ids, max_new_tokens=10, do_sample=False, eos_token_id=-1)
+    torch.cuda.synchronize()
+    # the rollout's gathered units, captured graph, KV cache and derived decode weight copies are
+    # all released: the sharded policy costs its shards again, not a second full model
+    mem1 = torch.cuda.memory_allocated(DEV)
+    layer_bytes = sum(p.numel() * p.element_size() for p in a_m.layers.parameters())
+    assert mem1 - mem0 < 0.1 * layer_bytes, (mem0, mem1, layer_bytes)
+    assert not any(k in p.__dict__ for p in b_m.parameters() for k in ops.decode.DERIVED_ATTRS)
     clear_graph_cache()
     assert torch.equal(a, b)
     assert b_m.layers_sharded() and not any(u.resident for u in eng.units if not u.is_root)
