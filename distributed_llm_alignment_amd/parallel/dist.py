@@ -81,11 +81,42 @@ def init_distributed(backend: Optional[str] = None, timeout_s: int = 1800,
                       timeout=datetime.timedelta(seconds=timeout_s))
         if be == "nccl":
             kwargs["device_id"] = dev
+            opts = comm_pg_options()
+            if opts is not None:
+                kwargs["pg_options"] = opts
         dist.init_process_group(**kwargs)
     forced = forced and dist.is_initialized()
     _STATE = DistState(rank=rank, world_size=world, local_rank=local, device=dev,
                        backend=be if (world > 1 or forced) else None, forced=forced)
     return _STATE
+
+
+# RCCL's internal streams at HIGH priority. HIP maps streams round-robin onto a few hardware queues
+# per process (GPU_MAX_HW_QUEUES, 4 by default) and one hardware queue runs its kernels in order:
+# a rocprofv3 trace of the ZeRO-1 bench on a forced one-rank group showed RCCL's stream on the SAME
+# hardware queue as torch's compute stream, its bucket kernels 0 % concurrent with the backward
+# (profiles/r5_force_pg_streams.md). A high-priority stream gets its own (priority) queue, so the
+# gradient collectives really run beside the backward GEMMs. DLA_RCCL_HIGH_PRIORITY=0 keeps torch's
+# default (normal-priority pool stream).
+RCCL_HIGH_PRIORITY = os.environ.get("DLA_RCCL_HIGH_PRIORITY", "1") != "0"
+
+
+def comm_pg_options():
+    """ProcessGroupNCCL options for every RCCL group this framework creates (world + sub-groups)."""
+    if not RCCL_HIGH_PRIORITY or not hasattr(dist, "ProcessGroupNCCL"):
+        return None
+    opts = dist.ProcessGroupNCCL.Options()
+    opts.is_high_priority_stream = True
+    return opts
+
+
+def new_group(ranks, **kw):
+    """dist.new_group with the framework's RCCL options (high-priority comm streams)."""
+    if _STATE.backend == "nccl" and "pg_options" not in kw:
+        opts = comm_pg_options()
+        if opts is not None:
+            kw["pg_options"] = opts
+    return dist.new_group(ranks, **kw)
 
 
 def state() -> DistState:

@@ -19,7 +19,7 @@ from typing import Optional
 
 import torch.distributed as dist
 
-from .dist import state as dist_state
+from .dist import new_group, state as dist_state
 
 
 @dataclass
@@ -73,12 +73,12 @@ def build_mesh(tp: int = 1, ep: int = 1, sp: int = 1) -> Mesh:
         mesh.dpsp_group = dist.group.WORLD
         for d in range(dp):  # SP groups: contiguous blocks (one xGMI hop between any two)
             ranks = [d * sp + s for s in range(sp)]
-            g = dist.new_group(ranks)
+            g = new_group(ranks)
             if rank in ranks:
                 mesh.sp_group = g
         for s in range(sp):  # DP groups (batch replicas): same sp rank
             ranks = [d * sp + s for d in range(dp)]
-            g = dist.new_group(ranks) if dp > 1 else None
+            g = new_group(ranks) if dp > 1 else None
             if rank in ranks:
                 mesh.dp_group = g
         _MESH = mesh
@@ -99,24 +99,24 @@ def build_mesh(tp: int = 1, ep: int = 1, sp: int = 1) -> Mesh:
     mesh.world_group = dist.group.WORLD
     for d in range(dp):  # TP groups
         ranks = [d * tp + t for t in range(tp)]
-        g = dist.new_group(ranks) if tp > 1 else None
+        g = new_group(ranks) if tp > 1 else None
         if rank in ranks:
             mesh.tp_group = g
     for t in range(tp):  # DP groups
         ranks = [d * tp + t for d in range(dp)]
-        g = dist.new_group(ranks) if dp > 1 else None
+        g = new_group(ranks) if dp > 1 else None
         if rank in ranks:
             mesh.dp_group = g
     if ep > 1:
         for t in range(tp):
             for blk in range(dp // ep):  # EP groups: ep consecutive DP replicas
                 ranks = [(blk * ep + e) * tp + t for e in range(ep)]
-                g = dist.new_group(ranks)
+                g = new_group(ranks)
                 if rank in ranks:
                     mesh.ep_group = g
             for e in range(ep):  # replicas of the same expert shard
                 ranks = [(blk * ep + e) * tp + t for blk in range(dp // ep)]
-                g = dist.new_group(ranks) if len(ranks) > 1 else None
+                g = new_group(ranks) if len(ranks) > 1 else None
                 if rank in ranks:
                     mesh.edp_group = g
     _MESH = mesh
