@@ -68,12 +68,22 @@ def parse(argv=None):
                          "two streams only contend)")
     ap.add_argument("--profile-dir", default=None, help="write a torch.profiler trace of 1 step")
     ap.add_argument("--tp-shape", type=int, default=1,
-                    help="debug: time ONE tensor-parallel rank's compute at world 1 (the model's "
-                         "per-rank shard shapes, models.config.tp_shard_config; no TP collectives)")
+                    help="debug: time ONE tensor-parallel rank of a TP=N group at world 1: the full "
+                         "model built on the meta device, TP-sharded for rank 0 of a "
+                         "parallel.collectives.ShapeGroup(N) and materialised, the overlapped TP layers "
+                         "(token-chunked GEMMs, vocab-parallel log-prob) with local stand-in collectives")
+    ap.add_argument("--fsdp-shape", type=int, default=1,
+                    help="debug (with --zero 3): time ONE rank of an N-way ZeRO-3 / FSDP group at "
+                         "world 1 (1/N shards, per-unit gathers / reduce-scatters as local stand-ins); "
+                         "with --tp-shape M: one rank of an N x M (FSDP x TP) mesh")
     ap.add_argument("--ep-shape", type=int, default=1,
                     help="debug: time ONE expert-parallel rank of an N-GPU MoE job at world 1: E/N "
                          "local experts per layer, the capacity-padded sync-free dispatch with the "
                          "all-to-alls as local copies, ZeRO-1 optimizer state of one of N ranks")
+    ap.add_argument("--edp-shape", type=int, default=1,
+                    help="debug (with --ep-shape N): the job has M expert-data-parallel replicas of "
+                         "each EP group (N x M GPUs): dense ZeRO-1 state over N*M ranks, expert "
+                         "optimizer state over the M replicas")
     ap.add_argument("--sharded-init", choices=("auto", "on", "off"), default="auto",
                     help="build on the meta device and materialise only this rank's TP / FSDP "
                          "shards (auto: with --tp > 1 or --zero 3)")
@@ -84,6 +94,10 @@ def parse(argv=None):
     ap.add_argument("--layers", type=int, default=None, help="debug only: override layer count "
                     "(a reduced model is NOT the benchmark config)")
     a = ap.parse_args(argv)
+    if a.edp_shape > 1 and a.ep_shape <= 1:
+        ap.error("--edp-shape needs --ep-shape")
+    if a.fsdp_shape > 1 and a.zero != 3:
+        ap.error("--fsdp-shape needs --zero 3")
     shape = a.ep_shape > 1
     if a.micro_pairs is None:
         a.micro_pairs = 2 if shape else 4
@@ -297,23 +311,27 @@ def main(argv=None) -> int:
     world = st.world_size
     mesh = build_mesh(tp=args.tp, ep=args.ep, sp=args.sp)
     overrides = {} if args.layers is None else {"num_layers": args.layers}
-    if args.tp_shape > 1:
-        if world != 1 or args.tp != 1:
-            raise SystemExit("bench.py: --tp-shape is a one-GPU debug mode (world 1, --tp 1)")
-        cfg = get_config(f"{args.model}@tp{args.tp_shape}", **overrides)
-    else:
-        cfg = get_config(args.model, **overrides)
+    from distributed_llm_alignment_amd.parallel.collectives import ShapeGroup
+
+    shape_mode = args.tp_shape > 1 or args.fsdp_shape > 1 or args.ep_shape > 1
+    if shape_mode and (world != 1 or args.tp != 1 or args.ep != 1 or args.sp != 1 or st.forced):
+        raise SystemExit("bench.py: the --*-shape modes are one-GPU debug modes (world 1, no --tp/--ep/--sp)")
+    # one rank of a TP group / FSDP group that does not exist: ShapeGroup stand-ins
+    tp_group = ShapeGroup(args.tp_shape) if args.tp_shape > 1 else mesh.tp_group
+    fsdp_group = ShapeGroup(args.fsdp_shape) if args.fsdp_shape > 1 else mesh.dp_group
+    cfg = get_config(args.model, **overrides)
     dtype = torch.bfloat16 if dev.type == "cuda" else torch.float32
 
-    meta = args.sharded_init == "on" or (args.sharded_init == "auto" and (args.tp > 1 or args.zero == 3))
+    meta = args.sharded_init == "on" or (args.sharded_init == "auto" and (
+        args.tp > 1 or args.zero == 3 or args.tp_shape > 1))
     policy = build_model(cfg, device=dev, dtype=dtype, seed=1234, meta=meta)
     ref = build_model(cfg, device=dev, dtype=dtype, seed=1234, meta=meta)
     ref.eval()
     for p in ref.parameters():
         p.requires_grad_(False)
-    if mesh.tp > 1:
-        apply_tensor_parallel(policy, mesh.tp_group, sequence_parallel=args.tp_seq)
-        apply_tensor_parallel(ref, mesh.tp_group, sequence_parallel=args.tp_seq)
+    if mesh.tp > 1 or args.tp_shape > 1:
+        apply_tensor_parallel(policy, tp_group, sequence_parallel=args.tp_seq)
+        apply_tensor_parallel(ref, tp_group, sequence_parallel=args.tp_seq)
     if mesh.sp > 1:
         from distributed_llm_alignment_amd.parallel.sequence import apply_sequence_parallel
 
@@ -341,19 +359,21 @@ def main(argv=None) -> int:
         from distributed_llm_alignment_amd.parallel.fsdp import FullyShardedEngine, ShardedInference
 
         engine = FullyShardedEngine(policy, lr=1e-6, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01,
-                                    max_grad_norm=1.0, group=mesh.dp_group, tp_group=mesh.tp_group)
-        ShardedInference(ref, group=mesh.dp_group)  # (materialises the meta ref unit by unit)
+                                    max_grad_norm=1.0, group=fsdp_group, tp_group=tp_group)
+        ShardedInference(ref, group=fsdp_group)  # (materialises the meta ref unit by unit)
     else:
         if meta:  # this rank's TP / EP shards only, one parameter at a time
             from distributed_llm_alignment_amd.models.materialize import materialize
 
             materialize(policy, dev)
             materialize(ref, dev)
+        edp_group = (ShapeGroup(args.edp_shape) if args.edp_shape > 1
+                     else (mesh.edp_group if mesh.ep > 1 else None))
         engine = DataParallelEngine(policy, lr=1e-6, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01,
                                     max_grad_norm=1.0, zero_stage=args.zero, bucket_mb=args.bucket_mb,
-                                    group=mesh.grad_group, tp_group=mesh.tp_group,
-                                    expert_group=mesh.edp_group if mesh.ep > 1 else None,
-                                    sp_size=mesh.sp, shape_world=args.ep_shape)
+                                    group=mesh.grad_group, tp_group=tp_group,
+                                    expert_group=edp_group, sp_size=mesh.sp,
+                                    shape_world=args.ep_shape * args.edp_shape)
     policy.train()
 
     gen = torch.Generator().manual_seed(17 + mesh.dp_rank)  # TP ranks share a batch
@@ -439,7 +459,26 @@ def main(argv=None) -> int:
     # model FLOPs: policy fwd+bwd (3x) + ref fwd (1x) over 2*seq tokens per pair
     tokens_per_pair = 2 * args.seq_len
     flops_pair = 4 * cfg.flops_per_token(args.seq_len) * tokens_per_pair
-    tflops_gpu = value * flops_pair / world / 1e12
+    # a TP group of G ranks shares each micro-batch: one rank does 1/G of the replica's FLOPs
+    per_replica_gpus = max(1, args.tp_shape) * mesh.tp
+    tflops_gpu = value * flops_pair / world / per_replica_gpus / 1e12
+    shape_info = None
+    if shape_mode:
+        from distributed_llm_alignment_amd.parallel.comm_model import dpo_comm_bytes
+
+        g_tp, g_fs, g_ep, g_edp = args.tp_shape, args.fsdp_shape, args.ep_shape, args.edp_shape
+        gpus = g_tp * g_fs * g_ep * g_edp
+        replicas = gpus // g_tp
+        cb = dpo_comm_bytes(cfg, args.seq_len, args.micro_pairs, args.accum, tp=g_tp, fsdp=g_fs,
+                            ep=g_ep, edp=g_edp, ep_capacity=args.ep_capacity, tp_seq=args.tp_seq)
+        shape_info = {
+            "mesh": "x".join(f"{n}{g}" for n, g in (("fsdp", g_fs), ("tp", g_tp), ("ep", g_ep),
+                                                      ("edp", g_edp)) if g > 1),
+            "job_gpus": gpus, "data_replicas": replicas,
+            "job_pairs_per_s_if_comm_hidden": round(value * replicas, 3),
+            "peak_gib": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1) if dev.type == "cuda" else None,
+            "comm_gb_per_step_per_rank": {k: round(v / 1e9, 2) for k, v in cb.items()},
+        }
     if st.rank == 0:
         rec = {
             "metric": "preference-samples/sec (whole node), Llama-3-8B DPO at 1/2/4/8 MI355X" if cfg.name == "llama3-8b"
@@ -460,7 +499,8 @@ def main(argv=None) -> int:
             "data": "synthetic preference pairs (random token ids), random-init weights",
             "config": {
                 "model": (cfg.name if args.layers is None else f"{cfg.name}-L{args.layers}(debug)")
-                         + ("(per-TP-rank shapes, debug)" if args.tp_shape > 1 else "")
+                         + (f"(one rank of a {shape_info['mesh']} mesh, local stand-in collectives, debug)"
+                            if shape_mode and args.ep_shape <= 1 else "")
                          + (f"(one EP rank of ep{args.ep_shape}: {cfg.num_experts // args.ep_shape} "
                             "local experts/layer, a2a as local copies, debug)" if args.ep_shape > 1 else ""),
                 "global_batch": pairs_per_step,
@@ -479,6 +519,7 @@ def main(argv=None) -> int:
                 "backend": st.backend or "single-process",
                 "final_loss": round(float(state["loss"].item()), 5),
                 "comm_exposed_ms_per_step": round(exposed_ms, 2),
+                **({"shape": shape_info} if shape_info else {}),
                 "gemm_selection": "tunableop:" + gemm_mode,
                 **({"rccl": coll_bw} if coll_bw else {}),
             },

@@ -482,7 +482,8 @@ void zero_rows_from(at::Tensor& x, const at::Tensor& from) {
 }
 
 std::tuple<at::Tensor, at::Tensor> moe_combine_bwd(const at::Tensor& dout, const at::Tensor& ys,
-                                                   const at::Tensor& pos, const at::Tensor& w) {
+                                                   const at::Tensor& pos, const at::Tensor& w,
+                                                   bool permutation) {
   check_bf16(dout, "dout");
   check_bf16(ys, "ys");
   check_f32(w, "w");
@@ -495,9 +496,12 @@ std::tuple<at::Tensor, at::Tensor> moe_combine_bwd(const at::Tensor& dout, const
   check_aligned16(ys, "ys");
   check_aligned16(dout, "dout");
   c10::hip::HIPGuardMasqueradingAsCUDA g(ys.device());
-  // not a permutation (capacity buffer): rows no slot reads get a zero gradient; the appended
-  // zero row shared by the dropped slots receives racing writes, and its gradient is discarded
-  auto dys = ys.size(0) == N * k ? at::empty_like(ys) : at::zeros_like(ys);
+  // `permutation` (the caller's promise: pos maps the N*k slots one-to-one onto the rows of ys,
+  // the dropless dispatch): every row is written. Otherwise (capacity buffer, possibly with
+  // ep*C == N*k by coincidence): rows no slot reads get a zero gradient and the appended zero row
+  // shared by the dropped slots receives racing writes whose gradient is discarded
+  TORCH_CHECK(!permutation || ys.size(0) == N * k, "permutation: ys must have N*k rows");
+  auto dys = permutation ? at::empty_like(ys) : at::zeros_like(ys);
   auto dw = at::empty({N, k}, w.options());
   launch_moe_combine_bwd(cbp(dout), cbp(ys), pos.data_ptr<int>(), w.data_ptr<float>(), N, (int)H,
                          (int)k, ys.size(0), bp(dys), dw.data_ptr<float>(), cur_stream(ys));
@@ -516,7 +520,7 @@ TORCH_LIBRARY_FRAGMENT(dla, m) {
   m.def("moe_topk_bwd(Tensor topv, Tensor topi, Tensor grad, int E) -> Tensor");
   m.def("moe_dispatch(Tensor x, Tensor pos) -> Tensor");
   m.def("moe_combine(Tensor ys, Tensor pos, Tensor? w) -> Tensor");
-  m.def("moe_combine_bwd(Tensor dout, Tensor ys, Tensor pos, Tensor w) -> (Tensor, Tensor)");
+  m.def("moe_combine_bwd(Tensor dout, Tensor ys, Tensor pos, Tensor w, bool permutation=False) -> (Tensor, Tensor)");
   m.def("zero_rows_from(Tensor(a!) x, Tensor from) -> ()");
   m.def("ep_route(Tensor topi, int E, int ep, int C, Tensor(a!) dropped) -> (Tensor, Tensor, Tensor)");
   m.def("ep_expert_order(Tensor rc, int C) -> (Tensor, Tensor, Tensor)");

@@ -166,9 +166,10 @@ class MLP(nn.Module):
             if tpm.TP_OVERLAP and self.up_bias is None and self.down_bias is None:
                 # Megatron-SP MLP in chunk-major token order (per-token block): the all-gather
                 # pipelined under gate|up, the reduce-scatter behind the down GEMM chunks
-                u = tpm.sp_gather_linear(h, self.up_proj, seq, token_order=False)
+                C = tpm.tp_chunks("mlp")  # (one count for both: chunk-major rows)
+                u = tpm.sp_gather_linear(h, self.up_proj, seq, chunks=C, token_order=False)
                 m = ops.swiglu(u) if self.cfg.activation == "swiglu" else ops.gelu_new(u)
-                return tpm.sp_linear_reduce_scatter(m, self.down_proj, seq, token_order=False)
+                return tpm.sp_linear_reduce_scatter(m, self.down_proj, seq, chunks=C, token_order=False)
             h = tpm.sp_gather(h, seq)
         elif self.tp is not None:
             from ..parallel import tensor_parallel as tpm
@@ -177,11 +178,11 @@ class MLP(nn.Module):
                     and self.down_bias is None and ops.swiglu_mlp_ok(h, self.up_proj, self.down_proj)):
                 # the whole Megatron MLP as one node, collectives overlapped (ops.activations)
                 return ops.swiglu_mlp(h, self.up_proj, self.down_proj, tp_group=self.tp,
-                                      chunks=tpm.TP_CHUNKS)
+                                      chunks=tpm.tp_chunks("mlp"))
             if tpm.TP_OVERLAP:
                 u = tpm.col_parallel_linear(h, self.up_proj, self.up_bias, self.tp)
                 m = ops.swiglu(u) if self.cfg.activation == "swiglu" else ops.gelu_new(u)
-                out = tpm.row_parallel_linear(m, self.down_proj, self.tp)
+                out = tpm.row_parallel_linear(m, self.down_proj, self.tp, chunks=tpm.tp_chunks("mlp"))
                 return out + self.down_bias if self.down_bias is not None else out
             h = tpm.tp_copy(h, self.tp)
         if (self.cfg.activation == "swiglu" and self.up_bias is None and self.down_bias is None
@@ -256,7 +257,7 @@ class MoE(nn.Module):
         pos, counts = ops.moe.expert_positions(topi, self.cfg.num_experts)
         xs = ops.moe.dispatch(h2, pos)
         ys = ops.moe.experts_swiglu(xs, self.expert_up, self.expert_down, counts, fp8=self.fp8)
-        return ops.moe.combine(ys, pos, topv).view(shp)
+        return ops.moe.combine(ys, pos, topv, permutation=True).view(shp)
 
 
 class DecoderLayer(nn.Module):

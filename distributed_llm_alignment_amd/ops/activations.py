@@ -13,6 +13,7 @@ import os
 
 from . import _ext
 from .linear import accumulate_weight_grad, input_grad, uses_main_grad
+from ..parallel import collectives as coll
 
 FUSED_MLP = os.environ.get("DLA_FUSED_MLP", "1") != "0"
 
@@ -65,7 +66,7 @@ class _SwiGLUMLPFn(torch.autograd.Function):
             works = []
             for a, b in _chunk_bounds(m.shape[0], chunks):
                 torch.mm(m[a:b], w_down.t(), out=y[a:b])
-                works.append(dist.all_reduce(y[a:b], group=tp_group, async_op=True))
+                works.append(coll.all_reduce(y[a:b], group=tp_group, async_op=True))
             for w in works:
                 w.wait()
         # (weights on ctx: see ops.linear._LinearMainGradFn)
@@ -93,7 +94,7 @@ class _SwiGLUMLPFn(torch.autograd.Function):
             import torch.distributed as dist
 
             dh = dh.contiguous()
-            work = dist.all_reduce(dh, group=ctx.tp_group, async_op=True)
+            work = coll.all_reduce(dh, group=ctx.tp_group, async_op=True)
         accumulate_weight_grad(w_up, du, h2, dyt=dut)
         if work is not None:
             work.wait()

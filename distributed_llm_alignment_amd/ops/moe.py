@@ -110,15 +110,16 @@ class _DispatchFn(torch.autograd.Function):
 
 class _CombineFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, ys, pos, w):
+    def forward(ctx, ys, pos, w, permutation):
         ctx.save_for_backward(ys, pos, w)
+        ctx.permutation = permutation
         return _ext.require().moe_combine(ys, pos, w)
 
     @staticmethod
     def backward(ctx, dout):
         ys, pos, w = ctx.saved_tensors
-        dys, dw = _ext.require().moe_combine_bwd(dout.contiguous(), ys, pos, w)
-        return dys, None, dw
+        dys, dw = _ext.require().moe_combine_bwd(dout.contiguous(), ys, pos, w, ctx.permutation)
+        return dys, None, dw, None
 
 
 def dispatch(x: torch.Tensor, pos: torch.Tensor) -> torch.Tensor:
@@ -128,11 +129,14 @@ def dispatch(x: torch.Tensor, pos: torch.Tensor) -> torch.Tensor:
     return _ref_dispatch(x, pos)
 
 
-def combine(ys: torch.Tensor, pos: torch.Tensor, w: Optional[torch.Tensor]) -> torch.Tensor:
-    """out[t] = sum_j w[t, j] * ys[pos[t, j]]."""
+def combine(ys: torch.Tensor, pos: torch.Tensor, w: Optional[torch.Tensor],
+            permutation: bool = False) -> torch.Tensor:
+    """out[t] = sum_j w[t, j] * ys[pos[t, j]]. `permutation`: pos maps the N*k slots one-to-one
+    onto the rows of ys (dropless dispatch), so the backward need not zero-fill ys' gradient;
+    leave it False for capacity buffers (holes, dropped slots)."""
     if _ext.use_native(ys) and ys.dtype == torch.bfloat16:
         return _CombineFn.apply(ys.contiguous(), pos.contiguous(),
-                                w.float().contiguous() if w is not None else None)
+                                w.float().contiguous() if w is not None else None, bool(permutation))
     return _ref_combine(ys, pos, w)
 
 

@@ -42,6 +42,7 @@ import torch.nn as nn
 
 from ..optim.adamw import adamw_update, clip_coefficient, grad_sumsq
 from .dist import DistState, ExposedCommTimer, state as dist_state
+from . import collectives as coll
 
 ALIGN = 64  # elements; keeps every param view 128-byte aligned for 16-byte vector kernels
 
@@ -96,11 +97,15 @@ class DataParallelEngine:
         # tensor parallel: grads of TP-sharded params differ per TP rank; params marked
         # `_dla_tp_replicated` are identical across TP ranks (counted once in the clip norm)
         self.tp_group = tp_group
-        self.tp_size = dist.get_world_size(tp_group) if (tp_group is not None and self.dist.initialized) else 1
-        if self.dist.initialized:
+        # (a parallel.collectives.ShapeGroup stands in for N ranks inside one process)
+        self.tp_size = coll.world_size(tp_group) if (tp_group is not None and (
+            self.dist.initialized or coll.is_shape(tp_group))) else 1
+        if group is not None and coll.is_shape(group):
+            self.world, self.rank = coll.world_size(group), coll.rank(group)
+        elif self.dist.initialized:
             if group is not None:
-                self.world, self.rank = dist.get_world_size(group), dist.get_rank(group)
-            elif self.tp_size > 1:
+                self.world, self.rank = coll.world_size(group), coll.rank(group)
+            elif self.tp_size > 1 and not coll.is_shape(tp_group):
                 # TP without a DP group: only legal when TP spans the whole world (dp = 1)
                 if self.tp_size != self.dist.world_size:
                     raise ValueError("pass the data-parallel group (mesh.dp_group) when tp < world")
@@ -109,6 +114,7 @@ class DataParallelEngine:
                 self.world, self.rank = self.dist.world_size, self.dist.rank
         else:
             self.world, self.rank = 1, 0
+        self.shape_group = coll.is_shape(group)
         self.shape_only = int(shape_world) > 1
         if self.shape_only:
             if self.world != 1:
@@ -149,8 +155,9 @@ class DataParallelEngine:
         # expert-parallel weights (parallel.expert) are reduced over the group of ranks holding
         # the SAME experts; dense weights over the data-parallel group
         self.expert_group = expert_group
-        if expert_group is not None and (self.dist.initialized or self.force_comm):
-            ew, er = dist.get_world_size(expert_group), dist.get_rank(expert_group)
+        if expert_group is not None and (self.dist.initialized or self.force_comm
+                                         or coll.is_shape(expert_group)):
+            ew, er = coll.world_size(expert_group), coll.rank(expert_group)
         else:
             ew, er = 1, 0
         kinds = {False: (group, self.world, self.rank), True: (expert_group, ew, er)}
@@ -379,18 +386,18 @@ class DataParallelEngine:
             gc = g.to(self.reduce_dtype)
             if self.zero:
                 oc = torch.empty(b.size // b.world, dtype=self.reduce_dtype, device=g.device)
-                h = dist.reduce_scatter_tensor(oc, gc, op=dist.ReduceOp.SUM, group=b.group, async_op=True)
+                h = coll.reduce_scatter_tensor(oc, gc, op=dist.ReduceOp.SUM, group=b.group, async_op=True)
                 dst = self.grad_shard[b.shard_off:b.shard_off + b.size // b.world]
                 self._handles.append((h, lambda oc=oc, dst=dst: dst.copy_(oc)))
             else:
-                h = dist.all_reduce(gc, op=dist.ReduceOp.SUM, group=b.group, async_op=True)
+                h = coll.all_reduce(gc, op=dist.ReduceOp.SUM, group=b.group, async_op=True)
                 self._handles.append((h, lambda gc=gc, g=g: g.copy_(gc)))
             return
         if self.zero:
             out = self.grad_shard[b.shard_off:b.shard_off + b.size // b.world]
-            h = dist.reduce_scatter_tensor(out, g, op=dist.ReduceOp.SUM, group=b.group, async_op=True)
+            h = coll.reduce_scatter_tensor(out, g, op=dist.ReduceOp.SUM, group=b.group, async_op=True)
         else:
-            h = dist.all_reduce(g, op=dist.ReduceOp.SUM, group=b.group, async_op=True)
+            h = coll.all_reduce(g, op=dist.ReduceOp.SUM, group=b.group, async_op=True)
         self._handles.append((h, None))
 
     def finish_grad_sync(self):
@@ -419,7 +426,7 @@ class DataParallelEngine:
     # ------------------------------------------------------------------------ step
     @property
     def grad_scale(self) -> float:
-        if self.shape_only:  # local gradients, nothing summed over ranks
+        if self.shape_only or self.shape_group:  # local gradients, nothing summed over ranks
             return float(self.sp_size)
         return self.sp_size / self.world
 
@@ -447,11 +454,11 @@ class DataParallelEngine:
             else:
                 ew = self.buckets[[b.expert for b in self.buckets].index(True)].world
                 self._sumsq = dense / self.world + self._esumsq / ew
-            dist.all_reduce(self._sumsq, op=dist.ReduceOp.SUM, group=self.group)
+            coll.all_reduce(self._sumsq, op=dist.ReduceOp.SUM, group=self.group)
         elif self.zero and self._comm:
-            dist.all_reduce(self._sumsq, op=dist.ReduceOp.SUM, group=self.group)
+            coll.all_reduce(self._sumsq, op=dist.ReduceOp.SUM, group=self.group)
         if self.tp_size > 1:
-            dist.all_reduce(self._sumsq, op=dist.ReduceOp.SUM, group=self.tp_group)
+            coll.all_reduce(self._sumsq, op=dist.ReduceOp.SUM, group=self.tp_group)
         sumsq = self._sumsq * (gs * gs)
         norm, coef = clip_coefficient(sumsq, self.max_grad_norm if self.max_grad_norm else 0.0)
         self.last_grad_norm = norm
@@ -482,7 +489,7 @@ class DataParallelEngine:
                     self._chunk(self.param_buf, b).copy_(self.param_shard[b.shard_off:b.shard_off + c])
                 else:
                     self.comm_ops += 1
-                    h = dist.all_gather_into_tensor(self.param_buf[b.start:b.end],
+                    h = coll.all_gather_into_tensor(self.param_buf[b.start:b.end],
                                                     self.param_shard[b.shard_off:b.shard_off + c],
                                                     group=b.group, async_op=self.overlap_param_gather)
                     if self.overlap_param_gather:
@@ -532,8 +539,8 @@ class DataParallelEngine:
         if self.world > 1:
             for b in self.buckets:
                 if b.world > 1:
-                    gsrc = dist.get_global_rank(b.group, src) if b.group is not None else src
-                    dist.broadcast(self.param_buf[b.start:b.end], src=gsrc, group=b.group)
+                    gsrc = coll.get_global_rank(b.group, src) if b.group is not None else src
+                    coll.broadcast(self.param_buf[b.start:b.end], src=gsrc, group=b.group)
             if self.zero:
                 torch.cat([self._chunk(self.param_buf, b) for b in self.buckets], out=self.param_shard)
             if self.master is not None:
@@ -612,6 +619,6 @@ class DataParallelEngine:
             if b.world == 1:
                 full[b.start:b.end].copy_(shard[b.shard_off:b.shard_off + c])
             else:
-                dist.all_gather_into_tensor(full[b.start:b.end], shard[b.shard_off:b.shard_off + c].contiguous(),
+                coll.all_gather_into_tensor(full[b.start:b.end], shard[b.shard_off:b.shard_off + c].contiguous(),
                                             group=b.group)
         return full

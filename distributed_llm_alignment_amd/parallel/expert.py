@@ -344,7 +344,7 @@ class ExpertParallel:
         ye = ops.moe.experts_swiglu(xe, moe.expert_up, moe.expert_down, counts_local, fp8=moe.fp8)
         yr = ye.index_select(0, inv)
         ys = all_to_all(yr, send_splits, recv_splits, self.group)
-        return ops.moe.combine(ys, pos, topv)
+        return ops.moe.combine(ys, pos, topv, permutation=True)  # dropless: N*k rows, one per slot
 
 
 @torch.no_grad()

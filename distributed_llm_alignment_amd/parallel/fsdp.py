@@ -41,6 +41,7 @@ import torch.nn as nn
 
 from ..optim.adamw import adamw_update, clip_coefficient, grad_sumsq
 from .dist import DistState, ExposedCommTimer, state as dist_state
+from . import collectives as coll
 
 ALIGN = 64
 
@@ -122,9 +123,11 @@ class _ShardedBase:
         self.module = module
         self.dist = dist_st or dist_state()
         self.group = group
-        if self.dist.initialized and not single:
-            self.world = dist.get_world_size(group) if group is not None else dist.get_world_size()
-            self.rank = dist.get_rank(group) if group is not None else dist.get_rank()
+        if coll.is_shape(group) and not single:  # one rank of an N-rank group, in this process
+            self.world, self.rank = coll.world_size(group), coll.rank(group)
+        elif self.dist.initialized and not single:
+            self.world = coll.world_size(group) if group is not None else coll.world_size()
+            self.rank = coll.rank(group) if group is not None else coll.rank()
         else:
             self.world, self.rank = 1, 0
         if force_comm is None:
@@ -226,7 +229,7 @@ class _ShardedBase:
         with torch.autograd._unsafe_preserve_version_counter(u.full):
             if self._comm:
                 self.comm_ops += 1
-                h = dist.all_gather_into_tensor(u.full, src, group=self.group, async_op=True)
+                h = coll.all_gather_into_tensor(u.full, src, group=self.group, async_op=True)
             else:
                 u.full.copy_(src)
                 h = None
@@ -353,7 +356,8 @@ class FullyShardedEngine(_ShardedBase):
                              "frozen part in ShardedInference instead")
         st = dist_st or dist_state()
         self.tp_group = tp_group
-        self.tp_size = dist.get_world_size(tp_group) if (tp_group is not None and st.initialized) else 1
+        self.tp_size = coll.world_size(tp_group) if (tp_group is not None and (
+            st.initialized or coll.is_shape(tp_group))) else 1
         if group is None and self.tp_size > 1 and self.tp_size != st.world_size:
             raise ValueError("pass the data-parallel group (mesh.dp_group) when tp < world")
         # TP spanning the whole world: dp = 1, nothing to shard over (kept for uniformity)
@@ -447,7 +451,7 @@ class FullyShardedEngine(_ShardedBase):
         if self._comm:
             self.comm_ops += 1
             tmp = torch.empty(u.chunk, dtype=self.dtype, device=self.device)
-            h = dist.reduce_scatter_tensor(tmp, u.gfull, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            h = coll.reduce_scatter_tensor(tmp, u.gfull, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         else:
             tmp, h = u.gfull, None
         self._pending.append((h, tmp, u))
@@ -492,16 +496,21 @@ class FullyShardedEngine(_ShardedBase):
         yield  # every micro-batch is reduce-scattered (full grads are never kept)
 
     # ------------------------------------------------------------------ step
+    @property
+    def grad_scale(self) -> float:
+        # a shape group's reduce-scatter copies this rank's own slot (nothing is summed)
+        return 1.0 if coll.is_shape(self.group) else 1.0 / self.world
+
     def clip_and_norm(self):
-        gs = 1.0 / self.world
+        gs = self.grad_scale
         grad_sumsq(self.grad_shard, self._sumsq, accumulate=False)
         if self._repl_ranges:
             rep = sum(self.grad_shard[a:e].float().pow(2).sum() for a, e in self._repl_ranges)
             self._sumsq -= (1.0 - 1.0 / self.tp_size) * rep
         if self._comm:
-            dist.all_reduce(self._sumsq, op=dist.ReduceOp.SUM, group=self.group)
+            coll.all_reduce(self._sumsq, op=dist.ReduceOp.SUM, group=self.group)
         if self.tp_size > 1:
-            dist.all_reduce(self._sumsq, op=dist.ReduceOp.SUM, group=self.tp_group)
+            coll.all_reduce(self._sumsq, op=dist.ReduceOp.SUM, group=self.tp_group)
         norm, coef = clip_coefficient(self._sumsq * (gs * gs), self.max_grad_norm or 0.0)
         self.last_grad_norm = norm
         return coef
@@ -514,7 +523,7 @@ class FullyShardedEngine(_ShardedBase):
         self._wt_epoch[0] += 1
         adamw_update(self.param_shard, self.master, self.grad_shard, self.exp_avg, self.exp_avg_sq,
                      lr, self.betas[0], self.betas[1], self.eps, self.wd, self.step_count,
-                     clip=coef if self.max_grad_norm else None, grad_scale=1.0 / self.world)
+                     clip=coef if self.max_grad_norm else None, grad_scale=self.grad_scale)
         root = self.units[-1]
         root.resident = False  # stale: re-gather the (resident) root from the updated shards
         self._gather(root)
@@ -550,9 +559,9 @@ class FullyShardedEngine(_ShardedBase):
     def broadcast_params(self, src: int = 0):
         if self.world > 1:
             with self.summon_full_params(writeback=True):
-                gsrc = dist.get_global_rank(self.group, src) if self.group is not None else src
+                gsrc = coll.get_global_rank(self.group, src) if self.group is not None else src
                 for u in self.units:
-                    dist.broadcast(u.full, src=gsrc, group=self.group)
+                    coll.broadcast(u.full, src=gsrc, group=self.group)
 
     @torch.no_grad()
     def sync_master_from_params(self):
@@ -581,7 +590,7 @@ class FullyShardedEngine(_ShardedBase):
         out = torch.empty(u.numel, dtype=shard.dtype, device=shard.device)
         src = shard[u.shard_off:u.shard_off + u.chunk].contiguous()
         if self._comm:
-            dist.all_gather_into_tensor(out, src, group=self.group)
+            coll.all_gather_into_tensor(out, src, group=self.group)
         else:
             out.copy_(src)
         return out

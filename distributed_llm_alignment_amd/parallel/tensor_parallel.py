@@ -33,6 +33,7 @@ import torch.distributed as dist
 import torch.nn.functional as F
 
 from ..ops import _ext
+from . import collectives as coll
 
 
 # ------------------------------------------------------------------------------ primitives
@@ -47,7 +48,7 @@ class _CopyToTP(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         g = g.contiguous()
-        dist.all_reduce(g, group=ctx.group)
+        coll.all_reduce(g, group=ctx.group)
         return g, None
 
 
@@ -57,7 +58,7 @@ class _ReduceFromTP(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, group):
         x = x.contiguous()
-        dist.all_reduce(x, group=group)
+        coll.all_reduce(x, group=group)
         return x
 
     @staticmethod
@@ -76,8 +77,8 @@ class TPSeq:
 
     def __init__(self, group):
         self.group = group
-        self.tp = dist.get_world_size(group)
-        self.rank = dist.get_rank(group)
+        self.tp = coll.world_size(group)
+        self.rank = coll.rank(group)
 
     def local(self, full: torch.Tensor) -> torch.Tensor:
         n = full.shape[0] // self.tp
@@ -92,14 +93,14 @@ class _SPGather(torch.autograd.Function):
     def forward(ctx, x, seq):
         ctx.seq = seq
         out = x.new_empty((x.shape[0] * seq.tp,) + tuple(x.shape[1:]))
-        dist.all_gather_into_tensor(out, x.contiguous(), group=seq.group)
+        coll.all_gather_into_tensor(out, x.contiguous(), group=seq.group)
         return out
 
     @staticmethod
     def backward(ctx, g):
         seq = ctx.seq
         out = g.new_empty((g.shape[0] // seq.tp,) + tuple(g.shape[1:]))
-        dist.reduce_scatter_tensor(out, g.contiguous(), group=seq.group)
+        coll.reduce_scatter_tensor(out, g.contiguous(), group=seq.group)
         return out, None
 
 
@@ -111,14 +112,14 @@ class _SPReduceScatter(torch.autograd.Function):
     def forward(ctx, x, seq):
         ctx.seq = seq
         out = x.new_empty((x.shape[0] // seq.tp,) + tuple(x.shape[1:]))
-        dist.reduce_scatter_tensor(out, x.contiguous(), group=seq.group)
+        coll.reduce_scatter_tensor(out, x.contiguous(), group=seq.group)
         return out
 
     @staticmethod
     def backward(ctx, g):
         seq = ctx.seq
         out = g.new_empty((g.shape[0] * seq.tp,) + tuple(g.shape[1:]))
-        dist.all_gather_into_tensor(out, g.contiguous(), group=seq.group)
+        coll.all_gather_into_tensor(out, g.contiguous(), group=seq.group)
         return out, None
 
 
@@ -130,7 +131,7 @@ class _SPGatherReplicatedGrad(torch.autograd.Function):
     def forward(ctx, x, seq):
         ctx.seq = seq
         out = x.new_empty((x.shape[0] * seq.tp,) + tuple(x.shape[1:]))
-        dist.all_gather_into_tensor(out, x.contiguous(), group=seq.group)
+        coll.all_gather_into_tensor(out, x.contiguous(), group=seq.group)
         return out
 
     @staticmethod
@@ -149,7 +150,7 @@ class _TPGradSum(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         g = g.contiguous().clone()
-        dist.all_reduce(g, group=ctx.group)
+        coll.all_reduce(g, group=ctx.group)
         return g, None
 
 
@@ -179,7 +180,7 @@ def _sp_gather_async(x_local: torch.Tensor, seq: TPSeq, C: int):
     out = x_local.new_empty((n * seq.tp, K))
     works = []
     for c in range(C):
-        works.append(dist.all_gather_into_tensor(out[c * seq.tp * m:(c + 1) * seq.tp * m],
+        works.append(coll.all_gather_into_tensor(out[c * seq.tp * m:(c + 1) * seq.tp * m],
                                                  x_local[c * m:(c + 1) * m].contiguous(),
                                                  group=seq.group, async_op=True))
     return out, works
@@ -248,7 +249,7 @@ class _SPGatherLinearFn(torch.autograd.Function):
                 part = dy2.new_empty((blk, xg.shape[1]))
                 _dgrad_into(dy2[c * blk:(c + 1) * blk], weight, part)
                 parts.append(part)
-                works.append(dist.reduce_scatter_tensor(dx[c * m:(c + 1) * m], part, group=seq.group,
+                works.append(coll.reduce_scatter_tensor(dx[c * m:(c + 1) * m], part, group=seq.group,
                                                         async_op=True))
         dw = _wgrad(ctx.needs_input_grad[1], weight, dy2, xg)  # overlaps the reduce-scatters
         for w in works:
@@ -273,7 +274,7 @@ class _SPLinearReduceScatterFn(torch.autograd.Function):
         for c in range(C):
             part = torch.mm(a_cm[c * blk:(c + 1) * blk], weight.t())
             parts.append(part)
-            works.append(dist.reduce_scatter_tensor(y[c * m:(c + 1) * m], part, group=seq.group,
+            works.append(coll.reduce_scatter_tensor(y[c * m:(c + 1) * m], part, group=seq.group,
                                                     async_op=True))
         for w in works:
             w.wait()
@@ -305,12 +306,12 @@ class _SPLinearReduceScatterFn(torch.autograd.Function):
 
 def sp_gather_linear(x, weight, seq: TPSeq, chunks: Optional[int] = None, token_order: bool = True):
     """Column-parallel GEMM on the SP-gathered input, gather chunk-pipelined (see above)."""
-    return _SPGatherLinearFn.apply(x, weight, seq, chunks or TP_CHUNKS, token_order)
+    return _SPGatherLinearFn.apply(x, weight, seq, chunks or tp_chunks("qkv"), token_order)
 
 
 def sp_linear_reduce_scatter(a, weight, seq: TPSeq, chunks: Optional[int] = None, token_order: bool = True):
     """Row-parallel GEMM reduce-scattered over SP, chunk-pipelined (see above)."""
-    return _SPLinearReduceScatterFn.apply(a, weight, seq, chunks or TP_CHUNKS, token_order)
+    return _SPLinearReduceScatterFn.apply(a, weight, seq, chunks or tp_chunks("o"), token_order)
 
 
 def sp_gather(x, seq: TPSeq):
@@ -349,6 +350,23 @@ def tp_reduce(x, group):
 #     collective is in flight.
 TP_OVERLAP = os.environ.get("DLA_TP_OVERLAP", "1") != "0"
 TP_CHUNKS = max(1, int(os.environ.get("DLA_TP_CHUNKS", "4")))
+# Token chunks per TP GEMM kind, instead of one global count: "qkv" (SP gather-linear), "o"
+# (row-parallel / SP reduce-scatter of the attention output) and "mlp" (gate|up AND down: in
+# the chunk-major Megatron-SP MLP both must use the same count). The 70B TP = 8 per-rank probe
+# (profiles/r4_70b_tpshape.md) prices the split: C = 2 costs qkv +27 %, o +12 %, gate|up +1 %,
+# down +4 % of the GEMM, C = 4 +68 / +45 / +25 / +29 % -- so 2 everywhere by default, each
+# hiding half of its collective. DLA_TP_CHUNKS_<KIND> overrides one kind, DLA_TP_CHUNKS all.
+TP_CHUNK_DEFAULTS = {"qkv": 2, "o": 2, "mlp": 2}
+
+
+def tp_chunks(kind: str) -> int:
+    env = os.environ.get(f"DLA_TP_CHUNKS_{kind.upper()}")
+    if env:
+        return max(1, int(env))
+    env = os.environ.get("DLA_TP_CHUNKS")
+    if env:
+        return max(1, int(env))
+    return TP_CHUNK_DEFAULTS[kind]
 
 
 def _chunk_bounds(M: int, chunks: int):
@@ -366,7 +384,7 @@ def _linear_backward(ctx, dy2, x2, weight, async_group=None):
         dx = input_grad(dy2, weight)
         if async_group is not None:
             dx = dx.contiguous()
-            work = dist.all_reduce(dx, group=async_group, async_op=True)
+            work = coll.all_reduce(dx, group=async_group, async_op=True)
     dw = None
     if ctx.needs_input_grad[1] and not accumulate_weight_grad(weight, dy2, x2):
         dw = dy2.t() @ x2
@@ -409,7 +427,7 @@ class _RowParallelLinearFn(torch.autograd.Function):
         works = []
         for a, b in _chunk_bounds(M, chunks):
             torch.mm(x2[a:b], weight.t(), out=y[a:b])
-            works.append(dist.all_reduce(y[a:b], group=group, async_op=True))
+            works.append(coll.all_reduce(y[a:b], group=group, async_op=True))
         for w in works:
             w.wait()
         ctx.save_for_backward(x)
@@ -439,14 +457,14 @@ def row_parallel_linear(x, weight, group, chunks: Optional[int] = None):
         from ..ops.linear import linear
 
         return tp_reduce(linear(x, weight, None), group)
-    return _RowParallelLinearFn.apply(x, weight, group, chunks or TP_CHUNKS)
+    return _RowParallelLinearFn.apply(x, weight, group, chunks or tp_chunks("o"))
 
 
 def tp_all_gather_last(x: torch.Tensor, group) -> torch.Tensor:
     """Concatenate per-rank shards along the last dim (inference only, e.g. full logits)."""
-    ws = dist.get_world_size(group)
+    ws = coll.world_size(group)
     parts = [torch.empty_like(x) for _ in range(ws)]
-    dist.all_gather(parts, x.contiguous(), group=group)
+    coll.all_gather(parts, x.contiguous(), group=group)
     return torch.cat(parts, dim=-1)
 
 
@@ -497,10 +515,10 @@ class _VPLogprobFn(torch.autograd.Function):
         # ONE latency-bound collective instead of three (max, sum-exp, target logit all-reduces):
         # every rank gathers all shards' (lse_r, target logit_r) and reduces them locally in a
         # fixed rank order (identical result on every rank)
-        tp = dist.get_world_size(group)
+        tp = coll.world_size(group)
         pair = torch.stack([lse_l.float(), tl_l.float()])
         allp = pair.new_empty((tp * 2,) + tuple(pair.shape[1:]))
-        dist.all_gather_into_tensor(allp, pair.contiguous(), group=group)
+        coll.all_gather_into_tensor(allp, pair.contiguous(), group=group)
         allp = allp.view((tp,) + tuple(pair.shape))
         lse = torch.logsumexp(allp[:, 0], dim=0)
         tl = allp[:, 1].sum(0)
@@ -521,7 +539,7 @@ class _VPLogprobFn(torch.autograd.Function):
 
             dh = input_grad(dlog, weight_l).contiguous()
             # in flight on RCCL's stream while the (vocab-shard) weight-gradient GEMM runs
-            work = dist.all_reduce(dh, group=ctx.group, async_op=True)
+            work = coll.all_reduce(dh, group=ctx.group, async_op=True)
         dw = None
         if ctx.needs_input_grad[1]:
             from ..ops.linear import accumulate_weight_grad
@@ -554,9 +572,9 @@ def shard_tensor(full: torch.Tensor, spec, r: int, tp: int) -> torch.Tensor:
 
 def gather_tensor(local: torch.Tensor, spec, group) -> torch.Tensor:
     dim, segs = spec
-    tp = dist.get_world_size(group)
+    tp = coll.world_size(group)
     pieces = [torch.empty_like(local) for _ in range(tp)]
-    dist.all_gather(pieces, local.contiguous(), group=group)
+    coll.all_gather(pieces, local.contiguous(), group=group)
     loc = [n // tp for n in segs]
     per_rank = [torch.split(pc, loc, dim) for pc in pieces]
     return torch.cat([per_rank[rk][i] for i in range(len(segs)) for rk in range(tp)], dim)
@@ -583,8 +601,8 @@ def apply_tensor_parallel(model, group, tp_rank: Optional[int] = None, tp_size: 
     the vocab-parallel log-prob issue their collectives on the communicator, on one GPU."""
     base = getattr(model, "backbone", model)
     cfg = base.cfg
-    tp = tp_size or dist.get_world_size(group)
-    r = dist.get_rank(group) if tp_rank is None else tp_rank
+    tp = tp_size or coll.world_size(group)
+    r = coll.rank(group) if tp_rank is None else tp_rank
     if tp == 1 and not (force and group is not None):
         return model
     if cfg.is_moe:

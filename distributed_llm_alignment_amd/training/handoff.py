@@ -116,7 +116,7 @@ class RewardHandoff:
     """Chooses and runs the hand-off once per trainer (`ppo.reward_handoff: auto|device|text`)."""
 
     def __init__(self, policy_tok, reward_tok, vocab_size: int, device, max_length: int,
-                 mode: str = "auto"):
+                 mode: str = "auto", validate_every: int = 16):
         mode = str(mode or "auto").lower()
         if mode not in ("auto", "device", "text"):
             raise ValueError(f"ppo.reward_handoff must be auto|device|text, got {mode!r}")
@@ -127,8 +127,14 @@ class RewardHandoff:
         self.ptok, self.rtok, self.max_length = policy_tok, reward_tok, int(max_length)
         from ..models.tokenizer import ByteTokenizer
 
-        # auto + BPE: validate the device ids against the text round trip on the first batch
+        # auto + BPE: validate the device ids against the text round trip on the first batch and
+        # then every `validate_every`-th batch (a later batch can hold a merge across the "\n\n"
+        # boundary or a non-canonical sample); the verdict is agreed over all ranks (MIN), so every
+        # DP rank stays on the same hand-off path
         self._validate = self.device_path and mode == "auto" and not isinstance(reward_tok, ByteTokenizer)
+        self._validate_every = max(1, int(validate_every))
+        self._calls = 0
+        self.fallback_reason = None
         if self.device_path:
             self.special = special_token_table(reward_tok, vocab_size, device)
             self.sep = separator_ids(reward_tok).to(device)
@@ -138,15 +144,35 @@ class RewardHandoff:
         if self.device_path:
             out = device_reward_inputs(ids, am, seqs, self.sep, self.special, self.pad,
                                        self.max_length, gen_mask)
-            if not self._validate:
+            due = self._validate and self._calls % self._validate_every == 0
+            self._calls += 1
+            if not due:
                 return out
-            self._validate = False
             ref = self._text(prompts, ids, seqs)
-            if self._same(out, ref):
+            if self._agree(self._same(out, ref)):
                 return out
-            self.device_path = False  # the tokenizer does not round-trip these ids: text from now on
+            # the tokenizer does not round-trip these ids (on some rank): text from now on
+            self.device_path = False
+            self.fallback_reason = f"device ids differ from the text round trip at batch {self._calls}"
+            import warnings
+
+            warnings.warn(f"reward hand-off: {self.fallback_reason}; using the text path from now on")
             return ref
         return self._text(prompts, ids, seqs)
+
+    @staticmethod
+    def _agree(ok: bool) -> bool:
+        """MIN of `ok` over every rank (identical decision everywhere); local value without a group."""
+        from ..parallel.dist import state
+
+        st = state()
+        if not st.initialized:
+            return ok
+        import torch.distributed as dist
+
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=st.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return bool(t.item())
 
     @staticmethod
     def _same(a, b) -> bool:

@@ -127,7 +127,8 @@ def main(argv=None) -> int:
     from .handoff import RewardHandoff
 
     handoff = RewardHandoff(tok, rtok, policy.model.cfg.vocab_size, ctx.device, max_len,
-                            ppo.get("reward_handoff", "auto"))
+                            ppo.get("reward_handoff", "auto"),
+                            validate_every=int(ppo.get("reward_handoff_validate_every", 16)))
     ctx.log(f"reward hand-off: {'device ids' if handoff.device_path else 'decode + re-tokenise'}")
 
     def rollout():
@@ -175,6 +176,17 @@ def main(argv=None) -> int:
     return 0
 
 
+def micro_bounds(n: int, micro: int):
+    """[start, stop) of each update micro-batch. A ragged tail (n % micro != 0) is folded into the
+    previous micro-batch instead of standing alone: a 1-rollout micro-batch's mean baseline is its
+    own reward, so its advantage (and policy gradient) would be exactly zero while it still
+    carried weight."""
+    b = [(s, min(n, s + micro)) for s in range(0, n, micro)]
+    if len(b) > 1 and b[-1][1] - b[-1][0] < micro:
+        b[-2:] = [(b[-2][0], n)]
+    return b
+
+
 def reinforce_update(policy, ref, engine, seqs, mask, scores, kl_coef: float, micro: int = 0):
     """Backward of the KL-penalised policy-gradient loss over this rank's rollouts.
 
@@ -189,12 +201,12 @@ def reinforce_update(policy, ref, engine, seqs, mask, scores, kl_coef: float, mi
         loss, m = rlhf_loss(policy, ref, seqs, mask, scores, kl_coef)
         loss.backward()
         return loss, m
-    starts = list(range(0, n, micro))
+    bounds = micro_bounds(n, micro)
     tot, kl = 0.0, 0.0
-    for i, s0 in enumerate(starts):
-        sl = slice(s0, min(n, s0 + micro))
+    for i, (s0, s1) in enumerate(bounds):
+        sl = slice(s0, s1)
         w = (sl.stop - sl.start) / n
-        ctx = engine.no_sync() if i < len(starts) - 1 else contextlib.nullcontext()
+        ctx = engine.no_sync() if i < len(bounds) - 1 else contextlib.nullcontext()
         with ctx:
             loss, m = rlhf_loss(policy, ref, seqs[sl], mask[sl], scores[sl], kl_coef)
             (loss * w).backward()

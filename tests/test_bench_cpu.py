@@ -115,3 +115,50 @@ def test_bench_records_collective_bandwidth():
     rec = _record(p.stdout)
     bw = rec["config"]["rccl"]
     assert bw["allreduce_2MB_busbw_GBps"] > 0, bw
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.parametrize("flags,mesh,gpus", [
+    (["--tp-shape", "2"], "tp2", 2),
+    (["--tp-shape", "2", "--tp-seq"], "tp2", 2),
+    (["--zero", "3", "--fsdp-shape", "2"], "fsdp2", 2),
+    (["--zero", "3", "--fsdp-shape", "2", "--tp-shape", "2"], "fsdp2xtp2", 4),
+    (["--model", "tiny-mixtral", "--ep-shape", "2", "--edp-shape", "2"], "ep2xedp2", 4),
+])
+def test_bench_shape_meshes_run_one_rank(flags, mesh, gpus):
+    """One rank of an FSDP x TP / EP x EDP mesh on one device (parallel.collectives.ShapeGroup
+    stand-ins): the step runs, the loss is finite and the record carries the mesh's per-rank
+    collective bytes (profiles/r5_70b_meshes.md)."""
+    args = ["--device", "cpu", "--model", "tiny-llama", "--steps", "1", "--warmup", "1",
+            "--seq-len", "64", "--micro-pairs", "2", "--accum", "2"]
+    if "--model" in flags:
+        i = args.index("--model")
+        del args[i:i + 2]
+    p = _run(args + flags)
+    assert p.returncode == 0, p.stderr[-3000:]
+    rec = _record(p.stdout)
+    shape = rec["config"]["shape"]
+    assert shape["mesh"] == mesh and shape["job_gpus"] == gpus
+    assert rec["config"]["final_loss"] == rec["config"]["final_loss"]  # not NaN
+    if "--tp-shape" in flags:
+        assert "tp_allreduce" in shape["comm_gb_per_step_per_rank"]
+
+
+def test_shape_group_collectives():
+    import torch
+
+    from distributed_llm_alignment_amd.parallel import collectives as coll
+
+    g = coll.ShapeGroup(4)
+    x = torch.arange(6.0)
+    out = torch.empty(24)
+    coll.all_gather_into_tensor(out, x, group=g)
+    assert torch.equal(out.view(4, 6), x.expand(4, 6))
+    rs = torch.empty(6)
+    assert coll.reduce_scatter_tensor(rs, out, group=g, async_op=True).wait()
+    assert torch.equal(rs, x)  # this rank's slot, not a sum: values stay at one rank's scale
+    y = x.clone()
+    coll.all_reduce(y, group=g)
+    assert torch.equal(y, x) and coll.world_size(g) == 4 and coll.rank(g) == 0

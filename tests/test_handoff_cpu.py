@@ -80,3 +80,37 @@ def test_handoff_mode_selection():
 
     with pytest.raises(ValueError):
         RewardHandoff(a, other, 300, "cpu", 64, "device")
+
+
+def test_auto_handoff_revalidates_and_falls_back(monkeypatch):
+    """auto mode re-checks the device ids against the text round trip every `validate_every`
+    batches (not only the first): a later mismatching batch switches to the text path."""
+    import pytest
+
+    tok = ByteTokenizer(vocab_size=300)
+    h = RewardHandoff(tok, tok, 300, "cpu", 1024, validate_every=2)
+    h._validate = True  # byte tokenizer fixture: force the BPE-style validation on
+    prompts, responses = ["Human: hi", "Q: x"], ["Sure.", "ok"]
+    ids, am, seqs, gmask = _rollouts(tok, prompts, responses, pad_to=16)
+    calls = []
+    real_same = RewardHandoff._same
+    monkeypatch.setattr(RewardHandoff, "_same",
+                        staticmethod(lambda a, b: calls.append(1) or (len(calls) < 2 and real_same(a, b))))
+    for _ in range(2):  # batch 0 validated (match), batch 1 not due
+        h(prompts, ids, am, seqs, gmask)
+        assert h.device_path
+    assert len(calls) == 1
+    with pytest.warns(UserWarning, match="text path"):
+        out = h(prompts, ids, am, seqs, gmask)  # batch 2 validated: mismatch -> text from now on
+    assert not h.device_path and h.fallback_reason and len(calls) == 2
+    want = _text_path(tok, prompts, ids, seqs, 1024)
+    assert torch.equal(out[0], want[0]) and torch.equal(out[1], want[1])
+
+
+def test_rlhf_micro_bounds_fold_ragged_tail():
+    from distributed_llm_alignment_amd.training.train_rlhf import micro_bounds
+
+    assert micro_bounds(16, 8) == [(0, 8), (8, 16)]
+    assert micro_bounds(17, 8) == [(0, 8), (8, 17)]  # a 1-rollout micro-batch has zero advantage
+    assert micro_bounds(5, 8) == [(0, 5)]
+    assert micro_bounds(20, 8) == [(0, 8), (8, 20)]

@@ -909,3 +909,33 @@ def test_attention_partial_rotary_d80_fused_bwd(case, bwd_waves):
     assert rel_err(g[..., :Hq * D], r[..., :Hq * D]) < 3e-2, "dq"
     assert rel_err(g[..., Hq * D:(Hq + Hkv) * D], r[..., Hq * D:(Hq + Hkv) * D]) < 3e-2, "dk"
     assert rel_err(g[..., (Hq + Hkv) * D:], r[..., (Hq + Hkv) * D:]) < 3e-2, "dv"
+
+
+@pytest.mark.parametrize("T", [4096, 8192])
+def test_attention_bwd_bf16_partials_long_context(T, monkeypatch):
+    """The 8-wave backward's bf16 dQ slabs / dK-dV head-split partials (DLA_ATTN_DQ_BF16,
+    DLA_ATTN_DKV_BF16, default on) round each per-key-block partial once before the fp32 sum;
+    at long context there are T/256 of them (32 at T=8192). Against an fp32 reference the bf16
+    partials must stay within a small factor of the fp32-partial path's own error."""
+    B, Hq, Hkv, D = 1, 8, 2, 128
+    g = torch.Generator(device="cuda").manual_seed(T)
+    q = torch.randn(B, T, Hq, D, device="cuda", generator=g).to(torch.bfloat16)
+    k = torch.randn(B, T, Hkv, D, device="cuda", generator=g).to(torch.bfloat16)
+    v = torch.randn(B, T, Hkv, D, device="cuda", generator=g).to(torch.bfloat16)
+    go = torch.randn(B, T, Hq, D, device="cuda", generator=g).to(torch.bfloat16)
+    qf, kf, vf = (t.float().requires_grad_() for t in (q, k, v))
+    of = ref_attention(qf, kf, vf, 1 / math.sqrt(D), True)
+    ref = torch.autograd.grad(of, [qf, kf, vf], go.float())
+    del of
+    errs = {}
+    for flag in ("0", "1"):
+        monkeypatch.setenv("DLA_ATTN_DQ_BF16", flag)
+        monkeypatch.setenv("DLA_ATTN_DKV_BF16", flag)
+        qq, kk, vv = (t.clone().requires_grad_() for t in (q, k, v))
+        o = ops.attention_core(qq, kk, vv, causal=True)
+        grads = torch.autograd.grad(o, [qq, kk, vv], go)
+        errs[flag] = [rel_err(a, b) for a, b in zip(grads, ref)]
+    for i, name in enumerate(("dq", "dk", "dv")):
+        e32, e16 = errs["0"][i], errs["1"][i]
+        assert e16 < 2e-2, (name, T, errs)
+        assert e16 <= 1.5 * e32 + 2e-3, (name, T, errs)

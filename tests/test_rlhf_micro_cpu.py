@@ -48,12 +48,11 @@ def test_micro_batched_reinforce_update_matches_per_rank_baselines():
     assert torch.allclose(loss, 0.5 * (parts[0][0] + parts[1][0]))
     assert torch.allclose(m["kl"], 0.5 * (parts[0][1] + parts[1][1]))
 
-    # uneven split (3 + 1): weights 3/4 and 1/4
+    # ragged split (3 + 1): the 1-rollout tail would have a zero advantage on its own, so it is
+    # folded into the previous micro-batch -> one micro-batch of 4 (= the full-batch loss)
     reinforce_update(pol, ref, _Eng(), seqs, mask, scores, 0.1, 3)
     g_uneven = _grads(pol)
-    for sl, w in ((slice(0, 3), 0.75), (slice(3, 4), 0.25)):
-        l, _ = rlhf_loss(pol, ref, seqs[sl], mask[sl], scores[sl], 0.1)
-        (w * l).backward()
+    rlhf_loss(pol, ref, seqs, mask, scores, 0.1)[0].backward()
     assert _close(g_uneven, _grads(pol))
 
     # micro = 0 (and micro >= batch): the full-batch loss with one baseline
