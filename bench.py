@@ -283,7 +283,7 @@ def main(argv=None) -> int:
     # a dead peer must end the run in bounded time, not after the 30 min default
     st = init_distributed(device="cpu" if args.device == "cpu" else None,
                           timeout_s=int(os.environ.get("DLA_BENCH_COLLECTIVE_TIMEOUT_S", "300")),
-                          force_pg=args.force_pg)
+                          force_pg=args.force_pg or None)
     if args.force_pg and not st.forced and st.world_size == 1:
         raise SystemExit("bench.py: --force-pg could not create the one-rank process group")
     dev = st.device

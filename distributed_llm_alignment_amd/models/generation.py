@@ -317,7 +317,7 @@ GRAPH_REUSE_MAX_BYTES = int(float(os.environ.get("DLA_GRAPH_REUSE_MAX_GB", "24")
 PROMPT_BUCKET = 64
 # KV cache storage head-major ([L, B, Hkv, T_max, D] behind the usual view; DLA_KV_HEAD_MAJOR=0 for
 # the token-major layout): B = 64 graph decode 4.984 / 4.991 vs 4.994 / 5.012 ms/token, B = 8 noise
-# (same box, round 4 end; the whole GPU tier passes on it, scripts/r4_gpu39.sh)
+# (same box, round 4 end; the whole GPU tier passes on it, tools/gpu_passes.py ab-kv-head-major)
 KV_HEAD_MAJOR = os.environ.get("DLA_KV_HEAD_MAJOR", "1") != "0"
 _GRAPH_SLOT: dict = {}  # id(model) -> (weakref(model), key, cache, decode graph)
 

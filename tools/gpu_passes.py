@@ -1,0 +1,286 @@
+#!/usr/bin/env python
+"""Named GPU passes as one table (replaces the round-4 one-off `scripts/r4_gpu*.sh` files).
+
+    python tools/gpu_passes.py --list
+    python tools/gpu_passes.py PASS [--out gpurun_out/PASS] [--dry]
+
+Run it as the `gpurun` command (`gpurun -- 'python tools/gpu_passes.py validate'`). Each pass is a
+list of steps, executed in order under their own `timeout -k 10`, stopping at the first failure
+(no retries; no GPU step after a fault, abort or time limit). A heartbeat file under the output
+directory is touched every 30 s so a long pass is never taken for a hung one. Step kinds:
+
+  pytest  a pytest selection (GPU tier flags added)
+  run     one command; its last line is echoed
+  ab      `rounds` interleaved repetitions of each arm (arms differ only by environment), the same
+          box for A and B: box-to-box clock variance exceeds most single optimisations
+  prof    `rocprofv3 --kernel-trace` of a command; the trace is summarised on the box
+          (scripts/prof_window.py, scripts/step_breakdown.py, scripts/prof_streams.py) and the
+          raw trace deleted, so only small files come back
+  pmc     one `rocprofv3 --pmc` counter pass (within the per-block slot limits), summarised by
+          scripts/pmc_summary_csv.py
+  smoke   __graft_entry__.smoke()
+
+Profiles cite `tools/gpu_passes.py <name>` as their reproduce line. This parent process never
+touches the GPU.
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import os
+import shlex
+import shutil
+import subprocess
+import sys
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FATAL = {124, 134, 137, 139, -6, -9, -11}
+
+GEN8 = "python -u tools/bench_generate.py --modes graph --new 128"
+GEN64 = GEN8 + " --batch 64 --prompt 512"
+DPO = "python -u bench.py"
+MIX_EP8 = DPO + " --model mixtral-8x7b --ep-shape 8 --micro-pairs 2 --accum 8 --ep-capacity 1.25"
+L70 = DPO + " --model llama3-70b --steps 2 --warmup 1"
+
+
+def pytest(sel, t=1000):
+    return {"kind": "pytest", "sel": sel, "timeout": t}
+
+
+def run(name, cmd, t=600, env=None):
+    return {"kind": "run", "name": name, "cmd": cmd, "timeout": t, "env": env or {}}
+
+
+def ab(name, cmd, arms, rounds=2, t=600):
+    return {"kind": "ab", "name": name, "cmd": cmd, "arms": arms, "rounds": rounds, "timeout": t}
+
+
+def prof(name, cmd, summaries, t=420, env=None):
+    return {"kind": "prof", "name": name, "cmd": cmd, "summaries": summaries, "timeout": t, "env": env or {}}
+
+
+def pmc(name, counters, cmd, kernels, t=170):
+    return {"kind": "pmc", "name": name, "counters": counters, "cmd": cmd, "kernels": kernels, "timeout": t}
+
+
+SMOKE = {"kind": "smoke", "timeout": 300}
+DPO_TABLES = [("breakdown", []), ("window", ["--window", "adamw", "--by-grid", "--top", "60"])]
+DEC_TABLE = [("window", ["--by-grid", "--top", "30", "--per", "4096"])]
+ATTN_P1 = ("SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY "
+           "SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE")
+ATTN_P2 = "SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_WAVES SQ_WAIT_INST_LDS GRBM_COUNT"
+
+PASSES = {
+    # ---- whole-tree validation (the driver's round-end tiers, then every headline number)
+    "tier": [pytest("tests -m gpu"), SMOKE, run("bench", DPO)],
+    "validate": [
+        pytest("tests -m gpu"), SMOKE, run("bench", DPO),
+        run("bench_force_pg", DPO + " --force-pg --steps 5 --warmup 2", 300),
+        run("gen8", GEN8, 300), run("gen64", GEN64, 300),
+        run("rlhf8", "python -u tools/bench_rlhf.py --batch 8", 400),
+        run("rlhf64_micro8", "python -u tools/bench_rlhf.py --batch 64 --micro 8"),
+        run("ppo_zero8", "python -u tools/bench_rlhf.py --algorithm ppo --zero-shape 8 --batch 8"),
+        run("mixtral_ep8", MIX_EP8 + " --steps 3 --warmup 2"),
+        run("mixtral_ep8_fp8", MIX_EP8 + " --fp8 --steps 3 --warmup 2"),
+    ],
+    # ---- round 5
+    "force-pg": [
+        pytest("tests/test_force_comm.py -m gpu", 400),
+        prof("force_pg", DPO + " --force-pg --steps 2 --warmup 1",
+             [("streams", ["--window", "adamw"])]),
+        ab("force_pg_ab", DPO + " --steps 5 --warmup 2", {"plain": {}, "forced": {"DLA_FORCE_PG": "1"}}, 2, 300),
+    ],
+    "meshes": [
+        run("tp8", L70 + " --tp-shape 8 --micro-pairs 2 --accum 8", 330),
+        run("fsdp2tp4", L70 + " --zero 3 --fsdp-shape 2 --tp-shape 4 --micro-pairs 2 --accum 8", 360),
+        run("fsdp8", L70 + " --zero 3 --fsdp-shape 8 --micro-pairs 1 --accum 16", 420),
+        run("mixtral_ep4edp2", MIX_EP8.replace("--ep-shape 8", "--ep-shape 4 --edp-shape 2") + " --steps 3 --warmup 1", 400),
+        run("mixtral_ep8", MIX_EP8 + " --steps 3 --warmup 1", 400),
+    ],
+    # ---- kernel tables and counters (round 4 passes 2/3/16/26/37)
+    "dpo-profile": [prof("dpo", DPO + " --steps 2 --warmup 1", DPO_TABLES)],
+    "decode-profile": [prof("dec8", GEN8, DEC_TABLE, 300), prof("dec64", GEN64, DEC_TABLE, 300)],
+    "mixtral-profile": [prof("mixtral", MIX_EP8 + " --steps 2 --warmup 1",
+                             [("breakdown", []), ("window", ["--window", "adamw", "--top", "45"])])],
+    "attn-pmc": [pmc("attn_p1", ATTN_P1, "python3 tools/attn_bench.py --iters 3",
+                     "attn_fwd attn_bwd8 attn_dq_reduce attn_dkv_reduce", 150),
+                 pmc("attn_p2", ATTN_P2, "python3 tools/attn_bench.py --iters 3",
+                     "attn_fwd attn_bwd8 attn_dq_reduce attn_dkv_reduce", 150)],
+    "decode64-pmc": [pmc("dec64", "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY "
+                         "SQ_ACTIVE_INST_ANY SQ_WAVES GRBM_GUI_ACTIVE FETCH_SIZE",
+                         "python3 tools/bench_generate.py --modes eager --new 4 --batch 64 --prompt 512",
+                         "m64_gemm m64_reduce decode_attn_loop")],
+    "tp-chunks": [run("tp_chunk_probe", "python -u tools/tp_chunk_probe.py", 300)],
+    # ---- round-4 A/Bs whose knobs are still in the tree (results in README "Tried, measured")
+    "ab-dq-bf16": [ab("dq_bf16", DPO + " --steps 4 --warmup 2", {"on": {"DLA_ATTN_DQ_BF16": "1"},
+                                                                 "off": {"DLA_ATTN_DQ_BF16": "0"}}, 1, 400)],
+    "ab-qkv-attn": [pytest("tests/test_decode_gpu.py -m gpu -k 'fused_qkv or slab or fsdp'", 300),
+                    ab("qkv_attn", GEN8, {"fused": {"DLA_DECODE_QKV_ATTN": "1"},
+                                          "split": {"DLA_DECODE_QKV_ATTN": "0"}}, 2, 300),
+                    ab("slab_attn", GEN64, {"on": {"DLA_DECODE_SLAB_ATTN": "1"},
+                                            "off": {"DLA_DECODE_SLAB_ATTN": "0"}}, 1, 300)],
+    "ab-tn-wgrad-max": [ab("tn_max", DPO + " --steps 6 --warmup 2",
+                           {"inf": {"DLA_TN_WGRAD_MAX": "4611686018427387904"},
+                            "3e8": {"DLA_TN_WGRAD_MAX": "300000000"}}, 2, 400)],
+    "ab-tn-wgrad-min": [ab("tn_min", MIX_EP8 + " --steps 3 --warmup 2",
+                           {"1Mi": {"DLA_TN_WGRAD_MIN": "1048576"}, "0": {"DLA_TN_WGRAD_MIN": "0"}})],
+    "ab-micro-shape": [ab("micro_4x4", DPO + " --micro-pairs 4 --accum 4 --steps 6 --warmup 2", {"4x4": {}}, 2, 400),
+                       ab("micro_8x2", DPO + " --micro-pairs 8 --accum 2 --steps 6 --warmup 2", {"8x2": {}}, 2, 400)],
+    "ab-mixtral-single-lib": [pytest("tests/test_moe_gpu.py -m gpu", 300),
+                              ab("single_lib", MIX_EP8 + " --steps 3 --warmup 2",
+                                 {"lib+route": {"DLA_MOE_SINGLE_LIB": "1", "DLA_EP_NATIVE_ROUTE": "1"},
+                                  "lib": {"DLA_MOE_SINGLE_LIB": "1", "DLA_EP_NATIVE_ROUTE": "0"},
+                                  "neither": {"DLA_MOE_SINGLE_LIB": "0", "DLA_EP_NATIVE_ROUTE": "0"}}, 1)],
+    "mixtral-ep-degrees": [run(f"ep{ep}", MIX_EP8.replace("--ep-shape 8", f"--ep-shape {ep}") + " --steps 3 --warmup 2")
+                           for ep in (4, 2)],
+    "ab-m64-split": [run("m64_probe", "python -u tools/m64_probe.py", 120),
+                     ab("m64_split", GEN64, {"new": {}, "old": {"DLA_M64_WG": "256"}}, 2, 300)],
+    "ab-decode-blocks": [ab("blocks", GEN8, {"base": {"DLA_DECODE_RING": "2"},
+                                             "b64r3": {"DLA_DECODE_BLOCKS": "64", "DLA_DECODE_RING": "3"},
+                                             "b128r3": {"DLA_DECODE_BLOCKS": "128", "DLA_DECODE_RING": "3"},
+                                             "b96r3": {"DLA_DECODE_BLOCKS": "96", "DLA_DECODE_RING": "3"},
+                                             "b64r2": {"DLA_DECODE_BLOCKS": "64", "DLA_DECODE_RING": "2"}}, 2, 300)],
+    "ab-kv-head-major": [pytest("tests -m gpu"),
+                         ab("khm_b64", GEN64, {"hm": {"DLA_KV_HEAD_MAJOR": "1"}, "tm": {"DLA_KV_HEAD_MAJOR": "0"}}, 2, 300),
+                         ab("khm_b8", GEN8, {"hm": {"DLA_KV_HEAD_MAJOR": "1"}, "tm": {"DLA_KV_HEAD_MAJOR": "0"}}, 2, 300)],
+}
+
+
+class Runner:
+    def __init__(self, out: str, dry: bool):
+        self.out, self.dry = out, dry
+        os.makedirs(out, exist_ok=True)
+
+    def _call(self, cmd, timeout_s, log, env=None, cwd=ROOT):
+        full = ["timeout", "-k", "10", str(timeout_s)] + (cmd if isinstance(cmd, list) else shlex.split(cmd))
+        if self.dry:
+            print("DRY", " ".join(f"{k}={v}" for k, v in (env or {}).items()), " ".join(full))
+            return 0
+        e = dict(os.environ, PYTHONUNBUFFERED="1", TMPDIR="/tmp", **(env or {}))
+        e.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        with open(log, "w") as fh:
+            return subprocess.call(full, cwd=cwd, env=e, stdout=fh, stderr=subprocess.STDOUT)
+
+    @staticmethod
+    def _last(log):
+        try:
+            lines = [ln for ln in open(log, errors="replace").read().splitlines() if ln.strip()]
+        except OSError:
+            return ""
+        return lines[-1][:400] if lines else ""
+
+    def _check(self, rc, what, log):
+        if rc != 0:
+            print(f"FAILED {what} rc={rc}; tail of {log}:")
+            try:
+                print("\n".join(open(log, errors="replace").read().splitlines()[-30:]))
+            except OSError:
+                pass
+            raise SystemExit(1)
+
+    def step(self, s):
+        k, t = s["kind"], s["timeout"]
+        o = self.out
+        if k == "pytest":
+            log = f"{o}/pytest_{abs(hash(s['sel'])) % 10000}.log"
+            cmd = f"python -u -m pytest {s['sel']} -x -q --timeout 200 --timeout-method thread"
+            self._check(self._call(cmd, t, log), s["sel"], log)
+            print(f"pytest {s['sel']}: {self._last(log)}")
+        elif k == "smoke":
+            log = f"{o}/smoke.log"
+            cmd = ["python", "-u", "-c", "import __graft_entry__ as g; g.smoke(); print('SMOKE_OK')"]
+            self._check(self._call(cmd, t, log), "smoke", log)
+            print("smoke:", self._last(log))
+        elif k == "run":
+            log = f"{o}/{s['name']}.log"
+            self._check(self._call(s["cmd"], t, log, s["env"]), s["name"], log)
+            print(f"{s['name']}: {self._last(log)}")
+        elif k == "ab":
+            for r in range(s["rounds"]):
+                for arm, env in s["arms"].items():
+                    log = f"{o}/{s['name']}_{arm}.{r}.log"
+                    self._check(self._call(s["cmd"], t, log, env), f"{s['name']}/{arm}", log)
+                    print(f"{s['name']} arm={arm} r={r}: {self._last(log)}")
+        elif k == "prof":
+            d = f"/tmp/prof_{s['name']}"
+            shutil.rmtree(d, ignore_errors=True)
+            log = os.path.abspath(f"{o}/prof_{s['name']}.log")
+            cmd = ["rocprofv3", "--kernel-trace", "--output-format", "csv", "-d", d, "-o", "run", "--"] \
+                + shlex.split(s["cmd"].replace("python -u ", "python3 -u ").replace("python ", "python3 "))
+            self._check(self._call(cmd, t, log, s["env"]), f"prof {s['name']}", log)
+            if self.dry:
+                return
+            tr = (glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True) or [None])[0]
+            if tr is None:
+                self._check(1, f"prof {s['name']} (no kernel trace)", log)
+            tools = {"window": "prof_window.py", "breakdown": "step_breakdown.py", "streams": "prof_streams.py"}
+            for kind, args in s["summaries"]:
+                dst = f"{o}/{s['name']}_{kind}.md"
+                with open(dst, "w") as fh:
+                    rc = subprocess.call([sys.executable, os.path.join(ROOT, "scripts", tools[kind]), tr, *args],
+                                         stdout=fh, stderr=subprocess.STDOUT)
+                self._check(rc, f"summary {dst}", dst)
+                print(f"prof {s['name']}: {dst}")
+            shutil.rmtree(d, ignore_errors=True)
+        elif k == "pmc":
+            d = f"/tmp/pmc_{s['name']}"
+            shutil.rmtree(d, ignore_errors=True)
+            log = os.path.abspath(f"{o}/pmc_{s['name']}.log")
+            cmd = ["rocprofv3", "--pmc", *s["counters"].split(), "--output-format", "csv", "-d", d, "-o", "run",
+                   "--", *shlex.split(s["cmd"])]
+            full = ["timeout", "-s", "KILL", str(t)] + cmd
+            if self.dry:
+                print("DRY", " ".join(full))
+                return
+            with open(log, "w") as fh:
+                rc = subprocess.call(full, cwd=ROOT, stdout=fh, stderr=subprocess.STDOUT,
+                                     env=dict(os.environ, TMPDIR="/tmp"))
+            self._check(rc, f"pmc {s['name']}", log)
+            c = (glob.glob(f"{d}/**/*counter_collection.csv", recursive=True) or [None])[0]
+            dst = f"{o}/{s['name']}_pmc.md"
+            with open(dst, "w") as fh:
+                rc = subprocess.call([sys.executable, os.path.join(ROOT, "scripts", "pmc_summary_csv.py"), c,
+                                      "-k", *s["kernels"].split()], stdout=fh, stderr=subprocess.STDOUT)
+            self._check(rc, f"pmc summary {dst}", dst)
+            shutil.rmtree(d, ignore_errors=True)
+            print(f"pmc {s['name']}: {dst}")
+        else:
+            raise ValueError(k)
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("name", nargs="?")
+    ap.add_argument("--out", default=None)
+    ap.add_argument("--list", action="store_true")
+    ap.add_argument("--dry", action="store_true", help="print the commands only")
+    a = ap.parse_args(argv)
+    if a.list or not a.name:
+        for n, steps in PASSES.items():
+            print(f"{n:24s} {len(steps)} step(s): " + ", ".join(s.get("name", s["kind"]) for s in steps))
+        return 0
+    if a.name not in PASSES:
+        raise SystemExit(f"unknown pass {a.name!r} (--list)")
+    out = a.out or os.path.join(ROOT, "gpurun_out", a.name)
+    r = Runner(out, a.dry)
+    stop = threading.Event()
+
+    def beat():
+        while not stop.wait(30):
+            with open(os.path.join(out, "heartbeat"), "w") as fh:
+                fh.write(time.ctime())
+
+    threading.Thread(target=beat, daemon=True).start()
+    try:
+        for s in PASSES[a.name]:
+            r.step(s)
+    finally:
+        stop.set()
+    print("ALL_DONE")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
