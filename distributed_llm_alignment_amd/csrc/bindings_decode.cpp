@@ -11,6 +11,7 @@
 #include <tuple>
 
 #include "bind_util.h"
+#include "decode_tail.h"
 #include "skinny_params.h"
 
 namespace dla {
@@ -753,6 +754,113 @@ at::Tensor sample_tokens(const at::Tensor& logits, double temperature, int64_t t
   return out;
 }
 
+static at::Tensor& tail_stamp_buffer() {
+  static at::Tensor t;
+  return t;
+}
+
+at::Tensor decode_tail_stamps(const at::Tensor& like) {
+  (void)like;
+  return tail_stamp_buffer().defined() ? tail_stamp_buffer().clone() : at::Tensor();
+}
+
+// Persistent decode layer tail (decode_tail.hip, B <= 16): o projection + residual, gate|up +
+// SwiGLU, down + residual [+ the next layer's qkv projection] in ONE launch. Weights in the tiled
+// layout [N/16, K/32, 4, 16, 8] (wgu: gate / up rows interleaved 8 + 8, ln2 folded; wq: the next
+// layer's ln1 folded). Returns (x_out [M, H], its row partials [16, H/16], qkv [M, Nq] or empty).
+static void check_tiled(const at::Tensor& w, const char* name) {
+  check_bf16(w, name);
+  TORCH_CHECK(w.dim() == 5 && w.size(2) == 4 && w.size(3) == 16 && w.size(4) == 8 && w.is_contiguous(), name,
+              ": tiled [N/16, K/32, 4, 16, 8]");
+  check_aligned16(w, name);
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> decode_tail(
+    const at::Tensor& a, const at::Tensor& x, const at::Tensor& wo, const at::Tensor& wgu, const at::Tensor& wd,
+    const c10::optional<at::Tensor>& wq, double eps, at::Tensor& cnt, const at::Tensor& kv_len,
+    const at::Tensor& len_first, at::Tensor& err) {
+  check_bf16(a, "a");
+  check_bf16(x, "x");
+  check_tiled(wo, "wo");
+  check_tiled(wgu, "wgu");
+  check_tiled(wd, "wd");
+  const int64_t M = x.size(0), H = x.size(1), Ko = a.size(1);
+  TORCH_CHECK(a.dim() == 2 && x.dim() == 2 && a.size(0) == M && a.stride(1) == 1 && x.stride(1) == 1 &&
+                  a.stride(0) % 8 == 0 && x.stride(0) % 8 == 0 && M >= 1 && M <= 16,
+              "decode_tail: a [M, Ko], x [M, H], 1 <= M <= 16, 16-byte aligned rows");
+  check_aligned16(a, "a");
+  check_aligned16(x, "x");
+  const int64_t F = wd.size(1) * 32;
+  TORCH_CHECK(wo.size(0) * 16 == H && wo.size(1) * 32 == Ko && wgu.size(0) * 16 == 2 * F && wgu.size(1) * 32 == H &&
+                  wd.size(0) * 16 == H,
+              "decode_tail: weight shapes (o [H, Ko], gate|up [2F, H], down [H, F])");
+  int64_t Nq = 0;
+  if (wq.has_value()) {
+    check_tiled(*wq, "wq");
+    TORCH_CHECK(wq->size(1) * 32 == H, "decode_tail: wq [Nq, H]");
+    Nq = wq->size(0) * 16;
+  }
+  TORCH_CHECK(cnt.scalar_type() == at::kInt && cnt.is_contiguous() && cnt.numel() >= 3 * 8 * 32 &&
+                  kv_len.scalar_type() == at::kInt && len_first.scalar_type() == at::kInt &&
+                  err.scalar_type() == at::kInt,
+              "decode_tail: int32 cnt [>= 768], kv_len, len_first, err");
+  same_device(x, a);
+  same_device(x, wo);
+  same_device(x, cnt);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  auto s = at::empty({M, H}, x.options());
+  auto m = at::empty({M, F}, x.options());
+  auto xo = at::empty({M, H}, x.options());
+  auto fopt = x.options().dtype(at::kFloat);
+  auto ssq_s = at::empty({16, H / 16}, fopt);
+  auto ssq_x = at::empty({16, H / 16}, fopt);
+  at::Tensor qkv = Nq ? at::empty({M, Nq}, x.options()) : at::Tensor();
+  TailArgs A{};
+  A.a = cbp(a);
+  A.lda = a.stride(0);
+  A.x = cbp(x);
+  A.ldx = x.stride(0);
+  A.Wo = cbp(wo);
+  A.Wgu = cbp(wgu);
+  A.Wd = cbp(wd);
+  A.Wq = Nq ? cbp(*wq) : nullptr;
+  A.s = bp(s);
+  A.ssq_s = ssq_s.data_ptr<float>();
+  A.m = bp(m);
+  A.xo = bp(xo);
+  A.ssq_x = ssq_x.data_ptr<float>();
+  A.qkv = Nq ? bp(qkv) : nullptr;
+  A.M = (int)M;
+  A.H = (int)H;
+  A.Ko = (int)Ko;
+  A.F = (int)F;
+  A.Nq = (int)Nq;
+  A.eps = static_cast<float>(eps);
+  A.cnt = cnt.data_ptr<int>();
+  A.kv_len = kv_len.data_ptr<int>();
+  A.len_first = len_first.data_ptr<int>();
+  A.err = err.data_ptr<int>();
+  // DLA_TAIL_STAMPS=1 (debug): per-workgroup phase-edge timestamps into a process-wide buffer,
+  // read back with decode_tail_stamps()
+  static const bool stamps_on = [] {
+    const char* e = std::getenv("DLA_TAIL_STAMPS");
+    return e && std::atoi(e) != 0;
+  }();
+  if (stamps_on) {
+    static at::Tensor buf;
+    if (!buf.defined() || buf.device() != x.device())
+      buf = at::zeros({1024, 8}, x.options().dtype(at::kLong));
+    tail_stamp_buffer() = buf;
+    A.stamps = reinterpret_cast<unsigned long long*>(buf.data_ptr<int64_t>());
+  }
+  const bool ok = launch_decode_tail(A, cur_stream(x));
+  TORCH_CHECK(ok, "decode_tail: shape outside the persistent kernel (M <= 16, H / Ko / F % 1024 == 0, "
+                  "x staged in LDS) or no resident workgroup per CU");
+  const hipError_t le = hipGetLastError();
+  TORCH_CHECK(le == hipSuccess, "decode_tail launch: ", hipGetErrorString(le));
+  return {xo, ssq_x, qkv};
+}
+
 }  // namespace dla
 
 TORCH_LIBRARY_FRAGMENT(dla, m) {
@@ -770,6 +878,8 @@ TORCH_LIBRARY_FRAGMENT(dla, m) {
   m.def("skinny64(Tensor x, Tensor w, Tensor? res, Tensor? ssq_in, float eps, bool glu) -> (Tensor, Tensor)");
   m.def("tile_weight(Tensor w, Tensor? nw, Tensor(a!) out, bool glu_il=False) -> ()");
   m.def("skinny_glu_il(Tensor x, Tensor wt, Tensor ssq_in, float eps) -> Tensor");
+  m.def("decode_tail_stamps(Tensor like) -> Tensor");
+  m.def("decode_tail(Tensor a, Tensor x, Tensor wo, Tensor wgu, Tensor wd, Tensor? wq, float eps, Tensor(a!) cnt, Tensor kv_len, Tensor len_first, Tensor(b!) err) -> (Tensor, Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(dla, CUDA, m) {
@@ -787,4 +897,6 @@ TORCH_LIBRARY_IMPL(dla, CUDA, m) {
   m.impl("skinny64", &dla::skinny64);
   m.impl("tile_weight", &dla::tile_weight);
   m.impl("skinny_glu_il", &dla::skinny_glu_il);
+  m.impl("decode_tail", &dla::decode_tail);
+  m.impl("decode_tail_stamps", &dla::decode_tail_stamps);
 }

@@ -62,6 +62,9 @@ class KVCache:
         self.sync = torch.zeros((L, 8, 32), dtype=torch.int32, device=dev)
         self.len_first = torch.ones(1, dtype=torch.int32, device=dev)
         self.sync_err = torch.zeros(1, dtype=torch.int32, device=dev)
+        # the persistent layer-tail kernel's phase counters (ops.decode.layer_tail): 3 phases x 8
+        # replicas x 32 ints per layer, monotonic within a generation like `sync`
+        self.tail_sync = torch.zeros((L, 3 * 8 * 32), dtype=torch.int32, device=dev)
         self.pos = torch.zeros((batch, 1), dtype=torch.int32, device=dev)
         self.fast_decode = (not self.split and dev.type == "cuda" and dt == torch.bfloat16
                             and ops.decode.decode_supported(self.h_local, Hkv, D))
@@ -170,8 +173,9 @@ class KVCache:
     def advance(self, T: int):
         """Host-driven advance (prefill / eager decode) keeping the device state in step."""
         self.len += T
-        if T > 1:  # a (new) prompt: the fused decode kernel's counters start over
+        if T > 1:  # a (new) prompt: the fused decode kernels' counters start over
             self.sync.zero_()
+            self.tail_sync.zero_()
             self.len_first.fill_(self.len + 1)
         self.slot.fill_(self.len)
         self.kv_len.fill_(self.len + 1)
@@ -473,7 +477,8 @@ def generate(model: CausalLM, input_ids: torch.Tensor, attention_mask: Optional[
         gm = torch.stack(gen_mask, 1)
     if was_training:
         model.train()
-    if ops.decode.DECODE_QKV_ATTN and cache.fast_decode and int(cache.sync_err.item()) != 0:
+    if ((ops.decode.DECODE_QKV_ATTN or ops.decode.DECODE_TAIL) and cache.fast_decode
+            and int(cache.sync_err.item()) != 0):
         # the fused qkv + attention kernel's counter wait timed out (it proceeds rather than hang
         # the GPU): the step's attention read an incomplete q / k / v row
         raise RuntimeError("decode_qkv_attn: a workgroup's wait for the qkv tiles timed out "

@@ -524,6 +524,23 @@ class CausalLM(nn.Module):
         # decode_fused calls the layers' kernels directly, skipping Module.__call__: a ZeRO-3
         # policy's layers are gathered by forward hooks, so sharded layers take the hooked path
         if (input_ids.shape[1] == 1 and self.layer_devices is None and self.layers
+                and not self.layers_sharded() and ops.decode.tail_ok(self, x)):
+            # decode step as two launches per layer: attention, then the persistent layer tail
+            # (o, gate|up, down and the NEXT layer's qkv; csrc/decode_tail.hip)
+            cfg, L = self.cfg, len(self.layers)
+            window = cfg.sliding_window if cfg.sliding_window else 0
+            s = x.reshape(-1, x.shape[-1])
+            h, _ = ops.add_norm(s, None, self.layers[0].ln1_w, None, cfg.norm_eps, True)
+            qkv = _lin(h, self.layers[0].attn.qkv_proj, None)
+            B = input_ids.shape[0]
+            for i, layer in enumerate(self.layers):
+                a = cache.attend(i, qkv.view(B, 1, -1), self.rope, window)
+                s, qkv = ops.decode.layer_tail(a, s, layer, self.layers[i + 1] if i + 1 < L else None,
+                                               cfg.norm_eps, cache, i)
+            h, _ = ops.add_norm(s.view(B, 1, -1), None, self.norm_w, self.norm_b, cfg.norm_eps, True)
+            cache.step_done(1)
+            return h
+        if (input_ids.shape[1] == 1 and self.layer_devices is None and self.layers
                 and not self.layers_sharded() and self.layers[0].decode_fused_ok(x)):
             # decode step: residual add + RMSNorm folded into the neighbouring projections
             s, ssq = x, None

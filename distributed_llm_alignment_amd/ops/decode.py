@@ -429,6 +429,37 @@ _DECODE_NT = os.environ.get("DLA_DECODE_NT", "1") != "0"  # the fused kernel str
 
 _COMBINE_ON = os.environ.get("DLA_DECODE_FUSED_COMBINE", "1") != "0"
 
+# <= 16 decode rows: the post-attention half of every layer (o + residual, gate|up + SwiGLU,
+# down + residual) AND the next layer's qkv projection as ONE persistent launch
+# (csrc/decode_tail.hip): the next phase's weights stream while the workgroups wait for the
+# previous phase; a step is then two launches per layer (this + the decode attention).
+DECODE_TAIL = os.environ.get("DLA_DECODE_TAIL", "0") == "1"
+
+
+def tail_ok(model, x) -> bool:
+    """The model's decode step can run on the persistent layer-tail kernel."""
+    if not (DECODE_TAIL and _DECODE_NT and DECODE_TILED >= 2 and x.is_cuda):
+        return False
+    cfg = model.cfg
+    rows = x.numel() // x.shape[-1]
+    H, F, Ko = cfg.hidden_size, cfg.intermediate_size, model.layers[0].attn.o_proj.shape[1]
+    return (rows <= 16 and H % 1024 == 0 and F % 1024 == 0 and Ko % 1024 == 0
+            and rows * (H + 8) * 2 <= 140 * 1024 and all(l.decode_fused_ok(x) for l in model.layers))
+
+
+def layer_tail(a: torch.Tensor, x: torch.Tensor, layer, nxt, eps: float, cache, idx: int):
+    """x_out = x + o(a); x_out += down(SwiGLU(gate|up(RMSNorm(x_out)))); and, with `nxt`, the next
+    layer's qkv = RMSNorm(x_out) @ Wqkv^T, in one persistent launch. Returns (x_out [M, H],
+    qkv [M, Nq] or None)."""
+    at, mlp = layer.attn, layer.mlp
+    wo = tiled_weight(at.o_proj)
+    wgu = folded_weight(mlp.up_proj, layer.ln2_w, tiled=True, glu_il=True)
+    wd = tiled_weight(mlp.down_proj)
+    wq = folded_weight(nxt.attn.qkv_proj, nxt.ln1_w, tiled=True) if nxt is not None else None
+    xo, _, qkv = _ext.require().decode_tail(_rows(a), _rows(x), wo, wgu, wd, wq, float(eps), cache.tail_sync[idx],
+                                            cache.kv_len, cache.len_first, cache.sync_err)
+    return xo, (qkv if nxt is not None else None)
+
 
 _CUS = {}
 

@@ -759,3 +759,58 @@ def test_skinny64_kernels_match_fp32(M):
     # row-major folded weight (DLA_M64_TILED=0) == the tiled default, bitwise
     mm_rm, _ = ops._ext.require().skinny64(s, ops.decode.folded_weight(wgu, nw), None, ssq, 1e-5, True)
     assert torch.equal(mm_rm, mm)
+
+
+@pytest.mark.parametrize("B,T,pad", [(1, 40, False), (5, 300, True), (8, 100, False), (16, 200, True)])
+def test_decode_layer_tail_matches_four_launches(B, T, pad, monkeypatch):
+    """<= 16 rows: the persistent layer tail (csrc/decode_tail.hip: o + residual, gate|up +
+    SwiGLU, down + residual and the next layer's qkv in ONE launch, phase hand-offs through
+    write-through stores and replicated counters) against the four-launch fused decode layer --
+    BITWISE (same per-wave K order, wave-order reductions, roundings) -- and an fp32 forward; every
+    phase counter replica saw every workgroup every step, no wait timed out; graph == eager."""
+    from distributed_llm_alignment_amd import ops
+    from distributed_llm_alignment_amd.models import build_model, generate
+    from distributed_llm_alignment_amd.models.generation import KVCache, clear_graph_cache
+    from distributed_llm_alignment_amd.models.transformer import attention_layout
+
+    cfg = _fused_cfg()
+    m = build_model(cfg, device=DEV, dtype=torch.bfloat16, seed=5).eval()
+    g = torch.Generator(device=DEV).manual_seed(13)
+    ids = torch.randint(3, cfg.vocab_size, (B, T), device=DEV, generator=g)
+    am = torch.ones_like(ids)
+    if pad:
+        for r in range(B):
+            am[r, :(5 * r) % 29] = 0
+    steps = [torch.randint(3, cfg.vocab_size, (B, 1), device=DEV, generator=g) for _ in range(3)]
+    kv_start = attention_layout(am)[0] if pad else None
+    outs, caches = {}, {}
+    with torch.no_grad():
+        for tail in (False, True):
+            monkeypatch.setattr(ops.decode, "DECODE_TAIL", tail)
+            cache = KVCache(m, B, T + 8, kv_start)
+            m(ids, am if pad else None, cache=cache)
+            assert ops.decode.tail_ok(m, m.embed_tokens(steps[0])) == tail
+            outs[tail] = [m(nx, cache=cache).float() for nx in steps]
+            caches[tail] = cache
+        full = torch.cat([ids] + steps, 1)
+        fam = torch.cat([am, torch.ones(B, len(steps), dtype=am.dtype, device=DEV)], 1)
+        ref = m(full, fam if pad else None)[:, -len(steps):].float()
+    ct = caches[True]
+    torch.cuda.synchronize()
+    assert int(ct.sync_err.item()) == 0
+    nwg = torch.cuda.get_device_properties(0).multi_processor_count  # one workgroup per CU
+    cnt = ct.tail_sync.view(cfg.num_layers, 3, 8, 32)[:, :, :, 0]
+    assert (cnt[:-1] == nwg * len(steps)).all(), cnt  # layers with a next-layer qkv phase: 3 counters
+    assert (cnt[-1, :2] == nwg * len(steps)).all() and int(cnt[-1, 2].abs().sum()) == 0, cnt[-1]
+    assert int(caches[False].tail_sync.abs().sum()) == 0
+    for k in range(len(steps)):
+        assert torch.equal(outs[True][k], outs[False][k]), k
+        assert float((outs[True][k][:, 0] - ref[:, k]).norm() / ref[:, k].norm()) < 3e-2, k
+    monkeypatch.setattr(ops.decode, "DECODE_TAIL", True)
+    clear_graph_cache()
+    a = generate(m, ids, am, max_new_tokens=12, do_sample=False, eos_token_id=-1, use_graph=False)
+    b = generate(m, ids, am, max_new_tokens=12, do_sample=False, eos_token_id=-1, use_graph=True)
+    monkeypatch.setattr(ops.decode, "DECODE_TAIL", False)
+    c = generate(m, ids, am, max_new_tokens=12, do_sample=False, eos_token_id=-1, use_graph=True)
+    clear_graph_cache()
+    assert torch.equal(a, b) and torch.equal(b, c)
