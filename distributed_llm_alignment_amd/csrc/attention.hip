@@ -29,6 +29,7 @@
 // Backward: see attn_bwd_kernel.
 #include <cstdlib>
 #include <stdexcept>
+#include <type_traits>
 #include "common.h"
 #include "attn_params.h"
 
@@ -167,6 +168,33 @@ __device__ __forceinline__ f32x16 unrotate_tile0_rot32(f32x16 x, const float* cp
 // ==============================================================================================
 constexpr int kFwdKeys = 64;      // keys per K/V tile
 
+// Workgroup i of a launch runs on XCD i % 8, and each XCD starts its workgroups in order of i / 8
+// (MI355X_MICROARCH §Workgroup dispatch; a speed assumption only, never a correctness one). The
+// bijective remap (cdna guide §5 'XCD swizzle must be bijective') gives XCD x the contiguous
+// logical range [start_x, start_x + size_x), walked in order; the forward lays logical blocks out
+// (batch, head block)-major with the query blocks of one column adjacent, so the ~32 workgroups an
+// XCD runs at once stream the same one or two K/V sequences through its L2 instead of 32 different
+// ones from HBM / the Infinity Cache.
+__device__ __forceinline__ int fwd_xcd_logical(int bid, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, x = bid % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+}
+
+// Logical block of item i of persistent workgroup g of G: a snake over the workgroups (causal:
+// heaviest-first blocks, equal tile sums), XCD-grouped as above when G % 8 == 0. Returns nblk
+// past the end (monotone: once past, every later item is past too).
+__device__ __forceinline__ int fwd_persist_logical(int i, int g, int G, int nblk, bool xcd) {
+  if (!xcd || (G & 7) != 0) {
+    const int idx = (i & 1) ? (i + 1) * G - 1 - g : i * G + g;
+    return idx < nblk ? idx : nblk;
+  }
+  const int x = g & 7, l = g >> 3, L = G >> 3;
+  const int bq = nblk >> 3, br = nblk & 7;
+  const int size = bq + (x < br ? 1 : 0), start = x < br ? x * (bq + 1) : br * (bq + 1) + (x - br) * bq;
+  const int idx = (i & 1) ? (i + 1) * L - 1 - l : i * L + l;
+  return idx < size ? start + idx : nblk;
+}
+
 // NW waves per workgroup, 32 queries each (NT = 64 NW threads). HP query heads of one GQA group
 // per workgroup (HP = 2: waves 0..NW/2-1 take head 2p, the rest head 2p+1): every K/V tile staged
 // in LDS still feeds 32 NW query rows, but a head's query block is only BQ = 32 NW / HP rows, so
@@ -194,8 +222,15 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
   const int nhb = p.Hq / HP;  // head blocks
   const int nbh = nhb * p.B;
   const int bid = blockIdx.x;
-  const int qb = CAUSAL ? nqb - 1 - bid / nbh : bid / nbh;
-  const int rest = bid % nbh;
+  int qb, rest;
+  if (p.fwd_xcd) {  // XCD-grouped: logical = this XCD's contiguous range, (head block, batch)-major
+    const int lg = fwd_xcd_logical(bid, gridDim.x);
+    rest = lg / nqb;
+    qb = CAUSAL ? nqb - 1 - lg % nqb : lg % nqb;
+  } else {  // query block slowest (causal: heaviest first)
+    qb = CAUSAL ? nqb - 1 - bid / nbh : bid / nbh;
+    rest = bid % nbh;
+  }
   const int hq = (rest % nhb) * HP + w / WPH, b = rest / nhb;
   const int hk = hq / (p.Hq / p.Hkv);  // the same for the HP heads (host: group % HP == 0)
   const int q0 = qb * BQ + (w % WPH) * 32;
@@ -313,10 +348,13 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
     if (ntiles > 1) gload(tile0 + BK);
   }
   __syncthreads();
-  for (int t = 0; t < ntiles; ++t) {
+  // the loop body runs as two copies (buffer 0 / buffer 1) so every LDS read address is a per-lane
+  // base plus an immediate: no per-tile buffer select in the VALU stream
+  auto step = [&](auto bufc, int t) {
+    constexpr int BUF = decltype(bufc)::value;
     const int kt = tile0 + t * BK;
-    const bf16_t* Ks = Kb[t & 1];
-    const bf16_t* Vs = Vb[t & 1];
+    const bf16_t* Ks = Kb[BUF];
+    const bf16_t* Vs = Vb[BUF];
     bool active = q0 < p.Tq && kt + BK > wseg_lo;
     if (CAUSAL) {
       active = active && (kt <= q0 + 31 + p.causal_off);
@@ -376,15 +414,17 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
         for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
       }
       const float muse = m == -INFINITY ? 0.f : m;
+      float lpart[2] = {0.f, 0.f};  // two independent add chains (the row sum was one 32-add chain)
 #pragma unroll
       for (int st = 0; st < 2; ++st) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const float pv = ex2(sacc[st][i] - muse);
           sacc[st][i] = pv;
-          lsum += pv;
+          lpart[st] += pv;
         }
       }
+      lsum += lpart[0] + lpart[1];
       s16x8 pf[2][2];
 #pragma unroll
       for (int st = 0; st < 2; ++st) {
@@ -405,10 +445,14 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
       }
     }
     if (t + 1 < ntiles) {  // stage tile t+1 into the other buffer, prefetch tile t+2
-      lwrite((t + 1) & 1, kt + BK);
+      lwrite(BUF ^ 1, kt + BK);
       if (t + 2 < ntiles) gload(kt + 2 * BK);
     }
     __syncthreads();
+  };
+  for (int t = 0; t < ntiles; t += 2) {
+    step(std::integral_constant<int, 0>{}, t);
+    if (t + 1 < ntiles) step(std::integral_constant<int, 1>{}, t + 1);
   }
 
   lsum += __shfl_xor(lsum, 32, 64);
@@ -437,6 +481,370 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
       p.lse2[(static_cast<int64_t>(b) * p.Hq + hq) * p.Tq + qi] =
           lsum > 0.f ? m + __log2f(lsum) : INFINITY;
     }
+  }
+}
+
+// ----------------------------------------------------------------------------------------------
+// persistent forward
+// ----------------------------------------------------------------------------------------------
+// attn_fwd_kernel pays a fixed cost per query block that the tile loop never hides: the Q rows
+// and the first K/V tile are fetched with every CU doing the same at once, and the O store tail
+// is issue-bound. Fitting t = blocks_per_CU x (c0 + tiles x c1) over T = 256..4096 at B*T = 8192
+// (tools/attn_fwd_sweep.py, graph-timed) gives c0 = 11.7 us against c1 = 1.87 us per 64-key tile:
+// at causal T = 1024 (8.5 tiles per block on average) ~45 % of the kernel is that seam.
+// This variant runs one workgroup per CU over a snake-ordered list of the same blocks (causal:
+// heaviest first, so the per-workgroup tile sums come out equal) and streams across the seams:
+//   * the next block's first K/V tile is register-staged during the current block's second-last
+//     tile (the same async-STAGE pipeline as inside a block);
+//   * its Q rows arrive by LDS-DMA (global_load_lds, lane-linear into a per-wave chunk-major
+//     [D/8][32 rows][8] image, conflict-free ds_read_b128 at the seam) issued at the top of the
+//     current block's last tile, so only the last tile's compute separates issue and use;
+//   * the seam reads the new Q, issues the next tile's loads, and only then stores the finished
+//     block's O / LSE, so the store tail drains under the next block's first tile.
+// The tile math (swapped scores, deferred max, P from the accumulator, tr-read V, T21 stores) is
+// attn_fwd_kernel's; outputs are bitwise equal to it (tests/test_kernels_gpu.py).
+template <int D, bool CAUSAL, int NW, int HP>
+__global__ __launch_bounds__(64 * NW) void attn_fwd_persist_kernel(AttnParams p, int nblk) {
+  constexpr int NT = 64 * NW, BQ = 32 * NW / HP, BK = kFwdKeys;
+  constexpr int WPH = NW / HP;
+  constexpr int DP = attn_dp<D>();
+  constexpr int NCH = DP / 8;
+  constexpr int NCHL = D / 8;
+  constexpr int KS = D / 16;
+  constexpr int DT = DP / 32;
+  constexpr int CPT = (BK * NCH + NT - 1) / NT;
+  constexpr bool CPT_EXACT = (BK * NCH) % NT == 0;
+  constexpr int KVE = BK * DP;   // elements of one K or V tile image
+  constexpr int QWE = 32 * D;    // elements of one wave's Q image
+  static_assert(CPT >= 1, "K/V tile smaller than the workgroup");
+  // ONE LDS array (a second __shared__ object beside an LDS-DMA target can make hipcc drain
+  // vmcnt before every ds_read: cdna guide §5 'Projection GEMM at M = 256' item 4(a))
+  __shared__ __attribute__((aligned(16))) bf16_t lds[4 * KVE + NW * QWE];
+
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l32 = lane & 31, h = lane >> 5;
+  const int nqb = (p.Tq + BQ - 1) / BQ;
+  const int nhb = p.Hq / HP;
+  const int nbh = nhb * p.B;
+  const int G = gridDim.x, g = blockIdx.x;
+  bf16_t* Qw = lds + 4 * KVE + w * QWE;
+
+  struct Blk {  // wave-uniform description of one query block (this wave's 32 rows of it)
+    bool valid;
+    int b, hq, hk, q0, kbeg, kend, ntiles, tile0, wseg_lo, wseg_hi;
+  };
+  auto make_blk = [&](int i) -> Blk {
+    Blk c{};
+    const int blk = fwd_persist_logical(i, g, G, nblk, p.fwd_xcd != 0);
+    c.valid = blk < nblk;
+    if (!c.valid) return c;
+    int qb, rest;
+    if (p.fwd_xcd && (G & 7) == 0) {
+      rest = blk / nqb;
+      qb = CAUSAL ? nqb - 1 - blk % nqb : blk % nqb;
+    } else {
+      qb = CAUSAL ? nqb - 1 - blk / nbh : blk / nbh;
+      rest = blk % nbh;
+    }
+    c.hq = (rest % nhb) * HP + w / WPH;
+    c.b = rest / nhb;
+    c.hk = c.hq / (p.Hq / p.Hkv);
+    c.q0 = qb * BQ + (w % WPH) * 32;
+    c.kbeg = p.kv_start ? p.kv_start[c.b] : 0;
+    c.kend = p.kv_end ? p.kv_end[c.b] : p.Tk;
+    const int blk_qmax = min(p.Tq, qb * BQ + BQ) - 1;
+    int kmax = c.kend;
+    if (CAUSAL) kmax = min(kmax, blk_qmax + p.causal_off + 1);
+    int kmin = c.kbeg;
+    if (CAUSAL && p.window > 0) kmin = max(kmin, qb * BQ + p.causal_off - p.window + 1);
+    c.wseg_lo = c.wseg_hi = 0;
+    if (p.seg_start) {
+      const int* ss = p.seg_start + static_cast<int64_t>(c.b) * p.Tq;
+      kmin = max(kmin, ss[qb * BQ]);
+      c.wseg_lo = __builtin_amdgcn_readfirstlane(ss[min(c.q0, p.Tq - 1)]);
+      c.wseg_hi = __builtin_amdgcn_readfirstlane(ss[min(c.q0 + 31, p.Tq - 1)]);
+    }
+    c.tile0 = (max(kmin, 0) / BK) * BK;
+    c.ntiles = kmax > c.tile0 ? (kmax - c.tile0 + BK - 1) / BK : 0;
+    return c;
+  };
+
+  bf16x8 kreg[CPT], vreg[CPT];
+  auto gload = [&](const Blk& c, int kt) {
+    const bf16_t* kp = p.k + c.b * p.k_sb + static_cast<int64_t>(c.hk) * p.k_sh;
+    const bf16_t* vp = p.v + c.b * p.v_sb + static_cast<int64_t>(c.hk) * p.v_sh;
+#pragma unroll
+    for (int cc = 0; cc < CPT; ++cc) {
+      const int ci = tid + NT * cc;
+      const int row = ci / NCH, ch = ci % NCH;
+      const int key = kt + row;
+      if (key < p.Tk && ch < NCHL && (CPT_EXACT || ci < BK * NCH)) {
+        kreg[cc] = load_bf16x8(kp + key * p.k_st + ch * 8);
+        vreg[cc] = load_bf16x8(vp + key * p.v_st + ch * 8);
+      } else {
+        kreg[cc] = bf16x8{};
+        vreg[cc] = bf16x8{};
+      }
+    }
+  };
+  const bool rope = p.rope_cos != nullptr;
+  auto lwrite = [&](const Blk& c, int buf, int kt) {
+    bf16_t* Kb = lds + buf * KVE;
+    bf16_t* Vb = lds + (2 + buf) * KVE;
+#pragma unroll
+    for (int cc = 0; cc < CPT; ++cc) {
+      const int ci = tid + NT * cc;
+      if (!CPT_EXACT && ci >= BK * NCH) continue;
+      const int row = ci / NCH, ch = ci % NCH;
+      bf16x8 kv = kreg[cc];
+      if constexpr (DP == D) {
+        if (rope)
+          kv = rope_rot_chunk<NCH>(kv, ch, kt + row < p.Tk, static_cast<int64_t>(c.b) * p.Tk + kt + row,
+                                   kt + row, p.rope_cos, p.rope_sin, p.rope_pos);
+      }
+      store_bf16x8(&Kb[swz<DP>(row, ch)], kv);
+      store_bf16x8(&Vb[swz<DP>(row, ch)], vreg[cc]);
+    }
+  };
+  // this wave's 32 Q rows of block c -> Qw by LDS-DMA: instruction j writes 1 KB lane-linear,
+  // position j*64 + lane = (chunk 2j + lane/32, row lane%32) of the chunk-major image
+  auto q_dma = [&](const Blk& c) {
+    const bf16_t* qp = p.q + c.b * p.q_sb + static_cast<int64_t>(c.hq) * p.q_sh;
+    const bf16_t* src = qp + static_cast<int64_t>(min(c.q0 + l32, p.Tq - 1)) * p.q_st + 8 * h;
+#pragma unroll
+    for (int j = 0; j < KS; ++j)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + 16 * j),
+                                       (__attribute__((address_space(3))) void*)(Qw + j * 512), 16, 0, 0);
+  };
+  s16x8 qf[KS];
+  auto q_read = [&](const Blk& c) {  // after this wave's DMA has landed (vmcnt)
+    const int qi = c.q0 + l32;
+    float qv[KS][8];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      bf16x8 raw = *(const __attribute__((address_space(3))) bf16x8*)(Qw + ((2 * s + h) * 32 + l32) * 8);
+      if (qi >= p.Tq) raw = bf16x8{};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qv[s][j] = bf2f(raw[j]);
+    }
+    if (DP == D && rope && qi < p.Tq) {
+      const int pos = p.rope_pos ? p.rope_pos[static_cast<int64_t>(c.b) * p.Tq + qi] : qi;
+      const float* cp = p.rope_cos + static_cast<int64_t>(pos) * (D / 2) + 8 * h;
+      const float* sp = p.rope_sin + static_cast<int64_t>(pos) * (D / 2) + 8 * h;
+#pragma unroll
+      for (int s = 0; s < KS / 2; ++s) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float cs = cp[16 * s + j], sn = sp[16 * s + j];
+          const float a = qv[s][j], bb = qv[s + KS / 2][j];
+          qv[s][j] = a * cs - bb * sn;
+          qv[s + KS / 2][j] = bb * cs + a * sn;
+        }
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      float t[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) t[j] = qv[s][j] * p.scale2;
+      qf[s] = __builtin_bit_cast(s16x8, pack_bf16x8(t));
+    }
+    if (rope && p.q_rot != nullptr && qi < p.Tq) {
+      bf16_t* qo = p.q_rot + c.b * p.qr_sb + qi * p.qr_st + static_cast<int64_t>(c.hq) * p.qr_sh + 8 * h;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) store_bf16x8(qo + 16 * s, pack_bf16x8(qv[s]));
+    }
+  };
+
+  f32x16 o[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) o[dt] = f32x16{};
+  float m = -INFINITY, lsum = 0.f;
+
+  auto tile = [&](const Blk& c, int kt, int buf) {
+    const bf16_t* Ks = lds + buf * KVE;
+    const bf16_t* Vs = lds + (2 + buf) * KVE;
+    const int qi = c.q0 + l32;
+    bool active = c.q0 < p.Tq && kt + BK > c.wseg_lo;
+    if (CAUSAL) {
+      active = active && (kt <= c.q0 + 31 + p.causal_off);
+      if (p.window > 0) active = active && (kt + BK - 1 > c.q0 + p.causal_off - p.window);
+    }
+    if (!active) return;  // wave-uniform
+    f32x16 sacc[2];
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      sacc[st] = f32x16{};
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const s16x8 a = *reinterpret_cast<const s16x8*>(Ks + swz<DP>(32 * st + l32, 2 * s + h));
+        sacc[st] = mfma32(a, qf[s], sacc[st]);
+      }
+    }
+    bool need_mask = kt < c.kbeg || kt + BK > c.kend || kt < c.wseg_hi;
+    if (CAUSAL) {
+      need_mask = need_mask || (kt + BK - 1 > c.q0 + p.causal_off);
+      if (p.window > 0) need_mask = need_mask || (kt <= c.q0 + 31 + p.causal_off - p.window);
+    }
+    if (need_mask) {
+      const int qseg = p.seg_start ? p.seg_start[static_cast<int64_t>(c.b) * p.Tq + min(qi, p.Tq - 1)] : 0;
+      const int base = kt + 4 * h;
+      int lo = max(c.kbeg, qseg) - base, hi = c.kend - base;
+      if (CAUSAL) {
+        hi = min(hi, qi + p.causal_off + 1 - base);
+        if (p.window > 0) lo = max(lo, qi + p.causal_off - p.window + 1 - base);
+      }
+      const unsigned span = hi > lo ? static_cast<unsigned>(hi - lo) : 0u;
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int r = 32 * st + (i & 3) + 8 * (i >> 2);
+          sacc[st][i] = static_cast<unsigned>(r - lo) < span ? sacc[st][i] : -INFINITY;
+        }
+      }
+    }
+    float mloc = -INFINITY;
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) mloc = fmaxf(mloc, sacc[st][i]);
+    mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+    if (!__all(mloc <= m + kRescaleThr)) {
+      const float mnew = fmaxf(m, mloc);
+      const float alpha = ex2(m - (mnew == -INFINITY ? 0.f : mnew));
+      m = mnew;
+      lsum *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
+    }
+    const float muse = m == -INFINITY ? 0.f : m;
+    float lpart[2] = {0.f, 0.f};  // two independent add chains (the row sum was one 32-add chain)
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float pv = ex2(sacc[st][i] - muse);
+        sacc[st][i] = pv;
+        lpart[st] += pv;
+      }
+    }
+    lsum += lpart[0] + lpart[1];
+    s16x8 pf[2][2];
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      pf[st][0] = pack8(sacc[st], 0);
+      pf[st][1] = pack8(sacc[st], 8);
+    }
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      const int c0 = 32 * dt + 16 * ((lane >> 4) & 1);
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const s16x8 a = tr_frag_perm<DP>(Vs, 32 * st + 16 * s + 4 * h, c0, lane);
+          o[dt] = mfma32(a, pf[st][s], o[dt]);
+        }
+      }
+    }
+  };
+
+  auto epilogue = [&](const Blk& c) {
+    const int qi = c.q0 + l32;
+    const float ls = lsum + __shfl_xor(lsum, 32, 64);
+    if (qi < p.Tq) {
+      const float inv = ls > 0.f ? 1.f / ls : 0.f;
+      bf16_t* op = p.o + c.b * p.o_sb + qi * p.o_st + static_cast<int64_t>(c.hq) * p.o_sh;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+#pragma unroll
+        for (int g4 = 0; g4 < 4; g4 += 2) {
+          uint2 a, cc;
+          a.x = pack2bf(o[dt][4 * g4 + 0] * inv, o[dt][4 * g4 + 1] * inv);
+          a.y = pack2bf(o[dt][4 * g4 + 2] * inv, o[dt][4 * g4 + 3] * inv);
+          cc.x = pack2bf(o[dt][4 * g4 + 4] * inv, o[dt][4 * g4 + 5] * inv);
+          cc.y = pack2bf(o[dt][4 * g4 + 6] * inv, o[dt][4 * g4 + 7] * inv);
+          const auto rx = __builtin_amdgcn_permlane32_swap(a.x, cc.x, false, false);
+          const auto ry = __builtin_amdgcn_permlane32_swap(a.y, cc.y, false, false);
+          const int d = 32 * dt + 8 * g4 + 8 * h;
+          if (d < D) *reinterpret_cast<uint4*>(op + d) = make_uint4(rx[0], ry[0], rx[1], ry[1]);
+        }
+      }
+      if (h == 0)
+        p.lse2[(static_cast<int64_t>(c.b) * p.Hq + c.hq) * p.Tq + qi] = ls > 0.f ? m + __log2f(ls) : INFINITY;
+    }
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) o[dt] = f32x16{};
+    m = -INFINITY;
+    lsum = 0.f;
+  };
+
+  int wb = 0, rb = 0;      // LDS buffer of the next tile written / computed
+  bool staged = false;     // kreg / vreg hold the first tile of the block after `cur`
+  // enter block y (its first tile staged or not), z = the block after it
+  auto enter = [&](const Blk& y, const Blk& z) {
+    if (y.ntiles > 0) {
+      if (!staged) gload(y, y.tile0);
+      lwrite(y, wb, y.tile0);
+      wb ^= 1;
+    }
+    staged = false;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's Q DMA has landed
+    q_read(y);
+    if (y.ntiles > 1) {
+      gload(y, y.tile0 + BK);
+    } else if (z.valid && z.ntiles > 0) {
+      gload(z, z.tile0);
+      staged = true;
+    }
+    if (y.ntiles == 0 && z.valid) q_dma(z);  // no last tile to issue it from
+  };
+
+  // debug stamps, 100 MHz clock: per (workgroup, item < 8) tiles start / tiles done / seam
+  // entered (next Q read, next loads issued) / epilogue issued
+  auto stamp = [&](int item, int k) {
+    if (p.stamps != nullptr && tid == 0 && item < 8)
+      p.stamps[(static_cast<int64_t>(g) * 8 + item) * 4 + k] = __builtin_amdgcn_s_memrealtime();
+  };
+  int it = 0;
+  Blk cur = make_blk(0);
+  if (!cur.valid) return;  // workgroup-uniform (the host launches at most nblk workgroups)
+  Blk nxt = make_blk(1);
+  q_dma(cur);
+  enter(cur, nxt);
+  __syncthreads();
+  for (;;) {
+    stamp(it, 0);
+    for (int t = 0; t < cur.ntiles; ++t) {
+      const int kt = cur.tile0 + t * BK;
+      const bool last = t + 1 == cur.ntiles;
+      if (last && nxt.valid) q_dma(nxt);
+      tile(cur, kt, rb);
+      rb ^= 1;
+      if (!last) {
+        lwrite(cur, wb, kt + BK);
+        wb ^= 1;
+        if (t + 2 < cur.ntiles) {
+          gload(cur, kt + 2 * BK);
+        } else if (nxt.valid && nxt.ntiles > 0) {
+          gload(nxt, nxt.tile0);
+          staged = true;
+        }
+        __syncthreads();
+      }
+    }
+    stamp(it, 1);
+    ++it;
+    const Blk z = nxt.valid ? make_blk(it + 1) : Blk{};
+    if (nxt.valid) enter(nxt, z);
+    stamp(it - 1, 2);
+    epilogue(cur);
+    stamp(it - 1, 3);
+    if (!nxt.valid) break;
+    cur = nxt;
+    nxt = z;
+    __syncthreads();
   }
 }
 
@@ -1645,11 +2053,51 @@ static inline unsigned stream_grid(int64_t work) {
 // it, else 2, else 1; DLA_ATTN_FWD_HP=1|2|4 caps it for A/B runs. Same-box A/B (B8 T1024 Hq32
 // Hkv8 D128, tools/gpu_attn_env_ab.sh): causal 140-148 / 131-133 / 124-129 us for HP 1 / 2 / 4,
 // non-causal 217 -> 205-209 us, T = 4096 unchanged (366-379 us).
+// Persistent forward (attn_fwd_persist_kernel): DLA_ATTN_FWD_PERSIST=1 always, =0 never, unset =
+// for key ranges of at most 512 (<= 8 tiles per block), where it measured faster: graph-timed,
+// B*T = 8192, Hq 32 / Hkv 8 / D 128 (profiles/r5_attention_fwd.md) causal 240 -> 290-318 TF/s
+// at T 256 and 413 -> 469-472 at T 512, equal at 1024, 5 % slower at 2048-4096. Read per call so
+// one process can A/B both (tools/attn_fwd_sweep.py --cfg, tests/test_kernels_gpu.py).
+static bool fwd_persist(int Tk) {
+  const char* e = std::getenv("DLA_ATTN_FWD_PERSIST");
+  if (e == nullptr || *e == '\0') return Tk <= 512;
+  return std::atoi(e) != 0;
+}
+
+static int device_cus() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  if (cached[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cached[dev] = n;
+  }
+  return cached[dev];
+}
+
+// XCD-grouped block order: opt-in (DLA_ATTN_FWD_XCD=1). It did not move the kernel at T >= 1024
+// (the tile loop is VALU / issue bound, not K/V-stream bound) and cost 5 % causal at T 1024.
+static int fwd_xcd_order() {
+  const char* e = std::getenv("DLA_ATTN_FWD_XCD");
+  return (e != nullptr && std::atoi(e) != 0) ? 1 : 0;
+}
+
 template <int D, int HP>
-static void fwd_launch(const AttnParams& p, bool causal, hipStream_t st) {
+static void fwd_launch(const AttnParams& p0, bool causal, hipStream_t st) {
   constexpr int NW = 8, BQ = 32 * NW / HP;
+  AttnParams p = p0;
+  p.fwd_xcd = fwd_xcd_order();
   const int nqb = (p.Tq + BQ - 1) / BQ;
-  const dim3 grid(nqb * (p.Hq / HP) * p.B);
+  const int64_t nblk = static_cast<int64_t>(nqb) * (p.Hq / HP) * p.B;
+  if (fwd_persist(p.Tk) && nblk < (int64_t(1) << 30)) {
+    // one 8-wave workgroup per CU (230 VGPRs: two waves per SIMD), never more than the blocks
+    const int grid = static_cast<int>(std::min<int64_t>(nblk, device_cus()));
+    if (causal) attn_fwd_persist_kernel<D, true, NW, HP><<<grid, 64 * NW, 0, st>>>(p, static_cast<int>(nblk));
+    else attn_fwd_persist_kernel<D, false, NW, HP><<<grid, 64 * NW, 0, st>>>(p, static_cast<int>(nblk));
+    return;
+  }
+  const dim3 grid(static_cast<unsigned>(nblk));
   if (causal) attn_fwd_kernel<D, true, NW, HP><<<grid, 64 * NW, 0, st>>>(p);
   else attn_fwd_kernel<D, false, NW, HP><<<grid, 64 * NW, 0, st>>>(p);
 }

@@ -30,6 +30,10 @@ struct AttnParams {
   const int* rope_pos;    // [B * T] token positions, or null: position = t
   bf16_t* q_rot;          // optional [B, T, Hq, D] out: the rotated Q (what the backward reads)
   int64_t qr_sb, qr_st, qr_sh;
+  // forward block order (set by the launcher): 1 = XCD-grouped, each XCD walks whole (batch,
+  // head block) query columns so the concurrent workgroups of one L2 share every K/V tile
+  int fwd_xcd;
+  unsigned long long* stamps;  // debug (DLA_ATTN_STAMPS=1): persistent forward seam stamps
 };
 
 // Backward geometry: one workgroup per (256-key block, GQA head subset, kv head, batch);

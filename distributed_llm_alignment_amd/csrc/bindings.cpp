@@ -367,6 +367,16 @@ static void rope_args(const c10::optional<at::Tensor>& rope_cos, const c10::opti
   *sin_p = rope_sin->data_ptr<float>();
 }
 
+static at::Tensor& attn_stamp_buffer() {
+  static at::Tensor buf;
+  return buf;
+}
+
+at::Tensor attn_stamps(const at::Tensor& like) {
+  (void)like;
+  return attn_stamp_buffer().defined() ? attn_stamp_buffer().clone() : at::Tensor();
+}
+
 std::tuple<at::Tensor, at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k,
                                             const at::Tensor& v, double scale, bool causal,
                                             int64_t causal_off, int64_t window,
@@ -421,6 +431,16 @@ std::tuple<at::Tensor, at::Tensor> attn_fwd(const at::Tensor& q, const at::Tenso
     same_device(q, *q_rot);
     p.q_rot = bp(*q_rot);
     p.qr_sb = q_rot->stride(0); p.qr_st = q_rot->stride(1); p.qr_sh = q_rot->stride(2);
+  }
+  static const bool stamps = [] {
+    const char* e = std::getenv("DLA_ATTN_STAMPS");
+    return e != nullptr && std::atoi(e) == 1;
+  }();
+  if (stamps) {  // debug: read back with attn_stamps()
+    auto& buf = attn_stamp_buffer();
+    if (!buf.defined() || buf.device() != q.device())
+      buf = at::zeros({1024 * 8 * 4}, q.options().dtype(at::kLong));
+    p.stamps = reinterpret_cast<unsigned long long*>(buf.data_ptr<int64_t>());
   }
   launch_attn_fwd(p, static_cast<int>(D), causal, cur_stream(q));
   return {o, lse2};
@@ -873,6 +893,7 @@ TORCH_LIBRARY(dla, m) {
   m.def("rope_bwd(Tensor dq, Tensor dk, Tensor(a!) dqkv, Tensor cos, Tensor sin, Tensor? pos, int Hq, int Hkv, int D, int rot, int T, int pos_offset) -> ()");
   m.def("attn_fwd(Tensor q, Tensor k, Tensor v, float scale, bool causal, int causal_off, int window, Tensor? kv_start, Tensor? kv_end, Tensor? segs=None, Tensor? rope_cos=None, Tensor? rope_sin=None, Tensor? rope_pos=None, Tensor(a!)? q_rot=None) -> (Tensor, Tensor)");
   m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse2, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, float scale, bool causal, int causal_off, int window, Tensor? kv_start, Tensor? kv_end, Tensor? segs=None, Tensor? rope_cos=None, Tensor? rope_sin=None, Tensor? rope_pos=None, bool rope_inputs=False) -> ()");
+  m.def("attn_stamps(Tensor like) -> Tensor");
   m.def("transpose_bf16(Tensor input, Tensor(a!) out) -> ()");
   m.def("logprob_fwd(Tensor logits, Tensor targets, int vocab_offset=0) -> (Tensor, Tensor)");
   m.def("logprob_bwd(Tensor(a!) logits, Tensor targets, Tensor lse, Tensor grad, int vocab_offset=0) -> ()");
@@ -904,6 +925,7 @@ TORCH_LIBRARY_IMPL(dla, CUDA, m) {
   m.impl("rope_bwd", &dla::rope_bwd);
   m.impl("attn_fwd", &dla::attn_fwd);
   m.impl("attn_bwd", &dla::attn_bwd);
+  m.impl("attn_stamps", &dla::attn_stamps);
   m.impl("transpose_bf16", &dla::transpose_bf16);
   m.impl("logprob_fwd", &dla::logprob_fwd);
   m.impl("logprob_bwd", &dla::logprob_bwd);

@@ -939,3 +939,77 @@ def test_attention_bwd_bf16_partials_long_context(T, monkeypatch):
         e32, e16 = errs["0"][i], errs["1"][i]
         assert e16 < 2e-2, (name, T, errs)
         assert e16 <= 1.5 * e32 + 2e-3, (name, T, errs)
+
+
+# ------------------------------------------------------------------ persistent attention forward
+@pytest.mark.parametrize("case", ["dpo_shape", "d64_noncausal", "d80_window", "pads_segs", "decode_off",
+                                  "mha_small", "rope_on_load", "ragged_rounds"])
+def test_attention_fwd_persistent_bitwise(case, monkeypatch):
+    """attn_fwd_persist_kernel (one workgroup per CU, Q by LDS-DMA, K/V staged across block seams)
+    against the one-block-per-workgroup attn_fwd_kernel on the same inputs: O and the log2 LSE
+    bitwise equal (same tile math, same order), over masks, head dims, GQA packings, segment
+    bounds, RoPE on load and grids with several uneven snake rounds."""
+    from distributed_llm_alignment_amd.models.transformer import packed_layout
+
+    B, Tq, Tk, Hq, Hkv, D = 2, 200, 200, 8, 2, 128
+    causal, off, window, ks, ke, segs, rope = True, 0, 0, None, None, None, False
+    if case == "dpo_shape":
+        B, Tq, Tk, Hq, Hkv = 8, 1024, 1024, 32, 8
+    elif case == "d64_noncausal":
+        D, causal, Tq, Tk = 64, False, 333, 333
+    elif case == "d80_window":
+        D, window, Tq, Tk, Hq, Hkv = 80, 48, 300, 300, 32, 32
+    elif case == "pads_segs":
+        Tq = Tk = 700
+        ks = torch.tensor([0, 77], device=DEV, dtype=torch.int32)
+        ke = torch.tensor([700, 640], device=DEV, dtype=torch.int32)
+        seg = torch.zeros(B, Tq, dtype=torch.long, device=DEV)
+        for b, bd in enumerate([[0, 37, 300, 301, 520, 700], [0, 250, 256, 640]]):
+            for j in range(len(bd) - 1):
+                seg[b, bd[j]:bd[j + 1]] = j + 1
+        segs = packed_layout(seg)[1]
+    elif case == "decode_off":
+        B, Tq, Tk = 3, 5, 300
+        off = Tk - Tq
+        ks = torch.tensor([0, 10, 33], device=DEV, dtype=torch.int32)
+    elif case == "mha_small":
+        B, Tq, Tk, Hq, Hkv = 1, 70, 70, 4, 4
+    elif case == "rope_on_load":
+        B, Tq, Tk, Hq, Hkv = 4, 512, 512, 16, 4
+        rope = True
+    elif case == "ragged_rounds":  # 3 heads-blocks x 13 query blocks x 9 batches: uneven rounds
+        B, Tq, Tk, Hq, Hkv = 9, 800, 800, 12, 3
+    q = bf(torch.randn(B, Tq, Hq, D))
+    k = bf(torch.randn(B, Tk, Hkv, D))
+    v = bf(torch.randn(B, Tk, Hkv, D))
+    C = _ext.require()
+    extra = ()
+    if rope:
+        cos, sin = RotaryCache(D, 500000.0, 4096).tables(q.device)
+        extra = (cos, sin, None)
+    outs = {}
+    # (ping-pong, persistent, XCD block order): "000" is the one-block-per-workgroup lockstep kernel
+    for pp, persist, xcd in (("0", "0", "0"), ("0", "0", "1"), ("0", "1", "0"), ("0", "1", "1"),
+                             ("1", "0", "0"), ("1", "0", "1")):
+        monkeypatch.setenv("DLA_ATTN_FWD_PP", pp)
+        monkeypatch.setenv("DLA_ATTN_FWD_PERSIST", persist)
+        monkeypatch.setenv("DLA_ATTN_FWD_XCD", xcd)
+        qr = torch.empty_like(q) if rope else None
+        o, lse = C.attn_fwd(q, k, v, 1.0 / math.sqrt(D), causal, off, window, ks, ke, segs, *extra,
+                            *((qr,) if rope else ()))
+        torch.cuda.synchronize()
+        outs[pp + persist + xcd] = (o, lse, qr)
+    o0, l0, q0 = outs["000"]
+    o1, l1, q1 = outs["011"]
+    for key in ("001", "010", "100", "101"):
+        ref_o, ref_l = (o1, l1) if key == "010" else (o0, l0)
+        assert torch.equal(outs[key][0], ref_o) and torch.equal(outs[key][1], ref_l), f"variant {key} changed O/LSE"
+    if rope:  # the rotation's a*c - b*s may contract to different FMAs in the two kernels
+        assert rel_err(o1, o0) < 5e-3 and rel_err(q1, q0) < 5e-3, "RoPE-on-load output differs"
+        assert (l1 - l0).abs().max().item() < 5e-2, "LSE differs"
+        return
+    assert torch.equal(o0, o1), "O differs"
+    assert torch.equal(l0, l1), "LSE differs"
+    r = ref_attention(q.float(), k.float(), v.float(), 1 / math.sqrt(D), causal, off, window, ks, ke, segs)
+    valid = torch.isfinite(l1).transpose(1, 2).unsqueeze(-1)  # [B, Tq, Hq, 1]: rows that see a key
+    assert rel_err(o1 * valid, r * valid) < 2e-2
