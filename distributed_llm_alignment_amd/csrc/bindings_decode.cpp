@@ -66,6 +66,10 @@ int m64_splits(int N, int K);
 void launch_tile_weight(const bf16_t*, int64_t, const bf16_t*, bf16_t*, int, int, bool, hipStream_t);
 void launch_skinny_glu_il(const bf16_t*, int64_t, const bf16_t*, bf16_t*, int64_t, int, int, int,
                           const KsFuse&, hipStream_t);
+void launch_skinny_ks_fused_f8(const bf16_t*, int64_t, const uint8_t*, bf16_t*, int64_t, int, int, int,
+                               const KsFuse&, bool, bool, hipStream_t);
+void launch_skinny_glu_il_f8(const bf16_t*, int64_t, const uint8_t*, bf16_t*, int64_t, int, int, int,
+                             const KsFuse&, hipStream_t);
 bool m64_shape_ok(int N, int K, bool glu);
 void launch_m64_gemm(const bf16_t*, int64_t, const bf16_t*, int64_t, bf16_t*, int64_t, float*, int,
                      int, int, int, bool, const float*, int, float, bool, hipStream_t);
@@ -201,6 +205,94 @@ at::Tensor skinny_glu_il(const at::Tensor& x, const at::Tensor& wt, const at::Te
   auto m = at::empty({M, N / 2}, x.options());
   launch_skinny_glu_il(cbp(x), x.stride(0), cbp(wt), bp(m), m.stride(0), (int)M, (int)N, (int)K, fz,
                        cur_stream(x));
+  return m;
+}
+
+// fp8 weight-only decode projections (ops/decode.py fp8_tiled_weight): w8 = e4m3 tiled copy
+// [N/16, K/64, 64, 16] (uint8 storage), wscale [N] fp32 per weight row; otherwise skinny_fused /
+// skinny_glu_il (res: o / down producing the residual; ssq_in: qkv / gate|up on a normalised input).
+static void check_w8(const at::Tensor& w8, const at::Tensor& wscale, const at::Tensor& x, int64_t* N,
+                     int64_t* K) {
+  check_cuda(w8, "w8");
+  TORCH_CHECK(w8.scalar_type() == at::kByte && w8.dim() == 4 && w8.size(2) == 64 && w8.size(3) == 16 &&
+                  w8.is_contiguous(),
+              "w8 uint8 [N/16, K/64, 64, 16] contiguous");
+  *N = w8.size(0) * 16;
+  *K = w8.size(1) * 64;
+  check_cuda(wscale, "wscale");
+  TORCH_CHECK(wscale.scalar_type() == at::kFloat && wscale.dim() == 1 && wscale.size(0) == *N &&
+                  wscale.is_contiguous(),
+              "wscale fp32 [N] contiguous");
+  check_aligned16(w8, "w8");
+  same_device(x, w8);
+  same_device(x, wscale);
+}
+
+static void check_ssq(const at::Tensor& sq, const at::Tensor& x, KsFuse* fz, double eps) {
+  check_cuda(sq, "ssq_in");
+  TORCH_CHECK(sq.scalar_type() == at::kFloat && sq.dim() == 2 && sq.size(0) == 16 && sq.is_contiguous() &&
+                  sq.size(1) >= 1 && sq.size(1) <= 512,
+              "ssq_in fp32 [16, nbp <= 512] contiguous");
+  same_device(x, sq);
+  fz->ssq_in = sq.data_ptr<float>();
+  fz->nbp = static_cast<int>(sq.size(1));
+  fz->eps = static_cast<float>(eps);
+}
+
+std::tuple<at::Tensor, at::Tensor> skinny_fused_f8(const at::Tensor& x, const at::Tensor& w8,
+                                                   const at::Tensor& wscale,
+                                                   const c10::optional<at::Tensor>& res,
+                                                   const c10::optional<at::Tensor>& ssq_in, double eps) {
+  check_bf16(x, "x");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0, "x [M, K], 16-byte aligned rows");
+  int64_t N = 0, K = 0;
+  check_w8(w8, wscale, x, &N, &K);
+  const int64_t M = x.size(0);
+  TORCH_CHECK(M >= 1 && M <= 16 && x.size(1) == K, "fp8 skinny: 1 <= M <= 16, x [M, K]");
+  TORCH_CHECK(N < (1ll << 30) && K < (1ll << 30) && skinny_use_ksplit((int)N, (int)K),
+              "fp8 skinny: N < 16384, N % 16 == 0, K % 1024 == 0");
+  check_aligned16(x, "x");
+  KsFuse fz{};
+  fz.wscale = wscale.data_ptr<float>();
+  const bool nin = ssq_in.has_value();
+  if (nin) check_ssq(*ssq_in, x, &fz, eps);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  auto y = at::empty({M, N}, x.options());
+  at::Tensor ssq;
+  if (res.has_value()) {
+    const at::Tensor& r = *res;
+    check_bf16(r, "res");
+    TORCH_CHECK(r.dim() == 2 && r.size(0) == M && r.size(1) == N && r.stride(1) == 1, "res [M, N]");
+    same_device(x, r);
+    fz.res = cbp(r);
+    fz.ldr = r.stride(0);
+    ssq = at::empty({16, N / 16}, x.options().dtype(at::kFloat));
+    fz.ssq_out = ssq.data_ptr<float>();
+  }
+  launch_skinny_ks_fused_f8(cbp(x), x.stride(0), w8.data_ptr<uint8_t>(), bp(y), y.stride(0), (int)M, (int)N,
+                            (int)K, fz, res.has_value(), nin, cur_stream(x));
+  return {y, ssq};
+}
+
+at::Tensor skinny_glu_il_f8(const at::Tensor& x, const at::Tensor& w8, const at::Tensor& wscale,
+                            const at::Tensor& ssq_in, double eps) {
+  check_bf16(x, "x");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0, "x [M, K]");
+  int64_t N = 0, K = 0;
+  check_w8(w8, wscale, x, &N, &K);
+  const int64_t M = x.size(0);
+  TORCH_CHECK(M >= 1 && M <= 16 && x.size(1) == K, "fp8 glu: 1 <= M <= 16, x [M, K]");
+  TORCH_CHECK(K % 512 == 0 && N % 32 == 0 && N < (1ll << 30) && K < (1ll << 30) &&
+                  M * (K + 8) * 2 <= 148 * 1024,
+              "fp8 glu: K % 512 == 0, 2F % 32 == 0, x fits LDS");
+  check_aligned16(x, "x");
+  KsFuse fz{};
+  fz.wscale = wscale.data_ptr<float>();
+  check_ssq(ssq_in, x, &fz, eps);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  auto m = at::empty({M, N / 2}, x.options());
+  launch_skinny_glu_il_f8(cbp(x), x.stride(0), w8.data_ptr<uint8_t>(), bp(m), m.stride(0), (int)M, (int)N,
+                          (int)K, fz, cur_stream(x));
   return m;
 }
 
@@ -878,6 +970,8 @@ TORCH_LIBRARY_FRAGMENT(dla, m) {
   m.def("skinny64(Tensor x, Tensor w, Tensor? res, Tensor? ssq_in, float eps, bool glu) -> (Tensor, Tensor)");
   m.def("tile_weight(Tensor w, Tensor? nw, Tensor(a!) out, bool glu_il=False) -> ()");
   m.def("skinny_glu_il(Tensor x, Tensor wt, Tensor ssq_in, float eps) -> Tensor");
+  m.def("skinny_fused_f8(Tensor x, Tensor w8, Tensor wscale, Tensor? res, Tensor? ssq_in, float eps) -> (Tensor, Tensor)");
+  m.def("skinny_glu_il_f8(Tensor x, Tensor w8, Tensor wscale, Tensor ssq_in, float eps) -> Tensor");
   m.def("decode_tail_stamps(Tensor like) -> Tensor");
   m.def("decode_tail(Tensor a, Tensor x, Tensor wo, Tensor wgu, Tensor wd, Tensor? wq, float eps, Tensor(a!) cnt, Tensor kv_len, Tensor len_first, Tensor(b!) err) -> (Tensor, Tensor, Tensor)");
 }
@@ -897,6 +991,8 @@ TORCH_LIBRARY_IMPL(dla, CUDA, m) {
   m.impl("skinny64", &dla::skinny64);
   m.impl("tile_weight", &dla::tile_weight);
   m.impl("skinny_glu_il", &dla::skinny_glu_il);
+  m.impl("skinny_fused_f8", &dla::skinny_fused_f8);
+  m.impl("skinny_glu_il_f8", &dla::skinny_glu_il_f8);
   m.impl("decode_tail", &dla::decode_tail);
   m.impl("decode_tail_stamps", &dla::decode_tail_stamps);
 }

@@ -422,17 +422,18 @@ void launch_skinny_gemm(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t l
 // per ring slot (4 at MT = 1; 2 above, which keeps the x fragments at ~110 VGPRs for MT = 4, four
 // waves per SIMD).
 template <int DEPTH, bool NT, bool GLU, int MT = 1, int UNR = kKsUnroll, bool RES = false, bool NIN = false,
-          bool TW = false>
+          bool TW = false, bool F8 = false>
 __global__ __launch_bounds__(512) void skinny_ksplit_kernel(
     const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ W, int64_t ldw,
     bf16_t* __restrict__ y, int64_t ldy, int M, int N, int K, KsFuse fz = KsFuse{}) {
-  ks_body<DEPTH, NT, GLU, MT, UNR, RES, NIN, TW>(blockIdx.x, gridDim.x, x, ldx, W, ldw, y, ldy, M, N, K, fz);
+  ks_body<DEPTH, NT, GLU, MT, UNR, RES, NIN, TW, false, F8>(blockIdx.x, gridDim.x, x, ldx, W, ldw, y, ldy, M,
+                                                             N, K, fz);
 }
 
 // fused decode-layer launches (KsFuse): the residual-producing projection and the
 // norm-consuming qkv projection on the in-workgroup split-K kernel, the gate|up GLU on the LDS
 // kernel. M <= 16.
-template <bool TW, bool NT>
+template <bool TW, bool NT, bool F8 = false>
 static void launch_ks_fused_t(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
                               int64_t ldy, int M, int N, int K, const KsFuse& fz, bool res, bool nin,
                               hipStream_t st) {
@@ -442,7 +443,7 @@ static void launch_ks_fused_t(const bf16_t* x, int64_t ldx, const bf16_t* W, int
   }();
   const int nb = N / 16;
   const bool deep = K >= deep_k;
-#define DLA_KSF(D, R, NI) skinny_ksplit_kernel<D, NT, false, 1, kKsUnroll, R, NI, TW><<<nb, 512, 0, st>>>(x, ldx, W, ldw, y, ldy, M, N, K, fz)
+#define DLA_KSF(D, R, NI) skinny_ksplit_kernel<D, NT, false, 1, kKsUnroll, R, NI, TW, F8><<<nb, 512, 0, st>>>(x, ldx, W, ldw, y, ldy, M, N, K, fz)
   if (res && nin) {
     if (deep) DLA_KSF(4, true, true); else DLA_KSF(2, true, true);
   } else if (res) {
@@ -463,6 +464,28 @@ void launch_skinny_ks_fused(const bf16_t* x, int64_t ldx, const bf16_t* W, int64
   if (tiled && decode_nt()) launch_ks_fused_t<true, true>(x, ldx, W, ldw, y, ldy, M, N, K, fz, res, nin, st);
   else if (tiled) launch_ks_fused_t<true, false>(x, ldx, W, ldw, y, ldy, M, N, K, fz, res, nin, st);
   else launch_ks_fused_t<false, false>(x, ldx, W, ldw, y, ldy, M, N, K, fz, res, nin, st);
+}
+
+// fp8 weights (e4m3 tiled copy + per-row scales in fz.wscale, ks_body F8): the o / down / qkv
+// projections of the decode layer at half the weight bytes. The ring keeps the bf16 kernel's
+// chunk count in flight, i.e. half its bytes: a 4-deep ring everywhere.
+void launch_skinny_ks_fused_f8(const bf16_t* x, int64_t ldx, const uint8_t* W8, bf16_t* y, int64_t ldy,
+                               int M, int N, int K, const KsFuse& fz, bool res, bool nin, hipStream_t st) {
+  const bf16_t* W = reinterpret_cast<const bf16_t*>(W8);
+  const int nb = N / 16;
+#define DLA_KSF8(NTV, R, NI) skinny_ksplit_kernel<4, NTV, false, 1, kKsUnroll, R, NI, true, true><<<nb, 512, 0, st>>>(x, ldx, W, K, y, ldy, M, N, K, fz)
+  if (decode_nt()) {
+    if (res && nin) DLA_KSF8(true, true, true);
+    else if (res) DLA_KSF8(true, true, false);
+    else if (nin) DLA_KSF8(true, false, true);
+    else DLA_KSF8(true, false, false);
+  } else {
+    if (res && nin) DLA_KSF8(false, true, true);
+    else if (res) DLA_KSF8(false, true, false);
+    else if (nin) DLA_KSF8(false, false, true);
+    else DLA_KSF8(false, false, false);
+  }
+#undef DLA_KSF8
 }
 
 template <bool TW, bool NT>
@@ -495,7 +518,10 @@ void launch_skinny_glu_normin(const bf16_t* x, int64_t ldx, const bf16_t* W, int
 // workgroups at Llama-3-8B (F = 14336: 1792 tiles), where the 8-wave gate|up kernel
 // (skinny_gemm_kernel GLU_OUT) runs 224 and leaves 32 CUs idle. Same K order, rstd and bf16
 // rounding as that kernel: bitwise the same output.
-template <int DEPTH>
+// F8: Wt is the e4m3 interleaved tiled copy [2F/16, K/64, 64, 16 B] (ks_body F8 layout) and
+// fz.wscale the per-row scales in the same interleaved row order; one 1-KB wave load feeds two
+// k-steps, so a ring slot of kSkUnroll k-steps is kSkUnroll / 2 loads.
+template <int DEPTH, bool F8 = false>
 __global__ __launch_bounds__(512) void skinny_glu_il_kernel(const bf16_t* __restrict__ x, int64_t ldx,
                                                            const bf16_t* __restrict__ Wt,
                                                            bf16_t* __restrict__ y, int64_t ldy, int M,
@@ -509,17 +535,27 @@ __global__ __launch_bounds__(512) void skinny_glu_il_kernel(const bf16_t* __rest
   const bool active = t < ntiles;
   const int ldl = K + 8;
   const bf16_t* wrow = Wt + static_cast<int64_t>(active ? t : 0) * 16 * K + lane * 8;
+  const uint8_t* wrow8 = reinterpret_cast<const uint8_t*>(Wt) + static_cast<int64_t>(active ? t : 0) * 16 * K +
+                         lane * 16;
+  constexpr int UB = F8 ? kSkUnroll / 2 : kSkUnroll;  // wave loads per ring slot
   const int nchunks = K / kSkChunk;
-  // DEPTH chunks of kSkUnroll 1 KB wave loads in flight (a ring of register sets)
-  s16x8 b[DEPTH][kSkUnroll];
+  // DEPTH chunks of kSkUnroll k-steps in flight (a ring of register sets)
+  s16x8 b[DEPTH][F8 ? 1 : kSkUnroll];
+  ks_u32x4 b8[DEPTH][F8 ? UB : 1];
+  auto wload = [&](int j, int c) {
+    if constexpr (F8) {
+#pragma unroll
+      for (int u = 0; u < UB; ++u) b8[j][u] = *reinterpret_cast<const ks_u32x4*>(wrow8 + (c * UB + u) * 1024);
+    } else {
+#pragma unroll
+      for (int u = 0; u < kSkUnroll; ++u)
+        b[j][u] = __builtin_bit_cast(s16x8, load_bf16x8(wrow + (c * kSkUnroll + u) * 512));
+    }
+  };
   if (active) {
 #pragma unroll
     for (int j = 0; j < DEPTH; ++j)
-      if (j < nchunks) {
-#pragma unroll
-        for (int u = 0; u < kSkUnroll; ++u)
-          b[j][u] = __builtin_bit_cast(s16x8, load_bf16x8(wrow + (j * kSkUnroll + u) * 512));
-      }
+      if (j < nchunks) wload(j, j);
   }
   // this wave's rows' norm partials (rows wave, wave + nwv, ...: 4 cover M <= 16 at >= 4 waves),
   // reduced after the main loop
@@ -559,12 +595,19 @@ __global__ __launch_bounds__(512) void skinny_glu_il_kernel(const bf16_t* __rest
   if (active) {
     const bf16_t* xrow = xs + r * ldl + q * 8;
     const bool arow = r < M;
-    auto compute = [&](const s16x8* b, int kk) {
+    auto compute = [&](int j, int kk) {
 #pragma unroll
       for (int u = 0; u < kSkUnroll; ++u) {
         s16x8 a = {0, 0, 0, 0, 0, 0, 0, 0};
         if (arow) a = __builtin_bit_cast(s16x8, load_bf16x8(xrow + kk + u * 32));
-        acc = mfma16(a, b[u], acc);
+        s16x8 bu;
+        if constexpr (F8) {
+          const ks_u32x4 wv = b8[j][u >> 1];
+          bu = (u & 1) ? f8x8_to_bf16(wv[2], wv[3]) : f8x8_to_bf16(wv[0], wv[1]);
+        } else {
+          bu = b[j][u];
+        }
+        acc = mfma16(a, bu, acc);
       }
     };
     for (int c0 = 0; c0 < nchunks; c0 += DEPTH) {
@@ -572,12 +615,8 @@ __global__ __launch_bounds__(512) void skinny_glu_il_kernel(const bf16_t* __rest
       for (int j = 0; j < DEPTH; ++j) {
         const int c = c0 + j;
         if (c < nchunks) {
-          compute(b[j], c * kSkChunk);
-          if (c + DEPTH < nchunks) {
-#pragma unroll
-            for (int u = 0; u < kSkUnroll; ++u)
-              b[j][u] = __builtin_bit_cast(s16x8, load_bf16x8(wrow + ((c + DEPTH) * kSkUnroll + u) * 512));
-          }
+          compute(j, c * kSkChunk);
+          if (c + DEPTH < nchunks) wload(j, c + DEPTH);
         }
       }
     }
@@ -595,10 +634,11 @@ __global__ __launch_bounds__(512) void skinny_glu_il_kernel(const bf16_t* __rest
   __syncthreads();
   if (!active) return;
   // lane holds C[m = 4q + i][row r of the tile]: gate (r < 8) and up (r >= 8) of feature 8t + (r & 7)
+  const float wsc = F8 ? fz.wscale[16 * t + r] : 1.f;  // this lane's weight row (interleaved order)
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int m = 4 * q + i;
-    const float v = bf2f(f2bf(acc[i] * (m < M ? rstd_s[m] : 0.f)));
+    const float v = bf2f(f2bf((F8 ? acc[i] * wsc : acc[i]) * (m < M ? rstd_s[m] : 0.f)));
     const float o = __shfl_xor(v, 8, 64);
     if (r < 8 && m < M) y[m * ldy + 8 * t + r] = f2bf(silu_sk(v) * o);
   }
@@ -606,18 +646,29 @@ __global__ __launch_bounds__(512) void skinny_glu_il_kernel(const bf16_t* __rest
 
 // gate|up over the interleaved tiled weight (2F rows -> [M, F]); waves per workgroup: the largest
 // of 8..4 dividing the tile count with >= 256 workgroups, else 8
-template <int DEPTH>
+template <int DEPTH, bool F8 = false>
 static void launch_glu_il_d(const bf16_t* x, int64_t ldx, const bf16_t* Wt, bf16_t* y, int64_t ldy, int M,
                             int ntiles, int K, const KsFuse& fz, int w, hipStream_t st) {
   static bool attr_set = [] {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_glu_il_kernel<DEPTH>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_glu_il_kernel<DEPTH, F8>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
     (void)hipGetLastError();
     return true;
   }();
   (void)attr_set;
-  skinny_glu_il_kernel<DEPTH><<<(ntiles + w - 1) / w, 64 * w, skinny_lds_bytes(M, K), st>>>(x, ldx, Wt, y, ldy,
-                                                                                          M, ntiles, K, fz);
+  skinny_glu_il_kernel<DEPTH, F8><<<(ntiles + w - 1) / w, 64 * w, skinny_lds_bytes(M, K), st>>>(
+      x, ldx, Wt, y, ldy, M, ntiles, K, fz);
+}
+
+// fp8 gate|up (interleaved e4m3 tiled copy, fz.wscale): the ring keeps 4 slots of half-size loads
+void launch_skinny_glu_il_f8(const bf16_t* x, int64_t ldx, const uint8_t* Wt8, bf16_t* y, int64_t ldy,
+                             int M, int N, int K, const KsFuse& fz, hipStream_t st) {
+  const int ntiles = N / 16;
+  int w = 8;
+  for (int c : {8, 7, 6, 5, 4}) {
+    if (ntiles % c == 0 && ntiles / c >= 256) { w = c; break; }
+  }
+  launch_glu_il_d<4, true>(x, ldx, reinterpret_cast<const bf16_t*>(Wt8), y, ldy, M, ntiles, K, fz, w, st);
 }
 
 void launch_skinny_glu_il(const bf16_t* x, int64_t ldx, const bf16_t* Wt, bf16_t* y, int64_t ldy, int M,

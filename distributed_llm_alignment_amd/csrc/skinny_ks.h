@@ -68,14 +68,40 @@ constexpr int kKsChunk = 32 * kKsUnroll;
 // consumer in another workgroup of the same launch that reads it with `sc1` loads after a counter
 // hand-off (decode.hip decode_qkv_attn_kernel; MI355X_MICROARCH inter-workgroup visibility, the
 // release-free valid form)
+// e4m3 -> bf16, 8 values from two dwords (exact: every e4m3 value is a bf16 value); the per-row
+// dequantisation scale is applied to the fp32 sum in the epilogue
+__device__ __forceinline__ s16x8 f8x8_to_bf16(uint32_t w0, uint32_t w1) {
+  typedef short s16x2v __attribute__((ext_vector_type(2)));
+  const s16x2v a = __builtin_bit_cast(s16x2v, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w0, 1.0f, false));
+  const s16x2v b = __builtin_bit_cast(s16x2v, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w0, 1.0f, true));
+  const s16x2v c = __builtin_bit_cast(s16x2v, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w1, 1.0f, false));
+  const s16x2v d = __builtin_bit_cast(s16x2v, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w1, 1.0f, true));
+  return s16x8{a[0], a[1], b[0], b[1], c[0], c[1], d[0], d[1]};
+}
+
+typedef uint32_t ks_u32x4 __attribute__((ext_vector_type(4)));
+
+template <bool NT>
+__device__ __forceinline__ ks_u32x4 load_w8(const uint8_t* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const ks_u32x4*>(p));
+  else return *reinterpret_cast<const ks_u32x4*>(p);
+}
+
+// F8 (decode weight-only fp8, TW only): W points at an e4m3 tiled copy [N/16, K/64, 64 lanes, 16 B]:
+// lane r + 16q of k-tile kt holds row r's k = 64kt + 8q + [0, 8) in bytes 0-7 and
+// 64kt + 32 + 8q + [0, 8) in bytes 8-15, i.e. its B fragments of two consecutive MFMA k-steps, so
+// one 16-byte load feeds two MFMAs and the stream is half the bf16 bytes (ops/decode.py
+// fp8_tiled_weight); y[:, n] = wscale[n] * (x . w8[n]).
 template <int DEPTH, bool NT, bool GLU, int MT = 1, int UNR = kKsUnroll, bool RES = false, bool NIN = false,
-          bool TW = false, bool WT = false>
+          bool TW = false, bool WT = false, bool F8 = false>
 __device__ __forceinline__ void ks_body(
     const int bx, const int nblk, const bf16_t* __restrict__ x, int64_t ldx,
     const bf16_t* __restrict__ W, int64_t ldw, bf16_t* __restrict__ y, int64_t ldy, int M, int N, int K,
     const KsFuse& fz) {
   constexpr int CH = 32 * UNR;  // k per ring slot
   static_assert(!(RES || NIN) || (MT == 1 && !GLU), "fused residual / norm: M <= 16, plain output");
+  static_assert(!F8 || (TW && !GLU && !WT && MT == 1 && UNR % 2 == 0), "fp8 weights: tiled, plain rows");
+  constexpr int UB = F8 ? UNR / 2 : UNR;  // weight loads per ring slot
   __shared__ float red[8][4 * MT][64];
   __shared__ float rstd_s[16];
   __shared__ float sqs[16][16];
@@ -89,6 +115,8 @@ __device__ __forceinline__ void ks_body(
   // TW: tiled weight layout (see skinny_gemm_kernel)
   const bf16_t* wrow = TW ? W + static_cast<int64_t>(n0 >> 4) * 16 * K + (k0 >> 5) * 512 + lane * 8
                           : W + static_cast<int64_t>(n0 + r) * ldw + k0 + q * 8;
+  const uint8_t* wrow8 = reinterpret_cast<const uint8_t*>(W) + static_cast<int64_t>(n0 >> 4) * 16 * K +
+                         (k0 >> 6) * 1024 + lane * 16;
   bool arow[MT];
   const bf16_t* xrow[MT];
 #pragma unroll
@@ -97,10 +125,16 @@ __device__ __forceinline__ void ks_body(
     xrow[t] = x + static_cast<int64_t>(arow[t] ? 16 * t + r : 0) * ldx + k0 + q * 8;
   }
   // DEPTH chunks (W and x fragments) in flight: a ring of register sets, refilled as consumed
-  s16x8 b[DEPTH][UNR], a[DEPTH][UNR][MT];
+  s16x8 b[DEPTH][F8 ? 1 : UNR], a[DEPTH][UNR][MT];
+  ks_u32x4 b8[DEPTH][F8 ? UB : 1];
   auto load = [&](int j, int c) {
+    if constexpr (F8) {
 #pragma unroll
-    for (int u = 0; u < UNR; ++u) b[j][u] = load_w<NT>(TW ? wrow + (c * UNR + u) * 512 : wrow + c * CH + u * 32);
+      for (int u = 0; u < UB; ++u) b8[j][u] = load_w8<NT>(wrow8 + (c * UB + u) * 1024);
+    } else {
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) b[j][u] = load_w<NT>(TW ? wrow + (c * UNR + u) * 512 : wrow + c * CH + u * 32);
+    }
 #pragma unroll
     for (int u = 0; u < UNR; ++u)
 #pragma unroll
@@ -123,9 +157,17 @@ __device__ __forceinline__ void ks_body(
       const int c = c0 + j;
       if (c < nchunks) {
 #pragma unroll
-        for (int u = 0; u < UNR; ++u)
+        for (int u = 0; u < UNR; ++u) {
+          s16x8 bu;
+          if constexpr (F8) {
+            const ks_u32x4 wv = b8[j][u >> 1];
+            bu = (u & 1) ? f8x8_to_bf16(wv[2], wv[3]) : f8x8_to_bf16(wv[0], wv[1]);
+          } else {
+            bu = b[j][u];
+          }
 #pragma unroll
-          for (int t = 0; t < MT; ++t) acc[t] = mfma16(a[j][u][t], b[j][u], acc[t]);
+          for (int t = 0; t < MT; ++t) acc[t] = mfma16(a[j][u][t], bu, acc[t]);
+        }
         if (c + DEPTH < nchunks) load(j, c + DEPTH);
       }
     }
@@ -179,6 +221,7 @@ __device__ __forceinline__ void ks_body(
       float t = 0.f;
 #pragma unroll
       for (int w = 0; w < 8; ++w) t += red[w][ti][l];
+      if constexpr (F8) t *= fz.wscale[n];
       if constexpr (NIN) t *= m < M ? rstd_s[m] : 0.f;
       if constexpr (RES) {
         if (m < M) {

@@ -12,6 +12,7 @@ struct KsFuse {
   const float* ssq_in;   // NIN: [16][nbp] partial sums of squares of x's rows (nbp <= 512)
   int nbp;
   float eps;             // NIN: RMSNorm epsilon (the norm weight is folded into W by the caller)
+  const float* wscale;   // F8 weights: per weight-row dequantisation scale (y[:, n] *= wscale[n])
 };
 
 }  // namespace dla

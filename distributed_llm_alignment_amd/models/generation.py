@@ -355,7 +355,8 @@ def generate(model: CausalLM, input_ids: torch.Tensor, attention_mask: Optional[
              max_new_tokens: int = 256, do_sample: bool = True, temperature: float = 1.0,
              top_p: float = 1.0, top_k: int = 0, eos_token_id: Optional[int] = None,
              pad_token_id: Optional[int] = None, generator: Optional[torch.Generator] = None,
-             return_mask: bool = False, use_graph: Optional[bool] = None, seed: Optional[int] = None):
+             return_mask: bool = False, use_graph: Optional[bool] = None, seed: Optional[int] = None,
+             weight_dtype: str = "bf16"):
     """Left-padded prompts [B, Tp] -> sequences [B, Tp + n] (n <= max_new_tokens).
 
     With `return_mask`, also returns the attention mask of the full sequence (prompt mask, then
@@ -364,7 +365,23 @@ def generate(model: CausalLM, input_ids: torch.Tensor, attention_mask: Optional[
 
     On MI355X the prompt is prefilled with the flash-attention kernel, then every new token is
     ONE replay of a captured hipGraph (decode kernel + fused sampler, no host sync except an
-    all-finished check every 16 tokens). `use_graph=False` forces the eager per-op loop."""
+    all-finished check every 16 tokens). `use_graph=False` forces the eager per-op loop.
+
+    `weight_dtype="fp8"`: the decode steps' qkv / o / gate|up / down projections stream an e4m3
+    copy of the weights with per-row scales (ops.decode.fp8_weights; half the bytes of the
+    dominant weight streams). The prefill and the LM head stay bf16."""
+    if weight_dtype not in ("bf16", "fp8"):
+        raise ValueError(f"weight_dtype must be 'bf16' or 'fp8', got {weight_dtype!r}")
+    with ops.decode.fp8_weights(weight_dtype == "fp8" or ops.decode.fp8_enabled()):
+        return _generate(model, input_ids, attention_mask, max_new_tokens, do_sample, temperature, top_p,
+                         top_k, eos_token_id, pad_token_id, generator, return_mask, use_graph, seed)
+
+
+def _generate(model: CausalLM, input_ids: torch.Tensor, attention_mask: Optional[torch.Tensor],
+              max_new_tokens: int, do_sample: bool, temperature: float, top_p: float, top_k: int,
+              eos_token_id: Optional[int], pad_token_id: Optional[int],
+              generator: Optional[torch.Generator], return_mask: bool, use_graph: Optional[bool],
+              seed: Optional[int]):
     if DECODE_GATHER and model.layers_sharded():
         # ZeRO-3 policy: gather it once for the whole rollout (fused decode kernels + captured
         # graph) instead of an all-gather per layer per token
@@ -374,9 +391,9 @@ def generate(model: CausalLM, input_ids: torch.Tensor, attention_mask: Optional[
             with contextlib.ExitStack() as stack:
                 for eng in model.sharding_engines():
                     stack.enter_context(eng.gathered_for_inference())
-                return generate(model, input_ids, attention_mask, max_new_tokens, do_sample, temperature,
-                                top_p, top_k, eos_token_id, pad_token_id, generator, return_mask, use_graph,
-                                seed)
+                return _generate(model, input_ids, attention_mask, max_new_tokens, do_sample, temperature,
+                                 top_p, top_k, eos_token_id, pad_token_id, generator, return_mask, use_graph,
+                                 seed)
         finally:
             # the gathered units are freed on exit: the captured graph (it reads their addresses),
             # its KV cache and the derived decode weight copies (a second full set of layer
@@ -409,7 +426,7 @@ def generate(model: CausalLM, input_ids: torch.Tensor, attention_mask: Optional[
     if GRAPH_REUSE and use_graph is not False and max_new_tokens > 2 and input_ids.is_cuda \
             and _graph_capable(model):
         reuse_key = (B, Tp, max_new_tokens, kv_start is None, greedy, float(temperature), int(top_k),
-                     float(top_p), eos, pad, input_ids.device, _weights_key(model))
+                     float(top_p), eos, pad, input_ids.device, _weights_key(model), ops.decode.fp8_enabled())
         hit = _GRAPH_SLOT.get(id(model))
         if hit is not None and hit[0]() is model and hit[1] == reuse_key:
             cache, dg = hit[2], hit[3]

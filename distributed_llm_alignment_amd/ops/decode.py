@@ -352,7 +352,81 @@ def tiled_weight(w: torch.Tensor) -> torch.Tensor:
     return _cached(w, "_dla_tile", _wkey(w), make)
 
 
-DERIVED_ATTRS = ("_dla_fold", "_dla_fold_t", "_dla_fold_g", "_dla_tile")
+# ---------------------------------------------------------------------------------------------
+# Weight-only fp8 decode (opt-in): the fused decode layer's four weight streams (qkv, o, gate|up,
+# down: 74 % of the bytes per token at Llama-3-8B B=8) read an e4m3 copy with one fp32 scale per
+# weight row (amax / 448), half the bf16 bytes; activations, the KV cache, the LM head and every
+# accumulation stay bf16 / fp32 (csrc/skinny_ks.h F8, csrc/skinny.hip skinny_glu_il_kernel F8). For
+# RLHF rollouts (`generate(..., weight_dtype="fp8")`, `ppo.rollout_weight_dtype`): the update's
+# old-policy log-probs are recomputed in bf16 on the sampled tokens (training/train_rlhf.py), so
+# the fp8 copy only changes which tokens are sampled. DLA_DECODE_FP8=1 turns it on process-wide.
+_FP8 = [os.environ.get("DLA_DECODE_FP8", "0") == "1"]
+
+
+class fp8_weights:
+    """Context manager: decode projections on fp8 weight copies inside the block."""
+
+    def __init__(self, enabled: bool = True):
+        self.enabled = bool(enabled)
+
+    def __enter__(self):
+        self.prev = _FP8[0]
+        _FP8[0] = self.enabled
+        return self
+
+    def __exit__(self, *exc):
+        _FP8[0] = self.prev
+        return False
+
+
+def fp8_enabled() -> bool:
+    return _FP8[0]
+
+
+F8_MAX = 448.0  # largest finite e4m3 (OCP e4m3fn) value
+
+
+def quantize_rows_f8(src: torch.Tensor):
+    """src [N, K] -> (e4m3 values as uint8 [N, K], fp32 scales [N]): per-row amax scaling."""
+    a = src.float()
+    sc = (a.abs().amax(dim=1) / F8_MAX).clamp_min(1e-12)
+    q = (a / sc[:, None]).clamp_(-F8_MAX, F8_MAX).to(torch.float8_e4m3fn)
+    return q.view(torch.uint8), sc.contiguous()
+
+
+def tile_f8(q: torch.Tensor) -> torch.Tensor:
+    """uint8 [N, K] -> the F8 tiled layout [N/16, K/64, 64, 16]: lane r + 16 qd of k-tile kt holds
+    row r's k = 64 kt + 8 qd + [0, 8) then 64 kt + 32 + 8 qd + [0, 8) (csrc/skinny_ks.h F8)."""
+    N, K = q.shape
+    return (q.view(N // 16, 16, K // 64, 2, 4, 8).permute(0, 2, 4, 1, 3, 5)
+            .reshape(N // 16, K // 64, 64, 16).contiguous())
+
+
+def fp8_tiled_weight(w: torch.Tensor, norm_w: Optional[torch.Tensor] = None, glu_il: bool = False):
+    """Cached (e4m3 tiled copy, per-row scales) of W (o norm_w folded in; glu_il: gate / up rows
+    interleaved 8 + 8 per 16-row tile), refreshed when W or norm_w moved (as folded_weight)."""
+    def make(prev):
+        src = w.detach() if norm_w is None else w.detach() * norm_w.detach().view(1, -1)
+        if glu_il:
+            src = _glu_interleave(src)
+        q, sc = quantize_rows_f8(src)
+        t = tile_f8(q)
+        if prev is not None:  # in place: a captured decode graph keeps reading the same storage
+            prev[0].copy_(t)
+            prev[1].copy_(sc)
+            return prev
+        return (t, sc)
+
+    attr = "_dla_f8_g" if glu_il else ("_dla_f8_n" if norm_w is not None else "_dla_f8")
+    key = (_wkey(w), _wkey(norm_w) if norm_w is not None else None)
+    return _cached(w, attr, key, make)
+
+
+def _f8_ok(rows: int, w: torch.Tensor) -> bool:
+    return _FP8[0] and rows <= 16 and w.shape[0] % 32 == 0 and w.shape[1] % 1024 == 0
+
+
+DERIVED_ATTRS = ("_dla_fold", "_dla_fold_t", "_dla_fold_g", "_dla_tile", "_dla_f8", "_dla_f8_n", "_dla_f8_g")
 
 
 def drop_derived_weights(model) -> int:
@@ -387,9 +461,15 @@ def refresh_folded_weights(model) -> None:
                 folded_weight(w, nw, tiled=True)
             if getattr(w, "_dla_fold_g", None) is not None:
                 folded_weight(w, nw, tiled=True, glu_il=True)
+            if getattr(w, "_dla_f8_n", None) is not None:
+                fp8_tiled_weight(w, nw)
+            if getattr(w, "_dla_f8_g", None) is not None:
+                fp8_tiled_weight(w, nw, glu_il=True)
         for w in (getattr(layer.attn, "o_proj", None), getattr(layer.mlp, "down_proj", None)):
             if w is not None and getattr(w, "_dla_tile", None) is not None:
                 tiled_weight(w)
+            if w is not None and getattr(w, "_dla_f8", None) is not None:
+                fp8_tiled_weight(w)
 
 
 def _fused_op(rows: int):
@@ -399,6 +479,10 @@ def _fused_op(rows: int):
 def skinny_residual(x: torch.Tensor, w: torch.Tensor, res: torch.Tensor):
     """s = res + x @ w^T (bf16 rounding as linear + add), plus the row-norm partials of s."""
     x2 = _rows(x)
+    if _f8_ok(x2.shape[0], w):
+        w8, sc = fp8_tiled_weight(w)
+        s, ssq = _ext.require().skinny_fused_f8(x2, w8, sc, _rows(res), None, 0.0)
+        return s.view(*res.shape[:-1], w.shape[0]), ssq
     wk = tiled_weight(w) if DECODE_TILED >= 2 else w
     s, ssq = _fused_op(x2.shape[0])(x2, wk, _rows(res), None, 0.0, False)
     return s.view(*res.shape[:-1], w.shape[0]), ssq
@@ -408,6 +492,14 @@ def skinny_normed(s: torch.Tensor, ssq: torch.Tensor, norm_w: torch.Tensor, eps:
                   w: torch.Tensor, glu: bool = False) -> torch.Tensor:
     """RMSNorm(s) * norm_w @ w^T from the producer's partials (glu: gate|up + SwiGLU epilogue)."""
     s2 = _rows(s)
+    if _f8_ok(s2.shape[0], w):
+        if glu:
+            w8, sc = fp8_tiled_weight(w, norm_w, glu_il=True)
+            m = _ext.require().skinny_glu_il_f8(s2, w8, sc, ssq, float(eps))
+            return m.view(*s.shape[:-1], m.shape[-1])
+        w8, sc = fp8_tiled_weight(w, norm_w)
+        y, _ = _ext.require().skinny_fused_f8(s2, w8, sc, None, ssq, float(eps))
+        return y.view(*s.shape[:-1], y.shape[-1])
     if (glu and DECODE_GLU_IL and DECODE_TILED >= 1 and s2.shape[0] <= 16 and w.shape[0] % 32 == 0
             and w.shape[1] % 512 == 0):
         m = _ext.require().skinny_glu_il(s2, folded_weight(w, norm_w, tiled=True, glu_il=True), ssq, float(eps))
@@ -438,7 +530,7 @@ DECODE_TAIL = os.environ.get("DLA_DECODE_TAIL", "0") == "1"
 
 def tail_ok(model, x) -> bool:
     """The model's decode step can run on the persistent layer-tail kernel."""
-    if not (DECODE_TAIL and _DECODE_NT and DECODE_TILED >= 2 and x.is_cuda):
+    if not (DECODE_TAIL and _DECODE_NT and DECODE_TILED >= 2 and x.is_cuda) or _FP8[0]:
         return False
     cfg = model.cfg
     rows = x.numel() // x.shape[-1]
@@ -498,7 +590,7 @@ def qkv_attend(s: torch.Tensor, ssq: torch.Tensor, norm_w: torch.Tensor, eps: fl
                 and w.shape[0] % 128 == 0):
             return None
         return cache.attend_slab(layer, s2, ssq, folded_weight(w, norm_w, tiled=True), eps, rope, window)
-    if not (DECODE_QKV_ATTN and _DECODE_NT and DECODE_TILED >= 1):
+    if not (DECODE_QKV_ATTN and _DECODE_NT and DECODE_TILED >= 1) or _FP8[0]:
         return None
     N = w.shape[0]
     nsplit = qkv_attn_splits(cache.max_len, B, cache.kv_local)

@@ -139,7 +139,8 @@ def main(argv=None) -> int:
                               do_sample=gen["do_sample"], temperature=gen.get("temperature", 1.0),
                               top_p=gen.get("top_p", 1.0), top_k=gen.get("top_k", 0),
                               pad_token_id=tok.pad_token_id, eos_token_id=getattr(tok, "eos_token_id", None),
-                              generator=gen_g, return_mask=True)
+                              generator=gen_g, return_mask=True,
+                              weight_dtype=ppo.get("rollout_weight_dtype", "bf16"))
         r_ids, r_mask = handoff(mine, ids, am, seqs, mask)
         with torch.no_grad():
             scores = rm(r_ids, r_mask)

@@ -814,3 +814,91 @@ def test_decode_layer_tail_matches_four_launches(B, T, pad, monkeypatch):
     c = generate(m, ids, am, max_new_tokens=12, do_sample=False, eos_token_id=-1, use_graph=True)
     clear_graph_cache()
     assert torch.equal(a, b) and torch.equal(b, c)
+
+
+# ------------------------------------------------------------------ weight-only fp8 decode
+def _dequant(w, norm_w=None):
+    from distributed_llm_alignment_amd import ops
+
+    src = w if norm_w is None else w * norm_w.view(1, -1)
+    q, sc = ops.decode.quantize_rows_f8(src)
+    return q.view(torch.float8_e4m3fn).float() * sc[:, None]
+
+
+@pytest.mark.parametrize("M", [1, 7, 16])
+def test_fp8_decode_projection_kernels_match_dequant_fp32(M):
+    """The e4m3 weight streams (csrc/skinny_ks.h F8, skinny_glu_il_kernel F8): residual producer,
+    norm-on-input qkv and the gate|up GLU against fp32 math on the DEQUANTISED weights (so only
+    accumulation order and bf16 output rounding differ), and within fp8 quantisation error of the
+    bf16 kernels."""
+    from distributed_llm_alignment_amd import ops
+    from distributed_llm_alignment_amd.ops.norm import _ref_norm
+
+    H, F = 4096, 14336
+    g = torch.Generator(device=DEV).manual_seed(5)
+    x = torch.randn(M, F, device=DEV, generator=g).to(torch.bfloat16)
+    w = (torch.randn(H, F, device=DEV, generator=g) * F ** -0.5).to(torch.bfloat16)
+    res = torch.randn(M, H, device=DEV, generator=g).to(torch.bfloat16)
+    rel = lambda a, b: float((a.float() - b.float()).norm() / b.float().norm())
+    s16, _ = ops.decode.skinny_residual(x, w, res)
+    with ops.decode.fp8_weights(True):
+        s, ssq = ops.decode.skinny_residual(x, w, res)
+    s_ref = ((x.float() @ _dequant(w).t()).to(torch.bfloat16).float() + res.float())
+    assert float((s.float() - s_ref).abs().max()) < 0.05
+    assert torch.allclose(ssq[:M].sum(1), (s.float() ** 2).sum(1), rtol=1e-4)
+    assert rel(s - res, s16 - res) < 0.06  # the projection part, fp8 vs bf16 weights
+    nw = (1 + 0.1 * torch.randn(H, device=DEV, generator=g)).to(torch.bfloat16)
+    h_ref = _ref_norm(s.float(), nw.float(), None, 1e-5, True)
+    wq = (torch.randn(6144, H, device=DEV, generator=g) * H ** -0.5).to(torch.bfloat16)
+    wgu = (torch.randn(2 * F, H, device=DEV, generator=g) * H ** -0.5).to(torch.bfloat16)
+    y16 = ops.decode.skinny_normed(s, ssq, nw, 1e-5, wq)
+    m16 = ops.decode.skinny_normed(s, ssq, nw, 1e-5, wgu, glu=True)
+    with ops.decode.fp8_weights(True):
+        y = ops.decode.skinny_normed(s, ssq, nw, 1e-5, wq)
+        mm = ops.decode.skinny_normed(s, ssq, nw, 1e-5, wgu, glu=True)
+    rstd = torch.rsqrt((s.float() ** 2).mean(1, keepdim=True) + 1e-5)
+    y_ref = (s.float() * rstd) @ _dequant(wq, nw).t()
+    assert rel(y, y_ref) < 1e-2
+    gu = (s.float() * rstd) @ _dequant(wgu, nw).t()
+    m_ref = torch.nn.functional.silu(gu[:, :F]) * gu[:, F:]
+    assert rel(mm, m_ref) < 1e-2
+    assert rel(y, y16) < 0.06 and rel(mm, m16) < 0.08
+    assert rel(y16, h_ref @ wq.float().t()) < 1e-2  # (the bf16 reference itself)
+
+
+def test_fp8_generation_graph_matches_eager_and_tracks_bf16():
+    """generate(weight_dtype="fp8") on the fused decode layer: graph == eager (greedy, bitwise),
+    the fp8 copies are refreshed when the weights move, and the first decode step's logits stay
+    within quantisation error of the bf16 decode."""
+    from distributed_llm_alignment_amd import ops
+    from distributed_llm_alignment_amd.models import build_model, generate
+    from distributed_llm_alignment_amd.models.generation import KVCache, clear_graph_cache
+
+    cfg = _fused_cfg()
+    m = build_model(cfg, device=DEV, dtype=torch.bfloat16, seed=4).eval()
+    g = torch.Generator(device=DEV).manual_seed(9)
+    B = 8
+    ids = torch.randint(3, cfg.vocab_size, (B, 40), device=DEV, generator=g)
+    nxt = torch.randint(3, cfg.vocab_size, (B, 1), device=DEV, generator=g)
+    logits = {}
+    with torch.no_grad():
+        for dt in ("bf16", "fp8"):
+            with ops.decode.fp8_weights(dt == "fp8"):
+                cache = KVCache(m, B, 48, None)
+                m(ids, cache=cache)
+                logits[dt] = m.logits(m(nxt, cache=cache)[:, -1]).float()
+    rel = float((logits["fp8"] - logits["bf16"]).norm() / logits["bf16"].norm())
+    assert rel < 0.1, rel
+    assert getattr(m.layers[0].mlp.down_proj, "_dla_f8", None) is not None  # the fp8 path ran
+    clear_graph_cache()
+    a = generate(m, ids, max_new_tokens=12, do_sample=False, eos_token_id=-1, use_graph=False, weight_dtype="fp8")
+    b = generate(m, ids, max_new_tokens=12, do_sample=False, eos_token_id=-1, use_graph=True, weight_dtype="fp8")
+    assert torch.equal(a, b)
+    # weights move (an optimizer step): the in-place refreshed fp8 copies follow, graph reused
+    with torch.no_grad():
+        for p in m.parameters():
+            p.mul_(1.01)
+    c = generate(m, ids, max_new_tokens=12, do_sample=False, eos_token_id=-1, use_graph=True, weight_dtype="fp8")
+    d = generate(m, ids, max_new_tokens=12, do_sample=False, eos_token_id=-1, use_graph=False, weight_dtype="fp8")
+    clear_graph_cache()
+    assert torch.equal(c, d)

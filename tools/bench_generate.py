@@ -23,6 +23,8 @@ def main() -> int:
     ap.add_argument("--prompt", type=int, default=1024)
     ap.add_argument("--new", type=int, default=256)
     ap.add_argument("--modes", default="eager,graph")
+    ap.add_argument("--weight-dtype", choices=("bf16", "fp8"), default="bf16",
+                    help="decode weight streams (generate(weight_dtype=...))")
     a = ap.parse_args()
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from distributed_llm_alignment_amd.models import build_model, generate, get_config
@@ -39,7 +41,7 @@ def main() -> int:
     am = torch.ones_like(ids)
     for mode in a.modes.split(","):
         kw = dict(max_new_tokens=a.new, do_sample=True, temperature=0.7, top_p=0.9, eos_token_id=-1,
-                  use_graph=(mode == "graph"), seed=1)
+                  use_graph=(mode == "graph"), seed=1, weight_dtype=a.weight_dtype)
         generate(m, ids[:, :64], am[:, :64], **{**kw, "max_new_tokens": 8})  # warm
         generate(m, ids, am, **kw)  # warm at the timed shapes (graph mode: the capture is reused)
         torch.cuda.synchronize()
@@ -54,6 +56,7 @@ def main() -> int:
         torch.cuda.synchronize()
         tp = time.perf_counter() - t1
         print(json.dumps({"mode": mode, "model": cfg.name, "batch": a.batch, "prompt": a.prompt,
+                          "weight_dtype": a.weight_dtype,
                           "new_tokens": n, "total_s": round(dt, 3), "prefill_s": round(tp, 3),
                           "decode_ms_per_token": round((dt - tp) / max(n - 1, 1) * 1e3, 3),
                           "decode_tokens_per_s": round(a.batch * (n - 1) / max(dt - tp, 1e-9), 1)}),

@@ -51,6 +51,8 @@ def main() -> int:
                          "a batch/micro-rank DDP job (the reference splits the batch across processes "
                          "and takes rewards.mean() per process), so no activation recompute is needed")
     ap.add_argument("--algorithm", choices=("reinforce", "ppo"), default="reinforce")
+    ap.add_argument("--rollout-dtype", choices=("bf16", "fp8"), default="bf16",
+                    help="decode weight streams of the rollout generation (ppo.rollout_weight_dtype)")
     ap.add_argument("--zero-shape", type=int, default=1,
                     help="engines laid out as rank 0 of an N-rank ZeRO-1 job (1/N optimizer state)")
     ap.add_argument("--ppo-epochs", type=int, default=2)
@@ -101,7 +103,8 @@ def main() -> int:
         am = torch.ones_like(ids)
         t0 = sync()
         seqs, mask = generate(pol, ids, am, max_new_tokens=a.new, do_sample=True, temperature=0.7,
-                              top_p=0.9, eos_token_id=-1, return_mask=True, seed=3)
+                              top_p=0.9, eos_token_id=-1, return_mask=True, seed=3,
+                              weight_dtype=a.rollout_dtype)
         t1 = sync()
         with torch.no_grad():
             if a.handoff == "none":
@@ -136,7 +139,8 @@ def main() -> int:
             ids = torch.randint(3, cfg.vocab_size, (a.batch, a.prompt), device=dev, generator=g)
             am = torch.ones_like(ids)
             seqs, mask = generate(snap, ids, am, max_new_tokens=a.new, do_sample=True, temperature=0.7,
-                                  top_p=0.9, eos_token_id=-1, return_mask=True, seed=3)
+                                  top_p=0.9, eos_token_id=-1, return_mask=True, seed=3,
+                              weight_dtype=a.rollout_dtype)
             with torch.no_grad():
                 if a.handoff == "none":
                     scores = rm(seqs, mask)
@@ -198,6 +202,7 @@ def main() -> int:
             step(True)
         dt = sync() - t
     print(json.dumps({"bench": "rlhf_step", "model": cfg.name, "rollouts_per_step": a.batch,
+                      "rollout_dtype": a.rollout_dtype,
                       "grad_ckpt": a.grad_ckpt or "none", "handoff": a.handoff,
                       "overlap": bool(a.overlap), "update_micro": a.micro or a.batch,
                       "peak_gib": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1),
@@ -269,7 +274,8 @@ def ppo_main(a) -> int:
         torch.cuda.reset_peak_memory_stats(dev)
         t0 = sync()
         seqs, mask = generate(pol, ids, am, max_new_tokens=a.new, do_sample=True, temperature=0.7,
-                              top_p=0.9, eos_token_id=-1, return_mask=True, seed=3)
+                              top_p=0.9, eos_token_id=-1, return_mask=True, seed=3,
+                              weight_dtype=a.rollout_dtype)
         t1 = sync()
         phase_peak("generate")
         with torch.no_grad():
@@ -312,6 +318,7 @@ def ppo_main(a) -> int:
               "critic_grad_norm": round(float(ceng.last_grad_norm), 5),
               "clipfrac": round(float(m["clipfrac"]), 4)}
     print(json.dumps({"bench": "ppo_step", "model": cfg.name, "rollouts_per_step": a.batch,
+                      "rollout_dtype": a.rollout_dtype,
                       "zero_shape": a.zero_shape, "ppo_epochs": a.ppo_epochs, "minibatches": a.minibatches,
                       "grad_ckpt": a.grad_ckpt or "none", "prompt": a.prompt, "new_tokens": a.new,
                       "s_per_step": round(dt / a.steps, 3), "rollouts_per_s": round(a.batch * a.steps / dt, 3),

@@ -27,6 +27,9 @@ def main():
     ap.add_argument("--iters", type=int, default=4)
     ap.add_argument("--ms", type=int, default=12)
     ap.add_argument("--only", default="", help="comma list of fwd,dx,dw,dxt,dwt,lm")
+    ap.add_argument("--rotating-mb", type=int, default=0,
+                    help="TunableOp rotating buffer: operands cycle through this many MB so each "
+                         "candidate is timed cache-cold, as in the step (0 = cache-warm)")
     a = ap.parse_args()
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from distributed_llm_alignment_amd.models import get_config
@@ -44,7 +47,7 @@ def main():
     tun.set_max_tuning_duration(a.ms)
     tun.set_filename(a.out, insert_device_ordinal=False)
     try:
-        tun.set_rotating_buffer_size(0)
+        tun.set_rotating_buffer_size(a.rotating_mb)
     except Exception:
         pass
     dev = torch.device("cuda", 0)
