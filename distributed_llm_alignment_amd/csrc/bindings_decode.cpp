@@ -64,6 +64,7 @@ void launch_skinny_glu_normin(const bf16_t*, int64_t, const bf16_t*, int64_t, bf
 
 int m64_splits(int N, int K);
 void launch_tile_weight(const bf16_t*, int64_t, const bf16_t*, bf16_t*, int, int, bool, hipStream_t);
+void launch_quant_tile_f8(const bf16_t*, int64_t, const bf16_t*, uint8_t*, float*, int, int, bool, hipStream_t);
 void launch_skinny_glu_il(const bf16_t*, int64_t, const bf16_t*, bf16_t*, int64_t, int, int, int,
                           const KsFuse&, hipStream_t);
 void launch_skinny_ks_fused_f8(const bf16_t*, int64_t, const uint8_t*, bf16_t*, int64_t, int, int, int,
@@ -177,6 +178,35 @@ void tile_weight(const at::Tensor& w, const c10::optional<at::Tensor>& nw, at::T
   launch_tile_weight(cbp(w), w.stride(0), np, bp(out), (int)N, (int)K, glu_il, cur_stream(w));
 }
 
+// w [N, K] bf16 (+ nw folded, glu_il interleave) -> out8 uint8 [N/16, K/64, 64, 16] e4m3 tiled
+// and scale fp32 [N] (per tiled row), in place (a captured decode graph keeps reading them)
+void quant_tile_f8(const at::Tensor& w, const c10::optional<at::Tensor>& nw, at::Tensor& out8, at::Tensor& scale,
+                   bool glu_il) {
+  check_bf16(w, "w");
+  TORCH_CHECK(w.dim() == 2 && w.stride(1) == 1 && w.stride(0) % 8 == 0, "w [N, K], unit inner stride");
+  const int64_t N = w.size(0), K = w.size(1);
+  TORCH_CHECK(N % 32 == 0 && K % 64 == 0 && N < (1ll << 30) && K < (1ll << 30), "N % 32 == 0, K % 64 == 0");
+  check_cuda(out8, "out8");
+  TORCH_CHECK(out8.scalar_type() == at::kByte && out8.is_contiguous() && out8.numel() == N * K,
+              "out8 uint8 contiguous, N * K bytes");
+  check_cuda(scale, "scale");
+  TORCH_CHECK(scale.scalar_type() == at::kFloat && scale.is_contiguous() && scale.numel() == N, "scale fp32 [N]");
+  check_aligned16(w, "w");
+  check_aligned16(out8, "out8");
+  same_device(w, out8);
+  same_device(w, scale);
+  const bf16_t* np = nullptr;
+  if (nw.has_value() && nw->defined()) {
+    check_bf16(*nw, "nw");
+    TORCH_CHECK(nw->dim() == 1 && nw->size(0) == K && nw->is_contiguous(), "nw [K] contiguous");
+    same_device(w, *nw);
+    np = cbp(*nw);
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA g(w.device());
+  launch_quant_tile_f8(cbp(w), w.stride(0), np, out8.data_ptr<uint8_t>(), scale.data_ptr<float>(), (int)N, (int)K,
+                       glu_il, cur_stream(w));
+}
+
 // Decode gate|up + SwiGLU at M <= 16 over the interleaved tiled weight (tile_weight glu_il, norm
 // folded) from the producer's row-norm partials: [M, F] = silu(rstd * g) * (rstd * u)
 at::Tensor skinny_glu_il(const at::Tensor& x, const at::Tensor& wt, const at::Tensor& ssq_in, double eps) {
@@ -249,8 +279,11 @@ std::tuple<at::Tensor, at::Tensor> skinny_fused_f8(const at::Tensor& x, const at
   check_w8(w8, wscale, x, &N, &K);
   const int64_t M = x.size(0);
   TORCH_CHECK(M >= 1 && M <= 16 && x.size(1) == K, "fp8 skinny: 1 <= M <= 16, x [M, K]");
-  TORCH_CHECK(N < (1ll << 30) && K < (1ll << 30) && skinny_use_ksplit((int)N, (int)K),
-              "fp8 skinny: N < 16384, N % 16 == 0, K % 1024 == 0");
+  // (a plain projection -- the LM head -- may be any width: one workgroup per 16 columns)
+  const bool plain = !res.has_value() && !ssq_in.has_value();
+  TORCH_CHECK(N < (1ll << 30) && K < (1ll << 30) &&
+                  (plain ? (N % 16 == 0 && K % 1024 == 0) : skinny_use_ksplit((int)N, (int)K)),
+              "fp8 skinny: N % 16 == 0, K % 1024 == 0 (fused forms: N < 16384)");
   check_aligned16(x, "x");
   KsFuse fz{};
   fz.wscale = wscale.data_ptr<float>();
@@ -969,6 +1002,7 @@ TORCH_LIBRARY_FRAGMENT(dla, m) {
   m.def("skinny_fused(Tensor x, Tensor w, Tensor? res, Tensor? ssq_in, float eps, bool glu) -> (Tensor, Tensor)");
   m.def("skinny64(Tensor x, Tensor w, Tensor? res, Tensor? ssq_in, float eps, bool glu) -> (Tensor, Tensor)");
   m.def("tile_weight(Tensor w, Tensor? nw, Tensor(a!) out, bool glu_il=False) -> ()");
+  m.def("quant_tile_f8(Tensor w, Tensor? nw, Tensor(a!) out8, Tensor(b!) scale, bool glu_il=False) -> ()");
   m.def("skinny_glu_il(Tensor x, Tensor wt, Tensor ssq_in, float eps) -> Tensor");
   m.def("skinny_fused_f8(Tensor x, Tensor w8, Tensor wscale, Tensor? res, Tensor? ssq_in, float eps) -> (Tensor, Tensor)");
   m.def("skinny_glu_il_f8(Tensor x, Tensor w8, Tensor wscale, Tensor ssq_in, float eps) -> Tensor");
@@ -990,6 +1024,7 @@ TORCH_LIBRARY_IMPL(dla, CUDA, m) {
   m.impl("skinny_fused", &dla::skinny_fused);
   m.impl("skinny64", &dla::skinny64);
   m.impl("tile_weight", &dla::tile_weight);
+  m.impl("quant_tile_f8", &dla::quant_tile_f8);
   m.impl("skinny_glu_il", &dla::skinny_glu_il);
   m.impl("skinny_fused_f8", &dla::skinny_fused_f8);
   m.impl("skinny_glu_il_f8", &dla::skinny_glu_il_f8);

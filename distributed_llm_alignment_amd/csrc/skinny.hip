@@ -473,18 +473,31 @@ void launch_skinny_ks_fused_f8(const bf16_t* x, int64_t ldx, const uint8_t* W8, 
                                int M, int N, int K, const KsFuse& fz, bool res, bool nin, hipStream_t st) {
   const bf16_t* W = reinterpret_cast<const bf16_t*>(W8);
   const int nb = N / 16;
-#define DLA_KSF8(NTV, R, NI) skinny_ksplit_kernel<4, NTV, false, 1, kKsUnroll, R, NI, true, true><<<nb, 512, 0, st>>>(x, ldx, W, K, y, ldy, M, N, K, fz)
-  if (decode_nt()) {
-    if (res && nin) DLA_KSF8(true, true, true);
-    else if (res) DLA_KSF8(true, true, false);
-    else if (nin) DLA_KSF8(true, false, true);
-    else DLA_KSF8(true, false, false);
-  } else {
-    if (res && nin) DLA_KSF8(false, true, true);
-    else if (res) DLA_KSF8(false, true, false);
-    else if (nin) DLA_KSF8(false, false, true);
-    else DLA_KSF8(false, false, false);
+  // DLA_KS_F8_DEPTH (2 or 4): ring depth. Graph decode, Llama-3-8B B=8, same box: 2.62 ms/token
+  // at depth 2 vs 2.73 at 4 (fewer VGPRs, more resident waves beat more bytes in flight per wave)
+  static const int depth = [] {
+    const char* e = getenv("DLA_KS_F8_DEPTH");
+    return (e && atoi(e) == 4) ? 4 : 2;
+  }();
+#define DLA_KSF8(D, NTV, R, NI) skinny_ksplit_kernel<D, NTV, false, 1, kKsUnroll, R, NI, true, true><<<nb, 512, 0, st>>>(x, ldx, W, K, y, ldy, M, N, K, fz)
+#define DLA_KSF8_NT(D)                           \
+  if (decode_nt()) {                             \
+    if (res && nin) DLA_KSF8(D, true, true, true);   \
+    else if (res) DLA_KSF8(D, true, true, false);    \
+    else if (nin) DLA_KSF8(D, true, false, true);    \
+    else DLA_KSF8(D, true, false, false);            \
+  } else {                                       \
+    if (res && nin) DLA_KSF8(D, false, true, true);  \
+    else if (res) DLA_KSF8(D, false, true, false);   \
+    else if (nin) DLA_KSF8(D, false, false, true);   \
+    else DLA_KSF8(D, false, false, false);           \
   }
+  if (depth == 2) {
+    DLA_KSF8_NT(2)
+  } else {
+    DLA_KSF8_NT(4)
+  }
+#undef DLA_KSF8_NT
 #undef DLA_KSF8
 }
 
@@ -668,7 +681,16 @@ void launch_skinny_glu_il_f8(const bf16_t* x, int64_t ldx, const uint8_t* Wt8, b
   for (int c : {8, 7, 6, 5, 4}) {
     if (ntiles % c == 0 && ntiles / c >= 256) { w = c; break; }
   }
-  launch_glu_il_d<4, true>(x, ldx, reinterpret_cast<const bf16_t*>(Wt8), y, ldy, M, ntiles, K, fz, w, st);
+  // DLA_GLU_IL_F8_DEPTH (2, 3 or 4): ring depth; same A/B: 2.712 / 2.710 / 2.729 ms/token
+  static const int depth = [] {
+    const char* e = getenv("DLA_GLU_IL_F8_DEPTH");
+    const int d = e ? atoi(e) : 3;
+    return d < 2 ? 2 : (d > 4 ? 4 : d);
+  }();
+  const bf16_t* W = reinterpret_cast<const bf16_t*>(Wt8);
+  if (depth == 2) launch_glu_il_d<2, true>(x, ldx, W, y, ldy, M, ntiles, K, fz, w, st);
+  else if (depth == 3) launch_glu_il_d<3, true>(x, ldx, W, y, ldy, M, ntiles, K, fz, w, st);
+  else launch_glu_il_d<4, true>(x, ldx, W, y, ldy, M, ntiles, K, fz, w, st);
 }
 
 void launch_skinny_glu_il(const bf16_t* x, int64_t ldx, const bf16_t* Wt, bf16_t* y, int64_t ldy, int M,

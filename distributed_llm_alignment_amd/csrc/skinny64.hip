@@ -451,4 +451,77 @@ void launch_tile_weight(const bf16_t* W, int64_t ldw, const bf16_t* nw, bf16_t* 
                                                                                  glu_il ? N / 2 : 0);
 }
 
+// Weight-only fp8 decode copy in one pass (ops/decode.py fp8_tiled_weight; refreshed every RLHF
+// step): W [N, K] (row stride ldw), nw folded as bf16(W * nw), glu_f > 0 = gate / up rows
+// interleaved 8 + 8 per tile (as tile_weight_kernel) -> per-row scale amax / 448 and the e4m3
+// tiled layout [N/16, K/64, 64, 16 B] of csrc/skinny_ks.h F8. One 256-thread workgroup per 16-row
+// tile: 16 threads per row reduce its amax (the rows then sit in L2 for the second pass), every
+// thread then writes whole 16-byte lane pieces (round to nearest even, values pre-clamped to
+// +-448 as the torch reference does).
+__global__ __launch_bounds__(256) void quant_tile_f8_kernel(const bf16_t* __restrict__ W, int64_t ldw,
+                                                            const bf16_t* __restrict__ nw,
+                                                            uint8_t* __restrict__ out, float* __restrict__ scale,
+                                                            int K, int glu_f) {
+  __shared__ float inv_s[16];
+  const int t = blockIdx.x, tid = threadIdx.x;
+  auto row_of = [&](int r) -> int64_t {
+    return glu_f > 0 ? (r < 8 ? 8 * static_cast<int64_t>(t) + r : glu_f + 8 * static_cast<int64_t>(t) + r - 8)
+                     : static_cast<int64_t>(t) * 16 + r;
+  };
+  auto fetch = [&](int64_t row, int col) {
+    bf16x8 v = load_bf16x8(W + row * ldw + col);
+    if (nw != nullptr) {
+      const bf16x8 g = load_bf16x8(nw + col);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = f2bf(bf2f(v[e]) * bf2f(g[e]));
+    }
+    return v;
+  };
+  {
+    const int r = tid >> 4, sub = tid & 15;
+    const int64_t row = row_of(r);
+    float am = 0.f;
+    for (int c = sub * 8; c < K; c += 128) {
+      const bf16x8 v = fetch(row, c);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) am = fmaxf(am, fabsf(bf2f(v[e])));
+    }
+#pragma unroll
+    for (int o = 8; o >= 1; o >>= 1) am = fmaxf(am, __shfl_xor(am, o, 16));
+    if (sub == 0) {
+      const float sc = fmaxf(am / 448.f, 1e-12f);
+      scale[16 * static_cast<int64_t>(t) + r] = sc;
+      inv_s[r] = sc;
+    }
+  }
+  __syncthreads();
+  const int pieces = (K >> 6) * 64;
+  uint8_t* otile = out + static_cast<int64_t>(t) * 16 * K;
+  for (int p = tid; p < pieces; p += 256) {
+    const int kt = p >> 6, lane = p & 63, r = lane & 15, qd = lane >> 4;
+    const int64_t row = row_of(r);
+    const float sc = inv_s[r];
+    const bf16x8 lo = fetch(row, 64 * kt + 8 * qd), hi = fetch(row, 64 * kt + 32 + 8 * qd);
+    auto q8 = [&](bf16_t x) { return fminf(fmaxf(bf2f(x) / sc, -448.f), 448.f); };
+    uint32_t wv[4];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const bf16x8& v = h ? hi : lo;
+      // bytes 4j .. 4j+3 of the piece: e4m3 of elements 4j .. 4j+3 (low half first)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        uint32_t wd = __builtin_amdgcn_cvt_pk_fp8_f32(q8(v[4 * j]), q8(v[4 * j + 1]), 0u, false);
+        wd = __builtin_amdgcn_cvt_pk_fp8_f32(q8(v[4 * j + 2]), q8(v[4 * j + 3]), wd, true);
+        wv[2 * h + j] = wd;
+      }
+    }
+    *reinterpret_cast<uint4*>(otile + static_cast<int64_t>(p) * 16) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+  }
+}
+
+void launch_quant_tile_f8(const bf16_t* W, int64_t ldw, const bf16_t* nw, uint8_t* out, float* scale, int N,
+                          int K, bool glu_il, hipStream_t st) {
+  quant_tile_f8_kernel<<<N / 16, 256, 0, st>>>(W, ldw, nw, out, scale, K, glu_il ? N / 2 : 0);
+}
+
 }  // namespace dla

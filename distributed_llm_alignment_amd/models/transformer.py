@@ -563,7 +563,9 @@ class CausalLM(nn.Module):
 
     def logits(self, hidden: torch.Tensor) -> torch.Tensor:
         lg = None
-        if self.lm_head_bias is None:
+        if self.lm_head_bias is None and self.vocab_parallel is None:
+            lg = ops.decode.head_f8(hidden, self.head_weight)  # fp8 decode mode only
+        if lg is None and self.lm_head_bias is None:
             lg = ops.decode.skinny_linear(hidden, self.head_weight)  # decode rows only
         if lg is None:
             lg = F.linear(hidden, self.head_weight, self.lm_head_bias)

@@ -405,13 +405,24 @@ def tile_f8(q: torch.Tensor) -> torch.Tensor:
 def fp8_tiled_weight(w: torch.Tensor, norm_w: Optional[torch.Tensor] = None, glu_il: bool = False):
     """Cached (e4m3 tiled copy, per-row scales) of W (o norm_w folded in; glu_il: gate / up rows
     interleaved 8 + 8 per 16-row tile), refreshed when W or norm_w moved (as folded_weight)."""
+    N, K = w.shape
+
     def make(prev):
+        if _ext.use_native(w) and w.stride(-1) == 1 and w.stride(0) % 8 == 0:
+            # one HIP pass (csrc/skinny64.hip quant_tile_f8_kernel), in place when refreshing: a
+            # captured decode graph keeps reading the same storage
+            t, sc = prev if prev is not None else (
+                torch.empty((N // 16, K // 64, 64, 16), dtype=torch.uint8, device=w.device),
+                torch.empty(N, dtype=torch.float32, device=w.device))
+            _ext.require().quant_tile_f8(w.detach(), norm_w.detach().contiguous() if norm_w is not None else None,
+                                         t, sc, bool(glu_il))
+            return (t, sc)
         src = w.detach() if norm_w is None else w.detach() * norm_w.detach().view(1, -1)
         if glu_il:
             src = _glu_interleave(src)
         q, sc = quantize_rows_f8(src)
         t = tile_f8(q)
-        if prev is not None:  # in place: a captured decode graph keeps reading the same storage
+        if prev is not None:
             prev[0].copy_(t)
             prev[1].copy_(sc)
             return prev
@@ -426,6 +437,18 @@ def _f8_ok(rows: int, w: torch.Tensor) -> bool:
     return _FP8[0] and rows <= 16 and w.shape[0] % 32 == 0 and w.shape[1] % 1024 == 0
 
 
+def head_f8(x: torch.Tensor, w: torch.Tensor) -> Optional[torch.Tensor]:
+    """LM-head logits x @ w^T on the fp8 copy of w (decode rows, fp8 mode), else None."""
+    if not (_FP8[0] and x.is_cuda and _ext.use_native(x)) or torch.is_grad_enabled() and x.requires_grad:
+        return None
+    rows = x.numel() // x.shape[-1]
+    if not (1 <= rows <= 16 and _f8_ok(rows, w) and x.dtype == torch.bfloat16):
+        return None
+    w8, sc = fp8_tiled_weight(w)
+    y, _ = _ext.require().skinny_fused_f8(_rows(x), w8, sc, None, None, 0.0)
+    return y.view(*x.shape[:-1], w.shape[0])
+
+
 DERIVED_ATTRS = ("_dla_fold", "_dla_fold_t", "_dla_fold_g", "_dla_tile", "_dla_f8", "_dla_f8_n", "_dla_f8_g")
 
 
@@ -438,8 +461,11 @@ def drop_derived_weights(model) -> int:
     for p in model.parameters():
         for k in DERIVED_ATTRS:
             c = p.__dict__.pop(k, None)
-            if c is not None and isinstance(c[1], torch.Tensor):
-                freed += c[1].numel() * c[1].element_size()
+            if c is None:
+                continue
+            for t in (c[1] if isinstance(c[1], tuple) else (c[1],)):  # fp8 copies: (bytes, scales)
+                if isinstance(t, torch.Tensor):
+                    freed += t.numel() * t.element_size()
     return freed
 
 
@@ -450,6 +476,9 @@ def refresh_folded_weights(model) -> None:
     ls = getattr(model, "layers_sharded", None)
     if ls is not None and ls():
         return
+    hw = getattr(model, "head_weight", None)
+    if isinstance(hw, torch.Tensor) and getattr(hw, "_dla_f8", None) is not None:
+        fp8_tiled_weight(hw)
     for layer in getattr(model, "layers", []):
         for w, nw in ((getattr(layer.attn, "qkv_proj", None), getattr(layer, "ln1_w", None)),
                       (getattr(layer.mlp, "up_proj", None), getattr(layer, "ln2_w", None))):

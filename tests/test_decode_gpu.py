@@ -902,3 +902,28 @@ def test_fp8_generation_graph_matches_eager_and_tracks_bf16():
     d = generate(m, ids, max_new_tokens=12, do_sample=False, eos_token_id=-1, use_graph=False, weight_dtype="fp8")
     clear_graph_cache()
     assert torch.equal(c, d)
+
+
+def test_quant_tile_f8_kernel_matches_torch_reference():
+    """The one-pass HIP quantiser (csrc/skinny64.hip quant_tile_f8_kernel) against the torch
+    quantise + tile reference: plain, norm-folded and gate / up interleaved."""
+    from distributed_llm_alignment_amd import ops
+
+    C = ops._ext.require()
+    g = torch.Generator(device=DEV).manual_seed(11)
+    for N, K, fold, glu in ((64, 1024, False, False), (96, 2048, True, False), (128, 1024, True, True)):
+        w = (torch.randn(N, K, device=DEV, generator=g) * torch.rand(N, 1, device=DEV, generator=g) * 3).to(torch.bfloat16)
+        nw = (1 + 0.2 * torch.randn(K, device=DEV, generator=g)).to(torch.bfloat16) if fold else None
+        t = torch.empty(N // 16, K // 64, 64, 16, dtype=torch.uint8, device=DEV)
+        sc = torch.empty(N, dtype=torch.float32, device=DEV)
+        C.quant_tile_f8(w, nw, t, sc, glu)
+        src = w if nw is None else w * nw.view(1, -1)
+        if glu:
+            src = ops.decode._glu_interleave(src)
+        q_ref, sc_ref = ops.decode.quantize_rows_f8(src)
+        assert torch.allclose(sc, sc_ref, rtol=1e-6, atol=0)
+        t_ref = ops.decode.tile_f8(q_ref)
+        mismatch = (t != t_ref).float().mean().item()
+        assert mismatch < 1e-2, mismatch  # rounding of values within an ulp of a tie only
+        # any difference is one e4m3 code step (same sign: adjacent byte values)
+        assert int((t.int() - t_ref.int()).abs().max()) <= 1

@@ -102,6 +102,8 @@ PASSES = {
     # ---- kernel tables and counters (round 4 passes 2/3/16/26/37)
     "dpo-profile": [prof("dpo", DPO + " --steps 2 --warmup 1", DPO_TABLES)],
     "decode-profile": [prof("dec8", GEN8, DEC_TABLE, 300), prof("dec64", GEN64, DEC_TABLE, 300)],
+    "decode-fp8-profile": [prof("dec8_fp8", GEN8 + " --weight-dtype fp8", DEC_TABLE, 300),
+                           prof("dec8_bf16", GEN8, DEC_TABLE, 300)],
     "mixtral-profile": [prof("mixtral", MIX_EP8 + " --steps 2 --warmup 1",
                              [("breakdown", []), ("window", ["--window", "adamw", "--top", "45"])])],
     "attn-pmc": [pmc("attn_p1", ATTN_P1, "python3 tools/attn_bench.py --iters 3",
