@@ -84,6 +84,9 @@ PASSES = {
         run("ppo_zero8", "python -u tools/bench_rlhf.py --algorithm ppo --zero-shape 8 --batch 8"),
         run("mixtral_ep8", MIX_EP8 + " --steps 3 --warmup 2"),
         run("mixtral_ep8_fp8", MIX_EP8 + " --fp8 --steps 3 --warmup 2"),
+        run("gen8_fp8", GEN8 + " --weight-dtype fp8", 300),
+        run("rlhf8_fp8", "python -u tools/bench_rlhf.py --batch 8 --rollout-dtype fp8", 400),
+        run("ppo_zero8_fp8", "python -u tools/bench_rlhf.py --algorithm ppo --zero-shape 8 --batch 8 --rollout-dtype fp8"),
     ],
     # ---- round 5
     "force-pg": [
@@ -101,6 +104,8 @@ PASSES = {
     ],
     # ---- kernel tables and counters (round 4 passes 2/3/16/26/37)
     "dpo-profile": [prof("dpo", DPO + " --steps 2 --warmup 1", DPO_TABLES)],
+    "ppo-profile": [prof("ppo", "python -u tools/bench_rlhf.py --algorithm ppo --zero-shape 8 --batch 8 --steps 1 --warmup 1",
+                         [("breakdown", []), ("window", ["--by-grid", "--top", "40"])], 500)],
     "decode-profile": [prof("dec8", GEN8, DEC_TABLE, 300), prof("dec64", GEN64, DEC_TABLE, 300)],
     "decode-fp8-profile": [prof("dec8_fp8", GEN8 + " --weight-dtype fp8", DEC_TABLE, 300),
                            prof("dec8_bf16", GEN8, DEC_TABLE, 300)],
