@@ -41,6 +41,7 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--comm-stream", default=None)
     ap.add_argument("--window", default="all", choices=("all", "adamw"))
+    ap.add_argument("--pairs", type=int, default=0, help="pairwise overlap table of the N busiest streams")
     a = ap.parse_args()
     rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestamp"]))
     if a.window == "adamw":
@@ -60,6 +61,24 @@ def main():
         top = collections.Counter(r["Kernel_Name"].split("(")[0][:48] for r in rs).most_common(3)
         tag = " (compute)" if s == comp else (" (comm)" if s == comm else "")
         print(f"| {s}{tag} | {len(rs)} | {busy:.2f} | " + ", ".join(f"`{n}` x{c}" for n, c in top) + " |")
+    if a.pairs:  # busy time of each top stream that some kernel of each other stream covers
+        top = [s for s, _ in sorted(by.items(), key=lambda kv: -len(kv[1]))][:a.pairs]
+        mer = {}
+        for s in top:
+            m = _union([(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in by[s]])
+            mer[s] = (m, [x[0] for x in m])
+        print("\n| stream A | busy ms | % of A concurrent with " + " | ".join(f"stream {t}" for t in top) + " |")
+        print("|---|---|" + "---|" * len(top))
+        for s in top:
+            tot = sum(b - a_ for a_, b in mer[s][0])
+            cells = []
+            for t in top:
+                if t == s:
+                    cells.append("—")
+                    continue
+                ov = sum(_covered(a_, b, *mer[t]) for a_, b in mer[s][0])
+                cells.append(f"{100.0 * ov / max(tot, 1):.1f}")
+            print(f"| {s} | {tot / 1e6:.2f} | " + " | ".join(cells) + " |")
     if comm is None:
         return
     merged = _union([(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in by[comp]])

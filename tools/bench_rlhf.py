@@ -53,11 +53,16 @@ def main() -> int:
     ap.add_argument("--algorithm", choices=("reinforce", "ppo"), default="reinforce")
     ap.add_argument("--rollout-dtype", choices=("bf16", "fp8"), default="bf16",
                     help="decode weight streams of the rollout generation (ppo.rollout_weight_dtype)")
+    ap.add_argument("--force-pg", action="store_true",
+                    help="reinforce: a real one-rank RCCL group and the policy engine's N-GPU path on it "
+                         "(bucket all-reduces on RCCL's stream during the update's backward), so "
+                         "--overlap runs generation beside real collectives")
     ap.add_argument("--zero-shape", type=int, default=1,
                     help="engines laid out as rank 0 of an N-rank ZeRO-1 job (1/N optimizer state)")
     ap.add_argument("--ppo-epochs", type=int, default=2)
     ap.add_argument("--minibatches", type=int, default=2)
     a = ap.parse_args()
+    a.overlap = a.overlap or os.environ.get("DLA_BENCH_RLHF_OVERLAP") == "1"  # (A/B arms by env)
     if a.micro and a.batch % a.micro:
         ap.error("--batch must be a multiple of --micro")
     if a.micro and (a.overlap or a.algorithm == "ppo"):
@@ -76,6 +81,11 @@ def main() -> int:
     dev = torch.device("cuda", 0)
     _ext.require()
     enable_gemm_tuning(0)
+    if a.force_pg:
+        from distributed_llm_alignment_amd.parallel.dist import init_distributed
+
+        torch.cuda.set_device(dev)
+        init_distributed(force_pg=True)
     cfg = get_config(a.model)
     pol = build_model(cfg, device=dev, dtype=torch.bfloat16, seed=1)
     ref = build_model(cfg, device=dev, dtype=torch.bfloat16, seed=1).requires_grad_(False).eval()
@@ -83,7 +93,8 @@ def main() -> int:
     rm.eval().requires_grad_(False)
     if a.grad_ckpt:
         pol.gradient_checkpointing_enable(a.grad_ckpt)
-    eng = DataParallelEngine(pol, lr=1e-6, betas=(0.9, 0.95), weight_decay=0.01, max_grad_norm=1.0)
+    eng = DataParallelEngine(pol, lr=1e-6, betas=(0.9, 0.95), weight_decay=0.01, max_grad_norm=1.0,
+                             force_comm=a.force_pg)
     g = torch.Generator(device=dev).manual_seed(0)
     from distributed_llm_alignment_amd.models.tokenizer import ByteTokenizer
     from distributed_llm_alignment_amd.training.handoff import RewardHandoff

@@ -104,6 +104,12 @@ PASSES = {
     ],
     # ---- kernel tables and counters (round 4 passes 2/3/16/26/37)
     "dpo-profile": [prof("dpo", DPO + " --steps 2 --warmup 1", DPO_TABLES)],
+    "rlhf-overlap": [
+        ab("rlhf_overlap_ab", "python -u tools/bench_rlhf.py --batch 8 --force-pg --steps 3 --warmup 1",
+           {"sync": {}, "overlap": {"DLA_BENCH_RLHF_OVERLAP": "1"}}, 1, 500),
+        prof("rlhf_overlap", "python -u tools/bench_rlhf.py --batch 8 --force-pg --overlap --steps 2 --warmup 1",
+             [("streams", ["--pairs", "4"])], 500),
+    ],
     "ppo-profile": [prof("ppo", "python -u tools/bench_rlhf.py --algorithm ppo --zero-shape 8 --batch 8 --steps 1 --warmup 1",
                          [("breakdown", []), ("window", ["--by-grid", "--top", "40"])], 500)],
     "decode-profile": [prof("dec8", GEN8, DEC_TABLE, 300), prof("dec64", GEN64, DEC_TABLE, 300)],
