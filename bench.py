@@ -87,6 +87,9 @@ def parse(argv=None):
     ap.add_argument("--sharded-init", choices=("auto", "on", "off"), default="auto",
                     help="build on the meta device and materialise only this rank's TP / FSDP "
                          "shards (auto: with --tp > 1 or --zero 3)")
+    ap.add_argument("--ref-fp8", action="store_true", default=os.environ.get("DLA_REF_FP8") == "1",
+                    help="the frozen reference's layer GEMMs on e4m3 weights + activations (row scales, "
+                         "hipBLASLt fp8); an opt-in configuration, not the bf16 headline")
     ap.add_argument("--force-pg", action="store_true",
                     help="one GPU: create a real ONE-rank RCCL process group before any GPU work and "
                          "run the N-GPU engine path on it (ZeRO-1 bucket hooks, reduce-scatter on "
@@ -329,6 +332,10 @@ def main(argv=None) -> int:
     ref.eval()
     for p in ref.parameters():
         p.requires_grad_(False)
+    if args.ref_fp8:
+        from distributed_llm_alignment_amd.ops import enable_fp8_inference
+
+        enable_fp8_inference(ref)
     if mesh.tp > 1 or args.tp_shape > 1:
         apply_tensor_parallel(policy, tp_group, sequence_parallel=args.tp_seq)
         apply_tensor_parallel(ref, tp_group, sequence_parallel=args.tp_seq)
@@ -513,7 +520,8 @@ def main(argv=None) -> int:
                                + ("(one-rank RCCL group, forced comm)" if st.forced else ""),
                 "micro_batch_pairs": args.micro_pairs,
                 "grad_accum": args.accum,
-                "ref_model": "frozen, co-resident" + (", own HIP stream" if ref_stream else ""),
+                "ref_model": "frozen, co-resident" + (", own HIP stream" if ref_stream else "")
+                             + (", fp8 layer GEMMs (e4m3 weights + activations, row scales)" if args.ref_fp8 else ""),
                 "model_tflops_per_gpu": round(tflops_gpu, 1),
                 "mfu": round(tflops_gpu / PEAK_DENSE_BF16_TFLOPS, 4) if dev.type == "cuda" else None,
                 "backend": st.backend or "single-process",

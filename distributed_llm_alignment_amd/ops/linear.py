@@ -151,7 +151,48 @@ class _LinearMainGradFn(torch.autograd.Function):
         return dx, dw, db
 
 
+# ---------------------------------------------------------------------------------------------
+# fp8 inference GEMMs for a FROZEN model (opt-in, `enable_fp8_inference`): e4m3 weights with
+# per-output-row scales (quantised once: the cache key is the weight's version) and e4m3
+# activations with per-row scales (one fused HIP pass, ops.moe.quant_fp8_rows), on hipBLASLt's fp8
+# MFMA path (torch._scaled_mm): 2.3-2.8 PF/s vs 1.2-1.6 bf16 at the Llama-3-8B DPO shapes
+# (tools/fp8_gemm_probe.py). Only without autograd and for >= 256 rows; the LM head, embeddings
+# and norms stay bf16. Use: the DPO reference model (`dpo.reference_fp8`, `bench.py --ref-fp8`).
+def fp8_inference_ok(x: torch.Tensor, weight: torch.Tensor, bias) -> bool:
+    return (bias is None and getattr(weight, "_dla_fp8_infer", False) and not torch.is_grad_enabled()
+            and x.is_cuda and x.dtype == torch.bfloat16 and weight.dim() == 2
+            and x.numel() // max(x.shape[-1], 1) >= 256 and x.shape[-1] % 16 == 0 and weight.shape[0] % 16 == 0)
+
+
+def fp8_linear_frozen(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    from .moe import fp8_mm, fp8_weight, quant_fp8_rows
+
+    x2 = x.reshape(-1, x.shape[-1])
+    xq, sx = quant_fp8_rows(x2)
+    wq, sw = fp8_weight(weight)
+    return fp8_mm(xq, sx, wq, sw).view(*x.shape[:-1], weight.shape[0])
+
+
+def enable_fp8_inference(model, enabled: bool = True) -> int:
+    """Mark the transformer-layer projection weights (qkv, o, gate|up, down) of a frozen model for
+    the fp8 inference GEMMs; returns the number of weights marked. MoE experts keep their own fp8
+    path (`moe.fp8`)."""
+    n = 0
+    for layer in getattr(model, "layers", []):
+        at, mlp = getattr(layer, "attn", None), getattr(layer, "mlp", None)
+        for w in (getattr(at, "qkv_proj", None), getattr(at, "o_proj", None),
+                  getattr(mlp, "up_proj", None), getattr(mlp, "down_proj", None)):
+            if isinstance(w, torch.Tensor) and w.dim() == 2:
+                w._dla_fp8_infer = bool(enabled)
+                if not enabled:
+                    w.__dict__.pop("_dla_fp8", None)
+                n += 1
+    return n
+
+
 def linear(x: torch.Tensor, weight: torch.Tensor, bias=None) -> torch.Tensor:
     if uses_main_grad(weight):
         return _LinearMainGradFn.apply(x, weight, bias)
+    if fp8_inference_ok(x, weight, bias):
+        return fp8_linear_frozen(x, weight)
     return F.linear(x, weight, bias)

@@ -8,7 +8,9 @@ Appendix A #11), `dpo_loss = -logsigmoid(beta*((pc-pr)-(rc-rr))).mean()`, beta f
 scheduler (set `optimization.apply_scheduler: true` to use lr_scheduler/warmup_steps),
 `train/loss` and `train/preference_rate` metrics, checkpoints contain policy (model.safetensors)
 then ref (model_1.safetensors). Options beyond the reference: `model.logprob_reduction: sum`,
-`data.mask_prompt: true` (score response tokens only), `model.label_smoothing` (cDPO).
+`data.mask_prompt: true` (score response tokens only), `model.label_smoothing` (cDPO),
+`model.reference_fp8: true` (the frozen reference's layer GEMMs on e4m3 weights and activations
+with row scales, hipBLASLt fp8: ops.linear.enable_fp8_inference).
 
 The frozen reference model is co-resident on every GPU (bf16, no grad); chosen and rejected
 sequences run as one [2B, T] batch per forward.
@@ -44,6 +46,10 @@ def main(argv=None) -> int:
                          device=ctx.device, seed=ctx.seed, meta_init=meta_init(ctx))
     ref.model.eval()
     ref.model.requires_grad_(False)
+    if model_cfg.get("reference_fp8", False):  # frozen reference on the fp8 inference GEMMs (opt-in)
+        from ..ops import enable_fp8_inference
+
+        enable_fp8_inference(ref.model)
     parallelize(ctx, policy.model)
     parallelize(ctx, ref.model)
     tok = policy.tokenizer

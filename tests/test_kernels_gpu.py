@@ -1013,3 +1013,39 @@ def test_attention_fwd_persistent_bitwise(case, monkeypatch):
     r = ref_attention(q.float(), k.float(), v.float(), 1 / math.sqrt(D), causal, off, window, ks, ke, segs)
     valid = torch.isfinite(l1).transpose(1, 2).unsqueeze(-1)  # [B, Tq, Hq, 1]: rows that see a key
     assert rel_err(o1 * valid, r * valid) < 2e-2
+
+
+# ------------------------------------------------------------------ fp8 inference GEMMs
+def test_fp8_frozen_inference_linear_and_model():
+    """ops.linear on a frozen weight marked by enable_fp8_inference: e4m3 weights + activations with
+    row scales on hipBLASLt's fp8 path, against fp32 math on the dequantised operands, and a whole
+    frozen model forward within fp8 error of its bf16 forward; autograd and short inputs stay bf16."""
+    from distributed_llm_alignment_amd.models import build_model, get_config
+    from distributed_llm_alignment_amd.ops.linear import enable_fp8_inference, fp8_inference_ok
+    from distributed_llm_alignment_amd.ops.moe import quant_fp8_rows
+
+    g = torch.Generator(device=DEV).manual_seed(3)
+    x = bf(torch.randn(512, 1024, device=DEV, generator=g))
+    w = bf(torch.randn(768, 1024, device=DEV, generator=g) * 0.03)
+    w._dla_fp8_infer = True
+    with torch.no_grad():
+        assert fp8_inference_ok(x, w, None) and not fp8_inference_ok(x[:100], w, None)
+        y = ops.linear(x, w)
+        xq, sx = quant_fp8_rows(x)
+        wq, sw = quant_fp8_rows(w)
+        ref = (xq.float() * sx) @ (wq.float() * sw).t()
+        assert rel_err(y, ref) < 1e-2
+        assert rel_err(y, x.float() @ w.float().t()) < 0.06
+    assert not fp8_inference_ok(x.requires_grad_(), w, None) or not torch.is_grad_enabled()
+    cfg = get_config("tiny-llama-d128", hidden_size=1024, num_heads=8, num_kv_heads=2, head_dim=128,
+                     intermediate_size=2048, num_layers=2, vocab_size=4096)
+    m = build_model(cfg, device=DEV, dtype=torch.bfloat16, seed=5).eval().requires_grad_(False)
+    ids = torch.randint(3, cfg.vocab_size, (2, 300), device=DEV, generator=g)
+    with torch.no_grad():
+        h16 = m(ids)
+        assert enable_fp8_inference(m) == 8
+        h8 = m(ids)
+        enable_fp8_inference(m, False)
+        h16b = m(ids)
+    assert torch.equal(h16, h16b)
+    assert 0 < rel_err(h8, h16) < 0.15
