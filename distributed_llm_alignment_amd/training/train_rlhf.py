@@ -98,6 +98,11 @@ def main(argv=None) -> int:
     if rpath and Path(rpath).exists():
         ctx.log(f"Loaded reward weights from {load_reward_checkpoint(rm, rpath)}")
     rm.eval().requires_grad_(False)
+    if ppo.get("frozen_fp8", False):  # reference + reward model on the fp8 inference GEMMs (opt-in)
+        from ..ops import enable_fp8_inference
+
+        enable_fp8_inference(ref.model)
+        enable_fp8_inference(rm.backbone)
     for m in (policy.model, ref.model, rm):
         parallelize(ctx, m)
 

@@ -53,6 +53,8 @@ def main() -> int:
     ap.add_argument("--algorithm", choices=("reinforce", "ppo"), default="reinforce")
     ap.add_argument("--rollout-dtype", choices=("bf16", "fp8"), default="bf16",
                     help="decode weight streams of the rollout generation (ppo.rollout_weight_dtype)")
+    ap.add_argument("--frozen-fp8", action="store_true",
+                    help="reference + reward model layer GEMMs on fp8 (ppo.frozen_fp8, ops.enable_fp8_inference)")
     ap.add_argument("--force-pg", action="store_true",
                     help="reinforce: a real one-rank RCCL group and the policy engine's N-GPU path on it "
                          "(bucket all-reduces on RCCL's stream during the update's backward), so "
@@ -90,6 +92,11 @@ def main() -> int:
     pol = build_model(cfg, device=dev, dtype=torch.bfloat16, seed=1)
     ref = build_model(cfg, device=dev, dtype=torch.bfloat16, seed=1).requires_grad_(False).eval()
     rm = RewardModel(build_model(cfg, device=dev, dtype=torch.bfloat16, seed=2, headless=True)).to(dev, torch.bfloat16)
+    if a.frozen_fp8:
+        from distributed_llm_alignment_amd.ops import enable_fp8_inference
+
+        enable_fp8_inference(ref)
+        enable_fp8_inference(rm.backbone)
     rm.eval().requires_grad_(False)
     if a.grad_ckpt:
         pol.gradient_checkpointing_enable(a.grad_ckpt)
@@ -213,7 +220,7 @@ def main() -> int:
             step(True)
         dt = sync() - t
     print(json.dumps({"bench": "rlhf_step", "model": cfg.name, "rollouts_per_step": a.batch,
-                      "rollout_dtype": a.rollout_dtype,
+                      "rollout_dtype": a.rollout_dtype, "frozen_fp8": a.frozen_fp8,
                       "grad_ckpt": a.grad_ckpt or "none", "handoff": a.handoff,
                       "overlap": bool(a.overlap), "update_micro": a.micro or a.batch,
                       "peak_gib": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1),
@@ -251,6 +258,11 @@ def ppo_main(a) -> int:
     ref = build_model(cfg, device=dev, dtype=torch.bfloat16, seed=1).requires_grad_(False).eval()
     note("reference")
     rm = RewardModel(build_model(cfg, device=dev, dtype=torch.bfloat16, seed=2, headless=True)).to(dev, torch.bfloat16)
+    if a.frozen_fp8:
+        from distributed_llm_alignment_amd.ops import enable_fp8_inference
+
+        enable_fp8_inference(ref)
+        enable_fp8_inference(rm.backbone)
     rm.eval().requires_grad_(False)
     note("reward")
     critic = ValueModel(build_model(cfg, device=dev, dtype=torch.bfloat16, seed=3, headless=True))
@@ -329,7 +341,7 @@ def ppo_main(a) -> int:
               "critic_grad_norm": round(float(ceng.last_grad_norm), 5),
               "clipfrac": round(float(m["clipfrac"]), 4)}
     print(json.dumps({"bench": "ppo_step", "model": cfg.name, "rollouts_per_step": a.batch,
-                      "rollout_dtype": a.rollout_dtype,
+                      "rollout_dtype": a.rollout_dtype, "frozen_fp8": a.frozen_fp8,
                       "zero_shape": a.zero_shape, "ppo_epochs": a.ppo_epochs, "minibatches": a.minibatches,
                       "grad_ckpt": a.grad_ckpt or "none", "prompt": a.prompt, "new_tokens": a.new,
                       "s_per_step": round(dt / a.steps, 3), "rollouts_per_s": round(a.batch * a.steps / dt, 3),
