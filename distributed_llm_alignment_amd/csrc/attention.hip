@@ -348,6 +348,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
     if (ntiles > 1) gload(tile0 + BK);
   }
   __syncthreads();
+  if (p.fwd_prio == 2 && w >= NW / 2) __builtin_amdgcn_s_setprio(1);  // (MI355X_MICROARCH §Two waves item 4)
   // the loop body runs as two copies (buffer 0 / buffer 1) so every LDS read address is a per-lane
   // base plus an immediate: no per-tile buffer select in the VALU stream
   auto step = [&](auto bufc, int t) {
@@ -362,6 +363,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
     }
     if (active) {  // wave-uniform
       f32x16 sacc[2];
+      if (p.fwd_prio == 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int st = 0; st < 2; ++st) {
         sacc[st] = f32x16{};
@@ -371,6 +373,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
           sacc[st] = mfma32(a, qf[s], sacc[st]);
         }
       }
+      if (p.fwd_prio == 1) __builtin_amdgcn_s_setprio(0);
       // mask only tiles that touch a boundary (kv range, causal diagonal, window edge)
       bool need_mask = kt < kbeg || kt + BK > kend || kt < wseg_hi;
       if (CAUSAL) {
@@ -431,6 +434,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
         pf[st][0] = pack8(sacc[st], 0);
         pf[st][1] = pack8(sacc[st], 8);
       }
+      if (p.fwd_prio == 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
         const int c0 = 32 * dt + 16 * ((lane >> 4) & 1);
@@ -443,6 +447,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
           }
         }
       }
+      if (p.fwd_prio == 1) __builtin_amdgcn_s_setprio(0);
     }
     if (t + 1 < ntiles) {  // stage tile t+1 into the other buffer, prefetch tile t+2
       lwrite(BUF ^ 1, kt + BK);
@@ -672,6 +677,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_persist_kernel(AttnParams p,
     }
     if (!active) return;  // wave-uniform
     f32x16 sacc[2];
+    if (p.fwd_prio == 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int st = 0; st < 2; ++st) {
       sacc[st] = f32x16{};
@@ -681,6 +687,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_persist_kernel(AttnParams p,
         sacc[st] = mfma32(a, qf[s], sacc[st]);
       }
     }
+    if (p.fwd_prio == 1) __builtin_amdgcn_s_setprio(0);
     bool need_mask = kt < c.kbeg || kt + BK > c.kend || kt < c.wseg_hi;
     if (CAUSAL) {
       need_mask = need_mask || (kt + BK - 1 > c.q0 + p.causal_off);
@@ -736,6 +743,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_persist_kernel(AttnParams p,
       pf[st][0] = pack8(sacc[st], 0);
       pf[st][1] = pack8(sacc[st], 8);
     }
+    if (p.fwd_prio == 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) {
       const int c0 = 32 * dt + 16 * ((lane >> 4) & 1);
@@ -748,6 +756,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_persist_kernel(AttnParams p,
         }
       }
     }
+    if (p.fwd_prio == 1) __builtin_amdgcn_s_setprio(0);
   };
 
   auto epilogue = [&](const Blk& c) {
@@ -2088,6 +2097,14 @@ static void fwd_launch(const AttnParams& p0, bool causal, hipStream_t st) {
   constexpr int NW = 8, BQ = 32 * NW / HP;
   AttnParams p = p0;
   p.fwd_xcd = fwd_xcd_order();
+  {
+    // 1 (default): s_setprio 1 around each MFMA chain, so the matrix chain of one wave issues
+    // ahead of its SIMD partner's softmax VALU (cdna guide T5). Same box, graph-timed, B*T 8192:
+    // causal T1024 654 vs 613 TF/s, T4096 937 vs 897; non-causal +4-6 %. 2 (static priority for
+    // waves 4-7) measured +0-7 % and below 1 everywhere; 0 = off.
+    const char* e = std::getenv("DLA_ATTN_FWD_PRIO");
+    p.fwd_prio = e ? std::atoi(e) : 1;
+  }
   const int nqb = (p.Tq + BQ - 1) / BQ;
   const int64_t nblk = static_cast<int64_t>(nqb) * (p.Hq / HP) * p.B;
   if (fwd_persist(p.Tk) && nblk < (int64_t(1) << 30)) {

@@ -33,6 +33,8 @@ struct AttnParams {
   // forward block order (set by the launcher): 1 = XCD-grouped, each XCD walks whole (batch,
   // head block) query columns so the concurrent workgroups of one L2 share every K/V tile
   int fwd_xcd;
+  int fwd_prio;  // issue priority A/B (DLA_ATTN_FWD_PRIO): 1 = s_setprio 1 around each MFMA chain,
+                 // 2 = static s_setprio 1 for the second wave of each SIMD (waves 4-7)
   unsigned long long* stamps;  // debug (DLA_ATTN_STAMPS=1): persistent forward seam stamps
 };
 
