@@ -76,6 +76,8 @@ void launch_m64_gemm(const bf16_t*, int64_t, const bf16_t*, int64_t, bf16_t*, in
                      int, int, int, bool, const float*, int, float, bool, hipStream_t);
 void launch_m64_reduce(const float*, int, int, int, bf16_t*, int64_t, const bf16_t*, int64_t,
                        const float*, int, int, float, float*, hipStream_t);
+void launch_m64_gemm_f8(const bf16_t*, int64_t, const uint8_t*, bf16_t*, int64_t, float*, int, int, int, int,
+                        bool, const float*, int, float, const float*, hipStream_t);
 
 // Decode projection at 17..64 rows (skinny64.hip), the same fused-layer contract as
 // skinny_fused below with row-norm partials per (row, 1024 columns):
@@ -304,6 +306,70 @@ std::tuple<at::Tensor, at::Tensor> skinny_fused_f8(const at::Tensor& x, const at
   }
   launch_skinny_ks_fused_f8(cbp(x), x.stride(0), w8.data_ptr<uint8_t>(), bp(y), y.stride(0), (int)M, (int)N,
                             (int)K, fz, res.has_value(), nin, cur_stream(x));
+  return {y, ssq};
+}
+
+// fp8 form of skinny64 (17..64 rows, csrc/skinny64.hip F8): w8 the e4m3 tiled copy
+// [N/16, K/64, 64, 16] with per-row scales `wscale` (ops/decode.py fp8_tiled_weight; gate|up: the
+// plain [gate; up] row order, norm weight folded in). Same epilogue contract as skinny64.
+std::tuple<at::Tensor, at::Tensor> skinny64_f8(const at::Tensor& x, const at::Tensor& w8, const at::Tensor& wscale,
+                                               const c10::optional<at::Tensor>& res,
+                                               const c10::optional<at::Tensor>& ssq_in, double eps, bool glu) {
+  check_bf16(x, "x");
+  int64_t N = 0, K = 0;
+  check_w8(w8, wscale, x, &N, &K);
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0, "x [M, K], unit inner stride");
+  const int64_t M = x.size(0);
+  TORCH_CHECK(M >= 1 && M <= 64 && x.size(1) == K, "fp8 skinny64: 1 <= M <= 64, x [M, K]");
+  TORCH_CHECK(N < (1ll << 30) && K < (1ll << 30) && m64_shape_ok((int)N, (int)K, glu),
+              "fp8 skinny64: K % 256 == 0 and N % 128 == 0");
+  check_aligned16(x, "x");
+  const float* sq = nullptr;
+  int nbp = 0;
+  if (ssq_in.has_value()) {
+    const at::Tensor& t = *ssq_in;
+    check_cuda(t, "ssq_in");
+    TORCH_CHECK(t.scalar_type() == at::kFloat && t.dim() == 2 && t.size(0) == M && t.is_contiguous() &&
+                    t.size(1) >= 1 && t.size(1) <= 8,
+                "ssq_in fp32 [M, nbp <= 8] contiguous");
+    same_device(x, t);
+    sq = t.data_ptr<float>();
+    nbp = static_cast<int>(t.size(1));
+  }
+  TORCH_CHECK(!(res.has_value() && (sq || glu)), "fp8 skinny64: residual output takes a plain input");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  auto st = cur_stream(x);
+  const uint8_t* wp = w8.data_ptr<uint8_t>();
+  const float* wsc = wscale.data_ptr<float>();
+  if (glu) {
+    auto m = at::empty({M, N / 2}, x.options());
+    launch_m64_gemm_f8(cbp(x), x.stride(0), wp, bp(m), m.stride(0), nullptr, (int)M, (int)N, (int)K, 1, true, sq,
+                       nbp, static_cast<float>(eps), wsc, st);
+    return {m, at::Tensor()};
+  }
+  const int S = m64_splits((int)N, (int)K);
+  TORCH_CHECK(S > 1 || !(sq || res.has_value()),
+              "fp8 skinny64: the residual / normalised-input epilogue needs a split-K shape");
+  auto y = at::empty({M, N}, x.options());
+  at::Tensor ws;
+  if (S > 1) ws = at::empty({S, M, N}, x.options().dtype(at::kFloat));
+  launch_m64_gemm_f8(cbp(x), x.stride(0), wp, bp(y), y.stride(0), S > 1 ? ws.data_ptr<float>() : nullptr, (int)M,
+                     (int)N, (int)K, S, false, nullptr, 0, 0.f, wsc, st);
+  const bf16_t* rp = nullptr;
+  int64_t ldr = 0;
+  at::Tensor ssq;
+  if (res.has_value()) {
+    const at::Tensor& r = *res;
+    check_bf16(r, "res");
+    TORCH_CHECK(r.dim() == 2 && r.size(0) == M && r.size(1) == N && r.stride(1) == 1, "res [M, N]");
+    same_device(x, r);
+    rp = cbp(r);
+    ldr = r.stride(0);
+    ssq = at::empty({M, (N + 1023) / 1024}, x.options().dtype(at::kFloat));
+  }
+  if (S > 1)
+    launch_m64_reduce(ws.data_ptr<float>(), S, (int)M, (int)N, bp(y), y.stride(0), rp, ldr, sq, nbp, (int)K,
+                      static_cast<float>(eps), ssq.defined() ? ssq.data_ptr<float>() : nullptr, st);
   return {y, ssq};
 }
 
@@ -1001,6 +1067,7 @@ TORCH_LIBRARY_FRAGMENT(dla, m) {
   m.def("skinny_glu_ks(Tensor x, Tensor w) -> Tensor");
   m.def("skinny_fused(Tensor x, Tensor w, Tensor? res, Tensor? ssq_in, float eps, bool glu) -> (Tensor, Tensor)");
   m.def("skinny64(Tensor x, Tensor w, Tensor? res, Tensor? ssq_in, float eps, bool glu) -> (Tensor, Tensor)");
+  m.def("skinny64_f8(Tensor x, Tensor w8, Tensor wscale, Tensor? res, Tensor? ssq_in, float eps, bool glu) -> (Tensor, Tensor)");
   m.def("tile_weight(Tensor w, Tensor? nw, Tensor(a!) out, bool glu_il=False) -> ()");
   m.def("quant_tile_f8(Tensor w, Tensor? nw, Tensor(a!) out8, Tensor(b!) scale, bool glu_il=False) -> ()");
   m.def("skinny_glu_il(Tensor x, Tensor wt, Tensor ssq_in, float eps) -> Tensor");
@@ -1023,6 +1090,7 @@ TORCH_LIBRARY_IMPL(dla, CUDA, m) {
   m.impl("skinny_glu_ks", &dla::skinny_glu_ks);
   m.impl("skinny_fused", &dla::skinny_fused);
   m.impl("skinny64", &dla::skinny64);
+  m.impl("skinny64_f8", &dla::skinny64_f8);
   m.impl("tile_weight", &dla::tile_weight);
   m.impl("quant_tile_f8", &dla::quant_tile_f8);
   m.impl("skinny_glu_il", &dla::skinny_glu_il);

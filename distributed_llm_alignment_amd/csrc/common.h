@@ -112,4 +112,16 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
 }
 
+// e4m3 -> bf16, 8 values from two dwords (exact: every e4m3 value is a bf16 value); the per-row
+// dequantisation scale is applied to the fp32 sum in the epilogue
+__device__ __forceinline__ s16x8 f8x8_to_bf16(uint32_t w0, uint32_t w1) {
+  typedef short s16x2v __attribute__((ext_vector_type(2)));
+  const s16x2v a = __builtin_bit_cast(s16x2v, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w0, 1.0f, false));
+  const s16x2v b = __builtin_bit_cast(s16x2v, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w0, 1.0f, true));
+  const s16x2v c = __builtin_bit_cast(s16x2v, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w1, 1.0f, false));
+  const s16x2v d = __builtin_bit_cast(s16x2v, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w1, 1.0f, true));
+  return s16x8{a[0], a[1], b[0], b[1], c[0], c[1], d[0], d[1]};
+}
+
+
 }  // namespace dla

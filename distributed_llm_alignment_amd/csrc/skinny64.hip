@@ -39,6 +39,11 @@ __device__ __forceinline__ f32x4 mfma16(s16x8 a, s16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+// F8 (weight-only fp8 decode, TW + nt only): W is the e4m3 tiled copy [N/16, K/64, 64 lanes, 16 B]
+// of csrc/skinny_ks.h F8 (ops/decode.py fp8_tiled_weight): one 16-byte load per lane holds its B
+// fragments of two consecutive k-steps, so a 256-deep chunk is 4 loads per lane instead of 8 and
+// the stream is half the bytes; e4m3 -> bf16 in registers (exact), the bf16 MFMA unchanged, and
+// the per-row scale wsc[n] applied to the fp32 sum before any epilogue.
 // Weight layouts: row-major W [N, K], or TW (tiled, ops/decode.py `tiled_weight`):
 // Wt[N / 16][K / 32][4][16][8] with Wt[t][kk][q][r][e] = W[16 t + r][32 kk + 8 q + e], i.e. the
 // 16-byte pieces in the order lane (r = lane & 15, q = lane >> 4) of an MFMA B fragment reads them:
@@ -51,11 +56,12 @@ __device__ __forceinline__ f32x4 mfma16(s16x8 a, s16x8 b, f32x4 c) {
 // from ssq_in (the producer's row partial sums, [M][nbp]) when NIN, else 1; gate / up are
 // rounded to bf16 before SwiGLU exactly as the unfused GEMM + swiglu pair.
 // Otherwise S == 1 writes y = bf16(x W^T); S > 1 writes fp32 slab ws[s][m][n].
-template <int MT, bool GLU, bool NIN, bool TW, int DEPTH, int NW = kM64Waves, bool NTL = false>
+template <int MT, bool GLU, bool NIN, bool TW, int DEPTH, int NW = kM64Waves, bool NTL = false, bool F8 = false>
 __global__ __launch_bounds__(64 * NW) void m64_gemm_kernel(
     const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ W, int64_t ldw,
     bf16_t* __restrict__ y, int64_t ldy, float* __restrict__ ws, int M, int N, int K, int kc,
-    const float* __restrict__ ssq_in, int nbp, float eps) {
+    const float* __restrict__ ssq_in, int nbp, float eps, const float* __restrict__ wsc) {
+  static_assert(!F8 || (TW && NTL), "fp8 weights: tiled layout, nt stream");
   extern __shared__ __attribute__((aligned(16))) bf16_t xs[];
   __shared__ float rstd_s[64];
   constexpr int RB = 16 * MT * kM64Ld;  // one ring slot
@@ -73,6 +79,8 @@ __global__ __launch_bounds__(64 * NW) void m64_gemm_kernel(
   const int nch = kc / kM64Ck;
   const bf16_t* wrow = TW ? W + static_cast<int64_t>(n0 >> 4) * 16 * K + (k0 >> 5) * 512 + lane * 8
                          : W + static_cast<int64_t>(n0 + r) * ldw + k0 + q * 8;
+  const uint8_t* wrow8 = reinterpret_cast<const uint8_t*>(W) + static_cast<int64_t>(n0 >> 4) * 16 * K +
+                         (k0 >> 6) * 1024 + lane * 16;
 
   // NIN: this row's producer partials, reduced in the epilogue (thread m < M holds row m)
   float pv[kM64MaxNbp];
@@ -88,8 +96,11 @@ __global__ __launch_bounds__(64 * NW) void m64_gemm_kernel(
   // full HBM round trip for the next weight chunk). DEPTH chunks are in flight; x rows >= M are
   // zeros so the A fragments need no row test.
   const int xm = tid >> 5, xc = (tid & 31) * 8;
+  typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+  constexpr int KS8 = kM64Steps / 2;  // fp8: 16-byte weight loads per lane per chunk
   bf16x8 xr[DEPTH][XPASS];
-  s16x8 b[DEPTH][kM64Steps];
+  s16x8 b[DEPTH][F8 ? 1 : kM64Steps];
+  u32x4v b8[DEPTH][F8 ? KS8 : 1];
   auto issue = [&](auto J, int c) {
     constexpr int j = decltype(J)::value;
 #pragma unroll
@@ -97,6 +108,12 @@ __global__ __launch_bounds__(64 * NW) void m64_gemm_kernel(
       const int m = xm + (NTH / 32) * t;
       xr[j][t] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
       if (m < M) xr[j][t] = load_bf16x8(x + static_cast<int64_t>(m) * ldx + k0 + c * kM64Ck + xc);
+    }
+    if constexpr (F8) {
+#pragma unroll
+      for (int u = 0; u < KS8; ++u)
+        b8[j][u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4v*>(wrow8 + (c * KS8 + u) * 1024));
+      return;
     }
 #pragma unroll
     for (int u = 0; u < kM64Steps; ++u)
@@ -129,10 +146,17 @@ __global__ __launch_bounds__(64 * NW) void m64_gemm_kernel(
     const bf16_t* xb = xs + (c & 1) * RB + aoff;
 #pragma unroll
     for (int u = 0; u < kM64Steps; ++u) {
+      s16x8 bu;
+      if constexpr (F8) {
+        const u32x4v wv = b8[j][u >> 1];
+        bu = (u & 1) ? f8x8_to_bf16(wv[2], wv[3]) : f8x8_to_bf16(wv[0], wv[1]);
+      } else {
+        bu = b[j][u];
+      }
 #pragma unroll
       for (int t = 0; t < MT; ++t) {
         const s16x8 a = __builtin_bit_cast(s16x8, *reinterpret_cast<const bf16x8*>(xb + t * 16 * kM64Ld + u * 32));
-        acc[t] = mfma16(a, b[j][u], acc[t]);
+        acc[t] = mfma16(a, bu, acc[t]);
       }
     }
     if (c + 1 < nch) xstore(std::integral_constant<int, (j + 1) % DEPTH>{}, (c + 1) & 1);
@@ -151,6 +175,11 @@ __global__ __launch_bounds__(64 * NW) void m64_gemm_kernel(
   }
 
   // lane holds C[m = 16 t + 4 q + i][n = n0 + r]
+  if constexpr (F8) {
+    const float sc = wsc[n0 + r];
+#pragma unroll
+    for (int t = 0; t < MT; ++t) acc[t] *= sc;
+  }
   if constexpr (GLU) {
     if constexpr (NIN) {
       if (tid < M) {
@@ -311,21 +340,21 @@ size_t m64_lds_bytes(int M) {
   return static_cast<size_t>(2 * 16 * mt * kM64Ld) * sizeof(bf16_t);
 }
 
-template <int MT, bool GLU, bool NIN, bool TW, int NW, bool NTL, int DEPTH = 2>
+template <int MT, bool GLU, bool NIN, bool TW, int NW, bool NTL, int DEPTH = 2, bool F8 = false>
 static void m64_launch_w(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
                          int64_t ldy, float* ws, int M, int N, int K, int S, const float* ssq_in,
-                         int nbp, float eps, hipStream_t st) {
+                         int nbp, float eps, hipStream_t st, const float* wsc = nullptr) {
   const size_t lds = static_cast<size_t>(2 * 16 * MT * kM64Ld) * sizeof(bf16_t);
   static bool attr = [] {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&m64_gemm_kernel<MT, GLU, NIN, TW, DEPTH, NW, NTL>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&m64_gemm_kernel<MT, GLU, NIN, TW, DEPTH, NW, NTL, F8>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
     (void)hipGetLastError();
     return true;
   }();
   (void)attr;
   dim3 grid(GLU ? N / 2 / (8 * NW) : N / (16 * NW), S);
-  m64_gemm_kernel<MT, GLU, NIN, TW, DEPTH, NW, NTL><<<grid, 64 * NW, lds, st>>>(x, ldx, W, ldw, y, ldy, ws, M,
-                                                                           N, K, K / S, ssq_in, nbp, eps);
+  m64_gemm_kernel<MT, GLU, NIN, TW, DEPTH, NW, NTL, F8><<<grid, 64 * NW, lds, st>>>(
+      x, ldx, W, ldw, y, ldy, ws, M, N, K, K / S, ssq_in, nbp, eps, wsc);
 }
 
 // NW = 8 waves per workgroup (gate|up: 64 features per workgroup). 4 waves (448 gate|up
@@ -357,6 +386,46 @@ static void m64_launch(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ld
     }
   }
   m64_launch_w<MT, GLU, NIN, TW, kM64Waves, false>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, ssq_in, nbp, eps, st);
+}
+
+// fp8 weights (tiled, nt): DLA_M64_F8_DEPTH = weight chunks in flight per wave (2, 3 or 4; a chunk
+// is half the bf16 bytes, so the same bytes in flight take twice the chunks)
+template <int MT, bool GLU, bool NIN>
+static void m64_launch_f8(const bf16_t* x, int64_t ldx, const uint8_t* W8, bf16_t* y, int64_t ldy, float* ws,
+                          int M, int N, int K, int S, const float* ssq_in, int nbp, float eps,
+                          const float* wsc, hipStream_t st) {
+  static const int depth = [] {
+    const char* e = getenv("DLA_M64_F8_DEPTH");
+    const int d = e ? atoi(e) : 3;
+    return d >= 2 && d <= 4 ? d : 3;
+  }();
+  const bf16_t* W = reinterpret_cast<const bf16_t*>(W8);
+  if (depth == 2)
+    m64_launch_w<MT, GLU, NIN, true, kM64Waves, true, 2, true>(x, ldx, W, 0, y, ldy, ws, M, N, K, S, ssq_in, nbp, eps, st, wsc);
+  else if (depth == 4)
+    m64_launch_w<MT, GLU, NIN, true, kM64Waves, true, 4, true>(x, ldx, W, 0, y, ldy, ws, M, N, K, S, ssq_in, nbp, eps, st, wsc);
+  else
+    m64_launch_w<MT, GLU, NIN, true, kM64Waves, true, 3, true>(x, ldx, W, 0, y, ldy, ws, M, N, K, S, ssq_in, nbp, eps, st, wsc);
+}
+
+template <int MT>
+static void m64_dispatch_f8(const bf16_t* x, int64_t ldx, const uint8_t* W8, bf16_t* y, int64_t ldy, float* ws,
+                            int M, int N, int K, int S, bool glu, const float* ssq_in, int nbp, float eps,
+                            const float* wsc, hipStream_t st) {
+  if (glu && ssq_in)
+    m64_launch_f8<MT, true, true>(x, ldx, W8, y, ldy, ws, M, N, K, 1, ssq_in, nbp, eps, wsc, st);
+  else if (glu)
+    m64_launch_f8<MT, true, false>(x, ldx, W8, y, ldy, ws, M, N, K, 1, nullptr, 0, 0.f, wsc, st);
+  else
+    m64_launch_f8<MT, false, false>(x, ldx, W8, y, ldy, ws, M, N, K, S, nullptr, 0, 0.f, wsc, st);
+}
+
+// fp8 form of launch_m64_gemm: W8 the e4m3 tiled copy, wsc its per-row scales
+void launch_m64_gemm_f8(const bf16_t* x, int64_t ldx, const uint8_t* W8, bf16_t* y, int64_t ldy, float* ws,
+                        int M, int N, int K, int S, bool glu, const float* ssq_in, int nbp, float eps,
+                        const float* wsc, hipStream_t st) {
+  if (M <= 32) m64_dispatch_f8<2>(x, ldx, W8, y, ldy, ws, M, N, K, S, glu, ssq_in, nbp, eps, wsc, st);
+  else m64_dispatch_f8<4>(x, ldx, W8, y, ldy, ws, M, N, K, S, glu, ssq_in, nbp, eps, wsc, st);
 }
 
 template <int MT, bool TW>

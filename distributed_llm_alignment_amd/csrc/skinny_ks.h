@@ -68,17 +68,6 @@ constexpr int kKsChunk = 32 * kKsUnroll;
 // consumer in another workgroup of the same launch that reads it with `sc1` loads after a counter
 // hand-off (decode.hip decode_qkv_attn_kernel; MI355X_MICROARCH inter-workgroup visibility, the
 // release-free valid form)
-// e4m3 -> bf16, 8 values from two dwords (exact: every e4m3 value is a bf16 value); the per-row
-// dequantisation scale is applied to the fp32 sum in the epilogue
-__device__ __forceinline__ s16x8 f8x8_to_bf16(uint32_t w0, uint32_t w1) {
-  typedef short s16x2v __attribute__((ext_vector_type(2)));
-  const s16x2v a = __builtin_bit_cast(s16x2v, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w0, 1.0f, false));
-  const s16x2v b = __builtin_bit_cast(s16x2v, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w0, 1.0f, true));
-  const s16x2v c = __builtin_bit_cast(s16x2v, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w1, 1.0f, false));
-  const s16x2v d = __builtin_bit_cast(s16x2v, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w1, 1.0f, true));
-  return s16x8{a[0], a[1], b[0], b[1], c[0], c[1], d[0], d[1]};
-}
-
 typedef uint32_t ks_u32x4 __attribute__((ext_vector_type(4)));
 
 template <bool NT>

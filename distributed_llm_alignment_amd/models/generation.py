@@ -350,6 +350,10 @@ def _weights_key(model: CausalLM) -> tuple:
     return tuple(t.data_ptr() for t in model.parameters()) + tuple(t.data_ptr() for t in model.buffers())
 
 
+# fp8 rollouts also prefill on the fp8 inference GEMMs (DLA_PREFILL_FP8=0: bf16 prefill, A/B)
+PREFILL_FP8 = os.environ.get("DLA_PREFILL_FP8", "1") != "0"
+
+
 @torch.no_grad()
 def generate(model: CausalLM, input_ids: torch.Tensor, attention_mask: Optional[torch.Tensor] = None,
              max_new_tokens: int = 256, do_sample: bool = True, temperature: float = 1.0,
@@ -367,12 +371,15 @@ def generate(model: CausalLM, input_ids: torch.Tensor, attention_mask: Optional[
     ONE replay of a captured hipGraph (decode kernel + fused sampler, no host sync except an
     all-finished check every 16 tokens). `use_graph=False` forces the eager per-op loop.
 
-    `weight_dtype="fp8"`: the decode steps' qkv / o / gate|up / down projections stream an e4m3
-    copy of the weights with per-row scales (ops.decode.fp8_weights; half the bytes of the
-    dominant weight streams). The prefill and the LM head stay bf16."""
+    `weight_dtype="fp8"`: the decode steps' qkv / o / gate|up / down projections and the LM head
+    stream an e4m3 copy of the weights with per-row scales (ops.decode.fp8_weights; half the
+    bytes of the dominant weight streams), and the prompt prefill runs those projections on the
+    fp8 inference GEMMs (ops.fp8_inference_scope: e4m3 weights and activations, row
+    scales, hipBLASLt fp8). Attention, norms and the KV cache stay bf16."""
     if weight_dtype not in ("bf16", "fp8"):
         raise ValueError(f"weight_dtype must be 'bf16' or 'fp8', got {weight_dtype!r}")
-    with ops.decode.fp8_weights(weight_dtype == "fp8" or ops.decode.fp8_enabled()):
+    f8 = weight_dtype == "fp8" or ops.decode.fp8_enabled()
+    with ops.decode.fp8_weights(f8), ops.fp8_inference_scope(model, f8 and PREFILL_FP8):
         return _generate(model, input_ids, attention_mask, max_new_tokens, do_sample, temperature, top_p,
                          top_k, eos_token_id, pad_token_id, generator, return_mask, use_graph, seed)
 

@@ -434,7 +434,13 @@ def fp8_tiled_weight(w: torch.Tensor, norm_w: Optional[torch.Tensor] = None, glu
 
 
 def _f8_ok(rows: int, w: torch.Tensor) -> bool:
-    return _FP8[0] and rows <= 16 and w.shape[0] % 32 == 0 and w.shape[1] % 1024 == 0
+    """fp8 mode and a shape the fp8 kernels take: <= 16 rows csrc/skinny_ks.h F8 / skinny_glu_il F8,
+    17..64 rows csrc/skinny64.hip F8."""
+    if not _FP8[0]:
+        return False
+    if rows <= 16:
+        return w.shape[0] % 32 == 0 and w.shape[1] % 1024 == 0
+    return DECODE_M64 and rows <= 64 and w.shape[0] % 128 == 0 and w.shape[1] % 256 == 0
 
 
 def head_f8(x: torch.Tensor, w: torch.Tensor) -> Optional[torch.Tensor]:
@@ -442,14 +448,18 @@ def head_f8(x: torch.Tensor, w: torch.Tensor) -> Optional[torch.Tensor]:
     if not (_FP8[0] and x.is_cuda and _ext.use_native(x)) or torch.is_grad_enabled() and x.requires_grad:
         return None
     rows = x.numel() // x.shape[-1]
-    if not (1 <= rows <= 16 and _f8_ok(rows, w) and x.dtype == torch.bfloat16):
+    if not (1 <= rows <= 64 and _f8_ok(rows, w) and x.dtype == torch.bfloat16):
         return None
     w8, sc = fp8_tiled_weight(w)
-    y, _ = _ext.require().skinny_fused_f8(_rows(x), w8, sc, None, None, 0.0)
+    if rows > 16:
+        y, _ = _ext.require().skinny64_f8(_rows(x), w8, sc, None, None, 0.0, False)
+    else:
+        y, _ = _ext.require().skinny_fused_f8(_rows(x), w8, sc, None, None, 0.0)
     return y.view(*x.shape[:-1], w.shape[0])
 
 
-DERIVED_ATTRS = ("_dla_fold", "_dla_fold_t", "_dla_fold_g", "_dla_tile", "_dla_f8", "_dla_f8_n", "_dla_f8_g")
+DERIVED_ATTRS = ("_dla_fold", "_dla_fold_t", "_dla_fold_g", "_dla_tile", "_dla_f8", "_dla_f8_n", "_dla_f8_g",
+                 "_dla_fp8")  # (the last: ops.moe.fp8_weight, the fp8 prefill GEMMs' weight copy)
 
 
 def drop_derived_weights(model) -> int:
@@ -510,7 +520,10 @@ def skinny_residual(x: torch.Tensor, w: torch.Tensor, res: torch.Tensor):
     x2 = _rows(x)
     if _f8_ok(x2.shape[0], w):
         w8, sc = fp8_tiled_weight(w)
-        s, ssq = _ext.require().skinny_fused_f8(x2, w8, sc, _rows(res), None, 0.0)
+        if x2.shape[0] > 16:
+            s, ssq = _ext.require().skinny64_f8(x2, w8, sc, _rows(res), None, 0.0, False)
+        else:
+            s, ssq = _ext.require().skinny_fused_f8(x2, w8, sc, _rows(res), None, 0.0)
         return s.view(*res.shape[:-1], w.shape[0]), ssq
     wk = tiled_weight(w) if DECODE_TILED >= 2 else w
     s, ssq = _fused_op(x2.shape[0])(x2, wk, _rows(res), None, 0.0, False)
@@ -521,6 +534,11 @@ def skinny_normed(s: torch.Tensor, ssq: torch.Tensor, norm_w: torch.Tensor, eps:
                   w: torch.Tensor, glu: bool = False) -> torch.Tensor:
     """RMSNorm(s) * norm_w @ w^T from the producer's partials (glu: gate|up + SwiGLU epilogue)."""
     s2 = _rows(s)
+    if _f8_ok(s2.shape[0], w) and s2.shape[0] > 16:
+        # 17..64 rows: gate|up in the plain [gate; up] row order (the m64 GLU epilogue pairs them)
+        w8, sc = fp8_tiled_weight(w, norm_w)
+        y, _ = _ext.require().skinny64_f8(s2, w8, sc, None, ssq, float(eps), bool(glu))
+        return y.view(*s.shape[:-1], y.shape[-1])
     if _f8_ok(s2.shape[0], w):
         if glu:
             w8, sc = fp8_tiled_weight(w, norm_w, glu_il=True)
@@ -615,7 +633,7 @@ def qkv_attend(s: torch.Tensor, ssq: torch.Tensor, norm_w: torch.Tensor, eps: fl
     s2 = _rows(s)
     B, K = s2.shape
     if B > 16:
-        if not (DECODE_SLAB_ATTN and DECODE_M64 and DECODE_TILED >= 1 and B <= 64 and K % 256 == 0
+        if _FP8[0] or not (DECODE_SLAB_ATTN and DECODE_M64 and DECODE_TILED >= 1 and B <= 64 and K % 256 == 0
                 and w.shape[0] % 128 == 0):
             return None
         return cache.attend_slab(layer, s2, ssq, folded_weight(w, norm_w, tiled=True), eps, rope, window)

@@ -190,9 +190,42 @@ def enable_fp8_inference(model, enabled: bool = True) -> int:
     return n
 
 
+class fp8_inference_scope:
+    """Context manager: the layer projections of `model` run the fp8 inference GEMMs inside the
+    block (no-grad calls of >= 256 rows only, as `enable_fp8_inference`), then the previous
+    marking is restored. For a trainable policy's rollout prefill under fp8 rollouts
+    (models.generation.generate(weight_dtype="fp8")): sampling-only, the update recomputes every
+    log-prob in bf16."""
+
+    def __init__(self, model, enabled: bool = True):
+        self.model, self.enabled, self.prev = model, bool(enabled), []
+
+    def __enter__(self):
+        if self.enabled:
+            for layer in getattr(self.model, "layers", []):
+                at, mlp = getattr(layer, "attn", None), getattr(layer, "mlp", None)
+                for w in (getattr(at, "qkv_proj", None), getattr(at, "o_proj", None),
+                          getattr(mlp, "up_proj", None), getattr(mlp, "down_proj", None)):
+                    if isinstance(w, torch.Tensor) and w.dim() == 2:
+                        self.prev.append((w, getattr(w, "_dla_fp8_infer", None)))
+                        w._dla_fp8_infer = True
+        return self
+
+    def __exit__(self, *exc):
+        for w, v in self.prev:
+            if v is None:
+                w.__dict__.pop("_dla_fp8_infer", None)
+            else:
+                w._dla_fp8_infer = v
+        self.prev = []
+        return False
+
+
 def linear(x: torch.Tensor, weight: torch.Tensor, bias=None) -> torch.Tensor:
-    if uses_main_grad(weight):
-        return _LinearMainGradFn.apply(x, weight, bias)
+    # (fp8 inference first: it needs grad disabled, so a training forward never takes it; a
+    # trainable policy's no-grad rollout prefill inside fp8_inference_scope does)
     if fp8_inference_ok(x, weight, bias):
         return fp8_linear_frozen(x, weight)
+    if uses_main_grad(weight):
+        return _LinearMainGradFn.apply(x, weight, bias)
     return F.linear(x, weight, bias)

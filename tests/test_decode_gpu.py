@@ -825,9 +825,10 @@ def _dequant(w, norm_w=None):
     return q.view(torch.float8_e4m3fn).float() * sc[:, None]
 
 
-@pytest.mark.parametrize("M", [1, 7, 16])
+@pytest.mark.parametrize("M", [1, 7, 16, 24, 64])
 def test_fp8_decode_projection_kernels_match_dequant_fp32(M):
-    """The e4m3 weight streams (csrc/skinny_ks.h F8, skinny_glu_il_kernel F8): residual producer,
+    """The e4m3 weight streams (csrc/skinny_ks.h F8, skinny_glu_il_kernel F8 at <= 16 rows,
+    csrc/skinny64.hip F8 at 17..64 rows, both m64 tile heights): residual producer,
     norm-on-input qkv and the gate|up GLU against fp32 math on the DEQUANTISED weights (so only
     accumulation order and bf16 output rounding differ), and within fp8 quantisation error of the
     bf16 kernels."""
@@ -866,10 +867,12 @@ def test_fp8_decode_projection_kernels_match_dequant_fp32(M):
     assert rel(y16, h_ref @ wq.float().t()) < 1e-2  # (the bf16 reference itself)
 
 
-def test_fp8_generation_graph_matches_eager_and_tracks_bf16():
-    """generate(weight_dtype="fp8") on the fused decode layer: graph == eager (greedy, bitwise),
-    the fp8 copies are refreshed when the weights move, and the first decode step's logits stay
-    within quantisation error of the bf16 decode."""
+@pytest.mark.parametrize("B", [8, 40])
+def test_fp8_generation_graph_matches_eager_and_tracks_bf16(B):
+    """generate(weight_dtype="fp8") on the fused decode layer (B 8: csrc/skinny.hip F8 kernels,
+    B 40: csrc/skinny64.hip F8): graph == eager (greedy, bitwise), the fp8 copies are refreshed
+    when the weights move, and the first decode step's logits stay within quantisation error of
+    the bf16 decode."""
     from distributed_llm_alignment_amd import ops
     from distributed_llm_alignment_amd.models import build_model, generate
     from distributed_llm_alignment_amd.models.generation import KVCache, clear_graph_cache
@@ -877,7 +880,6 @@ def test_fp8_generation_graph_matches_eager_and_tracks_bf16():
     cfg = _fused_cfg()
     m = build_model(cfg, device=DEV, dtype=torch.bfloat16, seed=4).eval()
     g = torch.Generator(device=DEV).manual_seed(9)
-    B = 8
     ids = torch.randint(3, cfg.vocab_size, (B, 40), device=DEV, generator=g)
     nxt = torch.randint(3, cfg.vocab_size, (B, 1), device=DEV, generator=g)
     logits = {}
@@ -892,6 +894,9 @@ def test_fp8_generation_graph_matches_eager_and_tracks_bf16():
     assert getattr(m.layers[0].mlp.down_proj, "_dla_f8", None) is not None  # the fp8 path ran
     clear_graph_cache()
     a = generate(m, ids, max_new_tokens=12, do_sample=False, eos_token_id=-1, use_graph=False, weight_dtype="fp8")
+    # the prefill ran the fp8 inference GEMMs (their weight copy exists) and the marking is undone
+    w0 = m.layers[0].mlp.up_proj
+    assert getattr(w0, "_dla_fp8", None) is not None and not getattr(w0, "_dla_fp8_infer", False)
     b = generate(m, ids, max_new_tokens=12, do_sample=False, eos_token_id=-1, use_graph=True, weight_dtype="fp8")
     assert torch.equal(a, b)
     # weights move (an optimizer step): the in-place refreshed fp8 copies follow, graph reused

@@ -84,7 +84,7 @@ PASSES = {
         run("ppo_zero8", "python -u tools/bench_rlhf.py --algorithm ppo --zero-shape 8 --batch 8"),
         run("mixtral_ep8", MIX_EP8 + " --steps 3 --warmup 2"),
         run("mixtral_ep8_fp8", MIX_EP8 + " --fp8 --steps 3 --warmup 2"),
-        run("gen8_fp8", GEN8 + " --weight-dtype fp8", 300),
+        run("gen8_fp8", GEN8 + " --weight-dtype fp8", 300), run("gen64_fp8", GEN64 + " --weight-dtype fp8", 300),
         run("rlhf8_fp8", "python -u tools/bench_rlhf.py --batch 8 --rollout-dtype fp8", 400),
         run("ppo_zero8_fp8", "python -u tools/bench_rlhf.py --algorithm ppo --zero-shape 8 --batch 8 --rollout-dtype fp8"),
     ],
@@ -115,6 +115,8 @@ PASSES = {
     "decode-profile": [prof("dec8", GEN8, DEC_TABLE, 300), prof("dec64", GEN64, DEC_TABLE, 300)],
     "decode-fp8-profile": [prof("dec8_fp8", GEN8 + " --weight-dtype fp8", DEC_TABLE, 300),
                            prof("dec8_bf16", GEN8, DEC_TABLE, 300)],
+    "decode64-fp8-profile": [prof("dec64_fp8", GEN64 + " --weight-dtype fp8", DEC_TABLE, 300),
+                             prof("dec64_bf16", GEN64, DEC_TABLE, 300)],
     "mixtral-profile": [prof("mixtral", MIX_EP8 + " --steps 2 --warmup 1",
                              [("breakdown", []), ("window", ["--window", "adamw", "--top", "45"])])],
     "attn-pmc": [pmc("attn_p1", ATTN_P1, "python3 tools/attn_bench.py --iters 3",
