@@ -1587,7 +1587,10 @@ __global__ __launch_bounds__(512) void attn_bwd8_kernel(AttnBwdParams p) {
 
   // static priority for the second-dispatched half (waves 4-7 share SIMDs with 0-3 and lose
   // every VALU arbitration by age otherwise; MI355X_MICROARCH "Two waves per SIMD" item 4)
-  if (w >= 4) __builtin_amdgcn_s_setprio(1);
+  const bool cprio = p.bwd_prio != 0;  // per-cluster priority flips (A/B, DLA_ATTN_BWD_PRIO)
+  if (p.bwd_prio != 1 && w >= 4) __builtin_amdgcn_s_setprio(1);
+  auto prio_on = [&]() { if (cprio) __builtin_amdgcn_s_setprio(1); };
+  auto prio_off = [&]() { if (cprio && (p.bwd_prio == 1 || w < 4)) __builtin_amdgcn_s_setprio(0); };
   for (int it = 0; it < n_iter; ++it) {
     advance(hq_r, qt_r);
     asm volatile("" : "+v"(rq), "+v"(rx), "+v"(tq0), "+v"(tx0), "+v"(tq1), "+v"(tx1), "+v"(wq), "+v"(wx));
@@ -1630,6 +1633,7 @@ __global__ __launch_bounds__(512) void attn_bwd8_kernel(AttnBwdParams p) {
           __builtin_amdgcn_sched_barrier(0);
         }
       };
+      prio_on();
       chain(Qs, Kw, sacc);
       chain(dOs, Vw, dpacc);
       {  // + the row-constant k-step (last: its loads get the whole chains as slack)
@@ -1644,6 +1648,7 @@ __global__ __launch_bounds__(512) void attn_bwd8_kernel(AttnBwdParams p) {
         sacc = mfma32(ax, ones, sacc);
         dpacc = mfma32(ay, ones, dpacc);
       }
+      prio_off();
       BWD_TS(1);
       const int kj = kw + l32;
       int lo = 0, hi = min(p.Tq, kse) - qt - 4 * h;
@@ -1678,6 +1683,7 @@ __global__ __launch_bounds__(512) void attn_bwd8_kernel(AttnBwdParams p) {
       };
       ld_kv(0, 0);
       __builtin_amdgcn_sched_barrier(0);
+      prio_on();
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
         if (dt + 1 < DT) ld_kv(dt + 1, (dt + 1) & 1);
@@ -1689,6 +1695,7 @@ __global__ __launch_bounds__(512) void attn_bwd8_kernel(AttnBwdParams p) {
         dk[dt] = mfma32(td[dt & 1], sb1, dk[dt]);
         __builtin_amdgcn_sched_barrier(0);
       }
+      prio_off();
       BWD_TS(3);
     }
     {  // dS^T rows -> [key][32 queries] image (zero for an inactive sub-tile)
@@ -1725,6 +1732,7 @@ __global__ __launch_bounds__(512) void attn_bwd8_kernel(AttnBwdParams p) {
       };
       ld_dq(0, 0);
       ld_dq(1, 1);
+      prio_on();
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) {
         if (ks + 2 < NKS) ld_dq(ks + 2, (ks + 2) % NB);
@@ -1734,6 +1742,7 @@ __global__ __launch_bounds__(512) void attn_bwd8_kernel(AttnBwdParams p) {
           acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks % NB][t], kf[ks % NB], acc[t], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
       }
+      prio_off();
       // lane holds d = 16*slice + i16 of query rows 16t + 4*g4l + e (64-B row segments)
       const int64_t rs = static_cast<int64_t>(p.Hq) * D;
       const int64_t sbase = ((static_cast<int64_t>(kb) * p.B + b) * p.slab_rows + qt) * rs +
@@ -2174,7 +2183,12 @@ bool attn_dkv_part_bf16() {
 }
 
 template <int D>
-static void bwd_dispatch(const AttnBwdParams& p, bool causal, hipStream_t st) {
+static void bwd_dispatch(const AttnBwdParams& p_in, bool causal, hipStream_t st) {
+  AttnBwdParams p = p_in;
+  {
+    const char* e = std::getenv("DLA_ATTN_BWD_PRIO");  // A/B, read per call
+    p.bwd_prio = e ? std::atoi(e) : 0;
+  }
   const int nkb = (p.Tk + kAttnBwdKeys - 1) / kAttnBwdKeys;
   const dim3 grid(nkb * p.Hkv * p.B * p.hsplit);
   if (attn_bwd_waves() == 8) {

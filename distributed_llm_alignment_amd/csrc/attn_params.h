@@ -86,6 +86,8 @@ struct AttnBwdParams {
                           // forward's q_rot output)
   int rope_rot;           // rotary dims: D (full), or 32 at D = 80 (phi-2's partial rotary:
                           // only dims [0, 32) rotate, d < 16 pairing with d + 16)
+  int bwd_prio;           // issue priority (attn_bwd8_kernel): 0 static for waves 4-7, 1 s_setprio
+                          // 1 around every MFMA cluster, 2 both
 };
 
 }  // namespace dla
