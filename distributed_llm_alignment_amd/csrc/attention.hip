@@ -123,6 +123,21 @@ __device__ __forceinline__ f32x16 mfma32(s16x8 a, s16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
+// max / sum of x over lanes l and l ^ 32 by one v_permlane32_swap (VALU) instead of a
+// ds_bpermute round trip through LDS (cdna guide T12): with both operands x, every lane gets
+// {its own x, its partner's x} in some order, so the max is exact and the sum bitwise equal to
+// x + partner.
+__device__ __forceinline__ float xhalf_max(float x) {
+  const uint32_t u = __float_as_uint(x);
+  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xhalf_sum(float x) {
+  const uint32_t u = __float_as_uint(x);
+  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 // transposed 8-row fragment for the 32x32x16 A operand whose k index follows the accumulator
 // row permutation: elements 0..3 <- rows r0..r0+3, 4..7 <- rows r0+8..r0+11 (column c0 + lane).
 template <int D>
@@ -267,7 +282,29 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
   const int ntiles = kmax > tile0 ? (kmax - tile0 + BK - 1) / BK : 0;
 
   bf16x8 kreg[CPT], vreg[CPT];
+  // whole tiles load from a wave-uniform (SGPR) tile base + a per-lane 32-bit byte offset fixed for
+  // the kernel, with no per-chunk key test; the last, partial tile keeps the guarded form
+  const bool ofs32 =
+      p.fwd_sgpr != 0 && static_cast<int64_t>(BK) * (p.k_st > p.v_st ? p.k_st : p.v_st) * 2 < (1ll << 31);
+  uint32_t kofs[CPT], vofs[CPT];
+#pragma unroll
+  for (int c = 0; c < CPT; ++c) {
+    const int ci = tid + NT * c;
+    const int row = ci / NCH, ch = ci % NCH;
+    kofs[c] = static_cast<uint32_t>((row * p.k_st + ch * 8) * 2);
+    vofs[c] = static_cast<uint32_t>((row * p.v_st + ch * 8) * 2);
+  }
   auto gload = [&](int kt) {
+    if (ofs32 && kt + BK <= p.Tk && NCHL == NCH && CPT_EXACT) {  // wave-uniform
+      const char* kb = reinterpret_cast<const char*>(kp + static_cast<int64_t>(kt) * p.k_st);
+      const char* vb = reinterpret_cast<const char*>(vp + static_cast<int64_t>(kt) * p.v_st);
+#pragma unroll
+      for (int c = 0; c < CPT; ++c) {
+        kreg[c] = load_bf16x8(reinterpret_cast<const bf16_t*>(kb + kofs[c]));
+        vreg[c] = load_bf16x8(reinterpret_cast<const bf16_t*>(vb + vofs[c]));
+      }
+      return;
+    }
 #pragma unroll
     for (int c = 0; c < CPT; ++c) {
       const int ci = tid + NT * c;
@@ -405,7 +442,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
       for (int st = 0; st < 2; ++st)
 #pragma unroll
         for (int i = 0; i < 16; ++i) mloc = fmaxf(mloc, sacc[st][i]);
-      mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+      mloc = xhalf_max(mloc);
       // deferred max: rescale O only when some row's max grew by more than kRescaleThr (the
       // previous tile's P.V is complete, and this tile's P is exponentiated after the decision)
       if (!__all(mloc <= m + kRescaleThr)) {
@@ -460,7 +497,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
     if (t + 1 < ntiles) step(std::integral_constant<int, 1>{}, t + 1);
   }
 
-  lsum += __shfl_xor(lsum, 32, 64);
+  lsum = xhalf_sum(lsum);
   if (qi < p.Tq) {
     const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
     bf16_t* op = p.o + b * p.o_sb + qi * p.o_st + static_cast<int64_t>(hq) * p.o_sh;
@@ -575,6 +612,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_persist_kernel(AttnParams p,
   };
 
   bf16x8 kreg[CPT], vreg[CPT];
+  // (the SGPR-base / 32-bit offset form of attn_fwd_kernel's loads spills here: 256 VGPRs)
   auto gload = [&](const Blk& c, int kt) {
     const bf16_t* kp = p.k + c.b * p.k_sb + static_cast<int64_t>(c.hk) * p.k_sh;
     const bf16_t* vp = p.v + c.b * p.v_sb + static_cast<int64_t>(c.hk) * p.v_sh;
@@ -716,7 +754,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_persist_kernel(AttnParams p,
     for (int st = 0; st < 2; ++st)
 #pragma unroll
       for (int i = 0; i < 16; ++i) mloc = fmaxf(mloc, sacc[st][i]);
-    mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+    mloc = xhalf_max(mloc);
     if (!__all(mloc <= m + kRescaleThr)) {
       const float mnew = fmaxf(m, mloc);
       const float alpha = ex2(m - (mnew == -INFINITY ? 0.f : mnew));
@@ -761,7 +799,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_persist_kernel(AttnParams p,
 
   auto epilogue = [&](const Blk& c) {
     const int qi = c.q0 + l32;
-    const float ls = lsum + __shfl_xor(lsum, 32, 64);
+    const float ls = xhalf_sum(lsum);
     if (qi < p.Tq) {
       const float inv = ls > 0.f ? 1.f / ls : 0.f;
       bf16_t* op = p.o + c.b * p.o_sb + qi * p.o_st + static_cast<int64_t>(c.hq) * p.o_sh;
@@ -2113,6 +2151,8 @@ static void fwd_launch(const AttnParams& p0, bool causal, hipStream_t st) {
     // waves 4-7) measured +0-7 % and below 1 everywhere; 0 = off.
     const char* e = std::getenv("DLA_ATTN_FWD_PRIO");
     p.fwd_prio = e ? std::atoi(e) : 1;
+    const char* g = std::getenv("DLA_ATTN_FWD_SGPR");
+    p.fwd_sgpr = g ? std::atoi(g) : 1;
   }
   const int nqb = (p.Tq + BQ - 1) / BQ;
   const int64_t nblk = static_cast<int64_t>(nqb) * (p.Hq / HP) * p.B;

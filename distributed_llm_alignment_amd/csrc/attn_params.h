@@ -34,6 +34,7 @@ struct AttnParams {
   // head block) query columns so the concurrent workgroups of one L2 share every K/V tile
   int fwd_xcd;
   int fwd_prio;  // issue priority A/B (DLA_ATTN_FWD_PRIO): 1 = s_setprio 1 around each MFMA chain,
+  int fwd_sgpr;   // 1: whole K/V tiles load from an SGPR tile base + 32-bit lane offsets (A/B: DLA_ATTN_FWD_SGPR=0)
                  // 2 = static s_setprio 1 for the second wave of each SIMD (waves 4-7)
   unsigned long long* stamps;  // debug (DLA_ATTN_STAMPS=1): persistent forward seam stamps
 };
