@@ -338,30 +338,69 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
   };
 
   // Q fragments stay in registers, pre-scaled by softmax_scale*log2(e) so the scores come
-  // out of the MFMA already in the exp2 domain (no per-score multiply). (Issuing the K/V tile-0
-  // loads ahead of the Q loads measured -2.5 % .. +3 % by shape: kept in this order.)
+  // out of the MFMA already in the exp2 domain (no per-score multiply).
+  // Prologue load order (p.fwd_pro, default): Q rows, [RoPE: position, then its cos / sin rows],
+  // then the K/V tile-0 rows, then the Q math. vmcnt is in-order, so the Q math waits for Q (and
+  // cos / sin) only and runs under the K/V flight: one fewer dependent HBM round trip per block.
+  // (K/V issued AHEAD of Q measured -2.5 % .. +3 %: the Q math then waited for K/V too.) Each
+  // variant is one straight-line copy (a template lambda per (early, rope) pair): a control-flow
+  // merge between the loads and the math would make the compiler's waits conservative (vmcnt(0)).
+  // Rows past Tq / Tk are clamped into range and zeroed (Q) or masked (K/V: their scores are
+  // masked because need_mask covers kt + BK > kend, and their P is 0).
   s16x8 qf[KS];
-  {
+  auto prologue = [&](auto early_c, auto rope_c) {
+    constexpr bool EARLY = decltype(early_c)::value;
+    constexpr bool ROPE = decltype(rope_c)::value && DP == D;
     float qv[KS][8];
+    {
+      const int qc = min(qi, p.Tq - 1);
+      bf16x8 qraw[KS];
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      const bf16x8 raw = qi < p.Tq ? load_bf16x8(qp + qi * p.q_st + 16 * s + 8 * h) : bf16x8{};
+      for (int s = 0; s < KS; ++s) qraw[s] = load_bf16x8(qp + qc * p.q_st + 16 * s + 8 * h);
+      f32x4 rc[ROPE ? KS : 1], rs[ROPE ? KS : 1];  // cos / sin of columns 16s + 8h + [0, 8), s < KS/2
+      if constexpr (ROPE) {
+        // branch-free position: a valid dummy address when there is no position table
+        const int* pp = p.rope_pos ? p.rope_pos + static_cast<int64_t>(b) * p.Tq + qc
+                                   : reinterpret_cast<const int*>(qp);
+        const int pv = *pp;
+        const int pos = p.rope_pos ? pv : qc;
+        const float* cp = p.rope_cos + static_cast<int64_t>(pos) * (D / 2) + 8 * h;
+        const float* sp = p.rope_sin + static_cast<int64_t>(pos) * (D / 2) + 8 * h;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) qv[s][j] = bf2f(raw[j]);
-    }
-    if (DP == D && rope && qi < p.Tq) {
-      // RoPE on load: fragment s (columns 16s + 8h + j) pairs with fragment s + KS/2 (+ D/2)
-      const int pos = p.rope_pos ? p.rope_pos[static_cast<int64_t>(b) * p.Tq + qi] : qi;
-      const float* cp = p.rope_cos + static_cast<int64_t>(pos) * (D / 2) + 8 * h;
-      const float* sp = p.rope_sin + static_cast<int64_t>(pos) * (D / 2) + 8 * h;
+        for (int s = 0; s < KS / 2; ++s) {
+          rc[2 * s] = *reinterpret_cast<const f32x4*>(cp + 16 * s);
+          rc[2 * s + 1] = *reinterpret_cast<const f32x4*>(cp + 16 * s + 4);
+          rs[2 * s] = *reinterpret_cast<const f32x4*>(sp + 16 * s);
+          rs[2 * s + 1] = *reinterpret_cast<const f32x4*>(sp + 16 * s + 4);
+        }
+      }
+      if constexpr (EARLY) {
 #pragma unroll
-      for (int s = 0; s < KS / 2; ++s) {
+        for (int c = 0; c < CPT; ++c) {
+          const int ci = tid + NT * c;
+          const int key = max(min(tile0 + ci / NCH, p.Tk - 1), 0), ch = ci % NCH;
+          kreg[c] = load_bf16x8(kp + key * p.k_st + ch * 8);
+          vreg[c] = load_bf16x8(vp + key * p.v_st + ch * 8);
+        }
+      }
+      const bool qin = qi < p.Tq;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float c = cp[16 * s + j], sn = sp[16 * s + j];
-          const float a = qv[s][j], bb = qv[s + KS / 2][j];
-          qv[s][j] = a * c - bb * sn;
-          qv[s + KS / 2][j] = bb * c + a * sn;
+      for (int s = 0; s < KS; ++s) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qv[s][j] = qin ? bf2f(qraw[s][j]) : 0.f;
+      }
+      if constexpr (ROPE) {
+        // RoPE on load: fragment s (columns 16s + 8h + j) pairs with fragment s + KS/2 (+ D/2)
+#pragma unroll
+        for (int s = 0; s < KS / 2; ++s) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float c = j < 4 ? rc[2 * s][j] : rc[2 * s + 1][j - 4];
+            const float sn = j < 4 ? rs[2 * s][j] : rs[2 * s + 1][j - 4];
+            const float a = qv[s][j], bb = qv[s + KS / 2][j];
+            qv[s][j] = a * c - bb * sn;
+            qv[s + KS / 2][j] = bb * c + a * sn;
+          }
         }
       }
     }
@@ -373,16 +412,27 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
       qf[s] = __builtin_bit_cast(s16x8, pack_bf16x8(t));
     }
     // the rotated (unscaled) Q rows for the backward; the HP heads' waves write disjoint rows
-    if (rope && p.q_rot != nullptr && qi < p.Tq) {
+    if (ROPE && p.q_rot != nullptr && qi < p.Tq) {
       bf16_t* qo = p.q_rot + b * p.qr_sb + qi * p.qr_st + static_cast<int64_t>(hq) * p.qr_sh + 8 * h;
 #pragma unroll
       for (int s = 0; s < KS; ++s) store_bf16x8(qo + 16 * s, pack_bf16x8(qv[s]));
     }
-  }
-  if (ntiles > 0) {
-    gload(tile0);
-    lwrite(0, tile0);
-    if (ntiles > 1) gload(tile0 + BK);
+    if (ntiles > 0) {
+      if constexpr (!EARLY) gload(tile0);
+      lwrite(0, tile0);
+      if (ntiles > 1) gload(tile0 + BK);
+    }
+  };
+  {
+    using T_ = std::true_type;
+    using F_ = std::false_type;
+    if (p.fwd_pro != 0 && NCHL == NCH && CPT_EXACT) {
+      if (rope) prologue(T_{}, T_{});
+      else prologue(T_{}, F_{});
+    } else {
+      if (rope) prologue(F_{}, T_{});
+      else prologue(F_{}, F_{});
+    }
   }
   __syncthreads();
   if (p.fwd_prio == 2 && w >= NW / 2) __builtin_amdgcn_s_setprio(1);  // (MI355X_MICROARCH §Two waves item 4)
@@ -2153,6 +2203,8 @@ static void fwd_launch(const AttnParams& p0, bool causal, hipStream_t st) {
     p.fwd_prio = e ? std::atoi(e) : 1;
     const char* g = std::getenv("DLA_ATTN_FWD_SGPR");
     p.fwd_sgpr = g ? std::atoi(g) : 1;
+    const char* r = std::getenv("DLA_ATTN_FWD_PRO");
+    p.fwd_pro = r ? std::atoi(r) : 1;
   }
   const int nqb = (p.Tq + BQ - 1) / BQ;
   const int64_t nblk = static_cast<int64_t>(nqb) * (p.Hq / HP) * p.B;
