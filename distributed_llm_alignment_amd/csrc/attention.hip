@@ -548,6 +548,47 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
   }
 
   lsum = xhalf_sum(lsum);
+  if constexpr (DP == D && D == 128) {
+    if (p.fwd_ostage != 0) {
+      // O through LDS, stored as whole rows (cdna guide §5.6, pwg4x64 notes: per-lane 16-B stores
+      // at a row stride touch 32-64 lines per instruction). The loop ended on a barrier, so the K/V
+      // buffers are free: wave w stages its 32 x 128 tile (8 KB) there, chunk-swizzled by row
+      // (both the 16-B writes and the row reads are bank-conflict free), then each store
+      // instruction writes 4 contiguous 256-B rows.
+      const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+      bf16_t* ost = (w < 4 ? &Kb[0][0] : &Vb[0][0]) + (w & 3) * (32 * 128);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+#pragma unroll
+        for (int g4 = 0; g4 < 4; g4 += 2) {
+          uint2 a, c;
+          a.x = pack2bf(o[dt][4 * g4 + 0] * inv, o[dt][4 * g4 + 1] * inv);
+          a.y = pack2bf(o[dt][4 * g4 + 2] * inv, o[dt][4 * g4 + 3] * inv);
+          c.x = pack2bf(o[dt][4 * g4 + 4] * inv, o[dt][4 * g4 + 5] * inv);
+          c.y = pack2bf(o[dt][4 * g4 + 6] * inv, o[dt][4 * g4 + 7] * inv);
+          const auto rx = __builtin_amdgcn_permlane32_swap(a.x, c.x, false, false);
+          const auto ry = __builtin_amdgcn_permlane32_swap(a.y, c.y, false, false);
+          const int ch = 4 * dt + g4 + h;  // 16-B chunk of the row
+          *reinterpret_cast<uint4*>(ost + l32 * 128 + ((ch ^ (l32 & 15)) << 3)) =
+              make_uint4(rx[0], ry[0], rx[1], ry[1]);
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes done
+      __builtin_amdgcn_wave_barrier();
+      const int rr = lane >> 4, cc = lane & 15;
+      bf16_t* obase = p.o + b * p.o_sb + static_cast<int64_t>(hq) * p.o_sh;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int r = 4 * i + rr;
+        const uint4 v = *reinterpret_cast<const uint4*>(ost + r * 128 + ((cc ^ (r & 15)) << 3));
+        if (q0 + r < p.Tq) *reinterpret_cast<uint4*>(obase + (q0 + r) * p.o_st + cc * 8) = v;
+      }
+      if (qi < p.Tq && h == 0) {
+        p.lse2[(static_cast<int64_t>(b) * p.Hq + hq) * p.Tq + qi] = lsum > 0.f ? m + __log2f(lsum) : INFINITY;
+      }
+      return;
+    }
+  }
   if (qi < p.Tq) {
     const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
     bf16_t* op = p.o + b * p.o_sb + qi * p.o_st + static_cast<int64_t>(hq) * p.o_sh;
@@ -2205,6 +2246,8 @@ static void fwd_launch(const AttnParams& p0, bool causal, hipStream_t st) {
     p.fwd_sgpr = g ? std::atoi(g) : 1;
     const char* r = std::getenv("DLA_ATTN_FWD_PRO");
     p.fwd_pro = r ? std::atoi(r) : 1;
+    const char* os = std::getenv("DLA_ATTN_FWD_OSTAGE");
+    p.fwd_ostage = os ? std::atoi(os) : 1;
   }
   const int nqb = (p.Tq + BQ - 1) / BQ;
   const int64_t nblk = static_cast<int64_t>(nqb) * (p.Hq / HP) * p.B;

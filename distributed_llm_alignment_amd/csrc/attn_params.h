@@ -36,6 +36,7 @@ struct AttnParams {
   int fwd_prio;  // issue priority A/B (DLA_ATTN_FWD_PRIO): 1 = s_setprio 1 around each MFMA chain,
   int fwd_sgpr;   // 1: whole K/V tiles load from an SGPR tile base + 32-bit lane offsets (A/B: DLA_ATTN_FWD_SGPR=0)
   int fwd_pro;    // 1: K/V tile-0 loads issued right after the Q loads (A/B: DLA_ATTN_FWD_PRO=0)
+  int fwd_ostage; // 1: O staged through LDS and stored as whole rows (A/B: DLA_ATTN_FWD_OSTAGE=0)
                  // 2 = static s_setprio 1 for the second wave of each SIMD (waves 4-7)
   unsigned long long* stamps;  // debug (DLA_ATTN_STAMPS=1): persistent forward seam stamps
 };
