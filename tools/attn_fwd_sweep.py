@@ -24,6 +24,9 @@ def main():
     ap.add_argument("--D", type=int, default=128)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--ab", default="", help="ENV=v0,v1: interleave the settings per shape")
+    ap.add_argument("--v-strided", action="store_true",
+                    help="v as the strided view of a fused [B, T, (Hq + 2 Hkv) * D] qkv buffer, as the "
+                         "training step passes it (q, k contiguous: the RoPE pass writes them)")
     ap.add_argument("--cfg", action="append", default=[],
                     help="NAME:VAR=VAL[,VAR=VAL...] (repeatable): interleave these env settings per shape")
     a = ap.parse_args()
@@ -45,6 +48,12 @@ def main():
         q = torch.randn(B, T, a.Hq, a.D, device=dev, generator=g).to(torch.bfloat16)
         k = torch.randn(B, T, a.Hkv, a.D, device=dev, generator=g).to(torch.bfloat16)
         v = torch.randn(B, T, a.Hkv, a.D, device=dev, generator=g).to(torch.bfloat16)
+        if a.v_strided:
+            C = (a.Hq + 2 * a.Hkv) * a.D
+            buf = torch.zeros(B, T, C, device=dev, dtype=torch.bfloat16)
+            vs = buf[..., (a.Hq + a.Hkv) * a.D:].view(B, T, a.Hkv, a.D)
+            vs.copy_(v)
+            v = vs
         for causal in (True, False):
             flops = 4.0 * B * a.Hq * T * T * a.D / (2 if causal else 1)
             rec = {"B": B, "T": T, "causal": causal}
