@@ -214,7 +214,7 @@ __device__ __forceinline__ int fwd_persist_logical(int i, int g, int G, int nblk
 // per workgroup (HP = 2: waves 0..NW/2-1 take head 2p, the rest head 2p+1): every K/V tile staged
 // in LDS still feeds 32 NW query rows, but a head's query block is only BQ = 32 NW / HP rows, so
 // the causal diagonal (whose tiles run with part of the waves idle) is HP times narrower.
-template <int D, bool CAUSAL, int NW, int HP>
+template <int D, bool CAUSAL, int NW, int HP, bool MSUB = false>
 __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
   constexpr int NT = 64 * NW, BQ = 32 * NW / HP, BK = kFwdKeys;
   constexpr int WPH = NW / HP;  // waves per head
@@ -436,6 +436,16 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
   }
   __syncthreads();
   if (p.fwd_prio == 2 && w >= NW / 2) __builtin_amdgcn_s_setprio(1);  // (MI355X_MICROARCH §Two waves item 4)
+  // p.fwd_msub: the running max leaves the scores inside the MFMA chain instead of by 32 v_sub per
+  // tile. m is kept exactly representable as hi + lo (two bf16); one extra MFMA per tile,
+  // ones[key][k 0..1] x (-hi, -lo)[k 0..1][query], yields the tile of -m that the first Q.K^T step
+  // of both key halves takes as its C input, so the chain ends at S - m (the same row constant
+  // every score of the row gets, so P, l, O and the LSE stay consistent; only the fp32 rounding
+  // order of the subtraction moves). Rescales (rare: deferred max) subtract the change by VALU.
+  constexpr bool msub_on = MSUB;  // (a runtime switch keeping both paths spilled: 380 B scratch)
+  const s16x8 ones = __builtin_bit_cast(s16x8, u32x4{h ? 0u : 0x3F803F80u, 0u, 0u, 0u});
+  s16x8 mfrag = s16x8{};  // B operand: (-hi, -lo) of this lane's query row in k slots 0, 1
+  float msub = 0.f;       // the value the chain subtracts (m, or 0 while m is -inf)
   // the loop body runs as two copies (buffer 0 / buffer 1) so every LDS read address is a per-lane
   // base plus an immediate: no per-tile buffer select in the VALU stream
   auto step = [&](auto bufc, int t) {
@@ -451,13 +461,26 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
     if (active) {  // wave-uniform
       f32x16 sacc[2];
       if (p.fwd_prio == 1) __builtin_amdgcn_s_setprio(1);
+      if (msub_on) {
+        const f32x16 negm = mfma32(ones, mfrag, f32x16{});
 #pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        sacc[st] = f32x16{};
+        for (int st = 0; st < 2; ++st) {
+          sacc[st] = mfma32(*reinterpret_cast<const s16x8*>(Ks + swz<DP>(32 * st + l32, h)), qf[0], negm);
 #pragma unroll
-        for (int s = 0; s < KS; ++s) {
-          const s16x8 a = *reinterpret_cast<const s16x8*>(Ks + swz<DP>(32 * st + l32, 2 * s + h));
-          sacc[st] = mfma32(a, qf[s], sacc[st]);
+          for (int s = 1; s < KS; ++s) {
+            const s16x8 a = *reinterpret_cast<const s16x8*>(Ks + swz<DP>(32 * st + l32, 2 * s + h));
+            sacc[st] = mfma32(a, qf[s], sacc[st]);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          sacc[st] = f32x16{};
+#pragma unroll
+          for (int s = 0; s < KS; ++s) {
+            const s16x8 a = *reinterpret_cast<const s16x8*>(Ks + swz<DP>(32 * st + l32, 2 * s + h));
+            sacc[st] = mfma32(a, qf[s], sacc[st]);
+          }
         }
       }
       if (p.fwd_prio == 1) __builtin_amdgcn_s_setprio(0);
@@ -493,25 +516,58 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) mloc = fmaxf(mloc, sacc[st][i]);
       mloc = xhalf_max(mloc);
-      // deferred max: rescale O only when some row's max grew by more than kRescaleThr (the
-      // previous tile's P.V is complete, and this tile's P is exponentiated after the decision)
-      if (!__all(mloc <= m + kRescaleThr)) {
-        const float mnew = fmaxf(m, mloc);
-        const float alpha = ex2(m - (mnew == -INFINITY ? 0.f : mnew));
-        m = mnew;
-        lsum *= alpha;
-#pragma unroll
-        for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
-      }
-      const float muse = m == -INFINITY ? 0.f : m;
       float lpart[2] = {0.f, 0.f};  // two independent add chains (the row sum was one 32-add chain)
+      if (msub_on) {
+        // the scores are S - msub; deferred max as below, on the true scale mloc + msub
+        if (!__all(mloc + msub <= m + kRescaleThr)) {
+          const float mnew = fmaxf(m, mloc + msub);
+          float mq = -INFINITY, hi = 0.f, lo = 0.f;
+          if (mnew != -INFINITY) {  // m as hi + lo (two bf16), exact in fp32
+            hi = bf2f(f2bf(mnew));
+            lo = bf2f(f2bf(mnew - hi));
+            mq = hi + lo;
+          }
+          const float alpha = ex2(m - (mq == -INFINITY ? 0.f : mq));
+          const float nsub = mq == -INFINITY ? 0.f : mq;
+          const float d = nsub - msub;
+          m = mq;
+          msub = nsub;
+          mfrag = __builtin_bit_cast(s16x8, u32x4{h ? 0u : pack2bf(-hi, -lo), 0u, 0u, 0u});
+          lsum *= alpha;
 #pragma unroll
-      for (int st = 0; st < 2; ++st) {
+          for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const float pv = ex2(sacc[st][i] - muse);
-          sacc[st][i] = pv;
-          lpart[st] += pv;
+          for (int st = 0; st < 2; ++st) sacc[st] -= d;
+        }
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const float pv = ex2(sacc[st][i]);
+            sacc[st][i] = pv;
+            lpart[st] += pv;
+          }
+        }
+      } else {
+        // deferred max: rescale O only when some row's max grew by more than kRescaleThr (the
+        // previous tile's P.V is complete, and this tile's P is exponentiated after the decision)
+        if (!__all(mloc <= m + kRescaleThr)) {
+          const float mnew = fmaxf(m, mloc);
+          const float alpha = ex2(m - (mnew == -INFINITY ? 0.f : mnew));
+          m = mnew;
+          lsum *= alpha;
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
+        }
+        const float muse = m == -INFINITY ? 0.f : m;
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const float pv = ex2(sacc[st][i] - muse);
+            sacc[st][i] = pv;
+            lpart[st] += pv;
+          }
         }
       }
       lsum += lpart[0] + lpart[1];
@@ -2263,6 +2319,10 @@ static void fwd_launch(const AttnParams& p0, bool causal, hipStream_t st) {
     p.fwd_pro = r ? std::atoi(r) : 1;
     const char* os = std::getenv("DLA_ATTN_FWD_OSTAGE");
     p.fwd_ostage = os ? std::atoi(os) : 1;
+    // MSUB (D = 128): same box, graph-timed, interleaved: causal T1024 701 vs 668 TF/s, T2048
+    // 898 vs 865, non-causal +3-7 % (gpurun_out/r5/attn13); outputs within one bf16 ulp
+    const char* mx = std::getenv("DLA_ATTN_FWD_MSUB");
+    p.fwd_msub = mx ? std::atoi(mx) : 1;
   }
   const int nqb = (p.Tq + BQ - 1) / BQ;
   const int64_t nblk = static_cast<int64_t>(nqb) * (p.Hq / HP) * p.B;
@@ -2274,6 +2334,13 @@ static void fwd_launch(const AttnParams& p0, bool causal, hipStream_t st) {
     return;
   }
   const dim3 grid(static_cast<unsigned>(nblk));
+  if constexpr (D == 128) {
+    if (p.fwd_msub) {
+      if (causal) attn_fwd_kernel<D, true, NW, HP, true><<<grid, 64 * NW, 0, st>>>(p);
+      else attn_fwd_kernel<D, false, NW, HP, true><<<grid, 64 * NW, 0, st>>>(p);
+      return;
+    }
+  }
   if (causal) attn_fwd_kernel<D, true, NW, HP><<<grid, 64 * NW, 0, st>>>(p);
   else attn_fwd_kernel<D, false, NW, HP><<<grid, 64 * NW, 0, st>>>(p);
 }

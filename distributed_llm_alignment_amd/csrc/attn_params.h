@@ -37,6 +37,7 @@ struct AttnParams {
   int fwd_sgpr;   // 1: whole K/V tiles load from an SGPR tile base + 32-bit lane offsets (A/B: DLA_ATTN_FWD_SGPR=0)
   int fwd_pro;    // 1: K/V tile-0 loads issued right after the Q loads (A/B: DLA_ATTN_FWD_PRO=0)
   int fwd_ostage; // 1: O staged through LDS and stored as whole rows (A/B: DLA_ATTN_FWD_OSTAGE=0)
+  int fwd_msub;   // 1: running max subtracted inside the Q.K^T MFMA chain (A/B: DLA_ATTN_FWD_MSUB)
                  // 2 = static s_setprio 1 for the second wave of each SIMD (waves 4-7)
   unsigned long long* stamps;  // debug (DLA_ATTN_STAMPS=1): persistent forward seam stamps
 };

@@ -359,9 +359,14 @@ def test_attention_bwd_deterministic(bwd_waves):
         assert torch.equal(a, b)
 
 
-def test_attention_fwd_forced_rescale():
+@pytest.mark.parametrize("persist", [None, "0"])
+def test_attention_fwd_forced_rescale(persist, monkeypatch):
     """Deferred-max rescale branch (cdna guide §5.4 rule 26): one key spikes against one query
-    row so that row's running max jumps far past the threshold at a late tile."""
+    row so that row's running max jumps far past the threshold at a late tile. persist "0": the
+    lockstep kernel, whose D = 128 form subtracts the running max inside the MFMA chain and
+    moves the rescale's difference by VALU (DLA_ATTN_FWD_MSUB)."""
+    if persist is not None:
+        monkeypatch.setenv("DLA_ATTN_FWD_PERSIST", persist)
     B, T, Hq, Hkv, D = 1, 512, 4, 1, 128
     q = torch.randn(B, T, Hq, D) * 0.3
     k = torch.randn(B, T, Hkv, D) * 0.3
@@ -988,6 +993,9 @@ def test_attention_fwd_persistent_bitwise(case, monkeypatch):
         cos, sin = RotaryCache(D, 500000.0, 4096).tables(q.device)
         extra = (cos, sin, None)
     outs = {}
+    # the persistent kernel runs the lockstep kernel's tile math without the in-MFMA max
+    # subtraction (DLA_ATTN_FWD_MSUB, D = 128 lockstep only; covered by the fp32-oracle tests)
+    monkeypatch.setenv("DLA_ATTN_FWD_MSUB", "0")
     # (ping-pong, persistent, XCD block order): "000" is the one-block-per-workgroup lockstep kernel
     for pp, persist, xcd in (("0", "0", "0"), ("0", "0", "1"), ("0", "1", "0"), ("0", "1", "1"),
                              ("1", "0", "0"), ("1", "0", "1")):
