@@ -1844,25 +1844,16 @@ __global__ __launch_bounds__(512) void attn_bwd8_kernel(AttnBwdParams p) {
         if (p.window > 0) hi = min(hi, dlt + p.window);
       }
       const unsigned span = hi > lo ? static_cast<unsigned>(hi - lo) : 0u;
-      if (p.bwd_msplit != 0) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) sacc[i] = ex2(sacc[i] * p.scale2);
-        // the mask as its own wave-uniform branch: fused into the exp loop (below), the compiler
-        // if-converts it and every tile pays 16 compares + 16 selects + the bound arithmetic
-        if (need_mask) {
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const int rr = (i & 3) + 8 * (i >> 2);
-            sacc[i] = static_cast<unsigned>(rr - lo) < span ? sacc[i] : 0.f;
-          }
-        }
-      } else {
+      for (int i = 0; i < 16; ++i) sacc[i] = ex2(sacc[i] * p.scale2);
+      // the mask as its own wave-uniform branch: fused into the exp loop, the compiler
+      // if-converted it and every tile paid 16 compares + 16 selects + the bound arithmetic
+      // (bwd +2-3 % causal, same box, bitwise: gpurun_out/r5/bwdms)
+      if (need_mask) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int rr = (i & 3) + 8 * (i >> 2);
-          float pv = ex2(sacc[i] * p.scale2);
-          if (need_mask) pv = static_cast<unsigned>(rr - lo) < span ? pv : 0.f;
-          sacc[i] = pv;
+          sacc[i] = static_cast<unsigned>(rr - lo) < span ? sacc[i] : 0.f;
         }
       }
 #pragma unroll
@@ -2405,8 +2396,7 @@ static void bwd_dispatch(const AttnBwdParams& p_in, bool causal, hipStream_t st)
   {
     const char* e = std::getenv("DLA_ATTN_BWD_PRIO");  // A/B, read per call
     p.bwd_prio = e ? std::atoi(e) : 0;
-    const char* ms = std::getenv("DLA_ATTN_BWD_MSPLIT");
-    p.bwd_msplit = ms ? std::atoi(ms) : 1;
+
   }
   const int nkb = (p.Tk + kAttnBwdKeys - 1) / kAttnBwdKeys;
   const dim3 grid(nkb * p.Hkv * p.B * p.hsplit);

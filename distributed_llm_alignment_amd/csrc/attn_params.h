@@ -92,7 +92,6 @@ struct AttnBwdParams {
                           // only dims [0, 32) rotate, d < 16 pairing with d + 16)
   int bwd_prio;           // issue priority (attn_bwd8_kernel): 0 static for waves 4-7, 1 s_setprio
                           // 1 around every MFMA cluster, 2 both
-  int bwd_msplit;         // 1: causal / bounds mask as its own branch (A/B: DLA_ATTN_BWD_MSPLIT=0)
 };
 
 }  // namespace dla

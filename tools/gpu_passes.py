@@ -89,6 +89,9 @@ PASSES = {
         run("ppo_zero8_fp8", "python -u tools/bench_rlhf.py --algorithm ppo --zero-shape 8 --batch 8 --rollout-dtype fp8"),
     ],
     # ---- round 5
+    # the validation table in two gpurun-sized halves (a call runs at most 20 minutes)
+    "validate-a": [],
+    "validate-b": [],
     "force-pg": [
         pytest("tests/test_force_comm.py -m gpu", 400),
         prof("force_pg", DPO + " --force-pg --steps 2 --warmup 1",
@@ -263,6 +266,10 @@ class Runner:
             print(f"pmc {s['name']}: {dst}")
         else:
             raise ValueError(k)
+
+
+PASSES["validate-a"] = PASSES["validate"][:4]
+PASSES["validate-b"] = PASSES["validate"][4:]
 
 
 def main(argv=None):
