@@ -369,6 +369,20 @@ def _single_lib(offs: torch.Tensor, w: torch.Tensor, rows: int) -> bool:
             and rows >= 256)
 
 
+# Single local expert, main + overflow rows: the capacity buffer holds ep * C = cf * n * k rows, of
+# which a balanced routing fills the first n * k (the expected load). The library GEMMs run over
+# those `main` rows only; the rows past them (filled only when this rank's expert draws more than
+# its share) run on the device-driven grouped kernels with offsets shifted by `main`, which exit
+# at once when that overflow is empty. No host sync either way. DLA_MOE_MAIN_ROWS=0: the library
+# GEMMs cover the whole buffer (every padding row computed).
+MOE_MAIN_ROWS = os.environ.get("DLA_MOE_MAIN_ROWS", "1") != "0"
+
+
+def _tail_offs(offs: torch.Tensor, main: int) -> torch.Tensor:
+    """Offsets of the rows past `main` (single group): [0, max(offs[-1] - main, 0)], on device."""
+    return torch.clamp(offs - main, min=0).to(torch.int32)
+
+
 # Capacity-buffer padding rows (past offs[-1]) zeroed in place on the node's own outputs instead of
 # by out-of-place masked_fills (a clone + fill of the [rows, H] buffer each way; Mixtral EP shape:
 # ~70 ms per step). DLA_MOE_TAIL_INPLACE=0 restores the masked_fills for A/B.
@@ -380,8 +394,10 @@ class _GroupedExpertsFn(torch.autograd.Function):
     `sync_free`: the backward also stays on the grouped kernels (never reads offs on the host)."""
 
     @staticmethod
-    def forward(ctx, xs, w_up, w_down, offs, fp8: bool, sync_free: bool = False):
+    def forward(ctx, xs, w_up, w_down, offs, fp8: bool, sync_free: bool = False, main_rows: int = 0):
         C = _ext.require()
+        rows = xs.shape[0]
+        main = main_rows if (MOE_MAIN_ROWS and 0 < main_rows < rows) else rows
         if fp8:
             wu_q, wu_s = fp8_weight(w_up)
             wd_q, wd_s = fp8_weight(w_down)
@@ -391,7 +407,11 @@ class _GroupedExpertsFn(torch.autograd.Function):
             ys = C.gg_fwd(aq, wd_q, offs, asc, wd_s)
         else:
             gu, a = C.gg_fwd_swiglu(xs, w_up, offs, None, None)
-            if _single_lib(offs, w_down, a.shape[0]):
+            if _single_lib(offs, w_down, a.shape[0]) and main < rows:
+                ys = torch.empty((rows, w_down.shape[1]), dtype=a.dtype, device=a.device)
+                torch.matmul(a[:main], w_down.detach()[0].t(), out=ys[:main])
+                ys[main:].copy_(C.gg_fwd(a[main:], w_down, _tail_offs(offs, main), None, None))
+            elif _single_lib(offs, w_down, a.shape[0]):
                 ys = F.linear(a, w_down.detach()[0])
             else:
                 ys = C.gg_fwd(a, w_down, offs, None, None)
@@ -402,6 +422,7 @@ class _GroupedExpertsFn(torch.autograd.Function):
         ctx.save_for_backward(xs, gu, offs)
         ctx.w_up, ctx.w_down = w_up, w_down  # (on ctx: see ops.linear._LinearMainGradFn)
         ctx.sync_free = sync_free
+        ctx.main = main
         return ys
 
     @staticmethod
@@ -425,12 +446,18 @@ class _GroupedExpertsFn(torch.autograd.Function):
             # unwritten must be zero (xs's and dys's already are)
             C.zero_rows_from(dgu, offs[1:])
             C.zero_rows_from(a, offs[1:])
+        rows, main = dgu.shape[0], min(ctx.main, dgu.shape[0])
+        offs_t = _tail_offs(offs, main) if single and main < rows else None
         outs = []
         for w, dy, x, need in ((w_up, dgu, xs, ctx.needs_input_grad[1]),
                                (w_down, dys, a, ctx.needs_input_grad[2])):
             mg = getattr(w, "main_grad", None)
             if single and mg is not None and mg.is_contiguous() and mg.dtype in (torch.bfloat16, torch.float32):
-                _wgrad_accumulate(mg[0], dy, x)
+                if offs_t is not None:  # main rows on the library, overflow rows on the grouped kernel
+                    _wgrad_accumulate(mg[0], dy[:main], x[:main])
+                    C.gg_wgrad(dy[main:].contiguous(), x[main:].contiguous(), offs_t, mg, True)
+                else:
+                    _wgrad_accumulate(mg[0], dy, x)
                 hook = getattr(w, "_dla_grad_hook", None)
                 if hook is not None:
                     hook(w)
@@ -449,7 +476,13 @@ class _GroupedExpertsFn(torch.autograd.Function):
                 outs.append(None)
         dxs = None
         if ctx.needs_input_grad[0]:
-            if _single_lib(offs, w_up, dgu.shape[0]):
+            if _single_lib(offs, w_up, dgu.shape[0]) and offs_t is not None:
+                dxs = torch.empty((rows, w_up.shape[2]), dtype=dgu.dtype, device=dgu.device)
+                torch.matmul(dgu[:main], _expert0_t(w_up).t(), out=dxs[:main])  # as F.linear below
+                tail = C.gg_dgrad(dgu[main:], w_up, offs_t)
+                C.zero_rows_from(tail, offs_t[-1:])  # overflow rows the grouped kernel left unwritten
+                dxs[main:].copy_(tail)
+            elif _single_lib(offs, w_up, dgu.shape[0]):
                 dxs = F.linear(dgu, _expert0_t(w_up))  # dgu [M, 2F] . W_up[0] [2F, H], TN layout
             else:
                 dxs = C.gg_dgrad(dgu, w_up, offs)
@@ -460,7 +493,7 @@ class _GroupedExpertsFn(torch.autograd.Function):
             # rows past offs[-1] (padding of a capacity buffer) are never written by the grouped
             # kernel (single: dgu's padding rows are zero, so dxs's are too)
             C.zero_rows_from(dxs, offs[-1:])
-        return dxs, outs[0], outs[1], None, None, None
+        return dxs, outs[0], outs[1], None, None, None, None
 
 
 def grouped_gemm_enabled() -> bool:
@@ -540,16 +573,17 @@ def _ref_grouped_experts(xs, w_up, w_down, offs):
 
 
 def experts_swiglu_offsets(xs: torch.Tensor, w_up: torch.Tensor, w_down: torch.Tensor,
-                           offs: torch.Tensor, fp8: bool = False) -> torch.Tensor:
+                           offs: torch.Tensor, fp8: bool = False, main_rows: int = 0) -> torch.Tensor:
     """Grouped experts over rows whose per-expert ranges are given ONLY as a device offsets array
     offs [E+1] (rows past offs[-1] are padding: ignored, zero output and gradient). Never reads
-    the offsets on the host, forward or backward: the sync-free expert-parallel path."""
+    the offsets on the host, forward or backward: the sync-free expert-parallel path.
+    `main_rows`: the expected fill of a single local expert's buffer (see MOE_MAIN_ROWS)."""
     xs = xs.contiguous()
     if _grouped_ok(xs, w_up, w_down):
         if fp8 and _FP8 is None:
             fp8 = False
         # rows past offs[-1] come back zero (zeroed in place inside the node)
-        ys = _GroupedExpertsFn.apply(xs, w_up, w_down, offs.to(torch.int32), bool(fp8), True)
+        ys = _GroupedExpertsFn.apply(xs, w_up, w_down, offs.to(torch.int32), bool(fp8), True, int(main_rows))
         if not _TAIL_INPLACE:
             tail = torch.arange(ys.shape[0], device=ys.device) >= offs[-1].long()
             ys = ys.masked_fill(tail.unsqueeze(-1), 0)

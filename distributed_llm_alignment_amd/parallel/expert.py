@@ -295,16 +295,20 @@ class ExpertParallel:
             # a token fills up to k slots: its gradient is the sum of theirs, gathered through pos
             xs = _gather_rows(h2c[ci], send_src, injective=False, inv=pos)
             xr = _A2AStart.apply(xs, self.group, holder)
-            stage.append((C, pos, w, rc, xr))
+            stage.append((C, pos, w, rc, xr, (b - a) * k))
         # 2) per chunk: wait for its rows, experts on the device-built order, return all-to-all
         back = []
-        for C, pos, w, rc, xr in stage:
+        for C, pos, w, rc, xr, nk in stage:
             if w is not None:
                 w.wait()
             xr = _A2AWait.apply(xr, holder)
             xe_src, inv, offs = self._expert_order(rc, C)
             xe = _gather_rows(xr, xe_src)
-            ye = ops.moe.experts_swiglu_offsets(xe, moe.expert_up, moe.expert_down, offs, fp8=moe.fp8)
+            # a single local expert's expected rows under balanced routing: the chunk's n * k slots
+            # (its buffer holds cf * n * k), as a multiple of the 256-row GEMM tile
+            main = min(xe.shape[0], (nk + 255) // 256 * 256) if self.El == 1 else 0
+            ye = ops.moe.experts_swiglu_offsets(xe, moe.expert_up, moe.expert_down, offs, fp8=moe.fp8,
+                                                main_rows=main)
             yr = _gather_rows(ye, inv)
             back.append((pos, _A2AStart.apply(yr, self.group, holder)))
         # 3) combine each chunk (dropped slots point one past the buffer: the native combine reads

@@ -431,3 +431,36 @@ def test_native_gather_rows_bwd_through_inverse_map():
     ref = torch.zeros(N, H, device=DEV).index_add_(0, src.clamp(min=0), go.float() * (src >= 0).unsqueeze(-1))
     assert torch.equal(out[0][1], ref.to(torch.bfloat16))  # k = 2: both sums are exact-order fp32
     assert torch.equal(out[0][1], out[1][1])
+
+
+@pytest.mark.parametrize("main", [512, 768, 1024])
+def test_single_expert_main_overflow_split_matches_whole_buffer(main):
+    """One local expert over a capacity buffer with the library GEMMs on the first `main` rows and
+    the overflow rows [main, offs[-1]) on the grouped kernels (ops.moe.MOE_MAIN_ROWS): forward,
+    input gradient and the main-grad weight gradients against the same node over the whole buffer
+    (main 1024 = every row on the library). Rows past offs[-1] stay zero."""
+    from distributed_llm_alignment_amd import ops
+
+    g = torch.Generator(device=DEV).manual_seed(21)
+    rows, H, F, valid = 1024, 512, 512, 900
+    xs = (torch.randn(rows, H, device=DEV, generator=g)).to(torch.bfloat16)
+    xs[valid:] = 0
+    w_up = (torch.randn(1, 2 * F, H, device=DEV, generator=g) * H ** -0.5).to(torch.bfloat16)
+    w_down = (torch.randn(1, H, F, device=DEV, generator=g) * F ** -0.5).to(torch.bfloat16)
+    offs = torch.tensor([0, valid], dtype=torch.int32, device=DEV)
+    dy = torch.randn(rows, H, device=DEV, generator=g).to(torch.bfloat16)
+    dy[valid:] = 0
+    res = {}
+    for m in (main, 0):
+        wu, wd = w_up.clone(), w_down.clone()
+        wu.main_grad = torch.zeros(wu.shape, dtype=torch.float32, device=DEV)
+        wd.main_grad = torch.zeros(wd.shape, dtype=torch.float32, device=DEV)
+        x = xs.clone().requires_grad_(True)
+        y = ops.moe.experts_swiglu_offsets(x, wu, wd, offs, main_rows=m)
+        (dx,) = torch.autograd.grad(y, [x], dy)
+        res[m] = (y.float(), dx.float(), wu.main_grad.clone(), wd.main_grad.clone())
+    rel = lambda a, b: float((a - b).norm() / b.norm().clamp_min(1e-12))
+    for a, b in zip(res[main], res[0]):
+        assert rel(a, b) < 1e-2
+    assert float(res[main][0][valid:].abs().max()) == 0.0
+    assert float(res[main][1][valid:].abs().max()) == 0.0
