@@ -433,6 +433,12 @@ __global__ __launch_bounds__(512) void skinny_ksplit_kernel(
 // fused decode-layer launches (KsFuse): the residual-producing projection and the
 // norm-consuming qkv projection on the in-workgroup split-K kernel, the gate|up GLU on the LDS
 // kernel. M <= 16.
+// DLA_SKINNY_STRAIGHT (A/B, read per launch): ks_body's branch-free ring (KsFuse::straight)
+static int ks_straight() {
+  const char* e = getenv("DLA_SKINNY_STRAIGHT");
+  return e ? atoi(e) : 1;
+}
+
 template <bool TW, bool NT, bool F8 = false>
 static void launch_ks_fused_t(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
                               int64_t ldy, int M, int N, int K, const KsFuse& fz, bool res, bool nin,
@@ -443,7 +449,9 @@ static void launch_ks_fused_t(const bf16_t* x, int64_t ldx, const bf16_t* W, int
   }();
   const int nb = N / 16;
   const bool deep = K >= deep_k;
-#define DLA_KSF(D, R, NI) skinny_ksplit_kernel<D, NT, false, 1, kKsUnroll, R, NI, TW, F8><<<nb, 512, 0, st>>>(x, ldx, W, ldw, y, ldy, M, N, K, fz)
+  KsFuse f = fz;
+  f.straight = ks_straight();
+#define DLA_KSF(D, R, NI) skinny_ksplit_kernel<D, NT, false, 1, kKsUnroll, R, NI, TW, F8><<<nb, 512, 0, st>>>(x, ldx, W, ldw, y, ldy, M, N, K, f)
   if (res && nin) {
     if (deep) DLA_KSF(4, true, true); else DLA_KSF(2, true, true);
   } else if (res) {
@@ -479,7 +487,9 @@ void launch_skinny_ks_fused_f8(const bf16_t* x, int64_t ldx, const uint8_t* W8, 
     const char* e = getenv("DLA_KS_F8_DEPTH");
     return (e && atoi(e) == 4) ? 4 : 2;
   }();
-#define DLA_KSF8(D, NTV, R, NI) skinny_ksplit_kernel<D, NTV, false, 1, kKsUnroll, R, NI, true, true><<<nb, 512, 0, st>>>(x, ldx, W, K, y, ldy, M, N, K, fz)
+  KsFuse f = fz;
+  f.straight = ks_straight();
+#define DLA_KSF8(D, NTV, R, NI) skinny_ksplit_kernel<D, NTV, false, 1, kKsUnroll, R, NI, true, true><<<nb, 512, 0, st>>>(x, ldx, W, K, y, ldy, M, N, K, f)
 #define DLA_KSF8_NT(D)                           \
   if (decode_nt()) {                             \
     if (res && nin) DLA_KSF8(D, true, true, true);   \

@@ -132,15 +132,67 @@ __device__ __forceinline__ void ks_body(
         if (arow[t]) a[j][u][t] = __builtin_bit_cast(s16x8, load_bf16x8(xrow[t] + c * CH + u * 32));
       }
   };
+  // fz.straight: the same ring with no load inside a branch. hipcc counts outstanding loads per
+  // path; a refill under `if (c + DEPTH < nchunks)` or an x load under `if (arow)` made it wait
+  // vmcnt(0) -- the whole ring -- before every chunk's MFMAs. Here x rows past M load row 0 and are
+  // masked to zero by AND, and the loop runs as a steady part whose refills are always in range
+  // plus a tail without loads (nchunks a multiple of DEPTH; other shapes keep the form below).
+  auto load_nb = [&](int j, int c) {
+    if constexpr (F8) {
 #pragma unroll
-  for (int j = 0; j < DEPTH; ++j)
-    if (j < nchunks) load(j, j);
-  KsPart part{};
-  if constexpr (NIN) part = ks_part_load(fz, M, wave, lane);  // reduced in the epilogue
+      for (int u = 0; u < UB; ++u) b8[j][u] = load_w8<NT>(wrow8 + (c * UB + u) * 1024);
+    } else {
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) b[j][u] = load_w<NT>(TW ? wrow + (c * UNR + u) * 512 : wrow + c * CH + u * 32);
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u)
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        const ks_u32x4 v = __builtin_bit_cast(ks_u32x4, load_bf16x8(xrow[t] + c * CH + u * 32));
+        const uint32_t keep = arow[t] ? 0xffffffffu : 0u;
+        a[j][u][t] = __builtin_bit_cast(s16x8, ks_u32x4{v[0] & keep, v[1] & keep, v[2] & keep, v[3] & keep});
+      }
+  };
   f32x4 acc[MT];
 #pragma unroll
   for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int c0 = 0; c0 < nchunks; c0 += DEPTH) {
+  auto compute = [&](int j) {
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      s16x8 bu;
+      if constexpr (F8) {
+        const ks_u32x4 wv = b8[j][u >> 1];
+        bu = (u & 1) ? f8x8_to_bf16(wv[2], wv[3]) : f8x8_to_bf16(wv[0], wv[1]);
+      } else {
+        bu = b[j][u];
+      }
+#pragma unroll
+      for (int t = 0; t < MT; ++t) acc[t] = mfma16(a[j][u][t], bu, acc[t]);
+    }
+  };
+  const bool sl = fz.straight != 0 && nchunks >= DEPTH && nchunks % DEPTH == 0;  // kernel-uniform
+  KsPart part{};
+  if (sl) {
+#pragma unroll
+    for (int j = 0; j < DEPTH; ++j) load_nb(j, j);
+    if constexpr (NIN) part = ks_part_load(fz, M, wave, lane);  // reduced in the epilogue
+    for (int c0 = 0; c0 + DEPTH < nchunks; c0 += DEPTH) {
+#pragma unroll
+      for (int j = 0; j < DEPTH; ++j) {
+        compute(j);
+        load_nb(j, c0 + DEPTH + j);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < DEPTH; ++j) compute(j);
+  } else {
+#pragma unroll
+    for (int j = 0; j < DEPTH; ++j)
+      if (j < nchunks) load(j, j);
+    if constexpr (NIN) part = ks_part_load(fz, M, wave, lane);  // reduced in the epilogue
+  }
+  for (int c0 = 0; c0 < (sl ? 0 : nchunks); c0 += DEPTH) {
 #pragma unroll
     for (int j = 0; j < DEPTH; ++j) {
       const int c = c0 + j;

@@ -13,6 +13,7 @@ struct KsFuse {
   int nbp;
   float eps;             // NIN: RMSNorm epsilon (the norm weight is folded into W by the caller)
   const float* wscale;   // F8 weights: per weight-row dequantisation scale (y[:, n] *= wscale[n])
+  int straight;          // 1: branch-free ring (ks_body): every slot refill issued unconditionally
 };
 
 }  // namespace dla
