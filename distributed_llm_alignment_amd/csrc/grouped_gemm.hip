@@ -84,6 +84,17 @@ __device__ __forceinline__ s16x4 gg_tr(const uint8_t* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
 }
 
+// The same read as inline asm: hipcc treats every ds_read_tr builtin as aliasing the LDS-DMA
+// writes in flight and waits vmcnt(0) before it, which would drain the counted pipeline of the
+// 4-phase schedule. Its results are waited for by hand (lgkmcnt(0) + sched_barrier before use).
+__device__ __forceinline__ s16x4 gg_tr_asm(const uint8_t* p) {
+  s16x4 r;
+  const uint32_t a = static_cast<uint32_t>(
+      reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) uint8_t*)(p)));
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a));
+  return r;
+}
+
 __device__ __forceinline__ float gg_sig(float x) { return 1.f / (1.f + __expf(-x)); }
 
 template <int I, int N, class Fn>
@@ -114,10 +125,17 @@ __device__ __forceinline__ void gg_barrier() {
 //      wave-group stagger of the cdna guide's 8-phase template). Next-tile DMA pieces go out
 //      in phases 1-2 (>= 2 barriers after the last read of that buffer: WAR-safe), each wave
 //      retires its own with vmcnt(0) in phase 3, one barrier before the tile's first read.
+//   4: (bf16, the default) counted 4-phase step: quarter tiles staged 2-6 phases ahead into
+//      whichever buffer slot is free, a counted vmcnt per phase, never vmcnt(0) in the loop
+//      (see the SCH == 4 loop). Mixtral expert block, same box: gate|up + SwiGLU forward 1205
+//      vs 1092 TF/s (schedule 0), down forward 1192 vs 1002, up dgrad 1110 vs 821 (schedule 3),
+//      down dgrad + SwiGLU backward 922 vs 768, weight gradients 813-936 vs 689-835.
 template <int MODE, bool BK, bool FP8, int EPI, bool OUTF32, int SCHED>
 __global__ __launch_bounds__(kGgThreads) void grouped_gemm_kernel(GGParams p) {
-  // the ping-pong schedule needs more registers than the fp8 fragments leave: fp8 uses 1
-  constexpr int SCH = (SCHED == 3 && FP8) ? 1 : SCHED;
+  // the ping-pong schedule needs more registers than the fp8 fragments leave: fp8 uses 1; the
+  // counted 4-phase schedule (4) is built for the bf16 k-contiguous forward only, others use 0
+  constexpr bool PH4 = SCHED == 4 && !FP8;
+  constexpr int SCH = PH4 ? 4 : SCHED == 4 ? 0 : (SCHED == 3 && FP8) ? 1 : SCHED;
   __shared__ __attribute__((aligned(16))) uint8_t smem[kGgSmem];
   constexpr int ESZ = FP8 ? 1 : 2;  // operand element size
   constexpr int KT = 128 / ESZ;     // reduction elements per K step
@@ -174,20 +192,33 @@ __global__ __launch_bounds__(kGgThreads) void grouped_gemm_kernel(GGParams p) {
   const uint8_t* srcA[4];
   const uint8_t* srcB[4];
   int cA[4], cB[4];  // K-contig: logical chunk; MN-contig: k-row within the tile
+  int pA[4], pB[4];  // 1-KiB piece (8 image rows) each source fills; wave-uniform
   const int64_t Kbytes = static_cast<int64_t>(p.K) * ESZ;
   const uint8_t* zp = g_gg_zero + lane * 16;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int piece = 4 * w + i;
+    pA[i] = pB[i] = piece;
+    if constexpr (SCH == 4) {
+      // quarter tiles (see the SCH == 4 loop), source i = 2h + j takes piece q = 2w + j of the
+      // 16 pieces of quarter h: k-contiguous A = rows of the waves' first / second 64-row
+      // halves, k-contiguous B = rows of their first / second 32-column halves, an
+      // mn-contiguous operand = k-rows [0, 32) / [32, 64) (16 KiB contiguous each)
+      const int h = i >> 1, q = 2 * w + (i & 1);
+      pA[i] = (MODE == kKVar) ? h * 16 + q : (q >> 3) * 16 + h * 8 + (q & 7);
+      pB[i] = !BK ? h * 16 + q : (EPI == kEpiSwigluFwd) ? h * 16 + q : (q >> 2) * 8 + h * 4 + (q & 3);
+    }
     if constexpr (MODE == kMVar) {
       // A: k-contiguous activation rows of the group (clamped: rows past the group end are
       // loaded from its last row and never stored)
-      const int r = piece * 8 + (lane >> 3);
+      const int r = pA[i] * 8 + (lane >> 3);
       const int c = (lane & 7) ^ gg_fsw(r);
       const int gr = min(row0 + r, row_end - 1);
       srcA[i] = p.A + static_cast<int64_t>(gr) * p.lda * ESZ;
       cA[i] = c;
       if constexpr (BK) {
+        const int r = pB[i] * 8 + (lane >> 3);
+        const int c = (lane & 7) ^ gg_fsw(r);
         int n;
         if constexpr (EPI == kEpiSwigluFwd) {
           const int f0 = nt * 128;
@@ -198,21 +229,20 @@ __global__ __launch_bounds__(kGgThreads) void grouped_gemm_kernel(GGParams p) {
         srcB[i] = p.B + (static_cast<int64_t>(g) * p.sBg + static_cast<int64_t>(n) * p.ldb) * ESZ;
         cB[i] = c;
       } else {
-        const int kr = piece * 2 + (lane >> 5);
+        const int kr = pB[i] * 2 + (lane >> 5);
         const int cc = (lane & 31) ^ gg_hsw(kr);
         const int ch = min(nt * 32 + cc, p.N / 8 - 1);
         srcB[i] = p.B + (static_cast<int64_t>(g) * p.sBg + static_cast<int64_t>(ch) * 8) * ESZ;
         cB[i] = kr;
       }
     } else {
-      const int kr = piece * 2 + (lane >> 5);
-      const int cc = (lane & 31) ^ gg_hsw(kr);
-      const int cha = min(mt * 32 + cc, p.M / 8 - 1);
-      const int chb = min(nt * 32 + cc, p.N / 8 - 1);
+      const int kra = pA[i] * 2 + (lane >> 5), krb = pB[i] * 2 + (lane >> 5);
+      const int cha = min(mt * 32 + ((lane & 31) ^ gg_hsw(kra)), p.M / 8 - 1);
+      const int chb = min(nt * 32 + ((lane & 31) ^ gg_hsw(krb)), p.N / 8 - 1);
       srcA[i] = p.A + (static_cast<int64_t>(row0) * p.lda + static_cast<int64_t>(cha) * 8) * ESZ;
       srcB[i] = p.B + (static_cast<int64_t>(row0) * p.ldb + static_cast<int64_t>(chb) * 8) * ESZ;
-      cA[i] = kr;
-      cB[i] = kr;
+      cA[i] = kra;
+      cB[i] = krb;
     }
   }
 
@@ -256,6 +286,14 @@ __global__ __launch_bounds__(kGgThreads) void grouped_gemm_kernel(GGParams p) {
     const int k1 = kk * 32 + 8 * fg + q;
     const s16x4 x = gg_tr(img + gg_moff(k1, ch) + sub);
     const s16x4 y = gg_tr(img + gg_moff(k1 + 4, ch) + sub);
+    return s16x8{x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
+  };
+  auto mfrag_asm = [&](const uint8_t* img, int c0, int kk) -> s16x8 {
+    const int q = fr >> 2, pp = fr & 3;
+    const int ch = (c0 >> 3) + (pp >> 1), sub = (pp & 1) * 8;
+    const int k1 = kk * 32 + 8 * fg + q;
+    const s16x4 x = gg_tr_asm(img + gg_moff(k1, ch) + sub);
+    const s16x4 y = gg_tr_asm(img + gg_moff(k1 + 4, ch) + sub);
     return s16x8{x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
   };
   // fp8 fragment (32 k per lane) of 16 rows from a k-contiguous image
@@ -355,7 +393,155 @@ __global__ __launch_bounds__(kGgThreads) void grouped_gemm_kernel(GGParams p) {
 
   // ---------------------------------------------------------------- main loop
   const int nk = (Kg + KT - 1) / KT;
-  if constexpr (SCH == 3) {
+  if constexpr (SCH == 4) {
+    // Counted 4-phase K step (cdna guide §5 "256² 8-phase template", T3+T4): each phase runs
+    // 16 MFMAs of the wave between two raw barriers, the second wave group (wm = 1) one barrier
+    // behind the first. A K tile is staged as 4 quarter tiles QA0 / QA1 / QB0 / QB1 (pieces:
+    // see pA / pB), each restaged as soon as its slot is 2 phases past its last read (the WAR
+    // distance the staggered groups need), so a quarter is in flight for 2-6 phases; each wave
+    // waits a counted vmcnt (never 0 in the loop) before the first barrier of a phase, which
+    // retires what the next phase reads (cdna guide: a staged buffer is read one phase after
+    // the wait that retires it). Zero page past the last tile. Layouts:
+    //   F (forward, both k-contiguous): phases = quadrants (mh, nh) (0,0) (0,1) (1,1) (1,0);
+    //     reads QA0+QB0 / QB1 / QA1 / - (QB0 held to phase 3); stages QB1, QA1 of tile t+1,
+    //     QA0, QB0 of tile t+2; vmcnt(8).
+    //   D (input gradient, B mn-contiguous): phases (kk, mh) (0,0) (0,1) (1,0) (1,1); reads
+    //     QA0+QB0 / QA1 / QA0+QB1 / QA1; stages QB1, QA0, QA1 of t+1, QB0 of t+2; vmcnt(4).
+    //   W (weight gradient, both mn-contiguous): phases (kk, mh); reads QA0+QB0 / QA0 / QA1+QB1
+    //     / QA1; stages QB1, QA1 of t+1, QB0, QA0 of t+2; vmcnt(8).
+    if (nk > 0) {
+      constexpr int LAY = (MODE == kKVar) ? 2 : BK ? 0 : 1;
+      constexpr bool KQA = MODE == kKVar, KQB = !BK;
+      const int Klim = (MODE == kMVar) ? p.K : Kg;
+      // quarter qi: 0 = QA0, 1 = QB0, 2 = QB1, 3 = QA1
+      auto stage_q = [&](int t, int buf, auto QI) {
+        constexpr int qi = decltype(QI)::value;
+        constexpr bool isA = qi == 0 || qi == 3;
+        constexpr int h = (qi == 0 || qi == 1) ? 0 : 1;
+        constexpr bool kq = isA ? KQA : KQB;
+        uint8_t* base = smem + buf * kGgBufBytes + (isA ? 0 : kGgTileBytes);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int i = h * 2 + j;
+          uint8_t* dst = base + (isA ? pA[i] : pB[i]) * 1024;
+          const uint8_t* src = isA ? srcA[i] : srcB[i];
+          if constexpr (!kq) {
+            const int64_t kb = static_cast<int64_t>(t) * 128 + (isA ? cA[i] : cB[i]) * 16;
+            glds16(kb < Kbytes ? src + kb : zp, dst);
+          } else {
+            const int k = t * KT + (isA ? cA[i] : cB[i]);
+            glds16(k < Klim ? src + static_cast<int64_t>(k) * (isA ? p.lda : p.ldb) * ESZ : zp, dst);
+          }
+        }
+      };
+      using Q0 = std::integral_constant<int, 0>;
+      using Q1 = std::integral_constant<int, 1>;
+      using Q2 = std::integral_constant<int, 2>;
+      using Q3 = std::integral_constant<int, 3>;
+      auto vwait = [&]() {
+        if constexpr (LAY == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      };
+      s16x8 af[2][4], blo[2][2], bhi[2][2], bq[4];
+      if constexpr (LAY == 0) {
+        stage_q(0, 0, Q0{}); stage_q(0, 0, Q1{}); stage_q(0, 0, Q2{}); stage_q(0, 0, Q3{});
+        stage_q(1, 1, Q0{}); stage_q(1, 1, Q1{});
+      } else if constexpr (LAY == 1) {
+        stage_q(0, 0, Q1{}); stage_q(0, 0, Q2{}); stage_q(0, 0, Q0{}); stage_q(0, 0, Q3{});
+        stage_q(1, 1, Q1{});
+      } else {
+        stage_q(0, 0, Q1{}); stage_q(0, 0, Q0{}); stage_q(0, 0, Q2{}); stage_q(0, 0, Q3{});
+        stage_q(1, 1, Q1{}); stage_q(1, 1, Q0{});
+      }
+      vwait();
+      gg_barrier();
+      if (wm == 1) gg_barrier();  // second wave group runs one barrier behind
+      for (int t = 0; t < nk; ++t) {
+        const uint8_t* imA = smem + (t & 1) * kGgBufBytes;
+        const uint8_t* imB = imA + kGgTileBytes;
+        gg_static_for<0, 4>([&](auto PH) {
+          constexpr int ph = decltype(PH)::value;
+          if constexpr (LAY == 0) {
+            constexpr int mh = ph >> 1;
+            if constexpr (ph == 0 || ph == 2) {
+#pragma unroll
+              for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) af[kk][i] = kfrag(imA, wm * 128 + (mh * 4 + i) * 16, kk);
+            }
+            if constexpr (ph == 0) {
+#pragma unroll
+              for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) blo[kk][j] = kfrag(imB, brow(j), kk);
+            }
+            if constexpr (ph == 1) {
+#pragma unroll
+              for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) bhi[kk][j] = kfrag(imB, brow(2 + j), kk);
+            }
+            if constexpr (ph == 0) stage_q(t + 1, (t + 1) & 1, Q2{});
+            if constexpr (ph == 1) stage_q(t + 1, (t + 1) & 1, Q3{});
+            if constexpr (ph == 2) stage_q(t + 2, t & 1, Q0{});
+            if constexpr (ph == 3) stage_q(t + 2, t & 1, Q1{});
+          } else {
+            constexpr int kk = ph >> 1, mh = ph & 1;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              if constexpr (KQA) af[0][i] = mfrag_asm(imA, wm * 128 + (mh * 4 + i) * 16, kk);
+              else af[0][i] = kfrag(imA, wm * 128 + (mh * 4 + i) * 16, kk);
+            }
+            if constexpr (mh == 0) {
+#pragma unroll
+              for (int ni = 0; ni < 4; ++ni) bq[ni] = mfrag_asm(imB, brow(ni), kk);
+            }
+            if constexpr (LAY == 1) {
+              if constexpr (ph == 0) stage_q(t + 1, (t + 1) & 1, Q2{});
+              if constexpr (ph == 1) stage_q(t + 1, (t + 1) & 1, Q0{});
+              if constexpr (ph == 2) stage_q(t + 1, (t + 1) & 1, Q3{});
+              if constexpr (ph == 3) stage_q(t + 2, t & 1, Q1{});
+            } else {
+              if constexpr (ph == 0) stage_q(t + 1, (t + 1) & 1, Q2{});
+              if constexpr (ph == 1) stage_q(t + 1, (t + 1) & 1, Q3{});
+              if constexpr (ph == 2) stage_q(t + 2, t & 1, Q1{});
+              if constexpr (ph == 3) stage_q(t + 2, t & 1, Q0{});
+            }
+          }
+          vwait();
+          gg_barrier();
+          if constexpr (LAY != 0) {  // the inline-asm transposed reads of this phase
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          __builtin_amdgcn_s_setprio(1);
+          if constexpr (LAY == 0) {
+            constexpr int mh = ph >> 1, nh = (ph == 1 || ph == 2) ? 1 : 0;
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+              for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                  acc[mh * 4 + i][nh * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                      af[kk][i], nh ? bhi[kk][j] : blo[kk][j], acc[mh * 4 + i][nh * 2 + j], 0, 0, 0);
+          } else {
+            constexpr int mh = ph & 1;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+              for (int ni = 0; ni < 4; ++ni)
+                acc[mh * 4 + i][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0][i], bq[ni], acc[mh * 4 + i][ni], 0, 0, 0);
+          }
+          __builtin_amdgcn_s_setprio(0);
+          gg_barrier();
+        });
+      }
+      if (wm == 0) gg_barrier();  // balance the barrier count of the two groups
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  } else if constexpr (SCH == 3) {
     if (nk > 0) {
       s16x8 af[4], bfv[4];
       i32x8 af8[2], bf8[4];
@@ -578,17 +764,18 @@ __global__ __launch_bounds__(kGgThreads) void grouped_gemm_kernel(GGParams p) {
 }
 
 // ---------------------------------------------------------------------------------------- host
-// Default schedule per operand layout (measured, tools/grouped_gemm_bench.py): the plain 2-phase
-// step for k-contiguous weights, the ping-pong phases when an operand takes transposed reads.
+// Default schedule (measured, tools/grouped_gemm_bench.py, profiles/r5_grouped_gemm.md): the
+// counted 4-phase step for every bf16 layout (fp8 keeps the plain 2-phase step). 0-3 stay
+// selectable for A/B.
 // DLA_GG_SCHED overrides (read per launch so a benchmark can A/B schedules in one process).
-static int gg_sched(bool transposed_operand) {
+static int gg_sched() {
   const char* e = std::getenv("DLA_GG_SCHED");
-  return e ? std::atoi(e) : (transposed_operand ? 3 : 0);
+  return e ? std::atoi(e) : 4;
 }
 
 template <int MODE, bool BK, bool FP8, int EPI, bool OUTF32>
 static void gg_launch(const GGParams& p, int nblk, hipStream_t st) {
-  switch (gg_sched(MODE == kKVar || !BK)) {
+  switch (gg_sched()) {
     case 1:
       hipLaunchKernelGGL((grouped_gemm_kernel<MODE, BK, FP8, EPI, OUTF32, 1>), dim3(nblk), dim3(kGgThreads),
                          0, st, p);
@@ -599,6 +786,10 @@ static void gg_launch(const GGParams& p, int nblk, hipStream_t st) {
       break;
     case 3:
       hipLaunchKernelGGL((grouped_gemm_kernel<MODE, BK, FP8, EPI, OUTF32, 3>), dim3(nblk), dim3(kGgThreads),
+                         0, st, p);
+      break;
+    case 4:
+      hipLaunchKernelGGL((grouped_gemm_kernel<MODE, BK, FP8, EPI, OUTF32, 4>), dim3(nblk), dim3(kGgThreads),
                          0, st, p);
       break;
     default:

@@ -13,11 +13,12 @@ with boolean masks, `index_add_` and a fresh weight-gradient tensor per expert. 
     epilogue and the SwiGLU backward into the down projection's input-gradient epilogue, and
     weight gradients accumulate straight into the engine's grad buffer (`main_grad`, bf16 or
     fp32). `DLA_MOE_GEMM=loop|grouped` forces the per-expert hipBLASLt loop (host counts) or the
-    grouped GEMM; the default `auto` takes the loop for bf16 experts outside a hipGraph capture
-    when autograd records or the call has >= 1024 rows (training fwd+bwd, the frozen reference
-    forward, prefill: the loop's hipBLASLt tiles are faster there, 59.5 vs 55.4 pairs/s on the
-    Mixtral 2-layer DPO bench, same box), and the grouped GEMM for decode-sized calls, captures and
-    the fp8 forward, whose backward then runs on the per-expert loop (67.4-67.7 vs 64.1-64.5);
+    grouped GEMM; the default `auto` takes the grouped GEMM everywhere since its counted 4-phase
+    K step (round 5): Mixtral expert block fwd+bwd 18.6 vs 20.5 ms on the loop; Mixtral 2-layer
+    DPO 60.8-60.9 vs 60.4-60.5 pairs/s (4 x 4 pairs), 67.8 vs 66.4 (16 pairs per micro-batch), fp8
+    expert forward with the grouped backward 69.3 vs 67.6-68.0 with the loop backward (same box;
+    `profiles/r5_grouped_gemm.md`). `DLA_MOE_GEMM=auto` + `DLA_MOE_BWD=loop` keeps the old fp8
+    hybrid (grouped fp8 forward, per-expert loop backward);
   * optional fp8 (e4m3, row-wise scales) forward GEMMs (`fp8=True`) on the block-scaled
     16x16x128 MFMA, bf16 backward.
 CPU (and non-bf16) inputs use the PyTorch reference path with identical semantics.
@@ -502,25 +503,16 @@ def grouped_gemm_enabled() -> bool:
 
 
 def _loop_backward_ok() -> bool:
-    """auto: the grouped node's backward (fp8-forward experts under autograd) runs the per-expert
-    loop (DLA_MOE_BWD=grouped keeps the grouped dgrad / wgrad kernels)."""
-    return (os.environ.get("DLA_MOE_GEMM", "auto") == "auto" and os.environ.get("DLA_MOE_BWD", "auto") != "grouped"
+    """DLA_MOE_BWD=loop (with DLA_MOE_GEMM=auto): the grouped node's backward runs the
+    per-expert hipBLASLt loop instead of the grouped dgrad / wgrad kernels (the default)."""
+    return (os.environ.get("DLA_MOE_GEMM", "auto") == "auto" and os.environ.get("DLA_MOE_BWD", "auto") == "loop"
             and not torch.cuda.is_current_stream_capturing())
 
 
-# auto: below this many expert rows a no-grad call (decode steps, eager or captured) stays on the
-# grouped GEMM, so eager and hipGraph decoding run the same kernels; larger no-grad calls (the
-# frozen reference forward, prefill) take the loop like training
-MOE_LOOP_MIN_ROWS = int(os.environ.get("DLA_MOE_LOOP_MIN_ROWS", "1024"))
-
-
 def _use_grouped(fp8: bool, rows: int = 0) -> bool:
-    mode = os.environ.get("DLA_MOE_GEMM", "auto")
-    if mode != "auto":
-        return mode != "loop"
-    if fp8 or torch.cuda.is_current_stream_capturing():
-        return True
-    return not torch.is_grad_enabled() and rows < MOE_LOOP_MIN_ROWS
+    """auto and grouped: the grouped GEMM (faster than the per-expert loop at every measured
+    size since the counted 4-phase schedule, and host-sync free); loop: the per-expert loop."""
+    return os.environ.get("DLA_MOE_GEMM", "auto") != "loop"
 
 
 def _grouped_ok(xs, w_up, w_down) -> bool:

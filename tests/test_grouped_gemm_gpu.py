@@ -42,8 +42,17 @@ def _rand(*shape, g, scale=1.0):
     return (torch.randn(*shape, device=DEV, generator=g) * scale).to(torch.bfloat16)
 
 
+@pytest.fixture(params=["default", "0", "3", "4"])
+def gg_sched(request, monkeypatch):
+    """every K-step schedule: the per-layout default, the plain 2-phase step (0), the ping-pong
+    phases (3) and the counted 4-phase step (4)"""
+    if request.param != "default":
+        monkeypatch.setenv("DLA_GG_SCHED", request.param)
+    return request.param
+
+
 @pytest.mark.parametrize("N,K", [(384, 256), (264, 136)])
-def test_grouped_fwd_vs_fp32(N, K):
+def test_grouped_fwd_vs_fp32(N, K, gg_sched):
     g = torch.Generator(device=DEV).manual_seed(0)
     M, G = sum(COUNTS), len(COUNTS)
     x = _rand(M, K, g=g)
@@ -66,7 +75,7 @@ def test_grouped_fwd_vs_fp32(N, K):
         s += c
 
 
-def test_grouped_fwd_swiglu_epilogue():
+def test_grouped_fwd_swiglu_epilogue(gg_sched):
     g = torch.Generator(device=DEV).manual_seed(1)
     M, G, K, Fd = sum(COUNTS), len(COUNTS), 192, 256
     x = _rand(M, K, g=g)
@@ -83,7 +92,46 @@ def test_grouped_fwd_swiglu_epilogue():
         s += c
 
 
-def test_grouped_dgrad_and_swiglu_bwd_epilogue():
+@pytest.mark.parametrize("kind", ["fwd", "fwd_swiglu", "dgrad", "dgrad_swiglu", "wgrad"])
+def test_grouped_counted_schedule_bitwise(monkeypatch, kind):
+    """DLA_GG_SCHED=4 (4 phases per K step, quarter tiles staged 2-6 phases ahead, counted
+    vmcnt) sums every output in the same k order as the 2-phase step (0): bitwise equal outputs
+    over ragged and empty groups, K tails and >= 16 K steps, for every operand layout."""
+    g = torch.Generator(device=DEV).manual_seed(5)
+    counts = [700, 0, 1, 256, 333, 1024, 90]
+    M, G, K, N = sum(counts), len(counts), 1000, 768
+    offs = _offs(counts)
+    if kind.startswith("fwd"):
+        x = _rand(M, K, g=g)
+        w = _rand(G, N, K, g=g, scale=0.05)
+        run = (lambda: _C().gg_fwd_swiglu(x, w, offs, None, None)) if kind == "fwd_swiglu" else \
+              (lambda: (_C().gg_fwd(x, w, offs, None, None),))
+    elif kind == "dgrad":
+        dy = _rand(M, N, g=g)
+        w = _rand(G, N, K, g=g, scale=0.05)
+        run = lambda: (_C().gg_dgrad(dy, w, offs),)
+    elif kind == "dgrad_swiglu":
+        dy = _rand(M, K, g=g)
+        w_down = _rand(G, K, N // 2, g=g, scale=0.05)
+        gu = _rand(M, N, g=g)
+        run = lambda: _C().gg_dgrad_swiglu(dy, w_down, offs, gu)
+    else:
+        dy = _rand(M, 264, g=g)
+        x = _rand(M, 520, g=g)
+
+        def run():
+            out = torch.zeros(G, 264, 520, device=DEV)
+            _C().gg_wgrad(dy, x, offs, out, True)
+            return (out,)
+    outs = []
+    for sc in ("0", "4"):
+        monkeypatch.setenv("DLA_GG_SCHED", sc)
+        outs.append(run())
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
+def test_grouped_dgrad_and_swiglu_bwd_epilogue(gg_sched):
     g = torch.Generator(device=DEV).manual_seed(2)
     M, G, H, Fd = sum(COUNTS), len(COUNTS), 256, 384
     dy = _rand(M, 2 * Fd, g=g)
@@ -113,7 +161,7 @@ def test_grouped_dgrad_and_swiglu_bwd_epilogue():
 
 
 @pytest.mark.parametrize("out_dtype", [torch.bfloat16, torch.float32])
-def test_grouped_wgrad_accumulate(out_dtype):
+def test_grouped_wgrad_accumulate(out_dtype, gg_sched):
     g = torch.Generator(device=DEV).manual_seed(3)
     M, G, N1, N2 = sum(COUNTS), len(COUNTS), 264, 512
     dy = _rand(M, N1, g=g)
@@ -174,7 +222,7 @@ def test_moe_layer_grouped_matches_loop_and_captures():
     moe = m.layers[0].mlp
     g = torch.Generator(device=DEV).manual_seed(5)
     h = _rand(4, 200, cfg.hidden_size, g=g).requires_grad_(True)
-    os.environ["DLA_MOE_GEMM"] = "grouped"  # auto would take the loop for bf16 training
+    os.environ["DLA_MOE_GEMM"] = "grouped"
     try:
         out = moe(h)
         go = _rand(*out.shape, g=g)

@@ -207,8 +207,9 @@ def test_moe_recompute_keeps_expert_grads(policy, gemm, monkeypatch):
 
 
 def test_moe_fp8_hybrid_backward_matches_grouped(monkeypatch):
-    """fp8 experts: `auto` runs the forward on the grouped fp8 kernel and the backward on the
-    per-expert hipBLASLt loop; its input / weight gradients match the all-grouped backward."""
+    """fp8 experts: `auto` with DLA_MOE_BWD=loop runs the forward on the grouped fp8 kernel and
+    the backward on the per-expert hipBLASLt loop; its input / weight gradients match the
+    all-grouped backward (the default)."""
     from distributed_llm_alignment_amd.models import build_model, get_config
 
     cfg = get_config("tiny-mixtral", hidden_size=256, intermediate_size=512, num_experts=8)
@@ -219,6 +220,7 @@ def test_moe_fp8_hybrid_backward_matches_grouped(monkeypatch):
     h = torch.randn(2, 160, cfg.hidden_size, device=DEV, generator=g).to(torch.bfloat16).requires_grad_(True)
     go = torch.randn(2, 160, cfg.hidden_size, device=DEV, generator=g).to(torch.bfloat16)
     res = {}
+    monkeypatch.setenv("DLA_MOE_BWD", "loop")
     for mode in ("auto", "grouped"):
         monkeypatch.setenv("DLA_MOE_GEMM", mode)
         out = moe(h)
