@@ -80,6 +80,10 @@ def parse(argv=None):
                     help="debug: time ONE expert-parallel rank of an N-GPU MoE job at world 1: E/N "
                          "local experts per layer, the capacity-padded sync-free dispatch with the "
                          "all-to-alls as local copies, ZeRO-1 optimizer state of one of N ranks")
+    ap.add_argument("--ep-hot", action="store_true",
+                    help="debug (with --ep-shape = num_experts): the timed rank hosts a HOT expert, "
+                         "every source sending its full capacity (ep-capacity x the balanced rows; "
+                         "the rows past the expected ones run on the overflow grouped kernels)")
     ap.add_argument("--edp-shape", type=int, default=1,
                     help="debug (with --ep-shape N): the job has M expert-data-parallel replicas of "
                          "each EP group (N x M GPUs): dense ZeRO-1 state over N*M ranks, expert "
@@ -99,6 +103,8 @@ def parse(argv=None):
     a = ap.parse_args(argv)
     if a.edp_shape > 1 and a.ep_shape <= 1:
         ap.error("--edp-shape needs --ep-shape")
+    if a.ep_hot and a.ep_shape <= 1:
+        ap.error("--ep-hot needs --ep-shape")
     if a.fsdp_shape > 1 and a.zero != 3:
         ap.error("--fsdp-shape needs --zero 3")
     shape = a.ep_shape > 1
@@ -355,7 +361,8 @@ def main(argv=None) -> int:
         from distributed_llm_alignment_amd.parallel.expert import apply_expert_parallel
 
         for m in (policy, ref):
-            apply_expert_parallel(m, None, capacity_factor=args.ep_capacity or 2.0, shape_ep=args.ep_shape)
+            apply_expert_parallel(m, None, capacity_factor=args.ep_capacity or 2.0, shape_ep=args.ep_shape,
+                                  shape_hot=args.ep_hot)
     if cfg.is_moe and args.fp8:
         for m in (policy, ref):
             for layer in m.layers:
@@ -509,7 +516,8 @@ def main(argv=None) -> int:
                          + (f"(one rank of a {shape_info['mesh']} mesh, local stand-in collectives, debug)"
                             if shape_mode and args.ep_shape <= 1 else "")
                          + (f"(one EP rank of ep{args.ep_shape}: {cfg.num_experts // args.ep_shape} "
-                            "local experts/layer, a2a as local copies, debug)" if args.ep_shape > 1 else ""),
+                            "local experts/layer, a2a as local copies, debug)" if args.ep_shape > 1 else "")
+                         + (f"(hot expert: every source at capacity {args.ep_capacity})" if args.ep_hot else ""),
                 "global_batch": pairs_per_step,
                 "seq_len": args.seq_len,
                 "parallelism": f"dp{mesh.dp}" + (f"-tp{mesh.tp}" if mesh.tp > 1 else "")

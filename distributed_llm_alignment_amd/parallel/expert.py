@@ -169,14 +169,17 @@ def _gather_rows(x: torch.Tensor, idx: torch.Tensor, injective: bool = True,
 
 class ExpertParallel:
     def __init__(self, group, num_experts: int, capacity_factor: float = 2.0, chunks: int = 2,
-                 shape_ep: int = 1):
+                 shape_ep: int = 1, shape_hot: bool = False):
         """`shape_ep` > 1 (one process, no group; bench.py --ep-shape): rank 0 of an EP group of
         that size. It keeps E/shape_ep experts and runs the capacity-padded, sync-free dispatch with
         every all-to-all replaced by the identity: the rows this rank would send to destination r
         stand in for the rows it would receive from source r. Under balanced routing that is the
         per-rank expert load of the real job (k x N slots into E/ep experts), so the timing is one
         EP rank's compute; the numerics are not the full model's (every slot meets the local
-        experts)."""
+        experts). `shape_hot` (bench.py --ep-hot, one local expert): the rank of a HOT expert under
+        imbalanced routing -- every source sends its full capacity C (the padding rows of each
+        source block are zero rows that no slot reads back), so the expert runs capacity_factor x
+        the balanced rows and everything past the expected n * k runs on the overflow path."""
         self.shape = int(shape_ep) > 1
         self.group = None if self.shape else group
         self.ep = int(shape_ep) if self.shape else dist.get_world_size(group)
@@ -187,6 +190,9 @@ class ExpertParallel:
         self.El = num_experts // self.ep
         self.capacity_factor = float(capacity_factor)
         self.chunks = max(1, int(chunks))
+        self.shape_hot = bool(shape_hot) and self.shape
+        if self.shape_hot and self.El != 1:
+            raise ValueError("shape_hot needs one local expert per rank (--ep-shape = num_experts)")
         self._dropped = None  # device int64 counter of dropped token slots (capacity mode)
 
     def dropped_slots(self, reset: bool = True) -> int:
@@ -288,7 +294,7 @@ class ExpertParallel:
                     self._dropped = torch.zeros((), dtype=torch.long, device=h2.device)
                 self._dropped += ndrop
             if self.shape:
-                rc, w = sent, None
+                rc, w = (torch.full_like(sent, C) if self.shape_hot else sent), None
             else:
                 rc = torch.empty_like(sent)
                 w = dist.all_to_all_single(rc, sent.contiguous(), group=self.group, async_op=True)
@@ -353,7 +359,7 @@ class ExpertParallel:
 
 @torch.no_grad()
 def apply_expert_parallel(model, mesh, capacity_factor: float = 2.0, chunks: int = 2,
-                          shape_ep: int = 1, force: bool = False):
+                          shape_ep: int = 1, force: bool = False, shape_hot: bool = False):
     """Keep this rank's E/ep experts of every MoE layer and attach the all-to-all router
     (`capacity_factor` 0: exact dropless dispatch with one host read per layer). `shape_ep` > 1
     with `mesh=None`: the one-process shape mode of ExpertParallel (bench.py --ep-shape).
@@ -367,7 +373,7 @@ def apply_expert_parallel(model, mesh, capacity_factor: float = 2.0, chunks: int
         if not cfg.is_moe:
             return model
         ep = ExpertParallel(None, cfg.num_experts, capacity_factor=capacity_factor, chunks=chunks,
-                            shape_ep=shape_ep)
+                            shape_ep=shape_ep, shape_hot=shape_hot)
         for layer in base.layers:
             m = layer.mlp
             for nm in ("expert_up", "expert_down"):

@@ -96,3 +96,39 @@ def test_expert_parallel_shape_mode_one_rank():
     loss.backward()
     assert torch.isfinite(loss) and float(eng.step()) > 0
     assert not torch.equal(w0, mlp.expert_up.detach())
+
+
+def test_expert_parallel_shape_hot_expert(monkeypatch):
+    """bench.py --ep-hot: in the EP shape mode with one local expert, every source sends its full
+    capacity, so the expert GEMM runs capacity x the balanced rows (the overflow path past the
+    expected n * k); the padding rows are zeros no slot reads back, so the layer output equals
+    the balanced shape mode's."""
+    from distributed_llm_alignment_amd import ops
+    from distributed_llm_alignment_amd.parallel.expert import apply_expert_parallel
+
+    cfg = get_config("tiny-mixtral")
+    E = cfg.num_experts
+    seen = []
+    real = ops.moe.experts_swiglu_offsets
+
+    def spy(xe, w_up, w_down, offs, **kw):
+        seen.append((xe.shape[0], int(offs[-1]), kw.get("main_rows", 0)))
+        return real(xe, w_up, w_down, offs, **kw)
+
+    monkeypatch.setattr(ops.moe, "experts_swiglu_offsets", spy)
+    outs = []
+    h = torch.randn(2, 512, cfg.hidden_size, generator=torch.Generator().manual_seed(1))
+    for hot in (False, True):
+        m = build_model(cfg, device="cpu", seed=0)
+        apply_expert_parallel(m, None, capacity_factor=1.5, shape_ep=E, shape_hot=hot)
+        seen.clear()
+        with torch.no_grad():
+            outs.append(m.layers[0].mlp(h))
+        rows, used, main = seen[0]
+        if hot:
+            assert used == rows > main  # every capacity row computed, past the expected rows
+        else:
+            assert used <= main
+    torch.testing.assert_close(outs[1], outs[0], rtol=1e-5, atol=1e-6)
+    with pytest.raises(ValueError):
+        apply_expert_parallel(build_model(cfg, device="cpu", seed=0), None, shape_ep=E // 2, shape_hot=True)
