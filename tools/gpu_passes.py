@@ -84,6 +84,7 @@ PASSES = {
         run("ppo_zero8", "python -u tools/bench_rlhf.py --algorithm ppo --zero-shape 8 --batch 8"),
         run("mixtral_ep8", MIX_EP8 + " --steps 3 --warmup 2"),
         run("mixtral_ep8_fp8", MIX_EP8 + " --fp8 --steps 3 --warmup 2"),
+        run("mixtral_ep8_hot", MIX_EP8 + " --ep-hot --steps 3 --warmup 2"),
         run("gen8_fp8", GEN8 + " --weight-dtype fp8", 300), run("gen64_fp8", GEN64 + " --weight-dtype fp8", 300),
         run("rlhf8_fp8", "python -u tools/bench_rlhf.py --batch 8 --rollout-dtype fp8", 400),
         run("ppo_zero8_fp8", "python -u tools/bench_rlhf.py --algorithm ppo --zero-shape 8 --batch 8 --rollout-dtype fp8"),
