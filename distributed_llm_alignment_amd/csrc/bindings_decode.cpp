@@ -73,11 +73,24 @@ void launch_skinny_glu_il_f8(const bf16_t*, int64_t, const uint8_t*, bf16_t*, in
                              const KsFuse&, hipStream_t);
 bool m64_shape_ok(int N, int K, bool glu);
 void launch_m64_gemm(const bf16_t*, int64_t, const bf16_t*, int64_t, bf16_t*, int64_t, float*, int,
-                     int, int, int, bool, const float*, int, float, bool, hipStream_t);
+                     int, int, int, bool, const float*, int, float, bool, hipStream_t, unsigned* = nullptr,
+                     const bf16_t* = nullptr, int64_t = 0, float* = nullptr);
 void launch_m64_reduce(const float*, int, int, int, bf16_t*, int64_t, const bf16_t*, int64_t,
                        const float*, int, int, float, float*, hipStream_t);
 void launch_m64_gemm_f8(const bf16_t*, int64_t, const uint8_t*, bf16_t*, int64_t, float*, int, int, int, int,
-                        bool, const float*, int, float, const float*, hipStream_t);
+                        bool, const float*, int, float, const float*, hipStream_t, unsigned* = nullptr,
+                        const bf16_t* = nullptr, int64_t = 0, float* = nullptr);
+
+// split-K arrival counters for the in-kernel combine (csrc/skinny64.hip M64Cmb): int32, zero,
+// at least one per 128-column block; the kernel re-arms them
+static unsigned* m64_counters(const c10::optional<at::Tensor>& cnt, const at::Tensor& x, int64_t N) {
+  if (!cnt.has_value()) return nullptr;
+  const at::Tensor& c = *cnt;
+  TORCH_CHECK(c.is_cuda() && c.scalar_type() == at::kInt && c.is_contiguous() && c.numel() >= N / 128,
+              "cnt: contiguous int32 counters, one per 128 output columns");
+  TORCH_CHECK(c.device() == x.device(), "cnt: same device as x");
+  return reinterpret_cast<unsigned*>(c.data_ptr<int>());
+}
 
 // Decode projection at 17..64 rows (skinny64.hip), the same fused-layer contract as
 // skinny_fused below with row-norm partials per (row, 1024 columns):
@@ -88,7 +101,7 @@ void launch_m64_gemm_f8(const bf16_t*, int64_t, const uint8_t*, bf16_t*, int64_t
 std::tuple<at::Tensor, at::Tensor> skinny64(const at::Tensor& x, const at::Tensor& w,
                                             const c10::optional<at::Tensor>& res,
                                             const c10::optional<at::Tensor>& ssq_in, double eps,
-                                            bool glu) {
+                                            bool glu, const c10::optional<at::Tensor>& cnt) {
   check_bf16(x, "x");
   check_bf16(w, "w");
   // w: [N, K] row-major, or the tiled layout [N / 16, K / 32, 4, 16, 8] (skinny64.hip TW)
@@ -111,8 +124,8 @@ std::tuple<at::Tensor, at::Tensor> skinny64(const at::Tensor& x, const at::Tenso
     const at::Tensor& t = *ssq_in;
     check_cuda(t, "ssq_in");
     TORCH_CHECK(t.scalar_type() == at::kFloat && t.dim() == 2 && t.size(0) == M && t.is_contiguous() &&
-                    t.size(1) >= 1 && t.size(1) <= 8,
-                "ssq_in fp32 [M, nbp <= 8] contiguous");
+                    t.size(1) >= 1 && t.size(1) <= 64,
+                "ssq_in fp32 [M, nbp <= 64] contiguous");
     same_device(x, t);
     sq = t.data_ptr<float>();
     nbp = static_cast<int>(t.size(1));
@@ -132,9 +145,7 @@ std::tuple<at::Tensor, at::Tensor> skinny64(const at::Tensor& x, const at::Tenso
   auto y = at::empty({M, N}, x.options());
   at::Tensor ws;
   if (S > 1) ws = at::empty({S, M, N}, x.options().dtype(at::kFloat));
-  launch_m64_gemm(cbp(x), x.stride(0), cbp(w), tiled ? K : w.stride(0), bp(y), y.stride(0),
-                  S > 1 ? ws.data_ptr<float>() : nullptr, (int)M, (int)N, (int)K, S, false, nullptr, 0,
-                  0.f, tiled, st);
+  unsigned* cp = S > 1 ? m64_counters(cnt, x, N) : nullptr;
   const bf16_t* rp = nullptr;
   int64_t ldr = 0;
   at::Tensor ssq;
@@ -145,11 +156,16 @@ std::tuple<at::Tensor, at::Tensor> skinny64(const at::Tensor& x, const at::Tenso
     same_device(x, r);
     rp = cbp(r);
     ldr = r.stride(0);
-    ssq = at::empty({M, (N + 1023) / 1024}, x.options().dtype(at::kFloat));
+    // row partials per 1024 columns (reduce launch) or per 128-column block (in-kernel combine)
+    ssq = at::empty({M, cp ? N / 128 : (N + 1023) / 1024}, x.options().dtype(at::kFloat));
   }
-  if (S > 1)
+  float* sqo = ssq.defined() ? ssq.data_ptr<float>() : nullptr;
+  launch_m64_gemm(cbp(x), x.stride(0), cbp(w), tiled ? K : w.stride(0), bp(y), y.stride(0),
+                  S > 1 ? ws.data_ptr<float>() : nullptr, (int)M, (int)N, (int)K, S, false, sq, nbp,
+                  static_cast<float>(eps), tiled, st, cp, rp, ldr, sqo);
+  if (S > 1 && !cp)
     launch_m64_reduce(ws.data_ptr<float>(), S, (int)M, (int)N, bp(y), y.stride(0), rp, ldr, sq, nbp,
-                      (int)K, static_cast<float>(eps), ssq.defined() ? ssq.data_ptr<float>() : nullptr, st);
+                      (int)K, static_cast<float>(eps), sqo, st);
   return {y, ssq};
 }
 
@@ -314,7 +330,8 @@ std::tuple<at::Tensor, at::Tensor> skinny_fused_f8(const at::Tensor& x, const at
 // plain [gate; up] row order, norm weight folded in). Same epilogue contract as skinny64.
 std::tuple<at::Tensor, at::Tensor> skinny64_f8(const at::Tensor& x, const at::Tensor& w8, const at::Tensor& wscale,
                                                const c10::optional<at::Tensor>& res,
-                                               const c10::optional<at::Tensor>& ssq_in, double eps, bool glu) {
+                                               const c10::optional<at::Tensor>& ssq_in, double eps, bool glu,
+                                               const c10::optional<at::Tensor>& cnt) {
   check_bf16(x, "x");
   int64_t N = 0, K = 0;
   check_w8(w8, wscale, x, &N, &K);
@@ -330,8 +347,8 @@ std::tuple<at::Tensor, at::Tensor> skinny64_f8(const at::Tensor& x, const at::Te
     const at::Tensor& t = *ssq_in;
     check_cuda(t, "ssq_in");
     TORCH_CHECK(t.scalar_type() == at::kFloat && t.dim() == 2 && t.size(0) == M && t.is_contiguous() &&
-                    t.size(1) >= 1 && t.size(1) <= 8,
-                "ssq_in fp32 [M, nbp <= 8] contiguous");
+                    t.size(1) >= 1 && t.size(1) <= 64,
+                "ssq_in fp32 [M, nbp <= 64] contiguous");
     same_device(x, t);
     sq = t.data_ptr<float>();
     nbp = static_cast<int>(t.size(1));
@@ -353,8 +370,7 @@ std::tuple<at::Tensor, at::Tensor> skinny64_f8(const at::Tensor& x, const at::Te
   auto y = at::empty({M, N}, x.options());
   at::Tensor ws;
   if (S > 1) ws = at::empty({S, M, N}, x.options().dtype(at::kFloat));
-  launch_m64_gemm_f8(cbp(x), x.stride(0), wp, bp(y), y.stride(0), S > 1 ? ws.data_ptr<float>() : nullptr, (int)M,
-                     (int)N, (int)K, S, false, nullptr, 0, 0.f, wsc, st);
+  unsigned* cp = S > 1 ? m64_counters(cnt, x, N) : nullptr;
   const bf16_t* rp = nullptr;
   int64_t ldr = 0;
   at::Tensor ssq;
@@ -365,11 +381,14 @@ std::tuple<at::Tensor, at::Tensor> skinny64_f8(const at::Tensor& x, const at::Te
     same_device(x, r);
     rp = cbp(r);
     ldr = r.stride(0);
-    ssq = at::empty({M, (N + 1023) / 1024}, x.options().dtype(at::kFloat));
+    ssq = at::empty({M, cp ? N / 128 : (N + 1023) / 1024}, x.options().dtype(at::kFloat));
   }
-  if (S > 1)
+  float* sqo = ssq.defined() ? ssq.data_ptr<float>() : nullptr;
+  launch_m64_gemm_f8(cbp(x), x.stride(0), wp, bp(y), y.stride(0), S > 1 ? ws.data_ptr<float>() : nullptr, (int)M,
+                     (int)N, (int)K, S, false, sq, nbp, static_cast<float>(eps), wsc, st, cp, rp, ldr, sqo);
+  if (S > 1 && !cp)
     launch_m64_reduce(ws.data_ptr<float>(), S, (int)M, (int)N, bp(y), y.stride(0), rp, ldr, sq, nbp, (int)K,
-                      static_cast<float>(eps), ssq.defined() ? ssq.data_ptr<float>() : nullptr, st);
+                      static_cast<float>(eps), sqo, st);
   return {y, ssq};
 }
 
@@ -1066,8 +1085,8 @@ TORCH_LIBRARY_FRAGMENT(dla, m) {
   m.def("skinny_glu_norm(Tensor x, Tensor res, Tensor norm_w, float eps, Tensor w) -> (Tensor, Tensor)");
   m.def("skinny_glu_ks(Tensor x, Tensor w) -> Tensor");
   m.def("skinny_fused(Tensor x, Tensor w, Tensor? res, Tensor? ssq_in, float eps, bool glu) -> (Tensor, Tensor)");
-  m.def("skinny64(Tensor x, Tensor w, Tensor? res, Tensor? ssq_in, float eps, bool glu) -> (Tensor, Tensor)");
-  m.def("skinny64_f8(Tensor x, Tensor w8, Tensor wscale, Tensor? res, Tensor? ssq_in, float eps, bool glu) -> (Tensor, Tensor)");
+  m.def("skinny64(Tensor x, Tensor w, Tensor? res, Tensor? ssq_in, float eps, bool glu, Tensor? cnt=None) -> (Tensor, Tensor)");
+  m.def("skinny64_f8(Tensor x, Tensor w8, Tensor wscale, Tensor? res, Tensor? ssq_in, float eps, bool glu, Tensor? cnt=None) -> (Tensor, Tensor)");
   m.def("tile_weight(Tensor w, Tensor? nw, Tensor(a!) out, bool glu_il=False) -> ()");
   m.def("quant_tile_f8(Tensor w, Tensor? nw, Tensor(a!) out8, Tensor(b!) scale, bool glu_il=False) -> ()");
   m.def("skinny_glu_il(Tensor x, Tensor wt, Tensor ssq_in, float eps) -> Tensor");

@@ -287,6 +287,7 @@ class _DecodeGraph:
 
     def capture(self):
         self.cache.capturing = True
+        ops.decode._skinny_counters(self.tok.device)  # split-K counters: never allocated in a capture
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         self.graph = torch.cuda.CUDAGraph()

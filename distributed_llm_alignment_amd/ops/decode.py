@@ -511,8 +511,19 @@ def refresh_folded_weights(model) -> None:
                 fp8_tiled_weight(w)
 
 
-def _fused_op(rows: int):
-    return _ext.require().skinny64 if rows > 16 else _ext.require().skinny_fused
+# 17..64 rows, opt-in (DLA_M64_COMBINE=1): the split-K projections (o, down, qkv) sum their fp32
+# slabs in the last arriving workgroup of each column block (csrc/skinny64.hip M64Cmb) instead of
+# a separate reduce launch; the residual producer then emits row partials per 128 columns.
+# Bitwise equal to the reduce launch and SLOWER on 1x MI355X (graph decode B=64, prompt 512:
+# 5.46 / 5.49 vs 5.02 / 5.03 ms/token bf16, 4.65 / 4.68 vs 4.29 / 4.28 fp8, same box): the
+# write-through slab drain + arrival atomic + one workgroup summing 8 slabs from memory cost more
+# than the 4.8 us reduce launch they replace (profiles/r5_decode.md).
+M64_COMBINE = os.environ.get("DLA_M64_COMBINE", "0") == "1"
+
+
+def _m64_cnt(x: torch.Tensor) -> Optional[torch.Tensor]:
+    """Arrival counters for the in-kernel split-K combine (None: the reduce launch)."""
+    return _skinny_counters(x.device) if M64_COMBINE else None
 
 
 def skinny_residual(x: torch.Tensor, w: torch.Tensor, res: torch.Tensor):
@@ -521,12 +532,15 @@ def skinny_residual(x: torch.Tensor, w: torch.Tensor, res: torch.Tensor):
     if _f8_ok(x2.shape[0], w):
         w8, sc = fp8_tiled_weight(w)
         if x2.shape[0] > 16:
-            s, ssq = _ext.require().skinny64_f8(x2, w8, sc, _rows(res), None, 0.0, False)
+            s, ssq = _ext.require().skinny64_f8(x2, w8, sc, _rows(res), None, 0.0, False, _m64_cnt(x2))
         else:
             s, ssq = _ext.require().skinny_fused_f8(x2, w8, sc, _rows(res), None, 0.0)
         return s.view(*res.shape[:-1], w.shape[0]), ssq
     wk = tiled_weight(w) if DECODE_TILED >= 2 else w
-    s, ssq = _fused_op(x2.shape[0])(x2, wk, _rows(res), None, 0.0, False)
+    if x2.shape[0] > 16:
+        s, ssq = _ext.require().skinny64(x2, wk, _rows(res), None, 0.0, False, _m64_cnt(x2))
+    else:
+        s, ssq = _ext.require().skinny_fused(x2, wk, _rows(res), None, 0.0, False)
     return s.view(*res.shape[:-1], w.shape[0]), ssq
 
 
@@ -537,7 +551,7 @@ def skinny_normed(s: torch.Tensor, ssq: torch.Tensor, norm_w: torch.Tensor, eps:
     if _f8_ok(s2.shape[0], w) and s2.shape[0] > 16:
         # 17..64 rows: gate|up in the plain [gate; up] row order (the m64 GLU epilogue pairs them)
         w8, sc = fp8_tiled_weight(w, norm_w)
-        y, _ = _ext.require().skinny64_f8(s2, w8, sc, None, ssq, float(eps), bool(glu))
+        y, _ = _ext.require().skinny64_f8(s2, w8, sc, None, ssq, float(eps), bool(glu), _m64_cnt(s2))
         return y.view(*s.shape[:-1], y.shape[-1])
     if _f8_ok(s2.shape[0], w):
         if glu:
@@ -552,7 +566,10 @@ def skinny_normed(s: torch.Tensor, ssq: torch.Tensor, norm_w: torch.Tensor, eps:
         m = _ext.require().skinny_glu_il(s2, folded_weight(w, norm_w, tiled=True, glu_il=True), ssq, float(eps))
         return m.view(*s.shape[:-1], m.shape[-1])
     wf = folded_weight(w, norm_w, tiled=DECODE_TILED >= 1)
-    y, _ = _fused_op(s2.shape[0])(s2, wf, None, ssq, float(eps), bool(glu))
+    if s2.shape[0] > 16:
+        y, _ = _ext.require().skinny64(s2, wf, None, ssq, float(eps), bool(glu), _m64_cnt(s2))
+    else:
+        y, _ = _ext.require().skinny_fused(s2, wf, None, ssq, float(eps), bool(glu))
     return y.view(*s.shape[:-1], y.shape[-1])
 
 

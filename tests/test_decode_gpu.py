@@ -741,11 +741,12 @@ def test_skinny64_kernels_match_fp32(M):
     w = (torch.randn(H, F, device=DEV, generator=g) * F ** -0.5).to(torch.bfloat16)
     res = torch.randn(M, H, device=DEV, generator=g).to(torch.bfloat16)
     s, ssq = ops.decode.skinny_residual(x, w, res)
-    assert ssq.shape == (M, H // 1024)
+    assert ssq.shape == (M, H // 128 if ops.decode.M64_COMBINE else H // 1024)
     s_ref = (x.float() @ w.float().t()).to(torch.bfloat16).float() + res.float()
     assert float((s.float() - s_ref).abs().max()) < 0.05
     assert torch.allclose(ssq.sum(1), (s.float() ** 2).sum(1), rtol=1e-4)
-    s_t, ssq_t = ops._ext.require().skinny64(x, ops.decode.tiled_weight(w), res, None, 0.0, False)
+    s_t, ssq_t = ops._ext.require().skinny64(x, ops.decode.tiled_weight(w), res, None, 0.0, False,
+                                             ops.decode._m64_cnt(x))
     assert torch.equal(s_t, s) and torch.equal(ssq_t, ssq)
     nw = (1 + 0.1 * torch.randn(H, device=DEV, generator=g)).to(torch.bfloat16)
     h_ref = _ref_norm(s.float(), nw.float(), None, 1e-5, True)
@@ -759,6 +760,57 @@ def test_skinny64_kernels_match_fp32(M):
     # row-major folded weight (DLA_M64_TILED=0) == the tiled default, bitwise
     mm_rm, _ = ops._ext.require().skinny64(s, ops.decode.folded_weight(wgu, nw), None, ssq, 1e-5, True)
     assert torch.equal(mm_rm, mm)
+
+
+@pytest.mark.parametrize("M", [17, 40, 64])
+def test_m64_inkernel_combine_matches_reduce_launch(M):
+    """17..64 rows: the split-K projections' in-kernel combine (the last arriving workgroup of a
+    column block sums the write-through fp32 slabs, csrc/skinny64.hip M64Cmb) against the separate
+    reduce launch, bf16 and fp8 weights: plain and residual outputs BITWISE equal (same split
+    order and roundings); row partials per 128 columns that sum to the per-1024 ones; the
+    normalised-input consumers (qkv via the combine, gate|up via the GLU epilogue) fed 32
+    partials within rounding of the 4-partial path; every counter re-armed to 0; repeat calls
+    identical."""
+    from distributed_llm_alignment_amd import ops
+
+    C = ops._ext.require()
+    cnt = torch.zeros(8192, dtype=torch.int32, device=DEV)
+    g = torch.Generator(device=DEV).manual_seed(100 + M)
+    rel = lambda a, b: float((a.float() - b.float()).norm() / b.float().norm())
+    H, F = 4096, 14336
+    for N, K in ((6144, H), (H, H), (H, F)):
+        x = torch.randn(M, K, device=DEV, generator=g).to(torch.bfloat16)
+        w = (torch.randn(N, K, device=DEV, generator=g) * K ** -0.5).to(torch.bfloat16)
+        wt = ops.decode.tiled_weight(w)
+        w8, sc = ops.decode.fp8_tiled_weight(w)
+        for fp8 in (False, True):
+            op = (lambda *a: C.skinny64_f8(a[0], w8, sc, *a[2:])) if fp8 else C.skinny64
+            y0, _ = op(x, wt, None, None, 0.0, False)
+            y1, _ = op(x, wt, None, None, 0.0, False, cnt)
+            y2, _ = op(x, wt, None, None, 0.0, False, cnt)
+            assert torch.equal(y0, y1) and torch.equal(y1, y2), (N, K, fp8)
+            assert int(cnt.abs().sum()) == 0
+            if N != H:
+                continue
+            res = torch.randn(M, N, device=DEV, generator=g).to(torch.bfloat16)
+            s0, q0 = op(x, wt, res, None, 0.0, False)
+            s1, q1 = op(x, wt, res, None, 0.0, False, cnt)
+            assert torch.equal(s0, s1) and q0.shape == (M, N // 1024) and q1.shape == (M, N // 128)
+            assert torch.allclose(q1.view(M, N // 1024, 8).sum(2), q0, rtol=1e-5)
+            assert int(cnt.abs().sum()) == 0
+            nw = (1 + 0.1 * torch.randn(H, device=DEV, generator=g)).to(torch.bfloat16)
+            wq = (torch.randn(6144, H, device=DEV, generator=g) * H ** -0.5).to(torch.bfloat16)
+            wgu = (torch.randn(2 * 1024, H, device=DEV, generator=g) * H ** -0.5).to(torch.bfloat16)
+            for ww, glu in ((wq, False), (wgu, True)):
+                if fp8:
+                    a8, asc = ops.decode.fp8_tiled_weight(ww, nw)
+                    f = lambda *a: C.skinny64_f8(a[0], a8, asc, *a[2:])
+                else:
+                    f, a8 = C.skinny64, ops.decode.folded_weight(ww, nw, tiled=True)
+                h0, _ = f(s0, a8, None, q0, 1e-5, glu)
+                h1, _ = f(s0, a8, None, q1, 1e-5, glu, cnt)
+                assert rel(h1, h0) < 1e-3, (glu, fp8, rel(h1, h0))
+                assert int(cnt.abs().sum()) == 0
 
 
 @pytest.mark.parametrize("B,T,pad", [(1, 40, False), (5, 300, True), (8, 100, False), (16, 200, True)])
