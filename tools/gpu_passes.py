@@ -90,6 +90,9 @@ PASSES = {
         run("ppo_zero8_fp8", "python -u tools/bench_rlhf.py --algorithm ppo --zero-shape 8 --batch 8 --rollout-dtype fp8"),
     ],
     # ---- round 5
+    # B = 64 decode attention: key splits per sequence (DLA_DECODE_BLOCKS = target grid)
+    "ab-b64-blocks": [ab("b64_blocks", GEN64, {"base": {}, "blk1024": {"DLA_DECODE_BLOCKS": "1024"},
+                                               "blk2048": {"DLA_DECODE_BLOCKS": "2048"}}, 2, 300)],
     # 17..64-row split-K projections: in-kernel last-arriver combine vs the reduce launch
     "m64-combine": [
         pytest("tests/test_decode_gpu.py -k 'skinny64 or m64 or b64 or graph or fp8'", 600),
