@@ -90,6 +90,10 @@ PASSES = {
         run("ppo_zero8_fp8", "python -u tools/bench_rlhf.py --algorithm ppo --zero-shape 8 --batch 8 --rollout-dtype fp8"),
     ],
     # ---- round 5
+    # long-context DPO on the final build (the shard one SP-group member runs)
+    "longctx": [run("longctx_4k", DPO + " --seq-len 4096 --micro-pairs 1 --accum 4 --steps 3 --warmup 1", 400),
+                run("longctx_8k", DPO + " --seq-len 8192 --micro-pairs 1 --accum 2 --steps 3 --warmup 1", 400),
+                run("ref_fp8", DPO + " --steps 5 --warmup 2", 300, {"DLA_REF_FP8": "1"})],
     # B = 64 decode attention: key splits per sequence (DLA_DECODE_BLOCKS = target grid)
     "ab-b64-blocks": [ab("b64_blocks", GEN64, {"base": {}, "blk1024": {"DLA_DECODE_BLOCKS": "1024"},
                                                "blk2048": {"DLA_DECODE_BLOCKS": "2048"}}, 2, 300)],
