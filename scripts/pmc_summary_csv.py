@@ -1,12 +1,15 @@
 #!/usr/bin/env python
 """Per-kernel PMC table from rocprofv3 --pmc CSV output(s) (counter_collection.csv): mean
 counter value per dispatch for every kernel whose name contains one of the filters.
-Usage: pmc_summary_csv.py <counter_collection.csv> [more.csv ...] [-k substr ...]"""
+Usage: pmc_summary_csv.py <counter_collection.csv> [more.csv ...] [--by-grid] [-k substr ...]
+--by-grid keys the table by (kernel, grid size): library GEMMs share one kernel name across shapes."""
 import csv
 import sys
 from collections import defaultdict
 
 args = sys.argv[1:]
+by_grid = "--by-grid" in args
+args = [a for a in args if a != "--by-grid"]
 filt = []
 if "-k" in args:
     i = args.index("-k")
@@ -19,6 +22,8 @@ for path in args:
         if filt and not any(f in name for f in filt):
             continue
         short = name.split("(")[0].replace("void ", "")[:70]
+        if by_grid:
+            short = f"{short} @grid {r['Grid_Size']}"
         vals[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
         meta[short] = (r["Grid_Size"], r["Workgroup_Size"], r["LDS_Block_Size"], r["VGPR_Count"],
                        r["Accum_VGPR_Count"], r["Scratch_Size"])

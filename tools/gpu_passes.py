@@ -61,8 +61,9 @@ def prof(name, cmd, summaries, t=420, env=None):
     return {"kind": "prof", "name": name, "cmd": cmd, "summaries": summaries, "timeout": t, "env": env or {}}
 
 
-def pmc(name, counters, cmd, kernels, t=170):
-    return {"kind": "pmc", "name": name, "counters": counters, "cmd": cmd, "kernels": kernels, "timeout": t}
+def pmc(name, counters, cmd, kernels, t=170, summary_args=(), include=None):
+    return {"kind": "pmc", "name": name, "counters": counters, "cmd": cmd, "kernels": kernels, "timeout": t,
+            "summary_args": list(summary_args), "include": include}
 
 
 SMOKE = {"kind": "smoke", "timeout": 300}
@@ -90,6 +91,11 @@ PASSES = {
         run("ppo_zero8_fp8", "python -u tools/bench_rlhf.py --algorithm ppo --zero-shape 8 --batch 8 --rollout-dtype fp8"),
     ],
     # ---- round 5
+    # DPO step GEMMs: MFMA busy and effective clock per library GEMM shape (by grid)
+    "dpo-gemm-pmc": [pmc("dpo_gemm", "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY GRBM_GUI_ACTIVE",
+                         "python3 bench.py --micro-pairs 4 --accum 1 --steps 1 --warmup 1",
+                         "Cijk attn_fwd attn_bwd8 adamw swiglu_bwd_t", 400, ["--by-grid"],
+                         "Cijk|attn_fwd|attn_bwd8|adamw|swiglu_bwd_t")],
     # long-context DPO on the final build (the shard one SP-group member runs)
     "longctx": [run("longctx_4k", DPO + " --seq-len 4096 --micro-pairs 1 --accum 4 --steps 3 --warmup 1", 400),
                 run("longctx_8k", DPO + " --seq-len 8192 --micro-pairs 1 --accum 2 --steps 3 --warmup 1", 400),
@@ -260,7 +266,8 @@ class Runner:
             d = f"/tmp/pmc_{s['name']}"
             shutil.rmtree(d, ignore_errors=True)
             log = os.path.abspath(f"{o}/pmc_{s['name']}.log")
-            cmd = ["rocprofv3", "--pmc", *s["counters"].split(), "--output-format", "csv", "-d", d, "-o", "run",
+            inc = ["--kernel-include-regex", s["include"]] if s.get("include") else []
+            cmd = ["rocprofv3", "--pmc", *s["counters"].split(), *inc, "--output-format", "csv", "-d", d, "-o", "run",
                    "--", *shlex.split(s["cmd"])]
             full = ["timeout", "-s", "KILL", str(t)] + cmd
             if self.dry:
@@ -274,7 +281,8 @@ class Runner:
             dst = f"{o}/{s['name']}_pmc.md"
             with open(dst, "w") as fh:
                 rc = subprocess.call([sys.executable, os.path.join(ROOT, "scripts", "pmc_summary_csv.py"), c,
-                                      "-k", *s["kernels"].split()], stdout=fh, stderr=subprocess.STDOUT)
+                                      *s.get("summary_args", []), "-k", *s["kernels"].split()],
+                                     stdout=fh, stderr=subprocess.STDOUT)
             self._check(rc, f"pmc summary {dst}", dst)
             shutil.rmtree(d, ignore_errors=True)
             print(f"pmc {s['name']}: {dst}")
