@@ -36,6 +36,7 @@ constexpr int kM64Ck = 256;             // k per x chunk and per weight ring slo
 constexpr int kM64Steps = kM64Ck / 32;  // MFMA k-steps per chunk
 constexpr int kM64Ld = kM64Ck + 8;      // LDS row stride in bf16 (16-byte pad)
 constexpr int kM64MaxNbp = 64;          // row-norm partials per row (N / 128 <= 64: H <= 8192)
+constexpr int kM64RegNbp = 8;           // partials held in registers (reduce-launch producers: N / 1024)
 
 __device__ __forceinline__ f32x4 mfma16(s16x8 a, s16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
@@ -84,7 +85,8 @@ struct M64Cmb {
 // from ssq_in (the producer's row partial sums, [M][nbp]) when NIN, else 1; gate / up are
 // rounded to bf16 before SwiGLU exactly as the unfused GEMM + swiglu pair.
 // Otherwise S == 1 writes y = bf16(x W^T); S > 1 writes fp32 slab ws[s][m][n].
-template <int MT, bool GLU, bool NIN, bool TW, int DEPTH, int NW = kM64Waves, bool NTL = false, bool F8 = false>
+template <int MT, bool GLU, bool NIN, bool TW, int DEPTH, int NW = kM64Waves, bool NTL = false, bool F8 = false,
+          bool CMB = false>
 __global__ __launch_bounds__(64 * NW) void m64_gemm_kernel(
     const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ W, int64_t ldw,
     bf16_t* __restrict__ y, int64_t ldy, float* __restrict__ ws, int M, int N, int K, int kc,
@@ -111,11 +113,13 @@ __global__ __launch_bounds__(64 * NW) void m64_gemm_kernel(
   const uint8_t* wrow8 = reinterpret_cast<const uint8_t*>(W) + static_cast<int64_t>(n0 >> 4) * 16 * K +
                          (k0 >> 6) * 1024 + lane * 16;
 
-  // NIN: this row's producer partials, reduced in the epilogue (thread m < M holds row m)
-  float pv[kM64MaxNbp];
+  // NIN: this row's producer partials (thread m < M holds row m); up to kM64RegNbp are loaded
+  // here, ahead of the first chunk, and summed once those loads land
+  float pv[kM64RegNbp];
   if constexpr (NIN) {
 #pragma unroll
-    for (int j = 0; j < kM64MaxNbp; ++j) pv[j] = (tid < M && j < nbp) ? ssq_in[tid * nbp + j] : 0.f;
+    for (int j = 0; j < kM64RegNbp; ++j)
+      pv[j] = (tid < M && j < nbp && nbp <= kM64RegNbp) ? ssq_in[tid * nbp + j] : 0.f;
   }
 
   // Pipeline: chunk j = x(j) (this thread's 16-byte pieces of 16 MT rows, into register set
@@ -163,12 +167,17 @@ __global__ __launch_bounds__(64 * NW) void m64_gemm_kernel(
   if constexpr (DEPTH > 3) {
     if (3 < nch) issue(std::integral_constant<int, 3>{}, 3);
   }
-  // NIN: the row's partials summed now (their loads are older than the chunk loads, so this
-  // waits only for them), keeping one register instead of kM64MaxNbp live through the loop
+  // NIN: the row's partials summed now, in order (their loads are older than the chunk loads, so
+  // this waits only for them), one register live through the loop; the in-kernel-combine
+  // producers' N / 128 partials (> kM64RegNbp) are summed by a plain loop
   float rsum = 0.f;
   if constexpr (NIN) {
+    if (nbp <= kM64RegNbp) {
 #pragma unroll
-    for (int j = 0; j < kM64MaxNbp; ++j) rsum += pv[j];
+      for (int j = 0; j < kM64RegNbp; ++j) rsum += pv[j];
+    } else if (tid < M) {
+      for (int j = 0; j < nbp; ++j) rsum += ssq_in[tid * nbp + j];
+    }
     asm volatile("" : "+v"(rsum));
   }
   xstore(std::integral_constant<int, 0>{}, 0);
@@ -260,7 +269,7 @@ __global__ __launch_bounds__(64 * NW) void m64_gemm_kernel(
     return;
   }
   float* slab = ws + static_cast<int64_t>(s) * M * N;
-  if (cmb.cnt == nullptr) {
+  if constexpr (!CMB) {
 #pragma unroll
     for (int t = 0; t < MT; ++t)
 #pragma unroll
@@ -469,6 +478,20 @@ static void m64_launch_w(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t 
   }();
   (void)attr;
   dim3 grid(GLU ? N / 2 / (8 * NW) : N / (16 * NW), S);
+  if constexpr (!GLU) {
+    if (cmb.cnt != nullptr) {  // in-kernel split-K combine (its own instantiation: the default keeps its registers)
+      static bool attr_c = [] {
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&m64_gemm_kernel<MT, GLU, NIN, TW, DEPTH, NW, NTL, F8, true>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+        (void)hipGetLastError();
+        return true;
+      }();
+      (void)attr_c;
+      m64_gemm_kernel<MT, GLU, NIN, TW, DEPTH, NW, NTL, F8, true><<<grid, 64 * NW, lds, st>>>(
+          x, ldx, W, ldw, y, ldy, ws, M, N, K, K / S, ssq_in, nbp, eps, wsc, cmb);
+      return;
+    }
+  }
   m64_gemm_kernel<MT, GLU, NIN, TW, DEPTH, NW, NTL, F8><<<grid, 64 * NW, lds, st>>>(
       x, ldx, W, ldw, y, ldy, ws, M, N, K, K / S, ssq_in, nbp, eps, wsc, cmb);
 }

@@ -106,8 +106,8 @@ PASSES = {
     # 17..64-row split-K projections: in-kernel last-arriver combine vs the reduce launch
     "m64-combine": [
         pytest("tests/test_decode_gpu.py -k 'skinny64 or m64 or b64 or graph or fp8'", 600),
-        ab("m64_combine", GEN64, {"reduce": {"DLA_M64_COMBINE": "0"}, "combine": {}}, 2, 300),
-        ab("m64_combine_fp8", GEN64 + " --weight-dtype fp8", {"reduce": {"DLA_M64_COMBINE": "0"}, "combine": {}}, 2, 300),
+        ab("m64_combine", GEN64, {"reduce": {}, "combine": {"DLA_M64_COMBINE": "1"}}, 2, 300),
+        ab("m64_combine_fp8", GEN64 + " --weight-dtype fp8", {"reduce": {}, "combine": {"DLA_M64_COMBINE": "1"}}, 2, 300),
     ],
     # the validation table in two gpurun-sized halves (a call runs at most 20 minutes)
     "validate-a": [],
