@@ -7,6 +7,8 @@
 // SwiGLU input is the fused gate_up GEMM output gu[N, 2F] (gate = columns [0,F), up = [F,2F)).
 #include "common.h"
 
+#include <cstdlib>
+
 namespace dla {
 
 __device__ __forceinline__ float silu_f(float g) { return g * sigmoidf_(g); }
@@ -166,6 +168,98 @@ __global__ __launch_bounds__(256) void swiglu_bwd_t_kernel(const bf16_t* __restr
   }
 }
 
+// Register-transpose forms (csrc/transpose.hip transpose_bf16_reg_kernel): each lane owns an
+// 8 x 8 block, loads its 8 row segments of every operand (16 B each; the 8 lanes of a row block
+// cover one 128-byte line), computes the SAME per-element math as the LDS-tiled kernels above
+// (bitwise equal), stores the row-major outputs as row segments and the transposed outputs after
+// a v_perm_b32 8 x 8 transpose as 16-byte column segments. No LDS round trip and 256-384 B of
+// loads in flight per lane. A wave covers 64 rows x 64 columns; grid (ceil(F / 256), rows / 64);
+// rows % 8 == 0 and F % 8 == 0 (checked by the launcher; other shapes take the LDS kernels).
+typedef uint32_t ew_u32x4 __attribute__((ext_vector_type(4)));
+
+// out[j] = column j of the 8 x 8 bf16 block held as 8 row vectors v[0..7]
+__device__ __forceinline__ void ew_tr8(const bf16x8 (&v)[8], bf16x8 (&out)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const uint32_t sel = (j & 1) ? 0x07060302u : 0x05040100u;
+    ew_u32x4 o;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      o[k] = __builtin_amdgcn_perm(__builtin_bit_cast(ew_u32x4, v[2 * k + 1])[j >> 1],
+                                   __builtin_bit_cast(ew_u32x4, v[2 * k])[j >> 1], sel);
+    out[j] = __builtin_bit_cast(bf16x8, o);
+  }
+}
+
+__global__ __launch_bounds__(256) void swiglu_fwd_t_reg_kernel(const bf16_t* __restrict__ gu,
+                                                                bf16_t* __restrict__ out,
+                                                                bf16_t* __restrict__ outT,
+                                                                int64_t rows, int F) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t r = static_cast<int64_t>(blockIdx.y) * 64 + (lane >> 3) * 8;
+  const int c = blockIdx.x * 256 + w * 64 + (lane & 7) * 8;
+  if (r >= rows || c >= F) return;
+  bf16x8 g[8], u[8], o[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const bf16_t* row = gu + (r + i) * 2 * F;
+    g[i] = load_bf16x8(row + c);
+    u[i] = load_bf16x8(row + F + c);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[i][j] = f2bf(silu_f(bf2f(g[i][j])) * bf2f(u[i][j]));
+    store_bf16x8(out + (r + i) * F + c, o[i]);
+  }
+  bf16x8 t[8];
+  ew_tr8(o, t);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) store_bf16x8(outT + static_cast<int64_t>(c + j) * rows + r, t[j]);
+}
+
+__global__ __launch_bounds__(256) void swiglu_bwd_t_reg_kernel(const bf16_t* __restrict__ gu,
+                                                                const bf16_t* __restrict__ dout,
+                                                                bf16_t* __restrict__ dgu,
+                                                                bf16_t* __restrict__ dguT,
+                                                                int64_t rows, int F) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t r = static_cast<int64_t>(blockIdx.y) * 64 + (lane >> 3) * 8;
+  const int c = blockIdx.x * 256 + w * 64 + (lane & 7) * 8;
+  if (r >= rows || c >= F) return;
+  bf16x8 dg[8], du[8];
+  {
+    bf16x8 g[8], u[8], d[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const bf16_t* row = gu + (r + i) * 2 * F;
+      g[i] = load_bf16x8(row + c);
+      u[i] = load_bf16x8(row + F + c);
+      d[i] = load_bf16x8(dout + (r + i) * F + c);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      swiglu_grad8(g[i], u[i], d[i], dg[i], du[i]);
+      store_bf16x8(dgu + (r + i) * 2 * F + c, dg[i]);
+      store_bf16x8(dgu + (r + i) * 2 * F + F + c, du[i]);
+    }
+  }
+  bf16x8 t[8];
+  ew_tr8(dg, t);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) store_bf16x8(dguT + static_cast<int64_t>(c + j) * rows + r, t[j]);
+  ew_tr8(du, t);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) store_bf16x8(dguT + static_cast<int64_t>(F + c + j) * rows + r, t[j]);
+}
+
+// DLA_SWIGLU_T_REG=0/1 picks the LDS-tiled or register-transpose form (read per call: tests A/B it)
+static bool swiglu_t_reg(int64_t rows, int F) {
+  const char* e = getenv("DLA_SWIGLU_T_REG");
+  const bool on = e == nullptr || atoi(e) != 0;
+  return on && rows % 8 == 0 && F % 8 == 0;
+}
+
 // gelu_new (tanh approximation), as used by GPT-2 and phi-2.
 __device__ __forceinline__ float gelu_tanh(float x, float* dgdx) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
@@ -216,12 +310,22 @@ void launch_swiglu_bwd(const bf16_t* gu, const bf16_t* dout, bf16_t* dgu, int64_
 void launch_swiglu_fwd_t(const bf16_t* gu, bf16_t* out, bf16_t* outT, int64_t rows, int F,
                          hipStream_t st) {
   if (rows == 0) return;
+  if (swiglu_t_reg(rows, F)) {
+    const dim3 g((F + 255) / 256, static_cast<unsigned>((rows + 63) / 64));
+    swiglu_fwd_t_reg_kernel<<<g, 256, 0, st>>>(gu, out, outT, rows, F);
+    return;
+  }
   const dim3 grid(F / kTT, static_cast<unsigned>((rows + kTT - 1) / kTT));
   swiglu_fwd_t_kernel<<<grid, 256, 0, st>>>(gu, out, outT, rows, F);
 }
 void launch_swiglu_bwd_t(const bf16_t* gu, const bf16_t* dout, bf16_t* dgu, bf16_t* dguT,
                          int64_t rows, int F, hipStream_t st) {
   if (rows == 0) return;
+  if (swiglu_t_reg(rows, F)) {
+    const dim3 g((F + 255) / 256, static_cast<unsigned>((rows + 63) / 64));
+    swiglu_bwd_t_reg_kernel<<<g, 256, 0, st>>>(gu, dout, dgu, dguT, rows, F);
+    return;
+  }
   const dim3 grid(F / kTT, static_cast<unsigned>((rows + kTT - 1) / kTT));
   swiglu_bwd_t_kernel<<<grid, 256, 0, st>>>(gu, dout, dgu, dguT, rows, F);
 }

@@ -91,6 +91,11 @@ PASSES = {
         run("ppo_zero8_fp8", "python -u tools/bench_rlhf.py --algorithm ppo --zero-shape 8 --batch 8 --rollout-dtype fp8"),
     ],
     # ---- round 5
+    # SwiGLU transposed-output kernels: LDS-tiled vs register transpose (bitwise test, microbench, DPO A/B)
+    "ab-swiglu-t-reg": [pytest("tests/test_kernels_gpu.py -k swiglu", 200),
+                        run("swiglu_t_bench", "python -u tools/transpose_bench.py", 200),
+                        ab("swiglu_t_reg", DPO + " --steps 5 --warmup 2", {"lds": {"DLA_SWIGLU_T_REG": "0"},
+                                                                          "reg": {"DLA_SWIGLU_T_REG": "1"}}, 2, 300)],
     # DPO step GEMMs: MFMA busy and effective clock per library GEMM shape (by grid)
     "dpo-gemm-pmc": [pmc("dpo_gemm", "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY GRBM_GUI_ACTIVE",
                          "python3 bench.py --micro-pairs 4 --accum 1 --steps 1 --warmup 1",
