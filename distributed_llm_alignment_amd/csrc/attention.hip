@@ -1045,6 +1045,8 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_persist_kernel(AttnParams p,
 // ==============================================================================================
 // backward preprocessing: delta[b,h,t] = sum_d dO * O   (one wave per (b, t, h) row)
 // ==============================================================================================
+// kDeltaRows: rows per lane group (DLA_ATTN_DELTA_ROWS=1 restores one row per group, A/B)
+template <int kDeltaRows>
 __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(const bf16_t* __restrict__ o,
                                                               const bf16_t* __restrict__ dout,
                                                               int64_t o_sb, int64_t o_st,
@@ -1053,24 +1055,36 @@ __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(const bf16_t* __res
                                                               int B, int H, int T, int D,
                                                               float* __restrict__ delta) {
   // delta[row] = <O[row], dO[row]>: D/8 lanes x 16-B loads per row (16 lanes at D = 128),
-  // 64 / (D/8) rows per wave, shuffle reduction inside the lane group
+  // 64 / (D/8) row groups per wave, kDeltaRows consecutive rows per lane group (all their loads
+  // in flight before any use: 4x the bytes per lane of one row), shuffle reduction inside the
+  // lane group -- per row the same arithmetic as one row per group
   const int lpr = D <= 64 ? 8 : 16;  // lanes per row (power of two; D = 80: 10 of 16 load)
   const int lane = threadIdx.x & 63;
-  const int64_t row = (blockIdx.x * 4ll + (threadIdx.x >> 6)) * (64 / lpr) + lane / lpr;
+  const int64_t row0 = ((blockIdx.x * 4ll + (threadIdx.x >> 6)) * (64 / lpr) + lane / lpr) * kDeltaRows;
   const int c = (lane % lpr) * 8;
-  float acc = 0.f;
-  const bool ok = row < static_cast<int64_t>(B) * H * T;
-  if (ok && c < D) {
-    const int t = static_cast<int>(row % T);
-    const int64_t bh = row / T;
-    const int hh = static_cast<int>(bh % H), b = static_cast<int>(bh / H);
-    const bf16x8 a = load_bf16x8(o + b * o_sb + t * o_st + hh * o_sh + c);
-    const bf16x8 g = load_bf16x8(dout + b * do_sb + t * do_st + hh * do_sh + c);
+  const int64_t nrows = static_cast<int64_t>(B) * H * T;
+  bf16x8 a[kDeltaRows], g[kDeltaRows];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc += bf2f(a[j]) * bf2f(g[j]);
+  for (int k = 0; k < kDeltaRows; ++k) {
+    const int64_t row = row0 + k;
+    a[k] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    g[k] = a[k];
+    if (row < nrows && c < D) {
+      const int t = static_cast<int>(row % T);
+      const int64_t bh = row / T;
+      const int hh = static_cast<int>(bh % H), b = static_cast<int>(bh / H);
+      a[k] = load_bf16x8(o + b * o_sb + t * o_st + hh * o_sh + c);
+      g[k] = load_bf16x8(dout + b * do_sb + t * do_st + hh * do_sh + c);
+    }
   }
-  for (int off = 1; off < lpr; off <<= 1) acc += __shfl_xor(acc, off, 64);
-  if (ok && (lane % lpr) == 0) delta[row] = acc;
+#pragma unroll
+  for (int k = 0; k < kDeltaRows; ++k) {
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += bf2f(a[k][j]) * bf2f(g[k][j]);
+    for (int off = 1; off < lpr; off <<= 1) acc += __shfl_xor(acc, off, 64);
+    if (row0 + k < nrows && (lane % lpr) == 0) delta[row0 + k] = acc;
+  }
 }
 
 // ==============================================================================================
@@ -2364,9 +2378,14 @@ void launch_attn_bwd_delta(const bf16_t* o, const bf16_t* dout, int64_t o_sb, in
                            int H, int T, int D, float* delta, hipStream_t st) {
   const int64_t rows = static_cast<int64_t>(B) * H * T;
   if (rows == 0) return;
-  const int64_t rows_per_block = 4 * (64 / (D <= 64 ? 8 : 16));  // as attn_bwd_delta_kernel
-  attn_bwd_delta_kernel<<<static_cast<unsigned>((rows + rows_per_block - 1) / rows_per_block), 256, 0, st>>>(
-      o, dout, o_sb, o_st, o_sh, do_sb, do_st, do_sh, B, H, T, D, delta);
+  const char* e = std::getenv("DLA_ATTN_DELTA_ROWS");  // read per call (A/B in one process)
+  const int rpl = (e && std::atoi(e) == 1) ? 1 : 4;
+  const int64_t rows_per_block = 4 * (64 / (D <= 64 ? 8 : 16)) * rpl;  // as attn_bwd_delta_kernel
+  const unsigned nb = static_cast<unsigned>((rows + rows_per_block - 1) / rows_per_block);
+  if (rpl == 1)
+    attn_bwd_delta_kernel<1><<<nb, 256, 0, st>>>(o, dout, o_sb, o_st, o_sh, do_sb, do_st, do_sh, B, H, T, D, delta);
+  else
+    attn_bwd_delta_kernel<4><<<nb, 256, 0, st>>>(o, dout, o_sb, o_st, o_sh, do_sb, do_st, do_sh, B, H, T, D, delta);
 }
 
 // Backward main kernel: attn_bwd8_kernel (8 waves, default) or attn_bwd_kernel
