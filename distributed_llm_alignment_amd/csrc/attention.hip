@@ -1045,7 +1045,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_persist_kernel(AttnParams p,
 // ==============================================================================================
 // backward preprocessing: delta[b,h,t] = sum_d dO * O   (one wave per (b, t, h) row)
 // ==============================================================================================
-// kDeltaRows: rows per lane group (DLA_ATTN_DELTA_ROWS=1 restores one row per group, A/B)
+// kDeltaRows: rows per lane group (1, the default, or 4 with DLA_ATTN_DELTA_ROWS=4)
 template <int kDeltaRows>
 __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(const bf16_t* __restrict__ o,
                                                               const bf16_t* __restrict__ dout,
@@ -2378,8 +2378,11 @@ void launch_attn_bwd_delta(const bf16_t* o, const bf16_t* dout, int64_t o_sb, in
                            int H, int T, int D, float* delta, hipStream_t st) {
   const int64_t rows = static_cast<int64_t>(B) * H * T;
   if (rows == 0) return;
-  const char* e = std::getenv("DLA_ATTN_DELTA_ROWS");  // read per call (A/B in one process)
-  const int rpl = (e && std::atoi(e) == 1) ? 1 : 4;
+  // DLA_ATTN_DELTA_ROWS=4: four rows per lane group (read per call, A/B in one process). Bitwise
+  // equal; 351.7 vs 352.7 us for the whole backward in tools/attn_bench.py, but 30.1 vs 27.3 us per
+  // call inside the DPO step (profiles/r5_dpo_kernels.md), so one row per group stays the default.
+  const char* e = std::getenv("DLA_ATTN_DELTA_ROWS");
+  const int rpl = (e && std::atoi(e) == 4) ? 4 : 1;
   const int64_t rows_per_block = 4 * (64 / (D <= 64 ? 8 : 16)) * rpl;  // as attn_bwd_delta_kernel
   const unsigned nb = static_cast<unsigned>((rows + rows_per_block - 1) / rows_per_block);
   if (rpl == 1)
