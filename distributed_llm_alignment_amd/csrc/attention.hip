@@ -2380,7 +2380,8 @@ void launch_attn_bwd_delta(const bf16_t* o, const bf16_t* dout, int64_t o_sb, in
   if (rows == 0) return;
   // DLA_ATTN_DELTA_ROWS=4: four rows per lane group (read per call, A/B in one process). Bitwise
   // equal; 351.7 vs 352.7 us for the whole backward in tools/attn_bench.py, but 30.1 vs 27.3 us per
-  // call inside the DPO step (profiles/r5_dpo_kernels.md), so one row per group stays the default.
+  // call inside the DPO step (two profiles, different boxes: profiles/r5_dpo_kernels.md), so one row
+  // per group stays the default.
   const char* e = std::getenv("DLA_ATTN_DELTA_ROWS");
   const int rpl = (e && std::atoi(e) == 4) ? 4 : 1;
   const int64_t rows_per_block = 4 * (64 / (D <= 64 ? 8 : 16)) * rpl;  // as attn_bwd_delta_kernel
