@@ -217,6 +217,11 @@ class fp8_inference_scope:
                 w.__dict__.pop("_dla_fp8_infer", None)
             else:
                 w._dla_fp8_infer = v
+            if not v:
+                # the e4m3 copy quantised for this scope (ops.moe.fp8_weight) would otherwise stay
+                # resident on a trainable policy between rollouts (and be re-quantised after every
+                # optimizer step anyway); a frozen model marked by enable_fp8_inference keeps it
+                w.__dict__.pop("_dla_fp8", None)
         self.prev = []
         return False
 

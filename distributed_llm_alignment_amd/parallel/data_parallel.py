@@ -88,7 +88,7 @@ class DataParallelEngine:
         DLA_FORCE_COMM=1) with a ONE-rank group: run the multi-rank code path anyway -- ZeRO-1
         layout, grad-ready bucket hooks, async reduce-scatters on RCCL's stream during backward,
         the shard AdamW and the overlapped all-gathers -- so every line the N-GPU job runs
-        executes on one GPU (bench.py --force-pg, tests/test_force_comm_gpu.py)."""
+        executes on one GPU (bench.py --force-pg, tests/test_force_comm.py)."""
         self.module = module
         # sequence parallel (parallel.sequence): `group` is DP x SP and the sp ranks of a replica
         # hold partial (token-slice) gradients of one replicated loss -> sum over SP, mean over DP
@@ -417,11 +417,18 @@ class DataParallelEngine:
                 if post is not None:
                     post()
             self.comm_timer.end()
+        self._reset_pass_state()
+
+    def _reset_pass_state(self):
+        # also clears _pass_armed: a backward that raised after its first gradient hook (OOM)
+        # never ran its queued _end_sync_pass, and a stuck flag would stop later sync passes
+        # from arming theirs
         self._handles = []
         self._launched = 0
         self._ready = [0] * len(self.buckets)
         self._seen = set()
         self._pass_launched = False
+        self._pass_armed = False
 
     # ------------------------------------------------------------------------ step
     @property
@@ -468,6 +475,7 @@ class DataParallelEngine:
         """Finish comm, clip, fused AdamW on the local shard, all-gather weights, zero grads.
         Returns the (device) global grad norm."""
         self.finish_grad_sync()
+        self.comm_timer.close_step()
         lr = self.lr if lr is None else lr
         coef = self.clip_and_norm()
         self.step_count += 1
@@ -525,6 +533,9 @@ class DataParallelEngine:
 
     def zero_grad(self):
         self.wait_params()  # an overlapped optimizer step still owns the grad buffer
+        for h, _ in self._handles:  # collectives still reading/writing the buffers (an aborted pass)
+            h.wait()
+        self._reset_pass_state()
         self.grad_buf.zero_()
         if self.grad_fp32:
             for p in self.params:

@@ -48,7 +48,7 @@ def init_distributed(backend: Optional[str] = None, timeout_s: int = 1800,
     process group anyway and mark the state `forced`, so the communication engines run their
     collective code paths (hooks, async works, RCCL's stream and events) on one GPU -- the same
     code the N-GPU job runs, exercised where there is only one device (bench.py --force-pg,
-    tests/test_force_comm_gpu.py)."""
+    tests/test_force_comm.py)."""
     global _STATE
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -69,16 +69,15 @@ def init_distributed(backend: Optional[str] = None, timeout_s: int = 1800,
     os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
     timeout_s = int(os.environ.get("DLA_COLLECTIVE_TIMEOUT_S", timeout_s))
     if (world > 1 or forced) and not dist.is_initialized():
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if forced and "MASTER_PORT" not in os.environ:
-            import socket
-
-            with socket.socket() as s:  # a private rendezvous port for the one-rank group
-                s.bind(("127.0.0.1", 0))
-                os.environ["MASTER_PORT"] = str(s.getsockname()[1])
-        os.environ.setdefault("MASTER_PORT", "29500")
         kwargs = dict(backend=be, rank=rank, world_size=world,
                       timeout=datetime.timedelta(seconds=timeout_s))
+        if forced:
+            # the one-rank group rendezvous in-process: no TCP port to race for, nothing written
+            # into MASTER_PORT for later inits or child processes to inherit
+            kwargs["store"] = dist.HashStore()
+        else:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29500")
         if be == "nccl":
             kwargs["device_id"] = dev
             opts = comm_pg_options()
@@ -207,6 +206,7 @@ class ExposedCommTimer:
         self._a = self._b = None
         self._t0 = self._host_ms = 0.0
         self._hist: list = []  # every interval since reset(): (start, end) events or host ms
+        self._step_from, self._last_step = 0, []  # close_step() / last_step_ms()
 
     def begin(self):
         if self.cuda:
@@ -229,9 +229,29 @@ class ExposedCommTimer:
             self._hist.append(self._host_ms)
         if len(self._hist) > 4096:
             del self._hist[:2048]
+            self._step_from = max(0, getattr(self, "_step_from", 0) - 2048)
 
     def reset(self):
         self._hist = []
+        self._step_from, self._last_step = 0, []
+
+    def close_step(self):
+        """Mark an optimizer-step boundary: the intervals recorded since the previous boundary
+        (one per drained backward pass under FSDP, plus the step's own wait) become the step's
+        exposed comm, read by `last_step_ms()`."""
+        start = getattr(self, "_step_from", 0)
+        self._last_step = self._hist[start:]
+        self._step_from = len(self._hist)
+
+    def last_step_ms(self) -> float:
+        """Exposed comm of the last closed step: the SUM of its intervals (synchronises)."""
+        iv = getattr(self, "_last_step", [])
+        if self.cuda:
+            if not iv:
+                return 0.0
+            iv[-1][1].synchronize()
+            return float(sum(a.elapsed_time(b) for a, b in iv))
+        return float(sum(iv))
 
     def total_ms(self) -> float:
         """Sum over every interval since reset() (synchronises on the last one)."""

@@ -133,7 +133,7 @@ class _ShardedBase:
         if force_comm is None:
             force_comm = self.dist.forced or os.environ.get("DLA_FORCE_COMM", "0") == "1"
         # `_comm`: gathers / reduce-scatters go through the communicator. A one-rank group with
-        # force_comm runs them too (the N-GPU code path on one GPU, tests/test_force_comm_gpu.py)
+        # force_comm runs them too (the N-GPU code path on one GPU, tests/test_force_comm.py)
         self._comm = self.world > 1 or (bool(force_comm) and not single and dist.is_available()
                                          and dist.is_initialized())
         self.comm_ops = 0  # collectives issued (tests check that the comm path ran)
@@ -477,6 +477,10 @@ class FullyShardedEngine(_ShardedBase):
             for u in sorted(self.units, key=lambda x: -x.idx):
                 if not u.reduced and (u.ready > 0 or u.in_backward or u.is_root):
                     self._reduce(u)
+        # one interval per drain that has something to wait for: the end-of-backward callback
+        # (_post_backward) drains every pass, so step()'s own call usually finds nothing and
+        # must not record an empty interval (the step's exposed comm is the sum: close_step)
+        timed = timed and bool(self._pending)
         if timed:
             self.comm_timer.begin()
         while self._pending:
@@ -517,6 +521,7 @@ class FullyShardedEngine(_ShardedBase):
 
     def step(self, lr: Optional[float] = None) -> torch.Tensor:
         self.finish_grad_sync()
+        self.comm_timer.close_step()
         lr = self.lr if lr is None else lr
         coef = self.clip_and_norm()
         self.step_count += 1

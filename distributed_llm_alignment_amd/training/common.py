@@ -314,7 +314,7 @@ def train_loop(ctx: TrainContext, loader, sampler, engine: DataParallelEngine, s
                 # out-of-range token ids since the last log (sticky device word), on every rank
                 check_ids(collective=True)
                 rec = {"train/loss": running.average, "train/grad_norm": engine.last_grad_norm,
-                       "train/comm_exposed_ms": engine.comm_timer.last_ms()}
+                       "train/comm_exposed_ms": engine.comm_timer.last_step_ms()}
                 dropped = _moe_dropped_slots(models_to_save[0])
                 if dropped is not None:
                     rec["moe/dropped_slots"] = dropped

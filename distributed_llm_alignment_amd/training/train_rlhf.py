@@ -172,7 +172,7 @@ def main(argv=None) -> int:
         if (step + 1) % log_every == 0:
             ctx.logger.log({"train/loss": running.average, "train/kl": m["kl"],
                             "train/reward_mean": scores.mean(), "train/grad_norm": engine.last_grad_norm,
-                            "train/comm_exposed_ms": engine.comm_timer.last_ms()},
+                            "train/comm_exposed_ms": engine.comm_timer.last_step_ms()},
                            step + 1)
             running = RunningLoss()
     barrier()
@@ -258,7 +258,10 @@ def _ppo_loop(ctx, config, ppo, policy, ref, rm, rollout, engine, steps, kl_coef
                 loss.backward()
                 last = ep == epochs - 1 and mi == len(bounds) - 1
                 if last and overlap and step + 1 < steps:
-                    pending = rollout()  # overlaps the in-flight gradient reduce-scatter
+                    # overlaps the in-flight ZeRO-0/1 bucket collectives (they are waited on in
+                    # step()); an FSDP engine has already drained its reduce-scatters in its
+                    # end-of-backward callback, so there the rollout only runs ahead of step()
+                    pending = rollout()
                 engine.step()
                 critic_engine.step()
                 running.update(loss.detach())
@@ -270,7 +273,7 @@ def _ppo_loop(ctx, config, ppo, policy, ref, rm, rollout, engine, steps, kl_coef
                             "train/policy_loss": m["policy_loss"], "train/value_loss": m["value_loss"],
                             "train/clipfrac": m["clipfrac"], "train/approx_kl": m["approx_kl"],
                             "train/grad_norm": engine.last_grad_norm,
-                            "train/comm_exposed_ms": engine.comm_timer.last_ms()}, step + 1)
+                            "train/comm_exposed_ms": engine.comm_timer.last_step_ms()}, step + 1)
             running = RunningLoss()
     barrier()
     out = save_state(config["logging"]["output_dir"], [policy.model, ref.model, rm, critic], engine, None,

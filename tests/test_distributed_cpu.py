@@ -859,7 +859,7 @@ def _exposed_comm(rank, world, zero):
             # slowest sync-mode exposure seen so far (at least 250 ms)
             time.sleep(max(0.25, 3e-3 * max(out.get("sync", [0.0]))))
         eng.step()
-        out.setdefault(mode, []).append(eng.comm_timer.last_ms())
+        out.setdefault(mode, []).append(eng.comm_timer.last_step_ms())
     return {k: statistics.median(v) for k, v in out.items()}
 
 
@@ -873,6 +873,31 @@ def test_async_rollout_order_hides_gradient_comm(zero):
         print(f"rank {r} zero{zero}: exposed comm sync {d['sync']:.1f} ms, overlapped {d['overlap']:.1f} ms")
         assert d["sync"] > 1.0, d  # the collectives take measurable time on this host
         assert d["overlap"] < 0.35 * d["sync"], d
+
+
+def _fsdp_exposed(rank, world):
+    from distributed_llm_alignment_amd.models import build_model, get_config
+    from distributed_llm_alignment_amd.parallel.fsdp import FullyShardedEngine
+
+    cfg = get_config("tiny-llama")
+    net = build_model(cfg, device="cpu", seed=0)
+    eng = FullyShardedEngine(net, lr=1e-3)
+    ids = torch.randint(3, cfg.vocab_size, (2, 16), generator=torch.Generator().manual_seed(rank))
+    for _ in range(2):  # two accumulated micro-batches: each backward drains in its callback
+        net.causal_lm_loss(ids, ids).backward()
+    n_iv = len(eng.comm_timer._hist)
+    eng.step()
+    return n_iv, len(eng.comm_timer._hist), eng.comm_timer.last_step_ms(), eng.comm_timer.total_ms()
+
+
+def test_fsdp_exposed_comm_sums_the_step():
+    """FSDP drains its reduce-scatters at the end of every backward pass, so step() must neither
+    record an empty interval nor report only the last one: the step's exposed comm is the sum of
+    the per-pass intervals (round-5 advice: it read ~0 ms)."""
+    res = run_ranks(_fsdp_exposed, 2, ())
+    for r, (before, after, step_ms, total) in res.items():
+        assert before == 2 and after == 2, (before, after)  # step() added no empty interval
+        assert step_ms > 0.0 and abs(step_ms - total) < 1e-6, (step_ms, total)
 
 
 def _fsdp_generate(rank, world, gather):
