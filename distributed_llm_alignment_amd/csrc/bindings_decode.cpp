@@ -11,7 +11,6 @@
 #include <tuple>
 
 #include "bind_util.h"
-#include "decode_tail.h"
 #include "skinny_params.h"
 
 namespace dla {
@@ -24,17 +23,6 @@ void launch_decode_attn_rope(const bf16_t*, int64_t, const float*, const float*,
                              const int*, const int*, int, float, int, int, int, int, int, float*,
                              float*, bf16_t*, int64_t, int64_t, int*, hipStream_t);
 int decode_num_splits(int Tmax, int B, int Hkv);
-int decode_qkv_attn_splits(int Tmax, int B, int Hkv);
-int decode_attn_slab_splits(int Tmax, int B, int Hkv);
-void launch_decode_attn_slab(const float*, int, int, const float*, int, int, float, const float*,
-                             const float*, const int*, const int64_t*, int, bf16_t*, bf16_t*, int64_t,
-                             int64_t, int64_t, const int*, const int*, int, float, int, int, int, int, int,
-                             float*, float*, bf16_t*, int64_t, int64_t, int*, hipStream_t);
-bool launch_decode_qkv_attn(const bf16_t*, int64_t, const bf16_t*, bf16_t*, int64_t, int, int, int,
-                            const KsFuse&, const float*, const float*, const int*, const int64_t*, int,
-                            bf16_t*, bf16_t*, int64_t, int64_t, int64_t, const int*, const int*, int,
-                            float, int, int, int, int, float*, float*, bf16_t*, int64_t, int64_t, int*,
-                            int*, const int*, int*, hipStream_t);
 void launch_rope_cache(const bf16_t*, int64_t, bf16_t*, bf16_t*, bf16_t*, int64_t, int64_t,
                        int64_t, const int64_t*, const float*, const float*, const int*, int, int,
                        int, int, int, hipStream_t);
@@ -73,24 +61,11 @@ void launch_skinny_glu_il_f8(const bf16_t*, int64_t, const uint8_t*, bf16_t*, in
                              const KsFuse&, hipStream_t);
 bool m64_shape_ok(int N, int K, bool glu);
 void launch_m64_gemm(const bf16_t*, int64_t, const bf16_t*, int64_t, bf16_t*, int64_t, float*, int,
-                     int, int, int, bool, const float*, int, float, bool, hipStream_t, unsigned* = nullptr,
-                     const bf16_t* = nullptr, int64_t = 0, float* = nullptr);
+                     int, int, int, bool, const float*, int, float, bool, hipStream_t);
 void launch_m64_reduce(const float*, int, int, int, bf16_t*, int64_t, const bf16_t*, int64_t,
                        const float*, int, int, float, float*, hipStream_t);
 void launch_m64_gemm_f8(const bf16_t*, int64_t, const uint8_t*, bf16_t*, int64_t, float*, int, int, int, int,
-                        bool, const float*, int, float, const float*, hipStream_t, unsigned* = nullptr,
-                        const bf16_t* = nullptr, int64_t = 0, float* = nullptr);
-
-// split-K arrival counters for the in-kernel combine (csrc/skinny64.hip M64Cmb): int32, zero,
-// at least one per 128-column block; the kernel re-arms them
-static unsigned* m64_counters(const c10::optional<at::Tensor>& cnt, const at::Tensor& x, int64_t N) {
-  if (!cnt.has_value()) return nullptr;
-  const at::Tensor& c = *cnt;
-  TORCH_CHECK(c.is_cuda() && c.scalar_type() == at::kInt && c.is_contiguous() && c.numel() >= N / 128,
-              "cnt: contiguous int32 counters, one per 128 output columns");
-  TORCH_CHECK(c.device() == x.device(), "cnt: same device as x");
-  return reinterpret_cast<unsigned*>(c.data_ptr<int>());
-}
+                        bool, const float*, int, float, const float*, hipStream_t);
 
 // Decode projection at 17..64 rows (skinny64.hip), the same fused-layer contract as
 // skinny_fused below with row-norm partials per (row, 1024 columns):
@@ -101,7 +76,7 @@ static unsigned* m64_counters(const c10::optional<at::Tensor>& cnt, const at::Te
 std::tuple<at::Tensor, at::Tensor> skinny64(const at::Tensor& x, const at::Tensor& w,
                                             const c10::optional<at::Tensor>& res,
                                             const c10::optional<at::Tensor>& ssq_in, double eps,
-                                            bool glu, const c10::optional<at::Tensor>& cnt) {
+                                            bool glu) {
   check_bf16(x, "x");
   check_bf16(w, "w");
   // w: [N, K] row-major, or the tiled layout [N / 16, K / 32, 4, 16, 8] (skinny64.hip TW)
@@ -145,7 +120,6 @@ std::tuple<at::Tensor, at::Tensor> skinny64(const at::Tensor& x, const at::Tenso
   auto y = at::empty({M, N}, x.options());
   at::Tensor ws;
   if (S > 1) ws = at::empty({S, M, N}, x.options().dtype(at::kFloat));
-  unsigned* cp = S > 1 ? m64_counters(cnt, x, N) : nullptr;
   const bf16_t* rp = nullptr;
   int64_t ldr = 0;
   at::Tensor ssq;
@@ -156,14 +130,14 @@ std::tuple<at::Tensor, at::Tensor> skinny64(const at::Tensor& x, const at::Tenso
     same_device(x, r);
     rp = cbp(r);
     ldr = r.stride(0);
-    // row partials per 1024 columns (reduce launch) or per 128-column block (in-kernel combine)
-    ssq = at::empty({M, cp ? N / 128 : (N + 1023) / 1024}, x.options().dtype(at::kFloat));
+    // row partials per 1024 columns (written by the reduce launch)
+    ssq = at::empty({M, (N + 1023) / 1024}, x.options().dtype(at::kFloat));
   }
   float* sqo = ssq.defined() ? ssq.data_ptr<float>() : nullptr;
   launch_m64_gemm(cbp(x), x.stride(0), cbp(w), tiled ? K : w.stride(0), bp(y), y.stride(0),
                   S > 1 ? ws.data_ptr<float>() : nullptr, (int)M, (int)N, (int)K, S, false, sq, nbp,
-                  static_cast<float>(eps), tiled, st, cp, rp, ldr, sqo);
-  if (S > 1 && !cp)
+                  static_cast<float>(eps), tiled, st);
+  if (S > 1)
     launch_m64_reduce(ws.data_ptr<float>(), S, (int)M, (int)N, bp(y), y.stride(0), rp, ldr, sq, nbp,
                       (int)K, static_cast<float>(eps), sqo, st);
   return {y, ssq};
@@ -330,8 +304,7 @@ std::tuple<at::Tensor, at::Tensor> skinny_fused_f8(const at::Tensor& x, const at
 // plain [gate; up] row order, norm weight folded in). Same epilogue contract as skinny64.
 std::tuple<at::Tensor, at::Tensor> skinny64_f8(const at::Tensor& x, const at::Tensor& w8, const at::Tensor& wscale,
                                                const c10::optional<at::Tensor>& res,
-                                               const c10::optional<at::Tensor>& ssq_in, double eps, bool glu,
-                                               const c10::optional<at::Tensor>& cnt) {
+                                               const c10::optional<at::Tensor>& ssq_in, double eps, bool glu) {
   check_bf16(x, "x");
   int64_t N = 0, K = 0;
   check_w8(w8, wscale, x, &N, &K);
@@ -370,7 +343,6 @@ std::tuple<at::Tensor, at::Tensor> skinny64_f8(const at::Tensor& x, const at::Te
   auto y = at::empty({M, N}, x.options());
   at::Tensor ws;
   if (S > 1) ws = at::empty({S, M, N}, x.options().dtype(at::kFloat));
-  unsigned* cp = S > 1 ? m64_counters(cnt, x, N) : nullptr;
   const bf16_t* rp = nullptr;
   int64_t ldr = 0;
   at::Tensor ssq;
@@ -381,12 +353,12 @@ std::tuple<at::Tensor, at::Tensor> skinny64_f8(const at::Tensor& x, const at::Te
     same_device(x, r);
     rp = cbp(r);
     ldr = r.stride(0);
-    ssq = at::empty({M, cp ? N / 128 : (N + 1023) / 1024}, x.options().dtype(at::kFloat));
+    ssq = at::empty({M, (N + 1023) / 1024}, x.options().dtype(at::kFloat));
   }
   float* sqo = ssq.defined() ? ssq.data_ptr<float>() : nullptr;
   launch_m64_gemm_f8(cbp(x), x.stride(0), wp, bp(y), y.stride(0), S > 1 ? ws.data_ptr<float>() : nullptr, (int)M,
-                     (int)N, (int)K, S, false, sq, nbp, static_cast<float>(eps), wsc, st, cp, rp, ldr, sqo);
-  if (S > 1 && !cp)
+                     (int)N, (int)K, S, false, sq, nbp, static_cast<float>(eps), wsc, st);
+  if (S > 1)
     launch_m64_reduce(ws.data_ptr<float>(), S, (int)M, (int)N, bp(y), y.stride(0), rp, ldr, sq, nbp, (int)K,
                       static_cast<float>(eps), sqo, st);
   return {y, ssq};
@@ -754,186 +726,6 @@ at::Tensor decode_attn_rope(const at::Tensor& qkv, const at::Tensor& cos, const 
   return out;
 }
 
-// Fused decode qkv projection + attention (decode.hip decode_qkv_attn_kernel, B <= 16): s [B, H]
-// the residual stream, ssq [16, nbp] its row-norm partials, wt the tiled qkv weight with the
-// RMSNorm weight folded in ([N/16, H/32, 4, 16, 8]); then the decode attention of the newest token
-// with its rope + cache write. sync_cnt: this layer's arrival counter (int32, zeroed by the cache
-// at prefill), len_first: kv_len of the first decode step, err: sticky wait-timeout word.
-// Returns the attention output [B, Hq, D], or an undefined tensor when the shape is outside the
-// fused kernel (the caller runs the two launches).
-at::Tensor decode_qkv_attn(const at::Tensor& s, const at::Tensor& ssq, const at::Tensor& wt, double eps,
-                           const at::Tensor& cos, const at::Tensor& sin, const at::Tensor& pos,
-                           at::Tensor& k_cache, at::Tensor& v_cache, const at::Tensor& slot,
-                           const at::Tensor& kv_len, const c10::optional<at::Tensor>& kv_start,
-                           int64_t window, double scale, int64_t Hq, int64_t Hkv, int64_t D, int64_t rot,
-                           at::Tensor& sync_cnt, const at::Tensor& len_first, at::Tensor& err) {
-  check_bf16(s, "s");
-  check_bf16(wt, "wt");
-  check_bf16(k_cache, "k_cache");
-  check_bf16(v_cache, "v_cache");
-  check_f32(cos, "cos");
-  check_f32(sin, "sin");
-  check_i32(pos, "pos");
-  check_i32(kv_len, "kv_len");
-  check_i32(sync_cnt, "sync_cnt");
-  check_i32(len_first, "len_first");
-  check_i32(err, "err");
-  check_cuda(slot, "slot");
-  TORCH_CHECK(slot.scalar_type() == at::kLong && slot.numel() >= 1, "slot int64");
-  TORCH_CHECK(ssq.scalar_type() == at::kFloat && ssq.dim() == 2 && ssq.size(0) == 16 && ssq.is_contiguous() &&
-                  ssq.size(1) >= 1 && ssq.size(1) <= 512,
-              "ssq fp32 [16, nbp <= 512] contiguous");
-  TORCH_CHECK(wt.dim() == 5 && wt.size(2) == 4 && wt.size(3) == 16 && wt.size(4) == 8 && wt.is_contiguous(),
-              "wt tiled [N/16, K/32, 4, 16, 8]");
-  const int64_t M = s.size(0), N = wt.size(0) * 16, K = wt.size(1) * 32;
-  TORCH_CHECK(s.dim() == 2 && s.size(1) == K && s.stride(1) == 1 && s.stride(0) % 8 == 0 && M >= 1 && M <= 16,
-              "s [B <= 16, K] with 16-byte aligned rows");
-  TORCH_CHECK(N == (Hq + 2 * Hkv) * D, "qkv weight rows must be (Hq + 2 Hkv) * D");
-  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(0) == M && k_cache.size(2) == Hkv && k_cache.size(3) == D &&
-                  k_cache.sizes() == v_cache.sizes() && k_cache.strides() == v_cache.strides() &&
-                  k_cache.stride(3) == 1 && k_cache.stride(1) % 8 == 0 && k_cache.stride(2) % 8 == 0 &&
-                  k_cache.stride(0) % 8 == 0,
-              "caches [B, Tmax, Hkv, D], 16-byte aligned rows");
-  TORCH_CHECK(rot % 16 == 0 && rot <= D && rot > 0, "rot % 16 == 0, 0 < rot <= D");
-  TORCH_CHECK(cos.is_contiguous() && sin.is_contiguous() && cos.size(-1) == rot / 2, "rope tables");
-  TORCH_CHECK(pos.numel() == M && pos.is_contiguous(), "pos [B]");
-  TORCH_CHECK(sync_cnt.numel() >= 8 * 32 && sync_cnt.is_contiguous() && len_first.numel() >= 1 &&
-                  err.numel() >= 1,
-              "sync words (sync_cnt: 8 counter replicas x 32 ints)");
-  check_aligned16(s, "s");
-  check_aligned16(wt, "wt");
-  check_aligned16(k_cache, "k_cache");
-  check_aligned16(v_cache, "v_cache");
-  const int* ks = nullptr;
-  if (kv_start && kv_start->defined()) {
-    check_i32(*kv_start, "kv_start");
-    TORCH_CHECK(kv_start->numel() == M && kv_start->is_contiguous(), "kv_start [B]");
-    ks = kv_start->data_ptr<int>();
-  }
-  const int64_t G = Hq / Hkv;
-  TORCH_CHECK(skinny_use_ksplit((int)N, (int)K) && Hq % Hkv == 0 && (G == 1 || G == 2 || G == 4 || G == 8) &&
-                  (D == 64 || D == 128),
-              "decode_qkv_attn: N < 16384, N % 16 == 0, K % 1024 == 0, GQA group 1/2/4/8, head_dim 64/128");
-  c10::hip::HIPGuardMasqueradingAsCUDA g(s.device());
-  const int64_t Tmax = k_cache.size(1);
-  const int nsplit = decode_qkv_attn_splits((int)Tmax, (int)M, (int)Hkv);
-  TORCH_CHECK(nsplit <= 8, "decode_qkv_attn: more than 8 key splits (use the two-launch path)");
-  int* ccnt = nsplit > 1 ? decode_counters(s, M * Hkv) : nullptr;
-  TORCH_CHECK(nsplit == 1 || ccnt != nullptr,
-              "decode_qkv_attn: split-combine counters unavailable (first call inside a capture, or "
-              "DLA_DECODE_FUSED_COMBINE=0)");
-  KsFuse fz{};
-  fz.ssq_in = ssq.data_ptr<float>();
-  fz.nbp = static_cast<int>(ssq.size(1));
-  fz.eps = static_cast<float>(eps);
-  auto qkv = at::empty({M, N}, s.options());
-  auto fopt = s.options().dtype(at::kFloat);
-  auto part_o = at::empty({M, Hq, nsplit, D}, fopt);
-  auto part_ml = at::empty({M, Hq, nsplit, 2}, fopt);
-  auto out = at::empty({M, Hq, D}, s.options());
-  const bool ok = launch_decode_qkv_attn(
-      cbp(s), s.stride(0), cbp(wt), bp(qkv), qkv.stride(0), (int)M, (int)N, (int)K, fz,
-      cos.data_ptr<float>(), sin.data_ptr<float>(), pos.data_ptr<int>(), slot.data_ptr<int64_t>(), (int)rot,
-      bp(k_cache), bp(v_cache), k_cache.stride(0), k_cache.stride(1), k_cache.stride(2),
-      kv_len.data_ptr<int>(), ks, static_cast<int>(window), static_cast<float>(scale * 1.4426950408889634),
-      (int)Hq, (int)Hkv, (int)D, (int)Tmax, part_o.data_ptr<float>(), part_ml.data_ptr<float>(), bp(out),
-      out.stride(0), out.stride(1), ccnt, sync_cnt.data_ptr<int>(), len_first.data_ptr<int>(),
-      err.data_ptr<int>(), cur_stream(s));
-  TORCH_CHECK(ok, "decode_qkv_attn: shape outside the fused kernel (more attention units than "
-                  "resident workgroups)");
-  const hipError_t le = hipGetLastError();
-  TORCH_CHECK(le == hipSuccess, "decode_qkv_attn launch: ", hipGetErrorString(le));
-  return out;
-}
-
-// 17..64 decode rows: the qkv projection's split-K slabs (no reduce launch) ...
-at::Tensor skinny64_slabs(const at::Tensor& x, const at::Tensor& w) {
-  check_bf16(x, "x");
-  check_bf16(w, "w");
-  TORCH_CHECK(w.dim() == 5 && w.size(2) == 4 && w.size(3) == 16 && w.size(4) == 8 && w.is_contiguous(),
-              "w tiled [N/16, K/32, 4, 16, 8]");
-  const int64_t M = x.size(0), N = w.size(0) * 16, K = w.size(1) * 32;
-  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0 && x.size(1) == K && M >= 1 && M <= 64,
-              "x [M <= 64, K]");
-  TORCH_CHECK(m64_shape_ok((int)N, (int)K, false), "skinny64: K % 256 == 0 and N % 128 == 0");
-  check_aligned16(x, "x");
-  check_aligned16(w, "w");
-  same_device(x, w);
-  const int S = m64_splits((int)N, (int)K);
-  TORCH_CHECK(S > 1, "skinny64_slabs: the shape has no split-K");
-  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
-  auto ws = at::empty({S, M, N}, x.options().dtype(at::kFloat));
-  launch_m64_gemm(cbp(x), x.stride(0), cbp(w), K, nullptr, 0, ws.data_ptr<float>(), (int)M, (int)N, (int)K, S,
-                  false, nullptr, 0, 0.f, true, cur_stream(x));
-  const hipError_t le = hipGetLastError();
-  TORCH_CHECK(le == hipSuccess, "skinny64_slabs launch: ", hipGetErrorString(le));
-  return ws;
-}
-
-// ... reduced (rstd x sum in split order, exactly the reduce launch's arithmetic) inside the
-// decode attention launch (decode.hip decode_attn_slab_kernel), rope + cache write fused as in
-// decode_attn_rope. ws [S, B, (Hq + 2 Hkv) D], ssq [B, nbp] the input rows' partials.
-at::Tensor decode_attn_rope_slab(const at::Tensor& ws, const at::Tensor& ssq, double eps, int64_t knorm,
-                                 const at::Tensor& cos,
-                                 const at::Tensor& sin, const at::Tensor& pos, at::Tensor& k_cache,
-                                 at::Tensor& v_cache, const at::Tensor& slot, const at::Tensor& kv_len,
-                                 const c10::optional<at::Tensor>& kv_start, int64_t window, double scale,
-                                 int64_t Hq, int64_t Hkv, int64_t D, int64_t rot) {
-  check_f32(ws, "ws");
-  check_f32(ssq, "ssq");
-  check_bf16(k_cache, "k_cache");
-  check_bf16(v_cache, "v_cache");
-  check_f32(cos, "cos");
-  check_f32(sin, "sin");
-  check_i32(pos, "pos");
-  check_i32(kv_len, "kv_len");
-  check_cuda(slot, "slot");
-  TORCH_CHECK(slot.scalar_type() == at::kLong && slot.numel() >= 1, "slot int64");
-  TORCH_CHECK(ws.dim() == 3 && ws.is_contiguous(), "ws [S, B, N] contiguous");
-  const int64_t S = ws.size(0), B = ws.size(1), N = ws.size(2);
-  TORCH_CHECK(N == (Hq + 2 * Hkv) * D, "ws width must be (Hq + 2 Hkv) * D");
-  TORCH_CHECK(ssq.dim() == 2 && ssq.size(0) == B && ssq.is_contiguous() && ssq.size(1) >= 1, "ssq [B, nbp]");
-  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(0) == B && k_cache.size(2) == Hkv && k_cache.size(3) == D &&
-                  k_cache.sizes() == v_cache.sizes() && k_cache.strides() == v_cache.strides() &&
-                  k_cache.stride(3) == 1 && k_cache.stride(1) % 8 == 0 && k_cache.stride(2) % 8 == 0 &&
-                  k_cache.stride(0) % 8 == 0,
-              "caches [B, Tmax, Hkv, D], 16-byte aligned rows");
-  TORCH_CHECK(D == 64 || D == 128, "decode attention supports head_dim 64 or 128");
-  TORCH_CHECK(Hq % Hkv == 0, "Hq % Hkv");
-  const int64_t G = Hq / Hkv;
-  TORCH_CHECK(G == 1 || G == 2 || G == 4 || G == 8, "GQA group size must be 1, 2, 4 or 8");
-  TORCH_CHECK(rot % 16 == 0 && rot <= D && rot > 0, "rot % 16 == 0, 0 < rot <= D");
-  TORCH_CHECK(cos.is_contiguous() && sin.is_contiguous() && cos.size(-1) == rot / 2, "rope tables");
-  TORCH_CHECK(pos.numel() == B && pos.is_contiguous(), "pos [B]");
-  check_aligned16(k_cache, "k_cache");
-  check_aligned16(v_cache, "v_cache");
-  const int* ks = nullptr;
-  if (kv_start && kv_start->defined()) {
-    check_i32(*kv_start, "kv_start");
-    TORCH_CHECK(kv_start->numel() == B && kv_start->is_contiguous(), "kv_start [B]");
-    ks = kv_start->data_ptr<int>();
-  }
-  c10::hip::HIPGuardMasqueradingAsCUDA g(ws.device());
-  const int64_t Tmax = k_cache.size(1);
-  const int nsplit = decode_attn_slab_splits((int)Tmax, (int)B, (int)Hkv);
-  auto fopt = ws.options();
-  auto part_o = at::empty({B, Hq, nsplit, D}, fopt);
-  auto part_ml = at::empty({B, Hq, nsplit, 2}, fopt);
-  auto out = at::empty({B, Hq, D}, k_cache.options());
-  launch_decode_attn_slab(ws.data_ptr<float>(), (int)S, (int)N, ssq.data_ptr<float>(), (int)ssq.size(1),
-                          (int)knorm, static_cast<float>(eps),
-                          cos.data_ptr<float>(), sin.data_ptr<float>(), pos.data_ptr<int>(),
-                          slot.data_ptr<int64_t>(), (int)rot, bp(k_cache), bp(v_cache), k_cache.stride(0),
-                          k_cache.stride(1), k_cache.stride(2), kv_len.data_ptr<int>(), ks,
-                          static_cast<int>(window), static_cast<float>(scale * 1.4426950408889634), (int)B,
-                          (int)Hq, (int)Hkv, (int)D, (int)Tmax, part_o.data_ptr<float>(),
-                          part_ml.data_ptr<float>(), bp(out), out.stride(0), out.stride(1),
-                          decode_counters(ws, B * Hkv), cur_stream(ws));
-  const hipError_t le = hipGetLastError();
-  TORCH_CHECK(le == hipSuccess, "decode_attn_rope_slab launch: ", hipGetErrorString(le));
-  return out;
-}
-
 at::Tensor sample_tokens(const at::Tensor& logits, double temperature, int64_t top_k,
                          double top_p, bool greedy, const at::Tensor& rng) {
   check_cuda(logits, "logits");
@@ -964,144 +756,29 @@ at::Tensor sample_tokens(const at::Tensor& logits, double temperature, int64_t t
   return out;
 }
 
-static at::Tensor& tail_stamp_buffer() {
-  static at::Tensor t;
-  return t;
-}
-
-at::Tensor decode_tail_stamps(const at::Tensor& like) {
-  (void)like;
-  return tail_stamp_buffer().defined() ? tail_stamp_buffer().clone() : at::Tensor();
-}
-
-// Persistent decode layer tail (decode_tail.hip, B <= 16): o projection + residual, gate|up +
-// SwiGLU, down + residual [+ the next layer's qkv projection] in ONE launch. Weights in the tiled
-// layout [N/16, K/32, 4, 16, 8] (wgu: gate / up rows interleaved 8 + 8, ln2 folded; wq: the next
-// layer's ln1 folded). Returns (x_out [M, H], its row partials [16, H/16], qkv [M, Nq] or empty).
-static void check_tiled(const at::Tensor& w, const char* name) {
-  check_bf16(w, name);
-  TORCH_CHECK(w.dim() == 5 && w.size(2) == 4 && w.size(3) == 16 && w.size(4) == 8 && w.is_contiguous(), name,
-              ": tiled [N/16, K/32, 4, 16, 8]");
-  check_aligned16(w, name);
-}
-
-std::tuple<at::Tensor, at::Tensor, at::Tensor> decode_tail(
-    const at::Tensor& a, const at::Tensor& x, const at::Tensor& wo, const at::Tensor& wgu, const at::Tensor& wd,
-    const c10::optional<at::Tensor>& wq, double eps, at::Tensor& cnt, const at::Tensor& kv_len,
-    const at::Tensor& len_first, at::Tensor& err) {
-  check_bf16(a, "a");
-  check_bf16(x, "x");
-  check_tiled(wo, "wo");
-  check_tiled(wgu, "wgu");
-  check_tiled(wd, "wd");
-  const int64_t M = x.size(0), H = x.size(1), Ko = a.size(1);
-  TORCH_CHECK(a.dim() == 2 && x.dim() == 2 && a.size(0) == M && a.stride(1) == 1 && x.stride(1) == 1 &&
-                  a.stride(0) % 8 == 0 && x.stride(0) % 8 == 0 && M >= 1 && M <= 16,
-              "decode_tail: a [M, Ko], x [M, H], 1 <= M <= 16, 16-byte aligned rows");
-  check_aligned16(a, "a");
-  check_aligned16(x, "x");
-  const int64_t F = wd.size(1) * 32;
-  TORCH_CHECK(wo.size(0) * 16 == H && wo.size(1) * 32 == Ko && wgu.size(0) * 16 == 2 * F && wgu.size(1) * 32 == H &&
-                  wd.size(0) * 16 == H,
-              "decode_tail: weight shapes (o [H, Ko], gate|up [2F, H], down [H, F])");
-  int64_t Nq = 0;
-  if (wq.has_value()) {
-    check_tiled(*wq, "wq");
-    TORCH_CHECK(wq->size(1) * 32 == H, "decode_tail: wq [Nq, H]");
-    Nq = wq->size(0) * 16;
-  }
-  TORCH_CHECK(cnt.scalar_type() == at::kInt && cnt.is_contiguous() && cnt.numel() >= 3 * 8 * 32 &&
-                  kv_len.scalar_type() == at::kInt && len_first.scalar_type() == at::kInt &&
-                  err.scalar_type() == at::kInt,
-              "decode_tail: int32 cnt [>= 768], kv_len, len_first, err");
-  same_device(x, a);
-  same_device(x, wo);
-  same_device(x, cnt);
-  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
-  auto s = at::empty({M, H}, x.options());
-  auto m = at::empty({M, F}, x.options());
-  auto xo = at::empty({M, H}, x.options());
-  auto fopt = x.options().dtype(at::kFloat);
-  auto ssq_s = at::empty({16, H / 16}, fopt);
-  auto ssq_x = at::empty({16, H / 16}, fopt);
-  at::Tensor qkv = Nq ? at::empty({M, Nq}, x.options()) : at::Tensor();
-  TailArgs A{};
-  A.a = cbp(a);
-  A.lda = a.stride(0);
-  A.x = cbp(x);
-  A.ldx = x.stride(0);
-  A.Wo = cbp(wo);
-  A.Wgu = cbp(wgu);
-  A.Wd = cbp(wd);
-  A.Wq = Nq ? cbp(*wq) : nullptr;
-  A.s = bp(s);
-  A.ssq_s = ssq_s.data_ptr<float>();
-  A.m = bp(m);
-  A.xo = bp(xo);
-  A.ssq_x = ssq_x.data_ptr<float>();
-  A.qkv = Nq ? bp(qkv) : nullptr;
-  A.M = (int)M;
-  A.H = (int)H;
-  A.Ko = (int)Ko;
-  A.F = (int)F;
-  A.Nq = (int)Nq;
-  A.eps = static_cast<float>(eps);
-  A.cnt = cnt.data_ptr<int>();
-  A.kv_len = kv_len.data_ptr<int>();
-  A.len_first = len_first.data_ptr<int>();
-  A.err = err.data_ptr<int>();
-  // DLA_TAIL_STAMPS=1 (debug): per-workgroup phase-edge timestamps into a process-wide buffer,
-  // read back with decode_tail_stamps()
-  static const bool stamps_on = [] {
-    const char* e = std::getenv("DLA_TAIL_STAMPS");
-    return e && std::atoi(e) != 0;
-  }();
-  if (stamps_on) {
-    static at::Tensor buf;
-    if (!buf.defined() || buf.device() != x.device())
-      buf = at::zeros({1024, 8}, x.options().dtype(at::kLong));
-    tail_stamp_buffer() = buf;
-    A.stamps = reinterpret_cast<unsigned long long*>(buf.data_ptr<int64_t>());
-  }
-  const bool ok = launch_decode_tail(A, cur_stream(x));
-  TORCH_CHECK(ok, "decode_tail: shape outside the persistent kernel (M <= 16, H / Ko / F % 1024 == 0, "
-                  "x staged in LDS) or no resident workgroup per CU");
-  const hipError_t le = hipGetLastError();
-  TORCH_CHECK(le == hipSuccess, "decode_tail launch: ", hipGetErrorString(le));
-  return {xo, ssq_x, qkv};
-}
-
 }  // namespace dla
 
 TORCH_LIBRARY_FRAGMENT(dla, m) {
   m.def("decode_attn(Tensor q, Tensor k_cache, Tensor v_cache, Tensor kv_len, Tensor? kv_start, int window, float scale) -> Tensor");
   m.def("rope_cache_write(Tensor qkv, Tensor cos, Tensor sin, Tensor pos, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor slot, int Hq, int Hkv, int D, int rot) -> Tensor");
   m.def("decode_attn_rope(Tensor qkv, Tensor cos, Tensor sin, Tensor pos, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor slot, Tensor kv_len, Tensor? kv_start, int window, float scale, int Hq, int Hkv, int D, int rot) -> Tensor");
-  m.def("decode_qkv_attn(Tensor s, Tensor ssq, Tensor wt, float eps, Tensor cos, Tensor sin, Tensor pos, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor slot, Tensor kv_len, Tensor? kv_start, int window, float scale, int Hq, int Hkv, int D, int rot, Tensor(c!) sync_cnt, Tensor len_first, Tensor(d!) err) -> Tensor");
-  m.def("skinny64_slabs(Tensor x, Tensor w) -> Tensor");
-  m.def("decode_attn_rope_slab(Tensor ws, Tensor ssq, float eps, int knorm, Tensor cos, Tensor sin, Tensor pos, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor slot, Tensor kv_len, Tensor? kv_start, int window, float scale, int Hq, int Hkv, int D, int rot) -> Tensor");
   m.def("sample_tokens(Tensor logits, float temperature, int top_k, float top_p, bool greedy, Tensor rng) -> Tensor");
   m.def("skinny_gemm(Tensor x, Tensor w, Tensor(a!) counters, bool swiglu, bool glu_out=False) -> Tensor");
   m.def("skinny_glu_norm(Tensor x, Tensor res, Tensor norm_w, float eps, Tensor w) -> (Tensor, Tensor)");
   m.def("skinny_glu_ks(Tensor x, Tensor w) -> Tensor");
   m.def("skinny_fused(Tensor x, Tensor w, Tensor? res, Tensor? ssq_in, float eps, bool glu) -> (Tensor, Tensor)");
-  m.def("skinny64(Tensor x, Tensor w, Tensor? res, Tensor? ssq_in, float eps, bool glu, Tensor? cnt=None) -> (Tensor, Tensor)");
-  m.def("skinny64_f8(Tensor x, Tensor w8, Tensor wscale, Tensor? res, Tensor? ssq_in, float eps, bool glu, Tensor? cnt=None) -> (Tensor, Tensor)");
+  m.def("skinny64(Tensor x, Tensor w, Tensor? res, Tensor? ssq_in, float eps, bool glu) -> (Tensor, Tensor)");
+  m.def("skinny64_f8(Tensor x, Tensor w8, Tensor wscale, Tensor? res, Tensor? ssq_in, float eps, bool glu) -> (Tensor, Tensor)");
   m.def("tile_weight(Tensor w, Tensor? nw, Tensor(a!) out, bool glu_il=False) -> ()");
   m.def("quant_tile_f8(Tensor w, Tensor? nw, Tensor(a!) out8, Tensor(b!) scale, bool glu_il=False) -> ()");
   m.def("skinny_glu_il(Tensor x, Tensor wt, Tensor ssq_in, float eps) -> Tensor");
   m.def("skinny_fused_f8(Tensor x, Tensor w8, Tensor wscale, Tensor? res, Tensor? ssq_in, float eps) -> (Tensor, Tensor)");
   m.def("skinny_glu_il_f8(Tensor x, Tensor w8, Tensor wscale, Tensor ssq_in, float eps) -> Tensor");
-  m.def("decode_tail_stamps(Tensor like) -> Tensor");
-  m.def("decode_tail(Tensor a, Tensor x, Tensor wo, Tensor wgu, Tensor wd, Tensor? wq, float eps, Tensor(a!) cnt, Tensor kv_len, Tensor len_first, Tensor(b!) err) -> (Tensor, Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(dla, CUDA, m) {
   m.impl("decode_attn", &dla::decode_attn);
   m.impl("sample_tokens", &dla::sample_tokens);
-  m.impl("decode_qkv_attn", &dla::decode_qkv_attn);
-  m.impl("skinny64_slabs", &dla::skinny64_slabs);
-  m.impl("decode_attn_rope_slab", &dla::decode_attn_rope_slab);
   m.impl("rope_cache_write", &dla::rope_cache_write);
   m.impl("decode_attn_rope", &dla::decode_attn_rope);
   m.impl("skinny_gemm", &dla::skinny_gemm);
@@ -1115,6 +792,4 @@ TORCH_LIBRARY_IMPL(dla, CUDA, m) {
   m.impl("skinny_glu_il", &dla::skinny_glu_il);
   m.impl("skinny_fused_f8", &dla::skinny_fused_f8);
   m.impl("skinny_glu_il_f8", &dla::skinny_glu_il_f8);
-  m.impl("decode_tail", &dla::decode_tail);
-  m.impl("decode_tail_stamps", &dla::decode_tail_stamps);
 }

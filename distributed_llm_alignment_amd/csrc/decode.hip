@@ -15,7 +15,7 @@
 #include <cstdlib>
 
 #include "common.h"
-#include "skinny_ks.h"
+
 
 namespace dla {
 
@@ -418,13 +418,9 @@ __device__ __forceinline__ void dec_glds16(const void* src, void* lds_base) {
                                    (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
 }
 
-// The loop kernel's body, shared with the fused qkv-projection + attention kernel below. WAITQ:
-// the qkv row of the newest token (q, k, v) is produced by other workgroups of the same launch;
-// the body issues every load that does not depend on it (the first two chunks' K / V), then
-// calls wait() and only then reads q and writes the newest K / V into the cache.
-// EARLYK: chunk c + RD's K loads leave right after chunk c's scores (the registers they refill are
-// free from there) instead of with its V refill after P.V
-template <int D, int G, bool ROPE, bool WAITQ = false, int RD = 2, bool EARLYK = false, class Wait>
+// The loop kernel's body: a block streams chunks [cbeg, cend) of one (split, kv head, sequence)
+// through a 2-deep K / V ring.
+template <int D, int G, bool ROPE>
 __device__ __forceinline__ void dec_loop_body(
     const int split, const int hk, const int b, const int Hkv_grid,
     const bf16_t* __restrict__ q, int64_t q_sb, int64_t q_sh,
@@ -432,8 +428,7 @@ __device__ __forceinline__ void dec_loop_body(
     int64_t c_sb, int64_t c_st, int64_t c_sh, const int* __restrict__ kv_len,
     const int* __restrict__ kv_start, int window, float scale_log2, int nsplit, int cpb,
     float* __restrict__ part_o, float* __restrict__ part_ml, int Hq, const DecRope& rp,
-    bf16_t* __restrict__ out, int64_t o_sb, int64_t o_sh, int* __restrict__ cnt, int Tcap,
-    Wait&& wait, const bf16_t* qkv_lds = nullptr) {
+    bf16_t* __restrict__ out, int64_t o_sb, int64_t o_sh, int* __restrict__ cnt, int Tcap) {
   // out != nullptr, cnt == nullptr (one split per sequence): the block writes the normalised bf16
   // output itself; out and cnt (nsplit > 1): partials + in-kernel combine (dec_arrive_combine).
   // Either way the combine launch is skipped.
@@ -441,9 +436,8 @@ __device__ __forceinline__ void dec_loop_body(
   constexpr int KST = D / 32;
   static_assert(G <= 16 && KPW == 32, "decode tile geometry");
   static_assert(G * D * 4 <= KPW * D * 2, "acc_s aliases one V image slot");
-  static_assert(!WAITQ || ROPE, "the fused qkv form reads the raw qkv row");
   // per wave: 2 V image slots (LDS-DMA ring), the first re-used for the wave's partial O
-  static_assert(RD >= 1 && RD <= 3, "ring depth");
+  constexpr int RD = 2;
   __shared__ __attribute__((aligned(16))) bf16_t vimg[4][RD][KPW * D];
   __shared__ float mls[4][G][2];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -452,8 +446,7 @@ __device__ __forceinline__ void dec_loop_body(
   const int sub = lane / LPK, dl = (lane % LPK) * 8;
   const int r16 = lane & 15, kg = lane >> 4;
   int newest = -1;
-  // this block's q heads, k and v of the newest token: a row of the qkv projection, or (qkv_lds)
-  // the block's [G + 2][D] slice staged in LDS by wait()
+  // this block's q heads, k and v of the newest token: a row of the qkv projection
   const bf16_t *qh = nullptr, *kh = nullptr, *vh = nullptr;
   const float *cs = nullptr, *sn = nullptr;
   const int cfirst = split * cpb;
@@ -470,20 +463,14 @@ __device__ __forceinline__ void dec_loop_body(
   };
   if constexpr (ROPE) {
     newest = static_cast<int>(rp.slot[0]);
-    if (qkv_lds != nullptr) {
-      qh = qkv_lds;
-      kh = qkv_lds + G * D;
-      vh = qkv_lds + (G + 1) * D;
-    } else {
-      const bf16_t* qrow = rp.qkv + (int64_t)b * rp.ld;
-      qh = qrow + (int64_t)(hk * G) * D;
-      kh = qrow + (int64_t)(Hq + hk) * D;
-      vh = qrow + (int64_t)(Hq + rp.Hkv + hk) * D;
-    }
+    const bf16_t* qrow = rp.qkv + (int64_t)b * rp.ld;
+    qh = qrow + (int64_t)(hk * G) * D;
+    kh = qrow + (int64_t)(Hq + hk) * D;
+    vh = qrow + (int64_t)(Hq + rp.Hkv + hk) * D;
     const int half = rp.rot >> 1;
     cs = rp.cos_t + (int64_t)rp.pos[b] * half;
     sn = rp.sin_t + (int64_t)rp.pos[b] * half;
-    if constexpr (!WAITQ) cache_write();
+    cache_write();
   }
   const bf16_t* kb0 = kc + (int64_t)b * c_sb + (int64_t)hk * c_sh;
   const bf16_t* vb0 = vc + (int64_t)b * c_sb + (int64_t)hk * c_sh;
@@ -518,7 +505,6 @@ __device__ __forceinline__ void dec_loop_body(
   const int64_t obase = (int64_t)b * o_sb + (int64_t)hk * G * o_sh;
   if (cbeg >= cend || max(cbeg * kDecChunk, lo) >= len) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the speculative K loads
-    if constexpr (WAITQ) wait();  // once on every path, before any other barrier of the block
     if (out != nullptr && !fuse) {  // no visible key: zeros, as the combine writes for an all-empty row
       for (int i = tid; i < G * D; i += 256)
         out[(int64_t)b * o_sb + (int64_t)(hk * G + i / D) * o_sh + i % D] = 0;
@@ -531,22 +517,18 @@ __device__ __forceinline__ void dec_loop_body(
     if (fuse) dec_arrive_combine<D, G>(cslot, part_o, part_ml, pbase0, nsplit, out, obase, o_sh);
     return;
   }
-  // q fragments (unfused: first, the oldest loads: S of chunk 0 waits for them and K(0) only;
-  // WAITQ: after the chunk prefetch and the wait)
+  // q fragments first, the oldest loads: S of chunk 0 waits for them and K(0) only
   s16x8 qf[KST];
-  auto load_q = [&]() {
 #pragma unroll
-    for (int s = 0; s < KST; ++s) {
-      qf[s] = s16x8{};
-      if (r16 < G) {
-        if constexpr (ROPE)
-          qf[s] = __builtin_bit_cast(s16x8, dec_rope8(qh + (int64_t)r16 * D, 32 * s + 8 * kg, rp.rot, cs, sn));
-        else
-          qf[s] = __builtin_bit_cast(s16x8, load_bf16x8(q + (int64_t)b * q_sb + (int64_t)(hk * G + r16) * q_sh + 32 * s + 8 * kg));
-      }
+  for (int s = 0; s < KST; ++s) {
+    qf[s] = s16x8{};
+    if (r16 < G) {
+      if constexpr (ROPE)
+        qf[s] = __builtin_bit_cast(s16x8, dec_rope8(qh + (int64_t)r16 * D, 32 * s + 8 * kg, rp.rot, cs, sn));
+      else
+        qf[s] = __builtin_bit_cast(s16x8, load_bf16x8(q + (int64_t)b * q_sb + (int64_t)(hk * G + r16) * q_sh + 32 * s + 8 * kg));
     }
-  };
-  if constexpr (!WAITQ) load_q();
+  }
   auto loadV = [&](auto J, int c) {
     constexpr int j = decltype(J)::value;
     const int base = c * kDecChunk, k0 = max(base, lo), k1 = min(base + kDecChunk, len);
@@ -592,8 +574,6 @@ __device__ __forceinline__ void dec_loop_body(
 #pragma unroll
       for (int s = 0; s < KST; ++s) sacc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[j][t][s], qf[s], sacc[t], 0, 0, 0);
     }
-    const bool kearly = EARLYK && c + RD < cend;
-    if (kearly) loadK(J, c + RD);
     float sc[2][4];
     float mc = -INFINITY;
 #pragma unroll
@@ -632,15 +612,7 @@ __device__ __forceinline__ void dec_loop_body(
     // (chunks issued after c: min(RD - 1, cend - 1 - c); the refill of c + RD comes after this)
     constexpr int PER = 2 * KST + NIT;
     const int nlater = min(RD - 1, cend - 1 - c);
-    if (kearly && nlater == 1) {  // K(c + 1), V(c + 1), then K(c + 2) behind V(c)
-      if constexpr (PER == 16) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
-      else if constexpr (PER == 8) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else if (nlater >= 2) {
-      if constexpr (PER == 16) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
-      else if constexpr (PER == 8) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else if (nlater == 1) {
+    if (nlater == 1) {
       if constexpr (PER == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
       else if constexpr (PER == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -677,27 +649,15 @@ __device__ __forceinline__ void dec_loop_body(
     if (c + RD < cend) {
       // WAR: this slot's transposed reads are complete before the DMA refill is issued
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (kearly) loadV(J, c + RD);
-      else load(J, c + RD);
+      load(J, c + RD);
     }
   };
   if (cbeg != cfirst) loadK(std::integral_constant<int, 0>{}, cbeg);  // left padding: the guess was wrong
   loadV(std::integral_constant<int, 0>{}, cbeg);
-  if constexpr (RD >= 2)
-    if (cbeg + 1 < cend) load(std::integral_constant<int, 1>{}, cbeg + 1);
-  if constexpr (RD >= 3)
-    if (cbeg + 2 < cend) load(std::integral_constant<int, 2>{}, cbeg + 2);
-  if constexpr (WAITQ) {  // every load above is independent of this step's qkv row
-    wait();
-    cache_write();
-    load_q();
-  }
+  if (cbeg + 1 < cend) load(std::integral_constant<int, 1>{}, cbeg + 1);
   for (int c = cbeg; c < cend; c += RD) {
     step(std::integral_constant<int, 0>{}, c);
-    if constexpr (RD >= 2)
-      if (c + 1 < cend) step(std::integral_constant<int, 1>{}, c + 1);
-    if constexpr (RD >= 3)
-      if (c + 2 < cend) step(std::integral_constant<int, 2>{}, c + 2);
+    if (c + 1 < cend) step(std::integral_constant<int, 1>{}, c + 1);
   }
   // this wave's partial O into its own (dead) first image slot
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -740,7 +700,7 @@ __device__ __forceinline__ void dec_loop_body(
   if (fuse) dec_arrive_combine<D, G>(cslot, part_o, part_ml, pbase0, nsplit, out, obase, o_sh);
 }
 
-template <int D, int G, bool ROPE, int RD = 2, bool EARLYK = false>
+template <int D, int G, bool ROPE>
 __global__ __launch_bounds__(256, 2) void decode_attn_loop_kernel(
     const bf16_t* __restrict__ q, int64_t q_sb, int64_t q_sh,
     bf16_t* __restrict__ kc, bf16_t* __restrict__ vc,
@@ -748,224 +708,9 @@ __global__ __launch_bounds__(256, 2) void decode_attn_loop_kernel(
     const int* __restrict__ kv_start, int window, float scale_log2, int nsplit, int cpb,
     float* __restrict__ part_o, float* __restrict__ part_ml, int Hq, DecRope rp,
     bf16_t* __restrict__ out, int64_t o_sb, int64_t o_sh, int* __restrict__ cnt, int Tcap) {
-  dec_loop_body<D, G, ROPE, false, RD, EARLYK>(blockIdx.x, blockIdx.y, blockIdx.z, gridDim.y, q, q_sb, q_sh, kc, vc,
-                            c_sb, c_st, c_sh, kv_len, kv_start, window, scale_log2, nsplit, cpb, part_o,
-                            part_ml, Hq, rp, out, o_sb, o_sh, cnt, Tcap, [] {});
-}
-
-// ---------------------------------------------------------------------------------------------
-// Fused decode qkv projection + attention (B <= 16, the fused decode layer; ops/decode.py
-// `qkv_attend`): ONE launch of exactly as many 512-thread workgroups as fit on the chip at once
-// (one per CU: the host checks the occupancy), each doing two phases:
-//   1. the qkv projection of its share of the 16-column tiles (skinny_ks.h body: RMSNorm folded
-//      into the tiled weight, the row factor from the producer's partials, non-temporal weight
-//      stream), then one agent-scope release and an add of its tile count to a per-layer counter;
-//   2. workgroups [0, na) then run one attention unit each on waves 0-3 (dec_loop_body, a
-//      (split, kv head, sequence) of the multi-chunk decode attention with the in-kernel split
-//      combine). Before phase 1 such a workgroup issues every load that does not depend on this
-//      step's q / k / v -- the first two 128-key chunks of its K (registers) and V (LDS-DMA) --
-//      so the KV-cache stream overlaps the qkv weight stream; after phase 1 one lane polls the
-//      counter (s_sleep) until every tile of this step has arrived, takes one agent-scope acquire,
-//      and only then are q read (rotated) and the newest K / V written into the cache.
-// The tiles are dealt so the work evens out: an attention workgroup takes `ta` tiles, the others
-// `tn`. Two dependent launches with their ramp / tail become one, and no CU idles behind an
-// uneven tile count. The counter is monotonic within a generation: step k of the decode
-// (kv_len = len_first + k - 1) waits for nq * k arrivals; the cache zeroes it and sets len_first
-// when a prompt is prefilled. Every workgroup is resident at once (one per CU), so the waits
-// cannot deadlock; a wait beyond ~2^22 polls (far past any real step) sets `err` and proceeds
-// rather than hanging the GPU. Barrier discipline: phase 1 runs on all 8 waves with the same
-// barrier sequence whichever call site reaches it, and waves 4-7 exit only after it.
-constexpr int kQaRep = 8;       // arrival-counter replicas (pollers per cache line / 8)
-constexpr int kQaRepStride = 32;  // ints between replicas: one 128-byte line each
-
-// 16-byte load that bypasses the CU's vector L1 and reads device-coherent data (`sc1`): the
-// consumer side of the write-through hand-off (global_, never flat_; waits for itself)
-__device__ __forceinline__ bf16x8 load_sc1_16(const bf16_t* p) {
-  typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
-  u32x4v v;
-  asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
-  return __builtin_bit_cast(bf16x8, v);
-}
-
-struct DecQkvSync {
-  int* cnt;              // this layer's arrival counter, kQaRep replicas kQaRepStride ints apart
-  const int* len_first;  // kv_len of the first decode step since the counter was zeroed
-  int nq;                // qkv tiles (16 columns each)
-  int na;                // attention units = workgroups [0, na)
-  int ta, tn;            // tiles per attention workgroup / per other workgroup
-  int* err;              // sticky: a wait timed out
-};
-
-template <int D, int G>
-__global__ __launch_bounds__(512) void decode_qkv_attn_kernel(
-    const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ Wt,
-    bf16_t* __restrict__ qkv, int64_t ldq, int M, int N, int K, KsFuse fz, int Hkv,
-    bf16_t* __restrict__ kc, bf16_t* __restrict__ vc, int64_t c_sb, int64_t c_st, int64_t c_sh,
-    const int* __restrict__ kv_len, const int* __restrict__ kv_start, int window,
-    float scale_log2, int nsplit, int cpb, float* __restrict__ part_o, float* __restrict__ part_ml,
-    int Hq, DecRope rp, bf16_t* __restrict__ out, int64_t o_sb, int64_t o_sh,
-    int* __restrict__ ccnt, int Tcap, DecQkvSync sy) {
-  const int bid = blockIdx.x, wave = threadIdx.x >> 6;
-  const bool attn = bid < sy.na;
-  const int t0 = attn ? bid * sy.ta : sy.na * sy.ta + (bid - sy.na) * sy.tn;
-  const int t1 = min(sy.nq, t0 + (attn ? sy.ta : sy.tn));
-  __shared__ __attribute__((aligned(16))) bf16_t qkv_s[(G + 2) * D];
-  // Hand-off without release / acquire fences (an agent release writes back the XCD's L2, ~1.7 us
-  // per workgroup; an acquire ~1.7 us per consumer): every qkv byte is stored write-through (`sc1`)
-  // and drained by its storing wave before the workgroup's counter add, and every consumer load
-  // of it is an `sc1` load after the poll. The counter is replicated on kQaRep lines (one add per
-  // replica, one wave instruction) so the ~200 pollers spread over 8 lines.
-  auto qkv_phase = [&]() {  // all 8 waves
-    for (int t = t0; t < t1; ++t) {
-      ks_body<2, true, false, 1, kKsUnroll, false, true, true, true>(t, sy.nq, x, ldx, Wt, K, qkv, ldq, M, N,
-                                                                       K, fz);
-      __syncthreads();  // the reduction buffer is reused by the next tile
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave's own stores
-    __syncthreads();
-    if (threadIdx.x < kQaRep && t1 > t0)
-      __hip_atomic_fetch_add(sy.cnt + threadIdx.x * kQaRepStride, t1 - t0, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-  };
-  if (!attn || wave >= 4) {
-    qkv_phase();
-    return;
-  }
-  const int split = bid % nsplit, r = bid / nsplit, hk = r % Hkv, b = r / Hkv;
-  auto wait = [&]() {
-    qkv_phase();
-    if (threadIdx.x == 0) {
-      const int target = sy.nq * (kv_len[0] - sy.len_first[0] + 1);
-      const int* rep = sy.cnt + (bid % kQaRep) * kQaRepStride;
-      int spins = 0;
-      while (__hip_atomic_load(rep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-        __builtin_amdgcn_s_sleep(4);
-        if (++spins > (1 << 21)) {
-          __hip_atomic_store(sy.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-      }
-    }
-    __syncthreads();  // (waves 4-7 have ended: the barrier counts waves 0-3)
-    // this block's q heads, k and v of the newest token into LDS, by `sc1` loads
-    const bf16_t* row = qkv + (int64_t)b * ldq;
-    for (int i = threadIdx.x; i < (G + 2) * D / 8; i += 256) {
-      const int e = i * 8;
-      const int col = e < G * D ? hk * G * D + e
-                                : (e < (G + 1) * D ? Hq * D + hk * D + (e - G * D)
-                                                   : (Hq + Hkv) * D + hk * D + (e - (G + 1) * D));
-      *reinterpret_cast<bf16x8*>(&qkv_s[e]) = load_sc1_16(row + col);
-    }
-    __syncthreads();
-  };
-  dec_loop_body<D, G, true, true, 2>(split, hk, b, Hkv, nullptr, 0, 0, kc, vc, c_sb, c_st, c_sh, kv_len,
-                                     kv_start, window, scale_log2, nsplit, cpb, part_o, part_ml, Hq, rp,
-                                     out, o_sb, o_sh, ccnt, Tcap, wait, qkv_s);
-}
-
-// splits of the fused kernel's attention units: ~256 units, in-kernel combine (<= 8 splits)
-int decode_qkv_attn_splits(int Tmax, int B, int Hkv) {
-  const int nch = (Tmax + kDecChunk - 1) / kDecChunk;
-  const int64_t blocks = static_cast<int64_t>(B) * Hkv * nch;
-  const int cpb = std::max({1, static_cast<int>((blocks + 255) / 256), (nch + kDecMaxFuse - 1) / kDecMaxFuse});
-  return (nch + cpb - 1) / cpb;
-}
-
-// workgroups that are resident at once (occupancy x CUs), per instantiation
-template <int D, int G>
-static int qkv_attn_capacity() {
-  static const int cap = [] {
-    int dev = 0, cus = 0, per = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, decode_qkv_attn_kernel<D, G>, 512, 0) != hipSuccess)
-      return 0;
-    return cus * per;
-  }();
-  return cap;
-}
-
-// returns false (nothing launched) when the shape is outside the fused kernel's range
-bool launch_decode_qkv_attn(const bf16_t* x, int64_t ldx, const bf16_t* Wt, bf16_t* qkv, int64_t ldq,
-                            int M, int N, int K, const KsFuse& fz, const float* cos_t,
-                            const float* sin_t, const int* pos, const int64_t* slot, int rot,
-                            bf16_t* kc, bf16_t* vc, int64_t c_sb, int64_t c_st, int64_t c_sh,
-                            const int* kv_len, const int* kv_start, int window, float scale_log2,
-                            int Hq, int Hkv, int D, int Tmax, float* part_o, float* part_ml,
-                            bf16_t* out, int64_t o_sb, int64_t o_sh, int* ccnt, int* sync_cnt,
-                            const int* len_first, int* err, hipStream_t st) {
-  const int B = M, G = Hq / Hkv;
-  const int nch = (Tmax + kDecChunk - 1) / kDecChunk;
-  const int nsplit = decode_qkv_attn_splits(Tmax, B, Hkv);
-  const int cpb = (nch + nsplit - 1) / nsplit;
-  if (nsplit > kDecMaxFuse || N % 16 != 0) return false;
-  int cap = 0;
-  if (D == 128) {
-    switch (G) {
-      case 1: cap = qkv_attn_capacity<128, 1>(); break;
-      case 2: cap = qkv_attn_capacity<128, 2>(); break;
-      case 4: cap = qkv_attn_capacity<128, 4>(); break;
-      case 8: cap = qkv_attn_capacity<128, 8>(); break;
-      default: return false;
-    }
-  } else if (D == 64) {
-    switch (G) {
-      case 1: cap = qkv_attn_capacity<64, 1>(); break;
-      case 2: cap = qkv_attn_capacity<64, 2>(); break;
-      case 4: cap = qkv_attn_capacity<64, 4>(); break;
-      case 8: cap = qkv_attn_capacity<64, 8>(); break;
-      default: return false;
-    }
-  } else {
-    return false;
-  }
-  const int nq = N / 16, na = nsplit * Hkv * B;
-  if (cap <= 0 || na > cap) return false;
-  const int grid = cap;
-  // even the work out: tile bytes 16 K bf16, attention unit bytes cpb chunks of K + V
-  const double wq = 32.0 * K, wa = 2.0 * cpb * kDecChunk * D * 2;
-  const double per = (nq * wq + na * wa) / grid;
-  int ta, tn;
-  // DLA_QA_TA (A/B knob): qkv tiles per attention workgroup; the rest are dealt to the others
-  static const int ta_env = [] {
-    const char* e = std::getenv("DLA_QA_TA");
-    return e ? std::atoi(e) : -1;
-  }();
-  if (na >= grid) {
-    ta = (nq + grid - 1) / grid;
-    tn = 0;
-  } else {
-    ta = std::max(0, static_cast<int>((per - wa) / wq + 0.5));
-    if (ta_env >= 0) ta = ta_env;
-    ta = std::min(ta, nq / std::max(na, 1));
-    tn = (nq - na * ta + (grid - na) - 1) / (grid - na);
-  }
-  if (static_cast<int64_t>(na) * ta + static_cast<int64_t>(grid - na) * tn < nq) return false;
-  const DecRope rp{qkv, ldq, cos_t, sin_t, pos, slot, rot, Hkv};
-  const DecQkvSync sy{sync_cnt, len_first, nq, na, ta, tn, err};
-  int* const cn = nsplit > 1 ? ccnt : nullptr;
-#define DLA_QA(DD, GG)                                                                                 \
-  decode_qkv_attn_kernel<DD, GG><<<grid, 512, 0, st>>>(x, ldx, Wt, qkv, ldq, M, N, K, fz, Hkv, kc, vc, \
-                                                        c_sb, c_st, c_sh, kv_len, kv_start, window,     \
-                                                        scale_log2, nsplit, cpb, part_o, part_ml, Hq,   \
-                                                        rp, out, o_sb, o_sh, cn, Tmax, sy)
-  if (D == 128) {
-    switch (G) {
-      case 1: DLA_QA(128, 1); break;
-      case 2: DLA_QA(128, 2); break;
-      case 4: DLA_QA(128, 4); break;
-      default: DLA_QA(128, 8); break;
-    }
-  } else {
-    switch (G) {
-      case 1: DLA_QA(64, 1); break;
-      case 2: DLA_QA(64, 2); break;
-      case 4: DLA_QA(64, 4); break;
-      default: DLA_QA(64, 8); break;
-    }
-  }
-#undef DLA_QA
-  return true;
+  dec_loop_body<D, G, ROPE>(blockIdx.x, blockIdx.y, blockIdx.z, gridDim.y, q, q_sb, q_sh, kc, vc, c_sb, c_st,
+                            c_sh, kv_len, kv_start, window, scale_log2, nsplit, cpb, part_o, part_ml, Hq, rp,
+                            out, o_sb, o_sh, cnt, Tcap);
 }
 
 // Decode-step prologue: rotate q (-> q_out [B, Hq, D]) and k of the newest token and write k and
@@ -1109,31 +854,8 @@ static void launch_decode_d(const bf16_t* q, int64_t q_sb, int64_t q_sh, bf16_t*
     // one split per sequence, or the in-kernel combine (arrival counters given): no combine launch
     int* const cn = (nsplit > 1 && nsplit <= kDecMaxFuse) ? cnt : nullptr;
     bf16_t* fin = (nsplit == 1 || cn != nullptr) ? out : nullptr;
-    // DLA_DECODE_RING=3 (A/B): all of a block's chunks in flight at once when it has >= 3 and the
-    // grid fits one block per CU (96 KB of V image per block)
-    static const int ring = [] {
-      const char* e = std::getenv("DLA_DECODE_RING");
-      return e ? std::atoi(e) : 2;
-    }();
-    const bool ring3 = ring == 3 && cpb >= 3 && (int64_t)nsplit * Hkv * B <= 256;
-    static const bool earlyk = [] {  // DLA_DECODE_EARLYK=1 (A/B)
-      const char* e = std::getenv("DLA_DECODE_EARLYK");
-      return e != nullptr && std::atoi(e) == 1;
-    }();
 #define DLA_DECL(GG)                                                                                    \
-  if (rp && earlyk && !ring3)                                                                           \
-    decode_attn_loop_kernel<D, GG, true, 2, true><<<grid, 256, 0, st>>>(q, q_sb, q_sh, kc, vc, c_sb,    \
-                                                                        c_st, c_sh, kv_len, kv_start,   \
-                                                                        window, scale_log2, nsplit, cpb, \
-                                                                        part_o, part_ml, Hq, r0, fin,   \
-                                                                        o_sb, o_sh, cn, Tmax);          \
-  else if (rp && ring3)                                                                                 \
-    decode_attn_loop_kernel<D, GG, true, 3><<<grid, 256, 0, st>>>(q, q_sb, q_sh, kc, vc, c_sb, c_st,    \
-                                                                  c_sh, kv_len, kv_start, window,       \
-                                                                  scale_log2, nsplit, cpb, part_o,      \
-                                                                  part_ml, Hq, r0, fin, o_sb, o_sh, cn, \
-                                                                  Tmax);                                \
-  else if (rp)                                                                                          \
+  if (rp)                                                                                               \
     decode_attn_loop_kernel<D, GG, true><<<grid, 256, 0, st>>>(q, q_sb, q_sh, kc, vc, c_sb, c_st, c_sh, \
                                                                kv_len, kv_start, window, scale_log2,    \
                                                                nsplit, cpb, part_o, part_ml, Hq, r0,    \
@@ -1237,97 +959,6 @@ void launch_decode_attn_rope(const bf16_t* qkv, int64_t ld, const float* cos_t, 
   else
     launch_decode_d<64>(nullptr, 0, 0, kc, vc, c_sb, c_st, c_sh, kv_len, kv_start, window,
                         scale_log2, B, Hq, Hkv, Tmax, part_o, part_ml, out, o_sb, o_sh, &rp, cnt, st);
-}
-
-// 17..64 decode rows (csrc/skinny64.hip): the qkv projection leaves S fp32 split-K slabs whose
-// reduce launch (m64_reduce_kernel MODE 1: y = bf16(rstd * sum_s slab_s)) is folded into this
-// attention launch instead. A block issues its first chunks' K / V loads, then reduces exactly the
-// (G + 2) x D values it reads -- its q heads, k and v of row b -- into LDS with the same
-// arithmetic and order as the reduce kernel (slabs summed in split order, rstd from the row's
-// partials in order), so the output equals the two-launch path bitwise; one launch and one
-// kernel boundary per layer fewer.
-struct DecSlab {
-  const float* ws;   // [S][M][N] fp32 slabs of the qkv projection
-  int S, M, N;
-  const float* ssq;  // [M][nbp] partial sums of squares of the input rows
-  int nbp, knorm;
-  float eps;
-};
-
-template <int D, int G>
-__global__ __launch_bounds__(256, 2) void decode_attn_slab_kernel(
-    bf16_t* __restrict__ kc, bf16_t* __restrict__ vc, int64_t c_sb, int64_t c_st, int64_t c_sh,
-    const int* __restrict__ kv_len, const int* __restrict__ kv_start, int window, float scale_log2,
-    int nsplit, int cpb, float* __restrict__ part_o, float* __restrict__ part_ml, int Hq, DecRope rp,
-    bf16_t* __restrict__ out, int64_t o_sb, int64_t o_sh, int* __restrict__ cnt, int Tcap, DecSlab sl) {
-  __shared__ __attribute__((aligned(16))) bf16_t qkv_s[(G + 2) * D];
-  const int split = blockIdx.x, hk = blockIdx.y, b = blockIdx.z, Hkv = gridDim.y;
-  auto stage = [&]() {
-    float a = 0.f;
-    for (int j = 0; j < sl.nbp; ++j) a += sl.ssq[b * sl.nbp + j];
-    const float rstd = rsqrtf(a / static_cast<float>(sl.knorm) + sl.eps);
-    const int64_t slab = static_cast<int64_t>(sl.M) * sl.N;
-    const float* row = sl.ws + static_cast<int64_t>(b) * sl.N;
-    for (int i = threadIdx.x; i < (G + 2) * D; i += 256) {
-      const int col = i < G * D ? hk * G * D + i
-                                : (i < (G + 1) * D ? Hq * D + hk * D + (i - G * D)
-                                                   : (Hq + Hkv) * D + hk * D + (i - (G + 1) * D));
-      float t = 0.f;
-      for (int sp = 0; sp < sl.S; ++sp) t += row[sp * slab + col];
-      qkv_s[i] = f2bf(t * rstd);
-    }
-    __syncthreads();
-  };
-  dec_loop_body<D, G, true, true, 2>(split, hk, b, Hkv, nullptr, 0, 0, kc, vc, c_sb, c_st, c_sh, kv_len,
-                                     kv_start, window, scale_log2, nsplit, cpb, part_o, part_ml, Hq, rp,
-                                     out, o_sb, o_sh, cnt, Tcap, stage, qkv_s);
-}
-
-void launch_decode_attn_slab(const float* ws, int S, int N, const float* ssq, int nbp, int knorm, float eps,
-                             const float* cos_t, const float* sin_t, const int* pos, const int64_t* slot,
-                             int rot, bf16_t* kc, bf16_t* vc, int64_t c_sb, int64_t c_st, int64_t c_sh,
-                             const int* kv_len, const int* kv_start, int window, float scale_log2, int B,
-                             int Hq, int Hkv, int D, int Tmax, float* part_o, float* part_ml, bf16_t* out,
-                             int64_t o_sb, int64_t o_sh, int* cnt, hipStream_t st) {
-  const int G = Hq / Hkv;
-  const int nch = (Tmax + kDecChunk - 1) / kDecChunk;
-  const int cpb = std::max(1, decode_cpb(Tmax, B, Hkv));
-  const int nsplit = (nch + cpb - 1) / cpb;
-  const DecRope rp{nullptr, 0, cos_t, sin_t, pos, slot, rot, Hkv};
-  const DecSlab sl{ws, S, B, N, ssq, nbp, knorm, eps};
-  int* const cn = (nsplit > 1 && nsplit <= kDecMaxFuse) ? cnt : nullptr;
-  bf16_t* fin = (nsplit == 1 || cn != nullptr) ? out : nullptr;
-  dim3 grid(nsplit, Hkv, B);
-#define DLA_SL(DD, GG)                                                                                   \
-  decode_attn_slab_kernel<DD, GG><<<grid, 256, 0, st>>>(kc, vc, c_sb, c_st, c_sh, kv_len, kv_start,      \
-                                                         window, scale_log2, nsplit, cpb, part_o, part_ml, \
-                                                         Hq, rp, fin, o_sb, o_sh, cn, Tmax, sl)
-  if (D == 128) {
-    switch (G) {
-      case 1: DLA_SL(128, 1); break;
-      case 2: DLA_SL(128, 2); break;
-      case 4: DLA_SL(128, 4); break;
-      default: DLA_SL(128, 8); break;
-    }
-  } else {
-    switch (G) {
-      case 1: DLA_SL(64, 1); break;
-      case 2: DLA_SL(64, 2); break;
-      case 4: DLA_SL(64, 4); break;
-      default: DLA_SL(64, 8); break;
-    }
-  }
-#undef DLA_SL
-  if (fin == nullptr)
-    (D == 128 ? decode_combine_kernel<128> : decode_combine_kernel<64>)<<<B * Hq, 64, 0, st>>>(
-        part_o, part_ml, nsplit, out, o_sb, o_sh, Hq);
-}
-
-// splits of the slab attention launch (host mirror for the partial buffers)
-int decode_attn_slab_splits(int Tmax, int B, int Hkv) {
-  const int nch = (Tmax + kDecChunk - 1) / kDecChunk;
-  const int cpb = std::max(1, decode_cpb(Tmax, B, Hkv));
-  return (nch + cpb - 1) / cpb;
 }
 
 }  // namespace dla

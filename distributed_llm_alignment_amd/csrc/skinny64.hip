@@ -16,10 +16,8 @@
 //     v_mfma_f32_16x16x32_bf16; every weight fragment feeds MT = M/16 MFMAs (one per 16 rows);
 //   * narrow outputs split K over workgroups (>= 256 workgroups) into fp32 slabs, reduced in a
 //     FIXED order with the decode-layer epilogue (residual add + row sum of squares, or the
-//     RMSNorm row factor) either by the last arriving workgroup of each column block (M64Cmb:
-//     write-through slabs + an arrival counter, no fence, no polling; opt-in, measured slower)
-//     or by a second small launch (m64_reduce_kernel, the default) -- deterministic, graph-capture
-//     safe;
+//     RMSNorm row factor) by a second small launch (m64_reduce_kernel) -- deterministic,
+//     graph-capture safe;
 //   * the gate|up projection (wide, no split) applies RMSNorm's row factor and SwiGLU in its
 //     own epilogue.
 #include "common.h"
@@ -42,17 +40,6 @@ __device__ __forceinline__ f32x4 mfma16(s16x8 a, s16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
-typedef __attribute__((address_space(1))) unsigned int m64_gu32;
-
-// write-through (`sc1`) 4-byte store / 16-byte load: the split-K slabs handed to the last
-// arriving workgroup of a column block, which may sit on another XCD (own L2)
-__device__ __forceinline__ void m64_st4_sc1(float* p, float v) {
-  __hip_atomic_store((m64_gu32*)p, __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ f32x4 m64_ld16_sc1(__amdgpu_buffer_rsrc_t r, int64_t float_off) {
-  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(float_off * 4), 0, 16));
-}
-
 // F8 (weight-only fp8 decode, TW + nt only): W is the e4m3 tiled copy [N/16, K/64, 64 lanes, 16 B]
 // of csrc/skinny_ks.h F8 (ops/decode.py fp8_tiled_weight): one 16-byte load per lane holds its B
 // fragments of two consecutive k-steps, so a 256-deep chunk is 4 loads per lane instead of 8 and
@@ -65,36 +52,19 @@ __device__ __forceinline__ f32x4 m64_ld16_sc1(__amdgpu_buffer_rsrc_t r, int64_t 
 // rows x 64 B at an 8 KB (K = 4096) stride.
 }  // namespace
 
-// In-kernel split-K combine (cmb.cnt given, S > 1; replaces the m64_reduce_kernel launch): every
-// workgroup stores its fp32 slab write-through, drains, and one thread adds 1 to its column
-// block's arrival counter; the workgroup that draws S - 1 re-arms the counter (graph replays need
-// no memset) and sums the S slabs of its 16 NW columns with sc1 loads in split order -- the same
-// arithmetic as m64_reduce_kernel, so y is bitwise the two-launch result -- then applies the
-// reduce's epilogue (MODE 1: rstd from ssq_in; MODE 2: residual add, ssq_out per (row, 16 NW
-// columns), i.e. nbp = N / 128 partials instead of N / 1024). No fences, no polling (MI355X
-// guide: release-free hand-off); the launch boundary after this kernel publishes y.
-struct M64Cmb {
-  unsigned* cnt;       // [gridDim.x] arrival counters, zero between launches
-  const bf16_t* res;   // MODE 2 residual [M, N] (row stride ldr)
-  int64_t ldr;
-  float* ssq_out;      // MODE 2 partials [M][gridDim.x]
-};
-
 // grid (N / 16 NW [GLU: F / 8 NW], S), 64 NW threads. LDS: 2 x 16 MT x kM64Ld bf16.
 // GLU: W = [gate; up] (2F rows), output m = silu(rstd * g) * (rstd * u) [M, F] where rstd comes
 // from ssq_in (the producer's row partial sums, [M][nbp]) when NIN, else 1; gate / up are
 // rounded to bf16 before SwiGLU exactly as the unfused GEMM + swiglu pair.
 // Otherwise S == 1 writes y = bf16(x W^T); S > 1 writes fp32 slab ws[s][m][n].
-template <int MT, bool GLU, bool NIN, bool TW, int DEPTH, int NW = kM64Waves, bool NTL = false, bool F8 = false,
-          bool CMB = false>
+template <int MT, bool GLU, bool NIN, bool TW, int DEPTH, int NW = kM64Waves, bool NTL = false, bool F8 = false>
 __global__ __launch_bounds__(64 * NW) void m64_gemm_kernel(
     const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ W, int64_t ldw,
     bf16_t* __restrict__ y, int64_t ldy, float* __restrict__ ws, int M, int N, int K, int kc,
-    const float* __restrict__ ssq_in, int nbp, float eps, const float* __restrict__ wsc, M64Cmb cmb) {
+    const float* __restrict__ ssq_in, int nbp, float eps, const float* __restrict__ wsc) {
   static_assert(!F8 || (TW && NTL), "fp8 weights: tiled layout, nt stream");
   extern __shared__ __attribute__((aligned(16))) bf16_t xs[];
   __shared__ float rstd_s[64];
-  __shared__ int last_s;
   constexpr int RB = 16 * MT * kM64Ld;  // one ring slot
   constexpr int NTH = 64 * NW;
   constexpr int XPASS = 16 * MT * 32 / NTH;  // x staging passes (32 threads per 256-deep row)
@@ -269,99 +239,13 @@ __global__ __launch_bounds__(64 * NW) void m64_gemm_kernel(
     return;
   }
   float* slab = ws + static_cast<int64_t>(s) * M * N;
-  if constexpr (!CMB) {
-#pragma unroll
-    for (int t = 0; t < MT; ++t)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int m = 16 * t + 4 * q + i;
-        if (m < M) slab[static_cast<int64_t>(m) * N + n] = acc[t][i];
-      }
-    return;
-  }
-  // ---- in-kernel combine (see M64Cmb)
 #pragma unroll
   for (int t = 0; t < MT; ++t)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int m = 16 * t + 4 * q + i;
-      if (m < M) m64_st4_sc1(slab + static_cast<int64_t>(m) * N + n, acc[t][i]);
+      if (m < M) slab[static_cast<int64_t>(m) * N + n] = acc[t][i];
     }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's slab stores are written through
-  __syncthreads();
-  const int S = gridDim.y;
-  if (tid == 0) {
-    const unsigned prev = __hip_atomic_fetch_add((m64_gu32*)(cmb.cnt + blockIdx.x), 1u, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-    const int last = prev == static_cast<unsigned>(S - 1);
-    if (last) __hip_atomic_store((m64_gu32*)(cmb.cnt + blockIdx.x), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last_s = last;
-  }
-  __syncthreads();
-  if (!last_s) return;
-  // the last arriver: thread -> (row mr + RPP p, 4 columns c0 + 4 c4); a row's F4R threads are
-  // consecutive lanes of one wave
-  constexpr int F4R = 4 * NW;        // float4 per row of the column block
-  constexpr int RPP = NTH / F4R;     // rows per pass
-  constexpr int NP = 64 / RPP;       // passes (M <= 64)
-  constexpr int SB = 8;              // slabs in flight per batch
-  const int c4 = tid % F4R, mr = tid / F4R;
-  const int c0 = blockIdx.x * (16 * NW) + 4 * c4;
-  const bool nin = cmb.res == nullptr && ssq_in != nullptr;
-  if (nin && tid < M) {  // MODE 1 row factors, partials summed in order (m64_reduce_kernel's)
-    float a = 0.f;
-    for (int j = 0; j < nbp; ++j) a += ssq_in[tid * nbp + j];
-    rstd_s[tid] = rsqrtf(a / static_cast<float>(K) + eps);
-  }
-  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(ws, 0, 0x7FFFFFFF, 0x00020000);
-  f32x4 tot[NP];
-#pragma unroll
-  for (int p = 0; p < NP; ++p) tot[p] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int s0 = 0; s0 < S; s0 += SB) {
-    f32x4 v[NP][SB];
-#pragma unroll
-    for (int p = 0; p < NP; ++p)
-#pragma unroll
-      for (int u = 0; u < SB; ++u) {
-        const int m = mr + RPP * p;
-        v[p][u] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (m < M && s0 + u < S)
-          v[p][u] = m64_ld16_sc1(wr, static_cast<int64_t>(s0 + u) * M * N + static_cast<int64_t>(m) * N + c0);
-      }
-#pragma unroll
-    for (int p = 0; p < NP; ++p)
-#pragma unroll
-      for (int u = 0; u < SB; ++u)
-        if (s0 + u < S) tot[p] += v[p][u];
-  }
-  __syncthreads();  // rstd_s
-#pragma unroll
-  for (int p = 0; p < NP; ++p) {
-    const int m = mr + RPP * p;
-    if (RPP * p >= M) break;  // wave-uniform: no row of this pass is live
-    const bool live = m < M;
-    f32x4 t = tot[p];
-    if (nin) t *= live ? rstd_s[m] : 0.f;
-    bf16x4 o;
-    float ss = 0.f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if (cmb.res != nullptr) {
-        const float rv = live ? bf2f(cmb.res[static_cast<int64_t>(m) * cmb.ldr + c0 + i]) : 0.f;
-        const float vv = bf2f(f2bf(bf2f(f2bf(t[i])) + rv));
-        o[i] = f2bf(vv);
-        ss += vv * vv;
-      } else {
-        o[i] = f2bf(t[i]);
-      }
-    }
-    if (live) *reinterpret_cast<bf16x4*>(y + static_cast<int64_t>(m) * ldy + c0) = o;
-    if (cmb.res != nullptr) {
-#pragma unroll
-      for (int off = F4R / 2; off > 0; off >>= 1) ss += __shfl_xor(ss, off, F4R);
-      if (live && c4 == 0) cmb.ssq_out[m * gridDim.x + blockIdx.x] = ss;
-    }
-  }
 }
 
 // Split-K reduce + decode-layer epilogue. grid (ceil(N / 1024), M), 256 threads x 4 columns.
@@ -468,7 +352,7 @@ size_t m64_lds_bytes(int M) {
 template <int MT, bool GLU, bool NIN, bool TW, int NW, bool NTL, int DEPTH = 2, bool F8 = false>
 static void m64_launch_w(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
                          int64_t ldy, float* ws, int M, int N, int K, int S, const float* ssq_in,
-                         int nbp, float eps, hipStream_t st, const float* wsc = nullptr, M64Cmb cmb = {}) {
+                         int nbp, float eps, hipStream_t st, const float* wsc = nullptr) {
   const size_t lds = static_cast<size_t>(2 * 16 * MT * kM64Ld) * sizeof(bf16_t);
   static bool attr = [] {
     hipFuncSetAttribute(reinterpret_cast<const void*>(&m64_gemm_kernel<MT, GLU, NIN, TW, DEPTH, NW, NTL, F8>),
@@ -478,22 +362,8 @@ static void m64_launch_w(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t 
   }();
   (void)attr;
   dim3 grid(GLU ? N / 2 / (8 * NW) : N / (16 * NW), S);
-  if constexpr (!GLU) {
-    if (cmb.cnt != nullptr) {  // in-kernel split-K combine (its own instantiation: the default keeps its registers)
-      static bool attr_c = [] {
-        hipFuncSetAttribute(reinterpret_cast<const void*>(&m64_gemm_kernel<MT, GLU, NIN, TW, DEPTH, NW, NTL, F8, true>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
-        (void)hipGetLastError();
-        return true;
-      }();
-      (void)attr_c;
-      m64_gemm_kernel<MT, GLU, NIN, TW, DEPTH, NW, NTL, F8, true><<<grid, 64 * NW, lds, st>>>(
-          x, ldx, W, ldw, y, ldy, ws, M, N, K, K / S, ssq_in, nbp, eps, wsc, cmb);
-      return;
-    }
-  }
   m64_gemm_kernel<MT, GLU, NIN, TW, DEPTH, NW, NTL, F8><<<grid, 64 * NW, lds, st>>>(
-      x, ldx, W, ldw, y, ldy, ws, M, N, K, K / S, ssq_in, nbp, eps, wsc, cmb);
+      x, ldx, W, ldw, y, ldy, ws, M, N, K, K / S, ssq_in, nbp, eps, wsc);
 }
 
 // NW = 8 waves per workgroup (gate|up: 64 features per workgroup). 4 waves (448 gate|up
@@ -501,7 +371,7 @@ static void m64_launch_w(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t 
 template <int MT, bool GLU, bool NIN, bool TW>
 static void m64_launch(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
                        int64_t ldy, float* ws, int M, int N, int K, int S, const float* ssq_in,
-                       int nbp, float eps, hipStream_t st, M64Cmb cmb = {}) {
+                       int nbp, float eps, hipStream_t st) {
   // non-temporal loads on the tiled weight stream (DLA_DECODE_NT, default on; see skinny.hip decode_nt)
   static const bool nt = [] {
     const char* e = getenv("DLA_DECODE_NT");
@@ -516,15 +386,15 @@ static void m64_launch(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ld
   if constexpr (TW) {
     if (nt) {
       if (depth == 3)
-        m64_launch_w<MT, GLU, NIN, TW, kM64Waves, true, 3>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, ssq_in, nbp, eps, st, nullptr, cmb);
+        m64_launch_w<MT, GLU, NIN, TW, kM64Waves, true, 3>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, ssq_in, nbp, eps, st);
       else if (depth == 4)
-        m64_launch_w<MT, GLU, NIN, TW, kM64Waves, true, 4>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, ssq_in, nbp, eps, st, nullptr, cmb);
+        m64_launch_w<MT, GLU, NIN, TW, kM64Waves, true, 4>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, ssq_in, nbp, eps, st);
       else
-        m64_launch_w<MT, GLU, NIN, TW, kM64Waves, true>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, ssq_in, nbp, eps, st, nullptr, cmb);
+        m64_launch_w<MT, GLU, NIN, TW, kM64Waves, true>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, ssq_in, nbp, eps, st);
       return;
     }
   }
-  m64_launch_w<MT, GLU, NIN, TW, kM64Waves, false>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, ssq_in, nbp, eps, st, nullptr, cmb);
+  m64_launch_w<MT, GLU, NIN, TW, kM64Waves, false>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, ssq_in, nbp, eps, st);
 }
 
 // fp8 weights (tiled, nt): DLA_M64_F8_DEPTH = weight chunks in flight per wave (2, 3 or 4; a chunk
@@ -532,7 +402,7 @@ static void m64_launch(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ld
 template <int MT, bool GLU, bool NIN>
 static void m64_launch_f8(const bf16_t* x, int64_t ldx, const uint8_t* W8, bf16_t* y, int64_t ldy, float* ws,
                           int M, int N, int K, int S, const float* ssq_in, int nbp, float eps,
-                          const float* wsc, hipStream_t st, M64Cmb cmb = {}) {
+                          const float* wsc, hipStream_t st) {
   static const int depth = [] {
     const char* e = getenv("DLA_M64_F8_DEPTH");
     const int d = e ? atoi(e) : 3;
@@ -540,23 +410,21 @@ static void m64_launch_f8(const bf16_t* x, int64_t ldx, const uint8_t* W8, bf16_
   }();
   const bf16_t* W = reinterpret_cast<const bf16_t*>(W8);
   if (depth == 2)
-    m64_launch_w<MT, GLU, NIN, true, kM64Waves, true, 2, true>(x, ldx, W, 0, y, ldy, ws, M, N, K, S, ssq_in, nbp, eps, st, wsc, cmb);
+    m64_launch_w<MT, GLU, NIN, true, kM64Waves, true, 2, true>(x, ldx, W, 0, y, ldy, ws, M, N, K, S, ssq_in, nbp, eps, st, wsc);
   else if (depth == 4)
-    m64_launch_w<MT, GLU, NIN, true, kM64Waves, true, 4, true>(x, ldx, W, 0, y, ldy, ws, M, N, K, S, ssq_in, nbp, eps, st, wsc, cmb);
+    m64_launch_w<MT, GLU, NIN, true, kM64Waves, true, 4, true>(x, ldx, W, 0, y, ldy, ws, M, N, K, S, ssq_in, nbp, eps, st, wsc);
   else
-    m64_launch_w<MT, GLU, NIN, true, kM64Waves, true, 3, true>(x, ldx, W, 0, y, ldy, ws, M, N, K, S, ssq_in, nbp, eps, st, wsc, cmb);
+    m64_launch_w<MT, GLU, NIN, true, kM64Waves, true, 3, true>(x, ldx, W, 0, y, ldy, ws, M, N, K, S, ssq_in, nbp, eps, st, wsc);
 }
 
 template <int MT>
 static void m64_dispatch_f8(const bf16_t* x, int64_t ldx, const uint8_t* W8, bf16_t* y, int64_t ldy, float* ws,
                             int M, int N, int K, int S, bool glu, const float* ssq_in, int nbp, float eps,
-                            const float* wsc, hipStream_t st, M64Cmb cmb) {
+                            const float* wsc, hipStream_t st) {
   if (glu && ssq_in)
     m64_launch_f8<MT, true, true>(x, ldx, W8, y, ldy, ws, M, N, K, 1, ssq_in, nbp, eps, wsc, st);
   else if (glu)
     m64_launch_f8<MT, true, false>(x, ldx, W8, y, ldy, ws, M, N, K, 1, nullptr, 0, 0.f, wsc, st);
-  else if (cmb.cnt != nullptr)  // the combine epilogue reads ssq_in (MODE 1)
-    m64_launch_f8<MT, false, false>(x, ldx, W8, y, ldy, ws, M, N, K, S, ssq_in, nbp, eps, wsc, st, cmb);
   else
     m64_launch_f8<MT, false, false>(x, ldx, W8, y, ldy, ws, M, N, K, S, nullptr, 0, 0.f, wsc, st);
 }
@@ -564,23 +432,19 @@ static void m64_dispatch_f8(const bf16_t* x, int64_t ldx, const uint8_t* W8, bf1
 // fp8 form of launch_m64_gemm: W8 the e4m3 tiled copy, wsc its per-row scales
 void launch_m64_gemm_f8(const bf16_t* x, int64_t ldx, const uint8_t* W8, bf16_t* y, int64_t ldy, float* ws,
                         int M, int N, int K, int S, bool glu, const float* ssq_in, int nbp, float eps,
-                        const float* wsc, hipStream_t st, unsigned* cnt, const bf16_t* res, int64_t ldr,
-                        float* ssq_out) {
-  const M64Cmb cmb{S > 1 && !glu ? cnt : nullptr, res, ldr, ssq_out};
-  if (M <= 32) m64_dispatch_f8<2>(x, ldx, W8, y, ldy, ws, M, N, K, S, glu, ssq_in, nbp, eps, wsc, st, cmb);
-  else m64_dispatch_f8<4>(x, ldx, W8, y, ldy, ws, M, N, K, S, glu, ssq_in, nbp, eps, wsc, st, cmb);
+                        const float* wsc, hipStream_t st) {
+  if (M <= 32) m64_dispatch_f8<2>(x, ldx, W8, y, ldy, ws, M, N, K, S, glu, ssq_in, nbp, eps, wsc, st);
+  else m64_dispatch_f8<4>(x, ldx, W8, y, ldy, ws, M, N, K, S, glu, ssq_in, nbp, eps, wsc, st);
 }
 
 template <int MT, bool TW>
 static void m64_dispatch(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
                          int64_t ldy, float* ws, int M, int N, int K, int S, bool glu,
-                         const float* ssq_in, int nbp, float eps, hipStream_t st, M64Cmb cmb) {
+                         const float* ssq_in, int nbp, float eps, hipStream_t st) {
   if (glu && ssq_in)
     m64_launch<MT, true, true, TW>(x, ldx, W, ldw, y, ldy, ws, M, N, K, 1, ssq_in, nbp, eps, st);
   else if (glu)
     m64_launch<MT, true, false, TW>(x, ldx, W, ldw, y, ldy, ws, M, N, K, 1, nullptr, 0, 0.f, st);
-  else if (cmb.cnt != nullptr)  // the combine epilogue reads ssq_in (MODE 1)
-    m64_launch<MT, false, false, TW>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, ssq_in, nbp, eps, st, cmb);
   else
     m64_launch<MT, false, false, TW>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, nullptr, 0, 0.f, st);
 }
@@ -589,15 +453,13 @@ static void m64_dispatch(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t 
 // tiled: W is the tiled layout (ldw unused).
 void launch_m64_gemm(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
                      int64_t ldy, float* ws, int M, int N, int K, int S, bool glu,
-                     const float* ssq_in, int nbp, float eps, bool tiled, hipStream_t st, unsigned* cnt,
-                     const bf16_t* res, int64_t ldr, float* ssq_out) {
-  const M64Cmb cmb{S > 1 && !glu ? cnt : nullptr, res, ldr, ssq_out};
+                     const float* ssq_in, int nbp, float eps, bool tiled, hipStream_t st) {
   if (M <= 32) {
-    if (tiled) m64_dispatch<2, true>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, glu, ssq_in, nbp, eps, st, cmb);
-    else m64_dispatch<2, false>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, glu, ssq_in, nbp, eps, st, cmb);
+    if (tiled) m64_dispatch<2, true>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, glu, ssq_in, nbp, eps, st);
+    else m64_dispatch<2, false>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, glu, ssq_in, nbp, eps, st);
   } else {
-    if (tiled) m64_dispatch<4, true>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, glu, ssq_in, nbp, eps, st, cmb);
-    else m64_dispatch<4, false>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, glu, ssq_in, nbp, eps, st, cmb);
+    if (tiled) m64_dispatch<4, true>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, glu, ssq_in, nbp, eps, st);
+    else m64_dispatch<4, false>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, glu, ssq_in, nbp, eps, st);
   }
 }
 

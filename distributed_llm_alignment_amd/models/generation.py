@@ -55,16 +55,6 @@ class KVCache:
         self._pos = None
         self.slot = torch.zeros(1, dtype=torch.long, device=dev)
         self.kv_len = torch.ones(1, dtype=torch.int32, device=dev)
-        # fused qkv + attention decode kernel (ops.decode.qkv_attend): per-layer arrival counters
-        # of its qkv blocks (monotonic within a generation, zeroed at every prefill), the kv_len of
-        # the first decode step, and a sticky wait-timeout word. Each layer's counter is kept in 8
-        # replicas on 128-byte lines of their own (csrc/decode.hip kQaRep / kQaRepStride)
-        self.sync = torch.zeros((L, 8, 32), dtype=torch.int32, device=dev)
-        self.len_first = torch.ones(1, dtype=torch.int32, device=dev)
-        self.sync_err = torch.zeros(1, dtype=torch.int32, device=dev)
-        # the persistent layer-tail kernel's phase counters (ops.decode.layer_tail): 3 phases x 8
-        # replicas x 32 ints per layer, monotonic within a generation like `sync`
-        self.tail_sync = torch.zeros((L, 3 * 8 * 32), dtype=torch.int32, device=dev)
         self.pos = torch.zeros((batch, 1), dtype=torch.int32, device=dev)
         self.fast_decode = (not self.split and dev.type == "cuda" and dt == torch.bfloat16
                             and ops.decode.decode_supported(self.h_local, Hkv, D))
@@ -135,48 +125,9 @@ class KVCache:
                                kv_start=kv_start, kv_end=None)
         return o.reshape(B, T, self.h_local * cfg.head_dim)
 
-    def attend_fused(self, layer: int, s: torch.Tensor, ssq: torch.Tensor, wt: torch.Tensor, eps: float,
-                     rope, window: int) -> Optional[torch.Tensor]:
-        """One decode step's qkv projection (RMSNorm folded into the tiled weight `wt`, the row
-        factor from the producer's partials `ssq`) and attention in ONE launch (csrc/decode.hip
-        decode_qkv_attn_kernel). None when the step or shape is not eligible."""
-        B = s.shape[0]
-        if not (self.len > 0 and self.len + 1 <= self.max_len and self.fast_decode and rope is not None
-                and rope.rot_dim % 16 == 0 and FUSED_DECODE_ROPE and s.dim() == 2 and B <= 16):
-            return None
-        D = self.cfg.head_dim
-        cos, sin = rope.tables(s.device)
-        o = ops._ext.require().decode_qkv_attn(
-            s, ssq, wt, float(eps), cos, sin, self.pos.view(-1), self.k[layer], self.v[layer], self.slot,
-            self.kv_len, self.kv_start, window, 1.0 / math.sqrt(D), self.h_local, self.kv_local, D,
-            rope.rot_dim, self.sync[layer], self.len_first, self.sync_err)
-        return o.reshape(B, 1, self.h_local * D)
-
-    def attend_slab(self, layer: int, s: torch.Tensor, ssq: torch.Tensor, wt: torch.Tensor, eps: float,
-                    rope, window: int) -> Optional[torch.Tensor]:
-        """17..64 decode rows: the qkv projection as split-K slabs (csrc/skinny64.hip, no reduce
-        launch) and the attention launch reducing the slabs it reads (csrc/decode.hip
-        decode_attn_slab_kernel). None when not eligible."""
-        B = s.shape[0]
-        if not (self.len > 0 and self.len + 1 <= self.max_len and self.fast_decode and rope is not None
-                and rope.rot_dim % 16 == 0 and FUSED_DECODE_ROPE and s.dim() == 2 and 16 < B <= 64):
-            return None
-        D = self.cfg.head_dim
-        ext = ops._ext.require()
-        ws = ext.skinny64_slabs(s, wt)
-        cos, sin = rope.tables(s.device)
-        o = ext.decode_attn_rope_slab(ws, ssq, float(eps), s.shape[1], cos, sin, self.pos.view(-1), self.k[layer],
-                                      self.v[layer], self.slot, self.kv_len, self.kv_start, window,
-                                      1.0 / math.sqrt(D), self.h_local, self.kv_local, D, rope.rot_dim)
-        return o.reshape(B, 1, self.h_local * D)
-
     def advance(self, T: int):
         """Host-driven advance (prefill / eager decode) keeping the device state in step."""
         self.len += T
-        if T > 1:  # a (new) prompt: the fused decode kernels' counters start over
-            self.sync.zero_()
-            self.tail_sync.zero_()
-            self.len_first.fill_(self.len + 1)
         self.slot.fill_(self.len)
         self.kv_len.fill_(self.len + 1)
         start = self.kv_start.view(-1, 1) if self.kv_start is not None else 0
@@ -502,12 +453,6 @@ def _generate(model: CausalLM, input_ids: torch.Tensor, attention_mask: Optional
         gm = torch.stack(gen_mask, 1)
     if was_training:
         model.train()
-    if ((ops.decode.DECODE_QKV_ATTN or ops.decode.DECODE_TAIL) and cache.fast_decode
-            and int(cache.sync_err.item()) != 0):
-        # the fused qkv + attention kernel's counter wait timed out (it proceeds rather than hang
-        # the GPU): the step's attention read an incomplete q / k / v row
-        raise RuntimeError("decode_qkv_attn: a workgroup's wait for the qkv tiles timed out "
-                           "(DLA_DECODE_QKV_ATTN=0 runs the two-launch path)")
     pm = attention_mask if attention_mask is not None else torch.ones_like(input_ids)
     if extra:
         seqs, pm = seqs[:, extra:].contiguous(), pm[:, extra:]

@@ -18,6 +18,7 @@ Parameters are stored fused (`qkv_proj`, `gate_up_proj`); `hf_state_dict()` /
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, List, Optional, Tuple
 
 import torch
@@ -81,7 +82,9 @@ class Attention(nn.Module):
         self.sp = None  # Ulysses sequence parallel (parallel.sequence.apply_sequence_parallel)
         self.h_local, self.kv_local = cfg.num_heads, cfg.num_kv_heads
 
-    def forward(self, h, rope, kv_start, kv_end, positions, cache=None, layer_idx=0, segs=None):
+    def forward(self, h, rope, kv_start, kv_end, positions, cache=None, layer_idx=0, segs=None,
+                resid=None):
+        """`resid` (no TP, no o bias): return resid + o_proj(attention), the add inside the o GEMM."""
         cfg = self.cfg
         seq = self.tp_seq if (h.dim() == 2 and cache is None) else None
         from ..parallel import tensor_parallel as tpm
@@ -116,7 +119,11 @@ class Attention(nn.Module):
         else:
             a = cache.attend(layer_idx, qkv, rope, window)
         if self.tp is None:
+            if resid is not None:
+                assert self.o_bias is None
+                return ops.linear_add(a, self.o_proj, resid)
             return _lin(a, self.o_proj, self.o_bias)
+        assert resid is None
         from ..parallel.tensor_parallel import sp_reduce_scatter, tp_grad_sum, tp_reduce
 
         if seq is not None:
@@ -158,7 +165,15 @@ class MLP(nn.Module):
         m, s = r
         return _lin(m, self.down_proj, None), s
 
-    def forward(self, h):
+    def forward(self, h, resid=None):
+        """`resid` (no TP): return resid + MLP(h); on the fused SwiGLU node the add runs inside
+        the down GEMM (its C input), elsewhere as a plain add."""
+        if resid is not None:
+            if (self.cfg.activation == "swiglu" and self.up_bias is None and self.down_bias is None
+                    and self.tp is None and self.tp_seq is None
+                    and ops.swiglu_mlp_ok(h, self.up_proj, self.down_proj)):
+                return ops.swiglu_mlp(h, self.up_proj, self.down_proj, resid=resid)
+            return self.forward(h) + resid
         seq = self.tp_seq if h.dim() == 2 else None
         if seq is not None:
             from ..parallel import tensor_parallel as tpm
@@ -260,6 +275,11 @@ class MoE(nn.Module):
         return ops.moe.combine(ys, pos, topv, permutation=True).view(shp)
 
 
+# Residual adds inside the o / down GEMMs (ops.linear.linear_add); DLA_FUSED_RESIDUAL=0 restores
+# the separate fused add + norm kernels for A/B runs.
+FUSED_RESIDUAL = os.environ.get("DLA_FUSED_RESIDUAL", "1") != "0"
+
+
 class DecoderLayer(nn.Module):
     def __init__(self, cfg: ModelConfig, device=None, dtype=None):
         super().__init__()
@@ -297,15 +317,17 @@ class DecoderLayer(nn.Module):
             a = cache.attend(layer_idx, qkv, rope, cfg.sliding_window if cfg.sliding_window else 0)
         else:
             window = cfg.sliding_window if cfg.sliding_window else 0
-            # qkv projection + attention in one launch (ops.decode.qkv_attend), else two
-            a = ops.decode.qkv_attend(s, ssq, self.ln1_w, cfg.norm_eps, at.qkv_proj, cache, layer_idx,
-                                      rope, window)
-            if a is None:
-                qkv = ops.decode.skinny_normed(s, ssq, self.ln1_w, cfg.norm_eps, at.qkv_proj)
-                a = cache.attend(layer_idx, qkv, rope, window)
+            qkv = ops.decode.skinny_normed(s, ssq, self.ln1_w, cfg.norm_eps, at.qkv_proj)
+            a = cache.attend(layer_idx, qkv, rope, window)
         s2, ssq2 = ops.decode.skinny_residual(a, at.o_proj, s)
         m = ops.decode.skinny_normed(s2, ssq2, self.ln2_w, cfg.norm_eps, mlp.up_proj, glu=True)
         return ops.decode.skinny_residual(m, mlp.down_proj, s2)
+
+    def fused_residual_ok(self, x, cache, seq) -> bool:
+        at, mlp = self.attn, self.mlp
+        return (FUSED_RESIDUAL and cache is None and seq is None and not self.cfg.parallel_block
+                and isinstance(mlp, MLP) and at.tp is None and mlp.tp is None and at.o_bias is None
+                and mlp.down_bias is None)
 
     def forward(self, x, resid, rope, kv_start, kv_end, positions, cache=None, layer_idx=0, segs=None):
         cfg = self.cfg
@@ -316,6 +338,20 @@ class DecoderLayer(nn.Module):
         else:
             w_ = _ident
         rc = self.recompute if (cache is None and self.training and torch.is_grad_enabled()) else None
+        if self.fused_residual_ok(x, cache, seq):
+            # the residual stream rides as the C input of the o and down GEMMs (beta = 1), so each
+            # norm reads and writes one [N, H] tensor instead of two each; the layer hands on the
+            # summed stream with resid = None
+            h, s = ops.add_norm(x, resid, self.ln1_w, self.ln1_b, cfg.norm_eps, rms, keep_stream=True)
+            if rc == "attention":
+                s = checkpoint(self.attn, h, rope, kv_start, kv_end, positions, None, layer_idx, segs, s,
+                               use_reentrant=False)
+            else:
+                s = self.attn(h, rope, kv_start, kv_end, positions, None, layer_idx, segs, resid=s)
+            h, s = ops.add_norm(s, None, self.ln2_w, self.ln2_b, cfg.norm_eps, rms, keep_stream=True)
+            if rc == "mlp":
+                return checkpoint(self.mlp, h, s, use_reentrant=False), None
+            return self.mlp(h, s), None
         h, resid = ops.add_norm(x, resid, w_(self.ln1_w, seq), w_(self.ln1_b, seq), cfg.norm_eps, rms)
         if rc == "attention":  # keep h; drop q/k/v, O and the LSE; recompute them in backward
             a = checkpoint(self.attn, h, rope, kv_start, kv_end, positions, None, layer_idx, segs,
@@ -523,23 +559,6 @@ class CausalLM(nn.Module):
         x = self.embed_tokens(input_ids, positions)
         # decode_fused calls the layers' kernels directly, skipping Module.__call__: a ZeRO-3
         # policy's layers are gathered by forward hooks, so sharded layers take the hooked path
-        if (input_ids.shape[1] == 1 and self.layer_devices is None and self.layers
-                and not self.layers_sharded() and ops.decode.tail_ok(self, x)):
-            # decode step as two launches per layer: attention, then the persistent layer tail
-            # (o, gate|up, down and the NEXT layer's qkv; csrc/decode_tail.hip)
-            cfg, L = self.cfg, len(self.layers)
-            window = cfg.sliding_window if cfg.sliding_window else 0
-            s = x.reshape(-1, x.shape[-1])
-            h, _ = ops.add_norm(s, None, self.layers[0].ln1_w, None, cfg.norm_eps, True)
-            qkv = _lin(h, self.layers[0].attn.qkv_proj, None)
-            B = input_ids.shape[0]
-            for i, layer in enumerate(self.layers):
-                a = cache.attend(i, qkv.view(B, 1, -1), self.rope, window)
-                s, qkv = ops.decode.layer_tail(a, s, layer, self.layers[i + 1] if i + 1 < L else None,
-                                               cfg.norm_eps, cache, i)
-            h, _ = ops.add_norm(s.view(B, 1, -1), None, self.norm_w, self.norm_b, cfg.norm_eps, True)
-            cache.step_done(1)
-            return h
         if (input_ids.shape[1] == 1 and self.layer_devices is None and self.layers
                 and not self.layers_sharded() and self.layers[0].decode_fused_ok(x)):
             # decode step: residual add + RMSNorm folded into the neighbouring projections

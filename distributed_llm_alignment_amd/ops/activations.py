@@ -47,13 +47,15 @@ class _SwiGLUMLPFn(torch.autograd.Function):
     per Llama-3-8B layer and micro-batch that removes a read+write of [M, 3F] bf16."""
 
     @staticmethod
-    def forward(ctx, h, w_up, w_down, tp_group=None, chunks=1):
+    def forward(ctx, h, w_up, w_down, tp_group=None, chunks=1, resid=None):
         ops = _ext.require()
         H = h.shape[-1]
         h2 = h.reshape(-1, H)
         u = F.linear(h2, w_up)
         m, mt = ops.swiglu_fwd_t(u)
-        if tp_group is None:
+        if resid is not None:  # residual stream as the down GEMM's C input (ops.linear.linear_add)
+            y = torch.addmm(resid.reshape(-1, w_down.shape[0]), m, w_down.t())
+        elif tp_group is None:
             y = F.linear(m, w_down)
         else:
             # tensor parallel (gate|up column-, down row-parallel): the down GEMM runs in token
@@ -74,6 +76,7 @@ class _SwiGLUMLPFn(torch.autograd.Function):
         ctx.w_up, ctx.w_down = w_up, w_down
         ctx.hshape = h.shape
         ctx.tp_group = tp_group
+        ctx.has_resid = resid is not None
         return y.view(*h.shape[:-1], w_down.shape[0])
 
     @staticmethod
@@ -98,7 +101,8 @@ class _SwiGLUMLPFn(torch.autograd.Function):
         accumulate_weight_grad(w_up, du, h2, dyt=dut)
         if work is not None:
             work.wait()
-        return (dh.view(ctx.hshape) if dh is not None else None), None, None, None, None
+        return ((dh.view(ctx.hshape) if dh is not None else None), None, None, None, None,
+                (dy if ctx.has_resid else None))
 
 
 def swiglu_mlp_ok(h: torch.Tensor, w_up: torch.Tensor, w_down: torch.Tensor) -> bool:
@@ -108,11 +112,13 @@ def swiglu_mlp_ok(h: torch.Tensor, w_up: torch.Tensor, w_down: torch.Tensor) -> 
 
 
 def swiglu_mlp(h: torch.Tensor, w_up: torch.Tensor, w_down: torch.Tensor, tp_group=None,
-               chunks: int = 1) -> torch.Tensor:
+               chunks: int = 1, resid: torch.Tensor = None) -> torch.Tensor:
     """Bias-free SwiGLU MLP with main_grad weight accumulation (see _SwiGLUMLPFn); callers check
     `swiglu_mlp_ok` first. With `tp_group` the node is the whole Megatron TP MLP (input
-    replicated, output all-reduced) with its collectives overlapped."""
-    return _SwiGLUMLPFn.apply(h, w_up, w_down, tp_group, chunks)
+    replicated, output all-reduced) with its collectives overlapped. With `resid` (no TP) the
+    result is resid + MLP(h), the add inside the down GEMM."""
+    assert resid is None or tp_group is None
+    return _SwiGLUMLPFn.apply(h, w_up, w_down, tp_group, chunks, resid)
 
 
 class _GeluFn(torch.autograd.Function):

@@ -511,34 +511,19 @@ def refresh_folded_weights(model) -> None:
                 fp8_tiled_weight(w)
 
 
-# 17..64 rows, opt-in (DLA_M64_COMBINE=1): the split-K projections (o, down, qkv) sum their fp32
-# slabs in the last arriving workgroup of each column block (csrc/skinny64.hip M64Cmb) instead of
-# a separate reduce launch; the residual producer then emits row partials per 128 columns.
-# Bitwise equal to the reduce launch and SLOWER on 1x MI355X (graph decode B=64, prompt 512:
-# 5.46 / 5.49 vs 5.02 / 5.03 ms/token bf16, 4.65 / 4.68 vs 4.29 / 4.28 fp8, same box): the
-# write-through slab drain + arrival atomic + one workgroup summing 8 slabs from memory cost more
-# than the 4.8 us reduce launch they replace (profiles/r5_decode.md).
-M64_COMBINE = os.environ.get("DLA_M64_COMBINE", "0") == "1"
-
-
-def _m64_cnt(x: torch.Tensor) -> Optional[torch.Tensor]:
-    """Arrival counters for the in-kernel split-K combine (None: the reduce launch)."""
-    return _skinny_counters(x.device) if M64_COMBINE else None
-
-
 def skinny_residual(x: torch.Tensor, w: torch.Tensor, res: torch.Tensor):
     """s = res + x @ w^T (bf16 rounding as linear + add), plus the row-norm partials of s."""
     x2 = _rows(x)
     if _f8_ok(x2.shape[0], w):
         w8, sc = fp8_tiled_weight(w)
         if x2.shape[0] > 16:
-            s, ssq = _ext.require().skinny64_f8(x2, w8, sc, _rows(res), None, 0.0, False, _m64_cnt(x2))
+            s, ssq = _ext.require().skinny64_f8(x2, w8, sc, _rows(res), None, 0.0, False)
         else:
             s, ssq = _ext.require().skinny_fused_f8(x2, w8, sc, _rows(res), None, 0.0)
         return s.view(*res.shape[:-1], w.shape[0]), ssq
     wk = tiled_weight(w) if DECODE_TILED >= 2 else w
     if x2.shape[0] > 16:
-        s, ssq = _ext.require().skinny64(x2, wk, _rows(res), None, 0.0, False, _m64_cnt(x2))
+        s, ssq = _ext.require().skinny64(x2, wk, _rows(res), None, 0.0, False)
     else:
         s, ssq = _ext.require().skinny_fused(x2, wk, _rows(res), None, 0.0, False)
     return s.view(*res.shape[:-1], w.shape[0]), ssq
@@ -551,7 +536,7 @@ def skinny_normed(s: torch.Tensor, ssq: torch.Tensor, norm_w: torch.Tensor, eps:
     if _f8_ok(s2.shape[0], w) and s2.shape[0] > 16:
         # 17..64 rows: gate|up in the plain [gate; up] row order (the m64 GLU epilogue pairs them)
         w8, sc = fp8_tiled_weight(w, norm_w)
-        y, _ = _ext.require().skinny64_f8(s2, w8, sc, None, ssq, float(eps), bool(glu), _m64_cnt(s2))
+        y, _ = _ext.require().skinny64_f8(s2, w8, sc, None, ssq, float(eps), bool(glu))
         return y.view(*s.shape[:-1], y.shape[-1])
     if _f8_ok(s2.shape[0], w):
         if glu:
@@ -567,103 +552,10 @@ def skinny_normed(s: torch.Tensor, ssq: torch.Tensor, norm_w: torch.Tensor, eps:
         return m.view(*s.shape[:-1], m.shape[-1])
     wf = folded_weight(w, norm_w, tiled=DECODE_TILED >= 1)
     if s2.shape[0] > 16:
-        y, _ = _ext.require().skinny64(s2, wf, None, ssq, float(eps), bool(glu), _m64_cnt(s2))
+        y, _ = _ext.require().skinny64(s2, wf, None, ssq, float(eps), bool(glu))
     else:
         y, _ = _ext.require().skinny_fused(s2, wf, None, ssq, float(eps), bool(glu))
     return y.view(*s.shape[:-1], y.shape[-1])
-
-
-# Fused decode qkv projection + attention (csrc/decode.hip decode_qkv_attn_kernel, B <= 16): the
-# attention blocks prefetch their first KV chunks while the qkv blocks of the same launch stream
-# the qkv weight, then wait on a device counter for this step's q / k / v. Off by default
-# (DLA_DECODE_QKV_ATTN=1 turns it on): measured slower in a real graph decode on 1x MI355X,
-# Llama-3-8B B=8 prompt 1024: 4.16 / 4.05 vs 3.58 / 3.57 ms/token for the two launches
-# (skinny_normed + the rope-fused decode attention); profiles/r4_decode.md.
-DECODE_QKV_ATTN = os.environ.get("DLA_DECODE_QKV_ATTN", "0") == "1"
-_DECODE_NT = os.environ.get("DLA_DECODE_NT", "1") != "0"  # the fused kernel streams with nt loads
-
-
-_COMBINE_ON = os.environ.get("DLA_DECODE_FUSED_COMBINE", "1") != "0"
-
-# <= 16 decode rows: the post-attention half of every layer (o + residual, gate|up + SwiGLU,
-# down + residual) AND the next layer's qkv projection as ONE persistent launch
-# (csrc/decode_tail.hip): the next phase's weights stream while the workgroups wait for the
-# previous phase; a step is then two launches per layer (this + the decode attention).
-DECODE_TAIL = os.environ.get("DLA_DECODE_TAIL", "0") == "1"
-
-
-def tail_ok(model, x) -> bool:
-    """The model's decode step can run on the persistent layer-tail kernel."""
-    if not (DECODE_TAIL and _DECODE_NT and DECODE_TILED >= 2 and x.is_cuda) or _FP8[0]:
-        return False
-    cfg = model.cfg
-    rows = x.numel() // x.shape[-1]
-    H, F, Ko = cfg.hidden_size, cfg.intermediate_size, model.layers[0].attn.o_proj.shape[1]
-    return (rows <= 16 and H % 1024 == 0 and F % 1024 == 0 and Ko % 1024 == 0
-            and rows * (H + 8) * 2 <= 140 * 1024 and all(l.decode_fused_ok(x) for l in model.layers))
-
-
-def layer_tail(a: torch.Tensor, x: torch.Tensor, layer, nxt, eps: float, cache, idx: int):
-    """x_out = x + o(a); x_out += down(SwiGLU(gate|up(RMSNorm(x_out)))); and, with `nxt`, the next
-    layer's qkv = RMSNorm(x_out) @ Wqkv^T, in one persistent launch. Returns (x_out [M, H],
-    qkv [M, Nq] or None)."""
-    at, mlp = layer.attn, layer.mlp
-    wo = tiled_weight(at.o_proj)
-    wgu = folded_weight(mlp.up_proj, layer.ln2_w, tiled=True, glu_il=True)
-    wd = tiled_weight(mlp.down_proj)
-    wq = folded_weight(nxt.attn.qkv_proj, nxt.ln1_w, tiled=True) if nxt is not None else None
-    xo, _, qkv = _ext.require().decode_tail(_rows(a), _rows(x), wo, wgu, wd, wq, float(eps), cache.tail_sync[idx],
-                                            cache.kv_len, cache.len_first, cache.sync_err)
-    return xo, (qkv if nxt is not None else None)
-
-
-_CUS = {}
-
-
-def _cu_count(dev: torch.device) -> int:
-    n = _CUS.get(dev.index)
-    if n is None:
-        n = _CUS[dev.index] = torch.cuda.get_device_properties(dev).multi_processor_count
-    return n
-
-
-def qkv_attn_splits(Tmax: int, B: int, Hkv: int) -> int:
-    """Key splits of the fused kernel's attention role (csrc/decode.hip decode_qkv_attn_splits)."""
-    nch = (Tmax + 127) // 128
-    cpb = max(1, (B * Hkv * nch + 255) // 256, (nch + 7) // 8)
-    return (nch + cpb - 1) // cpb
-
-
-# 17..64 rows: the qkv split-K slabs are reduced inside the attention launch (csrc/decode.hip
-# decode_attn_slab_kernel) instead of by a separate reduce launch. Off by default
-# (DLA_DECODE_SLAB_ATTN=1): a wash at B=64 prompt 512 (5.161 vs 5.143 ms/token, same box).
-DECODE_SLAB_ATTN = os.environ.get("DLA_DECODE_SLAB_ATTN", "0") == "1"
-
-
-def qkv_attend(s: torch.Tensor, ssq: torch.Tensor, norm_w: torch.Tensor, eps: float, w: torch.Tensor,
-               cache, layer: int, rope, window: int) -> Optional[torch.Tensor]:
-    """attention(RMSNorm(s) * norm_w @ w^T) for one decode step with fewer launches, or None:
-    <= 16 rows the qkv projection and the attention in ONE launch, 17..64 rows the qkv reduce
-    folded into the attention launch."""
-    if getattr(cache, "sync", None) is None or isinstance(cache.k, list):
-        return None
-    s2 = _rows(s)
-    B, K = s2.shape
-    if B > 16:
-        if _FP8[0] or not (DECODE_SLAB_ATTN and DECODE_M64 and DECODE_TILED >= 1 and B <= 64 and K % 256 == 0
-                and w.shape[0] % 128 == 0):
-            return None
-        return cache.attend_slab(layer, s2, ssq, folded_weight(w, norm_w, tiled=True), eps, rope, window)
-    if not (DECODE_QKV_ATTN and _DECODE_NT and DECODE_TILED >= 1) or _FP8[0]:
-        return None
-    N = w.shape[0]
-    nsplit = qkv_attn_splits(cache.max_len, B, cache.kv_local)
-    # one attention unit per resident workgroup (one 512-thread workgroup per CU)
-    cus = _cu_count(s2.device)
-    if not (B <= 16 and N < 16384 and N % 16 == 0 and K % 1024 == 0 and nsplit * cache.kv_local * B <= cus
-            and (nsplit == 1 or _COMBINE_ON)):
-        return None
-    return cache.attend_fused(layer, s2, ssq, folded_weight(w, norm_w, tiled=True), eps, rope, window)
 
 
 def skinny64_linear(x: torch.Tensor, w: torch.Tensor, tiled: bool = False) -> torch.Tensor:

@@ -226,6 +226,45 @@ class fp8_inference_scope:
         return False
 
 
+class _LinearAddMainGradFn(torch.autograd.Function):
+    """resid + x @ W^T as ONE hipBLASLt GEMM (the residual is the C input, beta = 1): the
+    decoder's o / down projections add their output onto the residual stream in the epilogue,
+    so the following RMSNorm reads one tensor and writes one instead of reading two and writing
+    two. Backward: d(resid) = dy, the rest as _LinearMainGradFn."""
+
+    @staticmethod
+    def forward(ctx, x, weight, resid):
+        ctx.save_for_backward(x)
+        ctx.weight = weight  # (on ctx: see _LinearMainGradFn)
+        N = weight.shape[0]
+        y = torch.addmm(resid.reshape(-1, N), x.reshape(-1, x.shape[-1]), weight.t())
+        return y.view(resid.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        weight = ctx.weight
+        K, N = x.shape[-1], dy.shape[-1]
+        dy2 = dy.reshape(-1, N)
+        dx = input_grad(dy2, weight).view(x.shape) if ctx.needs_input_grad[0] else None
+        dw = None
+        if ctx.needs_input_grad[1]:
+            x2 = x.reshape(-1, K)
+            if not accumulate_weight_grad(weight, dy2, x2):
+                dw = dy2.t() @ x2
+        return dx, dw, (dy if ctx.needs_input_grad[2] else None)
+
+
+def linear_add(x: torch.Tensor, weight: torch.Tensor, resid: torch.Tensor) -> torch.Tensor:
+    """resid + linear(x, weight), the add inside the GEMM (bias-free projections)."""
+    if fp8_inference_ok(x, weight, None):
+        return fp8_linear_frozen(x, weight).add_(resid)
+    if uses_main_grad(weight):
+        return _LinearAddMainGradFn.apply(x, weight, resid)
+    N = weight.shape[0]
+    return torch.addmm(resid.reshape(-1, N), x.reshape(-1, x.shape[-1]), weight.t()).view(resid.shape)
+
+
 def linear(x: torch.Tensor, weight: torch.Tensor, bias=None) -> torch.Tensor:
     # (fp8 inference first: it needs grad disabled, so a training forward never takes it; a
     # trainable policy's no-grad rollout prefill inside fp8_inference_scope does)

@@ -29,7 +29,7 @@ def _ref_norm(s: torch.Tensor, weight, bias, eps: float, rms: bool) -> torch.Ten
 
 class _NormFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, residual, weight, bias, eps, rms):
+    def forward(ctx, x, residual, weight, bias, eps, rms, keep_stream=False):
         ops = _ext.require()
         H = x.shape[-1]
         x2 = x.reshape(-1, H)
@@ -42,7 +42,11 @@ class _NormFn(torch.autograd.Function):
         ctx.has_res = residual is not None
         ctx.has_bias = bias is not None
         ctx.shape = x.shape
-        out_s = s.view(x.shape) if residual is not None else None
+        # keep_stream: the stream s (= x when there is no residual) leaves as a second output of
+        # THIS node, so whoever adds the next branch onto it (a GEMM with s as its C input,
+        # ops.linear.linear_add) hands its gradient back here, where norm_bwd folds it in as
+        # `dres` -- one kernel, no separate autograd accumulation of the two gradients of s
+        out_s = s.view(x.shape) if (residual is not None or keep_stream) else None
         ctx.mark_non_differentiable(rstd)
         return y.view(x.shape), out_s
 
@@ -55,16 +59,18 @@ class _NormFn(torch.autograd.Function):
         ds, dw, db = ops.norm_bwd(dy.reshape(-1, H).contiguous(), s, weight, rstd, mean, dres,
                                   ctx.has_bias, ctx.rms)
         ds = ds.view(ctx.shape)
-        return ds, (ds if ctx.has_res else None), dw, (db if ctx.has_bias else None), None, None
+        return ds, (ds if ctx.has_res else None), dw, (db if ctx.has_bias else None), None, None, None
 
 
 def add_norm(x: torch.Tensor, residual: Optional[torch.Tensor], weight: torch.Tensor,
              bias: Optional[torch.Tensor] = None, eps: float = 1e-5,
-             rms: bool = True) -> Tuple[torch.Tensor, torch.Tensor]:
+             rms: bool = True, keep_stream: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
+    """`keep_stream`: return the stream s as an output of the norm node even without a
+    residual (see _NormFn), for a caller that feeds s to ops.linear.linear_add."""
     if _ext.use_native(x):
         y, s = _NormFn.apply(x.contiguous(), residual.contiguous() if residual is not None else None,
-                             weight, bias, eps, rms)
-        return y, (s if residual is not None else x)
+                             weight, bias, eps, rms, keep_stream)
+        return y, (s if s is not None else x)
     s = x if residual is None else (x + residual)
     return _ref_norm(s, weight, bias, eps, rms), s
 

@@ -378,45 +378,6 @@ def test_fused_rope_decode_attention_matches_unfused(D, Hq, Hkv, rot, blocks, mo
     assert torch.equal(out, ref)
 
 
-@pytest.mark.parametrize("B,Tmax,L", [(24, 300, 257), (48, 37, 22), (64, 800, 700)])
-def test_slab_decode_attention_matches_reduce_then_attention(B, Tmax, L):
-    """decode_attn_rope_slab (17..64 rows: the qkv split-K slabs reduced inside the attention
-    launch) == the reduce (bf16(rstd * sum of slabs in split order)) + decode_attn_rope."""
-    from distributed_llm_alignment_amd.ops import RotaryCache, _ext
-
-    C = _ext.require()
-    D, Hq, Hkv, rot, S, K, eps = 128, 8, 2, 128, 8, 1024, 1e-5
-    N = (Hq + 2 * Hkv) * D
-    g = torch.Generator(device=DEV).manual_seed(9)
-    rope = RotaryCache(rot, 10000.0, 4096, None)
-    cos, sin = rope.tables(DEV)
-    kc = torch.randn(B, Tmax, Hkv, D, device=DEV, generator=g).to(torch.bfloat16)
-    vc = torch.randn(B, Tmax, Hkv, D, device=DEV, generator=g).to(torch.bfloat16)
-    kc[:, L:] = float("nan")  # never-written cache rows (torch.empty): must not leak into the output
-    vc[:, L:] = float("nan")
-    ws = torch.randn(S, B, N, device=DEV, generator=g) * 0.05
-    ssq = torch.rand(B, 1, device=DEV, generator=g) * K + 1.0
-    kv_start = (torch.arange(B, device=DEV, dtype=torch.int32) * 7) % 19
-    pos = (L - 1 - kv_start).to(torch.int32)
-    slot = torch.tensor([L - 1], device=DEV, dtype=torch.long)
-    kv_len = torch.tensor([L], device=DEV, dtype=torch.int32)
-    t = ws[0].clone()
-    for sp in range(1, S):
-        t = t + ws[sp]
-    rstd = torch.rsqrt(ssq[:, 0] / K + eps)
-    qkv = (t * rstd[:, None]).to(torch.bfloat16).view(B, 1, N)
-    k1, v1 = kc.clone(), vc.clone()
-    ref = C.decode_attn_rope(qkv, cos, sin, pos, k1, v1, slot, kv_len, kv_start, 0, D ** -0.5, Hq, Hkv, D, rot)
-    k2, v2 = kc.clone(), vc.clone()
-    out = C.decode_attn_rope_slab(ws, ssq, eps, K, cos, sin, pos, k2, v2, slot, kv_len, kv_start, 0,
-                                  D ** -0.5, Hq, Hkv, D, rot)
-    torch.cuda.synchronize()
-    assert torch.isfinite(out.float()).all() and torch.isfinite(ref.float()).all()
-    assert ((k1.float() - k2.float()).abs()[:, :L].max() <= 0.02
-            and (v1.float() - v2.float()).abs()[:, :L].max() <= 0.02)
-    assert torch.allclose(out.float(), ref.float(), atol=2e-2, rtol=2e-2), (out.float() - ref.float()).abs().max()
-
-
 @pytest.mark.parametrize("M,K,F", [(8, 4096, 1024), (1, 4096, 256), (16, 2048, 512), (3, 512, 128)])
 def test_fused_norm_glu_matches_add_norm_then_glu(M, K, F):
     """skinny_glu_norm (residual add + RMSNorm staged inside the gate|up GEMM) == add_norm +
@@ -545,62 +506,6 @@ def test_fused_decode_layer_matches_unfused(B, monkeypatch):
     clear_graph_cache()
     a = generate(m, ids, max_new_tokens=12, do_sample=False, eos_token_id=-1, use_graph=False)
     b = generate(m, ids, max_new_tokens=12, do_sample=False, eos_token_id=-1, use_graph=True)
-    clear_graph_cache()
-    assert torch.equal(a, b)
-
-
-@pytest.mark.parametrize("B,T,pad", [(1, 40, False), (5, 300, True), (8, 40, False), (16, 200, True),
-                                     (24, 100, True), (64, 300, False)])
-def test_fused_qkv_attention_matches_two_launches(B, T, pad, monkeypatch):
-    """<= 16 rows: decode steps with the qkv projection and the attention in ONE launch
-    (csrc/decode.hip decode_qkv_attn_kernel: every workgroup does its qkv tiles, the attention
-    units prefetch KV first and then wait on a device counter) against the two-launch path and an
-    fp32 full forward; the counter reached every step and no wait timed out. 17..64 rows: the qkv
-    split-K reduce folded into the attention launch (decode_attn_slab_kernel). graph == eager."""
-    from distributed_llm_alignment_amd import ops
-    from distributed_llm_alignment_amd.models import build_model, generate
-    from distributed_llm_alignment_amd.models.generation import KVCache, clear_graph_cache
-
-    cfg = _fused_cfg()
-    m = build_model(cfg, device=DEV, dtype=torch.bfloat16, seed=4).eval()
-    g = torch.Generator(device=DEV).manual_seed(11)
-    ids = torch.randint(3, cfg.vocab_size, (B, T), device=DEV, generator=g)
-    am = torch.ones_like(ids)
-    if pad:  # left padding: per-row kv_start
-        for r in range(B):
-            am[r, :(7 * r) % 33] = 0
-    steps = [torch.randint(3, cfg.vocab_size, (B, 1), device=DEV, generator=g) for _ in range(3)]
-    outs, caches = {}, {}
-    from distributed_llm_alignment_amd.models.transformer import attention_layout
-
-    kv_start = attention_layout(am)[0] if pad else None
-    flag = "DECODE_QKV_ATTN" if B <= 16 else "DECODE_SLAB_ATTN"
-    with torch.no_grad():
-        for fused in (False, True):
-            monkeypatch.setattr(ops.decode, flag, fused)
-            cache = KVCache(m, B, T + 8, kv_start)
-            m(ids, am if pad else None, cache=cache)
-            outs[fused] = [m(nx, cache=cache).float() for nx in steps]
-            caches[fused] = cache
-        full = torch.cat([ids] + steps, 1)
-        fam = torch.cat([am, torch.ones(B, len(steps), dtype=am.dtype, device=DEV)], 1)
-        ref = m(full, fam if pad else None)[:, -len(steps):].float()
-    cf = caches[True]
-    torch.cuda.synchronize()
-    assert int(cf.sync_err.item()) == 0
-    if B <= 16:
-        n_q = m.layers[1].attn.qkv_proj.shape[0] // 16
-        # layer 1 ran the fused kernel every step: every counter replica saw every tile
-        assert cf.sync[1, :, 0].tolist() == [n_q * len(steps)] * 8
-        assert int(caches[False].sync[1].abs().sum().item()) == 0
-    err = lambda a, b: float((a - b).norm() / b.norm())  # noqa: E731
-    for k in range(len(steps)):
-        assert err(outs[True][k], outs[False][k]) < 1e-2, k
-        assert err(outs[True][k][:, 0], ref[:, k]) < 3e-2, k
-    monkeypatch.setattr(ops.decode, flag, True)
-    clear_graph_cache()
-    a = generate(m, ids, am, max_new_tokens=12, do_sample=False, eos_token_id=-1, use_graph=False)
-    b = generate(m, ids, am, max_new_tokens=12, do_sample=False, eos_token_id=-1, use_graph=True)
     clear_graph_cache()
     assert torch.equal(a, b)
 
@@ -741,12 +646,11 @@ def test_skinny64_kernels_match_fp32(M):
     w = (torch.randn(H, F, device=DEV, generator=g) * F ** -0.5).to(torch.bfloat16)
     res = torch.randn(M, H, device=DEV, generator=g).to(torch.bfloat16)
     s, ssq = ops.decode.skinny_residual(x, w, res)
-    assert ssq.shape == (M, H // 128 if ops.decode.M64_COMBINE else H // 1024)
+    assert ssq.shape == (M, H // 1024)
     s_ref = (x.float() @ w.float().t()).to(torch.bfloat16).float() + res.float()
     assert float((s.float() - s_ref).abs().max()) < 0.05
     assert torch.allclose(ssq.sum(1), (s.float() ** 2).sum(1), rtol=1e-4)
-    s_t, ssq_t = ops._ext.require().skinny64(x, ops.decode.tiled_weight(w), res, None, 0.0, False,
-                                             ops.decode._m64_cnt(x))
+    s_t, ssq_t = ops._ext.require().skinny64(x, ops.decode.tiled_weight(w), res, None, 0.0, False)
     assert torch.equal(s_t, s) and torch.equal(ssq_t, ssq)
     nw = (1 + 0.1 * torch.randn(H, device=DEV, generator=g)).to(torch.bfloat16)
     h_ref = _ref_norm(s.float(), nw.float(), None, 1e-5, True)
@@ -760,112 +664,6 @@ def test_skinny64_kernels_match_fp32(M):
     # row-major folded weight (DLA_M64_TILED=0) == the tiled default, bitwise
     mm_rm, _ = ops._ext.require().skinny64(s, ops.decode.folded_weight(wgu, nw), None, ssq, 1e-5, True)
     assert torch.equal(mm_rm, mm)
-
-
-@pytest.mark.parametrize("M", [17, 40, 64])
-def test_m64_inkernel_combine_matches_reduce_launch(M):
-    """17..64 rows: the split-K projections' in-kernel combine (the last arriving workgroup of a
-    column block sums the write-through fp32 slabs, csrc/skinny64.hip M64Cmb) against the separate
-    reduce launch, bf16 and fp8 weights: plain and residual outputs BITWISE equal (same split
-    order and roundings); row partials per 128 columns that sum to the per-1024 ones; the
-    normalised-input consumers (qkv via the combine, gate|up via the GLU epilogue) fed 32
-    partials within rounding of the 4-partial path; every counter re-armed to 0; repeat calls
-    identical."""
-    from distributed_llm_alignment_amd import ops
-
-    C = ops._ext.require()
-    cnt = torch.zeros(8192, dtype=torch.int32, device=DEV)
-    g = torch.Generator(device=DEV).manual_seed(100 + M)
-    rel = lambda a, b: float((a.float() - b.float()).norm() / b.float().norm())
-    H, F = 4096, 14336
-    for N, K in ((6144, H), (H, H), (H, F)):
-        x = torch.randn(M, K, device=DEV, generator=g).to(torch.bfloat16)
-        w = (torch.randn(N, K, device=DEV, generator=g) * K ** -0.5).to(torch.bfloat16)
-        wt = ops.decode.tiled_weight(w)
-        w8, sc = ops.decode.fp8_tiled_weight(w)
-        for fp8 in (False, True):
-            op = (lambda *a: C.skinny64_f8(a[0], w8, sc, *a[2:])) if fp8 else C.skinny64
-            y0, _ = op(x, wt, None, None, 0.0, False)
-            y1, _ = op(x, wt, None, None, 0.0, False, cnt)
-            y2, _ = op(x, wt, None, None, 0.0, False, cnt)
-            assert torch.equal(y0, y1) and torch.equal(y1, y2), (N, K, fp8)
-            assert int(cnt.abs().sum()) == 0
-            if N != H:
-                continue
-            res = torch.randn(M, N, device=DEV, generator=g).to(torch.bfloat16)
-            s0, q0 = op(x, wt, res, None, 0.0, False)
-            s1, q1 = op(x, wt, res, None, 0.0, False, cnt)
-            assert torch.equal(s0, s1) and q0.shape == (M, N // 1024) and q1.shape == (M, N // 128)
-            assert torch.allclose(q1.view(M, N // 1024, 8).sum(2), q0, rtol=1e-5)
-            assert int(cnt.abs().sum()) == 0
-            nw = (1 + 0.1 * torch.randn(H, device=DEV, generator=g)).to(torch.bfloat16)
-            wq = (torch.randn(6144, H, device=DEV, generator=g) * H ** -0.5).to(torch.bfloat16)
-            wgu = (torch.randn(2 * 1024, H, device=DEV, generator=g) * H ** -0.5).to(torch.bfloat16)
-            for ww, glu in ((wq, False), (wgu, True)):
-                if fp8:
-                    a8, asc = ops.decode.fp8_tiled_weight(ww, nw)
-                    f = lambda *a: C.skinny64_f8(a[0], a8, asc, *a[2:])
-                else:
-                    f, a8 = C.skinny64, ops.decode.folded_weight(ww, nw, tiled=True)
-                h0, _ = f(s0, a8, None, q0, 1e-5, glu)
-                h1, _ = f(s0, a8, None, q1, 1e-5, glu, cnt)
-                assert rel(h1, h0) < 1e-3, (glu, fp8, rel(h1, h0))
-                assert int(cnt.abs().sum()) == 0
-
-
-@pytest.mark.parametrize("B,T,pad", [(1, 40, False), (5, 300, True), (8, 100, False), (16, 200, True)])
-def test_decode_layer_tail_matches_four_launches(B, T, pad, monkeypatch):
-    """<= 16 rows: the persistent layer tail (csrc/decode_tail.hip: o + residual, gate|up +
-    SwiGLU, down + residual and the next layer's qkv in ONE launch, phase hand-offs through
-    write-through stores and replicated counters) against the four-launch fused decode layer --
-    BITWISE (same per-wave K order, wave-order reductions, roundings) -- and an fp32 forward; every
-    phase counter replica saw every workgroup every step, no wait timed out; graph == eager."""
-    from distributed_llm_alignment_amd import ops
-    from distributed_llm_alignment_amd.models import build_model, generate
-    from distributed_llm_alignment_amd.models.generation import KVCache, clear_graph_cache
-    from distributed_llm_alignment_amd.models.transformer import attention_layout
-
-    cfg = _fused_cfg()
-    m = build_model(cfg, device=DEV, dtype=torch.bfloat16, seed=5).eval()
-    g = torch.Generator(device=DEV).manual_seed(13)
-    ids = torch.randint(3, cfg.vocab_size, (B, T), device=DEV, generator=g)
-    am = torch.ones_like(ids)
-    if pad:
-        for r in range(B):
-            am[r, :(5 * r) % 29] = 0
-    steps = [torch.randint(3, cfg.vocab_size, (B, 1), device=DEV, generator=g) for _ in range(3)]
-    kv_start = attention_layout(am)[0] if pad else None
-    outs, caches = {}, {}
-    with torch.no_grad():
-        for tail in (False, True):
-            monkeypatch.setattr(ops.decode, "DECODE_TAIL", tail)
-            cache = KVCache(m, B, T + 8, kv_start)
-            m(ids, am if pad else None, cache=cache)
-            assert ops.decode.tail_ok(m, m.embed_tokens(steps[0])) == tail
-            outs[tail] = [m(nx, cache=cache).float() for nx in steps]
-            caches[tail] = cache
-        full = torch.cat([ids] + steps, 1)
-        fam = torch.cat([am, torch.ones(B, len(steps), dtype=am.dtype, device=DEV)], 1)
-        ref = m(full, fam if pad else None)[:, -len(steps):].float()
-    ct = caches[True]
-    torch.cuda.synchronize()
-    assert int(ct.sync_err.item()) == 0
-    nwg = torch.cuda.get_device_properties(0).multi_processor_count  # one workgroup per CU
-    cnt = ct.tail_sync.view(cfg.num_layers, 3, 8, 32)[:, :, :, 0]
-    assert (cnt[:-1] == nwg * len(steps)).all(), cnt  # layers with a next-layer qkv phase: 3 counters
-    assert (cnt[-1, :2] == nwg * len(steps)).all() and int(cnt[-1, 2].abs().sum()) == 0, cnt[-1]
-    assert int(caches[False].tail_sync.abs().sum()) == 0
-    for k in range(len(steps)):
-        assert torch.equal(outs[True][k], outs[False][k]), k
-        assert float((outs[True][k][:, 0] - ref[:, k]).norm() / ref[:, k].norm()) < 3e-2, k
-    monkeypatch.setattr(ops.decode, "DECODE_TAIL", True)
-    clear_graph_cache()
-    a = generate(m, ids, am, max_new_tokens=12, do_sample=False, eos_token_id=-1, use_graph=False)
-    b = generate(m, ids, am, max_new_tokens=12, do_sample=False, eos_token_id=-1, use_graph=True)
-    monkeypatch.setattr(ops.decode, "DECODE_TAIL", False)
-    c = generate(m, ids, am, max_new_tokens=12, do_sample=False, eos_token_id=-1, use_graph=True)
-    clear_graph_cache()
-    assert torch.equal(a, b) and torch.equal(b, c)
 
 
 # ------------------------------------------------------------------ weight-only fp8 decode

@@ -126,6 +126,63 @@ def test_fused_swiglu_mlp_main_grad():
     assert len(fired) == 2 and w_up.grad is None
 
 
+def test_fused_residual_chain_main_grad():
+    """The decoder's fused-residual chain: norm (stream kept as a node output) -> o GEMM with the
+    stream as C input (ops.linear_add) -> norm -> SwiGLU MLP with the stream as the down GEMM's C
+    input, against the same chain in fp32 autograd with explicit adds. The stream's two gradients
+    meet inside norm_bwd (dres), so the input gradient checks that wiring."""
+    H, F_, M = 256, 384, 192
+    x = bf(torch.randn(M, H)).requires_grad_()
+    w1, w2 = (bf(1 + 0.1 * torch.randn(H)).requires_grad_() for _ in range(2))
+    wo = bf(torch.randn(H, H) / H ** 0.5).requires_grad_()
+    wu = bf(torch.randn(2 * F_, H) / H ** 0.5).requires_grad_()
+    wd = bf(torch.randn(H, F_) / F_ ** 0.5).requires_grad_()
+    for w in (wo, wu, wd):
+        w.main_grad = torch.zeros_like(w)
+    h, s = ops.add_norm(x, None, w1, None, 1e-5, True, keep_stream=True)
+    s2 = ops.linear_add(h, wo, s)
+    h2, s2k = ops.add_norm(s2, None, w2, None, 1e-5, True, keep_stream=True)
+    y = ops.swiglu_mlp(h2, wu, wd, resid=s2k)
+    gy = bf(torch.randn(M, H))
+    (y.float() * gy.float()).sum().backward()
+    xr, w1r, w2r, wor, wur, wdr = (t.detach().float().requires_grad_() for t in (x, w1, w2, wo, wu, wd))
+    hr = _ref_norm(xr, w1r, None, 1e-5, True)
+    s2r = xr + hr @ wor.t()
+    h2r = _ref_norm(s2r, w2r, None, 1e-5, True)
+    a, u = (h2r @ wur.t()).chunk(2, -1)
+    yr = s2r + (torch.nn.functional.silu(a) * u) @ wdr.t()
+    (yr * gy.float()).sum().backward()
+    assert rel_err(y, yr) < 2e-2
+    assert rel_err(x.grad, xr.grad) < 3e-2
+    assert rel_err(w1.grad, w1r.grad) < 3e-2 and rel_err(w2.grad, w2r.grad) < 3e-2
+    for w, r in ((wo, wor), (wu, wur), (wd, wdr)):
+        assert rel_err(w.main_grad, r.grad) < 3e-2
+
+
+def test_fused_residual_model_matches_unfused(monkeypatch):
+    """2-layer Llama policy: the fused-residual decoder (adds in the o / down GEMM epilogues) and
+    the separate add + norm kernels give the same DPO loss and weight gradients within bf16."""
+    from distributed_llm_alignment_amd.data.synthetic import synthetic_preference_batch
+    from distributed_llm_alignment_amd.models import build_model, get_config, transformer
+    from distributed_llm_alignment_amd.objectives import dpo_step_loss
+    from distributed_llm_alignment_amd.parallel.data_parallel import DataParallelEngine
+
+    cfg = get_config("tiny-llama-d128")
+    out = {}
+    for fused in (False, True):
+        monkeypatch.setattr(transformer, "FUSED_RESIDUAL", fused)
+        pol = build_model(cfg, device=DEV, seed=0)
+        ref = build_model(cfg, device=DEV, seed=1).requires_grad_(False)
+        eng = DataParallelEngine(pol, lr=1e-4)
+        b = synthetic_preference_batch(2, 128, cfg.vocab_size, device=DEV,
+                                       generator=torch.Generator().manual_seed(0), min_len=96)
+        loss, _ = dpo_step_loss(pol, ref, b, beta=0.1)
+        loss.backward()
+        out[fused] = (loss.detach().float(), eng.grad_buf.detach().float().clone())
+    assert abs(out[True][0] - out[False][0]) < 2e-3 * max(1.0, abs(out[False][0]))
+    assert rel_err(out[True][1], out[False][1]) < 3e-2
+
+
 # ------------------------------------------------------------------------------- attention
 @pytest.fixture(params=["4", "8"], ids=["bwd4", "bwd8"])
 def bwd_waves(request, monkeypatch):

@@ -90,6 +90,12 @@ PASSES = {
         run("rlhf8_fp8", "python -u tools/bench_rlhf.py --batch 8 --rollout-dtype fp8", 400),
         run("ppo_zero8_fp8", "python -u tools/bench_rlhf.py --algorithm ppo --zero-shape 8 --batch 8 --rollout-dtype fp8"),
     ],
+    # ---- round 6
+    # residual adds as the C input of the o / down GEMMs (norms read/write one tensor each)
+    "r6-resid": [pytest("tests/test_kernels_gpu.py -k 'fused_residual or norm_fwd_bwd or fused_swiglu'", 300),
+                 ab("fused_resid", DPO + " --steps 5 --warmup 2", {"on": {"DLA_FUSED_RESIDUAL": "1"},
+                                                                   "off": {"DLA_FUSED_RESIDUAL": "0"}}, 2, 300),
+                 prof("dpo", DPO + " --steps 2 --warmup 1", DPO_TABLES)],
     # ---- round 5
     # SwiGLU transposed-output kernels: LDS-tiled vs register transpose (bitwise test, microbench, DPO A/B)
     "ab-swiglu-t-reg": [pytest("tests/test_kernels_gpu.py -k swiglu", 200),
@@ -108,12 +114,6 @@ PASSES = {
     # B = 64 decode attention: key splits per sequence (DLA_DECODE_BLOCKS = target grid)
     "ab-b64-blocks": [ab("b64_blocks", GEN64, {"base": {}, "blk1024": {"DLA_DECODE_BLOCKS": "1024"},
                                                "blk2048": {"DLA_DECODE_BLOCKS": "2048"}}, 2, 300)],
-    # 17..64-row split-K projections: in-kernel last-arriver combine vs the reduce launch
-    "m64-combine": [
-        pytest("tests/test_decode_gpu.py -k 'skinny64 or m64 or b64 or graph or fp8'", 600),
-        ab("m64_combine", GEN64, {"reduce": {}, "combine": {"DLA_M64_COMBINE": "1"}}, 2, 300),
-        ab("m64_combine_fp8", GEN64 + " --weight-dtype fp8", {"reduce": {}, "combine": {"DLA_M64_COMBINE": "1"}}, 2, 300),
-    ],
     # the validation table in two gpurun-sized halves (a call runs at most 20 minutes)
     "validate-a": [],
     "validate-b": [],
@@ -159,11 +159,6 @@ PASSES = {
     # ---- round-4 A/Bs whose knobs are still in the tree (results in README "Tried, measured")
     "ab-dq-bf16": [ab("dq_bf16", DPO + " --steps 4 --warmup 2", {"on": {"DLA_ATTN_DQ_BF16": "1"},
                                                                  "off": {"DLA_ATTN_DQ_BF16": "0"}}, 1, 400)],
-    "ab-qkv-attn": [pytest("tests/test_decode_gpu.py -m gpu -k 'fused_qkv or slab or fsdp'", 300),
-                    ab("qkv_attn", GEN8, {"fused": {"DLA_DECODE_QKV_ATTN": "1"},
-                                          "split": {"DLA_DECODE_QKV_ATTN": "0"}}, 2, 300),
-                    ab("slab_attn", GEN64, {"on": {"DLA_DECODE_SLAB_ATTN": "1"},
-                                            "off": {"DLA_DECODE_SLAB_ATTN": "0"}}, 1, 300)],
     "ab-tn-wgrad-max": [ab("tn_max", DPO + " --steps 6 --warmup 2",
                            {"inf": {"DLA_TN_WGRAD_MAX": "4611686018427387904"},
                             "3e8": {"DLA_TN_WGRAD_MAX": "300000000"}}, 2, 400)],
@@ -178,8 +173,6 @@ PASSES = {
                                   "neither": {"DLA_MOE_SINGLE_LIB": "0", "DLA_EP_NATIVE_ROUTE": "0"}}, 1)],
     "mixtral-ep-degrees": [run(f"ep{ep}", MIX_EP8.replace("--ep-shape 8", f"--ep-shape {ep}") + " --steps 3 --warmup 2")
                            for ep in (4, 2)],
-    "ab-m64-split": [run("m64_probe", "python -u tools/m64_probe.py", 120),
-                     ab("m64_split", GEN64, {"new": {}, "old": {"DLA_M64_WG": "256"}}, 2, 300)],
     "ab-decode-blocks": [ab("blocks", GEN8, {"base": {"DLA_DECODE_RING": "2"},
                                              "b64r3": {"DLA_DECODE_BLOCKS": "64", "DLA_DECODE_RING": "3"},
                                              "b128r3": {"DLA_DECODE_BLOCKS": "128", "DLA_DECODE_RING": "3"},
