@@ -31,6 +31,8 @@
 #include <stdexcept>
 #include <type_traits>
 #include "common.h"
+
+#include <cstring>
 #include "attn_params.h"
 
 namespace dla {
@@ -183,31 +185,12 @@ __device__ __forceinline__ f32x16 unrotate_tile0_rot32(f32x16 x, const float* cp
 // ==============================================================================================
 constexpr int kFwdKeys = 64;      // keys per K/V tile
 
-// Workgroup i of a launch runs on XCD i % 8, and each XCD starts its workgroups in order of i / 8
-// (MI355X_MICROARCH §Workgroup dispatch; a speed assumption only, never a correctness one). The
-// bijective remap (cdna guide §5 'XCD swizzle must be bijective') gives XCD x the contiguous
-// logical range [start_x, start_x + size_x), walked in order; the forward lays logical blocks out
-// (batch, head block)-major with the query blocks of one column adjacent, so the ~32 workgroups an
-// XCD runs at once stream the same one or two K/V sequences through its L2 instead of 32 different
-// ones from HBM / the Infinity Cache.
-__device__ __forceinline__ int fwd_xcd_logical(int bid, int nwg) {
-  const int q = nwg / 8, r = nwg % 8, x = bid % 8;
-  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
-}
-
 // Logical block of item i of persistent workgroup g of G: a snake over the workgroups (causal:
-// heaviest-first blocks, equal tile sums), XCD-grouped as above when G % 8 == 0. Returns nblk
-// past the end (monotone: once past, every later item is past too).
-__device__ __forceinline__ int fwd_persist_logical(int i, int g, int G, int nblk, bool xcd) {
-  if (!xcd || (G & 7) != 0) {
-    const int idx = (i & 1) ? (i + 1) * G - 1 - g : i * G + g;
-    return idx < nblk ? idx : nblk;
-  }
-  const int x = g & 7, l = g >> 3, L = G >> 3;
-  const int bq = nblk >> 3, br = nblk & 7;
-  const int size = bq + (x < br ? 1 : 0), start = x < br ? x * (bq + 1) : br * (bq + 1) + (x - br) * bq;
-  const int idx = (i & 1) ? (i + 1) * L - 1 - l : i * L + l;
-  return idx < size ? start + idx : nblk;
+// heaviest-first blocks, equal tile sums). Returns nblk past the end (monotone: once past, every
+// later item is past too). (An XCD-grouped block order measured 5 % slower causal at T 1024: removed.)
+__device__ __forceinline__ int fwd_persist_logical(int i, int g, int G, int nblk) {
+  const int idx = (i & 1) ? (i + 1) * G - 1 - g : i * G + g;
+  return idx < nblk ? idx : nblk;
 }
 
 // NW waves per workgroup, 32 queries each (NT = 64 NW threads). HP query heads of one GQA group
@@ -237,15 +220,9 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
   const int nhb = p.Hq / HP;  // head blocks
   const int nbh = nhb * p.B;
   const int bid = blockIdx.x;
-  int qb, rest;
-  if (p.fwd_xcd) {  // XCD-grouped: logical = this XCD's contiguous range, (head block, batch)-major
-    const int lg = fwd_xcd_logical(bid, gridDim.x);
-    rest = lg / nqb;
-    qb = CAUSAL ? nqb - 1 - lg % nqb : lg % nqb;
-  } else {  // query block slowest (causal: heaviest first)
-    qb = CAUSAL ? nqb - 1 - bid / nbh : bid / nbh;
-    rest = bid % nbh;
-  }
+  // query block slowest (causal: heaviest first)
+  const int qb = CAUSAL ? nqb - 1 - bid / nbh : bid / nbh;
+  const int rest = bid % nbh;
   const int hq = (rest % nhb) * HP + w / WPH, b = rest / nhb;
   const int hk = hq / (p.Hq / p.Hkv);  // the same for the HP heads (host: group % HP == 0)
   const int q0 = qb * BQ + (w % WPH) * 32;
@@ -724,17 +701,11 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_persist_kernel(AttnParams p,
   };
   auto make_blk = [&](int i) -> Blk {
     Blk c{};
-    const int blk = fwd_persist_logical(i, g, G, nblk, p.fwd_xcd != 0);
+    const int blk = fwd_persist_logical(i, g, G, nblk);
     c.valid = blk < nblk;
     if (!c.valid) return c;
-    int qb, rest;
-    if (p.fwd_xcd && (G & 7) == 0) {
-      rest = blk / nqb;
-      qb = CAUSAL ? nqb - 1 - blk % nqb : blk % nqb;
-    } else {
-      qb = CAUSAL ? nqb - 1 - blk / nbh : blk / nbh;
-      rest = blk % nbh;
-    }
+    const int qb = CAUSAL ? nqb - 1 - blk / nbh : blk / nbh;
+    const int rest = blk % nbh;
     c.hq = (rest % nhb) * HP + w / WPH;
     c.b = rest / nhb;
     c.hk = c.hq / (p.Hq / p.Hkv);
@@ -1045,8 +1016,6 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_persist_kernel(AttnParams p,
 // ==============================================================================================
 // backward preprocessing: delta[b,h,t] = sum_d dO * O   (one wave per (b, t, h) row)
 // ==============================================================================================
-// kDeltaRows: rows per lane group (1, the default, or 4 with DLA_ATTN_DELTA_ROWS=4)
-template <int kDeltaRows>
 __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(const bf16_t* __restrict__ o,
                                                               const bf16_t* __restrict__ dout,
                                                               int64_t o_sb, int64_t o_st,
@@ -1055,9 +1024,9 @@ __global__ __launch_bounds__(256) void attn_bwd_delta_kernel(const bf16_t* __res
                                                               int B, int H, int T, int D,
                                                               float* __restrict__ delta) {
   // delta[row] = <O[row], dO[row]>: D/8 lanes x 16-B loads per row (16 lanes at D = 128),
-  // 64 / (D/8) row groups per wave, kDeltaRows consecutive rows per lane group (all their loads
-  // in flight before any use: 4x the bytes per lane of one row), shuffle reduction inside the
-  // lane group -- per row the same arithmetic as one row per group
+  // 64 / (D/8) rows per wave, shuffle reduction inside the lane group. (Four rows per lane group
+  // measured bitwise equal and slower inside the DPO step, 30.1 vs 27.3 us: removed.)
+  constexpr int kDeltaRows = 1;
   const int lpr = D <= 64 ? 8 : 16;  // lanes per row (power of two; D = 80: 10 of 16 load)
   const int lane = threadIdx.x & 63;
   const int64_t row0 = ((blockIdx.x * 4ll + (threadIdx.x >> 6)) * (64 / lpr) + lane / lpr) * kDeltaRows;
@@ -1786,10 +1755,9 @@ __global__ __launch_bounds__(512) void attn_bwd8_kernel(AttnBwdParams p) {
 
   // static priority for the second-dispatched half (waves 4-7 share SIMDs with 0-3 and lose
   // every VALU arbitration by age otherwise; MI355X_MICROARCH "Two waves per SIMD" item 4)
-  const bool cprio = p.bwd_prio != 0;  // per-cluster priority flips (A/B, DLA_ATTN_BWD_PRIO)
-  if (p.bwd_prio != 1 && w >= 4) __builtin_amdgcn_s_setprio(1);
-  auto prio_on = [&]() { if (cprio) __builtin_amdgcn_s_setprio(1); };
-  auto prio_off = [&]() { if (cprio && (p.bwd_prio == 1 || w < 4)) __builtin_amdgcn_s_setprio(0); };
+  // (per-MFMA-cluster s_setprio flips on top measured as noise: the clusters are already pinned
+  // by sched_barriers; removed)
+  if (w >= 4) __builtin_amdgcn_s_setprio(1);
   for (int it = 0; it < n_iter; ++it) {
     advance(hq_r, qt_r);
     asm volatile("" : "+v"(rq), "+v"(rx), "+v"(tq0), "+v"(tx0), "+v"(tq1), "+v"(tx1), "+v"(wq), "+v"(wx));
@@ -1832,7 +1800,6 @@ __global__ __launch_bounds__(512) void attn_bwd8_kernel(AttnBwdParams p) {
           __builtin_amdgcn_sched_barrier(0);
         }
       };
-      prio_on();
       chain(Qs, Kw, sacc);
       chain(dOs, Vw, dpacc);
       {  // + the row-constant k-step (last: its loads get the whole chains as slack)
@@ -1847,7 +1814,6 @@ __global__ __launch_bounds__(512) void attn_bwd8_kernel(AttnBwdParams p) {
         sacc = mfma32(ax, ones, sacc);
         dpacc = mfma32(ay, ones, dpacc);
       }
-      prio_off();
       BWD_TS(1);
       const int kj = kw + l32;
       int lo = 0, hi = min(p.Tq, kse) - qt - 4 * h;
@@ -1888,7 +1854,6 @@ __global__ __launch_bounds__(512) void attn_bwd8_kernel(AttnBwdParams p) {
       };
       ld_kv(0, 0);
       __builtin_amdgcn_sched_barrier(0);
-      prio_on();
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
         if (dt + 1 < DT) ld_kv(dt + 1, (dt + 1) & 1);
@@ -1900,7 +1865,6 @@ __global__ __launch_bounds__(512) void attn_bwd8_kernel(AttnBwdParams p) {
         dk[dt] = mfma32(td[dt & 1], sb1, dk[dt]);
         __builtin_amdgcn_sched_barrier(0);
       }
-      prio_off();
       BWD_TS(3);
     }
     {  // dS^T rows -> [key][32 queries] image (zero for an inactive sub-tile)
@@ -1937,7 +1901,6 @@ __global__ __launch_bounds__(512) void attn_bwd8_kernel(AttnBwdParams p) {
       };
       ld_dq(0, 0);
       ld_dq(1, 1);
-      prio_on();
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) {
         if (ks + 2 < NKS) ld_dq(ks + 2, (ks + 2) % NB);
@@ -1947,7 +1910,6 @@ __global__ __launch_bounds__(512) void attn_bwd8_kernel(AttnBwdParams p) {
           acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks % NB][t], kf[ks % NB], acc[t], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
       }
-      prio_off();
       // lane holds d = 16*slice + i16 of query rows 16t + 4*g4l + e (64-B row segments)
       const int64_t rs = static_cast<int64_t>(p.Hq) * D;
       const int64_t sbase = ((static_cast<int64_t>(kb) * p.B + b) * p.slab_rows + qt) * rs +
@@ -2259,12 +2221,8 @@ __global__ __launch_bounds__(256) void attn_dkv_reduce_kernel(
 // launchers
 // ----------------------------------------------------------------------------------------------
 static inline unsigned stream_grid(int64_t work) {
-  // grid-stride cap of the reduce passes (DLA_ATTN_REDUCE_GRID, A/B; default 2048 workgroups)
-  static const int64_t cap = [] {
-    const char* e = std::getenv("DLA_ATTN_REDUCE_GRID");
-    const int64_t v = e ? std::atoll(e) : 2048;
-    return v > 0 ? v : 2048;
-  }();
+  // grid-stride cap of the reduce passes: 1024 / 8192 / 32768 measured as noise against 2048
+  constexpr int64_t cap = 2048;
   int64_t g = (work + 255) / 256;
   if (g > cap) g = cap;
   return static_cast<unsigned>(g < 1 ? 1 : g);
@@ -2299,35 +2257,59 @@ static int device_cus() {
   return cached[dev];
 }
 
-// XCD-grouped block order: opt-in (DLA_ATTN_FWD_XCD=1). It did not move the kernel at T >= 1024
-// (the tile loop is VALU / issue bound, not K/V-stream bound) and cost 5 % causal at T 1024.
-static int fwd_xcd_order() {
-  const char* e = std::getenv("DLA_ATTN_FWD_XCD");
-  return (e != nullptr && std::atoi(e) != 0) ? 1 : 0;
+struct AttnFwdSwitches {
+  int prio, sgpr, pro, ostage, msub;
+};
+
+// Read from the environment once per process; tests flip a switch through attn_fwd_set_switch
+// (torch.ops.dla.attn_fwd_switch) instead of re-reading the environment on every launch.
+static AttnFwdSwitches& attn_fwd_switches() {
+  static AttnFwdSwitches sw = [] {
+    auto env = [](const char* name, int dflt) {
+      const char* e = std::getenv(name);
+      return e ? std::atoi(e) : dflt;
+    };
+    return AttnFwdSwitches{env("DLA_ATTN_FWD_PRIO", 1), env("DLA_ATTN_FWD_SGPR", 1), env("DLA_ATTN_FWD_PRO", 1),
+                           env("DLA_ATTN_FWD_OSTAGE", 1), env("DLA_ATTN_FWD_MSUB", 1)};
+  }();
+  return sw;
+}
+
+// Set one switch ("prio", "sgpr", "pro", "ostage", "msub"); returns its previous value, or
+// -1 for an unknown name (nothing changed).
+int attn_fwd_set_switch(const char* name, int value) {
+  AttnFwdSwitches& sw = attn_fwd_switches();
+  int* f = nullptr;
+  if (!std::strcmp(name, "prio")) f = &sw.prio;
+  else if (!std::strcmp(name, "sgpr")) f = &sw.sgpr;
+  else if (!std::strcmp(name, "pro")) f = &sw.pro;
+  else if (!std::strcmp(name, "ostage")) f = &sw.ostage;
+  else if (!std::strcmp(name, "msub")) f = &sw.msub;
+  if (f == nullptr) return -1;
+  const int prev = *f;
+  *f = value;
+  return prev;
 }
 
 template <int D, int HP>
 static void fwd_launch(const AttnParams& p0, bool causal, hipStream_t st) {
   constexpr int NW = 8, BQ = 32 * NW / HP;
   AttnParams p = p0;
-  p.fwd_xcd = fwd_xcd_order();
   {
-    // 1 (default): s_setprio 1 around each MFMA chain, so the matrix chain of one wave issues
-    // ahead of its SIMD partner's softmax VALU (cdna guide T5). Same box, graph-timed, B*T 8192:
-    // causal T1024 654 vs 613 TF/s, T4096 937 vs 897; non-causal +4-6 %. 2 (static priority for
-    // waves 4-7) measured +0-7 % and below 1 everywhere; 0 = off.
-    const char* e = std::getenv("DLA_ATTN_FWD_PRIO");
-    p.fwd_prio = e ? std::atoi(e) : 1;
-    const char* g = std::getenv("DLA_ATTN_FWD_SGPR");
-    p.fwd_sgpr = g ? std::atoi(g) : 1;
-    const char* r = std::getenv("DLA_ATTN_FWD_PRO");
-    p.fwd_pro = r ? std::atoi(r) : 1;
-    const char* os = std::getenv("DLA_ATTN_FWD_OSTAGE");
-    p.fwd_ostage = os ? std::atoi(os) : 1;
-    // MSUB (D = 128): same box, graph-timed, interleaved: causal T1024 701 vs 668 TF/s, T2048
-    // 898 vs 865, non-causal +3-7 % (gpurun_out/r5/attn13); outputs within one bf16 ulp
-    const char* mx = std::getenv("DLA_ATTN_FWD_MSUB");
-    p.fwd_msub = mx ? std::atoi(mx) : 1;
+    // The forward's structure switches, read ONCE per process (attn_fwd_switches; every switch
+    // defaults to its measured winner, the others exist for same-binary A/B runs):
+    //   prio 1: s_setprio 1 around each MFMA chain, so the matrix chain of one wave issues ahead
+    //     of its SIMD partner's softmax VALU (cdna guide T5). Same box, graph-timed, B*T 8192:
+    //     causal T1024 654 vs 613 TF/s, T4096 937 vs 897; non-causal +4-6 %. 2 (static priority
+    //     for waves 4-7) measured +0-7 % and below 1 everywhere; 0 = off.
+    //   msub (D = 128): same box, graph-timed, interleaved: causal T1024 701 vs 668 TF/s, T2048
+    //     898 vs 865, non-causal +3-7 % (gpurun_out/r5/attn13); outputs within one bf16 ulp
+    const AttnFwdSwitches& sw = attn_fwd_switches();
+    p.fwd_prio = sw.prio;
+    p.fwd_sgpr = sw.sgpr;
+    p.fwd_pro = sw.pro;
+    p.fwd_ostage = sw.ostage;
+    p.fwd_msub = sw.msub;
   }
   const int nqb = (p.Tq + BQ - 1) / BQ;
   const int64_t nblk = static_cast<int64_t>(nqb) * (p.Hq / HP) * p.B;
@@ -2378,18 +2360,9 @@ void launch_attn_bwd_delta(const bf16_t* o, const bf16_t* dout, int64_t o_sb, in
                            int H, int T, int D, float* delta, hipStream_t st) {
   const int64_t rows = static_cast<int64_t>(B) * H * T;
   if (rows == 0) return;
-  // DLA_ATTN_DELTA_ROWS=4: four rows per lane group (read per call, A/B in one process). Bitwise
-  // equal; 351.7 vs 352.7 us for the whole backward in tools/attn_bench.py, but 30.1 vs 27.3 us per
-  // call inside the DPO step (two profiles, different boxes: profiles/r5_dpo_kernels.md), so one row
-  // per group stays the default.
-  const char* e = std::getenv("DLA_ATTN_DELTA_ROWS");
-  const int rpl = (e && std::atoi(e) == 4) ? 4 : 1;
-  const int64_t rows_per_block = 4 * (64 / (D <= 64 ? 8 : 16)) * rpl;  // as attn_bwd_delta_kernel
+  const int64_t rows_per_block = 4 * (64 / (D <= 64 ? 8 : 16));  // as attn_bwd_delta_kernel
   const unsigned nb = static_cast<unsigned>((rows + rows_per_block - 1) / rows_per_block);
-  if (rpl == 1)
-    attn_bwd_delta_kernel<1><<<nb, 256, 0, st>>>(o, dout, o_sb, o_st, o_sh, do_sb, do_st, do_sh, B, H, T, D, delta);
-  else
-    attn_bwd_delta_kernel<4><<<nb, 256, 0, st>>>(o, dout, o_sb, o_st, o_sh, do_sb, do_st, do_sh, B, H, T, D, delta);
+  attn_bwd_delta_kernel<<<nb, 256, 0, st>>>(o, dout, o_sb, o_st, o_sh, do_sb, do_st, do_sh, B, H, T, D, delta);
 }
 
 // Backward main kernel: attn_bwd8_kernel (8 waves, default) or attn_bwd_kernel
@@ -2415,12 +2388,7 @@ bool attn_dkv_part_bf16() {
 
 template <int D>
 static void bwd_dispatch(const AttnBwdParams& p_in, bool causal, hipStream_t st) {
-  AttnBwdParams p = p_in;
-  {
-    const char* e = std::getenv("DLA_ATTN_BWD_PRIO");  // A/B, read per call
-    p.bwd_prio = e ? std::atoi(e) : 0;
-
-  }
+  const AttnBwdParams& p = p_in;
   const int nkb = (p.Tk + kAttnBwdKeys - 1) / kAttnBwdKeys;
   const dim3 grid(nkb * p.Hkv * p.B * p.hsplit);
   if (attn_bwd_waves() == 8) {

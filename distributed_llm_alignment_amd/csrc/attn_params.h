@@ -30,9 +30,7 @@ struct AttnParams {
   const int* rope_pos;    // [B * T] token positions, or null: position = t
   bf16_t* q_rot;          // optional [B, T, Hq, D] out: the rotated Q (what the backward reads)
   int64_t qr_sb, qr_st, qr_sh;
-  // forward block order (set by the launcher): 1 = XCD-grouped, each XCD walks whole (batch,
-  // head block) query columns so the concurrent workgroups of one L2 share every K/V tile
-  int fwd_xcd;
+  // forward structure switches (set once per process by the launcher, attn_fwd_switches)
   int fwd_prio;  // issue priority A/B (DLA_ATTN_FWD_PRIO): 1 = s_setprio 1 around each MFMA chain,
   int fwd_sgpr;   // 1: whole K/V tiles load from an SGPR tile base + 32-bit lane offsets (A/B: DLA_ATTN_FWD_SGPR=0)
   int fwd_pro;    // 1: K/V tile-0 loads issued right after the Q loads (A/B: DLA_ATTN_FWD_PRO=0)
@@ -90,7 +88,6 @@ struct AttnBwdParams {
                           // forward's q_rot output)
   int rope_rot;           // rotary dims: D (full), or 32 at D = 80 (phi-2's partial rotary:
                           // only dims [0, 32) rotate, d < 16 pairing with d + 16)
-  int bwd_prio;           // issue priority (attn_bwd8_kernel): 0 static for waves 4-7, 1 s_setprio
                           // 1 around every MFMA cluster, 2 both
 };
 

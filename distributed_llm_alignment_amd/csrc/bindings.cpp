@@ -68,6 +68,7 @@ int sumsq_grid(int64_t n);
 void launch_clip_coef(const float*, float, float*, float*, hipStream_t);
 
 void launch_attn_fwd(const AttnParams&, int, bool, hipStream_t);
+int attn_fwd_set_switch(const char* name, int value);
 void launch_attn_bwd_delta(const bf16_t*, const bf16_t*, int64_t, int64_t, int64_t, int64_t,
                            int64_t, int64_t, int, int, int, int, float*, hipStream_t);
 void launch_attn_bwd(const AttnBwdParams&, int, bool, hipStream_t);
@@ -878,6 +879,15 @@ std::tuple<at::Tensor, at::Tensor> clip_coef(const at::Tensor& sumsq, double max
   return {norm, coef};
 }
 
+// Flip one attention-forward structure switch for this process (tests / same-binary A/B): the
+// launcher reads DLA_ATTN_FWD_{PRIO,SGPR,PRO,OSTAGE,MSUB} once; returns the previous value.
+int64_t attn_fwd_switch(c10::string_view name, int64_t value) {
+  const std::string n(name.data(), name.size());
+  const int prev = attn_fwd_set_switch(n.c_str(), static_cast<int>(value));
+  TORCH_CHECK(prev != -1, "attn_fwd_switch: unknown switch ", n);
+  return prev;
+}
+
 }  // namespace dla
 
 TORCH_LIBRARY(dla, m) {
@@ -894,6 +904,7 @@ TORCH_LIBRARY(dla, m) {
   m.def("attn_fwd(Tensor q, Tensor k, Tensor v, float scale, bool causal, int causal_off, int window, Tensor? kv_start, Tensor? kv_end, Tensor? segs=None, Tensor? rope_cos=None, Tensor? rope_sin=None, Tensor? rope_pos=None, Tensor(a!)? q_rot=None) -> (Tensor, Tensor)");
   m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse2, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, float scale, bool causal, int causal_off, int window, Tensor? kv_start, Tensor? kv_end, Tensor? segs=None, Tensor? rope_cos=None, Tensor? rope_sin=None, Tensor? rope_pos=None, bool rope_inputs=False) -> ()");
   m.def("attn_stamps(Tensor like) -> Tensor");
+  m.def("attn_fwd_switch(str name, int value) -> int", &dla::attn_fwd_switch);
   m.def("transpose_bf16(Tensor input, Tensor(a!) out) -> ()");
   m.def("logprob_fwd(Tensor logits, Tensor targets, int vocab_offset=0) -> (Tensor, Tensor)");
   m.def("logprob_bwd(Tensor(a!) logits, Tensor targets, Tensor lse, Tensor grad, int vocab_offset=0) -> ()");

@@ -744,9 +744,10 @@ def test_fp8_generation_graph_matches_eager_and_tracks_bf16(B):
     assert getattr(m.layers[0].mlp.down_proj, "_dla_f8", None) is not None  # the fp8 path ran
     clear_graph_cache()
     a = generate(m, ids, max_new_tokens=12, do_sample=False, eos_token_id=-1, use_graph=False, weight_dtype="fp8")
-    # the prefill ran the fp8 inference GEMMs (their weight copy exists) and the marking is undone
+    # after the prefill's fp8 inference scope the marking is undone and its e4m3 weight copy is
+    # dropped (not left resident on a trainable policy between rollouts)
     w0 = m.layers[0].mlp.up_proj
-    assert getattr(w0, "_dla_fp8", None) is not None and not getattr(w0, "_dla_fp8_infer", False)
+    assert getattr(w0, "_dla_fp8", None) is None and not getattr(w0, "_dla_fp8_infer", False)
     b = generate(m, ids, max_new_tokens=12, do_sample=False, eos_token_id=-1, use_graph=True, weight_dtype="fp8")
     assert torch.equal(a, b)
     # weights move (an optimizer step): the in-place refreshed fp8 copies follow, graph reused

@@ -1054,24 +1054,20 @@ def test_attention_fwd_persistent_bitwise(case, monkeypatch):
         extra = (cos, sin, None)
     outs = {}
     # the persistent kernel runs the lockstep kernel's tile math without the in-MFMA max
-    # subtraction (DLA_ATTN_FWD_MSUB, D = 128 lockstep only; covered by the fp32-oracle tests)
-    monkeypatch.setenv("DLA_ATTN_FWD_MSUB", "0")
-    # (ping-pong, persistent, XCD block order): "000" is the one-block-per-workgroup lockstep kernel
-    for pp, persist, xcd in (("0", "0", "0"), ("0", "0", "1"), ("0", "1", "0"), ("0", "1", "1"),
-                             ("1", "0", "0"), ("1", "0", "1")):
-        monkeypatch.setenv("DLA_ATTN_FWD_PP", pp)
-        monkeypatch.setenv("DLA_ATTN_FWD_PERSIST", persist)
-        monkeypatch.setenv("DLA_ATTN_FWD_XCD", xcd)
-        qr = torch.empty_like(q) if rope else None
-        o, lse = C.attn_fwd(q, k, v, 1.0 / math.sqrt(D), causal, off, window, ks, ke, segs, *extra,
-                            *((qr,) if rope else ()))
-        torch.cuda.synchronize()
-        outs[pp + persist + xcd] = (o, lse, qr)
-    o0, l0, q0 = outs["000"]
-    o1, l1, q1 = outs["011"]
-    for key in ("001", "010", "100", "101"):
-        ref_o, ref_l = (o1, l1) if key == "010" else (o0, l0)
-        assert torch.equal(outs[key][0], ref_o) and torch.equal(outs[key][1], ref_l), f"variant {key} changed O/LSE"
+    # subtraction (the "msub" switch, D = 128 lockstep only; covered by the fp32-oracle tests)
+    prev = C.attn_fwd_switch("msub", 0)
+    try:
+        for persist in ("0", "1"):  # "0": the one-block-per-workgroup lockstep kernel
+            monkeypatch.setenv("DLA_ATTN_FWD_PERSIST", persist)
+            qr = torch.empty_like(q) if rope else None
+            o, lse = C.attn_fwd(q, k, v, 1.0 / math.sqrt(D), causal, off, window, ks, ke, segs, *extra,
+                                *((qr,) if rope else ()))
+            torch.cuda.synchronize()
+            outs[persist] = (o, lse, qr)
+    finally:
+        C.attn_fwd_switch("msub", prev)
+    o0, l0, q0 = outs["0"]
+    o1, l1, q1 = outs["1"]
     if rope:  # the rotation's a*c - b*s may contract to different FMAs in the two kernels
         assert rel_err(o1, o0) < 5e-3 and rel_err(q1, q0) < 5e-3, "RoPE-on-load output differs"
         assert (l1 - l0).abs().max().item() < 5e-2, "LSE differs"
