@@ -34,18 +34,10 @@ constexpr int kSkCols = 16 * kSkWaves;  // output columns (weight rows) per work
 constexpr int kSkUnroll = 8;          // k-steps (32 each) of weight loads in flight per wave
 constexpr int kSkChunk = 32 * kSkUnroll;
 
-// DLA_SKINNY_NT=1: non-temporal weight loads in every skinny kernel (read once per process)
-bool skinny_nt() {
-  static const bool nt = [] {
-    const char* e = getenv("DLA_SKINNY_NT");
-    return e != nullptr && atoi(e) != 0;
-  }();
-  return nt;
-}
-
 // Non-temporal loads on the TILED decode weight streams (each byte read once per step by one CU):
 // 3.54 vs 3.70 ms/token at B=8 (profiles/r3_decode_tiled.md). On the row-major layout nt lost
-// (DLA_SKINNY_NT above). DLA_DECODE_NT=0 turns it off.
+// (4.31 vs 4.19 ms/token: the weights rotated past the Infinity Cache), so the row-major kernels
+// use default-policy loads. DLA_DECODE_NT=0 turns it off.
 static bool decode_nt() {
   static const bool nt = [] {
     const char* e = getenv("DLA_DECODE_NT");
@@ -402,10 +394,7 @@ void launch_skinny_gemm_t(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t
 void launch_skinny_gemm(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
                         int64_t ldy, float* ws, unsigned* counters, int M, int N, int K, int S,
                         bool swiglu, bool glu_out, hipStream_t st) {
-  if (skinny_nt())
-    launch_skinny_gemm_t<true>(x, ldx, W, ldw, y, ldy, ws, counters, M, N, K, S, swiglu, glu_out, st);
-  else
-    launch_skinny_gemm_t<false>(x, ldx, W, ldw, y, ldy, ws, counters, M, N, K, S, swiglu, glu_out, st);
+  launch_skinny_gemm_t<false>(x, ldx, W, ldw, y, ldy, ws, counters, M, N, K, S, swiglu, glu_out, st);
 }
 
 // Narrow outputs (N <= ~16K: qkv, o, down at Llama-3-8B): ONE workgroup per 16 output columns,
@@ -433,10 +422,13 @@ __global__ __launch_bounds__(512) void skinny_ksplit_kernel(
 // fused decode-layer launches (KsFuse): the residual-producing projection and the
 // norm-consuming qkv projection on the in-workgroup split-K kernel, the gate|up GLU on the LDS
 // kernel. M <= 16.
-// DLA_SKINNY_STRAIGHT (A/B, read per launch): ks_body's branch-free ring (KsFuse::straight)
+// ks_body's branch-free ring (KsFuse::straight; DLA_SKINNY_STRAIGHT=0 for A/B, read once)
 static int ks_straight() {
-  const char* e = getenv("DLA_SKINNY_STRAIGHT");
-  return e ? atoi(e) : 1;
+  static const int v = [] {
+    const char* e = getenv("DLA_SKINNY_STRAIGHT");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
 }
 
 template <bool TW, bool NT, bool F8 = false>
@@ -756,19 +748,13 @@ static void launch_ks(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw
 
 void launch_skinny_ksplit(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
                           int64_t ldy, int M, int N, int K, hipStream_t st) {
-  if (skinny_nt())
-    launch_ks<true, false>(x, ldx, W, ldw, y, ldy, M, N, K, N / 16, st);
-  else
-    launch_ks<false, false>(x, ldx, W, ldw, y, ldy, M, N, K, N / 16, st);
+  launch_ks<false, false>(x, ldx, W, ldw, y, ldy, M, N, K, N / 16, st);
 }
 
 // gate|up (N = 2F weight rows) -> m = silu(gate) * up [M, F], F / 16 workgroups
 void launch_skinny_glu_ks(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
                           int64_t ldy, int M, int N, int K, hipStream_t st) {
-  if (skinny_nt())
-    launch_ks<true, true>(x, ldx, W, ldw, y, ldy, M, N, K, N / 32, st);
-  else
-    launch_ks<false, true>(x, ldx, W, ldw, y, ldy, M, N, K, N / 32, st);
+  launch_ks<false, true>(x, ldx, W, ldw, y, ldy, M, N, K, N / 32, st);
 }
 
 }  // namespace dla

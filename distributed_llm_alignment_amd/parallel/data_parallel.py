@@ -74,7 +74,6 @@ class DataParallelEngine:
                  dist_st: Optional[DistState] = None, group=None, tp_group=None, expert_group=None,
                  overlap_param_gather: bool = os.environ.get("DLA_OVERLAP_AG", "1") != "0",
                  sp_size: int = 1,
-                 overlap_optimizer: bool = os.environ.get("DLA_OVERLAP_OPT", "0") == "1",
                  grad_dtype: Optional[torch.dtype] = None, reduce_dtype: Optional[torch.dtype] = None,
                  shape_world: int = 1, force_comm: Optional[bool] = None):
         """`shape_world` > 1 (debug / benchmarking, one process only): lay the engine out as rank 0
@@ -263,19 +262,10 @@ class DataParallelEngine:
         self._ag_pending: Dict[int, object] = {}
         module._dla_dp_engine = self
         self.overlap_param_gather = overlap_param_gather and self.zero and self._comm
-        # Unsharded state (1 GPU, or ZeRO-0): the fused AdamW runs per bucket on its own HIP
-        # stream, in the order the previous forward first touched the buckets, and zeroes each
-        # bucket's grads behind it; the same pre-hooks make a module's forward wait (device-side
-        # event, no host sync) only for its own buckets, so the optimizer step of later layers
-        # overlaps the next forward. Off by default: on 1x MI355X (Llama-3-8B DPO, interleaved
-        # A/B, tools/ab_overlap_opt.sh) it measured 0.3-0.5 % slower (1640-1645 vs 1635-1637
-        # ms/step) — the bandwidth-bound AdamW only steals HBM and power from the forward GEMMs.
-        self.overlap_opt = bool(overlap_optimizer) and not self.zero and self.device.type == "cuda"
-        self._opt_events: Dict[int, object] = {}
-        self._opt_stream = None
-        self._fwd_order: List[int] = []
-        self._fwd_seen = set()
-        if self.overlap_param_gather or self.overlap_opt:
+        # (A per-bucket AdamW on a side stream overlapped with the next forward measured 0.3-0.5 %
+        # slower on 1x MI355X -- the bandwidth-bound update only takes HBM and power from the
+        # forward GEMMs -- and was removed; README "Tried".)
+        if self.overlap_param_gather:
             for mod in module.modules():
                 own = [self._bucket_of[id(p)] for p in mod.parameters(recurse=False) if id(p) in self._bucket_of]
                 if own:
@@ -284,22 +274,11 @@ class DataParallelEngine:
     # ------------------------------------------------------------------------ helpers
     def _make_wait_hook(self, buckets):
         def hook(_mod, _inp):
-            if len(self._fwd_seen) < len(self.buckets):  # first-use order for the optimizer
-                for bi in buckets:
-                    if bi not in self._fwd_seen:
-                        self._fwd_seen.add(bi)
-                        self._fwd_order.append(bi)
             if self._ag_pending:
                 for bi in buckets:
                     h = self._ag_pending.pop(bi, None)
                     if h is not None:
                         h.wait()
-            if self._opt_events and not torch.cuda.is_current_stream_capturing():
-                cur = torch.cuda.current_stream(self.device)
-                for bi in buckets:
-                    ev = self._opt_events.pop(bi, None)
-                    if ev is not None:
-                        cur.wait_event(ev)
         return hook
 
     def wait_params(self):
@@ -308,11 +287,6 @@ class DataParallelEngine:
         for h in self._ag_pending.values():
             h.wait()
         self._ag_pending.clear()
-        if self._opt_events:
-            cur = torch.cuda.current_stream(self.device)
-            for ev in self._opt_events.values():
-                cur.wait_event(ev)
-            self._opt_events.clear()
 
     def _chunk(self, buf: torch.Tensor, b: Bucket) -> torch.Tensor:
         c = b.size // b.world
@@ -479,10 +453,6 @@ class DataParallelEngine:
         lr = self.lr if lr is None else lr
         coef = self.clip_and_norm()
         self.step_count += 1
-        if self.overlap_opt:
-            self._overlapped_adamw(lr, coef)
-            self._wt_epoch[0] += 1
-            return self.last_grad_norm
         adamw_update(self.param_shard, self.master, self.grad_shard, self.exp_avg, self.exp_avg_sq,
                      lr, self.betas[0], self.betas[1], self.eps, self.wd, self.step_count,
                      clip=coef if self.max_grad_norm else None, grad_scale=self.grad_scale)
@@ -506,33 +476,7 @@ class DataParallelEngine:
         self.zero_grad()
         return self.last_grad_norm
 
-    def _overlapped_adamw(self, lr, coef):
-        self.wait_params()  # a previous step's updates not yet consumed by a forward
-        main = torch.cuda.current_stream(self.device)
-        if self._opt_stream is None:
-            self._opt_stream = torch.cuda.Stream(device=self.device)
-        side = self._opt_stream
-        side.wait_stream(main)  # grads complete, clip coefficient computed
-        clip = coef if self.max_grad_norm else None
-        if clip is not None:
-            clip.record_stream(side)
-        n = len(self.buckets)
-        order = list(self._fwd_order) + [bi for bi in reversed(range(n)) if bi not in self._fwd_seen]
-        with torch.cuda.stream(side):
-            for bi in order:
-                b = self.buckets[bi]
-                sl = slice(b.start, b.end)
-                adamw_update(self.param_buf[sl], None if self.master is None else self.master[sl],
-                             self.grad_buf[sl], self.exp_avg[sl], self.exp_avg_sq[sl], lr,
-                             self.betas[0], self.betas[1], self.eps, self.wd, self.step_count,
-                             clip=clip, grad_scale=self.grad_scale)
-                self.grad_buf[sl].zero_()
-                ev = torch.cuda.Event()
-                ev.record(side)
-                self._opt_events[bi] = ev
-
     def zero_grad(self):
-        self.wait_params()  # an overlapped optimizer step still owns the grad buffer
         for h, _ in self._handles:  # collectives still reading/writing the buffers (an aborted pass)
             h.wait()
         self._reset_pass_state()

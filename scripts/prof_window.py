@@ -5,7 +5,10 @@
 
 --window adamw: only the kernels between the last two fused-AdamW launches (one optimizer step
 of bench.py); --by-grid: group by (kernel, grid size) -- GEMM shapes show up as distinct grids;
---per N: divide totals by N (e.g. decode steps x layers) to get per-unit averages."""
+--per N: divide totals by N (e.g. decode steps x layers) to get per-unit averages;
+--seq START:COUNT: instead of the table, list COUNT launches of the window in issue order from
+launch START (negative START counts from the end), with their grids and durations -- which GEMM
+sits where in a layer's forward / backward, and what each call costs in place."""
 import argparse
 import collections
 import csv
@@ -19,6 +22,7 @@ def main():
     ap.add_argument("--by-grid", action="store_true")
     ap.add_argument("--per", type=float, default=1.0)
     ap.add_argument("--match", default=None, help="only kernels whose name contains this")
+    ap.add_argument("--seq", default=None, help="START:COUNT launches in issue order")
     a = ap.parse_args()
     rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestamp"]))
     if a.window == "adamw":
@@ -26,6 +30,16 @@ def main():
         rows = rows[ad[-2] + 1:ad[-1] + 1]
     if a.match:
         rows = [r for r in rows if a.match in r["Kernel_Name"]]
+    if a.seq:
+        st, cnt = (int(x) for x in a.seq.split(":"))
+        sel = rows[st:st + cnt] if st >= 0 else rows[len(rows) + st:len(rows) + st + cnt]
+        print("| # | us | grid | kernel |")
+        print("|---|---|---|---|")
+        for i, r in enumerate(sel):
+            d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+            g = "x".join(r.get(k, "?") for k in ("Grid_Size_X", "Grid_Size_Y", "Grid_Size_Z"))
+            print(f"| {i} | {d:.1f} | {g} | `{r['Kernel_Name'][:90]}` |")
+        return
     agg = collections.defaultdict(lambda: [0.0, 0])
     for r in rows:
         d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3

@@ -96,6 +96,11 @@ PASSES = {
                  ab("fused_resid", DPO + " --steps 5 --warmup 2", {"on": {"DLA_FUSED_RESIDUAL": "1"},
                                                                    "off": {"DLA_FUSED_RESIDUAL": "0"}}, 2, 300),
                  prof("dpo", DPO + " --steps 2 --warmup 1", DPO_TABLES)],
+    # the whole DPO step's launches in issue order (which GEMM runs where, at what cost in place)
+    # and the GEMM probe's arms under a kernel trace (which library kernel each form picks)
+    "r6-seq": [prof("dpo_seq", DPO + " --steps 2 --warmup 1", [("window", ["--window", "adamw", "--seq", "0:7000"])]),
+               prof("gemm_probe", "python -u tools/gemm_m_probe.py --model llama3-8b --ms 8192 --resid",
+                    [("window", ["--by-grid", "--top", "40"])], 300)],
     # ---- round 5
     # SwiGLU transposed-output kernels: LDS-tiled vs register transpose (bitwise test, microbench, DPO A/B)
     "ab-swiglu-t-reg": [pytest("tests/test_kernels_gpu.py -k swiglu", 200),
