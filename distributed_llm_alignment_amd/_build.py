@@ -130,7 +130,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False,
     if force or tasks or not out_so.exists() or any(o.stat().st_mtime > out_so.stat().st_mtime for o in objs):
         tmp = out_so.with_suffix(".so.tmp")
         _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *hsan, "-o", str(tmp), *map(str, objs),
-              f"-L{lib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
+              f"-L{lib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-lhipblaslt",
               f"-Wl,-rpath,{lib}"])
         os.replace(tmp, out_so)
     return out_so

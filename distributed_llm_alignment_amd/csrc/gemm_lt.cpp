@@ -1,0 +1,206 @@
+// Residual-fused projection GEMM on hipBLASLt with separate C and D: out = c + x @ w^T.
+//
+// torch.addmm(c, x, w.t()) first copies c into the output and then runs a beta = 1 GEMM in place
+// (one extra read + write of the [M, N] stream per call: 25-30 us for an [8192, 4096] bf16 stream,
+// measured in the DPO step, profiles/r6_dpo_kernels.md); hipBLASLt itself takes C and D as two
+// buffers, so the residual is read once by the GEMM epilogue and never copied. This lets the
+// decoder's o / down projections add their output onto the residual stream inside the GEMM, and
+// the RMSNorm that follows read and write one tensor instead of two each (ops/linear.py
+// linear_add).
+//
+// Algorithm choice: TunableOp's table does not cover the C != D problem, and hipBLASLt's first
+// heuristic pick is not reliably the fastest on gfx950 (the reason for the table, utils/tuning.py).
+// So the first call of each (shape, strides) times the heuristic's candidates on the live
+// operands (two warm-up + three timed launches each, hipEvents on the current stream) and keeps
+// the fastest; a caller-given solution index (e.g. TunableOp's pick for the beta = 0 problem) is
+// timed with them. Inside a stream capture nothing is timed: the heuristic's first pick is used
+// and not cached.
+//
+// Column-major view (hipBLASLt): D^T [N, M] = w [N, K] (as A, op T) x x^T (as B, op N) + C^T.
+#include <ATen/ATen.h>
+#include <ATen/hip/HIPContextLight.h>
+#include <torch/library.h>
+#include <hip/hip_runtime.h>
+#include <hipblaslt/hipblaslt-ext.hpp>
+#include <hipblaslt/hipblaslt.h>
+
+#include <algorithm>
+#include <map>
+#include <mutex>
+#include <tuple>
+#include <vector>
+
+#include "bind_util.h"
+
+namespace dla {
+namespace {
+
+#define DLA_LT_CHECK(expr)                                                                   \
+  do {                                                                                       \
+    hipblasStatus_t st_ = (expr);                                                            \
+    TORCH_CHECK(st_ == HIPBLAS_STATUS_SUCCESS, "hipBLASLt: ", #expr, " failed (", (int)st_, ")"); \
+  } while (0)
+
+// (m, n, k, lda, ldb, ldc, ldd, device)
+using LtKey = std::tuple<int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int>;
+
+struct LtPlan {
+  hipblasLtMatmulDesc_t desc = nullptr;
+  hipblasLtMatrixLayout_t a = nullptr, b = nullptr, c = nullptr, d = nullptr;
+  hipblasLtMatmulAlgo_t algo{};
+  size_t ws = 0;
+  int index = -1;     // hipBLASLt solution index of the chosen algorithm
+  float us = 0.f;     // its time at selection
+  bool tuned = false;
+};
+
+std::mutex g_mu;
+std::map<LtKey, LtPlan> g_plans;
+
+void make_layouts(LtPlan& p, int64_t m, int64_t n, int64_t k, int64_t lda, int64_t ldb, int64_t ldc,
+                  int64_t ldd) {
+  DLA_LT_CHECK(hipblasLtMatmulDescCreate(&p.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F));
+  const hipblasOperation_t ta = HIPBLAS_OP_T, tb = HIPBLAS_OP_N;
+  DLA_LT_CHECK(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta)));
+  DLA_LT_CHECK(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb)));
+  // A = w stored [N, K] row-major = column-major K x N (op T -> N x K); B = x column-major K x M
+  DLA_LT_CHECK(hipblasLtMatrixLayoutCreate(&p.a, HIP_R_16BF, k, m, lda));
+  DLA_LT_CHECK(hipblasLtMatrixLayoutCreate(&p.b, HIP_R_16BF, k, n, ldb));
+  DLA_LT_CHECK(hipblasLtMatrixLayoutCreate(&p.c, HIP_R_16BF, m, n, ldc));
+  DLA_LT_CHECK(hipblasLtMatrixLayoutCreate(&p.d, HIP_R_16BF, m, n, ldd));
+}
+
+hipblasStatus_t run(hipblasLtHandle_t h, LtPlan& p, const hipblasLtMatmulAlgo_t& algo, const void* A,
+                    const void* B, const void* C, void* D, void* ws, size_t ws_size, hipStream_t st) {
+  const float one = 1.f;
+  return hipblasLtMatmul(h, p.desc, &one, A, p.a, B, p.b, &one, C, p.c, D, p.d, &algo, ws, ws_size, st);
+}
+
+}  // namespace
+
+// out [M, N] = c [M, N] + x [M, K] @ w [N, K]^T (bf16, fp32 accumulate, one rounding).
+// `solution` >= 0: a hipBLASLt solution index to time with the heuristic's candidates.
+at::Tensor linear_add_lt(const at::Tensor& x, const at::Tensor& w, const at::Tensor& c, int64_t solution) {
+  TORCH_CHECK(x.is_cuda() && w.is_cuda() && c.is_cuda(), "linear_add_lt: CUDA tensors");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 &&
+                  c.scalar_type() == at::kBFloat16,
+              "linear_add_lt: bf16 operands");
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && c.dim() == 2, "linear_add_lt: x [M, K], w [N, K], c [M, N]");
+  TORCH_CHECK(x.stride(1) == 1 && w.stride(1) == 1 && c.stride(1) == 1, "linear_add_lt: unit inner strides");
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K && c.size(0) == M && c.size(1) == N, "linear_add_lt: shape mismatch");
+  TORCH_CHECK(x.get_device() == w.get_device() && x.get_device() == c.get_device(), "linear_add_lt: one device");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  auto out = at::empty({M, N}, x.options());
+  if (M == 0 || N == 0) return out;
+  if (K == 0) return out.copy_(c);
+  const int64_t m = N, n = M, k = K;
+  const int64_t lda = w.stride(0), ldb = x.stride(0), ldc = c.stride(0), ldd = out.stride(0);
+  const LtKey key{m, n, k, lda, ldb, ldc, ldd, x.get_device()};
+  hipblasLtHandle_t h = at::cuda::getCurrentCUDABlasLtHandle();
+  hipStream_t st = cur_stream(x);
+  void* ws = at::cuda::getCUDABlasLtWorkspace();
+  const size_t ws_size = at::cuda::getCUDABlasLtWorkspaceSize();
+  const void *A = w.data_ptr(), *B = x.data_ptr(), *C = c.data_ptr();
+  void* D = out.data_ptr();
+
+  std::lock_guard<std::mutex> lock(g_mu);
+  auto it = g_plans.find(key);
+  if (it == g_plans.end() || !it->second.tuned) {
+    LtPlan p;
+    if (it != g_plans.end()) p = it->second;
+    else make_layouts(p, m, n, k, lda, ldb, ldc, ldd);
+    std::vector<hipblasLtMatmulHeuristicResult_t> cand(16);
+    hipblasLtMatmulPreference_t pref;
+    DLA_LT_CHECK(hipblasLtMatmulPreferenceCreate(&pref));
+    uint64_t wsz = ws_size;
+    DLA_LT_CHECK(hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsz,
+                                                       sizeof(wsz)));
+    int returned = 0;
+    DLA_LT_CHECK(hipblasLtMatmulAlgoGetHeuristic(h, p.desc, p.a, p.b, p.c, p.d, pref, (int)cand.size(),
+                                                 cand.data(), &returned));
+    hipblasLtMatmulPreferenceDestroy(pref);
+    cand.resize(std::max(returned, 0));
+    if (solution >= 0) {
+      std::vector<int> idx{static_cast<int>(solution)};
+      std::vector<hipblasLtMatmulHeuristicResult_t> extra;
+      if (hipblaslt_ext::getAlgosFromIndex(h, idx, extra) == HIPBLAS_STATUS_SUCCESS)
+        for (auto& r : extra) cand.insert(cand.begin(), r);
+    }
+    const float one = 1.f;
+    std::vector<hipblasLtMatmulHeuristicResult_t> ok;
+    for (auto& r : cand) {
+      size_t need = 0;
+      if (hipblaslt_ext::matmulIsAlgoSupported(h, p.desc, &one, p.a, p.b, &one, p.c, p.d, r.algo, need) ==
+              HIPBLAS_STATUS_SUCCESS &&
+          need <= ws_size)
+        ok.push_back(r);
+    }
+    TORCH_CHECK(!ok.empty(), "linear_add_lt: no hipBLASLt algorithm for M=", M, " N=", N, " K=", K);
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(st, &cap);
+    if (cap != hipStreamCaptureStatusNone) {  // no timing under capture: first pick, not cached
+      DLA_LT_CHECK(run(h, p, ok.front().algo, A, B, C, D, ws, ws_size, st));
+      g_plans[key] = p;
+      return out;
+    }
+    hipEvent_t e0, e1;
+    TORCH_CHECK(hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess, "hipEventCreate");
+    float best = 1e30f;
+    for (auto& r : ok) {
+      bool good = true;
+      for (int i = 0; i < 2 && good; ++i) good = run(h, p, r.algo, A, B, C, D, ws, ws_size, st) == HIPBLAS_STATUS_SUCCESS;
+      if (!good) continue;
+      (void)hipEventRecord(e0, st);
+      for (int i = 0; i < 3; ++i) (void)run(h, p, r.algo, A, B, C, D, ws, ws_size, st);
+      (void)hipEventRecord(e1, st);
+      (void)hipEventSynchronize(e1);
+      float ms = 0.f;
+      (void)hipEventElapsedTime(&ms, e0, e1);
+      if (ms < best) {
+        best = ms;
+        p.algo = r.algo;
+        p.ws = r.workspaceSize;
+      }
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    TORCH_CHECK(best < 1e29f, "linear_add_lt: every candidate algorithm failed to launch");
+    p.index = hipblaslt_ext::getIndexFromAlgo(p.algo);
+    p.us = best * 1e3f / 3.f;
+    p.tuned = true;
+    g_plans[key] = p;
+    it = g_plans.find(key);
+  }
+  LtPlan& p = it->second;
+  DLA_LT_CHECK(run(h, p, p.algo, A, B, C, D, ws, ws_size, st));
+  return out;
+}
+
+// The selections made so far: one row per problem, [m, n, k, solution index, us at selection].
+at::Tensor linear_add_lt_plans() {
+  std::lock_guard<std::mutex> lock(g_mu);
+  auto t = at::empty({static_cast<int64_t>(g_plans.size()), 5}, at::TensorOptions().dtype(at::kDouble));
+  auto a = t.accessor<double, 2>();
+  int64_t i = 0;
+  for (auto& kv : g_plans) {
+    a[i][0] = static_cast<double>(std::get<0>(kv.first));
+    a[i][1] = static_cast<double>(std::get<1>(kv.first));
+    a[i][2] = static_cast<double>(std::get<2>(kv.first));
+    a[i][3] = kv.second.index;
+    a[i][4] = kv.second.us;
+    ++i;
+  }
+  return t;
+}
+
+}  // namespace dla
+
+TORCH_LIBRARY_FRAGMENT(dla, m) {
+  m.def("linear_add_lt(Tensor x, Tensor w, Tensor c, int solution=-1) -> Tensor");
+  m.def("linear_add_lt_plans() -> Tensor", &dla::linear_add_lt_plans);
+}
+
+TORCH_LIBRARY_IMPL(dla, CUDA, m) {
+  m.impl("linear_add_lt", &dla::linear_add_lt);
+}

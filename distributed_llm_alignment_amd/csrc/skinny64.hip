@@ -306,7 +306,7 @@ __global__ __launch_bounds__(256) void m64_reduce_kernel(const float* __restrict
 // Split-K count: the most splits that keep the grid within one workgroup per CU. A grid of 1.5
 // workgroups per CU (the qkv projection at Llama-3-8B: 48 column blocks x 8 splits = 384) leaves
 // half the CUs streaming twice the bytes of the rest; 48 x 4 = 192 workgroups ran the same GEMM +
-// reduce in 21.4 vs 26.9 us (B = 64, tools/m64_probe.py). DLA_M64_WG=n (A/B) restores the
+// reduce in 21.4 vs 26.9 us (B = 64, a round-4 probe since removed). DLA_M64_WG=n (A/B) restores the
 // round-3 rule: the fewest splits whose grid reaches n workgroups.
 int m64_splits(int N, int K) {
   static const int target = [] {

@@ -173,6 +173,11 @@ class MLP(nn.Module):
                     and self.tp is None and self.tp_seq is None
                     and ops.swiglu_mlp_ok(h, self.up_proj, self.down_proj)):
                 return ops.swiglu_mlp(h, self.up_proj, self.down_proj, resid=resid)
+            if self.tp is None and self.tp_seq is None and self.down_bias is None:
+                # (no autograd, e.g. the frozen DPO reference: the same add inside the down GEMM)
+                u = ops.linear(h, self.up_proj, self.up_bias)
+                m = ops.swiglu(u) if self.cfg.activation == "swiglu" else ops.gelu_new(u)
+                return ops.linear_add(m, self.down_proj, resid)
             return self.forward(h) + resid
         seq = self.tp_seq if h.dim() == 2 else None
         if seq is not None:

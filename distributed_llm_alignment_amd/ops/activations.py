@@ -12,7 +12,7 @@ import torch.nn.functional as F
 import os
 
 from . import _ext
-from .linear import accumulate_weight_grad, input_grad, uses_main_grad
+from .linear import accumulate_weight_grad, add_gemm, input_grad, uses_main_grad
 from ..parallel import collectives as coll
 
 FUSED_MLP = os.environ.get("DLA_FUSED_MLP", "1") != "0"
@@ -53,8 +53,8 @@ class _SwiGLUMLPFn(torch.autograd.Function):
         h2 = h.reshape(-1, H)
         u = F.linear(h2, w_up)
         m, mt = ops.swiglu_fwd_t(u)
-        if resid is not None:  # residual stream as the down GEMM's C input (ops.linear.linear_add)
-            y = torch.addmm(resid.reshape(-1, w_down.shape[0]), m, w_down.t())
+        if resid is not None:  # residual stream as the down GEMM's C input (ops.linear.add_gemm)
+            y = add_gemm(m, w_down, resid.reshape(-1, w_down.shape[0]))
         elif tp_group is None:
             y = F.linear(m, w_down)
         else:

@@ -156,7 +156,7 @@ class _LinearMainGradFn(torch.autograd.Function):
 # per-output-row scales (quantised once: the cache key is the weight's version) and e4m3
 # activations with per-row scales (one fused HIP pass, ops.moe.quant_fp8_rows), on hipBLASLt's fp8
 # MFMA path (torch._scaled_mm): 2.3-2.8 PF/s vs 1.2-1.6 bf16 at the Llama-3-8B DPO shapes
-# (tools/fp8_gemm_probe.py). Only without autograd and for >= 256 rows; the LM head, embeddings
+# (round-5 one-off probe, since removed). Only without autograd and for >= 256 rows; the LM head, embeddings
 # and norms stay bf16. Use: the DPO reference model (`dpo.reference_fp8`, `bench.py --ref-fp8`).
 def fp8_inference_ok(x: torch.Tensor, weight: torch.Tensor, bias) -> bool:
     return (bias is None and getattr(weight, "_dla_fp8_infer", False) and not torch.is_grad_enabled()
@@ -226,8 +226,22 @@ class fp8_inference_scope:
         return False
 
 
+def add_gemm(x2: torch.Tensor, weight: torch.Tensor, c2: torch.Tensor) -> torch.Tensor:
+    """c2 + x2 @ weight^T ([M, K], [N, K], [M, N]) as ONE GEMM that reads c2 as its C input and
+    writes a fresh D: hipBLASLt with C != D on the GPU (csrc/gemm_lt.cpp; torch.addmm would copy
+    c2 into the output first), torch.addmm elsewhere."""
+    if (x2.is_cuda and x2.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16 and c2.dtype == torch.bfloat16
+            and x2.stride(-1) == 1 and weight.stride(-1) == 1 and c2.stride(-1) == 1):
+        from ..utils.tuning import hipblaslt_solution
+
+        sol = hipblaslt_solution(weight.shape[0], x2.shape[0], x2.shape[1], weight.stride(0), x2.stride(0),
+                                 weight.shape[0])
+        return _ext.require().linear_add_lt(x2, weight, c2, sol)
+    return torch.addmm(c2, x2, weight.t())
+
+
 class _LinearAddMainGradFn(torch.autograd.Function):
-    """resid + x @ W^T as ONE hipBLASLt GEMM (the residual is the C input, beta = 1): the
+    """resid + x @ W^T as ONE hipBLASLt GEMM (the residual is the C input, beta = 1, C != D): the
     decoder's o / down projections add their output onto the residual stream in the epilogue,
     so the following RMSNorm reads one tensor and writes one instead of reading two and writing
     two. Backward: d(resid) = dy, the rest as _LinearMainGradFn."""
@@ -237,7 +251,7 @@ class _LinearAddMainGradFn(torch.autograd.Function):
         ctx.save_for_backward(x)
         ctx.weight = weight  # (on ctx: see _LinearMainGradFn)
         N = weight.shape[0]
-        y = torch.addmm(resid.reshape(-1, N), x.reshape(-1, x.shape[-1]), weight.t())
+        y = add_gemm(x.reshape(-1, x.shape[-1]), weight, resid.reshape(-1, N))
         return y.view(resid.shape)
 
     @staticmethod
@@ -262,7 +276,7 @@ def linear_add(x: torch.Tensor, weight: torch.Tensor, resid: torch.Tensor) -> to
     if uses_main_grad(weight):
         return _LinearAddMainGradFn.apply(x, weight, resid)
     N = weight.shape[0]
-    return torch.addmm(resid.reshape(-1, N), x.reshape(-1, x.shape[-1]), weight.t()).view(resid.shape)
+    return add_gemm(x.reshape(-1, x.shape[-1]), weight, resid.reshape(-1, N)).view(resid.shape)
 
 
 def linear(x: torch.Tensor, weight: torch.Tensor, bias=None) -> torch.Tensor:

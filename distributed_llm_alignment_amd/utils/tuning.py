@@ -54,3 +54,22 @@ def enable_gemm_tuning(device_index: int = 0) -> str:
     if not tune:
         tun.read_file(str(per_dev))
     return "tune" if tune else "read"
+
+
+_SOLUTIONS = {}
+
+
+def hipblaslt_solution(m: int, n: int, k: int, lda: int, ldb: int, ldc: int) -> int:
+    """The hipBLASLt solution index the shipped TunableOp table picked for the TN bf16 GEMM
+    (m, n, k, lda, ldb, ldc) in BLAS column-major terms, or -1 (no row, or a rocBLAS pick). Offered
+    as one more candidate to the C != D GEMM's own selection (csrc/gemm_lt.cpp)."""
+    if not _SOLUTIONS:
+        _SOLUTIONS[None] = None
+        try:
+            for line in tuned_table().read_text().splitlines():
+                parts = line.split(",")
+                if len(parts) >= 3 and parts[0] == "GemmTunableOp_BFloat16_TN" and parts[2].startswith("Gemm_Hipblaslt_"):
+                    _SOLUTIONS[parts[1]] = int(parts[2].rsplit("_", 1)[1])
+        except (OSError, ValueError):
+            pass
+    return _SOLUTIONS.get(f"tn_{m}_{n}_{k}_ld_{lda}_{ldb}_{ldc}", -1)

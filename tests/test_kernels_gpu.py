@@ -159,6 +159,25 @@ def test_fused_residual_chain_main_grad():
         assert rel_err(w.main_grad, r.grad) < 3e-2
 
 
+@pytest.mark.parametrize("M,N,K", [(256, 512, 384), (1000, 256, 128), (8, 128, 64)])
+def test_linear_add_lt_c_neq_d(M, N, K):
+    """csrc/gemm_lt.cpp: out = c + x @ w^T on hipBLASLt with C != D (no copy of c): against fp32,
+    c left untouched, and the per-shape selection cached after the first call."""
+    C = _ext.require()
+    x = bf(torch.randn(M, K))
+    w = bf(torch.randn(N, K) / K ** 0.5)
+    c = bf(torch.randn(M, N))
+    c0 = c.clone()
+    out = C.linear_add_lt(x, w, c, -1)
+    ref = c.float() + x.float() @ w.float().t()
+    assert out.shape == (M, N) and out.data_ptr() != c.data_ptr()
+    assert torch.equal(c, c0)
+    assert rel_err(out, ref) < 1e-2
+    assert torch.equal(C.linear_add_lt(x, w, c, -1), out)  # the cached plan: same algorithm, same bits
+    plans = C.linear_add_lt_plans()
+    assert any(int(r[0]) == N and int(r[1]) == M and int(r[2]) == K and r[3] >= 0 for r in plans.tolist())
+
+
 def test_fused_residual_model_matches_unfused(monkeypatch):
     """2-layer Llama policy: the fused-residual decoder (adds in the o / down GEMM epilogues) and
     the separate add + norm kernels give the same DPO loss and weight gradients within bf16."""
