@@ -305,7 +305,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
       const int row = ci / NCH, ch = ci % NCH;
       bf16x8 kv = kreg[c];
       if constexpr (DP == D) {  // RoPE on load: full rotary only (the host checks rot == D)
-        if (rope)
+        if (rope && p.rope_k)
           kv = rope_rot_chunk<NCH>(kv, ch, kt + row < p.Tk, static_cast<int64_t>(b) * p.Tk + kt + row,
                                    kt + row, p.rope_cos, p.rope_sin, p.rope_pos);
       }
@@ -759,7 +759,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_persist_kernel(AttnParams p,
       const int row = ci / NCH, ch = ci % NCH;
       bf16x8 kv = kreg[cc];
       if constexpr (DP == D) {
-        if (rope)
+        if (rope && p.rope_k)
           kv = rope_rot_chunk<NCH>(kv, ch, kt + row < p.Tk, static_cast<int64_t>(c.b) * p.Tk + kt + row,
                                    kt + row, p.rope_cos, p.rope_sin, p.rope_pos);
       }

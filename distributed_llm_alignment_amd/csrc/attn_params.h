@@ -28,6 +28,7 @@ struct AttnParams {
   const float* rope_cos;  // [max_pos, D/2] fp32
   const float* rope_sin;
   const int* rope_pos;    // [B * T] token positions, or null: position = t
+  int rope_k;             // 1: K rotated as it is staged too; 0: K arrives pre-rotated, Q only
   bf16_t* q_rot;          // optional [B, T, Hq, D] out: the rotated Q (what the backward reads)
   int64_t qr_sb, qr_st, qr_sh;
   // forward structure switches (set once per process by the launcher, attn_fwd_switches)

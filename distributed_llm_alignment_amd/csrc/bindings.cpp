@@ -387,7 +387,7 @@ std::tuple<at::Tensor, at::Tensor> attn_fwd(const at::Tensor& q, const at::Tenso
                                             const c10::optional<at::Tensor>& rope_cos,
                                             const c10::optional<at::Tensor>& rope_sin,
                                             const c10::optional<at::Tensor>& rope_pos,
-                                            const c10::optional<at::Tensor>& q_rot) {
+                                            const c10::optional<at::Tensor>& q_rot, bool rope_k) {
   check_bthd(q, "q");
   check_bthd(k, "k");
   check_bthd(v, "v");
@@ -425,6 +425,7 @@ std::tuple<at::Tensor, at::Tensor> attn_fwd(const at::Tensor& q, const at::Tenso
   rope_args(rope_cos, rope_sin, rope_pos, q, B, Tq, Tk, D, causal_off, &p.rope_cos, &p.rope_sin,
             &p.rope_pos);
   TORCH_CHECK(p.rope_cos == nullptr || D != 80, "RoPE on load: full-rotary head dims 64 / 128 only");
+  p.rope_k = rope_k ? 1 : 0;
   if (q_rot && q_rot->defined()) {
     TORCH_CHECK(p.rope_cos != nullptr, "q_rot needs the rotary tables");
     check_bthd(*q_rot, "q_rot");
@@ -901,7 +902,7 @@ TORCH_LIBRARY(dla, m) {
   m.def("gelu_bwd(Tensor x, Tensor dy) -> Tensor");
   m.def("rope_fwd(Tensor qkv, Tensor cos, Tensor sin, Tensor? pos, int Hq, int Hkv, int D, int rot, int T, int pos_offset) -> (Tensor, Tensor)");
   m.def("rope_bwd(Tensor dq, Tensor dk, Tensor(a!) dqkv, Tensor cos, Tensor sin, Tensor? pos, int Hq, int Hkv, int D, int rot, int T, int pos_offset) -> ()");
-  m.def("attn_fwd(Tensor q, Tensor k, Tensor v, float scale, bool causal, int causal_off, int window, Tensor? kv_start, Tensor? kv_end, Tensor? segs=None, Tensor? rope_cos=None, Tensor? rope_sin=None, Tensor? rope_pos=None, Tensor(a!)? q_rot=None) -> (Tensor, Tensor)");
+  m.def("attn_fwd(Tensor q, Tensor k, Tensor v, float scale, bool causal, int causal_off, int window, Tensor? kv_start, Tensor? kv_end, Tensor? segs=None, Tensor? rope_cos=None, Tensor? rope_sin=None, Tensor? rope_pos=None, Tensor(a!)? q_rot=None, bool rope_k=True) -> (Tensor, Tensor)");
   m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse2, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, float scale, bool causal, int causal_off, int window, Tensor? kv_start, Tensor? kv_end, Tensor? segs=None, Tensor? rope_cos=None, Tensor? rope_sin=None, Tensor? rope_pos=None, bool rope_inputs=False) -> ()");
   m.def("attn_stamps(Tensor like) -> Tensor");
   m.def("attn_fwd_switch(str name, int value) -> int", &dla::attn_fwd_switch);

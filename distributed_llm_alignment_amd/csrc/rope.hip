@@ -21,15 +21,19 @@ __global__ __launch_bounds__(256) void rope_kernel(
     int64_t k_dst_ld, const float* __restrict__ cos_t, const float* __restrict__ sin_t,
     const int* __restrict__ pos, int64_t tokens, int T, int pos_offset, int Hq, int Hkv, int D,
     int rot) {
-  // work item = (token, head, vec8 index within the head)
+  // work item = (token, head, item): items [0, hv) rotate one pair of 8-column chunks (v, v + hv),
+  // items [hv, dv - hv) copy one pass-through chunk (partial rotary). No idle lanes: an item per
+  // vec8 of the head would leave the hv high-half chunks' threads with nothing to do.
   const int dv = D >> 3;
   const int heads = Hq + Hkv;
-  const int64_t total = tokens * heads * dv;
   const int half = rot >> 1;
   const int hv = half >> 3;  // rotary pairs handled per head, in vec8 units
+  const int per = dv - hv;   // items per head
+  const int64_t total = tokens * heads * per;
   for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += static_cast<int64_t>(gridDim.x) * 256) {
-    const int v = static_cast<int>(i % dv);
-    const int64_t th = i / dv;
+    const int it = static_cast<int>(i % per);
+    const int v = it < hv ? it : it + hv;  // rotary pair v, or pass-through chunk v >= 2 hv
+    const int64_t th = i / per;
     const int h = static_cast<int>(th % heads);
     const int64_t tok = th / heads;
     const bool isq = h < Hq;
@@ -70,7 +74,7 @@ static inline unsigned rope_grid(int64_t work) {
 void launch_rope_fwd(const bf16_t* qkv, int64_t ld, bf16_t* q, bf16_t* k, const float* cos_t,
                      const float* sin_t, const int* pos, int64_t tokens, int T, int pos_offset,
                      int Hq, int Hkv, int D, int rot, hipStream_t st) {
-  const int64_t work = tokens * (Hq + Hkv) * (D / 8);
+  const int64_t work = tokens * (Hq + Hkv) * (D / 8 - rot / 16);
   rope_kernel<false><<<rope_grid(work), 256, 0, st>>>(
       qkv, qkv + static_cast<int64_t>(Hq) * D, ld, ld, q, k, static_cast<int64_t>(Hq) * D,
       static_cast<int64_t>(Hkv) * D, cos_t, sin_t, pos, tokens, T, pos_offset, Hq, Hkv, D, rot);
@@ -80,7 +84,7 @@ void launch_rope_fwd(const bf16_t* qkv, int64_t ld, bf16_t* q, bf16_t* k, const 
 void launch_rope_bwd(const bf16_t* dq_rot, const bf16_t* dk_rot, bf16_t* dqkv, int64_t ld,
                      const float* cos_t, const float* sin_t, const int* pos, int64_t tokens,
                      int T, int pos_offset, int Hq, int Hkv, int D, int rot, hipStream_t st) {
-  const int64_t work = tokens * (Hq + Hkv) * (D / 8);
+  const int64_t work = tokens * (Hq + Hkv) * (D / 8 - rot / 16);
   rope_kernel<true><<<rope_grid(work), 256, 0, st>>>(
       dq_rot, dk_rot, static_cast<int64_t>(Hq) * D, static_cast<int64_t>(Hkv) * D, dqkv,
       dqkv + static_cast<int64_t>(Hq) * D, ld, ld, cos_t, sin_t, pos, tokens, T, pos_offset, Hq,

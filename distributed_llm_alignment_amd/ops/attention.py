@@ -133,6 +133,11 @@ FUSED_ROPE_BWD = os.environ.get("DLA_FUSED_ROPE_BWD", "1") != "0"
 # forward workgroup re-rotates each K tile it stages (16 query blocks per sequence at T = 1024),
 # which costs more than the one 40 us rope pass it replaces. DLA_FUSED_ROPE_FWD=1 enables it.
 FUSED_ROPE_FWD = os.environ.get("DLA_FUSED_ROPE_FWD", "0") == "1"
+# Q-only RoPE on load (the default at full rotary, D 64 / 128): the forward kernel rotates the
+# Q rows it loads once per workgroup (and writes the rotated Q for the backward when there is
+# one), and the rope kernel rotates only K -- a fifth of the bytes of the q + k pass (Llama-3
+# GQA 32 / 8) -- so no workgroup re-rotates K tiles. DLA_ROPE_Q_ON_LOAD=0 restores the q + k pass.
+ROPE_Q_ON_LOAD = os.environ.get("DLA_ROPE_Q_ON_LOAD", "1") != "0"
 
 
 class _FusedQKVAttnFn(torch.autograd.Function):
@@ -147,7 +152,18 @@ class _FusedQKVAttnFn(torch.autograd.Function):
         off = qkv.storage_offset()
         v4 = qkv.as_strided((B, T, Hkv, D), (T * C, C, D, 1), off + (Hq + Hkv) * D)
         on_load = rot == D and D in (64, 128) and FUSED_ROPE_FWD
-        if on_load:
+        q_load = rot == D and D in (64, 128) and ROPE_Q_ON_LOAD and not on_load
+        if q_load:
+            # K rotated by the rope kernel over the K columns only; Q rotated on load
+            _, k_r = ops.rope_fwd(q2[:, Hq * D:], cos, sin, pos, 0, Hkv, D, rot, T, 0)
+            q4 = qkv.as_strided((B, T, Hq, D), (T * C, C, D, 1), off)
+            k4 = k_r.view(B, T, Hkv, D)
+            q_rot = torch.empty((B, T, Hq, D), dtype=qkv.dtype, device=qkv.device) \
+                if ctx.needs_input_grad[0] else None
+            o, lse2 = ops.attn_fwd(q4, k4, v4, float(scale), bool(causal), 0, int(window), kv_start,
+                                   kv_end, segs, cos, sin, pos, q_rot, False)
+            ctx.save_for_backward(qkv, q_rot, k4, o, lse2, cos, sin, pos, kv_start, kv_end, segs)
+        elif on_load:
             # RoPE on load: the kernel rotates Q in registers and K as it stages it; the rotated
             # Q leaves as a side output only when a backward will read it
             q4 = qkv.as_strided((B, T, Hq, D), (T * C, C, D, 1), off)

@@ -227,7 +227,13 @@ def _qkv_ref(qkv, Hq, Hkv, D, rope, kv_start, kv_end, window, positions):
 
 @pytest.mark.parametrize("D", [128, 64])
 @pytest.mark.parametrize("case", ["plain", "rightpad", "leftpad", "window", "norope"])
-def test_qkv_attention_fwd_bwd(D, case, bwd_waves):
+@pytest.mark.parametrize("qload", [True, False], ids=["q_on_load", "qk_rope_pass"])
+def test_qkv_attention_fwd_bwd(D, case, bwd_waves, qload, monkeypatch):
+    """qload: Q rotated inside the attention forward, K by the rope kernel over the K columns only
+    (the default), or both rotated by the rope kernel first (DLA_ROPE_Q_ON_LOAD=0)."""
+    from distributed_llm_alignment_amd.ops import attention as attn_mod
+
+    monkeypatch.setattr(attn_mod, "ROPE_Q_ON_LOAD", qload)
     B, T, Hq, Hkv = 2, 200, 8, 2
     C = (Hq + 2 * Hkv) * D
     qkv = bf(torch.randn(B, T, C)).requires_grad_()
@@ -258,6 +264,25 @@ def test_qkv_attention_fwd_bwd(D, case, bwd_waves):
     assert rel_err(o[valid], orf[valid]) < 2e-2, "forward"
     gmask = valid.unsqueeze(-1)
     assert rel_err(qkv.grad * gmask, qr.grad * gmask) < 3e-2, "backward"
+
+
+@pytest.mark.parametrize("D,rot", [(128, 128), (64, 64), (128, 64), (80, 32)])
+def test_rope_kernel_all_heads_and_k_slice(D, rot):
+    """rope_fwd (one work item per rotary chunk pair or pass-through chunk) against the fp32
+    rotate-half reference, over all q + k heads and over the K columns alone (Hq = 0 on a column
+    view of the fused qkv buffer: the Q-on-load attention path)."""
+    C_ = _ext.require()
+    B, T, Hq, Hkv = 2, 96, 4, 2
+    C = (Hq + 2 * Hkv) * D
+    qkv = bf(torch.randn(B * T, C))
+    cos, sin = RotaryCache(rot, 10000.0, 4096).tables(DEV)
+    pos = torch.arange(T, device=DEV).expand(B, T).contiguous()
+    q, k = C_.rope_fwd(qkv, cos, sin, None, Hq, Hkv, D, rot, T, 0)
+    qr = _ref_rope(qkv[:, :Hq * D].view(B, T, Hq, D), cos, sin, pos, rot)
+    kr = _ref_rope(qkv[:, Hq * D:(Hq + Hkv) * D].view(B, T, Hkv, D), cos, sin, pos, rot)
+    assert rel_err(q.view(B, T, Hq, D), qr) < 1e-2 and rel_err(k.view(B, T, Hkv, D), kr) < 1e-2
+    q0, k_only = C_.rope_fwd(qkv[:, Hq * D:], cos, sin, None, 0, Hkv, D, rot, T, 0)
+    assert q0.numel() == 0 and torch.equal(k_only, k)
 
 
 def test_attention_core_decode_offset():
