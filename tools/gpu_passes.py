@@ -96,6 +96,21 @@ PASSES = {
                  ab("fused_resid", DPO + " --steps 5 --warmup 2", {"on": {"DLA_FUSED_RESIDUAL": "1"},
                                                                    "off": {"DLA_FUSED_RESIDUAL": "0"}}, 2, 300),
                  prof("dpo", DPO + " --steps 2 --warmup 1", DPO_TABLES)],
+    # Q-only RoPE on load (rope kernel over K only) vs the q + k rope pass
+    "r6-rope": [pytest("tests/test_kernels_gpu.py -k 'qkv_attention or rope or persistent or forced_rescale or fused_rope'", 400),
+                ab("rope_qload", DPO + " --steps 5 --warmup 2", {"qload": {"DLA_ROPE_Q_ON_LOAD": "1"},
+                                                                "qkpass": {"DLA_ROPE_Q_ON_LOAD": "0"}}, 2, 300),
+                prof("dpo", DPO + " --steps 2 --warmup 1", DPO_TABLES)],
+    # RLHF / PPO update costs: the forced one-rank RCCL path vs plain (reinforce update), and the
+    # PPO update's kernels in issue order
+    "r6-rlhf": [prof("rlhf_plain", "python -u tools/bench_rlhf.py --batch 8 --steps 2 --warmup 1",
+                     [("window", ["--window", "adamw", "--by-grid", "--top", "40"]),
+                      ("window", ["--window", "adamw", "--seq", "-1500:1500"])], 500),
+                prof("rlhf_forced", "python -u tools/bench_rlhf.py --batch 8 --force-pg --steps 2 --warmup 1",
+                     [("window", ["--window", "adamw", "--by-grid", "--top", "40"]),
+                      ("window", ["--window", "adamw", "--seq", "-1500:1500"]), ("streams", ["--window", "adamw"])], 500),
+                prof("ppo", "python -u tools/bench_rlhf.py --algorithm ppo --zero-shape 8 --batch 8 --steps 1 --warmup 1",
+                     [("window", ["--by-grid", "--top", "50"]), ("window", ["--seq", "-6000:6000"])], 500)],
     # the whole DPO step's launches in issue order (which GEMM runs where, at what cost in place)
     # and the GEMM probe's arms under a kernel trace (which library kernel each form picks)
     "r6-seq": [prof("dpo_seq", DPO + " --steps 2 --warmup 1", [("window", ["--window", "adamw", "--seq", "0:7000"])]),
@@ -257,8 +272,10 @@ class Runner:
             if tr is None:
                 self._check(1, f"prof {s['name']} (no kernel trace)", log)
             tools = {"window": "prof_window.py", "breakdown": "step_breakdown.py", "streams": "prof_streams.py"}
-            for kind, args in s["summaries"]:
-                dst = f"{o}/{s['name']}_{kind}.md"
+            kinds = [k for k, _ in s["summaries"]]
+            for i, (kind, args) in enumerate(s["summaries"]):
+                dup = kinds.count(kind) > 1 and kinds.index(kind) != i
+                dst = f"{o}/{s['name']}_{kind}{i if dup else ''}.md"
                 with open(dst, "w") as fh:
                     rc = subprocess.call([sys.executable, os.path.join(ROOT, "scripts", tools[kind]), tr, *args],
                                          stdout=fh, stderr=subprocess.STDOUT)
