@@ -464,11 +464,6 @@ static int device_cus(int dev) {
 // sees every query), so target two workgroups per CU there and let the heaviest-first dispatch
 // balance them. Partial dK/dV of the splits are summed by a reduce pass.
 static int attn_bwd_hsplit(int64_t nkb, int64_t Hkv, int64_t B, int64_t group, bool causal, int cus) {
-  static const int forced = [] {
-    const char* e = std::getenv("DLA_ATTN_BWD_HSPLIT");
-    return e ? std::atoi(e) : 0;
-  }();
-  if (forced > 0 && group % forced == 0) return forced;
   const int64_t base = nkb * Hkv * B;
   const int64_t target = causal ? 2 * static_cast<int64_t>(cus) : cus;
   int hs = 1;

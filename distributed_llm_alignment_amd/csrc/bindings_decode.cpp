@@ -39,8 +39,6 @@ void launch_skinny_ksplit(const bf16_t*, int64_t, const bf16_t*, int64_t, bf16_t
                           int, int, hipStream_t);
 void launch_skinny_gemm(const bf16_t*, int64_t, const bf16_t*, int64_t, bf16_t*, int64_t, float*,
                         unsigned*, int, int, int, int, bool, bool, hipStream_t);
-void launch_skinny_glu_norm(const bf16_t*, const bf16_t*, const bf16_t*, bf16_t*, float, int64_t,
-                            const bf16_t*, int64_t, bf16_t*, int64_t, int, int, int, hipStream_t);
 bool skinny_glu_ks_ok(int N, int K);
 void launch_skinny_glu_ks(const bf16_t*, int64_t, const bf16_t*, int64_t, bf16_t*, int64_t, int,
                           int, int, hipStream_t);
@@ -474,36 +472,6 @@ at::Tensor skinny_glu_ks(const at::Tensor& x, const at::Tensor& w) {
   return m;
 }
 
-// Decode MLP entry with the residual add + RMSNorm fused in: s = x + res (returned: the next
-// residual), m = swiglu(RMSNorm(s) * norm_w @ w_up^T) with w_up = [gate; up] (2F rows).
-// Bitwise equal to add_norm + skinny_gemm(glu_out) (same reduction order as the row norm).
-std::tuple<at::Tensor, at::Tensor> skinny_glu_norm(const at::Tensor& x, const at::Tensor& res,
-                                                   const at::Tensor& norm_w, double eps,
-                                                   const at::Tensor& w) {
-  check_bf16(x, "x");
-  check_bf16(res, "res");
-  check_bf16(norm_w, "norm_w");
-  check_bf16(w, "w");
-  TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && res.sizes() == x.sizes() && res.is_contiguous(),
-              "x / res [M, K] contiguous");
-  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
-  TORCH_CHECK(M >= 1 && M <= 16, "1 <= M <= 16");
-  TORCH_CHECK((K == 512 || K == 1024 || K == 2048 || K == 4096) && M * K <= 16 * 4096,
-              "K in {512, 1024, 2048, 4096} (the kernel's chunk mapping)");
-  TORCH_CHECK(w.dim() == 2 && w.size(1) == K && w.stride(1) == 1 && w.stride(0) % 8 == 0 && N % 128 == 0,
-              "w [2F, K], F % 64 == 0, 16-byte aligned rows");
-  TORCH_CHECK(norm_w.numel() == K && norm_w.is_contiguous(), "norm_w [K]");
-  check_aligned16(x, "x");
-  check_aligned16(res, "res");
-  check_aligned16(w, "w");
-  check_aligned16(norm_w, "norm_w");
-  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
-  auto m = at::empty({M, N / 2}, x.options());
-  auto sum = at::empty({M, K}, x.options());
-  launch_skinny_glu_norm(cbp(x), cbp(res), cbp(norm_w), bp(sum), static_cast<float>(eps), K, cbp(w),
-                         w.stride(0), bp(m), m.stride(0), (int)M, (int)N, (int)K, cur_stream(x));
-  return {m, sum};
-}
 
 // y[M, N] = x[M, K] @ w[N, K]^T for M <= 16 (decode). With `swiglu`, x is the fused gate|up
 // output gu[M, 2K] and the kernel applies silu(g) * u while staging it. `counters` (int32,
@@ -764,7 +732,6 @@ TORCH_LIBRARY_FRAGMENT(dla, m) {
   m.def("decode_attn_rope(Tensor qkv, Tensor cos, Tensor sin, Tensor pos, Tensor(a!) k_cache, Tensor(b!) v_cache, Tensor slot, Tensor kv_len, Tensor? kv_start, int window, float scale, int Hq, int Hkv, int D, int rot) -> Tensor");
   m.def("sample_tokens(Tensor logits, float temperature, int top_k, float top_p, bool greedy, Tensor rng) -> Tensor");
   m.def("skinny_gemm(Tensor x, Tensor w, Tensor(a!) counters, bool swiglu, bool glu_out=False) -> Tensor");
-  m.def("skinny_glu_norm(Tensor x, Tensor res, Tensor norm_w, float eps, Tensor w) -> (Tensor, Tensor)");
   m.def("skinny_glu_ks(Tensor x, Tensor w) -> Tensor");
   m.def("skinny_fused(Tensor x, Tensor w, Tensor? res, Tensor? ssq_in, float eps, bool glu) -> (Tensor, Tensor)");
   m.def("skinny64(Tensor x, Tensor w, Tensor? res, Tensor? ssq_in, float eps, bool glu) -> (Tensor, Tensor)");
@@ -782,7 +749,6 @@ TORCH_LIBRARY_IMPL(dla, CUDA, m) {
   m.impl("rope_cache_write", &dla::rope_cache_write);
   m.impl("decode_attn_rope", &dla::decode_attn_rope);
   m.impl("skinny_gemm", &dla::skinny_gemm);
-  m.impl("skinny_glu_norm", &dla::skinny_glu_norm);
   m.impl("skinny_glu_ks", &dla::skinny_glu_ks);
   m.impl("skinny_fused", &dla::skinny_fused);
   m.impl("skinny64", &dla::skinny64);

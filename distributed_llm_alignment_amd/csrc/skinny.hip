@@ -55,17 +55,8 @@ static bool decode_nt() {
 // matching up rows F + [64b, 64b + 64); the tile is exchanged through LDS and SwiGLU applied in
 // the epilogue (after the same bf16 rounding of gate/up as the unfused path): no gu round trip,
 // no separate swiglu launch.
-// NORM (with GLU_OUT, decode MLP): the input is the attention output `x` plus the residual
-// stream `nres`; the kernel forms s = bf16(x + res), writes it to `nsum` (block 0 only: the next
-// residual), and stages RMSNorm(s) * w in LDS, replacing the separate add+norm launch. The row
-// statistics are reduced in exactly the order of norm_fwd_row_kernel (chunk c of a row is thread
-// c's; 64-chunk wave sums; wave sums added in order), so the result is bitwise identical.
-struct SkNorm {
-  const bf16_t* res;
-  const bf16_t* w;
-  bf16_t* sum_out;
-  float eps;
-};
+// (A NORM variant that formed s = x + res and RMSNorm(s) inside this kernel's staging measured
+// 4.39 vs 4.28 ms/token -- 224 workgroups each re-deriving the row norm -- and was removed.)
 
 // Decode-layer fusion of the residual add + RMSNorm across two launches (no norm launch):
 //   RES (producer, the o / down projections): the epilogue writes the new residual stream
@@ -80,15 +71,12 @@ struct SkNorm {
 // Deterministic (eager == graph); the rounding differs from the separate-norm path (h is never
 // rounded to bf16; W o w is), so the two agree to bf16 accuracy, not bitwise.
 
-template <bool SWIGLU, bool GLU_OUT = false, bool NORM = false, bool NTW = false, bool NPRE = false,
-          bool TW = false>
+template <bool SWIGLU, bool GLU_OUT = false, bool NTW = false, bool NPRE = false, bool TW = false>
 __global__ __launch_bounds__(64 * kSkWaves) void skinny_gemm_kernel(
     const bf16_t* __restrict__ x, int64_t ldx, const bf16_t* __restrict__ W, int64_t ldw,
     bf16_t* __restrict__ y, int64_t ldy, float* __restrict__ ws, unsigned* __restrict__ counters,
-    int M, int N, int K, int kc, SkNorm nrm = SkNorm{}, KsFuse fz = KsFuse{}) {
+    int M, int N, int K, int kc, KsFuse fz = KsFuse{}) {
   extern __shared__ __attribute__((aligned(16))) bf16_t xs[];
-  // NORM statistics (512 B, a multiple of 16 so the dynamic LDS base stays 16-byte aligned)
-  __shared__ __attribute__((aligned(16))) float nred[16][8];
   // NPRE: per-row rstd from the producer's partial sums (see KsFuse)
   __shared__ __attribute__((aligned(16))) float rstd_p[16];
   const int S = gridDim.y;
@@ -144,54 +132,6 @@ __global__ __launch_bounds__(64 * kSkWaves) void skinny_gemm_kernel(
       for (int j = 0; j < 8; ++j)
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[j][e] = f2bf(silu_sk(bf2f(gg[j][e])) * bf2f(uu[j][e]));
-    } else if constexpr (NORM) {
-      // s = bf16(x + res), squared sums per (row, 64-chunk group); the host guarantees
-      // vecs | NT, so every pass-slice j of this thread is the SAME chunk c of another row and
-      // one norm-weight load serves all of them. Loads of x, res and w go out together.
-      bf16x8 rr[8];
-      const int cc = (threadIdx.x % vecs) << 3;
-      const bf16x8 wv = load_bf16x8(nrm.w + cc);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int i = base + j * NT + threadIdx.x;
-        if (i < total) {
-          const int m = i / vecs;
-          v[j] = load_bf16x8(x + m * ldx + cc);
-          rr[j] = load_bf16x8(nrm.res + m * ldx + cc);
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int i = base + j * NT + threadIdx.x;
-        if (i < total) {  // wave-uniform: vecs % 64 == 0, so a wave's 64 chunks share one row
-          const int m = i / vecs;
-          float ss = 0.f;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            v[j][e] = f2bf(bf2f(v[j][e]) + bf2f(rr[j][e]));
-            const float f = bf2f(v[j][e]);
-            ss += f * f;
-          }
-          if (blockIdx.x == 0) store_bf16x8(nrm.sum_out + m * ldx + cc, v[j]);
-          ss = wave_sum(ss);
-          if ((threadIdx.x & 63) == 0) nred[m][(cc >> 3) >> 6] = ss;
-        }
-      }
-      __syncthreads();
-      // rstd of each row (wave sums added in chunk-group order, as norm_fwd_row_kernel), then
-      // h = bf16(s * rstd * w) straight from registers
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int i = base + j * NT + threadIdx.x;
-        if (i < total) {
-          const int m = i / vecs;
-          float r = 0.f;
-          for (int g = 0; g < (vecs >> 6); ++g) r += nred[m][g];
-          const float rs = rsqrtf(r / K + nrm.eps);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[j][e] = f2bf((bf2f(v[j][e]) - 0.f) * rs * bf2f(wv[e]));
-        }
-      }
     } else {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -341,23 +281,6 @@ int skinny_splits(int M, int N, int K) {
 
 size_t skinny_lds_bytes(int M, int kc) { return static_cast<size_t>(M) * (kc + 8) * sizeof(bf16_t); }
 
-// decode MLP entry: residual add + RMSNorm fused into the gate|up GEMM with the SwiGLU epilogue
-// (x = attention output, res = residual stream [M, K] with row stride ldx; sum_out <- x + res)
-void launch_skinny_glu_norm(const bf16_t* x, const bf16_t* res, const bf16_t* nw, bf16_t* sum_out,
-                            float eps, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
-                            int64_t ldy, int M, int N, int K, hipStream_t st) {
-  static bool attr_set = [] {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_gemm_kernel<false, true, true>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
-    (void)hipGetLastError();
-    return true;
-  }();
-  (void)attr_set;
-  dim3 g2(N / 2 / 64, 1);
-  skinny_gemm_kernel<false, true, true><<<g2, 64 * kSkWaves, skinny_lds_bytes(M, K), st>>>(
-      x, ldx, W, ldw, y, ldy, nullptr, nullptr, M, N, K, K, SkNorm{res, nw, sum_out, eps});
-}
-
 template <bool NT>
 void launch_skinny_gemm_t(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
                           int64_t ldy, float* ws, unsigned* counters, int M, int N, int K, int S,
@@ -366,12 +289,12 @@ void launch_skinny_gemm_t(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t
   dim3 grid((N + kSkCols - 1) / kSkCols, S);
   const size_t lds = skinny_lds_bytes(M, kc);
   static bool attr_set = [] {  // S = 1 at K = 4096 stages up to 16 x 4104 bf16 (> 64 KB default)
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_gemm_kernel<false, false, false, NT>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_gemm_kernel<false, false, NT>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_gemm_kernel<true, false, false, NT>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_gemm_kernel<true, false, NT>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     // the GLU variant also holds an 8 KB static exchange tile: dynamic + static <= 160 KB
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_gemm_kernel<false, true, false, NT>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_gemm_kernel<false, true, NT>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, 152 * 1024);
     (void)hipGetLastError();  // never leave a sticky error for the caller's next launch check
     return true;
@@ -379,15 +302,15 @@ void launch_skinny_gemm_t(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t
   (void)attr_set;
   if (glu_out) {  // N = 2F weight rows -> F outputs, 64 per block, never split
     dim3 g2(N / 2 / 64, 1);
-    skinny_gemm_kernel<false, true, false, NT><<<g2, 64 * kSkWaves, skinny_lds_bytes(M, K), st>>>(
+    skinny_gemm_kernel<false, true, NT><<<g2, 64 * kSkWaves, skinny_lds_bytes(M, K), st>>>(
         x, ldx, W, ldw, y, ldy, ws, counters, M, N, K, K);
     return;
   }
   if (swiglu)
-    skinny_gemm_kernel<true, false, false, NT><<<grid, 64 * kSkWaves, lds, st>>>(
+    skinny_gemm_kernel<true, false, NT><<<grid, 64 * kSkWaves, lds, st>>>(
         x, ldx, W, ldw, y, ldy, ws, counters, M, N, K, kc);
   else
-    skinny_gemm_kernel<false, false, false, NT><<<grid, 64 * kSkWaves, lds, st>>>(
+    skinny_gemm_kernel<false, false, NT><<<grid, 64 * kSkWaves, lds, st>>>(
         x, ldx, W, ldw, y, ldy, ws, counters, M, N, K, kc);
 }
 
@@ -507,15 +430,15 @@ template <bool TW, bool NT>
 static void launch_glu_normin_t(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
                                 int64_t ldy, int M, int N, int K, const KsFuse& fz, hipStream_t st) {
   static bool attr_set = [] {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_gemm_kernel<false, true, false, NT, true, TW>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&skinny_gemm_kernel<false, true, NT, true, TW>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
     (void)hipGetLastError();
     return true;
   }();
   (void)attr_set;
   dim3 g2(N / 2 / 64, 1);
-  skinny_gemm_kernel<false, true, false, NT, true, TW><<<g2, 64 * kSkWaves, skinny_lds_bytes(M, K), st>>>(
-      x, ldx, W, ldw, y, ldy, nullptr, nullptr, M, N, K, K, SkNorm{}, fz);
+  skinny_gemm_kernel<false, true, NT, true, TW><<<g2, 64 * kSkWaves, skinny_lds_bytes(M, K), st>>>(
+      x, ldx, W, ldw, y, ldy, nullptr, nullptr, M, N, K, K, fz);
 }
 
 void launch_skinny_glu_normin(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,

@@ -377,20 +377,11 @@ static void m64_launch(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ld
     const char* e = getenv("DLA_DECODE_NT");
     return !(e != nullptr && atoi(e) == 0);
   }();
-  // DLA_M64_DEPTH (A/B): weight chunks in flight per wave on the tiled nt stream (2, 3 or 4)
-  static const int depth = [] {
-    const char* e = getenv("DLA_M64_DEPTH");
-    const int d = e ? atoi(e) : 2;
-    return d >= 2 && d <= 4 ? d : 2;
-  }();
+  // two weight chunks in flight per wave on the tiled nt stream (3 or 4 measured 5.10 / 5.27 vs
+  // 5.01 ms/token at B = 64: more bytes in flight only lengthen the queues; removed)
   if constexpr (TW) {
     if (nt) {
-      if (depth == 3)
-        m64_launch_w<MT, GLU, NIN, TW, kM64Waves, true, 3>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, ssq_in, nbp, eps, st);
-      else if (depth == 4)
-        m64_launch_w<MT, GLU, NIN, TW, kM64Waves, true, 4>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, ssq_in, nbp, eps, st);
-      else
-        m64_launch_w<MT, GLU, NIN, TW, kM64Waves, true>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, ssq_in, nbp, eps, st);
+      m64_launch_w<MT, GLU, NIN, TW, kM64Waves, true>(x, ldx, W, ldw, y, ldy, ws, M, N, K, S, ssq_in, nbp, eps, st);
       return;
     }
   }

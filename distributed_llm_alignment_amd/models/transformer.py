@@ -153,18 +153,6 @@ class MLP(nn.Module):
         self.tp = None
         self.tp_seq = None
 
-    def decode_norm_glu(self, a, resid, norm_w, eps):
-        """Decode rows: (mlp(RMSNorm(a + resid) * norm_w), a + resid) with the add + norm fused
-        into the skinny gate|up launch; None when not eligible."""
-        if (self.cfg.activation != "swiglu" or self.up_bias is not None or self.down_bias is not None
-                or self.tp is not None):
-            return None
-        r = ops.decode.skinny_glu_norm(a, resid, norm_w, eps, self.up_proj)
-        if r is None:
-            return None
-        m, s = r
-        return _lin(m, self.down_proj, None), s
-
     def forward(self, h, resid=None):
         """`resid` (no TP): return resid + MLP(h); on the fused SwiGLU node the add runs inside
         the down GEMM (its C input), elsewhere as a plain add."""
@@ -366,10 +354,6 @@ class DecoderLayer(nn.Module):
         mlp = (lambda t: checkpoint(self.mlp, t, use_reentrant=False)) if rc == "mlp" else self.mlp
         if cfg.parallel_block:
             return a + mlp(h), resid
-        if cache is not None and rms and self.ln2_b is None and isinstance(self.mlp, MLP):
-            fused = self.mlp.decode_norm_glu(a, resid, self.ln2_w, cfg.norm_eps)
-            if fused is not None:  # decode: residual add + RMSNorm inside the gate|up launch
-                return fused
         h, resid = ops.add_norm(a, resid, w_(self.ln2_w, seq), w_(self.ln2_b, seq), cfg.norm_eps, rms)
         return mlp(h), resid
 

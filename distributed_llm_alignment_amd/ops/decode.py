@@ -175,30 +175,6 @@ def skinny_glu(x: torch.Tensor, weight: torch.Tensor, mode: Optional[str] = None
     return m.view(*x.shape[:-1], weight.shape[0] // 2)
 
 
-# Off by default: measured on 1x MI355X (Llama-3-8B, B=8, graph decode, same box) 4.39 ms/token
-# fused vs 4.28 unfused -- every one of the 224 gate|up workgroups re-derives the row norm on its
-# critical path before its weight stream, which costs more than the separate 5 us norm launch.
-FUSED_NORM_GLU = os.environ.get("DLA_FUSED_NORM_GLU", "0") == "1"
-
-
-def skinny_glu_norm(x: torch.Tensor, resid: torch.Tensor, norm_w: torch.Tensor, eps: float,
-                    weight: torch.Tensor):
-    """Decode MLP entry, one launch: s = x + resid, m = swiglu(RMSNorm(s) * norm_w @ [gate; up]^T).
-    Returns (m [.., F], s) or None when not eligible (caller runs add_norm + skinny_glu).
-    Bitwise equal to the unfused pair."""
-    if not FUSED_NORM_GLU or resid is None or resid.shape != x.shape:
-        return None
-    H = x.shape[-1]
-    rows = x.numel() // H
-    if not (skinny_ok(x, weight) and weight.shape[0] % 128 == 0 and H in (512, 1024, 2048, 4096)
-            and rows * H <= 16 * 4096 and norm_w.dtype == torch.bfloat16):
-        return None
-    x2 = x.reshape(rows, H).contiguous()
-    r2 = resid.reshape(rows, H).contiguous()
-    m, s = _ext.require().skinny_glu_norm(x2, r2, norm_w.contiguous(), float(eps), weight)
-    return m.view(*x.shape[:-1], weight.shape[0] // 2), s.view(x.shape)
-
-
 def ref_skinny_linear(x: torch.Tensor, weight: torch.Tensor, swiglu: bool = False) -> torch.Tensor:
     if swiglu:
         g, u = x.float().chunk(2, dim=-1)

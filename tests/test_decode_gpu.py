@@ -378,27 +378,6 @@ def test_fused_rope_decode_attention_matches_unfused(D, Hq, Hkv, rot, blocks, mo
     assert torch.equal(out, ref)
 
 
-@pytest.mark.parametrize("M,K,F", [(8, 4096, 1024), (1, 4096, 256), (16, 2048, 512), (3, 512, 128)])
-def test_fused_norm_glu_matches_add_norm_then_glu(M, K, F):
-    """skinny_glu_norm (residual add + RMSNorm staged inside the gate|up GEMM) == add_norm +
-    skinny GLU GEMM, bitwise, and returns the same next residual."""
-    from distributed_llm_alignment_amd import ops
-
-    dev = torch.device("cuda", 0)
-    g = torch.Generator(device=dev).manual_seed(11)
-    a = torch.randn(M, K, device=dev, generator=g).to(torch.bfloat16)
-    r = (torch.randn(M, K, device=dev, generator=g) * 3).to(torch.bfloat16)
-    nw = (1 + 0.1 * torch.randn(K, device=dev, generator=g)).to(torch.bfloat16)
-    w = (torch.randn(2 * F, K, device=dev, generator=g) * 0.02).to(torch.bfloat16)
-    with torch.no_grad():
-        h, s_ref = ops.add_norm(a, r, nw, None, 1e-5, True)
-        m_ref = ops.decode.skinny_glu(h, w, mode="lds")  # the kernel it stages the norm into
-        m, s = ops._ext.require().skinny_glu_norm(a, r, nw, 1e-5, w)
-    torch.cuda.synchronize()
-    assert torch.equal(s, s_ref)
-    assert torch.equal(m, m_ref)
-
-
 @pytest.mark.parametrize("M", [17, 24, 32, 40, 64])
 @pytest.mark.parametrize("N,K", [(6144, 4096), (4096, 14336), (1040, 1024)])
 def test_skinny_split_k_many_rows_matches_fp32(M, N, K, monkeypatch):

@@ -84,13 +84,11 @@ def test_swiglu_and_gelu():
     assert rel_err(z, zr) < 1e-2 and rel_err(x.grad, xr.grad) < 2e-2
 
 
-@pytest.mark.parametrize("reg", ["0", "1"])
-@pytest.mark.parametrize("rows", [256, 300, 8, 136])
-def test_swiglu_transposed_outputs(rows, reg, monkeypatch):
-    """swiglu_fwd_t / swiglu_bwd_t, LDS-tiled (reg 0) and register-transpose (reg 1, rows % 8 ==
-    0) forms: row-major outputs bit-equal to the plain kernels, second outputs their exact
+@pytest.mark.parametrize("rows", [256, 300, 8, 136, 13])
+def test_swiglu_transposed_outputs(rows):
+    """swiglu_fwd_t / swiglu_bwd_t (register-transpose form where rows % 8 == 0, the LDS-tiled
+    form otherwise): row-major outputs bit-equal to the plain kernels, second outputs their exact
     transposes (partial 64-row tiles and a partial 256-column block included)."""
-    monkeypatch.setenv("DLA_SWIGLU_T_REG", reg)
     C = _ext.require()
     F_ = 192
     gu = bf(torch.randn(rows, 2 * F_))

@@ -105,23 +105,18 @@ PASSES = {
     # PPO update's kernels in issue order
     "r6-rlhf": [prof("rlhf_plain", "python -u tools/bench_rlhf.py --batch 8 --steps 2 --warmup 1",
                      [("window", ["--window", "adamw", "--by-grid", "--top", "40"]),
-                      ("window", ["--window", "adamw", "--seq", "-1500:1500"])], 500),
+                      ("window", ["--window", "adamw", "--seq=-1500:1500"])], 500),
                 prof("rlhf_forced", "python -u tools/bench_rlhf.py --batch 8 --force-pg --steps 2 --warmup 1",
                      [("window", ["--window", "adamw", "--by-grid", "--top", "40"]),
-                      ("window", ["--window", "adamw", "--seq", "-1500:1500"]), ("streams", ["--window", "adamw"])], 500),
+                      ("window", ["--window", "adamw", "--seq=-1500:1500"]), ("streams", ["--window", "adamw"])], 500),
                 prof("ppo", "python -u tools/bench_rlhf.py --algorithm ppo --zero-shape 8 --batch 8 --steps 1 --warmup 1",
-                     [("window", ["--by-grid", "--top", "50"]), ("window", ["--seq", "-6000:6000"])], 500)],
+                     [("window", ["--by-grid", "--top", "50"]), ("window", ["--seq=-6000:6000"])], 500)],
     # the whole DPO step's launches in issue order (which GEMM runs where, at what cost in place)
     # and the GEMM probe's arms under a kernel trace (which library kernel each form picks)
     "r6-seq": [prof("dpo_seq", DPO + " --steps 2 --warmup 1", [("window", ["--window", "adamw", "--seq", "0:7000"])]),
                prof("gemm_probe", "python -u tools/gemm_m_probe.py --model llama3-8b --ms 8192 --resid",
                     [("window", ["--by-grid", "--top", "40"])], 300)],
     # ---- round 5
-    # SwiGLU transposed-output kernels: LDS-tiled vs register transpose (bitwise test, microbench, DPO A/B)
-    "ab-swiglu-t-reg": [pytest("tests/test_kernels_gpu.py -k swiglu", 200),
-                        run("swiglu_t_bench", "python -u tools/transpose_bench.py", 200),
-                        ab("swiglu_t_reg", DPO + " --steps 5 --warmup 2", {"lds": {"DLA_SWIGLU_T_REG": "0"},
-                                                                          "reg": {"DLA_SWIGLU_T_REG": "1"}}, 2, 300)],
     # DPO step GEMMs: MFMA busy and effective clock per library GEMM shape (by grid)
     "dpo-gemm-pmc": [pmc("dpo_gemm", "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY GRBM_GUI_ACTIVE",
                          "python3 bench.py --micro-pairs 4 --accum 1 --steps 1 --warmup 1",

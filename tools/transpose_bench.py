@@ -33,14 +33,10 @@ for R, K in [(8192, 4096), (8192, 6144), (8192, 14336), (4096, 14336)]:
     print(f"transpose [{R},{K}]: {us:.1f} us  {2 * x.numel() * 2 / us / 1e6:.2f} TB/s", flush=True)
 gu = torch.randn(8192, 28672, device="cuda", dtype=torch.bfloat16)
 d = torch.randn(8192, 14336, device="cuda", dtype=torch.bfloat16)
-for rnd in range(2):  # LDS-tiled vs register-transpose forms, interleaved (DLA_SWIGLU_T_REG per call)
-    for reg in ("0", "1"):
-        os.environ["DLA_SWIGLU_T_REG"] = reg
-        us = timeit(lambda: C.swiglu_fwd_t(gu), 20)
-        print(f"swiglu_fwd_t reg={reg}: {us:.1f} us  {(gu.numel() + 2 * d.numel()) * 2 / us / 1e6:.2f} TB/s", flush=True)
-        us = timeit(lambda: C.swiglu_bwd_t(gu, d), 20)
-        print(f"swiglu_bwd_t reg={reg}: {us:.1f} us  {(3 * gu.numel() + d.numel()) * 2 / us / 1e6:.2f} TB/s", flush=True)
-os.environ.pop("DLA_SWIGLU_T_REG")
+us = timeit(lambda: C.swiglu_fwd_t(gu), 20)
+print(f"swiglu_fwd_t: {us:.1f} us  {(gu.numel() + 2 * d.numel()) * 2 / us / 1e6:.2f} TB/s", flush=True)
+us = timeit(lambda: C.swiglu_bwd_t(gu, d), 20)
+print(f"swiglu_bwd_t: {us:.1f} us  {(3 * gu.numel() + d.numel()) * 2 / us / 1e6:.2f} TB/s", flush=True)
 us = timeit(lambda: C.swiglu_fwd(gu), 20)
 print(f"swiglu_fwd:   {us:.1f} us  {(gu.numel() + d.numel()) * 2 / us / 1e6:.2f} TB/s", flush=True)
 us = timeit(lambda: C.swiglu_bwd(gu, d), 20)
