@@ -331,15 +331,20 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_kernel(AttnParams p) {
     float qv[KS][8];
     {
       const int qc = min(qi, p.Tq - 1);
+      // RoPE: the row's position is loaded FIRST, so its round trip overlaps the Q loads' instead
+      // of queueing behind them (vmcnt is in-order); the cos / sin rows it addresses follow
+      int pv = 0;
+      if constexpr (ROPE) {
+        // branch-free position: a valid dummy address when there is no position table
+        const int* pp = p.rope_pos ? p.rope_pos + static_cast<int64_t>(b) * p.Tq + qc
+                                   : reinterpret_cast<const int*>(qp);
+        pv = *pp;
+      }
       bf16x8 qraw[KS];
 #pragma unroll
       for (int s = 0; s < KS; ++s) qraw[s] = load_bf16x8(qp + qc * p.q_st + 16 * s + 8 * h);
       f32x4 rc[ROPE ? KS : 1], rs[ROPE ? KS : 1];  // cos / sin of columns 16s + 8h + [0, 8), s < KS/2
       if constexpr (ROPE) {
-        // branch-free position: a valid dummy address when there is no position table
-        const int* pp = p.rope_pos ? p.rope_pos + static_cast<int64_t>(b) * p.Tq + qc
-                                   : reinterpret_cast<const int*>(qp);
-        const int pv = *pp;
         const int pos = p.rope_pos ? pv : qc;
         const float* cp = p.rope_cos + static_cast<int64_t>(pos) * (D / 2) + 8 * h;
         const float* sp = p.rope_sin + static_cast<int64_t>(pos) * (D / 2) + 8 * h;
