@@ -44,6 +44,8 @@ void launch_logprob_fwd(const bf16_t*, int64_t, int, int64_t, int64_t, const int
 void launch_logprob_bwd(bf16_t*, int64_t, int, int64_t, int64_t, const int64_t*, const float*,
                         const float*, hipStream_t);
 void launch_row_lse(const bf16_t*, int64_t, int, int64_t, float*, hipStream_t);
+bool launch_logprob_bwd_t(bf16_t*, int64_t, int, int64_t, int64_t, const int64_t*, const float*,
+                          const float*, bf16_t*, hipStream_t);
 void launch_ensemble_kl(bf16_t*, const bf16_t*, int64_t, int64_t, int, int, const float*,
                         const float*, int64_t, const float*, float*, bool, hipStream_t);
 void launch_seq_reduce(const float*, const float*, int, int, float*, float*, hipStream_t);
@@ -618,6 +620,28 @@ void logprob_bwd(at::Tensor& logits, const at::Tensor& tgt, const at::Tensor& ls
                      cur_stream(logits));
 }
 
+// logprob_bwd with the transposed gradient as a second output: logits <- dlogits (in place) and
+// returns dlogitsT [V, N] (the LM head's TN weight-gradient operand). An empty tensor when the
+// shape is outside the kernel (N, V or the row stride not a multiple of 8): run logprob_bwd.
+at::Tensor logprob_bwd_t(at::Tensor& logits, const at::Tensor& tgt, const at::Tensor& lse,
+                         const at::Tensor& grad, int64_t vocab_offset) {
+  check_logits(logits);
+  check_f32(lse, "lse");
+  check_f32(grad, "grad");
+  const int64_t N = logits.size(0), V = logits.size(1);
+  TORCH_CHECK(tgt.scalar_type() == at::kLong && tgt.numel() == N && tgt.is_contiguous(), "targets");
+  TORCH_CHECK(lse.numel() == N && grad.numel() == N && grad.is_contiguous() && lse.is_contiguous(),
+              "lse/grad shape");
+  if (N == 0 || N % 8 != 0 || V % 8 != 0 || logits.stride(0) % 8 != 0) return at::empty({0}, logits.options());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(logits.device());
+  auto outT = at::empty({V, N}, logits.options());
+  const bool ok = launch_logprob_bwd_t(bp(logits), logits.stride(0), static_cast<int>(V), N, vocab_offset,
+                                       tgt.data_ptr<int64_t>(), lse.data_ptr<float>(), grad.data_ptr<float>(),
+                                       bp(outT), cur_stream(logits));
+  TORCH_CHECK(ok, "logprob_bwd_t: shape");
+  return outT;
+}
+
 at::Tensor row_lse(const at::Tensor& logits) {
   check_logits(logits);
   c10::hip::HIPGuardMasqueradingAsCUDA g(logits.device());
@@ -904,6 +928,7 @@ TORCH_LIBRARY(dla, m) {
   m.def("transpose_bf16(Tensor input, Tensor(a!) out) -> ()");
   m.def("logprob_fwd(Tensor logits, Tensor targets, int vocab_offset=0) -> (Tensor, Tensor)");
   m.def("logprob_bwd(Tensor(a!) logits, Tensor targets, Tensor lse, Tensor grad, int vocab_offset=0) -> ()");
+  m.def("logprob_bwd_t(Tensor(a!) logits, Tensor targets, Tensor lse, Tensor grad, int vocab_offset=0) -> Tensor");
   m.def("row_lse(Tensor logits) -> Tensor");
   m.def("ensemble_kl(Tensor(a!) s_logits, Tensor t_logits, Tensor s_lse, Tensor t_lse, Tensor? grad, bool write_grad) -> Tensor");
   m.def("seq_reduce(Tensor lp, Tensor mask) -> (Tensor, Tensor)");
@@ -936,6 +961,7 @@ TORCH_LIBRARY_IMPL(dla, CUDA, m) {
   m.impl("transpose_bf16", &dla::transpose_bf16);
   m.impl("logprob_fwd", &dla::logprob_fwd);
   m.impl("logprob_bwd", &dla::logprob_bwd);
+  m.impl("logprob_bwd_t", &dla::logprob_bwd_t);
   m.impl("row_lse", &dla::row_lse);
   m.impl("ensemble_kl", &dla::ensemble_kl);
   m.impl("seq_reduce", &dla::seq_reduce);

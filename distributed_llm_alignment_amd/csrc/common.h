@@ -51,6 +51,23 @@ __device__ __forceinline__ bf16x8 pack_bf16x8(const float* v) {
   return __builtin_bit_cast(bf16x8, r);
 }
 
+// out[j] = column j of the 8 x 8 bf16 block held as 8 row vectors v[0..7] (32 v_perm_b32, no LDS):
+// the register transpose behind the kernels that write a transposed second output
+// (elementwise.hip SwiGLU, logprob.hip log-prob backward, transpose.hip)
+__device__ __forceinline__ void tr8_bf16(const bf16x8 (&v)[8], bf16x8 (&out)[8]) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const uint32_t sel = (j & 1) ? 0x07060302u : 0x05040100u;
+    u32x4 o;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      o[k] = __builtin_amdgcn_perm(__builtin_bit_cast(u32x4, v[2 * k + 1])[j >> 1],
+                                   __builtin_bit_cast(u32x4, v[2 * k])[j >> 1], sel);
+    out[j] = __builtin_bit_cast(bf16x8, o);
+  }
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -175,22 +175,6 @@ __global__ __launch_bounds__(256) void swiglu_bwd_t_kernel(const bf16_t* __restr
 // a v_perm_b32 8 x 8 transpose as 16-byte column segments. No LDS round trip and 256-384 B of
 // loads in flight per lane. A wave covers 64 rows x 64 columns; grid (ceil(F / 256), rows / 64);
 // rows % 8 == 0 and F % 8 == 0 (checked by the launcher; other shapes take the LDS kernels).
-typedef uint32_t ew_u32x4 __attribute__((ext_vector_type(4)));
-
-// out[j] = column j of the 8 x 8 bf16 block held as 8 row vectors v[0..7]
-__device__ __forceinline__ void ew_tr8(const bf16x8 (&v)[8], bf16x8 (&out)[8]) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const uint32_t sel = (j & 1) ? 0x07060302u : 0x05040100u;
-    ew_u32x4 o;
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      o[k] = __builtin_amdgcn_perm(__builtin_bit_cast(ew_u32x4, v[2 * k + 1])[j >> 1],
-                                   __builtin_bit_cast(ew_u32x4, v[2 * k])[j >> 1], sel);
-    out[j] = __builtin_bit_cast(bf16x8, o);
-  }
-}
-
 __global__ __launch_bounds__(256) void swiglu_fwd_t_reg_kernel(const bf16_t* __restrict__ gu,
                                                                 bf16_t* __restrict__ out,
                                                                 bf16_t* __restrict__ outT,
@@ -213,7 +197,7 @@ __global__ __launch_bounds__(256) void swiglu_fwd_t_reg_kernel(const bf16_t* __r
     store_bf16x8(out + (r + i) * F + c, o[i]);
   }
   bf16x8 t[8];
-  ew_tr8(o, t);
+  tr8_bf16(o, t);
 #pragma unroll
   for (int j = 0; j < 8; ++j) store_bf16x8(outT + static_cast<int64_t>(c + j) * rows + r, t[j]);
 }
@@ -245,10 +229,10 @@ __global__ __launch_bounds__(256) void swiglu_bwd_t_reg_kernel(const bf16_t* __r
     }
   }
   bf16x8 t[8];
-  ew_tr8(dg, t);
+  tr8_bf16(dg, t);
 #pragma unroll
   for (int j = 0; j < 8; ++j) store_bf16x8(dguT + static_cast<int64_t>(c + j) * rows + r, t[j]);
-  ew_tr8(du, t);
+  tr8_bf16(du, t);
 #pragma unroll
   for (int j = 0; j < 8; ++j) store_bf16x8(dguT + static_cast<int64_t>(F + c + j) * rows + r, t[j]);
 }

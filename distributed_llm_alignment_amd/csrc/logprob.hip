@@ -128,6 +128,42 @@ __global__ __launch_bounds__(256) void logprob_bwd_kernel(bf16_t* __restrict__ l
   }
 }
 
+// The same gradient with a transposed second output (the LM head's TN weight-gradient operand):
+// dlogits written in place AND dlogitsT [V, rows] (ld = rows), from one read of the logits, in
+// place of the in-place kernel + a separate transpose pass (which reads and writes the [rows, V]
+// gradient once more: 815 us per Llama-3-8B DPO micro-batch, profiles/r6_*). Each lane owns an
+// 8 x 8 block (8 rows x 8 vocab columns) and transposes it in registers (tr8_bf16); a wave covers
+// 64 rows x 64 columns; grid (ceil(V / 256), rows / 64); rows % 8 == 0, V % 8 == 0, ld % 8 == 0.
+__global__ __launch_bounds__(256) void logprob_bwd_t_kernel(bf16_t* __restrict__ logits, int64_t ld, int V,
+                                                             int64_t off, const int64_t* __restrict__ tgt,
+                                                             const float* __restrict__ lse_in,
+                                                             const float* __restrict__ g,
+                                                             bf16_t* __restrict__ outT, int64_t rows) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t r = static_cast<int64_t>(blockIdx.y) * 64 + (lane >> 3) * 8;
+  const int c = blockIdx.x * 256 + w * 64 + (lane & 7) * 8;
+  if (r >= rows || c >= V) return;
+  bf16x8 a[8], o[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a[i] = load_bf16x8(logits + (r + i) * ld + c);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int64_t t = tgt[r + i] - off;
+    const float gr = tgt[r + i] >= 0 ? g[r + i] : 0.f;
+    const float lse = lse_in[r + i];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float p = __expf(bf2f(a[i][j]) - lse);
+      o[i][j] = f2bf(gr * ((c + j == t ? 1.f : 0.f) - p));
+    }
+    store_bf16x8(logits + (r + i) * ld + c, o[i]);
+  }
+  bf16x8 tt[8];
+  tr8_bf16(o, tt);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) store_bf16x8(outT + static_cast<int64_t>(c + j) * rows + r, tt[j]);
+}
+
 // Ensemble forward-KL distillation, one row per block:
 //   p_bar = mean_k softmax(teacher_k), q = softmax(student)
 //   kl[r] = sum_v p_bar (log p_bar - log q)
@@ -185,6 +221,15 @@ void launch_logprob_bwd(bf16_t* logits, int64_t ld, int V, int64_t off, int64_t 
   const bool vec = (V % 8 == 0) && (ld % 8 == 0);
   if (vec) logprob_bwd_kernel<true><<<rows, 256, 0, st>>>(logits, ld, V, off, tgt, lse, g);
   else logprob_bwd_kernel<false><<<rows, 256, 0, st>>>(logits, ld, V, off, tgt, lse, g);
+}
+
+bool launch_logprob_bwd_t(bf16_t* logits, int64_t ld, int V, int64_t rows, int64_t off, const int64_t* tgt,
+                          const float* lse, const float* g, bf16_t* outT, hipStream_t st) {
+  if (rows % 8 != 0 || V % 8 != 0 || ld % 8 != 0) return false;
+  if (rows == 0) return true;
+  const dim3 grid((V + 255) / 256, static_cast<unsigned>((rows + 63) / 64));
+  logprob_bwd_t_kernel<<<grid, 256, 0, st>>>(logits, ld, V, off, tgt, lse, g, outT, rows);
+  return true;
 }
 
 void launch_row_lse(const bf16_t* logits, int64_t ld, int V, int64_t rows, float* lse,

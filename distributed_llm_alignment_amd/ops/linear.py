@@ -240,11 +240,13 @@ def add_gemm(x2: torch.Tensor, weight: torch.Tensor, c2: torch.Tensor) -> torch.
     return torch.addmm(c2, x2, weight.t())
 
 
-class _LinearAddMainGradFn(torch.autograd.Function):
+class _LinearAddFn(torch.autograd.Function):
     """resid + x @ W^T as ONE hipBLASLt GEMM (the residual is the C input, beta = 1, C != D): the
     decoder's o / down projections add their output onto the residual stream in the epilogue,
     so the following RMSNorm reads one tensor and writes one instead of reading two and writing
-    two. Backward: d(resid) = dy, the rest as _LinearMainGradFn."""
+    two. Backward: d(resid) = dy, the rest as _LinearMainGradFn (main_grad accumulation when the
+    engine attached one, a plain .grad otherwise: the custom op has no autograd kernel of its
+    own, so every differentiable call must come through here)."""
 
     @staticmethod
     def forward(ctx, x, weight, resid):
@@ -273,8 +275,8 @@ def linear_add(x: torch.Tensor, weight: torch.Tensor, resid: torch.Tensor) -> to
     """resid + linear(x, weight), the add inside the GEMM (bias-free projections)."""
     if fp8_inference_ok(x, weight, None):
         return fp8_linear_frozen(x, weight).add_(resid)
-    if uses_main_grad(weight):
-        return _LinearAddMainGradFn.apply(x, weight, resid)
+    if torch.is_grad_enabled() and (x.requires_grad or weight.requires_grad or resid.requires_grad):
+        return _LinearAddFn.apply(x, weight, resid)
     N = weight.shape[0]
     return add_gemm(x.reshape(-1, x.shape[-1]), weight, resid.reshape(-1, N)).view(resid.shape)
 

@@ -5,7 +5,9 @@ ever materialising fp32 [N, V] tensors:
   * forward: one hipBLASLt GEMM -> bf16 logits; the HIP row kernel streams each logits row once
     (online max/sum) and emits logp + lse (fp32, per row).
   * backward: the HIP kernel rewrites the SAVED bf16 logits in place into dlogits
-    (g * (onehot - softmax)), which feed the two grad GEMMs directly (dH = dL W, dW = dL^T H).
+    (g * (onehot - softmax)), which feed the two grad GEMMs directly (dH = dL W, dW = dL^T H);
+    with a main_grad on the LM head the same kernel also writes dL^T, the TN weight-gradient
+    operand, so no separate transpose pass re-reads the [N, V] gradient.
     With grads off (frozen reference / reward scoring) logits are produced chunk by chunk and
     dropped, so the no-grad footprint is one chunk.
 Semantics mirror the reference `compute_logprobs` (src/training/train_dpo.py:31-39): logits in
@@ -16,6 +18,7 @@ exactly the reference's `/ mask.sum(1).clamp(min=1)`, or sum) as a HIP kernel pa
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -28,6 +31,8 @@ from .linear import input_grad
 # Llama-3 vocabulary is a 2.1 GB bf16 transient, one GEMM per DPO micro-batch (two 4096-row
 # chunks ran 2 x 2.93 ms vs 5.5 ms for the one 8192-row GEMM in the step, profiles/r6_*)
 _NO_GRAD_CHUNK = 8192
+# dlogits^T from the logprob backward kernel (A/B switch, read once)
+LOGPROB_T = os.environ.get("DLA_LOGPROB_T", "1") != "0"
 
 
 def _ref_linear_logprob(hidden, weight, targets):
@@ -63,14 +68,26 @@ class _LinearLogprobFn(torch.autograd.Function):
         ops = _ext.require()
         hidden, targets, lse, logits = ctx.saved_tensors
         weight = ctx.weight
-        ops.logprob_bwd(logits, targets, lse, g.float().contiguous())
+        from .linear import _tn_ok, accumulate_weight_grad
+
+        g = g.float().contiguous()
+        dlt = None
+        mg = getattr(weight, "main_grad", None)
+        if (LOGPROB_T and ctx.needs_input_grad[1] and mg is not None and not getattr(weight, "_dla_shared", False)
+                and _tn_ok(mg, logits.shape[0])):
+            # the LM head's weight gradient runs as a TN GEMM on dlogits^T: write it from the
+            # same pass that turns the logits into dlogits (undefined when the shape is outside
+            # the kernel -> in-place kernel + transpose inside accumulate_weight_grad)
+            dlt = ops.logprob_bwd_t(logits, targets, lse, g)
+            if not dlt.numel():
+                dlt = None
+        if dlt is None:
+            ops.logprob_bwd(logits, targets, lse, g)
         dlogits = logits  # rewritten in place
         dh = input_grad(dlogits, weight) if ctx.needs_input_grad[0] else None
         dw = None
         if ctx.needs_input_grad[1]:
-            from .linear import accumulate_weight_grad
-
-            if not accumulate_weight_grad(weight, dlogits, hidden):
+            if not accumulate_weight_grad(weight, dlogits, hidden, dyt=dlt):
                 dw = dlogits.t() @ hidden
         return dh, dw, None
 

@@ -557,6 +557,41 @@ def test_linear_logprob(V):
     assert rel_err(W.grad, Wr.grad) < 3e-2
 
 
+@pytest.mark.parametrize("N,V", [(96, 32000), (200, 50264), (72, 128256)])
+def test_logprob_bwd_transposed_output(N, V):
+    """logprob_bwd_t: the in-place dlogits identical to logprob_bwd's, and the second output
+    exactly its transpose (rows not a multiple of 64, V not of 256 in the middle case)."""
+    x = bf(torch.randn(N, V) * 3)
+    tgt = torch.randint(0, V, (N,), device=DEV)
+    tgt[3] = -100
+    _, lse = _ext.require().logprob_fwd(x, tgt)
+    g = torch.randn(N, device=DEV)
+    a = x.clone()
+    _ext.require().logprob_bwd(a, tgt, lse, g)
+    b = x.clone()
+    bt = _ext.require().logprob_bwd_t(b, tgt, lse, g)
+    assert bt.shape == (V, N)
+    assert torch.equal(a, b)
+    assert torch.equal(bt, a.t())
+
+
+def test_lm_head_main_grad_uses_transposed_dlogits():
+    """linear_logprob on an LM head with an engine main_grad (the DPO step's path: dlogits^T
+    from the logprob backward kernel) against the plain .grad path."""
+    N, H, V = 256, 512, 4096
+    h = bf(torch.randn(N, H))
+    W = bf(torch.randn(V, H) * 0.05)
+    tgt = torch.randint(0, V, (N,), device=DEV)
+    g = torch.randn(N, device=DEV)
+    W1 = W.clone().requires_grad_()
+    W1.main_grad = torch.zeros(V, H, device=DEV, dtype=torch.float32)
+    (ops.linear_logprob(h, W1, tgt) * g).sum().backward()
+    W2 = W.clone().requires_grad_()
+    (ops.linear_logprob(h, W2, tgt) * g).sum().backward()
+    assert W1.grad is None
+    assert rel_err(W1.main_grad, W2.grad.float()) < 1e-2
+
+
 def test_sequence_logprob_and_dpo_loss_kernels():
     S, T = 6, 50
     lp = torch.randn(S, T, device=DEV).requires_grad_()

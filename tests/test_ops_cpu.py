@@ -88,6 +88,21 @@ def test_norms_match_torch():
     assert torch.allclose(y2, F.layer_norm(x, (32,), w, b, 1e-5), atol=1e-5)
 
 
+def test_linear_add_grads_without_main_grad():
+    """ops.linear_add (the residual add inside the projection GEMM) must be differentiable on
+    plain .grad weights too: its GPU custom op has no autograd kernel of its own."""
+    x = torch.randn(5, 8, requires_grad=True)
+    w = torch.randn(6, 8, requires_grad=True)
+    r = torch.randn(5, 6, requires_grad=True)
+    y = ops.linear_add(x, w, r)
+    g = torch.randn_like(y)
+    (y * g).sum().backward()
+    assert torch.allclose(y, r + x @ w.t(), atol=1e-5)
+    assert torch.allclose(x.grad, g @ w, atol=1e-5)
+    assert torch.allclose(w.grad, g.t() @ x, atol=1e-5)
+    assert torch.allclose(r.grad, g)
+
+
 def test_linear_logprob_matches_compute_logprobs():
     """Reference compute_logprobs (train_dpo.py:31-39) on explicit logits."""
     torch.manual_seed(1)

@@ -111,6 +111,11 @@ PASSES = {
                       ("window", ["--window", "adamw", "--seq=-1500:1500"]), ("streams", ["--window", "adamw"])], 500),
                 prof("ppo", "python -u tools/bench_rlhf.py --algorithm ppo --zero-shape 8 --batch 8 --steps 1 --warmup 1",
                      [("window", ["--by-grid", "--top", "50"]), ("window", ["--seq=-6000:6000"])], 500)],
+    # LM-head dlogits^T written by the logprob backward kernel vs in-place kernel + transpose
+    "r6-lpt": [pytest("tests/test_kernels_gpu.py tests/test_decode_gpu.py", 900),
+               ab("logprob_t", DPO + " --steps 5 --warmup 2", {"on": {"DLA_LOGPROB_T": "1"},
+                                                              "off": {"DLA_LOGPROB_T": "0"}}, 2, 300),
+               prof("dpo", DPO + " --steps 2 --warmup 1", DPO_TABLES)],
     # the whole DPO step's launches in issue order (which GEMM runs where, at what cost in place)
     # and the GEMM probe's arms under a kernel trace (which library kernel each form picks)
     "r6-seq": [prof("dpo_seq", DPO + " --steps 2 --warmup 1", [("window", ["--window", "adamw", "--seq", "0:7000"])]),
