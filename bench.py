@@ -323,10 +323,21 @@ def main(argv=None) -> int:
     from distributed_llm_alignment_amd.parallel.collectives import ShapeGroup
 
     shape_mode = args.tp_shape > 1 or args.fsdp_shape > 1 or args.ep_shape > 1
-    if shape_mode and (world != 1 or args.tp != 1 or args.ep != 1 or args.sp != 1 or st.forced):
-        raise SystemExit("bench.py: the --*-shape modes are one-GPU debug modes (world 1, no --tp/--ep/--sp)")
+    # --tp-shape N with --force-pg: rank 0's TP shards of an N-way group (per-rank GEMM shapes),
+    # but the TP collectives run on the real one-rank RCCL communicator (RCCL's stream, its
+    # kernels in the trace) instead of a ShapeGroup stand-in
+    tp_forced = args.tp_shape > 1 and st.forced
+    if shape_mode and (world != 1 or args.tp != 1 or args.ep != 1 or args.sp != 1
+                       or (st.forced and (args.fsdp_shape > 1 or args.ep_shape > 1))):
+        raise SystemExit("bench.py: the --*-shape modes are one-GPU debug modes (world 1, no --tp/--ep/--sp; "
+                         "--force-pg only with --tp-shape)")
     # one rank of a TP group / FSDP group that does not exist: ShapeGroup stand-ins
-    tp_group = ShapeGroup(args.tp_shape) if args.tp_shape > 1 else mesh.tp_group
+    if tp_forced:
+        import torch.distributed as dist
+
+        tp_group = dist.group.WORLD
+    else:
+        tp_group = ShapeGroup(args.tp_shape) if args.tp_shape > 1 else mesh.tp_group
     fsdp_group = ShapeGroup(args.fsdp_shape) if args.fsdp_shape > 1 else mesh.dp_group
     cfg = get_config(args.model, **overrides)
     dtype = torch.bfloat16 if dev.type == "cuda" else torch.float32
@@ -343,8 +354,9 @@ def main(argv=None) -> int:
 
         enable_fp8_inference(ref)
     if mesh.tp > 1 or args.tp_shape > 1:
-        apply_tensor_parallel(policy, tp_group, sequence_parallel=args.tp_seq)
-        apply_tensor_parallel(ref, tp_group, sequence_parallel=args.tp_seq)
+        kw = dict(tp_rank=0, tp_size=args.tp_shape, force=True) if tp_forced else {}
+        apply_tensor_parallel(policy, tp_group, sequence_parallel=args.tp_seq, **kw)
+        apply_tensor_parallel(ref, tp_group, sequence_parallel=args.tp_seq, **kw)
     if mesh.sp > 1:
         from distributed_llm_alignment_amd.parallel.sequence import apply_sequence_parallel
 
@@ -513,8 +525,9 @@ def main(argv=None) -> int:
             "data": "synthetic preference pairs (random token ids), random-init weights",
             "config": {
                 "model": (cfg.name if args.layers is None else f"{cfg.name}-L{args.layers}(debug)")
-                         + (f"(one rank of a {shape_info['mesh']} mesh, local stand-in collectives, debug)"
-                            if shape_mode and args.ep_shape <= 1 else "")
+                         + (f"(one rank of a {shape_info['mesh']} mesh, "
+                            + ("TP collectives on a one-rank RCCL group" if tp_forced else "local stand-in collectives")
+                            + ", debug)" if shape_mode and args.ep_shape <= 1 else "")
                          + (f"(one EP rank of ep{args.ep_shape}: {cfg.num_experts // args.ep_shape} "
                             "local experts/layer, a2a as local copies, debug)" if args.ep_shape > 1 else "")
                          + (f"(hot expert: every source at capacity {args.ep_capacity})" if args.ep_hot else ""),

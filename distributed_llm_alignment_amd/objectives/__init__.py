@@ -161,14 +161,56 @@ def ppo_rollout_stats(policy, ref, critic, seqs, mask, prompt_len: int, scores, 
             "kl": kl.sum(1) / act.sum(1).clamp(min=1), "scores": scores.float()}
 
 
+# The actor and the critic of a PPO minibatch are independent until the summed loss: the critic's
+# forward (and, through autograd's per-node streams, its backward) runs on a side stream so the two
+# models' kernels share the chip. At the PPO shapes (4 rollouts x 768 tokens per minibatch) the
+# o / down projections are [3072, 4096] outputs = 192 256x256 tiles for 256 CUs, so one model alone
+# leaves a quarter of the CUs idle in every such GEMM. DLA_PPO_CRITIC_STREAM=0: one stream.
+PPO_CRITIC_STREAM = os.environ.get("DLA_PPO_CRITIC_STREAM", "1") != "0"
+_CRITIC_STREAMS: Dict[int, "torch.cuda.Stream"] = {}
+
+
+def ppo_critic_stream(device: torch.device):
+    """The side stream the critic runs on (None off the GPU or when disabled)."""
+    if not (PPO_CRITIC_STREAM and device.type == "cuda"):
+        return None
+    i = device.index if device.index is not None else torch.cuda.current_device()
+    if i not in _CRITIC_STREAMS:
+        _CRITIC_STREAMS[i] = torch.cuda.Stream(device=i)
+    return _CRITIC_STREAMS[i]
+
+
 def ppo_loss(policy, critic, seqs, mask, stats: Dict[str, torch.Tensor], clip_eps: float = 0.2,
              value_clip: float = 0.2, vf_coef: float = 0.1):
-    """Clipped surrogate (HIP fused fwd+bwd) + vf_coef * clipped value loss on one minibatch."""
+    """Clipped surrogate (HIP fused fwd+bwd) + vf_coef * clipped value loss on one minibatch.
+    Run its backward through `ppo_backward` (joins the critic's stream afterwards)."""
+    cs = ppo_critic_stream(seqs.device)
+    main = torch.cuda.current_stream(seqs.device) if cs is not None else None
+    if cs is not None:
+        cs.wait_stream(main)  # the critic's weights (last optimizer step) and this minibatch
+        with torch.cuda.stream(cs):
+            v = critic(seqs, mask)
+            vl = ops.ppo_value_loss(v, stats["values"], stats["returns"], stats["act"], value_clip)
     lp = policy.token_logprobs(seqs, mask)
     pl, pm = ops.ppo_policy_loss(lp, stats["old_logp"], stats["advantages"], stats["act"], clip_eps)
-    v = critic(seqs, mask)
-    vl = ops.ppo_value_loss(v, stats["values"], stats["returns"], stats["act"], value_clip)
+    if cs is None:
+        v = critic(seqs, mask)
+        vl = ops.ppo_value_loss(v, stats["values"], stats["returns"], stats["act"], value_clip)
+    else:
+        main.wait_stream(cs)
+        vl.record_stream(main)
     return pl + vf_coef * vl, {"policy_loss": pl.detach(), "value_loss": vl.detach(), **pm}
+
+
+def ppo_backward(loss: torch.Tensor) -> None:
+    """loss.backward() for `ppo_loss`: the critic's backward nodes run on its side stream and its
+    weight gradients are accumulated there (GEMM-epilogue main_grad writes that autograd does not
+    order against the caller's stream), so the caller's stream waits for that stream before the
+    optimizer steps read the gradient buffers."""
+    loss.backward()
+    cs = ppo_critic_stream(loss.device)
+    if cs is not None:
+        torch.cuda.current_stream(loss.device).wait_stream(cs)
 
 
 # Tokens per ensemble-KL chunk: (teachers + 1) x chunk x V bf16 logits exist at a time

@@ -376,7 +376,7 @@ class DataParallelEngine:
 
     def finish_grad_sync(self):
         """Launch buckets whose params got no gradient (unused params), then wait for all."""
-        if self.shape_only and self._sync:  # the reduce-scatter's output: this rank's chunks
+        if self.shape_only:  # the reduce-scatter's output: this rank's chunks (overwritten)
             for b in self.buckets:
                 c = b.size // b.world
                 self.grad_shard[b.shard_off:b.shard_off + c].copy_(self._chunk(self.grad_buf, b))
@@ -484,7 +484,11 @@ class DataParallelEngine:
         if self.grad_fp32:
             for p in self.params:
                 p.grad = None
-        if self.zero:
+        if self.zero and not (self._comm or self.shape_only):
+            # with a collective (or its shape-only local copy) every bucket's reduce-scatter
+            # OVERWRITES its shard each step (finish_grad_sync launches the buckets no gradient
+            # reached), so zeroing it too only costs a pass over the shard: 16 GB of HBM writes
+            # per step on the forced one-rank Llama-3-8B layout (profiles/r6_rlhf_forced.md)
             self.grad_shard.zero_()
 
     @torch.no_grad()

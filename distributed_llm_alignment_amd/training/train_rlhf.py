@@ -37,7 +37,7 @@ import torch
 from ..data import read_jsonl
 from ..models import (build_reward_model, build_value_model, generate, load_causal_lm,
                       load_reward_checkpoint)
-from ..objectives import ppo_loss, ppo_rollout_stats, rlhf_loss
+from ..objectives import ppo_backward, ppo_loss, ppo_rollout_stats, rlhf_loss
 from ..parallel.dist import barrier, split_for_rank
 from ..utils.checkpoint import save_state
 from ..utils.config import add_config_args, config_from_args
@@ -255,7 +255,7 @@ def _ppo_loop(ctx, config, ppo, policy, ref, rm, rollout, engine, steps, kl_coef
                     continue
                 mb = {k: v[a:b] for k, v in stats.items() if k in ("old_logp", "values", "advantages", "returns", "act")}
                 loss, m = ppo_loss(policy.model, critic, seqs[a:b], mask[a:b], mb, clip, vclip, vf_coef)
-                loss.backward()
+                ppo_backward(loss)
                 last = ep == epochs - 1 and mi == len(bounds) - 1
                 if last and overlap and step + 1 < steps:
                     # overlaps the in-flight ZeRO-0/1 bucket collectives (they are waited on in

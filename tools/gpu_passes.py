@@ -116,6 +116,46 @@ PASSES = {
                ab("logprob_t", DPO + " --steps 5 --warmup 2", {"on": {"DLA_LOGPROB_T": "1"},
                                                               "off": {"DLA_LOGPROB_T": "0"}}, 2, 300),
                prof("dpo", DPO + " --steps 2 --warmup 1", DPO_TABLES)],
+    # forced-comm RLHF update after the shard-zeroing and C != D selection fixes: plain and forced
+    # interleaved on one box, then the PPO update at the 8-rank ZeRO-1 shape
+    "r6-rlhf2": [run("rlhf_plain0", "python -u tools/bench_rlhf.py --batch 8", 400),
+                 run("rlhf_forced0", "python -u tools/bench_rlhf.py --batch 8 --force-pg", 400),
+                 run("rlhf_plain1", "python -u tools/bench_rlhf.py --batch 8", 400),
+                 run("rlhf_forced1", "python -u tools/bench_rlhf.py --batch 8 --force-pg", 400),
+                 pytest("tests/test_ppo_shape.py", 300),
+                 ab("ppo_critic_stream", "python -u tools/bench_rlhf.py --algorithm ppo --zero-shape 8 --batch 8",
+                    {"side": {"DLA_PPO_CRITIC_STREAM": "1"}, "one": {"DLA_PPO_CRITIC_STREAM": "0"}}, 1, 500),
+                 prof("rlhf_forced", "python -u tools/bench_rlhf.py --batch 8 --force-pg --steps 2 --warmup 1",
+                      [("window", ["--window", "adamw", "--by-grid", "--top", "40"]), ("streams", ["--window", "adamw"])], 500)],
+    # Llama-3-70B meshes on one build: 8x1 ZeRO-3 with full recompute and an 8-pair micro-batch;
+    # 1x8 TP on the real one-rank RCCL group (per-rank shard shapes) vs the ShapeGroup stand-in;
+    # 2x4; then an 8-layer TP stack under a kernel trace for the comm-stream overlap table
+    "r6-70b": [run("zero3_8x1_recompute", L70 + " --zero 3 --fsdp-shape 8 --micro-pairs 8 --accum 2 --grad-ckpt full", 900),
+               run("tp8_forced", L70 + " --tp-shape 8 --force-pg --micro-pairs 2 --accum 8", 600),
+               run("tp8_shape", L70 + " --tp-shape 8 --micro-pairs 2 --accum 8", 600),
+               run("fsdp2_tp4", L70 + " --zero 3 --fsdp-shape 2 --tp-shape 4 --micro-pairs 2 --accum 8", 600),
+               prof("tp8_forced_stack", L70 + " --tp-shape 8 --force-pg --micro-pairs 2 --accum 8 --layers 8",
+                    [("streams", ["--window", "adamw"]), ("window", ["--window", "adamw", "--by-grid", "--top", "30"])], 500),
+               prof("tp8seq_forced_stack", L70 + " --tp-shape 8 --tp-seq --force-pg --micro-pairs 2 --accum 8 --layers 8",
+                    [("streams", ["--window", "adamw"]), ("window", ["--window", "adamw", "--by-grid", "--top", "30"])], 500)],
+    # Mixtral-8x7B on one build: EP 8 balanced vs the hot-expert rank (interleaved), EP 4 x EDP 2
+    # bf16 / fp8, and the hot / balanced pair at capacity 1.125
+    "r6-mixtral": [run("ep8_bal0", MIX_EP8 + " --steps 3 --warmup 2", 500),
+                   run("ep8_hot0", MIX_EP8 + " --ep-hot --steps 3 --warmup 2", 500),
+                   run("ep8_bal1", MIX_EP8 + " --steps 3 --warmup 2", 500),
+                   run("ep8_hot1", MIX_EP8 + " --ep-hot --steps 3 --warmup 2", 500),
+                   run("ep4_edp2", DPO + " --model mixtral-8x7b --ep-shape 4 --edp-shape 2 --micro-pairs 2 --accum 8"
+                       " --ep-capacity 1.25 --steps 3 --warmup 2", 500),
+                   run("ep4_edp2_fp8", DPO + " --model mixtral-8x7b --ep-shape 4 --edp-shape 2 --micro-pairs 2 --accum 8"
+                       " --ep-capacity 1.25 --fp8 --steps 3 --warmup 2", 500),
+                   run("ep8_bal_cf1125", DPO + " --model mixtral-8x7b --ep-shape 8 --micro-pairs 2 --accum 8"
+                       " --ep-capacity 1.125 --steps 3 --warmup 2", 500),
+                   run("ep8_hot_cf1125", DPO + " --model mixtral-8x7b --ep-shape 8 --micro-pairs 2 --accum 8"
+                       " --ep-capacity 1.125 --ep-hot --steps 3 --warmup 2", 500),
+                   prof("ep8_hot", MIX_EP8 + " --ep-hot --steps 2 --warmup 1",
+                        [("window", ["--window", "adamw", "--by-grid", "--top", "40"])], 500),
+                   prof("ep8_bal", MIX_EP8 + " --steps 2 --warmup 1",
+                        [("window", ["--window", "adamw", "--by-grid", "--top", "40"])], 500)],
     # the whole DPO step's launches in issue order (which GEMM runs where, at what cost in place)
     # and the GEMM probe's arms under a kernel trace (which library kernel each form picks)
     "r6-seq": [prof("dpo_seq", DPO + " --steps 2 --warmup 1", [("window", ["--window", "adamw", "--seq", "0:7000"])]),
