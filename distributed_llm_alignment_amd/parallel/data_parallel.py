@@ -221,7 +221,17 @@ class DataParallelEngine:
             b.shard_off = shard
             shard += b.size // b.world
         self.shard_numel = shard
-        if self.zero:
+        # every bucket over a ONE-rank group (the forced one-rank RCCL path, or EP buckets whose
+        # experts live on this rank only): a rank's chunk IS its bucket, in the same order, so the
+        # shards alias the flat buffers -- the reduce-scatter and all-gather are issued in place
+        # (sendbuff == recvbuff: nothing to move) instead of copying 2 x 16 GB per Llama-3-8B
+        # step into and out of separate shard buffers (profiles/r6_rlhf_forced.md), and the
+        # 16 GB + 16 GB of shard memory are not allocated
+        self.shard_alias = self.zero and not self.shape_only and all(b.world == 1 for b in self.buckets)
+        if self.zero and self.shard_alias:
+            self.grad_shard = self.grad_buf
+            self.param_shard = self.param_buf
+        elif self.zero:
             self.grad_shard = torch.zeros(shard, dtype=self.grad_dtype, device=self.device)
             self.param_shard = torch.empty(shard, dtype=self.dtype, device=self.device)
             torch.cat([self._chunk(self.param_buf, b) for b in self.buckets], out=self.param_shard)
@@ -351,7 +361,7 @@ class DataParallelEngine:
         b = self.buckets[bi]
         g = self.grad_buf[b.start:b.end]
         if b.world == 1 and not self.force_comm:  # expert bucket whose experts live here only
-            if self.zero:
+            if self.zero and not self.shard_alias:
                 self.grad_shard[b.shard_off:b.shard_off + b.size].copy_(g)
             return
         self.comm_ops += 1
@@ -462,7 +472,8 @@ class DataParallelEngine:
                 b = self.buckets[bi]
                 c = b.size // b.world
                 if b.world == 1 and not self.force_comm:
-                    self.param_buf[b.start:b.end].copy_(self.param_shard[b.shard_off:b.shard_off + c])
+                    if not self.shard_alias:
+                        self.param_buf[b.start:b.end].copy_(self.param_shard[b.shard_off:b.shard_off + c])
                 elif self.shape_only:  # the all-gather's local part
                     self._chunk(self.param_buf, b).copy_(self.param_shard[b.shard_off:b.shard_off + c])
                 else:
@@ -500,7 +511,7 @@ class DataParallelEngine:
                 if b.world > 1:
                     gsrc = coll.get_global_rank(b.group, src) if b.group is not None else src
                     coll.broadcast(self.param_buf[b.start:b.end], src=gsrc, group=b.group)
-            if self.zero:
+            if self.zero and not self.shard_alias:
                 torch.cat([self._chunk(self.param_buf, b) for b in self.buckets], out=self.param_shard)
             if self.master is not None:
                 self.master.copy_(self.param_shard)  # (copy_ converts in place: no fp32 temporary)
@@ -509,7 +520,7 @@ class DataParallelEngine:
     def sync_master_from_params(self):
         self.wait_params()
         self._wt_epoch[0] += 1
-        if self.zero:
+        if self.zero and not self.shard_alias:
             torch.cat([self._chunk(self.param_buf, b) for b in self.buckets], out=self.param_shard)
         if self.master is not None:
             self.master.copy_(self.param_shard)  # (copy_ converts in place: no fp32 temporary)

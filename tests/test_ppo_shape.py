@@ -64,10 +64,40 @@ def test_ppo_step_zero_shape_gpu():
     _check_shape(ceng, c0, 8)
 
 
+def _ppo_grads(dev):
+    """Policy and critic gradient buffers after one PPO minibatch backward (no optimizer step)."""
+    from distributed_llm_alignment_amd.models import build_model, get_config
+    from distributed_llm_alignment_amd.models.reward import ValueModel
+    from distributed_llm_alignment_amd.objectives import ppo_backward, ppo_loss, ppo_rollout_stats
+    from distributed_llm_alignment_amd.parallel.data_parallel import DataParallelEngine
+
+    cfg = get_config("tiny-llama-d128", num_layers=2)
+    torch.manual_seed(0)  # the value head's init draws from the global generator
+    pol = build_model(cfg, device=dev, dtype=torch.bfloat16, seed=0)
+    ref = build_model(cfg, device=dev, dtype=torch.bfloat16, seed=0).requires_grad_(False).eval()
+    critic = ValueModel(build_model(cfg, device=dev, dtype=torch.bfloat16, seed=1, headless=True))
+    eng, ceng = DataParallelEngine(pol, lr=1e-3), DataParallelEngine(critic, lr=1e-3)
+    g = torch.Generator().manual_seed(0)
+    P, R, S = 16, 16, 4
+    seqs = torch.randint(3, cfg.vocab_size, (S, P + R), generator=g).to(dev)
+    mask = torch.ones_like(seqs)
+    scores = torch.randn(S, generator=g).to(dev)
+    stats = ppo_rollout_stats(pol, ref, critic, seqs, mask, P, scores, 0.05, 1.0, 0.95)
+    mb = {k: v for k, v in stats.items() if k in ("old_logp", "values", "advantages", "returns", "act")}
+    # advantages are whitened over the batch: perturb old_logp so the ratio is not exactly 1
+    mb["old_logp"] = mb["old_logp"] - 0.05
+    loss, _ = ppo_loss(pol, critic, seqs, mask, mb, 0.2, 0.2, 0.1)
+    ppo_backward(loss)
+    torch.cuda.synchronize()
+    return eng.grad_buf.float().clone(), ceng.grad_buf.float().clone()
+
+
 @pytest.mark.gpu
 def test_ppo_critic_side_stream_matches_one_stream():
     """The critic's forward / backward on its side stream (objectives.PPO_CRITIC_STREAM) gives the
-    same updated weights of both models as the single-stream update."""
+    policy and critic gradients of the single-stream backward (compared before any optimizer
+    step: AdamW's first update is lr x sign(g), which turns rounding-level noise into lr-sized
+    weight differences)."""
     import distributed_llm_alignment_amd.objectives as obj
     from distributed_llm_alignment_amd.ops import _ext
 
@@ -77,10 +107,9 @@ def test_ppo_critic_side_stream_matches_one_stream():
     try:
         for on in (True, False):
             obj.PPO_CRITIC_STREAM = on
-            eng, ceng, _, _ = _ppo_step(torch.device("cuda", 0), 8)
-            torch.cuda.synchronize()
-            out[on] = (eng.param_buf.detach().float().clone(), ceng.param_buf.detach().float().clone())
+            out[on] = _ppo_grads(torch.device("cuda", 0))
     finally:
         obj.PPO_CRITIC_STREAM = prev
     for a, b in zip(out[True], out[False]):
-        assert torch.equal(a, b)
+        assert a.abs().sum() > 0
+        assert ((a - b).norm() / b.norm()).item() < 1e-2

@@ -122,7 +122,9 @@ PASSES = {
                  run("rlhf_forced0", "python -u tools/bench_rlhf.py --batch 8 --force-pg", 400),
                  run("rlhf_plain1", "python -u tools/bench_rlhf.py --batch 8", 400),
                  run("rlhf_forced1", "python -u tools/bench_rlhf.py --batch 8 --force-pg", 400),
-                 pytest("tests/test_ppo_shape.py", 300),
+                 pytest("tests/test_ppo_shape.py tests/test_engines_gpu.py tests/test_distributed_gpu.py", 600),
+                 run("dpo_plain", DPO + " --steps 5 --warmup 2", 300),
+                 run("dpo_force_pg", DPO + " --force-pg --steps 5 --warmup 2", 300),
                  ab("ppo_critic_stream", "python -u tools/bench_rlhf.py --algorithm ppo --zero-shape 8 --batch 8",
                     {"side": {"DLA_PPO_CRITIC_STREAM": "1"}, "one": {"DLA_PPO_CRITIC_STREAM": "0"}}, 1, 500),
                  prof("rlhf_forced", "python -u tools/bench_rlhf.py --batch 8 --force-pg --steps 2 --warmup 1",
