@@ -80,7 +80,7 @@ def init_distributed(backend: Optional[str] = None, timeout_s: int = 1800,
             os.environ.setdefault("MASTER_PORT", "29500")
         if be == "nccl":
             kwargs["device_id"] = dev
-            opts = comm_pg_options()
+            opts = comm_pg_options(world)
             if opts is not None:
                 kwargs["pg_options"] = opts
         dist.init_process_group(**kwargs)
@@ -97,12 +97,18 @@ def init_distributed(backend: Optional[str] = None, timeout_s: int = 1800,
 # (profiles/r5_force_pg_streams.md). A high-priority stream gets its own (priority) queue, so the
 # gradient collectives really run beside the backward GEMMs. DLA_RCCL_HIGH_PRIORITY=0 keeps torch's
 # default (normal-priority pool stream).
+# The priority queue is not free: with the one-rank group's collectives in place (no RCCL kernels
+# at all), the RLHF update ran 0.405 s with it vs 0.353 s without (= the no-group run, 0.354 s),
+# and the 70B TP-8 rank step 2132 vs 2034 ms: its pending stream waits alone slow the
+# bandwidth-bound kernels of the compute queue 2-3x (profiles/r6_rlhf_forced.md). So a ONE-rank
+# group, which has nothing to overlap, keeps the normal-priority stream; groups of >= 2 ranks
+# take the high-priority one for the overlap.
 RCCL_HIGH_PRIORITY = os.environ.get("DLA_RCCL_HIGH_PRIORITY", "1") != "0"
 
 
-def comm_pg_options():
+def comm_pg_options(group_size: int = 2):
     """ProcessGroupNCCL options for every RCCL group this framework creates (world + sub-groups)."""
-    if not RCCL_HIGH_PRIORITY or not hasattr(dist, "ProcessGroupNCCL"):
+    if not RCCL_HIGH_PRIORITY or group_size < 2 or not hasattr(dist, "ProcessGroupNCCL"):
         return None
     opts = dist.ProcessGroupNCCL.Options()
     opts.is_high_priority_stream = True
@@ -112,7 +118,7 @@ def comm_pg_options():
 def new_group(ranks, **kw):
     """dist.new_group with the framework's RCCL options (high-priority comm streams)."""
     if _STATE.backend == "nccl" and "pg_options" not in kw:
-        opts = comm_pg_options()
+        opts = comm_pg_options(len(ranks))
         if opts is not None:
             kw["pg_options"] = opts
     return dist.new_group(ranks, **kw)

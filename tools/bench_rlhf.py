@@ -101,7 +101,9 @@ def main() -> int:
     if a.grad_ckpt:
         pol.gradient_checkpointing_enable(a.grad_ckpt)
     eng = DataParallelEngine(pol, lr=1e-6, betas=(0.9, 0.95), weight_decay=0.01, max_grad_norm=1.0,
-                             force_comm=a.force_pg)
+                             # (DLA_BENCH_ENGINE_PLAIN=1: the process group exists, the engine
+                             # runs the one-rank path; isolates the group from the engine path)
+                             force_comm=a.force_pg and os.environ.get("DLA_BENCH_ENGINE_PLAIN") != "1")
     g = torch.Generator(device=dev).manual_seed(0)
     from distributed_llm_alignment_amd.models.tokenizer import ByteTokenizer
     from distributed_llm_alignment_amd.training.handoff import RewardHandoff
@@ -115,6 +117,8 @@ def main() -> int:
     def sync():
         torch.cuda.synchronize()
         return time.perf_counter()
+
+    exposed = []  # the update's gradient-collective wait nothing overlapped, ms per step
 
     def step(record):
         ids = torch.randint(3, cfg.vocab_size, (a.batch, a.prompt), device=dev, generator=g)
@@ -139,6 +143,7 @@ def main() -> int:
             phases["generate"] += t1 - t0
             phases["score"] += t2 - t1
             phases["train"] += t3 - t2
+            exposed.append(eng.comm_timer.last_step_ms())
 
     if a.overlap:
         import threading
@@ -226,7 +231,8 @@ def main() -> int:
                       "peak_gib": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1),
                       "prompt": a.prompt, "new_tokens": a.new, "s_per_step": round(dt / a.steps, 3),
                       "rollouts_per_s": round(a.batch * a.steps / dt, 3),
-                      **{f"{k}_s": round(v / a.steps, 3) for k, v in phases.items()}}), flush=True)
+                      **{f"{k}_s": round(v / a.steps, 3) for k, v in phases.items()},
+                      "comm_exposed_ms": round(sum(exposed) / len(exposed), 2) if exposed else None}), flush=True)
     return 0
 
 
@@ -290,6 +296,8 @@ def ppo_main(a) -> int:
         torch.cuda.synchronize()
         peaks[name] = max(peaks.get(name, 0.0), round(torch.cuda.max_memory_allocated(dev) / gib, 2))
         torch.cuda.reset_peak_memory_stats(dev)
+
+    exposed = []  # the update's gradient-collective wait nothing overlapped, ms per step
 
     def step(record):
         ids = torch.randint(3, cfg.vocab_size, (a.batch, a.prompt), device=dev, generator=g)

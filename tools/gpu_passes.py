@@ -158,6 +158,19 @@ PASSES = {
                         [("window", ["--window", "adamw", "--by-grid", "--top", "40"])], 500),
                    prof("ep8_bal", MIX_EP8 + " --steps 2 --warmup 1",
                         [("window", ["--window", "adamw", "--by-grid", "--top", "40"])], 500)],
+    # RLHF forced vs plain after the one-rank groups went back to the normal-priority RCCL stream
+    "r6-rlhf3": [run("rlhf_plain0", "python -u tools/bench_rlhf.py --batch 8", 400),
+                 run("rlhf_forced0", "python -u tools/bench_rlhf.py --batch 8 --force-pg", 400),
+                 run("rlhf_plain1", "python -u tools/bench_rlhf.py --batch 8", 400),
+                 run("rlhf_forced1", "python -u tools/bench_rlhf.py --batch 8 --force-pg", 400),
+                 run("dpo_force_pg", DPO + " --force-pg --steps 5 --warmup 2", 300),
+                 run("dpo_plain", DPO + " --steps 5 --warmup 2", 300)],
+    # which part of the forced one-rank RCCL path slows the RLHF update (no comm kernels run)
+    "r6-forced-probe": [ab("rlhf_forced_env", "python -u tools/bench_rlhf.py --batch 8 --force-pg",
+                           {"base": {}, "lowprio": {"DLA_RCCL_HIGH_PRIORITY": "0"},
+                            "no_ag_overlap": {"DLA_OVERLAP_AG": "0"},
+                            "no_async_err": {"TORCH_NCCL_ASYNC_ERROR_HANDLING": "0"},
+                            "pg_only": {"DLA_BENCH_ENGINE_PLAIN": "1"}}, 1, 400)],
     # the whole DPO step's launches in issue order (which GEMM runs where, at what cost in place)
     # and the GEMM probe's arms under a kernel trace (which library kernel each form picks)
     "r6-seq": [prof("dpo_seq", DPO + " --steps 2 --warmup 1", [("window", ["--window", "adamw", "--seq", "0:7000"])]),
