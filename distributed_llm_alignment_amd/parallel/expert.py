@@ -121,6 +121,16 @@ _NATIVE_ROUTE = os.environ.get("DLA_EP_NATIVE_ROUTE", "1") != "0"
 # combine kernel with unit weights) instead of an fp32 index_add + bf16 cast (Mixtral EP shape:
 # 41 + 11 ms/step); DLA_EP_GATHER_BWD_COMBINE=0 keeps the index_add for A/B.
 GATHER_BWD_COMBINE = os.environ.get("DLA_EP_GATHER_BWD_COMBINE", "1") != "0"
+# Load-adaptive library rows for a single local expert: the hipBLASLt GEMMs cover the expected
+# n * k rows of the capacity buffer, the rows past them run on the grouped kernels (ops.moe
+# MOE_MAIN_ROWS). Under imbalanced routing those overflow launches are small-M grids (<= 160
+# workgroups for 256 CUs over K = 14336 / 28672) at ~400 TF/s, so the rank of a hot expert paid
+# 3x the library's cost for its extra rows (profiles/r6_mixtral.md). Each (layer, chunk) keeps
+# the row count its expert actually received in a pinned host word, copied asynchronously after
+# the routing (no sync); the next call widens the library's share to that count. The split point
+# is only a performance hint -- every split gives the same rows -- so a value one call stale is
+# harmless. DLA_EP_ADAPTIVE_MAIN=0: the static expected-rows split.
+ADAPTIVE_MAIN = os.environ.get("DLA_EP_ADAPTIVE_MAIN", "1") != "0"
 
 
 def _native_route(topi: torch.Tensor, E: int, ep: int, slots: int) -> bool:
@@ -194,6 +204,7 @@ class ExpertParallel:
         if self.shape_hot and self.El != 1:
             raise ValueError("shape_hot needs one local expert per rank (--ep-shape = num_experts)")
         self._dropped = None  # device int64 counter of dropped token slots (capacity mode)
+        self._seen_rows: dict = {}  # (id(moe), chunk) -> pinned int32 [1]: rows received last call
 
     def dropped_slots(self, reset: bool = True) -> int:
         """Token slots dropped by the capacity limit since the last call (one host read)."""
@@ -304,15 +315,18 @@ class ExpertParallel:
             stage.append((C, pos, w, rc, xr, (b - a) * k))
         # 2) per chunk: wait for its rows, experts on the device-built order, return all-to-all
         back = []
-        for C, pos, w, rc, xr, nk in stage:
+        for ci, (C, pos, w, rc, xr, nk) in enumerate(stage):
             if w is not None:
                 w.wait()
             xr = _A2AWait.apply(xr, holder)
             xe_src, inv, offs = self._expert_order(rc, C)
             xe = _gather_rows(xr, xe_src)
             # a single local expert's expected rows under balanced routing: the chunk's n * k slots
-            # (its buffer holds cf * n * k), as a multiple of the 256-row GEMM tile
+            # (its buffer holds cf * n * k), as a multiple of the 256-row GEMM tile; widened to
+            # the rows this (layer, chunk) received last time (ADAPTIVE_MAIN)
             main = min(xe.shape[0], (nk + 255) // 256 * 256) if self.El == 1 else 0
+            if main and ADAPTIVE_MAIN and xe.is_cuda:
+                main = self._adaptive_main(moe, ci, main, xe.shape[0], offs)
             ye = ops.moe.experts_swiglu_offsets(xe, moe.expert_up, moe.expert_down, offs, fp8=moe.fp8,
                                                 main_rows=main)
             yr = _gather_rows(ye, inv)
@@ -326,6 +340,21 @@ class ExpertParallel:
                 ys = torch.cat([ys, ys.new_zeros(1, H)], 0)
             outs.append(ops.moe.combine(ys, pos.to(torch.int32), topvc[ci]))
         return outs[0] if len(outs) == 1 else torch.cat(outs, 0)
+
+    def _adaptive_main(self, moe, ci: int, main: int, rows: int, offs: torch.Tensor) -> int:
+        """Library rows for this call from the count the same (layer, chunk) received last call;
+        queues the copy of this call's count for the next one (never under graph capture)."""
+        key = (id(moe), ci)
+        seen = self._seen_rows.get(key)
+        if seen is not None:
+            got = int(seen[0])  # host read of a pinned word: no device sync
+            main = min(rows, max(main, (got + 255) // 256 * 256))
+        if not torch.cuda.is_current_stream_capturing():
+            if seen is None:
+                seen = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+                self._seen_rows[key] = seen
+            seen.copy_(offs[-1:], non_blocking=True)
+        return main
 
     # ------------------------------------------------------------------ exact (host splits)
     def _exact(self, moe, h2: torch.Tensor, topv: torch.Tensor, topi: torch.Tensor):

@@ -466,3 +466,42 @@ def test_single_expert_main_overflow_split_matches_whole_buffer(main):
         assert rel(a, b) < 1e-2
     assert float(res[main][0][valid:].abs().max()) == 0.0
     assert float(res[main][1][valid:].abs().max()) == 0.0
+
+
+def test_expert_parallel_adaptive_main_rows(monkeypatch):
+    """parallel.expert ADAPTIVE_MAIN: the rank of a hot expert (EP shape mode, every source at
+    capacity) starts with the library GEMMs on the expected n * k rows and, from the next call of
+    the same layer on, on every row its expert received (the count copied to a pinned host word
+    without a sync); outputs equal the static split's."""
+    from distributed_llm_alignment_amd import ops
+    from distributed_llm_alignment_amd.models import build_model, get_config
+    from distributed_llm_alignment_amd.parallel import expert as epmod
+
+    cfg = get_config("tiny-mixtral", hidden_size=256, intermediate_size=512, num_experts=8)
+    E = cfg.num_experts
+    seen = []
+    real = ops.moe.experts_swiglu_offsets
+
+    def spy(xe, w_up, w_down, offs, **kw):
+        seen.append((xe.shape[0], kw.get("main_rows", 0)))
+        return real(xe, w_up, w_down, offs, **kw)
+
+    monkeypatch.setattr(ops.moe, "experts_swiglu_offsets", spy)
+    h = torch.randn(2, 512, cfg.hidden_size, device=DEV).to(torch.bfloat16)
+    outs = {}
+    for adaptive in (False, True):
+        monkeypatch.setattr(epmod, "ADAPTIVE_MAIN", adaptive)
+        m = build_model(cfg, device=DEV, dtype=torch.bfloat16, seed=0)
+        epmod.apply_expert_parallel(m, None, capacity_factor=1.5, shape_ep=E, shape_hot=True)
+        seen.clear()
+        with torch.no_grad():
+            y0 = m.layers[0].mlp(h)
+            torch.cuda.synchronize()
+            y1 = m.layers[0].mlp(h)
+        (r0, m0), (r1, m1) = seen[0], seen[-1]
+        assert m0 < r0
+        assert (m1 == r1) if adaptive else (m1 == m0)
+        outs[adaptive] = (y0.float(), y1.float())
+    rel = lambda a, b: float((a - b).norm() / b.norm().clamp_min(1e-12))
+    assert rel(outs[True][0], outs[False][0]) == 0.0
+    assert rel(outs[True][1], outs[False][1]) < 1e-2

@@ -158,6 +158,27 @@ PASSES = {
                         [("window", ["--window", "adamw", "--by-grid", "--top", "40"])], 500),
                    prof("ep8_bal", MIX_EP8 + " --steps 2 --warmup 1",
                         [("window", ["--window", "adamw", "--by-grid", "--top", "40"])], 500)],
+    # B = 8 decode attention at the RLHF shape (prompt 512 + 256 new: 6 key chunks): one-chunk
+    # kernel + combine launch vs the loop kernel with the in-kernel combine (2 or 1 chunks/block)
+    "r6-decode-combine": [ab("dec_rlhf_shape", "python -u tools/bench_generate.py --modes graph --prompt 512 --new 256",
+                             {"base": {}, "loop2": {"DLA_DECODE_LOOP_MIN": "1"},
+                              "loop1": {"DLA_DECODE_LOOP_MIN": "1", "DLA_DECODE_BLOCKS": "384"}}, 2, 300)],
+    # the hot-expert rank at capacity 1.125, library rows adaptive vs static, under a kernel trace
+    "r6-mixtral-cf": [prof("hot_cf1125_adaptive", DPO + " --model mixtral-8x7b --ep-shape 8 --micro-pairs 2 --accum 8"
+                           " --ep-capacity 1.125 --ep-hot --steps 2 --warmup 1",
+                           [("window", ["--window", "adamw", "--by-grid", "--top", "40"])], 500),
+                      prof("hot_cf1125_static", DPO + " --model mixtral-8x7b --ep-shape 8 --micro-pairs 2 --accum 8"
+                           " --ep-capacity 1.125 --ep-hot --steps 2 --warmup 1",
+                           [("window", ["--window", "adamw", "--by-grid", "--top", "40"])], 500,
+                           {"DLA_EP_ADAPTIVE_MAIN": "0"})],
+    # load-adaptive library rows for the single local expert (parallel.expert ADAPTIVE_MAIN)
+    "r6-mixtral2": [pytest("tests/test_moe_gpu.py", 400),
+                    run("ep8_hot", MIX_EP8 + " --ep-hot --steps 3 --warmup 2", 500),
+                    run("ep8_bal", MIX_EP8 + " --steps 3 --warmup 2", 500),
+                    run("ep8_hot_cf1125", DPO + " --model mixtral-8x7b --ep-shape 8 --micro-pairs 2 --accum 8"
+                        " --ep-capacity 1.125 --ep-hot --steps 3 --warmup 2", 500),
+                    run("ep8_hot_fp8", MIX_EP8 + " --ep-hot --fp8 --steps 3 --warmup 2", 500),
+                    run("ep8_bal_fp8", MIX_EP8 + " --fp8 --steps 3 --warmup 2", 500)],
     # RLHF forced vs plain after the one-rank groups went back to the normal-priority RCCL stream
     "r6-rlhf3": [run("rlhf_plain0", "python -u tools/bench_rlhf.py --batch 8", 400),
                  run("rlhf_forced0", "python -u tools/bench_rlhf.py --batch 8 --force-pg", 400),
