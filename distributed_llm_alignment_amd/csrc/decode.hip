@@ -919,11 +919,15 @@ static int decode_cpb(int Tmax, int B, int Hkv) {
   if (target <= 0) return 0;
   const int64_t blocks = static_cast<int64_t>(B) * Hkv * nch;
   const int cpb = static_cast<int>((blocks + target - 1) / target);
-  // below DLA_DECODE_LOOP_MIN (default 3) chunks per block the one-chunk kernel (3 blocks per CU)
-  // measured faster (B = 8, 1152 keys: 4.05 vs 4.12 ms/token)
+  // Below DLA_DECODE_LOOP_MIN chunks per block the one-chunk kernel (3 blocks per CU) + the combine
+  // launch. Round 3 measured that faster under 3 chunks (B = 8, 1152 keys: 4.05 vs 4.12 ms/token);
+  // with the in-kernel combine the loop kernel now wins at 2 chunks and at 1 chunk whenever the
+  // splits fit the fused combine (B = 8, 512 + 256 tokens: 3.466-3.473 at 2, 3.485-3.497 at 1 vs
+  // 3.542-3.548 ms/token, same box, tools/gpu_passes.py r6-decode-combine)
   const char* mn = getenv("DLA_DECODE_LOOP_MIN");
-  const int min_cpb = mn ? atoi(mn) : 3;
-  return cpb < min_cpb ? 0 : std::min(cpb, nch);
+  const int min_cpb = mn ? atoi(mn) : 2;
+  if (cpb < min_cpb) return (mn == nullptr && cpb == 1 && nch <= kDecMaxFuse) ? 1 : 0;
+  return std::min(cpb, nch);
 }
 
 int decode_num_splits(int Tmax, int B, int Hkv) {

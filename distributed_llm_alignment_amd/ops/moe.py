@@ -379,6 +379,16 @@ def _single_lib(offs: torch.Tensor, w: torch.Tensor, rows: int) -> bool:
 MOE_MAIN_ROWS = os.environ.get("DLA_MOE_MAIN_ROWS", "1") != "0"
 
 
+def _row_pieces(main: int, base: int):
+    """Row ranges of the library GEMMs over [0, main): the expected rows [0, base) as one GEMM
+    (the tuned shape) and any load-adaptive extension [base, main) as a second one -- one GEMM over
+    an untuned row count (4608 at capacity 1.125) drew a hipBLASLt heuristic kernel 3x slower per
+    row than the tuned 4096-row one (profiles/r6_mixtral.md)."""
+    if 0 < base < main:
+        return [(0, base), (base, main)]
+    return [(0, main)]
+
+
 def _tail_offs(offs: torch.Tensor, main: int) -> torch.Tensor:
     """Offsets of the rows past `main` (single group): [0, max(offs[-1] - main, 0)], on device."""
     return torch.clamp(offs - main, min=0).to(torch.int32)
@@ -395,10 +405,12 @@ class _GroupedExpertsFn(torch.autograd.Function):
     `sync_free`: the backward also stays on the grouped kernels (never reads offs on the host)."""
 
     @staticmethod
-    def forward(ctx, xs, w_up, w_down, offs, fp8: bool, sync_free: bool = False, main_rows: int = 0):
+    def forward(ctx, xs, w_up, w_down, offs, fp8: bool, sync_free: bool = False, main_rows: int = 0,
+                base_rows: int = 0):
         C = _ext.require()
         rows = xs.shape[0]
         main = main_rows if (MOE_MAIN_ROWS and 0 < main_rows < rows) else rows
+        base = base_rows if MOE_MAIN_ROWS else 0
         if fp8:
             wu_q, wu_s = fp8_weight(w_up)
             wd_q, wd_s = fp8_weight(w_down)
@@ -408,10 +420,12 @@ class _GroupedExpertsFn(torch.autograd.Function):
             ys = C.gg_fwd(aq, wd_q, offs, asc, wd_s)
         else:
             gu, a = C.gg_fwd_swiglu(xs, w_up, offs, None, None)
-            if _single_lib(offs, w_down, a.shape[0]) and main < rows:
+            if _single_lib(offs, w_down, a.shape[0]) and (main < rows or 0 < base < main):
                 ys = torch.empty((rows, w_down.shape[1]), dtype=a.dtype, device=a.device)
-                torch.matmul(a[:main], w_down.detach()[0].t(), out=ys[:main])
-                ys[main:].copy_(C.gg_fwd(a[main:], w_down, _tail_offs(offs, main), None, None))
+                for lo, hi in _row_pieces(main, base):
+                    torch.matmul(a[lo:hi], w_down.detach()[0].t(), out=ys[lo:hi])
+                if main < rows:
+                    ys[main:].copy_(C.gg_fwd(a[main:], w_down, _tail_offs(offs, main), None, None))
             elif _single_lib(offs, w_down, a.shape[0]):
                 ys = F.linear(a, w_down.detach()[0])
             else:
@@ -423,7 +437,7 @@ class _GroupedExpertsFn(torch.autograd.Function):
         ctx.save_for_backward(xs, gu, offs)
         ctx.w_up, ctx.w_down = w_up, w_down  # (on ctx: see ops.linear._LinearMainGradFn)
         ctx.sync_free = sync_free
-        ctx.main = main
+        ctx.main, ctx.base = main, base
         return ys
 
     @staticmethod
@@ -477,12 +491,15 @@ class _GroupedExpertsFn(torch.autograd.Function):
                 outs.append(None)
         dxs = None
         if ctx.needs_input_grad[0]:
-            if _single_lib(offs, w_up, dgu.shape[0]) and offs_t is not None:
+            if _single_lib(offs, w_up, dgu.shape[0]) and (offs_t is not None or 0 < ctx.base < main):
                 dxs = torch.empty((rows, w_up.shape[2]), dtype=dgu.dtype, device=dgu.device)
-                torch.matmul(dgu[:main], _expert0_t(w_up).t(), out=dxs[:main])  # as F.linear below
-                tail = C.gg_dgrad(dgu[main:], w_up, offs_t)
-                C.zero_rows_from(tail, offs_t[-1:])  # overflow rows the grouped kernel left unwritten
-                dxs[main:].copy_(tail)
+                wt = _expert0_t(w_up)
+                for lo, hi in _row_pieces(main, ctx.base):
+                    torch.matmul(dgu[lo:hi], wt.t(), out=dxs[lo:hi])  # as F.linear below
+                if offs_t is not None:
+                    tail = C.gg_dgrad(dgu[main:], w_up, offs_t)
+                    C.zero_rows_from(tail, offs_t[-1:])  # overflow rows the grouped kernel left unwritten
+                    dxs[main:].copy_(tail)
             elif _single_lib(offs, w_up, dgu.shape[0]):
                 dxs = F.linear(dgu, _expert0_t(w_up))  # dgu [M, 2F] . W_up[0] [2F, H], TN layout
             else:
@@ -494,7 +511,7 @@ class _GroupedExpertsFn(torch.autograd.Function):
             # rows past offs[-1] (padding of a capacity buffer) are never written by the grouped
             # kernel (single: dgu's padding rows are zero, so dxs's are too)
             C.zero_rows_from(dxs, offs[-1:])
-        return dxs, outs[0], outs[1], None, None, None, None
+        return dxs, outs[0], outs[1], None, None, None, None, None
 
 
 def grouped_gemm_enabled() -> bool:
@@ -565,17 +582,20 @@ def _ref_grouped_experts(xs, w_up, w_down, offs):
 
 
 def experts_swiglu_offsets(xs: torch.Tensor, w_up: torch.Tensor, w_down: torch.Tensor,
-                           offs: torch.Tensor, fp8: bool = False, main_rows: int = 0) -> torch.Tensor:
+                           offs: torch.Tensor, fp8: bool = False, main_rows: int = 0,
+                           base_rows: int = 0) -> torch.Tensor:
     """Grouped experts over rows whose per-expert ranges are given ONLY as a device offsets array
     offs [E+1] (rows past offs[-1] are padding: ignored, zero output and gradient). Never reads
     the offsets on the host, forward or backward: the sync-free expert-parallel path.
-    `main_rows`: the expected fill of a single local expert's buffer (see MOE_MAIN_ROWS)."""
+    `main_rows`: the library rows of a single local expert's buffer (see MOE_MAIN_ROWS); `base_rows`
+    (<= main_rows) its expected fill, run as a GEMM of its own when main_rows extends past it."""
     xs = xs.contiguous()
     if _grouped_ok(xs, w_up, w_down):
         if fp8 and _FP8 is None:
             fp8 = False
         # rows past offs[-1] come back zero (zeroed in place inside the node)
-        ys = _GroupedExpertsFn.apply(xs, w_up, w_down, offs.to(torch.int32), bool(fp8), True, int(main_rows))
+        ys = _GroupedExpertsFn.apply(xs, w_up, w_down, offs.to(torch.int32), bool(fp8), True, int(main_rows),
+                                     int(base_rows))
         if not _TAIL_INPLACE:
             tail = torch.arange(ys.shape[0], device=ys.device) >= offs[-1].long()
             ys = ys.masked_fill(tail.unsqueeze(-1), 0)

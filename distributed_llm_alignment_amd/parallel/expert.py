@@ -324,11 +324,11 @@ class ExpertParallel:
             # a single local expert's expected rows under balanced routing: the chunk's n * k slots
             # (its buffer holds cf * n * k), as a multiple of the 256-row GEMM tile; widened to
             # the rows this (layer, chunk) received last time (ADAPTIVE_MAIN)
-            main = min(xe.shape[0], (nk + 255) // 256 * 256) if self.El == 1 else 0
+            base = main = min(xe.shape[0], (nk + 255) // 256 * 256) if self.El == 1 else 0
             if main and ADAPTIVE_MAIN and xe.is_cuda:
                 main = self._adaptive_main(moe, ci, main, xe.shape[0], offs)
             ye = ops.moe.experts_swiglu_offsets(xe, moe.expert_up, moe.expert_down, offs, fp8=moe.fp8,
-                                                main_rows=main)
+                                                main_rows=main, base_rows=base)
             yr = _gather_rows(ye, inv)
             back.append((pos, _A2AStart.apply(yr, self.group, holder)))
         # 3) combine each chunk (dropped slots point one past the buffer: the native combine reads

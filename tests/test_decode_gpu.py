@@ -16,14 +16,17 @@ def _native():
     _ext.require()
 
 
-@pytest.mark.parametrize("blocks", [None, "16", "60"])
+@pytest.mark.parametrize("blocks", [None, "16", "60", "one-chunk"])
 @pytest.mark.parametrize("D,Hq,Hkv,window", [(128, 32, 8, 0), (64, 8, 8, 0), (128, 16, 2, 300), (64, 16, 8, 0)])
 def test_decode_attention_matches_reference(D, Hq, Hkv, window, blocks, monkeypatch):
-    """blocks: DLA_DECODE_BLOCKS target -- None keeps the default (one 128-key chunk per block
-    at this size), 16 / 60 force the multi-chunk loop kernel with 1 / 2 splits per sequence."""
+    """blocks: DLA_DECODE_BLOCKS target -- None keeps the default (the loop kernel, 2 chunks per
+    block at this size), 16 / 60 force 1 / 2 splits per sequence, "one-chunk" the one-chunk kernel
+    + combine launch (DLA_DECODE_LOOP=0)."""
     from distributed_llm_alignment_amd.ops import decode
 
-    if blocks is not None:
+    if blocks == "one-chunk":
+        monkeypatch.setenv("DLA_DECODE_LOOP", "0")
+    elif blocks is not None:
         monkeypatch.setenv("DLA_DECODE_BLOCKS", blocks)
 
     g = torch.Generator(device=DEV).manual_seed(0)
@@ -345,14 +348,16 @@ def test_skinny_glu_epilogue_matches_unfused(M, F, K, mode):
 
 
 @pytest.mark.parametrize("D,Hq,Hkv,rot", [(128, 32, 8, 128), (64, 8, 8, 32), (128, 8, 1, 64)])
-@pytest.mark.parametrize("blocks", [None, "4"])
+@pytest.mark.parametrize("blocks", [None, "4", "one-chunk"])
 def test_fused_rope_decode_attention_matches_unfused(D, Hq, Hkv, rot, blocks, monkeypatch):
     """decode_attn_rope (rope + cache write of the newest token inside the attention launch) ==
     rope_cache_write + decode_attn, bitwise: output and the written cache row (blocks = 4: both
     on the multi-chunk loop kernel, the newest key's V patched into the DMA'd LDS image)."""
     from distributed_llm_alignment_amd.ops import RotaryCache, _ext
 
-    if blocks is not None:
+    if blocks == "one-chunk":
+        monkeypatch.setenv("DLA_DECODE_LOOP", "0")
+    elif blocks is not None:
         monkeypatch.setenv("DLA_DECODE_BLOCKS", blocks)
 
     C = _ext.require()

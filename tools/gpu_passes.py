@@ -171,6 +171,17 @@ PASSES = {
                            " --ep-capacity 1.125 --ep-hot --steps 2 --warmup 1",
                            [("window", ["--window", "adamw", "--by-grid", "--top", "40"])], 500,
                            {"DLA_EP_ADAPTIVE_MAIN": "0"})],
+    # round-6 decode default (fused-combine loop kernel at 1-2 chunks per block) and the adaptive
+    # expert rows as tuned base + extension GEMMs
+    "r6-check": [pytest("tests/test_decode_gpu.py tests/test_moe_gpu.py", 600),
+                 run("gen_rlhf_shape", "python -u tools/bench_generate.py --modes graph --prompt 512 --new 256", 300),
+                 run("rlhf8", "python -u tools/bench_rlhf.py --batch 8", 400),
+                 run("ep8_hot", MIX_EP8 + " --ep-hot --steps 3 --warmup 2", 500),
+                 run("ep8_bal", MIX_EP8 + " --steps 3 --warmup 2", 500),
+                 run("ep8_hot_cf1125", DPO + " --model mixtral-8x7b --ep-shape 8 --micro-pairs 2 --accum 8"
+                     " --ep-capacity 1.125 --ep-hot --steps 3 --warmup 2", 500),
+                 run("ep8_bal_cf1125", DPO + " --model mixtral-8x7b --ep-shape 8 --micro-pairs 2 --accum 8"
+                     " --ep-capacity 1.125 --steps 3 --warmup 2", 500)],
     # load-adaptive library rows for the single local expert (parallel.expert ADAPTIVE_MAIN)
     "r6-mixtral2": [pytest("tests/test_moe_gpu.py", 400),
                     run("ep8_hot", MIX_EP8 + " --ep-hot --steps 3 --warmup 2", 500),
