@@ -555,6 +555,8 @@ def main(argv=None) -> int:
         }
         print(json.dumps(rec), flush=True)
     if st.initialized:  # orderly teardown: no communicator threads left running at exit
+        if hasattr(engine, "wait_params"):
+            engine.wait_params()  # the last step's overlapped all-gathers (never waited otherwise)
         barrier()
         from distributed_llm_alignment_amd.parallel.dist import destroy
 

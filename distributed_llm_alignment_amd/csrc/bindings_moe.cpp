@@ -510,7 +510,15 @@ std::tuple<at::Tensor, at::Tensor> moe_combine_bwd(const at::Tensor& dout, const
 
 }  // namespace dla
 
+namespace dla {
+int gg_set_sched(int sched);
+// the grouped GEMM's K-step schedule for the rest of the process (-1: the default); returns the
+// previous one
+int64_t gg_set_sched_op(int64_t sched) { return gg_set_sched(static_cast<int>(sched)); }
+}  // namespace dla
+
 TORCH_LIBRARY_FRAGMENT(dla, m) {
+  m.def("gg_set_sched(int sched) -> int", &dla::gg_set_sched_op);
   m.def("moe_topk_fwd(Tensor logits, int k) -> (Tensor, Tensor)");
   m.def("quant_fp8_rows(Tensor x) -> (Tensor, Tensor)");
   m.def("embed_fwd(Tensor w, Tensor ids, Tensor(a!) bad) -> Tensor");

@@ -767,10 +767,23 @@ __global__ __launch_bounds__(kGgThreads) void grouped_gemm_kernel(GGParams p) {
 // Default schedule (measured, tools/grouped_gemm_bench.py, profiles/r5_grouped_gemm.md): the
 // counted 4-phase step for every bf16 layout (fp8 keeps the plain 2-phase step). 0-3 stay
 // selectable for A/B.
-// DLA_GG_SCHED overrides (read per launch so a benchmark can A/B schedules in one process).
-static int gg_sched() {
-  const char* e = std::getenv("DLA_GG_SCHED");
-  return e ? std::atoi(e) : 4;
+// K-step schedule: DLA_GG_SCHED read once per process (default 4, the counted 4-phase step);
+// tests and tools/grouped_gemm_bench.py switch it in-process through gg_set_sched
+// (torch.ops.dla.gg_set_sched) instead of an environment read on every launch.
+static int& gg_sched_slot() {
+  static int v = [] {
+    const char* e = std::getenv("DLA_GG_SCHED");
+    return e ? std::atoi(e) : 4;
+  }();
+  return v;
+}
+static int gg_sched() { return gg_sched_slot(); }
+
+int gg_set_sched(int sched) {
+  int& s = gg_sched_slot();
+  const int prev = s;
+  s = sched < 0 ? 4 : sched;
+  return prev;
 }
 
 template <int MODE, bool BK, bool FP8, int EPI, bool OUTF32>

@@ -43,12 +43,12 @@ def _rand(*shape, g, scale=1.0):
 
 
 @pytest.fixture(params=["default", "0", "3", "4"])
-def gg_sched(request, monkeypatch):
+def gg_sched(request):
     """every K-step schedule: the per-layout default, the plain 2-phase step (0), the ping-pong
-    phases (3) and the counted 4-phase step (4)"""
-    if request.param != "default":
-        monkeypatch.setenv("DLA_GG_SCHED", request.param)
-    return request.param
+    phases (3) and the counted 4-phase step (4); switched in-process (torch.ops.dla.gg_set_sched)"""
+    prev = _C().gg_set_sched(-1 if request.param == "default" else int(request.param))
+    yield request.param
+    _C().gg_set_sched(prev)
 
 
 @pytest.mark.parametrize("N,K", [(384, 256), (264, 136)])
@@ -124,9 +124,13 @@ def test_grouped_counted_schedule_bitwise(monkeypatch, kind):
             _C().gg_wgrad(dy, x, offs, out, True)
             return (out,)
     outs = []
-    for sc in ("0", "4"):
-        monkeypatch.setenv("DLA_GG_SCHED", sc)
-        outs.append(run())
+    prev = _C().gg_set_sched(0)
+    try:
+        for sc in (0, 4):
+            _C().gg_set_sched(sc)
+            outs.append(run())
+    finally:
+        _C().gg_set_sched(prev)
     for a, b in zip(*outs):
         assert torch.equal(a, b)
 

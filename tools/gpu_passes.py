@@ -90,6 +90,23 @@ PASSES = {
         run("rlhf8_fp8", "python -u tools/bench_rlhf.py --batch 8 --rollout-dtype fp8", 400),
         run("ppo_zero8_fp8", "python -u tools/bench_rlhf.py --algorithm ppo --zero-shape 8 --batch 8 --rollout-dtype fp8"),
     ],
+    # the same, in two gpurun-sized halves (a call runs at most 20 minutes)
+    "validate-a": [
+        pytest("tests -m gpu"), SMOKE, run("bench", DPO), run("bench20", DPO + " --steps 20 --warmup 5", 400),
+        run("bench_force_pg", DPO + " --force-pg --steps 5 --warmup 2", 300),
+        run("gen8", GEN8, 300), run("gen64", GEN64, 300),
+        run("rlhf8", "python -u tools/bench_rlhf.py --batch 8", 400),
+        run("rlhf64_micro8", "python -u tools/bench_rlhf.py --batch 64 --micro 8"),
+    ],
+    "validate-b": [
+        run("ppo_zero8", "python -u tools/bench_rlhf.py --algorithm ppo --zero-shape 8 --batch 8"),
+        run("mixtral_ep8", MIX_EP8 + " --steps 3 --warmup 2"),
+        run("mixtral_ep8_fp8", MIX_EP8 + " --fp8 --steps 3 --warmup 2"),
+        run("mixtral_ep8_hot", MIX_EP8 + " --ep-hot --steps 3 --warmup 2"),
+        run("gen8_fp8", GEN8 + " --weight-dtype fp8", 300), run("gen64_fp8", GEN64 + " --weight-dtype fp8", 300),
+        run("rlhf8_fp8", "python -u tools/bench_rlhf.py --batch 8 --rollout-dtype fp8", 400),
+        run("ppo_zero8_fp8", "python -u tools/bench_rlhf.py --algorithm ppo --zero-shape 8 --batch 8 --rollout-dtype fp8"),
+    ],
     # ---- round 6
     # residual adds as the C input of the o / down GEMMs (norms read/write one tensor each)
     "r6-resid": [pytest("tests/test_kernels_gpu.py -k 'fused_residual or norm_fwd_bwd or fused_swiglu'", 300),
@@ -221,9 +238,6 @@ PASSES = {
     # B = 64 decode attention: key splits per sequence (DLA_DECODE_BLOCKS = target grid)
     "ab-b64-blocks": [ab("b64_blocks", GEN64, {"base": {}, "blk1024": {"DLA_DECODE_BLOCKS": "1024"},
                                                "blk2048": {"DLA_DECODE_BLOCKS": "2048"}}, 2, 300)],
-    # the validation table in two gpurun-sized halves (a call runs at most 20 minutes)
-    "validate-a": [],
-    "validate-b": [],
     "force-pg": [
         pytest("tests/test_force_comm.py -m gpu", 400),
         prof("force_pg", DPO + " --force-pg --steps 2 --warmup 1",
@@ -397,8 +411,6 @@ class Runner:
             raise ValueError(k)
 
 
-PASSES["validate-a"] = PASSES["validate"][:4]
-PASSES["validate-b"] = PASSES["validate"][4:]
 
 
 def main(argv=None):

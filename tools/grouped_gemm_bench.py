@@ -95,13 +95,13 @@ def main(argv=None):
     for _ in range(a.rounds):
         for name, fn, fl in cases:
             for sc in scheds:
-                os.environ["DLA_GG_SCHED"] = str(sc)
+                torch.ops.dla.gg_set_sched(sc)
                 ms = _time(fn, a.iters)
                 best[(name, sc)] = min(ms, best.get((name, sc), 1e9))
     for name, fn, fl in cases:
         for sc in scheds:
             rep(f"grouped {name} sched{sc}", best[(name, sc)], fl)
-    os.environ.pop("DLA_GG_SCHED", None)  # per-layout defaults for the block timings
+    torch.ops.dla.gg_set_sched(-1)  # per-layout defaults for the block timings
     cl = counts.tolist()
     # hipBLASLt per-expert reference for the same projections
     def loop_up():
