@@ -199,6 +199,10 @@ PASSES = {
                      " --ep-capacity 1.125 --ep-hot --steps 3 --warmup 2", 500),
                  run("ep8_bal_cf1125", DPO + " --model mixtral-8x7b --ep-shape 8 --micro-pairs 2 --accum 8"
                      " --ep-capacity 1.125 --steps 3 --warmup 2", 500)],
+    # the new decode default at the GEN8 shape (prompt 1024 + 128) vs the round-5 rule (min 3)
+    "r6-gen8-ab": [ab("gen8_loopmin", GEN8, {"new": {}, "min3": {"DLA_DECODE_LOOP_MIN": "3"}}, 2, 300),
+                   ab("gen_rlhf_loopmin", "python -u tools/bench_generate.py --modes graph --prompt 512 --new 256",
+                      {"new": {}, "min3": {"DLA_DECODE_LOOP_MIN": "3"}}, 1, 300)],
     # load-adaptive library rows for the single local expert (parallel.expert ADAPTIVE_MAIN)
     "r6-mixtral2": [pytest("tests/test_moe_gpu.py", 400),
                     run("ep8_hot", MIX_EP8 + " --ep-hot --steps 3 --warmup 2", 500),
