@@ -91,13 +91,13 @@ __device__ __forceinline__ s16x4 dec_tr_read(const bf16_t* img, int r0, int c0, 
 // The previous version (one block-wide softmax: 6 barriers, the V loads behind the scores):
 // 17.3 -> 16.4 us per layer in a Llama-3-8B B=8 decode step. Neither the grid order (kv head
 // fastest) nor a head-major cache layout changed the time (tools/decode_attn_bench.py).
-// PVM (P.V on MFMA): the exponentiated scores stay in the S^T accumulator layout (lane = head g,
+// P.V on MFMA: the exponentiated scores stay in the S^T accumulator layout (lane = head g,
 // keys {4kg .. 4kg+3, 16+4kg .. 16+4kg+3}), which IS the A operand of v_mfma_f32_16x16x32_bf16
 // once packed to bf16 (k permuted the same way on both operands); V goes through a wave-private
 // swizzled LDS image and comes back as the B operand by ds_read_b64_tr_b16 (cdna guide T10). The
-// VALU form (PVM = false: P through LDS, 8 x G FMAs per key and lane, a 2-step shuffle reduction
-// of G x 8 partial sums) is kept for the A/B.
-template <int D, int G, bool ROPE, bool PVM = false>
+// (The VALU P.V form it replaced -- P through LDS, 8 x G FMAs per key and lane -- was deleted in
+// round 6; git history has it.)
+template <int D, int G, bool ROPE>
 __global__ __launch_bounds__(256, 3) void decode_attn_kernel(
     const bf16_t* __restrict__ q, int64_t q_sb, int64_t q_sh,     // q [B, Hq, D]
     bf16_t* __restrict__ kc, bf16_t* __restrict__ vc,              // [B, Tmax, Hkv, D]
@@ -109,8 +109,7 @@ __global__ __launch_bounds__(256, 3) void decode_attn_kernel(
   constexpr int LPK = D / 8, KPI = 64 / LPK, KPW = kDecChunk / 4, NIT = KPW / KPI;
   constexpr int KST = D / 32;  // MFMA k-steps over the head dim
   static_assert(G <= 16 && KPW == 32, "decode tile geometry");
-  __shared__ float pex[PVM ? 1 : 4][KPW][G];
-  __shared__ __attribute__((aligned(16))) bf16_t vimg[PVM ? 4 : 1][PVM ? KPW * D : 8];
+  __shared__ __attribute__((aligned(16))) bf16_t vimg[4][KPW * D];
   __shared__ float acc_s[4][G][D];
   __shared__ float mls[4][G][2];
   const int split = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
@@ -217,86 +216,42 @@ __global__ __launch_bounds__(256, 3) void decode_attn_kernel(
   m = fmaxf(m, __shfl_xor(m, 32, 64));
   const float muse = m == -INFINITY ? 0.f : m;
   float l = 0.f;
-  if constexpr (PVM) {
-    // V rows -> this wave's LDS image (row = key within the wave, swizzled 16-byte chunks)
-    bf16_t* vw = &vimg[wv][0];
+  // V rows -> this wave's LDS image (row = key within the wave, swizzled 16-byte chunks)
+  bf16_t* vw = &vimg[wv][0];
 #pragma unroll
-    for (int it = 0; it < NIT; ++it)
-      store_bf16x8(vw + dec_swz<D>(it * KPI + sub, dl >> 3), vvr[it]);
-    float pf[2][4];
+  for (int it = 0; it < NIT; ++it)
+    store_bf16x8(vw + dec_swz<D>(it * KPI + sub, dl >> 3), vvr[it]);
+  float pf[2][4];
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+  for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float p = __builtin_amdgcn_exp2f(sc[t][i] - muse);  // exp2(-inf) = 0 for masked keys
-        l += p;
-        pf[t][i] = r16 < G ? p : 0.f;
-      }
-    l += __shfl_xor(l, 16, 64);
-    l += __shfl_xor(l, 32, 64);
-    // A operand: k-slot e < 4 <-> key 4kg + e, e >= 4 <-> key 16 + 4kg + e - 4
-    const float pv8[8] = {pf[0][0], pf[0][1], pf[0][2], pf[0][3], pf[1][0], pf[1][1], pf[1][2], pf[1][3]};
-    const s16x8 pa = __builtin_bit_cast(s16x8, pack_bf16x8(pv8));
-    // wave-private image: this wave's LDS writes complete before its transposed reads
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-    f32x4 oacc[D / 16];
-#pragma unroll
-    for (int dt = 0; dt < D / 16; ++dt) {
-      const s16x4 v0 = dec_tr_read<D>(vw, 4 * kg, 16 * dt, lane);
-      const s16x4 v1 = dec_tr_read<D>(vw, 16 + 4 * kg, 16 * dt, lane);
-      const s16x8 vb = s16x8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-      oacc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vb, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    for (int i = 0; i < 4; ++i) {
+      const float p = __builtin_amdgcn_exp2f(sc[t][i] - muse);  // exp2(-inf) = 0 for masked keys
+      l += p;
+      pf[t][i] = r16 < G ? p : 0.f;
     }
-    // lane (d = 16 dt + r16, heads 4kg + i) -> this wave's partial O
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  // A operand: k-slot e < 4 <-> key 4kg + e, e >= 4 <-> key 16 + 4kg + e - 4
+  const float pv8[8] = {pf[0][0], pf[0][1], pf[0][2], pf[0][3], pf[1][0], pf[1][1], pf[1][2], pf[1][3]};
+  const s16x8 pa = __builtin_bit_cast(s16x8, pack_bf16x8(pv8));
+  // wave-private image: this wave's LDS writes complete before its transposed reads
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  f32x4 oacc[D / 16];
 #pragma unroll
-    for (int dt = 0; dt < D / 16; ++dt)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (4 * kg + i < G) acc_s[wv][4 * kg + i][16 * dt + r16] = oacc[dt][i];
-  } else {
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float p = __builtin_amdgcn_exp2f(sc[t][i] - muse);  // exp2(-inf) = 0 for masked keys
-        l += p;
-        if (r16 < G) pex[wv][16 * t + 4 * kg + i][r16] = p;
-      }
-    l += __shfl_xor(l, 16, 64);
-    l += __shfl_xor(l, 32, 64);
-    // wave-private exchange: this wave's LDS writes complete before its reads (in-order LDS queue)
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-    // ---- P.V in the row layout: lane (sub, dl) owns keys it * KPI + sub of the wave's 32
-    float o[G][8];
-#pragma unroll
-    for (int g = 0; g < G; ++g)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) o[g][j] = 0.f;
-#pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      const int kl = it * KPI + sub;
-#pragma unroll
-      for (int g = 0; g < G; ++g) {
-        const float p = pex[wv][kl][g];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) o[g][j] += p * bf2f(vvr[it][j]);
-      }
-    }
-#pragma unroll
-    for (int g = 0; g < G; ++g)
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-#pragma unroll
-        for (int off = LPK; off < 64; off <<= 1) o[g][j] += __shfl_xor(o[g][j], off, 64);
-    if (sub == 0) {
-#pragma unroll
-      for (int g = 0; g < G; ++g)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc_s[wv][g][dl + j] = o[g][j];
-    }
+  for (int dt = 0; dt < D / 16; ++dt) {
+    const s16x4 v0 = dec_tr_read<D>(vw, 4 * kg, 16 * dt, lane);
+    const s16x4 v1 = dec_tr_read<D>(vw, 16 + 4 * kg, 16 * dt, lane);
+    const s16x8 vb = s16x8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+    oacc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vb, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
   }
+  // lane (d = 16 dt + r16, heads 4kg + i) -> this wave's partial O
+#pragma unroll
+  for (int dt = 0; dt < D / 16; ++dt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (4 * kg + i < G) acc_s[wv][4 * kg + i][16 * dt + r16] = oacc[dt][i];
   if (kg == 0 && r16 < G) {
     mls[wv][r16][0] = m;
     mls[wv][r16][1] = l;
@@ -411,7 +366,7 @@ __device__ __forceinline__ void dec_arrive_combine(int* __restrict__ cnt, const 
 // RLHF rollout batch) the one-chunk-per-block grid ran 2560 blocks in ~3.3 rounds, each block
 // paying its own dependent round trips (scalars -> K/V -> merge); here 512 blocks stream ~4.5
 // chunks each and the per-block prologue / merge is paid once. Numerics: the same masked
-// exp2-domain softmax and P.V MFMA as decode_attn_kernel<PVM>, with the running max rescale
+// exp2-domain softmax and P.V MFMA as decode_attn_kernel, with the running max rescale
 // applied between chunks; partials (m, l, o) per split as before.
 __device__ __forceinline__ void dec_glds16(const void* src, void* lds_base) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
@@ -826,15 +781,6 @@ __global__ __launch_bounds__(64) void decode_combine_kernel(const float* __restr
     out[(int64_t)b * o_sb + (int64_t)h * o_sh + lane * DPT + j] = f2bf(acc[j] * inv);
 }
 
-// DLA_DECODE_PV=valu selects the VALU P.V form of decode_attn_kernel (read once per process)
-static bool decode_pv_mfma() {
-  static const bool v = [] {
-    const char* e = getenv("DLA_DECODE_PV");
-    return !(e != nullptr && e[0] == 'v');
-  }();
-  return v;
-}
-
 static int decode_cpb(int Tmax, int B, int Hkv);
 int decode_num_splits(int Tmax, int B, int Hkv);
 
@@ -877,23 +823,17 @@ static void launch_decode_d(const bf16_t* q, int64_t q_sb, int64_t q_sh, bf16_t*
       decode_combine_kernel<D><<<B * Hq, 64, 0, st>>>(part_o, part_ml, nsplit, out, o_sb, o_sh, Hq);
     return;
   }
-#define DLA_DEC2(GG, PV)                                                                         \
+#define DLA_DEC(GG)                                                                              \
   if (rp)                                                                                        \
-    decode_attn_kernel<D, GG, true, PV><<<grid, 256, 0, st>>>(q, q_sb, q_sh, kc, vc, c_sb, c_st, \
+    decode_attn_kernel<D, GG, true><<<grid, 256, 0, st>>>(q, q_sb, q_sh, kc, vc, c_sb, c_st,     \
                                                               c_sh, kv_len, kv_start, window,    \
                                                               scale_log2, nsplit, part_o,        \
                                                               part_ml, Hq, r0, Tmax);            \
   else                                                                                           \
-    decode_attn_kernel<D, GG, false, PV><<<grid, 256, 0, st>>>(q, q_sb, q_sh, kc, vc, c_sb,      \
+    decode_attn_kernel<D, GG, false><<<grid, 256, 0, st>>>(q, q_sb, q_sh, kc, vc, c_sb,          \
                                                                c_st, c_sh, kv_len, kv_start,     \
                                                                window, scale_log2, nsplit,       \
                                                                part_o, part_ml, Hq, r0, Tmax)
-#define DLA_DEC(GG)           \
-  if (decode_pv_mfma()) {     \
-    DLA_DEC2(GG, true);       \
-  } else {                    \
-    DLA_DEC2(GG, false);      \
-  }
   switch (G) {
     case 1: DLA_DEC(1); break;
     case 2: DLA_DEC(2); break;
@@ -901,7 +841,6 @@ static void launch_decode_d(const bf16_t* q, int64_t q_sb, int64_t q_sh, bf16_t*
     case 8: DLA_DEC(8); break;
     default: break;  // validated on the host
   }
-#undef DLA_DEC2
 #undef DLA_DEC
   decode_combine_kernel<D><<<B * Hq, 64, 0, st>>>(part_o, part_ml, nsplit, out, o_sb, o_sh, Hq);
 }

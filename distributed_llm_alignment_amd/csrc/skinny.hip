@@ -37,14 +37,8 @@ constexpr int kSkChunk = 32 * kSkUnroll;
 // Non-temporal loads on the TILED decode weight streams (each byte read once per step by one CU):
 // 3.54 vs 3.70 ms/token at B=8 (profiles/r3_decode_tiled.md). On the row-major layout nt lost
 // (4.31 vs 4.19 ms/token: the weights rotated past the Infinity Cache), so the row-major kernels
-// use default-policy loads. DLA_DECODE_NT=0 turns it off.
-static bool decode_nt() {
-  static const bool nt = [] {
-    const char* e = getenv("DLA_DECODE_NT");
-    return !(e != nullptr && atoi(e) == 0);
-  }();
-  return nt;
-}
+// use default-policy loads. (Its DLA_DECODE_NT A/B switch was removed in round 6.)
+static bool decode_nt() { return true; }
 
 }  // namespace
 
@@ -345,14 +339,9 @@ __global__ __launch_bounds__(512) void skinny_ksplit_kernel(
 // fused decode-layer launches (KsFuse): the residual-producing projection and the
 // norm-consuming qkv projection on the in-workgroup split-K kernel, the gate|up GLU on the LDS
 // kernel. M <= 16.
-// ks_body's branch-free ring (KsFuse::straight; DLA_SKINNY_STRAIGHT=0 for A/B, read once)
-static int ks_straight() {
-  static const int v = [] {
-    const char* e = getenv("DLA_SKINNY_STRAIGHT");
-    return e ? atoi(e) : 1;
-  }();
-  return v;
-}
+// ks_body's branch-free ring (KsFuse::straight) on every shape it covers; its A/B switch went
+// in round 6 (3.557 / 3.554 vs 3.581 / 3.569 ms/token at B = 8, profiles/r5_decode_fp8.md)
+static int ks_straight() { return 1; }
 
 template <bool TW, bool NT, bool F8 = false>
 static void launch_ks_fused_t(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,

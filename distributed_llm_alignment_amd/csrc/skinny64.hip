@@ -372,11 +372,8 @@ template <int MT, bool GLU, bool NIN, bool TW>
 static void m64_launch(const bf16_t* x, int64_t ldx, const bf16_t* W, int64_t ldw, bf16_t* y,
                        int64_t ldy, float* ws, int M, int N, int K, int S, const float* ssq_in,
                        int nbp, float eps, hipStream_t st) {
-  // non-temporal loads on the tiled weight stream (DLA_DECODE_NT, default on; see skinny.hip decode_nt)
-  static const bool nt = [] {
-    const char* e = getenv("DLA_DECODE_NT");
-    return !(e != nullptr && atoi(e) == 0);
-  }();
+  // non-temporal loads on the tiled weight stream (see skinny.hip decode_nt)
+  constexpr bool nt = true;
   // two weight chunks in flight per wave on the tiled nt stream (3 or 4 measured 5.10 / 5.27 vs
   // 5.01 ms/token at B = 64: more bytes in flight only lengthen the queues; removed)
   if constexpr (TW) {
