@@ -203,6 +203,13 @@ PASSES = {
     "r6-gen8-ab": [ab("gen8_loopmin", GEN8, {"new": {}, "min3": {"DLA_DECODE_LOOP_MIN": "3"}}, 2, 300),
                    ab("gen_rlhf_loopmin", "python -u tools/bench_generate.py --modes graph --prompt 512 --new 256",
                       {"new": {}, "min3": {"DLA_DECODE_LOOP_MIN": "3"}}, 1, 300)],
+    # final-build DPO step: kernel categories + table, and one PMC pass over the library GEMMs and
+    # the attention / SwiGLU kernels (MFMA busy, wave occupancy)
+    "r6-final-prof": [prof("dpo", DPO + " --steps 2 --warmup 1", DPO_TABLES),
+                      pmc("dpo_pmc", "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY GRBM_GUI_ACTIVE",
+                          "python3 bench.py --micro-pairs 4 --accum 1 --steps 1 --warmup 1",
+                          "Cijk attn_fwd attn_bwd8 adamw swiglu_bwd_t logprob_bwd_t", 400, ["--by-grid"],
+                          "Cijk|attn_fwd|attn_bwd8|adamw|swiglu_bwd_t|logprob_bwd_t")],
     # load-adaptive library rows for the single local expert (parallel.expert ADAPTIVE_MAIN)
     "r6-mixtral2": [pytest("tests/test_moe_gpu.py", 400),
                     run("ep8_hot", MIX_EP8 + " --ep-hot --steps 3 --warmup 2", 500),
