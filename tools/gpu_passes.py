@@ -210,6 +210,9 @@ PASSES = {
                           "python3 bench.py --micro-pairs 4 --accum 1 --steps 1 --warmup 1",
                           "Cijk attn_fwd attn_bwd8 adamw swiglu_bwd_t logprob_bwd_t", 400, ["--by-grid"],
                           "Cijk|attn_fwd|attn_bwd8|adamw|swiglu_bwd_t|logprob_bwd_t")],
+    # B = 8 graph decode at the RLHF shape under a kernel trace (per-layer kernel costs)
+    "r6-dec-prof": [prof("gen_rlhf", "python -u tools/bench_generate.py --modes graph --prompt 512 --new 256",
+                         [("window", ["--by-grid", "--top", "30", "--per", "8192"])], 300)],
     # load-adaptive library rows for the single local expert (parallel.expert ADAPTIVE_MAIN)
     "r6-mixtral2": [pytest("tests/test_moe_gpu.py", 400),
                     run("ep8_hot", MIX_EP8 + " --ep-hot --steps 3 --warmup 2", 500),
