@@ -210,6 +210,9 @@ PASSES = {
                           "python3 bench.py --micro-pairs 4 --accum 1 --steps 1 --warmup 1",
                           "Cijk attn_fwd attn_bwd8 adamw swiglu_bwd_t logprob_bwd_t", 400, ["--by-grid"],
                           "Cijk|attn_fwd|attn_bwd8|adamw|swiglu_bwd_t|logprob_bwd_t")],
+    # dense input gradients through the cached W^T (TN, refreshed every step) vs dY @ W (NN)
+    "r6-dgrad-ab": [ab("dgrad_layout", DPO + " --steps 5 --warmup 2", {"tn": {"DLA_TRANSPOSED_DGRAD": "1"},
+                                                                     "nn": {"DLA_TRANSPOSED_DGRAD": "0"}}, 2, 300)],
     # B = 8 graph decode at the RLHF shape under a kernel trace (per-layer kernel costs)
     "r6-dec-prof": [prof("gen_rlhf", "python -u tools/bench_generate.py --modes graph --prompt 512 --new 256",
                          [("window", ["--by-grid", "--top", "30", "--per", "8192"])], 300)],
