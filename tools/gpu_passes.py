@@ -213,6 +213,12 @@ PASSES = {
     # dense input gradients through the cached W^T (TN, refreshed every step) vs dY @ W (NN)
     "r6-dgrad-ab": [ab("dgrad_layout", DPO + " --steps 5 --warmup 2", {"tn": {"DLA_TRANSPOSED_DGRAD": "1"},
                                                                      "nn": {"DLA_TRANSPOSED_DGRAD": "0"}}, 2, 300)],
+    # B = 8 decode gate|up kernel variants at the RLHF shape (round-6 build)
+    "r6-glu-ab": [ab("glu", "python -u tools/bench_generate.py --modes graph --prompt 512 --new 256",
+                     {"lds": {}, "il": {"DLA_DECODE_GLU_IL": "1"}, "ks": {"DLA_SKINNY_GLU": "ks"}}, 2, 300)],
+    "r6-glu-ab2": [ab("glu_rlhf", "python -u tools/bench_generate.py --modes graph --prompt 512 --new 256",
+                      {"lds": {}, "ks": {"DLA_SKINNY_GLU": "ks"}}, 3, 300),
+                   ab("glu_gen8", GEN8, {"lds": {}, "ks": {"DLA_SKINNY_GLU": "ks"}}, 3, 300)],
     # B = 8 graph decode at the RLHF shape under a kernel trace (per-layer kernel costs)
     "r6-dec-prof": [prof("gen_rlhf", "python -u tools/bench_generate.py --modes graph --prompt 512 --new 256",
                          [("window", ["--by-grid", "--top", "30", "--per", "8192"])], 300)],
