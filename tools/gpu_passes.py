@@ -219,6 +219,10 @@ PASSES = {
     "r6-glu-ab2": [ab("glu_rlhf", "python -u tools/bench_generate.py --modes graph --prompt 512 --new 256",
                       {"lds": {}, "ks": {"DLA_SKINNY_GLU": "ks"}}, 3, 300),
                    ab("glu_gen8", GEN8, {"lds": {}, "ks": {"DLA_SKINNY_GLU": "ks"}}, 3, 300)],
+    # PPO with the critic on its side stream in the stats pass and the update vs one stream
+    "r6-ppo-ab": [pytest("tests/test_ppo_shape.py", 300),
+                  ab("ppo_critic_stream2", "python -u tools/bench_rlhf.py --algorithm ppo --zero-shape 8 --batch 8",
+                     {"side": {"DLA_PPO_CRITIC_STREAM": "1"}, "one": {"DLA_PPO_CRITIC_STREAM": "0"}}, 2, 500)],
     # B = 8 graph decode at the RLHF shape under a kernel trace (per-layer kernel costs)
     "r6-dec-prof": [prof("gen_rlhf", "python -u tools/bench_generate.py --modes graph --prompt 512 --new 256",
                          [("window", ["--by-grid", "--top", "30", "--per", "8192"])], 300)],
